@@ -1,0 +1,144 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node samples/sec of the reference's MNIST MLP
+trained with synchronous data-parallel SGD on N MI355X (BASELINE.json).
+
+    python bench.py --gpus 1 --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+Config = the reference's (main.py:30-31, worker.py:46-79): 784 -> 100 sigmoid
+-> 10, softmax cross-entropy, plain SGD lr 0.001, batch 100 PER WORKER (weak
+scaling: global batch = 100 * N), W ~ N(0, 1), f32 compute (the reference's
+dtype).  Data: synthetic MNIST-shaped batches resident in HBM.  Every timed
+step does the full work: forward, loss, backward, all-reduce of the 318 KB
+gradient (N > 1) and the SGD apply.
+
+Prints ONE JSON line on rank 0; value = total samples/sec over all N GPUs.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from distributedtensorflowexample_amd.data.synthetic import mnist_like_device  # noqa: E402
+from distributedtensorflowexample_amd.models.mlp import init_params  # noqa: E402
+from distributedtensorflowexample_amd.train.fused_mlp import FusedMLPTrainer  # noqa: E402
+
+METRIC = "samples/sec (whole node) MNIST MLP sync-SGD at 1/2/4/8 MI355X; scaling efficiency"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20000)
+    ap.add_argument("--warmup", type=int, default=2000)
+    ap.add_argument("--batch_size", type=int, default=100)
+    ap.add_argument("--learning_rate", type=float, default=0.001)
+    ap.add_argument("--max_graph_steps", type=int, default=1024,
+                    help="max steps per hipGraph (graphs are epoch-aligned)")
+    ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--comm", choices=["rccl", "native"], default="rccl")
+    ap.add_argument("--dataset_size", type=int, default=55000)
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            sys.exit("--gpus %d needs torch.distributed.run with %d processes" % (a.gpus, a.gpus))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    # identical replicas: the counter-based Philox init gives every rank the
+    # same parameters from the same seed (no broadcast needed; verified below)
+    params = init_params(dev, seed=1234)
+    x, y = mnist_like_device(a.dataset_size, seed=100 + rank, device=dev)
+
+    allreduce = None
+    if world > 1:
+        if a.comm == "native":
+            from distributedtensorflowexample_amd.parallel.comm import NativeComm
+
+            comm = NativeComm.from_process_group()
+            allreduce = comm.allreduce_sum_
+        else:
+            def allreduce(g):
+                dist.all_reduce(g)
+
+        chk = params.double().sum().reshape(1)
+        ref = chk.clone()
+        dist.broadcast(ref, 0)
+        if not torch.equal(chk, ref):
+            raise RuntimeError("replicas are not identical after init")
+
+    tr = FusedMLPTrainer(params, x, y, batch_size=a.batch_size, learning_rate=a.learning_rate,
+                         allreduce=allreduce, world_size=world,
+                         max_graph_steps=a.max_graph_steps)
+    barrier = (lambda: dist.barrier(device_ids=[local])) if world > 1 else None
+    use_graph = not a.no_graph
+
+    tr.run(a.warmup, use_graph)
+    if use_graph:
+        tr.prepare(a.steps)
+    if barrier:
+        barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tr.run(a.steps, use_graph)
+    torch.cuda.synchronize()
+    if barrier:
+        barrier()
+    elapsed = time.perf_counter() - t0
+
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss, acc = tr.stats()
+    ms = elapsed * 1e3 / a.steps
+    value = a.batch_size * world * a.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "samples/sec",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 6),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (MNIST-shaped, device-resident), random-init N(0,1) weights",
+            "config": {
+                "model": "MNIST MLP 784-100(sigmoid)-10, softmax-xent, SGD lr=%g" % a.learning_rate,
+                "global_batch": a.batch_size * world,
+                "per_gpu_batch": a.batch_size,
+                "seq_len": None,
+                "parallelism": "dp%d" % world,
+                "comm": a.comm if world > 1 else "none",
+                "hipgraph": use_graph,
+            },
+            "final_loss": round(loss, 5),
+            "final_train_acc": round(acc, 4),
+            "global_step": tr.global_step(),
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

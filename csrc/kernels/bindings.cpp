@@ -1,0 +1,130 @@
+// Python bindings of the gfx950 kernel launchers (module `_hip`).
+//
+// The binding deliberately takes raw device addresses and a hipStream_t handle
+// (Python passes tensor.data_ptr() and torch.cuda.current_stream().cuda_stream)
+// instead of including torch headers: the module then builds in seconds, has
+// no C++ ABI coupling to the torch build, and every launch lands on whatever
+// stream the caller is on, including a stream under hipGraph capture.
+// Shape/dtype/device validation lives in the Python wrappers
+// (distributedtensorflowexample_amd/ops/).
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+
+namespace dtfx {
+void mlp_fwd_launch(const float*, const float*, float, float*, const float*, float*, int,
+                    hipStream_t);
+void mlp_head_launch(const float*, const float*, float, float*, const int*, float*, int,
+                     hipStream_t);
+void mlp_wgrad_launch(float*, float, float*, const float*, float*, int*, float*, int, int,
+                      hipStream_t);
+long long mlp_workspace_floats(int);
+void calib_launch(int, int, int, const int*, const float*, float*, hipStream_t);
+void gemm_f32_launch(bool, bool, int, int, int, float, const float*, int, const float*, int,
+                     float, float*, int, const float*, int, const float*, int, bool, hipStream_t);
+void colsum_launch(int, int, const float*, int, float, float*, hipStream_t);
+void softmax_xent_launch(int, int, const float*, int, const int*, const float*, int, int, float,
+                         float*, float*, int, float*, float*, hipStream_t);
+void sgd_launch(long long, float*, const float*, float, const float*, float, hipStream_t);
+void momentum_launch(long long, float*, const float*, float*, float, const float*, float, float,
+                     bool, hipStream_t);
+void adam_launch(long long, float*, const float*, float*, float*, float, const float*, float,
+                 float, float, float, bool, int, const int*, hipStream_t);
+void scale_launch(long long, float*, float, hipStream_t);
+void counter_add_launch(int*, int, hipStream_t);
+void philox_init_launch(long long, float*, unsigned long long, unsigned long long, int, float,
+                        float, hipStream_t);
+void act_bwd_launch(long long, int, const float*, const float*, float*, hipStream_t);
+void act_fwd_launch(long long, int, const float*, float*, hipStream_t);
+}  // namespace dtfx
+
+template <typename T>
+static inline T* P(uintptr_t a) { return reinterpret_cast<T*>(a); }
+static inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "gfx950 HIP kernels of distributedtensorflowexample_amd";
+  m.attr("ARCH") = "gfx950";
+
+  m.def("mlp_workspace_floats", &dtfx::mlp_workspace_floats);
+  m.def("mlp_fwd", [](uintptr_t p_old, uintptr_t grad, float lr, uintptr_t p_new, uintptr_t x,
+                      uintptr_t ws, int B, uintptr_t s) {
+    dtfx::mlp_fwd_launch(P<const float>(p_old), P<const float>(grad), lr, P<float>(p_new),
+                         P<const float>(x), P<float>(ws), B, S(s));
+  });
+  m.def("mlp_head", [](uintptr_t p_old, uintptr_t grad, float lr, uintptr_t p_new, uintptr_t lab,
+                       uintptr_t ws, int B, uintptr_t s) {
+    dtfx::mlp_head_launch(P<const float>(p_old), P<const float>(grad), lr, P<float>(p_new),
+                          P<const int>(lab), P<float>(ws), B, S(s));
+  });
+  m.def("mlp_wgrad", [](uintptr_t p, float lr, uintptr_t grad, uintptr_t x, uintptr_t ws,
+                        uintptr_t ctr, uintptr_t stats, int ring, int B, uintptr_t s) {
+    dtfx::mlp_wgrad_launch(P<float>(p), lr, P<float>(grad), P<const float>(x), P<float>(ws),
+                           P<int>(ctr), P<float>(stats), ring, B, S(s));
+  });
+  m.def("gemm_f32", [](bool ta, bool tb, int M, int N, int K, float alpha, uintptr_t A, int lda,
+                       uintptr_t B, int ldb, float beta, uintptr_t C, int ldc, uintptr_t bias,
+                       int act, uintptr_t aux, int ldaux, bool act_grad, uintptr_t s) {
+    dtfx::gemm_f32_launch(ta, tb, M, N, K, alpha, P<const float>(A), lda, P<const float>(B), ldb,
+                          beta, P<float>(C), ldc, P<const float>(bias), act, P<const float>(aux),
+                          ldaux, act_grad, S(s));
+  });
+  m.def("colsum", [](int M, int N, uintptr_t G, int ldg, float beta, uintptr_t out, uintptr_t s) {
+    dtfx::colsum_launch(M, N, P<const float>(G), ldg, beta, P<float>(out), S(s));
+  });
+  m.def("softmax_xent", [](int N, int C, uintptr_t logits, int ldl, uintptr_t lab_idx,
+                           uintptr_t lab_dense, int ldy, int ignore, float scale, uintptr_t loss,
+                           uintptr_t dlogits, int ldd, uintptr_t correct, uintptr_t probs,
+                           uintptr_t s) {
+    dtfx::softmax_xent_launch(N, C, P<const float>(logits), ldl, P<const int>(lab_idx),
+                              P<const float>(lab_dense), ldy, ignore, scale, P<float>(loss),
+                              P<float>(dlogits), ldd, P<float>(correct), P<float>(probs), S(s));
+  });
+  m.def("sgd", [](long long n, uintptr_t p, uintptr_t g, float lr, uintptr_t lr_ptr, float wd,
+                  uintptr_t s) {
+    dtfx::sgd_launch(n, P<float>(p), P<const float>(g), lr, P<const float>(lr_ptr), wd, S(s));
+  });
+  m.def("momentum", [](long long n, uintptr_t p, uintptr_t g, uintptr_t v, float lr,
+                       uintptr_t lr_ptr, float mu, float wd, bool nesterov, uintptr_t s) {
+    dtfx::momentum_launch(n, P<float>(p), P<const float>(g), P<float>(v), lr,
+                          P<const float>(lr_ptr), mu, wd, nesterov, S(s));
+  });
+  m.def("adam", [](long long n, uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, float lr,
+                   uintptr_t lr_ptr, float b1, float b2, float eps, float wd, bool adamw, int step,
+                   uintptr_t step_ptr, uintptr_t s) {
+    dtfx::adam_launch(n, P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), lr,
+                      P<const float>(lr_ptr), b1, b2, eps, wd, adamw, step, P<const int>(step_ptr),
+                      S(s));
+  });
+  m.def("scale", [](long long n, uintptr_t x, float a, uintptr_t s) {
+    dtfx::scale_launch(n, P<float>(x), a, S(s));
+  });
+  m.def("counter_add", [](uintptr_t c, int d, uintptr_t s) {
+    dtfx::counter_add_launch(P<int>(c), d, S(s));
+  });
+  m.def("philox_init", [](long long n, uintptr_t out, unsigned long long seed,
+                          unsigned long long offset, int mode, float a, float b, uintptr_t s) {
+    dtfx::philox_init_launch(n, P<float>(out), seed, offset, mode, a, b, S(s));
+  });
+  m.def("act_bwd", [](long long n, int act, uintptr_t dy, uintptr_t sv, uintptr_t dz,
+                      uintptr_t s) {
+    dtfx::act_bwd_launch(n, act, P<const float>(dy), P<const float>(sv), P<float>(dz), S(s));
+  });
+  m.def("act_fwd", [](long long n, int act, uintptr_t x, uintptr_t y, uintptr_t s) {
+    dtfx::act_fwd_launch(n, act, P<const float>(x), P<float>(y), S(s));
+  });
+  m.def("calib", [](int mode, int grid, int block, uintptr_t ctr, uintptr_t data, uintptr_t out,
+                    uintptr_t s) {
+    dtfx::calib_launch(mode, grid, block, P<const int>(ctr), P<const float>(data), P<float>(out),
+                       S(s));
+  });
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+}

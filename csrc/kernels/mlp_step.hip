@@ -1,0 +1,435 @@
+// Fused training step for the reference's MNIST MLP (784 -> 100 sigmoid -> 10,
+// softmax cross-entropy, plain SGD).  Reference graph: worker.py:46-79.
+//
+// Design rule (measured, profiles/): at this size the step is bound by how
+// many bytes EACH CU must pull and by dependent kernel boundaries (~1.5 us),
+// not by FLOPs (32 MFLOP = 0.2 us of f32 MFMA).  A first version that gave
+// each of 49 workgroups a full-K 16x16 tile moved ~150 KB per CU and took
+// ~10 us per kernel.  This version keeps every workgroup at 7-21 KB and
+// spreads each phase over ~100-350 workgroups:
+//
+//   K1 mlp_fwd   grid (row tile 16) x (hidden tile 16) x (K slice of 112):
+//                partial z1 = x . W1 over its K slice -> slab[ks]
+//                (deferred-apply mode: W1 <- W1 - lr * G on the fly,
+//                 published to the ping-pong buffer by the rt == 0 blocks)
+//   K2 mlp_head  one wave per batch row: z1 = sum of 7 slabs + b1,
+//                h = sigmoid, logits = h . W2 + b2, softmax, xent, accuracy,
+//                dlogits = (p - y)/B, dz1 = (dlogits . W2^T) * h * (1 - h)
+//                -> hbuf [b][j], dz1T [j][b], dlT [c][b], rowstat [b]
+//   K3 mlp_wgrad 343 blocks: dW1^T tile = dz1^T . x   (f32 MFMA, K = batch)
+//                  7 blocks: dW2^T = dl^T . h, db1, db2 (MFMA against ones),
+//                            mean loss / accuracy -> stats ring
+//                direct mode: the SGD apply is fused into the epilogue
+//                (each parameter element is owned by exactly one lane);
+//                grad mode: writes the flat gradient for an all-reduce.
+//
+// All MFMA work is v_mfma_f32_16x16x4_f32 (exact f32).  Lane l supplies
+// A[i = l&15][k = l>>4], B[k = l>>4][j = l&15]; C[row = (l>>4)*4 + r][col = l&15].
+// A float4 load of k = 16g + 4q .. 16g + 4q + 3 feeds 4 MFMAs (element e is
+// k = 16g + 4q + e on BOTH operands: a consistent permutation of the K sum).
+//
+// Parameter layout (flat f32, 79,510 elements; gradients use the same layout
+// so one all-reduce covers everything):
+//   [0, 78400)      W1t [100][784]   (W1t[j][i] = TF kernel W1[i][j])
+//   [78400, 78500)  b1  [100]
+//   [78500, 79500)  W2t [10][100]    (W2t[c][j] = TF kernel W2[j][c])
+//   [79500, 79510)  b2  [10]
+//
+// Batch selection: every launch takes the batch's own x / label pointer.  A
+// captured hipGraph therefore freezes one batch per captured step; the
+// trainer captures a whole epoch (one graph = nbatches steps), so replaying
+// it walks the device-resident dataset exactly like next_batch does.  No
+// kernel starts with a dependent "which batch?" load (measured: ~0.5 us per
+// dependent round trip on this chip).
+//
+// global_step (worker.py:29-32,141) is a device int advanced by ONE thread of
+// mlp_wgrad after it has used the value as the stats-ring index; no other
+// thread of any launch touches it.
+#include "common.h"
+
+#include <stdexcept>
+#include <string>
+
+namespace dtfx {
+namespace mlp {
+
+constexpr int D = 784, H = 100, C = 10;
+constexpr int HT = 7;          // hidden tiles of 16 (112 padded)
+constexpr int HP = HT * 16;    // padded hidden width
+constexpr int KS = 7;          // K slices of K1
+constexpr int KW = D / KS;     // 112 = 7 groups of 16
+constexpr int FT = D / 16;     // 49 feature tiles (dW1)
+constexpr int OFF_W1 = 0;
+constexpr int OFF_B1 = H * D;
+constexpr int OFF_W2 = OFF_B1 + H;
+constexpr int OFF_B2 = OFF_W2 + C * H;
+constexpr int NPARAM = OFF_B2 + C;
+constexpr int MAXB = 256;
+
+static_assert(KW % 16 == 0 && KS * KW == D, "K slicing of 784");
+static_assert(NPARAM == 79510, "parameter count of worker.py:50-53");
+
+struct Bufs {            // workspace (zero-initialised once; padding stays 0)
+  float* slab;           // [KS][BP][HP]  partial z1
+  float* hbuf;           // [BP][HP]      h
+  float* dz1T;           // [HP][BP]      dz1 transposed
+  float* dlT;            // [16][BP]      dlogits transposed
+  float* rowstat;        // [BP][2]       per-row (loss, correct)
+};
+
+__device__ __forceinline__ float4 f4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// ---------------------------------------------------------------------------
+// K1: partial z1 over one K slice (+ deferred W1 apply)
+// ---------------------------------------------------------------------------
+template <bool APPLY>
+__global__ __launch_bounds__(64) void mlp_fwd_kernel(
+    const float* __restrict__ p_old, const float* __restrict__ grad, float lr,
+    float* __restrict__ p_new, const float* __restrict__ x, Bufs w, int B) {
+  const int RT = (B + 15) >> 4, BP = RT * 16;
+  const int rt = blockIdx.x % RT, jt = (blockIdx.x / RT) % HT, ks = blockIdx.x / (RT * HT);
+  const int lane = threadIdx.x, r = lane & 15, q = lane >> 4;
+
+  const int row = rt * 16 + r, col = jt * 16 + r;
+  const bool rv = row < B, cv = col < H;
+  const int k0 = ks * KW + q * 4;
+  const float* xr = x + (size_t)(rv ? row : 0) * D + k0;
+  const size_t woff = OFF_W1 + (size_t)(cv ? col : 0) * D + k0;
+
+  float4 xa[KW / 16], wa[KW / 16];
+#pragma unroll
+  for (int g = 0; g < KW / 16; ++g) {
+    xa[g] = rv ? f4(xr + g * 16) : make_float4(0, 0, 0, 0);
+    wa[g] = cv ? f4(p_old + woff + g * 16) : make_float4(0, 0, 0, 0);
+  }
+  if (APPLY) {
+#pragma unroll
+    for (int g = 0; g < KW / 16; ++g) {
+      const float4 gg = cv ? f4(grad + woff + g * 16) : make_float4(0, 0, 0, 0);
+      wa[g].x -= lr * gg.x;
+      wa[g].y -= lr * gg.y;
+      wa[g].z -= lr * gg.z;
+      wa[g].w -= lr * gg.w;
+      if (rt == 0 && cv) *reinterpret_cast<float4*>(p_new + woff + g * 16) = wa[g];
+    }
+  }
+  f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+#pragma unroll
+  for (int g = 0; g < KW / 16; ++g) {
+    acc0 = mfma16x16x4(xa[g].x, wa[g].x, acc0);
+    acc1 = mfma16x16x4(xa[g].y, wa[g].y, acc1);
+    acc0 = mfma16x16x4(xa[g].z, wa[g].z, acc0);
+    acc1 = mfma16x16x4(xa[g].w, wa[g].w, acc1);
+  }
+  float* out = w.slab + ((size_t)ks * BP + rt * 16 + q * 4) * HP + jt * 16 + r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[(size_t)i * HP] = acc0[i] + acc1[i];
+}
+
+// ---------------------------------------------------------------------------
+// K2: per-row head (one wave per batch row)
+// ---------------------------------------------------------------------------
+template <bool APPLY>
+__global__ __launch_bounds__(64) void mlp_head_kernel(
+    const float* __restrict__ p_old, const float* __restrict__ grad, float lr,
+    float* __restrict__ p_new, const int* __restrict__ labels, Bufs w, int B) {
+  const int BP = ((B + 15) >> 4) * 16;
+  const int row = blockIdx.x, lane = threadIdx.x;
+  const int y = labels[row];
+  const bool publish = APPLY && row == 0;
+
+  float hv[2], w2[2][C];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = lane + 64 * u;
+    hv[u] = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) w2[u][c] = 0.f;
+    if (j < H) {
+      float z = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) z += w.slab[((size_t)s * BP + row) * HP + j];
+      float b1 = p_old[OFF_B1 + j];
+      if (APPLY) {
+        b1 -= lr * grad[OFF_B1 + j];
+        if (publish) p_new[OFF_B1 + j] = b1;
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float wv = p_old[OFF_W2 + c * H + j];
+        if (APPLY) {
+          wv -= lr * grad[OFF_W2 + c * H + j];
+          if (publish) p_new[OFF_W2 + c * H + j] = wv;
+        }
+        w2[u][c] = wv;
+      }
+      hv[u] = sigmoidf_(z + b1);
+      w.hbuf[(size_t)row * HP + j] = hv[u];
+    }
+  }
+  // logits = h . W2 + b2 (wave reductions; every lane ends with all 10)
+  float lg[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    float b2 = p_old[OFF_B2 + c];
+    if (APPLY) b2 -= lr * grad[OFF_B2 + c];
+    lg[c] = wave_sum(hv[0] * w2[0][c] + hv[1] * w2[1][c]) + b2;
+  }
+  if (publish && lane < C) p_new[OFF_B2 + lane] = p_old[OFF_B2 + lane] - lr * grad[OFF_B2 + lane];
+
+  float m = lg[0];
+  int am = 0;
+#pragma unroll
+  for (int c = 1; c < C; ++c)
+    if (lg[c] > m) { m = lg[c]; am = c; }  // first max, like tf.argmax
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) se += __expf(lg[c] - m);
+  const float inv = 1.f / se, invB = 1.f / (float)B;
+  float dl[C], ly = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    dl[c] = (__expf(lg[c] - m) * inv - (c == y ? 1.f : 0.f)) * invB;
+    ly = (c == y) ? lg[c] : ly;
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = lane + 64 * u;
+    if (j < H) {
+      float dh = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) dh += dl[c] * w2[u][c];
+      w.dz1T[(size_t)j * BP + row] = dh * hv[u] * (1.f - hv[u]);
+    }
+  }
+  float mydl = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) mydl = (lane == c) ? dl[c] : mydl;
+  if (lane < C) w.dlT[(size_t)lane * BP + row] = mydl;
+  if (lane == 0) {
+    w.rowstat[2 * row] = m + __logf(se) - ly;  // xent of this row
+    w.rowstat[2 * row + 1] = (am == y) ? 1.f : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K3: weight gradients (+ fused SGD apply in direct mode)
+// ---------------------------------------------------------------------------
+template <bool DIRECT>
+__global__ __launch_bounds__(256) void mlp_wgrad_kernel(
+    float* __restrict__ p, float lr, float* __restrict__ grad, const float* __restrict__ x,
+    Bufs w, int* __restrict__ ctr, float* __restrict__ stats, int stats_ring, int B) {
+  const int BP = ((B + 15) >> 4) * 16, NG = BP / 16;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  constexpr int MAXG = MAXB / 16;
+  constexpr int FG = (FT + 3) / 4;  // 13 feature groups of 4 waves
+  const int bid = blockIdx.x;
+
+  if (bid < HT * FG) {
+    // ---- dW1^T tile (jt, kt) = dz1T[jt] . x[:, kt], one tile per wave ------
+    const int jt = bid / FG, kt = (bid % FG) * 4 + wave;
+    if (kt >= FT) return;
+    const float* xc = x + kt * 16 + r;
+    const float* a = w.dz1T + (size_t)(jt * 16 + r) * BP + q * 4;
+    float4 av[MAXG];
+    float xv[MAXG][4];
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g) {
+      if (g < NG) {
+        av[g] = f4(a + g * 16);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int b = g * 16 + q * 4 + e;
+          xv[g][e] = (b < B) ? xc[(size_t)b * D] : 0.f;
+        }
+      }
+    }
+    float pw[4];
+    if (DIRECT) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = jt * 16 + q * 4 + i;
+        pw[i] = (j < H) ? p[OFF_W1 + (size_t)j * D + kt * 16 + r] : 0.f;
+      }
+    }
+    f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g) {
+      if (g < NG) {
+        acc0 = mfma16x16x4(av[g].x, xv[g][0], acc0);
+        acc1 = mfma16x16x4(av[g].y, xv[g][1], acc1);
+        acc0 = mfma16x16x4(av[g].z, xv[g][2], acc0);
+        acc1 = mfma16x16x4(av[g].w, xv[g][3], acc1);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = jt * 16 + q * 4 + i;
+      if (j < H) {
+        const size_t off = OFF_W1 + (size_t)j * D + kt * 16 + r;
+        const float gv = acc0[i] + acc1[i];
+        if (DIRECT) p[off] = pw[i] - lr * gv;
+        else grad[off] = gv;
+      }
+    }
+    return;
+  }
+
+  // ---- small parameters of hidden tile jt: one product per wave -----------
+  //   wave 0: dW2^T[:, jt] = dlT . h[:, jt]   wave 1: db1[jt] = dz1T[jt] . 1
+  //   wave 2: db2 = dlT . 1 (jt == 0)         wave 3: loss/accuracy (jt == 0)
+  const int jt = bid - HT * FG;
+  if (wave == 3) {
+    if (jt != 0) return;
+    float l = 0.f, a = 0.f;
+    for (int b = lane; b < B; b += 64) {
+      l += w.rowstat[2 * b];
+      a += w.rowstat[2 * b + 1];
+    }
+    l = wave_sum(l);
+    a = wave_sum(a);
+    if (lane == 0) {
+      const int step = *ctr;  // this thread is the only reader/writer of ctr
+      if (stats) {
+        float* st = stats + (size_t)(step % stats_ring) * 2;
+        st[0] = l / (float)B;
+        st[1] = a / (float)B;
+      }
+      *ctr = step + 1;
+    }
+    return;
+  }
+  if (wave == 2 && jt != 0) return;
+  const float* A = (wave == 1) ? w.dz1T + (size_t)(jt * 16 + r) * BP + q * 4
+                               : w.dlT + (size_t)r * BP + q * 4;
+  const float* hb = w.hbuf + jt * 16 + r;
+  float4 av[MAXG];
+  float bv[MAXG][4];
+#pragma unroll
+  for (int g = 0; g < MAXG; ++g) {
+    if (g < NG) {
+      av[g] = f4(A + g * 16);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        bv[g][e] = (wave == 0) ? hb[(size_t)(g * 16 + q * 4 + e) * HP] : 1.f;
+    }
+  }
+  // NB: padded batch columns of dz1T/dlT are zero, so multiplying by 1 is exact.
+  f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+#pragma unroll
+  for (int g = 0; g < MAXG; ++g) {
+    if (g < NG) {
+      acc0 = mfma16x16x4(av[g].x, bv[g][0], acc0);
+      acc1 = mfma16x16x4(av[g].y, bv[g][1], acc1);
+      acc0 = mfma16x16x4(av[g].z, bv[g][2], acc0);
+      acc1 = mfma16x16x4(av[g].w, bv[g][3], acc1);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float v = acc0[i] + acc1[i];
+    size_t off = 0;
+    bool ok = false;
+    if (wave == 0) {  // C[c = q*4+i][j = jt*16 + r]
+      const int c = q * 4 + i, j = jt * 16 + r;
+      ok = c < C && j < H;
+      off = OFF_W2 + c * H + j;
+    } else if (wave == 1) {  // C[j = jt*16 + q*4+i][*]
+      const int j = jt * 16 + q * 4 + i;
+      ok = r == 0 && j < H;
+      off = OFF_B1 + j;
+    } else {  // C[c = q*4+i][*]
+      const int c = q * 4 + i;
+      ok = r == 0 && c < C;
+      off = OFF_B2 + c;
+    }
+    if (ok) {
+      if (DIRECT) p[off] -= lr * v;
+      else grad[off] = v;
+    }
+  }
+}
+
+}  // namespace mlp
+
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+static mlp::Bufs make_bufs(float* ws, int B) {
+  using namespace mlp;
+  const int BP = ((B + 15) / 16) * 16;
+  Bufs b;
+  b.slab = ws;
+  b.hbuf = b.slab + (size_t)KS * BP * HP;
+  b.dz1T = b.hbuf + (size_t)BP * HP;
+  b.dlT = b.dz1T + (size_t)HP * BP;
+  b.rowstat = b.dlT + (size_t)16 * BP;
+  return b;
+}
+
+long long mlp_workspace_floats(int B) {
+  using namespace mlp;
+  const long long BP = ((B + 15) / 16) * 16;
+  return (long long)KS * BP * HP + BP * HP + HP * BP + 16 * BP + 2 * BP;
+}
+
+static void check_b(int B) {
+  if (B < 1 || B > mlp::MAXB) throw std::runtime_error("fused MLP step: batch must be in [1, 256]");
+}
+
+// K1: grad != nullptr => deferred apply (p_new must differ from p_old)
+void mlp_fwd_launch(const float* p_old, const float* grad, float lr, float* p_new, const float* x,
+                    float* ws, int B, hipStream_t stream) {
+  using namespace mlp;
+  check_b(B);
+  const Bufs w = make_bufs(ws, B);
+  const int RT = (B + 15) / 16;
+  dim3 grid(RT * HT * KS), block(64);
+  if (grad) {
+    if (!p_new || p_new == p_old) throw std::runtime_error("mlp_fwd: apply needs ping-pong p_new");
+    hipLaunchKernelGGL(mlp_fwd_kernel<true>, grid, block, 0, stream, p_old, grad, lr, p_new, x, w,
+                       B);
+  } else {
+    hipLaunchKernelGGL(mlp_fwd_kernel<false>, grid, block, 0, stream, p_old, p_old, 0.f, nullptr,
+                       x, w, B);
+  }
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void mlp_head_launch(const float* p_old, const float* grad, float lr, float* p_new,
+                     const int* labels, float* ws, int B, hipStream_t stream) {
+  using namespace mlp;
+  check_b(B);
+  const Bufs w = make_bufs(ws, B);
+  if (grad) {
+    if (!p_new || p_new == p_old) throw std::runtime_error("mlp_head: apply needs ping-pong p_new");
+    hipLaunchKernelGGL(mlp_head_kernel<true>, dim3(B), dim3(64), 0, stream, p_old, grad, lr, p_new,
+                       labels, w, B);
+  } else {
+    hipLaunchKernelGGL(mlp_head_kernel<false>, dim3(B), dim3(64), 0, stream, p_old, p_old, 0.f,
+                       nullptr, labels, w, B);
+  }
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// K3: grad == nullptr => direct mode (p -= lr * g fused); else writes grad
+void mlp_wgrad_launch(float* p, float lr, float* grad, const float* x, float* ws, int* ctr,
+                      float* stats, int stats_ring, int B, hipStream_t stream) {
+  using namespace mlp;
+  check_b(B);
+  if (stats && stats_ring < 1) throw std::runtime_error("mlp_wgrad: stats_ring < 1");
+  if (!ctr) throw std::runtime_error("mlp_wgrad: needs the global_step counter");
+  const Bufs w = make_bufs(ws, B);
+  dim3 grid(HT * ((FT + 3) / 4) + HT), block(256);
+  if (grad) {
+    hipLaunchKernelGGL(mlp_wgrad_kernel<false>, grid, block, 0, stream, p, 0.f, grad, x, w, ctr,
+                       stats, stats_ring, B);
+  } else {
+    if (!p) throw std::runtime_error("mlp_wgrad: direct mode needs parameters");
+    hipLaunchKernelGGL(mlp_wgrad_kernel<true>, grid, block, 0, stream, p, lr, nullptr, x, w, ctr,
+                       stats, stats_ring, B);
+  }
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dtfx

@@ -1,0 +1,141 @@
+"""Fused three-launch training step of the reference MNIST MLP.
+
+Python side of ``csrc/kernels/mlp_step.hip``; see that file for the kernel
+design.  The step the reference runs per worker (worker.py:131-141: pull,
+forward, loss, backward, ApplyGradientDescent, global_step += 1) becomes::
+
+    mlp_fwd   : partial z1 = x . W1 over 7 K slices (343 single-wave blocks)
+    mlp_head  : per-row sigmoid, logits, softmax-xent, accuracy, dlogits, dz1
+    mlp_wgrad : dW1, dW2, db1, db2 (+ the SGD apply fused in, single GPU)
+
+Sync data-parallel mode instead writes the flat gradient, all-reduces it and
+applies it at the start of the next step (``mlp_fwd``/``mlp_head`` with
+``grad``/``p_new``: deferred apply into a ping-pong parameter buffer).
+
+Flat parameter layout (shared with gradients and all-reduce buckets)::
+
+    W1t [100][784] | b1 [100] | W2t [10][100] | b2 [10]      (79,510 f32)
+
+``reference_step`` is the same math in plain PyTorch (float64-capable), the
+numerics oracle of the kernel tests and the CPU path of the PS worker.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._ext import hip, ptr, stream_handle
+
+D, H, C = 784, 100, 10
+HT, HP = 7, 112
+OFF_W1 = 0
+OFF_B1 = OFF_W1 + H * D
+OFF_W2 = OFF_B1 + H
+OFF_B2 = OFF_W2 + C * H
+NPARAM = OFF_B2 + C
+MAX_BATCH = 256
+
+
+def unflatten(p):
+    """Views (W1t [H,D], b1 [H], W2t [C,H], b2 [C]) into a flat buffer."""
+    return (p[OFF_W1:OFF_B1].view(H, D), p[OFF_B1:OFF_W2], p[OFF_W2:OFF_B2].view(C, H),
+            p[OFF_B2:NPARAM])
+
+
+class StepWorkspace:
+    """Device scratch of the fused step for batch size ``B`` (zeroed once:
+    the padding rows/columns the kernels never write must stay zero)."""
+
+    def __init__(self, B, device, stats_ring=4096):
+        if not 1 <= B <= MAX_BATCH:
+            raise ValueError("fused MLP step supports 1 <= batch <= %d" % MAX_BATCH)
+        self.B = B
+        self.device = torch.device(device)
+        n = hip().mlp_workspace_floats(B) if self.device.type == "cuda" else 1
+        self.buf = torch.zeros(int(n), device=device, dtype=torch.float32)
+        # global_step (advanced on the device by mlp_wgrad)
+        self.ctr = torch.zeros(1, device=device, dtype=torch.int32)
+        self.stats_ring = stats_ring
+        self.stats = torch.zeros(stats_ring, 2, device=device, dtype=torch.float32)
+
+    def global_step(self) -> int:
+        return int(self.ctr[0].item())
+
+    def set_global_step(self, s: int):
+        self.ctr.fill_(int(s))
+
+
+def _check(x, labels, B):
+    if x.dtype != torch.float32 or not x.is_contiguous() or x.numel() != B * D or not x.is_cuda:
+        raise ValueError("x must be a contiguous f32 GPU batch of B*784 values")
+    if x.data_ptr() % 16:
+        raise ValueError("x batch must be 16-byte aligned")
+    if labels is not None and (labels.dtype != torch.int32 or labels.numel() != B
+                               or not labels.is_contiguous()):
+        raise ValueError("labels must be a contiguous int32 batch of B values")
+
+
+def _check_flat(*ts):
+    for t in ts:
+        if t is not None and (t.numel() != NPARAM or t.dtype != torch.float32 or not t.is_cuda
+                              or not t.is_contiguous()):
+            raise ValueError("parameter/gradient buffers must be contiguous f32 [79510] on the GPU")
+
+
+def step_direct(p, x, labels, ws: StepWorkspace, lr, stats=True):
+    """One full SGD step in place on ``p`` for the batch (x [B,784], labels [B])."""
+    _check(x, labels, ws.B)
+    _check_flat(p)
+    h, s = hip(), stream_handle()
+    h.mlp_fwd(ptr(p), 0, 0.0, 0, ptr(x), ptr(ws.buf), ws.B, s)
+    h.mlp_head(ptr(p), 0, 0.0, 0, ptr(labels), ptr(ws.buf), ws.B, s)
+    h.mlp_wgrad(ptr(p), float(lr), 0, ptr(x), ptr(ws.buf), ptr(ws.ctr),
+                ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B, s)
+
+
+def step_grad(p_old, x, labels, ws: StepWorkspace, grad, prev_grad=None, lr=0.0, p_new=None,
+              stats=True):
+    """Forward/backward writing ``grad``; optionally first applies ``prev_grad``.
+
+    With ``prev_grad`` the step computes on ``p_new = p_old - lr * prev_grad``
+    (published into ``p_new`` by the kernels) -- the deferred apply of sync DP.
+    Returns the parameter buffer the gradient belongs to.
+    """
+    _check(x, labels, ws.B)
+    _check_flat(p_old, grad, prev_grad, p_new)
+    if prev_grad is not None and (p_new is None or p_new.data_ptr() == p_old.data_ptr()):
+        raise ValueError("apply needs a distinct p_new buffer (ping-pong)")
+    h, s = hip(), stream_handle()
+    pg = ptr(prev_grad)
+    pn = ptr(p_new) if prev_grad is not None else 0
+    h.mlp_fwd(ptr(p_old), pg, float(lr), pn, ptr(x), ptr(ws.buf), ws.B, s)
+    h.mlp_head(ptr(p_old), pg, float(lr), pn, ptr(labels), ptr(ws.buf), ws.B, s)
+    h.mlp_wgrad(0, 0.0, ptr(grad), ptr(x), ptr(ws.buf), ptr(ws.ctr),
+                ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B, s)
+    return p_new if prev_grad is not None else p_old
+
+
+def reference_forward(p, x):
+    W1t, b1, W2t, b2 = unflatten(p)
+    h = torch.sigmoid(x @ W1t.t() + b1)
+    return h, h @ W2t.t() + b2
+
+
+def reference_step(p, x, labels):
+    """Plain-torch forward/backward of worker.py's graph: (grad, loss, accuracy)."""
+    W1t, b1, W2t, b2 = unflatten(p)
+    B = x.shape[0]
+    h, logits = reference_forward(p, x)
+    lse = torch.logsumexp(logits, 1)
+    lab = labels.long()
+    loss = (lse - logits.gather(1, lab[:, None])[:, 0]).mean()
+    acc = (logits.argmax(1) == lab).to(p.dtype).mean()
+    prob = torch.softmax(logits, 1)
+    dl = (prob - torch.nn.functional.one_hot(lab, C).to(p.dtype)) / B
+    dz = (dl @ W2t) * h * (1 - h)
+    g = torch.empty_like(p)
+    gW1t, gb1, gW2t, gb2 = unflatten(g)
+    gW1t.copy_(dz.t() @ x)
+    gb1.copy_(dz.sum(0))
+    gW2t.copy_(dl.t() @ h)
+    gb2.copy_(dl.sum(0))
+    return g, loss, acc

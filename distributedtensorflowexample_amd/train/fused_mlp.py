@@ -1,0 +1,207 @@
+"""Fused MNIST-MLP training engine: three HIP launches per step, hipGraph-replayed.
+
+This is the MI355X-native replacement of the reference's per-step session
+loop (worker.py:129-159).  Per step the reference makes three gRPC round
+trips (pull 318 KB, push 318 KB + remote ApplyGradientDescent, AssignAdd),
+a host->GPU feed of 317 KB and ~14 tiny TF kernels.  Here:
+
+* the dataset is resident in HBM; each launch gets its batch's pointer, and
+  one hipGraph is captured per epoch (``nbatches`` steps), so replaying it
+  walks the dataset like ``next_batch`` with no host work per step;
+* the step is ``mlp_fwd`` / ``mlp_head`` / ``mlp_wgrad`` (ops/mlp_step.py);
+  on one GPU the SGD apply is fused into ``mlp_wgrad``'s epilogue;
+* in sync data-parallel mode the flat 318 KB gradient is all-reduced after
+  ``mlp_wgrad`` by a pluggable ``allreduce(grad)`` callable (RCCL through
+  ``torch.distributed`` or the native communicator) and applied, averaged
+  through ``lr / world_size``, inside the next step's ``mlp_fwd``/``mlp_head``;
+* ``global_step`` is a device counter advanced by the kernels (AssignAdd of
+  worker.py:32,141); loss/accuracy land in a device ring read back lazily.
+
+Data-parallel update order: the all-reduced gradient of step t is applied at
+the start of step t+1 (ping-pong parameter buffers make the apply race-free
+across the launch's workgroups).  ``flush()`` applies the pending gradient,
+so ``params`` after ``flush()`` is exactly the result of t full SGD steps.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..ops import mlp_step, optim
+
+
+class FusedMLPTrainer:
+    def __init__(self, params, x, labels, batch_size=100, learning_rate=0.001, allreduce=None,
+                 world_size=1, stats_ring=4096, global_step=0, max_graph_steps=1024):
+        if not params.is_cuda:
+            raise ValueError("FusedMLPTrainer runs on the GPU; use the generic path on CPU")
+        if params.numel() != mlp_step.NPARAM:
+            raise ValueError("params must be the flat 79,510-element MLP buffer")
+        self.device = params.device
+        self.B = int(batch_size)
+        self.lr = float(learning_rate)
+        self.world_size = int(world_size)
+        self.allreduce = allreduce
+        x = x.reshape(-1, mlp_step.D).to(self.device, torch.float32).contiguous()
+        labels = labels.reshape(-1).to(self.device, torch.int32).contiguous()
+        self.nbatches = x.shape[0] // self.B
+        if self.nbatches < 1:
+            raise ValueError("dataset smaller than one batch")
+        self.x, self.labels = x, labels
+        self.bufs = [params.detach().clone().contiguous(), torch.empty_like(params)]
+        self.cur = 0
+        self.grad = torch.zeros_like(params)
+        self.ws = mlp_step.StepWorkspace(self.B, self.device, stats_ring)
+        self.ws.set_global_step(global_step)
+        self.pos = int(global_step) % self.nbatches  # next batch (host mirror)
+        self.pending = False
+        self.max_graph_steps = int(max_graph_steps)
+        self._graphs = {}
+        self._pool = None
+
+    # -- state --------------------------------------------------------------
+    @property
+    def direct(self):
+        """Single-GPU mode: SGD apply fused into the backward kernel."""
+        return self.allreduce is None and self.world_size == 1
+
+    @property
+    def params(self):
+        """Current parameters (excludes a pending, not yet applied gradient)."""
+        return self.bufs[self.cur]
+
+    def flush(self):
+        """Apply the pending gradient in place (p -= lr/N * grad)."""
+        if self.pending:
+            optim.sgd_(self.bufs[self.cur], self.grad, self.lr / self.world_size)
+            self.pending = False
+        return self.bufs[self.cur]
+
+    def load_params(self, p):
+        self.bufs[self.cur].copy_(p)
+        self.pending = False
+
+    def global_step(self) -> int:
+        return self.ws.global_step()
+
+    def batch(self, i):
+        sl = slice(i * self.B, (i + 1) * self.B)
+        return self.x[sl], self.labels[sl]
+
+    # -- one step (eager) -----------------------------------------------------
+    def _step_launches(self):
+        xb, yb = self.batch(self.pos)
+        self.pos = (self.pos + 1) % self.nbatches
+        if self.direct:
+            mlp_step.step_direct(self.bufs[self.cur], xb, yb, self.ws, self.lr)
+            return
+        cur = self.bufs[self.cur]
+        if self.pending:
+            mlp_step.step_grad(cur, xb, yb, self.ws, self.grad, prev_grad=self.grad,
+                               lr=self.lr / self.world_size, p_new=self.bufs[self.cur ^ 1])
+            self.cur ^= 1
+        else:
+            mlp_step.step_grad(cur, xb, yb, self.ws, self.grad)
+        if self.allreduce is not None:
+            self.allreduce(self.grad)
+        self.pending = True
+
+    def step(self):
+        self._step_launches()
+
+    # -- hipGraph capture/replay ---------------------------------------------
+    def _graph(self, n):
+        """Graph of ``n`` steps starting at batch ``self.pos`` and parity ``self.cur``.
+
+        Capture records without executing, so only the host mirrors (batch
+        position, ping-pong parity, pending flag) move during capture; they are
+        restored afterwards and advanced by the caller at replay.
+        """
+        key = (n, self.pos, self.cur)
+        g = self._graphs.get(key)
+        if g is None:
+            pos, cur, pend = self.pos, self.cur, self.pending
+            assert self.direct or pend
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, pool=self._pool, stream=s):
+                    for _ in range(n):
+                        self._step_launches()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._pool = g.pool()
+            self.pos, self.cur, self.pending = pos, cur, pend
+            self._graphs[key] = g
+        return g
+
+    def _plan(self, steps):
+        """Split ``steps`` into epoch-aligned graph chunks -> list of n."""
+        out, pos = [], self.pos
+        while steps > 0:
+            n = min(steps, self.nbatches - pos, self.max_graph_steps)
+            out.append(n)
+            pos = (pos + n) % self.nbatches
+            steps -= n
+        return out
+
+    def run(self, steps, use_graph=True):
+        """Run ``steps`` training steps (epoch-aligned hipGraph replays)."""
+        steps = int(steps)
+        if not use_graph:
+            for _ in range(steps):
+                self._step_launches()
+            return
+        if steps > 0 and not self.direct and not self.pending:
+            self._step_launches()  # the first DP step has nothing to apply
+            steps -= 1
+        for n in self._plan(steps):
+            self._graph(n).replay()
+            self.pos = (self.pos + n) % self.nbatches
+            if not self.direct:
+                self.cur ^= n & 1
+
+    def prepare(self, steps):
+        """Capture (not run) every graph a following ``run(steps)`` replays."""
+        steps = int(steps)
+        if steps > 0 and not self.direct and not self.pending:
+            raise RuntimeError("prepare() in DP mode needs one eager step first")
+        pos, cur = self.pos, self.cur
+        for n in self._plan(steps):
+            self._graph(n)
+            self.pos = (self.pos + n) % self.nbatches
+            if not self.direct:
+                self.cur ^= n & 1
+        self.pos, self.cur = pos, cur
+
+    # -- observability ------------------------------------------------------
+    def stats(self, step=None):
+        """(loss, accuracy) recorded by the kernel for ``step`` (default: last)."""
+        s = (self.global_step() - 1) if step is None else int(step)
+        v = self.ws.stats[s % self.ws.stats_ring].tolist()
+        return float(v[0]), float(v[1])
+
+    def stats_range(self, start, end):
+        """Loss/accuracy for steps [start, end) as a CPU tensor [n, 2]."""
+        ring = self.ws.stats_ring
+        if end - start > ring:
+            start = end - ring
+        idx = torch.arange(start, end) % ring
+        return self.ws.stats[idx.to(self.device)].cpu()
+
+
+def benchmark_steps(trainer, steps, warmup, barrier=None, use_graph=True):
+    """Time exactly ``steps`` steps after ``warmup`` (synchronised both sides)."""
+    trainer.run(warmup, use_graph)
+    if use_graph:
+        trainer.prepare(steps)
+    if barrier:
+        barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    trainer.run(steps, use_graph)
+    torch.cuda.synchronize()
+    if barrier:
+        barrier()
+    return time.perf_counter() - t0
