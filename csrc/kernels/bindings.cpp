@@ -17,13 +17,14 @@ namespace py = pybind11;
 
 namespace dtfx {
 void mlp_fwd_launch(const float*, const float*, float, float*, const float*, float*, int,
-                    hipStream_t);
+                    hipStream_t, unsigned long long*);
 void mlp_head_launch(const float*, const float*, float, float*, const int*, float*, int,
-                     hipStream_t);
+                     hipStream_t, unsigned long long*);
 void mlp_wgrad_launch(float*, float, float*, const float*, float*, int*, float*, int, int,
-                      hipStream_t);
+                      hipStream_t, unsigned long long*);
 long long mlp_workspace_floats(int);
 void calib_launch(int, int, int, const int*, const float*, float*, hipStream_t);
+void clock_probe_launch(int, int, unsigned long long*, float*, hipStream_t);
 void gemm_f32_launch(bool, bool, int, int, int, float, const float*, int, const float*, int,
                      float, float*, int, const float*, int, const float*, int, bool, hipStream_t);
 void colsum_launch(int, int, const float*, int, float, float*, hipStream_t);
@@ -52,20 +53,24 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("mlp_workspace_floats", &dtfx::mlp_workspace_floats);
   m.def("mlp_fwd", [](uintptr_t p_old, uintptr_t grad, float lr, uintptr_t p_new, uintptr_t x,
-                      uintptr_t ws, int B, uintptr_t s) {
+                      uintptr_t ws, int B, uintptr_t s, uintptr_t tr) {
     dtfx::mlp_fwd_launch(P<const float>(p_old), P<const float>(grad), lr, P<float>(p_new),
-                         P<const float>(x), P<float>(ws), B, S(s));
-  });
+                         P<const float>(x), P<float>(ws), B, S(s), P<unsigned long long>(tr));
+  }, py::arg("p_old"), py::arg("grad"), py::arg("lr"), py::arg("p_new"), py::arg("x"),
+     py::arg("ws"), py::arg("B"), py::arg("stream"), py::arg("trace") = 0);
   m.def("mlp_head", [](uintptr_t p_old, uintptr_t grad, float lr, uintptr_t p_new, uintptr_t lab,
-                       uintptr_t ws, int B, uintptr_t s) {
+                       uintptr_t ws, int B, uintptr_t s, uintptr_t tr) {
     dtfx::mlp_head_launch(P<const float>(p_old), P<const float>(grad), lr, P<float>(p_new),
-                          P<const int>(lab), P<float>(ws), B, S(s));
-  });
+                          P<const int>(lab), P<float>(ws), B, S(s), P<unsigned long long>(tr));
+  }, py::arg("p_old"), py::arg("grad"), py::arg("lr"), py::arg("p_new"), py::arg("labels"),
+     py::arg("ws"), py::arg("B"), py::arg("stream"), py::arg("trace") = 0);
   m.def("mlp_wgrad", [](uintptr_t p, float lr, uintptr_t grad, uintptr_t x, uintptr_t ws,
-                        uintptr_t ctr, uintptr_t stats, int ring, int B, uintptr_t s) {
+                        uintptr_t ctr, uintptr_t stats, int ring, int B, uintptr_t s,
+                        uintptr_t tr) {
     dtfx::mlp_wgrad_launch(P<float>(p), lr, P<float>(grad), P<const float>(x), P<float>(ws),
-                           P<int>(ctr), P<float>(stats), ring, B, S(s));
-  });
+                           P<int>(ctr), P<float>(stats), ring, B, S(s), P<unsigned long long>(tr));
+  }, py::arg("p"), py::arg("lr"), py::arg("grad"), py::arg("x"), py::arg("ws"), py::arg("ctr"),
+     py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"), py::arg("trace") = 0);
   m.def("gemm_f32", [](bool ta, bool tb, int M, int N, int K, float alpha, uintptr_t A, int lda,
                        uintptr_t B, int ldb, float beta, uintptr_t C, int ldc, uintptr_t bias,
                        int act, uintptr_t aux, int ldaux, bool act_grad, uintptr_t s) {
@@ -121,6 +126,9 @@ PYBIND11_MODULE(_hip, m) {
                     uintptr_t s) {
     dtfx::calib_launch(mode, grid, block, P<const int>(ctr), P<const float>(data), P<float>(out),
                        S(s));
+  });
+  m.def("clock_probe", [](int iters, int grid, uintptr_t out2, uintptr_t sink, uintptr_t s) {
+    dtfx::clock_probe_launch(iters, grid, P<unsigned long long>(out2), P<float>(sink), S(s));
   });
   m.def("device_count", []() {
     int n = 0;

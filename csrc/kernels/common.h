@@ -32,10 +32,22 @@ __device__ __forceinline__ float sigmoidf_(float z) {
   return e / (1.f + e);
 }
 
+// DPP wave reductions (VALU lane moves, no LDS round trip as __shfl_xor's
+// ds_bpermute needs): quad_perm xor1/xor2, row_ror 4/8 -> every lane holds its
+// 16-lane row sum; row_bcast15/31 fold rows into lane 63; readlane -> SGPR.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+  v += dpp_f<0xB1>(v);        // quad_perm(1,0,3,2)
+  v += dpp_f<0x4E>(v);        // quad_perm(2,3,0,1)
+  v += dpp_f<0x124>(v);       // row_ror:4
+  v += dpp_f<0x128>(v);       // row_ror:8
+  v += dpp_f<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f<0x143, 0xC>(v);  // row_bcast:31 -> rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
 __device__ __forceinline__ float wave_max(float v) {
@@ -45,6 +57,16 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+// Diagnostic stamps (trace builds only): 100 MHz constant-rate wall clock,
+// comparable across CUs/XCDs.  STAMP waits for this wave's outstanding memory
+// ops first, so each stamp marks "everything issued before has landed".
+__device__ __forceinline__ void trace_stamp(unsigned long long* tr, int slot) {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) tr[slot] = t;
+}
 
 // Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5,
 // "XCD swizzle must be bijective"): blocks that the dispatcher deals to the

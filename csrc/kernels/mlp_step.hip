@@ -82,10 +82,12 @@ __device__ __forceinline__ float4 f4(const float* p) { return *reinterpret_cast<
 // ---------------------------------------------------------------------------
 // K1: partial z1 over one K slice (+ deferred W1 apply)
 // ---------------------------------------------------------------------------
-template <bool APPLY>
+template <bool APPLY, bool TRACE>
 __global__ __launch_bounds__(64) void mlp_fwd_kernel(
     const float* __restrict__ p_old, const float* __restrict__ grad, float lr,
-    float* __restrict__ p_new, const float* __restrict__ x, Bufs w, int B) {
+    float* __restrict__ p_new, const float* __restrict__ x, Bufs w, int B,
+    unsigned long long* __restrict__ tr) {
+  if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 0);
   const int RT = (B + 15) >> 4, BP = RT * 16;
   const int rt = blockIdx.x % RT, jt = (blockIdx.x / RT) % HT, ks = blockIdx.x / (RT * HT);
   const int lane = threadIdx.x, r = lane & 15, q = lane >> 4;
@@ -96,16 +98,33 @@ __global__ __launch_bounds__(64) void mlp_fwd_kernel(
   const float* xr = x + (size_t)(rv ? row : 0) * D + k0;
   const size_t woff = OFF_W1 + (size_t)(cv ? col : 0) * D + k0;
 
+  // Loads are unconditional (clamped rows/cols) and masked after the fact:
+  // a guarded load becomes its own exec-masked branch in the ISA.
+  const float rm = rv ? 1.f : 0.f, cm = cv ? 1.f : 0.f;
   float4 xa[KW / 16], wa[KW / 16];
 #pragma unroll
   for (int g = 0; g < KW / 16; ++g) {
-    xa[g] = rv ? f4(xr + g * 16) : make_float4(0, 0, 0, 0);
-    wa[g] = cv ? f4(p_old + woff + g * 16) : make_float4(0, 0, 0, 0);
+    xa[g] = f4(xr + g * 16);
+    wa[g] = f4(p_old + woff + g * 16);
+  }
+  float4 ga[KW / 16];
+  if (APPLY) {
+#pragma unroll
+    for (int g = 0; g < KW / 16; ++g) ga[g] = f4(grad + woff + g * 16);
+  }
+  // Keep every load above this point in flight together: without the fence
+  // hipcc sinks them into the MFMA chain as 3-4 serial vmcnt(0) round trips.
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int g = 0; g < KW / 16; ++g) {
+    xa[g].x *= rm; xa[g].y *= rm; xa[g].z *= rm; xa[g].w *= rm;
+    wa[g].x *= cm; wa[g].y *= cm; wa[g].z *= cm; wa[g].w *= cm;
   }
   if (APPLY) {
 #pragma unroll
     for (int g = 0; g < KW / 16; ++g) {
-      const float4 gg = cv ? f4(grad + woff + g * 16) : make_float4(0, 0, 0, 0);
+      float4 gg = ga[g];
+      gg.x *= cm; gg.y *= cm; gg.z *= cm; gg.w *= cm;
       wa[g].x -= lr * gg.x;
       wa[g].y -= lr * gg.y;
       wa[g].z -= lr * gg.z;
@@ -113,6 +132,7 @@ __global__ __launch_bounds__(64) void mlp_fwd_kernel(
       if (rt == 0 && cv) *reinterpret_cast<float4*>(p_new + woff + g * 16) = wa[g];
     }
   }
+  if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 1);
   f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
   for (int g = 0; g < KW / 16; ++g) {
@@ -122,60 +142,96 @@ __global__ __launch_bounds__(64) void mlp_fwd_kernel(
     acc1 = mfma16x16x4(xa[g].w, wa[g].w, acc1);
   }
   float* out = w.slab + ((size_t)ks * BP + rt * 16 + q * 4) * HP + jt * 16 + r;
+  if (TRACE) {
+    asm volatile("" ::"v"(acc0[0]), "v"(acc1[0]));
+    trace_stamp(tr, blockIdx.x * 4 + 2);
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) out[(size_t)i * HP] = acc0[i] + acc1[i];
+  if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 3);
 }
 
 // ---------------------------------------------------------------------------
 // K2: per-row head (one wave per batch row)
 // ---------------------------------------------------------------------------
-template <bool APPLY>
+template <bool APPLY, bool TRACE>
 __global__ __launch_bounds__(64) void mlp_head_kernel(
     const float* __restrict__ p_old, const float* __restrict__ grad, float lr,
-    float* __restrict__ p_new, const int* __restrict__ labels, Bufs w, int B) {
+    float* __restrict__ p_new, const int* __restrict__ labels, Bufs w, int B,
+    unsigned long long* __restrict__ tr) {
+  if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 0);
   const int BP = ((B + 15) >> 4) * 16;
   const int row = blockIdx.x, lane = threadIdx.x;
   const int y = labels[row];
   const bool publish = APPLY && row == 0;
 
-  float hv[2], w2[2][C];
+  // All loads first, unconditional (j clamped to < H), masked afterwards.
+  float hv[2], w2[2][C], zs[2], b1v[2], b2v[C];
+  int jj[2];
+  bool jv[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int j = lane + 64 * u;
-    hv[u] = 0.f;
+    jv[u] = j < H;
+    jj[u] = jv[u] ? j : H - 1;
+    zs[u] = 0.f;
 #pragma unroll
-    for (int c = 0; c < C; ++c) w2[u][c] = 0.f;
-    if (j < H) {
-      float z = 0.f;
+    for (int s = 0; s < KS; ++s) zs[u] += w.slab[((size_t)s * BP + row) * HP + jj[u]];
+    b1v[u] = p_old[OFF_B1 + jj[u]];
 #pragma unroll
-      for (int s = 0; s < KS; ++s) z += w.slab[((size_t)s * BP + row) * HP + j];
-      float b1 = p_old[OFF_B1 + j];
-      if (APPLY) {
-        b1 -= lr * grad[OFF_B1 + j];
-        if (publish) p_new[OFF_B1 + j] = b1;
-      }
+    for (int c = 0; c < C; ++c) w2[u][c] = p_old[OFF_W2 + c * H + jj[u]];
+  }
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        float wv = p_old[OFF_W2 + c * H + j];
-        if (APPLY) {
-          wv -= lr * grad[OFF_W2 + c * H + j];
-          if (publish) p_new[OFF_W2 + c * H + j] = wv;
+  for (int c = 0; c < C; ++c) b2v[c] = p_old[OFF_B2 + c];
+  float gb1[2], gw2[2][C], gb2[C];
+  if (APPLY) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      gb1[u] = grad[OFF_B1 + jj[u]];
+#pragma unroll
+      for (int c = 0; c < C; ++c) gw2[u][c] = grad[OFF_W2 + c * H + jj[u]];
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) gb2[c] = grad[OFF_B2 + c];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // all loads in flight together
+  if (APPLY) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      b1v[u] -= lr * gb1[u];
+#pragma unroll
+      for (int c = 0; c < C; ++c) w2[u][c] -= lr * gw2[u][c];
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) b2v[c] -= lr * gb2[c];
+    if (publish) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (jv[u]) {
+          p_new[OFF_B1 + jj[u]] = b1v[u];
+#pragma unroll
+          for (int c = 0; c < C; ++c) p_new[OFF_W2 + c * H + jj[u]] = w2[u][c];
         }
-        w2[u][c] = wv;
+      if (lane < C) {
+        float b2l = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) b2l = (lane == c) ? b2v[c] : b2l;
+        p_new[OFF_B2 + lane] = b2l;
       }
-      hv[u] = sigmoidf_(z + b1);
-      w.hbuf[(size_t)row * HP + j] = hv[u];
     }
   }
-  // logits = h . W2 + b2 (wave reductions; every lane ends with all 10)
+  if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 1);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    hv[u] = jv[u] ? sigmoidf_(zs[u] + b1v[u]) : 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) w2[u][c] = jv[u] ? w2[u][c] : 0.f;
+    if (jv[u]) w.hbuf[(size_t)row * HP + jj[u]] = hv[u];
+  }
+  // logits = h . W2 + b2 (DPP wave reductions; every lane ends with all 10)
   float lg[C];
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    float b2 = p_old[OFF_B2 + c];
-    if (APPLY) b2 -= lr * grad[OFF_B2 + c];
-    lg[c] = wave_sum(hv[0] * w2[0][c] + hv[1] * w2[1][c]) + b2;
-  }
-  if (publish && lane < C) p_new[OFF_B2 + lane] = p_old[OFF_B2 + lane] - lr * grad[OFF_B2 + lane];
+  for (int c = 0; c < C; ++c) lg[c] = wave_sum(hv[0] * w2[0][c] + hv[1] * w2[1][c]) + b2v[c];
 
   float m = lg[0];
   int am = 0;
@@ -202,6 +258,7 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
       w.dz1T[(size_t)j * BP + row] = dh * hv[u] * (1.f - hv[u]);
     }
   }
+  if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 2);
   float mydl = 0.f;
 #pragma unroll
   for (int c = 0; c < C; ++c) mydl = (lane == c) ? dl[c] : mydl;
@@ -210,18 +267,25 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     w.rowstat[2 * row] = m + __logf(se) - ly;  // xent of this row
     w.rowstat[2 * row + 1] = (am == y) ? 1.f : 0.f;
   }
+  if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 3);
 }
 
 // ---------------------------------------------------------------------------
 // K3: weight gradients (+ fused SGD apply in direct mode)
 // ---------------------------------------------------------------------------
-template <bool DIRECT>
+// NGT > 0: batch padded to NGT*16 rows at compile time (branch-free loads);
+// NGT == 0: generic (runtime NG, guarded loops).
+template <bool DIRECT, bool TRACE, int NGT>
 __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
     float* __restrict__ p, float lr, float* __restrict__ grad, const float* __restrict__ x,
-    Bufs w, int* __restrict__ ctr, float* __restrict__ stats, int stats_ring, int B) {
-  const int BP = ((B + 15) >> 4) * 16, NG = BP / 16;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-  constexpr int MAXG = MAXB / 16;
+    Bufs w, int* __restrict__ ctr, float* __restrict__ stats, int stats_ring, int B,
+    unsigned long long* __restrict__ tr) {
+  const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
+  const int NG = NGT > 0 ? NGT : BP / 16;
+  // readfirstlane: make the wave id provably uniform (scalar branches, not exec masks)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  constexpr int MAXG = NGT > 0 ? NGT : MAXB / 16;
   constexpr int FG = (FT + 3) / 4;  // 13 feature groups of 4 waves
   const int bid = blockIdx.x;
 
@@ -229,6 +293,8 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
     // ---- dW1^T tile (jt, kt) = dz1T[jt] . x[:, kt], one tile per wave ------
     const int jt = bid / FG, kt = (bid % FG) * 4 + wave;
     if (kt >= FT) return;
+    unsigned long long* trw = tr + (size_t)(bid * 4 + wave) * 4;
+    if (TRACE) trace_stamp(trw, 0);
     const float* xc = x + kt * 16 + r;
     const float* a = w.dz1T + (size_t)(jt * 16 + r) * BP + q * 4;
     float4 av[MAXG];
@@ -239,8 +305,8 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
         av[g] = f4(a + g * 16);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int b = g * 16 + q * 4 + e;
-          xv[g][e] = (b < B) ? xc[(size_t)b * D] : 0.f;
+          const int b = g * 16 + q * 4 + e;  // rows >= B: dz1T is zero there
+          xv[g][e] = xc[(size_t)(b < B ? b : B - 1) * D];
         }
       }
     }
@@ -249,9 +315,11 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int j = jt * 16 + q * 4 + i;
-        pw[i] = (j < H) ? p[OFF_W1 + (size_t)j * D + kt * 16 + r] : 0.f;
+        pw[i] = p[OFF_W1 + (size_t)(j < H ? j : H - 1) * D + kt * 16 + r];
       }
     }
+    __builtin_amdgcn_sched_barrier(0);  // all loads in flight together
+    if (TRACE) trace_stamp(trw, 1);
     f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
     for (int g = 0; g < MAXG; ++g) {
@@ -261,6 +329,10 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
         acc0 = mfma16x16x4(av[g].z, xv[g][2], acc0);
         acc1 = mfma16x16x4(av[g].w, xv[g][3], acc1);
       }
+    }
+    if (TRACE) {
+      asm volatile("" ::"v"(acc0[0]), "v"(acc1[0]));
+      trace_stamp(trw, 2);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -272,6 +344,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
         else grad[off] = gv;
       }
     }
+    if (TRACE) trace_stamp(trw, 3);
     return;
   }
 
@@ -306,14 +379,44 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
   float4 av[MAXG];
   float bv[MAXG][4];
 #pragma unroll
-  for (int g = 0; g < MAXG; ++g) {
-    if (g < NG) {
-      av[g] = f4(A + g * 16);
+  for (int g = 0; g < MAXG; ++g)
+    if (g < NG) av[g] = f4(A + g * 16);
+  if (wave == 0) {  // one uniform branch around the whole B-operand load block
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        bv[g][e] = (wave == 0) ? hb[(size_t)(g * 16 + q * 4 + e) * HP] : 1.f;
-    }
+    for (int g = 0; g < MAXG; ++g)
+      if (g < NG)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[g][e] = hb[(size_t)(g * 16 + q * 4 + e) * HP];
+  } else {
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[g][e] = 1.f;
   }
+  __builtin_amdgcn_sched_barrier(0);  // all loads in flight together
+  // Destination offsets (and, in direct mode, the current values) resolved
+  // before the MFMAs so the epilogue is a pure store.
+  size_t off[4];
+  bool ok[4];
+  float pv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (wave == 0) {  // C[c = q*4+i][j = jt*16 + r] -> dW2t[c][j]
+      const int c = q * 4 + i, j = jt * 16 + r;
+      ok[i] = c < C && j < H;
+      off[i] = OFF_W2 + (ok[i] ? c * H + j : 0);
+    } else if (wave == 1) {  // C[j = jt*16 + q*4+i][*] -> db1[j]
+      const int j = jt * 16 + q * 4 + i;
+      ok[i] = r == 0 && j < H;
+      off[i] = OFF_B1 + (j < H ? j : 0);
+    } else {  // C[c = q*4+i][*] -> db2[c]
+      const int c = q * 4 + i;
+      ok[i] = r == 0 && c < C;
+      off[i] = OFF_B2 + (c < C ? c : 0);
+    }
+    if (DIRECT) pv[i] = p[off[i]];
+  }
+  __builtin_amdgcn_sched_barrier(0);
   // NB: padded batch columns of dz1T/dlT are zero, so multiplying by 1 is exact.
   f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
@@ -328,24 +431,9 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float v = acc0[i] + acc1[i];
-    size_t off = 0;
-    bool ok = false;
-    if (wave == 0) {  // C[c = q*4+i][j = jt*16 + r]
-      const int c = q * 4 + i, j = jt * 16 + r;
-      ok = c < C && j < H;
-      off = OFF_W2 + c * H + j;
-    } else if (wave == 1) {  // C[j = jt*16 + q*4+i][*]
-      const int j = jt * 16 + q * 4 + i;
-      ok = r == 0 && j < H;
-      off = OFF_B1 + j;
-    } else {  // C[c = q*4+i][*]
-      const int c = q * 4 + i;
-      ok = r == 0 && c < C;
-      off = OFF_B2 + c;
-    }
-    if (ok) {
-      if (DIRECT) p[off] -= lr * v;
-      else grad[off] = v;
+    if (ok[i]) {
+      if (DIRECT) p[off[i]] = pv[i] - lr * v;
+      else grad[off[i]] = v;
     }
   }
 }
@@ -379,7 +467,7 @@ static void check_b(int B) {
 
 // K1: grad != nullptr => deferred apply (p_new must differ from p_old)
 void mlp_fwd_launch(const float* p_old, const float* grad, float lr, float* p_new, const float* x,
-                    float* ws, int B, hipStream_t stream) {
+                    float* ws, int B, hipStream_t stream, unsigned long long* tr) {
   using namespace mlp;
   check_b(B);
   const Bufs w = make_bufs(ws, B);
@@ -387,48 +475,64 @@ void mlp_fwd_launch(const float* p_old, const float* grad, float lr, float* p_ne
   dim3 grid(RT * HT * KS), block(64);
   if (grad) {
     if (!p_new || p_new == p_old) throw std::runtime_error("mlp_fwd: apply needs ping-pong p_new");
-    hipLaunchKernelGGL(mlp_fwd_kernel<true>, grid, block, 0, stream, p_old, grad, lr, p_new, x, w,
-                       B);
+    hipLaunchKernelGGL((mlp_fwd_kernel<true, false>), grid, block, 0, stream, p_old, grad, lr,
+                       p_new, x, w, B, tr);
+  } else if (tr) {
+    hipLaunchKernelGGL((mlp_fwd_kernel<false, true>), grid, block, 0, stream, p_old, p_old, 0.f,
+                       nullptr, x, w, B, tr);
   } else {
-    hipLaunchKernelGGL(mlp_fwd_kernel<false>, grid, block, 0, stream, p_old, p_old, 0.f, nullptr,
-                       x, w, B);
+    hipLaunchKernelGGL((mlp_fwd_kernel<false, false>), grid, block, 0, stream, p_old, p_old, 0.f,
+                       nullptr, x, w, B, tr);
   }
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
 void mlp_head_launch(const float* p_old, const float* grad, float lr, float* p_new,
-                     const int* labels, float* ws, int B, hipStream_t stream) {
+                     const int* labels, float* ws, int B, hipStream_t stream,
+                     unsigned long long* tr) {
   using namespace mlp;
   check_b(B);
   const Bufs w = make_bufs(ws, B);
   if (grad) {
     if (!p_new || p_new == p_old) throw std::runtime_error("mlp_head: apply needs ping-pong p_new");
-    hipLaunchKernelGGL(mlp_head_kernel<true>, dim3(B), dim3(64), 0, stream, p_old, grad, lr, p_new,
-                       labels, w, B);
+    hipLaunchKernelGGL((mlp_head_kernel<true, false>), dim3(B), dim3(64), 0, stream, p_old, grad,
+                       lr, p_new, labels, w, B, tr);
+  } else if (tr) {
+    hipLaunchKernelGGL((mlp_head_kernel<false, true>), dim3(B), dim3(64), 0, stream, p_old, p_old,
+                       0.f, nullptr, labels, w, B, tr);
   } else {
-    hipLaunchKernelGGL(mlp_head_kernel<false>, dim3(B), dim3(64), 0, stream, p_old, p_old, 0.f,
-                       nullptr, labels, w, B);
+    hipLaunchKernelGGL((mlp_head_kernel<false, false>), dim3(B), dim3(64), 0, stream, p_old, p_old,
+                       0.f, nullptr, labels, w, B, tr);
   }
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
 // K3: grad == nullptr => direct mode (p -= lr * g fused); else writes grad
 void mlp_wgrad_launch(float* p, float lr, float* grad, const float* x, float* ws, int* ctr,
-                      float* stats, int stats_ring, int B, hipStream_t stream) {
+                      float* stats, int stats_ring, int B, hipStream_t stream,
+                      unsigned long long* tr) {
   using namespace mlp;
   check_b(B);
   if (stats && stats_ring < 1) throw std::runtime_error("mlp_wgrad: stats_ring < 1");
   if (!ctr) throw std::runtime_error("mlp_wgrad: needs the global_step counter");
   const Bufs w = make_bufs(ws, B);
   dim3 grid(HT * ((FT + 3) / 4) + HT), block(256);
+  const int NG = (B + 15) / 16;
+  if (!grad && !p) throw std::runtime_error("mlp_wgrad: direct mode needs parameters");
+#define DTFX_WG(DIR, TR, NGT)                                                                 \
+  hipLaunchKernelGGL((mlp_wgrad_kernel<DIR, TR, NGT>), grid, block, 0, stream, p,          \
+                     DIR ? lr : 0.f, DIR ? nullptr : grad, x, w, ctr, stats, stats_ring, B, tr)
   if (grad) {
-    hipLaunchKernelGGL(mlp_wgrad_kernel<false>, grid, block, 0, stream, p, 0.f, grad, x, w, ctr,
-                       stats, stats_ring, B);
+    if (NG == 7) DTFX_WG(false, false, 7);
+    else DTFX_WG(false, false, 0);
+  } else if (tr) {
+    if (NG == 7) DTFX_WG(true, true, 7);
+    else DTFX_WG(true, true, 0);
   } else {
-    if (!p) throw std::runtime_error("mlp_wgrad: direct mode needs parameters");
-    hipLaunchKernelGGL(mlp_wgrad_kernel<true>, grid, block, 0, stream, p, lr, nullptr, x, w, ctr,
-                       stats, stats_ring, B);
+    if (NG == 7) DTFX_WG(true, false, 7);
+    else DTFX_WG(true, false, 0);
   }
+#undef DTFX_WG
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
