@@ -46,8 +46,12 @@ def main():
     ap.add_argument("--max_graph_steps", type=int, default=1024,
                     help="max steps per hipGraph (graphs are epoch-aligned)")
     ap.add_argument("--no_graph", action="store_true")
-    ap.add_argument("--comm", choices=["rccl", "native"], default="rccl")
+    ap.add_argument("--comm", choices=["native", "torch"], default="native",
+                    help="native: the framework's C++ RCCL communicator (gloo control plane); "
+                         "torch: torch.distributed nccl(=RCCL) process group")
     ap.add_argument("--dataset_size", type=int, default=55000)
+    ap.add_argument("--dp", action="store_true",
+                    help="use the data-parallel path (gradient all-reduce) even on 1 GPU")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -59,7 +63,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.comm == "torch":
+            dist.init_process_group("nccl", device_id=dev)
+        else:  # control plane over TCP/gloo; gradients over the native RCCL communicator
+            dist.init_process_group("gloo")
 
     # identical replicas: the counter-based Philox init gives every rank the
     # same parameters from the same seed (no broadcast needed; verified below)
@@ -68,25 +75,28 @@ def main():
 
     allreduce = None
     if world > 1:
-        if a.comm == "native":
-            from distributedtensorflowexample_amd.parallel.comm import NativeComm
+        from distributedtensorflowexample_amd.parallel.comm import NativeComm, TorchComm
 
-            comm = NativeComm.from_process_group()
-            allreduce = comm.allreduce_sum_
-        else:
-            def allreduce(g):
-                dist.all_reduce(g)
-
-        chk = params.double().sum().reshape(1)
+        comm = NativeComm.from_process_group() if a.comm == "native" else TorchComm()
+        allreduce = comm.allreduce_sum_
+        chk = params.double().sum().reshape(1).cpu()
         ref = chk.clone()
-        dist.broadcast(ref, 0)
-        if not torch.equal(chk, ref):
+        dist.broadcast(ref if a.comm == "native" else ref.to(dev), 0)
+        if not torch.equal(chk, ref.cpu()):
             raise RuntimeError("replicas are not identical after init")
 
+    if world == 1 and a.dp:  # 1-rank communicator: exercises the sync-DP path on one GPU
+        from distributedtensorflowexample_amd.parallel.comm import NativeComm
+
+        comm = NativeComm(0, 1, store=dist.HashStore())
+        allreduce = comm.allreduce_sum_
     tr = FusedMLPTrainer(params, x, y, batch_size=a.batch_size, learning_rate=a.learning_rate,
                          allreduce=allreduce, world_size=world,
                          max_graph_steps=a.max_graph_steps)
-    barrier = (lambda: dist.barrier(device_ids=[local])) if world > 1 else None
+    if world > 1:
+        barrier = dist.barrier if a.comm == "native" else (lambda: dist.barrier(device_ids=[local]))
+    else:
+        barrier = None
     use_graph = not a.no_graph
 
     tr.run(a.warmup, use_graph)
@@ -103,7 +113,8 @@ def main():
     elapsed = time.perf_counter() - t0
 
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = t if a.comm == "native" else t.to(dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss, acc = tr.stats()
@@ -129,7 +140,7 @@ def main():
                 "per_gpu_batch": a.batch_size,
                 "seq_len": None,
                 "parallelism": "dp%d" % world,
-                "comm": a.comm if world > 1 else "none",
+                "comm": a.comm if (world > 1 or a.dp) else "none",
                 "hipgraph": use_graph,
             },
             "final_loss": round(loss, 5),

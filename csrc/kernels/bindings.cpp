@@ -43,6 +43,8 @@ void act_bwd_launch(long long, int, const float*, const float*, float*, hipStrea
 void act_fwd_launch(long long, int, const float*, float*, hipStream_t);
 }  // namespace dtfx
 
+void register_rccl(py::module_& m);
+
 template <typename T>
 static inline T* P(uintptr_t a) { return reinterpret_cast<T*>(a); }
 static inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
@@ -130,6 +132,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("clock_probe", [](int iters, int grid, uintptr_t out2, uintptr_t sink, uintptr_t s) {
     dtfx::clock_probe_launch(iters, grid, P<unsigned long long>(out2), P<float>(sink), S(s));
   });
+  register_rccl(m);
   m.def("device_count", []() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -1,0 +1,144 @@
+// Native RCCL communicator (the sync-DP transport of the framework).
+//
+// Replaces the reference's gRPC parameter-server fabric (main.py:67-75,
+// worker.py:123) for synchronous data parallelism: one process per GPU, one
+// RCCL communicator, collectives enqueued on the caller's HIP stream (so a
+// hipGraph capture of a training step records them as graph nodes and no
+// Python runs per step).  RCCL rides xGMI between the MI355X of a node.
+//
+// The unique id is exchanged by the Python layer through the
+// torch.distributed TCP store (parallel/comm.py), so the control plane can be
+// gloo/TCP while all tensor traffic is RCCL.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <rccl/rccl.h>
+
+#include <memory>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+
+namespace {
+
+void check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess)
+    throw std::runtime_error(std::string("RCCL ") + what + ": " + ncclGetErrorString(r));
+}
+
+ncclDataType_t dtype_of(const std::string& d) {
+  if (d == "float32") return ncclFloat32;
+  if (d == "float16") return ncclFloat16;
+  if (d == "bfloat16") return ncclBfloat16;
+  if (d == "float64") return ncclFloat64;
+  if (d == "int32") return ncclInt32;
+  if (d == "int64") return ncclInt64;
+  if (d == "uint8") return ncclUint8;
+  throw std::runtime_error("rccl: unsupported dtype " + d);
+}
+
+ncclRedOp_t op_of(const std::string& o) {
+  if (o == "sum") return ncclSum;
+  if (o == "max") return ncclMax;
+  if (o == "min") return ncclMin;
+  if (o == "prod") return ncclProd;
+  if (o == "avg") return ncclAvg;
+  throw std::runtime_error("rccl: unsupported op " + o);
+}
+
+class RcclComm {
+ public:
+  RcclComm(py::bytes uid, int nranks, int rank, int device) : nranks_(nranks), rank_(rank) {
+    std::string s = uid;
+    if (s.size() != sizeof(ncclUniqueId)) throw std::runtime_error("rccl: bad unique id size");
+    ncclUniqueId id;
+    std::memcpy(&id, s.data(), sizeof(id));
+    if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("rccl: hipSetDevice failed");
+    check(ncclCommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
+  }
+  ~RcclComm() { destroy(); }
+
+  void destroy() {
+    if (comm_) {
+      ncclCommDestroy(comm_);
+      comm_ = nullptr;
+    }
+  }
+  ncclComm_t get() const {
+    if (!comm_) throw std::runtime_error("rccl: communicator destroyed");
+    return comm_;
+  }
+
+  void all_reduce(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt,
+                  const std::string& op, uintptr_t stream) {
+    check(ncclAllReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
+                        dtype_of(dt), op_of(op), get(), reinterpret_cast<hipStream_t>(stream)),
+          "ncclAllReduce");
+  }
+  void reduce_scatter(uintptr_t send, uintptr_t recv, size_t recv_count, const std::string& dt,
+                      const std::string& op, uintptr_t stream) {
+    check(ncclReduceScatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv),
+                            recv_count, dtype_of(dt), op_of(op), get(),
+                            reinterpret_cast<hipStream_t>(stream)),
+          "ncclReduceScatter");
+  }
+  void all_gather(uintptr_t send, uintptr_t recv, size_t send_count, const std::string& dt,
+                  uintptr_t stream) {
+    check(ncclAllGather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv),
+                        send_count, dtype_of(dt), get(), reinterpret_cast<hipStream_t>(stream)),
+          "ncclAllGather");
+  }
+  void broadcast(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt, int root,
+                 uintptr_t stream) {
+    check(ncclBroadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
+                        dtype_of(dt), root, get(), reinterpret_cast<hipStream_t>(stream)),
+          "ncclBroadcast");
+  }
+  void all_to_all(uintptr_t send, uintptr_t recv, size_t count_per_rank, const std::string& dt,
+                  size_t elem_size, uintptr_t stream) {
+    // grouped send/recv: rank r's slice i goes to rank i
+    const ncclDataType_t t = dtype_of(dt);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    check(ncclGroupStart(), "ncclGroupStart");
+    for (int peer = 0; peer < nranks_; ++peer) {
+      const char* sp = reinterpret_cast<const char*>(send) + peer * count_per_rank * elem_size;
+      char* rp = reinterpret_cast<char*>(recv) + peer * count_per_rank * elem_size;
+      check(ncclSend(sp, count_per_rank, t, peer, get(), s), "ncclSend");
+      check(ncclRecv(rp, count_per_rank, t, peer, get(), s), "ncclRecv");
+    }
+    check(ncclGroupEnd(), "ncclGroupEnd");
+  }
+  int nranks() const { return nranks_; }
+  int rank() const { return rank_; }
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int nranks_, rank_;
+};
+
+}  // namespace
+
+void register_rccl(py::module_& m) {
+  m.def("rccl_unique_id", []() {
+    ncclUniqueId id;
+    check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    return py::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
+  });
+  m.def("rccl_version", []() {
+    int v = 0;
+    ncclGetVersion(&v);
+    return v;
+  });
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init<py::bytes, int, int, int>(), py::arg("unique_id"), py::arg("nranks"),
+           py::arg("rank"), py::arg("device"))
+      .def("all_reduce", &RcclComm::all_reduce, py::arg("send"), py::arg("recv"), py::arg("count"),
+           py::arg("dtype") = "float32", py::arg("op") = "sum", py::arg("stream") = 0)
+      .def("reduce_scatter", &RcclComm::reduce_scatter)
+      .def("all_gather", &RcclComm::all_gather)
+      .def("broadcast", &RcclComm::broadcast)
+      .def("all_to_all", &RcclComm::all_to_all)
+      .def("destroy", &RcclComm::destroy)
+      .def_property_readonly("nranks", &RcclComm::nranks)
+      .def_property_readonly("rank", &RcclComm::rank);
+}

@@ -105,13 +105,13 @@ def build_hip(verbose=False, force=False):
         objs.append(obj)
         if force or not _newer(obj, [src] + headers):
             jobs.append(([hipcc, "-c", "-x", "hip", src, "-o", obj] + common, obj))
-    bind_src = os.path.join(src_dir, "bindings.cpp")
-    bind_obj = os.path.join(obj_dir, "bindings.o")
-    objs.append(bind_obj)
-    if force or not _newer(bind_obj, [bind_src] + headers):
-        inc = sum([["-I", d] for d in _pybind_includes()], [])
-        jobs.append(([hipcc, "-c", bind_src, "-o", bind_obj, "-O2", "-std=c++17", "-fPIC",
-                      "-fvisibility=hidden", "-D__HIP_PLATFORM_AMD__"] + inc, bind_obj))
+    inc = sum([["-I", d] for d in _pybind_includes()], [])
+    for cpp in sorted(glob.glob(os.path.join(src_dir, "*.cpp"))):  # host-side C++ (bindings, RCCL)
+        obj = os.path.join(obj_dir, os.path.basename(cpp) + ".o")
+        objs.append(obj)
+        if force or not _newer(obj, [cpp] + headers):
+            jobs.append(([hipcc, "-c", cpp, "-o", obj, "-O2", "-std=c++17", "-fPIC",
+                          "-fvisibility=hidden", "-D__HIP_PLATFORM_AMD__"] + inc, obj))
     _compile_all(jobs, verbose)
     out = os.path.join(PKG_DIR, "_hip" + EXT_SUFFIX)
     if force or jobs or not _newer(out, objs):
@@ -119,7 +119,7 @@ def build_hip(verbose=False, force=False):
         tl = _torch_lib_dir()
         if tl:
             link += ["-L" + tl, "-Wl,-rpath," + tl]
-        link += ["-lamdhip64"]
+        link += ["-lamdhip64", "-lrccl"]
         _run(link)
     return out
 
