@@ -53,6 +53,7 @@ struct Reader {
   const uint8_t* end;
   Reader(const void* d, size_t n) : p(static_cast<const uint8_t*>(d)), end(p + n) {}
   explicit Reader(const std::string& s) : Reader(s.data(), s.size()) {}
+  explicit Reader(std::string&&) = delete;  // would dangle: keep the bytes alive
   bool done() const { return p >= end; }
   uint64_t varint() {
     uint64_t v = 0;

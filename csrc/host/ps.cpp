@@ -1,0 +1,622 @@
+// TCP parameter server + client: the async between-graph-replication fabric of
+// the reference (TF gRPC MasterService/WorkerService hosting /job:ps
+// variables, main.py:66-75, worker.py:24-32, 75-85, 112-113, 131-141).
+//
+// Server (one per ps task): named variables (f32 or int64), created by the
+// chief, assigned (init/restore), then served to workers:
+//   PULL        -> bytes of a variable group            (sync_op, worker.py:84-85)
+//   PUSH_APPLY  -> var -= lr * grad, lock-free Hogwild  (ApplyGradientDescent,
+//                  use_locking=False, worker.py:79) or per-variable mutex
+//   FETCH_ADD   -> atomic int64 add, returns old value  (AssignAdd global_step,
+//                  worker.py:32, 141)
+//   UNINIT      -> which of these are uninitialized     (report_uninitialized_
+//                  variables, the Supervisor ready_op, worker.py:112-113)
+// Variables are placed round-robin over ps tasks by the client, like
+// tf.train.replica_device_setter(ps_tasks) (worker.py:24).
+//
+// Wire format (little-endian): request = u32 len | u8 op | payload;
+// response = u32 len | u8 status (0 ok) | payload (error text if status != 0).
+// One thread per connection; the client pipelines requests to several ps
+// tasks (send all, then receive all).
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace {
+
+enum Op : uint8_t {
+  OP_CREATE = 1, OP_LOOKUP = 2, OP_ASSIGN = 3, OP_PULL = 4, OP_PUSH_APPLY = 5,
+  OP_FETCH_ADD = 6, OP_UNINIT = 7, OP_LIST = 8, OP_SHUTDOWN = 9, OP_PING = 10,
+  OP_STATS = 11
+};
+enum DType : uint8_t { DT_F32 = 0, DT_I64 = 1 };
+
+// ---------------------------------------------------------------- io helpers
+bool read_full(int fd, void* buf, size_t n) {
+  char* p = static_cast<char*>(buf);
+  while (n) {
+    const ssize_t r = ::recv(fd, p, n, 0);
+    if (r <= 0) return false;
+    p += r;
+    n -= static_cast<size_t>(r);
+  }
+  return true;
+}
+bool write_full(int fd, const void* buf, size_t n) {
+  const char* p = static_cast<const char*>(buf);
+  while (n) {
+    const ssize_t r = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (r <= 0) return false;
+    p += r;
+    n -= static_cast<size_t>(r);
+  }
+  return true;
+}
+void tune(int fd) {
+  int one = 1, buf = 8 << 20;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof(buf));
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof(buf));
+}
+
+struct Writer {
+  std::string b;
+  template <typename T> void put(T v) { b.append(reinterpret_cast<const char*>(&v), sizeof(T)); }
+  void str(const std::string& s) { put<uint16_t>(static_cast<uint16_t>(s.size())); b.append(s); }
+  void raw(const void* p, size_t n) { b.append(static_cast<const char*>(p), n); }
+};
+struct Reader {
+  const char* p;
+  const char* e;
+  template <typename T> T get() {
+    if (e - p < static_cast<ptrdiff_t>(sizeof(T))) throw std::runtime_error("ps: short message");
+    T v;
+    std::memcpy(&v, p, sizeof(T));
+    p += sizeof(T);
+    return v;
+  }
+  std::string str() {
+    const uint16_t n = get<uint16_t>();
+    if (e - p < n) throw std::runtime_error("ps: short string");
+    std::string s(p, n);
+    p += n;
+    return s;
+  }
+  const char* take(size_t n) {
+    if (static_cast<size_t>(e - p) < n) throw std::runtime_error("ps: short payload");
+    const char* q = p;
+    p += n;
+    return q;
+  }
+};
+
+// ---------------------------------------------------------------- server
+struct Var {
+  std::string name;
+  uint8_t dtype;
+  std::vector<int64_t> shape;
+  size_t count = 0;
+  std::vector<float> f;
+  std::atomic<int64_t> i{0};
+  std::atomic<bool> init{false};
+  std::mutex mu;
+  size_t nbytes() const { return dtype == DT_F32 ? count * 4 : 8; }
+};
+
+class PSServer {
+ public:
+  PSServer(const std::string& host, int port) : host_(host), port_(port) {}
+  ~PSServer() { stop(); }
+
+  void start() {
+    lfd_ = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (lfd_ < 0) throw std::runtime_error("ps: socket failed");
+    int one = 1;
+    setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons(static_cast<uint16_t>(port_));
+    a.sin_addr.s_addr = (host_.empty() || host_ == "0.0.0.0") ? INADDR_ANY : inet_addr(host_.c_str());
+    if (::bind(lfd_, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) {
+      ::close(lfd_);
+      lfd_ = -1;
+      throw std::runtime_error("ps: bind failed on port " + std::to_string(port_));
+    }
+    if (port_ == 0) {
+      socklen_t l = sizeof(a);
+      getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &l);
+      port_ = ntohs(a.sin_port);
+    }
+    ::listen(lfd_, 256);
+    running_ = true;
+    acc_ = std::thread([this] { accept_loop(); });
+  }
+
+  void stop() {
+    if (!running_.exchange(false)) return;
+    if (lfd_ >= 0) {
+      ::shutdown(lfd_, SHUT_RDWR);
+      ::close(lfd_);
+      lfd_ = -1;
+    }
+    if (acc_.joinable()) acc_.join();
+    std::vector<std::thread> ts;
+    {
+      std::lock_guard<std::mutex> g(cmu_);
+      for (int fd : conns_) ::shutdown(fd, SHUT_RDWR);
+      ts.swap(threads_);
+    }
+    for (auto& t : ts)
+      if (t.joinable()) t.join();
+  }
+
+  // block until a client sends SHUTDOWN or stop() is called
+  void join() {
+    while (running_ && !shutdown_req_) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    stop();
+  }
+
+  int port() const { return port_; }
+  size_t num_vars() {
+    std::lock_guard<std::mutex> g(vmu_);
+    return vars_.size();
+  }
+  py::dict stats() {
+    py::dict d;
+    d["pulls"] = pulls_.load();
+    d["pushes"] = pushes_.load();
+    d["bytes_in"] = bytes_in_.load();
+    d["bytes_out"] = bytes_out_.load();
+    return d;
+  }
+
+ private:
+  void accept_loop() {
+    while (running_) {
+      pollfd p{lfd_, POLLIN, 0};
+      if (::poll(&p, 1, 100) <= 0) continue;
+      const int fd = ::accept(lfd_, nullptr, nullptr);
+      if (fd < 0) continue;
+      tune(fd);
+      std::lock_guard<std::mutex> g(cmu_);
+      conns_.push_back(fd);
+      threads_.emplace_back([this, fd] { serve(fd); });
+    }
+  }
+
+  Var* var(uint32_t id) {
+    std::lock_guard<std::mutex> g(vmu_);
+    if (id >= vars_.size()) throw std::runtime_error("ps: bad variable id");
+    return vars_[id].get();
+  }
+
+  void serve(int fd) {
+    std::string req, resp;
+    while (running_) {
+      uint32_t len;
+      if (!read_full(fd, &len, 4)) break;
+      req.resize(len);
+      if (!read_full(fd, &req[0], len)) break;
+      bytes_in_ += len + 4;
+      Writer w;
+      uint8_t status = 0;
+      try {
+        handle(req, w);
+      } catch (const std::exception& e) {
+        status = 1;
+        w.b = e.what();
+      }
+      const uint32_t rl = static_cast<uint32_t>(w.b.size() + 1);
+      resp.clear();
+      resp.append(reinterpret_cast<const char*>(&rl), 4);
+      resp.push_back(static_cast<char>(status));
+      resp.append(w.b);
+      bytes_out_ += resp.size();
+      if (!write_full(fd, resp.data(), resp.size())) break;
+    }
+    ::close(fd);
+  }
+
+  void handle(const std::string& req, Writer& w) {
+    Reader r{req.data(), req.data() + req.size()};
+    const uint8_t op = r.get<uint8_t>();
+    switch (op) {
+      case OP_PING: break;
+      case OP_CREATE: {
+        const std::string name = r.str();
+        const uint8_t dt = r.get<uint8_t>();
+        const uint8_t nd = r.get<uint8_t>();
+        std::vector<int64_t> shape(nd);
+        size_t count = 1;
+        for (auto& d : shape) {
+          d = r.get<int64_t>();
+          count *= static_cast<size_t>(d);
+        }
+        std::lock_guard<std::mutex> g(vmu_);
+        auto it = by_name_.find(name);
+        if (it != by_name_.end()) {
+          Var* v = vars_[it->second].get();
+          if (v->dtype != dt || v->shape != shape)
+            throw std::runtime_error("ps: variable " + name + " re-created with another dtype/shape");
+          w.put<uint32_t>(it->second);
+          break;
+        }
+        auto v = std::make_unique<Var>();
+        v->name = name;
+        v->dtype = dt;
+        v->shape = shape;
+        v->count = dt == DT_F32 ? count : 1;
+        if (dt == DT_F32) v->f.assign(count, 0.f);
+        const uint32_t id = static_cast<uint32_t>(vars_.size());
+        vars_.push_back(std::move(v));
+        by_name_[name] = id;
+        w.put<uint32_t>(id);
+        break;
+      }
+      case OP_LOOKUP: {
+        const std::string name = r.str();
+        std::lock_guard<std::mutex> g(vmu_);
+        auto it = by_name_.find(name);
+        if (it == by_name_.end()) throw std::runtime_error("ps: no variable " + name);
+        w.put<uint32_t>(it->second);
+        break;
+      }
+      case OP_ASSIGN: {
+        Var* v = var(r.get<uint32_t>());
+        const char* d = r.take(v->nbytes());
+        std::lock_guard<std::mutex> g(v->mu);
+        if (v->dtype == DT_F32) std::memcpy(v->f.data(), d, v->nbytes());
+        else {
+          int64_t x;
+          std::memcpy(&x, d, 8);
+          v->i.store(x);
+        }
+        v->init.store(true);
+        break;
+      }
+      case OP_PULL: {
+        const uint32_t n = r.get<uint32_t>();
+        ++pulls_;
+        for (uint32_t k = 0; k < n; ++k) {
+          Var* v = var(r.get<uint32_t>());
+          if (!v->init.load()) throw std::runtime_error("ps: variable " + v->name + " is uninitialized");
+          if (v->dtype == DT_F32) w.raw(v->f.data(), v->nbytes());  // lock-free read (TF semantics)
+          else w.put<int64_t>(v->i.load());
+        }
+        break;
+      }
+      case OP_PUSH_APPLY: {
+        const float lr = r.get<float>();
+        const uint8_t locking = r.get<uint8_t>();
+        const uint32_t n = r.get<uint32_t>();
+        std::vector<Var*> vs(n);
+        for (auto& v : vs) v = var(r.get<uint32_t>());
+        ++pushes_;
+        for (Var* v : vs) {
+          if (v->dtype != DT_F32) throw std::runtime_error("ps: apply on non-float variable");
+          const float* g = reinterpret_cast<const float*>(r.take(v->nbytes()));
+          float* p = v->f.data();
+          const size_t cnt = v->count;
+          if (locking) {
+            std::lock_guard<std::mutex> lk(v->mu);
+            for (size_t i = 0; i < cnt; ++i) p[i] -= lr * g[i];
+          } else {
+            // Hogwild, as ApplyGradientDescent(use_locking=False): concurrent
+            // workers may interleave element updates.
+            for (size_t i = 0; i < cnt; ++i) p[i] -= lr * g[i];
+          }
+        }
+        break;
+      }
+      case OP_FETCH_ADD: {
+        Var* v = var(r.get<uint32_t>());
+        const int64_t d = r.get<int64_t>();
+        if (v->dtype != DT_I64) throw std::runtime_error("ps: fetch_add on non-int variable");
+        if (!v->init.load()) throw std::runtime_error("ps: variable " + v->name + " is uninitialized");
+        w.put<int64_t>(v->i.fetch_add(d));
+        break;
+      }
+      case OP_UNINIT: {
+        const uint32_t n = r.get<uint32_t>();
+        std::vector<uint32_t> bad;
+        for (uint32_t k = 0; k < n; ++k) {
+          const uint32_t id = r.get<uint32_t>();
+          if (!var(id)->init.load()) bad.push_back(id);
+        }
+        w.put<uint32_t>(static_cast<uint32_t>(bad.size()));
+        for (uint32_t id : bad) w.put<uint32_t>(id);
+        break;
+      }
+      case OP_LIST: {
+        std::lock_guard<std::mutex> g(vmu_);
+        w.put<uint32_t>(static_cast<uint32_t>(vars_.size()));
+        for (auto& v : vars_) {
+          w.str(v->name);
+          w.put<uint8_t>(v->dtype);
+          w.put<uint8_t>(static_cast<uint8_t>(v->shape.size()));
+          for (int64_t d : v->shape) w.put<int64_t>(d);
+          w.put<uint8_t>(v->init.load() ? 1 : 0);
+        }
+        break;
+      }
+      case OP_SHUTDOWN: shutdown_req_ = true; break;
+      default: throw std::runtime_error("ps: unknown op " + std::to_string(op));
+    }
+  }
+
+  std::string host_;
+  int port_;
+  int lfd_ = -1;
+  std::atomic<bool> running_{false}, shutdown_req_{false};
+  std::thread acc_;
+  std::mutex cmu_, vmu_;
+  std::vector<int> conns_;
+  std::vector<std::thread> threads_;
+  std::vector<std::unique_ptr<Var>> vars_;
+  std::map<std::string, uint32_t> by_name_;
+  std::atomic<uint64_t> pulls_{0}, pushes_{0}, bytes_in_{0}, bytes_out_{0};
+};
+
+// ---------------------------------------------------------------- client
+class PSClient {
+ public:
+  PSClient(std::vector<std::string> addrs, double connect_timeout_s) : addrs_(std::move(addrs)) {
+    for (auto& a : addrs_) fds_.push_back(connect_to(a, connect_timeout_s));
+  }
+  ~PSClient() { close(); }
+
+  void close() {
+    for (int& fd : fds_)
+      if (fd >= 0) {
+        ::close(fd);
+        fd = -1;
+      }
+  }
+  int num_tasks() const { return static_cast<int>(fds_.size()); }
+
+  // handle = task << 32 | id
+  int64_t create(const std::string& name, const std::string& dtype, std::vector<int64_t> shape,
+                 int task) {
+    Writer w;
+    w.put<uint8_t>(OP_CREATE);
+    w.str(name);
+    w.put<uint8_t>(dt(dtype));
+    w.put<uint8_t>(static_cast<uint8_t>(shape.size()));
+    for (int64_t d : shape) w.put<int64_t>(d);
+    std::string resp = locked_call(task, w.b);
+    Reader r{resp.data(), resp.data() + resp.size()};
+    return (static_cast<int64_t>(task) << 32) | r.get<uint32_t>();
+  }
+  int64_t lookup(const std::string& name, int task) {
+    Writer w;
+    w.put<uint8_t>(OP_LOOKUP);
+    w.str(name);
+    std::string resp = locked_call(task, w.b);
+    Reader r{resp.data(), resp.data() + resp.size()};
+    return (static_cast<int64_t>(task) << 32) | r.get<uint32_t>();
+  }
+  void assign(int64_t h, uintptr_t ptr, size_t nbytes) {
+    Writer w;
+    w.put<uint8_t>(OP_ASSIGN);
+    w.put<uint32_t>(static_cast<uint32_t>(h));
+    w.raw(reinterpret_cast<const void*>(ptr), nbytes);
+    locked_call(static_cast<int>(h >> 32), w.b);
+  }
+  // pull a group of variables into caller buffers (sizes in bytes)
+  void pull(std::vector<int64_t> hs, std::vector<uintptr_t> ptrs, std::vector<size_t> sizes) {
+    if (hs.size() != ptrs.size() || hs.size() != sizes.size())
+      throw std::runtime_error("ps pull: argument lengths differ");
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> lk(mu_);
+    std::vector<std::vector<size_t>> per(fds_.size());
+    for (size_t k = 0; k < hs.size(); ++k) per[hs[k] >> 32].push_back(k);
+    for (size_t t = 0; t < per.size(); ++t) {
+      if (per[t].empty()) continue;
+      Writer w;
+      w.put<uint8_t>(OP_PULL);
+      w.put<uint32_t>(static_cast<uint32_t>(per[t].size()));
+      for (size_t k : per[t]) w.put<uint32_t>(static_cast<uint32_t>(hs[k]));
+      send(static_cast<int>(t), w.b);
+    }
+    for (size_t t = 0; t < per.size(); ++t) {
+      if (per[t].empty()) continue;
+      std::string resp = recv(static_cast<int>(t));
+      size_t off = 0;
+      for (size_t k : per[t]) {
+        if (off + sizes[k] > resp.size()) throw std::runtime_error("ps pull: short response");
+        std::memcpy(reinterpret_cast<void*>(ptrs[k]), resp.data() + off, sizes[k]);
+        off += sizes[k];
+      }
+    }
+  }
+  // push gradients (f32) and apply var -= lr * grad on the owning ps tasks
+  void push_apply(std::vector<int64_t> hs, std::vector<uintptr_t> ptrs, std::vector<size_t> sizes,
+                  float lr, bool locking) {
+    if (hs.size() != ptrs.size() || hs.size() != sizes.size())
+      throw std::runtime_error("ps push: argument lengths differ");
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> lk(mu_);
+    std::vector<std::vector<size_t>> per(fds_.size());
+    for (size_t k = 0; k < hs.size(); ++k) per[hs[k] >> 32].push_back(k);
+    for (size_t t = 0; t < per.size(); ++t) {
+      if (per[t].empty()) continue;
+      Writer w;
+      w.put<uint8_t>(OP_PUSH_APPLY);
+      w.put<float>(lr);
+      w.put<uint8_t>(locking ? 1 : 0);
+      w.put<uint32_t>(static_cast<uint32_t>(per[t].size()));
+      for (size_t k : per[t]) w.put<uint32_t>(static_cast<uint32_t>(hs[k]));
+      for (size_t k : per[t]) w.raw(reinterpret_cast<const void*>(ptrs[k]), sizes[k]);
+      send(static_cast<int>(t), w.b);
+    }
+    for (size_t t = 0; t < per.size(); ++t)
+      if (!per[t].empty()) recv(static_cast<int>(t));
+  }
+  int64_t fetch_add(int64_t h, int64_t delta) {
+    Writer w;
+    w.put<uint8_t>(OP_FETCH_ADD);
+    w.put<uint32_t>(static_cast<uint32_t>(h));
+    w.put<int64_t>(delta);
+    std::string resp = locked_call(static_cast<int>(h >> 32), w.b);
+    Reader r{resp.data(), resp.data() + resp.size()};
+    return r.get<int64_t>();
+  }
+  std::vector<int64_t> uninitialized(std::vector<int64_t> hs) {
+    std::vector<int64_t> out;
+    std::vector<std::vector<int64_t>> per(fds_.size());
+    for (int64_t h : hs) per[h >> 32].push_back(h);
+    for (size_t t = 0; t < per.size(); ++t) {
+      if (per[t].empty()) continue;
+      Writer w;
+      w.put<uint8_t>(OP_UNINIT);
+      w.put<uint32_t>(static_cast<uint32_t>(per[t].size()));
+      for (int64_t h : per[t]) w.put<uint32_t>(static_cast<uint32_t>(h));
+      std::string resp = locked_call(static_cast<int>(t), w.b);
+      Reader r{resp.data(), resp.data() + resp.size()};
+      const uint32_t n = r.get<uint32_t>();
+      for (uint32_t k = 0; k < n; ++k)
+        out.push_back((static_cast<int64_t>(t) << 32) | r.get<uint32_t>());
+    }
+    return out;
+  }
+  py::list list_vars(int task) {
+    Writer w;
+    w.put<uint8_t>(OP_LIST);
+    std::string resp = locked_call(task, w.b);
+    Reader r{resp.data(), resp.data() + resp.size()};
+    py::list out;
+    const uint32_t n = r.get<uint32_t>();
+    for (uint32_t k = 0; k < n; ++k) {
+      std::string name = r.str();
+      const uint8_t d = r.get<uint8_t>();
+      const uint8_t nd = r.get<uint8_t>();
+      std::vector<int64_t> shape(nd);
+      for (auto& s : shape) s = r.get<int64_t>();
+      const bool init = r.get<uint8_t>() != 0;
+      out.append(py::make_tuple(name, d == DT_F32 ? "float32" : "int64", shape, init));
+    }
+    return out;
+  }
+  void ping(int task) {
+    Writer w;
+    w.put<uint8_t>(OP_PING);
+    locked_call(task, w.b);
+  }
+  void shutdown_server(int task) {
+    Writer w;
+    w.put<uint8_t>(OP_SHUTDOWN);
+    locked_call(task, w.b);
+  }
+
+ private:
+  static uint8_t dt(const std::string& s) {
+    if (s == "float32") return DT_F32;
+    if (s == "int64" || s == "int32") return DT_I64;
+    throw std::runtime_error("ps: unsupported dtype " + s);
+  }
+  static int connect_to(const std::string& addr, double timeout_s) {
+    const auto c = addr.rfind(':');
+    if (c == std::string::npos) throw std::runtime_error("ps: bad address " + addr);
+    const std::string host = addr.substr(0, c), port = addr.substr(c + 1);
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+    while (true) {
+      addrinfo hints{}, *res = nullptr;
+      hints.ai_family = AF_INET;
+      hints.ai_socktype = SOCK_STREAM;
+      if (getaddrinfo(host.c_str(), port.c_str(), &hints, &res) == 0 && res) {
+        const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+        if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
+          freeaddrinfo(res);
+          tune(fd);
+          return fd;
+        }
+        if (fd >= 0) ::close(fd);
+        freeaddrinfo(res);
+      }
+      if (std::chrono::steady_clock::now() > deadline)
+        throw std::runtime_error("ps: cannot connect to " + addr);
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));  // ps not up yet (run_*.sh sleep 1)
+    }
+  }
+  void send(int task, const std::string& payload) {
+    if (task < 0 || task >= static_cast<int>(fds_.size()) || fds_[task] < 0)
+      throw std::runtime_error("ps: bad task");
+    const uint32_t len = static_cast<uint32_t>(payload.size());
+    if (!write_full(fds_[task], &len, 4) || !write_full(fds_[task], payload.data(), payload.size()))
+      throw std::runtime_error("ps: connection to " + addrs_[task] + " lost (send)");
+  }
+  std::string recv(int task) {
+    uint32_t len;
+    if (!read_full(fds_[task], &len, 4))
+      throw std::runtime_error("ps: connection to " + addrs_[task] + " lost (recv)");
+    std::string resp(len, '\0');
+    if (!read_full(fds_[task], &resp[0], len))
+      throw std::runtime_error("ps: connection to " + addrs_[task] + " lost (recv body)");
+    if (resp.empty()) throw std::runtime_error("ps: empty response");
+    if (resp[0] != 0) throw std::runtime_error(resp.substr(1));
+    return resp.substr(1);
+  }
+  std::string call(int task, const std::string& payload) {
+    send(task, payload);
+    return recv(task);
+  }
+  // Thread-safe exchange; drops the GIL while blocked on the mutex and the socket.
+  std::string locked_call(int task, const std::string& payload) {
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> lk(mu_);
+    return call(task, payload);
+  }
+
+  std::vector<std::string> addrs_;
+  std::vector<int> fds_;
+  std::mutex mu_;  // one request/response exchange at a time (shared by Python threads)
+};
+
+}  // namespace
+
+void register_ps(py::module_& m) {
+  py::class_<PSServer>(m, "PSServer")
+      .def(py::init<const std::string&, int>(), py::arg("host") = "127.0.0.1", py::arg("port") = 0)
+      .def("start", &PSServer::start)
+      .def("stop", &PSServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def("join", &PSServer::join, py::call_guard<py::gil_scoped_release>())
+      .def("num_vars", &PSServer::num_vars)
+      .def("stats", &PSServer::stats)
+      .def_property_readonly("port", &PSServer::port);
+  py::class_<PSClient>(m, "PSClient")
+      .def(py::init<std::vector<std::string>, double>(), py::arg("addresses"),
+           py::arg("connect_timeout") = 60.0)
+      .def("create", &PSClient::create, py::arg("name"), py::arg("dtype"), py::arg("shape"),
+           py::arg("task"))
+      .def("lookup", &PSClient::lookup, py::arg("name"), py::arg("task"))
+      .def("assign", &PSClient::assign)
+      .def("pull", &PSClient::pull)
+      .def("push_apply", &PSClient::push_apply, py::arg("handles"), py::arg("ptrs"),
+           py::arg("sizes"), py::arg("lr"), py::arg("use_locking") = false)
+      .def("fetch_add", &PSClient::fetch_add)
+      .def("uninitialized", &PSClient::uninitialized)
+      .def("list_vars", &PSClient::list_vars)
+      .def("ping", &PSClient::ping)
+      .def("shutdown_server", &PSClient::shutdown_server)
+      .def("close", &PSClient::close)
+      .def_property_readonly("num_tasks", &PSClient::num_tasks);
+}

@@ -292,11 +292,13 @@ Entry parse_entry(const std::string& v) {
     const uint32_t f = tag >> 3, w = tag & 7;
     if (f == 1 && w == 0) e.dtype = static_cast<int>(r.varint());
     else if (f == 2 && w == 2) {
-      pb::Reader sr(r.bytes());
+      const std::string sbuf = r.bytes();
+      pb::Reader sr(sbuf);
       while (!sr.done()) {
         const uint64_t st = sr.varint();
         if ((st >> 3) == 2 && (st & 7) == 2) {
-          pb::Reader dr(sr.bytes());
+          const std::string dbuf = sr.bytes();
+          pb::Reader dr(dbuf);
           int64_t size = 0;
           while (!dr.done()) {
             const uint64_t dt = dr.varint();

@@ -1,0 +1,168 @@
+"""Synchronous data parallelism (``MirroredStrategy``-style), MI355X-first.
+
+Not in the reference (its only mode is async PS), but it is the north star of
+BASELINE.json: every replica computes gradients on its own batch, gradients
+are all-reduced over RCCL/xGMI and every replica applies the same averaged
+update, so replicas stay bit-identical.
+
+:class:`DistributedDataParallel` -- for arbitrary autograd models:
+
+* parameters are re-homed into ONE flat buffer per dtype (views), gradients
+  into a matching flat buffer, so optimizer kernels (ops/optim.py) and the
+  all-reduce work on contiguous memory;
+* the gradient buffer is cut into buckets (``bucket_mb``, default 32 MB -- big
+  enough that each of the 7 xGMI links per MI355X carries a large chunk,
+  small enough that the first bucket launches early in backward); buckets
+  follow reverse parameter order (the order autograd produces gradients);
+* a post-accumulate-grad hook per parameter counts arrivals; when a bucket
+  is complete its all-reduce is launched on a dedicated comm stream that
+  waits on the compute stream's event -- so communication overlaps the rest
+  of backward; ``finish()`` joins the comm stream before the optimizer.
+
+For the reference MLP itself, whose 318 KB gradient is produced by one fused
+kernel, bucketing buys nothing; ``train/fused_mlp.FusedMLPTrainer`` takes the
+all-reduce as a single graph-captured call instead.
+"""
+from __future__ import annotations
+
+import torch
+
+
+class DistributedDataParallel(torch.nn.Module):
+    def __init__(self, module, comm, bucket_mb=32.0, broadcast_init=True, average=True):
+        super().__init__()
+        self.module = module
+        self.comm = comm
+        self.world_size = comm.world_size
+        self.average = average
+        params = [p for p in module.parameters() if p.requires_grad]
+        if not params:
+            raise ValueError("no trainable parameters")
+        dev = params[0].device
+        dtype = params[0].dtype
+        if any(p.device != dev or p.dtype != dtype for p in params):
+            raise ValueError("DDP flat buffers need a single device and dtype")
+        self.device = dev
+        n = sum(p.numel() for p in params)
+        # 16-element alignment of every view keeps dwordx4 kernels legal
+        offs, off = [], 0
+        for p in params:
+            offs.append(off)
+            off += (p.numel() + 15) // 16 * 16
+        self.flat = torch.zeros(off, device=dev, dtype=dtype)
+        self.flat_grad = torch.zeros(off, device=dev, dtype=dtype)
+        for p, o in zip(params, offs):
+            self.flat[o:o + p.numel()].view_as(p).copy_(p.data)
+            p.data = self.flat[o:o + p.numel()].view_as(p)
+            p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
+        self.params, self.offsets, self.numel = params, offs, n
+        # buckets in reverse order (gradient production order)
+        cap = max(1, int(bucket_mb * 2 ** 20 / self.flat.element_size()))
+        self.buckets = []  # (lo, hi, [param idx])
+        cur, lo, hi = [], None, None
+        for i in reversed(range(len(params))):
+            o, e = offs[i], offs[i] + (params[i].numel() + 15) // 16 * 16
+            if cur and (max(hi, e) - min(lo, o)) > cap:
+                self.buckets.append((lo, hi, cur))
+                cur, lo, hi = [], None, None
+            cur.append(i)
+            lo = o if lo is None else min(lo, o)
+            hi = e if hi is None else max(hi, e)
+        if cur:
+            self.buckets.append((lo, hi, cur))
+        self.bucket_of = {}
+        for b, (_, _, idx) in enumerate(self.buckets):
+            for i in idx:
+                self.bucket_of[i] = b
+        self._pending = [0] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
+        self.comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self._hooks = []
+        for i, p in enumerate(params):
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        if broadcast_init and self.world_size > 1:
+            self.comm.broadcast_(self.flat, 0)
+        self.reset()
+
+    def _make_hook(self, i):
+        def hook(p):
+            b = self.bucket_of[i]
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self._launch(b)
+        return hook
+
+    def _launch(self, b):
+        lo, hi, _ = self.buckets[b]
+        view = self.flat_grad[lo:hi]
+        if self.comm_stream is not None:
+            self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.comm_stream):
+                self._reduce(view)
+        else:
+            self._reduce(view)
+        self._launched[b] = True
+
+    def _reduce(self, view):
+        if self.world_size == 1:
+            return
+        if self.average:
+            if hasattr(self.comm, "allreduce_avg_"):
+                self.comm.allreduce_avg_(view)
+            else:
+                self.comm.allreduce_sum_(view)
+                view.div_(self.world_size)
+        else:
+            self.comm.allreduce_sum_(view)
+
+    def reset(self):
+        """Zero gradients and re-arm the bucket counters (call before backward)."""
+        self.flat_grad.zero_()
+        for b, (_, _, idx) in enumerate(self.buckets):
+            self._pending[b] = len(idx)
+            self._launched[b] = False
+
+    zero_grad = reset
+
+    def finish(self):
+        """Launch any bucket whose hooks did not all fire; join the comm stream."""
+        for b in range(len(self.buckets)):
+            if not self._launched[b]:
+                self._launch(b)
+        if self.comm_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+
+    def forward(self, *a, **k):
+        return self.module(*a, **k)
+
+
+class MirroredStrategy:
+    """Thin strategy object: comm + replica bookkeeping (tf.distribute-like)."""
+
+    def __init__(self, comm):
+        self.comm = comm
+        self.num_replicas_in_sync = comm.world_size
+        self.rank = comm.rank
+
+    def wrap(self, module, **kw):
+        return DistributedDataParallel(module, self.comm, **kw)
+
+    def reduce_mean_(self, t):
+        if self.num_replicas_in_sync > 1:
+            self.comm.allreduce_sum_(t)
+            t.div_(self.num_replicas_in_sync)
+        return t
+
+    def broadcast_(self, t, root=0):
+        if self.num_replicas_in_sync > 1:
+            self.comm.broadcast_(t, root)
+        return t
+
+    def check_replicas_identical(self, t):
+        """Debug check: max over replicas of |t - t_rank0|."""
+        ref = t.detach().clone()
+        self.broadcast_(ref, 0)
+        d = (t.detach() - ref).abs().max().reshape(1).float()
+        if self.num_replicas_in_sync > 1:
+            self.comm.allreduce_max_(d)
+        return float(d.item())

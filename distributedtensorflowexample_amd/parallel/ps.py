@@ -1,0 +1,128 @@
+"""Asynchronous parameter-server data parallelism (between-graph replication).
+
+The reference's only strategy: every worker keeps a local copy
+of the model, pulls the global variables from the ps each step
+(``sync_op``, worker.py:81-85), computes gradients locally and pushes them
+to the ps, which applies them immediately with plain SGD (``train_op``,
+worker.py:70-79); ``global_step`` is incremented by a separate
+``AssignAdd`` (worker.py:32, 141).  Nothing synchronizes the workers, so
+gradients can be stale; updates are lock-free (``use_locking=False``).
+
+:func:`replica_device_setter` reproduces TF's placement: variables are
+assigned round-robin over the ps tasks in creation order.
+:class:`PSVariableStore` owns the global variables through the native C++
+client (``csrc/host/ps.cpp``): create/lookup, init/assign, uninitialized
+report (the Supervisor's ready_op), pull, push-and-apply, fetch-add.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from ..ops import host
+
+
+def replica_device_setter(ps_tasks, worker_device=None):
+    """Round-robin ps task chooser: call with the variable's creation index."""
+    ps_tasks = max(1, int(ps_tasks))
+
+    def place(index):
+        return int(index) % ps_tasks
+
+    place.ps_tasks = ps_tasks
+    place.worker_device = worker_device
+    return place
+
+
+class PSVariableStore:
+    """Global variables living on the ps job.
+
+    ``specs``: ordered list of (name, shape, dtype) with dtype 'float32' or
+    'int64'.  Float variables are exchanged through pinned host buffers.
+    """
+
+    def __init__(self, ps_addresses, specs, connect_timeout=120.0, setter=None):
+        self.client = host().PSClient(list(ps_addresses), float(connect_timeout))
+        self.specs = [(n, tuple(int(d) for d in s), dt) for n, s, dt in specs]
+        self.setter = setter or replica_device_setter(len(ps_addresses))
+        self.handles = {}
+        pin = torch.cuda.is_available()
+        self.bufs = {}
+        for n, s, dt in self.specs:
+            if dt == "float32":
+                b = torch.empty(s, dtype=torch.float32, pin_memory=pin)
+                self.bufs[n] = b
+        self._float_names = [n for n, _, dt in self.specs if dt == "float32"]
+
+    # -- bring-up ----------------------------------------------------------
+    def create(self):
+        """Chief: create every variable on its ps task (idempotent)."""
+        for i, (n, s, dt) in enumerate(self.specs):
+            self.handles[n] = self.client.create(n, dt, list(s), self.setter(i))
+        return self
+
+    def lookup(self, timeout=120.0, poll=0.05):
+        """Non-chief: wait until the chief has created the variables."""
+        t0 = time.time()
+        for i, (n, s, dt) in enumerate(self.specs):
+            while True:
+                try:
+                    self.handles[n] = self.client.lookup(n, self.setter(i))
+                    break
+                except RuntimeError:
+                    if time.time() - t0 > timeout:
+                        raise TimeoutError("ps variable %s never created" % n)
+                    time.sleep(poll)
+        return self
+
+    def uninitialized(self):
+        """report_uninitialized_variables (worker.py:112-113): list of names."""
+        inv = {h: n for n, h in self.handles.items()}
+        return [inv[h] for h in self.client.uninitialized(list(self.handles.values()))]
+
+    def assign(self, values):
+        """Assign {name: tensor/array/int} (init or restore)."""
+        for n, v in values.items():
+            h = self.handles[n]
+            if isinstance(v, torch.Tensor):
+                v = v.detach().cpu().numpy()
+            a = np.ascontiguousarray(np.asarray(v, dtype=np.float32 if n in self.bufs else np.int64))
+            self.client.assign(h, a.ctypes.data, a.nbytes)
+
+    # -- per-step traffic ---------------------------------------------------
+    def pull(self, names=None):
+        """Pull float variables into the pinned host buffers; returns them."""
+        names = names or self._float_names
+        bs = [self.bufs[n] for n in names]
+        self.client.pull([self.handles[n] for n in names], [b.data_ptr() for b in bs],
+                         [b.numel() * 4 for b in bs])
+        return {n: b for n, b in zip(names, bs)}
+
+    def push_apply(self, grads, lr, use_locking=False):
+        """{name: contiguous f32 CPU tensor} -> var -= lr * grad on the ps."""
+        names = list(grads)
+        gs = [grads[n] for n in names]
+        for g in gs:
+            if g.dtype != torch.float32 or g.device.type != "cpu" or not g.is_contiguous():
+                raise ValueError("push_apply needs contiguous f32 CPU tensors")
+        self.client.push_apply([self.handles[n] for n in names], [g.data_ptr() for g in gs],
+                               [g.numel() * 4 for g in gs], float(lr), bool(use_locking))
+
+    def fetch_add(self, name, delta=1):
+        return int(self.client.fetch_add(self.handles[name], int(delta)))
+
+    def read_int(self, name):
+        return self.fetch_add(name, 0)
+
+    def read_all(self):
+        """{name: CPU tensor} snapshot of every variable (the chief's Saver)."""
+        out = {n: b.clone() for n, b in self.pull().items()}
+        for n, s, dt in self.specs:
+            if dt != "float32":
+                out[n] = torch.tensor(self.read_int(n), dtype=torch.int32)
+        return out
+
+    def close(self):
+        self.client.close()

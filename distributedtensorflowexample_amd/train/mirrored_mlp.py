@@ -1,0 +1,176 @@
+"""Sync data-parallel training loop of the reference MLP (``--strategy mirrored``).
+
+One process per GPU (env RANK / WORLD_SIZE / LOCAL_RANK from the launcher
+or torch.distributed.run).  GPU: the fused two-launch step + the native RCCL
+all-reduce, hipGraph-replayed per epoch (train/fused_mlp.py).  CPU (gloo):
+the autograd MnistMLP wrapped in DistributedDataParallel.
+
+Observability mirrors the reference: ``step / cost / speed`` prints every
+``log_every`` steps (speed in global steps/sec; samples/sec = speed *
+batch_size * replicas), test accuracy every ``eval_every`` steps, loss and
+accuracy summaries (bulk-written from the device stats ring), and chief
+checkpoints in TF V2 format with the reference's variable names.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..models import mlp as mlp_model
+from ..ops import mlp_step, nn, optim
+from ..parallel.comm import NativeComm, TorchComm
+from ..parallel.mirrored import DistributedDataParallel
+from ..utils.summary import FileWriter
+from .fused_mlp import FusedMLPTrainer
+from .saver import FastSaver
+from .supervisor import Supervisor
+from .worker import flat_to_tf_vars, tf_vars_to_flat
+
+
+def _dist_env():
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def train_mirrored(flags, dataset, log=print, max_steps=None):
+    rank, world, local = _dist_env()
+    use_gpu = torch.cuda.is_available() and flags.device != "cpu"
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group("gloo")  # control plane; tensors over RCCL on GPU
+    if use_gpu:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        comm = NativeComm.from_process_group() if world > 1 else None
+    else:
+        dev = torch.device("cpu")
+        comm = TorchComm() if world > 1 else None
+    is_chief = rank == 0
+    steps_total = int(flags.training_steps if max_steps is None else max_steps)
+    B = int(flags.batch_size)
+
+    params = mlp_model.init_params(dev, seed=int(flags.seed))  # identical on every rank
+    # each replica trains on its own shard of the (shuffled) training set
+    tr_x = torch.from_numpy(dataset.train.images[rank::world]).float()
+    tr_y = torch.from_numpy(dataset.train.labels[rank::world])
+    tr_y = (tr_y.argmax(1) if tr_y.ndim == 2 else tr_y).to(torch.int32)
+
+    writer = FileWriter(flags.logdir + "_%d" % rank) if is_chief else None
+    state = {}
+
+    if use_gpu:
+        tr = FusedMLPTrainer(params, tr_x, tr_y, B, flags.learning_rate,
+                             allreduce=comm.allreduce_sum_ if comm else None, world_size=world)
+        get_params = lambda: tr.flush().clone()  # noqa: E731
+        step_fn = None
+    else:
+        model = mlp_model.MnistMLP(flat=params)
+        ddp = DistributedDataParallel(model, comm) if comm else None
+        state["pos"] = 0
+        get_params = lambda: model.flat.detach().clone()  # noqa: E731
+
+        def step_fn():
+            i = state["pos"]
+            n = tr_x.shape[0] // B
+            xb, yb = tr_x[(i % n) * B:(i % n + 1) * B], tr_y[(i % n) * B:(i % n + 1) * B]
+            state["pos"] = i + 1
+            if ddp:
+                ddp.reset()
+            else:
+                model.flat.grad = None
+            loss, acc = model.loss(xb, yb)
+            loss.backward()
+            if ddp:
+                ddp.finish()
+                g = ddp.flat_grad[:model.flat.numel()]
+            else:
+                g = model.flat.grad
+            with torch.no_grad():
+                optim.sgd_(model.flat.data, g, flags.learning_rate)
+            return float(loss), float(acc)
+
+    saver = FastSaver({n: None for n in
+                       ("global/dense/kernel", "global/dense/bias", "global/dense_1/kernel",
+                        "global/dense_1/bias", "global/global_step")})
+
+    def save_vars():
+        v = {k: t.contiguous() for k, t in flat_to_tf_vars(get_params().cpu()).items()}
+        v["global/global_step"] = torch.tensor(global_step(), dtype=torch.int32)
+        return v
+
+    def global_step():
+        return tr.global_step() if use_gpu else state.get("pos", 0)
+
+    def restore(values):
+        p = torch.zeros(mlp_step.NPARAM)
+        tf_vars_to_flat(values, p)
+        if use_gpu:
+            tr.load_params(p.to(dev))
+            tr.ws.set_global_step(int(values["global/global_step"]))
+            tr.pos = int(values["global/global_step"]) % tr.nbatches
+        else:
+            model.flat.data.copy_(p)
+            state["pos"] = int(values["global/global_step"])
+
+    saver.assign = restore
+    sv = Supervisor(is_chief=is_chief, logdir=flags.logdir if is_chief else None,
+                    saver=saver if is_chief else None, summary_writer=writer,
+                    global_step=global_step, save_model_secs=flags.save_model_secs,
+                    save_summaries_secs=flags.save_summaries_secs, save_variables=save_vars)
+
+    test_x = torch.from_numpy(dataset.test.images).float().to(dev)
+    test_y = dataset.test.labels.argmax(1) if dataset.test.labels.ndim == 2 else dataset.test.labels
+
+    def test_accuracy():
+        p = get_params()
+        W1t, b1, W2t, b2 = mlp_step.unflatten(p)
+        h = nn.gemm(test_x, W1t, trans_b=True, bias=b1, act="sigmoid")
+        logits = nn.gemm(h, W2t, trans_b=True, bias=b2)
+        return float((logits.argmax(1).cpu().numpy() == test_y).mean())
+
+    history = []
+    with sv.managed_session():
+        if world > 1 and sv.restored_from is not None:
+            pass  # chief-only restore: other ranks broadcast below
+        if world > 1:  # replicas start identical (restored or initialised on the chief)
+            p = get_params()
+            if comm is not None:
+                comm.broadcast_(p, 0)
+            if use_gpu:
+                tr.load_params(p)
+            else:
+                model.flat.data.copy_(p)
+        chunk = int(flags.log_every)
+        start_time, start_step = time.time(), global_step()
+        while not sv.should_stop():
+            s0 = global_step()
+            n = min(chunk - (s0 % chunk) if s0 % chunk else chunk, steps_total - s0)
+            if n <= 0:
+                break
+            if use_gpu:
+                tr.run(n)
+                stats = tr.stats_range(s0, s0 + n)
+            else:
+                stats = torch.tensor([step_fn() for _ in range(n)])
+            step = global_step()
+            if writer is not None:
+                writer.add_scalar_series(["loss", "accuracy"], range(s0, s0 + n), stats.tolist())
+            cost = float(stats[-1, 0])
+            history.append((step, cost, float(stats[-1, 1])))
+            if is_chief and step % chunk == 0:
+                if use_gpu:
+                    torch.cuda.synchronize()
+                elapsed = time.time() - start_time
+                log("step: {}\t| cost: {}\t| speed: {}step/sec".format(
+                    step, cost, float((step - start_step) / max(elapsed, 1e-9))))
+                start_time, start_step = time.time(), step
+            if is_chief and step % int(flags.eval_every) == 0:
+                log("test accuracy: {}".format(test_accuracy()))
+            if step >= steps_total:
+                break
+        if is_chief:
+            sv.save_checkpoint()
+    return history, get_params()

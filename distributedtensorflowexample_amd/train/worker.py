@@ -1,0 +1,183 @@
+"""The reference's ``Worker`` (worker.py:7-159), MI355X-native.
+
+Async parameter-server mode, with the reference's semantics step for step:
+
+=================  =========================================  ===================
+reference           here                                       native component
+=================  =========================================  ===================
+build_net global    ``global/dense/kernel`` ... on the ps      PSVariableStore
+  (+global_step)      (round-robin over ps tasks)               (C++ PSServer)
+build_net local     flat replica on the worker's GPU           fused HIP kernels
+sync_op             pull -> pinned host -> H2D                 C++ PSClient
+train_op            local grads (fused kernels) -> D2H ->      mlp_step kernels,
+                    push + ApplyGradientDescent on the ps       C++ apply on ps
+counter_op          atomic fetch_add(global_step, 1)           C++ PSServer
+summary_op          loss/accuracy -> TFRecord events           C++ EventWriter
+saver               FastSaver, TF V2 bundle, every 30 s        C++ bundle writer
+Supervisor          chief restore-or-init, ready wait          train/supervisor.py
+=================  =========================================  ===================
+
+On a CPU-only worker (BASELINE config 1, "1 ps + 1 worker on localhost
+CPU") the local forward/backward is the same math in PyTorch.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from ..models import mlp as mlp_model
+from ..ops import mlp_step
+from ..parallel.ps import PSVariableStore, replica_device_setter
+from ..utils.summary import FileWriter
+from .saver import FastSaver
+from .supervisor import Supervisor
+
+D, H, C = mlp_step.D, mlp_step.H, mlp_step.C
+GLOBAL_SPECS = [
+    ("global/dense/kernel", (D, H), "float32"),
+    ("global/dense/bias", (H,), "float32"),
+    ("global/dense_1/kernel", (H, C), "float32"),
+    ("global/dense_1/bias", (C,), "float32"),
+    ("global/global_step", (), "int64"),
+]
+TRAINABLE = [n for n, _, dt in GLOBAL_SPECS if dt == "float32"]
+
+
+def tf_vars_to_flat(v, out):
+    """TF-layout {name: tensor} -> flat internal buffer (W stored [out, in])."""
+    W1t, b1, W2t, b2 = mlp_step.unflatten(out)
+    W1t.copy_(v["global/dense/kernel"].t())
+    b1.copy_(v["global/dense/bias"])
+    W2t.copy_(v["global/dense_1/kernel"].t())
+    b2.copy_(v["global/dense_1/bias"])
+    return out
+
+
+def flat_to_tf_vars(p):
+    W1t, b1, W2t, b2 = mlp_step.unflatten(p)
+    return {"global/dense/kernel": W1t.t(), "global/dense/bias": b1,
+            "global/dense_1/kernel": W2t.t(), "global/dense_1/bias": b2}
+
+
+class Worker:
+    def __init__(self, job_name, task_index, server, flags, device=None, log=print):
+        self.job_name = job_name
+        self.task_index = int(task_index)
+        self.server = server
+        self.flags = flags
+        self.log = log
+        if device is None or device == "auto":
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(device)
+        self.is_chief = self.task_index == 0
+        self.batch_size = int(flags.batch_size)
+        self.lr = float(flags.learning_rate)
+        self.use_fused = self.device.type == "cuda" and 1 <= self.batch_size <= mlp_step.MAX_BATCH
+
+        # global variables on the ps (replica_device_setter(num_ps), worker.py:24-32)
+        self.store = PSVariableStore(server.target, GLOBAL_SPECS,
+                                     setter=replica_device_setter(len(server.target)))
+        # local replica (worker.py:34-40): one flat buffer on this worker's device
+        self.params = torch.zeros(mlp_step.NPARAM, device=self.device)
+        self.grad = torch.zeros_like(self.params)
+        if self.use_fused:
+            self.ws = mlp_step.StepWorkspace(self.batch_size, self.device)
+            self.grad_host = torch.empty(mlp_step.NPARAM, pin_memory=True)
+            self.xb = torch.empty(self.batch_size, D, device=self.device)
+            self.yb = torch.empty(self.batch_size, dtype=torch.int32, device=self.device)
+        self.summary_writer = FileWriter(flags.logdir + "_%d" % self.task_index)
+        # FastSaver over get_vars('global', False) (worker.py:102-103)
+        self.saver = FastSaver({n: None for n, _, _ in GLOBAL_SPECS}, assign=self.store.assign)
+
+    # -- graph pieces (as ops) ---------------------------------------------
+    def init_op(self):
+        """global_init_op: W ~ N(0, 1), b = 0, global_step = 0 (worker.py:51-53, 98-99)."""
+        p = mlp_model.init_params("cpu", seed=int(getattr(self.flags, "seed", 0)))
+        v = {k: t.contiguous() for k, t in flat_to_tf_vars(p).items()}
+        v["global/global_step"] = 0
+        self.store.assign(v)
+
+    def sync_op(self):
+        """worker.py:81-85: local <- global."""
+        vals = self.store.pull()
+        with torch.no_grad():
+            dev = {k: t.to(self.device, non_blocking=True) for k, t in vals.items()}
+            tf_vars_to_flat(dev, self.params)
+
+    def compute(self, batch_x, batch_y):
+        """Local forward/backward -> (grads in TF layout on CPU, loss, accuracy)."""
+        y = np.asarray(batch_y)
+        labels = y.argmax(1) if y.ndim == 2 else y
+        if self.use_fused and batch_x.shape[0] == self.batch_size:
+            self.xb.copy_(torch.from_numpy(np.ascontiguousarray(batch_x, np.float32)),
+                          non_blocking=False)
+            self.yb.copy_(torch.from_numpy(labels.astype(np.int32)))
+            mlp_step.step_grad(self.params, self.xb, self.yb, self.ws, self.grad)
+            self.grad_host.copy_(self.grad)
+            loss, acc = self.ws.stats[(self.ws.global_step() - 1) % self.ws.stats_ring].tolist()
+            g = self.grad_host
+        else:
+            x = torch.from_numpy(np.ascontiguousarray(batch_x, np.float32))
+            g, loss_t, acc_t = mlp_step.reference_step(self.params.cpu(), x,
+                                                       torch.from_numpy(labels))
+            loss, acc = float(loss_t), float(acc_t)
+        tfg = {k: t.contiguous() for k, t in flat_to_tf_vars(g.cpu()).items()}
+        return tfg, float(loss), float(acc)
+
+    def accuracy(self, images, labels):
+        """worker.py:87-90 on the local replica."""
+        x = torch.from_numpy(np.ascontiguousarray(images, np.float32)).to(self.device)
+        _, logits = mlp_step.reference_forward(self.params, x)
+        y = np.asarray(labels)
+        y = y.argmax(1) if y.ndim == 2 else y
+        return float((logits.argmax(1).cpu().numpy() == y).mean())
+
+    # -- training loop (worker.py:105-159) ------------------------------------
+    def learn(self, dataset, max_steps=None, stop_after_secs=None):
+        fl = self.flags
+        sv = Supervisor(is_chief=self.is_chief, logdir=fl.logdir, saver=self.saver,
+                        summary_writer=self.summary_writer, ready_op=self.store.uninitialized,
+                        global_step=lambda: self.store.read_int("global/global_step"),
+                        save_model_secs=getattr(fl, "save_model_secs", 30),
+                        save_summaries_secs=getattr(fl, "save_summaries_secs", 30),
+                        init_op=self.init_op, local_init_op=None,
+                        recovery_wait_secs=1.0, save_variables=self.store.read_all)
+        if self.is_chief:
+            self.store.create()
+        else:
+            self.store.lookup()
+        log_every = int(getattr(fl, "log_every", 100))
+        eval_every = int(getattr(fl, "eval_every", 10000))
+        local_steps = 0
+        history = []
+        t_begin = time.time()
+        with sv.managed_session(self.server.target):
+            start_time = time.time()
+            start_step = 0
+            while not sv.should_stop():
+                self.sync_op()
+                batch_x, batch_y = dataset.train.next_batch(self.batch_size)
+                grads, cost, acc = self.compute(batch_x, batch_y)
+                self.store.push_apply(grads, self.lr, bool(getattr(fl, "use_locking", False)))
+                step = self.store.fetch_add("global/global_step", 1)  # counter_op; old value
+                self.summary_writer.add_scalars({"loss": cost, "accuracy": acc}, step)
+                history.append((step, cost, acc))
+                local_steps += 1
+                if step % log_every == 0 and step != 0:
+                    elapsed = time.time() - start_time
+                    self.log("step: {}\t| cost: {}\t| speed: {}step/sec".format(
+                        step, cost, float((step - start_step) / max(elapsed, 1e-9))))
+                    start_time = time.time()
+                    start_step = step
+                if step % eval_every == 0:
+                    self.log("test accuracy: {}".format(
+                        self.accuracy(dataset.test.images, dataset.test.labels)))
+                if step >= fl.training_steps:
+                    break
+                if max_steps is not None and local_steps >= max_steps:
+                    break
+                if stop_after_secs is not None and time.time() - t_begin > stop_after_secs:
+                    break
+        return history

@@ -1,0 +1,84 @@
+"""End-to-end multi-process runs on CPU (the reference's localhost cluster style).
+
+* async PS: 1 ps + 2 workers through main.py and the launcher (BASELINE config 1:
+  "1 ps + 1 worker on localhost CPU", plumbing, no GPU);
+* sync DP: 2 ranks over gloo through main.py --strategy mirrored.
+"""
+import glob
+import os
+import re
+import socket
+
+import pytest
+
+from distributedtensorflowexample_amd.launch import launch_mirrored, launch_ps
+from distributedtensorflowexample_amd.train.saver import latest_checkpoint, load_checkpoint
+from distributedtensorflowexample_amd.utils.summary import read_events
+
+pytestmark = pytest.mark.slow
+
+
+def _free_port_block(n):
+    for _ in range(50):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            base = s.getsockname()[1]
+        if base + n < 65000:
+            ok = True
+            for p in range(base, base + n):
+                with socket.socket() as t:
+                    try:
+                        t.bind(("127.0.0.1", p))
+                    except OSError:
+                        ok = False
+                        break
+            if ok:
+                return base
+    raise RuntimeError("no free port block")
+
+
+def test_async_ps_cluster_cpu(tmp_path):
+    logdir = str(tmp_path / "mnist")
+    base = _free_port_block(4)
+    rc = launch_ps(num_workers=2, num_gpus=1, num_ps=1, cpu=True, base_port=base,
+                   log_dir=str(tmp_path / "logs"), quiet=True, timeout=240,
+                   extra=["--training_steps", "400", "--log_every", "100", "--eval_every", "200",
+                          "--logdir", logdir, "--save_model_secs", "0.5",
+                          "--learning_rate", "0.01"])
+    assert rc == {"worker0": 0, "worker1": 0}, rc
+    logs = "".join(open(p).read() for p in glob.glob(str(tmp_path / "logs" / "worker*.log")))
+    assert "Per-process GPU memory fraction: 0.45" in logs
+    costs = [float(c) for c in re.findall(r"cost: ([0-9.eE+-]+)", logs)]
+    assert costs, logs
+    assert "test accuracy:" in logs
+    # chief checkpoints carry the reference's variable names
+    ck = latest_checkpoint(logdir)
+    assert ck is not None
+    v = load_checkpoint(ck)
+    assert sorted(v) == ["global/dense/bias", "global/dense/kernel", "global/dense_1/bias",
+                         "global/dense_1/kernel", "global/global_step"]
+    assert tuple(v["global/dense/kernel"].shape) == (784, 100)
+    # per-worker TensorBoard files with loss/accuracy every step
+    for t in (0, 1):
+        ev = read_events(glob.glob(logdir + "_%d/events.out.tfevents.*" % t)[0])
+        tags = set().union(*[e["scalars"].keys() for e in ev])
+        assert {"loss", "accuracy"} <= tags
+    # both workers contributed: global steps are unique across workers
+    steps = []
+    for t in (0, 1):
+        ev = read_events(glob.glob(logdir + "_%d/events.out.tfevents.*" % t)[0])
+        steps += [e["step"] for e in ev if "loss" in e["scalars"]]
+    assert len(steps) == len(set(steps))
+
+
+def test_mirrored_two_ranks_gloo(tmp_path):
+    logdir = str(tmp_path / "mir")
+    rc = launch_mirrored(nproc=2, log_dir=str(tmp_path / "logs"), quiet=True, timeout=240,
+                         extra=["--training_steps", "300", "--log_every", "100",
+                                "--eval_every", "300", "--logdir", logdir, "--device", "cpu",
+                                "--learning_rate", "0.05", "--save_model_secs", "100"])
+    assert rc == {"rank0": 0, "rank1": 0}, rc
+    log0 = open(str(tmp_path / "logs" / "rank0.log")).read()
+    assert "step: 300" in log0 and "test accuracy:" in log0
+    v = load_checkpoint(latest_checkpoint(logdir))
+    assert int(v["global/global_step"]) == 300
