@@ -1,0 +1,60 @@
+"""Reference-equivalent baseline: async parameter-server SGD on MI355X.
+
+Runs the reference's topology (1 ps + N workers sharing the GPU(s), per-step
+pull 318 KB / push 318 KB + remote apply / fetch_add global_step) through
+``main.py`` and the launcher, with the reference's hyper-parameters, and
+reports cluster samples/sec = speed (global steps/sec, worker.py:144-146)
+x batch_size -- exactly what the reference prints.
+
+    python tools/bench_ps_async.py --num_workers 2 --steps 20000
+"""
+import argparse
+import glob
+import json
+import os
+import re
+import statistics
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributedtensorflowexample_amd.launch import launch_ps  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--num_workers", type=int, default=2)
+    ap.add_argument("--num_gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20000)
+    ap.add_argument("--batch_size", type=int, default=100)
+    ap.add_argument("--log_every", type=int, default=1000)
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--base_port", type=int, default=24222)
+    a = ap.parse_args()
+    tmp = tempfile.mkdtemp(prefix="psbench")
+    rc = launch_ps(a.num_workers, a.num_gpus, None, 1, cpu=a.cpu, base_port=a.base_port,
+                   log_dir=os.path.join(tmp, "logs"), quiet=True, timeout=1800,
+                   extra=["--training_steps", str(a.steps), "--log_every", str(a.log_every),
+                          "--eval_every", str(10 ** 9), "--logdir", os.path.join(tmp, "m"),
+                          "--save_model_secs", "1e9", "--save_summaries_secs", "1e9",
+                          "--batch_size", str(a.batch_size)])
+    speeds = []
+    for p in glob.glob(os.path.join(tmp, "logs", "worker*.log")):
+        for m in re.finditer(r"step: (\d+)\t\| cost: [^|]+\| speed: ([0-9.eE+-]+)step/sec",
+                             open(p).read()):
+            if int(m.group(1)) > 2 * a.log_every:  # skip warm-up prints
+                speeds.append(float(m.group(2)))
+    if not speeds:
+        print(json.dumps({"error": "no speed prints", "rc": rc}))
+        return 1
+    sps = statistics.median(speeds)
+    print(json.dumps({"metric": "samples/sec (cluster) MNIST MLP async PS (reference semantics)",
+                      "value": round(sps * a.batch_size, 1), "unit": "samples/sec",
+                      "global_steps_per_sec": round(sps, 1), "num_workers": a.num_workers,
+                      "num_gpus": a.num_gpus, "device": "cpu" if a.cpu else "MI355X",
+                      "steps": a.steps, "rc": rc, "n_speed_samples": len(speeds)}))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
