@@ -23,13 +23,11 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
 }
 
 __device__ __forceinline__ float sigmoidf_(float z) {
-  // Saturating form: exp of a non-positive argument never overflows.
-  if (z >= 0.f) {
-    float e = __expf(-z);
-    return 1.f / (1.f + e);
-  }
-  float e = __expf(z);
-  return e / (1.f + e);
+  // Saturating, branch-free: exp of a non-positive argument never overflows;
+  // v_rcp_f32 (1 ulp) instead of an IEEE division sequence.
+  const float e = __expf(-fabsf(z));
+  const float r = __builtin_amdgcn_rcpf(1.f + e);
+  return z >= 0.f ? r : e * r;
 }
 
 // DPP wave reductions (VALU lane moves, no LDS round trip as __shfl_xor's
@@ -40,15 +38,43 @@ __device__ __forceinline__ float dpp_f(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-  v += dpp_f<0xB1>(v);        // quad_perm(1,0,3,2)
-  v += dpp_f<0x4E>(v);        // quad_perm(2,3,0,1)
-  v += dpp_f<0x124>(v);       // row_ror:4
-  v += dpp_f<0x128>(v);       // row_ror:8
-  v += dpp_f<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3
-  v += dpp_f<0x143, 0xC>(v);  // row_bcast:31 -> rows 2, 3
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+// N independent wave sums, interleaved step by step so each DPP op's source
+// was written N instructions earlier (the VALU->DPP wait states are filled by
+// the other reductions, not s_nop).  Within a 16-lane row: quad_perm/row_ror
+// adds with old=0 (the identity of +), which the DPP combiner folds into
+// v_add_f32_dpp.  Across rows: gfx950 v_permlane16_swap / v_permlane32_swap,
+// so every lane ends with the total in a VGPR (no row_bcast masks, no readlane).
+template <int N>
+__device__ __forceinline__ void wave_sum_n(float (&v)[N]) {
+#define DTFX_STEP(CTRL)                                                                    \
+  _Pragma("unroll") for (int i = 0; i < N; ++i) v[i] += __int_as_float(                     \
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v[i]), CTRL, 0xF, 0xF, false));
+  DTFX_STEP(0xB1)
+  DTFX_STEP(0x4E)
+  DTFX_STEP(0x124)
+  DTFX_STEP(0x128)
+#undef DTFX_STEP
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int x = __float_as_int(v[i]);
+    auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    v[i] = __int_as_float(r[0]) + __int_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int x = __float_as_int(v[i]);
+    auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    v[i] = __int_as_float(r[0]) + __int_as_float(r[1]);
+  }
 }
+
+__device__ __forceinline__ float wave_sum(float v) {
+  float a[1] = {v};
+  wave_sum_n(a);
+  return a[0];
+}
+
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

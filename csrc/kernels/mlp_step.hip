@@ -228,10 +228,13 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     for (int c = 0; c < C; ++c) w2[u][c] = jv[u] ? w2[u][c] : 0.f;
     if (jv[u]) w.hbuf[(size_t)row * HP + jj[u]] = hv[u];
   }
-  // logits = h . W2 + b2 (DPP wave reductions; every lane ends with all 10)
+  // logits = h . W2 + b2 (10 interleaved DPP wave reductions; every lane ends with all 10)
   float lg[C];
 #pragma unroll
-  for (int c = 0; c < C; ++c) lg[c] = wave_sum(hv[0] * w2[0][c] + hv[1] * w2[1][c]) + b2v[c];
+  for (int c = 0; c < C; ++c) lg[c] = hv[0] * w2[0][c] + hv[1] * w2[1][c];
+  wave_sum_n(lg);
+#pragma unroll
+  for (int c = 0; c < C; ++c) lg[c] += b2v[c];
 
   float m = lg[0];
   int am = 0;
@@ -241,7 +244,7 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
   float se = 0.f;
 #pragma unroll
   for (int c = 0; c < C; ++c) se += __expf(lg[c] - m);
-  const float inv = 1.f / se, invB = 1.f / (float)B;
+  const float inv = fast_rcp(se), invB = 1.f / (float)B;
   float dl[C], ly = 0.f;
 #pragma unroll
   for (int c = 0; c < C; ++c) {
