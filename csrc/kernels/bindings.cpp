@@ -44,6 +44,7 @@ void act_fwd_launch(long long, int, const float*, float*, hipStream_t);
 }  // namespace dtfx
 
 void register_rccl(py::module_& m);
+void register_nn(py::module_& m);
 
 template <typename T>
 static inline T* P(uintptr_t a) { return reinterpret_cast<T*>(a); }
@@ -133,6 +134,7 @@ PYBIND11_MODULE(_hip, m) {
     dtfx::clock_probe_launch(iters, grid, P<unsigned long long>(out2), P<float>(sink), S(s));
   });
   register_rccl(m);
+  register_nn(m);
   m.def("device_count", []() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -1,0 +1,417 @@
+// bf16 GEMM on the gfx950 bf16 matrix cores (v_mfma_f32_16x16x32_bf16), f32
+// accumulate, with fused epilogues.  This is the workhorse of the north-star
+// models (BERT-base linear layers, ResNet-50 convolutions as implicit GEMM,
+// BASELINE.json configs 4-5); the reference itself only runs f32 dense layers
+// (worker.py:50-53), which use gemm_f32.hip.
+//
+//   C[M,N] = epi( alpha * op(A)[M,K] . op(B)[K,N] )
+//   op(A) = A stored [M][lda] (k contiguous)      or A^T, A stored [K][lda]
+//   op(B) = B stored [K][ldb] (n contiguous)      or B^T, B stored [N][ldb]
+//
+// so the three products of a linear layer need no transpose pass:
+//   forward  Y  = X . W^T       (TA=0, TB=1)
+//   dgrad    dX = dY . W        (TA=0, TB=0)
+//   wgrad    dW = dY^T . X      (TA=1, TB=0)
+//
+// Epilogue (all optional, in this order, f32):
+//   v = alpha*acc  (+ bias[n])  -> aux_out[m][n] = v (pre-activation, bf16)
+//   v = act(v)                   (gelu(tanh) / relu)
+//   v *= act'(aux_in[m][n])      (backward through an activation)
+//   v += residual[m][n]          (bf16)
+//   v += beta * C_old            (f32 output only: gradient accumulation)
+//   C = v as bf16 or f32
+//
+// Tiling: 128x128 output tile per 256-thread workgroup (4 waves, 2x2, each a
+// 64x64 sub-tile = 4x4 MFMA tiles), BK = 64, two LDS buffers of 32 KB.
+// Operand tiles are staged HBM->LDS with global_load_lds_dwordx4 (no VGPR
+// round trip; lane-linear LDS destination, so the bank swizzle is applied to
+// the per-lane SOURCE address).  LDS images keep the global layout of each
+// operand:
+//   k-contiguous operand  -> [128 rows][64 k]  128-B rows, fragments by
+//                            ds_read_b128, 16-B chunk c of row r stored at
+//                            chunk c ^ (r & 7)
+//   k-strided operand     -> [64 k][128 cols]  256-B rows, fragments by
+//                            two ds_read_b64_tr_b16 (hardware transpose),
+//                            chunk c of k-row r stored at c ^ swz_tr(r)
+// The next K tile is in flight while the current one feeds the MFMAs (one
+// barrier per K tile).  Block ids are XCD-remapped (bijective) so the tiles
+// that share an A row-panel run on one XCD's L2.
+//
+// Shape contract (checked on the host): K % 64 == 0, lda/ldb % 8 == 0 and
+// 16-byte aligned bases; M, N arbitrary (edge rows are clamped on load and
+// masked on store).
+#include "common.h"
+
+#include <stdexcept>
+#include <string>
+
+namespace dtfx {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ float bf2f(unsigned short h) {
+  return __uint_as_float((unsigned)h << 16);
+}
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN
+  return __builtin_bit_cast(unsigned short, b);
+}
+
+__device__ __forceinline__ float gelu_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float th = tanhf(k0 * (x + k1 * x * x * x));
+  return 0.5f * (1.f + th) + 0.5f * x * (1.f - th * th) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+namespace gb {
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB per operand tile
+constexpr int BUF_BYTES = 2 * TILE_BYTES;
+
+__device__ __forceinline__ int swz_tr(int r) { return ((r & 3) | (((r >> 3) & 1) << 2)) << 1; }
+
+// Stage one operand tile (16 KB) with 4 glds per thread.
+//  KCONT: tile rows = 128 outer (m or n) indices x 64 k; src row stride ld.
+//  else : tile rows = 64 k x 128 outer; src row stride ld.
+template <bool KCONT>
+__device__ __forceinline__ void stage(const unsigned short* __restrict__ src, int ld, int outer0,
+                                      int outer_max, int k0, char* lds_tile, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = i * 4 + wave;  // 1 KB block of the tile this wave-instruction fills
+    const unsigned short* g;
+    if (KCONT) {
+      const int row = blk * 8 + (lane >> 3), cs = lane & 7;
+      const int c = cs ^ (row & 7);
+      const int o = min(outer0 + row, outer_max);
+      g = src + (size_t)o * ld + k0 + c * 8;
+    } else {
+      const int kr = blk * 4 + (lane >> 4), cs = lane & 15;
+      const int c = cs ^ swz_tr(kr);
+      const int o = min(outer0 + c * 8, outer_max);  // outer_max is 8-aligned-safe (host)
+      g = src + (size_t)(k0 + kr) * ld + o;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(lds_tile + blk * 1024), 16, 0, 0);
+  }
+}
+
+// Fragment (8 bf16 along k) for MFMA 16x16x32: lane holds [outer = o0 + (l&15)][k = kk*32 + 8(l>>4) + j]
+template <bool KCONT>
+__device__ __forceinline__ bf16x8 frag(const char* lds_tile, int o0, int kk, int lane) {
+  if (KCONT) {
+    const int row = o0 + (lane & 15);
+    const int c = kk * 4 + (lane >> 4);
+    return *(const bf16x8*)(lds_tile + row * 128 + ((c ^ (row & 7)) << 4));
+  } else {
+    // ds_read_b64_tr_b16: 16-lane group g reads k rows kk*32+8g+{0..3} (+4 for the 2nd
+    // read), cols o0..o0+15; lane 4q+p addresses row q, cols 4p..4p+3.
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int col = o0 + 4 * p;
+    const int cch = col >> 3, cb = (col & 7) * 2;
+    const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
+    const char* a0 = lds_tile + r0 * 256 + ((cch ^ swz_tr(r0)) << 4) + cb;
+    const char* a1 = lds_tile + r1 * 256 + ((cch ^ swz_tr(r1)) << 4) + cb;
+    bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)a0);
+    bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)a1);
+    bf16x8 v;
+    v.lo = lo;
+    v.hi = hi;
+    return v;
+  }
+}
+}  // namespace gb
+
+struct GemmEpi {
+  float alpha, beta;
+  const float* bias;            // [N] or null
+  int act;                      // 0 none, 1 gelu, 2 relu
+  const unsigned short* aux_in; // [M][ld_aux] pre-activation (bf16) for act_grad, or null
+  unsigned short* aux_out;      // [M][ld_aux] store pre-activation, or null
+  int ld_aux;
+  const unsigned short* residual;  // [M][ld_res] bf16 or null
+  int ld_res;
+  int act_grad;                 // multiply by act'(aux_in)
+};
+
+template <bool TA, bool TB, bool OUT_F32>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
+    int M, int N, int K, const unsigned short* __restrict__ A, int lda,
+    const unsigned short* __restrict__ B, int ldb, void* __restrict__ Cv, int ldc, GemmEpi e,
+    long long sA, long long sB, long long sC) {
+  using namespace gb;
+  // strided batch over blockIdx.z (attention's per-(batch, head) products)
+  A += sA * blockIdx.z;
+  B += sB * blockIdx.z;
+  Cv = (char*)Cv + sC * blockIdx.z * (OUT_F32 ? 4 : 2);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_n * tiles_m);
+  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // Clamp limits for edge tiles: k-contiguous rows clamp to the last row; k-strided
+  // column chunks clamp to the last full 8-column chunk (ld % 8 == 0 makes it in-bounds).
+  const int a_max = TA ? ((M - 1) & ~7) : M - 1;
+  const int b_max = TB ? N - 1 : ((N - 1) & ~7);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // split-K: blockIdx.y owns K tiles [kt0, kt0 + nk)
+  const int nk_all = K / BK, per = (nk_all + gridDim.y - 1) / gridDim.y;
+  const int kt0 = blockIdx.y * per;
+  const int nk = max(0, min(per, nk_all - kt0));
+  auto stage_all = [&](int buf, int kt) {
+    char* base = smem + buf * BUF_BYTES;
+    stage<!TA>(A, lda, m0, a_max, (kt0 + kt) * BK, base, wave, lane);
+    stage<TB>(B, ldb, n0, b_max, (kt0 + kt) * BK, base + TILE_BYTES, wave, lane);
+  };
+  if (nk > 0) stage_all(0, 0);
+  __syncthreads();  // emits vmcnt(0): tile 0 landed for every wave
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage_all(cur ^ 1, kt + 1);
+    const char* At = smem + cur * BUF_BYTES;
+    const char* Bt = At + TILE_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag<!TA>(At, wm * 64 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<TB>(Bt, wn * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // Epilogue.  The accumulators (C/D map: col = lane & 15, row = (lane >> 4) * 4 + r)
+  // go through a per-wave LDS transpose, 32 rows at a time, so every lane then owns 8
+  // consecutive columns of a row: bias / aux / residual / C_old are read and the
+  // outputs written as 16-32 B vectors instead of 2-byte scattered accesses.
+  // Each wave uses its own 32 x 68 f32 region (row pad 4 floats: the 4 row groups of a
+  // ds_write land on distinct banks); the K loop's final barrier freed the buffers.
+  constexpr int EP_LD = 68;
+  float* ep = (float*)smem + wave * (32 * EP_LD);
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ep[(ii * 16 + row_l + r) * EP_LD + j * 16 + col_l] = acc[2 * h + ii][j][r];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
+      const int m = m0 + wm * 64 + h * 32 + rr;
+      const int n = n0 + wn * 64 + cg;
+      float v[8];
+      *(f32x4*)&v[0] = *(const f32x4*)&ep[rr * EP_LD + cg];
+      *(f32x4*)&v[4] = *(const f32x4*)&ep[rr * EP_LD + cg + 4];
+      if (m >= M || n >= N) continue;
+      if (OUT_F32 && gridDim.y > 1) {  // split-K partial: alpha only, hardware f32 atomics
+        float* C = (float*)Cv + (size_t)m * ldc + n;
+        for (int u = 0; u < 8 && n + u < N; ++u) unsafeAtomicAdd(C + u, e.alpha * v[u]);
+        continue;
+      }
+      const bool full = n + 8 <= N;  // N % 8 != 0 only reaches here with a ragged last group
+      float bn[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) bn[u] = 0.f;
+      if (e.bias) {
+        if (full) {
+          *(f32x4*)&bn[0] = *(const f32x4*)&e.bias[n];
+          *(f32x4*)&bn[4] = *(const f32x4*)&e.bias[n + 4];
+        } else {
+          for (int u = 0; u < 8 && n + u < N; ++u) bn[u] = e.bias[n + u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = e.alpha * v[u] + bn[u];
+      if (full) {
+        if (e.aux_out) {
+          bf16x8 o;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) o[u] = (short)f2bf(v[u]);
+          *(bf16x8*)&e.aux_out[(size_t)m * e.ld_aux + n] = o;
+        }
+        if (e.act == 1) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = gelu_f(v[u]);
+        } else if (e.act == 2) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = fmaxf(v[u], 0.f);
+        }
+        if (e.act_grad) {
+          const bf16x8 a8 = *(const bf16x8*)&e.aux_in[(size_t)m * e.ld_aux + n];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float uu = bf2f((unsigned short)a8[u]);
+            v[u] *= (e.act_grad == 1) ? gelu_grad_f(uu) : (uu > 0.f ? 1.f : 0.f);
+          }
+        }
+        if (e.residual) {
+          const bf16x8 r8 = *(const bf16x8*)&e.residual[(size_t)m * e.ld_res + n];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[u]);
+        }
+        if (OUT_F32) {
+          float* C = (float*)Cv + (size_t)m * ldc + n;
+          if (e.beta != 0.f) {
+            const f32x4 c0 = *(const f32x4*)C, c1 = *(const f32x4*)(C + 4);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              v[u] += e.beta * c0[u];
+              v[u + 4] += e.beta * c1[u];
+            }
+          }
+          *(f32x4*)C = *(f32x4*)&v[0];
+          *(f32x4*)(C + 4) = *(f32x4*)&v[4];
+        } else {
+          bf16x8 o;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) o[u] = (short)f2bf(v[u]);
+          *(bf16x8*)((unsigned short*)Cv + (size_t)m * ldc + n) = o;
+        }
+      } else {
+        for (int u = 0; u < 8 && n + u < N; ++u) {
+          float w = v[u];
+          if (e.aux_out) e.aux_out[(size_t)m * e.ld_aux + n + u] = f2bf(w);
+          if (e.act == 1) w = gelu_f(w);
+          else if (e.act == 2) w = fmaxf(w, 0.f);
+          if (e.act_grad) {
+            const float uu = bf2f(e.aux_in[(size_t)m * e.ld_aux + n + u]);
+            w *= (e.act_grad == 1) ? gelu_grad_f(uu) : (uu > 0.f ? 1.f : 0.f);
+          }
+          if (e.residual) w += bf2f(e.residual[(size_t)m * e.ld_res + n + u]);
+          if (OUT_F32) {
+            float* C = (float*)Cv + (size_t)m * ldc + n + u;
+            *C = (e.beta != 0.f) ? w + e.beta * *C : w;
+          } else {
+            ((unsigned short*)Cv)[(size_t)m * ldc + n + u] = f2bf(w);
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const void* A, int lda,
+                      const void* B, int ldb, void* C, int ldc, float alpha, float beta,
+                      const float* bias, int act, const void* aux_in, void* aux_out, int ld_aux,
+                      const void* residual, int ld_res, int act_grad, int splitk, int batch,
+                      long long sA, long long sB, long long sC, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || batch <= 0) return;
+  if (batch > 1 && (bias || aux_in || aux_out || residual))
+    throw std::runtime_error("gemm_bf16: batched GEMM supports alpha/beta/act epilogues only");
+  if (batch > 1 && ((sA | sB | sC) % 8))
+    throw std::runtime_error("gemm_bf16: batch strides must be multiples of 8 elements");
+  if (K % gb::BK) throw std::runtime_error("gemm_bf16: K must be a multiple of 64, got " + std::to_string(K));
+  if ((lda | ldb) % 8) throw std::runtime_error("gemm_bf16: lda/ldb must be multiples of 8");
+  if (((uintptr_t)A | (uintptr_t)B) & 15) throw std::runtime_error("gemm_bf16: A/B must be 16-byte aligned");
+  if (ta && M % 8) throw std::runtime_error("gemm_bf16: transposed A needs M % 8 == 0");
+  if (!tb && N % 8) throw std::runtime_error("gemm_bf16: non-transposed B needs N % 8 == 0");
+  if ((ldc % 8) || ((uintptr_t)C & 15))
+    throw std::runtime_error("gemm_bf16: C must be 16-byte aligned with ldc % 8 == 0");
+  if ((aux_in || aux_out) && (ld_aux % 8 || (((uintptr_t)aux_in | (uintptr_t)aux_out) & 15)))
+    throw std::runtime_error("gemm_bf16: aux must be 16-byte aligned with ld_aux % 8 == 0");
+  if (residual && (ld_res % 8 || ((uintptr_t)residual & 15)))
+    throw std::runtime_error("gemm_bf16: residual must be 16-byte aligned with ld_res % 8 == 0");
+  if (bias && ((uintptr_t)bias & 15)) throw std::runtime_error("gemm_bf16: bias must be 16-byte aligned");
+  if (act_grad && !aux_in) throw std::runtime_error("gemm_bf16: act_grad needs aux_in");
+  const int tiles = ((M + gb::BM - 1) / gb::BM) * ((N + gb::BN - 1) / gb::BN);
+  const int nkt = K / gb::BK;
+  if (splitk <= 0) {  // auto: fill the 256 CUs when the output has few tiles and K is deep
+    splitk = 1;
+    if (batch == 1 && out_f32 && !bias && !act && !act_grad && !residual && !aux_out && (beta == 0.f || beta == 1.f))
+      while (tiles * splitk < 256 && nkt / (splitk * 2) >= 8) splitk *= 2;
+  }
+  if (splitk > 1) {
+    if (batch > 1) throw std::runtime_error("gemm_bf16: split-K with batch > 1 is not supported");
+    if (!out_f32 || bias || act || act_grad || residual || aux_out || (beta != 0.f && beta != 1.f))
+      throw std::runtime_error("gemm_bf16: split-K supports f32 output with alpha and beta in {0,1} only");
+    if (beta == 0.f) {
+      if (ldc == N) DTFX_HIP_CHECK(hipMemsetAsync(C, 0, sizeof(float) * (size_t)M * N, stream));
+      else DTFX_HIP_CHECK(hipMemset2DAsync(C, sizeof(float) * ldc, 0, sizeof(float) * N, M, stream));
+    }
+  }
+  GemmEpi e{alpha, beta, bias, act, (const unsigned short*)aux_in, (unsigned short*)aux_out,
+            ld_aux, (const unsigned short*)residual, ld_res, act_grad};
+  const dim3 grid(tiles, splitk, batch);
+  const size_t lds = 2 * gb::BUF_BYTES;
+  auto* Au = (const unsigned short*)A;
+  auto* Bu = (const unsigned short*)B;
+#define DTFX_GB(TA_, TB_, F_)                                                                 \
+  if (ta == TA_ && tb == TB_ && out_f32 == F_) {                                              \
+    hipLaunchKernelGGL((gemm_bf16_kernel<TA_, TB_, F_>), grid, dim3(gb::NT), lds, stream, \
+                       M, N, K, Au, lda, Bu, ldb, C, ldc, e, sA, sB, sC);                                 \
+    DTFX_HIP_CHECK(hipGetLastError());                                                        \
+    return;                                                                                   \
+  }
+  DTFX_GB(false, true, false)
+  DTFX_GB(false, true, true)
+  DTFX_GB(false, false, false)
+  DTFX_GB(false, false, true)
+  DTFX_GB(true, false, false)
+  DTFX_GB(true, false, true)
+  DTFX_GB(true, true, false)
+  DTFX_GB(true, true, true)
+#undef DTFX_GB
+}
+
+// Column sums of a bf16 matrix (bias gradients): out[n] (+)= sum_m G[m][n], f32.
+__global__ __launch_bounds__(256) void colsum_bf16_kernel(const unsigned short* __restrict__ G, int M,
+                                                          int N, int ldg, float* __restrict__ out,
+                                                          float beta) {
+  // block: 64 columns x 4 row-groups; each thread sums a strided set of rows
+  __shared__ float part[4][64];
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  float s = 0.f;
+  if (n < N)
+    for (int m = blockIdx.y * 4 + rg; m < M; m += 4 * gridDim.y) s += bf2f(G[(size_t)m * ldg + n]);
+  part[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && n < N) {
+    s = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+    if (gridDim.y == 1) out[n] = s + (beta != 0.f ? beta * out[n] : 0.f);
+    else atomicAdd(out + n, s);
+  }
+}
+
+void colsum_bf16_launch(const void* G, int M, int N, int ldg, float* out, float beta,
+                        hipStream_t stream) {
+  if (N <= 0) return;
+  const int gx = (N + 63) / 64;
+  // Split rows over blocks when the matrix is tall; the caller's out is pre-scaled then.
+  int gy = 1;
+  if (M >= 4096) gy = std::min(64, std::max(1, 1024 / gx));
+  if (gy > 1) {
+    if (beta == 0.f) DTFX_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * N, stream));
+    else if (beta != 1.f) throw std::runtime_error("colsum_bf16: beta must be 0 or 1 for tall inputs");
+  }
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3(gx, gy), dim3(256), 0, stream,
+                     (const unsigned short*)G, M, N, ldg, out, beta);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dtfx

@@ -1,0 +1,694 @@
+// Transformer (BERT-base) kernels for gfx950: LayerNorm fwd/bwd, fused
+// embedding-sum + LayerNorm, embedding backward, fused self-attention
+// forward/backward (one workgroup per (sequence, head), everything in LDS),
+// mixed-precision Adam.  North-star config 5 of BASELINE.json (BERT-base MLM
+// bf16); the reference has no transformer (it runs an MLP, worker.py:47-54).
+//
+// Conventions: activations bf16 row-major [tokens][features]; LayerNorm
+// gamma/beta, statistics and all gradients of parameters f32; attention
+// reads the fused QKV projection output [T][3*Hd] in place (head h of Q at
+// columns h*64, of K at Hd + h*64, of V at 2*Hd + h*64) and writes its
+// gradient into the same layout, so no transpose/permute pass exists.
+#include "common.h"
+
+#include <stdexcept>
+#include <string>
+
+namespace dtfx {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+namespace tf {
+
+__device__ __forceinline__ float bf(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+__device__ __forceinline__ unsigned short tobf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(unsigned short, b);
+}
+__device__ __forceinline__ float tobf_round(float f) { return bf(tobf(f)); }
+__device__ __forceinline__ void unpack8(const bf16x8& v, float* f) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) f[u] = bf((unsigned short)v[u]);
+}
+__device__ __forceinline__ bf16x8 pack8(const float* f) {
+  bf16x8 v;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = (short)tobf(f[u]);
+  return v;
+}
+
+// Reductions inside one 16-lane DPP row (the 16 lanes of an MFMA C/D tile that
+// share a row group).
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false)));
+  return v;
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false));
+  return v;
+}
+
+// MFMA 16x16x32 bf16 operand fragment from an LDS matrix with row pitch `ld`
+// bytes: lane gets X[outer = o0 + (lane & 15)][k = k0 + 8 (lane >> 4) + j].
+//  KC : element (outer, k) at base + outer*ld + 2k   (one ds_read_b128)
+//  !KC: element (outer, k) at base + k*ld + 2*outer  (two ds_read_b64_tr_b16)
+template <bool KC>
+__device__ __forceinline__ bf16x8 lfrag(const char* base, int ld, int o0, int k0, int lane) {
+  if (KC) {
+    return *(const bf16x8*)(base + (o0 + (lane & 15)) * ld + (k0 + 8 * (lane >> 4)) * 2);
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const char* a = base + (k0 + 8 * g + q) * ld + (o0 + 4 * p) * 2;
+    bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)a);
+    bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(a + 4 * ld));
+    bf16x8 v;
+    v.lo = lo;
+    v.hi = hi;
+    return v;
+  }
+}
+__device__ __forceinline__ f32x4 mma(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+}  // namespace tf
+
+using namespace tf;
+
+// ---------------------------------------------------------------------------
+// LayerNorm: one wave per row, H % 8 == 0, H <= 2048 (<= 4 16-B chunks/lane)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void layernorm_fwd_kernel(
+    int T, int H, const unsigned short* __restrict__ x, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, unsigned short* __restrict__ y,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const int nch = H >> 3;
+  float v[4][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      unpack8(*(const bf16x8*)(x + (size_t)row * H + ch * 8), v[c]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[c][u];
+    }
+  }
+  const float mean = wave_sum(s) / H;
+  float s2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (lane + 64 * c < nch)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float d = v[c][u] - mean;
+        s2 += d * d;
+      }
+  const float rstd = rsqrtf(wave_sum(s2) / H + eps);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      float o[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        o[u] = (v[c][u] - mean) * rstd * gamma[ch * 8 + u] + beta[ch * 8 + u];
+      *(bf16x8*)(y + (size_t)row * H + ch * 8) = pack8(o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
+// dgamma += sum dy * xhat, dbeta += sum dy (per block in registers, then atomics)
+// optional dres: dx += dres (the residual branch gradient, fused)
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(
+    int T, int H, int rows_per_block, const unsigned short* __restrict__ dy,
+    const unsigned short* __restrict__ x, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const float* __restrict__ gamma,
+    const unsigned short* __restrict__ dres, unsigned short* __restrict__ dx,
+    float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[2][4][2048 / 4 + 4];  // [dgamma|dbeta][wave][...] partials, H <= 2048
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nch = H >> 3;
+  float dg[4][8], db[4][8];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) dg[c][u] = db[c][u] = 0.f;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(T, r0 + rows_per_block);
+  for (int row = r0 + wave; row < r1; row += 4) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float g[4][8], xh[4][8], dyv[4][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        float xv[8];
+        unpack8(*(const bf16x8*)(x + (size_t)row * H + ch * 8), xv);
+        unpack8(*(const bf16x8*)(dy + (size_t)row * H + ch * 8), dyv[c]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          xh[c][u] = (xv[u] - mean) * rstd;
+          g[c][u] = dyv[c][u] * gamma[ch * 8 + u];
+          s1 += g[c][u];
+          s2 += g[c][u] * xh[c][u];
+          dg[c][u] += dyv[c][u] * xh[c][u];
+          db[c][u] += dyv[c][u];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / H;
+    s2 = wave_sum(s2) / H;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        float o[8], rv[8];
+        if (dres) unpack8(*(const bf16x8*)(dres + (size_t)row * H + ch * 8), rv);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          o[u] = rstd * (g[c][u] - s1 - xh[c][u] * s2);
+          if (dres) o[u] += rv[u];
+        }
+        *(bf16x8*)(dx + (size_t)row * H + ch * 8) = pack8(o);
+      }
+    }
+  }
+  // cross-wave reduction of the parameter-gradient partials, then one atomic per column
+  for (int part = 0; part < 4; ++part) {  // H/4 columns per pass through the LDS buffer
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int col = ch * 8 + u;
+          if (col * 4 / H == part) {
+            red[0][wave][col - part * (H / 4)] = dg[c][u];
+            red[1][wave][col - part * (H / 4)] = db[c][u];
+          }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < H / 4; i += 256) {
+      const float a = red[0][0][i] + red[0][1][i] + red[0][2][i] + red[0][3][i];
+      const float b = red[1][0][i] + red[1][1][i] + red[1][2][i] + red[1][3][i];
+      unsafeAtomicAdd(dgamma + part * (H / 4) + i, a);
+      unsafeAtomicAdd(dbeta + part * (H / 4) + i, b);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Embedding: x = word[ids] + pos[t % S] + type[tt]; y = LN(x).  Saves x (bf16).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void embed_ln_fwd_kernel(
+    int T, int S, int H, const int* __restrict__ ids, const int* __restrict__ tt,
+    const unsigned short* __restrict__ word, const unsigned short* __restrict__ pos,
+    const unsigned short* __restrict__ type, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, unsigned short* __restrict__ xsum,
+    unsigned short* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const int nch = H >> 3;
+  const int id = ids[row], ty = tt ? tt[row] : 0, ps = row % S;
+  float v[4][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      float a[8], b[8], d[8];
+      unpack8(*(const bf16x8*)(word + (size_t)id * H + ch * 8), a);
+      unpack8(*(const bf16x8*)(pos + (size_t)ps * H + ch * 8), b);
+      unpack8(*(const bf16x8*)(type + (size_t)ty * H + ch * 8), d);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[c][u] = tobf_round(a[u] + b[u] + d[u]);
+        s += v[c][u];
+      }
+      *(bf16x8*)(xsum + (size_t)row * H + ch * 8) = pack8(v[c]);
+    }
+  }
+  const float mean = wave_sum(s) / H;
+  float s2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (lane + 64 * c < nch)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float d = v[c][u] - mean;
+        s2 += d * d;
+      }
+  const float rstd = rsqrtf(wave_sum(s2) / H + eps);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      float o[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        o[u] = (v[c][u] - mean) * rstd * gamma[ch * 8 + u] + beta[ch * 8 + u];
+      *(bf16x8*)(y + (size_t)row * H + ch * 8) = pack8(o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// word-embedding gradient: scatter-add of dx rows (f32 hardware atomics; ids are
+// spread over a 30K vocabulary, so contention is low).
+__global__ __launch_bounds__(256) void embed_word_bwd_kernel(int T, int H, const int* __restrict__ ids,
+                                                             const unsigned short* __restrict__ dx,
+                                                             float* __restrict__ dword) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const int nch = H >> 3;
+  float* dst = dword + (size_t)ids[row] * H;
+  for (int ch = lane; ch < nch; ch += 64) {
+    float v[8];
+    unpack8(*(const bf16x8*)(dx + (size_t)row * H + ch * 8), v);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) unsafeAtomicAdd(dst + ch * 8 + u, v[u]);
+  }
+}
+
+// position / token-type gradients: block per position s sums the B rows with that
+// position (no atomics for dpos), type partials then one atomic per column.
+__global__ __launch_bounds__(256) void embed_pos_type_bwd_kernel(
+    int Bn, int S, int H, const int* __restrict__ tt, const unsigned short* __restrict__ dx,
+    float* __restrict__ dpos, float* __restrict__ dtype_) {
+  const int s = blockIdx.x;
+  for (int col = threadIdx.x; col < H; col += 256) {
+    float acc = 0.f, t0 = 0.f, t1 = 0.f;
+    for (int b = 0; b < Bn; ++b) {
+      const int row = b * S + s;
+      const float v = bf(dx[(size_t)row * H + col]);
+      acc += v;
+      if (tt && tt[row]) t1 += v;
+      else t0 += v;
+    }
+    dpos[(size_t)s * H + col] += acc;
+    unsafeAtomicAdd(dtype_ + col, t0);
+    unsafeAtomicAdd(dtype_ + H + col, t1);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Self-attention, one workgroup (4 waves) per (sequence b, head h), S <= 128,
+// head dim 64.  Q, K, V (and dO) tiles live in LDS with 144-B rows (16-B pad:
+// conflict-free ds_read_b128 row reads); P / dS tiles 128 x 128 with 272-B rows.
+// Wave w owns query rows [32w, 32w + 32) for the row-wise products and key
+// rows [32w, 32w + 32) for dK / dV.
+// ---------------------------------------------------------------------------
+namespace at {
+constexpr int SP = 128, D = 64;
+constexpr int LDQ = D * 2 + 16;    // 144 B
+constexpr int LDP = SP * 2 + 16;   // 272 B
+constexpr int QB = SP * LDQ;       // 18432 B
+constexpr int PB = SP * LDP;       // 34816 B
+
+// Load a [S][64] head slice (row stride ld elements) into LDS, zero rows >= S.
+__device__ __forceinline__ void load_head(char* dst, const unsigned short* src, int ld, int S) {
+  for (int i = threadIdx.x; i < SP * 8; i += 256) {
+    const int r = i >> 3, c = i & 7;
+    bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r < S) v = *(const bf16x8*)(src + (size_t)r * ld + c * 8);
+    *(bf16x8*)(dst + r * LDQ + c * 16) = v;
+  }
+}
+}  // namespace at
+
+__global__ __launch_bounds__(256, 1) void attn_fwd_kernel(
+    int S, int nh, const unsigned short* __restrict__ qkv, unsigned short* __restrict__ out,
+    float* __restrict__ lse, const float* __restrict__ kmask, float scale) {
+  using namespace at;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* Qs = sm;
+  char* Ks = sm + QB;
+  char* Vs = sm + 2 * QB;
+  char* Ps = sm + 3 * QB;
+  const int b = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int Hd = nh * D, ld = 3 * Hd;
+  const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
+  at::load_head(Qs, base, ld, S);
+  at::load_head(Ks, base + Hd, ld, S);
+  at::load_head(Vs, base + 2 * Hd, ld, S);
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int cl = lane & 15, rg = (lane >> 4) * 4;
+
+  float km[8];  // additive key mask for this lane's key column in each key tile
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int key = 16 * j + cl;
+    km[j] = key < S ? (kmask ? kmask[(size_t)b * S + key] : 0.f) : -INFINITY;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r0 = 32 * wave + 16 * i;
+    f32x4 acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 a = lfrag<true>(Qs, LDQ, r0, 32 * kk, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = mma(a, lfrag<true>(Ks, LDQ, 16 * j, 32 * kk, lane), acc[j]);
+    }
+    // row softmax: row r0 + rg + r lives in the 16 lanes of this row group x 8 tiles
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc[j][r] = acc[j][r] * scale + km[j];
+        m = fmaxf(m, acc[j][r]);
+      }
+      m = row16_max(m);
+      const float msafe = (m == -INFINITY) ? 0.f : m;
+      float l = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc[j][r] = __expf(acc[j][r] - msafe);
+        l += acc[j][r];
+      }
+      l = row16_sum(l);
+      const float inv = l > 0.f ? 1.f / l : 0.f;
+      const int row = r0 + rg + r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        *(unsigned short*)(Ps + row * LDP + (16 * j + cl) * 2) = tobf(acc[j][r] * inv);
+      if (cl == 0 && row < S) lse[((size_t)b * nh + h) * SP + row] = msafe + __logf(l);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // P rows of this wave are read back only by this wave
+  // O = P . V  (32 rows x 64 d per wave, K = 128 keys)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r0 = 32 * wave + 16 * i;
+    f32x4 o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const bf16x8 a = lfrag<true>(Ps, LDP, r0, 32 * kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = mma(a, lfrag<false>(Vs, LDQ, 16 * j, 32 * kk, lane), o[j]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + rg + r;
+      if (row < S)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          out[((size_t)b * S + row) * Hd + h * D + 16 * j + cl] = tobf(o[j][r]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void attn_bwd_kernel(
+    int S, int nh, const unsigned short* __restrict__ qkv, const unsigned short* __restrict__ o,
+    const unsigned short* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ kmask, float scale, unsigned short* __restrict__ dqkv) {
+  using namespace at;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* Qs = sm;
+  char* Ks = sm + QB;
+  char* Vs = sm + 2 * QB;
+  char* dOs = sm + 3 * QB;
+  char* Ps = sm + 4 * QB;
+  char* dSs = Ps + PB;
+  float* Dr = (float*)(dSs + PB);  // [128] rowsum(dO * O)
+  const int b = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int Hd = nh * D, ld = 3 * Hd;
+  const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
+  at::load_head(Qs, base, ld, S);
+  at::load_head(Ks, base + Hd, ld, S);
+  at::load_head(Vs, base + 2 * Hd, ld, S);
+  at::load_head(dOs, dout + (size_t)b * S * Hd + h * D, Hd, S);
+  {  // D = rowsum(dO * O): 2 threads per row, 32 columns each
+    const int r = threadIdx.x >> 1, half = threadIdx.x & 1;
+    float s = 0.f;
+    if (r < S) {
+      const unsigned short* orow = o + ((size_t)b * S + r) * Hd + h * D + half * 32;
+      const unsigned short* drow = dout + ((size_t)b * S + r) * Hd + h * D + half * 32;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float ov[8], dv[8];
+        unpack8(*(const bf16x8*)(orow + c * 8), ov);
+        unpack8(*(const bf16x8*)(drow + c * 8), dv);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += ov[u] * dv[u];
+      }
+    }
+    s += __shfl_xor(s, 1);
+    if (half == 0) Dr[r] = s;
+  }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int cl = lane & 15, rg = (lane >> 4) * 4;
+  const float* L = lse + ((size_t)b * nh + h) * SP;
+  float km[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int key = 16 * j + cl;
+    km[j] = key < S ? (kmask ? kmask[(size_t)b * S + key] : 0.f) : -INFINITY;
+  }
+  // P and dS for this wave's 32 query rows
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r0 = 32 * wave + 16 * i;
+    f32x4 s[8], dp[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = dp[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 aq = lfrag<true>(Qs, LDQ, r0, 32 * kk, lane);
+      const bf16x8 ado = lfrag<true>(dOs, LDQ, r0, 32 * kk, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] = mma(aq, lfrag<true>(Ks, LDQ, 16 * j, 32 * kk, lane), s[j]);
+        dp[j] = mma(ado, lfrag<true>(Vs, LDQ, 16 * j, 32 * kk, lane), dp[j]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + rg + r;
+      const bool live = row < S;
+      const float lr = live ? L[row] : 0.f, dr = Dr[row];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float p = live ? __expf(s[j][r] * scale + km[j] - lr) : 0.f;
+        const float ds = p * (dp[j][r] - dr);
+        *(unsigned short*)(Ps + row * LDP + (16 * j + cl) * 2) = tobf(p);
+        *(unsigned short*)(dSs + row * LDP + (16 * j + cl) * 2) = tobf(ds);
+      }
+    }
+  }
+  __syncthreads();
+  unsigned short* dq = dqkv + (size_t)b * S * ld + h * D;
+  unsigned short* dk = dq + Hd;
+  unsigned short* dv = dq + 2 * Hd;
+  // dV = P^T dO, dK = scale * dS^T Q  (this wave's 32 key rows), dQ = scale * dS K (query rows)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int k0 = 32 * wave + 16 * i;
+    f32x4 av[4], ak[4], aq[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) av[j] = ak[j] = aq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const bf16x8 pT = lfrag<false>(Ps, LDP, k0, 32 * kk, lane);
+      const bf16x8 dsT = lfrag<false>(dSs, LDP, k0, 32 * kk, lane);
+      const bf16x8 dsr = lfrag<true>(dSs, LDP, k0, 32 * kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        av[j] = mma(pT, lfrag<false>(dOs, LDQ, 16 * j, 32 * kk, lane), av[j]);
+        ak[j] = mma(dsT, lfrag<false>(Qs, LDQ, 16 * j, 32 * kk, lane), ak[j]);
+        aq[j] = mma(dsr, lfrag<false>(Ks, LDQ, 16 * j, 32 * kk, lane), aq[j]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = k0 + rg + r;
+      if (row < S)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const size_t off = (size_t)row * ld + 16 * j + cl;
+          dv[off] = tobf(av[j][r]);
+          dk[off] = tobf(ak[j][r] * scale);
+          dq[off] = tobf(aq[j][r] * scale);
+        }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Mixed-precision Adam(W): f32 master p, grad g, moments m, v; writes the bf16
+// working copy pb used by the GEMMs.  Grad scale folds the 1/world average.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adam_mixed_kernel(
+    long long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+    float* __restrict__ v, unsigned short* __restrict__ pb, float lr, float b1, float b2,
+    float eps, float wd, float gscale, const int* __restrict__ step_ptr, int step) {
+  const int t = step_ptr ? *step_ptr : step;
+  const float bc1 = 1.f - powf(b1, (float)t), bc2 = 1.f - powf(b2, (float)t);
+  const float step_size = lr / bc1, rbc2 = rsqrtf(bc2);
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 pv = ((f32x4*)p)[i], gv = ((const f32x4*)g)[i], mv = ((f32x4*)m)[i], vv = ((f32x4*)v)[i];
+    bf16x4 o;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float gg = gv[u] * gscale;
+      mv[u] = b1 * mv[u] + (1.f - b1) * gg;
+      vv[u] = b2 * vv[u] + (1.f - b2) * gg * gg;
+      pv[u] -= lr * wd * pv[u];
+      pv[u] -= step_size * mv[u] / (sqrtf(vv[u]) * rbc2 + eps);
+      o[u] = (short)tobf(pv[u]);
+    }
+    ((f32x4*)p)[i] = pv;
+    ((f32x4*)m)[i] = mv;
+    ((f32x4*)v)[i] = vv;
+    if (pb) ((bf16x4*)pb)[i] = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(long long n, const float* __restrict__ x,
+                                                            unsigned short* __restrict__ y) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = tobf(x[i]);
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static void check_h(int H) {
+  if (H % 8 || H > 2048) throw std::runtime_error("transformer: H must be a multiple of 8 and <= 2048");
+}
+
+void layernorm_fwd_launch(int T, int H, const void* x, const float* gamma, const float* beta,
+                          float eps, void* y, float* mean, float* rstd, hipStream_t s) {
+  check_h(H);
+  if (T <= 0) return;
+  hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((T + 3) / 4), dim3(256), 0, s, T, H,
+                     (const unsigned short*)x, gamma, beta, eps, (unsigned short*)y, mean, rstd);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void layernorm_bwd_launch(int T, int H, const void* dy, const void* x, const float* mean,
+                          const float* rstd, const float* gamma, const void* dres, void* dx,
+                          float* dgamma, float* dbeta, hipStream_t s) {
+  check_h(H);
+  if (T <= 0) return;
+  const int rpb = 64;
+  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3((T + rpb - 1) / rpb), dim3(256), 0, s, T, H, rpb,
+                     (const unsigned short*)dy, (const unsigned short*)x, mean, rstd, gamma,
+                     (const unsigned short*)dres, (unsigned short*)dx, dgamma, dbeta);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void embed_ln_fwd_launch(int T, int S, int H, const int* ids, const int* tt, const void* word,
+                         const void* pos, const void* type, const float* gamma, const float* beta,
+                         float eps, void* xsum, void* y, float* mean, float* rstd, hipStream_t s) {
+  check_h(H);
+  if (T <= 0) return;
+  hipLaunchKernelGGL(embed_ln_fwd_kernel, dim3((T + 3) / 4), dim3(256), 0, s, T, S, H, ids, tt,
+                     (const unsigned short*)word, (const unsigned short*)pos,
+                     (const unsigned short*)type, gamma, beta, eps, (unsigned short*)xsum,
+                     (unsigned short*)y, mean, rstd);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void embed_bwd_launch(int Bn, int S, int H, const int* ids, const int* tt, const void* dx,
+                      float* dword, float* dpos, float* dtype_, hipStream_t s) {
+  check_h(H);
+  const int T = Bn * S;
+  if (T <= 0) return;
+  hipLaunchKernelGGL(embed_word_bwd_kernel, dim3((T + 3) / 4), dim3(256), 0, s, T, H, ids,
+                     (const unsigned short*)dx, dword);
+  DTFX_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(embed_pos_type_bwd_kernel, dim3(S), dim3(256), 0, s, Bn, S, H, tt,
+                     (const unsigned short*)dx, dpos, dtype_);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+static void check_attn(int S, int nh) {
+  if (S <= 0 || S > at::SP) throw std::runtime_error("attention: fused kernel needs 0 < S <= 128");
+  if (nh <= 0) throw std::runtime_error("attention: nh must be positive");
+}
+
+void attn_fwd_launch(int Bn, int S, int nh, const void* qkv, void* out, float* lse,
+                     const float* kmask, float scale, hipStream_t s) {
+  check_attn(S, nh);
+  const size_t lds = 3 * at::QB + at::PB;
+  static bool attr = false;
+  if (!attr) {
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(Bn * nh), dim3(256), lds, s, S, nh,
+                     (const unsigned short*)qkv, (unsigned short*)out, lse, kmask, scale);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, const void* dout,
+                     const float* lse, const float* kmask, float scale, void* dqkv, hipStream_t s) {
+  check_attn(S, nh);
+  const size_t lds = 4 * at::QB + 2 * at::PB + at::SP * 4;
+  static bool attr = false;
+  if (!attr) {
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(Bn * nh), dim3(256), lds, s, S, nh,
+                     (const unsigned short*)qkv, (const unsigned short*)o,
+                     (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void adam_mixed_launch(long long n, float* p, const float* g, float* m, float* v, void* pb,
+                       float lr, float b1, float b2, float eps, float wd, float gscale,
+                       const int* step_ptr, int step, hipStream_t s) {
+  if (n % 4) throw std::runtime_error("adam_mixed: n must be a multiple of 4");
+  if (n <= 0) return;
+  long long blocks = (n / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(adam_mixed_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
+                     (unsigned short*)pb, lr, b1, b2, eps, wd, gscale, step_ptr, step);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void cast_f32_bf16_launch(long long n, const float* x, void* y, hipStream_t s) {
+  if (n <= 0) return;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n, x,
+                     (unsigned short*)y);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dtfx

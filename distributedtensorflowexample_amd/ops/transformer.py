@@ -1,0 +1,200 @@
+"""Transformer ops backed by ``csrc/kernels/transformer.hip`` (gfx950).
+
+GPU tensors run the HIP kernels; CPU tensors run an f32 PyTorch reference of
+the same math (used by the CPU tier and by the GPU numerics tests).  There is
+no silent fallback for GPU tensors.  North-star BERT-base config of
+BASELINE.json; no counterpart in the reference.
+
+Layouts: activations bf16 ``[T, H]`` (T = batch * seq), LayerNorm parameters
+and statistics f32, fused QKV activations ``[T, 3 * nh * 64]`` (Q | K | V,
+head-major inside each third).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._ext import hip, ptr, stream_handle
+
+BF16 = torch.bfloat16
+
+
+def _f(t):
+    """f32 view of a low-precision tensor; f32/f64 pass through (reference precision)."""
+    return t if t.dtype in (torch.float32, torch.float64) else t.float()
+
+
+def _contig(t, name, dtype=None):
+    if t is None:
+        return
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % name)
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError("%s must be %s, got %s" % (name, dtype, t.dtype))
+
+
+# ---------------------------------------------------------------- LayerNorm
+def layernorm_fwd(x, gamma, beta, eps=1e-12):
+    T, H = x.shape
+    if not x.is_cuda:
+        xf = _f(x)
+        mean = xf.mean(1)
+        rstd = torch.rsqrt(xf.var(1, unbiased=False) + eps)
+        y = ((xf - mean[:, None]) * rstd[:, None] * gamma + beta).to(x.dtype)
+        return y, mean, rstd
+    _contig(x, "x", BF16)
+    _contig(gamma, "gamma", torch.float32)
+    _contig(beta, "beta", torch.float32)
+    y = torch.empty_like(x)
+    mean = torch.empty(T, device=x.device)
+    rstd = torch.empty(T, device=x.device)
+    hip().layernorm_fwd(T, H, ptr(x), ptr(gamma), ptr(beta), float(eps), ptr(y), ptr(mean),
+                        ptr(rstd), stream_handle())
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None):
+    """Returns dx; accumulates dgamma/dbeta (f32) in place."""
+    T, H = x.shape
+    if not x.is_cuda:
+        xf, g = _f(x), _f(dy)
+        xh = (xf - mean[:, None]) * rstd[:, None]
+        gg = g * gamma
+        dx = rstd[:, None] * (gg - gg.mean(1, keepdim=True) - xh * (gg * xh).mean(1, keepdim=True))
+        if dres is not None:
+            dx = dx + _f(dres)
+        dgamma += (g * xh).sum(0)
+        dbeta += g.sum(0)
+        return dx.to(x.dtype)
+    for t, n in ((dy, "dy"), (x, "x"), (dres, "dres")):
+        _contig(t, n, BF16)
+    dx = torch.empty_like(x)
+    hip().layernorm_bwd(T, H, ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), ptr(dres),
+                        ptr(dx), ptr(dgamma), ptr(dbeta), stream_handle())
+    return dx
+
+
+# ---------------------------------------------------------------- embeddings
+def embed_ln_fwd(ids, tt, word, pos, type_, gamma, beta, seq_len, eps=1e-12):
+    """x = word[ids] + pos[t % S] + type[tt]; returns (x bf16, LN(x), mean, rstd)."""
+    T = ids.numel()
+    H = word.shape[1]
+    if not ids.is_cuda:
+        p = torch.arange(T) % seq_len
+        x = (word[ids.long()].float() + pos[p].float() +
+             type_[(tt if tt is not None else torch.zeros_like(ids)).long()].float()).to(word.dtype)
+        y, mean, rstd = layernorm_fwd(x, gamma, beta, eps)
+        return x, y, mean, rstd
+    _contig(ids, "ids", torch.int32)
+    _contig(tt, "tt", torch.int32)
+    for t, n in ((word, "word"), (pos, "pos"), (type_, "type")):
+        _contig(t, n, BF16)
+    x = torch.empty(T, H, device=ids.device, dtype=BF16)
+    y = torch.empty_like(x)
+    mean = torch.empty(T, device=ids.device)
+    rstd = torch.empty(T, device=ids.device)
+    hip().embed_ln_fwd(T, seq_len, H, ptr(ids), ptr(tt), ptr(word), ptr(pos), ptr(type_),
+                       ptr(gamma), ptr(beta), float(eps), ptr(x), ptr(y), ptr(mean), ptr(rstd),
+                       stream_handle())
+    return x, y, mean, rstd
+
+
+def embed_bwd(ids, tt, dx, dword, dpos, dtype_, batch, seq_len):
+    """Accumulates word / position / token-type gradients (f32) in place."""
+    if not dx.is_cuda:
+        g = dx.float()
+        dword.index_add_(0, ids.long().view(-1), g)
+        dpos[:seq_len] += g.view(batch, seq_len, -1).sum(0)
+        t = (tt if tt is not None else torch.zeros_like(ids)).long().view(-1)
+        dtype_.index_add_(0, t, g)
+        return
+    _contig(dx, "dx", BF16)
+    hip().embed_bwd(batch, seq_len, dx.shape[1], ptr(ids), ptr(tt), ptr(dx), ptr(dword),
+                    ptr(dpos), ptr(dtype_), stream_handle())
+
+
+# ---------------------------------------------------------------- attention
+def _split(qkv, batch, seq, nh):
+    d = 64
+    q, k, v = qkv.float().view(batch, seq, 3, nh, d).permute(2, 0, 3, 1, 4)
+    return q, k, v  # [B, nh, S, d]
+
+
+def attn_fwd(qkv, batch, seq, nh, kmask=None, scale=None):
+    """softmax(Q K^T * scale + kmask) V per (sequence, head); returns (out [T, nh*64], lse)."""
+    scale = 1.0 / math.sqrt(64) if scale is None else scale
+    if not qkv.is_cuda:
+        q, k, v = _split(qkv, batch, seq, nh)
+        s = q @ k.transpose(-1, -2) * scale
+        if kmask is not None:
+            s = s + kmask.view(batch, 1, 1, seq)
+        lse = torch.logsumexp(s, -1)
+        p = torch.softmax(s, -1).to(BF16).float()
+        o = (p @ v).permute(0, 2, 1, 3).reshape(batch * seq, nh * 64).to(BF16)
+        return o, lse
+    _contig(qkv, "qkv", BF16)
+    _contig(kmask, "kmask", torch.float32)
+    out = torch.empty(batch * seq, nh * 64, device=qkv.device, dtype=BF16)
+    lse = torch.empty(batch * nh, 128, device=qkv.device)
+    hip().attn_fwd(batch, seq, nh, ptr(qkv), ptr(out), ptr(lse), ptr(kmask), float(scale),
+                   stream_handle())
+    return out, lse
+
+
+def attn_bwd(qkv, o, dout, lse, batch, seq, nh, kmask=None, scale=None):
+    """Gradient w.r.t. the fused QKV activations, same layout as ``qkv``."""
+    scale = 1.0 / math.sqrt(64) if scale is None else scale
+    if not qkv.is_cuda:
+        q, k, v = _split(qkv, batch, seq, nh)
+        do = dout.float().view(batch, seq, nh, 64).permute(0, 2, 1, 3)
+        of = o.float().view(batch, seq, nh, 64).permute(0, 2, 1, 3)
+        s = q @ k.transpose(-1, -2) * scale
+        if kmask is not None:
+            s = s + kmask.view(batch, 1, 1, seq)
+        lse_ = lse.view(batch, nh, -1)[..., :seq]
+        p = torch.exp(s - lse_[..., None])
+        D = (do * of).sum(-1, keepdim=True)
+        dp = do @ v.transpose(-1, -2)
+        ds = p * (dp - D)
+        dv = p.transpose(-1, -2) @ do
+        dk = ds.transpose(-1, -2) @ q * scale
+        dq = ds @ k * scale
+        g = torch.stack([dq, dk, dv], 0)  # [3, B, nh, S, d]
+        return g.permute(1, 3, 0, 2, 4).reshape(batch * seq, 3 * nh * 64).to(BF16)
+    for t, n in ((qkv, "qkv"), (o, "o"), (dout, "dout")):
+        _contig(t, n, BF16)
+    dqkv = torch.empty_like(qkv)
+    hip().attn_bwd(batch, seq, nh, ptr(qkv), ptr(o), ptr(dout), ptr(lse), ptr(kmask), float(scale),
+                   ptr(dqkv), stream_handle())
+    return dqkv
+
+
+# ---------------------------------------------------------------- optimizer / casts
+def adam_mixed(p, g, m, v, pb, lr, step, b1=0.9, b2=0.999, eps=1e-6, wd=0.01, gscale=1.0,
+               step_ptr=None):
+    """AdamW on an f32 master buffer; refreshes the bf16 working copy ``pb``."""
+    if not p.is_cuda:
+        gg = g * gscale
+        m.mul_(b1).add_((1 - b1) * gg)
+        v.mul_(b2).add_((1 - b2) * gg * gg)
+        t = int(step_ptr.item()) if step_ptr is not None else step
+        bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+        p.mul_(1 - lr * wd)
+        p.sub_(lr / bc1 * m / (v.sqrt() / math.sqrt(bc2) + eps))
+        if pb is not None:
+            pb.copy_(p)
+        return
+    hip().adam_mixed(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(pb), float(lr), float(b1),
+                     float(b2), float(eps), float(wd), float(gscale), ptr(step_ptr), int(step),
+                     stream_handle())
+
+
+def cast_bf16(x, out=None):
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=BF16)
+    if not x.is_cuda:
+        out.copy_(x)
+        return out
+    hip().cast_f32_bf16(x.numel(), ptr(x), ptr(out), stream_handle())
+    return out

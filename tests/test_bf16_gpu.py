@@ -1,0 +1,115 @@
+"""bf16 matrix-core kernels vs an f32 PyTorch reference of the same op (1 GPU)."""
+import pytest
+import torch
+
+from distributedtensorflowexample_amd.ops import bf16
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(*shape, dev, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return ((torch.rand(*shape, generator=g) * 2 - 1) * scale).to(dev).to(torch.bfloat16)
+
+
+def _ref(a, b, ta, tb):
+    A = a.float().t() if ta else a.float()
+    B = b.float().t() if tb else b.float()
+    return A @ B
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+def test_gemm_exact_integers(gpu, ta, tb):
+    # small integers: every product and partial sum is exact in f32, so any
+    # layout / fragment-map / swizzle error shows as an exact mismatch.
+    M, N, K = 256, 384, 192
+    g = torch.Generator().manual_seed(7)
+    a = torch.randint(-4, 5, ((K, M) if ta else (M, K)), generator=g).to(gpu, torch.bfloat16)
+    b = torch.randint(-4, 5, ((N, K) if tb else (K, N)), generator=g).to(gpu, torch.bfloat16)
+    y = bf16.gemm(a, b, ta, tb, out_dtype=torch.float32)
+    assert torch.equal(y, _ref(a, b, ta, tb))
+
+
+def test_gemm_identity_asymmetric(gpu):
+    I = torch.eye(128, device=gpu, dtype=torch.bfloat16)
+    B = (torch.arange(128 * 128, device=gpu) % 251).float().view(128, 128).to(torch.bfloat16)
+    assert torch.equal(bf16.gemm(I, B, out_dtype=torch.float32), B.float())
+    assert torch.equal(bf16.gemm(B, I, out_dtype=torch.float32), B.float())
+    assert torch.equal(bf16.gemm(I, B.t().contiguous(), False, True, out_dtype=torch.float32),
+                       B.float())
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
+@pytest.mark.parametrize("M,N,K", [(200, 136, 128), (1000, 768, 768), (64, 3072, 64), (8, 8, 64)])
+def test_gemm_random_edges(gpu, ta, tb, M, N, K):
+    a = _rand(*((K, M) if ta else (M, K)), dev=gpu, seed=1)
+    b = _rand(*((N, K) if tb else (K, N)), dev=gpu, seed=2)
+    y = bf16.gemm(a, b, ta, tb, out_dtype=torch.float32)
+    ref = _ref(a, b, ta, tb)
+    assert (y - ref).abs().max().item() < 1e-5 * K
+    yb = bf16.gemm(a, b, ta, tb)
+    assert yb.dtype == torch.bfloat16
+    assert torch.allclose(yb.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+def test_gemm_epilogue_bias_gelu_aux_residual(gpu):
+    M, N, K = 300, 256, 128
+    x = _rand(M, K, dev=gpu, seed=3)
+    w = _rand(N, K, dev=gpu, seed=4, scale=0.3)
+    bias = torch.randn(N, device=gpu)
+    res = _rand(M, N, dev=gpu, seed=5)
+    aux = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    y = bf16.gemm(x, w, False, True, bias=bias, act="gelu", aux_out=aux, residual=res,
+                  out_dtype=torch.float32)
+    u = x.float() @ w.float().t() + bias
+    assert torch.allclose(aux.float(), u, rtol=1e-2, atol=1e-2)
+    ref = torch.nn.functional.gelu(u, approximate="tanh") + res.float()
+    assert (y - ref).abs().max().item() < 1e-3
+
+
+def test_gemm_act_grad_and_beta(gpu):
+    M, N, K = 192, 128, 256
+    dy = _rand(M, K, dev=gpu, seed=6)
+    w = _rand(K, N, dev=gpu, seed=7, scale=0.2)
+    u = _rand(M, N, dev=gpu, seed=8, scale=2.0)
+    out = torch.randn(M, N, device=gpu)
+    out0 = out.clone()
+    bf16.gemm(dy, w, act_grad="gelu", aux_in=u, out=out, beta=1.0)
+    ref = (dy.float() @ w.float()) * bf16._gelu_grad_ref(u.float()) + out0
+    assert (out - ref).abs().max().item() < 1e-3
+    r = bf16.gemm(dy, w, act_grad="relu", aux_in=u, out_dtype=torch.float32)
+    assert (r - (dy.float() @ w.float()) * (u.float() > 0)).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("M", [37, 5000])
+def test_colsum_bf16(gpu, M):
+    g = _rand(M, 300, dev=gpu, seed=9)
+    s = bf16.colsum(g)
+    assert (s - g.float().sum(0)).abs().max().item() < 1e-3 * (M ** 0.5)
+    acc = torch.ones(300, device=gpu)
+    bf16.colsum(g, out=acc, beta=1.0)
+    assert (acc - 1 - g.float().sum(0)).abs().max().item() < 1e-3 * (M ** 0.5)
+
+
+@pytest.mark.parametrize("splitk,beta", [(0, 0.0), (3, 1.0), (8, 0.0)])
+def test_gemm_splitk_wgrad(gpu, splitk, beta):
+    # weight-gradient shape: few output tiles, deep K (dW = dY^T . X)
+    T, N, K = 4096, 256, 136
+    dy = _rand(T, N, dev=gpu, seed=10)
+    x = _rand(T, K, dev=gpu, seed=11)
+    out = torch.randn(N, K, device=gpu)
+    out0 = out.clone()
+    bf16.gemm(dy, x, True, False, out=out, beta=beta, splitk=splitk)
+    ref = dy.float().t() @ x.float() + beta * out0
+    assert (out - ref).abs().max().item() < 1e-4 * T ** 0.5
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
+def test_bmm_strided(gpu, ta, tb):
+    nb, M, N, K = 6, 128, 72, 64
+    a = _rand(nb, *((K, M) if ta else (M, K)), dev=gpu, seed=12)
+    b = _rand(nb, *((N, K) if tb else (K, N)), dev=gpu, seed=13)
+    y = bf16.bmm(a, b, ta, tb, out_dtype=torch.float32, alpha=0.5)
+    A = a.float().transpose(1, 2) if ta else a.float()
+    B = b.float().transpose(1, 2) if tb else b.float()
+    assert (y - 0.5 * torch.bmm(A, B)).abs().max().item() < 1e-4

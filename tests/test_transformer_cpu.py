@@ -1,0 +1,53 @@
+"""CPU reference math of the transformer ops vs torch autograd (no GPU)."""
+import math
+
+import torch
+
+from distributedtensorflowexample_amd.ops import transformer as T
+
+
+def test_layernorm_ref_matches_autograd():
+    x = torch.randn(20, 64, dtype=torch.float64, requires_grad=True)
+    g, b = torch.randn(64, dtype=torch.float64), torch.randn(64, dtype=torch.float64)
+    y = torch.nn.functional.layer_norm(x, (64,), g, b, eps=1e-12)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    y2, mean, rstd = T.layernorm_fwd(x.detach(), g, b)
+    assert torch.allclose(y2, y.detach(), atol=1e-10)
+    dg, db = torch.zeros(64, dtype=torch.float64), torch.zeros(64, dtype=torch.float64)
+    dx = T.layernorm_bwd(dy, x.detach(), mean.double(), rstd.double(), g, dg, db)
+    assert torch.allclose(dx, x.grad, atol=1e-8)
+    assert torch.allclose(dg, (dy * (x.detach() - mean[:, None]) * rstd[:, None]).sum(0))
+
+
+def test_attention_ref_matches_autograd():
+    B, S, nh = 2, 16, 2
+    qkv = torch.randn(B * S, 3 * nh * 64, dtype=torch.float64)
+    q, k, v = qkv.view(B, S, 3, nh, 64).permute(2, 0, 3, 1, 4)
+    q, k, v = (t.clone().requires_grad_(True) for t in (q, k, v))
+    mask = torch.zeros(B, S, dtype=torch.float64)
+    mask[1, 10:] = -10000.0
+    s = q @ k.transpose(-1, -2) / 8 + mask.view(B, 1, 1, S)
+    o = torch.softmax(s, -1) @ v
+    do = torch.randn_like(o)
+    o.backward(do)
+    lse = torch.logsumexp(s.detach(), -1)
+    of = o.detach().permute(0, 2, 1, 3).reshape(B * S, nh * 64)
+    dof = do.permute(0, 2, 1, 3).reshape(B * S, nh * 64)
+    # reference bwd works in f32 internally: compare at f32 precision
+    lse128 = torch.zeros(B, nh, 128, dtype=torch.float32)
+    lse128[..., :S] = lse.float()
+    g = T.attn_bwd(qkv.float().to(torch.bfloat16).float(), of.float(), dof.float(),
+                   lse128.view(B * nh, 128), B, S, nh, mask.float())
+    g = g.float().view(B, S, 3, nh, 64).permute(2, 0, 3, 1, 4)
+    for got, ref in zip(g, (q.grad, k.grad, v.grad)):
+        assert (got.double() - ref).abs().max() < 0.05 * ref.abs().max() + 1e-2
+
+
+def test_adam_mixed_ref():
+    p = torch.ones(8)
+    g = torch.full((8,), 2.0)
+    m, v = torch.zeros(8), torch.zeros(8)
+    T.adam_mixed(p, g, m, v, None, lr=0.1, step=1, wd=0.0)
+    # first bias-corrected Adam step moves by lr * sign(g)
+    assert torch.allclose(p, torch.full((8,), 0.9), atol=1e-5)

@@ -1,0 +1,86 @@
+"""Transformer HIP kernels vs the f32 PyTorch reference of the same op (1 GPU)."""
+import math
+
+import pytest
+import torch
+
+from distributedtensorflowexample_amd.ops import transformer as T
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def _r(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale)
+
+
+def test_layernorm_fwd_bwd(gpu):
+    Tn, H = 300, 768
+    x = _r(Tn, H, seed=1).to(BF)
+    gamma, beta = _r(H, seed=2) * 0.1 + 1, _r(H, seed=3) * 0.1
+    y, mean, rstd = T.layernorm_fwd(x.to(gpu), gamma.to(gpu), beta.to(gpu))
+    yr, mr, rr = T.layernorm_fwd(x, gamma, beta)
+    assert torch.allclose(mean.cpu(), mr, atol=1e-5) and torch.allclose(rstd.cpu(), rr, rtol=1e-4)
+    assert (y.cpu().float() - yr.float()).abs().max() < 3e-2
+    dy, dres = _r(Tn, H, seed=4).to(BF), _r(Tn, H, seed=5).to(BF)
+    dg, db = torch.zeros(H, device=gpu), torch.zeros(H, device=gpu)
+    dx = T.layernorm_bwd(dy.to(gpu), x.to(gpu), mean, rstd, gamma.to(gpu), dg, db, dres.to(gpu))
+    dgr, dbr = torch.zeros(H), torch.zeros(H)
+    dxr = T.layernorm_bwd(dy, x, mr, rr, gamma, dgr, dbr, dres)
+    assert (dx.cpu().float() - dxr.float()).abs().max() < 5e-2
+    assert torch.allclose(dg.cpu(), dgr, atol=1e-2, rtol=1e-3)
+    assert torch.allclose(db.cpu(), dbr, atol=1e-2, rtol=1e-3)
+
+
+def test_embedding_fwd_bwd(gpu):
+    B, S, H, V = 3, 40, 256, 1000
+    ids = torch.randint(0, V, (B * S,), dtype=torch.int32)
+    tt = torch.randint(0, 2, (B * S,), dtype=torch.int32)
+    word, pos, typ = _r(V, H, seed=6).to(BF), _r(64, H, seed=7).to(BF), _r(2, H, seed=8).to(BF)
+    gamma, beta = torch.ones(H), torch.zeros(H)
+    out = T.embed_ln_fwd(ids.to(gpu), tt.to(gpu), word.to(gpu), pos.to(gpu), typ.to(gpu),
+                         gamma.to(gpu), beta.to(gpu), S)
+    ref = T.embed_ln_fwd(ids, tt, word, pos, typ, gamma, beta, S)
+    assert torch.equal(out[0].cpu(), ref[0])
+    assert (out[1].cpu().float() - ref[1].float()).abs().max() < 3e-2
+    dx = _r(B * S, H, seed=9).to(BF)
+    g = [torch.zeros(V, H), torch.zeros(64, H), torch.zeros(2, H)]
+    gg = [t.to(gpu) for t in g]
+    T.embed_bwd(ids.to(gpu), tt.to(gpu), dx.to(gpu), *gg, B, S)
+    T.embed_bwd(ids, tt, dx, *g, B, S)
+    for a, b in zip(gg, g):
+        assert torch.allclose(a.cpu(), b, atol=1e-3)
+
+
+@pytest.mark.parametrize("S,masked", [(128, False), (128, True), (77, True), (64, False)])
+def test_attention_fwd_bwd(gpu, S, masked):
+    B, nh = 3, 4
+    qkv = _r(B * S, 3 * nh * 64, seed=10).to(BF)
+    kmask = None
+    if masked:
+        valid = torch.tensor([S, S - 5, S // 2])
+        kmask = torch.where(torch.arange(S)[None, :] < valid[:, None], 0.0, -10000.0)
+    o, lse = T.attn_fwd(qkv.to(gpu), B, S, nh, kmask.to(gpu) if masked else None)
+    orf, lser = T.attn_fwd(qkv, B, S, nh, kmask)
+    assert (o.cpu().float() - orf.float()).abs().max() < 2e-2
+    assert (lse.cpu().view(B, nh, 128)[..., :S] - lser).abs().max() < 1e-3
+    dout = _r(B * S, nh * 64, seed=11).to(BF)
+    dq = T.attn_bwd(qkv.to(gpu), o, dout.to(gpu), lse, B, S, nh, kmask.to(gpu) if masked else None)
+    dqr = T.attn_bwd(qkv, o.cpu(), dout, lse.cpu(), B, S, nh, kmask)
+    err = (dq.cpu().float() - dqr.float()).abs().max().item()
+    assert err < 3e-2 * max(1.0, dqr.float().abs().max().item()), err
+
+
+def test_adam_mixed_and_cast(gpu):
+    n = 4096
+    p, g = _r(n, seed=12), _r(n, seed=13)
+    m, v = torch.zeros(n), torch.zeros(n)
+    P, G, M, Vv = (t.to(gpu) for t in (p, g, m, v))
+    pb = torch.empty(n, device=gpu, dtype=BF)
+    for step in (1, 2, 3):
+        T.adam_mixed(P, G, M, Vv, pb, 1e-3, step, gscale=0.5)
+        T.adam_mixed(p, g, m, v, None, 1e-3, step, gscale=0.5)
+    assert torch.allclose(P.cpu(), p, atol=1e-6, rtol=1e-5)
+    assert torch.equal(pb.cpu(), P.cpu().to(BF))
+    assert torch.equal(T.cast_bf16(G).cpu(), g.to(BF))
