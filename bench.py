@@ -39,8 +39,14 @@ METRIC = "samples/sec (whole node) MNIST MLP sync-SGD at 1/2/4/8 MI355X; scaling
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20000)
-    ap.add_argument("--warmup", type=int, default=2000)
+    ap.add_argument("--model", choices=["mlp", "bert"], default="mlp",
+                    help="mlp: the headline MNIST MLP (BASELINE.json metric); bert: north-star "
+                         "BERT-base MLM config")
+    ap.add_argument("--steps", type=int, default=None, help="default 20000 (mlp) / 30 (bert)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 2000 (mlp) / 5 (bert)")
+    ap.add_argument("--bert_batch", type=int, default=64, help="BERT sequences per GPU")
+    ap.add_argument("--seq_len", type=int, default=128)
+    ap.add_argument("--bert_config", choices=["base", "tiny"], default="base")
     ap.add_argument("--batch_size", type=int, default=100)
     ap.add_argument("--learning_rate", type=float, default=0.001)
     ap.add_argument("--max_graph_steps", type=int, default=1024,
@@ -53,6 +59,10 @@ def main():
     ap.add_argument("--dp", action="store_true",
                     help="use the data-parallel path (gradient all-reduce) even on 1 GPU")
     a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 20000 if a.model == "mlp" else 30
+    if a.warmup is None:
+        a.warmup = 2000 if a.model == "mlp" else 5
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -67,6 +77,9 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:  # control plane over TCP/gloo; gradients over the native RCCL communicator
             dist.init_process_group("gloo")
+
+    if a.model == "bert":
+        return bench_bert(a, world, rank, local, dev)
 
     # identical replicas: the counter-based Philox init gives every rank the
     # same parameters from the same seed (no broadcast needed; verified below)
@@ -146,6 +159,61 @@ def main():
             "final_loss": round(loss, 5),
             "final_train_acc": round(acc, 4),
             "global_step": tr.global_step(),
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_bert(a, world, rank, local, dev):
+    """North-star config: BERT-base MLM pre-training step, bf16, sync DP over RCCL."""
+    from distributedtensorflowexample_amd.models.bert import BertConfig
+    from distributedtensorflowexample_amd.train.bert_trainer import BertTrainer
+
+    comm = None
+    if world > 1:
+        from distributedtensorflowexample_amd.parallel.comm import NativeComm, TorchComm
+
+        comm = NativeComm.from_process_group() if a.comm == "native" else TorchComm()
+    cfg = BertConfig.base() if a.bert_config == "base" else BertConfig.tiny()
+    tr = BertTrainer(cfg, a.bert_batch, a.seq_len, dev, comm=comm, data_seed=17 + rank)
+    use_graph = not a.no_graph
+    tr.run(a.warmup, use_graph)
+    barrier = (dist.barrier if a.comm == "native" else (lambda: dist.barrier(device_ids=[local]))) \
+        if world > 1 else None
+    if barrier:
+        barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tr.run(a.steps, use_graph)
+    torch.cuda.synchronize()
+    if barrier:
+        barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = t if a.comm == "native" else t.to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss, acc = tr.stats()
+    ms = elapsed * 1e3 / a.steps
+    seqs = a.bert_batch * world * a.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "sequences/sec (whole node) BERT-%s MLM pre-training, seq %d" % (a.bert_config,
+                                                                                     a.seq_len),
+            "value": round(seqs, 1), "unit": "sequences/sec", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random token ids / masked positions, device-resident), "
+                    "random-init weights",
+            "config": {"model": "BERT-%s MLM (L%d H%d A%d, vocab %d)" % (
+                a.bert_config, cfg.layers, cfg.hidden, cfg.heads, cfg.vocab_size),
+                "global_batch": a.bert_batch * world, "per_gpu_batch": a.bert_batch,
+                "seq_len": a.seq_len, "parallelism": "dp%d" % world,
+                "comm": a.comm if world > 1 else "none", "hipgraph": use_graph,
+                "optimizer": "AdamW (fused, f32 master)"},
+            "model_tflops_per_gpu": round(tr.flops_per_step() / (ms * 1e-3) / 1e12, 1),
+            "final_loss": round(loss, 4), "final_mlm_acc": round(acc, 4),
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -27,6 +27,7 @@ void attn_bwd_launch(int, int, int, const void*, const void*, const void*, const
 void adam_mixed_launch(long long, float*, const float*, float*, float*, void*, float, float, float,
                        float, float, float, const int*, int, hipStream_t);
 void cast_f32_bf16_launch(long long, const float*, void*, hipStream_t);
+void act_grad_bf16_launch(long long, int, const void*, const void*, void*, hipStream_t);
 }  // namespace dtfx
 
 template <typename T>
@@ -99,5 +100,9 @@ void register_nn(py::module_& m) {
   });
   m.def("cast_f32_bf16", [](long long n, uintptr_t x, uintptr_t y, uintptr_t s) {
     dtfx::cast_f32_bf16_launch(n, P<const float>(x), P<void>(y), S(s));
+  });
+  m.def("act_grad_bf16", [](long long n, int act, uintptr_t dy, uintptr_t u, uintptr_t dx,
+                            uintptr_t s) {
+    dtfx::act_grad_bf16_launch(n, act, P<const void>(dy), P<const void>(u), P<void>(dx), S(s));
   });
 }

@@ -574,6 +574,33 @@ __global__ __launch_bounds__(256) void adam_mixed_kernel(
   }
 }
 
+// dx = dy * act'(u), bf16 (gelu-tanh: act 1, relu: act 2); n % 8 == 0
+__global__ __launch_bounds__(256) void act_grad_bf16_kernel(long long n8, int act,
+                                                            const unsigned short* __restrict__ dy,
+                                                            const unsigned short* __restrict__ u,
+                                                            unsigned short* __restrict__ dx) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float a[8], b[8];
+    unpack8(((const bf16x8*)dy)[i], a);
+    unpack8(((const bf16x8*)u)[i], b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float x = b[k];
+      float d;
+      if (act == 1) {
+        const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+        const float th = tanhf(k0 * (x + k1 * x * x * x));
+        d = 0.5f * (1.f + th) + 0.5f * x * (1.f - th * th) * k0 * (1.f + 3.f * k1 * x * x);
+      } else {
+        d = x > 0.f ? 1.f : 0.f;
+      }
+      a[k] *= d;
+    }
+    ((bf16x8*)dx)[i] = pack8(a);
+  }
+}
+
 __global__ __launch_bounds__(256) void cast_f32_bf16_kernel(long long n, const float* __restrict__ x,
                                                             unsigned short* __restrict__ y) {
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -679,6 +706,17 @@ void adam_mixed_launch(long long n, float* p, const float* g, float* m, float* v
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(adam_mixed_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
                      (unsigned short*)pb, lr, b1, b2, eps, wd, gscale, step_ptr, step);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void act_grad_bf16_launch(long long n, int act, const void* dy, const void* u, void* dx,
+                          hipStream_t s) {
+  if (n % 8) throw std::runtime_error("act_grad_bf16: n must be a multiple of 8");
+  if (n <= 0) return;
+  long long blocks = (n / 8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(act_grad_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n / 8, act,
+                     (const unsigned short*)dy, (const unsigned short*)u, (unsigned short*)dx);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

@@ -1,0 +1,321 @@
+"""BERT-base masked-LM pre-training model on the bf16 gfx950 kernels.
+
+North-star config 5 of BASELINE.json ("BERT-base MLM bf16, bucketed RCCL
+all-reduce + fused Adam on 8x MI355X"); the reference itself only trains an
+MNIST MLP (worker.py:47-79), so this model follows the public BERT-base
+architecture (post-LN encoder, tanh-GELU, tied decoder) rather than any
+reference file.
+
+Design (MI355X-first, no autograd graph):
+
+* every parameter lives in ONE flat f32 master buffer (64-element aligned
+  slots, forward order), with a flat bf16 working copy used by the GEMMs, one
+  flat f32 gradient buffer and the Adam moments -- the optimizer is a single
+  fused ``adam_mixed`` launch and each encoder layer's gradients are one
+  contiguous all-reduce bucket (7.1 M params = 28 MB, sized for RCCL rings
+  over xGMI);
+* forward and backward are written out explicitly over the HIP ops
+  (``ops.bf16.gemm`` with fused bias/GELU/residual epilogues, fused
+  attention, LayerNorm, embedding kernels); backward calls
+  ``on_bucket_ready(i)`` as soon as bucket ``i``'s gradients are final, so
+  the data-parallel wrapper can start its all-reduce while earlier layers are
+  still in backward;
+* the QKV projection is one [3H, H] GEMM whose output the attention kernel
+  reads in place (no head permutes).
+
+All ops also run on CPU tensors through their f32 reference paths, so a tiny
+configuration trains on the CPU test tier.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import torch
+
+from ..ops import bf16 as B16
+from ..ops import init as I
+from ..ops import nn as NN
+from ..ops import transformer as TR
+
+BF16 = torch.bfloat16
+ALIGN = 64
+
+
+@dataclasses.dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    ffn: int = 3072
+    max_pos: int = 512
+    type_vocab: int = 2
+    eps: float = 1e-12
+    init_std: float = 0.02
+
+    @property
+    def vocab_padded(self):
+        return (self.vocab_size + ALIGN - 1) // ALIGN * ALIGN
+
+    @staticmethod
+    def base():
+        return BertConfig()
+
+    @staticmethod
+    def tiny():
+        return BertConfig(vocab_size=1000, hidden=128, layers=2, heads=2, ffn=256, max_pos=128)
+
+
+def param_layout(cfg: BertConfig):
+    """[(name, shape, init)] in forward order; init in {"normal", "zeros", "ones"}.
+
+    Weight matrices are [out, in] (GEMM operand op(B) = W^T, TB=1)."""
+    H, F, V = cfg.hidden, cfg.ffn, cfg.vocab_padded
+    L = [("embeddings/word_embeddings", (V, H), "normal"),
+         ("embeddings/position_embeddings", (cfg.max_pos, H), "normal"),
+         ("embeddings/token_type_embeddings", (cfg.type_vocab, H), "normal"),
+         ("embeddings/LayerNorm/gamma", (H,), "ones"),
+         ("embeddings/LayerNorm/beta", (H,), "zeros")]
+    for l in range(cfg.layers):
+        p = "encoder/layer_%d/" % l
+        L += [(p + "attention/qkv/kernel", (3 * H, H), "normal"),
+              (p + "attention/qkv/bias", (3 * H,), "zeros"),
+              (p + "attention/output/dense/kernel", (H, H), "normal"),
+              (p + "attention/output/dense/bias", (H,), "zeros"),
+              (p + "attention/output/LayerNorm/gamma", (H,), "ones"),
+              (p + "attention/output/LayerNorm/beta", (H,), "zeros"),
+              (p + "intermediate/dense/kernel", (F, H), "normal"),
+              (p + "intermediate/dense/bias", (F,), "zeros"),
+              (p + "output/dense/kernel", (H, F), "normal"),
+              (p + "output/dense/bias", (H,), "zeros"),
+              (p + "output/LayerNorm/gamma", (H,), "ones"),
+              (p + "output/LayerNorm/beta", (H,), "zeros")]
+    L += [("cls/predictions/transform/dense/kernel", (H, H), "normal"),
+          ("cls/predictions/transform/dense/bias", (H,), "zeros"),
+          ("cls/predictions/transform/LayerNorm/gamma", (H,), "ones"),
+          ("cls/predictions/transform/LayerNorm/beta", (H,), "zeros"),
+          ("cls/predictions/output_bias", (V,), "zeros")]
+    return L
+
+
+class FlatParams:
+    """Flat f32 master / bf16 copy / f32 grad / Adam moments with named views."""
+
+    def __init__(self, cfg: BertConfig, device, seed=0):
+        self.cfg = cfg
+        self.layout = param_layout(cfg)
+        self.offsets = {}
+        off = 0
+        for name, shape, _ in self.layout:
+            n = math.prod(shape)
+            self.offsets[name] = (off, shape)
+            off += (n + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        dev = torch.device(device)
+        self.master = torch.zeros(off, device=dev)
+        self.grad = torch.zeros(off, device=dev)
+        self.m = torch.zeros(off, device=dev)
+        self.v = torch.zeros(off, device=dev)
+        self.bf = torch.zeros(off, device=dev, dtype=BF16)
+        for i, (name, shape, kind) in enumerate(self.layout):
+            t = self.view(self.master, name)
+            if kind == "normal":
+                I.fill_(t.view(-1), "truncated_normal", 0.0, cfg.init_std, seed=seed, offset=i << 40)
+            elif kind == "ones":
+                t.fill_(1.0)
+        # padded vocabulary rows stay zero (never indexed; masked in the loss)
+        w = self.view(self.master, "embeddings/word_embeddings")
+        w[cfg.vocab_size:].zero_()
+        TR.cast_bf16(self.master, self.bf)
+        # buckets: [embeddings, layer 0 .. L-1, head] as contiguous flat ranges
+        self.buckets = []
+        first = lambda n: self.offsets[n][0]
+        lay0 = [first("encoder/layer_%d/attention/qkv/kernel" % l) for l in range(cfg.layers)]
+        head0 = first("cls/predictions/transform/dense/kernel")
+        edges = [0] + lay0 + [head0, self.numel]
+        self.buckets = [(edges[i], edges[i + 1]) for i in range(len(edges) - 1)]
+
+    def view(self, flat, name):
+        off, shape = self.offsets[name]
+        return flat[off:off + math.prod(shape)].view(shape)
+
+    def P(self, name):   # f32 master (biases, LayerNorm params)
+        return self.view(self.master, name)
+
+    def W(self, name):   # bf16 working copy (GEMM operands, embeddings)
+        return self.view(self.bf, name)
+
+    def G(self, name):
+        return self.view(self.grad, name)
+
+    def state_dict(self):
+        return {n: self.view(self.master, n).detach().cpu() for n, _, _ in self.layout}
+
+
+class BertMLM:
+    """Explicit forward + backward of BERT MLM over the HIP ops."""
+
+    def __init__(self, cfg: BertConfig, device, seed=0):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.params = FlatParams(cfg, device, seed)
+
+    # ------------------------------------------------------------------ forward
+    def _layer_fwd(self, l, x, batch, seq, kmask):
+        cfg, p = self.cfg, self.params
+        pre = "encoder/layer_%d/" % l
+        qkv = B16.gemm(x, p.W(pre + "attention/qkv/kernel"), False, True,
+                       bias=p.P(pre + "attention/qkv/bias"))
+        ctx, lse = TR.attn_fwd(qkv, batch, seq, cfg.heads, kmask)
+        a = B16.gemm(ctx, p.W(pre + "attention/output/dense/kernel"), False, True,
+                     bias=p.P(pre + "attention/output/dense/bias"), residual=x)
+        h1, m1, r1 = TR.layernorm_fwd(a, p.P(pre + "attention/output/LayerNorm/gamma"),
+                                      p.P(pre + "attention/output/LayerNorm/beta"), cfg.eps)
+        u = torch.empty(x.shape[0], cfg.ffn, device=x.device, dtype=BF16)
+        g = B16.gemm(h1, p.W(pre + "intermediate/dense/kernel"), False, True,
+                     bias=p.P(pre + "intermediate/dense/bias"), act="gelu", aux_out=u)
+        f = B16.gemm(g, p.W(pre + "output/dense/kernel"), False, True,
+                     bias=p.P(pre + "output/dense/bias"), residual=h1)
+        out, m2, r2 = TR.layernorm_fwd(f, p.P(pre + "output/LayerNorm/gamma"),
+                                       p.P(pre + "output/LayerNorm/beta"), cfg.eps)
+        return out, (x, qkv, ctx, lse, a, m1, r1, h1, u, g, f, m2, r2)
+
+    def forward_backward(self, ids, tt, mask_pos, mask_labels, kmask=None, on_bucket_ready=None,
+                         n_valid=None):
+        """One MLM training step's forward + backward; gradients land in params.grad.
+
+        ids, tt: int32 [B, S]; mask_pos: int64 flat token indices of the masked
+        positions [Tm]; mask_labels: int32 [Tm].  Returns (loss, accuracy) as
+        0-dim device tensors (no host sync)."""
+        cfg, p = self.cfg, self.params
+        batch, seq = ids.shape
+        if seq > cfg.max_pos:
+            raise ValueError("sequence length %d exceeds max_pos %d" % (seq, cfg.max_pos))
+        Tn = batch * seq
+        p.grad.zero_()
+        ids_f, tt_f = ids.reshape(-1), tt.reshape(-1)
+        x0, h, me, re = TR.embed_ln_fwd(ids_f, tt_f, p.W("embeddings/word_embeddings"),
+                                        p.W("embeddings/position_embeddings"),
+                                        p.W("embeddings/token_type_embeddings"),
+                                        p.P("embeddings/LayerNorm/gamma"),
+                                        p.P("embeddings/LayerNorm/beta"), seq, cfg.eps)
+        saved = []
+        for l in range(cfg.layers):
+            h, s = self._layer_fwd(l, h, batch, seq, kmask)
+            saved.append(s)
+        # ---- MLM head on the masked positions only
+        hm = h.index_select(0, mask_pos)
+        ut = torch.empty(hm.shape, device=h.device, dtype=BF16)
+        t = B16.gemm(hm, p.W("cls/predictions/transform/dense/kernel"), False, True,
+                     bias=p.P("cls/predictions/transform/dense/bias"), act="gelu", aux_out=ut)
+        tn, mt, rt = TR.layernorm_fwd(t, p.P("cls/predictions/transform/LayerNorm/gamma"),
+                                      p.P("cls/predictions/transform/LayerNorm/beta"), cfg.eps)
+        E = p.W("embeddings/word_embeddings")
+        logits = B16.gemm(tn, E, False, True, bias=p.P("cls/predictions/output_bias"),
+                          out_dtype=torch.float32)
+        Tm = tn.shape[0]
+        scale = 1.0 / max(1, n_valid if n_valid is not None else Tm)
+        if logits.is_cuda:
+            loss_rows, dlog, correct = self._xent_gpu(logits, mask_labels, Tm, scale)
+        else:
+            loss_rows, d, correct = NN.softmax_xent_stats(logits[:, :cfg.vocab_size], mask_labels,
+                                                          want_grad=True, scale=scale)
+            dlog = torch.zeros(Tm, cfg.vocab_padded)
+            dlog[:, :cfg.vocab_size] = d
+        dlog_b = TR.cast_bf16(dlog)
+        loss = loss_rows.sum() * scale
+        acc = correct.sum() * scale
+        # ---- backward: head
+        B16.gemm(dlog_b, tn, True, False, out=p.G("embeddings/word_embeddings"), beta=1.0)
+        B16.colsum(dlog_b, out=p.G("cls/predictions/output_bias"), beta=1.0)
+        dtn = B16.gemm(dlog_b, E)
+        dt = TR.layernorm_bwd(dtn, t, mt, rt, p.P("cls/predictions/transform/LayerNorm/gamma"),
+                              p.G("cls/predictions/transform/LayerNorm/gamma"),
+                              p.G("cls/predictions/transform/LayerNorm/beta"))
+        dut = TR.act_grad(dt, ut, "gelu")
+        B16.gemm(dut, hm, True, False, out=p.G("cls/predictions/transform/dense/kernel"), beta=1.0)
+        B16.colsum(dut, out=p.G("cls/predictions/transform/dense/bias"), beta=1.0)
+        dhm = B16.gemm(dut, p.W("cls/predictions/transform/dense/kernel"))
+        if on_bucket_ready is not None:
+            on_bucket_ready(len(p.buckets) - 1)
+        dh = torch.zeros(Tn, cfg.hidden, device=h.device, dtype=BF16)
+        dh.index_add_(0, mask_pos, dhm)  # padding rows carry zero gradient
+        # ---- backward: encoder
+        for l in reversed(range(cfg.layers)):
+            dh = self._layer_bwd(l, dh, saved[l], batch, seq, kmask)
+            saved[l] = None
+            if on_bucket_ready is not None:
+                on_bucket_ready(l + 1)
+        # ---- backward: embeddings
+        dx0 = TR.layernorm_bwd(dh, x0, me, re, p.P("embeddings/LayerNorm/gamma"),
+                               p.G("embeddings/LayerNorm/gamma"), p.G("embeddings/LayerNorm/beta"))
+        TR.embed_bwd(ids_f, tt_f, dx0, p.G("embeddings/word_embeddings"),
+                     p.G("embeddings/position_embeddings"),
+                     p.G("embeddings/token_type_embeddings"), batch, seq)
+        if on_bucket_ready is not None:
+            on_bucket_ready(0)
+        return loss, acc
+
+    def _xent_gpu(self, logits, labels, Tm, scale):
+        cfg = self.cfg
+        from ..ops._ext import hip, ptr, stream_handle
+
+        V, Vp = cfg.vocab_size, cfg.vocab_padded
+        loss = torch.empty(Tm, device=logits.device)
+        correct = torch.empty(Tm, device=logits.device)
+        d = torch.zeros(Tm, Vp, device=logits.device)  # padded columns stay 0
+        lab = labels.to(torch.int32).contiguous()
+        hip().softmax_xent(Tm, V, ptr(logits), Vp, ptr(lab), 0, 0, -100, scale, ptr(loss),
+                           ptr(d), Vp, ptr(correct), 0, stream_handle())
+        return loss, d, correct
+
+    def _layer_bwd(self, l, dout, s, batch, seq, kmask):
+        cfg, p = self.cfg, self.params
+        pre = "encoder/layer_%d/" % l
+        x, qkv, ctx, lse, a, m1, r1, h1, u, g, f, m2, r2 = s
+        df = TR.layernorm_bwd(dout, f, m2, r2, p.P(pre + "output/LayerNorm/gamma"),
+                              p.G(pre + "output/LayerNorm/gamma"), p.G(pre + "output/LayerNorm/beta"))
+        B16.gemm(df, g, True, False, out=p.G(pre + "output/dense/kernel"), beta=1.0)
+        B16.colsum(df, out=p.G(pre + "output/dense/bias"), beta=1.0)
+        du = B16.gemm(df, p.W(pre + "output/dense/kernel"), act_grad="gelu", aux_in=u)
+        B16.gemm(du, h1, True, False, out=p.G(pre + "intermediate/dense/kernel"), beta=1.0)
+        B16.colsum(du, out=p.G(pre + "intermediate/dense/bias"), beta=1.0)
+        dh1 = B16.gemm(du, p.W(pre + "intermediate/dense/kernel"), residual=df)
+        da = TR.layernorm_bwd(dh1, a, m1, r1, p.P(pre + "attention/output/LayerNorm/gamma"),
+                              p.G(pre + "attention/output/LayerNorm/gamma"),
+                              p.G(pre + "attention/output/LayerNorm/beta"))
+        B16.gemm(da, ctx, True, False, out=p.G(pre + "attention/output/dense/kernel"), beta=1.0)
+        B16.colsum(da, out=p.G(pre + "attention/output/dense/bias"), beta=1.0)
+        dctx = B16.gemm(da, p.W(pre + "attention/output/dense/kernel"))
+        dqkv = TR.attn_bwd(qkv, ctx, dctx, lse, batch, seq, cfg.heads, kmask)
+        B16.gemm(dqkv, x, True, False, out=p.G(pre + "attention/qkv/kernel"), beta=1.0)
+        B16.colsum(dqkv, out=p.G(pre + "attention/qkv/bias"), beta=1.0)
+        return B16.gemm(dqkv, p.W(pre + "attention/qkv/kernel"), residual=da)
+
+    # ------------------------------------------------------------------ optimizer
+    def adam_step(self, lr, step, gscale=1.0, wd=0.01, step_ptr=None):
+        p = self.params
+        TR.adam_mixed(p.master, p.grad, p.m, p.v, p.bf, lr, step, wd=wd, gscale=gscale,
+                      step_ptr=step_ptr)
+
+
+def synthetic_mlm_batch(cfg: BertConfig, batch, seq, device, max_pred=None, seed=0, pad_to=64):
+    """Random token ids / segments / masked positions + labels of the MLM shape.
+
+    Returns (ids, tt, mask_pos, labels, n_valid); the masked-position list is
+    padded to a multiple of ``pad_to`` with (position 0, label -100) rows."""
+    g = torch.Generator().manual_seed(seed)
+    max_pred = max_pred or max(1, round(0.15 * seq))
+    ids = torch.randint(0, cfg.vocab_size, (batch, seq), generator=g, dtype=torch.int32)
+    tt = (torch.arange(seq)[None, :] >= seq // 2).to(torch.int32).expand(batch, seq).contiguous()
+    pos = torch.stack([torch.randperm(seq, generator=g)[:max_pred] for _ in range(batch)])
+    flat = (pos + torch.arange(batch)[:, None] * seq).reshape(-1)
+    labels = torch.randint(0, cfg.vocab_size, (flat.numel(),), generator=g, dtype=torch.int32)
+    n_valid = flat.numel()
+    pad = (-n_valid) % pad_to
+    if pad:
+        flat = torch.cat([flat, torch.zeros(pad, dtype=flat.dtype)])
+        labels = torch.cat([labels, torch.full((pad,), -100, dtype=torch.int32)])
+    dev = torch.device(device)
+    return ids.to(dev), tt.to(dev), flat.to(dev), labels.to(dev), n_valid

@@ -80,6 +80,9 @@ def embed_ln_fwd(ids, tt, word, pos, type_, gamma, beta, seq_len, eps=1e-12):
     """x = word[ids] + pos[t % S] + type[tt]; returns (x bf16, LN(x), mean, rstd)."""
     T = ids.numel()
     H = word.shape[1]
+    if seq_len > pos.shape[0] or T % seq_len:
+        raise ValueError("embed_ln_fwd: seq_len %d vs %d positions / %d tokens"
+                         % (seq_len, pos.shape[0], T))
     if not ids.is_cuda:
         p = torch.arange(T) % seq_len
         x = (word[ids.long()].float() + pos[p].float() +
@@ -198,3 +201,22 @@ def cast_bf16(x, out=None):
         return out
     hip().cast_f32_bf16(x.numel(), ptr(x), ptr(out), stream_handle())
     return out
+
+
+def act_grad(dy, u, act="gelu"):
+    """dy * act'(u) for bf16 tensors (act in {"gelu", "relu"})."""
+    a = {"gelu": 1, "relu": 2}[act]
+    if not dy.is_cuda:
+        uf = _f(u)
+        if a == 1:
+            k0, k1 = 0.7978845608028654, 0.044715
+            th = torch.tanh(k0 * (uf + k1 * uf ** 3))
+            d = 0.5 * (1 + th) + 0.5 * uf * (1 - th * th) * k0 * (1 + 3 * k1 * uf * uf)
+        else:
+            d = (uf > 0).to(uf.dtype)
+        return (_f(dy) * d).to(dy.dtype)
+    _contig(dy, "dy", BF16)
+    _contig(u, "u", BF16)
+    dx = torch.empty_like(dy)
+    hip().act_grad_bf16(dy.numel(), a, ptr(dy), ptr(u), ptr(dx), stream_handle())
+    return dx

@@ -1,0 +1,108 @@
+"""Data-parallel BERT-base MLM trainer (north-star config 5 of BASELINE.json).
+
+One process per GPU.  Per step: explicit forward/backward
+(``models.bert.BertMLM``); as soon as an encoder layer's backward is done its
+gradient bucket (one contiguous 28 MB slice of the flat f32 gradient) is
+all-reduced (sum) on a dedicated comm stream, overlapping the remaining
+backward; then one fused mixed-precision AdamW launch over the whole flat
+buffer (gradient averaging folded in as ``gscale = 1/world``) refreshes the
+f32 master weights and the bf16 working copy.  The whole step can be
+captured into one hipGraph (``use_graph``): the RCCL calls of the native
+communicator are graph-capturable.
+
+Reference counterpart: the reference only has async-PS SGD of an MLP
+(worker.py:71-79, 129-159); this is the sync all-reduce design the
+BASELINE.json north star asks for, applied to BERT-base.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..models.bert import BertConfig, BertMLM, synthetic_mlm_batch
+from ..ops import optim as OPT
+
+
+class BertTrainer:
+    def __init__(self, cfg: BertConfig, batch, seq, device, comm=None, lr=1e-4, seed=0,
+                 overlap=True, weight_decay=0.01, data_seed=None):
+        self.cfg, self.batch, self.seq = cfg, batch, seq
+        self.device = torch.device(device)
+        self.comm = comm
+        self.world = comm.world_size if comm is not None else 1
+        self.lr, self.wd = lr, weight_decay
+        self.model = BertMLM(cfg, device, seed)
+        p = self.model.params
+        if self.world > 1:  # replicas start identical (Philox init is seed-determined; broadcast anyway)
+            comm.broadcast_(p.master, 0)
+            from ..ops import transformer as TR
+
+            TR.cast_bf16(p.master, p.bf)
+        self.gpu = self.device.type == "cuda"
+        self.comm_stream = torch.cuda.Stream(self.device) if (self.gpu and overlap and self.world > 1) else None
+        self.data = synthetic_mlm_batch(cfg, batch, seq, device,
+                                        seed=(data_seed if data_seed is not None else 17))
+        self.step_t = torch.ones(1, dtype=torch.int32, device=self.device)  # Adam step (device side)
+        self.step_count = 0
+        self.graph = None
+        self.last = None
+
+    # gradient bucket ready -> all-reduce on the comm stream
+    def _on_bucket(self, i):
+        if self.world == 1:
+            return
+        lo, hi = self.model.params.buckets[i]
+        view = self.model.params.grad[lo:hi]
+        if self.comm_stream is not None:
+            self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.comm_stream):
+                self.comm.allreduce_sum_(view)
+        else:
+            self.comm.allreduce_sum_(view)
+
+    def _step_body(self):
+        ids, tt, pos, lab, nv = self.data
+        loss, acc = self.model.forward_backward(ids, tt, pos, lab, n_valid=nv,
+                                                on_bucket_ready=self._on_bucket)
+        if self.comm_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+        self.model.adam_step(self.lr, 0, gscale=1.0 / self.world, wd=self.wd, step_ptr=self.step_t)
+        OPT.counter_add_(self.step_t, 1)
+        return loss, acc
+
+    def step(self, use_graph=False):
+        if not use_graph:
+            self.last = self._step_body()
+        elif self.graph is None:
+            # this call's step runs eagerly on a side stream (warms the allocator and
+            # the kernels' one-time attributes); the same body is then captured once
+            # and every later call replays it
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self.last = self._step_body()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.last = self._step_body()
+        else:
+            self.graph.replay()
+        self.step_count += 1
+        return self.last
+
+    def run(self, steps, use_graph=False):
+        for _ in range(steps):
+            self.step(use_graph)
+
+    def stats(self):
+        loss, acc = self.last
+        return float(loss.item()), float(acc.item())
+
+    def flops_per_step(self):
+        """Model FLOPs per step on this rank (6 * matmul params * tokens + attention)."""
+        c = self.cfg
+        T = self.batch * self.seq
+        Tm = self.data[2].numel()
+        layer = 2 * T * (3 * c.hidden * c.hidden + c.hidden * c.hidden + 2 * c.hidden * c.ffn)
+        attn = 2 * 2 * self.batch * c.heads * self.seq * self.seq * 64
+        head = 2 * Tm * (c.hidden * c.hidden + c.hidden * c.vocab_padded)
+        return 3 * (c.layers * (layer + attn) + head)
