@@ -10,12 +10,12 @@ namespace dtfx {
 void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const void*, int, void*,
                       int, float, float, const float*, int, const void*, void*, int, const void*,
                       int, int, int, int, long long, long long, long long,
-                      hipStream_t);
+                      float*, hipStream_t);
 void colsum_bf16_launch(const void*, int, int, int, float*, float, hipStream_t);
 void layernorm_fwd_launch(int, int, const void*, const float*, const float*, float, void*, float*,
                           float*, hipStream_t);
 void layernorm_bwd_launch(int, int, const void*, const void*, const float*, const float*,
-                          const float*, const void*, void*, float*, float*, hipStream_t);
+                          const float*, const void*, void*, float*, float*, float*, hipStream_t);
 void embed_ln_fwd_launch(int, int, int, const int*, const int*, const void*, const void*,
                          const void*, const float*, const float*, float, void*, void*, float*,
                          float*, hipStream_t);
@@ -23,11 +23,13 @@ void embed_bwd_launch(int, int, int, const int*, const int*, const void*, float*
                       hipStream_t);
 void attn_fwd_launch(int, int, int, const void*, void*, float*, const float*, float, hipStream_t);
 void attn_bwd_launch(int, int, int, const void*, const void*, const void*, const float*,
-                     const float*, float, void*, hipStream_t);
+                     const float*, float, void*, float*, hipStream_t);
 void adam_mixed_launch(long long, float*, const float*, float*, float*, void*, float, float, float,
                        float, float, float, const int*, int, hipStream_t);
 void cast_f32_bf16_launch(long long, const float*, void*, hipStream_t);
 void act_grad_bf16_launch(long long, int, const void*, const void*, void*, hipStream_t);
+void mlm_xent_launch(int, int, const float*, int, const int*, float, float*, float*, void*, int,
+                     hipStream_t);
 }  // namespace dtfx
 
 template <typename T>
@@ -39,18 +41,19 @@ void register_nn(py::module_& m) {
                         uintptr_t B, int ldb, uintptr_t C, int ldc, float alpha, float beta,
                         uintptr_t bias, int act, uintptr_t aux_in, uintptr_t aux_out, int ld_aux,
                         uintptr_t residual, int ld_res, int act_grad, int splitk, int batch, long long sA,
-                        long long sB, long long sC, uintptr_t s) {
+                        long long sB, long long sC, uintptr_t colsum, uintptr_t s) {
     dtfx::gemm_bf16_launch(ta, tb, out_f32, M, N, K, P<const void>(A), lda, P<const void>(B), ldb,
                            P<void>(C), ldc, alpha, beta, P<const float>(bias), act,
                            P<const void>(aux_in), P<void>(aux_out), ld_aux, P<const void>(residual),
-                           ld_res, act_grad, splitk, batch, sA, sB, sC, S(s));
+                           ld_res, act_grad, splitk, batch, sA, sB, sC,
+                           P<float>(colsum), S(s));
   }, py::arg("ta"), py::arg("tb"), py::arg("out_f32"), py::arg("M"), py::arg("N"), py::arg("K"),
      py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"),
      py::arg("alpha") = 1.f, py::arg("beta") = 0.f, py::arg("bias") = 0, py::arg("act") = 0,
      py::arg("aux_in") = 0, py::arg("aux_out") = 0, py::arg("ld_aux") = 0,
      py::arg("residual") = 0, py::arg("ld_res") = 0, py::arg("act_grad") = 0,
      py::arg("splitk") = 0, py::arg("batch") = 1, py::arg("sA") = 0, py::arg("sB") = 0,
-     py::arg("sC") = 0, py::arg("stream") = 0);
+     py::arg("sC") = 0, py::arg("colsum") = 0, py::arg("stream") = 0);
   m.def("colsum_bf16", [](uintptr_t G, int M, int N, int ldg, uintptr_t out, float beta,
                           uintptr_t s) {
     dtfx::colsum_bf16_launch(P<const void>(G), M, N, ldg, P<float>(out), beta, S(s));
@@ -62,10 +65,10 @@ void register_nn(py::module_& m) {
   });
   m.def("layernorm_bwd", [](int T, int H, uintptr_t dy, uintptr_t x, uintptr_t mean,
                             uintptr_t rstd, uintptr_t g, uintptr_t dres, uintptr_t dx,
-                            uintptr_t dg, uintptr_t db, uintptr_t s) {
+                            uintptr_t dg, uintptr_t db, uintptr_t dxsum, uintptr_t s) {
     dtfx::layernorm_bwd_launch(T, H, P<const void>(dy), P<const void>(x), P<const float>(mean),
                                P<const float>(rstd), P<const float>(g), P<const void>(dres),
-                               P<void>(dx), P<float>(dg), P<float>(db), S(s));
+                               P<void>(dx), P<float>(dg), P<float>(db), P<float>(dxsum), S(s));
   });
   m.def("embed_ln_fwd", [](int T, int Sq, int H, uintptr_t ids, uintptr_t tt, uintptr_t word,
                            uintptr_t pos, uintptr_t type, uintptr_t g, uintptr_t b, float eps,
@@ -87,9 +90,11 @@ void register_nn(py::module_& m) {
                           P<const float>(kmask), scale, S(s));
   });
   m.def("attn_bwd", [](int Bn, int Sq, int nh, uintptr_t qkv, uintptr_t o, uintptr_t dout,
-                       uintptr_t lse, uintptr_t kmask, float scale, uintptr_t dqkv, uintptr_t s) {
+                       uintptr_t lse, uintptr_t kmask, float scale, uintptr_t dqkv,
+                       uintptr_t dbias, uintptr_t s) {
     dtfx::attn_bwd_launch(Bn, Sq, nh, P<const void>(qkv), P<const void>(o), P<const void>(dout),
-                          P<const float>(lse), P<const float>(kmask), scale, P<void>(dqkv), S(s));
+                          P<const float>(lse), P<const float>(kmask), scale, P<void>(dqkv),
+                          P<float>(dbias), S(s));
   });
   m.def("adam_mixed", [](long long n, uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v,
                          uintptr_t pb, float lr, float b1, float b2, float eps, float wd,
@@ -104,5 +109,10 @@ void register_nn(py::module_& m) {
   m.def("act_grad_bf16", [](long long n, int act, uintptr_t dy, uintptr_t u, uintptr_t dx,
                             uintptr_t s) {
     dtfx::act_grad_bf16_launch(n, act, P<const void>(dy), P<const void>(u), P<void>(dx), S(s));
+  });
+  m.def("mlm_xent", [](int N, int C, uintptr_t logits, int ldl, uintptr_t labels, float scale,
+                       uintptr_t loss, uintptr_t correct, uintptr_t dl, int ldd, uintptr_t s) {
+    dtfx::mlm_xent_launch(N, C, P<const float>(logits), ldl, P<const int>(labels), scale,
+                          P<float>(loss), P<float>(correct), P<void>(dl), ldd, S(s));
   });
 }

@@ -137,6 +137,7 @@ struct GemmEpi {
   const unsigned short* residual;  // [M][ld_res] bf16 or null
   int ld_res;
   int act_grad;                 // multiply by act'(aux_in)
+  float* colsum;                // [N] += column sums of the final values (bias gradient), or null
 };
 
 template <bool TA, bool TB, bool OUT_F32>
@@ -209,6 +210,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
   constexpr int EP_LD = 68;
   float* ep = (float*)smem + wave * (32 * EP_LD);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  float cs[8];  // fused column sums (bias gradient) of this lane's 8 columns
+#pragma unroll
+  for (int u = 0; u < 8; ++u) cs[u] = 0.f;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -219,6 +223,18 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
         for (int r = 0; r < 4; ++r)
           ep[(ii * 16 + row_l + r) * EP_LD + j * 16 + col_l] = acc[2 * h + ii][j][r];
     __builtin_amdgcn_wave_barrier();
+    if (OUT_F32 && gridDim.y > 1) {
+      // split-K partial: alpha only; hardware f32 atomics, one 256-B row segment per
+      // wave instruction (lane = column) so each instruction is 4 full 64-B requests
+      const int n = n0 + wn * 64 + lane;
+      for (int rr = 0; rr < 32; ++rr) {
+        const int m = m0 + wm * 64 + h * 32 + rr;
+        if (m < M && n < N)
+          unsafeAtomicAdd((float*)Cv + (size_t)m * ldc + n, e.alpha * ep[rr * EP_LD + lane]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
@@ -228,11 +244,6 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
       *(f32x4*)&v[0] = *(const f32x4*)&ep[rr * EP_LD + cg];
       *(f32x4*)&v[4] = *(const f32x4*)&ep[rr * EP_LD + cg + 4];
       if (m >= M || n >= N) continue;
-      if (OUT_F32 && gridDim.y > 1) {  // split-K partial: alpha only, hardware f32 atomics
-        float* C = (float*)Cv + (size_t)m * ldc + n;
-        for (int u = 0; u < 8 && n + u < N; ++u) unsafeAtomicAdd(C + u, e.alpha * v[u]);
-        continue;
-      }
       const bool full = n + 8 <= N;  // N % 8 != 0 only reaches here with a ragged last group
       float bn[8];
 #pragma unroll
@@ -274,6 +285,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[u]);
         }
+        if (e.colsum) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) cs[u] += v[u];
+        }
         if (OUT_F32) {
           float* C = (float*)Cv + (size_t)m * ldc + n;
           if (e.beta != 0.f) {
@@ -303,6 +318,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
             w *= (e.act_grad == 1) ? gelu_grad_f(uu) : (uu > 0.f ? 1.f : 0.f);
           }
           if (e.residual) w += bf2f(e.residual[(size_t)m * e.ld_res + n + u]);
+          cs[u] += w;
           if (OUT_F32) {
             float* C = (float*)Cv + (size_t)m * ldc + n + u;
             *C = (e.beta != 0.f) ? w + e.beta * *C : w;
@@ -314,15 +330,30 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
     }
     __builtin_amdgcn_wave_barrier();
   }
+  if (e.colsum) {
+    // lanes l, l^8, ..., l^56 hold the same 8 columns for different rows
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      cs[u] += __shfl_xor(cs[u], 8);
+      cs[u] += __shfl_xor(cs[u], 16);
+      cs[u] += __shfl_xor(cs[u], 32);
+    }
+    const int n = n0 + wn * 64 + (lane & 7) * 8;
+    if (lane < 8)
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (n + u < N) unsafeAtomicAdd(e.colsum + n + u, cs[u]);
+  }
 }
 
 void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const void* A, int lda,
                       const void* B, int ldb, void* C, int ldc, float alpha, float beta,
                       const float* bias, int act, const void* aux_in, void* aux_out, int ld_aux,
                       const void* residual, int ld_res, int act_grad, int splitk, int batch,
-                      long long sA, long long sB, long long sC, hipStream_t stream) {
+                      long long sA, long long sB, long long sC, float* colsum,
+                      hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return;
-  if (batch > 1 && (bias || aux_in || aux_out || residual))
+  if (batch > 1 && (bias || aux_in || aux_out || residual || colsum))
     throw std::runtime_error("gemm_bf16: batched GEMM supports alpha/beta/act epilogues only");
   if (batch > 1 && ((sA | sB | sC) % 8))
     throw std::runtime_error("gemm_bf16: batch strides must be multiples of 8 elements");
@@ -343,12 +374,13 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   const int nkt = K / gb::BK;
   if (splitk <= 0) {  // auto: fill the 256 CUs when the output has few tiles and K is deep
     splitk = 1;
-    if (batch == 1 && out_f32 && !bias && !act && !act_grad && !residual && !aux_out && (beta == 0.f || beta == 1.f))
+    if (batch == 1 && out_f32 && !colsum && !bias && !act && !act_grad && !residual && !aux_out && (beta == 0.f || beta == 1.f))
       while (tiles * splitk < 256 && nkt / (splitk * 2) >= 8) splitk *= 2;
   }
   if (splitk > 1) {
     if (batch > 1) throw std::runtime_error("gemm_bf16: split-K with batch > 1 is not supported");
-    if (!out_f32 || bias || act || act_grad || residual || aux_out || (beta != 0.f && beta != 1.f))
+    if (!out_f32 || bias || act || act_grad || residual || aux_out || colsum ||
+        (beta != 0.f && beta != 1.f))
       throw std::runtime_error("gemm_bf16: split-K supports f32 output with alpha and beta in {0,1} only");
     if (beta == 0.f) {
       if (ldc == N) DTFX_HIP_CHECK(hipMemsetAsync(C, 0, sizeof(float) * (size_t)M * N, stream));
@@ -356,7 +388,7 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
     }
   }
   GemmEpi e{alpha, beta, bias, act, (const unsigned short*)aux_in, (unsigned short*)aux_out,
-            ld_aux, (const unsigned short*)residual, ld_res, act_grad};
+            ld_aux, (const unsigned short*)residual, ld_res, act_grad, colsum};
   const dim3 grid(tiles, splitk, batch);
   const size_t lds = 2 * gb::BUF_BYTES;
   auto* Au = (const unsigned short*)A;

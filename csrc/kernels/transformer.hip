@@ -139,15 +139,15 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(
     const unsigned short* __restrict__ x, const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, const float* __restrict__ gamma,
     const unsigned short* __restrict__ dres, unsigned short* __restrict__ dx,
-    float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  __shared__ float red[2][4][2048 / 4 + 4];  // [dgamma|dbeta][wave][...] partials, H <= 2048
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dxsum) {
+  __shared__ float red[3][4][2048 / 4 + 4];  // [dgamma|dbeta|dxsum][wave][...], H <= 2048
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nch = H >> 3;
-  float dg[4][8], db[4][8];
+  float dg[4][8], db[4][8], ds[4][8];
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) dg[c][u] = db[c][u] = 0.f;
+    for (int u = 0; u < 8; ++u) dg[c][u] = db[c][u] = ds[c][u] = 0.f;
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(T, r0 + rows_per_block);
   for (int row = r0 + wave; row < r1; row += 4) {
@@ -184,6 +184,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(
         for (int u = 0; u < 8; ++u) {
           o[u] = rstd * (g[c][u] - s1 - xh[c][u] * s2);
           if (dres) o[u] += rv[u];
+          ds[c][u] += o[u];
         }
         *(bf16x8*)(dx + (size_t)row * H + ch * 8) = pack8(o);
       }
@@ -202,6 +203,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(
           if (col * 4 / H == part) {
             red[0][wave][col - part * (H / 4)] = dg[c][u];
             red[1][wave][col - part * (H / 4)] = db[c][u];
+            red[2][wave][col - part * (H / 4)] = ds[c][u];
           }
         }
     }
@@ -211,6 +213,9 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(
       const float b = red[1][0][i] + red[1][1][i] + red[1][2][i] + red[1][3][i];
       unsafeAtomicAdd(dgamma + part * (H / 4) + i, a);
       unsafeAtomicAdd(dbeta + part * (H / 4) + i, b);
+      if (dxsum)
+        unsafeAtomicAdd(dxsum + part * (H / 4) + i,
+                        red[2][0][i] + red[2][1][i] + red[2][2][i] + red[2][3][i]);
     }
   }
 }
@@ -428,7 +433,8 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_kernel(
 __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(
     int S, int nh, const unsigned short* __restrict__ qkv, const unsigned short* __restrict__ o,
     const unsigned short* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ kmask, float scale, unsigned short* __restrict__ dqkv) {
+    const float* __restrict__ kmask, float scale, unsigned short* __restrict__ dqkv,
+    float* __restrict__ dbias) {
   using namespace at;
   extern __shared__ __attribute__((aligned(16))) char sm[];
   char* Qs = sm;
@@ -539,6 +545,30 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(
           dq[off] = tobf(aq[j][r] * scale);
         }
     }
+    if (dbias) {  // fused qkv bias gradient: column sums over this wave's 16 rows
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float sq = 0.f, sk = 0.f, sv = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // rows >= S hold exact zeros (zero dO / masked P)
+          sq += aq[j][r];
+          sk += ak[j][r];
+          sv += av[j][r];
+        }
+        sq += __shfl_xor(sq, 16);
+        sq += __shfl_xor(sq, 32);
+        sk += __shfl_xor(sk, 16);
+        sk += __shfl_xor(sk, 32);
+        sv += __shfl_xor(sv, 16);
+        sv += __shfl_xor(sv, 32);
+        if (lane < 16) {
+          const int c = h * D + 16 * j + cl;
+          unsafeAtomicAdd(dbias + c, sq * scale);
+          unsafeAtomicAdd(dbias + Hd + c, sk * scale);
+          unsafeAtomicAdd(dbias + 2 * Hd + c, sv);
+        }
+      }
+    }
   }
 }
 
@@ -571,6 +601,87 @@ __global__ __launch_bounds__(256) void adam_mixed_kernel(
     ((f32x4*)m)[i] = mv;
     ((f32x4*)v)[i] = vv;
     if (pb) ((bf16x4*)pb)[i] = o;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MLM loss: softmax cross-entropy over a large vocabulary, one 256-thread block
+// per row.  Pass 1: online (max, sum-exp) + argmax over float4 loads; pass 2:
+// dlogits = (softmax - onehot) * scale written directly as bf16 (the operand of
+// the decoder's dgrad/wgrad GEMMs).  Columns [C, ldd) of dlogits are zeroed.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mlm_xent_kernel(int C, const float* __restrict__ logits,
+                                                       int ldl, const int* __restrict__ labels,
+                                                       float scale, float* __restrict__ loss,
+                                                       float* __restrict__ correct,
+                                                       unsigned short* __restrict__ dl, int ldd) {
+  __shared__ float sm_m[4], sm_s[4];
+  __shared__ int sm_a[4];
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const float* l = logits + (size_t)row * ldl;
+  const int y = labels[row];
+  float m = -INFINITY, sum = 0.f, best = -INFINITY;
+  int am = 0x7fffffff;
+  const int C4 = C >> 2;
+  for (int i = t; i < C4; i += 256) {
+    const f32x4 v = ((const f32x4*)l)[i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float x = v[u];
+      if (x > best) { best = x; am = 4 * i + u; }
+      if (x > m) { sum = sum * __expf(m - x) + 1.f; m = x; }
+      else sum += __expf(x - m);
+    }
+  }
+  for (int c = 4 * C4 + t; c < C; c += 256) {
+    const float x = l[c];
+    if (x > best) { best = x; am = c; }
+    if (x > m) { sum = sum * __expf(m - x) + 1.f; m = x; }
+    else sum += __expf(x - m);
+  }
+  // wave reduce (max, sum) pairs and (best, argmax, lowest index on ties)
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float m2 = __shfl_xor(m, o), s2 = __shfl_xor(sum, o);
+    const float mm = fmaxf(m, m2);
+    sum = (m == -INFINITY ? 0.f : sum * __expf(m - mm)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
+    m = mm;
+    const float b2 = __shfl_xor(best, o);
+    const int a2 = __shfl_xor(am, o);
+    if (b2 > best || (b2 == best && a2 < am)) { best = b2; am = a2; }
+  }
+  if (lane == 0) { sm_m[wave] = m; sm_s[wave] = sum; sm_a[wave] = am; }
+  __syncthreads();
+  float M = sm_m[0], Ssum = 0.f;
+  for (int w = 1; w < 4; ++w) M = fmaxf(M, sm_m[w]);
+  for (int w = 0; w < 4; ++w) Ssum += sm_m[w] == -INFINITY ? 0.f : sm_s[w] * __expf(sm_m[w] - M);
+  // argmax across waves: recompute best value by index order
+  int A = sm_a[0];
+  float Bv = l[A < C ? A : 0];
+  for (int w = 1; w < 4; ++w) {
+    const int a = sm_a[w];
+    if (a < C) {
+      const float bv = l[a];
+      if (bv > Bv || (bv == Bv && a < A)) { Bv = bv; A = a; }
+    }
+  }
+  const bool valid = y >= 0 && y < C;
+  const float lse = M + __logf(Ssum);
+  if (t == 0) {
+    loss[row] = valid ? lse - l[y] : 0.f;
+    correct[row] = (valid && A == y) ? 1.f : 0.f;
+  }
+  unsigned short* d = dl + (size_t)row * ldd;
+  const float sc = valid ? scale : 0.f;
+  for (int i = t; i < (ldd >> 2); i += 256) {
+    bf16x4 o;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = 4 * i + u;
+      float g = 0.f;
+      if (c < C) g = (__expf(l[c] - lse) - (c == y ? 1.f : 0.f)) * sc;
+      o[u] = (short)tobf(g);
+    }
+    ((bf16x4*)d)[i] = o;
   }
 }
 
@@ -626,13 +737,13 @@ void layernorm_fwd_launch(int T, int H, const void* x, const float* gamma, const
 
 void layernorm_bwd_launch(int T, int H, const void* dy, const void* x, const float* mean,
                           const float* rstd, const float* gamma, const void* dres, void* dx,
-                          float* dgamma, float* dbeta, hipStream_t s) {
+                          float* dgamma, float* dbeta, float* dxsum, hipStream_t s) {
   check_h(H);
   if (T <= 0) return;
-  const int rpb = 64;
+  const int rpb = T >= 8192 ? 32 : 16;  // >= 256 blocks for BERT-size inputs
   hipLaunchKernelGGL(layernorm_bwd_kernel, dim3((T + rpb - 1) / rpb), dim3(256), 0, s, T, H, rpb,
                      (const unsigned short*)dy, (const unsigned short*)x, mean, rstd, gamma,
-                     (const unsigned short*)dres, (unsigned short*)dx, dgamma, dbeta);
+                     (const unsigned short*)dres, (unsigned short*)dx, dgamma, dbeta, dxsum);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
@@ -682,7 +793,8 @@ void attn_fwd_launch(int Bn, int S, int nh, const void* qkv, void* out, float* l
 }
 
 void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, const void* dout,
-                     const float* lse, const float* kmask, float scale, void* dqkv, hipStream_t s) {
+                     const float* lse, const float* kmask, float scale, void* dqkv, float* dbias,
+                     hipStream_t s) {
   check_attn(S, nh);
   const size_t lds = 4 * at::QB + 2 * at::PB + at::SP * 4;
   static bool attr = false;
@@ -693,7 +805,7 @@ void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, cons
   }
   hipLaunchKernelGGL(attn_bwd_kernel, dim3(Bn * nh), dim3(256), lds, s, S, nh,
                      (const unsigned short*)qkv, (const unsigned short*)o,
-                     (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv);
+                     (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv, dbias);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
@@ -706,6 +818,16 @@ void adam_mixed_launch(long long n, float* p, const float* g, float* m, float* v
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(adam_mixed_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
                      (unsigned short*)pb, lr, b1, b2, eps, wd, gscale, step_ptr, step);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void mlm_xent_launch(int N, int C, const float* logits, int ldl, const int* labels, float scale,
+                     float* loss, float* correct, void* dl, int ldd, hipStream_t s) {
+  if (ldl % 4 || ldd % 4 || ldd < C || ldl < C)
+    throw std::runtime_error("mlm_xent: ldl/ldd must be multiples of 4 and >= C");
+  if (N <= 0) return;
+  hipLaunchKernelGGL(mlm_xent_kernel, dim3(N), dim3(256), 0, s, C, logits, ldl, labels, scale, loss,
+                     correct, (unsigned short*)dl, ldd);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

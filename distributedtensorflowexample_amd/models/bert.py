@@ -216,14 +216,7 @@ class BertMLM:
                           out_dtype=torch.float32)
         Tm = tn.shape[0]
         scale = 1.0 / max(1, n_valid if n_valid is not None else Tm)
-        if logits.is_cuda:
-            loss_rows, dlog, correct = self._xent_gpu(logits, mask_labels, Tm, scale)
-        else:
-            loss_rows, d, correct = NN.softmax_xent_stats(logits[:, :cfg.vocab_size], mask_labels,
-                                                          want_grad=True, scale=scale)
-            dlog = torch.zeros(Tm, cfg.vocab_padded)
-            dlog[:, :cfg.vocab_size] = d
-        dlog_b = TR.cast_bf16(dlog)
+        loss_rows, correct, dlog_b = TR.mlm_xent(logits, mask_labels, cfg.vocab_size, scale)
         loss = loss_rows.sum() * scale
         acc = correct.sum() * scale
         # ---- backward: head
@@ -257,40 +250,29 @@ class BertMLM:
             on_bucket_ready(0)
         return loss, acc
 
-    def _xent_gpu(self, logits, labels, Tm, scale):
-        cfg = self.cfg
-        from ..ops._ext import hip, ptr, stream_handle
-
-        V, Vp = cfg.vocab_size, cfg.vocab_padded
-        loss = torch.empty(Tm, device=logits.device)
-        correct = torch.empty(Tm, device=logits.device)
-        d = torch.zeros(Tm, Vp, device=logits.device)  # padded columns stay 0
-        lab = labels.to(torch.int32).contiguous()
-        hip().softmax_xent(Tm, V, ptr(logits), Vp, ptr(lab), 0, 0, -100, scale, ptr(loss),
-                           ptr(d), Vp, ptr(correct), 0, stream_handle())
-        return loss, d, correct
-
     def _layer_bwd(self, l, dout, s, batch, seq, kmask):
         cfg, p = self.cfg, self.params
         pre = "encoder/layer_%d/" % l
         x, qkv, ctx, lse, a, m1, r1, h1, u, g, f, m2, r2 = s
+        # bias gradients are fused into the producer of each activation gradient:
+        # LayerNorm bwd (df, da), the act-grad GEMM epilogue (du), attention bwd (dqkv)
         df = TR.layernorm_bwd(dout, f, m2, r2, p.P(pre + "output/LayerNorm/gamma"),
-                              p.G(pre + "output/LayerNorm/gamma"), p.G(pre + "output/LayerNorm/beta"))
+                              p.G(pre + "output/LayerNorm/gamma"), p.G(pre + "output/LayerNorm/beta"),
+                              dxsum=p.G(pre + "output/dense/bias"))
         B16.gemm(df, g, True, False, out=p.G(pre + "output/dense/kernel"), beta=1.0)
-        B16.colsum(df, out=p.G(pre + "output/dense/bias"), beta=1.0)
-        du = B16.gemm(df, p.W(pre + "output/dense/kernel"), act_grad="gelu", aux_in=u)
+        du = B16.gemm(df, p.W(pre + "output/dense/kernel"), act_grad="gelu", aux_in=u,
+                      colsum=p.G(pre + "intermediate/dense/bias"))
         B16.gemm(du, h1, True, False, out=p.G(pre + "intermediate/dense/kernel"), beta=1.0)
-        B16.colsum(du, out=p.G(pre + "intermediate/dense/bias"), beta=1.0)
         dh1 = B16.gemm(du, p.W(pre + "intermediate/dense/kernel"), residual=df)
         da = TR.layernorm_bwd(dh1, a, m1, r1, p.P(pre + "attention/output/LayerNorm/gamma"),
                               p.G(pre + "attention/output/LayerNorm/gamma"),
-                              p.G(pre + "attention/output/LayerNorm/beta"))
+                              p.G(pre + "attention/output/LayerNorm/beta"),
+                              dxsum=p.G(pre + "attention/output/dense/bias"))
         B16.gemm(da, ctx, True, False, out=p.G(pre + "attention/output/dense/kernel"), beta=1.0)
-        B16.colsum(da, out=p.G(pre + "attention/output/dense/bias"), beta=1.0)
         dctx = B16.gemm(da, p.W(pre + "attention/output/dense/kernel"))
-        dqkv = TR.attn_bwd(qkv, ctx, dctx, lse, batch, seq, cfg.heads, kmask)
+        dqkv = TR.attn_bwd(qkv, ctx, dctx, lse, batch, seq, cfg.heads, kmask,
+                           dbias=p.G(pre + "attention/qkv/bias"))
         B16.gemm(dqkv, x, True, False, out=p.G(pre + "attention/qkv/kernel"), beta=1.0)
-        B16.colsum(dqkv, out=p.G(pre + "attention/qkv/bias"), beta=1.0)
         return B16.gemm(dqkv, p.W(pre + "attention/qkv/kernel"), residual=da)
 
     # ------------------------------------------------------------------ optimizer

@@ -39,7 +39,8 @@ def _check(t, name, dtype=torch.bfloat16):
 
 
 def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=None, aux_in=None,
-         act_grad=None, residual=None, out=None, out_dtype=torch.bfloat16, alpha=1.0, beta=0.0, splitk=0):
+         act_grad=None, residual=None, out=None, out_dtype=torch.bfloat16, alpha=1.0, beta=0.0, splitk=0,
+         colsum=None):
     """``out = epi(alpha * op(a) @ op(b))``, bf16 operands, f32 accumulate.
 
     Epilogue order: ``+bias`` -> ``aux_out = v`` (pre-activation, bf16) ->
@@ -47,6 +48,8 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
     ``act`` / ``act_grad`` in {None, "gelu", "relu"}.  ``splitk`` (0 = auto)
     splits K over workgroups for f32 outputs without epilogue (weight
     gradients: few output tiles, deep K), combining with f32 atomics.
+    ``colsum`` (f32 [N]) accumulates the column sums of the final values
+    (a fused bias gradient of the produced activation gradient).
     """
     act_i = ACT[act]
     ag_i = ACT[act_grad]
@@ -75,6 +78,8 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
             v = v * (_gelu_grad_ref(u) if ag_i == 1 else (u > 0).float())
         if residual is not None:
             v = v + residual.float()
+        if colsum is not None:
+            colsum += v.sum(0)
         if out is not None:
             if beta != 0.0:
                 v = v + beta * out.float()
@@ -107,13 +112,16 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
         if not (bias.is_cuda and bias.dtype == torch.float32 and bias.numel() == N
                 and bias.is_contiguous()):
             raise ValueError("gemm_bf16: bias must be a contiguous f32 GPU vector of N elements")
+    if colsum is not None and not (colsum.is_cuda and colsum.dtype == torch.float32 and
+                                   colsum.numel() == N and colsum.is_contiguous()):
+        raise ValueError("gemm_bf16: colsum must be a contiguous f32 GPU vector of N elements")
     aux = aux_in if aux_in is not None else aux_out
     hip().gemm_bf16(bool(trans_a), bool(trans_b), out.dtype == torch.float32, M, N, K,
                     ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(out), out.stride(0),
                     float(alpha), float(beta), ptr(bias), act_i, ptr(aux_in), ptr(aux_out),
                     aux.stride(0) if aux is not None else 0, ptr(residual),
                     residual.stride(0) if residual is not None else 0, ag_i, int(splitk),
-                    stream=stream_handle())
+                    colsum=ptr(colsum), stream=stream_handle())
     return out
 
 

@@ -54,8 +54,9 @@ def layernorm_fwd(x, gamma, beta, eps=1e-12):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None):
-    """Returns dx; accumulates dgamma/dbeta (f32) in place."""
+def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None, dxsum=None):
+    """Returns dx; accumulates dgamma/dbeta (f32) in place, and the column sums of
+    dx into ``dxsum`` when given (the next linear layer's bias gradient, fused)."""
     T, H = x.shape
     if not x.is_cuda:
         xf, g = _f(x), _f(dy)
@@ -66,12 +67,14 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None):
             dx = dx + _f(dres)
         dgamma += (g * xh).sum(0)
         dbeta += g.sum(0)
+        if dxsum is not None:
+            dxsum += dx.sum(0)
         return dx.to(x.dtype)
     for t, n in ((dy, "dy"), (x, "x"), (dres, "dres")):
         _contig(t, n, BF16)
     dx = torch.empty_like(x)
     hip().layernorm_bwd(T, H, ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), ptr(dres),
-                        ptr(dx), ptr(dgamma), ptr(dbeta), stream_handle())
+                        ptr(dx), ptr(dgamma), ptr(dbeta), ptr(dxsum), stream_handle())
     return dx
 
 
@@ -145,8 +148,9 @@ def attn_fwd(qkv, batch, seq, nh, kmask=None, scale=None):
     return out, lse
 
 
-def attn_bwd(qkv, o, dout, lse, batch, seq, nh, kmask=None, scale=None):
-    """Gradient w.r.t. the fused QKV activations, same layout as ``qkv``."""
+def attn_bwd(qkv, o, dout, lse, batch, seq, nh, kmask=None, scale=None, dbias=None):
+    """Gradient w.r.t. the fused QKV activations, same layout as ``qkv``; adds its
+    column sums (the QKV bias gradient) into ``dbias`` when given."""
     scale = 1.0 / math.sqrt(64) if scale is None else scale
     if not qkv.is_cuda:
         q, k, v = _split(qkv, batch, seq, nh)
@@ -164,12 +168,15 @@ def attn_bwd(qkv, o, dout, lse, batch, seq, nh, kmask=None, scale=None):
         dk = ds.transpose(-1, -2) @ q * scale
         dq = ds @ k * scale
         g = torch.stack([dq, dk, dv], 0)  # [3, B, nh, S, d]
-        return g.permute(1, 3, 0, 2, 4).reshape(batch * seq, 3 * nh * 64).to(BF16)
+        g = g.permute(1, 3, 0, 2, 4).reshape(batch * seq, 3 * nh * 64)
+        if dbias is not None:
+            dbias += g.sum(0)
+        return g.to(BF16)
     for t, n in ((qkv, "qkv"), (o, "o"), (dout, "dout")):
         _contig(t, n, BF16)
     dqkv = torch.empty_like(qkv)
     hip().attn_bwd(batch, seq, nh, ptr(qkv), ptr(o), ptr(dout), ptr(lse), ptr(kmask), float(scale),
-                   ptr(dqkv), stream_handle())
+                   ptr(dqkv), ptr(dbias), stream_handle())
     return dqkv
 
 
@@ -220,3 +227,26 @@ def act_grad(dy, u, act="gelu"):
     dx = torch.empty_like(dy)
     hip().act_grad_bf16(dy.numel(), a, ptr(dy), ptr(u), ptr(dx), stream_handle())
     return dx
+
+
+def mlm_xent(logits, labels, n_classes, scale):
+    """Softmax cross-entropy over the first ``n_classes`` columns of f32 ``logits``
+    [N, ldl]; labels int32 (-100 = ignore).  Returns (loss_rows, correct_rows,
+    dlogits bf16 [N, ldl] pre-scaled by ``scale``, zero beyond n_classes)."""
+    N, ldl = logits.shape
+    if not logits.is_cuda:
+        from .nn import softmax_xent_stats
+
+        loss, d, correct = softmax_xent_stats(logits[:, :n_classes].float(), labels,
+                                              want_grad=True, scale=scale)
+        dl = torch.zeros(N, ldl, dtype=BF16)
+        dl[:, :n_classes] = d.to(BF16)
+        return loss, correct, dl
+    _contig(logits, "logits", torch.float32)
+    lab = labels.to(torch.int32).contiguous()
+    loss = torch.empty(N, device=logits.device)
+    correct = torch.empty(N, device=logits.device)
+    dl = torch.empty(N, ldl, device=logits.device, dtype=BF16)
+    hip().mlm_xent(N, n_classes, ptr(logits), ldl, ptr(lab), float(scale), ptr(loss), ptr(correct),
+                   ptr(dl), ldl, stream_handle())
+    return loss, correct, dl

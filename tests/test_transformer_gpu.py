@@ -84,3 +84,41 @@ def test_adam_mixed_and_cast(gpu):
     assert torch.allclose(P.cpu(), p, atol=1e-6, rtol=1e-5)
     assert torch.equal(pb.cpu(), P.cpu().to(BF))
     assert torch.equal(T.cast_bf16(G).cpu(), g.to(BF))
+
+
+def test_mlm_xent_matches_reference(gpu):
+    N, C, ld = 70, 1003, 1024
+    logits = _r(N, ld, seed=20) * 3
+    lab = torch.randint(0, C, (N,), dtype=torch.int32)
+    lab[5] = -100
+    lg, cg, dg = T.mlm_xent(logits.to(gpu), lab.to(gpu), C, 1 / 69)
+    lr, cr, dr = T.mlm_xent(logits, lab, C, 1 / 69)
+    assert torch.allclose(lg.cpu(), lr, atol=1e-4)
+    assert torch.equal(cg.cpu(), cr)
+    assert (dg.cpu().float() - dr.float()).abs().max() < 1e-4
+    assert (dg[:, C:] == 0).all()
+
+
+def test_fused_bias_grads(gpu):
+    from distributedtensorflowexample_amd.ops import bf16
+
+    Tn, H = 256, 128
+    x = _r(Tn, H, seed=21).to(BF)
+    gamma = torch.ones(H)
+    y, mean, rstd = T.layernorm_fwd(x, gamma, torch.zeros(H))
+    dy = _r(Tn, H, seed=22).to(BF)
+    s = torch.zeros(H, device=gpu)
+    dx = T.layernorm_bwd(dy.to(gpu), x.to(gpu), mean.to(gpu), rstd.to(gpu), gamma.to(gpu),
+                         torch.zeros(H, device=gpu), torch.zeros(H, device=gpu), dxsum=s)
+    # f32 sums vs sums of the bf16-rounded outputs: ~sqrt(T) * 2^-9 apart
+    assert torch.allclose(s.cpu(), dx.cpu().float().sum(0), atol=0.15)
+    w = _r(64, H, seed=23).to(BF).to(gpu)
+    cs = torch.zeros(64, device=gpu)
+    out = bf16.gemm(dx, w, False, True, colsum=cs, out_dtype=torch.float32)
+    assert torch.allclose(cs, out.sum(0), atol=1e-3, rtol=1e-4)
+    B, S, nh = 2, 128, 2
+    qkv = _r(B * S, 3 * nh * 64, seed=24).to(BF).to(gpu)
+    o, lse = T.attn_fwd(qkv, B, S, nh)
+    db = torch.zeros(3 * nh * 64, device=gpu)
+    dq = T.attn_bwd(qkv, o, _r(B * S, nh * 64, seed=25).to(BF).to(gpu), lse, B, S, nh, dbias=db)
+    assert torch.allclose(db, dq.float().sum(0), atol=0.15, rtol=1e-2)
