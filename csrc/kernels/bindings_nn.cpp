@@ -12,6 +12,20 @@ void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const v
                       int, int, int, int, long long, long long, long long,
                       float*, hipStream_t);
 void colsum_bf16_launch(const void*, int, int, int, float*, float, hipStream_t);
+void conv_bf16_launch(int, int, int, int, int, int, int, int, int, int, const void*, const void*, int,
+                      void*, float, const void*, float*, float*, int, hipStream_t);
+void bn_finalize_launch(int, long long, const float*, const float*, float, float*, float*, float*,
+                        float*, float, hipStream_t);
+void bn_apply_launch(long long, int, const void*, const float*, const float*, const float*,
+                     const float*, const void*, int, void*, hipStream_t);
+void bn_bwd_launch(long long, int, const void*, const void*, const void*, const float*, const float*,
+                   const float*, int, float*, float*, void*, void*, hipStream_t);
+void maxpool_fwd_launch(int, int, int, int, const void*, void*, void*, hipStream_t);
+void maxpool_bwd_launch(int, int, int, int, const void*, const void*, void*, hipStream_t);
+void avgpool_fwd_launch(int, int, int, const void*, void*, hipStream_t);
+void avgpool_bwd_launch(int, int, int, const void*, void*, hipStream_t);
+void sgd_momentum_mixed_launch(long long, float*, const float*, float*, void*, float, float, float,
+                               float, hipStream_t);
 void layernorm_fwd_launch(int, int, const void*, const float*, const float*, float, void*, float*,
                           float*, hipStream_t);
 void layernorm_bwd_launch(int, int, const void*, const void*, const float*, const float*,
@@ -114,5 +128,50 @@ void register_nn(py::module_& m) {
                        uintptr_t loss, uintptr_t correct, uintptr_t dl, int ldd, uintptr_t s) {
     dtfx::mlm_xent_launch(N, C, P<const float>(logits), ldl, P<const int>(labels), scale,
                           P<float>(loss), P<float>(correct), P<void>(dl), ldd, S(s));
+  });
+  m.def("conv_bf16", [](int mode, int N, int H, int W, int C, int Cout, int KH, int KW, int stride,
+                        int pad, uintptr_t a, uintptr_t b, int ldw, uintptr_t out, float beta,
+                        uintptr_t residual, uintptr_t colsum, uintptr_t colsq, int splitk,
+                        uintptr_t s) {
+    dtfx::conv_bf16_launch(mode, N, H, W, C, Cout, KH, KW, stride, pad, P<const void>(a),
+                           P<const void>(b), ldw, P<void>(out), beta, P<const void>(residual),
+                           P<float>(colsum), P<float>(colsq), splitk, S(s));
+  });
+  m.def("bn_finalize", [](int C, long long M, uintptr_t s_, uintptr_t q, float eps, uintptr_t mean,
+                          uintptr_t rstd, uintptr_t rm, uintptr_t rv, float momentum, uintptr_t s) {
+    dtfx::bn_finalize_launch(C, M, P<const float>(s_), P<const float>(q), eps, P<float>(mean),
+                             P<float>(rstd), P<float>(rm), P<float>(rv), momentum, S(s));
+  });
+  m.def("bn_apply", [](long long M, int C, uintptr_t x, uintptr_t mean, uintptr_t rstd,
+                       uintptr_t g, uintptr_t b, uintptr_t res, int relu, uintptr_t y, uintptr_t s) {
+    dtfx::bn_apply_launch(M, C, P<const void>(x), P<const float>(mean), P<const float>(rstd),
+                          P<const float>(g), P<const float>(b), P<const void>(res), relu, P<void>(y),
+                          S(s));
+  });
+  m.def("bn_bwd", [](long long M, int C, uintptr_t dy, uintptr_t yout, uintptr_t x, uintptr_t mean,
+                     uintptr_t rstd, uintptr_t g, int relu, uintptr_t sdy, uintptr_t sdyxh,
+                     uintptr_t dx, uintptr_t dres, uintptr_t s) {
+    dtfx::bn_bwd_launch(M, C, P<const void>(dy), P<const void>(yout), P<const void>(x),
+                        P<const float>(mean), P<const float>(rstd), P<const float>(g), relu,
+                        P<float>(sdy), P<float>(sdyxh), P<void>(dx), P<void>(dres), S(s));
+  });
+  m.def("maxpool_fwd", [](int N, int H, int W, int C, uintptr_t x, uintptr_t y, uintptr_t idx,
+                          uintptr_t s) {
+    dtfx::maxpool_fwd_launch(N, H, W, C, P<const void>(x), P<void>(y), P<void>(idx), S(s));
+  });
+  m.def("maxpool_bwd", [](int N, int H, int W, int C, uintptr_t dy, uintptr_t idx, uintptr_t dx,
+                          uintptr_t s) {
+    dtfx::maxpool_bwd_launch(N, H, W, C, P<const void>(dy), P<const void>(idx), P<void>(dx), S(s));
+  });
+  m.def("avgpool_fwd", [](int N, int HW, int C, uintptr_t x, uintptr_t y, uintptr_t s) {
+    dtfx::avgpool_fwd_launch(N, HW, C, P<const void>(x), P<void>(y), S(s));
+  });
+  m.def("avgpool_bwd", [](int N, int HW, int C, uintptr_t dy, uintptr_t dx, uintptr_t s) {
+    dtfx::avgpool_bwd_launch(N, HW, C, P<const void>(dy), P<void>(dx), S(s));
+  });
+  m.def("sgd_momentum_mixed", [](long long n, uintptr_t p, uintptr_t g, uintptr_t v, uintptr_t pb,
+                                 float lr, float mu, float wd, float gscale, uintptr_t s) {
+    dtfx::sgd_momentum_mixed_launch(n, P<float>(p), P<const float>(g), P<float>(v), P<void>(pb), lr,
+                                    mu, wd, gscale, S(s));
   });
 }

@@ -1,0 +1,351 @@
+// CNN (ResNet-50) kernels for gfx950, NHWC bf16 activations viewed as
+// [M = N*H*W][C]: BatchNorm (statistics fused into the convolution GEMM
+// epilogue, see gemm_bf16.hip; here finalize / apply(+residual +ReLU) /
+// backward), 3x3/s2 max-pool fwd/bwd (argmax byte, gather backward: no
+// atomics), global average pool fwd/bwd, and mixed-precision momentum SGD.
+// North-star config 4 of BASELINE.json (ResNet-50 synthetic ImageNet); the
+// reference itself has no convolutional model (worker.py:47-54).
+#include "common.h"
+
+#include <stdexcept>
+
+namespace dtfx {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+namespace cn {
+__device__ __forceinline__ float bf(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+__device__ __forceinline__ unsigned short tobf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(unsigned short, b);
+}
+__device__ __forceinline__ void unpack8(const bf16x8& v, float* f) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) f[u] = bf((unsigned short)v[u]);
+}
+__device__ __forceinline__ bf16x8 pack8(const float* f) {
+  bf16x8 v;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = (short)tobf(f[u]);
+  return v;
+}
+}  // namespace cn
+using namespace cn;
+
+// mean = s / M, var = q / M - mean^2 (biased, as used for normalisation),
+// running stats updated with the unbiased variance (momentum form of tf/keras).
+__global__ void bn_finalize_kernel(int C, float inv_m, float unbias, const float* __restrict__ s,
+                                   const float* __restrict__ q, float eps, float* __restrict__ mean,
+                                   float* __restrict__ rstd, float* __restrict__ run_mean,
+                                   float* __restrict__ run_var, float momentum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float mu = s[c] * inv_m;
+  const float var = fmaxf(q[c] * inv_m - mu * mu, 0.f);
+  mean[c] = mu;
+  rstd[c] = rsqrtf(var + eps);
+  if (run_mean) {
+    run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * mu;
+    run_var[c] = momentum * run_var[c] + (1.f - momentum) * var * unbias;
+  }
+}
+
+// y = act((x - mean) * rstd * gamma + beta + residual); 8 channels per thread
+__global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
+                                                       const unsigned short* __restrict__ x,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta,
+                                                       const unsigned short* __restrict__ res,
+                                                       int relu, unsigned short* __restrict__ y) {
+  const int cg = C >> 3;
+  const long long n8 = M * cg;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const int c0 = (int)(i % cg) * 8;
+    float v[8], r[8];
+    unpack8(((const bf16x8*)x)[i], v);
+    if (res) unpack8(((const bf16x8*)res)[i], r);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = c0 + u;
+      float o = (v[u] - mean[c]) * rstd[c] * gamma[c] + beta[c];
+      if (res) o += r[u];
+      if (relu) o = fmaxf(o, 0.f);
+      v[u] = o;
+    }
+    ((bf16x8*)y)[i] = pack8(v);
+  }
+}
+
+// Backward reductions: dy_eff = dy * (y > 0 if relu); sums over rows of dy_eff and
+// dy_eff * xhat per channel.  Block = 256 threads over a [rows x C] slab; each thread
+// owns 8 channels of a fixed channel group and strides over rows.
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
+    long long M, int C, int rows_per_block, const unsigned short* __restrict__ dy,
+    const unsigned short* __restrict__ yout, const unsigned short* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ rstd, int relu,
+    float* __restrict__ sum_dy, float* __restrict__ sum_dyxh) {
+  const int cg = C >> 3;
+  const int tpr = min(cg, 256);           // threads per row (channel groups covered per pass)
+  const int rpp = 256 / tpr;              // rows per pass
+  const int t = threadIdx.x;
+  const int g = t % tpr, rr = t / tpr;
+  if (rr >= rpp) return;
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = min(M, r0 + rows_per_block);
+  for (int gg = g; gg < cg; gg += tpr) {
+    float a[8], b[8], mu[8], rs[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = b[u] = 0.f;
+      mu[u] = mean[gg * 8 + u];
+      rs[u] = rstd[gg * 8 + u];
+    }
+    for (long long r = r0 + rr; r < r1; r += rpp) {
+      const long long i = r * cg + gg;
+      float d[8], xv[8], yv[8];
+      unpack8(((const bf16x8*)dy)[i], d);
+      unpack8(((const bf16x8*)x)[i], xv);
+      if (relu) unpack8(((const bf16x8*)yout)[i], yv);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float de = (relu && yv[u] <= 0.f) ? 0.f : d[u];
+        a[u] += de;
+        b[u] += de * (xv[u] - mu[u]) * rs[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      unsafeAtomicAdd(sum_dy + gg * 8 + u, a[u]);
+      unsafeAtomicAdd(sum_dyxh + gg * 8 + u, b[u]);
+    }
+  }
+}
+
+// dx = gamma * rstd * (dy_eff - sum_dy / M - xhat * sum_dyxh / M); dres = dy_eff (optional)
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    long long M, int C, const unsigned short* __restrict__ dy, const unsigned short* __restrict__ yout,
+    const unsigned short* __restrict__ x, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ gamma,
+    const float* __restrict__ sum_dy, const float* __restrict__ sum_dyxh, int relu, float inv_m,
+    unsigned short* __restrict__ dx, unsigned short* __restrict__ dres) {
+  const int cg = C >> 3;
+  const long long n8 = M * cg;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const int c0 = (int)(i % cg) * 8;
+    float d[8], xv[8], yv[8], o[8];
+    unpack8(((const bf16x8*)dy)[i], d);
+    unpack8(((const bf16x8*)x)[i], xv);
+    if (relu) unpack8(((const bf16x8*)yout)[i], yv);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = c0 + u;
+      const float de = (relu && yv[u] <= 0.f) ? 0.f : d[u];
+      d[u] = de;
+      const float xh = (xv[u] - mean[c]) * rstd[c];
+      o[u] = gamma[c] * rstd[c] * (de - sum_dy[c] * inv_m - xh * sum_dyxh[c] * inv_m);
+    }
+    ((bf16x8*)dx)[i] = pack8(o);
+    if (dres) ((bf16x8*)dres)[i] = pack8(d);
+  }
+}
+
+// 3x3 / stride 2 / pad 1 max pool, NHWC; idx = argmax tap (first max) per output element
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(int N, int H, int W, int C, int OH, int OW,
+                                                          const unsigned short* __restrict__ x,
+                                                          unsigned short* __restrict__ y,
+                                                          unsigned char* __restrict__ idx) {
+  const long long total = (long long)N * OH * OW * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int c = (int)(i % C);
+    long long p = i / C;
+    const int ow = (int)(p % OW);
+    p /= OW;
+    const int oh = (int)(p % OH);
+    const int n = (int)(p / OH);
+    float best = -INFINITY;
+    int bi = 0;
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = oh * 2 - 1 + kh;
+      if (ih < 0 || ih >= H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = ow * 2 - 1 + kw;
+        if (iw < 0 || iw >= W) continue;
+        const float v = bf(x[(((size_t)n * H + ih) * W + iw) * C + c]);
+        if (v > best) { best = v; bi = kh * 3 + kw; }
+      }
+    }
+    y[i] = tobf(best);
+    idx[i] = (unsigned char)bi;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(int N, int H, int W, int C, int OH, int OW,
+                                                          const unsigned short* __restrict__ dy,
+                                                          const unsigned char* __restrict__ idx,
+                                                          unsigned short* __restrict__ dx) {
+  const long long total = (long long)N * H * W * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int c = (int)(i % C);
+    long long p = i / C;
+    const int iw = (int)(p % W);
+    p /= W;
+    const int ih = (int)(p % H);
+    const int n = (int)(p / H);
+    float acc = 0.f;
+    // outputs whose window covers (ih, iw): oh = (ih + 1 - kh) / 2 for kh in 0..2
+    for (int kh = 0; kh < 3; ++kh) {
+      const int t = ih + 1 - kh;
+      if (t < 0 || (t & 1)) continue;
+      const int oh = t >> 1;
+      if (oh >= OH) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int u = iw + 1 - kw;
+        if (u < 0 || (u & 1)) continue;
+        const int ow = u >> 1;
+        if (ow >= OW) continue;
+        const size_t o = (((size_t)n * OH + oh) * OW + ow) * C + c;
+        if (idx[o] == kh * 3 + kw) acc += bf(dy[o]);
+      }
+    }
+    dx[i] = tobf(acc);
+  }
+}
+
+// global average pool: x [N][HW][C] -> y [N][C] (bf16); thread per (n, c)
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(int N, int HW, int C,
+                                                          const unsigned short* __restrict__ x,
+                                                          unsigned short* __restrict__ y) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i % C;
+  float s = 0.f;
+  for (int p = 0; p < HW; ++p) s += bf(x[((size_t)n * HW + p) * C + c]);
+  y[i] = tobf(s / HW);
+}
+
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(int N, int HW, int C,
+                                                          const unsigned short* __restrict__ dy,
+                                                          unsigned short* __restrict__ dx) {
+  const long long total = (long long)N * HW * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int c = (int)(i % C);
+    const int n = (int)(i / ((long long)HW * C));
+    dx[i] = tobf(bf(dy[(size_t)n * C + c]) / HW);
+  }
+}
+
+// momentum SGD on f32 master weights (+ L2 weight decay), refreshes the bf16 copy
+__global__ __launch_bounds__(256) void sgd_momentum_mixed_kernel(
+    long long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ v,
+    unsigned short* __restrict__ pb, float lr, float mu, float wd, float gscale) {
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 pv = ((f32x4*)p)[i], gv = ((const f32x4*)g)[i], vv = ((f32x4*)v)[i];
+    ushort4 o;
+    unsigned short* op = (unsigned short*)&o;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      vv[u] = mu * vv[u] + gv[u] * gscale + wd * pv[u];
+      pv[u] -= lr * vv[u];
+      op[u] = tobf(pv[u]);
+    }
+    ((f32x4*)p)[i] = pv;
+    ((f32x4*)v)[i] = vv;
+    if (pb) ((ushort4*)pb)[i] = o;
+  }
+}
+
+static unsigned grid_for(long long n, int per = 256) {
+  long long b = (n + per - 1) / per;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+void bn_finalize_launch(int C, long long M, const float* s, const float* q, float eps, float* mean,
+                        float* rstd, float* run_mean, float* run_var, float momentum,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, 1.f / (float)M,
+                     M > 1 ? (float)M / (float)(M - 1) : 1.f, s, q, eps, mean, rstd, run_mean,
+                     run_var, momentum);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void bn_apply_launch(long long M, int C, const void* x, const float* mean, const float* rstd,
+                     const float* gamma, const float* beta, const void* res, int relu, void* y,
+                     hipStream_t st) {
+  if (C % 8) throw std::runtime_error("bn_apply: C % 8 != 0");
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(M * C / 8)), dim3(256), 0, st, M, C,
+                     (const unsigned short*)x, mean, rstd, gamma, beta,
+                     (const unsigned short*)res, relu, (unsigned short*)y);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void bn_bwd_launch(long long M, int C, const void* dy, const void* yout, const void* x,
+                   const float* mean, const float* rstd, const float* gamma, int relu,
+                   float* sum_dy, float* sum_dyxh, void* dx, void* dres, hipStream_t st) {
+  if (C % 8) throw std::runtime_error("bn_bwd: C % 8 != 0");
+  DTFX_HIP_CHECK(hipMemsetAsync(sum_dy, 0, sizeof(float) * C, st));
+  DTFX_HIP_CHECK(hipMemsetAsync(sum_dyxh, 0, sizeof(float) * C, st));
+  const int cg = C / 8, tpr = cg < 256 ? cg : 256, rpp = 256 / tpr;
+  // enough blocks to fill the chip, each covering a contiguous row range
+  long long rpb = (M + 1023) / 1024;
+  if (rpb < rpp * 4) rpb = rpp * 4;
+  const unsigned blocks = (unsigned)((M + rpb - 1) / rpb);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, st, M, C, (int)rpb,
+                     (const unsigned short*)dy, (const unsigned short*)yout,
+                     (const unsigned short*)x, mean, rstd, relu, sum_dy, sum_dyxh);
+  DTFX_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(M * C / 8)), dim3(256), 0, st, M, C,
+                     (const unsigned short*)dy, (const unsigned short*)yout,
+                     (const unsigned short*)x, mean, rstd, gamma, sum_dy, sum_dyxh, relu,
+                     1.f / (float)M, (unsigned short*)dx, (unsigned short*)dres);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void maxpool_fwd_launch(int N, int H, int W, int C, const void* x, void* y, void* idx, hipStream_t st) {
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * OH * OW * C)), dim3(256), 0,
+                     st, N, H, W, C, OH, OW, (const unsigned short*)x, (unsigned short*)y,
+                     (unsigned char*)idx);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void maxpool_bwd_launch(int N, int H, int W, int C, const void* dy, const void* idx, void* dx,
+                        hipStream_t st) {
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0, st,
+                     N, H, W, C, OH, OW, (const unsigned short*)dy, (const unsigned char*)idx,
+                     (unsigned short*)dx);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void avgpool_fwd_launch(int N, int HW, int C, const void* x, void* y, hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, N, HW, C,
+                     (const unsigned short*)x, (unsigned short*)y);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void avgpool_bwd_launch(int N, int HW, int C, const void* dy, void* dx, hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((long long)N * HW * C)), dim3(256), 0, st, N,
+                     HW, C, (const unsigned short*)dy, (unsigned short*)dx);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void sgd_momentum_mixed_launch(long long n, float* p, const float* g, float* v, void* pb, float lr,
+                               float mu, float wd, float gscale, hipStream_t st) {
+  if (n % 4) throw std::runtime_error("sgd_momentum_mixed: n % 4 != 0");
+  hipLaunchKernelGGL(sgd_momentum_mixed_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, n, p, g, v,
+                     (unsigned short*)pb, lr, mu, wd, gscale);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dtfx

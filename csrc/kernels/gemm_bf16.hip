@@ -69,6 +69,31 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return 0.5f * (1.f + th) + 0.5f * x * (1.f - th * th) * k0 * (1.f + 3.f * k1 * x * x);
 }
 
+// Convolution as implicit GEMM (NHWC bf16 activations, weights [Cout][KH][KW][Cin]).
+//   MODE 1 fwd   : C[pix][co]  = sum_k im2col(x)[pix][k] * W[co][k],   k = (kh, kw, ci)
+//   MODE 2 dgrad : dX[pix][ci] = sum_k col2im(dy)[pix][k] * W'[k][ci], k = (kh, kw, co)
+//   MODE 3 wgrad : dW[co][j]   = sum_p dy[p][co] * im2col(x)[p][j],    j = (kh, kw, ci)
+// The gathers run in the glds staging: every lane computes its own 16-B source
+// address (8 consecutive channels of one tap; C % 8 == 0), and padding taps /
+// K tails point at a 16-B zero page, so no im2col buffer ever exists.
+struct ConvDesc {
+  int N, H, W, C;        // input
+  int OH, OW, K;         // output spatial, output channels
+  int KH, KW, stride, pad;
+  int ktot;              // reduction length of the GEMM (MODE 1: KH*KW*C, MODE 2: KH*KW*K)
+  int wld;               // weight row stride (elements) for MODE 2
+};
+
+__device__ __attribute__((aligned(16))) unsigned short g_zero16[8];
+
+// q = a / d, r = a % d for 0 <= a < 2^24, d > 0 (float reciprocal + one correction)
+__device__ __forceinline__ void fdivmod(int a, int d, float inv, int& q, int& r) {
+  q = (int)((float)a * inv);
+  r = a - q * d;
+  if (r >= d) { ++q; r -= d; }
+  if (r < 0) { --q; r += d; }
+}
+
 namespace gb {
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB per operand tile
@@ -81,7 +106,8 @@ __device__ __forceinline__ int swz_tr(int r) { return ((r & 3) | (((r >> 3) & 1)
 //  else : tile rows = 64 k x 128 outer; src row stride ld.
 template <bool KCONT>
 __device__ __forceinline__ void stage(const unsigned short* __restrict__ src, int ld, int outer0,
-                                      int outer_max, int k0, char* lds_tile, int wave, int lane) {
+                                      int outer_max, int k0, char* lds_tile, int wave, int lane,
+                                      int kmax) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int blk = i * 4 + wave;  // 1 KB block of the tile this wave-instruction fills
@@ -95,7 +121,7 @@ __device__ __forceinline__ void stage(const unsigned short* __restrict__ src, in
       const int kr = blk * 4 + (lane >> 4), cs = lane & 15;
       const int c = cs ^ swz_tr(kr);
       const int o = min(outer0 + c * 8, outer_max);  // outer_max is 8-aligned-safe (host)
-      g = src + (size_t)(k0 + kr) * ld + o;
+      g = src + (size_t)min(k0 + kr, kmax) * ld + o;  // clamped K tail: partner operand is 0
     }
     __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(lds_tile + blk * 1024), 16, 0, 0);
   }
@@ -125,6 +151,110 @@ __device__ __forceinline__ bf16x8 frag(const char* lds_tile, int o0, int kk, int
     return v;
   }
 }
+// MODE 1/2 A operand (k-contiguous image [128 pix][64 k]): per-lane row state, computed once.
+struct RowState {
+  int nb[4], y0[4], x0[4];  // n*H*W (or -1 past M), spatial base of each of the lane's 4 rows
+};
+
+__device__ __forceinline__ void conv_rows(const ConvDesc& d, int mode, int M, int m0, int wave,
+                                          int lane, RowState& rs) {
+  const int PW = mode == 1 ? d.OW : d.W, PHW = mode == 1 ? d.OH * d.OW : d.H * d.W;
+  const float ipw = 1.f / PW, iphw = 1.f / PHW;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + (i * 4 + wave) * 8 + (lane >> 3);
+    int n, rem, py, px;
+    fdivmod(min(m, M - 1), PHW, iphw, n, rem);
+    fdivmod(rem, PW, ipw, py, px);
+    rs.nb[i] = m < M ? n : -1;
+    if (mode == 1) {
+      rs.y0[i] = py * d.stride - d.pad;
+      rs.x0[i] = px * d.stride - d.pad;
+    } else {  // dgrad: numerator base h + pad (minus kh per tap)
+      rs.y0[i] = py + d.pad;
+      rs.x0[i] = px + d.pad;
+    }
+  }
+}
+
+// A tile gather for conv fwd (mode 1: src = x, channels C) / dgrad (mode 2: src = dy, channels K)
+__device__ __forceinline__ void stage_a_conv(const ConvDesc& d, int mode, const RowState& rs,
+                                             const unsigned short* __restrict__ src, int k0,
+                                             char* lds_tile, int wave, int lane) {
+  const int CH = mode == 1 ? d.C : d.K;
+  const bool uni = (CH & 63) == 0;  // a 64-wide k step stays inside one tap
+  const int tap_u = k0 / CH, c_u = k0 - tap_u * CH;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = i * 4 + wave;
+    const int row = blk * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (row & 7);
+    const int k = k0 + c * 8;
+    int tap, ch;
+    if (uni) { tap = tap_u; ch = c_u + c * 8; }
+    else { tap = k / CH; ch = k - tap * CH; }
+    const int kh = tap / d.KW, kw = tap - (tap / d.KW) * d.KW;
+    bool ok = rs.nb[i] >= 0 && k < d.ktot;
+    int yy, xx;
+    if (mode == 1) {
+      yy = rs.y0[i] + kh;
+      xx = rs.x0[i] + kw;
+      ok = ok && yy >= 0 && yy < d.H && xx >= 0 && xx < d.W;
+    } else {
+      const int ny = rs.y0[i] - kh, nx = rs.x0[i] - kw;
+      yy = ny / d.stride;
+      xx = nx / d.stride;
+      ok = ok && ny >= 0 && nx >= 0 && yy * d.stride == ny && xx * d.stride == nx && yy < d.OH &&
+           xx < d.OW;
+    }
+    const int SH = mode == 1 ? d.H : d.OH, SW = mode == 1 ? d.W : d.OW;
+    const unsigned short* g =
+        ok ? src + ((size_t)(rs.nb[i] * SH + yy) * SW + xx) * CH + ch : g_zero16;
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(lds_tile + blk * 1024), 16, 0, 0);
+  }
+}
+
+// B tile for dgrad (k-strided image [64 k][128 ci]): W'[k = (kh, kw, co)][ci] = W[co][kh][kw][ci]
+__device__ __forceinline__ void stage_b_wtap(const ConvDesc& d, const unsigned short* __restrict__ w,
+                                             int n0, int k0, char* lds_tile, int wave, int lane) {
+  const int tap = k0 / d.K, co0 = k0 - tap * d.K;  // host: K % 64 == 0
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = i * 4 + wave;
+    const int kr = blk * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ swz_tr(kr);
+    const int o = n0 + c * 8;
+    const bool ok = k0 + kr < d.ktot && o < d.C;
+    const unsigned short* g =
+        ok ? w + (size_t)(co0 + kr) * d.wld + (size_t)tap * d.C + o : g_zero16;
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(lds_tile + blk * 1024), 16, 0, 0);
+  }
+}
+
+// B tile for wgrad (k-strided image [64 pixels][128 j]): im2col(x)[p][j = (kh, kw, ci)]
+__device__ __forceinline__ void stage_b_im2col(const ConvDesc& d, const unsigned short* __restrict__ x,
+                                               int NP, int n0, int k0, char* lds_tile, int wave,
+                                               int lane) {
+  const int ohw = d.OH * d.OW;
+  const float iohw = 1.f / ohw, iow = 1.f / d.OW, ikw = 1.f / d.KW, ic = 1.f / d.C;
+  const int jtot = d.KH * d.KW * d.C;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = i * 4 + wave;
+    const int kr = blk * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ swz_tr(kr);
+    const int p = k0 + kr, j = n0 + c * 8;
+    int n, rem, oh, ow, tap, ci, kh, kw;
+    fdivmod(min(p, NP - 1), ohw, iohw, n, rem);
+    fdivmod(rem, d.OW, iow, oh, ow);
+    fdivmod(min(j, jtot - 8), d.C, ic, tap, ci);
+    fdivmod(tap, d.KW, ikw, kh, kw);
+    const int yy = oh * d.stride - d.pad + kh, xx = ow * d.stride - d.pad + kw;
+    const bool ok = p < NP && j < jtot && yy >= 0 && yy < d.H && xx >= 0 && xx < d.W;
+    const unsigned short* g = ok ? x + ((size_t)(n * d.H + yy) * d.W + xx) * d.C + ci : g_zero16;
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(lds_tile + blk * 1024), 16, 0, 0);
+  }
+}
 }  // namespace gb
 
 struct GemmEpi {
@@ -138,13 +268,14 @@ struct GemmEpi {
   int ld_res;
   int act_grad;                 // multiply by act'(aux_in)
   float* colsum;                // [N] += column sums of the final values (bias gradient), or null
+  float* colsq;                 // [N] += column sums of squares (BatchNorm statistics), or null
 };
 
-template <bool TA, bool TB, bool OUT_F32>
+template <int MODE, bool TA, bool TB, bool OUT_F32>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
     int M, int N, int K, const unsigned short* __restrict__ A, int lda,
     const unsigned short* __restrict__ B, int ldb, void* __restrict__ Cv, int ldc, GemmEpi e,
-    long long sA, long long sB, long long sC) {
+    long long sA, long long sB, long long sC, ConvDesc cd) {
   using namespace gb;
   // strided batch over blockIdx.z (attention's per-(batch, head) products)
   A += sA * blockIdx.z;
@@ -169,13 +300,19 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // split-K: blockIdx.y owns K tiles [kt0, kt0 + nk)
-  const int nk_all = K / BK, per = (nk_all + gridDim.y - 1) / gridDim.y;
+  const int nk_all = (K + BK - 1) / BK, per = (nk_all + gridDim.y - 1) / gridDim.y;
   const int kt0 = blockIdx.y * per;
   const int nk = max(0, min(per, nk_all - kt0));
+  RowState rs;
+  if (MODE == 1 || MODE == 2) conv_rows(cd, MODE, M, m0, wave, lane, rs);
   auto stage_all = [&](int buf, int kt) {
     char* base = smem + buf * BUF_BYTES;
-    stage<!TA>(A, lda, m0, a_max, (kt0 + kt) * BK, base, wave, lane);
-    stage<TB>(B, ldb, n0, b_max, (kt0 + kt) * BK, base + TILE_BYTES, wave, lane);
+    const int k0 = (kt0 + kt) * BK;
+    if (MODE == 1 || MODE == 2) stage_a_conv(cd, MODE, rs, A, k0, base, wave, lane);
+    else stage<!TA>(A, lda, m0, a_max, k0, base, wave, lane, K - 1);
+    if (MODE == 2) stage_b_wtap(cd, B, n0, k0, base + TILE_BYTES, wave, lane);
+    else if (MODE == 3) stage_b_im2col(cd, B, K, n0, k0, base + TILE_BYTES, wave, lane);
+    else stage<TB>(B, ldb, n0, b_max, k0, base + TILE_BYTES, wave, lane, K - 1);
   };
   if (nk > 0) stage_all(0, 0);
   __syncthreads();  // emits vmcnt(0): tile 0 landed for every wave
@@ -210,9 +347,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
   constexpr int EP_LD = 68;
   float* ep = (float*)smem + wave * (32 * EP_LD);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
-  float cs[8];  // fused column sums (bias gradient) of this lane's 8 columns
+  float cs[8], cq[8];  // fused column sums / sums of squares of this lane's 8 columns
 #pragma unroll
-  for (int u = 0; u < 8; ++u) cs[u] = 0.f;
+  for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -285,9 +422,12 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[u]);
         }
-        if (e.colsum) {
+        if (e.colsum || e.colsq) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) cs[u] += v[u];
+          for (int u = 0; u < 8; ++u) {
+            cs[u] += v[u];
+            cq[u] += v[u] * v[u];
+          }
         }
         if (OUT_F32) {
           float* C = (float*)Cv + (size_t)m * ldc + n;
@@ -319,6 +459,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
           }
           if (e.residual) w += bf2f(e.residual[(size_t)m * e.ld_res + n + u]);
           cs[u] += w;
+          cq[u] += w * w;
           if (OUT_F32) {
             float* C = (float*)Cv + (size_t)m * ldc + n + u;
             *C = (e.beta != 0.f) ? w + e.beta * *C : w;
@@ -330,19 +471,25 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
     }
     __builtin_amdgcn_wave_barrier();
   }
-  if (e.colsum) {
+  if (e.colsum || e.colsq) {
     // lanes l, l^8, ..., l^56 hold the same 8 columns for different rows
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       cs[u] += __shfl_xor(cs[u], 8);
       cs[u] += __shfl_xor(cs[u], 16);
       cs[u] += __shfl_xor(cs[u], 32);
+      cq[u] += __shfl_xor(cq[u], 8);
+      cq[u] += __shfl_xor(cq[u], 16);
+      cq[u] += __shfl_xor(cq[u], 32);
     }
     const int n = n0 + wn * 64 + (lane & 7) * 8;
     if (lane < 8)
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (n + u < N) unsafeAtomicAdd(e.colsum + n + u, cs[u]);
+        if (n + u < N) {
+          if (e.colsum) unsafeAtomicAdd(e.colsum + n + u, cs[u]);
+          if (e.colsq) unsafeAtomicAdd(e.colsq + n + u, cq[u]);
+        }
   }
 }
 
@@ -388,15 +535,15 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
     }
   }
   GemmEpi e{alpha, beta, bias, act, (const unsigned short*)aux_in, (unsigned short*)aux_out,
-            ld_aux, (const unsigned short*)residual, ld_res, act_grad, colsum};
+            ld_aux, (const unsigned short*)residual, ld_res, act_grad, colsum, nullptr};
   const dim3 grid(tiles, splitk, batch);
   const size_t lds = 2 * gb::BUF_BYTES;
   auto* Au = (const unsigned short*)A;
   auto* Bu = (const unsigned short*)B;
 #define DTFX_GB(TA_, TB_, F_)                                                                 \
   if (ta == TA_ && tb == TB_ && out_f32 == F_) {                                              \
-    hipLaunchKernelGGL((gemm_bf16_kernel<TA_, TB_, F_>), grid, dim3(gb::NT), lds, stream, \
-                       M, N, K, Au, lda, Bu, ldb, C, ldc, e, sA, sB, sC);                                 \
+    hipLaunchKernelGGL((gemm_bf16_kernel<0, TA_, TB_, F_>), grid, dim3(gb::NT), lds, stream, \
+                       M, N, K, Au, lda, Bu, ldb, C, ldc, e, sA, sB, sC, ConvDesc{});     \
     DTFX_HIP_CHECK(hipGetLastError());                                                        \
     return;                                                                                   \
   }
@@ -409,6 +556,68 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   DTFX_GB(true, true, false)
   DTFX_GB(true, true, true)
 #undef DTFX_GB
+}
+
+// Convolution launcher (modes in the ConvDesc comment above).
+//  fwd  : x [N*H*W][C], w [Cout][ldw >= ceil64(KH*KW*C)] (zero-padded), y [N*OH*OW][Cout]
+//         optional fused BatchNorm statistics: colsum / colsq over y (f32 [Cout])
+//  dgrad: dy [N*OH*OW][Cout], w [Cout][ldw], dx [N*H*W][C]
+//         (+ residual)
+//  wgrad: dy, x -> dw [Cout][ldw] f32 (first KH*KW*C columns; += when beta == 1)
+void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, int KW, int stride,
+                      int pad, const void* a, const void* b, int ldw, void* out, float beta,
+                      const void* residual, float* colsum, float* colsq, int splitk,
+                      hipStream_t stream) {
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  if (C % 8 || Cout % 8) throw std::runtime_error("conv_bf16: channel counts must be multiples of 8");
+  if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) & 15)
+    throw std::runtime_error("conv_bf16: tensors must be 16-byte aligned");
+  ConvDesc d{N, H, W, C, OH, OW, Cout, KH, KW, stride, pad, 0, ldw > 0 ? ldw : KH * KW * C};
+  GemmEpi e{1.f, beta, nullptr, 0, nullptr, nullptr, 0, (const unsigned short*)residual, 0, 0,
+            colsum, colsq};
+  const size_t lds = 2 * gb::BUF_BYTES;
+  int M, Nn, K;
+  if (mode == 1) {
+    d.ktot = KH * KW * C;
+    M = N * OH * OW; Nn = Cout; K = d.ktot;
+    if (ldw < (K + 63) / 64 * 64) throw std::runtime_error("conv_bf16: fwd weights need ld >= ceil64(KH*KW*C)");
+    e.ld_res = Cout;
+    const int tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
+    hipLaunchKernelGGL((gemm_bf16_kernel<1, false, true, false>), dim3(tiles, 1, 1), dim3(gb::NT), lds,
+                       stream, M, Nn, K, (const unsigned short*)a, 0, (const unsigned short*)b, ldw,
+                       out, Cout, e, 0LL, 0LL, 0LL, d);
+  } else if (mode == 2) {
+    if (Cout % 64) throw std::runtime_error("conv_bf16: dgrad needs Cout % 64 == 0");
+    d.ktot = KH * KW * Cout;
+    M = N * H * W; Nn = C; K = d.ktot;
+    e.ld_res = C;
+    const int tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
+    hipLaunchKernelGGL((gemm_bf16_kernel<2, false, false, false>), dim3(tiles, 1, 1), dim3(gb::NT),
+                       lds, stream, M, Nn, K, (const unsigned short*)a, 0, (const unsigned short*)b, 0,
+                       out, C, e, 0LL, 0LL, 0LL, d);
+  } else if (mode == 3) {
+    if (residual || colsum || colsq) throw std::runtime_error("conv_bf16: wgrad has no epilogue options");
+    M = Cout; Nn = KH * KW * C; K = N * OH * OW;
+    const int tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
+    const int nkt = (K + 63) / 64;
+    if (splitk <= 0) {
+      splitk = 1;
+      while (tiles * splitk < 512 && nkt / (splitk * 2) >= 4) splitk *= 2;
+    }
+    const int ldo = ldw > 0 ? ldw : Nn;  // dW row stride (the padded fwd weight layout)
+    if (ldo < Nn || ldo % 8) throw std::runtime_error("conv_bf16: wgrad ld must be >= KH*KW*C, % 8");
+    if (splitk > 1) {
+      if (beta != 0.f && beta != 1.f) throw std::runtime_error("conv_bf16: split-K wgrad needs beta 0/1");
+      if (beta == 0.f)
+        DTFX_HIP_CHECK(hipMemset2DAsync(out, sizeof(float) * ldo, 0, sizeof(float) * Nn, M, stream));
+    }
+    hipLaunchKernelGGL((gemm_bf16_kernel<3, true, false, true>), dim3(tiles, splitk, 1), dim3(gb::NT),
+                       lds, stream, M, Nn, K, (const unsigned short*)a, Cout,
+                       (const unsigned short*)b, 0, out, ldo, e, 0LL, 0LL, 0LL, d);
+  } else {
+    throw std::runtime_error("conv_bf16: mode must be 1 (fwd), 2 (dgrad) or 3 (wgrad)");
+  }
+  DTFX_HIP_CHECK(hipGetLastError());
 }
 
 // Column sums of a bf16 matrix (bias gradients): out[n] (+)= sum_m G[m][n], f32.

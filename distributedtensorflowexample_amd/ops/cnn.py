@@ -1,0 +1,208 @@
+"""CNN ops (ResNet-50 path) on the gfx950 kernels.
+
+Convolutions are implicit GEMMs on the bf16 matrix cores
+(``csrc/kernels/gemm_bf16.hip`` modes 1-3: the im2col / col2im gathers happen
+in the glds staging, nothing is materialised); BatchNorm statistics are
+fused into the forward convolution's epilogue; the rest lives in
+``csrc/kernels/cnn.hip``.  Activations are NHWC bf16 tensors ``[N, H, W, C]``;
+conv weights are ``[Cout, ldw]`` bf16 rows holding ``[KH][KW][Cin]`` (``ldw``
+= KH*KW*Cin rounded up to 64, zero tail).  CPU tensors run f32 PyTorch
+references of the same math.  North-star config 4 of BASELINE.json.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ._ext import hip, ptr, stream_handle
+
+BF16 = torch.bfloat16
+
+
+def out_hw(H, W, k, stride, pad):
+    return (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+
+
+def kpad(kh, kw, c):
+    return (kh * kw * c + 63) // 64 * 64
+
+
+def _w4(w, Cout, KH, KW, C):
+    """[Cout, ldw] row layout -> torch OIHW f32."""
+    return w[:, :KH * KW * C].float().reshape(Cout, KH, KW, C).permute(0, 3, 1, 2)
+
+
+def _nchw(x):
+    return x.float().permute(0, 3, 1, 2)
+
+
+def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
+    """y = conv(x, w) (NHWC bf16); optional fused BN statistics (sum / sum of squares of y per
+    output channel, accumulated into f32 ``colsum`` / ``colsq``)."""
+    N, H, W, C = x.shape
+    Cout = w.shape[0]
+    OH, OW = out_hw(H, W, KH, stride, pad)
+    if not x.is_cuda:
+        y = F.conv2d(_nchw(x), _w4(w, Cout, KH, KW, C), stride=stride, padding=pad)
+        y = y.permute(0, 2, 3, 1)
+        if residual is not None:
+            y = y + residual.float()
+        if colsum is not None:
+            colsum += y.reshape(-1, Cout).sum(0)
+        if colsq is not None:
+            colsq += (y.reshape(-1, Cout) ** 2).sum(0)
+        return y.to(BF16)
+    y = torch.empty(N, OH, OW, Cout, device=x.device, dtype=BF16)
+    hip().conv_bf16(1, N, H, W, C, Cout, KH, KW, stride, pad, ptr(x), ptr(w), w.stride(0), ptr(y),
+                    0.0, ptr(residual), ptr(colsum), ptr(colsq), 0, stream_handle())
+    return y
+
+
+def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None):
+    """dx = conv^T(dy, w) (+ residual), NHWC bf16."""
+    N, H, W, C = x_shape
+    Cout = w.shape[0]
+    if not dy.is_cuda:
+        dx = torch.nn.grad.conv2d_input((N, C, H, W), _w4(w, Cout, KH, KW, C), _nchw(dy),
+                                        stride=stride, padding=pad).permute(0, 2, 3, 1)
+        if residual is not None:
+            dx = dx + residual.float()
+        return dx.to(BF16)
+    dx = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
+    hip().conv_bf16(2, N, H, W, C, Cout, KH, KW, stride, pad, ptr(dy), ptr(w), w.stride(0), ptr(dx),
+                    0.0, ptr(residual), 0, 0, 0, stream_handle())
+    return dx
+
+
+def conv_wgrad(dy, x, dw, KH, KW, stride, pad, beta=1.0):
+    """dw[:, :KH*KW*C] (f32 [Cout, ldw]) (+)= dL/dW."""
+    N, H, W, C = x.shape
+    Cout = dy.shape[-1]
+    if not dy.is_cuda:
+        g = torch.nn.grad.conv2d_weight(_nchw(x), (Cout, C, KH, KW), _nchw(dy), stride=stride,
+                                        padding=pad)
+        g = g.permute(0, 2, 3, 1).reshape(Cout, -1)
+        k = KH * KW * C
+        dw[:, :k] = g + (beta * dw[:, :k] if beta else 0)
+        return dw
+    hip().conv_bf16(3, N, H, W, C, Cout, KH, KW, stride, pad, ptr(dy), ptr(x), dw.stride(0),
+                    ptr(dw), float(beta), 0, 0, 0, 0, stream_handle())
+    return dw
+
+
+# ---------------------------------------------------------------- BatchNorm
+def bn_finalize(s, q, M, eps=1e-5, run_mean=None, run_var=None, momentum=0.9):
+    C = s.numel()
+    if not s.is_cuda:
+        mean = s / M
+        var = (q / M - mean * mean).clamp_min(0)
+        if run_mean is not None:
+            run_mean.mul_(momentum).add_((1 - momentum) * mean)
+            run_var.mul_(momentum).add_((1 - momentum) * var * (M / max(M - 1, 1)))
+        return mean, torch.rsqrt(var + eps)
+    mean = torch.empty(C, device=s.device)
+    rstd = torch.empty(C, device=s.device)
+    hip().bn_finalize(C, int(M), ptr(s), ptr(q), float(eps), ptr(mean), ptr(rstd), ptr(run_mean),
+                      ptr(run_var), float(momentum), stream_handle())
+    return mean, rstd
+
+
+def bn_apply(x, mean, rstd, gamma, beta, residual=None, relu=True):
+    C = x.shape[-1]
+    if not x.is_cuda:
+        y = (x.float() - mean) * rstd * gamma + beta
+        if residual is not None:
+            y = y + residual.float()
+        if relu:
+            y = torch.relu(y)
+        return y.to(BF16)
+    y = torch.empty_like(x)
+    hip().bn_apply(x.numel() // C, C, ptr(x), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta),
+                   ptr(residual), int(relu), ptr(y), stream_handle())
+    return y
+
+
+def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, relu=True, want_dres=False):
+    """Backward of y = act(bn(x) [+ res]).  Accumulates dgamma/dbeta; returns (dx, dres)
+    where dres = dy * act'(y) is the gradient of the residual input (if requested)."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    if not x.is_cuda:
+        de = dy.float() * (y.float() > 0) if relu else dy.float()
+        de2 = de.reshape(M, C)
+        xh = (x.float().reshape(M, C) - mean) * rstd
+        sdy, sdx = de2.sum(0), (de2 * xh).sum(0)
+        dx = gamma * rstd * (de2 - sdy / M - xh * sdx / M)
+        dgamma += sdx
+        dbeta += sdy
+        return dx.reshape(x.shape).to(BF16), (de.to(BF16) if want_dres else None)
+    sdy = torch.empty(C, device=x.device)
+    sdx = torch.empty(C, device=x.device)
+    dx = torch.empty_like(x)
+    dres = torch.empty_like(x) if want_dres else None
+    hip().bn_bwd(M, C, ptr(dy), ptr(y), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), int(relu),
+                 ptr(sdy), ptr(sdx), ptr(dx), ptr(dres), stream_handle())
+    dgamma += sdx
+    dbeta += sdy
+    return dx, dres
+
+
+# ---------------------------------------------------------------- pooling
+def maxpool_fwd(x):
+    """3x3 / stride 2 / pad 1 max pool; returns (y, argmax tap index uint8)."""
+    N, H, W, C = x.shape
+    OH, OW = out_hw(H, W, 3, 2, 1)
+    if not x.is_cuda:
+        xp = F.pad(_nchw(x), (1, 1, 1, 1), value=float("-inf"))
+        cols = F.unfold(xp, 3, stride=2).view(N, C, 9, OH * OW)
+        y, idx = cols.max(2)
+        y = y.view(N, C, OH, OW).permute(0, 2, 3, 1).to(BF16)
+        idx = idx.view(N, C, OH, OW).permute(0, 2, 3, 1).to(torch.uint8).contiguous()
+        return y.contiguous(), idx
+    y = torch.empty(N, OH, OW, C, device=x.device, dtype=BF16)
+    idx = torch.empty(N, OH, OW, C, device=x.device, dtype=torch.uint8)
+    hip().maxpool_fwd(N, H, W, C, ptr(x), ptr(y), ptr(idx), stream_handle())
+    return y, idx
+
+
+def maxpool_bwd(dy, idx, x_shape):
+    N, H, W, C = x_shape
+    if not dy.is_cuda:
+        OH, OW = dy.shape[1], dy.shape[2]
+        g = torch.zeros(N, C, 9, OH * OW)
+        g.scatter_(2, idx.permute(0, 3, 1, 2).reshape(N, C, 1, OH * OW).long(),
+                   dy.float().permute(0, 3, 1, 2).reshape(N, C, 1, OH * OW))
+        dx = F.fold(g.view(N, C * 9, OH * OW), (H + 2, W + 2), 3, stride=2)[:, :, 1:-1, 1:-1]
+        return dx.permute(0, 2, 3, 1).contiguous().to(BF16)
+    dx = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
+    hip().maxpool_bwd(N, H, W, C, ptr(dy), ptr(idx), ptr(dx), stream_handle())
+    return dx
+
+
+def avgpool_fwd(x):
+    N, H, W, C = x.shape
+    if not x.is_cuda:
+        return x.float().mean((1, 2)).to(BF16)
+    y = torch.empty(N, C, device=x.device, dtype=BF16)
+    hip().avgpool_fwd(N, H * W, C, ptr(x), ptr(y), stream_handle())
+    return y
+
+
+def avgpool_bwd(dy, x_shape):
+    N, H, W, C = x_shape
+    if not dy.is_cuda:
+        return (dy.float()[:, None, None, :] / (H * W)).expand(N, H, W, C).contiguous().to(BF16)
+    dx = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
+    hip().avgpool_bwd(N, H * W, C, ptr(dy), ptr(dx), stream_handle())
+    return dx
+
+
+def sgd_momentum_mixed(p, g, v, pb, lr, momentum=0.9, wd=0.0, gscale=1.0):
+    if not p.is_cuda:
+        v.mul_(momentum).add_(g * gscale + wd * p)
+        p.sub_(lr * v)
+        if pb is not None:
+            pb.copy_(p)
+        return
+    hip().sgd_momentum_mixed(p.numel(), ptr(p), ptr(g), ptr(v), ptr(pb), float(lr), float(momentum),
+                             float(wd), float(gscale), stream_handle())

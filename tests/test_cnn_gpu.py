@@ -1,0 +1,103 @@
+"""CNN kernels (implicit-GEMM convs, BatchNorm, pooling, SGD) vs the f32 PyTorch reference."""
+import pytest
+import torch
+
+from distributedtensorflowexample_amd.ops import cnn
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def _r(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+CONVS = [  # N, H, W, C, Cout, k, stride, pad
+    (2, 14, 14, 64, 64, 3, 1, 1),
+    (2, 14, 14, 64, 128, 3, 2, 1),
+    (2, 14, 14, 64, 256, 1, 2, 0),
+    (2, 9, 11, 256, 64, 1, 1, 0),
+    (2, 32, 32, 8, 64, 7, 2, 3),
+]
+
+
+@pytest.mark.parametrize("N,H,W,C,Co,k,s,p", CONVS)
+def test_conv_fwd_dgrad_wgrad(gpu, N, H, W, C, Co, k, s, p):
+    x = _r(N, H, W, C, seed=1).to(BF)
+    ld = cnn.kpad(k, k, C)
+    w = torch.zeros(Co, ld)
+    w[:, :k * k * C] = _r(Co, k * k * C, seed=2, scale=(k * k * C) ** -0.5)
+    w = w.to(BF)
+    cs, cq = torch.zeros(Co), torch.zeros(Co)
+    csg, cqg = torch.zeros(Co, device=gpu), torch.zeros(Co, device=gpu)
+    y = cnn.conv_fwd(x.to(gpu), w.to(gpu), k, k, s, p, colsum=csg, colsq=cqg)
+    yr = cnn.conv_fwd(x, w, k, k, s, p, colsum=cs, colsq=cq)
+    assert y.shape == yr.shape
+    assert (y.cpu().float() - yr.float()).abs().max() < 3e-2 * yr.float().abs().max()
+    assert torch.allclose(csg.cpu(), cs, rtol=1e-2, atol=0.5)
+    assert torch.allclose(cqg.cpu(), cq, rtol=1e-2, atol=0.5)
+    dy = _r(*yr.shape, seed=3).to(BF)
+    if C % 8 == 0 and Co % 64 == 0 and C >= 64:
+        dx = cnn.conv_dgrad(dy.to(gpu), w.to(gpu), x.shape, k, k, s, p)
+        dxr = cnn.conv_dgrad(dy, w, x.shape, k, k, s, p)
+        assert (dx.cpu().float() - dxr.float()).abs().max() < 3e-2 * dxr.float().abs().max()
+    dw = torch.full((Co, ld), 0.5, device=gpu)
+    dwr = torch.full((Co, ld), 0.5)
+    cnn.conv_wgrad(dy.to(gpu), x.to(gpu), dw, k, k, s, p, beta=1.0)
+    cnn.conv_wgrad(dy, x, dwr, k, k, s, p, beta=1.0)
+    kk = k * k * C
+    assert (dw.cpu()[:, :kk] - dwr[:, :kk]).abs().max() < 1e-2 * dwr[:, :kk].abs().max()
+    assert (dw.cpu()[:, kk:] == 0.5).all()  # padded columns untouched
+
+
+def test_batchnorm_fwd_bwd(gpu):
+    N, H, W, C = 4, 7, 7, 64
+    x = _r(N, H, W, C, seed=4, scale=2).to(BF) + 1
+    res = _r(N, H, W, C, seed=5).to(BF)
+    gamma, beta = _r(C, seed=6) * 0.1 + 1, _r(C, seed=7) * 0.1
+    M = N * H * W
+    s, q = x.float().reshape(M, C).sum(0), (x.float().reshape(M, C) ** 2).sum(0)
+    mean, rstd = cnn.bn_finalize(s.to(gpu), q.to(gpu), M)
+    mr, rr = cnn.bn_finalize(s, q, M)
+    assert torch.allclose(mean.cpu(), mr, atol=1e-5) and torch.allclose(rstd.cpu(), rr, rtol=1e-4)
+    y = cnn.bn_apply(x.to(gpu), mean, rstd, gamma.to(gpu), beta.to(gpu), res.to(gpu), relu=True)
+    yr = cnn.bn_apply(x, mr, rr, gamma, beta, res, relu=True)
+    assert (y.cpu().float() - yr.float()).abs().max() < 3e-2
+    dy = _r(N, H, W, C, seed=8).to(BF)
+    dg, db = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
+    dx, dres = cnn.bn_bwd(dy.to(gpu), y, x.to(gpu), mean, rstd, gamma.to(gpu), dg, db, True, True)
+    dgr, dbr = torch.zeros(C), torch.zeros(C)
+    dxr, dresr = cnn.bn_bwd(dy, y.cpu(), x, mr, rr, gamma, dgr, dbr, True, True)
+    assert (dx.cpu().float() - dxr.float()).abs().max() < 3e-2 * dxr.float().abs().max()
+    assert torch.equal(dres.cpu(), dresr)
+    assert torch.allclose(dg.cpu(), dgr, atol=1e-2, rtol=1e-3)
+    assert torch.allclose(db.cpu(), dbr, atol=1e-2, rtol=1e-3)
+
+
+def test_pools(gpu):
+    x = _r(2, 15, 16, 64, seed=9).to(BF)
+    y, idx = cnn.maxpool_fwd(x.to(gpu))
+    yr, idxr = cnn.maxpool_fwd(x)
+    assert torch.equal(y.cpu(), yr)
+    dy = _r(*yr.shape, seed=10).to(BF)
+    dx = cnn.maxpool_bwd(dy.to(gpu), idx, x.shape)
+    dxr = cnn.maxpool_bwd(dy, idxr, x.shape)
+    assert (dx.cpu().float() - dxr.float()).abs().max() < 2e-2
+    a = cnn.avgpool_fwd(x.to(gpu))
+    assert (a.cpu().float() - cnn.avgpool_fwd(x).float()).abs().max() < 1e-2
+    da = _r(2, 64, seed=11).to(BF)
+    assert (cnn.avgpool_bwd(da.to(gpu), x.shape).cpu().float() -
+            cnn.avgpool_bwd(da, x.shape).float()).abs().max() < 1e-3
+
+
+def test_sgd_momentum_mixed(gpu):
+    p, g = _r(1024, seed=12), _r(1024, seed=13)
+    v = torch.zeros(1024)
+    P, G, V = p.to(gpu), g.to(gpu), v.to(gpu)
+    pb = torch.empty(1024, device=gpu, dtype=BF)
+    for _ in range(3):
+        cnn.sgd_momentum_mixed(P, G, V, pb, 0.1, 0.9, 1e-4, 0.5)
+        cnn.sgd_momentum_mixed(p, g, v, None, 0.1, 0.9, 1e-4, 0.5)
+    assert torch.allclose(P.cpu(), p, atol=1e-6)
+    assert torch.equal(pb.cpu(), P.cpu().to(BF))
