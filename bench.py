@@ -39,7 +39,7 @@ METRIC = "samples/sec (whole node) MNIST MLP sync-SGD at 1/2/4/8 MI355X; scaling
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--model", choices=["mlp", "bert"], default="mlp",
+    ap.add_argument("--model", choices=["mlp", "bert", "resnet50"], default="mlp",
                     help="mlp: the headline MNIST MLP (BASELINE.json metric); bert: north-star "
                          "BERT-base MLM config")
     ap.add_argument("--steps", type=int, default=None, help="default 20000 (mlp) / 30 (bert)")
@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--bert_batch", type=int, default=64, help="BERT sequences per GPU")
     ap.add_argument("--seq_len", type=int, default=128)
     ap.add_argument("--bert_config", choices=["base", "tiny"], default="base")
+    ap.add_argument("--resnet_batch", type=int, default=256, help="ResNet-50 images per GPU")
+    ap.add_argument("--image_size", type=int, default=224)
     ap.add_argument("--batch_size", type=int, default=100)
     ap.add_argument("--learning_rate", type=float, default=0.001)
     ap.add_argument("--max_graph_steps", type=int, default=1024,
@@ -60,7 +62,7 @@ def main():
                     help="use the data-parallel path (gradient all-reduce) even on 1 GPU")
     a = ap.parse_args()
     if a.steps is None:
-        a.steps = 20000 if a.model == "mlp" else 30
+        a.steps = {"mlp": 20000, "bert": 30, "resnet50": 20}[a.model]
     if a.warmup is None:
         a.warmup = 2000 if a.model == "mlp" else 5
 
@@ -80,6 +82,8 @@ def main():
 
     if a.model == "bert":
         return bench_bert(a, world, rank, local, dev)
+    if a.model == "resnet50":
+        return bench_resnet(a, world, rank, local, dev)
 
     # identical replicas: the counter-based Philox init gives every rank the
     # same parameters from the same seed (no broadcast needed; verified below)
@@ -214,6 +218,54 @@ def bench_bert(a, world, rank, local, dev):
                 "optimizer": "AdamW (fused, f32 master)"},
             "model_tflops_per_gpu": round(tr.flops_per_step() / (ms * 1e-3) / 1e12, 1),
             "final_loss": round(loss, 4), "final_mlm_acc": round(acc, 4),
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_resnet(a, world, rank, local, dev):
+    """North-star config: ResNet-50 synthetic ImageNet, bf16, sync DP over RCCL."""
+    from distributedtensorflowexample_amd.train.resnet_trainer import ResNetTrainer
+
+    comm = None
+    if world > 1:
+        from distributedtensorflowexample_amd.parallel.comm import NativeComm, TorchComm
+
+        comm = NativeComm.from_process_group() if a.comm == "native" else TorchComm()
+    tr = ResNetTrainer(a.resnet_batch, dev, comm=comm, image_size=a.image_size, data_seed=rank)
+    use_graph = not a.no_graph
+    tr.run(a.warmup, use_graph)
+    barrier = (dist.barrier if a.comm == "native" else (lambda: dist.barrier(device_ids=[local]))) \
+        if world > 1 else None
+    if barrier:
+        barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tr.run(a.steps, use_graph)
+    torch.cuda.synchronize()
+    if barrier:
+        barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = t if a.comm == "native" else t.to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss, acc = tr.stats()
+    ms = elapsed * 1e3 / a.steps
+    if rank == 0:
+        print(json.dumps({
+            "metric": "images/sec (whole node) ResNet-50 v1.5 training, synthetic ImageNet",
+            "value": round(a.resnet_batch * world * a.steps / elapsed, 1), "unit": "images/sec",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random %dx%d images, device-resident), random-init weights"
+                    % (a.image_size, a.image_size),
+            "config": {"model": "ResNet-50 v1.5 (BN train mode, momentum SGD)",
+                       "global_batch": a.resnet_batch * world, "per_gpu_batch": a.resnet_batch,
+                       "seq_len": None, "parallelism": "dp%d" % world,
+                       "comm": a.comm if world > 1 else "none", "hipgraph": use_graph},
+            "final_loss": round(loss, 4), "final_train_acc": round(acc, 4),
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

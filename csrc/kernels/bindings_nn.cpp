@@ -19,7 +19,9 @@ void bn_finalize_launch(int, long long, const float*, const float*, float, float
 void bn_apply_launch(long long, int, const void*, const float*, const float*, const float*,
                      const float*, const void*, int, void*, hipStream_t);
 void bn_bwd_launch(long long, int, const void*, const void*, const void*, const float*, const float*,
-                   const float*, int, float*, float*, void*, void*, hipStream_t);
+                   const float*, int, float*, float*, float*, void*, void*, hipStream_t);
+long long bn_bwd_scratch_rows(long long, int);
+void colpart_reduce_launch(int, int, const float*, const float*, float*, float*, hipStream_t);
 void maxpool_fwd_launch(int, int, int, int, const void*, void*, void*, hipStream_t);
 void maxpool_bwd_launch(int, int, int, int, const void*, const void*, void*, hipStream_t);
 void avgpool_fwd_launch(int, int, int, const void*, void*, hipStream_t);
@@ -150,10 +152,17 @@ void register_nn(py::module_& m) {
   });
   m.def("bn_bwd", [](long long M, int C, uintptr_t dy, uintptr_t yout, uintptr_t x, uintptr_t mean,
                      uintptr_t rstd, uintptr_t g, int relu, uintptr_t sdy, uintptr_t sdyxh,
-                     uintptr_t dx, uintptr_t dres, uintptr_t s) {
+                     uintptr_t scratch, uintptr_t dx, uintptr_t dres, uintptr_t s) {
     dtfx::bn_bwd_launch(M, C, P<const void>(dy), P<const void>(yout), P<const void>(x),
                         P<const float>(mean), P<const float>(rstd), P<const float>(g), relu,
-                        P<float>(sdy), P<float>(sdyxh), P<void>(dx), P<void>(dres), S(s));
+                        P<float>(sdy), P<float>(sdyxh), P<float>(scratch), P<void>(dx),
+                        P<void>(dres), S(s));
+  });
+  m.def("bn_bwd_scratch_rows", &dtfx::bn_bwd_scratch_rows);
+  m.def("colpart_reduce", [](int R, int C, uintptr_t ps, uintptr_t pq, uintptr_t os, uintptr_t oq,
+                             uintptr_t s) {
+    dtfx::colpart_reduce_launch(R, C, P<const float>(ps), P<const float>(pq), P<float>(os),
+                                P<float>(oq), S(s));
   });
   m.def("maxpool_fwd", [](int N, int H, int W, int C, uintptr_t x, uintptr_t y, uintptr_t idx,
                           uintptr_t s) {

@@ -32,6 +32,30 @@ __device__ __forceinline__ bf16x8 pack8(const float* f) {
 }  // namespace cn
 using namespace cn;
 
+// Column reduction of partial rows: out_s[c] += sum_r part_s[r][c] (and the same for q).
+// grid (ceil(C / 64), S): 64 channels x 4 row groups per block, one atomic per channel per block.
+__global__ __launch_bounds__(256) void colpart_reduce_kernel(int R, int C, const float* __restrict__ ps,
+                                                             const float* __restrict__ pq,
+                                                             float* __restrict__ os,
+                                                             float* __restrict__ oq) {
+  __shared__ float red[2][4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  float a = 0.f, b = 0.f;
+  if (c < C)
+    for (int r = blockIdx.y * 4 + rg; r < R; r += 4 * gridDim.y) {
+      a += ps[(size_t)r * C + c];
+      if (pq) b += pq[(size_t)r * C + c];
+    }
+  red[0][rg][threadIdx.x & 63] = a;
+  red[1][rg][threadIdx.x & 63] = b;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    const int l = threadIdx.x;
+    unsafeAtomicAdd(os + c, red[0][0][l] + red[0][1][l] + red[0][2][l] + red[0][3][l]);
+    if (pq) unsafeAtomicAdd(oq + c, red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l]);
+  }
+}
+
 // mean = s / M, var = q / M - mean^2 (biased, as used for normalisation),
 // running stats updated with the unbiased variance (momentum form of tf/keras).
 __global__ void bn_finalize_kernel(int C, float inv_m, float unbias, const float* __restrict__ s,
@@ -79,47 +103,67 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
   }
 }
 
-// Backward reductions: dy_eff = dy * (y > 0 if relu); sums over rows of dy_eff and
-// dy_eff * xhat per channel.  Block = 256 threads over a [rows x C] slab; each thread
-// owns 8 channels of a fixed channel group and strides over rows.
+// Backward reductions: dy_eff = dy * (y > 0 if relu); per block, sums over its rows of
+// dy_eff and dy_eff * xhat per channel, reduced in LDS and written as ONE partial row per
+// block ([blocks][C], no atomics); colpart_reduce finishes the column sums.
+// Each thread owns 8 channels of one channel group and strides over the block's rows.
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     long long M, int C, int rows_per_block, const unsigned short* __restrict__ dy,
     const unsigned short* __restrict__ yout, const unsigned short* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, int relu,
-    float* __restrict__ sum_dy, float* __restrict__ sum_dyxh) {
+    float* __restrict__ part_dy, float* __restrict__ part_dyxh) {
+  __shared__ float red[2][2048];  // [sum][rr * tpr * 8 + channel-in-pass]
   const int cg = C >> 3;
-  const int tpr = min(cg, 256);           // threads per row (channel groups covered per pass)
-  const int rpp = 256 / tpr;              // rows per pass
+  const int tpr = min(cg, 256);  // threads per row (channel groups per pass)
+  const int rpp = 256 / tpr;     // rows per pass
   const int t = threadIdx.x;
   const int g = t % tpr, rr = t / tpr;
-  if (rr >= rpp) return;
   const long long r0 = (long long)blockIdx.x * rows_per_block;
   const long long r1 = min(M, r0 + rows_per_block);
-  for (int gg = g; gg < cg; gg += tpr) {
+  for (int base = 0; base < cg; base += tpr) {  // channel groups [base, base + tpr)
+    const int gg = base + g;
     float a[8], b[8], mu[8], rs[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      a[u] = b[u] = 0.f;
-      mu[u] = mean[gg * 8 + u];
-      rs[u] = rstd[gg * 8 + u];
-    }
-    for (long long r = r0 + rr; r < r1; r += rpp) {
-      const long long i = r * cg + gg;
-      float d[8], xv[8], yv[8];
-      unpack8(((const bf16x8*)dy)[i], d);
-      unpack8(((const bf16x8*)x)[i], xv);
-      if (relu) unpack8(((const bf16x8*)yout)[i], yv);
+    for (int u = 0; u < 8; ++u) a[u] = b[u] = 0.f;
+    if (rr < rpp && gg < cg) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const float de = (relu && yv[u] <= 0.f) ? 0.f : d[u];
-        a[u] += de;
-        b[u] += de * (xv[u] - mu[u]) * rs[u];
+        mu[u] = mean[gg * 8 + u];
+        rs[u] = rstd[gg * 8 + u];
+      }
+      for (long long r = r0 + rr; r < r1; r += rpp) {
+        const long long i = r * cg + gg;
+        float d[8], xv[8], yv[8];
+        unpack8(((const bf16x8*)dy)[i], d);
+        unpack8(((const bf16x8*)x)[i], xv);
+        if (relu) unpack8(((const bf16x8*)yout)[i], yv);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float de = (relu && yv[u] <= 0.f) ? 0.f : d[u];
+          a[u] += de;
+          b[u] += de * (xv[u] - mu[u]) * rs[u];
+        }
       }
     }
+    __syncthreads();
+    if (rr < rpp)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      unsafeAtomicAdd(sum_dy + gg * 8 + u, a[u]);
-      unsafeAtomicAdd(sum_dyxh + gg * 8 + u, b[u]);
+      for (int u = 0; u < 8; ++u) {
+        red[0][rr * tpr * 8 + g * 8 + u] = a[u];
+        red[1][rr * tpr * 8 + g * 8 + u] = b[u];
+      }
+    __syncthreads();
+    for (int ch = t; ch < tpr * 8; ch += 256) {
+      float sa = 0.f, sb = 0.f;
+      for (int q = 0; q < rpp; ++q) {
+        sa += red[0][q * tpr * 8 + ch];
+        sb += red[1][q * tpr * 8 + ch];
+      }
+      const int c = base * 8 + ch;
+      if (c < C) {
+        part_dy[(size_t)blockIdx.x * C + c] = sa;
+        part_dyxh[(size_t)blockIdx.x * C + c] = sb;
+      }
     }
   }
 }
@@ -153,34 +197,44 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
-// 3x3 / stride 2 / pad 1 max pool, NHWC; idx = argmax tap (first max) per output element
+// 3x3 / stride 2 / pad 1 max pool, NHWC, 8 channels (16 B) per thread;
+// idx = argmax tap (first max) per output element
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(int N, int H, int W, int C, int OH, int OW,
                                                           const unsigned short* __restrict__ x,
                                                           unsigned short* __restrict__ y,
                                                           unsigned char* __restrict__ idx) {
-  const long long total = (long long)N * OH * OW * C;
+  const int cg = C >> 3;
+  const long long total = (long long)N * OH * OW * cg;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c = (int)(i % C);
-    long long p = i / C;
+    const int g = (int)(i % cg);
+    long long p = i / cg;
     const int ow = (int)(p % OW);
     p /= OW;
     const int oh = (int)(p % OH);
     const int n = (int)(p / OH);
-    float best = -INFINITY;
-    int bi = 0;
+    float best[8];
+    unsigned char bi[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { best[u] = -INFINITY; bi[u] = 0; }
     for (int kh = 0; kh < 3; ++kh) {
       const int ih = oh * 2 - 1 + kh;
       if (ih < 0 || ih >= H) continue;
       for (int kw = 0; kw < 3; ++kw) {
         const int iw = ow * 2 - 1 + kw;
         if (iw < 0 || iw >= W) continue;
-        const float v = bf(x[(((size_t)n * H + ih) * W + iw) * C + c]);
-        if (v > best) { best = v; bi = kh * 3 + kw; }
+        float v[8];
+        unpack8(*(const bf16x8*)(x + (((size_t)n * H + ih) * W + iw) * C + g * 8), v);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (v[u] > best[u]) { best[u] = v[u]; bi[u] = (unsigned char)(kh * 3 + kw); }
       }
     }
-    y[i] = tobf(best);
-    idx[i] = (unsigned char)bi;
+    ((bf16x8*)y)[i] = pack8(best);
+    uint2 pk;
+    pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((unsigned)bi[3] << 24);
+    pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((unsigned)bi[7] << 24);
+    ((uint2*)idx)[i] = pk;
   }
 }
 
@@ -188,16 +242,19 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int N, int H, int W, i
                                                           const unsigned short* __restrict__ dy,
                                                           const unsigned char* __restrict__ idx,
                                                           unsigned short* __restrict__ dx) {
-  const long long total = (long long)N * H * W * C;
+  const int cg = C >> 3;
+  const long long total = (long long)N * H * W * cg;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c = (int)(i % C);
-    long long p = i / C;
+    const int g = (int)(i % cg);
+    long long p = i / cg;
     const int iw = (int)(p % W);
     p /= W;
     const int ih = (int)(p % H);
     const int n = (int)(p / H);
-    float acc = 0.f;
+    float acc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = 0.f;
     // outputs whose window covers (ih, iw): oh = (ih + 1 - kh) / 2 for kh in 0..2
     for (int kh = 0; kh < 3; ++kh) {
       const int t = ih + 1 - kh;
@@ -209,11 +266,19 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int N, int H, int W, i
         if (u < 0 || (u & 1)) continue;
         const int ow = u >> 1;
         if (ow >= OW) continue;
-        const size_t o = (((size_t)n * OH + oh) * OW + ow) * C + c;
-        if (idx[o] == kh * 3 + kw) acc += bf(dy[o]);
+        const size_t o = ((((size_t)n * OH + oh) * OW + ow) * C) / 8 + g;
+        const uint2 pk = ((const uint2*)idx)[o];
+        float d[8];
+        unpack8(((const bf16x8*)dy)[o], d);
+        const int tap = kh * 3 + kw;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const unsigned w = q < 4 ? pk.x : pk.y;
+          if (((w >> (8 * (q & 3))) & 0xFF) == (unsigned)tap) acc[q] += d[q];
+        }
       }
     }
-    dx[i] = tobf(acc);
+    ((bf16x8*)dx)[i] = pack8(acc);
   }
 }
 
@@ -270,6 +335,16 @@ static unsigned grid_for(long long n, int per = 256) {
   return (unsigned)b;
 }
 
+void colpart_reduce_launch(int R, int C, const float* ps, const float* pq, float* os, float* oq,
+                           hipStream_t st) {
+  int S = (R + 15) / 16;
+  if (S > 128) S = 128;
+  if (S < 1) S = 1;
+  hipLaunchKernelGGL(colpart_reduce_kernel, dim3((C + 63) / 64, S), dim3(256), 0, st, R, C, ps, pq,
+                     os, oq);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
 void bn_finalize_launch(int C, long long M, const float* s, const float* q, float eps, float* mean,
                         float* rstd, float* run_mean, float* run_var, float momentum,
                         hipStream_t st) {
@@ -289,21 +364,32 @@ void bn_apply_launch(long long M, int C, const void* x, const float* mean, const
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
-void bn_bwd_launch(long long M, int C, const void* dy, const void* yout, const void* x,
-                   const float* mean, const float* rstd, const float* gamma, int relu,
-                   float* sum_dy, float* sum_dyxh, void* dx, void* dres, hipStream_t st) {
-  if (C % 8) throw std::runtime_error("bn_bwd: C % 8 != 0");
-  DTFX_HIP_CHECK(hipMemsetAsync(sum_dy, 0, sizeof(float) * C, st));
-  DTFX_HIP_CHECK(hipMemsetAsync(sum_dyxh, 0, sizeof(float) * C, st));
+// sum_dy / sum_dyxh (f32 [C]) are ACCUMULATED (+=): pass zeroed buffers, or the
+// (zeroed) dbeta / dgamma gradient slots themselves -- they are exactly these sums.
+// scratch: f32 [2 * bn_bwd_scratch_rows(M, C)][C].
+long long bn_bwd_scratch_rows(long long M, int C) {
   const int cg = C / 8, tpr = cg < 256 ? cg : 256, rpp = 256 / tpr;
-  // enough blocks to fill the chip, each covering a contiguous row range
   long long rpb = (M + 1023) / 1024;
   if (rpb < rpp * 4) rpb = rpp * 4;
-  const unsigned blocks = (unsigned)((M + rpb - 1) / rpb);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, st, M, C, (int)rpb,
+  return (M + rpb - 1) / rpb;
+}
+
+void bn_bwd_launch(long long M, int C, const void* dy, const void* yout, const void* x,
+                   const float* mean, const float* rstd, const float* gamma, int relu,
+                   float* sum_dy, float* sum_dyxh, float* scratch, void* dx, void* dres,
+                   hipStream_t st) {
+  if (C % 8 || C > 2048 * 64) throw std::runtime_error("bn_bwd: C % 8 != 0");
+  const int cg = C / 8, tpr = cg < 256 ? cg : 256, rpp = 256 / tpr;
+  long long rpb = (M + 1023) / 1024;
+  if (rpb < rpp * 4) rpb = rpp * 4;
+  const long long blocks = (M + rpb - 1) / rpb;
+  float* part_dy = scratch;
+  float* part_dyxh = scratch + blocks * C;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, M, C, (int)rpb,
                      (const unsigned short*)dy, (const unsigned short*)yout,
-                     (const unsigned short*)x, mean, rstd, relu, sum_dy, sum_dyxh);
+                     (const unsigned short*)x, mean, rstd, relu, part_dy, part_dyxh);
   DTFX_HIP_CHECK(hipGetLastError());
+  colpart_reduce_launch((int)blocks, C, part_dy, part_dyxh, sum_dy, sum_dyxh, st);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(M * C / 8)), dim3(256), 0, st, M, C,
                      (const unsigned short*)dy, (const unsigned short*)yout,
                      (const unsigned short*)x, mean, rstd, gamma, sum_dy, sum_dyxh, relu,
@@ -312,8 +398,9 @@ void bn_bwd_launch(long long M, int C, const void* dy, const void* yout, const v
 }
 
 void maxpool_fwd_launch(int N, int H, int W, int C, const void* x, void* y, void* idx, hipStream_t st) {
+  if (C % 8) throw std::runtime_error("maxpool: C % 8 != 0");
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * OH * OW * C)), dim3(256), 0,
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * OH * OW * C / 8)), dim3(256), 0,
                      st, N, H, W, C, OH, OW, (const unsigned short*)x, (unsigned short*)y,
                      (unsigned char*)idx);
   DTFX_HIP_CHECK(hipGetLastError());
@@ -321,8 +408,9 @@ void maxpool_fwd_launch(int N, int H, int W, int C, const void* x, void* y, void
 
 void maxpool_bwd_launch(int N, int H, int W, int C, const void* dy, const void* idx, void* dx,
                         hipStream_t st) {
+  if (C % 8) throw std::runtime_error("maxpool: C % 8 != 0");
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0, st,
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * H * W * C / 8)), dim3(256), 0, st,
                      N, H, W, C, OH, OW, (const unsigned short*)dy, (const unsigned char*)idx,
                      (unsigned short*)dx);
   DTFX_HIP_CHECK(hipGetLastError());

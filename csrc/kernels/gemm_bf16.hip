@@ -269,6 +269,8 @@ struct GemmEpi {
   int act_grad;                 // multiply by act'(aux_in)
   float* colsum;                // [N] += column sums of the final values (bias gradient), or null
   float* colsq;                 // [N] += column sums of squares (BatchNorm statistics), or null
+  int col_partial;              // 1: colsum/colsq are [2 * m_tiles][N] partial rows (plain stores,
+                                //    no same-address atomics: BatchNorm statistics of tall convs)
 };
 
 template <int MODE, bool TA, bool TB, bool OUT_F32>
@@ -483,13 +485,23 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
       cq[u] += __shfl_xor(cq[u], 32);
     }
     const int n = n0 + wn * 64 + (lane & 7) * 8;
-    if (lane < 8)
+    if (e.col_partial) {
+      const size_t prow = (size_t)((m0 / BM) * 2 + wm) * N;
+      if (lane < 8)
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (n + u < N) {
+            if (e.colsum) e.colsum[prow + n + u] = cs[u];
+            if (e.colsq) e.colsq[prow + n + u] = cq[u];
+          }
+    } else if (lane < 8) {
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         if (n + u < N) {
           if (e.colsum) unsafeAtomicAdd(e.colsum + n + u, cs[u]);
           if (e.colsq) unsafeAtomicAdd(e.colsq + n + u, cq[u]);
         }
+    }
   }
 }
 
@@ -535,7 +547,7 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
     }
   }
   GemmEpi e{alpha, beta, bias, act, (const unsigned short*)aux_in, (unsigned short*)aux_out,
-            ld_aux, (const unsigned short*)residual, ld_res, act_grad, colsum, nullptr};
+            ld_aux, (const unsigned short*)residual, ld_res, act_grad, colsum, nullptr, 0};
   const dim3 grid(tiles, splitk, batch);
   const size_t lds = 2 * gb::BUF_BYTES;
   auto* Au = (const unsigned short*)A;
@@ -560,7 +572,8 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
 
 // Convolution launcher (modes in the ConvDesc comment above).
 //  fwd  : x [N*H*W][C], w [Cout][ldw >= ceil64(KH*KW*C)] (zero-padded), y [N*OH*OW][Cout]
-//         optional fused BatchNorm statistics: colsum / colsq over y (f32 [Cout])
+//         optional fused BatchNorm statistics: colsum / colsq = per-tile partial rows
+//         [2 * ceil(N*OH*OW / 128)][Cout] (f32, fully overwritten)
 //  dgrad: dy [N*OH*OW][Cout], w [Cout][ldw], dx [N*H*W][C]
 //         (+ residual)
 //  wgrad: dy, x -> dw [Cout][ldw] f32 (first KH*KW*C columns; += when beta == 1)
@@ -573,8 +586,11 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
   if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) & 15)
     throw std::runtime_error("conv_bf16: tensors must be 16-byte aligned");
   ConvDesc d{N, H, W, C, OH, OW, Cout, KH, KW, stride, pad, 0, ldw > 0 ? ldw : KH * KW * C};
+  // fwd statistics go to per-tile partial rows [2 * ceil(M / 128)][Cout] (reduced by
+  // colpart_reduce in cnn.hip): thousands of blocks would otherwise serialise on the same
+  // Cout addresses (f32 atomics execute at the memory side)
   GemmEpi e{1.f, beta, nullptr, 0, nullptr, nullptr, 0, (const unsigned short*)residual, 0, 0,
-            colsum, colsq};
+            colsum, colsq, mode == 1 ? 1 : 0};
   const size_t lds = 2 * gb::BUF_BYTES;
   int M, Nn, K;
   if (mode == 1) {

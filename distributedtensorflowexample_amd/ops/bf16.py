@@ -86,6 +86,19 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
             out.copy_(v)
             return out
         return v.to(out_dtype)
+    if K % 64:
+        # the kernel consumes K in 64-wide steps: zero-pad both operands along K (small
+        # GEMMs only in practice, e.g. a classifier's weight gradient at a small batch)
+        Kp = (K + 63) // 64 * 64
+        if trans_a:
+            a = torch.cat([a, a.new_zeros(Kp - K, a.shape[1])], 0)
+        else:
+            a = torch.cat([a, a.new_zeros(a.shape[0], Kp - K)], 1)
+        if trans_b:
+            b = torch.cat([b, b.new_zeros(b.shape[0], Kp - K)], 1)
+        else:
+            b = torch.cat([b, b.new_zeros(Kp - K, b.shape[1])], 0)
+        K = Kp
     _check(a, "a")
     _check(b, "b")
     _check(residual, "residual")

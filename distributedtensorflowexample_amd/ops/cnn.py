@@ -37,8 +37,11 @@ def _nchw(x):
 
 
 def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
-    """y = conv(x, w) (NHWC bf16); optional fused BN statistics (sum / sum of squares of y per
-    output channel, accumulated into f32 ``colsum`` / ``colsq``)."""
+    """y = conv(x, w) (NHWC bf16); optional fused BN statistics: the sum / sum of squares of y
+    per output channel are ACCUMULATED into f32 ``colsum`` / ``colsq`` [Cout] (both or neither).
+
+    GPU: the convolution epilogue writes per-tile partial rows (no same-address atomics) and
+    ``colpart_reduce`` folds them into colsum / colsq."""
     N, H, W, C = x.shape
     Cout = w.shape[0]
     OH, OW = out_hw(H, W, KH, stride, pad)
@@ -53,8 +56,16 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
             colsq += (y.reshape(-1, Cout) ** 2).sum(0)
         return y.to(BF16)
     y = torch.empty(N, OH, OW, Cout, device=x.device, dtype=BF16)
+    ps = pq = None
+    if colsum is not None:
+        rows = 2 * ((N * OH * OW + 127) // 128)
+        part = torch.empty(2, rows, Cout, device=x.device)
+        ps, pq = part[0], part[1]
     hip().conv_bf16(1, N, H, W, C, Cout, KH, KW, stride, pad, ptr(x), ptr(w), w.stride(0), ptr(y),
-                    0.0, ptr(residual), ptr(colsum), ptr(colsq), 0, stream_handle())
+                    0.0, ptr(residual), ptr(ps), ptr(pq), 0, stream_handle())
+    if colsum is not None:
+        hip().colpart_reduce(ps.shape[0], Cout, ptr(ps), ptr(pq), ptr(colsum), ptr(colsq),
+                             stream_handle())
     return y
 
 
@@ -122,9 +133,14 @@ def bn_apply(x, mean, rstd, gamma, beta, residual=None, relu=True):
     return y
 
 
-def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, relu=True, want_dres=False):
+def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, relu=True, want_dres=False,
+           grads_zeroed=False):
     """Backward of y = act(bn(x) [+ res]).  Accumulates dgamma/dbeta; returns (dx, dres)
-    where dres = dy * act'(y) is the gradient of the residual input (if requested)."""
+    where dres = dy * act'(y) is the gradient of the residual input (if requested).
+
+    ``grads_zeroed=True`` (the model's per-step zeroed gradient slots) lets the GPU kernels
+    reduce straight into dgamma / dbeta -- they are exactly sum(dy_eff * xhat) / sum(dy_eff)
+    -- instead of into zeroed temporaries that are then added."""
     C = x.shape[-1]
     M = x.numel() // C
     if not x.is_cuda:
@@ -136,14 +152,20 @@ def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, relu=True, want_dres=Fals
         dgamma += sdx
         dbeta += sdy
         return dx.reshape(x.shape).to(BF16), (de.to(BF16) if want_dres else None)
-    sdy = torch.empty(C, device=x.device)
-    sdx = torch.empty(C, device=x.device)
+    if grads_zeroed:
+        sdy, sdx = dbeta, dgamma
+    else:
+        sums = torch.zeros(2, C, device=x.device)
+        sdy, sdx = sums[0], sums[1]
+    rows = hip().bn_bwd_scratch_rows(M, C)
+    scratch = torch.empty(2 * rows * C, device=x.device)
     dx = torch.empty_like(x)
     dres = torch.empty_like(x) if want_dres else None
     hip().bn_bwd(M, C, ptr(dy), ptr(y), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), int(relu),
-                 ptr(sdy), ptr(sdx), ptr(dx), ptr(dres), stream_handle())
-    dgamma += sdx
-    dbeta += sdy
+                 ptr(sdy), ptr(sdx), ptr(scratch), ptr(dx), ptr(dres), stream_handle())
+    if not grads_zeroed:
+        dgamma += sdx
+        dbeta += sdy
     return dx, dres
 
 

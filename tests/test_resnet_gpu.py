@@ -1,0 +1,36 @@
+"""ResNet on the GPU kernels vs the same code on the CPU reference paths."""
+import pytest
+import torch
+
+from distributedtensorflowexample_amd.models.resnet import ResNet50, synthetic_imagenet
+
+pytestmark = pytest.mark.gpu
+STAGES = [(64, 2, 1), (128, 1, 2)]
+
+
+def test_small_resnet_gpu_matches_cpu(gpu):
+    mg = ResNet50(gpu, seed=1, stages=STAGES, num_classes=10)
+    mc = ResNet50("cpu", seed=1, stages=STAGES, num_classes=10)
+    mc.params.master.copy_(mg.params.master.cpu())
+    mc.params.bf.copy_(mg.params.bf.cpu())
+    x, y = synthetic_imagenet(8, "cpu", size=32, seed=2, num_classes=10)
+    lg, _ = mg.forward_backward(x.to(gpu), y.to(gpu))
+    lc, _ = mc.forward_backward(x, y)
+    assert abs(lg.item() - lc.item()) < 0.02 * lc.item()
+    P, Q = mg.params, mc.params
+    for name in ["conv1.weight", "layer1.0.conv2.weight", "layer2.0.downsample.weight",
+                 "layer1.1.conv3.bn.gamma", "fc.weight"]:
+        g, r = P.G(name).cpu().flatten(), Q.G(name).flatten()
+        cos = torch.dot(g, r) / (g.norm() * r.norm() + 1e-30)
+        assert cos > 0.97, (name, cos.item())
+
+
+def test_resnet50_trainer_steps(gpu):
+    from distributedtensorflowexample_amd.train.resnet_trainer import ResNetTrainer
+
+    tr = ResNetTrainer(64, gpu, image_size=64)
+    tr.run(2)
+    l0, _ = tr.stats()
+    tr.run(3, use_graph=True)
+    l1, _ = tr.stats()
+    assert 0 < l1 < 15 and l0 > 0
