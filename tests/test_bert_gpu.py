@@ -47,3 +47,14 @@ def test_bert_base_step_runs(gpu):
     tr.run(2)
     loss, acc = tr.stats()
     assert 5.0 < loss < 20.0   # ~ln(30522) = 10.3 at init
+
+
+def test_bert_fits_fixed_batch(gpu):
+    from distributedtensorflowexample_amd.train.bert_trainer import BertTrainer
+
+    tr = BertTrainer(BertConfig.tiny(), 8, 128, gpu, lr=2e-3)
+    tr.run(1)
+    l0, _ = tr.stats()
+    tr.run(30, use_graph=True)
+    l1, _ = tr.stats()
+    assert l1 < 0.7 * l0, (l0, l1)

@@ -34,3 +34,14 @@ def test_resnet50_trainer_steps(gpu):
     tr.run(3, use_graph=True)
     l1, _ = tr.stats()
     assert 0 < l1 < 15 and l0 > 0
+
+
+def test_resnet_fits_fixed_batch(gpu):
+    from distributedtensorflowexample_amd.train.resnet_trainer import ResNetTrainer
+
+    tr = ResNetTrainer(64, gpu, lr=0.05, image_size=32, stages=STAGES, num_classes=10)
+    tr.run(1)
+    l0, _ = tr.stats()
+    tr.run(24)
+    l1, a1 = tr.stats()
+    assert l1 < 0.5 * l0, (l0, l1)   # memorises the fixed synthetic batch
