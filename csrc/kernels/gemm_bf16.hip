@@ -42,6 +42,7 @@
 // masked on store).
 #include "common.h"
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -95,22 +96,24 @@ __device__ __forceinline__ void fdivmod(int a, int d, float inv, int& q, int& r)
 }
 
 namespace gb {
-constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
-constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB per operand tile
-constexpr int BUF_BYTES = 2 * TILE_BYTES;
+constexpr int BN = 128, BK = 64;  // tile N and K; the tile height BM is a template parameter
 
 __device__ __forceinline__ int swz_tr(int r) { return ((r & 3) | (((r >> 3) & 1) << 2)) << 1; }
 
-// Stage one operand tile (16 KB) with 4 glds per thread.
-//  KCONT: tile rows = 128 outer (m or n) indices x 64 k; src row stride ld.
-//  else : tile rows = 64 k x 128 outer; src row stride ld.
-template <bool KCONT>
+// Stage one operand tile of OUTER x 64 (OUTER * 128 bytes) with glds: NW waves, each wave
+// instruction fills one 1 KB block.
+//  KCONT: tile rows = OUTER outer (m or n) indices x 64 k (128-B rows); src row stride ld.
+//  else : tile rows = 64 k x OUTER outer (OUTER*2-B rows); src row stride ld.
+template <bool KCONT, int OUTER, int NW>
 __device__ __forceinline__ void stage(const unsigned short* __restrict__ src, int ld, int outer0,
                                       int outer_max, int k0, char* lds_tile, int wave, int lane,
                                       int kmax) {
+  constexpr int NB = OUTER / 8;            // 1 KB blocks per tile
+  constexpr int LPR = OUTER / 8;           // lanes per k-row in the k-strided image
+  constexpr int RPB = 64 / LPR;            // k-rows per block
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int blk = i * 4 + wave;  // 1 KB block of the tile this wave-instruction fills
+  for (int i = 0; i < NB / NW; ++i) {
+    const int blk = i * NW + wave;  // 1 KB block of the tile this wave-instruction fills
     const unsigned short* g;
     if (KCONT) {
       const int row = blk * 8 + (lane >> 3), cs = lane & 7;
@@ -118,7 +121,7 @@ __device__ __forceinline__ void stage(const unsigned short* __restrict__ src, in
       const int o = min(outer0 + row, outer_max);
       g = src + (size_t)o * ld + k0 + c * 8;
     } else {
-      const int kr = blk * 4 + (lane >> 4), cs = lane & 15;
+      const int kr = blk * RPB + lane / LPR, cs = lane % LPR;
       const int c = cs ^ swz_tr(kr);
       const int o = min(outer0 + c * 8, outer_max);  // outer_max is 8-aligned-safe (host)
       g = src + (size_t)min(k0 + kr, kmax) * ld + o;  // clamped K tail: partner operand is 0
@@ -128,8 +131,9 @@ __device__ __forceinline__ void stage(const unsigned short* __restrict__ src, in
 }
 
 // Fragment (8 bf16 along k) for MFMA 16x16x32: lane holds [outer = o0 + (l&15)][k = kk*32 + 8(l>>4) + j]
-template <bool KCONT>
+template <bool KCONT, int OUTER>
 __device__ __forceinline__ bf16x8 frag(const char* lds_tile, int o0, int kk, int lane) {
+  constexpr int RB = OUTER * 2;  // row bytes of the k-strided image
   if (KCONT) {
     const int row = o0 + (lane & 15);
     const int c = kk * 4 + (lane >> 4);
@@ -141,8 +145,8 @@ __device__ __forceinline__ bf16x8 frag(const char* lds_tile, int o0, int kk, int
     const int col = o0 + 4 * p;
     const int cch = col >> 3, cb = (col & 7) * 2;
     const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
-    const char* a0 = lds_tile + r0 * 256 + ((cch ^ swz_tr(r0)) << 4) + cb;
-    const char* a1 = lds_tile + r1 * 256 + ((cch ^ swz_tr(r1)) << 4) + cb;
+    const char* a0 = lds_tile + r0 * RB + ((cch ^ swz_tr(r0)) << 4) + cb;
+    const char* a1 = lds_tile + r1 * RB + ((cch ^ swz_tr(r1)) << 4) + cb;
     bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)a0);
     bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)a1);
     bf16x8 v;
@@ -156,13 +160,14 @@ struct RowState {
   int nb[4], y0[4], x0[4];  // n*H*W (or -1 past M), spatial base of each of the lane's 4 rows
 };
 
+template <int NW>
 __device__ __forceinline__ void conv_rows(const ConvDesc& d, int mode, int M, int m0, int wave,
                                           int lane, RowState& rs) {
   const int PW = mode == 1 ? d.OW : d.W, PHW = mode == 1 ? d.OH * d.OW : d.H * d.W;
   const float ipw = 1.f / PW, iphw = 1.f / PHW;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int m = m0 + (i * 4 + wave) * 8 + (lane >> 3);
+    const int m = m0 + (i * NW + wave) * 8 + (lane >> 3);
     int n, rem, py, px;
     fdivmod(min(m, M - 1), PHW, iphw, n, rem);
     fdivmod(rem, PW, ipw, py, px);
@@ -177,7 +182,9 @@ __device__ __forceinline__ void conv_rows(const ConvDesc& d, int mode, int M, in
   }
 }
 
-// A tile gather for conv fwd (mode 1: src = x, channels C) / dgrad (mode 2: src = dy, channels K)
+// A tile gather for conv fwd (mode 1: src = x, channels C) / dgrad (mode 2: src = dy, channels K);
+// tile height 32 * NW rows: 4 blocks per wave
+template <int NW>
 __device__ __forceinline__ void stage_a_conv(const ConvDesc& d, int mode, const RowState& rs,
                                              const unsigned short* __restrict__ src, int k0,
                                              char* lds_tile, int wave, int lane) {
@@ -186,7 +193,7 @@ __device__ __forceinline__ void stage_a_conv(const ConvDesc& d, int mode, const 
   const int tap_u = k0 / CH, c_u = k0 - tap_u * CH;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int blk = i * 4 + wave;
+    const int blk = i * NW + wave;
     const int row = blk * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (row & 7);
     const int k = k0 + c * 8;
@@ -215,12 +222,13 @@ __device__ __forceinline__ void stage_a_conv(const ConvDesc& d, int mode, const 
 }
 
 // B tile for dgrad (k-strided image [64 k][128 ci]): W'[k = (kh, kw, co)][ci] = W[co][kh][kw][ci]
+template <int NW>
 __device__ __forceinline__ void stage_b_wtap(const ConvDesc& d, const unsigned short* __restrict__ w,
                                              int n0, int k0, char* lds_tile, int wave, int lane) {
   const int tap = k0 / d.K, co0 = k0 - tap * d.K;  // host: K % 64 == 0
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int blk = i * 4 + wave;
+  for (int i = 0; i < 16 / NW; ++i) {
+    const int blk = i * NW + wave;
     const int kr = blk * 4 + (lane >> 4);
     const int c = (lane & 15) ^ swz_tr(kr);
     const int o = n0 + c * 8;
@@ -232,6 +240,7 @@ __device__ __forceinline__ void stage_b_wtap(const ConvDesc& d, const unsigned s
 }
 
 // B tile for wgrad (k-strided image [64 pixels][128 j]): im2col(x)[p][j = (kh, kw, ci)]
+template <int NW>
 __device__ __forceinline__ void stage_b_im2col(const ConvDesc& d, const unsigned short* __restrict__ x,
                                                int NP, int n0, int k0, char* lds_tile, int wave,
                                                int lane) {
@@ -239,8 +248,8 @@ __device__ __forceinline__ void stage_b_im2col(const ConvDesc& d, const unsigned
   const float iohw = 1.f / ohw, iow = 1.f / d.OW, ikw = 1.f / d.KW, ic = 1.f / d.C;
   const int jtot = d.KH * d.KW * d.C;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int blk = i * 4 + wave;
+  for (int i = 0; i < 16 / NW; ++i) {
+    const int blk = i * NW + wave;
     const int kr = blk * 4 + (lane >> 4);
     const int c = (lane & 15) ^ swz_tr(kr);
     const int p = k0 + kr, j = n0 + c * 8;
@@ -254,6 +263,13 @@ __device__ __forceinline__ void stage_b_im2col(const ConvDesc& d, const unsigned
     const unsigned short* g = ok ? x + ((size_t)(n * d.H + yy) * d.W + xx) * d.C + ci : g_zero16;
     __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(lds_tile + blk * 1024), 16, 0, 0);
   }
+}
+// s_waitcnt vmcnt(N) + lgkmcnt(0) + s_barrier in one asm statement: the LDS-DMA (glds) of
+// the newest N loads stays in flight across the barrier ("memory" keeps the compiler's
+// LDS reads of the retiring buffer before it).
+template <int N>
+__device__ __forceinline__ void vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 }  // namespace gb
 
@@ -273,12 +289,17 @@ struct GemmEpi {
                                 //    no same-address atomics: BatchNorm statistics of tall convs)
 };
 
-template <int MODE, bool TA, bool TB, bool OUT_F32>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
+// BM_ = 128 (4 waves, 2 blocks/CU) or 256 (8 waves); NBUF = LDS stages (2: next tile in
+// flight during compute; 3: two tiles in flight, counted vmcnt + raw barrier).
+template <int MODE, bool TA, bool TB, bool OUT_F32, int BM_, int NBUF>
+__global__ __launch_bounds__(BM_ * 2, BM_ == 128 && NBUF == 2 ? 2 : 1) void gemm_bf16_kernel(
     int M, int N, int K, const unsigned short* __restrict__ A, int lda,
     const unsigned short* __restrict__ B, int ldb, void* __restrict__ Cv, int ldc, GemmEpi e,
     long long sA, long long sB, long long sC, ConvDesc cd) {
   using namespace gb;
+  constexpr int BM = BM_, NW = BM_ / 32;           // waves: (BM/64) x 2
+  constexpr int TILE_A = BM * BK * 2, TILE_B = BN * BK * 2, BUF_BYTES = TILE_A + TILE_B;
+  constexpr int LPT = (BM / 8) / NW + 16 / NW;      // glds per thread per K tile
   // strided batch over blockIdx.z (attention's per-(batch, head) products)
   A += sA * blockIdx.z;
   B += sB * blockIdx.z;
@@ -306,39 +327,62 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
   const int kt0 = blockIdx.y * per;
   const int nk = max(0, min(per, nk_all - kt0));
   RowState rs;
-  if (MODE == 1 || MODE == 2) conv_rows(cd, MODE, M, m0, wave, lane, rs);
+  if (MODE == 1 || MODE == 2) conv_rows<NW>(cd, MODE, M, m0, wave, lane, rs);
   auto stage_all = [&](int buf, int kt) {
     char* base = smem + buf * BUF_BYTES;
     const int k0 = (kt0 + kt) * BK;
-    if (MODE == 1 || MODE == 2) stage_a_conv(cd, MODE, rs, A, k0, base, wave, lane);
-    else stage<!TA>(A, lda, m0, a_max, k0, base, wave, lane, K - 1);
-    if (MODE == 2) stage_b_wtap(cd, B, n0, k0, base + TILE_BYTES, wave, lane);
-    else if (MODE == 3) stage_b_im2col(cd, B, K, n0, k0, base + TILE_BYTES, wave, lane);
-    else stage<TB>(B, ldb, n0, b_max, k0, base + TILE_BYTES, wave, lane, K - 1);
+    if (MODE == 1 || MODE == 2) stage_a_conv<NW>(cd, MODE, rs, A, k0, base, wave, lane);
+    else stage<!TA, BM, NW>(A, lda, m0, a_max, k0, base, wave, lane, K - 1);
+    if (MODE == 2) stage_b_wtap<NW>(cd, B, n0, k0, base + TILE_A, wave, lane);
+    else if (MODE == 3) stage_b_im2col<NW>(cd, B, K, n0, k0, base + TILE_A, wave, lane);
+    else stage<TB, BN, NW>(B, ldb, n0, b_max, k0, base + TILE_A, wave, lane, K - 1);
   };
-  if (nk > 0) stage_all(0, 0);
-  __syncthreads();  // emits vmcnt(0): tile 0 landed for every wave
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage_all(cur ^ 1, kt + 1);
-    const char* At = smem + cur * BUF_BYTES;
-    const char* Bt = At + TILE_BYTES;
+  auto compute = [&](int buf) {
+    const char* At = smem + buf * BUF_BYTES;
+    const char* Bt = At + TILE_A;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag<!TA>(At, wm * 64 + i * 16, kk, lane);
+      for (int i = 0; i < 4; ++i) af[i] = frag<!TA, BM>(At, wm * 64 + i * 16, kk, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag<TB>(Bt, wn * 64 + j * 16, kk, lane);
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<TB, BN>(Bt, wn * 64 + j * 16, kk, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
+  };
+  if (NBUF == 2) {
+    if (nk > 0) stage_all(0, 0);
+    __syncthreads();  // emits vmcnt(0): tile 0 landed for every wave
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) stage_all(cur ^ 1, kt + 1);
+      compute(cur);
+      __syncthreads();
+    }
+  } else {
+    // 3 stages: tiles kt+1 and kt+2 in flight while tile kt computes.  Before computing
+    // tile t every wave has retired its own loads of t (counted vmcnt: the younger tiles
+    // stay in flight) and passed a barrier, so all waves' DMA into that buffer is visible.
+    if (nk > 0) stage_all(0, 0);
+    if (nk > 1) stage_all(1, 1);
+    if (nk > 1) vm_barrier<LPT>();
+    else vm_barrier<0>();
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool issue = kt + 2 < nk;
+      if (issue) stage_all(cur == 0 ? 2 : cur - 1, kt + 2);  // buffer of tile kt-1: retired
+      compute(cur);
+      // retire tile kt+1 (one younger tile may stay in flight)
+      if (issue) vm_barrier<LPT>();
+      else vm_barrier<0>();
+      cur = cur == 2 ? 0 : cur + 1;
+    }
   }
+  __syncthreads();
 
   // Epilogue.  The accumulators (C/D map: col = lane & 15, row = (lane >> 4) * 4 + r)
   // go through a per-wave LDS transpose, 32 rows at a time, so every lane then owns 8
@@ -486,8 +530,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
     }
     const int n = n0 + wn * 64 + (lane & 7) * 8;
     if (e.col_partial) {
-      const size_t prow = (size_t)((m0 / BM) * 2 + wm) * N;
-      if (lane < 8)
+      const size_t prow = (size_t)(m0 / 64 + wm) * N;  // one partial row per 64-row wave slab
+      if (lane < 8 && m0 + wm * 64 < M)
 #pragma unroll
         for (int u = 0; u < 8; ++u)
           if (n + u < N) {
@@ -503,6 +547,59 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(
         }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Launch-configuration choice.  cfg 0: 128x128 tile, 4 waves, 2 LDS stages (64 KB, 2 blocks
+// per CU); cfg 1: 256x128, 8 waves, 3 stages (144 KB, counted-vmcnt pipeline); cfg 2:
+// 256x128, 2 stages (96 KB).  Auto: the 256-row tile when it still yields >= 256 blocks
+// (one full wave of the 256 CUs), else 128.  DTFX_GEMM_CFG=0/1/2 forces one (benchmarks).
+// ---------------------------------------------------------------------------
+static int gemm_cfg_env() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("DTFX_GEMM_CFG");
+    v = e ? atoi(e) : -1;
+  }
+  return v;
+}
+
+static int choose_cfg(int M, int N, int zdim) {
+  const int f = gemm_cfg_env();
+  if (f >= 0 && f <= 2) return f;
+  const long long t256 = (long long)((M + 255) / 256) * ((N + 127) / 128) * zdim;
+  return t256 >= 256 ? 1 : 0;
+}
+
+template <int MODE, bool TA, bool TB, bool F, int BM_, int NBUF>
+static void launch_one(dim3 grid_yz, int M, int N, int K, const unsigned short* A, int lda,
+                       const unsigned short* B, int ldb, void* C, int ldc, const GemmEpi& e,
+                       long long sA, long long sB, long long sC, const ConvDesc& d,
+                       hipStream_t stream) {
+  constexpr size_t lds = (size_t)NBUF * (BM_ * gb::BK * 2 + gb::BN * gb::BK * 2);
+  static bool attr = false;
+  if (!attr) {
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int tiles = ((M + BM_ - 1) / BM_) * ((N + gb::BN - 1) / gb::BN);
+  hipLaunchKernelGGL((gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF>), dim3(tiles, grid_yz.y, grid_yz.z),
+                     dim3(BM_ * 2), lds, stream, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC, d);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+template <int MODE, bool TA, bool TB, bool F>
+static void launch_cfg(int cfg, dim3 grid_yz, int M, int N, int K, const unsigned short* A, int lda,
+                       const unsigned short* B, int ldb, void* C, int ldc, const GemmEpi& e,
+                       long long sA, long long sB, long long sC, const ConvDesc& d,
+                       hipStream_t stream) {
+  if (cfg == 1)
+    launch_one<MODE, TA, TB, F, 256, 3>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC, d, stream);
+  else if (cfg == 2)
+    launch_one<MODE, TA, TB, F, 256, 2>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC, d, stream);
+  else
+    launch_one<MODE, TA, TB, F, 128, 2>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC, d, stream);
 }
 
 void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const void* A, int lda,
@@ -529,7 +626,7 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
     throw std::runtime_error("gemm_bf16: residual must be 16-byte aligned with ld_res % 8 == 0");
   if (bias && ((uintptr_t)bias & 15)) throw std::runtime_error("gemm_bf16: bias must be 16-byte aligned");
   if (act_grad && !aux_in) throw std::runtime_error("gemm_bf16: act_grad needs aux_in");
-  const int tiles = ((M + gb::BM - 1) / gb::BM) * ((N + gb::BN - 1) / gb::BN);
+  const int tiles = ((M + 127) / 128) * ((N + gb::BN - 1) / gb::BN);
   const int nkt = K / gb::BK;
   if (splitk <= 0) {  // auto: fill the 256 CUs when the output has few tiles and K is deep
     splitk = 1;
@@ -548,16 +645,15 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   }
   GemmEpi e{alpha, beta, bias, act, (const unsigned short*)aux_in, (unsigned short*)aux_out,
             ld_aux, (const unsigned short*)residual, ld_res, act_grad, colsum, nullptr, 0};
-  const dim3 grid(tiles, splitk, batch);
-  const size_t lds = 2 * gb::BUF_BYTES;
+  const dim3 gyz(1, splitk, batch);
+  const int cfg = choose_cfg(M, N, splitk * batch);
   auto* Au = (const unsigned short*)A;
   auto* Bu = (const unsigned short*)B;
-#define DTFX_GB(TA_, TB_, F_)                                                                 \
-  if (ta == TA_ && tb == TB_ && out_f32 == F_) {                                              \
-    hipLaunchKernelGGL((gemm_bf16_kernel<0, TA_, TB_, F_>), grid, dim3(gb::NT), lds, stream, \
-                       M, N, K, Au, lda, Bu, ldb, C, ldc, e, sA, sB, sC, ConvDesc{});     \
-    DTFX_HIP_CHECK(hipGetLastError());                                                        \
-    return;                                                                                   \
+#define DTFX_GB(TA_, TB_, F_)                                                                  \
+  if (ta == TA_ && tb == TB_ && out_f32 == F_) {                                               \
+    launch_cfg<0, TA_, TB_, F_>(cfg, gyz, M, N, K, Au, lda, Bu, ldb, C, ldc, e, sA, sB, sC,    \
+                                ConvDesc{}, stream);                                           \
+    return;                                                                                    \
   }
   DTFX_GB(false, true, false)
   DTFX_GB(false, true, true)
@@ -572,8 +668,8 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
 
 // Convolution launcher (modes in the ConvDesc comment above).
 //  fwd  : x [N*H*W][C], w [Cout][ldw >= ceil64(KH*KW*C)] (zero-padded), y [N*OH*OW][Cout]
-//         optional fused BatchNorm statistics: colsum / colsq = per-tile partial rows
-//         [2 * ceil(N*OH*OW / 128)][Cout] (f32, fully overwritten)
+//         optional fused BatchNorm statistics: colsum / colsq = per-wave-slab partial rows
+//         [ceil(N*OH*OW / 64)][Cout] (f32, fully overwritten)
 //  dgrad: dy [N*OH*OW][Cout], w [Cout][ldw], dx [N*H*W][C]
 //         (+ residual)
 //  wgrad: dy, x -> dw [Cout][ldw] f32 (first KH*KW*C columns; += when beta == 1)
@@ -586,31 +682,28 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
   if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) & 15)
     throw std::runtime_error("conv_bf16: tensors must be 16-byte aligned");
   ConvDesc d{N, H, W, C, OH, OW, Cout, KH, KW, stride, pad, 0, ldw > 0 ? ldw : KH * KW * C};
-  // fwd statistics go to per-tile partial rows [2 * ceil(M / 128)][Cout] (reduced by
+  // fwd statistics go to partial rows [ceil(M / 64)][Cout] (reduced by
   // colpart_reduce in cnn.hip): thousands of blocks would otherwise serialise on the same
   // Cout addresses (f32 atomics execute at the memory side)
   GemmEpi e{1.f, beta, nullptr, 0, nullptr, nullptr, 0, (const unsigned short*)residual, 0, 0,
             colsum, colsq, mode == 1 ? 1 : 0};
-  const size_t lds = 2 * gb::BUF_BYTES;
   int M, Nn, K;
   if (mode == 1) {
     d.ktot = KH * KW * C;
     M = N * OH * OW; Nn = Cout; K = d.ktot;
     if (ldw < (K + 63) / 64 * 64) throw std::runtime_error("conv_bf16: fwd weights need ld >= ceil64(KH*KW*C)");
     e.ld_res = Cout;
-    const int tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
-    hipLaunchKernelGGL((gemm_bf16_kernel<1, false, true, false>), dim3(tiles, 1, 1), dim3(gb::NT), lds,
-                       stream, M, Nn, K, (const unsigned short*)a, 0, (const unsigned short*)b, ldw,
-                       out, Cout, e, 0LL, 0LL, 0LL, d);
+    launch_cfg<1, false, true, false>(choose_cfg(M, Nn, 1), dim3(1, 1, 1), M, Nn, K,
+                                      (const unsigned short*)a, 0, (const unsigned short*)b, ldw,
+                                      out, Cout, e, 0LL, 0LL, 0LL, d, stream);
   } else if (mode == 2) {
     if (Cout % 64) throw std::runtime_error("conv_bf16: dgrad needs Cout % 64 == 0");
     d.ktot = KH * KW * Cout;
     M = N * H * W; Nn = C; K = d.ktot;
     e.ld_res = C;
-    const int tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
-    hipLaunchKernelGGL((gemm_bf16_kernel<2, false, false, false>), dim3(tiles, 1, 1), dim3(gb::NT),
-                       lds, stream, M, Nn, K, (const unsigned short*)a, 0, (const unsigned short*)b, 0,
-                       out, C, e, 0LL, 0LL, 0LL, d);
+    launch_cfg<2, false, false, false>(choose_cfg(M, Nn, 1), dim3(1, 1, 1), M, Nn, K,
+                                       (const unsigned short*)a, 0, (const unsigned short*)b, 0,
+                                       out, C, e, 0LL, 0LL, 0LL, d, stream);
   } else if (mode == 3) {
     if (residual || colsum || colsq) throw std::runtime_error("conv_bf16: wgrad has no epilogue options");
     M = Cout; Nn = KH * KW * C; K = N * OH * OW;
@@ -627,13 +720,12 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
       if (beta == 0.f)
         DTFX_HIP_CHECK(hipMemset2DAsync(out, sizeof(float) * ldo, 0, sizeof(float) * Nn, M, stream));
     }
-    hipLaunchKernelGGL((gemm_bf16_kernel<3, true, false, true>), dim3(tiles, splitk, 1), dim3(gb::NT),
-                       lds, stream, M, Nn, K, (const unsigned short*)a, Cout,
-                       (const unsigned short*)b, 0, out, ldo, e, 0LL, 0LL, 0LL, d);
+    launch_cfg<3, true, false, true>(choose_cfg(M, Nn, splitk), dim3(1, splitk, 1), M, Nn, K,
+                                     (const unsigned short*)a, Cout, (const unsigned short*)b, 0,
+                                     out, ldo, e, 0LL, 0LL, 0LL, d, stream);
   } else {
     throw std::runtime_error("conv_bf16: mode must be 1 (fwd), 2 (dgrad) or 3 (wgrad)");
   }
-  DTFX_HIP_CHECK(hipGetLastError());
 }
 
 // Column sums of a bf16 matrix (bias gradients): out[n] (+)= sum_m G[m][n], f32.

@@ -58,7 +58,7 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
     y = torch.empty(N, OH, OW, Cout, device=x.device, dtype=BF16)
     ps = pq = None
     if colsum is not None:
-        rows = 2 * ((N * OH * OW + 127) // 128)
+        rows = (N * OH * OW + 63) // 64  # one partial row per 64-row output slab
         part = torch.empty(2, rows, Cout, device=x.device)
         ps, pq = part[0], part[1]
     hip().conv_bf16(1, N, H, W, C, Cout, KH, KW, stride, pad, ptr(x), ptr(w), w.stride(0), ptr(y),
