@@ -54,8 +54,10 @@ def main():
     ap.add_argument("--max_graph_steps", type=int, default=1024,
                     help="max steps per hipGraph (graphs are epoch-aligned)")
     ap.add_argument("--no_graph", action="store_true")
-    ap.add_argument("--comm", choices=["native", "torch"], default="native",
+    ap.add_argument("--comm", choices=["auto", "native", "xgmi", "torch"], default="auto",
                     help="native: the framework's C++ RCCL communicator (gloo control plane); "
+                         "xgmi: one-shot peer-memory all-reduce over xGMI (small buckets); "
+                         "auto (MLP, N>1): verify xgmi against RCCL, time both, use the faster; "
                          "torch: torch.distributed nccl(=RCCL) process group")
     ap.add_argument("--dataset_size", type=int, default=55000)
     ap.add_argument("--dp", action="store_true",
@@ -69,6 +71,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.comm == "auto" and (a.model != "mlp" or world == 1):
+        a.comm = "native"
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             sys.exit("--gpus %d needs torch.distributed.run with %d processes" % (a.gpus, a.gpus))
@@ -77,7 +81,7 @@ def main():
     if world > 1:
         if a.comm == "torch":
             dist.init_process_group("nccl", device_id=dev)
-        else:  # control plane over TCP/gloo; gradients over the native RCCL communicator
+        else:  # control plane over TCP/gloo; gradients over the native RCCL / xGMI communicator
             dist.init_process_group("gloo")
 
     if a.model == "bert":
@@ -94,7 +98,17 @@ def main():
     if world > 1:
         from distributedtensorflowexample_amd.parallel.comm import NativeComm, TorchComm
 
-        comm = NativeComm.from_process_group() if a.comm == "native" else TorchComm()
+        if a.comm == "torch":
+            comm = TorchComm()
+        else:
+            comm = NativeComm.from_process_group()
+            if a.comm in ("xgmi", "auto"):
+                from distributedtensorflowexample_amd.parallel.select import pick_small_allreduce
+                from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+                comm, probe = pick_small_allreduce(comm, a.comm, world, rank, dev)
+                a.comm_probe = probe
+                a.comm = "xgmi" if isinstance(comm, XgmiComm) else "native"
         allreduce = comm.allreduce_sum_
         chk = params.double().sum().reshape(1).cpu()
         ref = chk.clone()
@@ -103,9 +117,15 @@ def main():
             raise RuntimeError("replicas are not identical after init")
 
     if world == 1 and a.dp:  # 1-rank communicator: exercises the sync-DP path on one GPU
-        from distributedtensorflowexample_amd.parallel.comm import NativeComm
+        if a.comm == "xgmi":
+            from distributedtensorflowexample_amd.ops import mlp_step
+            from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
 
-        comm = NativeComm(0, 1, store=dist.HashStore())
+            comm = XgmiComm(0, 1, mlp_step.NPARAM, device=dev, store=dist.HashStore())
+        else:
+            from distributedtensorflowexample_amd.parallel.comm import NativeComm
+
+            comm = NativeComm(0, 1, store=dist.HashStore())
         allreduce = comm.allreduce_sum_
     tr = FusedMLPTrainer(params, x, y, batch_size=a.batch_size, learning_rate=a.learning_rate,
                          allreduce=allreduce, world_size=world,
@@ -128,6 +148,8 @@ def main():
     if barrier:
         barrier()
     elapsed = time.perf_counter() - t0
+    if hasattr(comm if world > 1 else None, "check"):
+        comm.check()  # raises if an xGMI all-reduce ever timed out
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -160,6 +182,7 @@ def main():
                 "comm": a.comm if (world > 1 or a.dp) else "none",
                 "hipgraph": use_graph,
             },
+            "comm_probe_us": getattr(a, "comm_probe", None),
             "final_loss": round(loss, 5),
             "final_train_acc": round(acc, 4),
             "global_step": tr.global_step(),

@@ -1,0 +1,128 @@
+// Host side of the xGMI one-shot all-reduce: IPC-shared uncached slots, peer
+// mapping, launch, error word.  Kernel and protocol: xgmi_allreduce.hip.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "xgmi.h"
+
+namespace py = pybind11;
+
+#define XG_CHECK(expr)                                                                 \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +     \
+                               " in " #expr);                                          \
+  } while (0)
+
+namespace dtfx {
+
+class XgmiAllReduce {
+ public:
+  XgmiAllReduce(int rank, int world, int device, long long max_numel)
+      : rank_(rank), world_(world), device_(device), S_((max_numel + 63) / 64 * 64) {
+    if (world < 1 || world > XG_MAX_WORLD) throw std::runtime_error("xgmi: world must be 1..16");
+    XG_CHECK(hipSetDevice(device));
+    // ONE fine-grained uncached (MTYPE UC) allocation: data slots [2][S] f32 followed by the
+    // flag array.  UC accesses bypass every GPU cache, so neither side needs L2 writeback /
+    // invalidation (a system-scope fence would write back or invalidate the whole L2):
+    // ordering alone (vmcnt waits) makes the protocol correct.  Rounded to 2 MiB.
+    bytes_ = sizeof(float) * 2 * S_ + sizeof(unsigned) * XG_MAX_WORLD * XG_BLOCKS;
+    bytes_ = (bytes_ + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+    XG_CHECK(hipExtMallocWithFlags(&base_, bytes_, hipDeviceMallocUncached));
+    XG_CHECK(hipMemset(base_, 0, bytes_));
+    XG_CHECK(hipMalloc(&epochs_, sizeof(unsigned) * XG_BLOCKS + sizeof(int)));
+    XG_CHECK(hipMemset(epochs_, 0, sizeof(unsigned) * XG_BLOCKS + sizeof(int)));
+    err_ = (int*)(epochs_ + XG_BLOCKS);
+    for (int i = 0; i < XG_MAX_WORLD; ++i) {
+      peers_.data[i] = nullptr;
+      peers_.flags[i] = nullptr;
+    }
+  }
+  ~XgmiAllReduce() { close(); }
+
+  py::bytes handle() {
+    hipIpcMemHandle_t h;
+    XG_CHECK(hipIpcGetMemHandle(&h, base_));
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  }
+
+  void open(const std::vector<std::string>& handles) {
+    if ((int)handles.size() != world_) throw std::runtime_error("xgmi: need one handle per rank");
+    XG_CHECK(hipSetDevice(device_));
+    for (int j = 0; j < world_; ++j) {
+      char* p;
+      if (j == rank_) {
+        p = (char*)base_;
+      } else {
+        hipIpcMemHandle_t h;
+        if (handles[j].size() != sizeof(h)) throw std::runtime_error("xgmi: bad handle size");
+        memcpy(&h, handles[j].data(), sizeof(h));
+        void* q = nullptr;
+        XG_CHECK(hipIpcOpenMemHandle(&q, h, hipIpcMemLazyEnablePeerAccess));
+        opened_.push_back(q);
+        p = (char*)q;
+      }
+      peers_.data[j] = (float*)p;
+      peers_.flags[j] = (unsigned*)(p + sizeof(float) * 2 * S_);
+    }
+    ready_ = true;
+  }
+
+  void all_reduce(uintptr_t g, long long n, uintptr_t stream, double timeout_s) {
+    if (!ready_) throw std::runtime_error("xgmi: open() the peer handles first");
+    if (n > S_) throw std::runtime_error("xgmi: buffer larger than max_numel");
+    if (g & 15) throw std::runtime_error("xgmi: buffer must be 16-byte aligned");
+    const long long ticks = (long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    xgmi_allreduce_launch((float*)g, n, rank_, world_, S_, peers_, epochs_, err_, ticks,
+                          (hipStream_t)stream);
+  }
+
+  int error() {
+    int e = 0;
+    XG_CHECK(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost));
+    return e;
+  }
+
+  void close() {
+    for (void* q : opened_) hipIpcCloseMemHandle(q);
+    opened_.clear();
+    if (base_) hipFree(base_);
+    if (epochs_) hipFree(epochs_);
+    base_ = nullptr;
+    epochs_ = nullptr;
+    ready_ = false;
+  }
+
+ private:
+  int rank_, world_, device_;
+  long long S_;
+  size_t bytes_ = 0;
+  void* base_ = nullptr;
+  unsigned* epochs_ = nullptr;
+  int* err_ = nullptr;
+  XgPeers peers_;
+  std::vector<void*> opened_;
+  bool ready_ = false;
+};
+
+}  // namespace dtfx
+
+void register_xgmi(py::module_& m) {
+  py::class_<dtfx::XgmiAllReduce>(m, "XgmiAllReduce")
+      .def(py::init<int, int, int, long long>(), py::arg("rank"), py::arg("world"),
+           py::arg("device"), py::arg("max_numel"))
+      .def("handle", &dtfx::XgmiAllReduce::handle)
+      .def("open", &dtfx::XgmiAllReduce::open)
+      .def("all_reduce", &dtfx::XgmiAllReduce::all_reduce, py::arg("g"), py::arg("n"),
+           py::arg("stream"), py::arg("timeout_s") = 2.0)
+      .def("error", &dtfx::XgmiAllReduce::error)
+      .def("close", &dtfx::XgmiAllReduce::close);
+}

@@ -45,6 +45,11 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         comm = NativeComm.from_process_group() if world > 1 else None
+        if comm is not None and os.environ.get("DTFX_MLP_COMM", "auto") != "rccl":
+            # the 318 KB gradient is latency bound: xGMI one-shot when verified and faster
+            from ..parallel.select import pick_small_allreduce
+
+            comm, _ = pick_small_allreduce(comm, "auto", world, rank, dev)
     else:
         dev = torch.device("cpu")
         comm = TorchComm() if world > 1 else None

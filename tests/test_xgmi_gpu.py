@@ -1,0 +1,115 @@
+"""xGMI one-shot all-reduce protocol, two processes sharing one GPU (IPC peers).
+
+On the single-GPU test box both ranks live on cuda:0, so the "peer" memory is
+the same device's HBM reached through IPC mappings; the protocol (publish,
+flag, bounded wait, ordered sum, parity slots, device-side epochs, hipGraph
+replay) is exercised end to end.  Cross-device xGMI transport is exercised by
+the 8-GPU driver runs only when selected.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+        n = 79510
+        comm = XgmiComm(rank, world, n, device="cuda:0")
+        ok = True
+        for it in range(5):  # eager calls: values depend on rank and iteration
+            t = torch.arange(n, device="cuda:0", dtype=torch.float32) * (rank + 1) + it
+            comm.allreduce_sum_(t)
+            exp = torch.arange(n, device="cuda:0", dtype=torch.float32) * sum(
+                r + 1 for r in range(world)) + it * world
+            ok &= bool(torch.equal(t, exp))
+        # captured into a graph and replayed: epochs must advance on the device
+        buf = torch.zeros(n, device="cuda:0")
+        s = torch.cuda.Stream()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            buf.fill_(rank + 1.0)
+            comm.allreduce_sum_(buf)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            buf.fill_(rank + 1.0)
+            comm.allreduce_sum_(buf)
+        for _ in range(20):
+            g.replay()
+        torch.cuda.synchronize()
+        ok &= bool((buf == sum(r + 1.0 for r in range(world))).all())
+        comm.check()
+        dist.barrier()
+        comm.destroy()
+        q.put((rank, ok, ""))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, False, repr(e)))
+
+
+def test_xgmi_allreduce_two_ranks_one_gpu(gpu):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    for r, ok, msg in res:
+        assert ok, (r, msg)
+
+
+def _auto_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from distributedtensorflowexample_amd.parallel.select import pick_small_allreduce
+        from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+        # stand-in for RCCL (two ranks cannot share a GPU under RCCL): a second,
+        # independent xGMI communicator -- graph-capturable and exact
+        ref = XgmiComm(rank, world, 79510, device="cuda:0", key="dtfx/xgmi/ref")
+        comm, probe = pick_small_allreduce(ref, "auto", world, rank, torch.device("cuda:0"),
+                                           iters=50)
+        t = torch.full((79510,), float(rank + 1), device="cuda:0")
+        comm.allreduce_sum_(t)
+        torch.cuda.synchronize()
+        q.put((rank, bool((t == 3.0).all()) and probe is not None, str(probe)))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, False, repr(e)))
+
+
+def test_auto_selection_path(gpu):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_auto_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    for r, ok, msg in res:
+        assert ok, (r, msg)
