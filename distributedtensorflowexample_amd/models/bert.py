@@ -301,3 +301,75 @@ def synthetic_mlm_batch(cfg: BertConfig, batch, seq, device, max_pred=None, seed
         labels = torch.cat([labels, torch.full((pad,), -100, dtype=torch.int32)])
     dev = torch.device(device)
     return ids.to(dev), tt.to(dev), flat.to(dev), labels.to(dev), n_valid
+
+
+# ---------------------------------------------------------------------------
+# TF checkpoint naming (google-research/bert layout): kernels [in, out], the
+# fused QKV split into query/key/value, the vocabulary unpadded.
+# ---------------------------------------------------------------------------
+def tf_variables(model: BertMLM):
+    """name -> CPU f32 tensor in the original BERT TF checkpoint layout."""
+    cfg, p = model.cfg, model.params
+    H, V = cfg.hidden, cfg.vocab_size
+    m = lambda n: p.P(n).detach().float().cpu()  # noqa: E731
+    out = {"bert/embeddings/word_embeddings": m("embeddings/word_embeddings")[:V],
+           "bert/embeddings/position_embeddings": m("embeddings/position_embeddings"),
+           "bert/embeddings/token_type_embeddings": m("embeddings/token_type_embeddings"),
+           "bert/embeddings/LayerNorm/gamma": m("embeddings/LayerNorm/gamma"),
+           "bert/embeddings/LayerNorm/beta": m("embeddings/LayerNorm/beta")}
+    for l in range(cfg.layers):
+        src, dst = "encoder/layer_%d/" % l, "bert/encoder/layer_%d/" % l
+        qkv_w, qkv_b = m(src + "attention/qkv/kernel"), m(src + "attention/qkv/bias")
+        for i, nm in enumerate(("query", "key", "value")):
+            out[dst + "attention/self/%s/kernel" % nm] = qkv_w[i * H:(i + 1) * H].t().contiguous()
+            out[dst + "attention/self/%s/bias" % nm] = qkv_b[i * H:(i + 1) * H].clone()
+        for a, b in (("attention/output/dense", "attention/output/dense"),
+                     ("intermediate/dense", "intermediate/dense"), ("output/dense", "output/dense")):
+            out[dst + b + "/kernel"] = m(src + a + "/kernel").t().contiguous()
+            out[dst + b + "/bias"] = m(src + a + "/bias")
+        for ln in ("attention/output/LayerNorm", "output/LayerNorm"):
+            out[dst + ln + "/gamma"] = m(src + ln + "/gamma")
+            out[dst + ln + "/beta"] = m(src + ln + "/beta")
+    out["cls/predictions/transform/dense/kernel"] = \
+        m("cls/predictions/transform/dense/kernel").t().contiguous()
+    out["cls/predictions/transform/dense/bias"] = m("cls/predictions/transform/dense/bias")
+    out["cls/predictions/transform/LayerNorm/gamma"] = m("cls/predictions/transform/LayerNorm/gamma")
+    out["cls/predictions/transform/LayerNorm/beta"] = m("cls/predictions/transform/LayerNorm/beta")
+    out["cls/predictions/output_bias"] = m("cls/predictions/output_bias")[:V]
+    return out
+
+
+def load_tf_variables(model: BertMLM, values):
+    """Inverse of :func:`tf_variables`; refreshes the bf16 working copy."""
+    cfg, p = model.cfg, model.params
+    H, V = cfg.hidden, cfg.vocab_size
+
+    def put(name, t):
+        dst = p.P(name)
+        dst.copy_(torch.as_tensor(t, dtype=torch.float32).reshape(dst.shape).to(dst.device))
+
+    w = p.P("embeddings/word_embeddings")
+    w[:V].copy_(torch.as_tensor(values["bert/embeddings/word_embeddings"]).to(w.device))
+    for n in ("position_embeddings", "token_type_embeddings", "LayerNorm/gamma", "LayerNorm/beta"):
+        put("embeddings/" + n, values["bert/embeddings/" + n])
+    for l in range(cfg.layers):
+        src, dst = "encoder/layer_%d/" % l, "bert/encoder/layer_%d/" % l
+        qkv_w = torch.cat([torch.as_tensor(values[dst + "attention/self/%s/kernel" % nm]).t()
+                           for nm in ("query", "key", "value")], 0)
+        qkv_b = torch.cat([torch.as_tensor(values[dst + "attention/self/%s/bias" % nm])
+                           for nm in ("query", "key", "value")], 0)
+        put(src + "attention/qkv/kernel", qkv_w)
+        put(src + "attention/qkv/bias", qkv_b)
+        for a in ("attention/output/dense", "intermediate/dense", "output/dense"):
+            put(src + a + "/kernel", torch.as_tensor(values[dst + a + "/kernel"]).t())
+            put(src + a + "/bias", values[dst + a + "/bias"])
+        for ln in ("attention/output/LayerNorm", "output/LayerNorm"):
+            put(src + ln + "/gamma", values[dst + ln + "/gamma"])
+            put(src + ln + "/beta", values[dst + ln + "/beta"])
+    put("cls/predictions/transform/dense/kernel",
+        torch.as_tensor(values["cls/predictions/transform/dense/kernel"]).t())
+    for n in ("transform/dense/bias", "transform/LayerNorm/gamma", "transform/LayerNorm/beta"):
+        put("cls/predictions/" + n, values["cls/predictions/" + n])
+    ob = p.P("cls/predictions/output_bias")
+    ob[:V].copy_(torch.as_tensor(values["cls/predictions/output_bias"]).to(ob.device))
+    TR.cast_bf16(p.master, p.bf)

@@ -87,6 +87,8 @@ class ResNetParams:
                 tmp = torch.empty(shape[0] * k_real, device=dev)
                 I.fill_(tmp, "normal", 0.0, math.sqrt(2.0 / kind[2]), seed=seed, offset=i << 40)
                 t[:, :k_real] = tmp.view(shape[0], k_real)
+                if name == "conv1.weight":  # pad input channels 3..7 carry no weight
+                    t[:, :k_real].view(shape[0], -1, IN_CH)[:, :, 3:] = 0
             elif isinstance(kind, tuple) and kind[0] == "normal":
                 I.fill_(t.view(-1), "normal", 0.0, kind[1], seed=seed, offset=i << 40)
                 t[num_classes:].zero_()
@@ -249,3 +251,51 @@ def synthetic_imagenet(batch, device, size=224, seed=0, num_classes=NUM_CLASSES)
     x[..., :3] = torch.randn(batch, size, size, 3, generator=g)
     y = torch.randint(0, num_classes, (batch,), generator=g, dtype=torch.int32)
     return x.to(BF16).to(device), y.to(device)
+
+
+# ---------------------------------------------------------------------------
+# Checkpoint naming: TF conv kernels HWIO [KH, KW, Cin, Cout] (real input
+# channels only), BatchNorm gamma/beta/moving_mean/moving_variance, dense
+# kernel [in, out].
+# ---------------------------------------------------------------------------
+def tf_variables(model: ResNet50, prefix="resnet50/"):
+    P = model.params
+    out = {}
+    for name, cin, cout, k, s, p in P.convs:
+        w = P.P(name + ".weight").detach().float().cpu()[:, :k * k * cin].reshape(cout, k, k, cin)
+        if name == "conv1":
+            w = w[..., :3]  # the image has 3 channels; 5 zero pad channels are not a parameter
+        out[prefix + name + "/kernel"] = w.permute(1, 2, 3, 0).contiguous()
+        bn = prefix + name + "/bn/"
+        out[bn + "gamma"] = P.P(name + ".bn.gamma").detach().cpu()
+        out[bn + "beta"] = P.P(name + ".bn.beta").detach().cpu()
+        rm, rv = P.running[name]
+        out[bn + "moving_mean"] = rm.detach().cpu()
+        out[bn + "moving_variance"] = rv.detach().cpu()
+    out[prefix + "fc/kernel"] = P.P("fc.weight").detach().cpu()[:P.num_classes].t().contiguous()
+    out[prefix + "fc/bias"] = P.P("fc.bias").detach().cpu()[:P.num_classes]
+    return out
+
+
+def load_tf_variables(model: ResNet50, values, prefix="resnet50/"):
+    P = model.params
+    for name, cin, cout, k, s, p in P.convs:
+        w = torch.as_tensor(values[prefix + name + "/kernel"]).float().permute(3, 0, 1, 2)
+        if name == "conv1":
+            w = torch.cat([w, w.new_zeros(cout, k, k, cin - w.shape[-1])], -1)
+        dst = P.P(name + ".weight")
+        dst.zero_()
+        dst[:, :k * k * cin] = w.reshape(cout, -1).to(dst.device)
+        bn = prefix + name + "/bn/"
+        P.P(name + ".bn.gamma").copy_(torch.as_tensor(values[bn + "gamma"]))
+        P.P(name + ".bn.beta").copy_(torch.as_tensor(values[bn + "beta"]))
+        rm, rv = P.running[name]
+        rm.copy_(torch.as_tensor(values[bn + "moving_mean"]))
+        rv.copy_(torch.as_tensor(values[bn + "moving_variance"]))
+    fw = P.P("fc.weight")
+    fw.zero_()
+    fw[:P.num_classes] = torch.as_tensor(values[prefix + "fc/kernel"]).t().to(fw.device)
+    fb = P.P("fc.bias")
+    fb.zero_()
+    fb[:P.num_classes] = torch.as_tensor(values[prefix + "fc/bias"]).to(fb.device)
+    TR.cast_bf16(P.master, P.bf)
