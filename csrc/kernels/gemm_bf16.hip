@@ -289,17 +289,23 @@ struct GemmEpi {
                                 //    no same-address atomics: BatchNorm statistics of tall convs)
 };
 
-// BM_ = 128 (4 waves, 2 blocks/CU) or 256 (8 waves); NBUF = LDS stages (2: next tile in
-// flight during compute; 3: two tiles in flight, counted vmcnt + raw barrier).
-template <int MODE, bool TA, bool TB, bool OUT_F32, int BM_, int NBUF>
-__global__ __launch_bounds__(BM_ * 2, BM_ == 128 && NBUF == 2 ? 2 : 1) void gemm_bf16_kernel(
+// Tile BM_ x BN_ (128x128: 4 waves of 64x64, 2 blocks/CU; 256x128: 8 waves of 64x64;
+// 256x256: 8 waves of 128x64).  NBUF = LDS stages (2: next tile in flight during
+// compute; 3: two tiles in flight, counted vmcnt + raw barrier).
+template <int MODE, bool TA, bool TB, bool OUT_F32, int BM_, int NBUF, int BN_>
+__global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
+                             BM_ == 128 && NBUF == 2 ? 2 : 1) void gemm_bf16_kernel(
     int M, int N, int K, const unsigned short* __restrict__ A, int lda,
     const unsigned short* __restrict__ B, int ldb, void* __restrict__ Cv, int ldc, GemmEpi e,
     long long sA, long long sB, long long sC, ConvDesc cd) {
   using namespace gb;
-  constexpr int BM = BM_, NW = BM_ / 32;           // waves: (BM/64) x 2
+  constexpr int BM = BM_, BN = BN_;
+  constexpr int WM = BN_ == 256 ? 128 : 64;        // wave tile WM x 64
+  constexpr int NWN = BN / 64, NW = (BM / WM) * NWN;
+  constexpr int TM = WM / 16;                      // 16-row MFMA tiles per wave
+  static_assert(BN_ == 128 || (MODE == 0 || MODE == 1), "gathered B operands need BN = 128");
   constexpr int TILE_A = BM * BK * 2, TILE_B = BN * BK * 2, BUF_BYTES = TILE_A + TILE_B;
-  constexpr int LPT = (BM / 8) / NW + 16 / NW;      // glds per thread per K tile
+  constexpr int LPT = (BM / 8) / NW + (BN / 8) / NW;  // glds per thread per K tile
   // strided batch over blockIdx.z (attention's per-(batch, head) products)
   A += sA * blockIdx.z;
   B += sB * blockIdx.z;
@@ -309,16 +315,16 @@ __global__ __launch_bounds__(BM_ * 2, BM_ == 128 && NBUF == 2 ? 2 : 1) void gemm
   const int bid = xcd_remap(blockIdx.x, tiles_n * tiles_m);
   const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / NWN, wn = wave % NWN;
 
   // Clamp limits for edge tiles: k-contiguous rows clamp to the last row; k-strided
   // column chunks clamp to the last full 8-column chunk (ld % 8 == 0 makes it in-bounds).
   const int a_max = TA ? ((M - 1) & ~7) : M - 1;
   const int b_max = TB ? N - 1 : ((N - 1) & ~7);
 
-  f32x4 acc[4][4];
+  f32x4 acc[TM][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -342,13 +348,13 @@ __global__ __launch_bounds__(BM_ * 2, BM_ == 128 && NBUF == 2 ? 2 : 1) void gemm
     const char* Bt = At + TILE_A;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[TM], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag<!TA, BM>(At, wm * 64 + i * 16, kk, lane);
+      for (int i = 0; i < TM; ++i) af[i] = frag<!TA, BM>(At, wm * WM + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = frag<TB, BN>(Bt, wn * 64 + j * 16, kk, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
@@ -396,22 +402,23 @@ __global__ __launch_bounds__(BM_ * 2, BM_ == 128 && NBUF == 2 ? 2 : 1) void gemm
   float cs[8], cq[8];  // fused column sums / sums of squares of this lane's 8 columns
 #pragma unroll
   for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
+  for (int h = 0; h < WM / 32; ++h) {
+    // static accumulator indices only (a runtime acc[2h+ii] index would put acc in scratch)
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+    for (int t = 0; t < TM; ++t)
+      if ((t >> 1) == h)
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          ep[(ii * 16 + row_l + r) * EP_LD + j * 16 + col_l] = acc[2 * h + ii][j][r];
+          for (int r = 0; r < 4; ++r)
+            ep[((t & 1) * 16 + row_l + r) * EP_LD + j * 16 + col_l] = acc[t][j][r];
     __builtin_amdgcn_wave_barrier();
     if (OUT_F32 && gridDim.y > 1) {
       // split-K partial: alpha only; hardware f32 atomics, one 256-B row segment per
       // wave instruction (lane = column) so each instruction is 4 full 64-B requests
       const int n = n0 + wn * 64 + lane;
       for (int rr = 0; rr < 32; ++rr) {
-        const int m = m0 + wm * 64 + h * 32 + rr;
+        const int m = m0 + wm * WM + h * 32 + rr;
         if (m < M && n < N)
           unsafeAtomicAdd((float*)Cv + (size_t)m * ldc + n, e.alpha * ep[rr * EP_LD + lane]);
       }
@@ -421,7 +428,7 @@ __global__ __launch_bounds__(BM_ * 2, BM_ == 128 && NBUF == 2 ? 2 : 1) void gemm
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
-      const int m = m0 + wm * 64 + h * 32 + rr;
+      const int m = m0 + wm * WM + h * 32 + rr;
       const int n = n0 + wn * 64 + cg;
       float v[8];
       *(f32x4*)&v[0] = *(const f32x4*)&ep[rr * EP_LD + cg];
@@ -530,7 +537,8 @@ __global__ __launch_bounds__(BM_ * 2, BM_ == 128 && NBUF == 2 ? 2 : 1) void gemm
     }
     const int n = n0 + wn * 64 + (lane & 7) * 8;
     if (e.col_partial) {
-      const size_t prow = (size_t)(m0 / 64 + wm) * N;  // one partial row per 64-row wave slab
+      // one partial row per 64-row wave slab (launchers use WM == 64 for partial stats)
+      const size_t prow = (size_t)(m0 / 64 + wm) * N;
       if (lane < 8 && m0 + wm * 64 < M)
 #pragma unroll
         for (int u = 0; u < 8; ++u)
@@ -552,8 +560,9 @@ __global__ __launch_bounds__(BM_ * 2, BM_ == 128 && NBUF == 2 ? 2 : 1) void gemm
 // ---------------------------------------------------------------------------
 // Launch-configuration choice.  cfg 0: 128x128 tile, 4 waves, 2 LDS stages (64 KB, 2 blocks
 // per CU); cfg 1: 256x128, 8 waves, 3 stages (144 KB, counted-vmcnt pipeline); cfg 2:
-// 256x128, 2 stages (96 KB).  Auto: the 256-row tile when it still yields >= 256 blocks
-// (one full wave of the 256 CUs), else 128.  DTFX_GEMM_CFG=0/1/2 forces one (benchmarks).
+// 256x128, 2 stages (96 KB); cfg 3 (plain GEMM only): 256x256, 8 waves of 128x64, 2 stages
+// (128 KB).  Auto: the largest tile that still yields >= 256 blocks (one full wave of the
+// 256 CUs).  DTFX_GEMM_CFG=0..3 forces one (benchmarks).
 // ---------------------------------------------------------------------------
 static int gemm_cfg_env() {
   static int v = -2;
@@ -564,28 +573,36 @@ static int gemm_cfg_env() {
   return v;
 }
 
-static int choose_cfg(int M, int N, int zdim) {
+static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
   const int f = gemm_cfg_env();
-  if (f >= 0 && f <= 2) return f;
+  if (f >= 0 && f <= 3) return f;
+  if (mode == 0 && !ta) {  // the 256x256 tile halves L2 traffic when it still fills the chip
+                           // (measured: 1.10 vs 0.89 PF at 8192^3; A^T operands lose with it)
+    const long long t = (long long)((M + 255) / 256) * ((N + 255) / 256) * zdim;
+    return t >= 256 ? 3 : 0;
+  }
   const long long t256 = (long long)((M + 255) / 256) * ((N + 127) / 128) * zdim;
   return t256 >= 256 ? 1 : 0;
 }
 
-template <int MODE, bool TA, bool TB, bool F, int BM_, int NBUF>
+template <int MODE, bool TA, bool TB, bool F, int BM_, int NBUF, int BN_ = 128>
 static void launch_one(dim3 grid_yz, int M, int N, int K, const unsigned short* A, int lda,
                        const unsigned short* B, int ldb, void* C, int ldc, const GemmEpi& e,
                        long long sA, long long sB, long long sC, const ConvDesc& d,
                        hipStream_t stream) {
-  constexpr size_t lds = (size_t)NBUF * (BM_ * gb::BK * 2 + gb::BN * gb::BK * 2);
+  constexpr size_t lds = (size_t)NBUF * (BM_ * gb::BK * 2 + BN_ * gb::BK * 2);
+  constexpr int threads = (BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64;
   static bool attr = false;
   if (!attr) {
-    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    DTFX_HIP_CHECK(hipFuncSetAttribute(
+        (const void*)gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF, BN_>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  const int tiles = ((M + BM_ - 1) / BM_) * ((N + gb::BN - 1) / gb::BN);
-  hipLaunchKernelGGL((gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF>), dim3(tiles, grid_yz.y, grid_yz.z),
-                     dim3(BM_ * 2), lds, stream, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC, d);
+  const int tiles = ((M + BM_ - 1) / BM_) * ((N + BN_ - 1) / BN_);
+  hipLaunchKernelGGL((gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF, BN_>),
+                     dim3(tiles, grid_yz.y, grid_yz.z), dim3(threads), lds, stream, M, N, K, A, lda,
+                     B, ldb, C, ldc, e, sA, sB, sC, d);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
@@ -594,6 +611,13 @@ static void launch_cfg(int cfg, dim3 grid_yz, int M, int N, int K, const unsigne
                        const unsigned short* B, int ldb, void* C, int ldc, const GemmEpi& e,
                        long long sA, long long sB, long long sC, const ConvDesc& d,
                        hipStream_t stream) {
+  if constexpr (MODE == 0) {
+    if (cfg == 3) {
+      launch_one<MODE, TA, TB, F, 256, 2, 256>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
+                                               d, stream);
+      return;
+    }
+  }
   if (cfg == 1)
     launch_one<MODE, TA, TB, F, 256, 3>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC, d, stream);
   else if (cfg == 2)
@@ -646,7 +670,7 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   GemmEpi e{alpha, beta, bias, act, (const unsigned short*)aux_in, (unsigned short*)aux_out,
             ld_aux, (const unsigned short*)residual, ld_res, act_grad, colsum, nullptr, 0};
   const dim3 gyz(1, splitk, batch);
-  const int cfg = choose_cfg(M, N, splitk * batch);
+  const int cfg = choose_cfg(M, N, splitk * batch, 0, ta);
   auto* Au = (const unsigned short*)A;
   auto* Bu = (const unsigned short*)B;
 #define DTFX_GB(TA_, TB_, F_)                                                                  \
@@ -693,7 +717,7 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
     M = N * OH * OW; Nn = Cout; K = d.ktot;
     if (ldw < (K + 63) / 64 * 64) throw std::runtime_error("conv_bf16: fwd weights need ld >= ceil64(KH*KW*C)");
     e.ld_res = Cout;
-    launch_cfg<1, false, true, false>(choose_cfg(M, Nn, 1), dim3(1, 1, 1), M, Nn, K,
+    launch_cfg<1, false, true, false>(choose_cfg(M, Nn, 1, 1), dim3(1, 1, 1), M, Nn, K,
                                       (const unsigned short*)a, 0, (const unsigned short*)b, ldw,
                                       out, Cout, e, 0LL, 0LL, 0LL, d, stream);
   } else if (mode == 2) {
@@ -701,7 +725,7 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
     d.ktot = KH * KW * Cout;
     M = N * H * W; Nn = C; K = d.ktot;
     e.ld_res = C;
-    launch_cfg<2, false, false, false>(choose_cfg(M, Nn, 1), dim3(1, 1, 1), M, Nn, K,
+    launch_cfg<2, false, false, false>(choose_cfg(M, Nn, 1, 2), dim3(1, 1, 1), M, Nn, K,
                                        (const unsigned short*)a, 0, (const unsigned short*)b, 0,
                                        out, C, e, 0LL, 0LL, 0LL, d, stream);
   } else if (mode == 3) {
@@ -720,7 +744,7 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
       if (beta == 0.f)
         DTFX_HIP_CHECK(hipMemset2DAsync(out, sizeof(float) * ldo, 0, sizeof(float) * Nn, M, stream));
     }
-    launch_cfg<3, true, false, true>(choose_cfg(M, Nn, splitk), dim3(1, splitk, 1), M, Nn, K,
+    launch_cfg<3, true, false, true>(choose_cfg(M, Nn, splitk, 3), dim3(1, splitk, 1), M, Nn, K,
                                      (const unsigned short*)a, Cout, (const unsigned short*)b, 0,
                                      out, ldo, e, 0LL, 0LL, 0LL, d, stream);
   } else {
