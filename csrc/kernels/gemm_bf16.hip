@@ -576,10 +576,10 @@ static int gemm_cfg_env() {
 static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
   const int f = gemm_cfg_env();
   if (f >= 0 && f <= 3) return f;
-  if (mode == 0 && !ta) {  // the 256x256 tile halves L2 traffic when it still fills the chip
-                           // (measured: 1.10 vs 0.89 PF at 8192^3; A^T operands lose with it)
+  if (mode == 0) {  // the 256x256 tile halves L2 traffic when it still fills the chip
+                    // (measured: 1.10 vs 0.89 PF at 8192^3); A^T operands stay on 128x128
     const long long t = (long long)((M + 255) / 256) * ((N + 255) / 256) * zdim;
-    return t >= 256 ? 3 : 0;
+    return (!ta && t >= 256) ? 3 : 0;
   }
   const long long t256 = (long long)((M + 255) / 256) * ((N + 127) / 128) * zdim;
   return t256 >= 256 ? 1 : 0;
