@@ -44,7 +44,7 @@ def main():
                          "BERT-base MLM config")
     ap.add_argument("--steps", type=int, default=None, help="default 20000 (mlp) / 30 (bert)")
     ap.add_argument("--warmup", type=int, default=None, help="default 2000 (mlp) / 5 (bert)")
-    ap.add_argument("--bert_batch", type=int, default=64, help="BERT sequences per GPU")
+    ap.add_argument("--bert_batch", type=int, default=128, help="BERT sequences per GPU")
     ap.add_argument("--seq_len", type=int, default=128)
     ap.add_argument("--bert_config", choices=["base", "tiny"], default="base")
     ap.add_argument("--resnet_batch", type=int, default=256, help="ResNet-50 images per GPU")
