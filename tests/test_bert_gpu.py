@@ -32,8 +32,12 @@ def test_bert_trainer_graph_replay_matches_eager(gpu):
     b = BertTrainer(cfg, 4, 128, gpu, lr=1e-3)
     a.run(4, use_graph=False)
     b.run(4, use_graph=True)
-    # atomics (LayerNorm/embedding grads) make the two runs differ in the last bits only
-    assert torch.allclose(a.model.params.master, b.model.params.master, atol=2e-5)
+    # f32 atomics (LayerNorm / embedding / split-K gradients) make the runs differ in the
+    # last bits of some gradients; Adam normalises by sqrt(v), so a parameter whose gradient
+    # is ~0 can move by up to lr per step either way.  Require bulk agreement + bounded tail.
+    d = (a.model.params.master - b.model.params.master).abs()
+    assert (d <= 2e-5).float().mean() > 0.999
+    assert d.max() <= 4 * 1e-3 * 1.01
     assert a.step_count == b.step_count == 4
     la, _ = a.stats()
     lb, _ = b.stats()
