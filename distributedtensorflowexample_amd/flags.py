@@ -185,4 +185,12 @@ def define_reference_flags(flag_values=FLAGS):
     DEFINE_float("save_summaries_secs", 30.0, "Chief step-rate summary interval", fv)
     DEFINE_boolean("use_locking", False, "Serialize PS updates per variable", fv)
     DEFINE_integer("seed", 0, "Parameter init seed", fv)
+    DEFINE_string("model", "mlp", "mlp (the reference) | bert | resnet50 (north-star configs)", fv)
+    DEFINE_string("model_config", "base", "base | tiny (tiny = CPU-sized variant of bert/resnet50)",
+                  fv)
+    DEFINE_integer("seq_len", 128, "BERT sequence length", fv)
+    DEFINE_integer("image_size", 224, "ResNet input resolution", fv)
+    DEFINE_string("dtype", "auto", "auto: fp32 for the MLP (reference dtype), bf16 for bert/resnet50",
+                  fv)
+    DEFINE_float("bucket_mb", 32.0, "All-reduce bucket size for generic DDP models (MiB)", fv)
     return fv

@@ -1,0 +1,119 @@
+"""``main.py --strategy mirrored --model {bert,resnet50}``: the north-star models under
+the same CLI, observability and fault-tolerance contract as the reference's MLP.
+
+* one process per GPU (``torch.distributed.run``; gloo control plane, RCCL data);
+* the chief's :class:`~..train.supervisor.Supervisor` restores the latest TF-V2
+  checkpoint from ``--logdir`` (or initialises) and saves every
+  ``--save_model_secs`` (variables in the TF layout of ``models.bert.tf_variables``
+  / ``models.resnet.tf_variables`` + ``global_step``); the other ranks receive the
+  chief's parameters by broadcast, so a killed job resumes where its last checkpoint
+  left off (``tests/test_fault_resume.py``);
+* ``step: N | cost: C | speed: S step/sec`` every ``--log_every`` steps (worker.py:145-146),
+  TensorBoard loss/accuracy scalars into ``<logdir>_<rank>``.
+
+The reference has no such models (it trains an MLP, worker.py:47-79); the
+contract mirrors worker.py:98-159.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..parallel.comm import NativeComm, TorchComm
+from ..utils.summary import FileWriter
+from .saver import FastSaver
+from .supervisor import Supervisor
+
+
+def _dist_env():
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def train_model_mirrored(flags, log=print):
+    rank, world, local = _dist_env()
+    use_gpu = torch.cuda.is_available() and flags.device != "cpu"
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group("gloo")
+    if use_gpu:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        comm = NativeComm.from_process_group() if world > 1 else None
+    else:
+        dev = torch.device("cpu")
+        comm = TorchComm() if world > 1 else None
+    is_chief = rank == 0
+    tiny = flags.model_config == "tiny"
+    if flags.model == "bert":
+        from ..models import bert as M
+        from .bert_trainer import BertTrainer
+
+        cfg = M.BertConfig.tiny() if tiny else M.BertConfig.base()
+        tr = BertTrainer(cfg, flags.batch_size, flags.seq_len, dev, comm=comm,
+                         lr=flags.learning_rate, seed=flags.seed, data_seed=17 + rank)
+    elif flags.model == "resnet50":
+        from ..models import resnet as M
+        from .resnet_trainer import ResNetTrainer
+
+        stages = [(8, 1, 1), (16, 1, 2)] if tiny else M.STAGES
+        ncls = 10 if tiny else 1000
+        tr = ResNetTrainer(flags.batch_size, dev, comm=comm, lr=flags.learning_rate,
+                           seed=flags.seed, image_size=32 if tiny else flags.image_size,
+                           stages=stages, num_classes=ncls, data_seed=rank)
+    else:
+        raise ValueError("--model must be bert or resnet50 here (mlp: train_mirrored)")
+    model = tr.model
+    state = {"step": 0}
+
+    def global_step():
+        return state["step"]
+
+    def save_vars():
+        v = M.tf_variables(model)
+        v["global_step"] = torch.tensor(global_step(), dtype=torch.int64)
+        return v
+
+    def restore(values):
+        M.load_tf_variables(model, values)
+        state["step"] = int(values["global_step"])
+
+    saver = FastSaver(assign=restore)
+    writer = FileWriter("%s_%d" % (flags.logdir, rank)) if flags.logdir else None
+    sv = Supervisor(is_chief=is_chief, logdir=flags.logdir if is_chief else None,
+                    saver=saver if is_chief else None, summary_writer=writer,
+                    global_step=global_step, save_model_secs=flags.save_model_secs,
+                    save_summaries_secs=flags.save_summaries_secs, save_variables=save_vars)
+    steps_total = int(flags.training_steps)
+    with sv.managed_session():
+        if is_chief and sv.restored_from is not None:
+            log("Restored %s (global_step %d)" % (sv.restored_from, global_step()))
+        if world > 1:  # every replica starts from the chief's parameters and step
+            p = model.params.master
+            comm.broadcast_(p, 0)
+            from ..ops import transformer as TR
+
+            TR.cast_bf16(p, model.params.bf)
+            s = torch.tensor([global_step()], dtype=torch.int64)
+            dist.broadcast(s, 0)
+            state["step"] = int(s.item())
+        use_graph = use_gpu
+        t0, s0 = time.time(), global_step()
+        while not sv.should_stop() and global_step() < steps_total:
+            tr.step(use_graph)
+            state["step"] += 1
+            step = global_step()
+            if step % int(flags.log_every) == 0 or step == steps_total:
+                loss, acc = tr.stats()
+                if writer is not None:
+                    writer.add_scalars({"loss": loss, "accuracy": acc}, step)
+                if is_chief:
+                    el = time.time() - t0
+                    log("step: {}\t| cost: {}\t| speed: {}step/sec".format(
+                        step, loss, float((step - s0) / max(el, 1e-9))))
+                    t0, s0 = time.time(), step
+        if is_chief:
+            sv.save_checkpoint()
+    return global_step()

@@ -1,0 +1,53 @@
+"""Fault injection: SIGKILL a training job mid-run, restart it, it resumes from the last
+checkpoint (chief restore-or-init + time-based checkpoints)."""
+import os
+import signal
+import subprocess
+import sys
+import time
+
+import pytest
+
+from distributedtensorflowexample_amd.train.saver import latest_checkpoint, load_checkpoint
+
+pytestmark = pytest.mark.slow
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, log):
+    return subprocess.Popen([sys.executable, os.path.join(ROOT, "main.py")] + args,
+                            stdout=open(log, "w"), stderr=subprocess.STDOUT, cwd=ROOT,
+                            env=dict(os.environ, HIP_VISIBLE_DEVICES=""))
+
+
+@pytest.mark.parametrize("model,step_key", [("mlp", "global/global_step"),
+                                            ("bert", "global_step")])
+def test_kill_and_resume(tmp_path, model, step_key):
+    logdir = str(tmp_path / "run")
+    common = ["--strategy", "mirrored", "--device", "cpu", "--logdir", logdir,
+              "--save_model_secs", "0.3", "--log_every", "10", "--eval_every", "100000"]
+    if model == "bert":
+        args = common + ["--model", "bert", "--model_config", "tiny", "--batch_size", "2",
+                         "--seq_len", "32", "--training_steps", "200"]
+    else:
+        args = common + ["--training_steps", "8000", "--learning_rate", "0.01"]
+    p = _run(args, str(tmp_path / "a.log"))
+    killed_at = None
+    t0 = time.time()
+    while time.time() - t0 < 120:
+        ck = latest_checkpoint(logdir)
+        if ck and int(load_checkpoint(ck)[step_key]) > 0:
+            killed_at = int(load_checkpoint(ck)[step_key])
+            break
+        time.sleep(0.2)
+    p.send_signal(signal.SIGKILL)
+    p.wait(30)
+    assert killed_at is not None, open(str(tmp_path / "a.log")).read()[-2000:]
+    q = _run(args, str(tmp_path / "b.log"))
+    assert q.wait(300) == 0, open(str(tmp_path / "b.log")).read()[-2000:]
+    final = int(load_checkpoint(latest_checkpoint(logdir))[step_key])
+    assert final == int(args[args.index("--training_steps") + 1])
+    log_b = open(str(tmp_path / "b.log")).read()
+    # the restarted job continued from the checkpoint instead of step 0
+    first = [int(l.split()[1]) for l in log_b.splitlines() if l.startswith("step: ")]
+    assert first and first[0] > killed_at - 1, (killed_at, first[:3])
