@@ -44,6 +44,10 @@ void adam_mixed_launch(long long, float*, const float*, float*, float*, void*, f
                        float, float, float, const int*, int, hipStream_t);
 void cast_f32_bf16_launch(long long, const float*, void*, hipStream_t);
 void act_grad_bf16_launch(long long, int, const void*, const void*, void*, hipStream_t);
+void flash_fwd_launch(int, int, int, const void*, void*, float*, int, const float*, float,
+                      hipStream_t);
+void flash_bwd_launch(int, int, int, const void*, const void*, const void*, const float*, int,
+                      const float*, float, void*, float*, float*, hipStream_t);
 void mlm_xent_launch(int, int, const float*, int, const int*, float, float*, float*, void*, int,
                      hipStream_t);
 }  // namespace dtfx
@@ -182,5 +186,17 @@ void register_nn(py::module_& m) {
                                  float lr, float mu, float wd, float gscale, uintptr_t s) {
     dtfx::sgd_momentum_mixed_launch(n, P<float>(p), P<const float>(g), P<float>(v), P<void>(pb), lr,
                                     mu, wd, gscale, S(s));
+  });
+  m.def("flash_fwd", [](int Bn, int Sq, int nh, uintptr_t qkv, uintptr_t out, uintptr_t lse,
+                        int ld_lse, uintptr_t kmask, float scale, uintptr_t s) {
+    dtfx::flash_fwd_launch(Bn, Sq, nh, P<const void>(qkv), P<void>(out), P<float>(lse), ld_lse,
+                           P<const float>(kmask), scale, S(s));
+  });
+  m.def("flash_bwd", [](int Bn, int Sq, int nh, uintptr_t qkv, uintptr_t o, uintptr_t dout,
+                        uintptr_t lse, int ld_lse, uintptr_t kmask, float scale, uintptr_t dqkv,
+                        uintptr_t dbias, uintptr_t scratch, uintptr_t s) {
+    dtfx::flash_bwd_launch(Bn, Sq, nh, P<const void>(qkv), P<const void>(o), P<const void>(dout),
+                           P<const float>(lse), ld_lse, P<const float>(kmask), scale, P<void>(dqkv),
+                           P<float>(dbias), P<float>(scratch), S(s));
   });
 }

@@ -12,6 +12,7 @@ head-major inside each third).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -127,8 +128,19 @@ def _split(qkv, batch, seq, nh):
     return q, k, v  # [B, nh, S, d]
 
 
+def _use_flash(seq):
+    """S <= 128: whole (sequence, head) in one workgroup's LDS (attn_*_kernel); longer
+    sequences: flash-style tiles (flash_attn.hip).  DTFX_ATTN=flash forces the latter."""
+    return seq > 128 or os.environ.get("DTFX_ATTN") == "flash"
+
+
+def lse_ld(seq):
+    return max(128, (seq + 63) // 64 * 64)
+
+
 def attn_fwd(qkv, batch, seq, nh, kmask=None, scale=None):
-    """softmax(Q K^T * scale + kmask) V per (sequence, head); returns (out [T, nh*64], lse)."""
+    """softmax(Q K^T * scale + kmask) V per (sequence, head); returns (out [T, nh*64], lse)
+    with lse f32 [batch * nh, lse_ld(seq)]."""
     scale = 1.0 / math.sqrt(64) if scale is None else scale
     if not qkv.is_cuda:
         q, k, v = _split(qkv, batch, seq, nh)
@@ -136,15 +148,20 @@ def attn_fwd(qkv, batch, seq, nh, kmask=None, scale=None):
         if kmask is not None:
             s = s + kmask.view(batch, 1, 1, seq)
         lse = torch.logsumexp(s, -1)
+        lse = torch.nn.functional.pad(lse, (0, lse_ld(seq) - seq)).reshape(batch * nh, -1)
         p = torch.softmax(s, -1).to(BF16).float()
         o = (p @ v).permute(0, 2, 1, 3).reshape(batch * seq, nh * 64).to(BF16)
         return o, lse
     _contig(qkv, "qkv", BF16)
     _contig(kmask, "kmask", torch.float32)
     out = torch.empty(batch * seq, nh * 64, device=qkv.device, dtype=BF16)
-    lse = torch.empty(batch * nh, 128, device=qkv.device)
-    hip().attn_fwd(batch, seq, nh, ptr(qkv), ptr(out), ptr(lse), ptr(kmask), float(scale),
-                   stream_handle())
+    lse = torch.empty(batch * nh, lse_ld(seq), device=qkv.device)
+    if _use_flash(seq):
+        hip().flash_fwd(batch, seq, nh, ptr(qkv), ptr(out), ptr(lse), lse.shape[1], ptr(kmask),
+                        float(scale), stream_handle())
+    else:
+        hip().attn_fwd(batch, seq, nh, ptr(qkv), ptr(out), ptr(lse), ptr(kmask), float(scale),
+                       stream_handle())
     return out, lse
 
 
@@ -175,8 +192,14 @@ def attn_bwd(qkv, o, dout, lse, batch, seq, nh, kmask=None, scale=None, dbias=No
     for t, n in ((qkv, "qkv"), (o, "o"), (dout, "dout")):
         _contig(t, n, BF16)
     dqkv = torch.empty_like(qkv)
-    hip().attn_bwd(batch, seq, nh, ptr(qkv), ptr(o), ptr(dout), ptr(lse), ptr(kmask), float(scale),
-                   ptr(dqkv), ptr(dbias), stream_handle())
+    if _use_flash(seq):
+        scratch = torch.empty_like(lse)
+        hip().flash_bwd(batch, seq, nh, ptr(qkv), ptr(o), ptr(dout), ptr(lse), lse.shape[1],
+                        ptr(kmask), float(scale), ptr(dqkv), ptr(dbias), ptr(scratch),
+                        stream_handle())
+    else:
+        hip().attn_bwd(batch, seq, nh, ptr(qkv), ptr(o), ptr(dout), ptr(lse), ptr(kmask),
+                       float(scale), ptr(dqkv), ptr(dbias), stream_handle())
     return dqkv
 
 
