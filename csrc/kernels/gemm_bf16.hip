@@ -650,9 +650,12 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
     throw std::runtime_error("gemm_bf16: residual must be 16-byte aligned with ld_res % 8 == 0");
   if (bias && ((uintptr_t)bias & 15)) throw std::runtime_error("gemm_bf16: bias must be 16-byte aligned");
   if (act_grad && !aux_in) throw std::runtime_error("gemm_bf16: act_grad needs aux_in");
-  const int tiles = ((M + 127) / 128) * ((N + gb::BN - 1) / gb::BN);
   const int nkt = K / gb::BK;
-  if (splitk <= 0) {  // auto: fill the 256 CUs when the output has few tiles and K is deep
+  const bool auto_split = splitk <= 0;
+  const int cfg = choose_cfg(M, N, batch * (auto_split ? 1 : splitk), 0, ta);
+  const int bm = cfg == 0 ? 128 : 256, bn = cfg == 3 ? 256 : 128;
+  const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  if (auto_split) {  // fill the 256 CUs when the output has few tiles and K is deep
     splitk = 1;
     if (batch == 1 && out_f32 && !colsum && !bias && !act && !act_grad && !residual && !aux_out && (beta == 0.f || beta == 1.f))
       while (tiles * splitk < 256 && nkt / (splitk * 2) >= 8) splitk *= 2;
@@ -670,7 +673,6 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   GemmEpi e{alpha, beta, bias, act, (const unsigned short*)aux_in, (unsigned short*)aux_out,
             ld_aux, (const unsigned short*)residual, ld_res, act_grad, colsum, nullptr, 0};
   const dim3 gyz(1, splitk, batch);
-  const int cfg = choose_cfg(M, N, splitk * batch, 0, ta);
   auto* Au = (const unsigned short*)A;
   auto* Bu = (const unsigned short*)B;
 #define DTFX_GB(TA_, TB_, F_)                                                                  \

@@ -38,8 +38,13 @@ def main():
         b = torch.randn(*((N, K) if tb else (K, N)), device=dev).to(torch.bfloat16)
         A = a.t() if ta else a
         B = b.t() if tb else b
-        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        t_ours = timeit(lambda: bf16.gemm(a, b, ta, tb, out=out))
+        if ta:  # weight gradients accumulate into f32 master-gradient buffers (split-K path)
+            out = torch.zeros(M, N, device=dev, dtype=torch.float32)
+            t_ours = timeit(lambda: bf16.gemm(a, b, ta, tb, out=out, beta=1.0))
+            out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        else:
+            out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            t_ours = timeit(lambda: bf16.gemm(a, b, ta, tb, out=out))
         t_lib = timeit(lambda: torch.matmul(A, B, out=out))
         fl = 2.0 * M * N * K
         err = (bf16.gemm(a, b, ta, tb, out_dtype=torch.float32) - A.float() @ B.float()).abs().max()
