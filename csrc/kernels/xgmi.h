@@ -17,4 +17,7 @@ void xgmi_allreduce_launch(float* g, long long n, int rank, int world, long long
                            const XgPeers& peers, unsigned* epochs, int* err, long long ticks,
                            hipStream_t stream);
 
+void xgmi_ll_launch(float* g, long long n, int rank, int world, long long S, const XgPeers& peers,
+                    unsigned* epochs, int* err, long long ticks, hipStream_t stream);
+
 }  // namespace dtfx

@@ -95,6 +95,83 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
   if (t == 0) epochs[b] = epoch;
 }
 
+// ---------------------------------------------------------------------------
+// LL ("low-latency") variant: every element travels as ONE 8-byte word {f32 value,
+// u32 epoch}, so the data carries its own ready flag -- no store-acknowledge wait,
+// no separate flag round trip.  Readers load the W peers' words of an element
+// together and re-poll only the ones whose epoch is not yet current.  Slots are
+// u64 [2][S], parity by epoch as in the flag protocol (same overwrite argument).
+// ---------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(256) void xgmi_ll_kernel(float* __restrict__ g, long long n, int rank,
+                                                      long long S, XgPeers peers,
+                                                      unsigned* __restrict__ epochs,
+                                                      int* __restrict__ err, long long timeout_ticks) {
+  __shared__ unsigned s_epoch;
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (t == 0) s_epoch = epochs[b] + 1;
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  const long long par = (long long)(epoch & 1u) * S;
+  const long long per = (n + gridDim.x - 1) / gridDim.x;
+  const long long lo = b * per, hi = min(n, lo + per);
+  unsigned long long* mine = (unsigned long long*)peers.data[rank] + par;
+  for (long long i = lo + t; i < hi; i += blockDim.x)
+    __hip_atomic_store(mine + i, ((unsigned long long)epoch << 32) | __float_as_uint(g[i]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  bool fail = false;
+  for (long long i = lo + t; i < hi; i += blockDim.x) {
+    unsigned long long w[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j)
+      w[j] = j == rank ? 0ull
+                       : __hip_atomic_load((unsigned long long*)peers.data[j] + par + i,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      bool ready = true;
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+        if (j != rank && (unsigned)(w[j] >> 32) != epoch) {
+          ready = false;
+          w[j] = __hip_atomic_load((unsigned long long*)peers.data[j] + par + i, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      if (ready) break;
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+        fail = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (fail) break;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc += j == rank ? g[i] : __uint_as_float((unsigned)w[j]);
+    g[i] = acc;
+  }
+  if (fail) atomicExch(err, 1);
+  __syncthreads();
+  if (t == 0) epochs[b] = epoch;
+}
+
+void xgmi_ll_launch(float* g, long long n, int rank, int world, long long S, const XgPeers& peers,
+                    unsigned* epochs, int* err, long long ticks, hipStream_t stream) {
+  const dim3 grid(XG_BLOCKS), block(256);
+  switch (world) {
+#define DTFX_LL(WW)                                                                            \
+  case WW:                                                                                     \
+    hipLaunchKernelGGL(xgmi_ll_kernel<WW>, grid, block, 0, stream, g, n, rank, S, peers, epochs, \
+                       err, ticks);                                                            \
+    break;
+    DTFX_LL(1) DTFX_LL(2) DTFX_LL(3) DTFX_LL(4) DTFX_LL(5) DTFX_LL(6) DTFX_LL(7) DTFX_LL(8)
+#undef DTFX_LL
+    default:
+      throw std::runtime_error("xgmi LL protocol: world must be <= 8");
+  }
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
 void xgmi_allreduce_launch(float* g, long long n, int rank, int world, long long S,
                            const XgPeers& peers, unsigned* epochs, int* err, long long ticks,
                            hipStream_t stream) {

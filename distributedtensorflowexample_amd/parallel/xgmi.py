@@ -19,13 +19,17 @@ from ..ops import hip
 
 class XgmiComm:
     def __init__(self, rank, world_size, max_numel, device=None, store=None,
-                 key="dtfx/xgmi/0", timeout_s=2.0):
+                 key="dtfx/xgmi/0", timeout_s=2.0, protocol=None):
         self.rank, self.world_size = int(rank), int(world_size)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None
                                    else torch.device(device).index)
         self.timeout_s = float(timeout_s)
         self.max_numel = int(max_numel)
-        self._h = hip().XgmiAllReduce(self.rank, self.world_size, self.device.index, self.max_numel)
+        # "ll": 8-byte {value, epoch} words (no flag round trip; world <= 8); "flag": slots +
+        # per-block epoch flags (any world <= 16)
+        self.protocol = protocol or ("ll" if self.world_size <= 8 else "flag")
+        self._h = hip().XgmiAllReduce(self.rank, self.world_size, self.device.index,
+                                      self.max_numel, self.protocol)
         if store is None:
             store = dist.distributed_c10d._get_default_store()
         store.set("%s/%d" % (key, self.rank), self._h.handle())

@@ -23,7 +23,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, protocol="ll"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -31,7 +31,7 @@ def _worker(rank, world, port, q):
         from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
 
         n = 79510
-        comm = XgmiComm(rank, world, n, device="cuda:0")
+        comm = XgmiComm(rank, world, n, device="cuda:0", protocol=protocol, key="x/" + protocol)
         ok = True
         for it in range(5):  # eager calls: values depend on rank and iteration
             t = torch.arange(n, device="cuda:0", dtype=torch.float32) * (rank + 1) + it
@@ -63,12 +63,13 @@ def _worker(rank, world, port, q):
         q.put((rank, False, repr(e)))
 
 
-def test_xgmi_allreduce_two_ranks_one_gpu(gpu):
+@pytest.mark.parametrize("protocol", ["ll", "flag"])
+def test_xgmi_allreduce_two_ranks_one_gpu(gpu, protocol):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, protocol)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
