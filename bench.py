@@ -36,6 +36,33 @@ from distributedtensorflowexample_amd.train.fused_mlp import FusedMLPTrainer  # 
 METRIC = "samples/sec (whole node) MNIST MLP sync-SGD at 1/2/4/8 MI355X; scaling efficiency"
 
 
+# Rehearsal mode for the multi-rank paths on a ONE-GPU box: every rank shares device 0 and
+# an xGMI-IPC communicator (flag protocol) stands in for RCCL, which refuses two ranks on
+# one GPU.  Never set for real runs; the JSON records it.
+SHARED_GPU = os.environ.get("DTFX_SHARED_GPU") == "1"
+
+
+def _comm_label(a):
+    return a.comm + ("+shared-gpu-rehearsal" if SHARED_GPU else "")
+
+
+def mlp_numel():
+    from distributedtensorflowexample_amd.ops import mlp_step
+
+    return mlp_step.NPARAM
+
+
+def _native_comm(world, rank, dev, max_numel):
+    if SHARED_GPU:
+        from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+        return XgmiComm(rank, world, max_numel, device=dev, key="dtfx/shared", protocol="flag",
+                        timeout_s=120.0)  # peers time-share the GPU (and start skewed)
+    from distributedtensorflowexample_amd.parallel.comm import NativeComm
+
+    return NativeComm.from_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,6 +103,8 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             sys.exit("--gpus %d needs torch.distributed.run with %d processes" % (a.gpus, a.gpus))
+    if SHARED_GPU:
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -96,23 +125,25 @@ def main():
 
     allreduce = None
     if world > 1:
-        from distributedtensorflowexample_amd.parallel.comm import NativeComm, TorchComm
+        from distributedtensorflowexample_amd.parallel.comm import TorchComm
 
         if a.comm == "torch":
             comm = TorchComm()
         else:
-            comm = NativeComm.from_process_group()
+            comm = _native_comm(world, rank, dev, mlp_numel())
             if a.comm in ("xgmi", "auto"):
                 from distributedtensorflowexample_amd.parallel.select import pick_small_allreduce
                 from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
 
                 comm, probe = pick_small_allreduce(comm, a.comm, world, rank, dev)
                 a.comm_probe = probe
-                a.comm = "xgmi" if isinstance(comm, XgmiComm) else "native"
+                a.comm = ("xgmi-" + comm.protocol) if isinstance(comm, XgmiComm) else "native"
         allreduce = comm.allreduce_sum_
         chk = params.double().sum().reshape(1).cpu()
         ref = chk.clone()
-        dist.broadcast(ref if a.comm == "native" else ref.to(dev), 0)
+        if a.comm == "torch":  # nccl process group: device tensors
+            ref = ref.to(dev)
+        dist.broadcast(ref, 0)  # else the gloo control plane
         if not torch.equal(chk, ref.cpu()):
             raise RuntimeError("replicas are not identical after init")
 
@@ -131,7 +162,7 @@ def main():
                          allreduce=allreduce, world_size=world,
                          max_graph_steps=a.max_graph_steps)
     if world > 1:
-        barrier = dist.barrier if a.comm == "native" else (lambda: dist.barrier(device_ids=[local]))
+        barrier = dist.barrier if a.comm != "torch" else (lambda: dist.barrier(device_ids=[local]))
     else:
         barrier = None
     use_graph = not a.no_graph
@@ -153,7 +184,7 @@ def main():
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
-        t = t if a.comm == "native" else t.to(dev)
+        t = t if a.comm != "torch" else t.to(dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss, acc = tr.stats()
@@ -179,7 +210,7 @@ def main():
                 "per_gpu_batch": a.batch_size,
                 "seq_len": None,
                 "parallelism": "dp%d" % world,
-                "comm": a.comm if (world > 1 or a.dp) else "none",
+                "comm": _comm_label(a) if (world > 1 or a.dp) else "none",
                 "hipgraph": use_graph,
             },
             "comm_probe_us": getattr(a, "comm_probe", None),
@@ -198,14 +229,14 @@ def bench_bert(a, world, rank, local, dev):
 
     comm = None
     if world > 1:
-        from distributedtensorflowexample_amd.parallel.comm import NativeComm, TorchComm
+        from distributedtensorflowexample_amd.parallel.comm import TorchComm
 
-        comm = NativeComm.from_process_group() if a.comm == "native" else TorchComm()
+        comm = _native_comm(world, rank, dev, 160 << 20) if a.comm != "torch" else TorchComm()
     cfg = BertConfig.base() if a.bert_config == "base" else BertConfig.tiny()
     tr = BertTrainer(cfg, a.bert_batch, a.seq_len, dev, comm=comm, data_seed=17 + rank)
     use_graph = not a.no_graph
     tr.run(a.warmup, use_graph)
-    barrier = (dist.barrier if a.comm == "native" else (lambda: dist.barrier(device_ids=[local]))) \
+    barrier = (dist.barrier if a.comm != "torch" else (lambda: dist.barrier(device_ids=[local]))) \
         if world > 1 else None
     if barrier:
         barrier()
@@ -218,7 +249,7 @@ def bench_bert(a, world, rank, local, dev):
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
-        t = t if a.comm == "native" else t.to(dev)
+        t = t if a.comm != "torch" else t.to(dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss, acc = tr.stats()
@@ -237,7 +268,7 @@ def bench_bert(a, world, rank, local, dev):
                 a.bert_config, cfg.layers, cfg.hidden, cfg.heads, cfg.vocab_size),
                 "global_batch": a.bert_batch * world, "per_gpu_batch": a.bert_batch,
                 "seq_len": a.seq_len, "parallelism": "dp%d" % world,
-                "comm": a.comm if world > 1 else "none", "hipgraph": use_graph,
+                "comm": _comm_label(a) if world > 1 else "none", "hipgraph": use_graph,
                 "optimizer": "AdamW (fused, f32 master)"},
             "model_tflops_per_gpu": round(tr.flops_per_step() / (ms * 1e-3) / 1e12, 1),
             "final_loss": round(loss, 4), "final_mlm_acc": round(acc, 4),
@@ -252,13 +283,13 @@ def bench_resnet(a, world, rank, local, dev):
 
     comm = None
     if world > 1:
-        from distributedtensorflowexample_amd.parallel.comm import NativeComm, TorchComm
+        from distributedtensorflowexample_amd.parallel.comm import TorchComm
 
-        comm = NativeComm.from_process_group() if a.comm == "native" else TorchComm()
+        comm = _native_comm(world, rank, dev, 32 << 20) if a.comm != "torch" else TorchComm()
     tr = ResNetTrainer(a.resnet_batch, dev, comm=comm, image_size=a.image_size, data_seed=rank)
     use_graph = not a.no_graph
     tr.run(a.warmup, use_graph)
-    barrier = (dist.barrier if a.comm == "native" else (lambda: dist.barrier(device_ids=[local]))) \
+    barrier = (dist.barrier if a.comm != "torch" else (lambda: dist.barrier(device_ids=[local]))) \
         if world > 1 else None
     if barrier:
         barrier()
@@ -271,7 +302,7 @@ def bench_resnet(a, world, rank, local, dev):
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
-        t = t if a.comm == "native" else t.to(dev)
+        t = t if a.comm != "torch" else t.to(dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss, acc = tr.stats()
@@ -287,7 +318,7 @@ def bench_resnet(a, world, rank, local, dev):
             "config": {"model": "ResNet-50 v1.5 (BN train mode, momentum SGD)",
                        "global_batch": a.resnet_batch * world, "per_gpu_batch": a.resnet_batch,
                        "seq_len": None, "parallelism": "dp%d" % world,
-                       "comm": a.comm if world > 1 else "none", "hipgraph": use_graph},
+                       "comm": _comm_label(a) if world > 1 else "none", "hipgraph": use_graph},
             "final_loss": round(loss, 4), "final_train_acc": round(acc, 4),
         }), flush=True)
     if world > 1:

@@ -17,7 +17,13 @@ void xgmi_allreduce_launch(float* g, long long n, int rank, int world, long long
                            const XgPeers& peers, unsigned* epochs, int* err, long long ticks,
                            hipStream_t stream);
 
-void xgmi_ll_launch(float* g, long long n, int rank, int world, long long S, const XgPeers& peers,
-                    unsigned* epochs, int* err, long long ticks, hipStream_t stream);
+enum { XG_LL_PULL = 0, XG_LL_PUSH = 1, XG_LL_PUSH2 = 2 };
+
+// bytes of one rank's LL data region (the flag array follows it)
+long long xgmi_ll_bytes(int mode, int world, long long S);
+
+void xgmi_ll_launch(int mode, float* g, long long n, int rank, int world, long long S,
+                    const XgPeers& peers, unsigned* epochs, int* err, long long ticks,
+                    hipStream_t stream);
 
 }  // namespace dtfx

@@ -96,79 +96,185 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// LL ("low-latency") variant: every element travels as ONE 8-byte word {f32 value,
-// u32 epoch}, so the data carries its own ready flag -- no store-acknowledge wait,
-// no separate flag round trip.  Readers load the W peers' words of an element
-// together and re-poll only the ones whose epoch is not yet current.  Slots are
-// u64 [2][S], parity by epoch as in the flag protocol (same overwrite argument).
+// LL ("low-latency") protocols: every element travels as ONE 8-byte word {f32 value,
+// u32 epoch}, so the data carries its own ready flag -- no store-acknowledge wait and no
+// separate flag round trip.  Receivers re-poll only the words whose epoch is not yet
+// current (bounded by s_memrealtime).  All slot regions alternate by epoch parity, with
+// the same "a rank can only reach epoch e+2 after every peer finished epoch e" argument
+// as the flag protocol (docs/COMM.md).  Three data-flow variants:
+//   LL_PULL  one-shot, each rank publishes into its OWN slot [2][S]; readers load the
+//            peers' words over xGMI (remote polling).
+//   LL_PUSH  one-shot, each rank stores its words into slot[me] of EVERY peer
+//            ([2][W][S] per rank); receivers poll LOCAL memory only.  Per link: n words.
+//   LL_PUSH2 two-shot (reduce-scatter + all-gather): element i is owned by rank
+//            i / ceil(n/W); senders push only the owner's share, the owner sums it in
+//            rank order and pushes the result into every peer's result region [2][S].
+//            Per link: 2n/W words -- the choice for larger worlds / buffers.
+// Every rank sums in rank order, so the replicas stay bit-identical.
 // ---------------------------------------------------------------------------
-template <int W>
+namespace {
+
+using u64 = unsigned long long;
+
+__device__ __forceinline__ u64 ll_word(float v, unsigned e) {
+  return ((u64)e << 32) | __float_as_uint(v);
+}
+__device__ __forceinline__ void ll_store(u64* p, u64 w) {
+  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ u64 ll_load(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Loads word i of every peer j != rank from base(j) and re-polls the stale ones; returns
+// the rank-ordered sum with `own` at position `rank`, or sets fail on timeout.
+template <int W, class Base>
+__device__ __forceinline__ float ll_gather_sum(Base base, long long i, int rank, unsigned epoch,
+                                               float own, long long ticks, bool& fail) {
+  u64 w[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) w[j] = j == rank ? 0ull : ll_load(base(j) + i);
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ready = true;
+#pragma unroll
+    for (int j = 0; j < W; ++j)
+      if (j != rank && (unsigned)(w[j] >> 32) != epoch) {
+        ready = false;
+        w[j] = ll_load(base(j) + i);
+      }
+    if (ready) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      fail = true;
+      return 0.f;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < W; ++j) acc += j == rank ? own : __uint_as_float((unsigned)w[j]);
+  return acc;
+}
+
+__device__ __forceinline__ float ll_wait_one(const u64* p, unsigned epoch, long long ticks,
+                                             bool& fail) {
+  u64 w = ll_load(p);
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  while ((unsigned)(w >> 32) != epoch) {
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      fail = true;
+      return 0.f;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    w = ll_load(p);
+  }
+  return __uint_as_float((unsigned)w);
+}
+
+}  // namespace
+
+template <int W, int MODE>
 __global__ __launch_bounds__(256) void xgmi_ll_kernel(float* __restrict__ g, long long n, int rank,
                                                       long long S, XgPeers peers,
                                                       unsigned* __restrict__ epochs,
-                                                      int* __restrict__ err, long long timeout_ticks) {
+                                                      int* __restrict__ err, long long ticks) {
   __shared__ unsigned s_epoch;
-  const int b = blockIdx.x, t = threadIdx.x;
-  if (t == 0) s_epoch = epochs[b] + 1;
+  const int b = blockIdx.x, t = threadIdx.x, nb = gridDim.x;
+  if (t == 0) s_epoch = epochs[b] + 1;  // block-private counter; all blocks advance in step
   __syncthreads();
   const unsigned epoch = s_epoch;
-  const long long par = (long long)(epoch & 1u) * S;
-  const long long per = (n + gridDim.x - 1) / gridDim.x;
+  const long long par = epoch & 1u;
+  const long long per = (n + nb - 1) / nb;
   const long long lo = b * per, hi = min(n, lo + per);
-  unsigned long long* mine = (unsigned long long*)peers.data[rank] + par;
-  for (long long i = lo + t; i < hi; i += blockDim.x)
-    __hip_atomic_store(mine + i, ((unsigned long long)epoch << 32) | __float_as_uint(g[i]),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   bool fail = false;
-  for (long long i = lo + t; i < hi; i += blockDim.x) {
-    unsigned long long w[W];
-#pragma unroll
-    for (int j = 0; j < W; ++j)
-      w[j] = j == rank ? 0ull
-                       : __hip_atomic_load((unsigned long long*)peers.data[j] + par + i,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    for (;;) {
-      bool ready = true;
-#pragma unroll
-      for (int j = 0; j < W; ++j)
-        if (j != rank && (unsigned)(w[j] >> 32) != epoch) {
-          ready = false;
-          w[j] = __hip_atomic_load((unsigned long long*)peers.data[j] + par + i, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      if (ready) break;
-      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
-        fail = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
+  if constexpr (MODE == XG_LL_PULL) {
+    // slot: rank j's [2][S] words
+    u64* mine = (u64*)peers.data[rank] + par * S;
+    for (long long i = lo + t; i < hi; i += blockDim.x) ll_store(mine + i, ll_word(g[i], epoch));
+    auto base = [&](int j) { return (const u64*)peers.data[j] + par * S; };
+    for (long long i = lo + t; i < hi && !fail; i += blockDim.x) {
+      const float acc = ll_gather_sum<W>(base, i, rank, epoch, g[i], ticks, fail);
+      if (!fail) g[i] = acc;
     }
-    if (fail) break;
-    float acc = 0.f;
+  } else {
+    // slot(dst, src) = rank dst's words from sender src: [2][W][S]; result region [2][S] after
+    auto slot = [&](int dst, int src) { return (u64*)peers.data[dst] + (par * W + src) * S; };
+    auto local = [&](int j) { return (const u64*)slot(rank, j); };
+    if constexpr (MODE == XG_LL_PUSH) {
+      for (long long i = lo + t; i < hi; i += blockDim.x) {
+        const u64 w = ll_word(g[i], epoch);
 #pragma unroll
-    for (int j = 0; j < W; ++j) acc += j == rank ? g[i] : __uint_as_float((unsigned)w[j]);
-    g[i] = acc;
+        for (int j = 0; j < W; ++j)
+          if (j != rank) ll_store(slot(j, rank) + i, w);
+      }
+      for (long long i = lo + t; i < hi && !fail; i += blockDim.x) {
+        const float acc = ll_gather_sum<W>(local, i, rank, epoch, g[i], ticks, fail);
+        if (!fail) g[i] = acc;
+      }
+    } else {  // XG_LL_PUSH2
+      auto result = [&](int dst) { return (u64*)peers.data[dst] + (2 * W + par) * S; };
+      const long long shard = (n + W - 1) / W;
+      // 1) reduce-scatter sends: element i goes to its owner only
+      for (long long i = lo + t; i < hi; i += blockDim.x) {
+        const int o = (int)(i / shard);
+        if (o != rank) ll_store(slot(o, rank) + i, ll_word(g[i], epoch));
+      }
+      // 2) owner: sum my shard (split over the blocks), push the result to every peer
+      const long long s0 = rank * shard, s1 = min(n, s0 + shard);
+      const long long sper = (s1 - s0 + nb - 1) / nb;
+      const long long slo = s0 + b * sper, shi = min(s1, slo + sper);
+      for (long long i = slo + t; i < shi && !fail; i += blockDim.x) {
+        const float acc = ll_gather_sum<W>(local, i, rank, epoch, g[i], ticks, fail);
+        if (fail) break;
+        g[i] = acc;
+        const u64 w = ll_word(acc, epoch);
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+          if (j != rank) ll_store(result(j) + i, w);
+      }
+      // 3) all-gather receives: every element owned by a peer
+      const u64* res = result(rank);
+      for (long long i = lo + t; i < hi && !fail; i += blockDim.x) {
+        if ((int)(i / shard) == rank) continue;
+        const float v = ll_wait_one(res + i, epoch, ticks, fail);
+        if (!fail) g[i] = v;
+      }
+    }
   }
   if (fail) atomicExch(err, 1);
   __syncthreads();
   if (t == 0) epochs[b] = epoch;
 }
 
-void xgmi_ll_launch(float* g, long long n, int rank, int world, long long S, const XgPeers& peers,
-                    unsigned* epochs, int* err, long long ticks, hipStream_t stream) {
+long long xgmi_ll_bytes(int mode, int world, long long S) {
+  if (mode == XG_LL_PULL) return 8LL * 2 * S;
+  return 8LL * (2LL * world * S + 2 * S);
+}
+
+void xgmi_ll_launch(int mode, float* g, long long n, int rank, int world, long long S,
+                    const XgPeers& peers, unsigned* epochs, int* err, long long ticks,
+                    hipStream_t stream) {
   const dim3 grid(XG_BLOCKS), block(256);
-  switch (world) {
-#define DTFX_LL(WW)                                                                            \
-  case WW:                                                                                     \
-    hipLaunchKernelGGL(xgmi_ll_kernel<WW>, grid, block, 0, stream, g, n, rank, S, peers, epochs, \
-                       err, ticks);                                                            \
+#define DTFX_LL(WW, MM)                                                                       \
+  hipLaunchKernelGGL((xgmi_ll_kernel<WW, MM>), grid, block, 0, stream, g, n, rank, S, peers, \
+                     epochs, err, ticks)
+#define DTFX_LLW(WW)                   \
+  case WW:                             \
+    if (mode == XG_LL_PULL)            \
+      DTFX_LL(WW, XG_LL_PULL);         \
+    else if (mode == XG_LL_PUSH)       \
+      DTFX_LL(WW, XG_LL_PUSH);         \
+    else                               \
+      DTFX_LL(WW, XG_LL_PUSH2);        \
     break;
-    DTFX_LL(1) DTFX_LL(2) DTFX_LL(3) DTFX_LL(4) DTFX_LL(5) DTFX_LL(6) DTFX_LL(7) DTFX_LL(8)
-#undef DTFX_LL
+  switch (world) {
+    DTFX_LLW(1) DTFX_LLW(2) DTFX_LLW(3) DTFX_LLW(4) DTFX_LLW(5) DTFX_LLW(6) DTFX_LLW(7)
+    DTFX_LLW(8)
     default:
-      throw std::runtime_error("xgmi LL protocol: world must be <= 8");
+      throw std::runtime_error("xgmi LL protocols: world must be <= 8");
   }
+#undef DTFX_LLW
+#undef DTFX_LL
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

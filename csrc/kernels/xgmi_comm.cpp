@@ -27,18 +27,21 @@ namespace dtfx {
 class XgmiAllReduce {
  public:
   XgmiAllReduce(int rank, int world, int device, long long max_numel, const std::string& protocol)
-      : rank_(rank), world_(world), device_(device), S_((max_numel + 63) / 64 * 64),
-        ll_(protocol == "ll") {
-    if (protocol != "ll" && protocol != "flag") throw std::runtime_error("xgmi: protocol ll|flag");
-    if (ll_ && world > 8) throw std::runtime_error("xgmi: the LL protocol supports world <= 8");
+      : rank_(rank), world_(world), device_(device), S_((max_numel + 63) / 64 * 64) {
+    if (protocol == "flag") mode_ = -1;
+    else if (protocol == "ll") mode_ = XG_LL_PULL;
+    else if (protocol == "push") mode_ = XG_LL_PUSH;
+    else if (protocol == "push2") mode_ = XG_LL_PUSH2;
+    else throw std::runtime_error("xgmi: protocol must be flag|ll|push|push2");
+    if (mode_ >= 0 && world > 8) throw std::runtime_error("xgmi: LL protocols support world <= 8");
     if (world < 1 || world > XG_MAX_WORLD) throw std::runtime_error("xgmi: world must be 1..16");
     XG_CHECK(hipSetDevice(device));
     // ONE fine-grained uncached (MTYPE UC) allocation: data slots [2][S] f32 followed by the
-    // flag array.  UC accesses bypass every GPU cache, so neither side needs L2 writeback /
+    // flag array (LL protocols: their word regions, see xgmi_allreduce.hip).  UC accesses bypass every GPU cache, so neither side needs L2 writeback /
     // invalidation (a system-scope fence would write back or invalidate the whole L2):
     // ordering alone (vmcnt waits) makes the protocol correct.  Rounded to 2 MiB.
-    // data region sized for the LL protocol's 8-byte {value, epoch} words
-    bytes_ = sizeof(unsigned long long) * 2 * S_ + sizeof(unsigned) * XG_MAX_WORLD * XG_BLOCKS;
+    data_bytes_ = mode_ < 0 ? (long long)sizeof(float) * 2 * S_ : xgmi_ll_bytes(mode_, world, S_);
+    bytes_ = data_bytes_ + sizeof(unsigned) * XG_MAX_WORLD * XG_BLOCKS;
     bytes_ = (bytes_ + (2u << 20) - 1) / (2u << 20) * (2u << 20);
     XG_CHECK(hipExtMallocWithFlags(&base_, bytes_, hipDeviceMallocUncached));
     XG_CHECK(hipMemset(base_, 0, bytes_));
@@ -75,7 +78,7 @@ class XgmiAllReduce {
         p = (char*)q;
       }
       peers_.data[j] = (float*)p;
-      peers_.flags[j] = (unsigned*)(p + sizeof(unsigned long long) * 2 * S_);
+      peers_.flags[j] = (unsigned*)(p + data_bytes_);
     }
     ready_ = true;
   }
@@ -85,8 +88,8 @@ class XgmiAllReduce {
     if (n > S_) throw std::runtime_error("xgmi: buffer larger than max_numel");
     if (g & 15) throw std::runtime_error("xgmi: buffer must be 16-byte aligned");
     const long long ticks = (long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
-    if (ll_)
-      xgmi_ll_launch((float*)g, n, rank_, world_, S_, peers_, epochs_, err_, ticks,
+    if (mode_ >= 0)
+      xgmi_ll_launch(mode_, (float*)g, n, rank_, world_, S_, peers_, epochs_, err_, ticks,
                      (hipStream_t)stream);
     else
       xgmi_allreduce_launch((float*)g, n, rank_, world_, S_, peers_, epochs_, err_, ticks,
@@ -112,7 +115,8 @@ class XgmiAllReduce {
  private:
   int rank_, world_, device_;
   long long S_;
-  bool ll_ = false;
+  int mode_ = -1;  // -1: flag protocol, else XG_LL_*
+  long long data_bytes_ = 0;
   size_t bytes_ = 0;
   void* base_ = nullptr;
   unsigned* epochs_ = nullptr;

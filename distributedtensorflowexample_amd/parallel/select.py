@@ -1,9 +1,10 @@
 """Choice of the all-reduce backend for the latency-bound MLP gradient.
 
-``pick_small_allreduce`` creates the xGMI one-shot communicator, verifies it
-against RCCL on a random gradient (every rank must agree), times both inside a
-captured hipGraph (max over ranks) and returns the faster -- falling back to
-RCCL whenever xGMI is unavailable, wrong or slower.  Used by ``bench.py`` and
+``pick_small_allreduce`` creates one xGMI communicator per protocol (LL pull,
+LL push one-shot, LL push two-shot, flag), verifies each against RCCL on random
+gradients (every rank must agree), times all of them and RCCL inside captured
+hipGraphs (max over ranks) and returns the fastest -- RCCL whenever no xGMI
+protocol is available, correct and faster.  Used by ``bench.py`` and
 the mirrored MLP trainer for N > 1.
 """
 from __future__ import annotations
@@ -18,10 +19,19 @@ from ..ops import mlp_step
 from .xgmi import XgmiComm
 
 
-def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_key="dtfx/xgmi/0"):
-    """MLP gradient all-reduce backend: the xGMI one-shot kernel when it is available,
-    agrees with RCCL on a random gradient, and is faster (mode "auto"); else RCCL.
-    Every rank takes the same decision (gloo control plane)."""
+def xgmi_protocols(world):
+    """Candidate xGMI protocols for a world size (LL variants need world <= 8)."""
+    return ["push2", "push", "ll", "flag"] if world <= 8 else ["flag"]
+
+
+def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_key="dtfx/xgmi/0",
+                         protocols=None):
+    """MLP gradient all-reduce backend.  Every candidate xGMI protocol (``xgmi_protocols``)
+    that can be created on every rank and agrees with RCCL on ten random gradients is timed
+    against RCCL inside captured hipGraphs (max over ranks, interleaved, best of three); mode
+    "auto" returns the fastest of all, mode "xgmi" the fastest xGMI protocol.  Falls back to
+    RCCL when no xGMI protocol qualifies.  Every rank takes the same decision (gloo control
+    plane).  Returns (communicator, {name: us_per_call} or None)."""
     n = mlp_step.NPARAM if n is None else n
 
     def agree(ok):
@@ -29,33 +39,43 @@ def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_k
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
 
-    xg, err = None, ""
-    try:
-        xg = XgmiComm(rank, world, n, device=dev, key=xgmi_key)
-    except Exception as e:  # no IPC / peer mapping on this node
-        err = repr(e)
-    if not agree(xg is not None):
-        print("[bench] xgmi unavailable (%s): RCCL" % err, file=sys.stderr)
+    cands = {}
+    for proto in (protocols or xgmi_protocols(world)):
+        xg, err = None, ""
+        try:
+            xg = XgmiComm(rank, world, n, device=dev, key="%s/%s" % (xgmi_key, proto),
+                          protocol=proto)
+        except Exception as e:  # no IPC / peer mapping on this node
+            err = repr(e)
+        if not agree(xg is not None):
+            if rank == 0:
+                print("[bench] xgmi-%s unavailable (%s)" % (proto, err), file=sys.stderr)
+            continue
+        g = torch.Generator(device="cpu").manual_seed(1000 + rank)
+        ok = True
+        try:
+            for it in range(10):  # fresh random gradients: both backends must agree every time
+                base = torch.randn(n, generator=g).to(dev) * (1 + it)
+                ra, xa = base.clone(), base.clone()
+                rccl.allreduce_sum_(ra)
+                torch.cuda.synchronize()
+                dist.barrier()
+                xg.allreduce_sum_(xa)
+                xg.check()
+                ok &= bool(((ra - xa).abs().max() <= 1e-5 * ra.abs().max()).item())
+        except Exception as e:
+            ok, err = False, repr(e)
+        if agree(ok):
+            cands["xgmi-" + proto] = xg
+        else:
+            if rank == 0:
+                print("[bench] xgmi-%s failed verification (%s)" % (proto, err), file=sys.stderr)
+            xg.destroy()
+    if not cands:
+        print("[bench] no xgmi protocol available: RCCL", file=sys.stderr)
         return rccl, None
-    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
-    ok = True
-    try:
-        for it in range(10):  # fresh random gradients: both backends must agree every time
-            base = torch.randn(n, generator=g).to(dev) * (1 + it)
-            ra, xa = base.clone(), base.clone()
-            rccl.allreduce_sum_(ra)
-            torch.cuda.synchronize()
-            dist.barrier()
-            xg.allreduce_sum_(xa)
-            xg.check()
-            ok &= bool(((ra - xa).abs().max() <= 1e-5 * ra.abs().max()).item())
-    except Exception as e:
-        ok, err = False, repr(e)
-    if not agree(ok):
-        print("[bench] xgmi failed verification (%s): RCCL" % err, file=sys.stderr)
-        return rccl, None
-    if mode == "xgmi":
-        return xg, None
+    if mode != "xgmi":
+        cands["rccl"] = rccl
 
     def graph_of(c, buf):
         s = torch.cuda.Stream(dev)
@@ -82,16 +102,21 @@ def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_k
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
         return float(dt.item())
 
-    bufs = [torch.zeros(n, device=dev), torch.zeros(n, device=dev)]
-    gr_r, gr_x = graph_of(rccl, bufs[0]), graph_of(xg, bufs[1])
-    t_r = t_x = float("inf")
+    names = sorted(cands)  # same order on every rank
+    graphs = {k: graph_of(cands[k], torch.zeros(n, device=dev)) for k in names}
+    probe = {k: float("inf") for k in names}
     for _ in range(3):  # interleaved, best of three each
-        t_r = min(t_r, timed(gr_r))
-        t_x = min(t_x, timed(gr_x))
-    xg.check()
-    probe = {"rccl": round(t_r, 2), "xgmi": round(t_x, 2)}
-    use_x = agree(t_x < t_r)
+        for k in names:
+            probe[k] = min(probe[k], timed(graphs[k]))
+    for k in names:
+        if k != "rccl":
+            cands[k].check()
+    probe = {k: round(v, 2) for k, v in probe.items()}
+    best = min(names, key=lambda k: (probe[k], k))  # times are max-reduced: identical everywhere
+    for k in names:
+        if k not in (best, "rccl"):
+            cands[k].destroy()
     if rank == 0:
         print("[bench] small all-reduce probe (us/call, max over ranks): %s -> %s"
-              % (probe, "xgmi" if use_x else "rccl"), file=sys.stderr)
-    return (xg if use_x else rccl), probe
+              % (probe, best), file=sys.stderr)
+    return cands[best], probe

@@ -45,6 +45,12 @@ class XgmiComm:
                            self.timeout_s)
         return t
 
+    def broadcast_(self, t, root=0):
+        """Broadcast as a sum with zeros off the root (small control-path use)."""
+        if self.rank != root:
+            t.zero_()
+        return self.allreduce_sum_(t)
+
     def check(self):
         """Raise if any all-reduce timed out waiting for a peer (synchronizes the device)."""
         torch.cuda.synchronize(self.device)

@@ -1,6 +1,7 @@
-"""xGMI one-shot all-reduce protocol, two processes sharing one GPU (IPC peers).
+"""xGMI all-reduce protocols (flag, LL pull, LL push, LL push two-shot), two or
+three processes sharing one GPU (IPC peers).
 
-On the single-GPU test box both ranks live on cuda:0, so the "peer" memory is
+On the single-GPU test box all ranks live on cuda:0, so the "peer" memory is
 the same device's HBM reached through IPC mappings; the protocol (publish,
 flag, bounded wait, ordered sum, parity slots, device-side epochs, hipGraph
 replay) is exercised end to end.  Cross-device xGMI transport is exercised by
@@ -63,9 +64,9 @@ def _worker(rank, world, port, q, protocol="ll"):
         q.put((rank, False, repr(e)))
 
 
-@pytest.mark.parametrize("protocol", ["ll", "flag"])
-def test_xgmi_allreduce_two_ranks_one_gpu(gpu, protocol):
-    world = 2
+@pytest.mark.parametrize("protocol,world", [("ll", 2), ("flag", 2), ("push", 2), ("push2", 2),
+                                            ("push", 3), ("push2", 3), ("flag", 3)])
+def test_xgmi_allreduce_ranks_one_gpu(gpu, protocol, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
@@ -95,7 +96,8 @@ def _auto_worker(rank, world, port, q):
         t = torch.full((79510,), float(rank + 1), device="cuda:0")
         comm.allreduce_sum_(t)
         torch.cuda.synchronize()
-        q.put((rank, bool((t == 3.0).all()) and probe is not None, str(probe)))
+        q.put((rank, bool((t == 3.0).all()) and probe is not None and len(probe) >= 4,
+               str(probe)))
         dist.destroy_process_group()
     except Exception as e:
         q.put((rank, False, repr(e)))
