@@ -86,6 +86,10 @@ def main():
                          "xgmi: one-shot peer-memory all-reduce over xGMI (small buckets); "
                          "auto (MLP, N>1): verify xgmi against RCCL, time both, use the faster; "
                          "torch: torch.distributed nccl(=RCCL) process group")
+    ap.add_argument("--engine", choices=["auto", "fused", "allreduce"], default="auto",
+                    help="MLP, N>1: fused = gradient exchange inside the backward kernel (xGMI LL "
+                         "push); allreduce = separate all-reduce launch; auto = verify + time "
+                         "both, keep the faster")
     ap.add_argument("--dataset_size", type=int, default=55000)
     ap.add_argument("--dp", action="store_true",
                     help="use the data-parallel path (gradient all-reduce) even on 1 GPU")
@@ -123,7 +127,7 @@ def main():
     params = init_params(dev, seed=1234)
     x, y = mnist_like_device(a.dataset_size, seed=100 + rank, device=dev)
 
-    allreduce = None
+    allreduce = fused_comm = None
     if world > 1:
         from distributedtensorflowexample_amd.parallel.comm import TorchComm
 
@@ -138,7 +142,16 @@ def main():
                 comm, probe = pick_small_allreduce(comm, a.comm, world, rank, dev)
                 a.comm_probe = probe
                 a.comm = ("xgmi-" + comm.protocol) if isinstance(comm, XgmiComm) else "native"
-        allreduce = comm.allreduce_sum_
+            if a.engine != "allreduce":
+                # exchange fused into the backward kernel vs separate all-reduce: measured
+                from distributedtensorflowexample_amd.parallel.select import pick_mlp_engine
+
+                kind, c, eprobe = pick_mlp_engine(params, x, y, a.batch_size, a.learning_rate,
+                                                  comm, world, rank, dev, mode=a.engine)
+                a.engine_probe = eprobe
+                if kind == "fused":
+                    fused_comm, a.comm = c, "xgmi-fused-push"
+        allreduce = None if fused_comm is not None else comm.allreduce_sum_
         chk = params.double().sum().reshape(1).cpu()
         ref = chk.clone()
         if a.comm == "torch":  # nccl process group: device tensors
@@ -160,7 +173,7 @@ def main():
         allreduce = comm.allreduce_sum_
     tr = FusedMLPTrainer(params, x, y, batch_size=a.batch_size, learning_rate=a.learning_rate,
                          allreduce=allreduce, world_size=world,
-                         max_graph_steps=a.max_graph_steps)
+                         max_graph_steps=a.max_graph_steps, fused_comm=fused_comm)
     if world > 1:
         barrier = dist.barrier if a.comm != "torch" else (lambda: dist.barrier(device_ids=[local]))
     else:
@@ -214,6 +227,7 @@ def main():
                 "hipgraph": use_graph,
             },
             "comm_probe_us": getattr(a, "comm_probe", None),
+            "engine_probe_us_per_step": getattr(a, "engine_probe", None),
             "final_loss": round(loss, 5),
             "final_train_acc": round(acc, 4),
             "global_step": tr.global_step(),

@@ -46,6 +46,7 @@
 // mlp_wgrad after it has used the value as the stats-ring index; no other
 // thread of any launch touches it.
 #include "common.h"
+#include "xgmi_ll.h"
 
 #include <stdexcept>
 #include <string>
@@ -278,11 +279,33 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
 // ---------------------------------------------------------------------------
 // NGT > 0: batch padded to NGT*16 rows at compile time (branch-free loads);
 // NGT == 0: generic (runtime NG, guarded loops).
-template <bool DIRECT, bool TRACE, int NGT>
+// XW > 0: fused xGMI gradient exchange over XW ranks before the (direct) apply.
+template <int XW>
+__device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const size_t (&off)[4],
+                                            const bool (&ok)[4], float (&v)[4], bool& fail) {
+  using xgll::u64;
+  const long long par = ep & 1u;
+  const int me = xg.rank;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (!ok[i]) continue;
+    const u64 wd = xgll::word(v[i], ep);
+#pragma unroll
+    for (int d = 0; d < XW; ++d)
+      if (d != me) xgll::store((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + off[i], wd);
+  }
+  auto local = [&](int j) { return (const u64*)xg.peers.data[me] + (par * XW + j) * xg.S; };
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (ok[i] && !fail) v[i] = xgll::gather_sum<XW>(local, (long long)off[i], me, ep, v[i], xg.ticks, fail);
+}
+
+template <bool DIRECT, bool TRACE, int NGT, int XW = 0>
 __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
     float* __restrict__ p, float lr, float* __restrict__ grad, const float* __restrict__ x,
     Bufs w, int* __restrict__ ctr, float* __restrict__ stats, int stats_ring, int B,
-    unsigned long long* __restrict__ tr) {
+    unsigned long long* __restrict__ tr, MlpXg xg) {
+  static_assert(XW == 0 || DIRECT, "the fused exchange applies the update directly");
   const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
   const int NG = NGT > 0 ? NGT : BP / 16;
   // readfirstlane: make the wave id provably uniform (scalar branches, not exec masks)
@@ -313,6 +336,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
         }
       }
     }
+    const unsigned ep = XW > 0 ? xg.epochs[bid * 4 + wave] + 1 : 0u;
     float pw[4];
     if (DIRECT) {
 #pragma unroll
@@ -337,15 +361,28 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
       asm volatile("" ::"v"(acc0[0]), "v"(acc1[0]));
       trace_stamp(trw, 2);
     }
+    size_t offw[4];
+    bool okw[4];
+    float gv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int j = jt * 16 + q * 4 + i;
-      if (j < H) {
-        const size_t off = OFF_W1 + (size_t)j * D + kt * 16 + r;
-        const float gv = acc0[i] + acc1[i];
-        if (DIRECT) p[off] = pw[i] - lr * gv;
-        else grad[off] = gv;
+      okw[i] = j < H;
+      offw[i] = OFF_W1 + (size_t)(j < H ? j : 0) * D + kt * 16 + r;
+      gv[i] = acc0[i] + acc1[i];
+    }
+    bool fail = false;
+    if constexpr (XW > 0) xg_exchange<XW>(xg, ep, offw, okw, gv, fail);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (okw[i] && !fail) {
+        if (DIRECT) p[offw[i]] = pw[i] - lr * gv[i];
+        else grad[offw[i]] = gv[i];
       }
+    }
+    if constexpr (XW > 0) {
+      if (lane == 0) xg.epochs[bid * 4 + wave] = ep;
+      if (fail) atomicExch(xg.err, 1);
     }
     if (TRACE) trace_stamp(trw, 3);
     return;
@@ -379,6 +416,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
   const float* A = (wave == 1) ? w.dz1T + (size_t)(jt * 16 + r) * BP + q * 4
                                : w.dlT + (size_t)r * BP + q * 4;
   const float* hb = w.hbuf + jt * 16 + r;
+  const unsigned ep = XW > 0 ? xg.epochs[bid * 4 + wave] + 1 : 0u;
   float4 av[MAXG];
   float bv[MAXG][4];
 #pragma unroll
@@ -431,13 +469,21 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
       acc1 = mfma16x16x4(av[g].w, bv[g][3], acc1);
     }
   }
+  float v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = acc0[i] + acc1[i];
+  bool fail = false;
+  if constexpr (XW > 0) xg_exchange<XW>(xg, ep, off, ok, v, fail);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float v = acc0[i] + acc1[i];
-    if (ok[i]) {
-      if (DIRECT) p[off[i]] = pv[i] - lr * v;
-      else grad[off[i]] = v;
+    if (ok[i] && !fail) {
+      if (DIRECT) p[off[i]] = pv[i] - lr * v[i];
+      else grad[off[i]] = v[i];
     }
+  }
+  if constexpr (XW > 0) {
+    if (lane == 0) xg.epochs[bid * 4 + wave] = ep;
+    if (fail) atomicExch(xg.err, 1);
   }
 }
 
@@ -522,9 +568,11 @@ void mlp_wgrad_launch(float* p, float lr, float* grad, const float* x, float* ws
   dim3 grid(HT * ((FT + 3) / 4) + HT), block(256);
   const int NG = (B + 15) / 16;
   if (!grad && !p) throw std::runtime_error("mlp_wgrad: direct mode needs parameters");
+  const MlpXg noxg{};
 #define DTFX_WG(DIR, TR, NGT)                                                                 \
   hipLaunchKernelGGL((mlp_wgrad_kernel<DIR, TR, NGT>), grid, block, 0, stream, p,          \
-                     DIR ? lr : 0.f, DIR ? nullptr : grad, x, w, ctr, stats, stats_ring, B, tr)
+                     DIR ? lr : 0.f, DIR ? nullptr : grad, x, w, ctr, stats, stats_ring, B, tr, \
+                     noxg)
   if (grad) {
     if (NG == 7) DTFX_WG(false, false, 7);
     else DTFX_WG(false, false, 0);
@@ -536,6 +584,37 @@ void mlp_wgrad_launch(float* p, float lr, float* grad, const float* x, float* ws
     else DTFX_WG(true, false, 0);
   }
 #undef DTFX_WG
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// K3 with the fused xGMI gradient exchange (direct apply with lr = lr / world).
+void mlp_wgrad_xg_launch(float* p, float lr, const float* x, float* ws, int* ctr, float* stats,
+                         int stats_ring, int B, hipStream_t stream, const MlpXg& xg, int world) {
+  using namespace mlp;
+  check_b(B);
+  if (stats && stats_ring < 1) throw std::runtime_error("mlp_wgrad: stats_ring < 1");
+  if (!ctr || !p) throw std::runtime_error("mlp_wgrad_xg: needs parameters and the step counter");
+  if (xg.S < NPARAM) throw std::runtime_error("mlp_wgrad_xg: exchange slots smaller than the model");
+  const Bufs w = make_bufs(ws, B);
+  const int nblk = HT * ((FT + 3) / 4) + HT;
+  if (nblk * 4 > MLP_XG_EPOCHS) throw std::runtime_error("mlp_wgrad_xg: epoch array too small");
+  dim3 grid(nblk), block(256);
+  const int NG = (B + 15) / 16;
+#define DTFX_WGX(WW, NGT)                                                                    \
+  hipLaunchKernelGGL((mlp_wgrad_kernel<true, false, NGT, WW>), grid, block, 0, stream, p, lr, \
+                     nullptr, x, w, ctr, stats, stats_ring, B, nullptr, xg)
+#define DTFX_WGW(WW)             \
+  case WW:                       \
+    if (NG == 7) DTFX_WGX(WW, 7); \
+    else DTFX_WGX(WW, 0);        \
+    break;
+  switch (world) {
+    DTFX_WGW(2) DTFX_WGW(3) DTFX_WGW(4) DTFX_WGW(5) DTFX_WGW(6) DTFX_WGW(7) DTFX_WGW(8)
+    default:
+      throw std::runtime_error("mlp_wgrad_xg: world must be 2..8");
+  }
+#undef DTFX_WGW
+#undef DTFX_WGX
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

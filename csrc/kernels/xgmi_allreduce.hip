@@ -24,6 +24,7 @@
 #include "common.h"
 
 #include "xgmi.h"
+#include "xgmi_ll.h"
 
 #include <stdexcept>
 
@@ -112,66 +113,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
 //            Per link: 2n/W words -- the choice for larger worlds / buffers.
 // Every rank sums in rank order, so the replicas stay bit-identical.
 // ---------------------------------------------------------------------------
-namespace {
-
-using u64 = unsigned long long;
-
-__device__ __forceinline__ u64 ll_word(float v, unsigned e) {
-  return ((u64)e << 32) | __float_as_uint(v);
-}
-__device__ __forceinline__ void ll_store(u64* p, u64 w) {
-  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ u64 ll_load(const u64* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Loads word i of every peer j != rank from base(j) and re-polls the stale ones; returns
-// the rank-ordered sum with `own` at position `rank`, or sets fail on timeout.
-template <int W, class Base>
-__device__ __forceinline__ float ll_gather_sum(Base base, long long i, int rank, unsigned epoch,
-                                               float own, long long ticks, bool& fail) {
-  u64 w[W];
-#pragma unroll
-  for (int j = 0; j < W; ++j) w[j] = j == rank ? 0ull : ll_load(base(j) + i);
-  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    bool ready = true;
-#pragma unroll
-    for (int j = 0; j < W; ++j)
-      if (j != rank && (unsigned)(w[j] >> 32) != epoch) {
-        ready = false;
-        w[j] = ll_load(base(j) + i);
-      }
-    if (ready) break;
-    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
-      fail = true;
-      return 0.f;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  float acc = 0.f;
-#pragma unroll
-  for (int j = 0; j < W; ++j) acc += j == rank ? own : __uint_as_float((unsigned)w[j]);
-  return acc;
-}
-
-__device__ __forceinline__ float ll_wait_one(const u64* p, unsigned epoch, long long ticks,
-                                             bool& fail) {
-  u64 w = ll_load(p);
-  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-  while ((unsigned)(w >> 32) != epoch) {
-    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
-      fail = true;
-      return 0.f;
-    }
-    __builtin_amdgcn_s_sleep(1);
-    w = ll_load(p);
-  }
-  return __uint_as_float((unsigned)w);
-}
-
-}  // namespace
+using xgll::u64;
 
 template <int W, int MODE>
 __global__ __launch_bounds__(256) void xgmi_ll_kernel(float* __restrict__ g, long long n, int rank,
@@ -190,10 +132,10 @@ __global__ __launch_bounds__(256) void xgmi_ll_kernel(float* __restrict__ g, lon
   if constexpr (MODE == XG_LL_PULL) {
     // slot: rank j's [2][S] words
     u64* mine = (u64*)peers.data[rank] + par * S;
-    for (long long i = lo + t; i < hi; i += blockDim.x) ll_store(mine + i, ll_word(g[i], epoch));
+    for (long long i = lo + t; i < hi; i += blockDim.x) xgll::store(mine + i, xgll::word(g[i], epoch));
     auto base = [&](int j) { return (const u64*)peers.data[j] + par * S; };
     for (long long i = lo + t; i < hi && !fail; i += blockDim.x) {
-      const float acc = ll_gather_sum<W>(base, i, rank, epoch, g[i], ticks, fail);
+      const float acc = xgll::gather_sum<W>(base, i, rank, epoch, g[i], ticks, fail);
       if (!fail) g[i] = acc;
     }
   } else {
@@ -202,13 +144,13 @@ __global__ __launch_bounds__(256) void xgmi_ll_kernel(float* __restrict__ g, lon
     auto local = [&](int j) { return (const u64*)slot(rank, j); };
     if constexpr (MODE == XG_LL_PUSH) {
       for (long long i = lo + t; i < hi; i += blockDim.x) {
-        const u64 w = ll_word(g[i], epoch);
+        const u64 w = xgll::word(g[i], epoch);
 #pragma unroll
         for (int j = 0; j < W; ++j)
-          if (j != rank) ll_store(slot(j, rank) + i, w);
+          if (j != rank) xgll::store(slot(j, rank) + i, w);
       }
       for (long long i = lo + t; i < hi && !fail; i += blockDim.x) {
-        const float acc = ll_gather_sum<W>(local, i, rank, epoch, g[i], ticks, fail);
+        const float acc = xgll::gather_sum<W>(local, i, rank, epoch, g[i], ticks, fail);
         if (!fail) g[i] = acc;
       }
     } else {  // XG_LL_PUSH2
@@ -217,26 +159,26 @@ __global__ __launch_bounds__(256) void xgmi_ll_kernel(float* __restrict__ g, lon
       // 1) reduce-scatter sends: element i goes to its owner only
       for (long long i = lo + t; i < hi; i += blockDim.x) {
         const int o = (int)(i / shard);
-        if (o != rank) ll_store(slot(o, rank) + i, ll_word(g[i], epoch));
+        if (o != rank) xgll::store(slot(o, rank) + i, xgll::word(g[i], epoch));
       }
       // 2) owner: sum my shard (split over the blocks), push the result to every peer
       const long long s0 = rank * shard, s1 = min(n, s0 + shard);
       const long long sper = (s1 - s0 + nb - 1) / nb;
       const long long slo = s0 + b * sper, shi = min(s1, slo + sper);
       for (long long i = slo + t; i < shi && !fail; i += blockDim.x) {
-        const float acc = ll_gather_sum<W>(local, i, rank, epoch, g[i], ticks, fail);
+        const float acc = xgll::gather_sum<W>(local, i, rank, epoch, g[i], ticks, fail);
         if (fail) break;
         g[i] = acc;
-        const u64 w = ll_word(acc, epoch);
+        const u64 w = xgll::word(acc, epoch);
 #pragma unroll
         for (int j = 0; j < W; ++j)
-          if (j != rank) ll_store(result(j) + i, w);
+          if (j != rank) xgll::store(result(j) + i, w);
       }
       // 3) all-gather receives: every element owned by a peer
       const u64* res = result(rank);
       for (long long i = lo + t; i < hi && !fail; i += blockDim.x) {
         if ((int)(i / shard) == rank) continue;
-        const float v = ll_wait_one(res + i, epoch, ticks, fail);
+        const float v = xgll::wait_one(res + i, epoch, ticks, fail);
         if (!fail) g[i] = v;
       }
     }

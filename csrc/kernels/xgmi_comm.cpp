@@ -48,6 +48,8 @@ class XgmiAllReduce {
     XG_CHECK(hipMalloc(&epochs_, sizeof(unsigned) * XG_BLOCKS + sizeof(int)));
     XG_CHECK(hipMemset(epochs_, 0, sizeof(unsigned) * XG_BLOCKS + sizeof(int)));
     err_ = (int*)(epochs_ + XG_BLOCKS);
+    XG_CHECK(hipMalloc(&mlp_epochs_, sizeof(unsigned) * MLP_XG_EPOCHS));
+    XG_CHECK(hipMemset(mlp_epochs_, 0, sizeof(unsigned) * MLP_XG_EPOCHS));
     for (int i = 0; i < XG_MAX_WORLD; ++i) {
       peers_.data[i] = nullptr;
       peers_.flags[i] = nullptr;
@@ -96,6 +98,23 @@ class XgmiAllReduce {
                             (hipStream_t)stream);
   }
 
+  // MNIST-MLP weight-gradient kernel with the gradient exchange fused into its epilogue
+  // (push layout only): p -= lr * sum_over_ranks(grad), one launch.
+  void mlp_wgrad(uintptr_t p, float lr, uintptr_t x, uintptr_t ws, uintptr_t ctr, uintptr_t stats,
+                 int ring, int B, uintptr_t stream, double timeout_s) {
+    if (!ready_) throw std::runtime_error("xgmi: open() the peer handles first");
+    if (mode_ != XG_LL_PUSH) throw std::runtime_error("xgmi: the fused MLP exchange needs protocol push");
+    MlpXg xg;
+    xg.peers = peers_;
+    xg.S = S_;
+    xg.rank = rank_;
+    xg.epochs = mlp_epochs_;
+    xg.err = err_;
+    xg.ticks = (long long)(timeout_s * 1e8);
+    mlp_wgrad_xg_launch((float*)p, lr, (const float*)x, (float*)ws, (int*)ctr, (float*)stats, ring, B,
+                        (hipStream_t)stream, xg, world_);
+  }
+
   int error() {
     int e = 0;
     XG_CHECK(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost));
@@ -107,8 +126,10 @@ class XgmiAllReduce {
     opened_.clear();
     if (base_) hipFree(base_);
     if (epochs_) hipFree(epochs_);
+    if (mlp_epochs_) hipFree(mlp_epochs_);
     base_ = nullptr;
     epochs_ = nullptr;
+    mlp_epochs_ = nullptr;
     ready_ = false;
   }
 
@@ -120,6 +141,7 @@ class XgmiAllReduce {
   size_t bytes_ = 0;
   void* base_ = nullptr;
   unsigned* epochs_ = nullptr;
+  unsigned* mlp_epochs_ = nullptr;
   int* err_ = nullptr;
   XgPeers peers_;
   std::vector<void*> opened_;
@@ -136,6 +158,9 @@ void register_xgmi(py::module_& m) {
       .def("handle", &dtfx::XgmiAllReduce::handle)
       .def("open", &dtfx::XgmiAllReduce::open)
       .def("all_reduce", &dtfx::XgmiAllReduce::all_reduce, py::arg("g"), py::arg("n"),
+           py::arg("stream"), py::arg("timeout_s") = 2.0)
+      .def("mlp_wgrad", &dtfx::XgmiAllReduce::mlp_wgrad, py::arg("p"), py::arg("lr"), py::arg("x"),
+           py::arg("ws"), py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"),
            py::arg("stream"), py::arg("timeout_s") = 2.0)
       .def("error", &dtfx::XgmiAllReduce::error)
       .def("close", &dtfx::XgmiAllReduce::close);

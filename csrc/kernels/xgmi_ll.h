@@ -1,0 +1,74 @@
+// Device helpers of the xGMI LL ("low-latency") protocols: one 8-byte word per
+// element = {f32 value, u32 epoch}, stored / loaded with single relaxed
+// system-scope 64-bit accesses into uncached IPC memory, so a word with the
+// current epoch always carries the value written with it.  Shared by the
+// stand-alone all-reduce (xgmi_allreduce.hip) and the MLP step kernel that
+// exchanges its gradient in the epilogue (mlp_step.hip).
+#pragma once
+
+#include "common.h"
+#include "xgmi.h"
+
+namespace dtfx {
+namespace xgll {
+
+using u64 = unsigned long long;
+
+__device__ __forceinline__ u64 word(float v, unsigned e) {
+  return ((u64)e << 32) | __float_as_uint(v);
+}
+__device__ __forceinline__ void store(u64* p, u64 w) {
+  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ u64 load(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Loads word i of every peer j != rank from base(j) and re-polls the stale ones; returns
+// the rank-ordered sum with `own` at position `rank` (identical on every rank), or sets
+// fail after `ticks` of s_memrealtime (100 MHz).
+template <int W, class Base>
+__device__ __forceinline__ float gather_sum(Base base, long long i, int rank, unsigned epoch,
+                                            float own, long long ticks, bool& fail) {
+  u64 w[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) w[j] = j == rank ? 0ull : load(base(j) + i);
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ready = true;
+#pragma unroll
+    for (int j = 0; j < W; ++j)
+      if (j != rank && (unsigned)(w[j] >> 32) != epoch) {
+        ready = false;
+        w[j] = load(base(j) + i);
+      }
+    if (ready) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      fail = true;
+      return 0.f;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < W; ++j) acc += j == rank ? own : __uint_as_float((unsigned)w[j]);
+  return acc;
+}
+
+__device__ __forceinline__ float wait_one(const u64* p, unsigned epoch, long long ticks,
+                                          bool& fail) {
+  u64 w = load(p);
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  while ((unsigned)(w >> 32) != epoch) {
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      fail = true;
+      return 0.f;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    w = load(p);
+  }
+  return __uint_as_float((unsigned)w);
+}
+
+}  // namespace xgll
+}  // namespace dtfx

@@ -92,6 +92,18 @@ def step_direct(p, x, labels, ws: StepWorkspace, lr, stats=True):
                 ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B, s)
 
 
+def step_xgmi(p, x, labels, ws: StepWorkspace, lr, comm, stats=True):
+    """One synchronous data-parallel SGD step in place on ``p`` with the gradient exchange
+    fused into the weight-gradient kernel (``comm``: an ``XgmiComm`` with protocol "push";
+    ``lr`` already divided by the world size).  Three launches, like ``step_direct``."""
+    _check(x, labels, ws.B)
+    _check_flat(p)
+    h, s = hip(), stream_handle()
+    h.mlp_fwd(ptr(p), 0, 0.0, 0, ptr(x), ptr(ws.buf), ws.B, s)
+    h.mlp_head(ptr(p), 0, 0.0, 0, ptr(labels), ptr(ws.buf), ws.B, s)
+    comm.mlp_wgrad(p, lr, x, ws, stats)
+
+
 def step_grad(p_old, x, labels, ws: StepWorkspace, grad, prev_grad=None, lr=0.0, p_new=None,
               stats=True):
     """Forward/backward writing ``grad``; optionally first applies ``prev_grad``.

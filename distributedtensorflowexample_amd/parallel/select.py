@@ -120,3 +120,89 @@ def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_k
         print("[bench] small all-reduce probe (us/call, max over ranks): %s -> %s"
               % (probe, best), file=sys.stderr)
     return cands[best], probe
+
+
+def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mode="auto",
+                    xgmi_key="dtfx/xgmi/fused", verify_steps=20, time_steps=400):
+    """Data-parallel engine of the fused MLP trainer: ``("fused", XgmiComm)`` -- gradient
+    exchange inside the weight-gradient kernel -- or ``("allreduce", ar_comm)`` -- separate
+    all-reduce launch + deferred apply.  The fused engine must (on every rank) build, agree
+    with the all-reduce engine after ``verify_steps`` identical SGD steps, and be faster over
+    ``time_steps`` graph-replayed steps (max over ranks); else the all-reduce engine is kept.
+    Returns (kind, comm, {engine: us_per_step} or None)."""
+    from ..train.fused_mlp import FusedMLPTrainer
+
+    def agree(ok):
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    if world < 2 or world > 8:
+        return "allreduce", ar_comm, None
+    fc, err = None, ""
+    try:
+        fc = XgmiComm(rank, world, mlp_step.NPARAM, device=dev, key=xgmi_key, protocol="push")
+    except Exception as e:
+        err = repr(e)
+    if not agree(fc is not None):
+        if rank == 0:
+            print("[bench] fused xgmi engine unavailable (%s)" % err, file=sys.stderr)
+        return "allreduce", ar_comm, None
+
+    def make(kind):
+        if kind == "fused":
+            return FusedMLPTrainer(params, x, y, batch_size, lr, world_size=world, fused_comm=fc)
+        return FusedMLPTrainer(params, x, y, batch_size, lr, allreduce=ar_comm.allreduce_sum_,
+                               world_size=world)
+
+    ok = True
+    try:
+        tf, ta = make("fused"), make("allreduce")
+        tf.run(verify_steps, use_graph=False)
+        ta.run(verify_steps, use_graph=False)
+        fc.check()
+        pf, pa = tf.flush(), ta.flush()
+        tol = 1e-4 * (1.0 + float(pa.abs().max()))
+        ok = bool(((pf - pa).abs().max() <= tol).item())
+        # replicas must stay bit-identical under the fused engine
+        chk = pf.double().sum().reshape(1).cpu()
+        ref = chk.clone()
+        dist.broadcast(ref, 0)
+        ok &= bool(torch.equal(chk, ref))
+    except Exception as e:
+        ok, err = False, repr(e)
+    if not agree(ok):
+        if rank == 0:
+            print("[bench] fused xgmi engine failed verification (%s)" % err, file=sys.stderr)
+        fc.destroy()
+        return "allreduce", ar_comm, None
+    if mode == "fused":
+        return "fused", fc, None
+
+    def timed(tr):
+        tr.run(50)  # warm (captures the graphs)
+        tr.prepare(time_steps)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tr.run(time_steps)
+        torch.cuda.synchronize()
+        dt = torch.tensor([(time.perf_counter() - t0) / time_steps * 1e6], dtype=torch.float64)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return float(dt.item())
+
+    probe = {"fused": float("inf"), "allreduce": float("inf")}
+    for _ in range(2):
+        probe["fused"] = min(probe["fused"], timed(tf))
+        probe["allreduce"] = min(probe["allreduce"], timed(ta))
+    fc.check()
+    probe = {k: round(v, 2) for k, v in probe.items()}
+    use_f = probe["fused"] < probe["allreduce"]
+    if rank == 0:
+        print("[bench] MLP step engine probe (us/step, max over ranks): %s -> %s"
+              % (probe, "fused" if use_f else "allreduce"), file=sys.stderr)
+    del tf, ta
+    if use_f:
+        return "fused", fc, probe
+    fc.destroy()
+    return "allreduce", ar_comm, probe

@@ -45,6 +45,16 @@ class XgmiComm:
                            self.timeout_s)
         return t
 
+    def mlp_wgrad(self, p, lr, x, ws, stats=True):
+        """MNIST-MLP weight-gradient launch with the gradient all-reduce fused into its
+        epilogue (protocol "push"): ``p -= lr * sum over ranks of the gradient``; see
+        ``ops.mlp_step.step_xgmi``."""
+        from ..ops._ext import ptr
+
+        self._h.mlp_wgrad(ptr(p), float(lr), ptr(x), ptr(ws.buf), ptr(ws.ctr),
+                          ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B,
+                          torch.cuda.current_stream().cuda_stream, self.timeout_s)
+
     def broadcast_(self, t, root=0):
         """Broadcast as a sum with zeros off the root (small control-path use)."""
         if self.rank != root:

@@ -14,6 +14,10 @@ a host->GPU feed of 317 KB and ~14 tiny TF kernels.  Here:
   ``mlp_wgrad`` by a pluggable ``allreduce(grad)`` callable (RCCL through
   ``torch.distributed`` or the native communicator) and applied, averaged
   through ``lr / world_size``, inside the next step's ``mlp_fwd``/``mlp_head``;
+* or, with ``fused_comm`` (an ``XgmiComm`` with protocol "push"), the gradient
+  exchange is fused into ``mlp_wgrad``'s epilogue (LL words pushed straight to
+  the peers, gathered, summed in rank order and applied in the same launch):
+  three launches per data-parallel step, no pending gradient;
 * ``global_step`` is a device counter advanced by the kernels (AssignAdd of
   worker.py:32,141); loss/accuracy land in a device ring read back lazily.
 
@@ -33,7 +37,8 @@ from ..ops import mlp_step, optim
 
 class FusedMLPTrainer:
     def __init__(self, params, x, labels, batch_size=100, learning_rate=0.001, allreduce=None,
-                 world_size=1, stats_ring=4096, global_step=0, max_graph_steps=1024):
+                 world_size=1, stats_ring=4096, global_step=0, max_graph_steps=1024,
+                 fused_comm=None):
         if not params.is_cuda:
             raise ValueError("FusedMLPTrainer runs on the GPU; use the generic path on CPU")
         if params.numel() != mlp_step.NPARAM:
@@ -43,6 +48,9 @@ class FusedMLPTrainer:
         self.lr = float(learning_rate)
         self.world_size = int(world_size)
         self.allreduce = allreduce
+        self.fused_comm = fused_comm
+        if fused_comm is not None and (allreduce is not None or world_size < 2):
+            raise ValueError("fused_comm replaces allreduce and needs world_size >= 2")
         x = x.reshape(-1, mlp_step.D).to(self.device, torch.float32).contiguous()
         labels = labels.reshape(-1).to(self.device, torch.int32).contiguous()
         self.nbatches = x.shape[0] // self.B
@@ -63,8 +71,8 @@ class FusedMLPTrainer:
     # -- state --------------------------------------------------------------
     @property
     def direct(self):
-        """Single-GPU mode: SGD apply fused into the backward kernel."""
-        return self.allreduce is None and self.world_size == 1
+        """SGD apply fused into the backward kernel (one GPU, or the fused xGMI exchange)."""
+        return self.fused_comm is not None or (self.allreduce is None and self.world_size == 1)
 
     @property
     def params(self):
@@ -93,6 +101,10 @@ class FusedMLPTrainer:
     def _step_launches(self):
         xb, yb = self.batch(self.pos)
         self.pos = (self.pos + 1) % self.nbatches
+        if self.fused_comm is not None:
+            mlp_step.step_xgmi(self.bufs[self.cur], xb, yb, self.ws, self.lr / self.world_size,
+                               self.fused_comm)
+            return
         if self.direct:
             mlp_step.step_direct(self.bufs[self.cur], xb, yb, self.ws, self.lr)
             return

@@ -67,8 +67,17 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
     state = {}
 
     if use_gpu:
+        fused = None
+        if comm is not None and os.environ.get("DTFX_MLP_COMM", "auto") != "rccl":
+            # gradient exchange fused into the backward kernel when verified and faster
+            from ..parallel.select import pick_mlp_engine
+
+            kind, c, _ = pick_mlp_engine(params, tr_x.to(dev), tr_y.to(dev), B,
+                                         flags.learning_rate, comm, world, rank, dev)
+            fused = c if kind == "fused" else None
         tr = FusedMLPTrainer(params, tr_x, tr_y, B, flags.learning_rate,
-                             allreduce=comm.allreduce_sum_ if comm else None, world_size=world)
+                             allreduce=comm.allreduce_sum_ if (comm and not fused) else None,
+                             world_size=world, fused_comm=fused)
         get_params = lambda: tr.flush().clone()  # noqa: E731
         step_fn = None
     else:
