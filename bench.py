@@ -86,10 +86,12 @@ def main():
                          "xgmi: one-shot peer-memory all-reduce over xGMI (small buckets); "
                          "auto (MLP, N>1): verify xgmi against RCCL, time both, use the faster; "
                          "torch: torch.distributed nccl(=RCCL) process group")
-    ap.add_argument("--engine", choices=["auto", "fused", "allreduce"], default="auto",
+    ap.add_argument("--engine", choices=["auto", "fused", "factor", "allreduce"], default="auto",
                     help="MLP, N>1: fused = gradient exchange inside the backward kernel (xGMI LL "
-                         "push); allreduce = separate all-reduce launch; auto = verify + time "
-                         "both, keep the faster")
+                         "push); factor = sufficient-factor exchange (dz1 all-gathered in the "
+                         "head kernel, global W1 gradient formed on every rank from every "
+                         "rank's resident batch); allreduce = separate all-reduce launch; auto "
+                         "= verify + time all, keep the fastest")
     ap.add_argument("--dataset_size", type=int, default=55000)
     ap.add_argument("--dp", action="store_true",
                     help="use the data-parallel path (gradient all-reduce) even on 1 GPU")
@@ -126,8 +128,17 @@ def main():
     # same parameters from the same seed (no broadcast needed; verified below)
     params = init_params(dev, seed=1234)
     x, y = mnist_like_device(a.dataset_size, seed=100 + rank, device=dev)
+    x_all = None
+    if 2 <= world <= 8 and a.engine in ("auto", "factor") and a.comm != "torch":
+        # every rank's batch stream resident on every GPU (each reference process loads the
+        # whole dataset, main.py:43-44): the factor engine then exchanges only dz1
+        x_all = torch.empty(world, a.dataset_size, 784, device=dev)
+        for q in range(world):
+            x_all[q].copy_(x if q == rank else mnist_like_device(a.dataset_size, seed=100 + q,
+                                                                 device=dev)[0])
+        x = x_all[rank]
 
-    allreduce = fused_comm = None
+    allreduce = fused_comm = factor_comm = None
     if world > 1:
         from distributedtensorflowexample_amd.parallel.comm import TorchComm
 
@@ -147,11 +158,16 @@ def main():
                 from distributedtensorflowexample_amd.parallel.select import pick_mlp_engine
 
                 kind, c, eprobe = pick_mlp_engine(params, x, y, a.batch_size, a.learning_rate,
-                                                  comm, world, rank, dev, mode=a.engine)
+                                                  comm, world, rank, dev, mode=a.engine,
+                                                  x_all=x_all)
                 a.engine_probe = eprobe
                 if kind == "fused":
                     fused_comm, a.comm = c, "xgmi-fused-push"
-        allreduce = None if fused_comm is not None else comm.allreduce_sum_
+                elif kind == "factor":
+                    factor_comm, a.comm = c, "xgmi-factor-allgather"
+        if factor_comm is None:
+            x_all = None
+        allreduce = None if (fused_comm is not None or factor_comm is not None) else comm.allreduce_sum_
         chk = params.double().sum().reshape(1).cpu()
         ref = chk.clone()
         if a.comm == "torch":  # nccl process group: device tensors
@@ -173,7 +189,8 @@ def main():
         allreduce = comm.allreduce_sum_
     tr = FusedMLPTrainer(params, x, y, batch_size=a.batch_size, learning_rate=a.learning_rate,
                          allreduce=allreduce, world_size=world,
-                         max_graph_steps=a.max_graph_steps, fused_comm=fused_comm)
+                         max_graph_steps=a.max_graph_steps, fused_comm=fused_comm,
+                         factor_comm=factor_comm, x_all=x_all, rank=rank)
     if world > 1:
         barrier = dist.barrier if a.comm != "torch" else (lambda: dist.barrier(device_ids=[local]))
     else:

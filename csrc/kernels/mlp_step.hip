@@ -155,15 +155,21 @@ __global__ __launch_bounds__(64) void mlp_fwd_kernel(
 // ---------------------------------------------------------------------------
 // K2: per-row head (one wave per batch row)
 // ---------------------------------------------------------------------------
-template <bool APPLY, bool TRACE>
+// XW > 0 (factor exchange, MlpXg in xgmi.h): the row's dz1 values are also pushed as LL
+// words into slot (parity, me) of every peer and every peer's values for the same (j, row)
+// are gathered from local memory into dz1A [XW][HP][BP] -- the all-gather of the backprop
+// factors that mlp_wgrad_factor_kernel turns into the global weight gradient.
+template <bool APPLY, bool TRACE, int XW = 0>
 __global__ __launch_bounds__(64) void mlp_head_kernel(
     const float* __restrict__ p_old, const float* __restrict__ grad, float lr,
     float* __restrict__ p_new, const int* __restrict__ labels, Bufs w, int B,
-    unsigned long long* __restrict__ tr) {
+    unsigned long long* __restrict__ tr, MlpXg xg, float* __restrict__ dz1A) {
+  static_assert(XW == 0 || (!APPLY && !TRACE), "the factor exchange runs the direct step");
   if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 0);
   const int BP = ((B + 15) >> 4) * 16;
   const int row = blockIdx.x, lane = threadIdx.x;
   const int y = labels[row];
+  const unsigned ep = XW > 0 ? xg.epochs[MLP_XG_HEAD_EPOCH + row] + 1 : 0u;
   const bool publish = APPLY && row == 0;
 
   // All loads first, unconditional (j clamped to < H), masked afterwards.
@@ -252,15 +258,49 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     dl[c] = (__expf(lg[c] - m) * inv - (c == y ? 1.f : 0.f)) * invB;
     ly = (c == y) ? lg[c] : ly;
   }
+  float dzv[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int j = lane + 64 * u;
+    dzv[u] = 0.f;
     if (j < H) {
       float dh = 0.f;
 #pragma unroll
       for (int c = 0; c < C; ++c) dh += dl[c] * w2[u][c];
-      w.dz1T[(size_t)j * BP + row] = dh * hv[u] * (1.f - hv[u]);
+      dzv[u] = dh * hv[u] * (1.f - hv[u]);
+      w.dz1T[(size_t)j * BP + row] = dzv[u];
     }
+  }
+  if constexpr (XW > 0) {
+    using xgll::u64;
+    const long long par = ep & 1u, plane = (long long)HP * BP;
+    const int me = xg.rank;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {  // push first: every peer's wait overlaps ours
+      const int j = lane + 64 * u;
+      if (j < H) {
+        const long long off = (long long)j * BP + row;
+        const u64 wd = xgll::word(dzv[u], ep);
+#pragma unroll
+        for (int d = 0; d < XW; ++d)
+          if (d != me) xgll::store((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + off, wd);
+      }
+    }
+    auto local = [&](int q) { return (const u64*)xg.peers.data[me] + (par * XW + q) * xg.S; };
+    bool fail = false;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = lane + 64 * u;
+      if (j < H) {
+        const long long off = (long long)j * BP + row;
+        float vals[XW];
+        xgll::gather_all<XW>(local, off, me, ep, dzv[u], xg.ticks, vals, fail);
+#pragma unroll
+        for (int q = 0; q < XW; ++q) dz1A[q * plane + off] = vals[q];
+      }
+    }
+    if (lane == 0) xg.epochs[MLP_XG_HEAD_EPOCH + row] = ep;
+    if (fail) atomicExch(xg.err, 1);
   }
   if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 2);
   float mydl = 0.f;
@@ -298,6 +338,116 @@ __device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const 
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     if (ok[i] && !fail) v[i] = xgll::gather_sum<XW>(local, (long long)off[i], me, ep, v[i], xg.ticks, fail);
+}
+
+// Small parameters of hidden tile jt (one product per wave), shared by mlp_wgrad_kernel and
+// mlp_wgrad_factor_kernel; eidx = this wave's exchange-epoch slot.
+template <bool DIRECT, int NGT, int XW>
+__device__ __forceinline__ void wgrad_small(int jt, int wave, int lane, int eidx,
+                                            float* __restrict__ p, float lr,
+                                            float* __restrict__ grad, const Bufs& w,
+                                            int* __restrict__ ctr, float* __restrict__ stats,
+                                            int stats_ring, int B, const MlpXg& xg) {
+  const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
+  const int NG = NGT > 0 ? NGT : BP / 16;
+  const int r = lane & 15, q = lane >> 4;
+  constexpr int MAXG = NGT > 0 ? NGT : MAXB / 16;
+  // ---- small parameters of hidden tile jt: one product per wave -----------
+  //   wave 0: dW2^T[:, jt] = dlT . h[:, jt]   wave 1: db1[jt] = dz1T[jt] . 1
+  //   wave 2: db2 = dlT . 1 (jt == 0)         wave 3: loss/accuracy (jt == 0)
+  if (wave == 3) {
+    if (jt != 0) return;
+    float l = 0.f, a = 0.f;
+    for (int b = lane; b < B; b += 64) {
+      l += w.rowstat[2 * b];
+      a += w.rowstat[2 * b + 1];
+    }
+    l = wave_sum(l);
+    a = wave_sum(a);
+    if (lane == 0) {
+      const int step = *ctr;  // this thread is the only reader/writer of ctr
+      if (stats) {
+        float* st = stats + (size_t)(step % stats_ring) * 2;
+        st[0] = l / (float)B;
+        st[1] = a / (float)B;
+      }
+      *ctr = step + 1;
+    }
+    return;
+  }
+  if (wave == 2 && jt != 0) return;
+  const float* A = (wave == 1) ? w.dz1T + (size_t)(jt * 16 + r) * BP + q * 4
+                               : w.dlT + (size_t)r * BP + q * 4;
+  const float* hb = w.hbuf + jt * 16 + r;
+  const unsigned ep = XW > 0 ? xg.epochs[eidx] + 1 : 0u;
+  float4 av[MAXG];
+  float bv[MAXG][4];
+#pragma unroll
+  for (int g = 0; g < MAXG; ++g)
+    if (g < NG) av[g] = f4(A + g * 16);
+  if (wave == 0) {  // one uniform branch around the whole B-operand load block
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g)
+      if (g < NG)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[g][e] = hb[(size_t)(g * 16 + q * 4 + e) * HP];
+  } else {
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[g][e] = 1.f;
+  }
+  __builtin_amdgcn_sched_barrier(0);  // all loads in flight together
+  // Destination offsets (and, in direct mode, the current values) resolved
+  // before the MFMAs so the epilogue is a pure store.
+  size_t off[4];
+  bool ok[4];
+  float pv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (wave == 0) {  // C[c = q*4+i][j = jt*16 + r] -> dW2t[c][j]
+      const int c = q * 4 + i, j = jt * 16 + r;
+      ok[i] = c < C && j < H;
+      off[i] = OFF_W2 + (ok[i] ? c * H + j : 0);
+    } else if (wave == 1) {  // C[j = jt*16 + q*4+i][*] -> db1[j]
+      const int j = jt * 16 + q * 4 + i;
+      ok[i] = r == 0 && j < H;
+      off[i] = OFF_B1 + (j < H ? j : 0);
+    } else {  // C[c = q*4+i][*] -> db2[c]
+      const int c = q * 4 + i;
+      ok[i] = r == 0 && c < C;
+      off[i] = OFF_B2 + (c < C ? c : 0);
+    }
+    if (DIRECT) pv[i] = p[off[i]];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // NB: padded batch columns of dz1T/dlT are zero, so multiplying by 1 is exact.
+  f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+#pragma unroll
+  for (int g = 0; g < MAXG; ++g) {
+    if (g < NG) {
+      acc0 = mfma16x16x4(av[g].x, bv[g][0], acc0);
+      acc1 = mfma16x16x4(av[g].y, bv[g][1], acc1);
+      acc0 = mfma16x16x4(av[g].z, bv[g][2], acc0);
+      acc1 = mfma16x16x4(av[g].w, bv[g][3], acc1);
+    }
+  }
+  float v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = acc0[i] + acc1[i];
+  bool fail = false;
+  if constexpr (XW > 0) xg_exchange<XW>(xg, ep, off, ok, v, fail);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (ok[i] && !fail) {
+      if (DIRECT) p[off[i]] = pv[i] - lr * v[i];
+      else grad[off[i]] = v[i];
+    }
+  }
+  if constexpr (XW > 0) {
+    if (lane == 0) xg.epochs[eidx] = ep;
+    if (fail) atomicExch(xg.err, 1);
+  }
 }
 
 template <bool DIRECT, bool TRACE, int NGT, int XW = 0>
@@ -388,102 +538,103 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
     return;
   }
 
-  // ---- small parameters of hidden tile jt: one product per wave -----------
-  //   wave 0: dW2^T[:, jt] = dlT . h[:, jt]   wave 1: db1[jt] = dz1T[jt] . 1
-  //   wave 2: db2 = dlT . 1 (jt == 0)         wave 3: loss/accuracy (jt == 0)
-  const int jt = bid - HT * FG;
-  if (wave == 3) {
-    if (jt != 0) return;
-    float l = 0.f, a = 0.f;
-    for (int b = lane; b < B; b += 64) {
-      l += w.rowstat[2 * b];
-      a += w.rowstat[2 * b + 1];
-    }
-    l = wave_sum(l);
-    a = wave_sum(a);
-    if (lane == 0) {
-      const int step = *ctr;  // this thread is the only reader/writer of ctr
-      if (stats) {
-        float* st = stats + (size_t)(step % stats_ring) * 2;
-        st[0] = l / (float)B;
-        st[1] = a / (float)B;
-      }
-      *ctr = step + 1;
-    }
+  wgrad_small<DIRECT, NGT, XW>(bid - HT * FG, wave, lane, bid * 4 + wave, p, lr, grad, w, ctr,
+                               stats, stats_ring, B, xg);
+}
+
+
+// ---------------------------------------------------------------------------
+// K3, factor engine (sufficient-factor exchange, world XW): the backprop factors dz1 of
+// every rank were all-gathered by mlp_head_kernel<.., XW> into dz1A [XW][HP][BP], and every
+// rank holds every rank's (deterministic, device-resident) batch, so each rank computes the
+// GLOBAL dW1^T = sum_q dz1_q^T . x_q itself (K = XW * BP) and applies it -- the 313 KB W1
+// gradient never crosses xGMI; only the 1,110 small-parameter gradients are exchanged
+// (wgrad_small, LL push).  Identical inputs + a fixed summation order keep the replicas
+// bit-identical.
+//   blocks [0, 8 * FT): one 16x16 dW1^T tile per block, the K range split over 4 waves and
+//     the 4 partial tiles added in wave order through LDS.  Block b runs on XCD b % 8
+//     (round-robin dispatch; speed only): feature tile kt = 8 * s + b % 8 keeps each
+//     XCD's x columns to ~1/8 of every rank's batch (x is the one large fresh read).
+//   blocks [8 * FT, 8 * FT + HT): wgrad_small (dW2 / db1 / db2 partials exchanged).
+// xstride: elements between consecutive ranks' datasets (x of rank q = x + (q - me) * xstride).
+template <int XW, int NGT>
+__global__ __launch_bounds__(256) void mlp_wgrad_factor_kernel(
+    float* __restrict__ p, float lr, const float* __restrict__ x, long long xstride,
+    const float* __restrict__ dz1A, Bufs w, int* __restrict__ ctr, float* __restrict__ stats,
+    int stats_ring, int B, MlpXg xg) {
+  const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
+  const int NG = NGT > 0 ? NGT : BP / 16;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, r = lane & 15, q4 = lane >> 4;
+  const int bid = blockIdx.x;
+  constexpr int NSLOT = (FT + 7) / 8;  // 7 feature-tile slots per XCD
+  if (bid >= 8 * HT * NSLOT) {
+    const int jt = bid - 8 * HT * NSLOT;
+    wgrad_small<true, NGT, XW>(jt, wave, lane, MLP_XG_SMALL_EPOCH + jt * 4 + wave, p, lr,
+                               nullptr, w, ctr, stats, stats_ring, B, xg);
     return;
   }
-  if (wave == 2 && jt != 0) return;
-  const float* A = (wave == 1) ? w.dz1T + (size_t)(jt * 16 + r) * BP + q * 4
-                               : w.dlT + (size_t)r * BP + q * 4;
-  const float* hb = w.hbuf + jt * 16 + r;
-  const unsigned ep = XW > 0 ? xg.epochs[bid * 4 + wave] + 1 : 0u;
-  float4 av[MAXG];
-  float bv[MAXG][4];
+  const int xcd = bid & 7, s = bid >> 3;
+  const int jt = s / NSLOT, kt = (s % NSLOT) * 8 + xcd;
+  if (kt >= FT) return;  // whole block: uniform
+  __shared__ f32x4 red[3][64];
+  const int G = XW * NG, per = (G + 3) / 4;
+  const int g0 = wave * per, g1 = min(G, g0 + per);
+  const int me = xg.rank;
+  float pw[4];
+  if (wave == 0) {
 #pragma unroll
-  for (int g = 0; g < MAXG; ++g)
-    if (g < NG) av[g] = f4(A + g * 16);
-  if (wave == 0) {  // one uniform branch around the whole B-operand load block
-#pragma unroll
-    for (int g = 0; g < MAXG; ++g)
-      if (g < NG)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bv[g][e] = hb[(size_t)(g * 16 + q * 4 + e) * HP];
-  } else {
-#pragma unroll
-    for (int g = 0; g < MAXG; ++g)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bv[g][e] = 1.f;
-  }
-  __builtin_amdgcn_sched_barrier(0);  // all loads in flight together
-  // Destination offsets (and, in direct mode, the current values) resolved
-  // before the MFMAs so the epilogue is a pure store.
-  size_t off[4];
-  bool ok[4];
-  float pv[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (wave == 0) {  // C[c = q*4+i][j = jt*16 + r] -> dW2t[c][j]
-      const int c = q * 4 + i, j = jt * 16 + r;
-      ok[i] = c < C && j < H;
-      off[i] = OFF_W2 + (ok[i] ? c * H + j : 0);
-    } else if (wave == 1) {  // C[j = jt*16 + q*4+i][*] -> db1[j]
-      const int j = jt * 16 + q * 4 + i;
-      ok[i] = r == 0 && j < H;
-      off[i] = OFF_B1 + (j < H ? j : 0);
-    } else {  // C[c = q*4+i][*] -> db2[c]
-      const int c = q * 4 + i;
-      ok[i] = r == 0 && c < C;
-      off[i] = OFF_B2 + (c < C ? c : 0);
+    for (int i = 0; i < 4; ++i) {
+      const int j = jt * 16 + q4 * 4 + i;
+      pw[i] = p[OFF_W1 + (size_t)(j < H ? j : H - 1) * D + kt * 16 + r];
     }
-    if (DIRECT) pv[i] = p[off[i]];
   }
-  __builtin_amdgcn_sched_barrier(0);
-  // NB: padded batch columns of dz1T/dlT are zero, so multiplying by 1 is exact.
   f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+  constexpr int CH = 7;  // groups of 16 batch rows per load round (all in flight together)
+  for (int c0 = g0; c0 < g1; c0 += CH) {
+    float4 av[CH];
+    float xv[CH][4];
 #pragma unroll
-  for (int g = 0; g < MAXG; ++g) {
-    if (g < NG) {
-      acc0 = mfma16x16x4(av[g].x, bv[g][0], acc0);
-      acc1 = mfma16x16x4(av[g].y, bv[g][1], acc1);
-      acc0 = mfma16x16x4(av[g].z, bv[g][2], acc0);
-      acc1 = mfma16x16x4(av[g].w, bv[g][3], acc1);
+    for (int i = 0; i < CH; ++i) {
+      const int g = c0 + i;
+      if (g < g1) {  // wave-uniform
+        const int qq = g / NG, gg = g - qq * NG;
+        av[i] = f4(dz1A + ((size_t)qq * HP + jt * 16 + r) * BP + gg * 16 + q4 * 4);
+        const float* xq = x + (long long)(qq - me) * xstride + kt * 16 + r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int b = gg * 16 + q4 * 4 + e;  // rows >= B: dz1A is zero there
+          xv[i][e] = xq[(size_t)(b < B ? b : B - 1) * D];
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the round's loads in flight together
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      if (c0 + i < g1) {
+        acc0 = mfma16x16x4(av[i].x, xv[i][0], acc0);
+        acc1 = mfma16x16x4(av[i].y, xv[i][1], acc1);
+        acc0 = mfma16x16x4(av[i].z, xv[i][2], acc0);
+        acc1 = mfma16x16x4(av[i].w, xv[i][3], acc1);
+      }
     }
   }
-  float v[4];
+  f32x4 part;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = acc0[i] + acc1[i];
-  bool fail = false;
-  if constexpr (XW > 0) xg_exchange<XW>(xg, ep, off, ok, v, fail);
+  for (int i = 0; i < 4; ++i) part[i] = acc0[i] + acc1[i];
+  if (wave > 0) red[wave - 1][lane] = part;
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const f32x4 o = red[k][lane];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[i] += o[i];
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    if (ok[i] && !fail) {
-      if (DIRECT) p[off[i]] = pv[i] - lr * v[i];
-      else grad[off[i]] = v[i];
-    }
-  }
-  if constexpr (XW > 0) {
-    if (lane == 0) xg.epochs[bid * 4 + wave] = ep;
-    if (fail) atomicExch(xg.err, 1);
+    const int j = jt * 16 + q4 * 4 + i;
+    if (j < H) p[OFF_W1 + (size_t)j * D + kt * 16 + r] = pw[i] - lr * part[i];
   }
 }
 
@@ -545,13 +696,13 @@ void mlp_head_launch(const float* p_old, const float* grad, float lr, float* p_n
   if (grad) {
     if (!p_new || p_new == p_old) throw std::runtime_error("mlp_head: apply needs ping-pong p_new");
     hipLaunchKernelGGL((mlp_head_kernel<true, false>), dim3(B), dim3(64), 0, stream, p_old, grad,
-                       lr, p_new, labels, w, B, tr);
+                       lr, p_new, labels, w, B, tr, MlpXg{}, nullptr);
   } else if (tr) {
     hipLaunchKernelGGL((mlp_head_kernel<false, true>), dim3(B), dim3(64), 0, stream, p_old, p_old,
-                       0.f, nullptr, labels, w, B, tr);
+                       0.f, nullptr, labels, w, B, tr, MlpXg{}, nullptr);
   } else {
     hipLaunchKernelGGL((mlp_head_kernel<false, false>), dim3(B), dim3(64), 0, stream, p_old, p_old,
-                       0.f, nullptr, labels, w, B, tr);
+                       0.f, nullptr, labels, w, B, tr, MlpXg{}, nullptr);
   }
   DTFX_HIP_CHECK(hipGetLastError());
 }
@@ -615,6 +766,58 @@ void mlp_wgrad_xg_launch(float* p, float lr, const float* x, float* ws, int* ctr
   }
 #undef DTFX_WGW
 #undef DTFX_WGX
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+
+// Factor engine launches (see mlp_wgrad_factor_kernel).
+void mlp_head_xg_launch(const float* p, const int* labels, float* ws, float* dz1A, int B,
+                        hipStream_t stream, const MlpXg& xg, int world) {
+  using namespace mlp;
+  check_b(B);
+  if (xg.S < (long long)HP * (((B + 15) / 16) * 16))
+    throw std::runtime_error("mlp_head_xg: exchange slots smaller than the factor plane");
+  const Bufs w = make_bufs(ws, B);
+#define DTFX_HX(WW)                                                                            \
+  case WW:                                                                                     \
+    hipLaunchKernelGGL((mlp_head_kernel<false, false, WW>), dim3(B), dim3(64), 0, stream, p, p, \
+                       0.f, nullptr, labels, w, B, nullptr, xg, dz1A);                         \
+    break;
+  switch (world) {
+    DTFX_HX(2) DTFX_HX(3) DTFX_HX(4) DTFX_HX(5) DTFX_HX(6) DTFX_HX(7) DTFX_HX(8)
+    default:
+      throw std::runtime_error("mlp_head_xg: world must be 2..8");
+  }
+#undef DTFX_HX
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void mlp_wgrad_factor_launch(float* p, float lr, const float* x, long long xstride,
+                             const float* dz1A, float* ws, int* ctr, float* stats, int stats_ring,
+                             int B, hipStream_t stream, const MlpXg& xg, int world) {
+  using namespace mlp;
+  check_b(B);
+  if (stats && stats_ring < 1) throw std::runtime_error("mlp_wgrad: stats_ring < 1");
+  if (!ctr || !p || !dz1A) throw std::runtime_error("mlp_wgrad_factor: null buffer");
+  if (xg.S < NPARAM) throw std::runtime_error("mlp_wgrad_factor: exchange slots smaller than the model");
+  const Bufs w = make_bufs(ws, B);
+  dim3 grid(8 * HT * ((FT + 7) / 8) + HT), block(256);
+  const int NG = (B + 15) / 16;
+#define DTFX_WF(WW, NGT)                                                                       \
+  hipLaunchKernelGGL((mlp_wgrad_factor_kernel<WW, NGT>), grid, block, 0, stream, p, lr, x,     \
+                     xstride, dz1A, w, ctr, stats, stats_ring, B, xg)
+#define DTFX_WFW(WW)             \
+  case WW:                       \
+    if (NG == 7) DTFX_WF(WW, 7); \
+    else DTFX_WF(WW, 0);         \
+    break;
+  switch (world) {
+    DTFX_WFW(2) DTFX_WFW(3) DTFX_WFW(4) DTFX_WFW(5) DTFX_WFW(6) DTFX_WFW(7) DTFX_WFW(8)
+    default:
+      throw std::runtime_error("mlp_wgrad_factor: world must be 2..8");
+  }
+#undef DTFX_WFW
+#undef DTFX_WF
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

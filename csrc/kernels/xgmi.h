@@ -39,6 +39,19 @@ struct MlpXg {
   long long ticks;      // wait bound in s_memrealtime ticks (100 MHz)
 };
 constexpr int MLP_XG_EPOCHS = 1024;
+// epoch slots of the factor engine (mlp_head_kernel<.., XW> rows / mlp_wgrad_factor_kernel's
+// small-parameter waves); mlp_wgrad_kernel<.., XW> uses [0, 392)
+constexpr int MLP_XG_SMALL_EPOCH = 400;
+constexpr int MLP_XG_HEAD_EPOCH = 512;
+
+// Factor engine (sufficient-factor exchange): head launch that all-gathers the backprop
+// factors dz1 of every rank into dz1A [world][112][BP], then the weight-gradient launch that
+// forms the global dW1 from them and every rank's (resident) batch x, applying directly.
+void mlp_head_xg_launch(const float* p, const int* labels, float* ws, float* dz1A, int B,
+                        hipStream_t stream, const MlpXg& xg, int world);
+void mlp_wgrad_factor_launch(float* p, float lr, const float* x, long long xstride,
+                             const float* dz1A, float* ws, int* ctr, float* stats, int stats_ring,
+                             int B, hipStream_t stream, const MlpXg& xg, int world);
 
 void mlp_wgrad_xg_launch(float* p, float lr, const float* x, float* ws, int* ctr, float* stats,
                          int stats_ring, int B, hipStream_t stream, const MlpXg& xg, int world);

@@ -115,6 +115,36 @@ class XgmiAllReduce {
                         (hipStream_t)stream, xg, world_);
   }
 
+  MlpXg mlp_xg(double timeout_s) const {
+    MlpXg xg;
+    xg.peers = peers_;
+    xg.S = S_;
+    xg.rank = rank_;
+    xg.epochs = mlp_epochs_;
+    xg.err = err_;
+    xg.ticks = (long long)(timeout_s * 1e8);
+    return xg;
+  }
+
+  // Factor engine: head launch with the dz1 all-gather, then the global-dW1 launch.
+  void mlp_head(uintptr_t p, uintptr_t labels, uintptr_t ws, uintptr_t dz1A, int B,
+                uintptr_t stream, double timeout_s) {
+    if (!ready_) throw std::runtime_error("xgmi: open() the peer handles first");
+    if (mode_ != XG_LL_PUSH) throw std::runtime_error("xgmi: the factor exchange needs protocol push");
+    mlp_head_xg_launch((const float*)p, (const int*)labels, (float*)ws, (float*)dz1A, B,
+                       (hipStream_t)stream, mlp_xg(timeout_s), world_);
+  }
+
+  void mlp_wgrad_factor(uintptr_t p, float lr, uintptr_t x, long long xstride, uintptr_t dz1A,
+                        uintptr_t ws, uintptr_t ctr, uintptr_t stats, int ring, int B,
+                        uintptr_t stream, double timeout_s) {
+    if (!ready_) throw std::runtime_error("xgmi: open() the peer handles first");
+    if (mode_ != XG_LL_PUSH) throw std::runtime_error("xgmi: the factor exchange needs protocol push");
+    mlp_wgrad_factor_launch((float*)p, lr, (const float*)x, xstride, (const float*)dz1A,
+                            (float*)ws, (int*)ctr, (float*)stats, ring, B, (hipStream_t)stream,
+                            mlp_xg(timeout_s), world_);
+  }
+
   int error() {
     int e = 0;
     XG_CHECK(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost));
@@ -162,6 +192,13 @@ void register_xgmi(py::module_& m) {
       .def("mlp_wgrad", &dtfx::XgmiAllReduce::mlp_wgrad, py::arg("p"), py::arg("lr"), py::arg("x"),
            py::arg("ws"), py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"),
            py::arg("stream"), py::arg("timeout_s") = 2.0)
+      .def("mlp_head", &dtfx::XgmiAllReduce::mlp_head, py::arg("p"), py::arg("labels"),
+           py::arg("ws"), py::arg("dz1A"), py::arg("B"), py::arg("stream"),
+           py::arg("timeout_s") = 2.0)
+      .def("mlp_wgrad_factor", &dtfx::XgmiAllReduce::mlp_wgrad_factor, py::arg("p"),
+           py::arg("lr"), py::arg("x"), py::arg("xstride"), py::arg("dz1A"), py::arg("ws"),
+           py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"),
+           py::arg("timeout_s") = 2.0)
       .def("error", &dtfx::XgmiAllReduce::error)
       .def("close", &dtfx::XgmiAllReduce::close);
 }

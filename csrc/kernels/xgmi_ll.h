@@ -55,6 +55,35 @@ __device__ __forceinline__ float gather_sum(Base base, long long i, int rank, un
   return acc;
 }
 
+// Like gather_sum, but returns every peer's value (out[rank] = own): the all-gather form used
+// by the MLP factor exchange.
+template <int W, class Base>
+__device__ __forceinline__ void gather_all(Base base, long long i, int rank, unsigned epoch,
+                                           float own, long long ticks, float (&out)[W],
+                                           bool& fail) {
+  u64 w[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) w[j] = j == rank ? 0ull : load(base(j) + i);
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ready = true;
+#pragma unroll
+    for (int j = 0; j < W; ++j)
+      if (j != rank && (unsigned)(w[j] >> 32) != epoch) {
+        ready = false;
+        w[j] = load(base(j) + i);
+      }
+    if (ready) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      fail = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int j = 0; j < W; ++j) out[j] = j == rank ? own : __uint_as_float((unsigned)w[j]);
+}
+
 __device__ __forceinline__ float wait_one(const u64* p, unsigned epoch, long long ticks,
                                           bool& fail) {
   u64 w = load(p);

@@ -104,6 +104,30 @@ def step_xgmi(p, x, labels, ws: StepWorkspace, lr, comm, stats=True):
     comm.mlp_wgrad(p, lr, x, ws, stats)
 
 
+def factor_plane(B):
+    """Elements of one rank's dz1 plane in the factor engine's gather buffer ([112][BP])."""
+    return HP * ((B + 15) // 16) * 16
+
+
+def step_factor(p, x, labels, ws: StepWorkspace, lr, comm, dz1A, xstride, stats=True):
+    """One synchronous data-parallel SGD step by sufficient-factor exchange (``comm``: an
+    ``XgmiComm`` with protocol "push"; ``lr`` already divided by the world size).
+
+    The head launch all-gathers every rank's backprop factors dz1 [B, 100] into ``dz1A``
+    (zero-initialised [world, 112, BP]); every rank holds every rank's batch (rank q's at
+    ``x + (q - rank) * xstride`` elements), so the weight-gradient launch forms the GLOBAL
+    dW1 = sum_q dz1_q^T x_q locally and applies it -- 40 KB of factors per rank cross xGMI
+    instead of the 313 KB W1 gradient.  Three launches, like ``step_direct``."""
+    _check(x, labels, ws.B)
+    _check_flat(p)
+    if dz1A.numel() < comm.world_size * factor_plane(ws.B) or dz1A.dtype != torch.float32:
+        raise ValueError("dz1A must hold world * 112 * BP f32 values")
+    h, s = hip(), stream_handle()
+    h.mlp_fwd(ptr(p), 0, 0.0, 0, ptr(x), ptr(ws.buf), ws.B, s)
+    comm.mlp_head(p, labels, ws, dz1A)
+    comm.mlp_wgrad_factor(p, lr, x, xstride, dz1A, ws, stats)
+
+
 def step_grad(p_old, x, labels, ws: StepWorkspace, grad, prev_grad=None, lr=0.0, p_new=None,
               stats=True):
     """Forward/backward writing ``grad``; optionally first applies ``prev_grad``.

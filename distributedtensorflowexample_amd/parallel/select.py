@@ -123,12 +123,18 @@ def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_k
 
 
 def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mode="auto",
-                    xgmi_key="dtfx/xgmi/fused", verify_steps=20, time_steps=400):
-    """Data-parallel engine of the fused MLP trainer: ``("fused", XgmiComm)`` -- gradient
-    exchange inside the weight-gradient kernel -- or ``("allreduce", ar_comm)`` -- separate
-    all-reduce launch + deferred apply.  The fused engine must (on every rank) build, agree
-    with the all-reduce engine after ``verify_steps`` identical SGD steps, and be faster over
-    ``time_steps`` graph-replayed steps (max over ranks); else the all-reduce engine is kept.
+                    xgmi_key="dtfx/xgmi/fused", verify_steps=20, time_steps=400, x_all=None):
+    """Data-parallel engine of the fused MLP trainer, one of
+      ``("allreduce", ar_comm)`` -- flat gradient, separate all-reduce launch, deferred apply;
+      ``("fused", XgmiComm)``   -- gradient exchange inside the weight-gradient kernel;
+      ``("factor", XgmiComm)``  -- sufficient-factor exchange: the backprop factors dz1 are
+                                   all-gathered inside the head kernel and every rank forms
+                                   the global W1 gradient from them and every rank's batch
+                                   (needs ``x_all`` [world, n, 784], ``x = x_all[rank]``).
+    An xGMI engine must (on every rank) build, agree with the all-reduce engine after
+    ``verify_steps`` identical SGD steps, keep the replicas bit-identical, and (mode "auto") be
+    the fastest over ``time_steps`` graph-replayed steps (max over ranks); mode "fused" /
+    "factor" forces that engine once verified.  Every rank takes the same decision.
     Returns (kind, comm, {engine: us_per_step} or None)."""
     from ..train.fused_mlp import FusedMLPTrainer
 
@@ -137,47 +143,67 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
 
-    if world < 2 or world > 8:
+    if world < 2 or world > 8 or mode == "allreduce":
         return "allreduce", ar_comm, None
-    fc, err = None, ""
-    try:
-        fc = XgmiComm(rank, world, mlp_step.NPARAM, device=dev, key=xgmi_key, protocol="push")
-    except Exception as e:
-        err = repr(e)
-    if not agree(fc is not None):
-        if rank == 0:
-            print("[bench] fused xgmi engine unavailable (%s)" % err, file=sys.stderr)
+    kinds = {"auto": ["fused", "factor"], "fused": ["fused"], "factor": ["factor"]}[mode]
+    if x_all is None:
+        kinds = [k for k in kinds if k != "factor"]
+    comms = {}
+    for kind in kinds:
+        c, err = None, ""
+        try:
+            c = XgmiComm(rank, world, mlp_step.NPARAM, device=dev, key="%s/%s" % (xgmi_key, kind),
+                         protocol="push")
+        except Exception as e:
+            err = repr(e)
+        if agree(c is not None):
+            comms[kind] = c
+        elif rank == 0:
+            print("[bench] %s xgmi engine unavailable (%s)" % (kind, err), file=sys.stderr)
+    if not comms:
         return "allreduce", ar_comm, None
 
     def make(kind):
         if kind == "fused":
-            return FusedMLPTrainer(params, x, y, batch_size, lr, world_size=world, fused_comm=fc)
+            return FusedMLPTrainer(params, x, y, batch_size, lr, world_size=world,
+                                   fused_comm=comms[kind])
+        if kind == "factor":
+            return FusedMLPTrainer(params, None, y, batch_size, lr, world_size=world,
+                                   factor_comm=comms[kind], x_all=x_all, rank=rank)
         return FusedMLPTrainer(params, x, y, batch_size, lr, allreduce=ar_comm.allreduce_sum_,
                                world_size=world)
 
-    ok = True
-    try:
-        tf, ta = make("fused"), make("allreduce")
-        tf.run(verify_steps, use_graph=False)
-        ta.run(verify_steps, use_graph=False)
-        fc.check()
-        pf, pa = tf.flush(), ta.flush()
-        tol = 1e-4 * (1.0 + float(pa.abs().max()))
-        ok = bool(((pf - pa).abs().max() <= tol).item())
-        # replicas must stay bit-identical under the fused engine
-        chk = pf.double().sum().reshape(1).cpu()
-        ref = chk.clone()
-        dist.broadcast(ref, 0)
-        ok &= bool(torch.equal(chk, ref))
-    except Exception as e:
-        ok, err = False, repr(e)
-    if not agree(ok):
-        if rank == 0:
-            print("[bench] fused xgmi engine failed verification (%s)" % err, file=sys.stderr)
-        fc.destroy()
+    ta = make("allreduce")
+    ta.run(verify_steps, use_graph=False)
+    pa = ta.flush().clone()
+    trainers = {"allreduce": ta}
+    for kind in list(comms):
+        ok, err = True, ""
+        try:
+            tk = make(kind)
+            tk.run(verify_steps, use_graph=False)
+            comms[kind].check()
+            pk = tk.flush()
+            tol = 1e-4 * (1.0 + float(pa.abs().max()))
+            ok = bool(((pk - pa).abs().max() <= tol).item())
+            chk = pk.double().sum().reshape(1).cpu()  # replicas must stay bit-identical
+            ref = chk.clone()
+            dist.broadcast(ref, 0)
+            ok &= bool(torch.equal(chk, ref))
+        except Exception as e:
+            ok, err = False, repr(e)
+        if agree(ok):
+            trainers[kind] = tk
+        else:
+            if rank == 0:
+                print("[bench] %s xgmi engine failed verification (%s)" % (kind, err),
+                      file=sys.stderr)
+            comms.pop(kind).destroy()
+    if not comms:
         return "allreduce", ar_comm, None
-    if mode == "fused":
-        return "fused", fc, None
+    if mode != "auto":
+        kind = next(iter(comms))
+        return kind, comms[kind], None
 
     def timed(tr):
         tr.run(50)  # warm (captures the graphs)
@@ -191,18 +217,22 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
         return float(dt.item())
 
-    probe = {"fused": float("inf"), "allreduce": float("inf")}
+    names = sorted(trainers)  # same order on every rank
+    probe = {k: float("inf") for k in names}
     for _ in range(2):
-        probe["fused"] = min(probe["fused"], timed(tf))
-        probe["allreduce"] = min(probe["allreduce"], timed(ta))
-    fc.check()
+        for k in names:
+            probe[k] = min(probe[k], timed(trainers[k]))
+    for c in comms.values():
+        c.check()
     probe = {k: round(v, 2) for k, v in probe.items()}
-    use_f = probe["fused"] < probe["allreduce"]
+    best = min(names, key=lambda k: (probe[k], k))  # max-reduced: identical everywhere
     if rank == 0:
         print("[bench] MLP step engine probe (us/step, max over ranks): %s -> %s"
-              % (probe, "fused" if use_f else "allreduce"), file=sys.stderr)
-    del tf, ta
-    if use_f:
-        return "fused", fc, probe
-    fc.destroy()
-    return "allreduce", ar_comm, probe
+              % (probe, best), file=sys.stderr)
+    del trainers
+    for k in list(comms):
+        if k != best:
+            comms.pop(k).destroy()
+    if best == "allreduce":
+        return "allreduce", ar_comm, probe
+    return best, comms[best], probe

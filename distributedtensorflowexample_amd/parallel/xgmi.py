@@ -55,6 +55,24 @@ class XgmiComm:
                           ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B,
                           torch.cuda.current_stream().cuda_stream, self.timeout_s)
 
+    def mlp_head(self, p, labels, ws, dz1A):
+        """Factor engine: MLP head launch that also all-gathers every rank's backprop factors
+        dz1 into ``dz1A`` [world, 112, BP] (protocol "push"); see ``ops.mlp_step.step_factor``."""
+        from ..ops._ext import ptr
+
+        self._h.mlp_head(ptr(p), ptr(labels), ptr(ws.buf), ptr(dz1A), ws.B,
+                         torch.cuda.current_stream().cuda_stream, self.timeout_s)
+
+    def mlp_wgrad_factor(self, p, lr, x, xstride, dz1A, ws, stats=True):
+        """Factor engine: global dW1 from the gathered factors and every rank's batch
+        (``x`` = this rank's batch, rank q's at ``x + (q - rank) * xstride`` elements),
+        small-parameter gradients exchanged, SGD applied in place."""
+        from ..ops._ext import ptr
+
+        self._h.mlp_wgrad_factor(ptr(p), float(lr), ptr(x), int(xstride), ptr(dz1A), ptr(ws.buf),
+                                 ptr(ws.ctr), ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B,
+                                 torch.cuda.current_stream().cuda_stream, self.timeout_s)
+
     def broadcast_(self, t, root=0):
         """Broadcast as a sum with zeros off the root (small control-path use)."""
         if self.rank != root:

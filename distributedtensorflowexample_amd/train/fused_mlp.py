@@ -18,6 +18,11 @@ a host->GPU feed of 317 KB and ~14 tiny TF kernels.  Here:
   exchange is fused into ``mlp_wgrad``'s epilogue (LL words pushed straight to
   the peers, gathered, summed in rank order and applied in the same launch):
   three launches per data-parallel step, no pending gradient;
+* or, with ``factor_comm`` (also protocol "push") and ``x_all`` [world, n, 784]
+  -- every rank's deterministic batch stream resident on every GPU, as every
+  reference process loads the whole dataset (main.py:43-44) -- the ranks
+  all-gather only the backprop factors dz1 (40 KB) inside ``mlp_head`` and
+  each forms the global W1 gradient itself (sufficient-factor exchange);
 * ``global_step`` is a device counter advanced by the kernels (AssignAdd of
   worker.py:32,141); loss/accuracy land in a device ring read back lazily.
 
@@ -38,7 +43,7 @@ from ..ops import mlp_step, optim
 class FusedMLPTrainer:
     def __init__(self, params, x, labels, batch_size=100, learning_rate=0.001, allreduce=None,
                  world_size=1, stats_ring=4096, global_step=0, max_graph_steps=1024,
-                 fused_comm=None):
+                 fused_comm=None, factor_comm=None, x_all=None, rank=0):
         if not params.is_cuda:
             raise ValueError("FusedMLPTrainer runs on the GPU; use the generic path on CPU")
         if params.numel() != mlp_step.NPARAM:
@@ -51,7 +56,22 @@ class FusedMLPTrainer:
         self.fused_comm = fused_comm
         if fused_comm is not None and (allreduce is not None or world_size < 2):
             raise ValueError("fused_comm replaces allreduce and needs world_size >= 2")
+        self.factor_comm = factor_comm
+        self.xstride = 0
+        if factor_comm is not None:
+            if fused_comm is not None or allreduce is not None or world_size < 2:
+                raise ValueError("factor_comm replaces allreduce/fused_comm and needs world >= 2")
+            if (x_all is None or x_all.dim() != 3 or x_all.shape[0] != world_size
+                    or not x_all.is_contiguous() or x_all.dtype != torch.float32
+                    or x_all.device != self.device):
+                raise ValueError("factor_comm needs x_all: contiguous f32 [world, n, 784] on the GPU")
+            x = x_all[int(rank)]  # a view: the other ranks' batches sit at +/- xstride
+            self.xstride = x_all.stride(0)
+            self.dz1A = torch.zeros(world_size * mlp_step.factor_plane(int(batch_size)),
+                                    device=self.device, dtype=torch.float32)
         x = x.reshape(-1, mlp_step.D).to(self.device, torch.float32).contiguous()
+        if factor_comm is not None and x.data_ptr() != x_all[int(rank)].data_ptr():
+            raise ValueError("x_all slice must stay a view")
         labels = labels.reshape(-1).to(self.device, torch.int32).contiguous()
         self.nbatches = x.shape[0] // self.B
         if self.nbatches < 1:
@@ -72,7 +92,8 @@ class FusedMLPTrainer:
     @property
     def direct(self):
         """SGD apply fused into the backward kernel (one GPU, or the fused xGMI exchange)."""
-        return self.fused_comm is not None or (self.allreduce is None and self.world_size == 1)
+        return (self.fused_comm is not None or self.factor_comm is not None
+                or (self.allreduce is None and self.world_size == 1))
 
     @property
     def params(self):
@@ -101,6 +122,10 @@ class FusedMLPTrainer:
     def _step_launches(self):
         xb, yb = self.batch(self.pos)
         self.pos = (self.pos + 1) % self.nbatches
+        if self.factor_comm is not None:
+            mlp_step.step_factor(self.bufs[self.cur], xb, yb, self.ws, self.lr / self.world_size,
+                                 self.factor_comm, self.dz1A, self.xstride)
+            return
         if self.fused_comm is not None:
             mlp_step.step_xgmi(self.bufs[self.cur], xb, yb, self.ws, self.lr / self.world_size,
                                self.fused_comm)

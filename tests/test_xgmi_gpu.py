@@ -171,3 +171,65 @@ def test_fused_mlp_exchange_matches_allreduce_engine(gpu, world):
         p.join(60)
     for r, ok, msg in res:
         assert ok, (r, msg)
+
+
+def _factor_worker(rank, world, port, q, B):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from distributedtensorflowexample_amd.data.synthetic import mnist_like_device
+        from distributedtensorflowexample_amd.models.mlp import init_params
+        from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+        from distributedtensorflowexample_amd.train.fused_mlp import FusedMLPTrainer
+
+        dev = torch.device("cuda:0")
+        params = init_params(dev, seed=7)
+        n = 20 * B
+        # every rank holds every rank's dataset; rank q trains on x_all[q]
+        x_all = torch.stack([mnist_like_device(n, seed=50 + r, device=dev)[0]
+                             for r in range(world)]).contiguous()
+        y = mnist_like_device(n, seed=50 + rank, device=dev)[1]
+        fc = XgmiComm(rank, world, params.numel(), device=dev, key="s/push", protocol="push")
+        ref = XgmiComm(rank, world, params.numel(), device=dev, key="s/flag", protocol="flag")
+        lr = 0.05
+        tf = FusedMLPTrainer(params, None, y, B, lr, world_size=world, factor_comm=fc,
+                             x_all=x_all, rank=rank)
+        ta = FusedMLPTrainer(params, x_all[rank], y, B, lr, world_size=world,
+                             allreduce=ref.allreduce_sum_)
+        tf.run(7, use_graph=False)   # eager
+        tf.run(33, use_graph=True)   # graph replays (device-side epochs), crosses an epoch
+        ta.run(7, use_graph=False)
+        ta.run(33, use_graph=True)
+        fc.check()
+        ref.check()
+        pf, pa = tf.flush(), ta.flush()
+        err = float((pf - pa).abs().max())
+        moved = float((pf - params).abs().max())
+        chk = pf.double().sum().reshape(1).cpu()
+        r0 = chk.clone()
+        dist.broadcast(r0, 0)
+        ok = err <= 1e-4 and moved > 1e-3 and torch.equal(chk, r0) and tf.global_step() == 40
+        q.put((rank, ok, "err %.3g moved %.3g step %d" % (err, moved, tf.global_step())))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, False, repr(e)))
+
+
+@pytest.mark.parametrize("world,B", [(2, 100), (3, 100), (2, 64)])
+def test_factor_mlp_exchange_matches_allreduce_engine(gpu, world, B):
+    """Sufficient-factor engine (dz1 all-gathered in the head kernel, global W1 gradient
+    formed on every rank from every rank's batch) follows the all-reduce engine's SGD
+    trajectory, with bit-identical replicas."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_factor_worker, args=(r, world, port, q, B)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    for r, ok, msg in res:
+        assert ok, (r, msg)
