@@ -76,6 +76,13 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
+// tanh(u) = 1 - 2 / (1 + e^{2u}): one v_exp_f32 + one v_rcp_f32 (libm tanhf is a long
+// branchy sequence, and GEMM epilogues evaluate it per output element).  Saturates
+// correctly (e^{2u} -> inf gives 1, -> 0 gives -1); absolute error ~1e-7.
+__device__ __forceinline__ float fast_tanh(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u));
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));

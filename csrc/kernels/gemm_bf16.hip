@@ -60,13 +60,16 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
   return __builtin_bit_cast(unsigned short, b);
 }
 
+// GELU (tanh form) and its derivative on fast_tanh: epilogue VALU work per output element
+// is ~10 instructions instead of libm tanhf's ~40 (measured: it set the time of the
+// GELU-grad dgrad GEMM of BERT's FFN).
 __device__ __forceinline__ float gelu_f(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+  return 0.5f * x * (1.f + fast_tanh(k0 * (x + k1 * x * x * x)));
 }
 __device__ __forceinline__ float gelu_grad_f(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float th = tanhf(k0 * (x + k1 * x * x * x));
+  const float th = fast_tanh(k0 * (x + k1 * x * x * x));
   return 0.5f * (1.f + th) + 0.5f * x * (1.f - th * th) * k0 * (1.f + 3.f * k1 * x * x);
 }
 
@@ -403,6 +406,30 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
 #pragma unroll
   for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
   for (int h = 0; h < WM / 32; ++h) {
+    // (issued before the slab's LDS transpose, so their latency overlaps it)
+    // Side inputs (bias / aux_in / residual / C_old) of the slab's 4 row groups are all
+    // loaded before any is used: one memory round trip per 32-row slab instead of one per
+    // 8-row group (the loads used to sit between dependent compute and stores).
+    bool full[4], live[4];
+    int mm[4], nn[4];
+    bf16x8 a8[4], r8[4];
+    f32x4 c0[4], c1[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
+      mm[it] = m0 + wm * WM + h * 32 + rr;
+      nn[it] = n0 + wn * 64 + cg;
+      live[it] = mm[it] < M && nn[it] < N;
+      full[it] = live[it] && nn[it] + 8 <= N;  // N % 8 != 0 only with a ragged last group
+      const int ms = live[it] ? mm[it] : 0, ns = full[it] ? nn[it] : 0;
+      if (e.act_grad) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)ms * e.ld_aux + ns];
+      if (e.residual) r8[it] = *(const bf16x8*)&e.residual[(size_t)ms * e.ld_res + ns];
+      if (OUT_F32 && e.beta != 0.f && gridDim.y == 1) {  // (split-K adds atomically)
+        const float* C = (const float*)Cv + (size_t)ms * ldc + ns;
+        c0[it] = *(const f32x4*)C;
+        c1[it] = *(const f32x4*)(C + 4);
+      }
+    }
     // static accumulator indices only (a runtime acc[2h+ii] index would put acc in scratch)
 #pragma unroll
     for (int t = 0; t < TM; ++t)
@@ -428,18 +455,16 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
-      const int m = m0 + wm * WM + h * 32 + rr;
-      const int n = n0 + wn * 64 + cg;
+      const int m = mm[it], n = nn[it];
       float v[8];
       *(f32x4*)&v[0] = *(const f32x4*)&ep[rr * EP_LD + cg];
       *(f32x4*)&v[4] = *(const f32x4*)&ep[rr * EP_LD + cg + 4];
-      if (m >= M || n >= N) continue;
-      const bool full = n + 8 <= N;  // N % 8 != 0 only reaches here with a ragged last group
+      if (!live[it]) continue;
       float bn[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) bn[u] = 0.f;
       if (e.bias) {
-        if (full) {
+        if (full[it]) {
           *(f32x4*)&bn[0] = *(const f32x4*)&e.bias[n];
           *(f32x4*)&bn[4] = *(const f32x4*)&e.bias[n + 4];
         } else {
@@ -448,7 +473,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = e.alpha * v[u] + bn[u];
-      if (full) {
+      if (full[it]) {
         if (e.aux_out) {
           bf16x8 o;
 #pragma unroll
@@ -463,17 +488,15 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
           for (int u = 0; u < 8; ++u) v[u] = fmaxf(v[u], 0.f);
         }
         if (e.act_grad) {
-          const bf16x8 a8 = *(const bf16x8*)&e.aux_in[(size_t)m * e.ld_aux + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const float uu = bf2f((unsigned short)a8[u]);
+            const float uu = bf2f((unsigned short)a8[it][u]);
             v[u] *= (e.act_grad == 1) ? gelu_grad_f(uu) : (uu > 0.f ? 1.f : 0.f);
           }
         }
         if (e.residual) {
-          const bf16x8 r8 = *(const bf16x8*)&e.residual[(size_t)m * e.ld_res + n];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[u]);
+          for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[it][u]);
         }
         if (e.colsum || e.colsq) {
 #pragma unroll
@@ -485,11 +508,10 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
         if (OUT_F32) {
           float* C = (float*)Cv + (size_t)m * ldc + n;
           if (e.beta != 0.f) {
-            const f32x4 c0 = *(const f32x4*)C, c1 = *(const f32x4*)(C + 4);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              v[u] += e.beta * c0[u];
-              v[u + 4] += e.beta * c1[u];
+              v[u] += e.beta * c0[it][u];
+              v[u + 4] += e.beta * c1[it][u];
             }
           }
           *(f32x4*)C = *(f32x4*)&v[0];
@@ -657,8 +679,15 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   if (auto_split) {  // fill the 256 CUs when the output has few tiles and K is deep
     splitk = 1;
-    if (batch == 1 && out_f32 && !colsum && !bias && !act && !act_grad && !residual && !aux_out && (beta == 0.f || beta == 1.f))
-      while (tiles * splitk < 256 && nkt / (splitk * 2) >= 8) splitk *= 2;
+    // Fill the resident block slots in ONE wave: the largest split with tiles * splitk <=
+    // slots (cfg 0: 2 blocks/CU x 256 CUs; else 1/CU).  Measured on the BERT-base weight
+    // gradients (tools/gemm_sweep.py): 144 tiles x 3 = 432 blocks 110 us vs x 2 (288,
+    // unbalanced) 146 us and x 4 (576, a second partial wave) 154 us; 108 x 4 and 36 x 12
+    // likewise the fastest of 1..16.
+    if (batch == 1 && out_f32 && !colsum && !bias && !act && !act_grad && !residual && !aux_out && (beta == 0.f || beta == 1.f)) {
+      const int slots = cfg == 0 ? 512 : 256;
+      if (tiles < slots / 2) splitk = std::max(1, std::min(slots / tiles, nkt / 8));
+    }
   }
   if (splitk > 1) {
     if (batch > 1) throw std::runtime_error("gemm_bf16: split-K with batch > 1 is not supported");
@@ -736,8 +765,8 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
     const int tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
     const int nkt = (K + 63) / 64;
     if (splitk <= 0) {
-      splitk = 1;
-      while (tiles * splitk < 512 && nkt / (splitk * 2) >= 4) splitk *= 2;
+      splitk = 1;  // one wave of the 512 resident 128x128 slots (see gemm_bf16_launch)
+      if (tiles < 256) splitk = std::max(1, std::min(512 / tiles, nkt / 4));
     }
     const int ldo = ldw > 0 ? ldw : Nn;  // dW row stride (the padded fwd weight layout)
     if (ldo < Nn || ldo % 8) throw std::runtime_error("conv_bf16: wgrad ld must be >= KH*KW*C, % 8");
@@ -755,6 +784,45 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
 }
 
 // Column sums of a bf16 matrix (bias gradients): out[n] (+)= sum_m G[m][n], f32.
+// Vector form (ldg % 8 == 0, 16-B aligned G): each thread owns 8 columns and streams rows
+// with 16-B loads, 4 rows in flight; blockIdx.y splits the rows (partials combined with one
+// atomic per column and row group).
+__global__ __launch_bounds__(256) void colsum8_bf16_kernel(const unsigned short* __restrict__ G,
+                                                           int M, int N, int ldg,
+                                                           float* __restrict__ out, float beta) {
+  const int ch = blockIdx.x * 256 + threadIdx.x, n0 = ch * 8;
+  if (n0 >= N) return;
+  float s[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s[u] = 0.f;
+  const int per = (M + gridDim.y - 1) / gridDim.y;
+  const int m0 = blockIdx.y * per, m1 = min(M, m0 + per);
+  int m = m0;
+  for (; m + 4 <= m1; m += 4) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = *(const bf16x8*)(G + (size_t)(m + i) * ldg + n0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += bf2f((unsigned short)v[i][u]);
+  }
+  for (; m < m1; ++m) {
+    const bf16x8 v = *(const bf16x8*)(G + (size_t)m * ldg + n0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += bf2f((unsigned short)v[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int n = n0 + u;
+    if (n < N) {
+      if (gridDim.y == 1) out[n] = s[u] + (beta != 0.f ? beta * out[n] : 0.f);
+      else unsafeAtomicAdd(out + n, s[u]);
+    }
+  }
+}
+
+// Scalar form for unaligned / odd-stride inputs.
 __global__ __launch_bounds__(256) void colsum_bf16_kernel(const unsigned short* __restrict__ G, int M,
                                                           int N, int ldg, float* __restrict__ out,
                                                           float beta) {
@@ -776,16 +844,22 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const unsigned short* 
 void colsum_bf16_launch(const void* G, int M, int N, int ldg, float* out, float beta,
                         hipStream_t stream) {
   if (N <= 0) return;
-  const int gx = (N + 63) / 64;
-  // Split rows over blocks when the matrix is tall; the caller's out is pre-scaled then.
+  const bool vec = ldg % 8 == 0 && ((uintptr_t)G & 15) == 0 && ldg >= ((N + 7) / 8) * 8;
+  const int gx = vec ? (N + 2047) / 2048 : (N + 63) / 64;
+  // Split rows over blocks when the matrix is tall (>= ~1024 blocks in flight); the
+  // caller's out is pre-scaled then.
   int gy = 1;
-  if (M >= 4096) gy = std::min(64, std::max(1, 1024 / gx));
+  if (M >= 512 && (beta == 0.f || beta == 1.f)) gy = std::min(std::max(1, M / (vec ? 64 : 32)), std::max(1, 1024 / gx));
   if (gy > 1) {
     if (beta == 0.f) DTFX_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * N, stream));
     else if (beta != 1.f) throw std::runtime_error("colsum_bf16: beta must be 0 or 1 for tall inputs");
   }
-  hipLaunchKernelGGL(colsum_bf16_kernel, dim3(gx, gy), dim3(256), 0, stream,
-                     (const unsigned short*)G, M, N, ldg, out, beta);
+  if (vec)
+    hipLaunchKernelGGL(colsum8_bf16_kernel, dim3(gx, gy), dim3(256), 0, stream,
+                       (const unsigned short*)G, M, N, ldg, out, beta);
+  else
+    hipLaunchKernelGGL(colsum_bf16_kernel, dim3(gx, gy), dim3(256), 0, stream,
+                       (const unsigned short*)G, M, N, ldg, out, beta);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

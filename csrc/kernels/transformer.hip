@@ -134,6 +134,10 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
 // dgamma += sum dy * xhat, dbeta += sum dy (per block in registers, then atomics)
 // optional dres: dx += dres (the residual branch gradient, fused)
+// NC = ceil(H / 512) column chunks of 8 per lane.  Each wave streams rows r0+wave, +4, ...
+// with the NEXT row's x / dy / dres loads issued before the current row is reduced
+// (software pipeline: one memory round trip per row instead of two) and gamma hoisted.
+template <int NC>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(
     int T, int H, int rows_per_block, const unsigned short* __restrict__ dy,
     const unsigned short* __restrict__ x, const float* __restrict__ mean_in,
@@ -143,47 +147,67 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(
   __shared__ float red[3][4][2048 / 4 + 4];  // [dgamma|dbeta|dxsum][wave][...], H <= 2048
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nch = H >> 3;
-  float dg[4][8], db[4][8], ds[4][8];
+  float dg[NC][8], db[NC][8], ds[NC][8], gm[NC][8];
 #pragma unroll
-  for (int c = 0; c < 4; ++c)
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) dg[c][u] = db[c][u] = ds[c][u] = 0.f;
+    for (int u = 0; u < 8; ++u) {
+      dg[c][u] = db[c][u] = ds[c][u] = 0.f;
+      gm[c][u] = ch < nch ? gamma[ch * 8 + u] : 0.f;
+    }
+  }
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(T, r0 + rows_per_block);
-  for (int row = r0 + wave; row < r1; row += 4) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float g[4][8], xh[4][8], dyv[4][8];
+  bf16x8 xb[NC], yb[NC], rb[NC];
+  float mean = 0.f, rstd = 0.f;
+  auto load = [&](int row) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ch = min(lane + 64 * c, nch - 1);  // clamped: masked at use
+      xb[c] = *(const bf16x8*)(x + (size_t)row * H + ch * 8);
+      yb[c] = *(const bf16x8*)(dy + (size_t)row * H + ch * 8);
+      if (dres) rb[c] = *(const bf16x8*)(dres + (size_t)row * H + ch * 8);
+    }
+    mean = mean_in[row];
+    rstd = rstd_in[row];
+  };
+  int row = r0 + wave;
+  if (row < r1) load(row);
+  for (; row < r1; row += 4) {
+    float xh[NC][8], g[NC][8], dyv[NC][8], rv[NC][8];
     float s1 = 0.f, s2 = 0.f;
+    const float mu = mean, rs = rstd;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int ch = lane + 64 * c;
-      if (ch < nch) {
-        float xv[8];
-        unpack8(*(const bf16x8*)(x + (size_t)row * H + ch * 8), xv);
-        unpack8(*(const bf16x8*)(dy + (size_t)row * H + ch * 8), dyv[c]);
+    for (int c = 0; c < NC; ++c) {
+      const bool ok = lane + 64 * c < nch;
+      float xv[8];
+      unpack8(xb[c], xv);
+      unpack8(yb[c], dyv[c]);
+      if (dres) unpack8(rb[c], rv[c]);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          xh[c][u] = (xv[u] - mean) * rstd;
-          g[c][u] = dyv[c][u] * gamma[ch * 8 + u];
-          s1 += g[c][u];
-          s2 += g[c][u] * xh[c][u];
-          dg[c][u] += dyv[c][u] * xh[c][u];
-          db[c][u] += dyv[c][u];
-        }
+      for (int u = 0; u < 8; ++u) {
+        if (!ok) dyv[c][u] = 0.f;
+        xh[c][u] = (xv[u] - mu) * rs;
+        g[c][u] = dyv[c][u] * gm[c][u];
+        s1 += g[c][u];
+        s2 += g[c][u] * xh[c][u];
+        dg[c][u] += dyv[c][u] * xh[c][u];
+        db[c][u] += dyv[c][u];
       }
     }
+    if (row + 4 < r1) load(row + 4);  // next row in flight during the reductions
     s1 = wave_sum(s1) / H;
     s2 = wave_sum(s2) / H;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < NC; ++c) {
       const int ch = lane + 64 * c;
       if (ch < nch) {
-        float o[8], rv[8];
-        if (dres) unpack8(*(const bf16x8*)(dres + (size_t)row * H + ch * 8), rv);
+        float o[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          o[u] = rstd * (g[c][u] - s1 - xh[c][u] * s2);
-          if (dres) o[u] += rv[u];
+          o[u] = rs * (g[c][u] - s1 - xh[c][u] * s2);
+          if (dres) o[u] += rv[c][u];
           ds[c][u] += o[u];
         }
         *(bf16x8*)(dx + (size_t)row * H + ch * 8) = pack8(o);
@@ -194,7 +218,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(
   for (int part = 0; part < 4; ++part) {  // H/4 columns per pass through the LDS buffer
     __syncthreads();
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < NC; ++c) {
       const int ch = lane + 64 * c;
       if (ch < nch)
 #pragma unroll
@@ -284,36 +308,79 @@ __global__ __launch_bounds__(256) void embed_ln_fwd_kernel(
 __global__ __launch_bounds__(256) void embed_word_bwd_kernel(int T, int H, const int* __restrict__ ids,
                                                              const unsigned short* __restrict__ dx,
                                                              float* __restrict__ dword) {
+  // one row per wave; lane l owns columns l, l + 64, ...: every wave-wide atomic covers one
+  // contiguous 256-B segment (four full 64-B requests at the memory side) instead of 64
+  // lanes scattered 32 B apart
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= T) return;
-  const int nch = H >> 3;
   float* dst = dword + (size_t)ids[row] * H;
-  for (int ch = lane; ch < nch; ch += 64) {
-    float v[8];
-    unpack8(*(const bf16x8*)(dx + (size_t)row * H + ch * 8), v);
+  const unsigned short* src = dx + (size_t)row * H;
+  constexpr int U = 12;  // loads in flight per lane (H = 768: the whole row)
+  for (int c0 = 0; c0 < H; c0 += 64 * U) {
+    float v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) unsafeAtomicAdd(dst + ch * 8 + u, v[u]);
+    for (int u = 0; u < U; ++u) {
+      const int col = c0 + u * 64 + lane;
+      v[u] = col < H ? bf(src[col]) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int col = c0 + u * 64 + lane;
+      if (col < H) unsafeAtomicAdd(dst + col, v[u]);
+    }
   }
 }
 
-// position / token-type gradients: block per position s sums the B rows with that
-// position (no atomics for dpos), type partials then one atomic per column.
-__global__ __launch_bounds__(256) void embed_pos_type_bwd_kernel(
+// position / token-type gradients: one 1024-thread block per position s; 8 row streams x
+// 128 threads of 8 columns (16-B loads, 4 rows in flight) fold into LDS with ds_add_f32,
+// then thread i writes column i: dpos row s has a single writer (no atomics), and the
+// token-type sums leave as lane-contiguous atomics (S adders per address).
+__global__ __launch_bounds__(1024) void embed_pos_type_bwd_kernel(
     int Bn, int S, int H, const int* __restrict__ tt, const unsigned short* __restrict__ dx,
     float* __restrict__ dpos, float* __restrict__ dtype_) {
-  const int s = blockIdx.x;
-  for (int col = threadIdx.x; col < H; col += 256) {
-    float acc = 0.f, t0 = 0.f, t1 = 0.f;
-    for (int b = 0; b < Bn; ++b) {
-      const int row = b * S + s;
-      const float v = bf(dx[(size_t)row * H + col]);
-      acc += v;
-      if (tt && tt[row]) t1 += v;
-      else t0 += v;
+  __shared__ float red[3][2048];
+  const int s = blockIdx.x, stream = threadIdx.x >> 7, t = threadIdx.x & 127;
+  const int nch = H >> 3;
+  for (int i = threadIdx.x; i < 3 * H; i += 1024) red[i / H][i % H] = 0.f;
+  __syncthreads();
+  for (int ch = t; ch < nch; ch += 128) {
+    float acc[8], t1[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = t1[u] = 0.f;
+    for (int b0 = stream; b0 < Bn; b0 += 32) {
+      bf16x8 v[4];
+      bool one[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = b0 + 8 * i;
+        const int row = (b < Bn ? b : 0) * S + s;
+        v[i] = *(const bf16x8*)(dx + (size_t)row * H + ch * 8);
+        one[i] = b < Bn && tt && tt[row];
+        if (b >= Bn) v[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float f[8];
+        unpack8(v[i], f);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          acc[u] += f[u];
+          t1[u] += one[i] ? f[u] : 0.f;
+        }
+      }
     }
-    dpos[(size_t)s * H + col] += acc;
-    unsafeAtomicAdd(dtype_ + col, t0);
-    unsafeAtomicAdd(dtype_ + H + col, t1);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      atomicAdd(&red[0][ch * 8 + u], acc[u]);
+      atomicAdd(&red[2][ch * 8 + u], t1[u]);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < H; i += 1024) {
+    const float a = red[0][i], one = red[2][i];
+    dpos[(size_t)s * H + i] += a;
+    unsafeAtomicAdd(dtype_ + i, a - one);
+    unsafeAtomicAdd(dtype_ + H + i, one);
   }
 }
 
@@ -331,14 +398,29 @@ constexpr int LDP = SP * 2 + 16;   // 272 B
 constexpr int QB = SP * LDQ;       // 18432 B
 constexpr int PB = SP * LDP;       // 34816 B
 
-// Load a [S][64] head slice (row stride ld elements) into LDS, zero rows >= S.
-__device__ __forceinline__ void load_head(char* dst, const unsigned short* src, int ld, int S) {
-  for (int i = threadIdx.x; i < SP * 8; i += 256) {
-    const int r = i >> 3, c = i & 7;
-    bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (r < S) v = *(const bf16x8*)(src + (size_t)r * ld + c * 8);
-    *(bf16x8*)(dst + r * LDQ + c * 16) = v;
-  }
+// Load N [S][64] head slices (row stride ld[i] elements) into LDS, zero rows >= S.  All
+// 4N 16-B loads of a thread are issued before the first LDS store (one memory round trip
+// instead of 4N dependent load -> store pairs).
+template <int N>
+__device__ __forceinline__ void load_heads(char* const (&dst)[N], const unsigned short* const (&src)[N],
+                                           const int (&ld)[N], int S) {
+  constexpr int PER = SP * 8 / 256;  // 16-B chunks per thread per head
+  bf16x8 v[N][PER];
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + 256 * k, r = i >> 3, c = i & 7;
+      v[n][k] = *(const bf16x8*)(src[n] + (size_t)min(r, S - 1) * ld[n] + c * 8);
+    }
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + 256 * k, r = i >> 3, c = i & 7;
+      if (r >= S) v[n][k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *(bf16x8*)(dst[n] + r * LDQ + c * 16) = v[n][k];
+    }
 }
 }  // namespace at
 
@@ -354,9 +436,12 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_kernel(
   const int b = blockIdx.x / nh, h = blockIdx.x % nh;
   const int Hd = nh * D, ld = 3 * Hd;
   const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
-  at::load_head(Qs, base, ld, S);
-  at::load_head(Ks, base + Hd, ld, S);
-  at::load_head(Vs, base + 2 * Hd, ld, S);
+  {
+    char* const dst[3] = {Qs, Ks, Vs};
+    const unsigned short* const src[3] = {base, base + Hd, base + 2 * Hd};
+    const int lds[3] = {ld, ld, ld};
+    at::load_heads<3>(dst, src, lds, S);
+  }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int cl = lane & 15, rg = (lane >> 4) * 4;
@@ -447,10 +532,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(
   const int b = blockIdx.x / nh, h = blockIdx.x % nh;
   const int Hd = nh * D, ld = 3 * Hd;
   const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
-  at::load_head(Qs, base, ld, S);
-  at::load_head(Ks, base + Hd, ld, S);
-  at::load_head(Vs, base + 2 * Hd, ld, S);
-  at::load_head(dOs, dout + (size_t)b * S * Hd + h * D, Hd, S);
+  {
+    char* const dst[4] = {Qs, Ks, Vs, dOs};
+    const unsigned short* const src[4] = {base, base + Hd, base + 2 * Hd,
+                                          dout + (size_t)b * S * Hd + h * D};
+    const int lds[4] = {ld, ld, ld, Hd};
+    at::load_heads<4>(dst, src, lds, S);
+  }
   {  // D = rowsum(dO * O): 2 threads per row, 32 columns each
     const int r = threadIdx.x >> 1, half = threadIdx.x & 1;
     float s = 0.f;
@@ -741,9 +829,16 @@ void layernorm_bwd_launch(int T, int H, const void* dy, const void* x, const flo
   check_h(H);
   if (T <= 0) return;
   const int rpb = T >= 8192 ? 32 : 16;  // >= 256 blocks for BERT-size inputs
-  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3((T + rpb - 1) / rpb), dim3(256), 0, s, T, H, rpb,
-                     (const unsigned short*)dy, (const unsigned short*)x, mean, rstd, gamma,
-                     (const unsigned short*)dres, (unsigned short*)dx, dgamma, dbeta, dxsum);
+  const int nc = (H / 8 + 63) / 64;
+#define DTFX_LNB(NC_)                                                                           \
+  hipLaunchKernelGGL(layernorm_bwd_kernel<NC_>, dim3((T + rpb - 1) / rpb), dim3(256), 0, s, T, H, \
+                     rpb, (const unsigned short*)dy, (const unsigned short*)x, mean, rstd, gamma,  \
+                     (const unsigned short*)dres, (unsigned short*)dx, dgamma, dbeta, dxsum)
+  if (nc == 1) DTFX_LNB(1);
+  else if (nc == 2) DTFX_LNB(2);
+  else if (nc == 3) DTFX_LNB(3);
+  else DTFX_LNB(4);
+#undef DTFX_LNB
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
@@ -767,7 +862,7 @@ void embed_bwd_launch(int Bn, int S, int H, const int* ids, const int* tt, const
   hipLaunchKernelGGL(embed_word_bwd_kernel, dim3((T + 3) / 4), dim3(256), 0, s, T, H, ids,
                      (const unsigned short*)dx, dword);
   DTFX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(embed_pos_type_bwd_kernel, dim3(S), dim3(256), 0, s, Bn, S, H, tt,
+  hipLaunchKernelGGL(embed_pos_type_bwd_kernel, dim3(S), dim3(1024), 0, s, Bn, S, H, tt,
                      (const unsigned short*)dx, dpos, dtype_);
   DTFX_HIP_CHECK(hipGetLastError());
 }
