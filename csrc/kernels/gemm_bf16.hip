@@ -349,6 +349,29 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
   auto compute = [&](int buf) {
     const char* At = smem + buf * BUF_BYTES;
     const char* Bt = At + TILE_A;
+    if constexpr (BM_ == 128 && NBUF == 2 && BN_ == 128) {
+      // 128x128 (two blocks per CU): both k-halves' fragments are requested before the
+      // first MFMA (half 1's LDS latency hides under half 0's MFMAs) and the MFMAs issue at
+      // raised priority, so the partner wave on the SIMD does its reads in the gaps
+      bf16x8 af2[2][TM], bf2[2][4];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af2[kk][i] = frag<!TA, BM>(At, wm * WM + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf2[kk][j] = frag<TB, BN>(Bt, wn * 64 + j * 16, kk, lane);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af2[kk][i], bf2[kk][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[TM], bfr[4];
@@ -407,13 +430,12 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
   for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
   for (int h = 0; h < WM / 32; ++h) {
     // (issued before the slab's LDS transpose, so their latency overlaps it)
-    // Side inputs (bias / aux_in / residual / C_old) of the slab's 4 row groups are all
+    // Side inputs (aux_in / residual) of the slab's 4 row groups are all
     // loaded before any is used: one memory round trip per 32-row slab instead of one per
     // 8-row group (the loads used to sit between dependent compute and stores).
     bool full[4], live[4];
     int mm[4], nn[4];
     bf16x8 a8[4], r8[4];
-    f32x4 c0[4], c1[4];
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
@@ -422,12 +444,9 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
       live[it] = mm[it] < M && nn[it] < N;
       full[it] = live[it] && nn[it] + 8 <= N;  // N % 8 != 0 only with a ragged last group
       const int ms = live[it] ? mm[it] : 0, ns = full[it] ? nn[it] : 0;
-      if (e.act_grad) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)ms * e.ld_aux + ns];
-      if (e.residual) r8[it] = *(const bf16x8*)&e.residual[(size_t)ms * e.ld_res + ns];
-      if (OUT_F32 && e.beta != 0.f && gridDim.y == 1) {  // (split-K adds atomically)
-        const float* C = (const float*)Cv + (size_t)ms * ldc + ns;
-        c0[it] = *(const f32x4*)C;
-        c1[it] = *(const f32x4*)(C + 4);
+      if (!OUT_F32) {  // (f32-output tiles load at use: the 256x256 f32 variant would spill)
+        if (e.act_grad) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)ms * e.ld_aux + ns];
+        if (e.residual) r8[it] = *(const bf16x8*)&e.residual[(size_t)ms * e.ld_res + ns];
       }
     }
     // static accumulator indices only (a runtime acc[2h+ii] index would put acc in scratch)
@@ -488,6 +507,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
           for (int u = 0; u < 8; ++u) v[u] = fmaxf(v[u], 0.f);
         }
         if (e.act_grad) {
+          if (OUT_F32) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)m * e.ld_aux + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             const float uu = bf2f((unsigned short)a8[it][u]);
@@ -495,6 +515,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
           }
         }
         if (e.residual) {
+          if (OUT_F32) r8[it] = *(const bf16x8*)&e.residual[(size_t)m * e.ld_res + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[it][u]);
         }
@@ -507,11 +528,12 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
         }
         if (OUT_F32) {
           float* C = (float*)Cv + (size_t)m * ldc + n;
-          if (e.beta != 0.f) {
+          if (e.beta != 0.f) {  // (f32 outputs: C_old read here, no 32-VGPR slab batch)
+            const f32x4 c0 = *(const f32x4*)C, c1 = *(const f32x4*)(C + 4);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              v[u] += e.beta * c0[it][u];
-              v[u + 4] += e.beta * c1[it][u];
+              v[u] += e.beta * c0[u];
+              v[u + 4] += e.beta * c1[u];
             }
           }
           *(f32x4*)C = *(f32x4*)&v[0];
@@ -599,9 +621,17 @@ static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
   const int f = gemm_cfg_env();
   if (f >= 0 && f <= 3) return f;
   if (mode == 0) {  // the 256x256 tile halves L2 traffic when it still fills the chip
-                    // (measured: 1.10 vs 0.89 PF at 8192^3); A^T operands stay on 128x128
-    const long long t = (long long)((M + 255) / 256) * ((N + 255) / 256) * zdim;
-    return (!ta && t >= 256) ? 3 : 0;
+                    // (measured: 1.11 vs 0.92 PF at 8192^3); A^T operands stay on 128x128.
+    // Wave quantisation decides between them: 256x256 runs 1 block/CU (256 slots),
+    // 128x128 two (512 slots); 256x256 wins when its last wave is about as full as the
+    // 128x128 grid's, allowing for its ~15% faster main loop (BERT QKV 16384x2304:
+    // 576 blocks = 2.25 waves, 86 us, vs 2304 / 512 = 4.5 waves on 128x128, 79 us).
+    const long long t3 = (long long)((M + 255) / 256) * ((N + 255) / 256) * zdim;
+    const long long t0 = (long long)((M + 127) / 128) * ((N + 127) / 128) * zdim;
+    if (ta || t3 < 256) return 0;
+    const double e3 = (double)t3 / (double)(((t3 + 255) / 256) * 256);
+    const double e0 = (double)t0 / (double)(((t0 + 511) / 512) * 512);
+    return e3 * 1.15 >= e0 ? 3 : 0;
   }
   // convolutions (ResNet-50 end to end: 6881 img/s on 128x128 vs 6411-6416 on 256x128)
   return 0;
