@@ -205,6 +205,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     tr.run(a.steps, use_graph)
+    tr.flush()  # the last step's deferred update is part of the timed work
     torch.cuda.synchronize()
     if barrier:
         barrier()
@@ -242,6 +243,7 @@ def main():
                 "parallelism": "dp%d" % world,
                 "comm": _comm_label(a) if (world > 1 or a.dp) else "none",
                 "hipgraph": use_graph,
+                "launches_per_step": 2 if tr.pipelined else 3,
             },
             "comm_probe_us": getattr(a, "comm_probe", None),
             "engine_probe_us_per_step": getattr(a, "engine_probe", None),

@@ -23,6 +23,9 @@ void mlp_head_launch(const float*, const float*, float, float*, const int*, floa
 void mlp_wgrad_launch(float*, float, float*, const float*, float*, int*, float*, int, int,
                       hipStream_t, unsigned long long*);
 long long mlp_workspace_floats(int);
+void mlp_fwdapply_launch(const float*, float*, float, const float*, const float*, float*, int*,
+                         float*, int, int, int, hipStream_t);
+void mlp_head2_launch(const float*, const int*, float*, int, hipStream_t);
 void calib_launch(int, int, int, const int*, const float*, float*, hipStream_t);
 void clock_probe_launch(int, int, unsigned long long*, float*, hipStream_t);
 void gemm_f32_launch(bool, bool, int, int, int, float, const float*, int, const float*, int,
@@ -75,6 +78,18 @@ PYBIND11_MODULE(_hip, m) {
                            P<int>(ctr), P<float>(stats), ring, B, S(s), P<unsigned long long>(tr));
   }, py::arg("p"), py::arg("lr"), py::arg("grad"), py::arg("x"), py::arg("ws"), py::arg("ctr"),
      py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"), py::arg("trace") = 0);
+  m.def("mlp_fwdapply", [](uintptr_t p_old, uintptr_t p_new, float lr, uintptr_t x_prev,
+                           uintptr_t x, uintptr_t ws, uintptr_t ctr, uintptr_t stats, int ring,
+                           int B, int stats_on, uintptr_t s) {
+    dtfx::mlp_fwdapply_launch(P<const float>(p_old), P<float>(p_new), lr, P<const float>(x_prev),
+                              P<const float>(x), P<float>(ws), P<int>(ctr), P<float>(stats), ring,
+                              B, stats_on, S(s));
+  }, py::arg("p_old"), py::arg("p_new"), py::arg("lr"), py::arg("x_prev"), py::arg("x"),
+     py::arg("ws"), py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"),
+     py::arg("stats_on"), py::arg("stream"));
+  m.def("mlp_head2", [](uintptr_t p, uintptr_t lab, uintptr_t ws, int B, uintptr_t s) {
+    dtfx::mlp_head2_launch(P<const float>(p), P<const int>(lab), P<float>(ws), B, S(s));
+  }, py::arg("p"), py::arg("labels"), py::arg("ws"), py::arg("B"), py::arg("stream"));
   m.def("gemm_f32", [](bool ta, bool tb, int M, int N, int K, float alpha, uintptr_t A, int lda,
                        uintptr_t B, int ldb, float beta, uintptr_t C, int ldc, uintptr_t bias,
                        int act, uintptr_t aux, int ldaux, bool act_grad, uintptr_t s) {

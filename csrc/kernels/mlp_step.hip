@@ -60,6 +60,9 @@ constexpr int HP = HT * 16;    // padded hidden width
 constexpr int KS = 7;          // K slices of K1
 constexpr int KW = D / KS;     // 112 = 7 groups of 16
 constexpr int FT = D / 16;     // 49 feature tiles (dW1)
+constexpr int KS2 = 14;        // K slices of the pipelined step's fused apply+forward launch
+constexpr int KW2 = D / KS2;   // 56 features = 3.5 MFMA groups of 16
+constexpr int NSLAB_MAX = KS2; // slab planes in the workspace
 constexpr int OFF_W1 = 0;
 constexpr int OFF_B1 = H * D;
 constexpr int OFF_W2 = OFF_B1 + H;
@@ -68,10 +71,11 @@ constexpr int NPARAM = OFF_B2 + C;
 constexpr int MAXB = 256;
 
 static_assert(KW % 16 == 0 && KS * KW == D, "K slicing of 784");
+static_assert(KS2 * KW2 == D && KW2 % 8 == 0, "K slicing of the pipelined step");
 static_assert(NPARAM == 79510, "parameter count of worker.py:50-53");
 
 struct Bufs {            // workspace (zero-initialised once; padding stays 0)
-  float* slab;           // [KS][BP][HP]  partial z1
+  float* slab;           // [NSLAB_MAX][BP][HP]  partial z1 (KS or KS2 planes used)
   float* hbuf;           // [BP][HP]      h
   float* dz1T;           // [HP][BP]      dz1 transposed
   float* dlT;            // [16][BP]      dlogits transposed
@@ -159,7 +163,7 @@ __global__ __launch_bounds__(64) void mlp_fwd_kernel(
 // words into slot (parity, me) of every peer and every peer's values for the same (j, row)
 // are gathered from local memory into dz1A [XW][HP][BP] -- the all-gather of the backprop
 // factors that mlp_wgrad_factor_kernel turns into the global weight gradient.
-template <bool APPLY, bool TRACE, int XW = 0>
+template <bool APPLY, bool TRACE, int XW = 0, int NSLAB = KS>
 __global__ __launch_bounds__(64) void mlp_head_kernel(
     const float* __restrict__ p_old, const float* __restrict__ grad, float lr,
     float* __restrict__ p_new, const int* __restrict__ labels, Bufs w, int B,
@@ -183,7 +187,7 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     jj[u] = jv[u] ? j : H - 1;
     zs[u] = 0.f;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) zs[u] += w.slab[((size_t)s * BP + row) * HP + jj[u]];
+    for (int s = 0; s < NSLAB; ++s) zs[u] += w.slab[((size_t)s * BP + row) * HP + jj[u]];
     b1v[u] = p_old[OFF_B1 + jj[u]];
 #pragma unroll
     for (int c = 0; c < C; ++c) w2[u][c] = p_old[OFF_W2 + c * H + jj[u]];
@@ -342,12 +346,18 @@ __device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const 
 
 // Small parameters of hidden tile jt (one product per wave), shared by mlp_wgrad_kernel and
 // mlp_wgrad_factor_kernel; eidx = this wave's exchange-epoch slot.
+// p_src: where the current parameter values are read (== p except in the pipelined step,
+// which reads the old ping-pong buffer and writes the new one); stats_on = 0 skips the
+// loss/accuracy record and the global_step increment.
 template <bool DIRECT, int NGT, int XW>
 __device__ __forceinline__ void wgrad_small(int jt, int wave, int lane, int eidx,
                                             float* __restrict__ p, float lr,
                                             float* __restrict__ grad, const Bufs& w,
                                             int* __restrict__ ctr, float* __restrict__ stats,
-                                            int stats_ring, int B, const MlpXg& xg) {
+                                            int stats_ring, int B, const MlpXg& xg,
+                                            const float* __restrict__ p_src = nullptr,
+                                            int stats_on = 1) {
+  if (p_src == nullptr) p_src = p;
   const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
   const int NG = NGT > 0 ? NGT : BP / 16;
   const int r = lane & 15, q = lane >> 4;
@@ -356,7 +366,7 @@ __device__ __forceinline__ void wgrad_small(int jt, int wave, int lane, int eidx
   //   wave 0: dW2^T[:, jt] = dlT . h[:, jt]   wave 1: db1[jt] = dz1T[jt] . 1
   //   wave 2: db2 = dlT . 1 (jt == 0)         wave 3: loss/accuracy (jt == 0)
   if (wave == 3) {
-    if (jt != 0) return;
+    if (jt != 0 || !stats_on) return;
     float l = 0.f, a = 0.f;
     for (int b = lane; b < B; b += 64) {
       l += w.rowstat[2 * b];
@@ -418,7 +428,7 @@ __device__ __forceinline__ void wgrad_small(int jt, int wave, int lane, int eidx
       ok[i] = r == 0 && c < C;
       off[i] = OFF_B2 + (c < C ? c : 0);
     }
-    if (DIRECT) pv[i] = p[off[i]];
+    if (DIRECT) pv[i] = p_src[off[i]];
   }
   __builtin_amdgcn_sched_barrier(0);
   // NB: padded batch columns of dz1T/dlT are zero, so multiplying by 1 is exact.
@@ -543,6 +553,149 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
 }
 
 
+
+// ---------------------------------------------------------------------------
+// Pipelined single-GPU step (2 launches): K1' applies step t-1's SGD update and runs
+// step t's forward in ONE launch, then mlp_head_kernel<.., KS2> finishes step t.
+//   blocks [0, HT*KS2): block (jt, ks) OWNS the W1 tile [16 hidden][56 features]:
+//     wave w forms dW1^T[jt][ks*56 + 16w .. +16) = dz1T[jt] . x_prev (f32 MFMA,
+//     K = batch; wave 3 has 8 live columns), W1new = W1old - lr * g -> LDS + p_new;
+//     barrier; then z1 partial of row tiles rt = w, w+4, .. over the block's 56 features
+//     with W1new from LDS -> slab[ks].  No tile is computed twice and no W1 gradient is
+//     ever stored.
+//   blocks [HT*KS2, +HT): wgrad_small (dW2 / db1 / db2 of step t-1, p_old -> p_new; the
+//     loss/accuracy record and global_step += 1 of step t-1).
+// lr = 0 / stats_on = 0 (the first step after a flush): a pure copy p_old -> p_new.
+// Removes one dependent kernel boundary and one cold-load phase per step vs the 3-launch
+// step (fwd / head / wgrad).
+template <int NGT>
+__global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
+    const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
+    const float* __restrict__ x_prev, const float* __restrict__ x, Bufs w, int* __restrict__ ctr,
+    float* __restrict__ stats, int stats_ring, int B, int stats_on) {
+  const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
+  const int NG = NGT > 0 ? NGT : BP / 16;
+  const int RT = (B + 15) >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  constexpr int MAXG = NGT > 0 ? NGT : MAXB / 16;
+  const int bid = blockIdx.x;
+  if (bid >= HT * KS2) {
+    wgrad_small<true, NGT, 0>(bid - HT * KS2, wave, lane, 0, p_new, lr, nullptr, w, ctr, stats,
+                              stats_ring, B, MlpXg{}, p_old, stats_on);
+    return;
+  }
+  constexpr int LW = KW2 + 4;  // LDS row pitch (floats)
+  __shared__ float Wt[16][LW];
+  const int jt = bid / KS2, ks = bid % KS2;
+  const int f0 = ks * KW2;
+  // phase B's x rows are independent of phase A: requested first, so the whole launch
+  // makes one memory round trip (B <= 128 -> at most 2 row tiles per wave held here)
+  constexpr int RTW = 2;
+  float4 xa[RTW][4];
+  float rmv[RTW];
+#pragma unroll
+  for (int t = 0; t < RTW; ++t) {
+    const int row = (wave + 4 * t) * 16 + r;
+    const float* xr = x + (size_t)(row < B ? row : B - 1) * D + f0;
+    rmv[t] = row < B ? 1.f : 0.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int k = 16 * g + 4 * q;
+      xa[t][g] = f4(xr + (k < KW2 ? k : 0));
+    }
+  }
+
+  // ---- phase A: this wave's 16 x 16 slice of the updated W1 tile ---------------------
+  {
+    const int fl = wave * 16 + r;           // feature within the 56-wide slice
+    const bool cv = fl < KW2;               // wave 3: 8 live columns
+    const int fc = f0 + (cv ? fl : KW2 - 1);
+    const float* a = w.dz1T + (size_t)(jt * 16 + r) * BP + q * 4;
+    const float* xc = x_prev + fc;
+    float4 av[MAXG];
+    float xv[MAXG][4];
+    float pw[4];
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g) {
+      if (g < NG) {
+        av[g] = f4(a + g * 16);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int b = g * 16 + q * 4 + e;  // rows >= B: dz1T is zero there
+          xv[g][e] = xc[(size_t)(b < B ? b : B - 1) * D];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = jt * 16 + q * 4 + i;
+      pw[i] = p_old[OFF_W1 + (size_t)(j < H ? j : H - 1) * D + fc];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // all loads in flight together
+    f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g) {
+      if (g < NG) {
+        acc0 = mfma16x16x4(av[g].x, xv[g][0], acc0);
+        acc1 = mfma16x16x4(av[g].y, xv[g][1], acc1);
+        acc0 = mfma16x16x4(av[g].z, xv[g][2], acc0);
+        acc1 = mfma16x16x4(av[g].w, xv[g][3], acc1);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hl = q * 4 + i, j = jt * 16 + hl;
+      const float v = pw[i] - lr * (acc0[i] + acc1[i]);
+      if (cv) {
+        Wt[hl][fl] = j < H ? v : 0.f;  // padded hidden rows contribute exact zeros
+        if (j < H) p_new[OFF_W1 + (size_t)j * D + f0 + fl] = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase B: z1 partial over the block's 56 features, row tiles rt = wave, wave + 4, ..
+  // lane (r, q): A = x[rt*16 + r][f0 + 16g + 4q + e], B = Wt[r][16g + 4q + e]; group 3 has
+  // 8 live features (q < 2)
+  float4 wb[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int k = 16 * g + 4 * q;
+    wb[g] = k < KW2 ? *reinterpret_cast<const float4*>(&Wt[r][k]) : float4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int rt = wave, t = 0; rt < RT; rt += 4, ++t) {
+    float4 xg[4];
+    float rm;
+    if (t < RTW) {  // prefetched (wave-uniform)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xg[g] = t == 0 ? xa[0][g] : xa[1][g];
+      rm = t == 0 ? rmv[0] : rmv[1];
+    } else {        // B > 128: later row tiles load here
+      const int row = rt * 16 + r;
+      const float* xr = x + (size_t)(row < B ? row : B - 1) * D + f0;
+      rm = row < B ? 1.f : 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int k = 16 * g + 4 * q;
+        xg[g] = f4(xr + (k < KW2 ? k : 0));
+      }
+    }
+    f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      // (wb is zero for the dead half of group 3, so no mask is needed on xg there)
+      acc0 = mfma16x16x4(xg[g].x * rm, wb[g].x, acc0);
+      acc1 = mfma16x16x4(xg[g].y * rm, wb[g].y, acc1);
+      acc0 = mfma16x16x4(xg[g].z * rm, wb[g].z, acc0);
+      acc1 = mfma16x16x4(xg[g].w * rm, wb[g].w, acc1);
+    }
+    float* out = w.slab + ((size_t)ks * BP + rt * 16 + q * 4) * HP + jt * 16 + r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(size_t)i * HP] = acc0[i] + acc1[i];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K3, factor engine (sufficient-factor exchange, world XW): the backprop factors dz1 of
 // every rank were all-gathered by mlp_head_kernel<.., XW> into dz1A [XW][HP][BP], and every
@@ -648,7 +801,7 @@ static mlp::Bufs make_bufs(float* ws, int B) {
   const int BP = ((B + 15) / 16) * 16;
   Bufs b;
   b.slab = ws;
-  b.hbuf = b.slab + (size_t)KS * BP * HP;
+  b.hbuf = b.slab + (size_t)NSLAB_MAX * BP * HP;
   b.dz1T = b.hbuf + (size_t)BP * HP;
   b.dlT = b.dz1T + (size_t)HP * BP;
   b.rowstat = b.dlT + (size_t)16 * BP;
@@ -658,7 +811,7 @@ static mlp::Bufs make_bufs(float* ws, int B) {
 long long mlp_workspace_floats(int B) {
   using namespace mlp;
   const long long BP = ((B + 15) / 16) * 16;
-  return (long long)KS * BP * HP + BP * HP + HP * BP + 16 * BP + 2 * BP;
+  return (long long)NSLAB_MAX * BP * HP + BP * HP + HP * BP + 16 * BP + 2 * BP;
 }
 
 static void check_b(int B) {
@@ -821,4 +974,33 @@ void mlp_wgrad_factor_launch(float* p, float lr, const float* x, long long xstri
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+
+// Pipelined single-GPU step (see mlp_fwdapply_kernel): K1' then the head over KS2 slabs.
+void mlp_fwdapply_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
+                         const float* x, float* ws, int* ctr, float* stats, int stats_ring, int B,
+                         int stats_on, hipStream_t stream) {
+  using namespace mlp;
+  check_b(B);
+  if (!p_old || !p_new || p_old == p_new || !x_prev || !x || !ctr)
+    throw std::runtime_error("mlp_fwdapply: needs distinct ping-pong buffers, both batches, ctr");
+  if (stats && stats_ring < 1) throw std::runtime_error("mlp_fwdapply: stats_ring < 1");
+  const Bufs w = make_bufs(ws, B);
+  dim3 grid(HT * KS2 + HT), block(256);
+  if ((B + 15) / 16 == 7)
+    hipLaunchKernelGGL((mlp_fwdapply_kernel<7>), grid, block, 0, stream, p_old, p_new, lr, x_prev,
+                       x, w, ctr, stats, stats_ring, B, stats_on);
+  else
+    hipLaunchKernelGGL((mlp_fwdapply_kernel<0>), grid, block, 0, stream, p_old, p_new, lr, x_prev,
+                       x, w, ctr, stats, stats_ring, B, stats_on);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipStream_t stream) {
+  using namespace mlp;
+  check_b(B);
+  const Bufs w = make_bufs(ws, B);
+  hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS2>), dim3(B), dim3(64), 0, stream, p, p,
+                     0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
 }  // namespace dtfx

@@ -92,6 +92,34 @@ def step_direct(p, x, labels, ws: StepWorkspace, lr, stats=True):
                 ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B, s)
 
 
+def step_pipelined(p_old, p_new, x_prev, x, labels, ws: StepWorkspace, lr, apply, stats=True):
+    """Two-launch single-GPU step: ``mlp_fwdapply`` applies the PREVIOUS step's SGD update
+    (from the factors dz1/h/dlogits the last head left in ``ws`` and the previous batch
+    ``x_prev``; W1 never materialises a gradient) reading ``p_old`` and writing ``p_new``,
+    and runs this step's forward on the updated W1; ``mlp_head`` (14 partial slabs)
+    finishes the step.  ``apply=False`` (nothing pending): a plain copy + forward.  The
+    last step's update stays pending until ``flush_pipelined``."""
+    _check(x, labels, ws.B)
+    _check(x_prev, None, ws.B)
+    _check_flat(p_old, p_new)
+    if p_old.data_ptr() == p_new.data_ptr():
+        raise ValueError("the pipelined step needs distinct ping-pong buffers")
+    h, s = hip(), stream_handle()
+    h.mlp_fwdapply(ptr(p_old), ptr(p_new), float(lr) if apply else 0.0,
+                   ptr(x_prev if apply else x), ptr(x), ptr(ws.buf), ptr(ws.ctr),
+                   ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B, 1 if apply else 0, s)
+    h.mlp_head2(ptr(p_new), ptr(labels), ptr(ws.buf), ws.B, s)
+
+
+def flush_pipelined(p, x_prev, ws: StepWorkspace, lr, stats=True):
+    """Apply the pending update of the last pipelined step in place (the 3-launch step's
+    weight-gradient kernel in direct mode: same factors, same batch)."""
+    _check(x_prev, None, ws.B)
+    _check_flat(p)
+    hip().mlp_wgrad(ptr(p), float(lr), 0, ptr(x_prev), ptr(ws.buf), ptr(ws.ctr),
+                    ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B, stream_handle())
+
+
 def step_xgmi(p, x, labels, ws: StepWorkspace, lr, comm, stats=True):
     """One synchronous data-parallel SGD step in place on ``p`` with the gradient exchange
     fused into the weight-gradient kernel (``comm``: an ``XgmiComm`` with protocol "push";

@@ -8,8 +8,13 @@ a host->GPU feed of 317 KB and ~14 tiny TF kernels.  Here:
 * the dataset is resident in HBM; each launch gets its batch's pointer, and
   one hipGraph is captured per epoch (``nbatches`` steps), so replaying it
   walks the dataset like ``next_batch`` with no host work per step;
-* the step is ``mlp_fwd`` / ``mlp_head`` / ``mlp_wgrad`` (ops/mlp_step.py);
-  on one GPU the SGD apply is fused into ``mlp_wgrad``'s epilogue;
+* on one GPU the step is TWO launches (``pipeline=True``, default):
+  ``mlp_fwdapply`` applies step t-1's update -- formed tile by tile from the
+  factors the previous head left behind, never stored as a gradient -- and runs
+  step t's forward; ``mlp_head`` finishes step t.  The last update stays pending
+  until ``flush()`` (ping-pong parameter buffers, like the DP path below).
+  ``pipeline=False``: the three-launch step ``mlp_fwd`` / ``mlp_head`` /
+  ``mlp_wgrad`` with the SGD apply fused into ``mlp_wgrad``'s epilogue;
 * in sync data-parallel mode the flat 318 KB gradient is all-reduced after
   ``mlp_wgrad`` by a pluggable ``allreduce(grad)`` callable (RCCL through
   ``torch.distributed`` or the native communicator) and applied, averaged
@@ -43,7 +48,7 @@ from ..ops import mlp_step, optim
 class FusedMLPTrainer:
     def __init__(self, params, x, labels, batch_size=100, learning_rate=0.001, allreduce=None,
                  world_size=1, stats_ring=4096, global_step=0, max_graph_steps=1024,
-                 fused_comm=None, factor_comm=None, x_all=None, rank=0):
+                 fused_comm=None, factor_comm=None, x_all=None, rank=0, pipeline=True):
         if not params.is_cuda:
             raise ValueError("FusedMLPTrainer runs on the GPU; use the generic path on CPU")
         if params.numel() != mlp_step.NPARAM:
@@ -84,6 +89,9 @@ class FusedMLPTrainer:
         self.ws.set_global_step(global_step)
         self.pos = int(global_step) % self.nbatches  # next batch (host mirror)
         self.pending = False
+        # single GPU, no communicator: the two-launch pipelined step
+        self.pipelined = bool(pipeline and self.world_size == 1 and allreduce is None
+                              and fused_comm is None and factor_comm is None)
         self.max_graph_steps = int(max_graph_steps)
         self._graphs = {}
         self._pool = None
@@ -93,7 +101,7 @@ class FusedMLPTrainer:
     def direct(self):
         """SGD apply fused into the backward kernel (one GPU, or the fused xGMI exchange)."""
         return (self.fused_comm is not None or self.factor_comm is not None
-                or (self.allreduce is None and self.world_size == 1))
+                or (self.allreduce is None and self.world_size == 1 and not self.pipelined))
 
     @property
     def params(self):
@@ -101,9 +109,14 @@ class FusedMLPTrainer:
         return self.bufs[self.cur]
 
     def flush(self):
-        """Apply the pending gradient in place (p -= lr/N * grad)."""
+        """Apply the pending update in place (DP: p -= lr/N * grad; pipelined: the last
+        step's factors)."""
         if self.pending:
-            optim.sgd_(self.bufs[self.cur], self.grad, self.lr / self.world_size)
+            if self.pipelined:
+                xp, _ = self.batch((self.pos - 1) % self.nbatches)
+                mlp_step.flush_pipelined(self.bufs[self.cur], xp, self.ws, self.lr)
+            else:
+                optim.sgd_(self.bufs[self.cur], self.grad, self.lr / self.world_size)
             self.pending = False
         return self.bufs[self.cur]
 
@@ -112,7 +125,9 @@ class FusedMLPTrainer:
         self.pending = False
 
     def global_step(self) -> int:
-        return self.ws.global_step()
+        # the pipelined step records step t (stats, global_step += 1) inside step t+1's
+        # first launch (or flush())
+        return self.ws.global_step() + (1 if (self.pipelined and self.pending) else 0)
 
     def batch(self, i):
         sl = slice(i * self.B, (i + 1) * self.B)
@@ -132,6 +147,13 @@ class FusedMLPTrainer:
             return
         if self.direct:
             mlp_step.step_direct(self.bufs[self.cur], xb, yb, self.ws, self.lr)
+            return
+        if self.pipelined:
+            xp, _ = self.batch((self.pos - 2) % self.nbatches)  # pos already advanced
+            mlp_step.step_pipelined(self.bufs[self.cur], self.bufs[self.cur ^ 1], xp, xb, yb,
+                                    self.ws, self.lr, apply=self.pending)
+            self.cur ^= 1
+            self.pending = True
             return
         cur = self.bufs[self.cur]
         if self.pending:
@@ -215,12 +237,16 @@ class FusedMLPTrainer:
     # -- observability ------------------------------------------------------
     def stats(self, step=None):
         """(loss, accuracy) recorded by the kernel for ``step`` (default: last)."""
+        if self.pipelined and self.pending:
+            self.flush()  # the last step's record is written by its apply
         s = (self.global_step() - 1) if step is None else int(step)
         v = self.ws.stats[s % self.ws.stats_ring].tolist()
         return float(v[0]), float(v[1])
 
     def stats_range(self, start, end):
         """Loss/accuracy for steps [start, end) as a CPU tensor [n, 2]."""
+        if self.pipelined and self.pending:
+            self.flush()
         ring = self.ws.stats_ring
         if end - start > ring:
             start = end - ring

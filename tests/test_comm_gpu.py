@@ -57,6 +57,7 @@ def test_dp_trainer_with_native_comm_matches_direct(comm, gpu):
     a.run(37)
     b.run(37)
     a.flush()
+    b.flush()  # (the pipelined single-GPU step defers its last update too)
     torch.cuda.synchronize()
     assert a.global_step() == b.global_step() == 37
     assert (a.params - b.params).abs().max().item() < 1e-5

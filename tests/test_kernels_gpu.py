@@ -221,3 +221,43 @@ def test_trainer_graph_replay_matches_eager(gpu, dp):
     assert t1.global_step() == t2.global_step() == 23
     assert torch.equal(t1.params, t2.params)
     assert t1.stats() == t2.stats()
+
+
+@pytest.mark.parametrize("B", [100, 64, 200])
+def test_pipelined_trainer_matches_reference_and_three_launch(gpu, B):
+    """Two-launch pipelined step (apply of step t-1 fused with the forward of step t):
+    same SGD trajectory as the float64 reference and as the three-launch trainer, through
+    graph replays, a mid-run flush and the generic-batch kernel variants."""
+    from distributedtensorflowexample_amd.train.fused_mlp import FusedMLPTrainer
+
+    nb, lr = 4, 0.3
+    p, x, y = _mlp_setup(gpu, B, nb, seed=4)
+    p.mul_(0.1)
+    tp = FusedMLPTrainer(p, x, y, B, lr)                   # pipelined (default)
+    t3 = FusedMLPTrainer(p, x, y, B, lr, pipeline=False)   # three launches
+    assert tp.pipelined and not t3.pipelined
+    tp.max_graph_steps = 3
+    t3.max_graph_steps = 3
+    tp.run(6, use_graph=False)
+    t3.run(6, use_graph=False)
+    # float64 reference of the first 6 steps
+    ref = p.double().cpu()
+    xr, yr = x.double().cpu(), y.cpu()
+    for s in range(6):
+        sl = slice((s % nb) * B, (s % nb + 1) * B)
+        g, _, _ = mlp_step.reference_step(ref, xr[sl], yr[sl])
+        ref = ref - lr * g
+    assert tp.global_step() == 6
+    tp.flush()
+    torch.cuda.synchronize()
+    assert (tp.params.double().cpu() - ref).abs().max().item() < 1e-4
+    tp.run(11, use_graph=True)  # graph replays after a flush (first step re-primes)
+    t3.run(11, use_graph=True)
+    tp.flush()
+    torch.cuda.synchronize()
+    assert tp.global_step() == t3.global_step() == 17
+    assert (tp.params - t3.params).abs().max().item() < 1e-5
+    lp, ap = tp.stats()
+    l3, a3 = t3.stats()
+    assert abs(lp - l3) < 1e-4 and ap == a3
+    assert torch.allclose(tp.stats_range(0, 17), t3.stats_range(0, 17), atol=1e-4)
