@@ -37,7 +37,7 @@ METRIC = "samples/sec (whole node) MNIST MLP sync-SGD at 1/2/4/8 MI355X; scaling
 
 
 # Rehearsal mode for the multi-rank paths on a ONE-GPU box: every rank shares device 0 and
-# an xGMI-IPC communicator (flag protocol) stands in for RCCL, which refuses two ranks on
+# an xGMI-IPC communicator (LL push protocol) stands in for RCCL, which refuses two ranks on
 # one GPU.  Never set for real runs; the JSON records it.
 SHARED_GPU = os.environ.get("DTFX_SHARED_GPU") == "1"
 
@@ -56,7 +56,8 @@ def _native_comm(world, rank, dev, max_numel):
     if SHARED_GPU:
         from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
 
-        return XgmiComm(rank, world, max_numel, device=dev, key="dtfx/shared", protocol="flag",
+        return XgmiComm(rank, world, max_numel, device=dev, key="dtfx/shared",
+                        protocol="push" if world <= 8 else "flag",
                         timeout_s=120.0)  # peers time-share the GPU (and start skewed)
     from distributedtensorflowexample_amd.parallel.comm import NativeComm
 

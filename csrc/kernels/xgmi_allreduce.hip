@@ -57,9 +57,14 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
   // the slice's UC stores are acknowledged (globally visible) before any flag goes out
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // 2) raise my flag for this block at every rank (remote stores over xGMI)
+  // 2) raise my flag for this block at every rank (remote stores over xGMI).  RELEASE at
+  // system scope: an acknowledged store (vmcnt) is not yet ordered before a store to
+  // another channel, and a reader that saw the flag read the previous epoch's slice
+  // (measured: 3 ranks on one GPU, a few stale elements per 40 steps).  The LL protocols
+  // below carry the epoch inside every data word and need no such fence; this one is
+  // only used beyond 8 ranks.
   if (t < world)
-    __hip_atomic_store(peers.flags[t] + rank * XG_BLOCKS + b, epoch, __ATOMIC_RELAXED,
+    __hip_atomic_store(peers.flags[t] + rank * XG_BLOCKS + b, epoch, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   // 3) wait until every rank published this block for this epoch (bounded spin)
   if (t < world) {
@@ -78,7 +83,8 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
     if (t == 0) atomicExch(err, 1);
     return;  // g keeps the local gradient; the host sees err and raises
   }
-  asm volatile("" ::: "memory");  // no load of peer data above this point
+  // acquire: no load of peer data above this point, none served by a stale cache line
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // 4) sum the world slices in rank order (identical on every rank) into g
   for (long long i = lo + t; i < hi; i += blockDim.x) {
     f32x4 acc = ((const f32x4*)(peers.data[0] + par))[i];

@@ -20,8 +20,11 @@ from .xgmi import XgmiComm
 
 
 def xgmi_protocols(world):
-    """Candidate xGMI protocols for a world size (LL variants need world <= 8)."""
-    return ["push2", "push", "ll", "flag"] if world <= 8 else ["flag"]
+    """Candidate xGMI protocols for a world size.  The LL variants (epoch inside every data
+    word) need world <= 8; the flag protocol (separate per-block flags, release-ordered)
+    is the fallback beyond that only -- a 3-rank probe caught it serving stale slices
+    before its flag store was release-ordered (tools/probes/fused_flake.py)."""
+    return ["push2", "push", "ll"] if world <= 8 else ["flag"]
 
 
 def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_key="dtfx/xgmi/0",

@@ -96,7 +96,7 @@ def _auto_worker(rank, world, port, q):
         t = torch.full((79510,), float(rank + 1), device="cuda:0")
         comm.allreduce_sum_(t)
         torch.cuda.synchronize()
-        q.put((rank, bool((t == 3.0).all()) and probe is not None and len(probe) >= 4,
+        q.put((rank, bool((t == 3.0).all()) and probe is not None and len(probe) >= 3,
                str(probe)))
         dist.destroy_process_group()
     except Exception as e:
@@ -132,7 +132,7 @@ def _fused_worker(rank, world, port, q):
         params = init_params(dev, seed=7)
         x, y = mnist_like_device(2000, seed=50 + rank, device=dev)  # per-rank data
         fc = XgmiComm(rank, world, params.numel(), device=dev, key="f/push", protocol="push")
-        ref = XgmiComm(rank, world, params.numel(), device=dev, key="f/flag", protocol="flag")
+        ref = XgmiComm(rank, world, params.numel(), device=dev, key="f/ll", protocol="ll")
         lr = 0.05
         tf = FusedMLPTrainer(params, x, y, 100, lr, world_size=world, fused_comm=fc)
         ta = FusedMLPTrainer(params, x, y, 100, lr, world_size=world, allreduce=ref.allreduce_sum_)
@@ -191,7 +191,7 @@ def _factor_worker(rank, world, port, q, B):
                              for r in range(world)]).contiguous()
         y = mnist_like_device(n, seed=50 + rank, device=dev)[1]
         fc = XgmiComm(rank, world, params.numel(), device=dev, key="s/push", protocol="push")
-        ref = XgmiComm(rank, world, params.numel(), device=dev, key="s/flag", protocol="flag")
+        ref = XgmiComm(rank, world, params.numel(), device=dev, key="s/ll", protocol="ll")
         lr = 0.05
         tf = FusedMLPTrainer(params, None, y, B, lr, world_size=world, factor_comm=fc,
                              x_all=x_all, rank=rank)
