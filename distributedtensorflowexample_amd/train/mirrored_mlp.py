@@ -67,17 +67,27 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
     state = {}
 
     if use_gpu:
-        fused = None
+        fused = factor = x_all = None
         if comm is not None and os.environ.get("DTFX_MLP_COMM", "auto") != "rccl":
-            # gradient exchange fused into the backward kernel when verified and faster
+            # exchange engine (fused into the backward kernel / factor all-gather) when
+            # verified and faster than the all-reduce engine
             from ..parallel.select import pick_mlp_engine
 
+            if world <= 8:
+                # every process holds the whole training set (like every reference
+                # process, main.py:43-44): equal-length shards of all ranks, resident
+                n = min(len(dataset.train.images[q::world]) for q in range(world))
+                x_all = torch.stack([torch.from_numpy(dataset.train.images[q::world][:n]).float()
+                                     for q in range(world)]).to(dev).contiguous()
+                tr_x, tr_y = x_all[rank], tr_y[:n]
             kind, c, _ = pick_mlp_engine(params, tr_x.to(dev), tr_y.to(dev), B,
-                                         flags.learning_rate, comm, world, rank, dev)
+                                         flags.learning_rate, comm, world, rank, dev, x_all=x_all)
             fused = c if kind == "fused" else None
+            factor = c if kind == "factor" else None
         tr = FusedMLPTrainer(params, tr_x, tr_y, B, flags.learning_rate,
-                             allreduce=comm.allreduce_sum_ if (comm and not fused) else None,
-                             world_size=world, fused_comm=fused)
+                             allreduce=comm.allreduce_sum_ if (comm and not (fused or factor))
+                             else None, world_size=world, fused_comm=fused, factor_comm=factor,
+                             x_all=x_all if factor is not None else None, rank=rank)
         get_params = lambda: tr.flush().clone()  # noqa: E731
         step_fn = None
     else:
