@@ -65,6 +65,10 @@ def _native_comm(world, rank, dev, max_numel):
 
 
 def main():
+    if os.environ.get("DTFX_WATCHDOG_S"):  # debugging aid: dump every thread's stack, then exit
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["DTFX_WATCHDOG_S"]), exit=True)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--model", choices=["mlp", "bert", "resnet50"], default="mlp",
@@ -87,7 +91,8 @@ def main():
                          "xgmi: one-shot peer-memory all-reduce over xGMI (small buckets); "
                          "auto (MLP, N>1): verify xgmi against RCCL, time both, use the faster; "
                          "torch: torch.distributed nccl(=RCCL) process group")
-    ap.add_argument("--engine", choices=["auto", "fused", "factor", "allreduce"], default="auto",
+    ap.add_argument("--engine", choices=["auto", "fused", "factor", "factor2", "allreduce"],
+                    default="auto",
                     help="MLP, N>1: fused = gradient exchange inside the backward kernel (xGMI LL "
                          "push); factor = sufficient-factor exchange (dz1 all-gathered in the "
                          "head kernel, global W1 gradient formed on every rank from every "
@@ -118,7 +123,10 @@ def main():
         if a.comm == "torch":
             dist.init_process_group("nccl", device_id=dev)
         else:  # control plane over TCP/gloo; gradients over the native RCCL / xGMI communicator
-            dist.init_process_group("gloo")
+            import datetime
+
+            # a collective that cannot complete errors out in minutes instead of hanging
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
 
     if a.model == "bert":
         return bench_bert(a, world, rank, local, dev)
@@ -130,7 +138,7 @@ def main():
     params = init_params(dev, seed=1234)
     x, y = mnist_like_device(a.dataset_size, seed=100 + rank, device=dev)
     x_all = None
-    if 2 <= world <= 8 and a.engine in ("auto", "factor") and a.comm != "torch":
+    if 2 <= world <= 8 and a.engine in ("auto", "factor", "factor2") and a.comm != "torch":
         # every rank's batch stream resident on every GPU (each reference process loads the
         # whole dataset, main.py:43-44): the factor engine then exchanges only dz1
         x_all = torch.empty(world, a.dataset_size, 784, device=dev)
@@ -164,8 +172,9 @@ def main():
                 a.engine_probe = eprobe
                 if kind == "fused":
                     fused_comm, a.comm = c, "xgmi-fused-push"
-                elif kind == "factor":
+                elif kind in ("factor", "factor2"):
                     factor_comm, a.comm = c, "xgmi-factor-allgather"
+                    a.factor_pipeline = kind == "factor2"
         if factor_comm is None:
             x_all = None
         allreduce = None if (fused_comm is not None or factor_comm is not None) else comm.allreduce_sum_
@@ -191,7 +200,8 @@ def main():
     tr = FusedMLPTrainer(params, x, y, batch_size=a.batch_size, learning_rate=a.learning_rate,
                          allreduce=allreduce, world_size=world,
                          max_graph_steps=a.max_graph_steps, fused_comm=fused_comm,
-                         factor_comm=factor_comm, x_all=x_all, rank=rank)
+                         factor_comm=factor_comm, x_all=x_all, rank=rank,
+                         pipeline=getattr(a, "factor_pipeline", True))
     if world > 1:
         barrier = dist.barrier if a.comm != "torch" else (lambda: dist.barrier(device_ids=[local]))
     else:
@@ -211,8 +221,9 @@ def main():
     if barrier:
         barrier()
     elapsed = time.perf_counter() - t0
-    if hasattr(comm if world > 1 else None, "check"):
-        comm.check()  # raises if an xGMI all-reduce ever timed out
+    for c in ((comm, fused_comm, factor_comm) if world > 1 else ()):
+        if hasattr(c, "check"):
+            c.check()  # raises if an xGMI exchange ever timed out
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)

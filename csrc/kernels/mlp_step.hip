@@ -696,6 +696,141 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Pipelined FACTOR engine (world XW, 2 launches per data-parallel step): the
+// mlp_fwdapply_kernel structure with the W1 update formed from EVERY rank's factors:
+//   g = sum_q dz1A[q][jt]^T . x_q(t-1)   (K = XW * BP, the all-gathered factors of step
+//   t-1 and every rank's resident batch), W1new = W1old - lr * g,
+// then step t's forward on W1new.  1024-thread blocks: wave (c, s) owns column slice c
+// (16 of the tile's 56 features) and K split s of 4; the 4 partial slices are added in
+// split order through LDS (identical order on every rank: bit-identical replicas).
+// Small-parameter blocks exchange dW2/db1/db2 partials of step t-1 as in the 3-launch
+// factor engine (waves 0..3 of the block).  The head of step t all-gathers dz1 into dz1A
+// (mlp_head_kernel<.., XW, KS2>).
+template <int XW, int NGT>
+__global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
+    const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
+    const float* __restrict__ x_prev, const float* __restrict__ x, long long xstride,
+    const float* __restrict__ dz1A, Bufs w, int* __restrict__ ctr, float* __restrict__ stats,
+    int stats_ring, int B, int stats_on, MlpXg xg) {
+  const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
+  const int NG = NGT > 0 ? NGT : BP / 16;
+  const int RT = (B + 15) >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int bid = blockIdx.x;
+  if (bid >= HT * KS2) {
+    if (wave < 4)
+      wgrad_small<true, NGT, XW>(bid - HT * KS2, wave, lane,
+                                 MLP_XG_SMALL_EPOCH + (bid - HT * KS2) * 4 + wave, p_new, lr,
+                                 nullptr, w, ctr, stats, stats_ring, B, xg, p_old, stats_on);
+    return;
+  }
+  constexpr int LW = KW2 + 4;
+  __shared__ float Wt[16][LW];
+  __shared__ f32x4 red[4][64];
+  const int jt = bid / KS2, ks = bid % KS2;
+  const int f0 = ks * KW2;
+  const int me = xg.rank;
+  // phase B's x rows (wave w < RT owns row tile w; B <= 128): requested first
+  float4 xa[4];
+  const int rowB = wave * 16 + r;
+  const float rmB = rowB < B ? 1.f : 0.f;
+  if (wave < RT) {
+    const float* xr = x + (size_t)(rowB < B ? rowB : B - 1) * D + f0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int k = 16 * g + 4 * q;
+      xa[g] = f4(xr + (k < KW2 ? k : 0));
+    }
+  }
+  // ---- phase A: slice c, K split s (2 splits) ------------------------------------------
+  const int c = wave & 3, sp = wave >> 2;
+  const int fl = c * 16 + r;
+  const bool cv = fl < KW2;
+  const int fc = f0 + (cv ? fl : KW2 - 1);
+  const int G = XW * NG, per = (G + 1) / 2;
+  const int g0 = sp * per, g1 = min(G, g0 + per);
+  float pw[4];
+  if (sp == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = jt * 16 + q * 4 + i;
+      pw[i] = p_old[OFF_W1 + (size_t)(j < H ? j : H - 1) * D + fc];
+    }
+  }
+  f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+  constexpr int CH = 7;
+  for (int c0 = g0; c0 < g1; c0 += CH) {
+    float4 av[CH];
+    float xv[CH][4];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int g = c0 + i;
+      if (g < g1) {  // wave-uniform
+        const int qq = g / NG, gg = g - qq * NG;
+        av[i] = f4(dz1A + ((size_t)qq * HP + jt * 16 + r) * BP + gg * 16 + q * 4);
+        const float* xq = x_prev + (long long)(qq - me) * xstride + fc;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int b = gg * 16 + q * 4 + e;  // rows >= B: dz1A is zero there
+          xv[i][e] = xq[(size_t)(b < B ? b : B - 1) * D];
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      if (c0 + i < g1) {
+        acc0 = mfma16x16x4(av[i].x, xv[i][0], acc0);
+        acc1 = mfma16x16x4(av[i].y, xv[i][1], acc1);
+        acc0 = mfma16x16x4(av[i].z, xv[i][2], acc0);
+        acc1 = mfma16x16x4(av[i].w, xv[i][3], acc1);
+      }
+    }
+  }
+  f32x4 part;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) part[i] = acc0[i] + acc1[i];
+  if (sp > 0) red[c][lane] = part;
+  __syncthreads();
+  if (sp == 0) {
+    const f32x4 o = red[c][lane];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[i] += o[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hl = q * 4 + i, j = jt * 16 + hl;
+      const float v = pw[i] - lr * part[i];
+      if (cv) {
+        Wt[hl][fl] = j < H ? v : 0.f;
+        if (j < H) p_new[OFF_W1 + (size_t)j * D + f0 + fl] = v;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- phase B: z1 partial of row tile `wave` over the block's 56 features ----------
+  if (wave >= RT) return;
+  float4 wb[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int k = 16 * g + 4 * q;
+    wb[g] = k < KW2 ? *reinterpret_cast<const float4*>(&Wt[r][k]) : float4{0.f, 0.f, 0.f, 0.f};
+  }
+  f32x4 o0 = {0, 0, 0, 0}, o1 = {0, 0, 0, 0};
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    o0 = mfma16x16x4(xa[g].x * rmB, wb[g].x, o0);
+    o1 = mfma16x16x4(xa[g].y * rmB, wb[g].y, o1);
+    o0 = mfma16x16x4(xa[g].z * rmB, wb[g].z, o0);
+    o1 = mfma16x16x4(xa[g].w * rmB, wb[g].w, o1);
+  }
+  float* out = w.slab + ((size_t)ks * BP + wave * 16 + q * 4) * HP + jt * 16 + r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[(size_t)i * HP] = o0[i] + o1[i];
+}
+
 // ---------------------------------------------------------------------------
 // K3, factor engine (sufficient-factor exchange, world XW): the backprop factors dz1 of
 // every rank were all-gathered by mlp_head_kernel<.., XW> into dz1A [XW][HP][BP], and every
@@ -925,16 +1060,21 @@ void mlp_wgrad_xg_launch(float* p, float lr, const float* x, float* ws, int* ctr
 
 // Factor engine launches (see mlp_wgrad_factor_kernel).
 void mlp_head_xg_launch(const float* p, const int* labels, float* ws, float* dz1A, int B,
-                        hipStream_t stream, const MlpXg& xg, int world) {
+                        hipStream_t stream, const MlpXg& xg, int world, int nslab) {
   using namespace mlp;
   check_b(B);
+  if (nslab != KS && nslab != KS2) throw std::runtime_error("mlp_head_xg: nslab must be 7 or 14");
   if (xg.S < (long long)HP * (((B + 15) / 16) * 16))
     throw std::runtime_error("mlp_head_xg: exchange slots smaller than the factor plane");
   const Bufs w = make_bufs(ws, B);
 #define DTFX_HX(WW)                                                                            \
   case WW:                                                                                     \
-    hipLaunchKernelGGL((mlp_head_kernel<false, false, WW>), dim3(B), dim3(64), 0, stream, p, p, \
-                       0.f, nullptr, labels, w, B, nullptr, xg, dz1A);                         \
+    if (nslab == KS)                                                                           \
+      hipLaunchKernelGGL((mlp_head_kernel<false, false, WW>), dim3(B), dim3(64), 0, stream, p, \
+                         p, 0.f, nullptr, labels, w, B, nullptr, xg, dz1A);                    \
+    else                                                                                       \
+      hipLaunchKernelGGL((mlp_head_kernel<false, false, WW, KS2>), dim3(B), dim3(64), 0, stream, \
+                         p, p, 0.f, nullptr, labels, w, B, nullptr, xg, dz1A);                 \
     break;
   switch (world) {
     DTFX_HX(2) DTFX_HX(3) DTFX_HX(4) DTFX_HX(5) DTFX_HX(6) DTFX_HX(7) DTFX_HX(8)
@@ -1001,6 +1141,38 @@ void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipSt
   const Bufs w = make_bufs(ws, B);
   hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS2>), dim3(B), dim3(64), 0, stream, p, p,
                      0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// Pipelined factor engine, first launch (see mlp_fwdapply_factor_kernel).
+void mlp_fwdapply_factor_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
+                                const float* x, long long xstride, const float* dz1A, float* ws,
+                                int* ctr, float* stats, int stats_ring, int B, int stats_on,
+                                hipStream_t stream, const MlpXg& xg, int world) {
+  using namespace mlp;
+  check_b(B);
+  if ((B + 15) / 16 > 8) throw std::runtime_error("mlp_fwdapply_factor: batch must be <= 128");
+  if (!p_old || !p_new || p_old == p_new || !x_prev || !x || !ctr || !dz1A)
+    throw std::runtime_error("mlp_fwdapply_factor: needs ping-pong buffers, batches, ctr, dz1A");
+  if (xg.S < NPARAM) throw std::runtime_error("mlp_fwdapply_factor: exchange slots too small");
+  const Bufs w = make_bufs(ws, B);
+  dim3 grid(HT * KS2 + HT), block(512);
+#define DTFX_FF(WW, NGT)                                                                       \
+  hipLaunchKernelGGL((mlp_fwdapply_factor_kernel<WW, NGT>), grid, block, 0, stream, p_old,     \
+                     p_new, lr, x_prev, x, xstride, dz1A, w, ctr, stats, stats_ring, B,        \
+                     stats_on, xg)
+#define DTFX_FFW(WW)                                 \
+  case WW:                                           \
+    if ((B + 15) / 16 == 7) DTFX_FF(WW, 7);          \
+    else DTFX_FF(WW, 0);                             \
+    break;
+  switch (world) {
+    DTFX_FFW(2) DTFX_FFW(3) DTFX_FFW(4) DTFX_FFW(5) DTFX_FFW(6) DTFX_FFW(7) DTFX_FFW(8)
+    default:
+      throw std::runtime_error("mlp_fwdapply_factor: world must be 2..8");
+  }
+#undef DTFX_FFW
+#undef DTFX_FF
   DTFX_HIP_CHECK(hipGetLastError());
 }
 }  // namespace dtfx

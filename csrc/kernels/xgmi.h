@@ -48,7 +48,13 @@ constexpr int MLP_XG_HEAD_EPOCH = 512;
 // factors dz1 of every rank into dz1A [world][112][BP], then the weight-gradient launch that
 // forms the global dW1 from them and every rank's (resident) batch x, applying directly.
 void mlp_head_xg_launch(const float* p, const int* labels, float* ws, float* dz1A, int B,
-                        hipStream_t stream, const MlpXg& xg, int world);
+                        hipStream_t stream, const MlpXg& xg, int world, int nslab = 7);
+// Pipelined factor engine: step t-1's global W1 update (from dz1A and every rank's x_prev)
+// fused with step t's forward (head of step t: mlp_head_xg_launch with nslab = 14).
+void mlp_fwdapply_factor_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
+                                const float* x, long long xstride, const float* dz1A, float* ws,
+                                int* ctr, float* stats, int stats_ring, int B, int stats_on,
+                                hipStream_t stream, const MlpXg& xg, int world);
 void mlp_wgrad_factor_launch(float* p, float lr, const float* x, long long xstride,
                              const float* dz1A, float* ws, int* ctr, float* stats, int stats_ring,
                              int B, hipStream_t stream, const MlpXg& xg, int world);

@@ -128,11 +128,23 @@ class XgmiAllReduce {
 
   // Factor engine: head launch with the dz1 all-gather, then the global-dW1 launch.
   void mlp_head(uintptr_t p, uintptr_t labels, uintptr_t ws, uintptr_t dz1A, int B,
-                uintptr_t stream, double timeout_s) {
+                uintptr_t stream, double timeout_s, int nslab) {
     if (!ready_) throw std::runtime_error("xgmi: open() the peer handles first");
     if (mode_ != XG_LL_PUSH) throw std::runtime_error("xgmi: the factor exchange needs protocol push");
     mlp_head_xg_launch((const float*)p, (const int*)labels, (float*)ws, (float*)dz1A, B,
-                       (hipStream_t)stream, mlp_xg(timeout_s), world_);
+                       (hipStream_t)stream, mlp_xg(timeout_s), world_, nslab);
+  }
+
+  void mlp_fwdapply_factor(uintptr_t p_old, uintptr_t p_new, float lr, uintptr_t x_prev,
+                           uintptr_t x, long long xstride, uintptr_t dz1A, uintptr_t ws,
+                           uintptr_t ctr, uintptr_t stats, int ring, int B, int stats_on,
+                           uintptr_t stream, double timeout_s) {
+    if (!ready_) throw std::runtime_error("xgmi: open() the peer handles first");
+    if (mode_ != XG_LL_PUSH) throw std::runtime_error("xgmi: the factor exchange needs protocol push");
+    mlp_fwdapply_factor_launch((const float*)p_old, (float*)p_new, lr, (const float*)x_prev,
+                               (const float*)x, xstride, (const float*)dz1A, (float*)ws,
+                               (int*)ctr, (float*)stats, ring, B, stats_on, (hipStream_t)stream,
+                               mlp_xg(timeout_s), world_);
   }
 
   void mlp_wgrad_factor(uintptr_t p, float lr, uintptr_t x, long long xstride, uintptr_t dz1A,
@@ -194,7 +206,11 @@ void register_xgmi(py::module_& m) {
            py::arg("stream"), py::arg("timeout_s") = 2.0)
       .def("mlp_head", &dtfx::XgmiAllReduce::mlp_head, py::arg("p"), py::arg("labels"),
            py::arg("ws"), py::arg("dz1A"), py::arg("B"), py::arg("stream"),
-           py::arg("timeout_s") = 2.0)
+           py::arg("timeout_s") = 2.0, py::arg("nslab") = 7)
+      .def("mlp_fwdapply_factor", &dtfx::XgmiAllReduce::mlp_fwdapply_factor, py::arg("p_old"),
+           py::arg("p_new"), py::arg("lr"), py::arg("x_prev"), py::arg("x"), py::arg("xstride"),
+           py::arg("dz1A"), py::arg("ws"), py::arg("ctr"), py::arg("stats"), py::arg("ring"),
+           py::arg("B"), py::arg("stats_on"), py::arg("stream"), py::arg("timeout_s") = 2.0)
       .def("mlp_wgrad_factor", &dtfx::XgmiAllReduce::mlp_wgrad_factor, py::arg("p"),
            py::arg("lr"), py::arg("x"), py::arg("xstride"), py::arg("dz1A"), py::arg("ws"),
            py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"),

@@ -156,6 +156,32 @@ def step_factor(p, x, labels, ws: StepWorkspace, lr, comm, dz1A, xstride, stats=
     comm.mlp_wgrad_factor(p, lr, x, xstride, dz1A, ws, stats)
 
 
+def step_factor_pipelined(p_old, p_new, x_prev, x, labels, ws: StepWorkspace, lr, apply, comm,
+                          dz1A, xstride, stats=True):
+    """Two-launch data-parallel step of the factor engine: (1) step t-1's GLOBAL update --
+    W1 from every rank's gathered dz1 and resident previous batch, dW2/db1/db2 exchanged --
+    fused with step t's forward; (2) the head of step t, which all-gathers dz1 into
+    ``dz1A``.  ``lr`` already divided by the world size; ``apply=False``: copy + forward.
+    The last update stays pending until ``flush_factor``."""
+    _check(x, labels, ws.B)
+    _check(x_prev, None, ws.B)
+    _check_flat(p_old, p_new)
+    if ws.B > 128:
+        raise ValueError("the pipelined factor step supports batch <= 128")
+    if dz1A.numel() < comm.world_size * factor_plane(ws.B):
+        raise ValueError("dz1A must hold world * 112 * BP f32 values")
+    comm.mlp_fwdapply_factor(p_old, p_new, lr, x_prev, x, xstride, dz1A, ws, apply, stats)
+    comm.mlp_head(p_new, labels, ws, dz1A, nslab=14)
+
+
+def flush_factor(p, x_prev, ws: StepWorkspace, lr, comm, dz1A, xstride, stats=True):
+    """Apply the pending update of the last pipelined factor step in place (the 3-launch
+    factor engine's weight-gradient launch on the same factors and batches)."""
+    _check(x_prev, None, ws.B)
+    _check_flat(p)
+    comm.mlp_wgrad_factor(p, lr, x_prev, xstride, dz1A, ws, stats)
+
+
 def step_grad(p_old, x, labels, ws: StepWorkspace, grad, prev_grad=None, lr=0.0, p_new=None,
               stats=True):
     """Forward/backward writing ``grad``; optionally first applies ``prev_grad``.

@@ -50,7 +50,10 @@ def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_k
                           protocol=proto)
         except Exception as e:  # no IPC / peer mapping on this node
             err = repr(e)
+            print("[bench] rank %d: xgmi-%s: %s" % (rank, proto, err), file=sys.stderr)
         if not agree(xg is not None):
+            if xg is not None:
+                xg.destroy()
             if rank == 0:
                 print("[bench] xgmi-%s unavailable (%s)" % (proto, err), file=sys.stderr)
             continue
@@ -111,11 +114,14 @@ def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_k
     for _ in range(3):  # interleaved, best of three each
         for k in names:
             probe[k] = min(probe[k], timed(graphs[k]))
-    for k in names:
-        if k != "rccl":
-            cands[k].check()
+    for k in names:  # a protocol that timed out on ANY rank is out, on every rank
+        if k != "rccl" and not agree(not cands[k].failed()):
+            probe[k] = float("inf")
     probe = {k: round(v, 2) for k, v in probe.items()}
     best = min(names, key=lambda k: (probe[k], k))  # times are max-reduced: identical everywhere
+    if probe[best] == float("inf"):
+        best = "rccl"
+        cands["rccl"] = rccl
     for k in names:
         if k not in (best, "rccl"):
             cands[k].destroy()
@@ -133,7 +139,9 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
       ``("factor", XgmiComm)``  -- sufficient-factor exchange: the backprop factors dz1 are
                                    all-gathered inside the head kernel and every rank forms
                                    the global W1 gradient from them and every rank's batch
-                                   (needs ``x_all`` [world, n, 784], ``x = x_all[rank]``).
+                                   (needs ``x_all`` [world, n, 784], ``x = x_all[rank]``);
+      ``("factor2", XgmiComm)`` -- the same exchange in the two-launch pipelined step (the
+                                   global update of step t-1 inside step t's forward launch).
     An xGMI engine must (on every rank) build, agree with the all-reduce engine after
     ``verify_steps`` identical SGD steps, keep the replicas bit-identical, and (mode "auto") be
     the fastest over ``time_steps`` graph-replayed steps (max over ranks); mode "fused" /
@@ -148,9 +156,12 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
 
     if world < 2 or world > 8 or mode == "allreduce":
         return "allreduce", ar_comm, None
-    kinds = {"auto": ["fused", "factor"], "fused": ["fused"], "factor": ["factor"]}[mode]
+    kinds = {"auto": ["fused", "factor", "factor2"], "fused": ["fused"],
+             "factor": ["factor"], "factor2": ["factor2"]}[mode]
     if x_all is None:
-        kinds = [k for k in kinds if k != "factor"]
+        kinds = [k for k in kinds if not k.startswith("factor")]
+    if batch_size > 128:
+        kinds = [k for k in kinds if k != "factor2"]
     comms = {}
     for kind in kinds:
         c, err = None, ""
@@ -159,10 +170,14 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
                          protocol="push")
         except Exception as e:
             err = repr(e)
+            print("[bench] rank %d: %s xgmi engine: %s" % (rank, kind, err), file=sys.stderr)
         if agree(c is not None):
             comms[kind] = c
-        elif rank == 0:
-            print("[bench] %s xgmi engine unavailable (%s)" % (kind, err), file=sys.stderr)
+        else:
+            if c is not None:
+                c.destroy()
+            if rank == 0:
+                print("[bench] %s xgmi engine unavailable (%s)" % (kind, err), file=sys.stderr)
     if not comms:
         return "allreduce", ar_comm, None
 
@@ -170,9 +185,10 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
         if kind == "fused":
             return FusedMLPTrainer(params, x, y, batch_size, lr, world_size=world,
                                    fused_comm=comms[kind])
-        if kind == "factor":
+        if kind in ("factor", "factor2"):  # factor2: the two-launch pipelined variant
             return FusedMLPTrainer(params, None, y, batch_size, lr, world_size=world,
-                                   factor_comm=comms[kind], x_all=x_all, rank=rank)
+                                   factor_comm=comms[kind], x_all=x_all, rank=rank,
+                                   pipeline=kind == "factor2")
         return FusedMLPTrainer(params, x, y, batch_size, lr, allreduce=ar_comm.allreduce_sum_,
                                world_size=world)
 
@@ -225,8 +241,9 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
     for _ in range(2):
         for k in names:
             probe[k] = min(probe[k], timed(trainers[k]))
-    for c in comms.values():
-        c.check()
+    for k, c in comms.items():  # an engine that timed out on ANY rank is out, on every rank
+        if not agree(not c.failed()):
+            probe[k] = float("inf")
     probe = {k: round(v, 2) for k, v in probe.items()}
     best = min(names, key=lambda k: (probe[k], k))  # max-reduced: identical everywhere
     if rank == 0:

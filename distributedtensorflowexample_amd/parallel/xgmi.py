@@ -28,12 +28,26 @@ class XgmiComm:
         # "ll": 8-byte {value, epoch} words (no flag round trip; world <= 8); "flag": slots +
         # per-block epoch flags (any world <= 16)
         self.protocol = protocol or ("ll" if self.world_size <= 8 else "flag")
-        self._h = hip().XgmiAllReduce(self.rank, self.world_size, self.device.index,
-                                      self.max_numel, self.protocol)
         if store is None:
             store = dist.distributed_c10d._get_default_store()
-        store.set("%s/%d" % (key, self.rank), self._h.handle())
+        # Every rank ALWAYS publishes its key -- an empty handle when its own allocation or
+        # export failed -- so no peer blocks in store.get on a rank that gave up; every rank
+        # then fails the same way (callers agree on availability through a collective).
+        err, handle = None, b""
+        try:
+            self._h = hip().XgmiAllReduce(self.rank, self.world_size, self.device.index,
+                                          self.max_numel, self.protocol)
+            handle = self._h.handle()
+        except Exception as e:  # noqa: BLE001 - re-raised below, after publishing
+            err, self._h = e, None
+        store.set("%s/%d" % (key, self.rank), handle)
         handles = [bytes(store.get("%s/%d" % (key, j))) for j in range(self.world_size)]
+        if err is not None:
+            raise RuntimeError("xgmi rank %d: %r" % (self.rank, err))
+        missing = [j for j, h in enumerate(handles) if not h]
+        if missing:
+            self._h.close()
+            raise RuntimeError("xgmi: ranks %s could not export their buffers" % missing)
         self._h.open(handles)
 
     def allreduce_sum_(self, t):
@@ -55,13 +69,27 @@ class XgmiComm:
                           ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B,
                           torch.cuda.current_stream().cuda_stream, self.timeout_s)
 
-    def mlp_head(self, p, labels, ws, dz1A):
+    def mlp_head(self, p, labels, ws, dz1A, nslab=7):
         """Factor engine: MLP head launch that also all-gathers every rank's backprop factors
-        dz1 into ``dz1A`` [world, 112, BP] (protocol "push"); see ``ops.mlp_step.step_factor``."""
+        dz1 into ``dz1A`` [world, 112, BP] (protocol "push"); see ``ops.mlp_step.step_factor``.
+        ``nslab``: partial-z1 planes left by the forward (7: 3-launch, 14: pipelined)."""
         from ..ops._ext import ptr
 
         self._h.mlp_head(ptr(p), ptr(labels), ptr(ws.buf), ptr(dz1A), ws.B,
-                         torch.cuda.current_stream().cuda_stream, self.timeout_s)
+                         torch.cuda.current_stream().cuda_stream, self.timeout_s, int(nslab))
+
+    def mlp_fwdapply_factor(self, p_old, p_new, lr, x_prev, x, xstride, dz1A, ws, apply,
+                            stats=True):
+        """Pipelined factor engine, first launch: step t-1's global W1 update from the
+        gathered factors and every rank's previous batch (+ small-parameter exchange),
+        fused with step t's forward; ``p_old`` -> ``p_new``."""
+        from ..ops._ext import ptr
+
+        self._h.mlp_fwdapply_factor(ptr(p_old), ptr(p_new), float(lr) if apply else 0.0,
+                                    ptr(x_prev if apply else x), ptr(x), int(xstride), ptr(dz1A),
+                                    ptr(ws.buf), ptr(ws.ctr), ptr(ws.stats) if stats else 0,
+                                    ws.stats_ring, ws.B, 1 if apply else 0,
+                                    torch.cuda.current_stream().cuda_stream, self.timeout_s)
 
     def mlp_wgrad_factor(self, p, lr, x, xstride, dz1A, ws, stats=True):
         """Factor engine: global dW1 from the gathered factors and every rank's batch
@@ -78,6 +106,11 @@ class XgmiComm:
         if self.rank != root:
             t.zero_()
         return self.allreduce_sum_(t)
+
+    def failed(self):
+        """True if any call timed out waiting for a peer (synchronizes the device)."""
+        torch.cuda.synchronize(self.device)
+        return bool(self._h.error())
 
     def check(self):
         """Raise if any all-reduce timed out waiting for a peer (synchronizes the device)."""

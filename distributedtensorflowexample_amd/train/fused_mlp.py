@@ -89,9 +89,11 @@ class FusedMLPTrainer:
         self.ws.set_global_step(global_step)
         self.pos = int(global_step) % self.nbatches  # next batch (host mirror)
         self.pending = False
-        # single GPU, no communicator: the two-launch pipelined step
-        self.pipelined = bool(pipeline and self.world_size == 1 and allreduce is None
-                              and fused_comm is None and factor_comm is None)
+        # single GPU, no communicator -- or the factor engine -- : the two-launch pipelined
+        # step (the factor engine's needs batch <= 128)
+        self.pipelined = bool(pipeline and allreduce is None and fused_comm is None and (
+            (self.world_size == 1 and factor_comm is None)
+            or (factor_comm is not None and self.B <= 128)))
         self.max_graph_steps = int(max_graph_steps)
         self._graphs = {}
         self._pool = None
@@ -100,8 +102,9 @@ class FusedMLPTrainer:
     @property
     def direct(self):
         """SGD apply fused into the backward kernel (one GPU, or the fused xGMI exchange)."""
-        return (self.fused_comm is not None or self.factor_comm is not None
-                or (self.allreduce is None and self.world_size == 1 and not self.pipelined))
+        return not self.pipelined and (
+            self.fused_comm is not None or self.factor_comm is not None
+            or (self.allreduce is None and self.world_size == 1))
 
     @property
     def params(self):
@@ -112,7 +115,11 @@ class FusedMLPTrainer:
         """Apply the pending update in place (DP: p -= lr/N * grad; pipelined: the last
         step's factors)."""
         if self.pending:
-            if self.pipelined:
+            if self.pipelined and self.factor_comm is not None:
+                xp, _ = self.batch((self.pos - 1) % self.nbatches)
+                mlp_step.flush_factor(self.bufs[self.cur], xp, self.ws, self.lr / self.world_size,
+                                      self.factor_comm, self.dz1A, self.xstride)
+            elif self.pipelined:
                 xp, _ = self.batch((self.pos - 1) % self.nbatches)
                 mlp_step.flush_pipelined(self.bufs[self.cur], xp, self.ws, self.lr)
             else:
@@ -137,6 +144,14 @@ class FusedMLPTrainer:
     def _step_launches(self):
         xb, yb = self.batch(self.pos)
         self.pos = (self.pos + 1) % self.nbatches
+        if self.factor_comm is not None and self.pipelined:
+            xp, _ = self.batch((self.pos - 2) % self.nbatches)  # pos already advanced
+            mlp_step.step_factor_pipelined(self.bufs[self.cur], self.bufs[self.cur ^ 1], xp, xb,
+                                           yb, self.ws, self.lr / self.world_size, self.pending,
+                                           self.factor_comm, self.dz1A, self.xstride)
+            self.cur ^= 1
+            self.pending = True
+            return
         if self.factor_comm is not None:
             mlp_step.step_factor(self.bufs[self.cur], xb, yb, self.ws, self.lr / self.world_size,
                                  self.factor_comm, self.dz1A, self.xstride)

@@ -68,6 +68,7 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
 
     if use_gpu:
         fused = factor = x_all = None
+        pipe = True
         if comm is not None and os.environ.get("DTFX_MLP_COMM", "auto") != "rccl":
             # exchange engine (fused into the backward kernel / factor all-gather) when
             # verified and faster than the all-reduce engine
@@ -83,11 +84,13 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
             kind, c, _ = pick_mlp_engine(params, tr_x.to(dev), tr_y.to(dev), B,
                                          flags.learning_rate, comm, world, rank, dev, x_all=x_all)
             fused = c if kind == "fused" else None
-            factor = c if kind == "factor" else None
+            factor = c if kind in ("factor", "factor2") else None
+            pipe = kind != "factor"
         tr = FusedMLPTrainer(params, tr_x, tr_y, B, flags.learning_rate,
                              allreduce=comm.allreduce_sum_ if (comm and not (fused or factor))
                              else None, world_size=world, fused_comm=fused, factor_comm=factor,
-                             x_all=x_all if factor is not None else None, rank=rank)
+                             x_all=x_all if factor is not None else None, rank=rank,
+                             pipeline=pipe if comm is not None else True)
         get_params = lambda: tr.flush().clone()  # noqa: E731
         step_fn = None
     else:

@@ -173,7 +173,7 @@ def test_fused_mlp_exchange_matches_allreduce_engine(gpu, world):
         assert ok, (r, msg)
 
 
-def _factor_worker(rank, world, port, q, B):
+def _factor_worker(rank, world, port, q, B, pipeline):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -194,7 +194,8 @@ def _factor_worker(rank, world, port, q, B):
         ref = XgmiComm(rank, world, params.numel(), device=dev, key="s/ll", protocol="ll")
         lr = 0.05
         tf = FusedMLPTrainer(params, None, y, B, lr, world_size=world, factor_comm=fc,
-                             x_all=x_all, rank=rank)
+                             x_all=x_all, rank=rank, pipeline=pipeline)
+        assert tf.pipelined == pipeline
         ta = FusedMLPTrainer(params, x_all[rank], y, B, lr, world_size=world,
                              allreduce=ref.allreduce_sum_)
         tf.run(7, use_graph=False)   # eager
@@ -217,15 +218,17 @@ def _factor_worker(rank, world, port, q, B):
         q.put((rank, False, repr(e)))
 
 
-@pytest.mark.parametrize("world,B", [(2, 100), (3, 100), (2, 64)])
-def test_factor_mlp_exchange_matches_allreduce_engine(gpu, world, B):
+@pytest.mark.parametrize("world,B,pipeline", [(2, 100, False), (3, 100, False), (2, 64, False),
+                                               (2, 100, True), (3, 100, True), (2, 64, True)])
+def test_factor_mlp_exchange_matches_allreduce_engine(gpu, world, B, pipeline):
     """Sufficient-factor engine (dz1 all-gathered in the head kernel, global W1 gradient
     formed on every rank from every rank's batch) follows the all-reduce engine's SGD
     trajectory, with bit-identical replicas."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_factor_worker, args=(r, world, port, q, B)) for r in range(world)]
+    procs = [ctx.Process(target=_factor_worker, args=(r, world, port, q, B, pipeline))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
