@@ -160,9 +160,28 @@ class MirroredStrategy:
 
     def check_replicas_identical(self, t):
         """Debug check: max over replicas of |t - t_rank0|."""
-        ref = t.detach().clone()
-        self.broadcast_(ref, 0)
-        d = (t.detach() - ref).abs().max().reshape(1).float()
-        if self.num_replicas_in_sync > 1:
-            self.comm.allreduce_max_(d)
-        return float(d.item())
+        return replica_divergence(self.comm, t, self.num_replicas_in_sync)
+
+
+def replica_divergence(comm, t, world):
+    """Max over replicas of |t - t_rank0| (0.0 when the sync replicas are bit-identical).
+    Debug check of the deterministic sync mode: every step applies the same
+    reduced gradient in the same order, so any nonzero value is a race or a lost update."""
+    ref = t.detach().clone()
+    if world > 1:
+        comm.broadcast_(ref, 0)
+    d = (t.detach() - ref).abs().max().reshape(1).float()
+    if world > 1:
+        comm.allreduce_max_(d)
+    return float(d.item())
+
+
+class ReplicaDivergenceError(RuntimeError):
+    pass
+
+
+def assert_replicas_identical(comm, t, world, step):
+    d = replica_divergence(comm, t, world)
+    if d != 0.0:
+        raise ReplicaDivergenceError("replicas diverged at step %d: max |p - p_rank0| = %g"
+                                     % (step, d))

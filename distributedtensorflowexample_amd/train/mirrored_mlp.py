@@ -196,6 +196,11 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
                 start_time, start_step = time.time(), step
             if is_chief and step % int(flags.eval_every) == 0:
                 log("test accuracy: {}".format(test_accuracy()))
+            k = int(getattr(flags, "check_replicas_every", 0) or 0)
+            if k > 0 and world > 1 and step % k == 0:
+                from ..parallel.mirrored import assert_replicas_identical
+
+                assert_replicas_identical(comm, get_params(), world, step)
             if step >= steps_total:
                 break
         if is_chief:

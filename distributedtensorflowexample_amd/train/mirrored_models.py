@@ -105,6 +105,11 @@ def train_model_mirrored(flags, log=print):
             tr.step(use_graph)
             state["step"] += 1
             step = global_step()
+            k = int(getattr(flags, "check_replicas_every", 0) or 0)
+            if k > 0 and world > 1 and step % k == 0:
+                from ..parallel.mirrored import assert_replicas_identical
+
+                assert_replicas_identical(comm, model.params.master, world, step)
             if step % int(flags.log_every) == 0 or step == steps_total:
                 loss, acc = tr.stats()
                 if writer is not None:

@@ -93,3 +93,47 @@ def test_ddp_equals_large_batch_single_process():
             for p in m.parameters():
                 p -= 0.5 * p.grad
     assert torch.allclose(res[0][0], _flat(m), atol=1e-5)
+
+
+def _divergence_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from distributedtensorflowexample_amd.parallel.comm import TorchComm
+        from distributedtensorflowexample_amd.parallel.mirrored import (ReplicaDivergenceError,
+                                                                        assert_replicas_identical,
+                                                                        replica_divergence)
+
+        comm = TorchComm()
+        t = torch.arange(1000, dtype=torch.float32)
+        assert_replicas_identical(comm, t, world, step=10)  # identical: passes
+        t2 = t.clone()
+        if rank == 1:
+            t2[123] = torch.nextafter(t2[123], t2[124])  # one ulp off on one replica
+        d = replica_divergence(comm, t2, world)
+        raised = False
+        try:
+            assert_replicas_identical(comm, t2, world, step=20)
+        except ReplicaDivergenceError:
+            raised = True
+        q.put((rank, d > 0 and raised, "d=%g raised=%s" % (d, raised)))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, False, repr(e)))
+
+
+def test_replica_divergence_check():
+    """--check_replicas_every: bit-identical replicas pass, one differing element on one
+    replica is caught on EVERY rank."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_divergence_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(30)
+    for r, ok, msg in res:
+        assert ok, (r, msg)
