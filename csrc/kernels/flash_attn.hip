@@ -72,14 +72,25 @@ __device__ __forceinline__ bf16x8 gfrag(const unsigned short* base, int ld, int 
   const int r = min(r0 + (lane & 15), rmax);
   return *(const bf16x8*)(base + (size_t)r * ld + k0 + 8 * (lane >> 4));
 }
-// cooperative load of a 64-row x 64-col bf16 tile (rows >= nrows zeroed) into an LDS image
-__device__ __forceinline__ void load_tile(char* dst, const unsigned short* src, int ld, int r0,
-                                          int S) {
-  for (int i = threadIdx.x; i < T * 8; i += 256) {
-    const int r = i >> 3, c = i & 7;
-    bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (r0 + r < S) v = *(const bf16x8*)(src + (size_t)(r0 + r) * ld + c * 8);
-    *(bf16x8*)(dst + r * LD + c * 16) = v;
+// Register-staged tile load, split in two so the NEXT tile's global loads are in flight
+// while the current tile is computed (one LDS image, refilled between two barriers):
+// fetch_tile issues this thread's two 16-B loads (rows >= S read as zero), put_tile
+// writes them to the LDS image.
+__device__ __forceinline__ void fetch_tile(bf16x8 (&v)[2], const unsigned short* src, int ld,
+                                           int r0, int S) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = threadIdx.x + 256 * k, r = i >> 3, c = i & 7;
+    const int row = r0 + r;
+    v[k] = *(const bf16x8*)(src + (size_t)(row < S ? row : S - 1) * ld + c * 8);
+    if (row >= S) v[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+__device__ __forceinline__ void put_tile(char* dst, const bf16x8 (&v)[2]) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = threadIdx.x + 256 * k, r = i >> 3, c = i & 7;
+    *(bf16x8*)(dst + r * LD + c * 16) = v[k];
   }
 }
 // C-layout (16 rows x 64 cols per wave: rows 4*(lane>>4)+r, col 16j+(lane&15)) -> bf16 LDS tile
@@ -116,10 +127,17 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(int S, int nh,
 #pragma unroll
   for (int j = 0; j < 4; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nkt = (S + T - 1) / T;
+  bf16x8 kr[2], vr[2];
+  fetch_tile(kr, base + Hd, ld, 0, S);
+  fetch_tile(vr, base + 2 * Hd, ld, 0, S);
   for (int kt = 0; kt < nkt; ++kt) {
     __syncthreads();
-    load_tile(Ks, base + Hd, ld, kt * T, S);
-    load_tile(Vs, base + 2 * Hd, ld, kt * T, S);
+    put_tile(Ks, kr);
+    put_tile(Vs, vr);
+    if (kt + 1 < nkt) {  // next key tile in flight during this tile's math
+      fetch_tile(kr, base + Hd, ld, (kt + 1) * T, S);
+      fetch_tile(vr, base + 2 * Hd, ld, (kt + 1) * T, S);
+    }
     __syncthreads();
     f32x4 s[4];
 #pragma unroll
@@ -229,15 +247,27 @@ __global__ __launch_bounds__(256) void flash_dkdv_kernel(
 #pragma unroll
   for (int j = 0; j < 4; ++j) dv[j] = dk[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nqt = (S + T - 1) / T;
-  for (int qt = 0; qt < nqt; ++qt) {
-    __syncthreads();
-    load_tile(Qs, base, ld, qt * T, S);
-    load_tile(dOs, dob, Hd, qt * T, S);
+  bf16x8 qr[2], dr[2];
+  float lv = 0.f, dvv = 0.f;
+  auto fetch = [&](int qt) {
+    fetch_tile(qr, base, ld, qt * T, S);
+    fetch_tile(dr, dob, Hd, qt * T, S);
     if (threadIdx.x < T) {
       const int q = qt * T + threadIdx.x;
-      Ls[threadIdx.x] = q < S ? lse[(size_t)bh * ld_lse + q] : INFINITY;  // P = 0 past S
-      Ds[threadIdx.x] = q < S ? Dv[(size_t)bh * ld_lse + q] : 0.f;
+      lv = q < S ? lse[(size_t)bh * ld_lse + q] : INFINITY;  // P = 0 past S
+      dvv = q < S ? Dv[(size_t)bh * ld_lse + q] : 0.f;
     }
+  };
+  fetch(0);
+  for (int qt = 0; qt < nqt; ++qt) {
+    __syncthreads();
+    put_tile(Qs, qr);
+    put_tile(dOs, dr);
+    if (threadIdx.x < T) {
+      Ls[threadIdx.x] = lv;
+      Ds[threadIdx.x] = dvv;
+    }
+    if (qt + 1 < nqt) fetch(qt + 1);  // next query tile in flight during this tile's math
     __syncthreads();
     f32x4 st[4], dpt[4];
 #pragma unroll
@@ -333,10 +363,17 @@ __global__ __launch_bounds__(256) void flash_dq_kernel(
 #pragma unroll
   for (int j = 0; j < 4; ++j) dq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nkt = (S + T - 1) / T;
+  bf16x8 kr[2], vr[2];
+  fetch_tile(kr, base + Hd, ld, 0, S);
+  fetch_tile(vr, base + 2 * Hd, ld, 0, S);
   for (int kt = 0; kt < nkt; ++kt) {
     __syncthreads();
-    load_tile(Ks, base + Hd, ld, kt * T, S);
-    load_tile(Vs, base + 2 * Hd, ld, kt * T, S);
+    put_tile(Ks, kr);
+    put_tile(Vs, vr);
+    if (kt + 1 < nkt) {  // next key tile in flight during this tile's math
+      fetch_tile(kr, base + Hd, ld, (kt + 1) * T, S);
+      fetch_tile(vr, base + 2 * Hd, ld, (kt + 1) * T, S);
+    }
     __syncthreads();
     f32x4 s[4], dp[4];
 #pragma unroll
