@@ -424,27 +424,40 @@ __device__ __forceinline__ void load_heads(char* const (&dst)[N], const unsigned
 }
 }  // namespace at
 
-__global__ __launch_bounds__(256, 1) void attn_fwd_kernel(
+// Q never goes through LDS: each wave's 32 query rows are only its own A operands, read
+// as MFMA fragments straight from global memory (issued before the K/V staging).  K, V
+// and P then take 70 KB of LDS: two blocks per CU.
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     int S, int nh, const unsigned short* __restrict__ qkv, unsigned short* __restrict__ out,
     float* __restrict__ lse, const float* __restrict__ kmask, float scale) {
   using namespace at;
   extern __shared__ __attribute__((aligned(16))) char sm[];
-  char* Qs = sm;
-  char* Ks = sm + QB;
-  char* Vs = sm + 2 * QB;
-  char* Ps = sm + 3 * QB;
+  char* Ks = sm;
+  char* Vs = sm + QB;
+  char* Ps = sm + 2 * QB;
   const int b = blockIdx.x / nh, h = blockIdx.x % nh;
   const int Hd = nh * D, ld = 3 * Hd;
   const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
-  {
-    char* const dst[3] = {Qs, Ks, Vs};
-    const unsigned short* const src[3] = {base, base + Hd, base + 2 * Hd};
-    const int lds[3] = {ld, ld, ld};
-    at::load_heads<3>(dst, src, lds, S);
-  }
-  __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int cl = lane & 15, rg = (lane >> 4) * 4;
+  bf16x8 qf[2][2];  // [row group i][k half]: rows 32 wave + 16 i + (lane & 15)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 32 * wave + 16 * i + cl;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      qf[i][kk] = *(const bf16x8*)(base + (size_t)(row < S ? row : S - 1) * ld + 32 * kk +
+                                   8 * (lane >> 4));
+      if (row >= S) qf[i][kk] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  {
+    char* const dst[2] = {Ks, Vs};
+    const unsigned short* const src[2] = {base + Hd, base + 2 * Hd};
+    const int lds[2] = {ld, ld};
+    at::load_heads<2>(dst, src, lds, S);
+  }
+  __syncthreads();
 
   float km[8];  // additive key mask for this lane's key column in each key tile
 #pragma unroll
@@ -460,7 +473,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_kernel(
     for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 a = lfrag<true>(Qs, LDQ, r0, 32 * kk, lane);
+      const bf16x8 a = qf[i][kk];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] = mma(a, lfrag<true>(Ks, LDQ, 16 * j, 32 * kk, lane), acc[j]);
     }
@@ -875,7 +888,7 @@ static void check_attn(int S, int nh) {
 void attn_fwd_launch(int Bn, int S, int nh, const void* qkv, void* out, float* lse,
                      const float* kmask, float scale, hipStream_t s) {
   check_attn(S, nh);
-  const size_t lds = 3 * at::QB + at::PB;
+  const size_t lds = 2 * at::QB + at::PB;
   static bool attr = false;
   if (!attr) {
     DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_kernel,
