@@ -74,7 +74,12 @@ __global__ void bn_finalize_kernel(int C, float inv_m, float unbias, const float
   }
 }
 
-// y = act((x - mean) * rstd * gamma + beta + residual); 8 channels per thread
+// y = act((x - mean) * rstd * gamma + beta + residual); 8 channels per thread, computed as
+// y = x * sc + sh (+ res) (ReLU), sc = rstd * gamma, sh = beta - mean * sc.
+// When the grid stride is a multiple of the channel-group count (every power-of-two C
+// up to 2048: 256 % (C / 8) == 0) each thread keeps ONE channel group for its whole
+// grid-stride walk, so its 8 coefficients pairs are loaded once (not 32 scalar loads and
+// a 64-bit modulo per 16-B chunk), and the walk keeps 4 chunks in flight.
 __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
                                                        const unsigned short* __restrict__ x,
                                                        const float* __restrict__ mean,
@@ -86,7 +91,46 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
   const int cg = C >> 3;
   const long long n8 = M * cg;
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (stride % cg == 0) {
+    const int c0 = (int)(i0 % cg) * 8;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = c0 + u;
+      sc[u] = rstd[c] * gamma[c];
+      sh[u] = beta[c] - mean[c] * sc[u];
+    }
+    constexpr int U = 4;
+    for (long long ib = i0; ib < n8; ib += U * stride) {
+      bf16x8 xv[U], rv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const long long i = ib + k * stride;
+        const long long ic = i < n8 ? i : i0;  // in-bounds dummy for the tail
+        xv[k] = ((const bf16x8*)x)[ic];
+        if (res) rv[k] = ((const bf16x8*)res)[ic];
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const long long i = ib + k * stride;
+        if (i >= n8) break;
+        float v[8], r[8];
+        unpack8(xv[k], v);
+        if (res) unpack8(rv[k], r);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          float o = v[u] * sc[u] + sh[u];
+          if (res) o += r[u];
+          if (relu) o = fmaxf(o, 0.f);
+          v[u] = o;
+        }
+        ((bf16x8*)y)[i] = pack8(v);
+      }
+    }
+    return;
+  }
+  for (long long i = i0; i < n8; i += stride) {  // general C
     const int c0 = (int)(i % cg) * 8;
     float v[8], r[8];
     unpack8(((const bf16x8*)x)[i], v);
@@ -131,17 +175,30 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         mu[u] = mean[gg * 8 + u];
         rs[u] = rstd[gg * 8 + u];
       }
-      for (long long r = r0 + rr; r < r1; r += rpp) {
-        const long long i = r * cg + gg;
-        float d[8], xv[8], yv[8];
-        unpack8(((const bf16x8*)dy)[i], d);
-        unpack8(((const bf16x8*)x)[i], xv);
-        if (relu) unpack8(((const bf16x8*)yout)[i], yv);
+      constexpr int U = 4;  // rows in flight per thread
+      for (long long rb = r0 + rr; rb < r1; rb += U * rpp) {
+        bf16x8 dv[U], xq[U], yq[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const float de = (relu && yv[u] <= 0.f) ? 0.f : d[u];
-          a[u] += de;
-          b[u] += de * (xv[u] - mu[u]) * rs[u];
+        for (int k = 0; k < U; ++k) {
+          const long long r = rb + (long long)k * rpp;
+          const long long i = (r < r1 ? r : r0 + rr) * cg + gg;  // in-bounds dummy row
+          dv[k] = ((const bf16x8*)dy)[i];
+          xq[k] = ((const bf16x8*)x)[i];
+          if (relu) yq[k] = ((const bf16x8*)yout)[i];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+          if (rb + (long long)k * rpp >= r1) break;
+          float d[8], xv[8], yv[8];
+          unpack8(dv[k], d);
+          unpack8(xq[k], xv);
+          if (relu) unpack8(yq[k], yv);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float de = (relu && yv[u] <= 0.f) ? 0.f : d[u];
+            a[u] += de;
+            b[u] += de * (xv[u] - mu[u]) * rs[u];
+          }
         }
       }
     }
@@ -169,6 +226,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 }
 
 // dx = gamma * rstd * (dy_eff - sum_dy / M - xhat * sum_dyxh / M); dres = dy_eff (optional)
+// dx = gamma * rstd * (dy_eff - mean(dy_eff) - xhat * mean(dy_eff * xhat))
+//    = A * dy_eff + K1 * x + K0 per channel (A = gamma rstd, K1 = -A rstd S2,
+//      K0 = -A S1 + A rstd S2 mean; S1, S2 = the two column sums / M); dres = dy_eff.
+// Same per-thread channel group / 4-in-flight walk as bn_apply_kernel.
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     long long M, int C, const unsigned short* __restrict__ dy, const unsigned short* __restrict__ yout,
     const unsigned short* __restrict__ x, const float* __restrict__ mean,
@@ -178,7 +239,50 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const int cg = C >> 3;
   const long long n8 = M * cg;
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (stride % cg == 0) {
+    const int c0 = (int)(i0 % cg) * 8;
+    float ka[8], k1[8], k0[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = c0 + u;
+      const float A = gamma[c] * rstd[c], s1 = sum_dy[c] * inv_m, s2 = sum_dyxh[c] * inv_m;
+      ka[u] = A;
+      k1[u] = -A * rstd[c] * s2;
+      k0[u] = -A * s1 + A * rstd[c] * s2 * mean[c];
+    }
+    constexpr int U = 4;
+    for (long long ib = i0; ib < n8; ib += U * stride) {
+      bf16x8 dv[U], xv[U], yv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const long long i = ib + k * stride;
+        const long long ic = i < n8 ? i : i0;
+        dv[k] = ((const bf16x8*)dy)[ic];
+        xv[k] = ((const bf16x8*)x)[ic];
+        if (relu) yv[k] = ((const bf16x8*)yout)[ic];
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const long long i = ib + k * stride;
+        if (i >= n8) break;
+        float d[8], xf[8], yf[8], o[8];
+        unpack8(dv[k], d);
+        unpack8(xv[k], xf);
+        if (relu) unpack8(yv[k], yf);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float de = (relu && yf[u] <= 0.f) ? 0.f : d[u];
+          d[u] = de;
+          o[u] = ka[u] * de + k1[u] * xf[u] + k0[u];
+        }
+        ((bf16x8*)dx)[i] = pack8(o);
+        if (dres) ((bf16x8*)dres)[i] = pack8(d);
+      }
+    }
+    return;
+  }
+  for (long long i = i0; i < n8; i += stride) {  // general C
     const int c0 = (int)(i % cg) * 8;
     float d[8], xv[8], yv[8], o[8];
     unpack8(((const bf16x8*)dy)[i], d);
