@@ -91,13 +91,15 @@ def main():
                          "xgmi: one-shot peer-memory all-reduce over xGMI (small buckets); "
                          "auto (MLP, N>1): verify xgmi against RCCL, time both, use the faster; "
                          "torch: torch.distributed nccl(=RCCL) process group")
-    ap.add_argument("--engine", choices=["auto", "fused", "factor", "factor2", "allreduce"],
+    ap.add_argument("--engine",
+                    choices=["auto", "fused", "fused2", "factor", "factor2", "allreduce"],
                     default="auto",
                     help="MLP, N>1: fused = gradient exchange inside the backward kernel (xGMI LL "
                          "push); factor = sufficient-factor exchange (dz1 all-gathered in the "
                          "head kernel, global W1 gradient formed on every rank from every "
-                         "rank's resident batch); allreduce = separate all-reduce launch; auto "
-                         "= verify + time all, keep the fastest")
+                         "rank's resident batch); fused2 / factor2 = the same exchanges in the "
+                         "two-launch pipelined step; allreduce = separate all-reduce launch; "
+                         "auto = verify + time all, keep the fastest")
     ap.add_argument("--dataset_size", type=int, default=55000)
     ap.add_argument("--dp", action="store_true",
                     help="use the data-parallel path (gradient all-reduce) even on 1 GPU")
@@ -170,11 +172,12 @@ def main():
                                                   comm, world, rank, dev, mode=a.engine,
                                                   x_all=x_all)
                 a.engine_probe = eprobe
-                if kind == "fused":
+                if kind in ("fused", "fused2"):
                     fused_comm, a.comm = c, "xgmi-fused-push"
                 elif kind in ("factor", "factor2"):
                     factor_comm, a.comm = c, "xgmi-factor-allgather"
-                    a.factor_pipeline = kind == "factor2"
+                a.engine_pipeline = kind in ("fused2", "factor2")
+                a.engine_kind = kind
         if factor_comm is None:
             x_all = None
         allreduce = None if (fused_comm is not None or factor_comm is not None) else comm.allreduce_sum_
@@ -201,7 +204,7 @@ def main():
                          allreduce=allreduce, world_size=world,
                          max_graph_steps=a.max_graph_steps, fused_comm=fused_comm,
                          factor_comm=factor_comm, x_all=x_all, rank=rank,
-                         pipeline=getattr(a, "factor_pipeline", True))
+                         pipeline=getattr(a, "engine_pipeline", True))
     if world > 1:
         barrier = dist.barrier if a.comm != "torch" else (lambda: dist.barrier(device_ids=[local]))
     else:
@@ -255,6 +258,7 @@ def main():
                 "parallelism": "dp%d" % world,
                 "comm": _comm_label(a) if (world > 1 or a.dp) else "none",
                 "hipgraph": use_graph,
+                "engine": getattr(a, "engine_kind", "allreduce" if allreduce else "single"),
                 "launches_per_step": 2 if tr.pipelined else 3,
             },
             "comm_probe_us": getattr(a, "comm_probe", None),

@@ -568,11 +568,15 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
 // lr = 0 / stats_on = 0 (the first step after a flush): a pure copy p_old -> p_new.
 // Removes one dependent kernel boundary and one cold-load phase per step vs the 3-launch
 // step (fwd / head / wgrad).
-template <int NGT>
+// XW > 0 (pipelined FUSED data-parallel engine): each wave's local 16x16 gradient slice is
+// exchanged in LL words with the XW - 1 peers (xg_exchange, epoch slot bid*4 + wave) and
+// summed in rank order before the apply -- the all-reduce of the 3-launch fused engine,
+// moved into the next step's first launch (2 launches per data-parallel step).
+template <int NGT, int XW = 0>
 __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
     const float* __restrict__ x_prev, const float* __restrict__ x, Bufs w, int* __restrict__ ctr,
-    float* __restrict__ stats, int stats_ring, int B, int stats_on) {
+    float* __restrict__ stats, int stats_ring, int B, int stats_on, MlpXg xg) {
   const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
   const int NG = NGT > 0 ? NGT : BP / 16;
   const int RT = (B + 15) >> 4;
@@ -581,8 +585,9 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
   constexpr int MAXG = NGT > 0 ? NGT : MAXB / 16;
   const int bid = blockIdx.x;
   if (bid >= HT * KS2) {
-    wgrad_small<true, NGT, 0>(bid - HT * KS2, wave, lane, 0, p_new, lr, nullptr, w, ctr, stats,
-                              stats_ring, B, MlpXg{}, p_old, stats_on);
+    const int jt = bid - HT * KS2;
+    wgrad_small<true, NGT, XW>(jt, wave, lane, MLP_XG_SMALL_EPOCH + jt * 4 + wave, p_new, lr,
+                               nullptr, w, ctr, stats, stats_ring, B, xg, p_old, stats_on);
     return;
   }
   constexpr int LW = KW2 + 4;  // LDS row pitch (floats)
@@ -616,6 +621,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     float4 av[MAXG];
     float xv[MAXG][4];
     float pw[4];
+    const unsigned ep = XW > 0 ? xg.epochs[bid * 4 + wave] + 1 : 0u;
 #pragma unroll
     for (int g = 0; g < MAXG; ++g) {
       if (g < NG) {
@@ -643,14 +649,33 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         acc1 = mfma16x16x4(av[g].w, xv[g][3], acc1);
       }
     }
+    float gv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gv[i] = acc0[i] + acc1[i];
+    bool fail = false;
+    if constexpr (XW > 0) {
+      size_t offw[4];
+      bool okw[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = jt * 16 + q * 4 + i;
+        okw[i] = cv && j < H;
+        offw[i] = OFF_W1 + (size_t)(j < H ? j : 0) * D + fc;
+      }
+      xg_exchange<XW>(xg, ep, offw, okw, gv, fail);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int hl = q * 4 + i, j = jt * 16 + hl;
-      const float v = pw[i] - lr * (acc0[i] + acc1[i]);
+      const float v = fail ? pw[i] : pw[i] - lr * gv[i];  // timed out: keep W1 (err raised)
       if (cv) {
         Wt[hl][fl] = j < H ? v : 0.f;  // padded hidden rows contribute exact zeros
         if (j < H) p_new[OFF_W1 + (size_t)j * D + f0 + fl] = v;
       }
+    }
+    if constexpr (XW > 0) {
+      if (lane == 0) xg.epochs[bid * 4 + wave] = ep;
+      if (fail) atomicExch(xg.err, 1);
     }
   }
   __syncthreads();
@@ -1128,10 +1153,42 @@ void mlp_fwdapply_launch(const float* p_old, float* p_new, float lr, const float
   dim3 grid(HT * KS2 + HT), block(256);
   if ((B + 15) / 16 == 7)
     hipLaunchKernelGGL((mlp_fwdapply_kernel<7>), grid, block, 0, stream, p_old, p_new, lr, x_prev,
-                       x, w, ctr, stats, stats_ring, B, stats_on);
+                       x, w, ctr, stats, stats_ring, B, stats_on, MlpXg{});
   else
     hipLaunchKernelGGL((mlp_fwdapply_kernel<0>), grid, block, 0, stream, p_old, p_new, lr, x_prev,
-                       x, w, ctr, stats, stats_ring, B, stats_on);
+                       x, w, ctr, stats, stats_ring, B, stats_on, MlpXg{});
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// Pipelined fused data-parallel step, first launch (mlp_fwdapply_kernel<.., XW>); the head is
+// mlp_head2_launch.  lr already divided by the world size.
+void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
+                            const float* x, float* ws, int* ctr, float* stats, int stats_ring,
+                            int B, int stats_on, hipStream_t stream, const MlpXg& xg, int world) {
+  using namespace mlp;
+  check_b(B);
+  if (!p_old || !p_new || p_old == p_new || !x_prev || !x || !ctr)
+    throw std::runtime_error("mlp_fwdapply_xg: needs distinct ping-pong buffers, both batches, ctr");
+  if (stats && stats_ring < 1) throw std::runtime_error("mlp_fwdapply_xg: stats_ring < 1");
+  if (xg.S < NPARAM) throw std::runtime_error("mlp_fwdapply_xg: exchange slots smaller than the model");
+  static_assert(HT * KS2 * 4 <= MLP_XG_SMALL_EPOCH, "W1 epoch slots overlap the small ones");
+  const Bufs w = make_bufs(ws, B);
+  dim3 grid(HT * KS2 + HT), block(256);
+#define DTFX_FX(WW, NGT)                                                                     \
+  hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, WW>), grid, block, 0, stream, p_old, p_new, lr, \
+                     x_prev, x, w, ctr, stats, stats_ring, B, stats_on, xg)
+#define DTFX_FXW(WW)                        \
+  case WW:                                  \
+    if ((B + 15) / 16 == 7) DTFX_FX(WW, 7); \
+    else DTFX_FX(WW, 0);                    \
+    break;
+  switch (world) {
+    DTFX_FXW(2) DTFX_FXW(3) DTFX_FXW(4) DTFX_FXW(5) DTFX_FXW(6) DTFX_FXW(7) DTFX_FXW(8)
+    default:
+      throw std::runtime_error("mlp_fwdapply_xg: world must be 2..8");
+  }
+#undef DTFX_FXW
+#undef DTFX_FX
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

@@ -40,7 +40,8 @@ struct MlpXg {
 };
 constexpr int MLP_XG_EPOCHS = 1024;
 // epoch slots of the factor engine (mlp_head_kernel<.., XW> rows / mlp_wgrad_factor_kernel's
-// small-parameter waves); mlp_wgrad_kernel<.., XW> uses [0, 392)
+// small-parameter waves; also the pipelined fused engine's); mlp_wgrad_kernel<.., XW> and
+// mlp_fwdapply_kernel<.., XW> use [0, 392) (never on the same communicator)
 constexpr int MLP_XG_SMALL_EPOCH = 400;
 constexpr int MLP_XG_HEAD_EPOCH = 512;
 
@@ -58,6 +59,12 @@ void mlp_fwdapply_factor_launch(const float* p_old, float* p_new, float lr, cons
 void mlp_wgrad_factor_launch(float* p, float lr, const float* x, long long xstride,
                              const float* dz1A, float* ws, int* ctr, float* stats, int stats_ring,
                              int B, hipStream_t stream, const MlpXg& xg, int world);
+
+// Pipelined fused engine: step t-1's local W1/W2/b gradient tiles exchanged and applied
+// (p_old -> p_new) in the launch that runs step t's forward; the head is the plain one.
+void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
+                            const float* x, float* ws, int* ctr, float* stats, int stats_ring,
+                            int B, int stats_on, hipStream_t stream, const MlpXg& xg, int world);
 
 void mlp_wgrad_xg_launch(float* p, float lr, const float* x, float* ws, int* ctr, float* stats,
                          int stats_ring, int B, hipStream_t stream, const MlpXg& xg, int world);

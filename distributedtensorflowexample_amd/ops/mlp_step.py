@@ -132,6 +132,31 @@ def step_xgmi(p, x, labels, ws: StepWorkspace, lr, comm, stats=True):
     comm.mlp_wgrad(p, lr, x, ws, stats)
 
 
+def step_xgmi_pipelined(p_old, p_new, x_prev, x, labels, ws: StepWorkspace, lr, apply, comm,
+                        stats=True):
+    """Two-launch data-parallel step of the fused engine: (1) step t-1's local gradient
+    tiles exchanged over xGMI and applied (``p_old`` -> ``p_new``) inside the launch that
+    runs step t's forward; (2) the plain head.  ``lr`` already divided by the world size;
+    ``apply=False``: exchange of nothing useful + copy + forward.  The last update stays
+    pending until ``flush_xgmi`` (which must run the same kernel: the exchange-epoch slots
+    of a communicator belong to one kernel's tiling)."""
+    _check(x, labels, ws.B)
+    _check(x_prev, None, ws.B)
+    _check_flat(p_old, p_new)
+    if p_old.data_ptr() == p_new.data_ptr():
+        raise ValueError("the pipelined step needs distinct ping-pong buffers")
+    comm.mlp_fwdapply(p_old, p_new, lr, x_prev, x, ws, apply, stats)
+    hip().mlp_head2(ptr(p_new), ptr(labels), ptr(ws.buf), ws.B, stream_handle())
+
+
+def flush_xgmi(p_old, p_new, x_prev, ws: StepWorkspace, lr, comm, stats=True):
+    """Apply the pending update of the last pipelined fused step: the first launch once
+    more (its forward on ``x_prev`` is discarded).  Result in ``p_new``."""
+    _check(x_prev, None, ws.B)
+    _check_flat(p_old, p_new)
+    comm.mlp_fwdapply(p_old, p_new, lr, x_prev, x_prev, ws, True, stats)
+
+
 def factor_plane(B):
     """Elements of one rank's dz1 plane in the factor engine's gather buffer ([112][BP])."""
     return HP * ((B + 15) // 16) * 16

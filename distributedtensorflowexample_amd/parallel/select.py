@@ -136,6 +136,9 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
     """Data-parallel engine of the fused MLP trainer, one of
       ``("allreduce", ar_comm)`` -- flat gradient, separate all-reduce launch, deferred apply;
       ``("fused", XgmiComm)``   -- gradient exchange inside the weight-gradient kernel;
+      ``("fused2", XgmiComm)``  -- the same exchange in the two-launch pipelined step (step
+                                   t-1's local gradient tiles exchanged and applied inside
+                                   step t's forward launch);
       ``("factor", XgmiComm)``  -- sufficient-factor exchange: the backprop factors dz1 are
                                    all-gathered inside the head kernel and every rank forms
                                    the global W1 gradient from them and every rank's batch
@@ -156,8 +159,8 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
 
     if world < 2 or world > 8 or mode == "allreduce":
         return "allreduce", ar_comm, None
-    kinds = {"auto": ["fused", "factor", "factor2"], "fused": ["fused"],
-             "factor": ["factor"], "factor2": ["factor2"]}[mode]
+    kinds = {"auto": ["fused", "fused2", "factor", "factor2"], "fused": ["fused"],
+             "fused2": ["fused2"], "factor": ["factor"], "factor2": ["factor2"]}[mode]
     if x_all is None:
         kinds = [k for k in kinds if not k.startswith("factor")]
     if batch_size > 128:
@@ -182,9 +185,9 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
         return "allreduce", ar_comm, None
 
     def make(kind):
-        if kind == "fused":
+        if kind in ("fused", "fused2"):  # fused2: the two-launch pipelined variant
             return FusedMLPTrainer(params, x, y, batch_size, lr, world_size=world,
-                                   fused_comm=comms[kind])
+                                   fused_comm=comms[kind], pipeline=kind == "fused2")
         if kind in ("factor", "factor2"):  # factor2: the two-launch pipelined variant
             return FusedMLPTrainer(params, None, y, batch_size, lr, world_size=world,
                                    factor_comm=comms[kind], x_all=x_all, rank=rank,

@@ -91,6 +91,18 @@ class XgmiComm:
                                     ws.stats_ring, ws.B, 1 if apply else 0,
                                     torch.cuda.current_stream().cuda_stream, self.timeout_s)
 
+    def mlp_fwdapply(self, p_old, p_new, lr, x_prev, x, ws, apply, stats=True):
+        """Pipelined fused engine, first launch: step t-1's local gradient tiles (from the
+        factors its head left in ``ws`` and ``x_prev``) exchanged with the peers, summed in
+        rank order and applied ``p_old`` -> ``p_new``, fused with step t's forward."""
+        from ..ops._ext import ptr
+
+        self._h.mlp_fwdapply(ptr(p_old), ptr(p_new), float(lr) if apply else 0.0,
+                             ptr(x_prev if apply else x), ptr(x), ptr(ws.buf), ptr(ws.ctr),
+                             ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B,
+                             1 if apply else 0, torch.cuda.current_stream().cuda_stream,
+                             self.timeout_s)
+
     def mlp_wgrad_factor(self, p, lr, x, xstride, dz1A, ws, stats=True):
         """Factor engine: global dW1 from the gathered factors and every rank's batch
         (``x`` = this rank's batch, rank q's at ``x + (q - rank) * xstride`` elements),

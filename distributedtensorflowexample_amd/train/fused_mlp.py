@@ -89,10 +89,11 @@ class FusedMLPTrainer:
         self.ws.set_global_step(global_step)
         self.pos = int(global_step) % self.nbatches  # next batch (host mirror)
         self.pending = False
-        # single GPU, no communicator -- or the factor engine -- : the two-launch pipelined
-        # step (the factor engine's needs batch <= 128)
-        self.pipelined = bool(pipeline and allreduce is None and fused_comm is None and (
-            (self.world_size == 1 and factor_comm is None)
+        # single GPU without a communicator, the fused engine or the factor engine (batch
+        # <= 128): the two-launch pipelined step
+        self.pipelined = bool(pipeline and allreduce is None and (
+            (self.world_size == 1 and factor_comm is None and fused_comm is None)
+            or fused_comm is not None
             or (factor_comm is not None and self.B <= 128)))
         self.max_graph_steps = int(max_graph_steps)
         self._graphs = {}
@@ -119,6 +120,11 @@ class FusedMLPTrainer:
                 xp, _ = self.batch((self.pos - 1) % self.nbatches)
                 mlp_step.flush_factor(self.bufs[self.cur], xp, self.ws, self.lr / self.world_size,
                                       self.factor_comm, self.dz1A, self.xstride)
+            elif self.pipelined and self.fused_comm is not None:
+                xp, _ = self.batch((self.pos - 1) % self.nbatches)
+                mlp_step.flush_xgmi(self.bufs[self.cur], self.bufs[self.cur ^ 1], xp, self.ws,
+                                    self.lr / self.world_size, self.fused_comm)
+                self.cur ^= 1
             elif self.pipelined:
                 xp, _ = self.batch((self.pos - 1) % self.nbatches)
                 mlp_step.flush_pipelined(self.bufs[self.cur], xp, self.ws, self.lr)
@@ -155,6 +161,14 @@ class FusedMLPTrainer:
         if self.factor_comm is not None:
             mlp_step.step_factor(self.bufs[self.cur], xb, yb, self.ws, self.lr / self.world_size,
                                  self.factor_comm, self.dz1A, self.xstride)
+            return
+        if self.fused_comm is not None and self.pipelined:
+            xp, _ = self.batch((self.pos - 2) % self.nbatches)  # pos already advanced
+            mlp_step.step_xgmi_pipelined(self.bufs[self.cur], self.bufs[self.cur ^ 1], xp, xb,
+                                         yb, self.ws, self.lr / self.world_size, self.pending,
+                                         self.fused_comm)
+            self.cur ^= 1
+            self.pending = True
             return
         if self.fused_comm is not None:
             mlp_step.step_xgmi(self.bufs[self.cur], xb, yb, self.ws, self.lr / self.world_size,

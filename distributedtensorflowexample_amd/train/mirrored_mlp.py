@@ -83,9 +83,9 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
                 tr_x, tr_y = x_all[rank], tr_y[:n]
             kind, c, _ = pick_mlp_engine(params, tr_x.to(dev), tr_y.to(dev), B,
                                          flags.learning_rate, comm, world, rank, dev, x_all=x_all)
-            fused = c if kind == "fused" else None
+            fused = c if kind in ("fused", "fused2") else None
             factor = c if kind in ("factor", "factor2") else None
-            pipe = kind != "factor"
+            pipe = kind not in ("fused", "factor")  # fused2 / factor2: two-launch variants
         tr = FusedMLPTrainer(params, tr_x, tr_y, B, flags.learning_rate,
                              allreduce=comm.allreduce_sum_ if (comm and not (fused or factor))
                              else None, world_size=world, fused_comm=fused, factor_comm=factor,

@@ -118,7 +118,7 @@ def test_auto_selection_path(gpu):
         assert ok, (r, msg)
 
 
-def _fused_worker(rank, world, port, q):
+def _fused_worker(rank, world, port, q, pipeline):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -134,11 +134,15 @@ def _fused_worker(rank, world, port, q):
         fc = XgmiComm(rank, world, params.numel(), device=dev, key="f/push", protocol="push")
         ref = XgmiComm(rank, world, params.numel(), device=dev, key="f/ll", protocol="ll")
         lr = 0.05
-        tf = FusedMLPTrainer(params, x, y, 100, lr, world_size=world, fused_comm=fc)
+        tf = FusedMLPTrainer(params, x, y, 100, lr, world_size=world, fused_comm=fc,
+                             pipeline=pipeline)
+        assert tf.pipelined == pipeline
         ta = FusedMLPTrainer(params, x, y, 100, lr, world_size=world, allreduce=ref.allreduce_sum_)
         tf.run(7, use_graph=False)   # eager
+        tf.flush()                   # (pipelined: the pending update, then a fresh start)
         tf.run(33, use_graph=True)   # graph replays (device-side epochs)
         ta.run(7, use_graph=False)
+        ta.flush()
         ta.run(33, use_graph=True)
         fc.check()
         ref.check()
@@ -156,14 +160,16 @@ def _fused_worker(rank, world, port, q):
         q.put((rank, False, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_fused_mlp_exchange_matches_allreduce_engine(gpu, world):
-    """The gradient exchange fused into the MLP backward kernel gives the same SGD
-    trajectory as the separate all-reduce engine, and bit-identical replicas."""
+@pytest.mark.parametrize("world,pipeline", [(2, False), (3, False), (2, True), (3, True)])
+def test_fused_mlp_exchange_matches_allreduce_engine(gpu, world, pipeline):
+    """The gradient exchange fused into the MLP backward kernel (pipeline: into the next
+    step's forward launch) gives the same SGD trajectory as the separate all-reduce engine,
+    and bit-identical replicas."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_fused_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_fused_worker, args=(r, world, port, q, pipeline))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
