@@ -166,8 +166,13 @@ class EventWriter {
   }
   void loop() {
     std::unique_lock<std::mutex> lk(mu_);
+    const auto period = std::chrono::duration_cast<std::chrono::system_clock::duration>(
+        std::chrono::duration<double>(flush_secs_));
     while (!closed_) {
-      cv_.wait_for(lk, std::chrono::duration<double>(flush_secs_));
+      // system_clock deadline: pthread_cond_timedwait, which ThreadSanitizer intercepts
+      // (wait_for's steady clock maps to pthread_cond_clockwait, which GCC 11's TSan does
+      // not, and then reports a false double lock -- tools/sanitize_host.py)
+      cv_.wait_until(lk, std::chrono::system_clock::now() + period);
       if (closed_) break;
       lk.unlock();
       flush();

@@ -110,6 +110,22 @@ struct Reader {
 };
 
 // ---------------------------------------------------------------- server
+// The two INTENTIONAL data races of the reference's semantics live in these functions (and
+// only here), so ThreadSanitizer runs (tools/sanitize_host.py) suppress exactly them:
+//  * lock-free read of a variable while workers apply (TF's pull reads without locking);
+//  * Hogwild apply, ApplyGradientDescent(use_locking=False) (worker.py:79).
+__attribute__((noinline)) void dtfx_racy_read(Writer& w, const float* p, size_t nbytes) {
+  w.raw(p, nbytes);
+}
+// g: the gradient bytes inside the request buffer (no alignment guarantee: loaded by memcpy)
+__attribute__((noinline)) void dtfx_hogwild_apply(float* p, const char* g, size_t n, float lr) {
+  for (size_t i = 0; i < n; ++i) {
+    float gi;
+    std::memcpy(&gi, g + 4 * i, 4);
+    p[i] -= lr * gi;
+  }
+}
+
 struct Var {
   std::string name;
   uint8_t dtype;
@@ -153,12 +169,14 @@ class PSServer {
 
   void stop() {
     if (!running_.exchange(false)) return;
+    // the accept thread polls lfd_ (100 ms ticks): join it BEFORE closing the fd, so it
+    // never reads a closed (and possibly reused) descriptor
+    if (lfd_ >= 0) ::shutdown(lfd_, SHUT_RDWR);
+    if (acc_.joinable()) acc_.join();
     if (lfd_ >= 0) {
-      ::shutdown(lfd_, SHUT_RDWR);
       ::close(lfd_);
       lfd_ = -1;
     }
-    if (acc_.joinable()) acc_.join();
     std::vector<std::thread> ts;
     {
       std::lock_guard<std::mutex> g(cmu_);
@@ -233,6 +251,14 @@ class PSServer {
       bytes_out_ += resp.size();
       if (!write_full(fd, resp.data(), resp.size())) break;
     }
+    // deregister before closing: stop() shuts down the fds in conns_, and a closed fd number
+    // can be reused by any other socket of the process
+    std::lock_guard<std::mutex> g(cmu_);
+    for (auto it = conns_.begin(); it != conns_.end(); ++it)
+      if (*it == fd) {
+        conns_.erase(it);
+        break;
+      }
     ::close(fd);
   }
 
@@ -299,7 +325,7 @@ class PSServer {
         for (uint32_t k = 0; k < n; ++k) {
           Var* v = var(r.get<uint32_t>());
           if (!v->init.load()) throw std::runtime_error("ps: variable " + v->name + " is uninitialized");
-          if (v->dtype == DT_F32) w.raw(v->f.data(), v->nbytes());  // lock-free read (TF semantics)
+          if (v->dtype == DT_F32) dtfx_racy_read(w, v->f.data(), v->nbytes());  // lock-free (TF)
           else w.put<int64_t>(v->i.load());
         }
         break;
@@ -313,16 +339,18 @@ class PSServer {
         ++pushes_;
         for (Var* v : vs) {
           if (v->dtype != DT_F32) throw std::runtime_error("ps: apply on non-float variable");
-          const float* g = reinterpret_cast<const float*>(r.take(v->nbytes()));
+          const char* g = r.take(v->nbytes());
           float* p = v->f.data();
           const size_t cnt = v->count;
           if (locking) {
+            // (still races with lock-free pulls, as in TF: the apply goes through the same
+            // suppressed function)
             std::lock_guard<std::mutex> lk(v->mu);
-            for (size_t i = 0; i < cnt; ++i) p[i] -= lr * g[i];
+            dtfx_hogwild_apply(p, g, cnt, lr);
           } else {
             // Hogwild, as ApplyGradientDescent(use_locking=False): concurrent
             // workers may interleave element updates.
-            for (size_t i = 0; i < cnt; ++i) p[i] -= lr * g[i];
+            dtfx_hogwild_apply(p, g, cnt, lr);
           }
         }
         break;
@@ -385,6 +413,9 @@ class PSClient {
   ~PSClient() { close(); }
 
   void close() {
+    // (waits for an exchange another thread has in flight; that thread holds mu_ without
+    // the GIL and releases mu_ before re-taking the GIL, so this cannot deadlock)
+    std::lock_guard<std::mutex> lk(mu_);
     for (int& fd : fds_)
       if (fd >= 0) {
         ::close(fd);
@@ -392,6 +423,11 @@ class PSClient {
       }
   }
   int num_tasks() const { return static_cast<int>(fds_.size()); }
+  size_t task_of(int64_t h) const {
+    const size_t t = static_cast<size_t>(static_cast<uint64_t>(h) >> 32);
+    if (t >= fds_.size()) throw std::runtime_error("ps: handle of an unknown ps task");
+    return t;
+  }
 
   // handle = task << 32 | id
   int64_t create(const std::string& name, const std::string& dtype, std::vector<int64_t> shape,
@@ -428,7 +464,7 @@ class PSClient {
     py::gil_scoped_release nogil;
     std::lock_guard<std::mutex> lk(mu_);
     std::vector<std::vector<size_t>> per(fds_.size());
-    for (size_t k = 0; k < hs.size(); ++k) per[hs[k] >> 32].push_back(k);
+    for (size_t k = 0; k < hs.size(); ++k) per[task_of(hs[k])].push_back(k);
     for (size_t t = 0; t < per.size(); ++t) {
       if (per[t].empty()) continue;
       Writer w;
@@ -456,7 +492,7 @@ class PSClient {
     py::gil_scoped_release nogil;
     std::lock_guard<std::mutex> lk(mu_);
     std::vector<std::vector<size_t>> per(fds_.size());
-    for (size_t k = 0; k < hs.size(); ++k) per[hs[k] >> 32].push_back(k);
+    for (size_t k = 0; k < hs.size(); ++k) per[task_of(hs[k])].push_back(k);
     for (size_t t = 0; t < per.size(); ++t) {
       if (per[t].empty()) continue;
       Writer w;
@@ -483,7 +519,7 @@ class PSClient {
   std::vector<int64_t> uninitialized(std::vector<int64_t> hs) {
     std::vector<int64_t> out;
     std::vector<std::vector<int64_t>> per(fds_.size());
-    for (int64_t h : hs) per[h >> 32].push_back(h);
+    for (int64_t h : hs) per[task_of(h)].push_back(h);
     for (size_t t = 0; t < per.size(); ++t) {
       if (per[t].empty()) continue;
       Writer w;
