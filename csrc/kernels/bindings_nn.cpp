@@ -13,7 +13,10 @@ void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const v
                       float*, hipStream_t);
 void colsum_bf16_launch(const void*, int, int, int, float*, float, hipStream_t);
 void conv_bf16_launch(int, int, int, int, int, int, int, int, int, int, const void*, const void*, int,
-                      void*, float, const void*, float*, float*, int, hipStream_t);
+                      void*, float, const void*, float*, float*, int, hipStream_t, const void*,
+                      const void*, const float*, const float*);
+void bn_bwd_apply_launch(long long, int, const void*, const void*, const float*, const float*,
+                         const float*, const float*, const float*, void*, hipStream_t);
 void bn_finalize_launch(int, long long, const float*, const float*, float, float*, float*, float*,
                         float*, float, hipStream_t);
 void bn_apply_launch(long long, int, const void*, const float*, const float*, const float*,
@@ -138,10 +141,24 @@ void register_nn(py::module_& m) {
   m.def("conv_bf16", [](int mode, int N, int H, int W, int C, int Cout, int KH, int KW, int stride,
                         int pad, uintptr_t a, uintptr_t b, int ldw, uintptr_t out, float beta,
                         uintptr_t residual, uintptr_t colsum, uintptr_t colsq, int splitk,
-                        uintptr_t s) {
+                        uintptr_t s, uintptr_t relu_y, uintptr_t bn_x, uintptr_t bn_mean,
+                        uintptr_t bn_rstd) {
     dtfx::conv_bf16_launch(mode, N, H, W, C, Cout, KH, KW, stride, pad, P<const void>(a),
                            P<const void>(b), ldw, P<void>(out), beta, P<const void>(residual),
-                           P<float>(colsum), P<float>(colsq), splitk, S(s));
+                           P<float>(colsum), P<float>(colsq), splitk, S(s),
+                           P<const void>(relu_y), P<const void>(bn_x), P<const float>(bn_mean),
+                           P<const float>(bn_rstd));
+  }, py::arg("mode"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Cout"),
+     py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("a"), py::arg("b"),
+     py::arg("ldw"), py::arg("out"), py::arg("beta"), py::arg("residual"), py::arg("colsum"),
+     py::arg("colsq"), py::arg("splitk"), py::arg("stream"), py::arg("relu_y") = 0,
+     py::arg("bn_x") = 0, py::arg("bn_mean") = 0, py::arg("bn_rstd") = 0);
+  m.def("bn_bwd_apply", [](long long M, int C, uintptr_t de, uintptr_t x, uintptr_t mean,
+                           uintptr_t rstd, uintptr_t g, uintptr_t sdy, uintptr_t sdyxh,
+                           uintptr_t dx, uintptr_t s) {
+    dtfx::bn_bwd_apply_launch(M, C, P<const void>(de), P<const void>(x), P<const float>(mean),
+                              P<const float>(rstd), P<const float>(g), P<const float>(sdy),
+                              P<const float>(sdyxh), P<void>(dx), S(s));
   });
   m.def("bn_finalize", [](int C, long long M, uintptr_t s_, uintptr_t q, float eps, uintptr_t mean,
                           uintptr_t rstd, uintptr_t rm, uintptr_t rv, float momentum, uintptr_t s) {

@@ -501,6 +501,20 @@ void bn_bwd_launch(long long M, int C, const void* dy, const void* yout, const v
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+// Apply half of BatchNorm backward when the reductions were fused into the producing conv
+// dgrad (conv_bf16 mode 2 with relu_y / bn_x): de is already dL/d(BN output) (masked),
+// sum_dy / sum_dyxh are final.
+void bn_bwd_apply_launch(long long M, int C, const void* de, const void* x, const float* mean,
+                         const float* rstd, const float* gamma, const float* sum_dy,
+                         const float* sum_dyxh, void* dx, hipStream_t st) {
+  if (C % 8) throw std::runtime_error("bn_bwd_apply: C % 8 != 0");
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(M * C / 8)), dim3(256), 0, st, M, C,
+                     (const unsigned short*)de, (const unsigned short*)nullptr,
+                     (const unsigned short*)x, mean, rstd, gamma, sum_dy, sum_dyxh, 0,
+                     1.f / (float)M, (unsigned short*)dx, (unsigned short*)nullptr);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
 void maxpool_fwd_launch(int N, int H, int W, int C, const void* x, void* y, void* idx, hipStream_t st) {
   if (C % 8) throw std::runtime_error("maxpool: C % 8 != 0");
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;

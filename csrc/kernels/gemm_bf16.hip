@@ -17,7 +17,8 @@
 //   v = alpha*acc  (+ bias[n])  -> aux_out[m][n] = v (pre-activation, bf16)
 //   v = act(v)                   (gelu(tanh) / relu)
 //   v *= act'(aux_in[m][n])      (backward through an activation)
-//   v += residual[m][n]          (bf16)
+//   v += residual[m][n]          (bf16; convolutions: added BEFORE act', so a conv dgrad
+//                                 can emit dL/d(BN output) = (dgrad + shortcut) * relu'(y))
 //   v += beta * C_old            (f32 output only: gradient accumulation)
 //   C = v as bf16 or f32
 //
@@ -290,6 +291,12 @@ struct GemmEpi {
   float* colsq;                 // [N] += column sums of squares (BatchNorm statistics), or null
   int col_partial;              // 1: colsum/colsq are [2 * m_tiles][N] partial rows (plain stores,
                                 //    no same-address atomics: BatchNorm statistics of tall convs)
+  // BatchNorm-backward statistics fused into a conv dgrad: with bn_x set, colsq accumulates
+  // v * xhat, xhat = (bn_x[m][n] - bn_mean[n]) * bn_rstd[n] (bn_x: the BN input, ld = ldc),
+  // instead of v^2 -- colsum / colsq are then exactly BatchNorm's sum(dy) / sum(dy * xhat).
+  const unsigned short* bn_x;
+  const float* bn_mean;
+  const float* bn_rstd;
 };
 
 // Tile BM_ x BN_ (128x128: 4 waves of 64x64, 2 blocks/CU; 256x128: 8 waves of 64x64;
@@ -428,6 +435,15 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
   float cs[8], cq[8];  // fused column sums / sums of squares of this lane's 8 columns
 #pragma unroll
   for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
+  float bmu[8], brs[8];  // BN mean / rstd of this lane's 8 columns (bn_x epilogue only)
+  if (MODE == 2 && !OUT_F32 && e.bn_x) {
+    const int n = n0 + wn * 64 + (lane & 7) * 8;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      bmu[u] = n + u < N ? e.bn_mean[n + u] : 0.f;
+      brs[u] = n + u < N ? e.bn_rstd[n + u] : 0.f;
+    }
+  }
   for (int h = 0; h < WM / 32; ++h) {
     // (issued before the slab's LDS transpose, so their latency overlaps it)
     // Side inputs (aux_in / residual) of the slab's 4 row groups are all
@@ -435,7 +451,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
     // 8-row group (the loads used to sit between dependent compute and stores).
     bool full[4], live[4];
     int mm[4], nn[4];
-    bf16x8 a8[4], r8[4];
+    bf16x8 a8[4], r8[4], x8[4];
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
@@ -447,6 +463,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
       if (!OUT_F32) {  // (f32-output tiles load at use: the 256x256 f32 variant would spill)
         if (e.act_grad) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)ms * e.ld_aux + ns];
         if (e.residual) r8[it] = *(const bf16x8*)&e.residual[(size_t)ms * e.ld_res + ns];
+        if (MODE == 2 && e.bn_x) x8[it] = *(const bf16x8*)&e.bn_x[(size_t)ms * ldc + ns];
       }
     }
     // static accumulator indices only (a runtime acc[2h+ii] index would put acc in scratch)
@@ -506,6 +523,11 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] = fmaxf(v[u], 0.f);
         }
+        if (MODE != 0 && e.residual) {  // convolutions: shortcut gradient before the mask
+          if (OUT_F32) r8[it] = *(const bf16x8*)&e.residual[(size_t)m * e.ld_res + n];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[it][u]);
+        }
         if (e.act_grad) {
           if (OUT_F32) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)m * e.ld_aux + n];
 #pragma unroll
@@ -514,16 +536,27 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
             v[u] *= (e.act_grad == 1) ? gelu_grad_f(uu) : (uu > 0.f ? 1.f : 0.f);
           }
         }
-        if (e.residual) {
+        if (MODE == 0 && e.residual) {
           if (OUT_F32) r8[it] = *(const bf16x8*)&e.residual[(size_t)m * e.ld_res + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[it][u]);
         }
         if (e.colsum || e.colsq) {
+          if (MODE == 2 && !OUT_F32 && e.bn_x) {
+            // statistics of the VALUES STORED (bf16-rounded), as a separate reduction over
+            // the output tensor would see them
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            cs[u] += v[u];
-            cq[u] += v[u] * v[u];
+            for (int u = 0; u < 8; ++u) {
+              const float vr = bf2f(f2bf(v[u]));
+              cs[u] += vr;
+              cq[u] += vr * (bf2f((unsigned short)x8[it][u]) - bmu[u]) * brs[u];
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              cs[u] += v[u];
+              cq[u] += v[u] * v[u];
+            }
           }
         }
         if (OUT_F32) {
@@ -550,13 +583,20 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
           if (e.aux_out) e.aux_out[(size_t)m * e.ld_aux + n + u] = f2bf(w);
           if (e.act == 1) w = gelu_f(w);
           else if (e.act == 2) w = fmaxf(w, 0.f);
+          if (MODE != 0 && e.residual) w += bf2f(e.residual[(size_t)m * e.ld_res + n + u]);
           if (e.act_grad) {
             const float uu = bf2f(e.aux_in[(size_t)m * e.ld_aux + n + u]);
             w *= (e.act_grad == 1) ? gelu_grad_f(uu) : (uu > 0.f ? 1.f : 0.f);
           }
-          if (e.residual) w += bf2f(e.residual[(size_t)m * e.ld_res + n + u]);
-          cs[u] += w;
-          cq[u] += w * w;
+          if (MODE == 0 && e.residual) w += bf2f(e.residual[(size_t)m * e.ld_res + n + u]);
+          if (MODE == 2 && !OUT_F32 && e.bn_x) {
+            const float wr = bf2f(f2bf(w));
+            cs[u] += wr;
+            cq[u] += wr * (bf2f(e.bn_x[(size_t)m * ldc + n + u]) - bmu[u]) * brs[u];
+          } else {
+            cs[u] += w;
+            cq[u] += w * w;
+          }
           if (OUT_F32) {
             float* C = (float*)Cv + (size_t)m * ldc + n + u;
             *C = (e.beta != 0.f) ? w + e.beta * *C : w;
@@ -756,12 +796,16 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
 //         optional fused BatchNorm statistics: colsum / colsq = per-wave-slab partial rows
 //         [ceil(N*OH*OW / 64)][Cout] (f32, fully overwritten)
 //  dgrad: dy [N*OH*OW][Cout], w [Cout][ldw], dx [N*H*W][C]
-//         (+ residual)
+//         (+ residual); optional fused BatchNorm backward of the BN that produced x
+//         (y = relu(bn(bn_x) [+ res])): relu_y masks the output, dx = (dgrad + residual) *
+//         (relu_y > 0) = dL/d(BN output), and colsum / colsq (partial rows [ceil(M/64)][C])
+//         receive sum(dx) and sum(dx * xhat) -- BatchNorm backward's two reductions
 //  wgrad: dy, x -> dw [Cout][ldw] f32 (first KH*KW*C columns; += when beta == 1)
 void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, int KW, int stride,
                       int pad, const void* a, const void* b, int ldw, void* out, float beta,
                       const void* residual, float* colsum, float* colsq, int splitk,
-                      hipStream_t stream) {
+                      hipStream_t stream, const void* relu_y, const void* bn_x,
+                      const float* bn_mean, const float* bn_rstd) {
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   if (C % 8 || Cout % 8) throw std::runtime_error("conv_bf16: channel counts must be multiples of 8");
   if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) & 15)
@@ -786,11 +830,26 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
     d.ktot = KH * KW * Cout;
     M = N * H * W; Nn = C; K = d.ktot;
     e.ld_res = C;
+    if (relu_y) {
+      if ((uintptr_t)relu_y & 15) throw std::runtime_error("conv_bf16: relu_y must be 16-byte aligned");
+      e.aux_in = (const unsigned short*)relu_y;
+      e.ld_aux = C;
+      e.act_grad = 2;
+    }
+    if (bn_x) {
+      if (!colsum || !colsq || !bn_mean || !bn_rstd || ((uintptr_t)bn_x & 15))
+        throw std::runtime_error("conv_bf16: fused BN statistics need colsum, colsq, mean, rstd");
+      e.bn_x = (const unsigned short*)bn_x;
+      e.bn_mean = bn_mean;
+      e.bn_rstd = bn_rstd;
+    }
+    e.col_partial = (colsum || colsq) ? 1 : 0;
     launch_cfg<2, false, false, false>(choose_cfg(M, Nn, 1, 2), dim3(1, 1, 1), M, Nn, K,
                                        (const unsigned short*)a, 0, (const unsigned short*)b, 0,
                                        out, C, e, 0LL, 0LL, 0LL, d, stream);
   } else if (mode == 3) {
-    if (residual || colsum || colsq) throw std::runtime_error("conv_bf16: wgrad has no epilogue options");
+    if (residual || colsum || colsq || relu_y || bn_x)
+      throw std::runtime_error("conv_bf16: wgrad has no epilogue options");
     M = Cout; Nn = KH * KW * C; K = N * OH * OW;
     const int tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
     const int nkt = (K + 63) / 64;

@@ -198,8 +198,16 @@ class ResNet50:
             on_bucket_ready(len(P.buckets) - 1)
         dx = CN.avgpool_bwd(dpool, x.shape)
         bucket = len(P.buckets) - 2
-        for pre, x_in, (c1, m1, r1, a1), (c2, m2, r2, a2), (c3, m3, r3), ds, out in reversed(blocks):
-            dx = self._block_bwd(pre, dx, x_in, c1, m1, r1, a1, c2, m2, r2, a2, c3, m3, r3, ds, out)
+        dx_is_de = False  # dx already dL/d(BN output) of the block's conv3 (fused reductions)
+        for i in range(len(blocks) - 1, -1, -1):
+            pre, x_in, (c1, m1, r1, a1), (c2, m2, r2, a2), (c3, m3, r3), ds, out = blocks[i]
+            # the previous block's conv3 BatchNorm consumes this block's input gradient:
+            # its reductions go into this block's last dgrad epilogue
+            prev = blocks[i - 1] if i > 0 else None
+            fuse = None if prev is None else (prev[0] + "conv3", x_in, prev[4])
+            dx = self._block_bwd(pre, dx, x_in, c1, m1, r1, a1, c2, m2, r2, a2, c3, m3, r3, ds,
+                                 out, dout_is_de=dx_is_de, fuse_prev=fuse)
+            dx_is_de = fuse is not None
             if on_bucket_ready is not None:
                 on_bucket_ready(bucket)
             bucket -= 1
@@ -218,27 +226,54 @@ class ResNet50:
         return CN.bn_bwd(dy, y, x, mean, rstd, P.P(name + ".bn.gamma"), P.G(name + ".bn.gamma"),
                          P.G(name + ".bn.beta"), relu, want_dres, grads_zeroed=True)
 
-    def _wgrad_dgrad(self, name, dc, x_in, residual=None, need_dx=True):
+    def _bn_fused(self, name, y, x, mean, rstd):
+        """``bn`` argument of CN.conv_dgrad: BatchNorm ``name`` (input x, post-ReLU output y)
+        has its backward reductions fused into the dgrad that produces its output gradient,
+        straight into the (per-step zeroed) dbeta / dgamma slots."""
+        P = self.params
+        return (y, x, mean, rstd, P.G(name + ".bn.beta"), P.G(name + ".bn.gamma"))
+
+    def _bn_apply_bwd(self, name, de, x, mean, rstd):
+        P = self.params
+        return CN.bn_bwd_apply(de, x, mean, rstd, P.P(name + ".bn.gamma"), P.G(name + ".bn.beta"),
+                               P.G(name + ".bn.gamma"))
+
+    def _wgrad_dgrad(self, name, dc, x_in, residual=None, need_dx=True, bn=None):
         P = self.params
         _, cin, cout, k, s, p = self.specs[name]
         CN.conv_wgrad(dc, x_in, P.G(name + ".weight"), k, k, s, p, beta=1.0)
         if not need_dx:
             return None
-        return CN.conv_dgrad(dc, P.W(name + ".weight"), x_in.shape, k, k, s, p, residual=residual)
+        return CN.conv_dgrad(dc, P.W(name + ".weight"), x_in.shape, k, k, s, p, residual=residual,
+                             bn=bn)
 
-    def _block_bwd(self, pre, dout, x_in, c1, m1, r1, a1, c2, m2, r2, a2, c3, m3, r3, ds, out):
-        dc3, dres = self._bn_bwd(pre + "conv3", dout, out, c3, m3, r3, relu=True, want_dres=True)
+    def _block_bwd(self, pre, dout, x_in, c1, m1, r1, a1, c2, m2, r2, a2, c3, m3, r3, ds, out,
+                   dout_is_de=False, fuse_prev=None):
+        """Backward of one bottleneck.  ``dout_is_de``: ``dout`` is already the gradient at
+        conv3's BN output with its reductions done (fused into the next block's dgrad).
+        ``fuse_prev = (bn name, y, (c, mean, rstd))``: the BatchNorm that produced this block's
+        input; its reductions are fused into this block's last dgrad (whose result is then
+        that BN's output gradient)."""
+        if dout_is_de:
+            dres = dout
+            dc3 = self._bn_apply_bwd(pre + "conv3", dout, c3, m3, r3)
+        else:
+            dc3, dres = self._bn_bwd(pre + "conv3", dout, out, c3, m3, r3, relu=True, want_dres=True)
         if ds is not None:
             cs_, ms, rs = ds
             dcs, _ = self._bn_bwd(pre + "downsample", dres, None, cs_, ms, rs, relu=False)
             dshort = self._wgrad_dgrad(pre + "downsample", dcs, x_in)
         else:
             dshort = dres
-        da2 = self._wgrad_dgrad(pre + "conv3", dc3, a2)
-        dc2, _ = self._bn_bwd(pre + "conv2", da2, a2, c2, m2, r2, relu=True)
-        da1 = self._wgrad_dgrad(pre + "conv2", dc2, a1)
-        dc1, _ = self._bn_bwd(pre + "conv1", da1, a1, c1, m1, r1, relu=True)
-        return self._wgrad_dgrad(pre + "conv1", dc1, x_in, residual=dshort)
+        de2 = self._wgrad_dgrad(pre + "conv3", dc3, a2, bn=self._bn_fused(pre + "conv2", a2, c2, m2, r2))
+        dc2 = self._bn_apply_bwd(pre + "conv2", de2, c2, m2, r2)
+        de1 = self._wgrad_dgrad(pre + "conv2", dc2, a1, bn=self._bn_fused(pre + "conv1", a1, c1, m1, r1))
+        dc1 = self._bn_apply_bwd(pre + "conv1", de1, c1, m1, r1)
+        bn = None
+        if fuse_prev is not None:
+            name, y, (c, m, r) = fuse_prev
+            bn = self._bn_fused(name, y, c, m, r)
+        return self._wgrad_dgrad(pre + "conv1", dc1, x_in, residual=dshort, bn=bn)
 
     def sgd_step(self, lr, momentum=0.9, wd=5e-5, gscale=1.0):
         p = self.params

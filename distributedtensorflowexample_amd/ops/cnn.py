@@ -69,8 +69,15 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
     return y
 
 
-def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None):
-    """dx = conv^T(dy, w) (+ residual), NHWC bf16."""
+def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
+    """dx = conv^T(dy, w) (+ residual), NHWC bf16.
+
+    ``bn = (y, x, mean, rstd, sum_dy, sum_dyxh)``: the input of this conv is
+    ``y = relu(batchnorm(x) [+ shortcut])`` and its backward's reductions are fused into the
+    dgrad epilogue: the result is ``de = (dgrad + residual) * (y > 0)`` (the gradient at the
+    BN output, which is also the shortcut's gradient), and ``sum_dy += sum(de)``,
+    ``sum_dyxh += sum(de * xhat)`` per channel (f32 [C]; the zeroed dbeta / dgamma slots).
+    Finish with :func:`bn_bwd_apply`."""
     N, H, W, C = x_shape
     Cout = w.shape[0]
     if not dy.is_cuda:
@@ -78,10 +85,44 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None):
                                         stride=stride, padding=pad).permute(0, 2, 3, 1)
         if residual is not None:
             dx = dx + residual.float()
+        if bn is not None:
+            y, x, mean, rstd, sdy, sdx = bn
+            dx = dx * (y.float() > 0)
+            de = dx.to(BF16).float().reshape(-1, C)
+            xh = (x.float().reshape(-1, C) - mean) * rstd
+            sdy += de.sum(0)
+            sdx += (de * xh).sum(0)
         return dx.to(BF16)
     dx = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
-    hip().conv_bf16(2, N, H, W, C, Cout, KH, KW, stride, pad, ptr(dy), ptr(w), w.stride(0), ptr(dx),
-                    0.0, ptr(residual), 0, 0, 0, stream_handle())
+    if bn is None:
+        hip().conv_bf16(2, N, H, W, C, Cout, KH, KW, stride, pad, ptr(dy), ptr(w), w.stride(0),
+                        ptr(dx), 0.0, ptr(residual), 0, 0, 0, stream_handle())
+        return dx
+    y, x, mean, rstd, sdy, sdx = bn
+    if y.shape != dx.shape or x.shape != dx.shape:
+        raise ValueError("fused BN backward: y and x must have the dgrad output's shape")
+    rows = (N * H * W + 63) // 64  # one partial row per 64-row output slab
+    part = torch.empty(2, rows, C, device=dy.device)
+    hip().conv_bf16(2, N, H, W, C, Cout, KH, KW, stride, pad, ptr(dy), ptr(w), w.stride(0),
+                    ptr(dx), 0.0, ptr(residual), ptr(part[0]), ptr(part[1]), 0, stream_handle(),
+                    relu_y=ptr(y), bn_x=ptr(x), bn_mean=ptr(mean), bn_rstd=ptr(rstd))
+    hip().colpart_reduce(rows, C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx), stream_handle())
+    return dx
+
+
+def bn_bwd_apply(de, x, mean, rstd, gamma, sum_dy, sum_dyxh):
+    """dx of BatchNorm from the gradient at its output ``de`` and the final reductions
+    (``conv_dgrad(..., bn=...)``): dx = gamma*rstd*(de - mean(de) - xhat*mean(de*xhat))."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    if not x.is_cuda:
+        d = de.float().reshape(M, C)
+        xh = (x.float().reshape(M, C) - mean) * rstd
+        dx = gamma * rstd * (d - sum_dy / M - xh * sum_dyxh / M)
+        return dx.reshape(x.shape).to(BF16)
+    dx = torch.empty_like(x)
+    hip().bn_bwd_apply(M, C, ptr(de), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), ptr(sum_dy),
+                       ptr(sum_dyxh), ptr(dx), stream_handle())
     return dx
 
 

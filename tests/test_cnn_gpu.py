@@ -51,6 +51,45 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, W, C, Co, k, s, p):
     assert (dw.cpu()[:, kk:] == 0.5).all()  # padded columns untouched
 
 
+@pytest.mark.parametrize("N,H,W,C,Co,k,s,p,with_res", [
+    (2, 14, 14, 64, 64, 3, 1, 1, True),
+    (2, 14, 14, 64, 256, 1, 2, 0, False),
+    (2, 9, 11, 256, 64, 1, 1, 0, True),   # M = 198: ragged last partial-statistics slab
+])
+def test_conv_dgrad_fused_batchnorm_backward(gpu, N, H, W, C, Co, k, s, p, with_res):
+    """dgrad with BatchNorm backward's reductions in its epilogue (+ shortcut gradient, ReLU
+    mask) and the apply-only BN kernel == dgrad, then the two-pass bn_bwd (f32 CPU path)."""
+    c = _r(N, H, W, C, seed=11, scale=2).to(BF) + 0.5      # BN input (a conv output)
+    M = N * H * W
+    cf = c.float().reshape(M, C)
+    mean_r, rstd_r = cnn.bn_finalize(cf.sum(0), (cf * cf).sum(0), M)
+    gamma, beta = _r(C, seed=12) * 0.1 + 1, _r(C, seed=13) * 0.1
+    y = cnn.bn_apply(c, mean_r, rstd_r, gamma, beta, None, relu=True)   # block input
+    ld = cnn.kpad(k, k, C)
+    w = torch.zeros(Co, ld)
+    w[:, :k * k * C] = _r(Co, k * k * C, seed=14, scale=(k * k * C) ** -0.5)
+    w = w.to(BF)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = _r(N, OH, OW, Co, seed=15).to(BF)
+    res = _r(N, H, W, C, seed=16).to(BF) if with_res else None
+    # reference: unfused, CPU
+    dconv = cnn.conv_dgrad(dy, w, c.shape, k, k, s, p, residual=res)
+    dgr, dbr = torch.zeros(C), torch.zeros(C)
+    dxr, der = cnn.bn_bwd(dconv, y, c, mean_r, rstd_r, gamma, dgr, dbr, True, True)
+    # fused, GPU
+    g = lambda t: None if t is None else t.to(gpu)  # noqa: E731
+    dg, db = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
+    de = cnn.conv_dgrad(g(dy), g(w), c.shape, k, k, s, p, residual=g(res),
+                        bn=(g(y), g(c), g(mean_r), g(rstd_r), db, dg))
+    dx = cnn.bn_bwd_apply(de, g(c), g(mean_r), g(rstd_r), g(gamma), db, dg)
+    scale = der.float().abs().max()
+    assert (de.cpu().float() - der.float()).abs().max() < 3e-2 * scale
+    assert ((de.cpu().float() == 0) == (der.float() == 0)).float().mean() > 0.995  # ReLU mask
+    assert torch.allclose(db.cpu(), dbr, atol=0.05 * float(dbr.abs().max()) + 1e-2, rtol=2e-2)
+    assert torch.allclose(dg.cpu(), dgr, atol=0.05 * float(dgr.abs().max()) + 1e-2, rtol=2e-2)
+    assert (dx.cpu().float() - dxr.float()).abs().max() < 4e-2 * dxr.float().abs().max()
+
+
 def test_batchnorm_fwd_bwd(gpu):
     N, H, W, C = 4, 7, 7, 64
     x = _r(N, H, W, C, seed=4, scale=2).to(BF) + 1
