@@ -322,7 +322,20 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
   Cv = (char*)Cv + sC * blockIdx.z * (OUT_F32 ? 4 : 2);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, tiles_n * tiles_m);
+  // Split-K (gridDim.y > 1): one XCD-contiguous range of (split, tile) pairs per XCD, so the
+  // tiles of one K chunk -- which read the same operand rows (conv wgrad: the same dy chunk
+  // and the same x neighbourhood for every tap) -- share that XCD's L2 instead of fetching
+  // them once per XCD.  Otherwise the tiles sharing an A row-panel are XCD-contiguous.
+  int bid, split;
+  if (gridDim.y > 1) {
+    const int T = tiles_n * tiles_m;
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    bid = lam % T;
+    split = lam / T;
+  } else {
+    bid = xcd_remap(blockIdx.x, tiles_n * tiles_m);
+    split = 0;
+  }
   const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave / NWN, wn = wave % NWN;
@@ -338,9 +351,9 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // split-K: blockIdx.y owns K tiles [kt0, kt0 + nk)
+  // split-K: split owns K tiles [kt0, kt0 + nk)
   const int nk_all = (K + BK - 1) / BK, per = (nk_all + gridDim.y - 1) / gridDim.y;
-  const int kt0 = blockIdx.y * per;
+  const int kt0 = split * per;
   const int nk = max(0, min(per, nk_all - kt0));
   RowState rs;
   if (MODE == 1 || MODE == 2) conv_rows<NW>(cd, MODE, M, m0, wave, lane, rs);
