@@ -11,6 +11,7 @@
 // gradient into the same layout, so no transpose/permute pass exists.
 #include "common.h"
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(
     const float* __restrict__ rstd_in, const float* __restrict__ gamma,
     const unsigned short* __restrict__ dres, unsigned short* __restrict__ dx,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dxsum) {
-  __shared__ float red[3][4][2048 / 4 + 4];  // [dgamma|dbeta|dxsum][wave][...], H <= 2048
+  __shared__ float red[3][4][8 * 72];  // [dgamma|dbeta|dxsum][wave][u * 72 + lane], one chunk
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nch = H >> 3;
   float dg[NC][8], db[NC][8], ds[NC][8], gm[NC][8];
@@ -214,32 +215,29 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(
       }
     }
   }
-  // cross-wave reduction of the parameter-gradient partials, then one atomic per column
-  for (int part = 0; part < 4; ++part) {  // H/4 columns per pass through the LDS buffer
-    __syncthreads();
+  // cross-wave reduction of the parameter-gradient partials, then one atomic per column:
+  // one pass per column chunk c (512 columns), LDS image [array][wave][u * 72 + lane].
+  // Writes (fixed u, lanes 0..63) and reads (thread j -> column 512c + j, u = j % 8,
+  // lane = j / 8: bank 8u + lane) are both bank-conflict free, and each wave's atomics
+  // cover 64 CONSECUTIVE columns (2 cache lines: atomics to scattered lines serialise).
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int ch = lane + 64 * c;
-      if (ch < nch)
+  for (int c = 0; c < NC; ++c) {
+    if (c > 0) __syncthreads();
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int col = ch * 8 + u;
-          if (col * 4 / H == part) {
-            red[0][wave][col - part * (H / 4)] = dg[c][u];
-            red[1][wave][col - part * (H / 4)] = db[c][u];
-            red[2][wave][col - part * (H / 4)] = ds[c][u];
-          }
-        }
+    for (int u = 0; u < 8; ++u) {
+      red[0][wave][u * 72 + lane] = dg[c][u];
+      red[1][wave][u * 72 + lane] = db[c][u];
+      red[2][wave][u * 72 + lane] = ds[c][u];
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < H / 4; i += 256) {
-      const float a = red[0][0][i] + red[0][1][i] + red[0][2][i] + red[0][3][i];
-      const float b = red[1][0][i] + red[1][1][i] + red[1][2][i] + red[1][3][i];
-      unsafeAtomicAdd(dgamma + part * (H / 4) + i, a);
-      unsafeAtomicAdd(dbeta + part * (H / 4) + i, b);
+    for (int j = threadIdx.x; j < 512; j += 256) {
+      const int col = 512 * c + j;
+      if (col >= H) continue;
+      const int i = (j & 7) * 72 + (j >> 3);
+      unsafeAtomicAdd(dgamma + col, red[0][0][i] + red[0][1][i] + red[0][2][i] + red[0][3][i]);
+      unsafeAtomicAdd(dbeta + col, red[1][0][i] + red[1][1][i] + red[1][2][i] + red[1][3][i]);
       if (dxsum)
-        unsafeAtomicAdd(dxsum + part * (H / 4) + i,
-                        red[2][0][i] + red[2][1][i] + red[2][2][i] + red[2][3][i]);
+        unsafeAtomicAdd(dxsum + col, red[2][0][i] + red[2][1][i] + red[2][2][i] + red[2][3][i]);
     }
   }
 }
@@ -841,7 +839,13 @@ void layernorm_bwd_launch(int T, int H, const void* dy, const void* x, const flo
                           float* dgamma, float* dbeta, float* dxsum, hipStream_t s) {
   check_h(H);
   if (T <= 0) return;
-  const int rpb = T >= 8192 ? 64 : 16;  // BERT 16384 rows: 256 blocks (measured 16: 54 us, 32: 35, 64: 31, 128: 38 -- atomics vs parallelism)
+  // BERT 16384 rows: 256 blocks (measured 16: 54 us, 32: 35, 64: 31, 128: 38 -- atomics vs
+  // parallelism).  DTFX_LN_RPB overrides (sweeps).
+  static const int rpb_env = [] {
+    const char* e = getenv("DTFX_LN_RPB");
+    return e ? atoi(e) : 0;
+  }();
+  const int rpb = rpb_env > 0 ? rpb_env : (T >= 8192 ? 64 : 16);
   const int nc = (H / 8 + 63) / 64;
 #define DTFX_LNB(NC_)                                                                           \
   hipLaunchKernelGGL(layernorm_bwd_kernel<NC_>, dim3((T + rpb - 1) / rpb), dim3(256), 0, s, T, H, \
