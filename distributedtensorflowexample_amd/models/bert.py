@@ -35,7 +35,6 @@ import torch
 
 from ..ops import bf16 as B16
 from ..ops import init as I
-from ..ops import nn as NN
 from ..ops import transformer as TR
 
 BF16 = torch.bfloat16

@@ -5,7 +5,6 @@
 * sync DP: 2 ranks over gloo through main.py --strategy mirrored.
 """
 import glob
-import os
 import re
 import socket
 

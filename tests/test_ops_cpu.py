@@ -1,5 +1,4 @@
 """CPU paths of the ops (the CPU tier / plumbing config) vs plain autograd."""
-import pytest
 import torch
 
 from distributedtensorflowexample_amd.models.mlp import MnistMLP, from_tf_variables, init_params, \

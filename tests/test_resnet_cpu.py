@@ -67,8 +67,6 @@ def test_tiny_resnet_matches_autograd():
 def test_resnet50_layout():
     specs = conv_specs()
     assert len(specs) == 53  # 1 stem + 16 blocks x 3 + 4 projections
-    from distributedtensorflowexample_amd.models.resnet import ResNetParams
-
     n = 0
     for name, cin, cout, k, s, p in specs:
         n += cout * k * k * cin + 2 * cout

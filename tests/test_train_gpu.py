@@ -2,7 +2,6 @@
 import types
 
 import pytest
-import torch
 
 pytestmark = pytest.mark.gpu
 

@@ -1,5 +1,4 @@
 """CPU reference math of the transformer ops vs torch autograd (no GPU)."""
-import math
 
 import torch
 

@@ -1,5 +1,4 @@
 """Transformer HIP kernels vs the f32 PyTorch reference of the same op (1 GPU)."""
-import math
 
 import pytest
 import torch
