@@ -159,18 +159,21 @@ __device__ __forceinline__ bf16x8 frag(const char* lds_tile, int o0, int kk, int
     return v;
   }
 }
-// MODE 1/2 A operand (k-contiguous image [128 pix][64 k]): per-lane row state, computed once.
+// MODE 1/2 A operand (k-contiguous image [BM pix][64 k]): per-lane row state, computed once.
+// NBLK = 1 KB blocks (8 rows each) per wave: BM / 8 / NW (4 for 128x128 / 256x128, 8 for the
+// 256x64 tile); entries past NBLK are never referenced (registers only for the used ones).
 struct RowState {
-  int nb[4], y0[4], x0[4];  // n*H*W (or -1 past M), spatial base of each of the lane's 4 rows
+  int nb[8], y0[8], x0[8];  // n*H*W (or -1 past M), spatial base of each of the lane's rows
 };
 
-template <int NW>
+template <int NW, int NBLK>
 __device__ __forceinline__ void conv_rows(const ConvDesc& d, int mode, int M, int m0, int wave,
                                           int lane, RowState& rs) {
+  static_assert(NBLK <= 8, "RowState holds 8 rows per lane");
   const int PW = mode == 1 ? d.OW : d.W, PHW = mode == 1 ? d.OH * d.OW : d.H * d.W;
   const float ipw = 1.f / PW, iphw = 1.f / PHW;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NBLK; ++i) {
     const int m = m0 + (i * NW + wave) * 8 + (lane >> 3);
     int n, rem, py, px;
     fdivmod(min(m, M - 1), PHW, iphw, n, rem);
@@ -187,8 +190,8 @@ __device__ __forceinline__ void conv_rows(const ConvDesc& d, int mode, int M, in
 }
 
 // A tile gather for conv fwd (mode 1: src = x, channels C) / dgrad (mode 2: src = dy, channels K);
-// tile height 32 * NW rows: 4 blocks per wave
-template <int NW>
+// tile height 8 * NBLK * NW rows: NBLK blocks per wave
+template <int NW, int NBLK>
 __device__ __forceinline__ void stage_a_conv(const ConvDesc& d, int mode, const RowState& rs,
                                              const unsigned short* __restrict__ src, int k0,
                                              char* lds_tile, int wave, int lane) {
@@ -196,7 +199,7 @@ __device__ __forceinline__ void stage_a_conv(const ConvDesc& d, int mode, const 
   const bool uni = (CH & 63) == 0;  // a 64-wide k step stays inside one tap
   const int tap_u = k0 / CH, c_u = k0 - tap_u * CH;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NBLK; ++i) {
     const int blk = i * NW + wave;
     const int row = blk * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (row & 7);
@@ -300,11 +303,12 @@ struct GemmEpi {
 };
 
 // Tile BM_ x BN_ (128x128: 4 waves of 64x64, 2 blocks/CU; 256x128: 8 waves of 64x64;
-// 256x256: 8 waves of 128x64).  NBUF = LDS stages (2: next tile in flight during
+// 256x256: 8 waves of 128x64; 256x64 (conv fwd with 64 output channels): 4 waves of 64x64
+// stacked along M, 2 blocks/CU -- no MFMA work on a 128-wide tile's dead half).  NBUF = LDS stages (2: next tile in flight during
 // compute; 3: two tiles in flight, counted vmcnt + raw barrier).
 template <int MODE, bool TA, bool TB, bool OUT_F32, int BM_, int NBUF, int BN_>
 __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
-                             BM_ == 128 && NBUF == 2 ? 2 : 1) void gemm_bf16_kernel(
+                             (BM_ == 128 || BN_ == 64) && NBUF == 2 ? 2 : 1) void gemm_bf16_kernel(
     int M, int N, int K, const unsigned short* __restrict__ A, int lda,
     const unsigned short* __restrict__ B, int ldb, void* __restrict__ Cv, int ldc, GemmEpi e,
     long long sA, long long sB, long long sC, ConvDesc cd) {
@@ -356,11 +360,11 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
   const int kt0 = split * per;
   const int nk = max(0, min(per, nk_all - kt0));
   RowState rs;
-  if (MODE == 1 || MODE == 2) conv_rows<NW>(cd, MODE, M, m0, wave, lane, rs);
+  if (MODE == 1 || MODE == 2) conv_rows<NW, BM / 8 / NW>(cd, MODE, M, m0, wave, lane, rs);
   auto stage_all = [&](int buf, int kt) {
     char* base = smem + buf * BUF_BYTES;
     const int k0 = (kt0 + kt) * BK;
-    if (MODE == 1 || MODE == 2) stage_a_conv<NW>(cd, MODE, rs, A, k0, base, wave, lane);
+    if (MODE == 1 || MODE == 2) stage_a_conv<NW, BM / 8 / NW>(cd, MODE, rs, A, k0, base, wave, lane);
     else stage<!TA, BM, NW>(A, lda, m0, a_max, k0, base, wave, lane, K - 1);
     if (MODE == 2) stage_b_wtap<NW>(cd, B, n0, k0, base + TILE_A, wave, lane);
     else if (MODE == 3) stage_b_im2col<NW>(cd, B, K, n0, k0, base + TILE_A, wave, lane);
@@ -369,8 +373,8 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
   auto compute = [&](int buf) {
     const char* At = smem + buf * BUF_BYTES;
     const char* Bt = At + TILE_A;
-    if constexpr (BM_ == 128 && NBUF == 2 && BN_ == 128) {
-      // 128x128 (two blocks per CU): both k-halves' fragments are requested before the
+    if constexpr (NBUF == 2 && ((BM_ == 128 && BN_ == 128) || (BM_ == 256 && BN_ == 64))) {
+      // 128x128 / 256x64 (two blocks per CU, 64x64 per wave): both k-halves' fragments are requested before the
       // first MFMA (half 1's LDS latency hides under half 0's MFMAs) and the MFMAs issue at
       // raised priority, so the partner wave on the SIMD does its reads in the gaps
       bf16x8 af2[2][TM], bf2[2][4];
@@ -672,7 +676,7 @@ static int gemm_cfg_env() {
 
 static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
   const int f = gemm_cfg_env();
-  if (f >= 0 && f <= 3) return f;
+  if (f >= 0 && f <= 4) return f;
   if (mode == 0) {  // the 256x256 tile halves L2 traffic when it still fills the chip
                     // (measured: 1.11 vs 0.92 PF at 8192^3); A^T operands stay on 128x128.
     // Wave quantisation decides between them: 256x256 runs 1 block/CU (256 slots),
@@ -686,7 +690,9 @@ static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
     const double e0 = (double)t0 / (double)(((t0 + 511) / 512) * 512);
     return e3 * 1.15 >= e0 ? 3 : 0;
   }
-  // convolutions (ResNet-50 end to end: 6881 img/s on 128x128 vs 6411-6416 on 256x128)
+  // convolutions (ResNet-50 end to end: 6881 img/s on 128x128 vs 6411-6416 on 256x128);
+  // a forward conv with <= 64 output channels takes the 256x64 tile (no dead half)
+  if (mode == 1 && N <= 64) return 4;
   return 0;
 }
 
@@ -720,6 +726,13 @@ static void launch_cfg(int cfg, dim3 grid_yz, int M, int N, int K, const unsigne
     if (cfg == 3) {
       launch_one<MODE, TA, TB, F, 256, 2, 256>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
                                                d, stream);
+      return;
+    }
+  }
+  if constexpr (MODE == 1) {
+    if (cfg == 4) {
+      launch_one<MODE, TA, TB, F, 256, 2, 64>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
+                                              d, stream);
       return;
     }
   }
