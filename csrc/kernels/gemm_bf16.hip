@@ -103,6 +103,12 @@ namespace gb {
 constexpr int BN = 128, BK = 64;  // tile N and K; the tile height BM is a template parameter
 
 __device__ __forceinline__ int swz_tr(int r) { return ((r & 3) | (((r >> 3) & 1) << 2)) << 1; }
+// 64-wide k-strided images (128-B rows: even rows on banks 0-31, odd rows on 32-63): a
+// ds_read_b64_tr_b16 half-wave reads rows {q, q+8} (q = 0..3) x 2 chunks; the XOR puts the 4
+// same-parity rows on 4 disjoint chunk pairs (conflict-free; values stay < 8 chunks)
+__device__ __forceinline__ int swz64(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
+template <int OUTER>
+__device__ __forceinline__ int swz_k(int r) { return OUTER == 64 ? swz64(r) : swz_tr(r); }
 
 // Stage one operand tile of OUTER x 64 (OUTER * 128 bytes) with glds: NW waves, each wave
 // instruction fills one 1 KB block.
@@ -126,7 +132,7 @@ __device__ __forceinline__ void stage(const unsigned short* __restrict__ src, in
       g = src + (size_t)o * ld + k0 + c * 8;
     } else {
       const int kr = blk * RPB + lane / LPR, cs = lane % LPR;
-      const int c = cs ^ swz_tr(kr);
+      const int c = cs ^ swz_k<OUTER>(kr);
       const int o = min(outer0 + c * 8, outer_max);  // outer_max is 8-aligned-safe (host)
       g = src + (size_t)min(k0 + kr, kmax) * ld + o;  // clamped K tail: partner operand is 0
     }
@@ -149,8 +155,8 @@ __device__ __forceinline__ bf16x8 frag(const char* lds_tile, int o0, int kk, int
     const int col = o0 + 4 * p;
     const int cch = col >> 3, cb = (col & 7) * 2;
     const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
-    const char* a0 = lds_tile + r0 * RB + ((cch ^ swz_tr(r0)) << 4) + cb;
-    const char* a1 = lds_tile + r1 * RB + ((cch ^ swz_tr(r1)) << 4) + cb;
+    const char* a0 = lds_tile + r0 * RB + ((cch ^ swz_k<OUTER>(r0)) << 4) + cb;
+    const char* a1 = lds_tile + r1 * RB + ((cch ^ swz_k<OUTER>(r1)) << 4) + cb;
     bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)a0);
     bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)a1);
     bf16x8 v;
@@ -228,16 +234,18 @@ __device__ __forceinline__ void stage_a_conv(const ConvDesc& d, int mode, const 
   }
 }
 
-// B tile for dgrad (k-strided image [64 k][128 ci]): W'[k = (kh, kw, co)][ci] = W[co][kh][kw][ci]
-template <int NW>
+// B tile for dgrad (k-strided image [64 k][OUTER ci], OUTER = 128 or 64):
+// W'[k = (kh, kw, co)][ci] = W[co][kh][kw][ci]
+template <int NW, int OUTER>
 __device__ __forceinline__ void stage_b_wtap(const ConvDesc& d, const unsigned short* __restrict__ w,
                                              int n0, int k0, char* lds_tile, int wave, int lane) {
+  constexpr int LPR = OUTER / 8, RPB = 64 / LPR;  // lanes per k-row, k-rows per 1 KB block
   const int tap = k0 / d.K, co0 = k0 - tap * d.K;  // host: K % 64 == 0
 #pragma unroll
-  for (int i = 0; i < 16 / NW; ++i) {
+  for (int i = 0; i < (OUTER / 8) / NW; ++i) {
     const int blk = i * NW + wave;
-    const int kr = blk * 4 + (lane >> 4);
-    const int c = (lane & 15) ^ swz_tr(kr);
+    const int kr = blk * RPB + lane / LPR;
+    const int c = (lane % LPR) ^ swz_k<OUTER>(kr);
     const int o = n0 + c * 8;
     const bool ok = k0 + kr < d.ktot && o < d.C;
     const unsigned short* g =
@@ -317,7 +325,8 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
   constexpr int WM = BN_ == 256 ? 128 : 64;        // wave tile WM x 64
   constexpr int NWN = BN / 64, NW = (BM / WM) * NWN;
   constexpr int TM = WM / 16;                      // 16-row MFMA tiles per wave
-  static_assert(BN_ == 128 || (MODE == 0 || MODE == 1), "gathered B operands need BN = 128");
+  static_assert(BN_ == 128 || MODE == 0 || MODE == 1 || (MODE == 2 && BN_ == 64),
+                "gathered B operands need BN = 128 (dgrad: or 64)");
   constexpr int TILE_A = BM * BK * 2, TILE_B = BN * BK * 2, BUF_BYTES = TILE_A + TILE_B;
   constexpr int LPT = (BM / 8) / NW + (BN / 8) / NW;  // glds per thread per K tile
   // strided batch over blockIdx.z (attention's per-(batch, head) products)
@@ -366,7 +375,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
     const int k0 = (kt0 + kt) * BK;
     if (MODE == 1 || MODE == 2) stage_a_conv<NW, BM / 8 / NW>(cd, MODE, rs, A, k0, base, wave, lane);
     else stage<!TA, BM, NW>(A, lda, m0, a_max, k0, base, wave, lane, K - 1);
-    if (MODE == 2) stage_b_wtap<NW>(cd, B, n0, k0, base + TILE_A, wave, lane);
+    if (MODE == 2) stage_b_wtap<NW, BN>(cd, B, n0, k0, base + TILE_A, wave, lane);
     else if (MODE == 3) stage_b_im2col<NW>(cd, B, K, n0, k0, base + TILE_A, wave, lane);
     else stage<TB, BN, NW>(B, ldb, n0, b_max, k0, base + TILE_A, wave, lane, K - 1);
   };
@@ -691,8 +700,9 @@ static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
     return e3 * 1.15 >= e0 ? 3 : 0;
   }
   // convolutions (ResNet-50 end to end: 6881 img/s on 128x128 vs 6411-6416 on 256x128);
-  // a forward conv with <= 64 output channels takes the 256x64 tile (no dead half)
-  if (mode == 1 && N <= 64) return 4;
+  // a forward conv with <= 64 output channels, or a dgrad with <= 64 input channels, takes
+  // the 256x64 tile (no dead half)
+  if ((mode == 1 || mode == 2) && N <= 64) return 4;
   return 0;
 }
 
@@ -729,7 +739,7 @@ static void launch_cfg(int cfg, dim3 grid_yz, int M, int N, int K, const unsigne
       return;
     }
   }
-  if constexpr (MODE == 1) {
+  if constexpr (MODE == 1 || MODE == 2) {
     if (cfg == 4) {
       launch_one<MODE, TA, TB, F, 256, 2, 64>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
                                               d, stream);
