@@ -159,6 +159,12 @@ class BertMLM:
         self.cfg = cfg
         self.device = torch.device(device)
         self.params = FlatParams(cfg, device, seed)
+        # encoder weight gradients on a second HIP stream: they only need the layer's output
+        # gradient and saved input, so they overlap the (independent) dgrad GEMMs -- whose
+        # last wave is half empty at M = 16K tokens, N = 768 (768 tiles on 512 resident
+        # slots).  ``wgrad_sync_buckets``: join before every gradient-bucket hook (sync DP).
+        self.wgrad_stream = None
+        self.wgrad_sync_buckets = True
 
     # ------------------------------------------------------------------ forward
     def _layer_fwd(self, l, x, batch, seq, kmask):
@@ -236,10 +242,23 @@ class BertMLM:
         dh = torch.zeros(Tn, cfg.hidden, device=h.device, dtype=BF16)
         dh.index_add_(0, mask_pos, dhm)  # padding rows carry zero gradient
         # ---- backward: encoder
+        ws, keep = self.wgrad_stream, []  # keep: operands the side stream still reads
+
+        def wgrad(dy, xin, name):
+            if ws is None:
+                B16.gemm(dy, xin, True, False, out=p.G(name), beta=1.0)
+                return
+            ws.wait_stream(torch.cuda.current_stream(dy.device))
+            with torch.cuda.stream(ws):
+                B16.gemm(dy, xin, True, False, out=p.G(name), beta=1.0)
+            keep.append((dy, xin))
+
         for l in reversed(range(cfg.layers)):
-            dh = self._layer_bwd(l, dh, saved[l], batch, seq, kmask)
+            dh = self._layer_bwd(l, dh, saved[l], batch, seq, kmask, wgrad)
             saved[l] = None
             if on_bucket_ready is not None:
+                if ws is not None and self.wgrad_sync_buckets:
+                    torch.cuda.current_stream(dh.device).wait_stream(ws)
                 on_bucket_ready(l + 1)
         # ---- backward: embeddings
         dx0 = TR.layernorm_bwd(dh, x0, me, re, p.P("embeddings/LayerNorm/gamma"),
@@ -247,11 +266,14 @@ class BertMLM:
         TR.embed_bwd(ids_f, tt_f, dx0, p.G("embeddings/word_embeddings"),
                      p.G("embeddings/position_embeddings"),
                      p.G("embeddings/token_type_embeddings"), batch, seq)
+        if ws is not None:  # join: every gradient final on the main stream
+            torch.cuda.current_stream(dx0.device).wait_stream(ws)
+            keep.clear()
         if on_bucket_ready is not None:
             on_bucket_ready(0)
         return loss, acc
 
-    def _layer_bwd(self, l, dout, s, batch, seq, kmask):
+    def _layer_bwd(self, l, dout, s, batch, seq, kmask, wgrad):
         cfg, p = self.cfg, self.params
         pre = "encoder/layer_%d/" % l
         x, qkv, ctx, lse, a, m1, r1, h1, u, g, f, m2, r2 = s
@@ -260,20 +282,20 @@ class BertMLM:
         df = TR.layernorm_bwd(dout, f, m2, r2, p.P(pre + "output/LayerNorm/gamma"),
                               p.G(pre + "output/LayerNorm/gamma"), p.G(pre + "output/LayerNorm/beta"),
                               dxsum=p.G(pre + "output/dense/bias"))
-        B16.gemm(df, g, True, False, out=p.G(pre + "output/dense/kernel"), beta=1.0)
+        wgrad(df, g, pre + "output/dense/kernel")
         du = B16.gemm(df, p.W(pre + "output/dense/kernel"), act_grad="gelu", aux_in=u,
                       colsum=p.G(pre + "intermediate/dense/bias"))
-        B16.gemm(du, h1, True, False, out=p.G(pre + "intermediate/dense/kernel"), beta=1.0)
+        wgrad(du, h1, pre + "intermediate/dense/kernel")
         dh1 = B16.gemm(du, p.W(pre + "intermediate/dense/kernel"), residual=df)
         da = TR.layernorm_bwd(dh1, a, m1, r1, p.P(pre + "attention/output/LayerNorm/gamma"),
                               p.G(pre + "attention/output/LayerNorm/gamma"),
                               p.G(pre + "attention/output/LayerNorm/beta"),
                               dxsum=p.G(pre + "attention/output/dense/bias"))
-        B16.gemm(da, ctx, True, False, out=p.G(pre + "attention/output/dense/kernel"), beta=1.0)
+        wgrad(da, ctx, pre + "attention/output/dense/kernel")
         dctx = B16.gemm(da, p.W(pre + "attention/output/dense/kernel"))
         dqkv = TR.attn_bwd(qkv, ctx, dctx, lse, batch, seq, cfg.heads, kmask,
                            dbias=p.G(pre + "attention/qkv/bias"))
-        B16.gemm(dqkv, x, True, False, out=p.G(pre + "attention/qkv/kernel"), beta=1.0)
+        wgrad(dqkv, x, pre + "attention/qkv/kernel")
         return B16.gemm(dqkv, p.W(pre + "attention/qkv/kernel"), residual=da)
 
     # ------------------------------------------------------------------ optimizer

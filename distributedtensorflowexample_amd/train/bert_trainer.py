@@ -16,6 +16,8 @@ BASELINE.json north star asks for, applied to BERT-base.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..models.bert import BertConfig, BertMLM, synthetic_mlm_batch
@@ -39,6 +41,9 @@ class BertTrainer:
             TR.cast_bf16(p.master, p.bf)
         self.gpu = self.device.type == "cuda"
         self.comm_stream = torch.cuda.Stream(self.device) if (self.gpu and overlap and self.world > 1) else None
+        if self.gpu and os.environ.get("DTFX_BERT_WSTREAM", "1") != "0":
+            self.model.wgrad_stream = torch.cuda.Stream(self.device)
+            self.model.wgrad_sync_buckets = self.world > 1
         self.data = synthetic_mlm_batch(cfg, batch, seq, device,
                                         seed=(data_seed if data_seed is not None else 17))
         self.step_t = torch.ones(1, dtype=torch.int32, device=self.device)  # Adam step (device side)
