@@ -56,8 +56,12 @@ def _native_comm(world, rank, dev, max_numel):
     if SHARED_GPU:
         from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
 
+        # LL push words take 8 B per element per peer slot: model-sized buckets (BERT's 110M
+        # parameters: 3.5 GB per rank) use the flag protocol's f32 slots instead (an IPC
+        # mapping of that size did not open within minutes on the shared GPU)
+        small = world <= 8 and max_numel <= (4 << 20)
         return XgmiComm(rank, world, max_numel, device=dev, key="dtfx/shared",
-                        protocol="push" if world <= 8 else "flag",
+                        protocol="push" if small else "flag",
                         timeout_s=120.0)  # peers time-share the GPU (and start skewed)
     from distributedtensorflowexample_amd.parallel.comm import NativeComm
 
