@@ -731,20 +731,39 @@ __global__ __launch_bounds__(256) void mlm_xent_kernel(int C, const float* __res
   float m = -INFINITY, sum = 0.f, best = -INFINITY;
   int am = 0x7fffffff;
   const int C4 = C >> 2;
-  for (int i = t; i < C4; i += 256) {
-    const f32x4 v = ((const f32x4*)l)[i];
+  // U 16-B chunks in flight per thread; the running (max, sum) is rescaled once per pass
+  // of U*4 values (branch-free inner loop) instead of per element
+  constexpr int U = 4;
+  for (int i0 = t; i0 < C4; i0 += 256 * U) {
+    f32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float x = v[u];
-      if (x > best) { best = x; am = 4 * i + u; }
-      if (x > m) { sum = sum * __expf(m - x) + 1.f; m = x; }
-      else sum += __expf(x - m);
+    for (int k = 0; k < U; ++k) {
+      const int i = i0 + 256 * k;
+      v[k] = i < C4 ? ((const f32x4*)l)[i] : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     }
+    float lm = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float x = v[k][u];
+        if (x > best) { best = x; am = 4 * (i0 + 256 * k) + u; }  // first index on ties
+        lm = fmaxf(lm, x);
+      }
+    if (lm > m) {
+      sum = m == -INFINITY ? 0.f : sum * __expf(m - lm);
+      m = lm;
+    }
+    if (m != -INFINITY)
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sum += __expf(v[k][u] - m);  // -inf pads add 0
   }
   for (int c = 4 * C4 + t; c < C; c += 256) {
     const float x = l[c];
     if (x > best) { best = x; am = c; }
-    if (x > m) { sum = sum * __expf(m - x) + 1.f; m = x; }
+    if (x > m) { sum = (m == -INFINITY ? 0.f : sum * __expf(m - x)) + 1.f; m = x; }
     else sum += __expf(x - m);
   }
   // wave reduce (max, sum) pairs and (best, argmax, lowest index on ties)
@@ -781,12 +800,14 @@ __global__ __launch_bounds__(256) void mlm_xent_kernel(int C, const float* __res
   unsigned short* d = dl + (size_t)row * ldd;
   const float sc = valid ? scale : 0.f;
   for (int i = t; i < (ldd >> 2); i += 256) {
+    const bool vec = 4 * i + 3 < C;  // (ldl % 4 == 0: the 16-B load is aligned)
+    const f32x4 lv = vec ? ((const f32x4*)l)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
     bf16x4 o;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = 4 * i + u;
       float g = 0.f;
-      if (c < C) g = (__expf(l[c] - lse) - (c == y ? 1.f : 0.f)) * sc;
+      if (c < C) g = (__expf((vec ? lv[u] : l[c]) - lse) - (c == y ? 1.f : 0.f)) * sc;
       o[u] = (short)tobf(g);
     }
     ((bf16x4*)d)[i] = o;
