@@ -29,7 +29,8 @@ import torch
 
 
 class DistributedDataParallel(torch.nn.Module):
-    def __init__(self, module, comm, bucket_mb=32.0, broadcast_init=True, average=True):
+    def __init__(self, module, comm, bucket_mb=32.0, broadcast_init=True, average=True,
+                 shard=False):
         super().__init__()
         self.module = module
         self.comm = comm
@@ -44,11 +45,31 @@ class DistributedDataParallel(torch.nn.Module):
             raise ValueError("DDP flat buffers need a single device and dtype")
         self.device = dev
         n = sum(p.numel() for p in params)
-        # 16-element alignment of every view keeps dwordx4 kernels legal
-        offs, off = [], 0
-        for p in params:
-            offs.append(off)
-            off += (p.numel() + 15) // 16 * 16
+        # buckets in reverse parameter order (gradient production order), each a contiguous
+        # span of the flat buffer; 16-element alignment of every view keeps dwordx4 kernels
+        # legal.  shard=True (ZeRO-1, parallel/sharded.py) pads every bucket to a multiple of
+        # 16 * world so each rank owns an aligned 1/world slice of every bucket.
+        self.shard = bool(shard)
+        align = 16 * (self.world_size if self.shard else 1)
+        sz = [(p.numel() + 15) // 16 * 16 for p in params]
+        cap = max(1, int(bucket_mb * 2 ** 20 / params[0].element_size()))
+        groups, cur, span = [], [], 0
+        for i in reversed(range(len(params))):
+            if cur and span + sz[i] > cap:
+                groups.append(cur)
+                cur, span = [], 0
+            cur.append(i)
+            span += sz[i]
+        if cur:
+            groups.append(cur)
+        offs, off, spans = [0] * len(params), 0, {}
+        for g in reversed(groups):  # ascending parameter order in memory
+            lo = off
+            for i in sorted(g):
+                offs[i] = off
+                off += sz[i]
+            off = (off + align - 1) // align * align
+            spans[id(g)] = (lo, off)
         self.flat = torch.zeros(off, device=dev, dtype=dtype)
         self.flat_grad = torch.zeros(off, device=dev, dtype=dtype)
         for p, o in zip(params, offs):
@@ -56,20 +77,10 @@ class DistributedDataParallel(torch.nn.Module):
             p.data = self.flat[o:o + p.numel()].view_as(p)
             p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
         self.params, self.offsets, self.numel = params, offs, n
-        # buckets in reverse order (gradient production order)
-        cap = max(1, int(bucket_mb * 2 ** 20 / self.flat.element_size()))
-        self.buckets = []  # (lo, hi, [param idx])
-        cur, lo, hi = [], None, None
-        for i in reversed(range(len(params))):
-            o, e = offs[i], offs[i] + (params[i].numel() + 15) // 16 * 16
-            if cur and (max(hi, e) - min(lo, o)) > cap:
-                self.buckets.append((lo, hi, cur))
-                cur, lo, hi = [], None, None
-            cur.append(i)
-            lo = o if lo is None else min(lo, o)
-            hi = e if hi is None else max(hi, e)
-        if cur:
-            self.buckets.append((lo, hi, cur))
+        self.buckets = [spans[id(g)] + (g,) for g in groups]  # (lo, hi, [param idx])
+        # ZeRO-1: this rank's reduced gradient slice of every bucket (1/world of the buffer)
+        self.grad_shards = ([torch.zeros((hi - lo) // self.world_size, device=dev, dtype=dtype)
+                             for lo, hi, _ in self.buckets] if self.shard else None)
         self.bucket_of = {}
         for b, (_, _, idx) in enumerate(self.buckets):
             for i in idx:
@@ -98,12 +109,21 @@ class DistributedDataParallel(torch.nn.Module):
         if self.comm_stream is not None:
             self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.comm_stream):
-                self._reduce(view)
+                self._reduce(view, b)
         else:
-            self._reduce(view)
+            self._reduce(view, b)
         self._launched[b] = True
 
-    def _reduce(self, view):
+    def _reduce(self, view, b):
+        if self.shard:  # reduce-scatter: this rank keeps only the slice it owns
+            out = self.grad_shards[b]
+            if self.world_size == 1:
+                out.copy_(view)
+                return
+            self.comm.reduce_scatter(out, view)
+            if self.average:
+                out.div_(self.world_size)
+            return
         if self.world_size == 1:
             return
         if self.average:
@@ -146,6 +166,13 @@ class MirroredStrategy:
 
     def wrap(self, module, **kw):
         return DistributedDataParallel(module, self.comm, **kw)
+
+    def shard_optimizer(self, optimizer, ddp):
+        """ZeRO-1: ``ddp = wrap(model, shard=True)``; the returned optimizer updates only
+        this replica's slice of every bucket and all-gathers it (parallel/sharded.py)."""
+        from .sharded import ShardedOptimizer
+
+        return ShardedOptimizer(optimizer, ddp)
 
     def reduce_mean_(self, t):
         if self.num_replicas_in_sync > 1:

@@ -137,3 +137,66 @@ def test_replica_divergence_check():
         p.join(30)
     for r, ok, msg in res:
         assert ok, (r, msg)
+
+
+def _zero1_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from distributedtensorflowexample_amd.optim import AdamOptimizer, MomentumOptimizer
+        from distributedtensorflowexample_amd.parallel.comm import TorchComm
+        from distributedtensorflowexample_amd.parallel.mirrored import (DistributedDataParallel,
+                                                                        replica_divergence)
+        from distributedtensorflowexample_amd.parallel.sharded import ShardedOptimizer
+
+        comm = TorchComm()
+        torch.manual_seed(0)
+        x = torch.rand(8 * world, 784)
+        y = torch.randint(0, 10, (8 * world,))
+        xb, yb = x[rank * 8:(rank + 1) * 8], y[rank * 8:(rank + 1) * 8]
+        out = []
+        for make in (lambda: AdamOptimizer(0.01), lambda: MomentumOptimizer(0.1, 0.9)):
+            ref, zm = _MLP4(), _MLP4()
+            ddp_ref = DistributedDataParallel(ref, comm, bucket_mb=0.05)
+            ddp_z = DistributedDataParallel(zm, comm, bucket_mb=0.05, shard=True)
+            assert len(ddp_z.buckets) > 1
+            assert all((hi - lo) % (16 * world) == 0 for lo, hi, _ in ddp_z.buckets)
+            opt_ref, zopt = make(), ShardedOptimizer(make(), ddp_z)
+            for _ in range(3):
+                for m, d in ((ref, ddp_ref), (zm, ddp_z)):
+                    d.reset()
+                    m.loss(xb, yb)[0].backward()
+                ddp_ref.finish()
+                opt_ref.apply_gradients([(ddp_ref.flat_grad, ddp_ref.flat)])
+                zopt.step()
+            err = (_flat(ref) - _flat(zm)).abs().max().item()
+            # optimizer state is 1/world of the replicated form
+            ratio = zopt.state_numel() / sum(t.numel() for t in opt_ref._slots.values())
+            out.append((err, ratio, replica_divergence(comm, ddp_z.flat, world)))
+        q.put((rank, out, ""))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported through the queue
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_zero1_sharded_optimizer_matches_replicated():
+    """ZeRO-1 (reduce-scatter -> owner update -> all-gather, parallel/sharded.py) gives the
+    replicated-optimizer result with 1/world of the optimizer state; world 3 exercises the
+    bucket padding (79,510 parameters do not divide by 3 * 16)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_zero1_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    for r, out, msg in res:
+        assert out is not None, (r, msg)
+        for err, ratio, div in out:
+            assert err < 1e-5, (r, err)
+            assert abs(ratio - 1.0 / world) < 0.01, (r, ratio)
+            assert div == 0.0
