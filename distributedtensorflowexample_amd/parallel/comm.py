@@ -75,6 +75,12 @@ class TorchComm:
         dist.all_gather_into_tensor(out, inp, group=self.group)
         return out
 
+    def all_to_all(self, out, inp):
+        """Slice i (of world equal slices along dim 0) of ``inp`` goes to rank i; ``out``
+        slice j comes from rank j."""
+        dist.all_to_all_single(out, inp, group=self.group)
+        return out
+
     def barrier(self):
         dist.barrier(group=self.group)
 
@@ -135,6 +141,11 @@ class NativeComm:
     def all_gather(self, out, inp):
         self._comm.all_gather(inp.data_ptr(), out.data_ptr(), inp.numel(), self._check(inp),
                               _stream())
+        return out
+
+    def all_to_all(self, out, inp):
+        self._comm.all_to_all(inp.data_ptr(), out.data_ptr(), inp.numel() // self.world_size,
+                              self._check(inp), inp.element_size(), _stream())
         return out
 
     def barrier(self):
