@@ -193,6 +193,8 @@ def define_reference_flags(flag_values=FLAGS):
     DEFINE_string("dtype", "auto", "auto: fp32 for the MLP (reference dtype), bf16 for bert/resnet50",
                   fv)
     DEFINE_float("bucket_mb", 32.0, "All-reduce bucket size for generic DDP models (MiB)", fv)
+    DEFINE_boolean("zero1", False, "Autograd sync-DP path: shard the optimizer update over the "
+                   "replicas (ZeRO-1: reduce-scatter, owner update, all-gather)", fv)
     DEFINE_integer("check_replicas_every", 0,
                    "Sync DP debug check (SURVEY 5.2): every N steps compare every replica's "
                    "parameters with rank 0's and stop if they are not bit-identical (0 = off)", fv)

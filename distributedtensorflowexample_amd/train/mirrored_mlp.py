@@ -22,7 +22,9 @@ import torch.distributed as dist
 from ..models import mlp as mlp_model
 from ..ops import mlp_step, nn, optim
 from ..parallel.comm import NativeComm, TorchComm
+from ..optim import GradientDescentOptimizer
 from ..parallel.mirrored import DistributedDataParallel
+from ..parallel.sharded import ShardedOptimizer
 from ..utils.summary import FileWriter
 from .fused_mlp import FusedMLPTrainer
 from .saver import FastSaver
@@ -94,7 +96,10 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
         step_fn = None
     else:
         model = mlp_model.MnistMLP(flat=params)
-        ddp = DistributedDataParallel(model, comm) if comm else None
+        zero1 = bool(getattr(flags, "zero1", False)) and comm is not None
+        ddp = DistributedDataParallel(model, comm, shard=zero1) if comm else None
+        zopt = (ShardedOptimizer(GradientDescentOptimizer(flags.learning_rate), ddp)
+                if zero1 else None)
         state["pos"] = 0
         get_params = lambda: model.flat.detach().clone()  # noqa: E731
 
@@ -109,6 +114,9 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
                 model.flat.grad = None
             loss, acc = model.loss(xb, yb)
             loss.backward()
+            if zopt is not None:  # reduce-scatter -> owner SGD on 1/world -> all-gather
+                zopt.step()
+                return float(loss), float(acc)
             if ddp:
                 ddp.finish()
                 g = ddp.flat_grad[:model.flat.numel()]

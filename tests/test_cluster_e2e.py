@@ -81,3 +81,25 @@ def test_mirrored_two_ranks_gloo(tmp_path):
     assert "step: 300" in log0 and "test accuracy:" in log0
     v = load_checkpoint(latest_checkpoint(logdir))
     assert int(v["global/global_step"]) == 300
+
+
+def test_mirrored_zero1_matches_allreduce(tmp_path):
+    """main.py --strategy mirrored --zero1 (reduce-scatter, owner SGD on 1/2 of the
+    parameters, all-gather) reaches the same parameters as the all-reduce path."""
+    import numpy as np
+
+    out = {}
+    for tag, extra in (("ar", []), ("z1", ["--zero1"])):
+        logdir = str(tmp_path / tag)
+        rc = launch_mirrored(nproc=2, log_dir=str(tmp_path / ("logs_" + tag)), quiet=True,
+                             timeout=240,
+                             extra=["--training_steps", "60", "--log_every", "30",
+                                    "--eval_every", "60", "--logdir", logdir, "--device", "cpu",
+                                    "--learning_rate", "0.05", "--save_model_secs", "100"] + extra)
+        assert rc == {"rank0": 0, "rank1": 0}, (tag, rc)
+        out[tag] = load_checkpoint(latest_checkpoint(logdir))
+    assert int(out["z1"]["global/global_step"]) == 60
+    for k in ("global/dense/kernel", "global/dense/bias", "global/dense_1/kernel",
+              "global/dense_1/bias"):
+        a, b = np.asarray(out["ar"][k]), np.asarray(out["z1"][k])
+        assert np.abs(a - b).max() < 1e-5, k
