@@ -473,16 +473,24 @@ class PSClient {
       for (size_t k : per[t]) w.put<uint32_t>(static_cast<uint32_t>(hs[k]));
       send(static_cast<int>(t), w.b);
     }
+    // drain EVERY task's response before reporting a failure: an unread reply would stay
+    // queued on its socket and answer the next call on that connection
+    std::string first_error;
     for (size_t t = 0; t < per.size(); ++t) {
       if (per[t].empty()) continue;
-      std::string resp = recv(static_cast<int>(t));
-      size_t off = 0;
-      for (size_t k : per[t]) {
-        if (off + sizes[k] > resp.size()) throw std::runtime_error("ps pull: short response");
-        std::memcpy(reinterpret_cast<void*>(ptrs[k]), resp.data() + off, sizes[k]);
-        off += sizes[k];
+      try {
+        std::string resp = recv(static_cast<int>(t));
+        size_t off = 0;
+        for (size_t k : per[t]) {
+          if (off + sizes[k] > resp.size()) throw std::runtime_error("ps pull: short response");
+          std::memcpy(reinterpret_cast<void*>(ptrs[k]), resp.data() + off, sizes[k]);
+          off += sizes[k];
+        }
+      } catch (const std::exception& e) {
+        if (first_error.empty()) first_error = e.what();
       }
     }
+    if (!first_error.empty()) throw std::runtime_error(first_error);
   }
   // push gradients (f32) and apply var -= lr * grad on the owning ps tasks
   void push_apply(std::vector<int64_t> hs, std::vector<uintptr_t> ptrs, std::vector<size_t> sizes,
@@ -504,8 +512,16 @@ class PSClient {
       for (size_t k : per[t]) w.raw(reinterpret_cast<const void*>(ptrs[k]), sizes[k]);
       send(static_cast<int>(t), w.b);
     }
-    for (size_t t = 0; t < per.size(); ++t)
-      if (!per[t].empty()) recv(static_cast<int>(t));
+    std::string first_error;  // drain every task's reply first (see pull)
+    for (size_t t = 0; t < per.size(); ++t) {
+      if (per[t].empty()) continue;
+      try {
+        recv(static_cast<int>(t));
+      } catch (const std::exception& e) {
+        if (first_error.empty()) first_error = e.what();
+      }
+    }
+    if (!first_error.empty()) throw std::runtime_error(first_error);
   }
   int64_t fetch_add(int64_t h, int64_t delta) {
     Writer w;

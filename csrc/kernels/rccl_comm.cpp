@@ -13,6 +13,7 @@
 #include <pybind11/pybind11.h>
 #include <rccl/rccl.h>
 
+#include <cstring>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -99,14 +100,30 @@ class RcclComm {
     // grouped send/recv: rank r's slice i goes to rank i
     const ncclDataType_t t = dtype_of(dt);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    ncclComm_t c = get();
     check(ncclGroupStart(), "ncclGroupStart");
-    for (int peer = 0; peer < nranks_; ++peer) {
+    // the group is ALWAYS closed: an error inside it is recorded and raised after
+    // ncclGroupEnd, so the next collective is never merged into an unfinished group
+    ncclResult_t first = ncclSuccess;
+    const char* what = "";
+    for (int peer = 0; peer < nranks_ && first == ncclSuccess; ++peer) {
       const char* sp = reinterpret_cast<const char*>(send) + peer * count_per_rank * elem_size;
       char* rp = reinterpret_cast<char*>(recv) + peer * count_per_rank * elem_size;
-      check(ncclSend(sp, count_per_rank, t, peer, get(), s), "ncclSend");
-      check(ncclRecv(rp, count_per_rank, t, peer, get(), s), "ncclRecv");
+      ncclResult_t r = ncclSend(sp, count_per_rank, t, peer, c, s);
+      if (r != ncclSuccess) {
+        first = r;
+        what = "ncclSend";
+        break;
+      }
+      r = ncclRecv(rp, count_per_rank, t, peer, c, s);
+      if (r != ncclSuccess) {
+        first = r;
+        what = "ncclRecv";
+      }
     }
-    check(ncclGroupEnd(), "ncclGroupEnd");
+    const ncclResult_t end = ncclGroupEnd();
+    check(first, what);
+    check(end, "ncclGroupEnd");
   }
   int nranks() const { return nranks_; }
   int rank() const { return rank_; }

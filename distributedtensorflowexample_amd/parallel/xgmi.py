@@ -119,6 +119,14 @@ class XgmiComm:
             t.zero_()
         return self.allreduce_sum_(t)
 
+    def allreduce_max_(self, t):
+        """Element-wise max over ranks for control-path checks (``--check_replicas_every``):
+        over the default torch.distributed group (the gloo control plane), not xGMI."""
+        c = t.detach().cpu()
+        dist.all_reduce(c, op=dist.ReduceOp.MAX)
+        t.copy_(c)
+        return t
+
     def failed(self):
         """True if any call timed out waiting for a peer (synchronizes the device)."""
         torch.cuda.synchronize(self.device)

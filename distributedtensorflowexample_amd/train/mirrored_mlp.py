@@ -46,6 +46,11 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         comm = NativeComm.from_process_group() if world > 1 else None
+        if getattr(flags, "zero1", False) and world > 1:
+            # the fused GPU engines exchange gradients inside their kernels; a 1/N-sharded
+            # update of a 318 KB model would only add two collectives per step
+            raise ValueError("--zero1 is implemented on the autograd (CPU) mirrored path; the "
+                             "fused GPU MLP engines replicate the update")
         if comm is not None and os.environ.get("DTFX_MLP_COMM", "auto") != "rccl":
             # the 318 KB gradient is latency bound: xGMI one-shot when verified and faster
             from ..parallel.select import pick_small_allreduce
@@ -65,7 +70,9 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
     tr_y = (tr_y.argmax(1) if tr_y.ndim == 2 else tr_y).to(torch.int32)
 
     writer = FileWriter(flags.logdir + "_%d" % rank) if is_chief else None
-    state = {}
+    # host mirror of global_step, advanced by the training loop only: the Supervisor's
+    # service threads read it instead of touching trainer/device state
+    state = {"step": 0}
 
     if use_gpu:
         fused = factor = x_all = None
@@ -138,6 +145,9 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
     def global_step():
         return tr.global_step() if use_gpu else state.get("pos", 0)
 
+    def published_step():
+        return state["step"]
+
     def restore(values):
         p = torch.zeros(mlp_step.NPARAM)
         tf_vars_to_flat(values, p)
@@ -148,12 +158,16 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
         else:
             model.flat.data.copy_(p)
             state["pos"] = int(values["global/global_step"])
+        state["step"] = int(values["global/global_step"])
 
     saver.assign = restore
+    # checkpoints are taken by the training loop between chunks (Supervisor.service): the
+    # fused trainer's deferred update may only be flushed where every rank flushes it
     sv = Supervisor(is_chief=is_chief, logdir=flags.logdir if is_chief else None,
                     saver=saver if is_chief else None, summary_writer=writer,
-                    global_step=global_step, save_model_secs=flags.save_model_secs,
-                    save_summaries_secs=flags.save_summaries_secs, save_variables=save_vars)
+                    global_step=published_step, save_model_secs=flags.save_model_secs,
+                    save_summaries_secs=flags.save_summaries_secs, save_variables=save_vars,
+                    checkpoint_on_main_thread=True)
 
     test_x = torch.from_numpy(dataset.test.images).float().to(dev)
     test_y = dataset.test.labels.argmax(1) if dataset.test.labels.ndim == 2 else dataset.test.labels
@@ -178,7 +192,8 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
             else:
                 model.flat.data.copy_(p)
         chunk = int(flags.log_every)
-        start_time, start_step = time.time(), global_step()
+        state["step"] = global_step()
+        start_time, start_step = time.time(), state["step"]
         while not sv.should_stop():
             s0 = global_step()
             n = min(chunk - (s0 % chunk) if s0 % chunk else chunk, steps_total - s0)
@@ -190,6 +205,7 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
             else:
                 stats = torch.tensor([step_fn() for _ in range(n)])
             step = global_step()
+            state["step"] = step
             if writer is not None:
                 writer.add_scalar_series(["loss", "accuracy"], range(s0, s0 + n), stats.tolist())
             cost = float(stats[-1, 0])
@@ -208,6 +224,7 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
                 from ..parallel.mirrored import assert_replicas_identical
 
                 assert_replicas_identical(comm, get_params(), world, step)
+            sv.service()  # a requested checkpoint, on this thread, between chunks
             if step >= steps_total:
                 break
         if is_chief:

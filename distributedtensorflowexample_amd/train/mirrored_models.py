@@ -46,6 +46,9 @@ def train_model_mirrored(flags, log=print):
         dev = torch.device("cpu")
         comm = TorchComm() if world > 1 else None
     is_chief = rank == 0
+    if getattr(flags, "zero1", False) and world > 1:
+        raise ValueError("--zero1 is not implemented for --model %s (replicated fused "
+                         "optimizer); it applies to the autograd MLP path" % flags.model)
     tiny = flags.model_config == "tiny"
     if flags.model == "bert":
         from ..models import bert as M
@@ -85,7 +88,8 @@ def train_model_mirrored(flags, log=print):
     sv = Supervisor(is_chief=is_chief, logdir=flags.logdir if is_chief else None,
                     saver=saver if is_chief else None, summary_writer=writer,
                     global_step=global_step, save_model_secs=flags.save_model_secs,
-                    save_summaries_secs=flags.save_summaries_secs, save_variables=save_vars)
+                    save_summaries_secs=flags.save_summaries_secs, save_variables=save_vars,
+                    checkpoint_on_main_thread=True)  # never read parameters mid-step
     steps_total = int(flags.training_steps)
     with sv.managed_session():
         if is_chief and sv.restored_from is not None:
@@ -110,6 +114,7 @@ def train_model_mirrored(flags, log=print):
                 from ..parallel.mirrored import assert_replicas_identical
 
                 assert_replicas_identical(comm, model.params.master, world, step)
+            sv.service()  # a requested checkpoint, between steps
             if step % int(flags.log_every) == 0 or step == steps_total:
                 loss, acc = tr.stats()
                 if writer is not None:

@@ -14,6 +14,14 @@ What the reference relies on (worker.py:107-123):
 Everything is passed as callables so the same Supervisor drives the async
 PS mode (variables on the parameter server) and the sync-DP mode (variables
 replicated on the GPUs).
+
+``checkpoint_on_main_thread=True`` (sync-DP trainers): the timer thread only
+*requests* a checkpoint and the training loop performs it between steps via
+:meth:`Supervisor.service`.  A trainer whose parameters live in ping-pong
+device buffers with deferred updates (``train/fused_mlp.py``) must never be
+read from another thread: flushing it there would mutate trainer state
+concurrently with the loop and, with the xGMI exchange engines, start a peer
+exchange that only the chief joins.
 """
 from __future__ import annotations
 
@@ -69,7 +77,8 @@ class Supervisor:
     def __init__(self, is_chief=True, logdir=None, saver=None, summary_writer=None,
                  ready_op=None, global_step=None, save_model_secs=600, save_summaries_secs=120,
                  init_op=None, local_init_op=None, recovery_wait_secs=30, save_variables=None,
-                 checkpoint_basename="model.ckpt", ready_timeout_secs=None, final_checkpoint=False):
+                 checkpoint_basename="model.ckpt", ready_timeout_secs=None, final_checkpoint=False,
+                 checkpoint_on_main_thread=False):
         self.is_chief = bool(is_chief)
         self.logdir = logdir
         self.saver = saver
@@ -85,6 +94,8 @@ class Supervisor:
         self.save_path = os.path.join(logdir, checkpoint_basename) if logdir else None
         self.ready_timeout_secs = ready_timeout_secs
         self.final_checkpoint = final_checkpoint
+        self.checkpoint_on_main_thread = bool(checkpoint_on_main_thread)
+        self._ckpt_request = threading.Event()
         self.coord = Coordinator()
         self._threads = []
         self.restored_from = None
@@ -127,10 +138,19 @@ class Supervisor:
         return self.saver.save(None, self.save_path, global_step=step,
                                variables=self.save_variables() if self.save_variables else None)
 
+    def service(self):
+        """Run requested main-thread services (``checkpoint_on_main_thread``): call between
+        training steps.  Returns the checkpoint path when one was written."""
+        if self._ckpt_request.is_set():
+            self._ckpt_request.clear()
+            return self.save_checkpoint()
+        return None
+
     def start_standard_services(self):
         if self.saver is not None and self.save_model_secs and self.save_path:
-            self._threads.append(_LoopThread(self.coord, self.save_model_secs,
-                                             self.save_checkpoint, "SVTimerCheckpointThread"))
+            fn = self._ckpt_request.set if self.checkpoint_on_main_thread else self.save_checkpoint
+            self._threads.append(_LoopThread(self.coord, self.save_model_secs, fn,
+                                             "SVTimerCheckpointThread"))
         if self.summary_writer is not None and self.save_summaries_secs and self.global_step:
             state = {"t": time.time(), "s": self._step()}
 

@@ -83,6 +83,22 @@ def test_mirrored_two_ranks_gloo(tmp_path):
     assert int(v["global/global_step"]) == 300
 
 
+def test_mirrored_two_ranks_frequent_checkpoints_with_replica_check(tmp_path):
+    """A checkpoint timer much faster than the steps plus the replica-identity check every
+    10 steps: the chief saves between chunks on its training thread, so the replicas never
+    diverge (the check would stop the run) and no rank waits on a collective the other
+    never joins."""
+    logdir = str(tmp_path / "mir")
+    rc = launch_mirrored(nproc=2, log_dir=str(tmp_path / "logs"), quiet=True, timeout=240,
+                         extra=["--training_steps", "200", "--log_every", "10",
+                                "--eval_every", "200", "--logdir", logdir, "--device", "cpu",
+                                "--learning_rate", "0.05", "--save_model_secs", "0.01",
+                                "--check_replicas_every", "10"])
+    assert rc == {"rank0": 0, "rank1": 0}, rc
+    v = load_checkpoint(latest_checkpoint(logdir))
+    assert int(v["global/global_step"]) == 200
+
+
 def test_mirrored_zero1_matches_allreduce(tmp_path):
     """main.py --strategy mirrored --zero1 (reduce-scatter, owner SGD on 1/2 of the
     parameters, all-gather) reaches the same parameters as the all-reduce path."""

@@ -62,7 +62,7 @@ def _worker(rank, world, port, q):
         ddp.finish()
         optim.sgd_(ddp.flat, ddp.flat_grad, 0.5)
     st = MirroredStrategy(comm)
-    q.put((rank, _flat(model), st.check_replicas_identical(ddp.flat)))
+    q.put((rank, _flat(model).numpy().copy(), st.check_replicas_identical(ddp.flat)))  # by value
     dist.destroy_process_group()
 
 
@@ -74,7 +74,7 @@ def test_ddp_equals_large_batch_single_process():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (p, d)) for r, p, d in [q.get(timeout=120) for _ in range(world)])
+    res = dict((r, (torch.from_numpy(p), d)) for r, p, d in [q.get(timeout=120) for _ in range(world)])
     for p in procs:
         p.join(60)
         assert p.exitcode == 0

@@ -45,7 +45,8 @@ def _worker(rank, world, port, q):
         x = _rows(qkv, rank, world).clone().requires_grad_(True)
         o = ulysses_attention(x, TorchComm(), B, S // world, NH, kmask)
         o.backward(_rows(dout, rank, world))
-        q.put((rank, o.detach().float(), x.grad.float(), ""))
+        # by value: a shared-memory tensor dies with the child before the parent reads it
+        q.put((rank, o.detach().float().numpy().copy(), x.grad.float().numpy().copy(), ""))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover - reported through the queue
         import traceback
@@ -70,6 +71,7 @@ def test_ulysses_matches_full_sequence_attention():
     dqkv_ref = T.attn_bwd(qkv, o_ref, dout, lse, B, S, NH, kmask)
     for rank, o, g, msg in res:
         assert o is not None, msg
+        o, g = torch.from_numpy(o), torch.from_numpy(g)
         assert (o - _rows(o_ref, rank, world).float()).abs().max().item() < 1e-2
         assert (g - _rows(dqkv_ref, rank, world).float()).abs().max().item() < 1e-2
 

@@ -68,3 +68,40 @@ def test_mirrored_gpu_single_rank_with_restore(gpu, tmp_path, mnist):
     fl2 = _flags(tmp_path, training_steps=1200, learning_rate=0.1, eval_every=10 ** 9)
     hist2, _ = train_mirrored(fl2, mnist, log=logs.append)
     assert hist2[0][0] > 1100 and hist2[-1][0] == 1200
+
+
+def test_mirrored_gpu_periodic_checkpoints_do_not_perturb_training(gpu, tmp_path, mnist):
+    """Checkpoints requested every 20 ms by the Supervisor's timer are taken by the training
+    loop between chunks (never by the timer thread, which must not flush the fused
+    trainer): training ends bit-identical to a run without periodic saves."""
+    import glob
+    import time
+
+    import torch
+
+    from distributedtensorflowexample_amd.train import saver as saver_mod
+    from distributedtensorflowexample_amd.train.mirrored_mlp import train_mirrored
+
+    out = {}
+    for tag, secs in (("quiet", 1000.0), ("busy", 0.02)):
+        fl = _flags(tmp_path / tag, training_steps=3000, log_every=50, eval_every=10 ** 9,
+                    save_model_secs=secs, check_replicas_every=100)
+        orig = saver_mod.Saver.save
+        n_saves, threads = [0], set()
+
+        def counting(self, *a, **k):
+            n_saves[0] += 1
+            threads.add(__import__("threading").current_thread().name)
+            time.sleep(0.005)  # give the timer a chance to fire again mid-run
+            return orig(self, *a, **k)
+
+        saver_mod.Saver.save = counting
+        try:
+            hist, p = train_mirrored(fl, mnist, log=lambda *_: None)
+        finally:
+            saver_mod.Saver.save = orig
+        assert hist[-1][0] == 3000
+        out[tag] = (p.cpu(), n_saves[0], threads)
+    assert out["busy"][1] > out["quiet"][1] >= 1, (out["busy"][1], out["quiet"][1])
+    assert out["busy"][2] == {"MainThread"}, out["busy"][2]
+    assert torch.equal(out["busy"][0], out["quiet"][0])
