@@ -26,6 +26,8 @@ long long mlp_workspace_floats(int);
 void mlp_fwdapply_launch(const float*, float*, float, const float*, const float*, float*, int*,
                          float*, int, int, int, hipStream_t);
 void mlp_head2_launch(const float*, const int*, float*, int, hipStream_t);
+void mlp_run_pipelined_launch(float*, float*, int, int, float, const float*, const int*, int, int,
+                              int, float*, int*, float*, int, int, hipStream_t);
 void calib_launch(int, int, int, const int*, const float*, float*, hipStream_t);
 void clock_probe_launch(int, int, unsigned long long*, float*, hipStream_t);
 void gemm_f32_launch(bool, bool, int, int, int, float, const float*, int, const float*, int,
@@ -90,6 +92,17 @@ PYBIND11_MODULE(_hip, m) {
   m.def("mlp_head2", [](uintptr_t p, uintptr_t lab, uintptr_t ws, int B, uintptr_t s) {
     dtfx::mlp_head2_launch(P<const float>(p), P<const int>(lab), P<float>(ws), B, S(s));
   }, py::arg("p"), py::arg("labels"), py::arg("ws"), py::arg("B"), py::arg("stream"));
+  m.def("mlp_run_pipelined", [](uintptr_t p0, uintptr_t p1, int cur, int pending, float lr,
+                                uintptr_t x, uintptr_t lab, int nbatches, int pos, int n,
+                                uintptr_t ws, uintptr_t ctr, uintptr_t stats, int ring, int B,
+                                uintptr_t s) {
+    py::gil_scoped_release nogil;
+    dtfx::mlp_run_pipelined_launch(P<float>(p0), P<float>(p1), cur, pending, lr, P<const float>(x),
+                                   P<const int>(lab), nbatches, pos, n, P<float>(ws), P<int>(ctr),
+                                   P<float>(stats), ring, B, S(s));
+  }, py::arg("p0"), py::arg("p1"), py::arg("cur"), py::arg("pending"), py::arg("lr"), py::arg("x"),
+     py::arg("labels"), py::arg("nbatches"), py::arg("pos"), py::arg("n"), py::arg("ws"),
+     py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"));
   m.def("gemm_f32", [](bool ta, bool tb, int M, int N, int K, float alpha, uintptr_t A, int lda,
                        uintptr_t B, int ldb, float beta, uintptr_t C, int ldc, uintptr_t bias,
                        int act, uintptr_t aux, int ldaux, bool act_grad, uintptr_t s) {

@@ -1201,6 +1201,50 @@ void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipSt
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+// n pipelined single-GPU steps issued from ONE host call (no Python, no hipGraph): step i
+// trains on batch (pos + i) % nbatches of the device-resident dataset and ping-pongs the
+// parameter buffers exactly like n calls of mlp_fwdapply_launch + mlp_head2_launch.  A graph
+// replay pays ~15 us of submission before its first kernel runs; these launches reach the GPU
+// one by one while the host keeps queueing ahead (host ~2 us per launch < ~4 us of GPU time
+// per launch), so a short run starts at once.  Returns nothing: the caller advances its host
+// mirrors (batch position, parity, pending) by n.
+void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float lr,
+                              const float* x, const int* labels, int nbatches, int pos, int n,
+                              float* ws, int* ctr, float* stats, int stats_ring, int B,
+                              hipStream_t stream) {
+  using namespace mlp;
+  check_b(B);
+  if (!p0 || !p1 || p0 == p1 || !x || !labels || !ctr || nbatches < 1 || pos < 0 ||
+      pos >= nbatches || n < 0)
+    throw std::runtime_error("mlp_run_pipelined: bad buffers / position / count");
+  if (stats && stats_ring < 1) throw std::runtime_error("mlp_run_pipelined: stats_ring < 1");
+  const Bufs w = make_bufs(ws, B);
+  float* bufs[2] = {p0, p1};
+  const size_t xb = (size_t)B * D;
+  const bool rt7 = (B + 15) / 16 == 7;
+  for (int i = 0; i < n; ++i) {
+    const int prev = (pos + nbatches - 1) % nbatches;
+    const float* xcur = x + (size_t)pos * xb;
+    const float* xprev = pending ? x + (size_t)prev * xb : xcur;
+    const float* po = bufs[cur];
+    float* pn = bufs[cur ^ 1];
+    const float l = pending ? lr : 0.f;
+    if (rt7)
+      hipLaunchKernelGGL((mlp_fwdapply_kernel<7>), dim3(HT * KS2 + HT), dim3(256), 0, stream, po,
+                         pn, l, xprev, xcur, w, ctr, stats, stats_ring, B, 1, MlpXg{});
+    else
+      hipLaunchKernelGGL((mlp_fwdapply_kernel<0>), dim3(HT * KS2 + HT), dim3(256), 0, stream, po,
+                         pn, l, xprev, xcur, w, ctr, stats, stats_ring, B, 1, MlpXg{});
+    hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS2>), dim3(B), dim3(64), 0, stream, pn,
+                       pn, 0.f, nullptr, labels + (size_t)pos * B, w, B, nullptr, MlpXg{},
+                       nullptr);
+    cur ^= 1;
+    pending = 1;
+    pos = (pos + 1) % nbatches;
+  }
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
 // Pipelined factor engine, first launch (see mlp_fwdapply_factor_kernel).
 void mlp_fwdapply_factor_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
                                 const float* x, long long xstride, const float* dz1A, float* ws,

@@ -234,13 +234,44 @@ class FusedMLPTrainer:
             steps -= n
         return out
 
-    def run(self, steps, use_graph=True):
-        """Run ``steps`` training steps (epoch-aligned hipGraph replays)."""
+    @property
+    def host_loop_ok(self):
+        """The plain single-GPU pipelined step can be issued by the C++ host loop."""
+        return (self.pipelined and self.world_size == 1 and self.fused_comm is None
+                and self.factor_comm is None and self.allreduce is None)
+
+    def run_launched(self, steps):
+        """``steps`` pipelined single-GPU steps issued by ONE C++ call (kernel launches, no
+        graph): no ~15 us graph-submission latency before the first kernel."""
+        from ..ops._ext import hip, ptr, stream_handle
+
+        steps = int(steps)
+        if not self.host_loop_ok:
+            raise RuntimeError("run_launched: single-GPU pipelined step only")
+        if steps <= 0:
+            return
+        ws = self.ws
+        hip().mlp_run_pipelined(ptr(self.bufs[0]), ptr(self.bufs[1]), self.cur,
+                                1 if self.pending else 0, self.lr, ptr(self.x), ptr(self.labels),
+                                self.nbatches, self.pos, steps, ptr(ws.buf), ptr(ws.ctr),
+                                ptr(ws.stats), ws.stats_ring, self.B, stream_handle())
+        self.pos = (self.pos + steps) % self.nbatches
+        self.cur ^= steps & 1
+        self.pending = True
+
+    def run(self, steps, use_graph=True, lead=0):
+        """Run ``steps`` training steps (epoch-aligned hipGraph replays).  ``lead`` > 0 (single
+        GPU): the first ``lead`` steps are launched directly from C++ so the GPU starts at
+        once, and the graph replay of the rest is submitted while they run."""
         steps = int(steps)
         if not use_graph:
             for _ in range(steps):
                 self._step_launches()
             return
+        if lead > 0 and self.host_loop_ok:
+            k = min(int(lead), steps)
+            self.run_launched(k)
+            steps -= k
         if steps > 0 and not self.direct and not self.pending:
             self._step_launches()  # the first DP step has nothing to apply
             steps -= 1
@@ -250,12 +281,17 @@ class FusedMLPTrainer:
             if not self.direct:
                 self.cur ^= n & 1
 
-    def prepare(self, steps):
-        """Capture (not run) every graph a following ``run(steps)`` replays."""
+    def prepare(self, steps, lead=0):
+        """Capture (not run) every graph a following ``run(steps, lead=lead)`` replays."""
         steps = int(steps)
         if steps > 0 and not self.direct and not self.pending:
             raise RuntimeError("prepare() in DP mode needs one eager step first")
         pos, cur = self.pos, self.cur
+        if lead > 0 and self.host_loop_ok:
+            k = min(int(lead), steps)
+            self.pos = (self.pos + k) % self.nbatches
+            self.cur ^= k & 1
+            steps -= k
         for n in self._plan(steps):
             self._graph(n)
             self.pos = (self.pos + n) % self.nbatches

@@ -261,3 +261,35 @@ def test_pipelined_trainer_matches_reference_and_three_launch(gpu, B):
     l3, a3 = t3.stats()
     assert abs(lp - l3) < 1e-4 and ap == a3
     assert torch.allclose(tp.stats_range(0, 17), t3.stats_range(0, 17), atol=1e-4)
+
+
+def test_host_loop_matches_graph_replay(gpu):
+    """FusedMLPTrainer.run_launched (one C++ call issuing every step's kernels) and the
+    graph path (with and without host-launched lead steps) walk the dataset identically:
+    bit-identical parameters, global_step and stats, across an epoch boundary."""
+    from distributedtensorflowexample_amd.data.synthetic import mnist_like_device
+    from distributedtensorflowexample_amd.models.mlp import init_params
+    from distributedtensorflowexample_amd.train.fused_mlp import FusedMLPTrainer
+
+    p = init_params(gpu, seed=3)
+    x, y = mnist_like_device(1300, seed=4, device=gpu)  # 13 batches: runs wrap the epoch
+    runs = {}
+    for mode in ("graph", "host", "lead"):
+        tr = FusedMLPTrainer(p, x, y, 100, 0.05)
+        if mode == "graph":
+            tr.run(3)
+            tr.run(20)
+        elif mode == "host":
+            tr.run_launched(3)
+            tr.run_launched(20)
+        else:
+            tr.run(3)
+            tr.prepare(20, lead=4)
+            tr.run(20, lead=4)
+        st = tr.stats_range(0, 23).clone()
+        runs[mode] = (tr.flush().clone(), tr.global_step(), st, tr.pos)
+    for mode in ("host", "lead"):
+        assert torch.equal(runs[mode][0], runs["graph"][0]), mode
+        assert runs[mode][1] == runs["graph"][1] == 23
+        assert torch.equal(runs[mode][2], runs["graph"][2]), mode
+        assert runs[mode][3] == runs["graph"][3] == 23 % 13

@@ -35,6 +35,7 @@ def main():
     for rep in range(3):  # the bench sequence, fresh graph each time
         tr.prepare(K)
         res["bench_seq_%d" % rep] = t_us(lambda: (tr.run(K), tr.flush()))
+        tr.run(1, use_graph=False)
     for rep in range(3):
         tr.prepare(K)
         res["run_only_first_replay_%d" % rep] = t_us(lambda: tr.run(K))
