@@ -68,6 +68,30 @@ def _native_comm(world, rank, dev, max_numel):
     return NativeComm.from_process_group()
 
 
+def _timing_barrier(comm, local):
+    """Barrier that brackets the timed region (both sides, after torch.cuda.synchronize()).
+
+    A gloo barrier is a TCP round trip through rank 0 (~0.1-0.3 ms), as long as a whole
+    short MLP run; the ranks' GPUs already share a RCCL communicator, so the bracket is a
+    one-element RCCL all-reduce + synchronize (a device-side rendezvous of every rank).
+    Falls back to the process-group barrier where there is no RCCL communicator (the
+    shared-GPU rehearsal, --comm torch)."""
+    from distributedtensorflowexample_amd.parallel.comm import NativeComm
+
+    if isinstance(comm, NativeComm):
+        one = torch.zeros(1, device=comm.device)
+
+        def bar():
+            comm.allreduce_sum_(one)
+            torch.cuda.synchronize()
+
+        bar()  # first call of this size: RCCL sets up outside the timed region
+        return bar
+    if dist.get_backend() == "nccl":
+        return lambda: dist.barrier(device_ids=[local])
+    return dist.barrier
+
+
 def main():
     if os.environ.get("DTFX_WATCHDOG_S"):  # debugging aid: dump every thread's stack, then exit
         import faulthandler
@@ -161,6 +185,8 @@ def main():
             comm = TorchComm()
         else:
             comm = _native_comm(world, rank, dev, mlp_numel())
+        rendezvous = comm  # RCCL communicator kept for the timing barrier
+        if a.comm != "torch":
             if a.comm in ("xgmi", "auto"):
                 from distributedtensorflowexample_amd.parallel.select import pick_small_allreduce
                 from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
@@ -209,27 +235,20 @@ def main():
                          max_graph_steps=a.max_graph_steps, fused_comm=fused_comm,
                          factor_comm=factor_comm, x_all=x_all, rank=rank,
                          pipeline=getattr(a, "engine_pipeline", True))
-    if world > 1:
-        barrier = dist.barrier if a.comm != "torch" else (lambda: dist.barrier(device_ids=[local]))
-    else:
-        barrier = None
+    barrier = _timing_barrier(rendezvous, local) if world > 1 else None
     use_graph = not a.no_graph
 
+    # hipGraph replay in the timed region.  (The C++ host loop, FusedMLPTrainer.run_launched,
+    # is 1 % faster per step once warm -- tools/probes/host_loop.py -- but in a fresh process
+    # its first direct launches ran 10.6-14.9 us/step at K = 20 against 10.0 for the graph.)
     tr.run(a.warmup, use_graph)
-    # one GPU, short timed region: the C++ host loop issues the steps' kernels directly (no
-    # graph submission ahead of the first kernel; tools/probes/host_loop.py: 9.29 vs 9.40
-    # us/step at K = 20, equal at K >= 200, identical parameters); long runs replay graphs
-    host_loop = use_graph and tr.host_loop_ok and a.steps <= 200
-    if use_graph and not host_loop:
+    if use_graph:
         tr.prepare(a.steps)
     if barrier:
         barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if host_loop:
-        tr.run_launched(a.steps)
-    else:
-        tr.run(a.steps, use_graph)
+    tr.run(a.steps, use_graph)
     tr.flush()  # the last step's deferred update is part of the timed work
     torch.cuda.synchronize()
     if barrier:
@@ -268,8 +287,7 @@ def main():
                 "seq_len": None,
                 "parallelism": "dp%d" % world,
                 "comm": _comm_label(a) if (world > 1 or a.dp) else "none",
-                "hipgraph": use_graph and not host_loop,
-                "launch": "cpp-host-loop" if host_loop else ("hipgraph" if use_graph else "eager"),
+                "hipgraph": use_graph,
                 "engine": getattr(a, "engine_kind", "allreduce" if allreduce else "single"),
                 "launches_per_step": 2 if tr.pipelined else 3,
             },
@@ -297,8 +315,7 @@ def bench_bert(a, world, rank, local, dev):
     tr = BertTrainer(cfg, a.bert_batch, a.seq_len, dev, comm=comm, data_seed=17 + rank)
     use_graph = not a.no_graph
     tr.run(a.warmup, use_graph)
-    barrier = (dist.barrier if a.comm != "torch" else (lambda: dist.barrier(device_ids=[local]))) \
-        if world > 1 else None
+    barrier = _timing_barrier(comm, local) if world > 1 else None
     if barrier:
         barrier()
     torch.cuda.synchronize()
@@ -350,8 +367,7 @@ def bench_resnet(a, world, rank, local, dev):
     tr = ResNetTrainer(a.resnet_batch, dev, comm=comm, image_size=a.image_size, data_seed=rank)
     use_graph = not a.no_graph
     tr.run(a.warmup, use_graph)
-    barrier = (dist.barrier if a.comm != "torch" else (lambda: dist.barrier(device_ids=[local]))) \
-        if world > 1 else None
+    barrier = _timing_barrier(comm, local) if world > 1 else None
     if barrier:
         barrier()
     torch.cuda.synchronize()
