@@ -7,6 +7,7 @@
 namespace py = pybind11;
 
 namespace dtfx {
+void gemm_bf16_set_cfg(int);
 void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const void*, int, void*,
                       int, float, float, const float*, int, const void*, void*, int, const void*,
                       int, int, int, int, long long, long long, long long,
@@ -60,6 +61,9 @@ static inline T* P(uintptr_t a) { return reinterpret_cast<T*>(a); }
 static inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 void register_nn(py::module_& m) {
+  m.def("gemm_bf16_set_cfg", &dtfx::gemm_bf16_set_cfg,
+        "force the bf16 GEMM tile configuration (-1 = auto; 0: 128x128, 3: 256x256 2-stage, "
+        "5: 256x256 8-phase)");
   m.def("gemm_bf16", [](bool ta, bool tb, bool out_f32, int M, int N, int K, uintptr_t A, int lda,
                         uintptr_t B, int ldb, uintptr_t C, int ldc, float alpha, float beta,
                         uintptr_t bias, int act, uintptr_t aux_in, uintptr_t aux_out, int ld_aux,

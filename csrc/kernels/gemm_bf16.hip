@@ -30,7 +30,7 @@
 // operand:
 //   k-contiguous operand  -> [128 rows][64 k]  128-B rows, fragments by
 //                            ds_read_b128, 16-B chunk c of row r stored at
-//                            chunk c ^ (r & 7)
+//                            chunk c ^ ((r >> 1) & 7)
 //   k-strided operand     -> [64 k][128 cols]  256-B rows, fragments by
 //                            two ds_read_b64_tr_b16 (hardware transpose),
 //                            chunk c of k-row r stored at c ^ swz_tr(r)
@@ -102,6 +102,12 @@ __device__ __forceinline__ void fdivmod(int a, int d, float inv, int& q, int& r)
 namespace gb {
 constexpr int BN = 128, BK = 64;  // tile N and K; the tile height BM is a template parameter
 
+// k-contiguous images (128-B rows, 8 chunks of 16 B): chunk c of row r is stored at
+// c ^ swz_kc(r).  A ds_read_b128 16-lane group reads 16 consecutive rows at one chunk; even
+// and odd rows sit on opposite 128-B halves of the 256-B bank row, so XOR-ing with r >> 1
+// (not r) spreads the 16 reads over all 16 slots (r & 7 left rows r and r + 8 on one slot:
+// 2-way conflicts).
+__device__ __forceinline__ int swz_kc(int r) { return (r >> 1) & 7; }
 __device__ __forceinline__ int swz_tr(int r) { return ((r & 3) | (((r >> 3) & 1) << 2)) << 1; }
 // 64-wide k-strided images (128-B rows: even rows on banks 0-31, odd rows on 32-63): a
 // ds_read_b64_tr_b16 half-wave reads rows {q, q+8} (q = 0..3) x 2 chunks; the XOR puts the 4
@@ -127,7 +133,7 @@ __device__ __forceinline__ void stage(const unsigned short* __restrict__ src, in
     const unsigned short* g;
     if (KCONT) {
       const int row = blk * 8 + (lane >> 3), cs = lane & 7;
-      const int c = cs ^ (row & 7);
+      const int c = cs ^ swz_kc(row);
       const int o = min(outer0 + row, outer_max);
       g = src + (size_t)o * ld + k0 + c * 8;
     } else {
@@ -147,7 +153,7 @@ __device__ __forceinline__ bf16x8 frag(const char* lds_tile, int o0, int kk, int
   if (KCONT) {
     const int row = o0 + (lane & 15);
     const int c = kk * 4 + (lane >> 4);
-    return *(const bf16x8*)(lds_tile + row * 128 + ((c ^ (row & 7)) << 4));
+    return *(const bf16x8*)(lds_tile + row * 128 + ((c ^ swz_kc(row)) << 4));
   } else {
     // ds_read_b64_tr_b16: 16-lane group g reads k rows kk*32+8g+{0..3} (+4 for the 2nd
     // read), cols o0..o0+15; lane 4q+p addresses row q, cols 4p..4p+3.
@@ -208,7 +214,7 @@ __device__ __forceinline__ void stage_a_conv(const ConvDesc& d, int mode, const 
   for (int i = 0; i < NBLK; ++i) {
     const int blk = i * NW + wave;
     const int row = blk * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ (row & 7);
+    const int c = (lane & 7) ^ swz_kc(row);
     const int k = k0 + c * 8;
     int tap, ch;
     if (uni) { tap = tap_u; ch = c_u + c * 8; }
@@ -419,7 +425,130 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
-  if (NBUF == 2) {
+  if constexpr (NBUF == 8) {
+    // 8-phase schedule (256x256 tile, BK = 64, 8 waves, 128 KB of LDS as 8 half-tile
+    // images of 16 KB: [buffer 0/1][A rows 0-127, A rows 128-255, B cols 0-127, B cols
+    // 128-255]).  A K tile is four phases, one per block quadrant (MQ, NQ) in the order
+    // (0,0) (1,0) (1,1) (0,1); in each quadrant wave (wm8, wn8) = (wave / 2, wave % 2) owns
+    // a 32 x 64 piece (2 x 4 MFMA tiles, K = 64: 16 MFMAs).  Fragments are kept across
+    // phases (A0 + B0 read in phase 1, A1 in 2, B1 in 3, A0 again in 4), so the half images
+    // retire one per phase and every phase restages ONE half image (2 LDS-DMA loads per
+    // thread); the schedule is listed at the loop.  Counted vmcnt (never 0 inside the loop
+    // while a next tile exists) and raw s_barrier everywhere: __syncthreads' fence would
+    // drain every DMA in flight.  One K tile per iteration with the buffer parity computed at
+    // run time: a two-tile body with literal buffers let hipcc hoist a per-lane LDS address
+    // for every buffer x half x fragment and spill ~100 VGPRs.
+    // (cdna_hip_programming.md §5 "The 256^2 8-phase template" and its glds rules.)
+    constexpr int HB = 16384;
+    const int wm8 = wave >> 1, wn8 = wave & 1;
+    auto hbuf = [&](int buf, int which) -> char* { return smem + (buf * 4 + which) * HB; };
+    // Staging through buffer loads with LDS destination: each lane's byte offset at k = 0 is
+    // computed ONCE (8 VGPRs for the 4 half images x 2 instructions); the K advance is the
+    // wave-uniform soffset.  (64-bit per-lane pointers for 8 staging sites spilled.)
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7fffffff, 0x00020000);
+    auto voff = [&](bool isA, int which, int i) -> int {
+      const bool kc = isA ? !TA : TB;
+      const int ld = isA ? lda : ldb, omax = isA ? a_max : b_max;
+      const int outer0 = isA ? m0 + which * 128 : n0 + (which - 2) * 128;
+      const int blk = i * NW + wave;
+      if (kc) {
+        const int row = blk * 8 + (lane >> 3), c = (lane & 7) ^ swz_kc(row);
+        return (min(outer0 + row, omax) * ld + c * 8) * 2;
+      }
+      const int kr = blk * 4 + (lane >> 4), c = (lane & 15) ^ swz_tr(kr);
+      return (kr * ld + min(outer0 + c * 8, omax)) * 2;
+    };
+    const int vo0_0 = voff(true, 0, 0), vo0_1 = voff(true, 0, 1);
+    const int vo1_0 = voff(true, 1, 0), vo1_1 = voff(true, 1, 1);
+    const int vo2_0 = voff(false, 2, 0), vo2_1 = voff(false, 2, 1);
+    const int vo3_0 = voff(false, 3, 0), vo3_1 = voff(false, 3, 1);
+#define DTFX_PH8_STAGE(BUF, WHICH, KT)                                                          \
+  do {                                                                                          \
+    const int k0_ = (kt0 + (KT)) * BK;                                                          \
+    const int so_ = (WHICH) < 2 ? (TA ? k0_ * lda * 2 : k0_ * 2) : (TB ? k0_ * 2 : k0_ * ldb * 2); \
+    char* d_ = hbuf((BUF), (WHICH));                                                            \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds((WHICH) < 2 ? rA : rB, (lds_void*)(d_ + wave * 1024), \
+                                             16, vo##WHICH##_0, so_, 0, 0);                     \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds((WHICH) < 2 ? rA : rB,                             \
+                                             (lds_void*)(d_ + (NW + wave) * 1024), 16,          \
+                                             vo##WHICH##_1, so_, 0, 0);                         \
+  } while (0)
+    bf16x8 af[2][2], bq[4][2];
+    auto loadA = [&](int buf, int mq) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) af[mi][kk] = frag<!TA, 128>(hbuf(buf, mq), wm8 * 32 + mi * 16, kk, lane);
+    };
+    auto loadB = [&](int buf, int nq) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bq[j][kk] = frag<TB, 128>(hbuf(buf, 2 + nq), wn8 * 64 + j * 16, kk, lane);
+    };
+#define DTFX_PH8_MMA(Q)                                                                         \
+  __builtin_amdgcn_s_barrier();                                                                 \
+  __builtin_amdgcn_sched_barrier(0);                                                            \
+  __builtin_amdgcn_s_setprio(1);                                                                \
+  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                              \
+  _Pragma("unroll") for (int mi = 0; mi < 2; ++mi)                                              \
+  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                 \
+    acc[(Q) * 2 + mi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][kk], bq[j][kk],       \
+                                                                   acc[(Q) * 2 + mi][j], 0, 0, 0); \
+  __builtin_amdgcn_s_setprio(0);                                                                \
+  __builtin_amdgcn_sched_barrier(0);                                                            \
+  __builtin_amdgcn_s_barrier();                                                                 \
+  __builtin_amdgcn_sched_barrier(0);
+    // Waves 4-7 (the second wave of every SIMD) run one barrier behind waves 0-3, so on each
+    // SIMD one wave issues its 16 MFMAs while the other reads fragments / issues its staging
+    // (cdna_hip_programming.md: the template's `if (wr == 1) s_barrier`).  With the groups a
+    // barrier apart a half image is restaged TWO phases after its last read (WAR), and read
+    // at least one phase after the vmcnt that retires it (RAW).
+    //   iteration kt (buffer b = kt & 1):
+    //     phase 1 (0,0): read A0 B0   stage B1 of tile kt+1 -> b^1 (B1 of b^1 last read kt-1 ph3)
+    //     phase 2 (1,0): read A1      stage A0 of tile kt+1 -> b^1 (read kt-1 ph4)
+    //     phase 3 (1,1): read B1      stage B0 of tile kt+2 -> b   (read ph1)
+    //     phase 4 (0,1): read A0      stage A1 of tile kt+2 -> b   (read ph2)
+    //   vmcnt(4) in phase 4 retires tile kt+1 (its last half, A0, went out in phase 2).
+    const bool late = wave >= NW / 2;
+    // prologue: tile 0 -> buffer 0; tile 1's B0 and A1 halves -> buffer 1
+    if (nk > 0) {
+      DTFX_PH8_STAGE(0, 2, 0); DTFX_PH8_STAGE(0, 1, 0); DTFX_PH8_STAGE(0, 3, 0); DTFX_PH8_STAGE(0, 0, 0);
+    }
+    if (nk > 1) {
+      DTFX_PH8_STAGE(1, 2, 1); DTFX_PH8_STAGE(1, 1, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (late) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int b = kt & 1;
+      const bool has1 = kt + 1 < nk, has2 = kt + 2 < nk;
+      loadA(b, 0); loadB(b, 0);                       // phase 1: quadrant (0,0)
+      if (has1) DTFX_PH8_STAGE(b ^ 1, 3, kt + 1);
+      DTFX_PH8_MMA(0)
+      loadA(b, 1);                                    // phase 2: (1,0), B0 kept
+      if (has1) DTFX_PH8_STAGE(b ^ 1, 0, kt + 1);
+      DTFX_PH8_MMA(2)
+      loadB(b, 1);                                    // phase 3: (1,1), A1 kept
+      if (has2) DTFX_PH8_STAGE(b, 2, kt + 2);
+      DTFX_PH8_MMA(3)
+      loadA(b, 0);                                    // phase 4: (0,1), B1 kept
+      if (has2) DTFX_PH8_STAGE(b, 1, kt + 2);
+      if (has2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      DTFX_PH8_MMA(1)
+    }
+    if (!late) __builtin_amdgcn_s_barrier();  // the early group's share of the offset
+    __builtin_amdgcn_sched_barrier(0);
+#undef DTFX_PH8_MMA
+#undef DTFX_PH8_STAGE
+  } else if (NBUF == 2) {
     if (nk > 0) stage_all(0, 0);
     __syncthreads();  // emits vmcnt(0): tile 0 landed for every wave
     for (int kt = 0; kt < nk; ++kt) {
@@ -470,7 +599,43 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
       brs[u] = n + u < N ? e.bn_rstd[n + u] : 0.f;
     }
   }
+  // Rows / columns of the wave's h-th 32 x 64 output slab: 8-phase layout (one slab per block
+  // quadrant) or a contiguous WM x 64 wave tile.
+  auto slab_r0 = [&](int h) { return NBUF == 8 ? (h >> 1) * 128 + (wave >> 1) * 32 : wm * WM + h * 32; };
+  auto slab_c0 = [&](int h) { return NBUF == 8 ? (h & 1) * 128 + (wave & 1) * 64 : wn * 64; };
+  auto flush_cols = [&](int c0) {
+    // lanes l, l^8, ..., l^56 hold the same 8 columns for different rows
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      cs[u] += __shfl_xor(cs[u], 8);
+      cs[u] += __shfl_xor(cs[u], 16);
+      cs[u] += __shfl_xor(cs[u], 32);
+      cq[u] += __shfl_xor(cq[u], 8);
+      cq[u] += __shfl_xor(cq[u], 16);
+      cq[u] += __shfl_xor(cq[u], 32);
+    }
+    const int n = n0 + c0 + (lane & 7) * 8;
+    if (e.col_partial) {
+      // one partial row per 64-row wave slab (launchers use WM == 64 for partial stats)
+      const size_t prow = (size_t)(m0 / 64 + wm) * N;
+      if (lane < 8 && m0 + wm * 64 < M)
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (n + u < N) {
+            if (e.colsum) e.colsum[prow + n + u] = cs[u];
+            if (e.colsq) e.colsq[prow + n + u] = cq[u];
+          }
+    } else if (lane < 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (n + u < N) {
+          if (e.colsum) unsafeAtomicAdd(e.colsum + n + u, cs[u]);
+          if (e.colsq) unsafeAtomicAdd(e.colsq + n + u, cq[u]);
+        }
+    }
+  };
   for (int h = 0; h < WM / 32; ++h) {
+    const int r0 = slab_r0(h), c0 = slab_c0(h);
     // (issued before the slab's LDS transpose, so their latency overlaps it)
     // Side inputs (aux_in / residual) of the slab's 4 row groups are all
     // loaded before any is used: one memory round trip per 32-row slab instead of one per
@@ -481,8 +646,8 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
-      mm[it] = m0 + wm * WM + h * 32 + rr;
-      nn[it] = n0 + wn * 64 + cg;
+      mm[it] = m0 + r0 + rr;
+      nn[it] = n0 + c0 + cg;
       live[it] = mm[it] < M && nn[it] < N;
       full[it] = live[it] && nn[it] + 8 <= N;  // N % 8 != 0 only with a ragged last group
       const int ms = live[it] ? mm[it] : 0, ns = full[it] ? nn[it] : 0;
@@ -505,9 +670,9 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
     if (OUT_F32 && gridDim.y > 1) {
       // split-K partial: alpha only; hardware f32 atomics, one 256-B row segment per
       // wave instruction (lane = column) so each instruction is 4 full 64-B requests
-      const int n = n0 + wn * 64 + lane;
+      const int n = n0 + c0 + lane;
       for (int rr = 0; rr < 32; ++rr) {
-        const int m = m0 + wm * WM + h * 32 + rr;
+        const int m = m0 + r0 + rr;
         if (m < M && n < N)
           unsafeAtomicAdd((float*)Cv + (size_t)m * ldc + n, e.alpha * ep[rr * EP_LD + lane]);
       }
@@ -633,37 +798,52 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
       }
     }
     __builtin_amdgcn_wave_barrier();
-  }
-  if (e.colsum || e.colsq) {
-    // lanes l, l^8, ..., l^56 hold the same 8 columns for different rows
+    if (NBUF == 8 && (e.colsum || e.colsq)) {
+      // the next slab covers other columns: park this slab's column sums in LDS (beyond the
+      // per-wave transpose regions), reduced across the block below -- one atomic per column
+      // per block instead of one per slab and wave (8x fewer same-address atomics; the BERT
+      // FFN dgrad with its fused bias gradient ran 225 us with per-slab atomics)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      cs[u] += __shfl_xor(cs[u], 8);
-      cs[u] += __shfl_xor(cs[u], 16);
-      cs[u] += __shfl_xor(cs[u], 32);
-      cq[u] += __shfl_xor(cq[u], 8);
-      cq[u] += __shfl_xor(cq[u], 16);
-      cq[u] += __shfl_xor(cq[u], 32);
-    }
-    const int n = n0 + wn * 64 + (lane & 7) * 8;
-    if (e.col_partial) {
-      // one partial row per 64-row wave slab (launchers use WM == 64 for partial stats)
-      const size_t prow = (size_t)(m0 / 64 + wm) * N;
-      if (lane < 8 && m0 + wm * 64 < M)
+      for (int u = 0; u < 8; ++u) {
+        cs[u] += __shfl_xor(cs[u], 8);
+        cs[u] += __shfl_xor(cs[u], 16);
+        cs[u] += __shfl_xor(cs[u], 32);
+        cq[u] += __shfl_xor(cq[u], 8);
+        cq[u] += __shfl_xor(cq[u], 16);
+        cq[u] += __shfl_xor(cq[u], 32);
+      }
+      float* red = (float*)(smem + 98304);  // [colsum|colsq][Nq][wn8][wm8 * 2 + Mq][64]
+      const int slot = (((h & 1) * 2 + (wave & 1)) * 8 + (wave >> 1) * 2 + (h >> 1)) * 64;
+      if (lane < 8)
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (n + u < N) {
-            if (e.colsum) e.colsum[prow + n + u] = cs[u];
-            if (e.colsq) e.colsq[prow + n + u] = cq[u];
-          }
-    } else if (lane < 8) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (n + u < N) {
-          if (e.colsum) unsafeAtomicAdd(e.colsum + n + u, cs[u]);
-          if (e.colsq) unsafeAtomicAdd(e.colsq + n + u, cq[u]);
+        for (int u = 0; u < 8; ++u) {
+          red[slot + lane * 8 + u] = cs[u];
+          red[2048 + slot + lane * 8 + u] = cq[u];
         }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
     }
+  }
+  if constexpr (NBUF == 8) {
+    if (e.colsum || e.colsq) {
+      __syncthreads();
+      const float* red = (const float*)(smem + 98304);
+      if (threadIdx.x < 256) {
+        const int c = threadIdx.x, nq = c >> 7, w = (c >> 6) & 1, col = c & 63;
+        float a = 0.f, q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          a += red[((nq * 2 + w) * 8 + i) * 64 + col];
+          q += red[2048 + ((nq * 2 + w) * 8 + i) * 64 + col];
+        }
+        if (n0 + c < N) {
+          if (e.colsum) unsafeAtomicAdd(e.colsum + n0 + c, a);
+          if (e.colsq) unsafeAtomicAdd(e.colsq + n0 + c, q);
+        }
+      }
+    }
+  } else if (e.colsum || e.colsq) {
+    flush_cols(wn * 64);
   }
 }
 
@@ -671,33 +851,47 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
 // Launch-configuration choice.  cfg 0: 128x128 tile, 4 waves, 2 LDS stages (64 KB, 2 blocks
 // per CU); cfg 1: 256x128, 8 waves, 3 stages (144 KB, counted-vmcnt pipeline); cfg 2:
 // 256x128, 2 stages (96 KB); cfg 3 (plain GEMM only): 256x256, 8 waves of 128x64, 2 stages
-// (128 KB).  Auto: the largest tile that still yields >= 256 blocks (one full wave of the
-// 256 CUs).  DTFX_GEMM_CFG=0..3 forces one (benchmarks).
+// (128 KB); cfg 4 (convolutions): 256x64; cfg 5 (plain GEMM only): 256x256, 8-phase
+// schedule (128 KB) -- the default large tile.  Auto: by wave quantisation (choose_cfg).
+// DTFX_GEMM_CFG=0..5 or gemm_bf16_set_cfg() forces one (tests, benchmarks).
 // ---------------------------------------------------------------------------
+static int g_gemm_cfg = -2;  // -2: not read yet; -1: auto; 0..5 forced
 static int gemm_cfg_env() {
-  static int v = -2;
-  if (v == -2) {
+  if (g_gemm_cfg == -2) {
     const char* e = getenv("DTFX_GEMM_CFG");
-    v = e ? atoi(e) : -1;
+    g_gemm_cfg = e ? atoi(e) : -1;
   }
-  return v;
+  return g_gemm_cfg;
 }
+// Force a tile configuration (-1 = auto) for tests and A/B benchmarks in one process.
+void gemm_bf16_set_cfg(int cfg) { g_gemm_cfg = cfg; }
 
 static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
   const int f = gemm_cfg_env();
-  if (f >= 0 && f <= 4) return f;
+  if (f >= 0 && f <= 5) return (f == 5 && mode != 0) ? 0 : f;
   if (mode == 0) {  // the 256x256 tile halves L2 traffic when it still fills the chip
                     // (measured: 1.11 vs 0.92 PF at 8192^3); A^T operands stay on 128x128.
     // Wave quantisation decides between them: 256x256 runs 1 block/CU (256 slots),
     // 128x128 two (512 slots); 256x256 wins when its last wave is about as full as the
     // 128x128 grid's, allowing for its ~15% faster main loop (BERT QKV 16384x2304:
     // 576 blocks = 2.25 waves, 86 us, vs 2304 / 512 = 4.5 waves on 128x128, 79 us).
+    // The 8-phase 256x256 schedule (cfg 5) replaced the 2-stage one (cfg 3): faster on every
+    // BERT forward / dgrad shape and on squares (tools/gemm_cfg_ab.py, interleaved rounds:
+    // ffn1 dgrad 16384x768x3072 939 vs 745 TFLOP/s, ffn2 fwd 1068 vs 917, 4096^3 1282 vs
+    // 1209), and still ahead of 128x128 with only 192 blocks (N = 768: 649-1068 vs 624-916)
+    // -- so no "fills the chip" floor any more, only the wave-quantisation comparison.
+    // A^T operands (weight gradients) stay on 128x128 + split-K (730 vs 689).
     const long long t3 = (long long)((M + 255) / 256) * ((N + 255) / 256) * zdim;
     const long long t0 = (long long)((M + 127) / 128) * ((N + 127) / 128) * zdim;
-    if (ta || t3 < 256) return 0;
+    if (ta) return 0;
+    static const int big = [] {  // DTFX_GEMM_BIG=3: the previous 2-stage large tile (A/B runs)
+      const char* e = getenv("DTFX_GEMM_BIG");
+      return e && atoi(e) == 3 ? 3 : 5;
+    }();
+    if (big == 3 && t3 < 256) return 0;
     const double e3 = (double)t3 / (double)(((t3 + 255) / 256) * 256);
     const double e0 = (double)t0 / (double)(((t0 + 511) / 512) * 512);
-    return e3 * 1.15 >= e0 ? 3 : 0;
+    return e3 * 1.15 >= e0 ? big : 0;
   }
   // convolutions (ResNet-50 end to end: 6881 img/s on 128x128 vs 6411-6416 on 256x128);
   // a forward conv with <= 64 output channels, or a dgrad with <= 64 input channels, takes
@@ -711,7 +905,8 @@ static void launch_one(dim3 grid_yz, int M, int N, int K, const unsigned short* 
                        const unsigned short* B, int ldb, void* C, int ldc, const GemmEpi& e,
                        long long sA, long long sB, long long sC, const ConvDesc& d,
                        hipStream_t stream) {
-  constexpr size_t lds = (size_t)NBUF * (BM_ * gb::BK * 2 + BN_ * gb::BK * 2);
+  constexpr size_t lds = NBUF == 8 ? (size_t)131072  // 8 half-tile images of 16 KB
+                                   : (size_t)NBUF * (BM_ * gb::BK * 2 + BN_ * gb::BK * 2);
   constexpr int threads = (BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64;
   static bool attr = false;
   if (!attr) {
@@ -733,6 +928,11 @@ static void launch_cfg(int cfg, dim3 grid_yz, int M, int N, int K, const unsigne
                        long long sA, long long sB, long long sC, const ConvDesc& d,
                        hipStream_t stream) {
   if constexpr (MODE == 0) {
+    if (cfg == 5) {
+      launch_one<MODE, TA, TB, F, 256, 8, 256>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
+                                               d, stream);
+      return;
+    }
     if (cfg == 3) {
       launch_one<MODE, TA, TB, F, 256, 2, 256>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
                                                d, stream);
@@ -781,7 +981,7 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   const int nkt = K / gb::BK;
   const bool auto_split = splitk <= 0;
   const int cfg = choose_cfg(M, N, batch * (auto_split ? 1 : splitk), 0, ta);
-  const int bm = cfg == 0 ? 128 : 256, bn = cfg == 3 ? 256 : 128;
+  const int bm = cfg == 0 ? 128 : 256, bn = (cfg == 3 || cfg == 5) ? 256 : 128;
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   if (auto_split) {  // fill the 256 CUs when the output has few tiles and K is deep
     splitk = 1;

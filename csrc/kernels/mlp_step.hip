@@ -1228,13 +1228,14 @@ void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float 
     const float* xprev = pending ? x + (size_t)prev * xb : xcur;
     const float* po = bufs[cur];
     float* pn = bufs[cur ^ 1];
-    const float l = pending ? lr : 0.f;
+    const float l = pending ? lr : 0.f;  // (pending doubles as the kernel's "apply / record
+                                         //  the previous step" flag, as in step_pipelined)
     if (rt7)
       hipLaunchKernelGGL((mlp_fwdapply_kernel<7>), dim3(HT * KS2 + HT), dim3(256), 0, stream, po,
-                         pn, l, xprev, xcur, w, ctr, stats, stats_ring, B, 1, MlpXg{});
+                         pn, l, xprev, xcur, w, ctr, stats, stats_ring, B, pending, MlpXg{});
     else
       hipLaunchKernelGGL((mlp_fwdapply_kernel<0>), dim3(HT * KS2 + HT), dim3(256), 0, stream, po,
-                         pn, l, xprev, xcur, w, ctr, stats, stats_ring, B, 1, MlpXg{});
+                         pn, l, xprev, xcur, w, ctr, stats, stats_ring, B, pending, MlpXg{});
     hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS2>), dim3(B), dim3(64), 0, stream, pn,
                        pn, 0.f, nullptr, labels + (size_t)pos * B, w, B, nullptr, MlpXg{},
                        nullptr);

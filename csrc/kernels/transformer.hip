@@ -408,23 +408,23 @@ constexpr int PB = SP * LDP;       // 34816 B
 // Load N [S][64] head slices (row stride ld[i] elements) into LDS, zero rows >= S.  All
 // 4N 16-B loads of a thread are issued before the first LDS store (one memory round trip
 // instead of 4N dependent load -> store pairs).
-template <int N>
+template <int N, int NT = 256>
 __device__ __forceinline__ void load_heads(char* const (&dst)[N], const unsigned short* const (&src)[N],
                                            const int (&ld)[N], int S) {
-  constexpr int PER = SP * 8 / 256;  // 16-B chunks per thread per head
+  constexpr int PER = SP * 8 / NT;  // 16-B chunks per thread per head (NT threads)
   bf16x8 v[N][PER];
 #pragma unroll
   for (int n = 0; n < N; ++n)
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const int i = threadIdx.x + 256 * k, r = i >> 3, c = i & 7;
+      const int i = threadIdx.x + NT * k, r = i >> 3, c = i & 7;
       v[n][k] = *(const bf16x8*)(src[n] + (size_t)min(r, S - 1) * ld[n] + c * 8);
     }
 #pragma unroll
   for (int n = 0; n < N; ++n)
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const int i = threadIdx.x + 256 * k, r = i >> 3, c = i & 7;
+      const int i = threadIdx.x + NT * k, r = i >> 3, c = i & 7;
       if (r >= S) v[n][k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       *(bf16x8*)(dst[n] + r * LDQ + c * 16) = v[n][k];
     }
@@ -535,12 +535,19 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   }
 }
 
-__global__ __launch_bounds__(256, 1) void attn_bwd_kernel(
+// NW waves per (sequence, head): 4 (32 query / key rows per wave) or 8 (16 rows per wave:
+// the 144 KB of LDS allow one block per CU, so 8 waves give every SIMD two waves to
+// overlap LDS / global latency with the other's MFMAs).
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 1) void attn_bwd_kernel(
     int S, int nh, const unsigned short* __restrict__ qkv, const unsigned short* __restrict__ o,
     const unsigned short* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ kmask, float scale, unsigned short* __restrict__ dqkv,
     float* __restrict__ dbias) {
   using namespace at;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int NT = NW * 64, RPW = SP / NW, NI = RPW / 16;  // rows per wave, 16-row tiles
+  constexpr int TPR = NT / SP, CPT = 64 / TPR / 8;           // rowsum: threads / row, chunks
   extern __shared__ __attribute__((aligned(16))) char sm[];
   char* Qs = sm;
   char* Ks = sm + QB;
@@ -557,16 +564,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(
     const unsigned short* const src[4] = {base, base + Hd, base + 2 * Hd,
                                           dout + (size_t)b * S * Hd + h * D};
     const int lds[4] = {ld, ld, ld, Hd};
-    at::load_heads<4>(dst, src, lds, S);
+    at::load_heads<4, NT>(dst, src, lds, S);
   }
-  {  // D = rowsum(dO * O): 2 threads per row, 32 columns each
-    const int r = threadIdx.x >> 1, half = threadIdx.x & 1;
+  {  // D = rowsum(dO * O): TPR threads per row, 64 / TPR columns each
+    const int r = threadIdx.x / TPR, part = threadIdx.x % TPR;
     float s = 0.f;
     if (r < S) {
-      const unsigned short* orow = o + ((size_t)b * S + r) * Hd + h * D + half * 32;
-      const unsigned short* drow = dout + ((size_t)b * S + r) * Hd + h * D + half * 32;
+      const unsigned short* orow = o + ((size_t)b * S + r) * Hd + h * D + part * (64 / TPR);
+      const unsigned short* drow = dout + ((size_t)b * S + r) * Hd + h * D + part * (64 / TPR);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
+      for (int c = 0; c < CPT; ++c) {
         float ov[8], dv[8];
         unpack8(*(const bf16x8*)(orow + c * 8), ov);
         unpack8(*(const bf16x8*)(drow + c * 8), dv);
@@ -574,8 +581,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(
         for (int u = 0; u < 8; ++u) s += ov[u] * dv[u];
       }
     }
-    s += __shfl_xor(s, 1);
-    if (half == 0) Dr[r] = s;
+#pragma unroll
+    for (int w = 1; w < TPR; w <<= 1) s += __shfl_xor(s, w);
+    if (part == 0) Dr[r] = s;
   }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -589,8 +597,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(
   }
   // P and dS for this wave's 32 query rows
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r0 = 32 * wave + 16 * i;
+  for (int i = 0; i < NI; ++i) {
+    const int r0 = RPW * wave + 16 * i;
     f32x4 s[8], dp[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[j] = dp[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -624,8 +632,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(
   unsigned short* dv = dq + 2 * Hd;
   // dV = P^T dO, dK = scale * dS^T Q  (this wave's 32 key rows), dQ = scale * dS K (query rows)
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int k0 = 32 * wave + 16 * i;
+  for (int i = 0; i < NI; ++i) {
+    const int k0 = RPW * wave + 16 * i;
     f32x4 av[4], ak[4], aq[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) av[j] = ak[j] = aq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -941,13 +949,26 @@ void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, cons
   const size_t lds = 4 * at::QB + 2 * at::PB + at::SP * 4;
   static bool attr = false;
   if (!attr) {
-    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_kernel,
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_kernel<4>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_kernel<8>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(Bn * nh), dim3(256), lds, s, S, nh,
-                     (const unsigned short*)qkv, (const unsigned short*)o,
-                     (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv, dbias);
+  static const int nw = [] {
+    const char* e = std::getenv("DTFX_ATTN_BWD_WAVES");
+    return e && std::atoi(e) == 4 ? 4 : 8;
+  }();
+  if (nw == 4)
+    hipLaunchKernelGGL(attn_bwd_kernel<4>, dim3(Bn * nh), dim3(256), lds, s, S, nh,
+                       (const unsigned short*)qkv, (const unsigned short*)o,
+                       (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv,
+                       dbias);
+  else
+    hipLaunchKernelGGL(attn_bwd_kernel<8>, dim3(Bn * nh), dim3(512), lds, s, S, nh,
+                       (const unsigned short*)qkv, (const unsigned short*)o,
+                       (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv,
+                       dbias);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

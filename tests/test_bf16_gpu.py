@@ -113,3 +113,53 @@ def test_bmm_strided(gpu, ta, tb):
     A = a.float().transpose(1, 2) if ta else a.float()
     B = b.float().transpose(1, 2) if tb else b.float()
     assert (y - 0.5 * torch.bmm(A, B)).abs().max().item() < 1e-4
+
+
+@pytest.fixture
+def cfg8(gpu):
+    """Force the 256x256 8-phase tile for the duration of a test (then back to auto)."""
+    from distributedtensorflowexample_amd.ops import hip
+
+    hip().gemm_bf16_set_cfg(5)
+    yield
+    hip().gemm_bf16_set_cfg(-1)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(512, 512, 64), (512, 256, 128), (256, 512, 192),
+                                   (296, 520, 320), (1000, 768, 1024), (8, 8, 64)])
+def test_gemm_8phase_exact_integers(cfg8, gpu, ta, tb, M, N, K):
+    """8-phase schedule (one, two, three and many K tiles; odd and even tile counts; ragged
+    edges): small-integer operands make every partial sum exact, so a mis-staged half
+    image, a wrong buffer parity or a read before its DMA landed shows as a mismatch."""
+    g = torch.Generator().manual_seed(M + N + K)
+    a = torch.randint(-3, 4, ((K, M) if ta else (M, K)), generator=g).to(gpu, torch.bfloat16)
+    b = torch.randint(-3, 4, ((N, K) if tb else (K, N)), generator=g).to(gpu, torch.bfloat16)
+    for _ in range(3):  # repeated: a race that lands late only sometimes
+        y = bf16.gemm(a, b, ta, tb, out_dtype=torch.float32)
+        assert torch.equal(y, _ref(a, b, ta, tb))
+
+
+def test_gemm_8phase_epilogues_and_splitk(cfg8, gpu):
+    M, N, K = 600, 512, 256
+    x = _rand(M, K, dev=gpu, seed=13)
+    w = _rand(N, K, dev=gpu, seed=14, scale=0.3)
+    bias = torch.randn(N, device=gpu)
+    res = _rand(M, N, dev=gpu, seed=15)
+    aux = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    y = bf16.gemm(x, w, False, True, bias=bias, act="gelu", aux_out=aux, residual=res,
+                  out_dtype=torch.float32)
+    u = x.float() @ w.float().t() + bias
+    assert torch.allclose(aux.float(), u, rtol=1e-2, atol=1e-2)
+    assert (y - (torch.nn.functional.gelu(u, approximate="tanh") + res.float())).abs().max() < 1e-3
+    # fused column sums (bias gradient) over the quadrant-distributed wave layout
+    cs = torch.zeros(N, device=gpu)
+    yb = bf16.gemm(x, w, False, True, colsum=cs)
+    assert (cs - yb.float().sum(0)).abs().max().item() < 2e-2 * M ** 0.5
+    # split-K weight gradient on the 8-phase tile
+    T = 4096
+    dy = _rand(T, 512, dev=gpu, seed=16)
+    xx = _rand(T, 256, dev=gpu, seed=17)
+    out = torch.zeros(512, 256, device=gpu)
+    bf16.gemm(dy, xx, True, False, out=out, splitk=4)
+    assert (out - dy.float().t() @ xx.float()).abs().max().item() < 1e-4 * T ** 0.5

@@ -1,0 +1,94 @@
+"""A/B of the bf16 GEMM tile configurations on the BERT-base training shapes and squares, in
+ONE process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24), random operands.
+
+    python tools/gemm_cfg_ab.py [--cfgs 0,3,5] [--rounds 5]
+
+Prints one JSON line per shape: TFLOP/s (median over rounds) per configuration plus
+hipBLASLt (torch.matmul) and the max error of config 5 against an f32 reference.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributedtensorflowexample_amd.ops import bf16, hip  # noqa: E402
+
+
+def timeit(fn, iters=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfgs", default="0,3,5")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--shapes", default="all")
+    a = ap.parse_args()
+    cfgs = [int(c) for c in a.cfgs.split(",")]
+    dev = torch.device("cuda:0")
+    T = 128 * 128
+    shapes = [  # (name, M, N, K, ta, tb, epilogue)
+        ("qkv_fwd", T, 2304, 768, False, True, None), ("out_fwd", T, 768, 768, False, True, None),
+        ("ffn1_fwd_gelu", T, 3072, 768, False, True, "gelu"),
+        ("ffn2_fwd", T, 768, 3072, False, True, None),
+        ("qkv_dgrad", T, 768, 2304, False, False, None), ("ffn1_dgrad", T, 768, 3072, False, False, None),
+        ("ffn2_dgrad_gelu", T, 3072, 768, False, False, "gelu_grad"),
+        ("ffn1_wgrad", 3072, 768, T, True, False, "f32"), ("qkv_wgrad", 2304, 768, T, True, False, "f32"),
+        ("sq4096", 4096, 4096, 4096, False, True, None), ("sq8192", 8192, 8192, 8192, False, True, None)]
+    if a.shapes != "all":
+        keep = a.shapes.split(",")
+        shapes = [s for s in shapes if s[0] in keep]
+    h = hip()
+    for name, M, N, K, ta, tb, epi in shapes:
+        x = (torch.rand(*((K, M) if ta else (M, K)), device=dev) * 2 - 1).to(torch.bfloat16)
+        w = (torch.rand(*((N, K) if tb else (K, N)), device=dev) * 2 - 1).to(torch.bfloat16)
+        kw = {}
+        if epi == "f32":
+            out = torch.zeros(M, N, device=dev)
+            kw = dict(out=out, beta=1.0)
+        elif epi == "gelu":
+            kw = dict(bias=torch.zeros(N, device=dev), act="gelu",
+                      aux_out=torch.empty(M, N, device=dev, dtype=torch.bfloat16),
+                      out=torch.empty(M, N, device=dev, dtype=torch.bfloat16))
+        elif epi == "gelu_grad":
+            kw = dict(act_grad="gelu", aux_in=torch.zeros(M, N, device=dev, dtype=torch.bfloat16),
+                      out=torch.empty(M, N, device=dev, dtype=torch.bfloat16))
+        else:
+            kw = dict(out=torch.empty(M, N, device=dev, dtype=torch.bfloat16))
+        A = x.t() if ta else x
+        B = w.t() if tb else w
+        lib_out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        res = {c: [] for c in cfgs}
+        res["hipblaslt"] = []
+        for _ in range(a.rounds):
+            for c in cfgs:
+                h.gemm_bf16_set_cfg(c)
+                res[c].append(timeit(lambda: bf16.gemm(x, w, ta, tb, **kw)))
+            res["hipblaslt"].append(timeit(lambda: torch.matmul(A, B, out=lib_out)))
+        h.gemm_bf16_set_cfg(-1)
+        res["auto"] = [timeit(lambda: bf16.gemm(x, w, ta, tb, **kw)) for _ in range(a.rounds)]
+        fl = 2.0 * M * N * K
+        line = {"shape": name, "M": M, "N": N, "K": K}
+        for k, v in res.items():
+            line["tflops_%s" % k] = round(fl / sorted(v)[len(v) // 2] / 1e12, 1)
+        if 5 in cfgs and epi is None:
+            h.gemm_bf16_set_cfg(5)
+            y = bf16.gemm(x, w, ta, tb, out_dtype=torch.float32)
+            h.gemm_bf16_set_cfg(-1)
+            line["err5"] = float((y - A.float() @ B.float()).abs().max())
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
