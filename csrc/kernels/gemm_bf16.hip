@@ -355,7 +355,16 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
     bid = xcd_remap(blockIdx.x, tiles_n * tiles_m);
     split = 0;
   }
-  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+  int tm = bid / tiles_n, tn = bid % tiles_n;
+  if (NBUF == 8 && gridDim.y == 1) {
+    // grouped raster: an XCD's consecutive tile ids walk GM tile-rows column by column, so
+    // its ~32 resident blocks share 4 A and ~8 B panels in its L2 instead of 1 A and 32 B
+    const int GM = 4, group = GM * tiles_n, fm = (bid / group) * GM;
+    const int gm = min(tiles_m - fm, GM), r = bid % group;
+    tm = fm + r % gm;
+    tn = r / gm;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave / NWN, wn = wave % NWN;
 
