@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round evidence in one gpurun call: GPU tests, MLP bench (driver-size and long runs), BERT and
+# ResNet benches, rocprofv3 kernel stats of the MLP and BERT steps.  Stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd); OUT=$R/gpurun_out/ev; mkdir -p "$OUT"; export TMPDIR=/tmp
+step() { echo "== $1"; }
+step tests
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
+tail -1 "$OUT/pytest_gpu.log"
+step mlp
+timeout -k 10 120 python bench.py --steps 20 --warmup 5 > "$OUT/bench_mlp_k20.json" 2>&1 || exit 1
+timeout -k 10 200 python bench.py > "$OUT/bench_mlp.json" 2>&1 || exit 1
+tail -1 "$OUT/bench_mlp_k20.json" | cut -c 1-160; tail -1 "$OUT/bench_mlp.json" | cut -c 1-160
+step bert
+timeout -k 10 200 python bench.py --model bert > "$OUT/bench_bert.json" 2>&1 || exit 1
+timeout -k 10 200 python bench.py --model bert --bert_batch 32 --seq_len 512 > "$OUT/bench_bert512.json" 2>&1 || exit 1
+tail -1 "$OUT/bench_bert.json" | cut -c 1-180; tail -1 "$OUT/bench_bert512.json" | cut -c 1-180
+step resnet
+timeout -k 10 200 python bench.py --model resnet50 > "$OUT/bench_resnet.json" 2>&1 || exit 1
+tail -1 "$OUT/bench_resnet.json" | cut -c 1-180
+step prof
+cd /tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/mprof" -o run -- python "$R/bench.py" --steps 2000 --warmup 200 > "$OUT/mprof.log" 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bprof" -o run -- python "$R/bench.py" --model bert --steps 6 --warmup 3 > "$OUT/bprof.log" 2>&1 || exit 1
+python "$R/tools/prof_summary.py" "$OUT/mprof/run_kernel_stats.csv" > "$OUT/mlp_kernel_stats.txt"
+python "$R/tools/prof_summary.py" "$OUT/bprof/run_kernel_stats.csv" > "$OUT/bert_kernel_stats.txt"
+python "$R/tools/trace_by_shape.py" "$OUT/bprof/run_kernel_trace.csv" 40 > "$OUT/bert_kernel_shapes.txt"
+rm -f "$OUT"/mprof/*trace.csv
+head -4 "$OUT/mlp_kernel_stats.txt"; head -12 "$OUT/bert_kernel_shapes.txt"

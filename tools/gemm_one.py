@@ -12,8 +12,9 @@ ta, tb = (sys.argv[4] == "1", sys.argv[5] == "1") if len(sys.argv) > 5 else (Fal
 dev = torch.device("cuda:0")
 a = torch.randn(*((K, M) if ta else (M, K)), device=dev).to(torch.bfloat16)
 b = torch.randn(*((N, K) if tb else (K, N)), device=dev).to(torch.bfloat16)
-out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+# weight gradients (A^T) accumulate into f32 gradient buffers, as in training (split-K path)
+out = torch.zeros(M, N, device=dev, dtype=torch.float32 if ta else torch.bfloat16)
 for _ in range(5):
-    bf16.gemm(a, b, ta, tb, out=out)
+    bf16.gemm(a, b, ta, tb, out=out, beta=1.0 if ta else 0.0)
 torch.cuda.synchronize()
 print("done", M, N, K, ta, tb)
