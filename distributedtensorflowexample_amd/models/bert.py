@@ -299,10 +299,14 @@ class BertMLM:
         return B16.gemm(dqkv, p.W(pre + "attention/qkv/kernel"), residual=da)
 
     # ------------------------------------------------------------------ optimizer
-    def adam_step(self, lr, step, gscale=1.0, wd=0.01, step_ptr=None):
+    def adam_step(self, lr, step, gscale=1.0, wd=0.01, step_ptr=None, lo=0, hi=None):
+        """Fused AdamW over the flat range [lo, hi) (default: every parameter); ranges split
+        at bucket edges (ALIGN-aligned) give bit-identical results to one launch."""
         p = self.params
-        TR.adam_mixed(p.master, p.grad, p.m, p.v, p.bf, lr, step, wd=wd, gscale=gscale,
-                      step_ptr=step_ptr)
+        hi = p.numel if hi is None else hi
+        sl = slice(lo, hi)
+        TR.adam_mixed(p.master[sl], p.grad[sl], p.m[sl], p.v[sl], p.bf[sl], lr, step, wd=wd,
+                      gscale=gscale, step_ptr=step_ptr)
 
 
 def synthetic_mlm_batch(cfg: BertConfig, batch, seq, device, max_pred=None, seed=0, pad_to=64):

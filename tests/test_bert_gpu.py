@@ -65,3 +65,35 @@ def test_bert_fits_fixed_batch(gpu):
     tr.run(30, use_graph=True)
     l1, _ = tr.stats()
     assert l1 < 0.7 * l0, (l0, l1)
+
+
+def test_bert_dp_adam_waits_for_each_bucket_reduction(gpu):
+    """Sync-DP step ordering on the GPU: AdamW of the body buckets runs after THEIR
+    all-reduces (comm-stream event) and overlaps the embedding bucket's; AdamW of the
+    embeddings after the whole comm stream.  A fake 2-replica communicator makes every
+    reduction slow (a GPU spin) and adds 1.0 to each element, so a reduced gradient is
+    (g + 1) / 2 > 0 everywhere and the first Adam step moves EVERY parameter down by about
+    lr; an AdamW that ran before its bucket's reduction would see g / 2 and move about half
+    of them up."""
+    from distributedtensorflowexample_amd.train.bert_trainer import BertTrainer
+
+    class SlowPeer:
+        world_size, rank = 2, 0
+
+        def allreduce_sum_(self, t):
+            torch.cuda._sleep(2_000_000)  # ~1 ms on the comm stream
+            return t.add_(1.0)
+
+        def broadcast_(self, t, root=0):
+            return t
+
+    lr = 1e-3
+    tr = BertTrainer(BertConfig.tiny(), 4, 128, gpu, comm=SlowPeer(), lr=lr, weight_decay=0.0)
+    assert tr.comm_stream is not None
+    p0 = tr.model.params.master.clone()
+    tr.run(1, use_graph=False)
+    torch.cuda.synchronize()
+    d = tr.model.params.master - p0
+    split = tr.model.params.buckets[1][0]
+    for part in (d[split:], d[:split]):  # body (overlapped AdamW), embeddings (after the rest)
+        assert (part < -0.9 * lr).float().mean().item() > 0.999
