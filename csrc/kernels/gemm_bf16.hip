@@ -321,16 +321,18 @@ struct GemmEpi {
 // stacked along M, 2 blocks/CU -- no MFMA work on a 128-wide tile's dead half).  NBUF = LDS stages (2: next tile in flight during
 // compute; 3: two tiles in flight, counted vmcnt + raw barrier).
 template <int MODE, bool TA, bool TB, bool OUT_F32, int BM_, int NBUF, int BN_>
-__global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
+__global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
                              (BM_ == 128 || BN_ == 64) && NBUF == 2 ? 2 : 1) void gemm_bf16_kernel(
     int M, int N, int K, const unsigned short* __restrict__ A, int lda,
     const unsigned short* __restrict__ B, int ldb, void* __restrict__ Cv, int ldc, GemmEpi e,
     long long sA, long long sB, long long sC, ConvDesc cd) {
   using namespace gb;
   constexpr int BM = BM_, BN = BN_;
-  constexpr int WM = BN_ == 256 ? 128 : 64;        // wave tile WM x 64
-  constexpr int NWN = BN / 64, NW = (BM / WM) * NWN;
+  // wave tile WM x 64 (8-phase: 4 pieces of 32 x SW, one per block quadrant, 8 waves)
+  constexpr int WM = (BN_ == 256 || NBUF == 8) ? 128 : 64;
+  constexpr int NWN = NBUF == 8 ? 4 : BN / 64, NW = NBUF == 8 ? 8 : (BM / WM) * NWN;
   constexpr int TM = WM / 16;                      // 16-row MFMA tiles per wave
+  constexpr int NQN = BN / 2, SW = NQN / 2;        // 8-phase: B half width, wave slab width
   static_assert(BN_ == 128 || MODE == 0 || MODE == 1 || (MODE == 2 && BN_ == 64),
                 "gathered B operands need BN = 128 (dgrad: or 64)");
   constexpr int TILE_A = BM * BK * 2, TILE_B = BN * BK * 2, BUF_BYTES = TILE_A + TILE_B;
@@ -459,7 +461,9 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
     auto voff = [&](bool isA, int which, int i) -> int {
       const bool kc = isA ? !TA : TB;
       const int ld = isA ? lda : ldb, omax = isA ? a_max : b_max;
-      const int outer0 = isA ? m0 + which * 128 : n0 + (which - 2) * 128;
+      // B halves start NQN apart (BN = 192: 96-column halves staged as 128-column images,
+      // the last 32 columns loaded but never read)
+      const int outer0 = isA ? m0 + which * 128 : n0 + (which - 2) * NQN;
       const int blk = i * NW + wave;
       if (kc) {
         const int row = blk * 8 + (lane >> 3), c = (lane & 7) ^ swz_kc(row);
@@ -494,7 +498,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bq[j][kk] = frag<TB, 128>(hbuf(buf, 2 + nq), wn8 * 64 + j * 16, kk, lane);
+        for (int j = 0; j < SW / 16; ++j) bq[j][kk] = frag<TB, 128>(hbuf(buf, 2 + nq), wn8 * SW + j * 16, kk, lane);
     };
 #define DTFX_PH8_MMA(Q)                                                                         \
   __builtin_amdgcn_s_barrier();                                                                 \
@@ -502,7 +506,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
   __builtin_amdgcn_s_setprio(1);                                                                \
   _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                              \
   _Pragma("unroll") for (int mi = 0; mi < 2; ++mi)                                              \
-  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                 \
+  _Pragma("unroll") for (int j = 0; j < SW / 16; ++j)                                           \
     acc[(Q) * 2 + mi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][kk], bq[j][kk],       \
                                                                    acc[(Q) * 2 + mi][j], 0, 0, 0); \
   __builtin_amdgcn_s_setprio(0);                                                                \
@@ -611,7 +615,8 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
   // Rows / columns of the wave's h-th 32 x 64 output slab: 8-phase layout (one slab per block
   // quadrant) or a contiguous WM x 64 wave tile.
   auto slab_r0 = [&](int h) { return NBUF == 8 ? (h >> 1) * 128 + (wave >> 1) * 32 : wm * WM + h * 32; };
-  auto slab_c0 = [&](int h) { return NBUF == 8 ? (h & 1) * 128 + (wave & 1) * 64 : wn * 64; };
+  auto slab_c0 = [&](int h) { return NBUF == 8 ? (h & 1) * NQN + (wave & 1) * SW : wn * 64; };
+  constexpr int SLW = NBUF == 8 ? SW : 64;  // slab width (columns)
   auto flush_cols = [&](int c0) {
     // lanes l, l^8, ..., l^56 hold the same 8 columns for different rows
 #pragma unroll
@@ -657,7 +662,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
       const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
       mm[it] = m0 + r0 + rr;
       nn[it] = n0 + c0 + cg;
-      live[it] = mm[it] < M && nn[it] < N;
+      live[it] = mm[it] < M && nn[it] < N && cg < SLW;
       full[it] = live[it] && nn[it] + 8 <= N;  // N % 8 != 0 only with a ragged last group
       const int ms = live[it] ? mm[it] : 0, ns = full[it] ? nn[it] : 0;
       if (!OUT_F32) {  // (f32-output tiles load at use: the 256x256 f32 variant would spill)
@@ -671,7 +676,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
     for (int t = 0; t < TM; ++t)
       if ((t >> 1) == h)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < SLW / 16; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             ep[((t & 1) * 16 + row_l + r) * EP_LD + j * 16 + col_l] = acc[t][j][r];
@@ -682,7 +687,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
       const int n = n0 + c0 + lane;
       for (int rr = 0; rr < 32; ++rr) {
         const int m = m0 + r0 + rr;
-        if (m < M && n < N)
+        if (m < M && n < N && lane < SLW)
           unsafeAtomicAdd((float*)Cv + (size_t)m * ldc + n, e.alpha * ep[rr * EP_LD + lane]);
       }
       __builtin_amdgcn_wave_barrier();
@@ -823,7 +828,7 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
       }
       float* red = (float*)(smem + 98304);  // [colsum|colsq][Nq][wn8][wm8 * 2 + Mq][64]
       const int slot = (((h & 1) * 2 + (wave & 1)) * 8 + (wave >> 1) * 2 + (h >> 1)) * 64;
-      if (lane < 8)
+      if (lane < SLW / 8)
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           red[slot + lane * 8 + u] = cs[u];
@@ -837,8 +842,8 @@ __global__ __launch_bounds__((BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
     if (e.colsum || e.colsq) {
       __syncthreads();
       const float* red = (const float*)(smem + 98304);
-      if (threadIdx.x < 256) {
-        const int c = threadIdx.x, nq = c >> 7, w = (c >> 6) & 1, col = c & 63;
+      if (threadIdx.x < BN) {
+        const int c = threadIdx.x, nq = c / NQN, w = (c % NQN) / SW, col = c % SW;
         float a = 0.f, q = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -877,30 +882,44 @@ void gemm_bf16_set_cfg(int cfg) { g_gemm_cfg = cfg; }
 
 static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
   const int f = gemm_cfg_env();
-  if (f >= 0 && f <= 5) return (f == 5 && mode != 0) ? 0 : f;
-  if (mode == 0) {  // the 256x256 tile halves L2 traffic when it still fills the chip
-                    // (measured: 1.11 vs 0.92 PF at 8192^3); A^T operands stay on 128x128.
-    // Wave quantisation decides between them: 256x256 runs 1 block/CU (256 slots),
-    // 128x128 two (512 slots); 256x256 wins when its last wave is about as full as the
-    // 128x128 grid's, allowing for its ~15% faster main loop (BERT QKV 16384x2304:
-    // 576 blocks = 2.25 waves, 86 us, vs 2304 / 512 = 4.5 waves on 128x128, 79 us).
-    // The 8-phase 256x256 schedule (cfg 5) replaced the 2-stage one (cfg 3): faster on every
-    // BERT forward / dgrad shape and on squares (tools/gemm_cfg_ab.py, interleaved rounds:
-    // ffn1 dgrad 16384x768x3072 939 vs 745 TFLOP/s, ffn2 fwd 1068 vs 917, 4096^3 1282 vs
-    // 1209), and still ahead of 128x128 with only 192 blocks (N = 768: 649-1068 vs 624-916)
-    // -- so no "fills the chip" floor any more, only the wave-quantisation comparison.
-    // A^T operands (weight gradients) stay on 128x128 + split-K (730 vs 689).
-    const long long t3 = (long long)((M + 255) / 256) * ((N + 255) / 256) * zdim;
-    const long long t0 = (long long)((M + 127) / 128) * ((N + 127) / 128) * zdim;
+  if (f >= 0 && f <= 6) return (f >= 5 && mode != 0) ? 0 : f;
+  if (mode == 0) {
+    // The 8-phase schedules (cfg 5: 256x256, cfg 6: 256x192) replaced the 2-stage 256x256
+    // (cfg 3) on every BERT forward / dgrad shape and on squares (tools/gemm_cfg_ab.py,
+    // interleaved rounds: ffn1 dgrad 16384x768x3072 987 (cfg 6) / 915 (cfg 5) vs 745 (cfg 3)
+    // TFLOP/s, 4096^3 1303 vs 1209).  Choice by a time model calibrated on those shapes:
+    // waves x tile work / relative per-block efficiency, one block per CU for the 8-phase
+    // tiles, two for 128x128 (cfg 6: 0.75 of a 256x256 block's work at 0.81 of its efficiency
+    // -- the N = 768 GEMMs fill all 256 CUs instead of 192; cfg 0: 0.25 at 0.47).
+    // A^T operands (weight gradients) stay on 128x128 + split-K (760 vs 705 TFLOP/s).
     if (ta) return 0;
     static const int big = [] {  // DTFX_GEMM_BIG=3: the previous 2-stage large tile (A/B runs)
       const char* e = getenv("DTFX_GEMM_BIG");
       return e && atoi(e) == 3 ? 3 : 5;
     }();
-    if (big == 3 && t3 < 256) return 0;
-    const double e3 = (double)t3 / (double)(((t3 + 255) / 256) * 256);
-    const double e0 = (double)t0 / (double)(((t0 + 511) / 512) * 512);
-    return e3 * 1.15 >= e0 ? big : 0;
+    const long long t3 = (long long)((M + 255) / 256) * ((N + 255) / 256) * zdim;
+    const long long t6 = (long long)((M + 255) / 256) * ((N + 191) / 192) * zdim;
+    const long long t0 = (long long)((M + 127) / 128) * ((N + 127) / 128) * zdim;
+    if (big == 3) {
+      if (t3 < 256) return 0;
+      const double e3 = (double)t3 / (double)(((t3 + 255) / 256) * 256);
+      const double e0 = (double)t0 / (double)(((t0 + 511) / 512) * 512);
+      return e3 * 1.15 >= e0 ? 3 : 0;
+    }
+    const double est5 = (double)((t3 + 255) / 256);
+    const double est6 = (double)((t6 + 255) / 256) * 0.75 / 0.81;
+    const double est0 = (double)((t0 + 511) / 512) * 0.25 / 0.47;
+    // cfg 6 is opt-in (DTFX_GEMM_TILE192=1): alone it is 6-8 % faster on the N = 768
+    // GEMMs, but in the BERT step those run beside the weight-gradient kernels on a second
+    // stream, which use the 64 CUs a 192-block 256x256 grid leaves free (BERT-base, same box,
+    // two rounds: 7928 / 7890 seq/s with cfg 5 vs 7697 / 7639 with cfg 6; without the second
+    // stream both ~7840 -- scripts/gpu_bert_ab.sh)
+    static const bool use6 = [] {
+      const char* e = getenv("DTFX_GEMM_TILE192");
+      return e && atoi(e) == 1;
+    }();
+    if (use6 && est6 < est5 && est6 < est0 && N > 128) return 6;
+    return est5 <= est0 ? 5 : 0;
   }
   // convolutions (ResNet-50 end to end: 6881 img/s on 128x128 vs 6411-6416 on 256x128);
   // a forward conv with <= 64 output channels, or a dgrad with <= 64 input channels, takes
@@ -916,7 +935,7 @@ static void launch_one(dim3 grid_yz, int M, int N, int K, const unsigned short* 
                        hipStream_t stream) {
   constexpr size_t lds = NBUF == 8 ? (size_t)131072  // 8 half-tile images of 16 KB
                                    : (size_t)NBUF * (BM_ * gb::BK * 2 + BN_ * gb::BK * 2);
-  constexpr int threads = (BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64;
+  constexpr int threads = NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64;
   static bool attr = false;
   if (!attr) {
     DTFX_HIP_CHECK(hipFuncSetAttribute(
@@ -939,6 +958,11 @@ static void launch_cfg(int cfg, dim3 grid_yz, int M, int N, int K, const unsigne
   if constexpr (MODE == 0) {
     if (cfg == 5) {
       launch_one<MODE, TA, TB, F, 256, 8, 256>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
+                                               d, stream);
+      return;
+    }
+    if (cfg == 6) {
+      launch_one<MODE, TA, TB, F, 256, 8, 192>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
                                                d, stream);
       return;
     }
@@ -990,7 +1014,7 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   const int nkt = K / gb::BK;
   const bool auto_split = splitk <= 0;
   const int cfg = choose_cfg(M, N, batch * (auto_split ? 1 : splitk), 0, ta);
-  const int bm = cfg == 0 ? 128 : 256, bn = (cfg == 3 || cfg == 5) ? 256 : 128;
+  const int bm = cfg == 0 ? 128 : 256, bn = (cfg == 3 || cfg == 5) ? 256 : cfg == 6 ? 192 : 128;
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   if (auto_split) {  // fill the 256 CUs when the output has few tiles and K is deep
     splitk = 1;

@@ -115,19 +115,20 @@ def test_bmm_strided(gpu, ta, tb):
     assert (y - 0.5 * torch.bmm(A, B)).abs().max().item() < 1e-4
 
 
-@pytest.fixture
-def cfg8(gpu):
-    """Force the 256x256 8-phase tile for the duration of a test (then back to auto)."""
+@pytest.fixture(params=[5, 6], ids=["256x256", "256x192"])
+def cfg8(gpu, request):
+    """Force an 8-phase tile (256x256 or 256x192) for the duration of a test (then auto)."""
     from distributedtensorflowexample_amd.ops import hip
 
-    hip().gemm_bf16_set_cfg(5)
-    yield
+    hip().gemm_bf16_set_cfg(request.param)
+    yield request.param
     hip().gemm_bf16_set_cfg(-1)
 
 
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(512, 512, 64), (512, 256, 128), (256, 512, 192),
-                                   (296, 520, 320), (1000, 768, 1024), (8, 8, 64)])
+                                   (296, 520, 320), (1000, 768, 1024), (8, 8, 64),
+                                   (512, 384, 128), (264, 200, 64)])
 def test_gemm_8phase_exact_integers(cfg8, gpu, ta, tb, M, N, K):
     """8-phase schedule (one, two, three and many K tiles; odd and even tile counts; ragged
     edges): small-integer operands make every partial sum exact, so a mis-staged half

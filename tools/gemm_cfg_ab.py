@@ -31,7 +31,7 @@ def timeit(fn, iters=10):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfgs", default="0,3,5")
+    ap.add_argument("--cfgs", default="0,5,6")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shapes", default="all")
     a = ap.parse_args()
@@ -82,11 +82,12 @@ def main():
         line = {"shape": name, "M": M, "N": N, "K": K}
         for k, v in res.items():
             line["tflops_%s" % k] = round(fl / sorted(v)[len(v) // 2] / 1e12, 1)
-        if 5 in cfgs and epi is None:
-            h.gemm_bf16_set_cfg(5)
-            y = bf16.gemm(x, w, ta, tb, out_dtype=torch.float32)
-            h.gemm_bf16_set_cfg(-1)
-            line["err5"] = float((y - A.float() @ B.float()).abs().max())
+        for c in (5, 6):
+            if c in cfgs and epi is None:
+                h.gemm_bf16_set_cfg(c)
+                y = bf16.gemm(x, w, ta, tb, out_dtype=torch.float32)
+                h.gemm_bf16_set_cfg(-1)
+                line["err%d" % c] = float((y - A.float() @ B.float()).abs().max())
         print(json.dumps(line), flush=True)
 
 
