@@ -264,6 +264,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss, acc = tr.stats()
+    identical = None
+    if world > 1:  # after the clock: the sync replicas must still be bit-identical
+        chk = tr.params.double().sum().reshape(1).cpu()
+        ref = chk.clone()
+        ref = ref if a.comm != "torch" else ref.to(dev)
+        dist.broadcast(ref, 0)
+        same = torch.tensor([1 if torch.equal(chk, ref.cpu()) else 0], dtype=torch.int32)
+        same = same if a.comm != "torch" else same.to(dev)
+        dist.all_reduce(same, op=dist.ReduceOp.MIN)
+        identical = bool(same.item())
     ms = elapsed * 1e3 / a.steps
     value = a.batch_size * world * a.steps / elapsed
     if rank == 0:
@@ -296,6 +306,7 @@ def main():
             "final_loss": round(loss, 5),
             "final_train_acc": round(acc, 4),
             "global_step": tr.global_step(),
+            "replicas_identical": identical,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()
