@@ -11,6 +11,14 @@
 //                  worker.py:32, 141)
 //   UNINIT      -> which of these are uninitialized     (report_uninitialized_
 //                  variables, the Supervisor ready_op, worker.py:112-113)
+//   SYNC_PUSH   -> synchronous replicas (TF's SyncReplicasOptimizer, the sync
+//                  alternative of the reference's async apply): gradients tagged
+//                  with the worker's local step are accumulated; stale ones
+//                  (local step behind the round) are dropped, as TF's
+//                  ConditionalAccumulator does; the R-th gradient of a round
+//                  applies the MEAN, advances the round (and global_step, on
+//                  the task that holds it) and releases every waiting pusher --
+//                  the token queue of SyncReplicasOptimizer.
 // Variables are placed round-robin over ps tasks by the client, like
 // tf.train.replica_device_setter(ps_tasks) (worker.py:24).
 //
@@ -28,8 +36,10 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -46,8 +56,9 @@ namespace {
 enum Op : uint8_t {
   OP_CREATE = 1, OP_LOOKUP = 2, OP_ASSIGN = 3, OP_PULL = 4, OP_PUSH_APPLY = 5,
   OP_FETCH_ADD = 6, OP_UNINIT = 7, OP_LIST = 8, OP_SHUTDOWN = 9, OP_PING = 10,
-  OP_STATS = 11
+  OP_STATS = 11, OP_SYNC_PUSH = 12
 };
+constexpr uint32_t kNoVar = 0xffffffffu;
 enum DType : uint8_t { DT_F32 = 0, DT_I64 = 1 };
 
 // ---------------------------------------------------------------- io helpers
@@ -169,6 +180,10 @@ class PSServer {
 
   void stop() {
     if (!running_.exchange(false)) return;
+    {
+      std::lock_guard<std::mutex> g(sync_mu_);  // release sync pushers blocked in a round
+      sync_cv_.notify_all();
+    }
     // the accept thread polls lfd_ (100 ms ticks): join it BEFORE closing the fd, so it
     // never reads a closed (and possibly reused) descriptor
     if (lfd_ >= 0) ::shutdown(lfd_, SHUT_RDWR);
@@ -204,6 +219,8 @@ class PSServer {
     d["pushes"] = pushes_.load();
     d["bytes_in"] = bytes_in_.load();
     d["bytes_out"] = bytes_out_.load();
+    d["sync_rounds"] = sync_rounds_.load();
+    d["sync_stale"] = sync_stale_.load();
     return d;
   }
 
@@ -386,9 +403,78 @@ class PSServer {
         }
         break;
       }
+      case OP_SYNC_PUSH: sync_push(r, w); break;
       case OP_SHUTDOWN: shutdown_req_ = true; break;
       default: throw std::runtime_error("ps: unknown op " + std::to_string(op));
     }
+  }
+
+  // SYNC_PUSH: lr f32 | R u32 | local_step i64 | step var id u32 (kNoVar: not on this task) |
+  // timeout_ms u32 | n u32 | n ids | n gradients.  Reply: round (global step) after the push
+  // i64 | applied-in-a-round u8 (0: dropped as stale).
+  void sync_push(Reader& r, Writer& w) {
+    const float lr = r.get<float>();
+    const uint32_t R = r.get<uint32_t>();
+    const int64_t local_step = r.get<int64_t>();
+    const uint32_t step_id = r.get<uint32_t>();
+    const uint32_t timeout_ms = r.get<uint32_t>();
+    const uint32_t n = r.get<uint32_t>();
+    if (R < 1) throw std::runtime_error("ps: replicas_to_aggregate must be >= 1");
+    std::vector<Var*> vs(n);
+    std::vector<uint32_t> ids(n);
+    for (uint32_t k = 0; k < n; ++k) vs[k] = var(ids[k] = r.get<uint32_t>());
+    Var* stepv = step_id == kNoVar ? nullptr : var(step_id);
+    std::unique_lock<std::mutex> lk(sync_mu_);
+    if (sync_gen_ < 0 || (sync_count_ == 0 && local_step > sync_gen_))
+      sync_gen_ = local_step;  // first round of a (fresh or restored) job: adopt its step
+    if (local_step < sync_gen_) {  // stale: its round was applied without it
+      ++sync_stale_;
+      w.put<int64_t>(sync_gen_);
+      w.put<uint8_t>(0);
+      return;
+    }
+    if (local_step > sync_gen_)
+      throw std::runtime_error("ps: sync push from step " + std::to_string(local_step) +
+                               " while round " + std::to_string(sync_gen_) + " is open");
+    for (uint32_t k = 0; k < n; ++k) {
+      Var* v = vs[k];
+      if (v->dtype != DT_F32) throw std::runtime_error("ps: sync push to a non-float variable");
+      const char* g = r.take(v->nbytes());
+      std::vector<float>& a = sync_acc_[ids[k]];
+      if (a.size() != v->count) a.assign(v->count, 0.f);
+      for (size_t i = 0; i < v->count; ++i) {
+        float gi;
+        std::memcpy(&gi, g + 4 * i, 4);
+        a[i] += gi;
+      }
+    }
+    const int64_t round = sync_gen_;
+    if (++sync_count_ >= static_cast<int>(R)) {
+      // apply the mean of the round's R gradients (SyncReplicasOptimizer averages)
+      const float scale = lr / static_cast<float>(R);
+      for (auto& kv : sync_acc_) {
+        Var* v = var(kv.first);
+        std::lock_guard<std::mutex> vl(v->mu);
+        float* p = v->f.data();
+        for (size_t i = 0; i < kv.second.size(); ++i) {
+          p[i] -= scale * kv.second[i];
+          kv.second[i] = 0.f;
+        }
+      }
+      sync_count_ = 0;
+      ++sync_gen_;
+      ++sync_rounds_;
+      if (stepv) stepv->i.store(sync_gen_);
+      sync_cv_.notify_all();
+    } else if (!sync_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms),
+                                  [&] { return sync_gen_ > round || !running_; })) {
+      throw std::runtime_error("ps: sync round " + std::to_string(round) + " timed out with " +
+                               std::to_string(sync_count_) + " of " + std::to_string(R) +
+                               " replicas");
+    }
+    if (sync_gen_ <= round) throw std::runtime_error("ps: server stopped during a sync round");
+    w.put<int64_t>(sync_gen_);
+    w.put<uint8_t>(1);
   }
 
   std::string host_;
@@ -402,6 +488,12 @@ class PSServer {
   std::vector<std::unique_ptr<Var>> vars_;
   std::map<std::string, uint32_t> by_name_;
   std::atomic<uint64_t> pulls_{0}, pushes_{0}, bytes_in_{0}, bytes_out_{0};
+  std::mutex sync_mu_;
+  std::condition_variable sync_cv_;
+  int64_t sync_gen_ = -1;
+  int sync_count_ = 0;
+  std::map<uint32_t, std::vector<float>> sync_acc_;
+  std::atomic<uint64_t> sync_rounds_{0}, sync_stale_{0};
 };
 
 // ---------------------------------------------------------------- client
@@ -522,6 +614,58 @@ class PSClient {
       }
     }
     if (!first_error.empty()) throw std::runtime_error(first_error);
+  }
+  // Synchronous-replicas push (see SYNC_PUSH): every task gets its variables' gradients; the
+  // task holding `step_handle` (global_step) advances it with each applied round.  Returns
+  // (round after the push -- the new global step --, applied (False: dropped as stale)).
+  py::tuple sync_push(std::vector<int64_t> hs, std::vector<uintptr_t> ptrs,
+                      std::vector<size_t> sizes, float lr, int replicas_to_aggregate,
+                      int64_t local_step, int64_t step_handle, double timeout_s) {
+    if (hs.size() != ptrs.size() || hs.size() != sizes.size())
+      throw std::runtime_error("ps sync_push: argument lengths differ");
+    if (replicas_to_aggregate < 1) throw std::runtime_error("ps sync_push: replicas_to_aggregate < 1");
+    int64_t round = -1;
+    bool applied = true;
+    {
+      py::gil_scoped_release nogil;
+      std::lock_guard<std::mutex> lk(mu_);
+      std::vector<std::vector<size_t>> per(fds_.size());
+      for (size_t k = 0; k < hs.size(); ++k) per[task_of(hs[k])].push_back(k);
+      const size_t step_task = task_of(step_handle);
+      const uint32_t tmo = static_cast<uint32_t>(std::min(timeout_s, 4.0e6) * 1000.0);
+      std::vector<bool> sent(fds_.size(), false);
+      for (size_t t = 0; t < per.size(); ++t) {
+        if (per[t].empty() && t != step_task) continue;
+        Writer w;
+        w.put<uint8_t>(OP_SYNC_PUSH);
+        w.put<float>(lr);
+        w.put<uint32_t>(static_cast<uint32_t>(replicas_to_aggregate));
+        w.put<int64_t>(local_step);
+        w.put<uint32_t>(t == step_task ? static_cast<uint32_t>(step_handle) : kNoVar);
+        w.put<uint32_t>(tmo);
+        w.put<uint32_t>(static_cast<uint32_t>(per[t].size()));
+        for (size_t k : per[t]) w.put<uint32_t>(static_cast<uint32_t>(hs[k]));
+        for (size_t k : per[t]) w.raw(reinterpret_cast<const void*>(ptrs[k]), sizes[k]);
+        send(static_cast<int>(t), w.b);
+        sent[t] = true;
+      }
+      std::string first_error;  // drain every task's reply first (see pull)
+      for (size_t t = 0; t < per.size(); ++t) {
+        if (!sent[t]) continue;
+        try {
+          std::string resp = recv(static_cast<int>(t));
+          Reader r{resp.data(), resp.data() + resp.size()};
+          const int64_t g = r.get<int64_t>();
+          const bool a = r.get<uint8_t>() != 0;
+          if (t == step_task || round < 0) round = g;
+          applied = applied && a;
+        } catch (const std::exception& e) {
+          if (first_error.empty()) first_error = e.what();
+        }
+      }
+      if (!first_error.empty()) throw std::runtime_error(first_error);
+    }
+    return py::make_tuple(round, applied);
   }
   int64_t fetch_add(int64_t h, int64_t delta) {
     Writer w;
@@ -664,6 +808,9 @@ void register_ps(py::module_& m) {
       .def("pull", &PSClient::pull)
       .def("push_apply", &PSClient::push_apply, py::arg("handles"), py::arg("ptrs"),
            py::arg("sizes"), py::arg("lr"), py::arg("use_locking") = false)
+      .def("sync_push", &PSClient::sync_push, py::arg("handles"), py::arg("ptrs"),
+           py::arg("sizes"), py::arg("lr"), py::arg("replicas_to_aggregate"),
+           py::arg("local_step"), py::arg("step_handle"), py::arg("timeout_s") = 600.0)
       .def("fetch_add", &PSClient::fetch_add)
       .def("uninitialized", &PSClient::uninitialized)
       .def("list_vars", &PSClient::list_vars)

@@ -193,6 +193,13 @@ def define_reference_flags(flag_values=FLAGS):
     DEFINE_string("dtype", "auto", "auto: fp32 for the MLP (reference dtype), bf16 for bert/resnet50",
                   fv)
     DEFINE_float("bucket_mb", 32.0, "All-reduce bucket size for generic DDP models (MiB)", fv)
+    DEFINE_boolean("sync_replicas", False,
+                   "ps_async strategy: aggregate each step's gradients over "
+                   "--replicas_to_aggregate workers on the ps before ONE apply "
+                   "(tf.train.SyncReplicasOptimizer); stale gradients are dropped", fv)
+    DEFINE_integer("replicas_to_aggregate", 0,
+                   "--sync_replicas: gradients averaged per step (0 = --num_workers; fewer "
+                   "than --num_workers makes the slowest workers backups)", fv)
     DEFINE_boolean("zero1", False, "Autograd sync-DP path: shard the optimizer update over the "
                    "replicas (ZeRO-1: reduce-scatter, owner update, all-gather)", fv)
     DEFINE_integer("check_replicas_every", 0,

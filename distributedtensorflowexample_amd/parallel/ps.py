@@ -12,7 +12,10 @@ gradients can be stale; updates are lock-free (``use_locking=False``).
 assigned round-robin over the ps tasks in creation order.
 :class:`PSVariableStore` owns the global variables through the native C++
 client (``csrc/host/ps.cpp``): create/lookup, init/assign, uninitialized
-report (the Supervisor's ready_op), pull, push-and-apply, fetch-add.
+report (the Supervisor's ready_op), pull, push-and-apply, fetch-add, and the
+synchronous-replicas push (:meth:`PSVariableStore.sync_push`, TF's
+``SyncReplicasOptimizer``: gradients of one step are averaged over
+``replicas_to_aggregate`` workers before ONE apply, stale ones dropped).
 """
 from __future__ import annotations
 
@@ -110,6 +113,26 @@ class PSVariableStore:
         self.client.push_apply([self.handles[n] for n in names], [g.data_ptr() for g in gs],
                                [g.numel() * 4 for g in gs], float(lr), bool(use_locking))
 
+    def sync_push(self, grads, lr, replicas_to_aggregate, local_step,
+                  step_name="global/global_step", timeout_s=600.0):
+        """Synchronous replicas (tf.train.SyncReplicasOptimizer): push this worker's
+        gradients of ``local_step``; the ps accumulates them per variable and, with the
+        ``replicas_to_aggregate``-th gradient of the round, applies ``var -= lr * mean`` and
+        advances ``global_step``.  Blocks until the round is applied (the token queue) and
+        returns ``(new_global_step, applied)``; ``applied`` is False when the gradient was
+        stale (its round closed without it -- backup workers, R < num_workers) and dropped,
+        as TF's ConditionalAccumulator drops it."""
+        names = list(grads)
+        gs = [grads[n] for n in names]
+        for g in gs:
+            if g.dtype != torch.float32 or g.device.type != "cpu" or not g.is_contiguous():
+                raise ValueError("sync_push needs contiguous f32 CPU tensors")
+        step, applied = self.client.sync_push(
+            [self.handles[n] for n in names], [g.data_ptr() for g in gs],
+            [g.numel() * 4 for g in gs], float(lr), int(replicas_to_aggregate), int(local_step),
+            self.handles[step_name], float(timeout_s))
+        return int(step), bool(applied)
+
     def fetch_add(self, name, delta=1):
         return int(self.client.fetch_add(self.handles[name], int(delta)))
 
@@ -126,3 +149,49 @@ class PSVariableStore:
 
     def close(self):
         self.client.close()
+
+
+class SyncReplicasOptimizer:
+    """``tf.train.SyncReplicasOptimizer(opt, replicas_to_aggregate, total_num_replicas)`` for
+    variables hosted on the ps (a :class:`PSVariableStore`).
+
+    ``apply_gradients([(grad, name), ...])`` pushes this worker's gradients for its local
+    step; the ps averages ``replicas_to_aggregate`` of them and applies ``var -= lr * mean``
+    once per step (the wrapped optimizer must be a ``GradientDescentOptimizer``: the apply
+    runs on the ps, like TF's ApplyGradientDescent colocated with the variables,
+    worker.py:75-79).  The call blocks until the step's round is applied -- the token queue
+    -- and returns the new global step, which becomes the next local step.  Gradients from a
+    worker whose step was already applied (a backup replica, ``replicas_to_aggregate <
+    total_num_replicas``) are dropped, as TF's accumulators drop stale gradients.
+    """
+
+    def __init__(self, opt, replicas_to_aggregate, total_num_replicas=None, store=None,
+                 step_name="global/global_step", timeout_s=600.0):
+        from ..optim import GradientDescentOptimizer
+
+        if not isinstance(opt, GradientDescentOptimizer):
+            raise TypeError("the ps applies plain SGD: wrap a GradientDescentOptimizer")
+        if store is None:
+            raise ValueError("SyncReplicasOptimizer needs the PSVariableStore of the variables")
+        self.opt, self.store = opt, store
+        self.replicas_to_aggregate = int(replicas_to_aggregate)
+        self.total_num_replicas = int(total_num_replicas or replicas_to_aggregate)
+        if self.replicas_to_aggregate < 1 or self.total_num_replicas < self.replicas_to_aggregate:
+            raise ValueError("need 1 <= replicas_to_aggregate <= total_num_replicas")
+        self.step_name, self.timeout_s = step_name, float(timeout_s)
+        self.local_step = None
+        self.dropped = 0
+
+    def compute_gradients(self, loss, var_list):
+        return self.opt.compute_gradients(loss, var_list)
+
+    def apply_gradients(self, grads_and_vars, global_step=None):
+        if self.local_step is None:
+            self.local_step = self.store.read_int(self.step_name)
+        grads = {name: g.detach().float().cpu().contiguous() for g, name in grads_and_vars}
+        step, applied = self.store.sync_push(grads, self.opt.learning_rate,
+                                             self.replicas_to_aggregate, self.local_step,
+                                             self.step_name, self.timeout_s)
+        self.dropped += 0 if applied else 1
+        self.local_step = step
+        return step

@@ -148,6 +148,8 @@ class Worker:
             self.store.create()
         else:
             self.store.lookup()
+        sync = bool(getattr(fl, "sync_replicas", False))
+        replicas = int(getattr(fl, "replicas_to_aggregate", 0) or 0) or int(fl.num_workers)
         log_every = int(getattr(fl, "log_every", 100))
         eval_every = int(getattr(fl, "eval_every", 10000))
         local_steps = 0
@@ -156,12 +158,20 @@ class Worker:
         with sv.managed_session(self.server.target):
             start_time = time.time()
             start_step = 0
+            # --sync_replicas (TF's SyncReplicasOptimizer): this worker's local step is the
+            # global step it read; each push joins that step's round on the ps, which applies
+            # the mean of replicas_to_aggregate gradients and advances global_step
+            local_step = self.store.read_int("global/global_step") if sync else 0
             while not sv.should_stop():
                 self.sync_op()
                 batch_x, batch_y = dataset.train.next_batch(self.batch_size)
                 grads, cost, acc = self.compute(batch_x, batch_y)
-                self.store.push_apply(grads, self.lr, bool(getattr(fl, "use_locking", False)))
-                step = self.store.fetch_add("global/global_step", 1)  # counter_op; old value
+                if sync:
+                    step = local_step
+                    local_step, _ = self.store.sync_push(grads, self.lr, replicas, local_step)
+                else:
+                    self.store.push_apply(grads, self.lr, bool(getattr(fl, "use_locking", False)))
+                    step = self.store.fetch_add("global/global_step", 1)  # counter_op; old value
                 self.summary_writer.add_scalars({"loss": cost, "accuracy": acc}, step)
                 history.append((step, cost, acc))
                 local_steps += 1

@@ -70,6 +70,27 @@ def test_async_ps_cluster_cpu(tmp_path):
     assert len(steps) == len(set(steps))
 
 
+def test_sync_replicas_ps_cluster_cpu(tmp_path):
+    """main.py --sync_replicas (tf.train.SyncReplicasOptimizer): 1 ps + 2 workers; every step
+    is ONE averaged apply, so global_step counts rounds (not pushes) and both workers log the
+    same steps."""
+    logdir = str(tmp_path / "sync")
+    base = _free_port_block(4)
+    rc = launch_ps(num_workers=2, num_gpus=1, num_ps=1, cpu=True, base_port=base,
+                   log_dir=str(tmp_path / "logs"), quiet=True, timeout=240,
+                   extra=["--training_steps", "200", "--log_every", "50", "--eval_every", "100",
+                          "--logdir", logdir, "--save_model_secs", "0.2", "--sync_replicas",
+                          "--learning_rate", "0.05"])
+    assert rc == {"worker0": 0, "worker1": 0}, rc
+    v = load_checkpoint(latest_checkpoint(logdir))  # the chief's periodic saves
+    assert 0 < int(v["global/global_step"]) <= 201  # rounds 0..200, one apply each
+    steps = []
+    for t in (0, 1):
+        log = open(str(tmp_path / "logs" / ("worker%d.log" % t))).read()
+        steps.append(re.findall(r"step: (\d+)", log))
+    assert steps[0] == steps[1] == ["50", "100", "150", "200"], steps
+
+
 def test_mirrored_two_ranks_gloo(tmp_path):
     logdir = str(tmp_path / "mir")
     rc = launch_mirrored(nproc=2, log_dir=str(tmp_path / "logs"), quiet=True, timeout=240,

@@ -214,3 +214,91 @@ def test_ps_sharding_two_tasks(h):
     finally:
         for s in servers:
             s.stop()
+
+
+def test_ps_sync_replicas_rounds(h):
+    """SYNC_PUSH (tf.train.SyncReplicasOptimizer semantics) over two ps tasks: 3 workers x 5
+    rounds with R = 3 -- each round applies the MEAN of the 3 gradients once and advances
+    global_step; a stale push (old local step) is dropped; an incomplete round times out."""
+    import torch
+
+    from distributedtensorflowexample_amd.parallel.ps import PSVariableStore
+
+    servers = [h.PSServer("127.0.0.1", 0) for _ in range(2)]
+    for s in servers:
+        s.start()
+    try:
+        addrs = ["127.0.0.1:%d" % s.port for s in servers]
+        specs = [("a", (64,), "float32"), ("b", (3,), "float32"),
+                 ("global/global_step", (), "int64")]
+        st0 = PSVariableStore(addrs, specs).create()
+        st0.assign({"a": np.zeros(64), "b": np.zeros(3), "global/global_step": 7})
+        results = {}
+
+        def worker(k):
+            st = PSVariableStore(addrs, specs).lookup()
+            step = st.read_int("global/global_step")
+            seq = []
+            for _ in range(5):
+                g = {"a": torch.full((64,), float(k + 1)), "b": torch.full((3,), 10.0 * (k + 1))}
+                step, applied = st.sync_push(g, 0.5, 3, step, timeout_s=30)
+                seq.append((step, applied))
+            results[k] = seq
+            st.close()
+
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(3)]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        for k in range(3):  # every worker saw rounds 8..12, all applied
+            assert results[k] == [(8 + i, True) for i in range(5)], results[k]
+        v = st0.read_all()
+        # mean gradient (1 + 2 + 3) / 3 = 2 per round for a, 20 for b: 5 rounds x 0.5 lr
+        assert torch.allclose(v["a"], torch.full((64,), -5.0))
+        assert torch.allclose(v["b"], torch.full((3,), -50.0))
+        assert int(v["global/global_step"]) == 12
+        assert sum(s.stats()["sync_rounds"] for s in servers) == 10  # 5 rounds on each task
+        # a push tagged with an old step is dropped, not applied
+        step, applied = st0.sync_push({"a": torch.ones(64), "b": torch.ones(3)}, 0.5, 3, 9)
+        assert (step, applied) == (12, False)
+        assert torch.allclose(st0.read_all()["a"], torch.full((64,), -5.0))
+        # a round that never completes fails after its timeout instead of hanging
+        with pytest.raises(RuntimeError, match="timed out"):
+            st0.sync_push({"a": torch.ones(64), "b": torch.ones(3)}, 0.5, 3, 12, timeout_s=0.3)
+        st0.close()
+    finally:
+        for s in servers:
+            s.stop()
+
+
+def test_sync_replicas_optimizer_api(h, ps):
+    """tf.train.SyncReplicasOptimizer-style wrapper: 2 replicas, R = 2, one averaged apply
+    per step; R = 1 of 2 makes the slower replica a backup whose gradient is dropped."""
+    import torch
+
+    from distributedtensorflowexample_amd.optim import GradientDescentOptimizer
+    from distributedtensorflowexample_amd.parallel.ps import PSVariableStore, SyncReplicasOptimizer
+
+    addr = ["127.0.0.1:%d" % ps.port]
+    specs = [("w", (8,), "float32"), ("global/global_step", (), "int64")]
+    st = PSVariableStore(addr, specs).create()
+    st.assign({"w": np.zeros(8), "global/global_step": 0})
+    with pytest.raises(TypeError):
+        SyncReplicasOptimizer(object(), 2, store=st)
+    out = {}
+
+    def replica(k, R):
+        s = PSVariableStore(addr, specs).lookup()
+        opt = SyncReplicasOptimizer(GradientDescentOptimizer(0.1), R, 2, store=s, timeout_s=20)
+        steps = [opt.apply_gradients([(torch.full((8,), float(k + 1)), "w")]) for _ in range(3)]
+        out[k] = (steps, opt.dropped)
+
+    ts = [threading.Thread(target=replica, args=(k, 2)) for k in range(2)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert out[0][0] == out[1][0] == [1, 2, 3]
+    assert torch.allclose(st.read_all()["w"], torch.full((8,), -0.1 * 1.5 * 3))
+    # R = 1: the first push of a step applies alone; a push for an applied step is dropped
+    opt = SyncReplicasOptimizer(GradientDescentOptimizer(0.1), 1, 2, store=st)
+    assert opt.apply_gradients([(torch.ones(8), "w")]) == 4
+    opt.local_step = 3  # a backup replica still on step 3
+    assert opt.apply_gradients([(torch.ones(8), "w")]) == 4 and opt.dropped == 1
