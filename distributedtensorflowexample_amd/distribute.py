@@ -12,6 +12,8 @@ two training modes a ``tf.distribute``-shaped front door:
   framework's communicator (native RCCL on the GPU, gloo on the CPU);
   ``distribute_dataset`` shards a dataset by replica; ``wrap`` returns the bucketed,
   backward-overlapped :class:`~.parallel.mirrored.DistributedDataParallel`.
+* :class:`MultiWorkerMirroredStrategy` -- the same over the workers of a ``TF_CONFIG``
+  cluster (multi-node), rendezvous at the first task's address.
 * :class:`ParameterServerStrategy` -- the reference's asynchronous PS mode: variables
   placed round-robin over the ps tasks of a :class:`~.cluster.ClusterSpec`
   (``replica_device_setter`` semantics), held by the native C++ parameter server and
@@ -132,6 +134,40 @@ class MirroredStrategy(_mirrored.MirroredStrategy, _ScopeMixin):
 
     def experimental_local_results(self, value):
         return (value,)
+
+
+class MultiWorkerMirroredStrategy(MirroredStrategy):
+    """``tf.distribute.experimental.MultiWorkerMirroredStrategy``: synchronous data
+    parallelism over the workers (optionally a ``chief``) of a ``TF_CONFIG`` cluster,
+    across nodes.  One process per GPU; the rendezvous is the TCP store on the FIRST task's
+    address (chief, else worker 0), rank = position in [chief..., worker...], the local GPU
+    is ``LOCAL_RANK`` (default: rank modulo the visible GPUs).  Tensors go over the
+    framework's RCCL communicator (xGMI inside a node; RCCL's inter-node transport
+    between them); the xGMI peer-memory paths of the MLP engines are used only where every
+    rank can map every peer (selection falls back to RCCL otherwise, parallel/select.py)."""
+
+    @classmethod
+    def from_tf_config(cls, env=None, comm_kind="auto", timeout_s=600):
+        cluster, task_type, task_index = ClusterSpec.from_tf_config(env)
+        tasks = [("chief", a) for a in (cluster.job_tasks("chief") if "chief" in cluster.jobs
+                                        else [])]
+        tasks += [("worker", a) for a in cluster.job_tasks("worker")]
+        if not tasks:
+            raise ValueError("TF_CONFIG names no chief / worker tasks")
+        ttype = task_type or "worker"
+        mine = [i for i, (t, _) in enumerate(tasks) if t == ttype]
+        if task_index >= len(mine):
+            raise ValueError("task %s:%d is not in the cluster" % (ttype, task_index))
+        rank, world = mine[task_index], len(tasks)
+        if not dist.is_initialized():
+            host, port = tasks[0][1].rsplit(":", 1)
+            if torch.cuda.is_available():
+                local = int(os.environ.get("LOCAL_RANK", rank % max(1, torch.cuda.device_count())))
+                torch.cuda.set_device(local)
+            dist.init_process_group("gloo", init_method="tcp://%s:%s" % (host, port), rank=rank,
+                                    world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s))
+        return cls(comm_kind=comm_kind)
 
 
 class ParameterServerStrategy(_ScopeMixin):

@@ -68,6 +68,52 @@ def test_mirrored_strategy_gloo_two_replicas():
         assert ok, (r, msg)
 
 
+def _multiworker(idx, cfg, q):
+    try:
+        os.environ["TF_CONFIG"] = json.dumps(dict(cfg, task={"type": "worker", "index": idx}))
+        from distributedtensorflowexample_amd import distribute as D
+
+        st = D.MultiWorkerMirroredStrategy.from_tf_config(comm_kind="torch")
+        v = torch.tensor([float(idx + 1)])
+        ok = st.num_replicas_in_sync == 3 and st.rank == idx + 1  # the chief is rank 0
+        ok &= torch.equal(st.reduce(D.ReduceOp.MAX, v), torch.tensor([2.0]))
+        ok &= torch.equal(st.reduce(D.ReduceOp.SUM, v), torch.tensor([6.0]))
+        q.put((idx, bool(ok), ""))
+    except Exception as e:  # noqa: BLE001
+        q.put((idx, False, repr(e)))
+
+
+def _multichief(cfg, q):
+    try:
+        os.environ["TF_CONFIG"] = json.dumps(dict(cfg, task={"type": "chief", "index": 0}))
+        from distributedtensorflowexample_amd import distribute as D
+
+        st = D.MultiWorkerMirroredStrategy.from_tf_config(comm_kind="torch")
+        ok = st.rank == 0 and torch.equal(st.reduce(D.ReduceOp.MAX, torch.tensor([0.0])),
+                                          torch.tensor([2.0]))
+        ok &= torch.equal(st.reduce(D.ReduceOp.SUM, torch.tensor([3.0])), torch.tensor([6.0]))
+        q.put(("chief", bool(ok), ""))
+    except Exception as e:  # noqa: BLE001
+        q.put(("chief", False, repr(e)))
+
+
+def test_multi_worker_mirrored_from_tf_config():
+    """TF_CONFIG with a chief + 2 workers -> one sync replica group of 3 (gloo)."""
+    cfg = {"cluster": {"chief": ["127.0.0.1:%d" % _port()],
+                       "worker": ["127.0.0.1:%d" % _port(), "127.0.0.1:%d" % _port()]}}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_multichief, args=(cfg, q))]
+    procs += [ctx.Process(target=_multiworker, args=(i, cfg, q)) for i in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(3)]
+    for p in procs:
+        p.join(30)
+    for who, ok, msg in res:
+        assert ok, (who, msg)
+
+
 def test_parameter_server_strategy_round_robin(native_host):
     from distributedtensorflowexample_amd import distribute as D
     from distributedtensorflowexample_amd.cluster import Server, cluster_spec
