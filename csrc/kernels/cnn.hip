@@ -41,11 +41,29 @@ __global__ __launch_bounds__(256) void colpart_reduce_kernel(int R, int C, const
   __shared__ float red[2][4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
   float a = 0.f, b = 0.f;
-  if (c < C)
-    for (int r = blockIdx.y * 4 + rg; r < R; r += 4 * gridDim.y) {
+  if (c < C) {
+    // four rows in flight per thread (independent loads, then the adds): the plain loop
+    // made one dependent memory round trip per row
+    const int step = 4 * gridDim.y;
+    int r = blockIdx.y * 4 + rg;
+    for (; r + 3 * step < R; r += 4 * step) {
+      float va[4], vb[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        va[u] = ps[(size_t)(r + u * step) * C + c];
+        if (pq) vb[u] = pq[(size_t)(r + u * step) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a += va[u];
+        b += vb[u];
+      }
+    }
+    for (; r < R; r += step) {
       a += ps[(size_t)r * C + c];
       if (pq) b += pq[(size_t)r * C + c];
     }
+  }
   red[0][rg][threadIdx.x & 63] = a;
   red[1][rg][threadIdx.x & 63] = b;
   __syncthreads();
@@ -452,8 +470,10 @@ static unsigned grid_for(long long n, int per = 256) {
 
 void colpart_reduce_launch(int R, int C, const float* ps, const float* pq, float* os, float* oq,
                            hipStream_t st) {
+  // >= 16 rows per block (4 per thread), at most 256 row blocks: every block ends in one
+  // same-address atomic per channel, so more blocks trade load latency for atomic serialisation
   int S = (R + 15) / 16;
-  if (S > 128) S = 128;
+  if (S > 256) S = 256;
   if (S < 1) S = 1;
   hipLaunchKernelGGL(colpart_reduce_kernel, dim3((C + 63) / 64, S), dim3(256), 0, st, R, C, ps, pq,
                      os, oq);

@@ -50,6 +50,16 @@ __device__ __forceinline__ float rsum16(float v) {
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false));
   return v;
 }
+// (tile, batch*head) of this block: the tiles of one (batch, head) share its K/V (forward,
+// dq) or Q/dO (dkdv) stream, so they are given consecutive ids of ONE XCD (bijective XCD
+// remap of the linear block id) instead of the dispatcher's round robin, which put the tiles
+// of every (batch, head) on 8 different XCDs -- 8 L2s each fetching the same operands.
+__device__ __forceinline__ void tile_bh(int& tile, int& bh) {
+  const int nt = gridDim.x;
+  const int id = xcd_remap(blockIdx.y * nt + blockIdx.x, nt * gridDim.y);
+  tile = id % nt;
+  bh = id / nt;
+}
 // operand fragment from an LDS image (see transformer.hip lfrag)
 template <bool KC>
 __device__ __forceinline__ bf16x8 frag(const char* base, int o0, int k0, int lane) {
@@ -111,11 +121,13 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(int S, int nh,
                                                         float* __restrict__ lse, int ld_lse,
                                                         const float* __restrict__ kmask, float scale) {
   __shared__ __attribute__((aligned(16))) char Ks[TILE], Vs[TILE], Ps[4][16 * LD];
-  const int bh = blockIdx.y, b = bh / nh, h = bh % nh;
+  int tile, bh;
+  tile_bh(tile, bh);
+  const int b = bh / nh, h = bh % nh;
   const int Hd = nh * D, ld = 3 * Hd;
   const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int q0 = blockIdx.x * T + wave * 16;
+  const int q0 = tile * T + wave * 16;
   const int cl = lane & 15, rg = 4 * (lane >> 4);
   bf16x8 qa[2];
 #pragma unroll
@@ -224,12 +236,14 @@ __global__ __launch_bounds__(256) void flash_dkdv_kernel(
     float* __restrict__ dbias) {
   __shared__ __attribute__((aligned(16))) char Qs[TILE], dOs[TILE], PT[4][16 * LD], DT[4][16 * LD];
   __shared__ float Ls[T], Ds[T];
-  const int bh = blockIdx.y, b = bh / nh, h = bh % nh;
+  int tile, bh;
+  tile_bh(tile, bh);
+  const int b = bh / nh, h = bh % nh;
   const int Hd = nh * D, ld = 3 * Hd;
   const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
   const unsigned short* dob = dout + (size_t)b * S * Hd + h * D;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int k0 = blockIdx.x * T + wave * 16;
+  const int k0 = tile * T + wave * 16;
   const int cl = lane & 15, rg = 4 * (lane >> 4);
   bf16x8 ka[2], va[2];
 #pragma unroll
@@ -339,12 +353,14 @@ __global__ __launch_bounds__(256) void flash_dq_kernel(
     const float* __restrict__ kmask, float scale, unsigned short* __restrict__ dqkv,
     float* __restrict__ dbias) {
   __shared__ __attribute__((aligned(16))) char Ks[TILE], Vs[TILE], DS[4][16 * LD];
-  const int bh = blockIdx.y, b = bh / nh, h = bh % nh;
+  int tile, bh;
+  tile_bh(tile, bh);
+  const int b = bh / nh, h = bh % nh;
   const int Hd = nh * D, ld = 3 * Hd;
   const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
   const unsigned short* dob = dout + (size_t)b * S * Hd + h * D;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int q0 = blockIdx.x * T + wave * 16;
+  const int q0 = tile * T + wave * 16;
   const int cl = lane & 15, rg = 4 * (lane >> 4);
   bf16x8 qa[2], oa[2];
 #pragma unroll
