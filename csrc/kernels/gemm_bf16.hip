@@ -81,13 +81,43 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
 // The gathers run in the glds staging: every lane computes its own 16-B source
 // address (8 consecutive channels of one tap; C % 8 == 0), and padding taps /
 // K tails point at a 16-B zero page, so no im2col buffer ever exists.
+//
+// MODE 2 runs as stride x stride phase classes (blockIdx.z): the input pixels
+// h = i*s + ph, w = j*s + pw of class (ph, pw) only receive the taps kh = kh0 + s*th,
+// kw = kw0 + s*tw (kh0 = (ph + pad) % s), and for those taps dy is read at
+// (i + oy - th, j + ox - tw), oy = (ph + pad - kh0) / s -- a dense stride-1 product over
+// the class's pixels with a nkh x nkw kernel.  A strided dgrad thus does no MFMA work on
+// the (s^2 - 1)/s^2 taps a pixel never receives (it used to gather zeros for them: the
+// stride-2 dgrads of ResNet-50 ran at ~100 TFLOP/s against ~330 at stride 1).  The
+// epilogue maps class row m back to pixel (n, i*s + ph, j*s + pw).
 struct ConvDesc {
   int N, H, W, C;        // input
   int OH, OW, K;         // output spatial, output channels
   int KH, KW, stride, pad;
   int ktot;              // reduction length of the GEMM (MODE 1: KH*KW*C, MODE 2: KH*KW*K)
   int wld;               // weight row stride (elements) for MODE 2
+  // MODE 2 phase class (set in the kernel from blockIdx.z; see above)
+  int ph, pw, Hc, Wc, oy, ox, kh0, kw0, nkh, nkw;
+  int prc;               // partial statistic rows per class (MODE 2, col_partial)
 };
+
+// MODE 2: this block's phase class -> the class fields of d, d.ktot; returns the class's
+// pixel count (GEMM M)
+__device__ __forceinline__ int dgrad_class(ConvDesc& d, int z) {
+  const int s = d.stride;
+  d.ph = z / s;
+  d.pw = z - d.ph * s;
+  d.Hc = (d.H - d.ph + s - 1) / s;
+  d.Wc = (d.W - d.pw + s - 1) / s;
+  d.kh0 = (d.ph + d.pad) % s;
+  d.kw0 = (d.pw + d.pad) % s;
+  d.nkh = d.KH > d.kh0 ? (d.KH - d.kh0 + s - 1) / s : 0;
+  d.nkw = d.KW > d.kw0 ? (d.KW - d.kw0 + s - 1) / s : 0;
+  d.oy = (d.ph + d.pad - d.kh0) / s;
+  d.ox = (d.pw + d.pad - d.kw0) / s;
+  d.ktot = d.nkh * d.nkw * d.K;
+  return d.N * d.Hc * d.Wc;
+}
 
 __device__ __attribute__((aligned(16))) unsigned short g_zero16[8];
 
@@ -182,7 +212,7 @@ template <int NW, int NBLK>
 __device__ __forceinline__ void conv_rows(const ConvDesc& d, int mode, int M, int m0, int wave,
                                           int lane, RowState& rs) {
   static_assert(NBLK <= 8, "RowState holds 8 rows per lane");
-  const int PW = mode == 1 ? d.OW : d.W, PHW = mode == 1 ? d.OH * d.OW : d.H * d.W;
+  const int PW = mode == 1 ? d.OW : d.Wc, PHW = mode == 1 ? d.OH * d.OW : d.Hc * d.Wc;
   const float ipw = 1.f / PW, iphw = 1.f / PHW;
 #pragma unroll
   for (int i = 0; i < NBLK; ++i) {
@@ -194,9 +224,9 @@ __device__ __forceinline__ void conv_rows(const ConvDesc& d, int mode, int M, in
     if (mode == 1) {
       rs.y0[i] = py * d.stride - d.pad;
       rs.x0[i] = px * d.stride - d.pad;
-    } else {  // dgrad: numerator base h + pad (minus kh per tap)
-      rs.y0[i] = py + d.pad;
-      rs.x0[i] = px + d.pad;
+    } else {  // dgrad (class-local pixel): dy row of tap th is y0 - th
+      rs.y0[i] = py + d.oy;
+      rs.x0[i] = px + d.ox;
     }
   }
 }
@@ -219,7 +249,8 @@ __device__ __forceinline__ void stage_a_conv(const ConvDesc& d, int mode, const 
     int tap, ch;
     if (uni) { tap = tap_u; ch = c_u + c * 8; }
     else { tap = k / CH; ch = k - tap * CH; }
-    const int kh = tap / d.KW, kw = tap - (tap / d.KW) * d.KW;
+    const int TW = mode == 1 ? d.KW : d.nkw;  // (mode 2: class taps)
+    const int kh = tap / TW, kw = tap - kh * TW;
     bool ok = rs.nb[i] >= 0 && k < d.ktot;
     int yy, xx;
     if (mode == 1) {
@@ -227,11 +258,9 @@ __device__ __forceinline__ void stage_a_conv(const ConvDesc& d, int mode, const 
       xx = rs.x0[i] + kw;
       ok = ok && yy >= 0 && yy < d.H && xx >= 0 && xx < d.W;
     } else {
-      const int ny = rs.y0[i] - kh, nx = rs.x0[i] - kw;
-      yy = ny / d.stride;
-      xx = nx / d.stride;
-      ok = ok && ny >= 0 && nx >= 0 && yy * d.stride == ny && xx * d.stride == nx && yy < d.OH &&
-           xx < d.OW;
+      yy = rs.y0[i] - kh;
+      xx = rs.x0[i] - kw;
+      ok = ok && yy >= 0 && xx >= 0 && yy < d.OH && xx < d.OW;
     }
     const int SH = mode == 1 ? d.H : d.OH, SW = mode == 1 ? d.W : d.OW;
     const unsigned short* g =
@@ -246,7 +275,9 @@ template <int NW, int OUTER>
 __device__ __forceinline__ void stage_b_wtap(const ConvDesc& d, const unsigned short* __restrict__ w,
                                              int n0, int k0, char* lds_tile, int wave, int lane) {
   constexpr int LPR = OUTER / 8, RPB = 64 / LPR;  // lanes per k-row, k-rows per 1 KB block
-  const int tap = k0 / d.K, co0 = k0 - tap * d.K;  // host: K % 64 == 0
+  const int ctap = k0 / d.K, co0 = k0 - ctap * d.K;  // host: K % 64 == 0
+  const int th = ctap / max(d.nkw, 1), tw = ctap - th * d.nkw;  // class tap -> kernel tap
+  const int tap = (d.kh0 + d.stride * th) * d.KW + d.kw0 + d.stride * tw;
 #pragma unroll
   for (int i = 0; i < (OUTER / 8) / NW; ++i) {
     const int blk = i * NW + wave;
@@ -341,6 +372,10 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   A += sA * blockIdx.z;
   B += sB * blockIdx.z;
   Cv = (char*)Cv + sC * blockIdx.z * (OUT_F32 ? 4 : 2);
+  if constexpr (MODE == 2) {  // phase class blockIdx.z: its pixels, its taps
+    M = dgrad_class(cd, blockIdx.z);
+    K = cd.ktot;
+  }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
   // Split-K (gridDim.y > 1): one XCD-contiguous range of (split, tile) pairs per XCD, so the
@@ -354,8 +389,10 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
     bid = lam % T;
     split = lam / T;
   } else {
-    bid = xcd_remap(blockIdx.x, tiles_n * tiles_m);
+    // (MODE 2: the grid is sized for the largest phase class)
+    bid = xcd_remap(blockIdx.x, MODE == 2 ? (int)gridDim.x : tiles_n * tiles_m);
     split = 0;
+    if (MODE == 2 && bid >= tiles_n * tiles_m) return;
   }
   int tm = bid / tiles_n, tn = bid % tiles_n;
   if (NBUF == 8 && gridDim.y == 1) {
@@ -631,7 +668,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
     const int n = n0 + c0 + (lane & 7) * 8;
     if (e.col_partial) {
       // one partial row per 64-row wave slab (launchers use WM == 64 for partial stats)
-      const size_t prow = (size_t)(m0 / 64 + wm) * N;
+      const size_t prow = (size_t)((MODE == 2 ? blockIdx.z * cd.prc : 0) + m0 / 64 + wm) * N;
       if (lane < 8 && m0 + wm * 64 < M)
 #pragma unroll
         for (int u = 0; u < 8; ++u)
@@ -655,7 +692,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
     // loaded before any is used: one memory round trip per 32-row slab instead of one per
     // 8-row group (the loads used to sit between dependent compute and stores).
     bool full[4], live[4];
-    int mm[4], nn[4];
+    int mm[4], nn[4], pm[4];  // pm: memory row of GEMM row mm (MODE 2: class pixel -> pixel)
     bf16x8 a8[4], r8[4], x8[4];
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
@@ -665,10 +702,17 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
       live[it] = mm[it] < M && nn[it] < N && cg < SLW;
       full[it] = live[it] && nn[it] + 8 <= N;  // N % 8 != 0 only with a ragged last group
       const int ms = live[it] ? mm[it] : 0, ns = full[it] ? nn[it] : 0;
+      pm[it] = ms;
+      if (MODE == 2 && cd.stride > 1) {
+        int nimg, rem, i, j;
+        fdivmod(ms, cd.Hc * cd.Wc, 1.f / (cd.Hc * cd.Wc), nimg, rem);
+        fdivmod(rem, cd.Wc, 1.f / cd.Wc, i, j);
+        pm[it] = (nimg * cd.H + i * cd.stride + cd.ph) * cd.W + j * cd.stride + cd.pw;
+      }
       if (!OUT_F32) {  // (f32-output tiles load at use: the 256x256 f32 variant would spill)
-        if (e.act_grad) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)ms * e.ld_aux + ns];
-        if (e.residual) r8[it] = *(const bf16x8*)&e.residual[(size_t)ms * e.ld_res + ns];
-        if (MODE == 2 && e.bn_x) x8[it] = *(const bf16x8*)&e.bn_x[(size_t)ms * ldc + ns];
+        if (e.act_grad) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)pm[it] * e.ld_aux + ns];
+        if (e.residual) r8[it] = *(const bf16x8*)&e.residual[(size_t)pm[it] * e.ld_res + ns];
+        if (MODE == 2 && e.bn_x) x8[it] = *(const bf16x8*)&e.bn_x[(size_t)pm[it] * ldc + ns];
       }
     }
     // static accumulator indices only (a runtime acc[2h+ii] index would put acc in scratch)
@@ -696,7 +740,8 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
-      const int m = mm[it], n = nn[it];
+      const int n = nn[it];
+      const size_t mp = pm[it];
       float v[8];
       *(f32x4*)&v[0] = *(const f32x4*)&ep[rr * EP_LD + cg];
       *(f32x4*)&v[4] = *(const f32x4*)&ep[rr * EP_LD + cg + 4];
@@ -719,7 +764,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           bf16x8 o;
 #pragma unroll
           for (int u = 0; u < 8; ++u) o[u] = (short)f2bf(v[u]);
-          *(bf16x8*)&e.aux_out[(size_t)m * e.ld_aux + n] = o;
+          *(bf16x8*)&e.aux_out[(size_t)mp * e.ld_aux + n] = o;
         }
         if (e.act == 1) {
 #pragma unroll
@@ -729,12 +774,12 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           for (int u = 0; u < 8; ++u) v[u] = fmaxf(v[u], 0.f);
         }
         if (MODE != 0 && e.residual) {  // convolutions: shortcut gradient before the mask
-          if (OUT_F32) r8[it] = *(const bf16x8*)&e.residual[(size_t)m * e.ld_res + n];
+          if (OUT_F32) r8[it] = *(const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[it][u]);
         }
         if (e.act_grad) {
-          if (OUT_F32) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)m * e.ld_aux + n];
+          if (OUT_F32) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)mp * e.ld_aux + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             const float uu = bf2f((unsigned short)a8[it][u]);
@@ -742,7 +787,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           }
         }
         if (MODE == 0 && e.residual) {
-          if (OUT_F32) r8[it] = *(const bf16x8*)&e.residual[(size_t)m * e.ld_res + n];
+          if (OUT_F32) r8[it] = *(const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[it][u]);
         }
@@ -765,7 +810,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           }
         }
         if (OUT_F32) {
-          float* C = (float*)Cv + (size_t)m * ldc + n;
+          float* C = (float*)Cv + (size_t)mp * ldc + n;
           if (e.beta != 0.f) {  // (f32 outputs: C_old read here, no 32-VGPR slab batch)
             const f32x4 c0 = *(const f32x4*)C, c1 = *(const f32x4*)(C + 4);
 #pragma unroll
@@ -780,33 +825,33 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           bf16x8 o;
 #pragma unroll
           for (int u = 0; u < 8; ++u) o[u] = (short)f2bf(v[u]);
-          *(bf16x8*)((unsigned short*)Cv + (size_t)m * ldc + n) = o;
+          *(bf16x8*)((unsigned short*)Cv + (size_t)mp * ldc + n) = o;
         }
       } else {
         for (int u = 0; u < 8 && n + u < N; ++u) {
           float w = v[u];
-          if (e.aux_out) e.aux_out[(size_t)m * e.ld_aux + n + u] = f2bf(w);
+          if (e.aux_out) e.aux_out[(size_t)mp * e.ld_aux + n + u] = f2bf(w);
           if (e.act == 1) w = gelu_f(w);
           else if (e.act == 2) w = fmaxf(w, 0.f);
-          if (MODE != 0 && e.residual) w += bf2f(e.residual[(size_t)m * e.ld_res + n + u]);
+          if (MODE != 0 && e.residual) w += bf2f(e.residual[(size_t)mp * e.ld_res + n + u]);
           if (e.act_grad) {
-            const float uu = bf2f(e.aux_in[(size_t)m * e.ld_aux + n + u]);
+            const float uu = bf2f(e.aux_in[(size_t)mp * e.ld_aux + n + u]);
             w *= (e.act_grad == 1) ? gelu_grad_f(uu) : (uu > 0.f ? 1.f : 0.f);
           }
-          if (MODE == 0 && e.residual) w += bf2f(e.residual[(size_t)m * e.ld_res + n + u]);
+          if (MODE == 0 && e.residual) w += bf2f(e.residual[(size_t)mp * e.ld_res + n + u]);
           if (MODE == 2 && !OUT_F32 && e.bn_x) {
             const float wr = bf2f(f2bf(w));
             cs[u] += wr;
-            cq[u] += wr * (bf2f(e.bn_x[(size_t)m * ldc + n + u]) - bmu[u]) * brs[u];
+            cq[u] += wr * (bf2f(e.bn_x[(size_t)mp * ldc + n + u]) - bmu[u]) * brs[u];
           } else {
             cs[u] += w;
             cq[u] += w * w;
           }
           if (OUT_F32) {
-            float* C = (float*)Cv + (size_t)m * ldc + n + u;
+            float* C = (float*)Cv + (size_t)mp * ldc + n + u;
             *C = (e.beta != 0.f) ? w + e.beta * *C : w;
           } else {
-            ((unsigned short*)Cv)[(size_t)m * ldc + n + u] = f2bf(w);
+            ((unsigned short*)Cv)[(size_t)mp * ldc + n + u] = f2bf(w);
           }
         }
       }
@@ -1113,7 +1158,18 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
       e.bn_rstd = bn_rstd;
     }
     e.col_partial = (colsum || colsq) ? 1 : 0;
-    launch_cfg<2, false, false, false>(choose_cfg(M, Nn, 1, 2), dim3(1, 1, 1), M, Nn, K,
+    // stride x stride phase classes over blockIdx.z (ConvDesc comment); the grid and the
+    // partial statistic rows are sized for the largest class, ceil(H / s) x ceil(W / s)
+    const int s = stride, Hc = (H + s - 1) / s, Wc = (W + s - 1) / s;
+    M = N * Hc * Wc;
+    d.prc = (M + 63) / 64;
+    if (e.col_partial && (H % s || W % s)) {
+      // smaller classes leave some of their partial rows unwritten: zero them all first
+      const size_t bytes = sizeof(float) * (size_t)s * s * d.prc * C;
+      if (colsum) DTFX_HIP_CHECK(hipMemsetAsync(colsum, 0, bytes, stream));
+      if (colsq) DTFX_HIP_CHECK(hipMemsetAsync(colsq, 0, bytes, stream));
+    }
+    launch_cfg<2, false, false, false>(choose_cfg(M, Nn, s * s, 2), dim3(1, 1, s * s), M, Nn, K,
                                        (const unsigned short*)a, 0, (const unsigned short*)b, 0,
                                        out, C, e, 0LL, 0LL, 0LL, d, stream);
   } else if (mode == 3) {

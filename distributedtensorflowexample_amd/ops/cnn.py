@@ -101,7 +101,10 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
     y, x, mean, rstd, sdy, sdx = bn
     if y.shape != dx.shape or x.shape != dx.shape:
         raise ValueError("fused BN backward: y and x must have the dgrad output's shape")
-    rows = (N * H * W + 63) // 64  # one partial row per 64-row output slab
+    # one partial row per 64-row output slab of each stride x stride phase class (the
+    # kernel sizes every class like the largest, ceil(H / s) x ceil(W / s) pixels)
+    hc, wc = -(-H // stride), -(-W // stride)
+    rows = stride * stride * ((N * hc * wc + 63) // 64)
     part = torch.empty(2, rows, C, device=dy.device)
     hip().conv_bf16(2, N, H, W, C, Cout, KH, KW, stride, pad, ptr(dy), ptr(w), w.stride(0),
                     ptr(dx), 0.0, ptr(residual), ptr(part[0]), ptr(part[1]), 0, stream_handle(),

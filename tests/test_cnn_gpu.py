@@ -19,6 +19,9 @@ CONVS = [  # N, H, W, C, Cout, k, stride, pad
     (2, 14, 14, 64, 256, 1, 2, 0),
     (2, 9, 11, 256, 64, 1, 1, 0),
     (2, 32, 32, 8, 64, 7, 2, 3),
+    (2, 15, 13, 64, 128, 3, 2, 1),   # stride-2 dgrad: phase classes of unequal size
+    (2, 14, 14, 64, 64, 3, 2, 1),    # stride-2 dgrad on the 256x64 tile
+    (2, 13, 15, 128, 64, 1, 2, 0),   # 1x1 stride 2: three of four classes have no taps
 ]
 
 
@@ -55,6 +58,9 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, W, C, Co, k, s, p):
     (2, 14, 14, 64, 64, 3, 1, 1, True),
     (2, 14, 14, 64, 256, 1, 2, 0, False),
     (2, 9, 11, 256, 64, 1, 1, 0, True),   # M = 198: ragged last partial-statistics slab
+    (2, 14, 14, 128, 128, 3, 2, 1, True),  # stride-2 phase classes, one partial block each
+    (2, 15, 13, 64, 128, 3, 2, 1, True),   # unequal classes: zeroed partial rows
+    (2, 13, 15, 128, 64, 1, 2, 0, True),   # empty classes: residual + mask only
 ])
 def test_conv_dgrad_fused_batchnorm_backward(gpu, N, H, W, C, Co, k, s, p, with_res):
     """dgrad with BatchNorm backward's reductions in its epilogue (+ shortcut gradient, ReLU
