@@ -887,7 +887,22 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
     if (e.colsum || e.colsq) {
       __syncthreads();
       const float* red = (const float*)(smem + 98304);
-      if (threadIdx.x < BN) {
+      if (e.col_partial && threadIdx.x < BN) {
+        // partial rows, one per 64-row output slab (the conv launchers' layout, reduced by
+        // colpart_reduce): slab g of the block is entries wm8 * 2 + Mq with Mq = g >> 1,
+        // wm8 >> 1 = g & 1 (slab_r0: rows Mq * 128 + wm8 * 32)
+        const int c = threadIdx.x, nq = c / NQN, w = (c % NQN) / SW, col = c % SW;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int i0 = (g & 1) * 4 + (g >> 1), i1 = i0 + 2;
+          const int e0 = ((nq * 2 + w) * 8 + i0) * 64 + col, e1 = ((nq * 2 + w) * 8 + i1) * 64 + col;
+          if (m0 + g * 64 < M && n0 + c < N) {
+            const size_t prow = (size_t)(m0 / 64 + g) * N + n0 + c;
+            if (e.colsum) e.colsum[prow] = red[e0] + red[e1];
+            if (e.colsq) e.colsq[prow] = red[2048 + e0] + red[2048 + e1];
+          }
+        }
+      } else if (threadIdx.x < BN) {
         const int c = threadIdx.x, nq = c / NQN, w = (c % NQN) / SW, col = c % SW;
         float a = 0.f, q = 0.f;
 #pragma unroll
@@ -1136,6 +1151,22 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
     M = N * OH * OW; Nn = Cout; K = d.ktot;
     if (ldw < (K + 63) / 64 * 64) throw std::runtime_error("conv_bf16: fwd weights need ld >= ceil64(KH*KW*C)");
     e.ld_res = Cout;
+    static const int plain1x1 = [] {  // DTFX_CONV1X1_GEMM=0: keep 1x1 convs on the gather path
+      const char* v = getenv("DTFX_CONV1X1_GEMM");
+      return v ? atoi(v) : 1;
+    }();
+    if (plain1x1 && KH == 1 && KW == 1 && stride == 1 && pad == 0 && C % 64 == 0) {
+      // a 1x1 stride-1 convolution is the plain GEMM y[M][Cout] = x[M][C] W[Cout][C]^T:
+      // the 8-phase 256x256 tile when the time model picks it (partial statistic rows per
+      // 64-row slab, as above)
+      const int cfg = choose_cfg(M, Nn, 1, 0);
+      if (cfg == 5) {
+        launch_cfg<0, false, true, false>(cfg, dim3(1, 1, 1), M, Nn, K, (const unsigned short*)a, C,
+                                          (const unsigned short*)b, ldw, out, Cout, e, 0LL, 0LL,
+                                          0LL, d, stream);
+        return;
+      }
+    }
     launch_cfg<1, false, true, false>(choose_cfg(M, Nn, 1, 1), dim3(1, 1, 1), M, Nn, K,
                                       (const unsigned short*)a, 0, (const unsigned short*)b, ldw,
                                       out, Cout, e, 0LL, 0LL, 0LL, d, stream);
