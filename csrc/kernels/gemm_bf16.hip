@@ -364,7 +364,8 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   constexpr int NWN = NBUF == 8 ? 4 : BN / 64, NW = NBUF == 8 ? 8 : (BM / WM) * NWN;
   constexpr int TM = WM / 16;                      // 16-row MFMA tiles per wave
   constexpr int NQN = BN / 2, SW = NQN / 2;        // 8-phase: B half width, wave slab width
-  static_assert(BN_ == 128 || MODE == 0 || MODE == 1 || (MODE == 2 && BN_ == 64),
+  static_assert(BN_ == 128 || MODE == 0 || MODE == 1 || (MODE == 2 && BN_ == 64) ||
+                    (NBUF == 8 && MODE != 3),
                 "gathered B operands need BN = 128 (dgrad: or 64)");
   constexpr int TILE_A = BM * BK * 2, TILE_B = BN * BK * 2, BUF_BYTES = TILE_A + TILE_B;
   constexpr int LPT = (BM / 8) / NW + (BN / 8) / NW;  // glds per thread per K tile
@@ -423,7 +424,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   const int kt0 = split * per;
   const int nk = max(0, min(per, nk_all - kt0));
   RowState rs;
-  if (MODE == 1 || MODE == 2) conv_rows<NW, BM / 8 / NW>(cd, MODE, M, m0, wave, lane, rs);
+  if (NBUF != 8 && (MODE == 1 || MODE == 2)) conv_rows<NW, BM / 8 / NW>(cd, MODE, M, m0, wave, lane, rs);
   auto stage_all = [&](int buf, int kt) {
     char* base = smem + buf * BUF_BYTES;
     const int k0 = (kt0 + kt) * BK;
@@ -493,7 +494,55 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
     // Staging through buffer loads with LDS destination: each lane's byte offset at k = 0 is
     // computed ONCE (8 VGPRs for the 4 half images x 2 instructions); the K advance is the
     // wave-uniform soffset.  (64-bit per-lane pointers for 8 staging sites spilled.)
-    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7fffffff, 0x00020000);
+    // Convolutions (MODE 1 / 2): the A rows are gathered pixels.  NHWC makes a tap's offset
+    // from the pixel the same for every lane, so each lane keeps its row's pixel base and
+    // (y0, x0) and per K tile forms base + tap delta, or an offset past the buffer's extent
+    // (the hardware then returns zeros) for padding taps and rows past M; the channel offset
+    // inside the tap is the uniform soffset.  (Host: source < 2 GB, channels % 64 == 0.)
+    constexpr bool CONV8 = MODE == 1 || MODE == 2;
+    const int csh = MODE == 1 ? cd.H : cd.OH, csw = MODE == 1 ? cd.W : cd.OW;  // source image
+    const int cch = MODE == 1 ? cd.C : cd.K;                                   // source channels
+    const int a_bytes = CONV8 ? (int)min((long long)cd.N * csh * csw * cch * 2, 0x7fffffffLL) : 0x7fffffff;
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
+    int cpb[4] = {0, 0, 0, 0}, cyx[4] = {0, 0, 0, 0};  // per A row (half * 2 + i): pixel base, y0 << 16 | x0
+    if constexpr (CONV8) {
+      const int PW = MODE == 1 ? cd.OW : cd.Wc, PHW = MODE == 1 ? cd.OH * cd.OW : cd.Hc * cd.Wc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + (r >> 1) * 128 + ((r & 1) * NW + wave) * 8 + (lane >> 3);
+        int n, rem, py, px;
+        fdivmod(min(m, M - 1), PHW, 1.f / PHW, n, rem);
+        fdivmod(rem, PW, 1.f / PW, py, px);
+        const int y0 = m < M ? (MODE == 1 ? py * cd.stride - cd.pad : py + cd.oy) : -30000;
+        const int x0 = MODE == 1 ? px * cd.stride - cd.pad : px + cd.ox;
+        cpb[r] = (n * csh + y0) * csw + x0;
+        cyx[r] = (y0 << 16) | (x0 & 0xffff);
+      }
+    }
+    auto conv_stage_a = [&](int buf, int which, int kt) {
+      const int k0 = (kt0 + kt) * BK, tap = k0 / cch, ch0 = k0 - tap * cch;
+      const int tw_ = MODE == 1 ? cd.KW : max(cd.nkw, 1);
+      const int th = tap / tw_, tw = tap - th * tw_;
+      const int dy = MODE == 1 ? th : -th, dx = MODE == 1 ? tw : -tw;  // source pixel delta
+      char* d_ = smem + (buf * 4 + which) * 16384;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = which * 2 + i, row = (i * NW + wave) * 8 + (lane >> 3);
+        const int y = (cyx[r] >> 16) + dy, x = (int)(short)(cyx[r] & 0xffff) + dx;
+        const bool ok = (unsigned)y < (unsigned)csh && (unsigned)x < (unsigned)csw;
+        const int vo = ok ? (cpb[r] + dy * csw + dx) * cch * 2 + (((lane & 7) ^ swz_kc(row)) << 4)
+                          : (int)0x80000000;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(d_ + (i * NW + wave) * 1024), 16, vo,
+                                                 ch0 * 2, 0, 0);
+      }
+    };
+    // MODE 2 B (weights, k-strided [64 co][ci] image): row co0 + kr of the tap's column block
+    auto wtap_soff = [&](int kt) {
+      const int k0 = (kt0 + kt) * BK, ctap = k0 / cd.K, co0 = k0 - ctap * cd.K;
+      const int th = ctap / max(cd.nkw, 1), tw = ctap - th * cd.nkw;
+      const int tap = (cd.kh0 + cd.stride * th) * cd.KW + cd.kw0 + cd.stride * tw;
+      return (co0 * ldb + tap * cd.C) * 2;
+    };
     const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7fffffff, 0x00020000);
     auto voff = [&](bool isA, int which, int i) -> int {
       const bool kc = isA ? !TA : TB;
@@ -515,8 +564,13 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
     const int vo3_0 = voff(false, 3, 0), vo3_1 = voff(false, 3, 1);
 #define DTFX_PH8_STAGE(BUF, WHICH, KT)                                                          \
   do {                                                                                          \
+    if constexpr (CONV8 && (WHICH) < 2) {                                                       \
+      conv_stage_a((BUF), (WHICH), (KT));                                                       \
+      break;                                                                                    \
+    }                                                                                           \
     const int k0_ = (kt0 + (KT)) * BK;                                                          \
-    const int so_ = (WHICH) < 2 ? (TA ? k0_ * lda * 2 : k0_ * 2) : (TB ? k0_ * 2 : k0_ * ldb * 2); \
+    const int so_ = (WHICH) < 2 ? (TA ? k0_ * lda * 2 : k0_ * 2)                                \
+                                : (MODE == 2 ? wtap_soff(KT) : TB ? k0_ * 2 : k0_ * ldb * 2);   \
     char* d_ = hbuf((BUF), (WHICH));                                                            \
     __builtin_amdgcn_raw_ptr_buffer_load_lds((WHICH) < 2 ? rA : rB, (lds_void*)(d_ + wave * 1024), \
                                              16, vo##WHICH##_0, so_, 0, 0);                     \
@@ -635,20 +689,25 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   // Each wave uses its own 32 x 68 f32 region (row pad 4 floats: the 4 row groups of a
   // ds_write land on distinct banks); the K loop's final barrier freed the buffers.
   constexpr int EP_LD = 68;
+  // Side inputs of a slab are prefetched before its LDS transpose, except where the registers
+  // are not there: f32 outputs, and the 8-phase dgrad with the fused BatchNorm backward
+  // (3 side inputs beside 128 accumulators) -- those load at use.
+  constexpr bool PREF = !OUT_F32 && !(NBUF == 8 && MODE == 2);
   float* ep = (float*)smem + wave * (32 * EP_LD);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
   float cs[8], cq[8];  // fused column sums / sums of squares of this lane's 8 columns
 #pragma unroll
   for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
   float bmu[8], brs[8];  // BN mean / rstd of this lane's 8 columns (bn_x epilogue only)
-  if (MODE == 2 && !OUT_F32 && e.bn_x) {
-    const int n = n0 + wn * 64 + (lane & 7) * 8;
+  auto load_bn = [&](int c0) {
+    const int n = n0 + c0 + (lane & 7) * 8;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       bmu[u] = n + u < N ? e.bn_mean[n + u] : 0.f;
       brs[u] = n + u < N ? e.bn_rstd[n + u] : 0.f;
     }
-  }
+  };
+  if (MODE == 2 && PREF && e.bn_x) load_bn(wn * 64);
   // Rows / columns of the wave's h-th 32 x 64 output slab: 8-phase layout (one slab per block
   // quadrant) or a contiguous WM x 64 wave tile.
   auto slab_r0 = [&](int h) { return NBUF == 8 ? (h >> 1) * 128 + (wave >> 1) * 32 : wm * WM + h * 32; };
@@ -687,6 +746,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   };
   for (int h = 0; h < WM / 32; ++h) {
     const int r0 = slab_r0(h), c0 = slab_c0(h);
+    // (8-phase: consecutive slabs alternate between the two column halves)
     // (issued before the slab's LDS transpose, so their latency overlaps it)
     // Side inputs (aux_in / residual) of the slab's 4 row groups are all
     // loaded before any is used: one memory round trip per 32-row slab instead of one per
@@ -709,7 +769,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
         fdivmod(rem, cd.Wc, 1.f / cd.Wc, i, j);
         pm[it] = (nimg * cd.H + i * cd.stride + cd.ph) * cd.W + j * cd.stride + cd.pw;
       }
-      if (!OUT_F32) {  // (f32-output tiles load at use: the 256x256 f32 variant would spill)
+      if (PREF) {
         if (e.act_grad) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)pm[it] * e.ld_aux + ns];
         if (e.residual) r8[it] = *(const bf16x8*)&e.residual[(size_t)pm[it] * e.ld_res + ns];
         if (MODE == 2 && e.bn_x) x8[it] = *(const bf16x8*)&e.bn_x[(size_t)pm[it] * ldc + ns];
@@ -774,12 +834,12 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           for (int u = 0; u < 8; ++u) v[u] = fmaxf(v[u], 0.f);
         }
         if (MODE != 0 && e.residual) {  // convolutions: shortcut gradient before the mask
-          if (OUT_F32) r8[it] = *(const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n];
+          if (!PREF) r8[it] = *(const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[it][u]);
         }
         if (e.act_grad) {
-          if (OUT_F32) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)mp * e.ld_aux + n];
+          if (!PREF) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)mp * e.ld_aux + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             const float uu = bf2f((unsigned short)a8[it][u]);
@@ -787,7 +847,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           }
         }
         if (MODE == 0 && e.residual) {
-          if (OUT_F32) r8[it] = *(const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n];
+          if (!PREF) r8[it] = *(const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[it][u]);
         }
@@ -795,6 +855,13 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           if (MODE == 2 && !OUT_F32 && e.bn_x) {
             // statistics of the VALUES STORED (bf16-rounded), as a separate reduction over
             // the output tensor would see them
+            if (!PREF) {  // load at use: x, and the BN mean / rstd of the 8 columns
+              x8[it] = *(const bf16x8*)&e.bn_x[mp * ldc + n];
+              *(f32x4*)&bmu[0] = *(const f32x4*)&e.bn_mean[n];
+              *(f32x4*)&bmu[4] = *(const f32x4*)&e.bn_mean[n + 4];
+              *(f32x4*)&brs[0] = *(const f32x4*)&e.bn_rstd[n];
+              *(f32x4*)&brs[4] = *(const f32x4*)&e.bn_rstd[n + 4];
+            }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
               const float vr = bf2f(f2bf(v[u]));
@@ -828,6 +895,11 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           *(bf16x8*)((unsigned short*)Cv + (size_t)mp * ldc + n) = o;
         }
       } else {
+        if (MODE == 2 && !PREF && e.bn_x)
+          for (int u = 0; u < 8 && n + u < N; ++u) {
+            bmu[u] = e.bn_mean[n + u];
+            brs[u] = e.bn_rstd[n + u];
+          }
         for (int u = 0; u < 8 && n + u < N; ++u) {
           float w = v[u];
           if (e.aux_out) e.aux_out[(size_t)mp * e.ld_aux + n + u] = f2bf(w);
@@ -897,7 +969,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           const int i0 = (g & 1) * 4 + (g >> 1), i1 = i0 + 2;
           const int e0 = ((nq * 2 + w) * 8 + i0) * 64 + col, e1 = ((nq * 2 + w) * 8 + i1) * 64 + col;
           if (m0 + g * 64 < M && n0 + c < N) {
-            const size_t prow = (size_t)(m0 / 64 + g) * N + n0 + c;
+            const size_t prow = (size_t)((MODE == 2 ? blockIdx.z * cd.prc : 0) + m0 / 64 + g) * N + n0 + c;
             if (e.colsum) e.colsum[prow] = red[e0] + red[e1];
             if (e.colsq) e.colsq[prow] = red[2048 + e0] + red[2048 + e1];
           }
@@ -1033,6 +1105,11 @@ static void launch_cfg(int cfg, dim3 grid_yz, int M, int N, int K, const unsigne
     }
   }
   if constexpr (MODE == 1 || MODE == 2) {
+    if (cfg == 5) {
+      launch_one<MODE, TA, TB, F, 256, 8, 256>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
+                                               d, stream);
+      return;
+    }
     if (cfg == 4) {
       launch_one<MODE, TA, TB, F, 256, 2, 64>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
                                               d, stream);
@@ -1120,6 +1197,22 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
 #undef DTFX_GB
 }
 
+// Convolutions on the 8-phase 256x256 schedule (gathered A rows, gemm_bf16_kernel): when the
+// plain-GEMM tile model picks it for the GEMM shape, the source channels are a multiple of 64
+// (a K tile stays inside one tap), the source tensor is < 2 GB (32-bit buffer offsets) and the
+// reduction has >= 4 K tiles: with 1-2 tiles nothing overlaps the one resident block's loads
+// and epilogue (ResNet-50 layer1 1x1 dgrads with the fused BN backward, K = 64 / 128: 377 ->
+// 525 us and 426 -> 548 us on the 8-phase tile; layer3 3x3 forward, K = 2304: 120 -> 74 us).
+// DTFX_CONV_PH8=0 keeps every convolution on the 128x128 / 256x64 tiles (A/B runs).
+static bool conv_ph8(int M, int N, int K, int zdim, int src_ch, long long src_elems) {
+  static const bool on = [] {
+    const char* v = getenv("DTFX_CONV_PH8");
+    return v ? atoi(v) != 0 : true;
+  }();
+  return on && K >= 4 * gb::BK && src_ch % 64 == 0 && src_elems * 2 < 0x7fffffffLL &&
+         choose_cfg(M, N, zdim, 0) == 5;
+}
+
 // Convolution launcher (modes in the ConvDesc comment above).
 //  fwd  : x [N*H*W][C], w [Cout][ldw >= ceil64(KH*KW*C)] (zero-padded), y [N*OH*OW][Cout]
 //         optional fused BatchNorm statistics: colsum / colsq = per-wave-slab partial rows
@@ -1167,7 +1260,8 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
         return;
       }
     }
-    launch_cfg<1, false, true, false>(choose_cfg(M, Nn, 1, 1), dim3(1, 1, 1), M, Nn, K,
+    const int cfg1 = conv_ph8(M, Nn, K, 1, C, (long long)N * H * W * C) ? 5 : choose_cfg(M, Nn, 1, 1);
+    launch_cfg<1, false, true, false>(cfg1, dim3(1, 1, 1), M, Nn, K,
                                       (const unsigned short*)a, 0, (const unsigned short*)b, ldw,
                                       out, Cout, e, 0LL, 0LL, 0LL, d, stream);
   } else if (mode == 2) {
@@ -1182,7 +1276,8 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
       e.act_grad = 2;
     }
     if (bn_x) {
-      if (!colsum || !colsq || !bn_mean || !bn_rstd || ((uintptr_t)bn_x & 15))
+      if (!colsum || !colsq || !bn_mean || !bn_rstd ||
+          (((uintptr_t)bn_x | (uintptr_t)bn_mean | (uintptr_t)bn_rstd) & 15))
         throw std::runtime_error("conv_bf16: fused BN statistics need colsum, colsq, mean, rstd");
       e.bn_x = (const unsigned short*)bn_x;
       e.bn_mean = bn_mean;
@@ -1200,8 +1295,10 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
       if (colsum) DTFX_HIP_CHECK(hipMemsetAsync(colsum, 0, bytes, stream));
       if (colsq) DTFX_HIP_CHECK(hipMemsetAsync(colsq, 0, bytes, stream));
     }
-    launch_cfg<2, false, false, false>(choose_cfg(M, Nn, s * s, 2), dim3(1, 1, s * s), M, Nn, K,
-                                       (const unsigned short*)a, 0, (const unsigned short*)b, 0,
+    const int cfg2 = conv_ph8(M, Nn, ((KH + s - 1) / s) * ((KW + s - 1) / s) * Cout, s * s, Cout, (long long)N * OH * OW * Cout)
+                         ? 5 : choose_cfg(M, Nn, s * s, 2);
+    launch_cfg<2, false, false, false>(cfg2, dim3(1, 1, s * s), M, Nn, K,
+                                       (const unsigned short*)a, 0, (const unsigned short*)b, d.wld,
                                        out, C, e, 0LL, 0LL, 0LL, d, stream);
   } else if (mode == 3) {
     if (residual || colsum || colsq || relu_y || bn_x)

@@ -24,6 +24,8 @@ CONVS = [  # N, H, W, C, Cout, k, stride, pad
     (2, 13, 15, 128, 64, 1, 2, 0),   # 1x1 stride 2: three of four classes have no taps
     (4, 64, 64, 64, 1024, 1, 1, 0),  # 1x1 stride 1 on the 8-phase plain GEMM
     (3, 60, 60, 128, 1024, 1, 1, 0),  # same, M = 10800: ragged 256-row block and 64-row slab
+    (3, 60, 60, 64, 1024, 3, 1, 1),  # 3x3 forward on the 8-phase gather (ragged M)
+    (4, 64, 64, 1024, 256, 3, 2, 1),  # stride-2 dgrad classes on the 8-phase gather
 ]
 
 
@@ -63,6 +65,8 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, W, C, Co, k, s, p):
     (2, 14, 14, 128, 128, 3, 2, 1, True),  # stride-2 phase classes, one partial block each
     (2, 15, 13, 64, 128, 3, 2, 1, True),   # unequal classes: zeroed partial rows
     (2, 13, 15, 128, 64, 1, 2, 0, True),   # empty classes: residual + mask only
+    (4, 64, 64, 1024, 256, 3, 2, 1, True),  # 8-phase dgrad: per-slab BN columns, class rows
+    (4, 64, 64, 1024, 256, 1, 1, 0, True),  # 8-phase 1x1 dgrad
 ])
 def test_conv_dgrad_fused_batchnorm_backward(gpu, N, H, W, C, Co, k, s, p, with_res):
     """dgrad with BatchNorm backward's reductions in its epilogue (+ shortcut gradient, ReLU
