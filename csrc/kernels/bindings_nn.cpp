@@ -11,11 +11,13 @@ void gemm_bf16_set_cfg(int);
 void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const void*, int, void*,
                       int, float, float, const float*, int, const void*, void*, int, const void*,
                       int, int, int, int, long long, long long, long long,
-                      float*, hipStream_t);
+                      float*, hipStream_t, float*, long long);
 void colsum_bf16_launch(const void*, int, int, int, float*, float, hipStream_t);
+long long gemm_bf16_ws_floats(bool, bool, int, int, int, int, float);
+long long conv_wgrad_ws_floats(int, int, int, int, int, int, int, int, int);
 void conv_bf16_launch(int, int, int, int, int, int, int, int, int, int, const void*, const void*, int,
                       void*, float, const void*, float*, float*, int, hipStream_t, const void*,
-                      const void*, const float*, const float*);
+                      const void*, const float*, const float*, float*, long long);
 void bn_bwd_apply_launch(long long, int, const void*, const void*, const float*, const float*,
                          const float*, const float*, const float*, void*, hipStream_t);
 void bn_finalize_launch(int, long long, const float*, const float*, float, float*, float*, float*,
@@ -68,19 +70,25 @@ void register_nn(py::module_& m) {
                         uintptr_t B, int ldb, uintptr_t C, int ldc, float alpha, float beta,
                         uintptr_t bias, int act, uintptr_t aux_in, uintptr_t aux_out, int ld_aux,
                         uintptr_t residual, int ld_res, int act_grad, int splitk, int batch, long long sA,
-                        long long sB, long long sC, uintptr_t colsum, uintptr_t s) {
+                        long long sB, long long sC, uintptr_t colsum, uintptr_t s, uintptr_t ws,
+                        long long ws_floats) {
     dtfx::gemm_bf16_launch(ta, tb, out_f32, M, N, K, P<const void>(A), lda, P<const void>(B), ldb,
                            P<void>(C), ldc, alpha, beta, P<const float>(bias), act,
                            P<const void>(aux_in), P<void>(aux_out), ld_aux, P<const void>(residual),
                            ld_res, act_grad, splitk, batch, sA, sB, sC,
-                           P<float>(colsum), S(s));
+                           P<float>(colsum), S(s), P<float>(ws), ws_floats);
   }, py::arg("ta"), py::arg("tb"), py::arg("out_f32"), py::arg("M"), py::arg("N"), py::arg("K"),
      py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"),
      py::arg("alpha") = 1.f, py::arg("beta") = 0.f, py::arg("bias") = 0, py::arg("act") = 0,
      py::arg("aux_in") = 0, py::arg("aux_out") = 0, py::arg("ld_aux") = 0,
      py::arg("residual") = 0, py::arg("ld_res") = 0, py::arg("act_grad") = 0,
      py::arg("splitk") = 0, py::arg("batch") = 1, py::arg("sA") = 0, py::arg("sB") = 0,
-     py::arg("sC") = 0, py::arg("colsum") = 0, py::arg("stream") = 0);
+     py::arg("sC") = 0, py::arg("colsum") = 0, py::arg("stream") = 0, py::arg("ws") = 0,
+     py::arg("ws_floats") = 0);
+  m.def("gemm_bf16_ws_floats", &dtfx::gemm_bf16_ws_floats,
+        "f32 elements of split-K workspace gemm_bf16 would use (0: no split-K)");
+  m.def("conv_wgrad_ws_floats", &dtfx::conv_wgrad_ws_floats,
+        "f32 elements of split-K workspace a conv weight gradient would use (0: no split-K)");
   m.def("colsum_bf16", [](uintptr_t G, int M, int N, int ldg, uintptr_t out, float beta,
                           uintptr_t s) {
     dtfx::colsum_bf16_launch(P<const void>(G), M, N, ldg, P<float>(out), beta, S(s));
@@ -146,17 +154,18 @@ void register_nn(py::module_& m) {
                         int pad, uintptr_t a, uintptr_t b, int ldw, uintptr_t out, float beta,
                         uintptr_t residual, uintptr_t colsum, uintptr_t colsq, int splitk,
                         uintptr_t s, uintptr_t relu_y, uintptr_t bn_x, uintptr_t bn_mean,
-                        uintptr_t bn_rstd) {
+                        uintptr_t bn_rstd, uintptr_t ws, long long ws_floats) {
     dtfx::conv_bf16_launch(mode, N, H, W, C, Cout, KH, KW, stride, pad, P<const void>(a),
                            P<const void>(b), ldw, P<void>(out), beta, P<const void>(residual),
                            P<float>(colsum), P<float>(colsq), splitk, S(s),
                            P<const void>(relu_y), P<const void>(bn_x), P<const float>(bn_mean),
-                           P<const float>(bn_rstd));
+                           P<const float>(bn_rstd), P<float>(ws), ws_floats);
   }, py::arg("mode"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Cout"),
      py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("a"), py::arg("b"),
      py::arg("ldw"), py::arg("out"), py::arg("beta"), py::arg("residual"), py::arg("colsum"),
      py::arg("colsq"), py::arg("splitk"), py::arg("stream"), py::arg("relu_y") = 0,
-     py::arg("bn_x") = 0, py::arg("bn_mean") = 0, py::arg("bn_rstd") = 0);
+     py::arg("bn_x") = 0, py::arg("bn_mean") = 0, py::arg("bn_rstd") = 0, py::arg("ws") = 0,
+     py::arg("ws_floats") = 0);
   m.def("bn_bwd_apply", [](long long M, int C, uintptr_t de, uintptr_t x, uintptr_t mean,
                            uintptr_t rstd, uintptr_t g, uintptr_t sdy, uintptr_t sdyxh,
                            uintptr_t dx, uintptr_t s) {

@@ -345,6 +345,10 @@ struct GemmEpi {
   const unsigned short* bn_x;
   const float* bn_mean;
   const float* bn_rstd;
+  // split-K partials: with ws set, split s writes its tile to ws[s][M][N] with plain stores and
+  // splitk_reduce folds them into C afterwards (f32 atomics run at the memory side, ~1.3 TB/s
+  // chip-wide: a 512-block split-K wave adds ~34 MB, ~26 us, against ~6 us of plain stores)
+  float* ws;
 };
 
 // Tile BM_ x BN_ (128x128: 4 waves of 64x64, 2 blocks/CU; 256x128: 8 waves of 64x64;
@@ -792,7 +796,8 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
       for (int rr = 0; rr < 32; ++rr) {
         const int m = m0 + r0 + rr;
         if (m < M && n < N && lane < SLW)
-          unsafeAtomicAdd((float*)Cv + (size_t)m * ldc + n, e.alpha * ep[rr * EP_LD + lane]);
+          if (e.ws) e.ws[((size_t)split * M + m) * N + n] = e.alpha * ep[rr * EP_LD + lane];
+          else unsafeAtomicAdd((float*)Cv + (size_t)m * ldc + n, e.alpha * ep[rr * EP_LD + lane]);
       }
       __builtin_amdgcn_wave_barrier();
       continue;
@@ -1124,12 +1129,91 @@ static void launch_cfg(int cfg, dim3 grid_yz, int M, int N, int K, const unsigne
     launch_one<MODE, TA, TB, F, 128, 2>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC, d, stream);
 }
 
+// C[m][n] = beta * C[m][n] + sum_s ws[s][m][n] (N % 4 == 0, C rows 16-byte aligned).  A block
+// covers 256 / L float4 columns with L split lanes each (L = 1..16, a power of two): lane l sums
+// splits l, l + L, ... (each wave reads contiguous 1 KB runs of one plane), then the L partial
+// sums meet in LDS.  (A plain loop over S per thread ran the ResNet-50 layer1 weight gradients,
+// S = 102-256 splits of a 64 x 576 output, 3x slower than the atomics it replaced.)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S, int L,
+                                                            const float* __restrict__ ws,
+                                                            float* __restrict__ C, int ldc,
+                                                            float beta) {
+  __shared__ f32x4 red[256];
+  const int nq = N >> 2, cpb = 256 / L;
+  const int col = threadIdx.x % cpb, sl = threadIdx.x / cpb;
+  const long long i = (long long)blockIdx.x * cpb + col, total = (long long)M * nq;
+  const bool live = i < total;
+  const int m = live ? (int)(i / nq) : 0, n = live ? (int)(i - (long long)m * nq) * 4 : 0;
+  const size_t plane = (size_t)M * N;
+  const float* w = ws + (size_t)m * N + n;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  if (live) {
+#pragma unroll 4
+    for (int s = sl; s < S; s += L) a += *(const f32x4*)(w + s * plane);
+  }
+  red[threadIdx.x] = a;
+  __syncthreads();
+  if (sl == 0 && live) {
+    for (int j = 1; j < L; ++j) a += red[j * cpb + col];
+    float* c = C + (size_t)m * ldc + n;
+    if (beta != 0.f) a += beta * *(const f32x4*)c;
+    *(f32x4*)c = a;
+  }
+}
+
+// Split-K through the partial workspace when it fits (else f32 atomics into a pre-zeroed /
+// accumulating C).  Returns true when the caller must NOT pre-zero C.
+static bool splitk_ws_ok(float* ws, long long ws_floats, int splitk, int M, int N, void* C, int ldc) {
+  return ws && splitk > 1 && N % 4 == 0 && ldc % 4 == 0 && ((uintptr_t)C & 15) == 0 &&
+         ((uintptr_t)ws & 15) == 0 && (long long)splitk * M * N <= ws_floats;
+}
+static void splitk_reduce(int M, int N, int S, const float* ws, float* C, int ldc, float beta,
+                          hipStream_t stream) {
+  int L = 1;
+  while (L < S && L < 16) L <<= 1;
+  const long long n = (long long)M * (N / 4), cpb = 256 / L;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + cpb - 1) / cpb)), dim3(256), 0,
+                     stream, M, N, S, L, ws, C, ldc, beta);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// Split-K factor of a GEMM (splitk <= 0: auto) and its tile configuration.
+static int gemm_splitk(bool ta, bool out_f32, int M, int N, int K, int splitk, int batch, float beta,
+                       bool plain_epilogue, int* cfg_out) {
+  const int nkt = K / gb::BK;
+  const bool auto_split = splitk <= 0;
+  const int cfg = choose_cfg(M, N, batch * (auto_split ? 1 : splitk), 0, ta);
+  *cfg_out = cfg;
+  if (!auto_split) return splitk;
+  const int bm = cfg == 0 ? 128 : 256, bn = (cfg == 3 || cfg == 5) ? 256 : cfg == 6 ? 192 : 128;
+  const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  // Fill the 256 CUs when the output has few tiles and K is deep: the largest split with
+  // tiles * splitk <= resident block slots (cfg 0: 2 blocks/CU x 256 CUs; else 1/CU), ONE
+  // wave.  Measured on the BERT-base weight gradients (tools/gemm_sweep.py): 144 tiles x 3 =
+  // 432 blocks 110 us vs x 2 (288, unbalanced) 146 us and x 4 (576, a second partial wave)
+  // 154 us; 108 x 4 and 36 x 12 likewise the fastest of 1..16.
+  if (batch == 1 && out_f32 && plain_epilogue && (beta == 0.f || beta == 1.f)) {
+    const int slots = cfg == 0 ? 512 : 256;
+    if (tiles < slots / 2) return std::max(1, std::min(slots / tiles, nkt / 8));
+  }
+  return 1;
+}
+
+// f32 elements of the split-K partial workspace gemm_bf16_launch can use for this GEMM (0: no
+// split-K), for callers that provide one.
+long long gemm_bf16_ws_floats(bool ta, bool out_f32, int M, int N, int K, int splitk, float beta) {
+  int cfg;
+  const int s = gemm_splitk(ta, out_f32, M, N, (K + gb::BK - 1) / gb::BK * gb::BK, splitk, 1, beta,
+                            true, &cfg);
+  return s > 1 ? (long long)s * M * N : 0;
+}
+
 void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const void* A, int lda,
                       const void* B, int ldb, void* C, int ldc, float alpha, float beta,
                       const float* bias, int act, const void* aux_in, void* aux_out, int ld_aux,
                       const void* residual, int ld_res, int act_grad, int splitk, int batch,
                       long long sA, long long sB, long long sC, float* colsum,
-                      hipStream_t stream) {
+                      hipStream_t stream, float* ws, long long ws_floats) {
   if (M <= 0 || N <= 0 || batch <= 0) return;
   if (batch > 1 && (bias || aux_in || aux_out || residual || colsum))
     throw std::runtime_error("gemm_bf16: batched GEMM supports alpha/beta/act epilogues only");
@@ -1148,35 +1232,25 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
     throw std::runtime_error("gemm_bf16: residual must be 16-byte aligned with ld_res % 8 == 0");
   if (bias && ((uintptr_t)bias & 15)) throw std::runtime_error("gemm_bf16: bias must be 16-byte aligned");
   if (act_grad && !aux_in) throw std::runtime_error("gemm_bf16: act_grad needs aux_in");
-  const int nkt = K / gb::BK;
-  const bool auto_split = splitk <= 0;
-  const int cfg = choose_cfg(M, N, batch * (auto_split ? 1 : splitk), 0, ta);
-  const int bm = cfg == 0 ? 128 : 256, bn = (cfg == 3 || cfg == 5) ? 256 : cfg == 6 ? 192 : 128;
-  const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
-  if (auto_split) {  // fill the 256 CUs when the output has few tiles and K is deep
-    splitk = 1;
-    // Fill the resident block slots in ONE wave: the largest split with tiles * splitk <=
-    // slots (cfg 0: 2 blocks/CU x 256 CUs; else 1/CU).  Measured on the BERT-base weight
-    // gradients (tools/gemm_sweep.py): 144 tiles x 3 = 432 blocks 110 us vs x 2 (288,
-    // unbalanced) 146 us and x 4 (576, a second partial wave) 154 us; 108 x 4 and 36 x 12
-    // likewise the fastest of 1..16.
-    if (batch == 1 && out_f32 && !colsum && !bias && !act && !act_grad && !residual && !aux_out && (beta == 0.f || beta == 1.f)) {
-      const int slots = cfg == 0 ? 512 : 256;
-      if (tiles < slots / 2) splitk = std::max(1, std::min(slots / tiles, nkt / 8));
-    }
-  }
+  const bool plain = !colsum && !bias && !act && !act_grad && !residual && !aux_out;
+  int cfg;
+  splitk = gemm_splitk(ta, out_f32, M, N, K, splitk, batch, beta, plain, &cfg);
   if (splitk > 1) {
     if (batch > 1) throw std::runtime_error("gemm_bf16: split-K with batch > 1 is not supported");
     if (!out_f32 || bias || act || act_grad || residual || aux_out || colsum ||
         (beta != 0.f && beta != 1.f))
       throw std::runtime_error("gemm_bf16: split-K supports f32 output with alpha and beta in {0,1} only");
-    if (beta == 0.f) {
+    if (splitk_ws_ok(ws, ws_floats, splitk, M, N, C, ldc)) {
+      // (C is only read by the reduce: nothing to zero)
+    } else if (beta == 0.f) {
       if (ldc == N) DTFX_HIP_CHECK(hipMemsetAsync(C, 0, sizeof(float) * (size_t)M * N, stream));
       else DTFX_HIP_CHECK(hipMemset2DAsync(C, sizeof(float) * ldc, 0, sizeof(float) * N, M, stream));
     }
   }
   GemmEpi e{alpha, beta, bias, act, (const unsigned short*)aux_in, (unsigned short*)aux_out,
             ld_aux, (const unsigned short*)residual, ld_res, act_grad, colsum, nullptr, 0};
+  const bool use_ws = splitk > 1 && splitk_ws_ok(ws, ws_floats, splitk, M, N, C, ldc);
+  if (use_ws) e.ws = ws;
   const dim3 gyz(1, splitk, batch);
   auto* Au = (const unsigned short*)A;
   auto* Bu = (const unsigned short*)B;
@@ -1184,6 +1258,7 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   if (ta == TA_ && tb == TB_ && out_f32 == F_) {                                               \
     launch_cfg<0, TA_, TB_, F_>(cfg, gyz, M, N, K, Au, lda, Bu, ldb, C, ldc, e, sA, sB, sC,    \
                                 ConvDesc{}, stream);                                           \
+    if (use_ws) splitk_reduce(M, N, splitk, ws, (float*)C, ldc, beta, stream);                 \
     return;                                                                                    \
   }
   DTFX_GB(false, true, false)
@@ -1213,6 +1288,20 @@ static bool conv_ph8(int M, int N, int K, int zdim, int src_ch, long long src_el
          choose_cfg(M, N, zdim, 0) == 5;
 }
 
+// Split-K of a conv weight gradient (M = Cout, N = KH*KW*C, K = pixels): one wave of the 512
+// resident 128x128 slots (see gemm_splitk)
+static int conv_wgrad_splitk(int M, int Nn, int K) {
+  const int tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
+  const int nkt = (K + 63) / 64;
+  return tiles < 256 ? std::max(1, std::min(512 / tiles, nkt / 4)) : 1;
+}
+long long conv_wgrad_ws_floats(int N, int H, int W, int C, int Cout, int KH, int KW, int stride,
+                               int pad) {
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  const int Nn = KH * KW * C, s = conv_wgrad_splitk(Cout, Nn, N * OH * OW);
+  return s > 1 ? (long long)s * Cout * Nn : 0;
+}
+
 // Convolution launcher (modes in the ConvDesc comment above).
 //  fwd  : x [N*H*W][C], w [Cout][ldw >= ceil64(KH*KW*C)] (zero-padded), y [N*OH*OW][Cout]
 //         optional fused BatchNorm statistics: colsum / colsq = per-wave-slab partial rows
@@ -1227,7 +1316,7 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
                       int pad, const void* a, const void* b, int ldw, void* out, float beta,
                       const void* residual, float* colsum, float* colsq, int splitk,
                       hipStream_t stream, const void* relu_y, const void* bn_x,
-                      const float* bn_mean, const float* bn_rstd) {
+                      const float* bn_mean, const float* bn_rstd, float* ws, long long ws_floats) {
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   if (C % 8 || Cout % 8) throw std::runtime_error("conv_bf16: channel counts must be multiples of 8");
   if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) & 15)
@@ -1304,22 +1393,20 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
     if (residual || colsum || colsq || relu_y || bn_x)
       throw std::runtime_error("conv_bf16: wgrad has no epilogue options");
     M = Cout; Nn = KH * KW * C; K = N * OH * OW;
-    const int tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
-    const int nkt = (K + 63) / 64;
-    if (splitk <= 0) {
-      splitk = 1;  // one wave of the 512 resident 128x128 slots (see gemm_bf16_launch)
-      if (tiles < 256) splitk = std::max(1, std::min(512 / tiles, nkt / 4));
-    }
+    if (splitk <= 0) splitk = conv_wgrad_splitk(M, Nn, K);
     const int ldo = ldw > 0 ? ldw : Nn;  // dW row stride (the padded fwd weight layout)
     if (ldo < Nn || ldo % 8) throw std::runtime_error("conv_bf16: wgrad ld must be >= KH*KW*C, % 8");
     if (splitk > 1) {
       if (beta != 0.f && beta != 1.f) throw std::runtime_error("conv_bf16: split-K wgrad needs beta 0/1");
-      if (beta == 0.f)
+      if (beta == 0.f && !splitk_ws_ok(ws, ws_floats, splitk, M, Nn, out, ldo))
         DTFX_HIP_CHECK(hipMemset2DAsync(out, sizeof(float) * ldo, 0, sizeof(float) * Nn, M, stream));
     }
+    const bool use_ws = splitk > 1 && splitk_ws_ok(ws, ws_floats, splitk, M, Nn, out, ldo);
+    if (use_ws) e.ws = ws;
     launch_cfg<3, true, false, true>(choose_cfg(M, Nn, splitk, 3), dim3(1, splitk, 1), M, Nn, K,
                                      (const unsigned short*)a, Cout, (const unsigned short*)b, 0,
                                      out, ldo, e, 0LL, 0LL, 0LL, d, stream);
+    if (use_ws) splitk_reduce(M, Nn, splitk, ws, (float*)out, ldo, beta, stream);
   } else {
     throw std::runtime_error("conv_bf16: mode must be 1 (fwd), 2 (dgrad) or 3 (wgrad)");
   }

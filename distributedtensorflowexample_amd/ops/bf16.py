@@ -10,9 +10,14 @@ worker.py:50-53); they serve BASELINE.json's ResNet-50 / BERT-base configs.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._ext import hip, ptr, stream_handle
+
+# split-K partials through a workspace + reduce pass (DTFX_SPLITK_WS=0: f32 atomics into the output)
+_SPLITK_WS = os.environ.get("DTFX_SPLITK_WS", "1") != "0"
 
 ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2}
 
@@ -129,12 +134,21 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
                                    colsum.numel() == N and colsum.is_contiguous()):
         raise ValueError("gemm_bf16: colsum must be a contiguous f32 GPU vector of N elements")
     aux = aux_in if aux_in is not None else aux_out
+    ws, nws = None, 0
+    plain = (bias is None and act_i == 0 and ag_i == 0 and residual is None and aux_out is None
+             and colsum is None)
+    if out.dtype == torch.float32 and plain and _SPLITK_WS:
+        # split-K partials go to a workspace and one reduce pass (plain stores instead of f32
+        # atomics, which run at the memory side at ~1.3 TB/s chip-wide)
+        nws = hip().gemm_bf16_ws_floats(bool(trans_a), True, M, N, K, int(splitk), float(beta))
+        if nws:
+            ws = torch.empty(nws, device=a.device, dtype=torch.float32)
     hip().gemm_bf16(bool(trans_a), bool(trans_b), out.dtype == torch.float32, M, N, K,
                     ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(out), out.stride(0),
                     float(alpha), float(beta), ptr(bias), act_i, ptr(aux_in), ptr(aux_out),
                     aux.stride(0) if aux is not None else 0, ptr(residual),
                     residual.stride(0) if residual is not None else 0, ag_i, int(splitk),
-                    colsum=ptr(colsum), stream=stream_handle())
+                    colsum=ptr(colsum), stream=stream_handle(), ws=ptr(ws), ws_floats=nws)
     return out
 
 

@@ -11,10 +11,15 @@ references of the same math.  North-star config 4 of BASELINE.json.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
 from ._ext import hip, ptr, stream_handle
+
+# split-K partials through a workspace + reduce pass (DTFX_SPLITK_WS=0: f32 atomics into the output)
+_SPLITK_WS = os.environ.get("DTFX_SPLITK_WS", "1") != "0"
 
 BF16 = torch.bfloat16
 
@@ -140,8 +145,11 @@ def conv_wgrad(dy, x, dw, KH, KW, stride, pad, beta=1.0):
         k = KH * KW * C
         dw[:, :k] = g + (beta * dw[:, :k] if beta else 0)
         return dw
+    # split-K partials through a workspace + one reduce pass instead of f32 atomics
+    nws = hip().conv_wgrad_ws_floats(N, H, W, C, Cout, KH, KW, stride, pad) if _SPLITK_WS else 0
+    ws = torch.empty(nws, device=dy.device) if nws else None
     hip().conv_bf16(3, N, H, W, C, Cout, KH, KW, stride, pad, ptr(dy), ptr(x), dw.stride(0),
-                    ptr(dw), float(beta), 0, 0, 0, 0, stream_handle())
+                    ptr(dw), float(beta), 0, 0, 0, 0, stream_handle(), ws=ptr(ws), ws_floats=nws)
     return dw
 
 
