@@ -19,12 +19,18 @@ tail -1 "$OUT/bench_bert.json" | cut -c 1-180; tail -1 "$OUT/bench_bert512.json"
 step resnet
 timeout -k 10 200 python bench.py --model resnet50 > "$OUT/bench_resnet.json" 2>&1 || exit 1
 tail -1 "$OUT/bench_resnet.json" | cut -c 1-180
+timeout -k 10 240 python -u tools/probes/resnet_layers.py > "$OUT/resnet_layers.jsonl" 2>&1 || exit 1
+tail -1 "$OUT/resnet_layers.jsonl"
 step prof
 cd /tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/mprof" -o run -- python "$R/bench.py" --steps 2000 --warmup 200 > "$OUT/mprof.log" 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bprof" -o run -- python "$R/bench.py" --model bert --steps 6 --warmup 3 > "$OUT/bprof.log" 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rprof" -o run -- python "$R/bench.py" --model resnet50 --steps 6 --warmup 3 > "$OUT/rprof.log" 2>&1 || exit 1
 python "$R/tools/prof_summary.py" "$OUT/mprof/run_kernel_stats.csv" > "$OUT/mlp_kernel_stats.txt"
 python "$R/tools/prof_summary.py" "$OUT/bprof/run_kernel_stats.csv" > "$OUT/bert_kernel_stats.txt"
 python "$R/tools/trace_by_shape.py" "$OUT/bprof/run_kernel_trace.csv" 40 > "$OUT/bert_kernel_shapes.txt"
+python "$R/tools/prof_summary.py" "$OUT/rprof/run_kernel_stats.csv" > "$OUT/resnet_kernel_stats.txt"
+python "$R/tools/trace_by_shape.py" "$OUT/rprof/run_kernel_trace.csv" 40 > "$OUT/resnet_kernel_shapes.txt"
+rm -f "$OUT"/rprof/*trace.csv
 rm -f "$OUT"/mprof/*trace.csv
 head -4 "$OUT/mlp_kernel_stats.txt"; head -12 "$OUT/bert_kernel_shapes.txt"
