@@ -114,6 +114,11 @@ def main():
     ap.add_argument("--max_graph_steps", type=int, default=1024,
                     help="max steps per hipGraph (graphs are epoch-aligned)")
     ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--launch", choices=["auto", "graph", "host"], default="auto",
+                    help="MLP, 1 GPU: how the timed steps are issued -- graph = hipGraph "
+                         "replays, host = the C++ host loop launching both kernels of every "
+                         "step (no graph-submission latency), auto = time both on K steps "
+                         "before the timed region and use the faster")
     ap.add_argument("--comm", choices=["auto", "native", "xgmi", "torch"], default="auto",
                     help="native: the framework's C++ RCCL communicator (gloo control plane); "
                          "xgmi: one-shot peer-memory all-reduce over xGMI (small buckets); "
@@ -238,17 +243,59 @@ def main():
     barrier = _timing_barrier(rendezvous, local) if world > 1 else None
     use_graph = not a.no_graph
 
-    # hipGraph replay in the timed region.  (The C++ host loop, FusedMLPTrainer.run_launched,
-    # is 1 % faster per step once warm -- tools/probes/host_loop.py -- but in a fresh process
-    # its first direct launches ran 10.6-14.9 us/step at K = 20 against 10.0 for the graph.)
     tr.run(a.warmup, use_graph)
-    if use_graph:
+    # How the timed steps are issued.  A graph replay pays a fixed submission latency
+    # (t(n) = 17 us + 8.2 us * n, tools/probes/graph_fixed_cost.py) that a short timed region
+    # (the driver's K = 20) feels; the C++ host loop (FusedMLPTrainer.run_launched) launches
+    # the first kernel at once but pays a host launch per kernel.  In a fresh process the
+    # host loop's first launches were slow (10.6-14.9 us/step at K = 20 against 10.0 for the
+    # graph), so for K <= 200 both are warmed and timed here on K steps (untimed; the JSON
+    # records every step run before the clock as pre_timing_steps) and the faster is used.
+    # Longer regions take the graph: its fixed cost is amortised, while the host loop falls
+    # behind once the launch queue fills (K = 20000: 9.02 us/step against 8.15 for the graph,
+    # though both timed 8.3-8.4 on a 200-step probe).
+    launch = "graph" if use_graph else "eager"
+    a.launch_probe = None
+    if use_graph and tr.host_loop_ok and (a.launch == "host" or
+                                          (a.launch == "auto" and a.steps <= 200)):
+        kp = a.steps
+
+        def run_k(mode):
+            if mode == "host":
+                tr.run_launched(kp)
+            else:
+                tr.run(kp)
+            tr.flush()
+
+        probe = {"graph": [], "host": []}
+        tr.run_launched(max(a.warmup, 8))  # warm the direct-launch path
+        for _ in range(3 if a.launch == "auto" else 0):
+            for mode in probe:
+                if mode == "graph":
+                    tr.prepare(kp)
+                torch.cuda.synchronize()
+                t_0 = time.perf_counter()
+                run_k(mode)
+                torch.cuda.synchronize()
+                probe[mode].append((time.perf_counter() - t_0) * 1e6 / kp)
+                tr.run(1, use_graph=False)  # pending update again, as after the warmup
+        if a.launch == "host":
+            launch = "host"
+        else:
+            med = {m: sorted(v)[len(v) // 2] for m, v in probe.items()}
+            launch = min(med, key=med.get)
+            a.launch_probe = {m: round(v, 3) for m, v in med.items()}
+    if launch == "graph":
         tr.prepare(a.steps)
+    pre_steps = tr.global_step()
     if barrier:
         barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tr.run(a.steps, use_graph)
+    if launch == "host":
+        tr.run_launched(a.steps)
+    else:
+        tr.run(a.steps, use_graph)
     tr.flush()  # the last step's deferred update is part of the timed work
     torch.cuda.synchronize()
     if barrier:
@@ -297,12 +344,15 @@ def main():
                 "seq_len": None,
                 "parallelism": "dp%d" % world,
                 "comm": _comm_label(a) if (world > 1 or a.dp) else "none",
-                "hipgraph": use_graph,
+                "hipgraph": launch == "graph",
+                "launch": launch,
                 "engine": getattr(a, "engine_kind", "allreduce" if allreduce else "single"),
                 "launches_per_step": 2 if tr.pipelined else 3,
             },
             "comm_probe_us": getattr(a, "comm_probe", None),
             "engine_probe_us_per_step": getattr(a, "engine_probe", None),
+            "launch_probe_us_per_step": a.launch_probe,
+            "pre_timing_steps": pre_steps,
             "final_loss": round(loss, 5),
             "final_train_acc": round(acc, 4),
             "global_step": tr.global_step(),

@@ -149,7 +149,10 @@ class Worker:
         else:
             self.store.lookup()
         sync = bool(getattr(fl, "sync_replicas", False))
-        replicas = int(getattr(fl, "replicas_to_aggregate", 0) or 0) or int(fl.num_workers)
+        replicas = 0
+        if sync:  # default: one gradient from every worker per round
+            replicas = (int(getattr(fl, "replicas_to_aggregate", 0) or 0)
+                        or int(getattr(fl, "num_workers", 1)))
         log_every = int(getattr(fl, "log_every", 100))
         eval_every = int(getattr(fl, "eval_every", 10000))
         local_steps = 0
