@@ -1337,10 +1337,11 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
       const char* v = getenv("DTFX_CONV1X1_GEMM");
       return v ? atoi(v) : 1;
     }();
-    if (plain1x1 && KH == 1 && KW == 1 && stride == 1 && pad == 0 && C % 64 == 0) {
+    if (plain1x1 && KH == 1 && KW == 1 && stride == 1 && pad == 0 && C % 64 == 0 && C >= 256) {
       // a 1x1 stride-1 convolution is the plain GEMM y[M][Cout] = x[M][C] W[Cout][C]^T:
       // the 8-phase 256x256 tile when the time model picks it (partial statistic rows per
-      // 64-row slab, as above)
+      // 64-row slab, as above) and K >= 4 tiles (layer1 conv3, K = 64: 224 us on the 8-phase
+      // tile vs 194 on the 128x128 gather path; layer3 conv1, K = 1024: 40 vs 45 us)
       const int cfg = choose_cfg(M, Nn, 1, 0);
       if (cfg == 5) {
         launch_cfg<0, false, true, false>(cfg, dim3(1, 1, 1), M, Nn, K, (const unsigned short*)a, C,

@@ -22,8 +22,8 @@ CONVS = [  # N, H, W, C, Cout, k, stride, pad
     (2, 15, 13, 64, 128, 3, 2, 1),   # stride-2 dgrad: phase classes of unequal size
     (2, 14, 14, 64, 64, 3, 2, 1),    # stride-2 dgrad on the 256x64 tile
     (2, 13, 15, 128, 64, 1, 2, 0),   # 1x1 stride 2: three of four classes have no taps
-    (4, 64, 64, 64, 1024, 1, 1, 0),  # 1x1 stride 1 on the 8-phase plain GEMM
-    (3, 60, 60, 128, 1024, 1, 1, 0),  # same, M = 10800: ragged 256-row block and 64-row slab
+    (4, 64, 64, 256, 1024, 1, 1, 0),  # 1x1 stride 1 on the 8-phase plain GEMM
+    (3, 60, 60, 256, 1024, 1, 1, 0),  # same, M = 10800: ragged 256-row block and 64-row slab
     (3, 60, 60, 64, 1024, 3, 1, 1),  # 3x3 forward on the 8-phase gather (ragged M)
     (4, 64, 64, 1024, 256, 3, 2, 1),  # stride-2 dgrad classes on the 8-phase gather
 ]
