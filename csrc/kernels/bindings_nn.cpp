@@ -28,6 +28,9 @@ void bn_bwd_launch(long long, int, const void*, const void*, const void*, const 
                    const float*, int, float*, float*, float*, void*, void*, hipStream_t);
 long long bn_bwd_scratch_rows(long long, int);
 void colpart_reduce_launch(int, int, const float*, const float*, float*, float*, hipStream_t);
+bool stem_conv_applies(int, int, int, int, int, int, int, int);
+void stem_conv_fwd_launch(int, int, int, const void*, const void*, int, void*, float*, float*,
+                          hipStream_t);
 void maxpool_fwd_launch(int, int, int, int, const void*, void*, void*, hipStream_t);
 void maxpool_bwd_launch(int, int, int, int, const void*, const void*, void*, hipStream_t);
 void avgpool_fwd_launch(int, int, int, const void*, void*, hipStream_t);
@@ -193,6 +196,13 @@ void register_nn(py::module_& m) {
                         P<void>(dres), S(s));
   });
   m.def("bn_bwd_scratch_rows", &dtfx::bn_bwd_scratch_rows);
+  m.def("stem_conv_applies", &dtfx::stem_conv_applies,
+        "the ResNet stem kernel handles this conv (7x7/2, pad 3, 8 -> 64 channels, OH % 8, OW % 16)");
+  m.def("stem_conv_fwd", [](int N, int H, int W, uintptr_t x, uintptr_t w, int ldw, uintptr_t y,
+                            uintptr_t ps, uintptr_t pq, uintptr_t s) {
+    dtfx::stem_conv_fwd_launch(N, H, W, P<const void>(x), P<const void>(w), ldw, P<void>(y),
+                               P<float>(ps), P<float>(pq), S(s));
+  });
   m.def("colpart_reduce", [](int R, int C, uintptr_t ps, uintptr_t pq, uintptr_t os, uintptr_t oq,
                              uintptr_t s) {
     dtfx::colpart_reduce_launch(R, C, P<const float>(ps), P<const float>(pq), P<float>(os),

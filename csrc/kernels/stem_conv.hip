@@ -1,0 +1,181 @@
+// ResNet-50 stem convolution forward (7x7, stride 2, pad 3, 8 input channels -- the image's
+// 3 + 5 zero channels -- 64 output channels), NHWC bf16, with the BatchNorm statistics of the
+// output fused (partial rows, one per 32 output pixels, reduced by colpart_reduce).
+//
+// Why a kernel of its own: as an implicit GEMM (gemm_bf16.hip MODE 1, 256x64 tile) the stem
+// gathers every input pixel once per tap it feeds -- 49 taps x 16 B per output pixel through
+// L2 -- and ran 606 us at ResNet-50's 256x224x224 input (MI355X), against ~95 us of HBM
+// traffic (205 MB in, 411 MB out).  Here a persistent block keeps all 64 x 392 weights in LDS
+// for its whole life and, per 8 x 16-pixel output tile, stages the 21 x 37-pixel input patch
+// the tile reads ONCE (12 KB); the MFMA A fragments (16 output pixels x 4 taps x 8 channels)
+// are read from the patch at the tap's offset, so nothing is re-fetched per tap.
+//
+// MFMA v_mfma_f32_16x16x32_bf16: k-group kg = taps 4kg..4kg+3 x 8 channels (13 groups, taps
+// 49-51 zero weights); wave w owns output rows 2w, 2w+1 of the tile (2 x 16 pixels) x 64
+// channels = 2 x 4 accumulator tiles.
+#include "common.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace dtfx {
+namespace stem {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int KS = 7, STR = 2, PAD = 3, CIN = 8, COUT = 64;
+constexpr int TH = 8, TW = 16;                                  // output tile
+constexpr int PR = (TH - 1) * STR + KS, PC = (TW - 1) * STR + KS;  // 21 x 37 input patch
+constexpr int NKG = 13;                                        // k-groups of 4 taps
+constexpr int WP = 456;                                        // weight row pitch (bf16): 912 B
+constexpr int W_BYTES = COUT * WP * 2;                         // 58368
+constexpr int P_BYTES = 16384;  // patch (777 x 16 B) / output staging (4 waves x 32 px x 128 B)
+
+__device__ __forceinline__ unsigned short tobf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(unsigned short, b);
+}
+
+__global__ __launch_bounds__(256, 2) void stem_conv_fwd_kernel(
+    int N, int H, int W, int OH, int OW, const unsigned short* __restrict__ x,
+    const unsigned short* __restrict__ w, int ldw, unsigned short* __restrict__ y,
+    float* __restrict__ psum, float* __restrict__ psq) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* Ws = sm;
+  char* Ps = sm + W_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // weights, once: [64 co][448 k] -> 912-B rows (k >= 392 are the zero pad of the layout)
+  for (int i = tid; i < COUT * 56; i += 256) {
+    const int co = i / 56, c = i - co * 56;
+    *(bf16x8*)(Ws + co * WP * 2 + c * 16) = *(const bf16x8*)(w + (size_t)co * ldw + c * 8);
+  }
+  const int tiles_w = OW / TW, tiles_img = (OH / TH) * tiles_w;
+  const int tiles = N * tiles_img;
+  const int cl = lane & 15, g = lane >> 4;
+  // input patch of tile tt into registers (zero outside the image): 777 16-B pixels, 4 per
+  // thread -- issued one tile ahead, so the loads are in flight during the MFMAs
+  bf16x8 v[4];
+  auto load_patch = [&](int tt) {
+    const int n = tt / tiles_img, r = tt - n * tiles_img;
+    const int ih0 = (r / tiles_w) * TH * STR - PAD, iw0 = (r % tiles_w) * TW * STR - PAD;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = tid + 256 * k, pr = p / PC, pc = p - pr * PC;
+      const int ih = ih0 + pr, iw = iw0 + pc;
+      v[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (p < PR * PC && ih >= 0 && ih < H && iw >= 0 && iw < W)
+        v[k] = *(const bf16x8*)(x + (((size_t)n * H + ih) * W + iw) * CIN);
+    }
+  };
+  if (blockIdx.x < tiles) load_patch(blockIdx.x);
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int n = t / tiles_img, r = t - n * tiles_img;
+    const int oh0 = (r / tiles_w) * TH, ow0 = (r % tiles_w) * TW;
+    __syncthreads();  // the previous tile's output staging (same LDS) is done
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = tid + 256 * k;
+      if (p < PR * PC) *(bf16x8*)(Ps + p * 16) = v[k];
+    }
+    __syncthreads();
+    if (t + (int)gridDim.x < tiles) load_patch(t + gridDim.x);
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kg = 0; kg < NKG; ++kg) {
+      const int tap = 4 * kg + g, kh = tap / KS, kw = tap - kh * KS;
+      bf16x8 a[2], b[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {  // this lane's pixel: output row 2 wave + i, column cl
+        const int pr = (2 * wave + i) * STR + kh, pc = cl * STR + kw;
+        a[i] = tap < KS * KS ? *(const bf16x8*)(Ps + (pr * PC + pc) * 16)
+                             : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = *(const bf16x8*)(Ws + (16 * j + cl) * WP * 2 + (32 * kg + 8 * g) * 2);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    // BN statistics of the f32 values: lane (cl, g) holds channel 16 j + cl of pixels 4 g + r
+    const int prow = t * 4 + wave;  // one partial row per wave (32 pixels)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          s += acc[i][j][rr];
+          q += acc[i][j][rr] * acc[i][j][rr];
+        }
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      if (g == 0) {
+        psum[(size_t)prow * COUT + 16 * j + cl] = s;
+        psq[(size_t)prow * COUT + 16 * j + cl] = q;
+      }
+    }
+    __syncthreads();  // every wave is done reading the patch: reuse it for the output
+    char* st = Ps + wave * 4096;  // [32 px][64 co] bf16, 128-B rows (px = 16 i + column)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          *(unsigned short*)(st + (16 * i + 4 * g + rr) * 128 + (16 * j + cl) * 2) =
+              tobf(acc[i][j][rr]);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // 32 px x 8 chunks: 4 per lane, 16 B each, coalesced rows
+      const int e = lane + 64 * k, px = e >> 3, c = e & 7;
+      const int oh = oh0 + 2 * wave + (px >> 4), ow = ow0 + (px & 15);
+      *(bf16x8*)(y + (((size_t)n * OH + oh) * OW + ow) * COUT + c * 8) =
+          *(const bf16x8*)(st + px * 128 + c * 16);
+    }
+  }
+}
+
+}  // namespace stem
+
+// True when the stem kernel takes this convolution (the caller then sizes the partial
+// statistic rows as N * OH * OW / 32).
+bool stem_conv_applies(int H, int W, int C, int Cout, int KH, int KW, int stride, int pad) {
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  return C == stem::CIN && Cout == stem::COUT && KH == stem::KS && KW == stem::KS &&
+         stride == stem::STR && pad == stem::PAD && OH % stem::TH == 0 && OW % stem::TW == 0;
+}
+
+void stem_conv_fwd_launch(int N, int H, int W, const void* x, const void* w, int ldw, void* y,
+                          float* psum, float* psq, hipStream_t s) {
+  using namespace stem;
+  if (!stem_conv_applies(H, W, CIN, COUT, KS, KS, STR, PAD))
+    throw std::runtime_error("stem_conv: unsupported geometry");
+  if (ldw < 56 * 8 || ldw % 8 || (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) & 15))
+    throw std::runtime_error("stem_conv: weights need ld >= 448 (% 8), 16-B aligned tensors");
+  const int OH = (H + 2 * PAD - KS) / STR + 1, OW = (W + 2 * PAD - KS) / STR + 1;
+  const int tiles = N * (OH / TH) * (OW / TW);
+  const size_t lds = W_BYTES + P_BYTES;
+  static bool attr = false;
+  if (!attr) {
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)stem_conv_fwd_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int blocks = std::min(tiles, 2 * 256);  // persistent: two blocks per CU
+  hipLaunchKernelGGL(stem_conv_fwd_kernel, dim3(blocks), dim3(256), lds, s, N, H, W, OH, OW,
+                     (const unsigned short*)x, (const unsigned short*)w, ldw, (unsigned short*)y,
+                     psum, psq);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dtfx
