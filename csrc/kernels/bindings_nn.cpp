@@ -31,6 +31,8 @@ void colpart_reduce_launch(int, int, const float*, const float*, float*, float*,
 bool stem_conv_applies(int, int, int, int, int, int, int, int);
 void stem_conv_fwd_launch(int, int, int, const void*, const void*, int, void*, float*, float*,
                           hipStream_t);
+void stem_conv_wgrad_launch(int, int, int, const void*, const void*, float*, int, float,
+                            hipStream_t);
 void maxpool_fwd_launch(int, int, int, int, const void*, void*, void*, hipStream_t);
 void maxpool_bwd_launch(int, int, int, int, const void*, const void*, void*, hipStream_t);
 void avgpool_fwd_launch(int, int, int, const void*, void*, hipStream_t);
@@ -202,6 +204,11 @@ void register_nn(py::module_& m) {
                             uintptr_t ps, uintptr_t pq, uintptr_t s) {
     dtfx::stem_conv_fwd_launch(N, H, W, P<const void>(x), P<const void>(w), ldw, P<void>(y),
                                P<float>(ps), P<float>(pq), S(s));
+  });
+  m.def("stem_conv_wgrad", [](int N, int H, int W, uintptr_t x, uintptr_t dy, uintptr_t dw, int ldw,
+                              float beta, uintptr_t s) {
+    dtfx::stem_conv_wgrad_launch(N, H, W, P<const void>(x), P<const void>(dy), P<float>(dw), ldw,
+                                 beta, S(s));
   });
   m.def("colpart_reduce", [](int R, int C, uintptr_t ps, uintptr_t pq, uintptr_t os, uintptr_t oq,
                              uintptr_t s) {

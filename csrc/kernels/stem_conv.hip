@@ -145,6 +145,109 @@ __global__ __launch_bounds__(256, 2) void stem_conv_fwd_kernel(
   }
 }
 
+
+// Weight gradient dW[co][k] (+)= sum_p dy[p][co] * x_patch[p][k], k = (kh, kw, c): per
+// 8 x 16-pixel tile the dy tile (128 px x 64 co) and the input patch are staged once; the
+// GEMM is M = 64 co x N = 7 kh x 4 blocks of 16 (kw pairs x 8 channels: 16 bf16 contiguous in
+// a patch row, the 8th kw of the last block discarded) x K = 128 pixels.  Both operands are
+// k-strided (k = pixel), read with ds_read_b64_tr_b16 from per-lane row addresses (the
+// pixel -> patch offset is not a uniform stride).  Wave w owns n-blocks 7w..7w+6 x all 4
+// co blocks (28 accumulator tiles); a persistent block sums all its tiles in registers and
+// adds its 64 x 392 partial with one f32 atomic per element at the end.
+constexpr int DP = 144;  // dy tile row pitch (bytes)
+
+__device__ __forceinline__ bf16x8 tr_pair(const char* a0, const char* a1) {
+  typedef short bf16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) bf16x4 lds4;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)a0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)a1);
+  bf16x8 v;
+  v.lo = lo;
+  v.hi = hi;
+  return v;
+}
+
+__global__ __launch_bounds__(256, 1) void stem_conv_wgrad_kernel(
+    int N, int H, int W, int OH, int OW, const unsigned short* __restrict__ x,
+    const unsigned short* __restrict__ dy, float* __restrict__ dw, int ldw) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* Ds = sm;             // [128 px][64 co] bf16, 144-B rows
+  char* Ps = sm + 128 * DP;  // [21][37] pixels x 8 channels
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_w = OW / TW, tiles_img = (OH / TH) * tiles_w;
+  const int tiles = N * tiles_img;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  f32x4 acc[4][7];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // dy tile and input patch of tile tt into registers, issued one tile ahead (in flight
+  // during the previous tile's MFMAs)
+  bf16x8 dv[4], pv[4];
+  auto load_tile = [&](int tt) {
+    const int n = tt / tiles_img, r = tt - n * tiles_img;
+    const int oh0 = (r / tiles_w) * TH, ow0 = (r % tiles_w) * TW;
+    const int ih0 = oh0 * STR - PAD, iw0 = ow0 * STR - PAD;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // dy tile: 128 px x 8 chunks; patch: 777 pixels
+      const int e = tid + 256 * k, px = e >> 3, c = e & 7;
+      dv[k] = *(const bf16x8*)(dy + (((size_t)n * OH + oh0 + (px >> 4)) * OW + ow0 + (px & 15)) * COUT + c * 8);
+      const int pr = e / PC, pc = e - pr * PC, ih = ih0 + pr, iw = iw0 + pc;
+      pv[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (e < PR * PC && ih >= 0 && ih < H && iw >= 0 && iw < W)
+        pv[k] = *(const bf16x8*)(x + (((size_t)n * H + ih) * W + iw) * CIN);
+    }
+  };
+  if (blockIdx.x < tiles) load_tile(blockIdx.x);
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    __syncthreads();  // the previous tile's fragment reads are done
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = tid + 256 * k, px = e >> 3, c = e & 7;
+      *(bf16x8*)(Ds + px * DP + c * 16) = dv[k];
+      if (e < PR * PC) *(bf16x8*)(Ps + e * 16) = pv[k];
+    }
+    __syncthreads();
+    if (t + (int)gridDim.x < tiles) load_tile(t + gridDim.x);
+#pragma unroll
+    for (int kg = 0; kg < 4; ++kg) {  // 32 pixels = tile rows 2 kg, 2 kg + 1
+      const int k0 = 32 * kg + 8 * g + q, k1 = k0 + 4;  // this lane's two pixel rows
+      bf16x8 a[4], b[7];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)  // A: (co 16 i + ..., pixel) from the dy tile
+        a[i] = tr_pair(Ds + k0 * DP + (16 * i + 4 * p4) * 2, Ds + k1 * DP + (16 * i + 4 * p4) * 2);
+      const int pb0 = ((k0 >> 4) * STR) * PC + (k0 & 15) * STR;  // patch pixel of (kh 0, kw 0)
+      const int pb1 = ((k1 >> 4) * STR) * PC + (k1 & 15) * STR;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {  // B: (k = kh, kw0 + n / 8, c = n % 8) from the patch
+        const int nb = 7 * wave + j, kh = nb >> 2, kw0 = 2 * (nb & 3);
+        const int off = (kh * PC + kw0) * 16 + 4 * p4 * 2;
+        b[j] = tr_pair(Ps + pb0 * 16 + off, Ps + pb1 * 16 + off);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 7; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // lane (cl, g): column n = cl of block nb, co rows 16 i + 4 g + r
+  const int cl = lane & 15;
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int nb = 7 * wave + j, kh = nb >> 2, kw = 2 * (nb & 3) + (cl >> 3), c = cl & 7;
+    if (kw >= KS) continue;
+    const int k = (kh * KS + kw) * CIN + c;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        unsafeAtomicAdd(dw + (size_t)(16 * i + 4 * g + rr) * ldw + k, acc[i][j][rr]);
+  }
+}
+
 }  // namespace stem
 
 // True when the stem kernel takes this convolution (the caller then sizes the partial
@@ -153,6 +256,28 @@ bool stem_conv_applies(int H, int W, int C, int Cout, int KH, int KW, int stride
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   return C == stem::CIN && Cout == stem::COUT && KH == stem::KS && KW == stem::KS &&
          stride == stem::STR && pad == stem::PAD && OH % stem::TH == 0 && OW % stem::TW == 0;
+}
+
+// dw (f32 [64][ldw], the first 392 columns) (+)= the stem's weight gradient: beta 1
+// accumulates, beta 0 overwrites.
+void stem_conv_wgrad_launch(int N, int H, int W, const void* x, const void* dy, float* dw, int ldw,
+                            float beta, hipStream_t s) {
+  using namespace stem;
+  if (!stem_conv_applies(H, W, CIN, COUT, KS, KS, STR, PAD))
+    throw std::runtime_error("stem_conv: unsupported geometry");
+  if (ldw < KS * KS * CIN || (((uintptr_t)x | (uintptr_t)dy) & 15))
+    throw std::runtime_error("stem_conv_wgrad: ld >= 392 and 16-B aligned inputs");
+  if (beta != 0.f && beta != 1.f) throw std::runtime_error("stem_conv_wgrad: beta must be 0 or 1");
+  if (beta == 0.f)
+    DTFX_HIP_CHECK(hipMemset2DAsync(dw, sizeof(float) * ldw, 0, sizeof(float) * KS * KS * CIN,
+                                    COUT, s));
+  const int OH = (H + 2 * PAD - KS) / STR + 1, OW = (W + 2 * PAD - KS) / STR + 1;
+  const int tiles = N * (OH / TH) * (OW / TW);
+  const size_t lds = 128 * DP + P_BYTES;
+  const int blocks = std::min(tiles, 256);  // one persistent block per CU: 28 accumulator tiles
+  hipLaunchKernelGGL(stem_conv_wgrad_kernel, dim3(blocks), dim3(256), lds, s, N, H, W, OH, OW,
+                     (const unsigned short*)x, (const unsigned short*)dy, dw, ldw);
+  DTFX_HIP_CHECK(hipGetLastError());
 }
 
 void stem_conv_fwd_launch(int N, int H, int W, const void* x, const void* w, int ldw, void* y,

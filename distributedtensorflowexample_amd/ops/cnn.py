@@ -155,6 +155,12 @@ def conv_wgrad(dy, x, dw, KH, KW, stride, pad, beta=1.0):
         k = KH * KW * C
         dw[:, :k] = g + (beta * dw[:, :k] if beta else 0)
         return dw
+    if hip().stem_conv_applies(H, W, C, Cout, KH, KW, stride, pad) and beta in (0.0, 1.0):
+        # the ResNet stem: csrc/kernels/stem_conv.hip (dy tile + input patch staged once per
+        # 8 x 16 output tile, per-block partial gradient summed in registers)
+        hip().stem_conv_wgrad(N, H, W, ptr(x), ptr(dy), ptr(dw), dw.stride(0), float(beta),
+                              stream_handle())
+        return dw
     # split-K partials through a workspace + one reduce pass instead of f32 atomics
     nws = hip().conv_wgrad_ws_floats(N, H, W, C, Cout, KH, KW, stride, pad) if _SPLITK_WS else 0
     ws = torch.empty(nws, device=dy.device) if nws else None
