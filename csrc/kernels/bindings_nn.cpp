@@ -33,6 +33,9 @@ void stem_conv_fwd_launch(int, int, int, const void*, const void*, int, void*, f
                           hipStream_t);
 void stem_conv_wgrad_launch(int, int, int, const void*, const void*, float*, int, float,
                             hipStream_t);
+bool conv3x3_c64_applies(int, int, int, int, int, int, int, int);
+void conv3x3_c64_fwd_launch(int, int, int, const void*, const void*, int, void*, float*, float*,
+                            hipStream_t);
 void maxpool_fwd_launch(int, int, int, int, const void*, void*, void*, hipStream_t);
 void maxpool_bwd_launch(int, int, int, int, const void*, const void*, void*, hipStream_t);
 void avgpool_fwd_launch(int, int, int, const void*, void*, hipStream_t);
@@ -209,6 +212,13 @@ void register_nn(py::module_& m) {
                               float beta, uintptr_t s) {
     dtfx::stem_conv_wgrad_launch(N, H, W, P<const void>(x), P<const void>(dy), P<float>(dw), ldw,
                                  beta, S(s));
+  });
+  m.def("conv3x3_c64_applies", &dtfx::conv3x3_c64_applies,
+        "the 64-channel 3x3 kernel handles this conv (stride 1, pad 1, H % 4, W % 28)");
+  m.def("conv3x3_c64_fwd", [](int N, int H, int W, uintptr_t x, uintptr_t w, int ldw, uintptr_t y,
+                              uintptr_t ps, uintptr_t pq, uintptr_t s) {
+    dtfx::conv3x3_c64_fwd_launch(N, H, W, P<const void>(x), P<const void>(w), ldw, P<void>(y),
+                                 P<float>(ps), P<float>(pq), S(s));
   });
   m.def("colpart_reduce", [](int R, int C, uintptr_t ps, uintptr_t pq, uintptr_t os, uintptr_t oq,
                              uintptr_t s) {

@@ -71,6 +71,16 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
         hip().colpart_reduce(part.shape[1], Cout, ptr(part[0]), ptr(part[1]), ptr(colsum),
                              ptr(colsq), stream_handle())
         return y
+    if (colsum is not None and residual is None
+            and hip().conv3x3_c64_applies(H, W, C, Cout, KH, KW, stride, pad)):
+        # layer1's 64-channel 3x3 conv: csrc/kernels/conv3x3_c64.hip (weights resident in
+        # LDS, input patch staged once per 4 x 28 output tile); 2 partial rows per tile
+        part = torch.empty(2, 2 * (N * OH * OW // 112), Cout, device=x.device)
+        hip().conv3x3_c64_fwd(N, H, W, ptr(x), ptr(w), w.stride(0), ptr(y), ptr(part[0]),
+                              ptr(part[1]), stream_handle())
+        hip().colpart_reduce(part.shape[1], Cout, ptr(part[0]), ptr(part[1]), ptr(colsum),
+                             ptr(colsq), stream_handle())
+        return y
     ps = pq = None
     if colsum is not None:
         rows = (N * OH * OW + 63) // 64  # one partial row per 64-row output slab

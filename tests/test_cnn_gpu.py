@@ -20,6 +20,7 @@ CONVS = [  # N, H, W, C, Cout, k, stride, pad
     (2, 9, 11, 256, 64, 1, 1, 0),
     (2, 32, 32, 8, 64, 7, 2, 3),     # the stem kernel (stem_conv.hip): one 16x16 output image
     (3, 48, 64, 8, 64, 7, 2, 3),     # stem kernel, 3 x 2 x 3 tiles per image and batch
+    (2, 8, 56, 64, 64, 3, 1, 1),     # the 64-channel 3x3 kernel (conv3x3_c64.hip), 4 tiles
     (2, 15, 13, 64, 128, 3, 2, 1),   # stride-2 dgrad: phase classes of unequal size
     (2, 14, 14, 64, 64, 3, 2, 1),    # stride-2 dgrad on the 256x64 tile
     (2, 13, 15, 128, 64, 1, 2, 0),   # 1x1 stride 2: three of four classes have no taps
