@@ -36,6 +36,10 @@ void stem_conv_wgrad_launch(int, int, int, const void*, const void*, float*, int
 bool conv3x3_c64_applies(int, int, int, int, int, int, int, int);
 void conv3x3_c64_fwd_launch(int, int, int, const void*, const void*, int, void*, float*, float*,
                             hipStream_t);
+void conv3x3_c64_wgrad_launch(int, int, int, const void*, const void*, float*, int, float,
+                              hipStream_t);
+void conv3x3_c64_dgrad_launch(int, int, int, const void*, const void*, int, void*, const void*,
+                              const void*, const float*, const float*, float*, float*, hipStream_t);
 void maxpool_fwd_launch(int, int, int, int, const void*, void*, void*, hipStream_t);
 void maxpool_bwd_launch(int, int, int, int, const void*, const void*, void*, hipStream_t);
 void avgpool_fwd_launch(int, int, int, const void*, void*, hipStream_t);
@@ -219,6 +223,18 @@ void register_nn(py::module_& m) {
                               uintptr_t ps, uintptr_t pq, uintptr_t s) {
     dtfx::conv3x3_c64_fwd_launch(N, H, W, P<const void>(x), P<const void>(w), ldw, P<void>(y),
                                  P<float>(ps), P<float>(pq), S(s));
+  });
+  m.def("conv3x3_c64_wgrad", [](int N, int H, int W, uintptr_t x, uintptr_t dy, uintptr_t dw,
+                                int ldw, float beta, uintptr_t s) {
+    dtfx::conv3x3_c64_wgrad_launch(N, H, W, P<const void>(x), P<const void>(dy), P<float>(dw), ldw,
+                                   beta, S(s));
+  });
+  m.def("conv3x3_c64_dgrad", [](int N, int H, int W, uintptr_t dy, uintptr_t w, int ldw,
+                                uintptr_t dx, uintptr_t relu_y, uintptr_t bn_x, uintptr_t mean,
+                                uintptr_t rstd, uintptr_t ps, uintptr_t pq, uintptr_t s) {
+    dtfx::conv3x3_c64_dgrad_launch(N, H, W, P<const void>(dy), P<const void>(w), ldw, P<void>(dx),
+                                   P<const void>(relu_y), P<const void>(bn_x), P<const float>(mean),
+                                   P<const float>(rstd), P<float>(ps), P<float>(pq), S(s));
   });
   m.def("colpart_reduce", [](int R, int C, uintptr_t ps, uintptr_t pq, uintptr_t os, uintptr_t oq,
                              uintptr_t s) {

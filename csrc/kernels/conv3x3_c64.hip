@@ -136,11 +136,323 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_fwd_kernel(
   }
 }
 
+
+// Weight gradient dW[co][k] (+)= sum_p dy[p][co] * x[p + tap][ci], k = tap * 64 + ci: per
+// 4 x 28 tile the dy tile (112 px x 64 co, 144-B rows) and the input patch are staged once
+// (prefetched a tile ahead); M = 64 co x N = 576 (36 blocks of 16 = tap x channel quarter)
+// x K = 112 pixels (+16 zero pixels: 4 k-groups of 32).  Both operands are k-strided, read
+// with ds_read_b64_tr_b16 from per-lane pixel rows; wave w owns n-blocks w, w + 8, ... (4-5
+// blocks) x all 4 co blocks; a persistent block sums its tiles in registers and adds its
+// 64 x 576 partial with one f32 atomic per element at the end.
+constexpr int DP = 144;  // dy tile row pitch (bytes)
+
+__device__ __forceinline__ bf16x8 tr_pair(const char* a0, const char* a1) {
+  typedef short bf16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) bf16x4 lds4;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)a0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)a1);
+  bf16x8 v;
+  v.lo = lo;
+  v.hi = hi;
+  return v;
+}
+
+__global__ __launch_bounds__(512, 1) void conv3x3_c64_wgrad_kernel(
+    int N, int H, int W, const unsigned short* __restrict__ x, const unsigned short* __restrict__ dy,
+    float* __restrict__ dw, int ldw) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* Ds = sm;             // [128 px][64 co] (rows >= 112 zero)
+  char* Ps = sm + 128 * DP;  // patch, swizzled 16-B chunks as in the forward
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_w = W / TW, tiles_img = (H / TH) * tiles_w, tiles = N * tiles_img;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  const int nnb = wave < 4 ? 5 : 4;  // n-blocks w + 8 j, j < nnb (36 blocks over 8 waves)
+  for (int i = tid; i < 16 * 8; i += 512)  // the 16 pad pixel rows of the dy tile stay zero
+    *(bf16x8*)(Ds + (NPX + (i >> 3)) * DP + (i & 7) * 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  f32x4 acc[4][5];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 dv[2], pv[3];
+  auto load_tile = [&](int tt) {
+    const int n = tt / tiles_img, r = tt - n * tiles_img;
+    const int oh0 = (r / tiles_w) * TH, ow0 = (r % tiles_w) * TW;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // dy: 112 px x 8 chunks = 896 over 512 threads
+      const int e = tid + 512 * k, p = e >> 3, c = e & 7;
+      dv[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (e < NPX * 8)
+        dv[k] = *(const bf16x8*)(dy + (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + c * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int e = tid + 512 * k, qq = e >> 3, c = e & 7, pr = qq / PW, pc = qq - pr * PW;
+      const int ih = oh0 - 1 + pr, iw = ow0 - 1 + pc;
+      pv[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (e < PCH && ih >= 0 && ih < H && iw >= 0 && iw < W)
+        pv[k] = *(const bf16x8*)(x + (((size_t)n * H + ih) * W + iw) * C + c * 8);
+    }
+  };
+  if (blockIdx.x < tiles) load_tile(blockIdx.x);
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    __syncthreads();  // the previous tile's fragment reads are done
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + 512 * k;
+      if (e < NPX * 8) *(bf16x8*)(Ds + (e >> 3) * DP + (e & 7) * 16) = dv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int e = tid + 512 * k, qq = e >> 3, c = e & 7;
+      if (e < PCH) *(bf16x8*)(Ps + qq * 128 + ((c ^ (qq & 7)) << 4)) = pv[k];
+    }
+    __syncthreads();
+    if (t + (int)gridDim.x < tiles) load_tile(t + gridDim.x);
+#pragma unroll
+    for (int kg = 0; kg < 4; ++kg) {
+      const int k0 = 32 * kg + 8 * g + q, k1 = k0 + 4;  // this lane's two pixel rows
+      bf16x8 a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = tr_pair(Ds + k0 * DP + (16 * i + 4 * p4) * 2, Ds + k1 * DP + (16 * i + 4 * p4) * 2);
+      // patch pixel of tap (0, 0) for the two pixel rows (pad pixels >= 112: any valid pixel,
+      // their dy rows are zero)
+      const int pk0 = min(k0, NPX - 1), pk1 = min(k1, NPX - 1);
+      const int pb0 = (pk0 / TW) * PW + pk0 % TW, pb1 = (pk1 / TW) * PW + pk1 % TW;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        if (j < nnb) {
+          const int nb = wave + 8 * j, tap = nb >> 2, kh = tap / 3, kw = tap - kh * 3;
+          const int ch = (nb & 3) * 16 + 4 * p4;  // this lane's 4 channels
+          const int q0 = pb0 + kh * PW + kw, q1 = pb1 + kh * PW + kw;
+          const int off = (ch & 7) * 2;  // byte offset inside the 16-B chunk
+          const bf16x8 b = tr_pair(Ps + q0 * 128 + (((ch >> 3) ^ (q0 & 7)) << 4) + off,
+                                   Ps + q1 * 128 + (((ch >> 3) ^ (q1 & 7)) << 4) + off);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // lane (cl, g): column n = cl of block nb (k = tap * 64 + 16 (nb & 3) + cl), co 16 i + 4 g + rr
+  const int cl = lane & 15;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    if (j >= nnb) continue;
+    const int nb = wave + 8 * j, k = (nb >> 2) * C + (nb & 3) * 16 + cl;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        unsafeAtomicAdd(dw + (size_t)(16 * i + 4 * g + rr) * ldw + k, acc[i][j][rr]);
+  }
+}
+
+
+// Data gradient with BatchNorm backward fused: dx = conv3x3(dy, W') with W'[ci][tap][co] =
+// W[co][8 - tap][ci] (a stride-1 3x3 data gradient is the forward conv of dy with the kernel
+// flipped and transposed; built while the block loads its resident weights), then, as the
+// GEMM path's fused epilogue, de = dx * (relu_y > 0) and the BN's sum(de), sum(de * xhat)
+// (xhat from bn_x, mean, rstd) as partial rows, one per wave and tile ([8 * tiles][64]).
+// relu_y / bn_x may be null (plain dgrad, no statistics).
+__global__ __launch_bounds__(512, 1) void conv3x3_c64_dgrad_kernel(
+    int N, int H, int W, const unsigned short* __restrict__ dy, const unsigned short* __restrict__ w,
+    int ldw, unsigned short* __restrict__ dx, const unsigned short* __restrict__ relu_y,
+    const unsigned short* __restrict__ bn_x, const float* __restrict__ bn_mean,
+    const float* __restrict__ bn_rstd, float* __restrict__ psum, float* __restrict__ psq) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* Ws = sm;
+  char* Ps = sm + W_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < C * 72; i += 512) {  // W'[ci][tap * 64 + co8 * 8 .. + 7], once
+    const int ci = i / 72, rem = i - ci * 72, tap = rem >> 3, co8 = rem & 7;
+    bf16x8 v;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (short)w[(size_t)(co8 * 8 + u) * ldw + (8 - tap) * C + ci];
+    *(bf16x8*)(Ws + ci * WP * 2 + rem * 16) = v;
+  }
+  const int tiles_w = W / TW, tiles_img = (H / TH) * tiles_w, tiles = N * tiles_img;
+  const int cl = lane & 15, g = lane >> 4;
+  const int cb = wave & 3;
+  const int g0 = wave < 4 ? 0 : 4, ng = wave < 4 ? 4 : 3;
+  const bool fused = relu_y != nullptr;
+  const int ec = tid & 7;  // the 8-channel chunk this thread handles in the epilogue
+  float mu[8], rs[8];
+  if (fused) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      mu[u] = bn_mean[ec * 8 + u];
+      rs[u] = bn_rstd[ec * 8 + u];
+    }
+  }
+  bf16x8 v[3];
+  auto load_patch = [&](int tt) {
+    const int n = tt / tiles_img, r = tt - n * tiles_img;
+    const int ih0 = (r / tiles_w) * TH - 1, iw0 = (r % tiles_w) * TW - 1;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int e = tid + 512 * k, q = e >> 3, c = e & 7, pr = q / PW, pc = q - pr * PW;
+      const int ih = ih0 + pr, iw = iw0 + pc;
+      v[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (e < PCH && ih >= 0 && ih < H && iw >= 0 && iw < W)
+        v[k] = *(const bf16x8*)(dy + (((size_t)n * H + ih) * W + iw) * C + c * 8);
+    }
+  };
+  if (blockIdx.x < tiles) load_patch(blockIdx.x);
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int n = t / tiles_img, r = t - n * tiles_img;
+    const int oh0 = (r / tiles_w) * TH, ow0 = (r % tiles_w) * TW;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int e = tid + 512 * k, q = e >> 3, c = e & 7;
+      if (e < PCH) *(bf16x8*)(Ps + q * 128 + ((c ^ (q & 7)) << 4)) = v[k];
+    }
+    __syncthreads();
+    if (t + (int)gridDim.x < tiles) load_patch(t + gridDim.x);
+    // the epilogue's side inputs of this tile, in flight during the MFMAs
+    bf16x8 yv[2], xv[2];
+    if (fused) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int e = tid + 512 * k, p = e >> 3;
+        const size_t o = (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8;
+        if (e < NPX * 8) {
+          yv[k] = *(const bf16x8*)(relu_y + o);
+          xv[k] = *(const bf16x8*)(bn_x + o);
+        }
+      }
+    }
+    int pq[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = 16 * (g0 + i) + cl;
+      pq[i] = (p / TW) * PW + (p % TW);
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int kg = 0; kg < 18; ++kg) {
+      const int tap = kg >> 1, kh = tap / 3, kw = tap - kh * 3, chunk = (kg & 1) * 4 + g;
+      const bf16x8 b = *(const bf16x8*)(Ws + (16 * cb + cl) * WP * 2 + (32 * kg + 8 * g) * 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i < ng) {
+          const int q = pq[i] + kh * PW + kw;
+          const bf16x8 a = *(const bf16x8*)(Ps + q * 128 + ((chunk ^ (q & 7)) << 4));
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // every wave is done with the patch: stage the output there
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < ng)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          *(unsigned short*)(Ps + (16 * (g0 + i) + 4 * g + rr) * 128 + (16 * cb + cl) * 2) =
+              tobf(acc[i][rr]);
+    __syncthreads();
+    float cs[8], cq[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + 512 * k, p = e >> 3;
+      if (e >= NPX * 8) continue;
+      bf16x8 o = *(const bf16x8*)(Ps + p * 128 + ec * 16);
+      if (fused) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float yy = __uint_as_float((unsigned)(unsigned short)yv[k][u] << 16);
+          const float d = yy > 0.f ? __uint_as_float((unsigned)(unsigned short)o[u] << 16) : 0.f;
+          o[u] = yy > 0.f ? o[u] : (short)0;
+          const float xx = __uint_as_float((unsigned)(unsigned short)xv[k][u] << 16);
+          cs[u] += d;
+          cq[u] += d * (xx - mu[u]) * rs[u];
+        }
+      }
+      *(bf16x8*)(dx + (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8) = o;
+    }
+    if (fused) {  // lanes of one chunk: lane & 7 equal -> partial row of this wave
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        cs[u] += __shfl_xor(cs[u], 8);
+        cs[u] += __shfl_xor(cs[u], 16);
+        cs[u] += __shfl_xor(cs[u], 32);
+        cq[u] += __shfl_xor(cq[u], 8);
+        cq[u] += __shfl_xor(cq[u], 16);
+        cq[u] += __shfl_xor(cq[u], 32);
+      }
+      if (lane < 8) {
+        const size_t o = (size_t)(8 * t + wave) * C + ec * 8;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          psum[o + u] = cs[u];
+          psq[o + u] = cq[u];
+        }
+      }
+    }
+  }
+}
+
 }  // namespace c3
 
 bool conv3x3_c64_applies(int H, int W, int C, int Cout, int KH, int KW, int stride, int pad) {
   return C == c3::C && Cout == c3::C && KH == 3 && KW == 3 && stride == 1 && pad == 1 &&
          H % c3::TH == 0 && W % c3::TW == 0;
+}
+
+// dx (+ fused BN backward when relu_y is given: psum / psq partial rows [8 * tiles][64])
+void conv3x3_c64_dgrad_launch(int N, int H, int W, const void* dy, const void* w, int ldw, void* dx,
+                              const void* relu_y, const void* bn_x, const float* bn_mean,
+                              const float* bn_rstd, float* psum, float* psq, hipStream_t s) {
+  using namespace c3;
+  if (!conv3x3_c64_applies(H, W, C, C, 3, 3, 1, 1))
+    throw std::runtime_error("conv3x3_c64: unsupported geometry");
+  if (ldw < 9 * C || (((uintptr_t)dy | (uintptr_t)dx | (uintptr_t)relu_y | (uintptr_t)bn_x) & 15))
+    throw std::runtime_error("conv3x3_c64_dgrad: ld >= 576 and 16-B aligned tensors");
+  if (relu_y && (!bn_x || !bn_mean || !bn_rstd || !psum || !psq))
+    throw std::runtime_error("conv3x3_c64_dgrad: fused BN backward needs bn_x, mean, rstd, partials");
+  const int tiles = N * (H / TH) * (W / TW);
+  const size_t lds = W_BYTES + P_BYTES;
+  static bool attr = false;
+  if (!attr) {
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_c64_dgrad_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int blocks = std::min(tiles, 256);
+  hipLaunchKernelGGL(conv3x3_c64_dgrad_kernel, dim3(blocks), dim3(512), lds, s, N, H, W,
+                     (const unsigned short*)dy, (const unsigned short*)w, ldw, (unsigned short*)dx,
+                     (const unsigned short*)relu_y, (const unsigned short*)bn_x, bn_mean, bn_rstd,
+                     psum, psq);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// dw (f32 [64][ldw], the first 576 columns) (+)= the weight gradient: beta 1 accumulates,
+// beta 0 overwrites.
+void conv3x3_c64_wgrad_launch(int N, int H, int W, const void* x, const void* dy, float* dw,
+                              int ldw, float beta, hipStream_t s) {
+  using namespace c3;
+  if (!conv3x3_c64_applies(H, W, C, C, 3, 3, 1, 1))
+    throw std::runtime_error("conv3x3_c64: unsupported geometry");
+  if (ldw < 9 * C || (((uintptr_t)x | (uintptr_t)dy) & 15))
+    throw std::runtime_error("conv3x3_c64_wgrad: ld >= 576 and 16-B aligned inputs");
+  if (beta != 0.f && beta != 1.f) throw std::runtime_error("conv3x3_c64_wgrad: beta must be 0 or 1");
+  if (beta == 0.f)
+    DTFX_HIP_CHECK(hipMemset2DAsync(dw, sizeof(float) * ldw, 0, sizeof(float) * 9 * C, C, s));
+  const int tiles = N * (H / TH) * (W / TW);
+  const size_t lds = 128 * DP + P_BYTES;
+  const int blocks = std::min(tiles, 256);
+  hipLaunchKernelGGL(conv3x3_c64_wgrad_kernel, dim3(blocks), dim3(512), lds, s, N, H, W,
+                     (const unsigned short*)x, (const unsigned short*)dy, dw, ldw);
+  DTFX_HIP_CHECK(hipGetLastError());
 }
 
 // y = conv3x3(x, w), psum / psq: partial statistic rows [2 * tiles][64] (tiles = N*H*W / 112)

@@ -119,6 +119,20 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
             sdx += (de * xh).sum(0)
         return dx.to(BF16)
     dx = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
+    if residual is None and hip().conv3x3_c64_applies(H, W, C, Cout, KH, KW, stride, pad):
+        # layer1's 64-channel 3x3 conv: csrc/kernels/conv3x3_c64.hip (dy patch staged once
+        # per 4 x 28 tile, flipped weights resident in LDS, BN backward in the epilogue)
+        if bn is None:
+            hip().conv3x3_c64_dgrad(N, H, W, ptr(dy), ptr(w), w.stride(0), ptr(dx), 0, 0, 0, 0,
+                                    0, 0, stream_handle())
+            return dx
+        y, x, mean, rstd, sdy, sdx = bn
+        part = torch.empty(2, 8 * (N * H * W // 112), C, device=dy.device)
+        hip().conv3x3_c64_dgrad(N, H, W, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(y), ptr(x),
+                                ptr(mean), ptr(rstd), ptr(part[0]), ptr(part[1]), stream_handle())
+        hip().colpart_reduce(part.shape[1], C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
+                             stream_handle())
+        return dx
     if bn is None:
         hip().conv_bf16(2, N, H, W, C, Cout, KH, KW, stride, pad, ptr(dy), ptr(w), w.stride(0),
                         ptr(dx), 0.0, ptr(residual), 0, 0, 0, stream_handle())
@@ -170,6 +184,12 @@ def conv_wgrad(dy, x, dw, KH, KW, stride, pad, beta=1.0):
         # 8 x 16 output tile, per-block partial gradient summed in registers)
         hip().stem_conv_wgrad(N, H, W, ptr(x), ptr(dy), ptr(dw), dw.stride(0), float(beta),
                               stream_handle())
+        return dw
+    if hip().conv3x3_c64_applies(H, W, C, Cout, KH, KW, stride, pad) and beta in (0.0, 1.0):
+        # layer1's 64-channel 3x3 conv: csrc/kernels/conv3x3_c64.hip (dy tile + input patch
+        # staged once per 4 x 28 tile, per-block partial gradient summed in registers)
+        hip().conv3x3_c64_wgrad(N, H, W, ptr(x), ptr(dy), ptr(dw), dw.stride(0), float(beta),
+                                stream_handle())
         return dw
     # split-K partials through a workspace + one reduce pass instead of f32 atomics
     nws = hip().conv_wgrad_ws_floats(N, H, W, C, Cout, KH, KW, stride, pad) if _SPLITK_WS else 0

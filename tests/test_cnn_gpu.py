@@ -67,6 +67,7 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, W, C, Co, k, s, p):
     (2, 14, 14, 128, 128, 3, 2, 1, True),  # stride-2 phase classes, one partial block each
     (2, 15, 13, 64, 128, 3, 2, 1, True),   # unequal classes: zeroed partial rows
     (2, 13, 15, 128, 64, 1, 2, 0, True),   # empty classes: residual + mask only
+    (2, 8, 56, 64, 64, 3, 1, 1, False),    # 64-channel 3x3 kernel with the fused BN backward
     (4, 64, 64, 1024, 256, 3, 2, 1, True),  # 8-phase dgrad: per-slab BN columns, class rows
     (4, 64, 64, 1024, 256, 1, 1, 0, True),  # 8-phase 1x1 dgrad
 ])
