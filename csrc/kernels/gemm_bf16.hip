@@ -1081,8 +1081,22 @@ static void launch_one(dim3 grid_yz, int M, int N, int K, const unsigned short* 
     attr = true;
   }
   const int tiles = ((M + BM_ - 1) / BM_) * ((N + BN_ - 1) / BN_);
+  // One K tile (and no split): only LDS stage 0 is ever staged, so the block needs just that
+  // stage or the epilogue's per-wave transpose rows, whichever is larger -- three resident
+  // 128x128 blocks per CU instead of two (ResNet-50 layer1 conv3 forward, K = 64: 236 -> 194
+  // us; DTFX_GEMM_1STAGE=0: full stages)
+  static const bool one_stage_ok = [] {
+    const char* v = getenv("DTFX_GEMM_1STAGE");
+    return v ? atoi(v) != 0 : true;
+  }();
+  size_t lds_launch = lds;
+  if (NBUF == 2 && one_stage_ok && K <= gb::BK && grid_yz.y == 1) {
+    const size_t stage = (size_t)(BM_ * gb::BK * 2 + BN_ * gb::BK * 2);
+    const size_t ep = (size_t)(threads / 64) * 32 * 68 * 4;
+    lds_launch = stage > ep ? stage : ep;
+  }
   hipLaunchKernelGGL((gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF, BN_>),
-                     dim3(tiles, grid_yz.y, grid_yz.z), dim3(threads), lds, stream, M, N, K, A, lda,
+                     dim3(tiles, grid_yz.y, grid_yz.z), dim3(threads), lds_launch, stream, M, N, K, A, lda,
                      B, ldb, C, ldc, e, sA, sB, sC, d);
   DTFX_HIP_CHECK(hipGetLastError());
 }
