@@ -45,7 +45,11 @@ def main():
         ("qkv_dgrad", T, 768, 2304, False, False, None), ("ffn1_dgrad", T, 768, 3072, False, False, None),
         ("ffn2_dgrad_gelu", T, 3072, 768, False, False, "gelu_grad"),
         ("ffn1_wgrad", 3072, 768, T, True, False, "f32"), ("qkv_wgrad", 2304, 768, T, True, False, "f32"),
-        ("sq4096", 4096, 4096, 4096, False, True, None), ("sq8192", 8192, 8192, 8192, False, True, None)]
+        ("sq4096", 4096, 4096, 4096, False, True, None), ("sq8192", 8192, 8192, 8192, False, True, None),
+        # ResNet-50 1x1 convolutions at batch 256 as plain GEMMs (x [pixels][Cin] W[Cout][Cin]^T)
+        ("r_l3c3_fwd", 50176, 1024, 256, False, True, None), ("r_l2c3_fwd", 200704, 512, 128, False, True, None),
+        ("r_l3c1_fwd", 50176, 256, 1024, False, True, None), ("r_l4c3_fwd", 12544, 2048, 512, False, True, None),
+        ("r_l1c3_fwd", 802816, 256, 64, False, True, None), ("r_l4c1_fwd", 12544, 512, 2048, False, True, None)]
     if a.shapes != "all":
         keep = a.shapes.split(",")
         shapes = [s for s in shapes if s[0] in keep]
