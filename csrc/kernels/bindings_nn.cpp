@@ -40,6 +40,10 @@ void conv3x3_c64_wgrad_launch(int, int, int, const void*, const void*, float*, i
                               hipStream_t);
 void conv3x3_c64_dgrad_launch(int, int, int, const void*, const void*, int, void*, const void*,
                               const void*, const float*, const float*, float*, float*, hipStream_t);
+bool conv3x3_c128_applies(int, int, int, int, int, int, int, int);
+void conv3x3_c128_launch(int, int, int, int, const void*, const void*, int, void*, void*,
+                         const void*, const void*, const float*, const float*, float*, float*,
+                         hipStream_t);
 void maxpool_fwd_launch(int, int, int, int, const void*, void*, void*, hipStream_t);
 void maxpool_bwd_launch(int, int, int, int, const void*, const void*, void*, hipStream_t);
 void avgpool_fwd_launch(int, int, int, const void*, void*, hipStream_t);
@@ -235,6 +239,16 @@ void register_nn(py::module_& m) {
     dtfx::conv3x3_c64_dgrad_launch(N, H, W, P<const void>(dy), P<const void>(w), ldw, P<void>(dx),
                                    P<const void>(relu_y), P<const void>(bn_x), P<const float>(mean),
                                    P<const float>(rstd), P<float>(ps), P<float>(pq), S(s));
+  });
+  m.def("conv3x3_c128_applies", &dtfx::conv3x3_c128_applies,
+        "the 128-channel 3x3 kernel handles this conv (stride 1, pad 1, H % 4, W % 28)");
+  m.def("conv3x3_c128", [](int mode, int N, int H, int W, uintptr_t x, uintptr_t w, int ldw,
+                           uintptr_t y, uintptr_t wf, uintptr_t relu_y, uintptr_t bn_x,
+                           uintptr_t mean, uintptr_t rstd, uintptr_t ps, uintptr_t pq, uintptr_t s) {
+    dtfx::conv3x3_c128_launch(mode, N, H, W, P<const void>(x), P<const void>(w), ldw, P<void>(y),
+                              P<void>(wf), P<const void>(relu_y), P<const void>(bn_x),
+                              P<const float>(mean), P<const float>(rstd), P<float>(ps),
+                              P<float>(pq), S(s));
   });
   m.def("colpart_reduce", [](int R, int C, uintptr_t ps, uintptr_t pq, uintptr_t os, uintptr_t oq,
                              uintptr_t s) {

@@ -72,6 +72,16 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
                              ptr(colsq), stream_handle())
         return y
     if (colsum is not None and residual is None
+            and hip().conv3x3_c128_applies(H, W, C, Cout, KH, KW, stride, pad)):
+        # layer2's 128-channel 3x3 conv: csrc/kernels/conv3x3_c128.hip (input patch staged
+        # once per 4 x 28 output tile, weights streamed one tap at a time); 1 row per tile
+        part = torch.empty(2, N * OH * OW // 112, Cout, device=x.device)
+        hip().conv3x3_c128(1, N, H, W, ptr(x), ptr(w), w.stride(0), ptr(y), 0, 0, 0, 0, 0,
+                           ptr(part[0]), ptr(part[1]), stream_handle())
+        hip().colpart_reduce(part.shape[1], Cout, ptr(part[0]), ptr(part[1]), ptr(colsum),
+                             ptr(colsq), stream_handle())
+        return y
+    if (colsum is not None and residual is None
             and hip().conv3x3_c64_applies(H, W, C, Cout, KH, KW, stride, pad)):
         # layer1's 64-channel 3x3 conv: csrc/kernels/conv3x3_c64.hip (weights resident in
         # LDS, input patch staged once per 4 x 28 output tile); 2 partial rows per tile
@@ -119,6 +129,22 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
             sdx += (de * xh).sum(0)
         return dx.to(BF16)
     dx = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
+    if residual is None and hip().conv3x3_c128_applies(H, W, C, Cout, KH, KW, stride, pad):
+        # layer2's 128-channel 3x3 conv: csrc/kernels/conv3x3_c128.hip (flipped weights in a
+        # workspace, dy patch staged once per 4 x 28 tile, BN backward in the epilogue)
+        wf = torch.empty(C, 9 * Cout, device=dy.device, dtype=BF16)
+        if bn is None:
+            hip().conv3x3_c128(2, N, H, W, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(wf), 0, 0,
+                               0, 0, 0, 0, stream_handle())
+            return dx
+        y, x, mean, rstd, sdy, sdx = bn
+        part = torch.empty(2, 8 * (N * H * W // 112), C, device=dy.device)
+        hip().conv3x3_c128(2, N, H, W, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(wf), ptr(y),
+                           ptr(x), ptr(mean), ptr(rstd), ptr(part[0]), ptr(part[1]),
+                           stream_handle())
+        hip().colpart_reduce(part.shape[1], C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
+                             stream_handle())
+        return dx
     if residual is None and hip().conv3x3_c64_applies(H, W, C, Cout, KH, KW, stride, pad):
         # layer1's 64-channel 3x3 conv: csrc/kernels/conv3x3_c64.hip (dy patch staged once
         # per 4 x 28 tile, flipped weights resident in LDS, BN backward in the epilogue)
