@@ -8,6 +8,7 @@ namespace py = pybind11;
 
 namespace dtfx {
 void gemm_bf16_set_cfg(int);
+void attn_bwd_set_variant(int);
 void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const void*, int, void*,
                       int, float, float, const float*, int, const void*, void*, int, const void*,
                       int, int, int, int, long long, long long, long long,
@@ -41,6 +42,11 @@ void conv3x3_c64_wgrad_launch(int, int, int, const void*, const void*, float*, i
 void conv3x3_c64_dgrad_launch(int, int, int, const void*, const void*, int, void*, const void*,
                               const void*, const float*, const float*, float*, float*, hipStream_t);
 bool conv3x3_c128_applies(int, int, int, int, int, int, int, int);
+bool conv1x1_applies(int, int, int);
+int conv1x1_rows(int, int, int, int);
+void conv1x1_launch(int, int, int, int, const void*, const void*, int, void*, const void*,
+                    const void*, const void*, const float*, const float*, float*, float*,
+                    hipStream_t);
 void conv3x3_c128_launch(int, int, int, int, const void*, const void*, int, void*, void*,
                          const void*, const void*, const float*, const float*, float*, float*,
                          hipStream_t);
@@ -79,6 +85,9 @@ static inline T* P(uintptr_t a) { return reinterpret_cast<T*>(a); }
 static inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 void register_nn(py::module_& m) {
+  m.def("attn_bwd_set_variant", &dtfx::attn_bwd_set_variant,
+        "force the attention-backward kernel (-1 = environment; 0: 8 waves, 1: 4 waves, "
+        "2: two query halves, two blocks per CU)");
   m.def("gemm_bf16_set_cfg", &dtfx::gemm_bf16_set_cfg,
         "force the bf16 GEMM tile configuration (-1 = auto; 0: 128x128, 3: 256x256 2-stage, "
         "5: 256x256 8-phase)");
@@ -239,6 +248,17 @@ void register_nn(py::module_& m) {
     dtfx::conv3x3_c64_dgrad_launch(N, H, W, P<const void>(dy), P<const void>(w), ldw, P<void>(dx),
                                    P<const void>(relu_y), P<const void>(bn_x), P<const float>(mean),
                                    P<const float>(rstd), P<float>(ps), P<float>(pq), S(s));
+  });
+  m.def("conv1x1_applies", &dtfx::conv1x1_applies,
+        "(M, K, N): the streaming 1x1 kernel takes this product (K 64 / 128, N = 256 * 2^i)");
+  m.def("conv1x1_rows", &dtfx::conv1x1_rows, "(mode, M, K, N): partial statistics rows a launch writes");
+  m.def("conv1x1", [](int mode, int M, int K, int N, uintptr_t x, uintptr_t w, int ldw,
+                      uintptr_t y, uintptr_t res, uintptr_t relu_y, uintptr_t bn_x, uintptr_t mean,
+                      uintptr_t rstd, uintptr_t ps, uintptr_t pq, uintptr_t s) {
+    dtfx::conv1x1_launch(mode, M, K, N, P<const void>(x), P<const void>(w), ldw, P<void>(y),
+                         P<const void>(res), P<const void>(relu_y), P<const void>(bn_x),
+                         P<const float>(mean), P<const float>(rstd), P<float>(ps), P<float>(pq),
+                         S(s));
   });
   m.def("conv3x3_c128_applies", &dtfx::conv3x3_c128_applies,
         "the 128-channel 3x3 kernel handles this conv (stride 1, pad 1, H % 4, W % 28)");

@@ -1,0 +1,597 @@
+// 1x1 / stride 1 convolutions with 64 or 128 reduction channels and >= 256 output channels
+// (ResNet-50's layer1 / layer2 expansions: conv3 and layer1's downsample forward, 64 -> 256
+// and 128 -> 512; conv1's data gradient, 64 -> 256 and 128 -> 256 / 512), NHWC bf16, as a
+// streaming product: persistent blocks, the weights held in REGISTERS for the block's life,
+// per 32-pixel tile only the pixels' K channels read (prefetched a tile ahead) and the
+// output written, with the BatchNorm work fused:
+//   forward:  y = x W^T, partial rows of sum(y) / sum(y^2) per output channel;
+//   dgrad:    de = (dy W + residual) * (relu_y > 0), partial rows of sum(de) and
+//             sum(de * xhat) (xhat = (bn_x - mean) * rstd, formed at the end from
+//             sum(de * bn_x) - mean * sum(de)), for bn_bwd_apply.
+// These are memory-bound products (K = 64: 2 FLOP per output byte): on the implicit-GEMM
+// tile they ran at 2.6-3.5 TB/s (layer1 conv3 forward 195 us against 79 us of HBM traffic)
+// because every 128 x 128 block waited on its one K tile's load before its epilogue could
+// stream; here nothing waits on a barrier and every wave keeps a tile of loads in flight.
+//
+// The product is computed transposed, D[channel][pixel] = W[channel][:] . x[pixel][:], so
+// an MFMA lane's 4 accumulator rows are 4 CONSECUTIVE channels of one pixel: outputs and side
+// inputs move as 8-B vectors of NHWC rows, and a lane's statistics stay its own 4 channels
+// for the whole block (one shuffle reduction at the end).  Wave w owns 32 channels (2 MFMA
+// row tiles) of the block's 256; all 8 waves read the same x fragments (L1 hits).
+#include "common.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <stdexcept>
+
+namespace dtfx {
+namespace pw {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int NTW = 2, NW = 8;
+constexpr int NC = NW * NTW * 16;  // 256 channels per block
+constexpr int TM = 32;             // pixels per tile (16 for the 128-channel dgrad: registers)
+
+__device__ __forceinline__ unsigned short tobf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(unsigned short, b);
+}
+__device__ __forceinline__ float bf(short v) {
+  return __uint_as_float((unsigned)(unsigned short)v << 16);
+}
+
+// DG = false: x = input [M][K], w = weights [N][ldw] (row n: the K input channels).
+// DG = true:  x = dy [M][K], w = weights [K][ldw] (row k = output channel, N input channels).
+template <int K, bool DG>
+__global__ __launch_bounds__(512, 4) void conv1x1_kernel(
+    int M, int N, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
+    int ldw, unsigned short* __restrict__ y, const unsigned short* __restrict__ res,
+    const unsigned short* __restrict__ relu_y, const unsigned short* __restrict__ bn_x,
+    const float* __restrict__ bn_mean, const float* __restrict__ bn_rstd, float* __restrict__ ps,
+    float* __restrict__ pq) {
+  constexpr int KK = K / 32, MT = (K == 128 && DG) ? 1 : 2, TMK = 16 * MT;
+  const int nbn = N / NC, PB = gridDim.x / nbn;
+  // blocks b and b + 8 sit on one XCD: the column blocks of a pixel block share its x in L2
+  const int b = blockIdx.x, i8 = b >> 3;
+  const int cb = i8 % nbn, pb = (i8 / nbn) * 8 + (b & 7);
+  const int tid = threadIdx.x, lane = tid & 63, cl = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c0 = cb * NC + wave * (NTW * 16);
+  bf16x8 wf[NTW][KK];  // A operand: row = channel c0 + 16 j + cl, k = 32 kk + 8 g .. + 7
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int n = c0 + 16 * j + cl, k = 32 * kk + 8 * g;
+      if constexpr (!DG) {
+        wf[j][kk] = *(const bf16x8*)(w + (size_t)n * ldw + k);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) wf[j][kk][u] = (short)w[(size_t)(k + u) * ldw + n];
+      }
+    }
+  const bool stats = ps != nullptr;
+  float s1[NTW][4], s2[NTW][4];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+  const int T = M / TMK;
+  // B operand: pixel tt * TMK + 16 i + cl, k = 32 kk + 8 g .. + 7
+  auto load_x = [&](int tt, bf16x8 (&f)[MT][KK]) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+        f[i][kk] = *(const bf16x8*)(x + (size_t)(tt * TMK + 16 * i + cl) * K + 32 * kk + 8 * g);
+  };
+  bf16x8 xf[MT][KK];
+  if (pb < T) load_x(pb, xf);
+  for (int t = pb; t < T; t += PB) {
+    // this tile's side inputs (dgrad), then the next tile's pixels: both in flight during
+    // the MFMAs and ahead of this tile's stores
+    bf16x4 rv[NTW][MT], yv[NTW][MT], xv[NTW][MT];
+    if constexpr (DG) {
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const size_t off = (size_t)(t * TMK + 16 * i + cl) * N + c0 + 16 * j + 4 * g;
+          if (res) rv[j][i] = *(const bf16x4*)(res + off);
+          if (relu_y) yv[j][i] = *(const bf16x4*)(relu_y + off);
+          if (stats) xv[j][i] = *(const bf16x4*)(bn_x + off);
+        }
+    }
+    const bool more = t + PB < T;
+    bf16x8 xn[MT][KK];
+    if (more) load_x(t + PB, xn);
+    f32x4 acc[NTW][MT];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[i][kk], acc[j][i], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const size_t off = (size_t)(t * TMK + 16 * i + cl) * N + c0 + 16 * j + 4 * g;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[j][i][r];
+          if constexpr (DG) {
+            if (res) v += bf(rv[j][i][r]);
+            if (relu_y && !(bf(yv[j][i][r]) > 0.f)) v = 0.f;
+          }
+          o[r] = (short)tobf(v);
+          if constexpr (DG) {
+            const float d = bf(o[r]);
+            s1[j][r] += d;
+            s2[j][r] += d * (stats ? bf(xv[j][i][r]) : 0.f);
+          } else {
+            s1[j][r] += v;
+            s2[j][r] += v * v;
+          }
+        }
+        *(bf16x4*)(y + off) = o;
+      }
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) xf[i][kk] = xn[i][kk];
+    }
+  }
+  if (!stats) return;
+  // lanes cl = 0..15 hold the same 4 channels for 16 pixels: sum them
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {
+        s1[j][r] += __shfl_xor(s1[j][r], m);
+        s2[j][r] += __shfl_xor(s2[j][r], m);
+      }
+    }
+  if (cl == 0) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int ch = c0 + 16 * j + 4 * g;
+      f32x4 a, q;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = s1[j][r];
+        q[r] = DG ? bn_rstd[ch + r] * (s2[j][r] - bn_mean[ch + r] * s1[j][r]) : s2[j][r];
+      }
+      *(f32x4*)(ps + (size_t)pb * N + ch) = a;
+      *(f32x4*)(pq + (size_t)pb * N + ch) = q;
+    }
+  }
+}
+
+// Forward with a loader wave: wave NW (the ninth) only moves 64-pixel x tiles into a ring of
+// 3 LDS buffers (global_load_lds, counted vmcnt), the 8 compute waves only read LDS and store.
+// A wave that waits on a load also waits for every store it issued before that load (one
+// in-order vmcnt counter), so when the compute waves fetched their own pixels each held at
+// most a tile of stores in flight: ~5 us per 32-pixel tile, 2.2 TB/s.  Here nothing behind
+// the stores waits on memory.  x rows in LDS: 16-B chunk c of row r at c ^ swz(r) (K = 64:
+// 128-B rows, swz = (r >> 1) & 7; K = 128: 256-B rows, swz = r & 15): the 16 rows a fragment
+// read touches land on distinct bank groups.
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr int NBUF = 3;
+constexpr int OPITCH = NC * 2 + 16;  // output staging row (bytes): 16-B skew per pixel
+template <int K>
+constexpr int ftm() {  // pixels per tile: 64 (K = 64) / 32 (K = 128: LDS for 2 blocks per CU)
+  return K == 64 ? 64 : 32;
+}
+
+template <int K>
+__device__ __forceinline__ int xswz(int r) {
+  return K == 64 ? (r >> 1) & 7 : r & 15;
+}
+
+template <int K>
+__global__ __launch_bounds__(576, 5) void conv1x1_fwd_kernel(
+    int M, int N, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
+    int ldw, unsigned short* __restrict__ y, float* __restrict__ ps, float* __restrict__ pq) {
+  constexpr int FTM = ftm<K>(), KK = K / 32, MT = FTM / 16, CPR = K / 8;  // chunks per row
+  constexpr int TB = FTM * K * 2, NQ = TB / 1024;  // tile bytes, DMA rounds per tile
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* stg = sm + NBUF * TB;  // output staging [FTM][OPITCH]
+  const int nbn = N / NC, PB = gridDim.x / nbn;
+  const int b = blockIdx.x, i8 = b >> 3;
+  const int cb = i8 % nbn, pb = (i8 / nbn) * 8 + (b & 7);
+  const int tid = threadIdx.x, lane = tid & 63, cl = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T = M / FTM;
+  const int nmy = pb < T ? (T - pb + PB - 1) / PB : 0;  // this block's tiles pb, pb + PB, ...
+  if (wave == NW) {
+    auto issue = [&](int it) {
+      const int tile = pb + it * PB;
+      char* d = sm + (it % NBUF) * TB;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int P = q * 64 + lane, r = P / CPR, c = (P % CPR) ^ xswz<K>(r);
+        const unsigned short* src = x + ((size_t)tile * FTM + r) * K + c * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(d + q * 1024), 16, 0, 0);
+      }
+    };
+    if (nmy > 0) issue(0);
+    if (nmy > 1) {
+      issue(1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (int it = 0; it < nmy; ++it) {
+      if (it + 2 < nmy) {
+        issue(it + 2);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ) : "memory");  // tile it + 1 landed
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();  // (the compute waves' staging barrier)
+      __syncthreads();
+    }
+    return;
+  }
+  const int c0 = cb * NC + wave * (NTW * 16);
+  bf16x8 wf[NTW][KK];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+      wf[j][kk] = *(const bf16x8*)(w + (size_t)(c0 + 16 * j + cl) * ldw + 32 * kk + 8 * g);
+  float s1[NTW][4], s2[NTW][4];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+  __syncthreads();  // tile 0 in LDS
+  for (int it = 0; it < nmy; ++it) {
+    const char* xs = sm + (it % NBUF) * TB;
+    const int p0 = (pb + it * PB) * FTM;
+#pragma unroll(K == 64 ? MT : 1)
+    for (int i = 0; i < MT; ++i) {
+      bf16x8 xf[KK];
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const int r = 16 * i + cl;
+        xf[kk] = *(const bf16x8*)(xs + r * (K * 2) + (((4 * kk + g) ^ xswz<K>(r)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[kk], acc, 0, 0, 0);
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o[r] = (short)tobf(acc[r]);
+          s1[j][r] += acc[r];
+          s2[j][r] += acc[r] * acc[r];
+        }
+        *(bf16x4*)(stg + (16 * i + cl) * OPITCH + (wave * (NTW * 16) + 16 * j + 4 * g) * 2) = o;
+      }
+    }
+    __syncthreads();
+    // the block's FTM x 256 output rows as 16-B chunks: 32 chunks per pixel, 16 pixels per pass
+#pragma unroll
+    for (int q = 0; q < FTM / 16; ++q) {
+      const int e = q * 512 + tid, p = e >> 5, c = e & 31;
+      *(bf16x8*)(y + (size_t)(p0 + p) * N + cb * NC + c * 8) = *(const bf16x8*)(stg + p * OPITCH + c * 16);
+    }
+    __syncthreads();
+  }
+  if (!ps) return;
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {
+        s1[j][r] += __shfl_xor(s1[j][r], m);
+        s2[j][r] += __shfl_xor(s2[j][r], m);
+      }
+    }
+  if (cl == 0) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int ch = c0 + 16 * j + 4 * g;
+      f32x4 a, q;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = s1[j][r];
+        q[r] = s2[j][r];
+      }
+      *(f32x4*)(ps + (size_t)pb * N + ch) = a;
+      *(f32x4*)(pq + (size_t)pb * N + ch) = q;
+    }
+  }
+}
+
+// Data gradient with the loader wave: per 16-pixel tile the loader moves the dy rows
+// (swizzled, for the MFMA fragments) and the block's 256-channel slices of the shortcut
+// gradient, relu_y and bn_x (plain rows) into a 4-deep LDS ring; the compute waves stage the
+// f32 products through LDS and run the epilogue in row layout, so every side input is read and
+// every output written as 16-B chunks of whole 512-B row slices, and nothing that stores waits
+// on a load.  Thread t always owns channels 8 (t & 31) .. + 7 of the slice: its statistics
+// are summed over the block's pixels in registers and reduced across waves once at the end.
+constexpr int DTM = 16, DBUF = 4;
+constexpr int SPITCH = NC * 4 + 16;  // f32 staging row (bytes), 16-B skew per pixel
+
+template <int K, bool RES, bool BN>
+__global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
+    int M, int N, const unsigned short* __restrict__ dy, const unsigned short* __restrict__ w,
+    int ldw, unsigned short* __restrict__ dx, const unsigned short* __restrict__ res,
+    const unsigned short* __restrict__ relu_y, const unsigned short* __restrict__ bn_x,
+    const float* __restrict__ bn_mean, const float* __restrict__ bn_rstd, float* __restrict__ ps,
+    float* __restrict__ pq) {
+  constexpr int KK = K / 32, CPR = K / 8;
+  constexpr int DYB = DTM * K * 2, SB = DTM * NC * 2, NSIDE = (RES ? 1 : 0) + (BN ? 2 : 0);
+  constexpr int STAGE = DYB + NSIDE * SB, NQD = DYB / 1024, NQS = SB / 1024;
+  constexpr int NQT = NQD + NSIDE * NQS;  // DMA instructions per tile (<= 28)
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* stg = sm + DBUF * STAGE;
+  const int nbn = N / NC, PB = gridDim.x / nbn;
+  const int b = blockIdx.x, i8 = b >> 3;
+  const int cb = i8 % nbn, pb = (i8 / nbn) * 8 + (b & 7);
+  const int tid = threadIdx.x, lane = tid & 63, cl = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T = M / DTM;
+  const int nmy = pb < T ? (T - pb + PB - 1) / PB : 0;
+  if (wave == NW) {
+    auto issue = [&](int it) {
+      const int tile = pb + it * PB;
+      char* d = sm + (it % DBUF) * STAGE;
+#pragma unroll
+      for (int q = 0; q < NQD; ++q) {
+        const int P = q * 64 + lane, r = P / CPR, c = (P % CPR) ^ xswz<K>(r);
+        const unsigned short* src = dy + ((size_t)tile * DTM + r) * K + c * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(d + q * 1024), 16, 0, 0);
+      }
+      const unsigned short* sides[3] = {res, relu_y, bn_x};
+#pragma unroll
+      for (int si = 0; si < 3; ++si) {
+        if ((si == 0 && !RES) || (si > 0 && !BN)) continue;
+        const int slot = (RES ? si : si - 1);
+#pragma unroll
+        for (int q = 0; q < NQS; ++q) {
+          const int r = 2 * q + (lane >> 5), c = lane & 31;
+          const unsigned short* src = sides[si] + ((size_t)tile * DTM + r) * N + cb * NC + c * 8;
+          __builtin_amdgcn_global_load_lds((const void*)src,
+                                           (lds_void*)(d + DYB + slot * SB + q * 1024), 16, 0, 0);
+        }
+      }
+    };
+    for (int it = 0; it < 3 && it < nmy; ++it) issue(it);
+    if (nmy >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NQT) : "memory");
+    else if (nmy == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int it = 0; it < nmy; ++it) {
+      if (it + 3 < nmy) {
+        issue(it + 3);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NQT) : "memory");  // tile it + 1 landed
+      } else if (it + 2 < nmy) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQT) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();  // (the compute waves' staging barrier)
+      __syncthreads();
+    }
+    __syncthreads();  // (the statistics reduction's barrier)
+    return;
+  }
+  const int c0 = wave * (NTW * 16);  // the wave's channels inside the slice
+  bf16x8 wf[NTW][KK];                // A operand: W^T[n][k] = w[k][n]
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int n = cb * NC + c0 + 16 * j + cl, k = 32 * kk + 8 * g;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wf[j][kk][u] = (short)w[(size_t)(k + u) * ldw + n];
+    }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s1[u] = s2[u] = 0.f;
+  const int ep = tid >> 5, ec = tid & 31;  // epilogue: pixel, 16-B chunk of the slice
+  __syncthreads();  // tile 0 in LDS
+  for (int it = 0; it < nmy; ++it) {
+    const char* buf = sm + (it % DBUF) * STAGE;
+    const int p0 = (pb + it * PB) * DTM;
+    bf16x8 xf[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+      xf[kk] = *(const bf16x8*)(buf + cl * (K * 2) + (((4 * kk + g) ^ xswz<K>(cl)) << 4));
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[kk], acc, 0, 0, 0);
+      *(f32x4*)(stg + cl * SPITCH + (c0 + 16 * j + 4 * g) * 4) = acc;
+    }
+    __syncthreads();
+    {
+      const f32x4 a0 = *(const f32x4*)(stg + ep * SPITCH + ec * 32);
+      const f32x4 a1 = *(const f32x4*)(stg + ep * SPITCH + ec * 32 + 16);
+      float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const int so = ep * (NC * 2) + ec * 16;
+      if constexpr (RES) {
+        const bf16x8 r8 = *(const bf16x8*)(buf + DYB + so);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] += bf(r8[u]);
+      }
+      bf16x8 o;
+      if constexpr (BN) {
+        const bf16x8 y8 = *(const bf16x8*)(buf + DYB + (RES ? 1 : 0) * SB + so);
+        const bf16x8 x8 = *(const bf16x8*)(buf + DYB + (RES ? 2 : 1) * SB + so);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          o[u] = (short)tobf(bf(y8[u]) > 0.f ? v[u] : 0.f);
+          const float d = bf(o[u]);
+          s1[u] += d;
+          s2[u] += d * bf(x8[u]);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o[u] = (short)tobf(v[u]);
+      }
+      *(bf16x8*)(dx + (size_t)(p0 + ep) * N + cb * NC + ec * 8) = o;
+    }
+    __syncthreads();
+  }
+  if constexpr (BN) {
+    // channels 8 ec .. + 7: lanes l and l ^ 32 of a wave, then the 8 waves through LDS
+    float* red = (float*)stg;  // [8 waves][32 chunks][16]
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s1[u] += __shfl_xor(s1[u], 32);
+      s2[u] += __shfl_xor(s2[u], 32);
+    }
+    if (lane < 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        red[(wave * 32 + ec) * 16 + u] = s1[u];
+        red[(wave * 32 + ec) * 16 + 8 + u] = s2[u];
+      }
+    }
+    __syncthreads();
+    if (tid < NC) {
+      const int c = tid >> 3, u = tid & 7;
+      float a = 0.f, q = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < NW; ++wv) {
+        a += red[(wv * 32 + c) * 16 + u];
+        q += red[(wv * 32 + c) * 16 + 8 + u];
+      }
+      const int ch = cb * NC + tid;
+      ps[(size_t)pb * N + ch] = a;
+      pq[(size_t)pb * N + ch] = bn_rstd[ch] * (q - bn_mean[ch] * a);
+    }
+  } else {
+    __syncthreads();
+  }
+}
+
+}  // namespace pw
+
+bool conv1x1_applies(int M, int K, int N) {
+  const int nbn = N / pw::NC;  // column blocks: a power of two <= 8 (512 / nbn pixel blocks)
+  return (K == 64 || K == 128) && N % pw::NC == 0 && (nbn & (nbn - 1)) == 0 && nbn <= 8 &&
+         M % pw::TM == 0 && M > 0;
+}
+
+static bool conv1x1_loader() {  // DTFX_CONV1X1_LOADER=0: the kernels without the loader wave
+  static const bool on = [] {
+    const char* e = std::getenv("DTFX_CONV1X1_LOADER");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
+// Partial statistics rows a launch of this mode writes ([rows][N] each of ps / pq).
+int conv1x1_rows(int mode, int M, int K, int N) {
+  (void)K;
+  const int nbn = N / pw::NC;
+  if (conv1x1_loader() && mode == 2 && M % pw::DTM == 0) return 256 / nbn;  // 1 block per CU
+  return 512 / nbn;
+}
+
+// mode 1: forward (x [M][K], w [N][ldw]); mode 2: data gradient (x = dy [M][K], w [K][ldw],
+// optional residual, relu_y (mask), bn_x / mean / rstd (statistics)).  ps / pq (optional):
+// conv1x1_rows() partial rows of N floats each.
+void conv1x1_launch(int mode, int M, int K, int N, const void* x, const void* w, int ldw, void* y,
+                    const void* res, const void* relu_y, const void* bn_x, const float* mean,
+                    const float* rstd, float* ps, float* pq, hipStream_t s) {
+  using namespace pw;
+  if (!conv1x1_applies(M, K, N)) throw std::runtime_error("conv1x1: unsupported shape");
+  if (ldw % 8 || (mode == 1 ? ldw < K : ldw < N) ||
+      (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) & 15) ||
+      (((uintptr_t)res | (uintptr_t)relu_y | (uintptr_t)bn_x) & 7))
+    throw std::runtime_error("conv1x1: ldw % 8, ldw >= reduction row, aligned tensors");
+  if ((ps != nullptr) != (pq != nullptr) ||
+      (mode == 2 && ps && (!bn_x || !mean || !rstd)))
+    throw std::runtime_error("conv1x1: statistics need ps, pq (and for dgrad bn_x, mean, rstd)");
+  const int nbn = N / NC;
+  // 2 blocks of 8 waves per CU; the pixel-block count a multiple of 8 (XCD pairing)
+  const int PB = 512 / nbn;
+  const dim3 grid(PB * nbn), blk(512);
+#define DTFX_PW_LAUNCH(KV, DGV)                                                                 \
+  hipLaunchKernelGGL((conv1x1_kernel<KV, DGV>), grid, blk, 0, s, M, N, (const unsigned short*)x, \
+                     (const unsigned short*)w, ldw, (unsigned short*)y,                           \
+                     (const unsigned short*)res, (const unsigned short*)relu_y,                   \
+                     (const unsigned short*)bn_x, mean, rstd, ps, pq)
+  const bool loader = conv1x1_loader();
+  if (mode == 2 && loader && M % DTM == 0) {
+    const bool res_ = res != nullptr, bn_ = ps != nullptr;
+    if (bn_ && !relu_y) throw std::runtime_error("conv1x1 dgrad: statistics need relu_y");
+    const size_t lds = (size_t)DBUF * (DTM * K * 2 + ((res_ ? 1 : 0) + (bn_ ? 2 : 0)) * DTM * NC * 2) +
+                       (size_t)DTM * SPITCH;
+    const dim3 g2(256 / nbn * nbn);
+#define DTFX_PW_DG(KV, RV, BV)                                                                  \
+  do {                                                                                          \
+    static bool attr_ = false;                                                                  \
+    if (!attr_) {                                                                               \
+      DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_dgrad_kernel<KV, RV, BV>,         \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); \
+      attr_ = true;                                                                             \
+    }                                                                                           \
+    hipLaunchKernelGGL((conv1x1_dgrad_kernel<KV, RV, BV>), g2, dim3(576), lds, s, M, N,         \
+                       (const unsigned short*)x, (const unsigned short*)w, ldw,                 \
+                       (unsigned short*)y, (const unsigned short*)res,                          \
+                       (const unsigned short*)relu_y, (const unsigned short*)bn_x, mean, rstd,  \
+                       ps, pq);                                                                 \
+  } while (0)
+    if (K == 64) {
+      if (res_ && bn_) DTFX_PW_DG(64, true, true);
+      else if (res_) DTFX_PW_DG(64, true, false);
+      else if (bn_) DTFX_PW_DG(64, false, true);
+      else DTFX_PW_DG(64, false, false);
+    } else {
+      if (res_ && bn_) DTFX_PW_DG(128, true, true);
+      else if (res_) DTFX_PW_DG(128, true, false);
+      else if (bn_) DTFX_PW_DG(128, false, true);
+      else DTFX_PW_DG(128, false, false);
+    }
+#undef DTFX_PW_DG
+  } else if (mode == 1 && loader && M % (K == 64 ? ftm<64>() : ftm<128>()) == 0) {
+    const int ft = K == 64 ? ftm<64>() : ftm<128>();
+    const size_t lds = (size_t)NBUF * ft * K * 2 + (size_t)ft * OPITCH;
+    if (K == 64)
+      hipLaunchKernelGGL(conv1x1_fwd_kernel<64>, grid, dim3(576), lds, s, M, N,
+                         (const unsigned short*)x, (const unsigned short*)w, ldw,
+                         (unsigned short*)y, ps, pq);
+    else
+      hipLaunchKernelGGL(conv1x1_fwd_kernel<128>, grid, dim3(576), lds, s, M, N,
+                         (const unsigned short*)x, (const unsigned short*)w, ldw,
+                         (unsigned short*)y, ps, pq);
+  } else if (mode == 1) {
+    if (K == 64) DTFX_PW_LAUNCH(64, false);
+    else DTFX_PW_LAUNCH(128, false);
+  } else if (mode == 2) {
+    if (K == 64) DTFX_PW_LAUNCH(64, true);
+    else DTFX_PW_LAUNCH(128, true);
+  } else {
+    throw std::runtime_error("conv1x1: mode 1 (forward) or 2 (dgrad)");
+  }
+#undef DTFX_PW_LAUNCH
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dtfx

@@ -688,6 +688,198 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_kernel(
   }
 }
 
+// Attention backward in two query halves: the same math as attn_bwd_kernel with 72 KB of LDS
+// instead of 141 KB, so two blocks share a CU (the first version's single resident block
+// left every global-load and barrier latency exposed: 69 us at BERT-base's seq 128 against
+// ~13 us of MFMA work).  K stays in LDS for the block; per half of 64 queries Q_h, dO_h and
+// P_h^T / dS_h^T (keys x queries) are staged, V's fragments are read from L2 (each wave needs
+// only its 4 key tiles); dV / dK accumulate in registers over the halves, dQ_h is final per
+// half.  P = exp(S * scale + mask - lse) needs no row maximum, so any tiling works.
+namespace atb {
+constexpr int HQ = 64;                  // queries per half
+constexpr int QH = HQ * at::LDQ;        // 9216 B
+constexpr int PT = at::SP * at::LDQ;    // [128 keys][64 queries] with 144-B rows: 18432 B
+constexpr int LDS = at::QB + 2 * QH + 2 * PT + HQ * 4;  // 73984
+}  // namespace atb
+
+__global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
+    int S, int nh, const unsigned short* __restrict__ qkv, const unsigned short* __restrict__ o,
+    const unsigned short* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ kmask, float scale, unsigned short* __restrict__ dqkv,
+    float* __restrict__ dbias) {
+  using namespace at;
+  using namespace atb;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* Ks = sm;
+  char* Qh = Ks + QB;
+  char* dOh = Qh + QH;
+  char* PTs = dOh + QH;
+  char* dSTs = PTs + PT;
+  float* Dr = (float*)(dSTs + PT);
+  const int b = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int Hd = nh * D, ld = 3 * Hd;
+  const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
+  const unsigned short* obase = o + (size_t)b * S * Hd + h * D;
+  const unsigned short* dobase = dout + (size_t)b * S * Hd + h * D;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int cl = lane & 15, g = lane >> 4, rg = g * 4;
+  {  // K: 128 rows x 8 chunks, 2 per thread (rows >= S zero)
+    bf16x8 kv[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + 512 * k, r = e >> 3, c = e & 7;
+      kv[k] = *(const bf16x8*)(base + Hd + (size_t)min(r, S - 1) * ld + c * 8);
+      if (r >= S) kv[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + 512 * k;
+      *(bf16x8*)(Ks + (e >> 3) * LDQ + (e & 7) * 16) = kv[k];
+    }
+  }
+  const float* L = lse + ((size_t)b * nh + h) * SP;
+  const int qt = wave & 3, kt0 = (wave >> 2) * 4;  // phase 1: query tile, 4 key tiles
+  f32x4 av[4], ak[4];  // dV / dK of key tile `wave`, 4 d tiles, over both halves
+#pragma unroll
+  for (int j = 0; j < 4; ++j) av[j] = ak[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  unsigned short* dq = dqkv + (size_t)b * S * ld + h * D;
+  for (int q0 = 0; q0 < S; q0 += HQ) {
+    {  // Q_h, dO_h (64 rows x 8 chunks: one each per thread) and D = rowsum(dO * O)
+      const int r = tid >> 3, c = tid & 7, row = q0 + r, rr = min(row, S - 1);
+      bf16x8 qv = *(const bf16x8*)(base + (size_t)rr * ld + c * 8);
+      bf16x8 dv = *(const bf16x8*)(dobase + (size_t)rr * Hd + c * 8);
+      const bf16x8 ov = *(const bf16x8*)(obase + (size_t)rr * Hd + c * 8);
+      float f0[8], f1[8], d = 0.f;
+      unpack8(ov, f0);
+      unpack8(dv, f1);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) d += f0[u] * f1[u];
+      d += __shfl_xor(d, 1);
+      d += __shfl_xor(d, 2);
+      d += __shfl_xor(d, 4);
+      if (row >= S) {
+        qv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        dv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+      __syncthreads();  // the previous half's phase 2 is done with Q_h / dO_h / P^T / dS^T
+      *(bf16x8*)(Qh + r * LDQ + c * 16) = qv;
+      *(bf16x8*)(dOh + r * LDQ + c * 16) = dv;
+      if (c == 0) Dr[r] = row < S ? d : 0.f;
+      __syncthreads();
+    }
+    // phase 1: S and dP tiles (query tile qt x key tiles kt0..kt0+3) -> P^T, dS^T
+    {
+      bf16x8 aq[2], ado[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        aq[kk] = lfrag<true>(Qh, LDQ, 16 * qt, 32 * kk, lane);
+        ado[kk] = lfrag<true>(dOh, LDQ, 16 * qt, 32 * kk, lane);
+      }
+      float lr[4], dr[4];
+      bool live[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = 16 * qt + rg + r, row = q0 + ql;
+        live[r] = row < S;
+        lr[r] = live[r] ? L[row] : 0.f;
+        dr[r] = Dr[ql];
+      }
+#pragma unroll 1
+      for (int j = 0; j < 4; ++j) {
+        const int kt = kt0 + j, key = 16 * kt + cl;
+        const float kmj = key < S ? (kmask ? kmask[(size_t)b * S + key] : 0.f) : -INFINITY;
+        f32x4 sa = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          bf16x8 vb = *(const bf16x8*)(base + 2 * Hd + (size_t)min(key, S - 1) * ld + 32 * kk + 8 * g);
+          if (key >= S) vb = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+          sa = mma(aq[kk], lfrag<true>(Ks, LDQ, 16 * kt, 32 * kk, lane), sa);
+          dp = mma(ado[kk], vb, dp);
+        }
+        bf16x4 pv, dsv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = live[r] ? __expf(sa[r] * scale + kmj - lr[r]) : 0.f;
+          pv[r] = (short)tobf(p);
+          dsv[r] = (short)tobf(p * (dp[r] - dr[r]));
+        }
+        const int off = key * LDQ + (16 * qt + rg) * 2;
+        *(bf16x4*)(PTs + off) = pv;
+        *(bf16x4*)(dSTs + off) = dsv;
+      }
+    }
+    __syncthreads();
+    // phase 2: dV += P^T dO_h, dK += dS^T Q_h (key tile `wave`); dQ_h = dS K
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 pT = lfrag<true>(PTs, LDQ, 16 * wave, 32 * kk, lane);
+      const bf16x8 dsT = lfrag<true>(dSTs, LDQ, 16 * wave, 32 * kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        av[j] = mma(pT, lfrag<false>(dOh, LDQ, 16 * j, 32 * kk, lane), av[j]);
+        ak[j] = mma(dsT, lfrag<false>(Qh, LDQ, 16 * j, 32 * kk, lane), ak[j]);
+      }
+    }
+    {
+      const int dt0 = 2 * (wave >> 2);
+      f32x4 aq[2];
+      aq[0] = aq[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const bf16x8 dsr = lfrag<false>(dSTs, LDQ, 16 * qt, 32 * kk, lane);
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          aq[jj] = mma(dsr, lfrag<false>(Ks, LDQ, 16 * (dt0 + jj), 32 * kk, lane), aq[jj]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = q0 + 16 * qt + rg + r;
+        if (row < S)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            dq[(size_t)row * ld + 16 * (dt0 + jj) + cl] = tobf(aq[jj][r] * scale);
+      }
+      if (dbias) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          float sq = aq[jj][0] + aq[jj][1] + aq[jj][2] + aq[jj][3];
+          sq += __shfl_xor(sq, 16);
+          sq += __shfl_xor(sq, 32);
+          if (lane < 16) unsafeAtomicAdd(dbias + h * D + 16 * (dt0 + jj) + cl, sq * scale);
+        }
+      }
+    }
+  }
+  // dK, dV of key tile `wave`
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 16 * wave + rg + r;
+    if (row < S)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t off = (size_t)row * ld + 16 * j + cl;
+        dq[off + Hd] = tobf(ak[j][r] * scale);
+        dq[off + 2 * Hd] = tobf(av[j][r]);
+      }
+  }
+  if (dbias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float sk = ak[j][0] + ak[j][1] + ak[j][2] + ak[j][3];
+      float sv = av[j][0] + av[j][1] + av[j][2] + av[j][3];
+      sk += __shfl_xor(sk, 16);
+      sk += __shfl_xor(sk, 32);
+      sv += __shfl_xor(sv, 16);
+      sv += __shfl_xor(sv, 32);
+      if (lane < 16) {
+        const int c = h * D + 16 * j + cl;
+        unsafeAtomicAdd(dbias + Hd + c, sk * scale);
+        unsafeAtomicAdd(dbias + 2 * Hd + c, sv);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Mixed-precision Adam(W): f32 master p, grad g, moments m, v; writes the bf16
 // working copy pb used by the GEMMs.  Grad scale folds the 1/world average.
@@ -942,6 +1134,11 @@ void attn_fwd_launch(int Bn, int S, int nh, const void* qkv, void* out, float* l
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+// Attention-backward kernel: -1 = from the environment, 0: attn_bwd_kernel<8>,
+// 1: attn_bwd_kernel<4>, 2: attn_bwd_half_kernel (tests run every variant in one process).
+static int g_attn_bwd_variant = -1;
+void attn_bwd_set_variant(int v) { g_attn_bwd_variant = v; }
+
 void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, const void* dout,
                      const float* lse, const float* kmask, float scale, void* dqkv, float* dbias,
                      hipStream_t s) {
@@ -959,7 +1156,27 @@ void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, cons
     const char* e = std::getenv("DTFX_ATTN_BWD_WAVES");
     return e && std::atoi(e) == 4 ? 4 : 8;
   }();
-  if (nw == 4)
+  // DTFX_ATTN_BWD_HALF=1: the two-blocks-per-CU kernel.  Alone it is 18 % faster (BERT-base
+  // shape, batch 128: 56 vs 69 us), but in the BERT step it runs beside the weight-gradient
+  // GEMMs of the second stream and both take 94 us there (rocprofv3, same box); end to end
+  // 7892 vs 7924 seq/s over 3 interleaved rounds, so it stays opt-in.
+  static const bool half = [] {
+    const char* e = std::getenv("DTFX_ATTN_BWD_HALF");
+    return e && std::atoi(e) == 1;
+  }();
+  const int var = g_attn_bwd_variant >= 0 ? g_attn_bwd_variant : half ? 2 : nw == 4 ? 1 : 0;
+  if (var == 2) {
+    static bool hattr = false;
+    if (!hattr) {
+      DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_half_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, atb::LDS));
+      hattr = true;
+    }
+    hipLaunchKernelGGL(attn_bwd_half_kernel, dim3(Bn * nh), dim3(512), atb::LDS, s, S, nh,
+                       (const unsigned short*)qkv, (const unsigned short*)o,
+                       (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv,
+                       dbias);
+  } else if (var == 1)
     hipLaunchKernelGGL(attn_bwd_kernel<4>, dim3(Bn * nh), dim3(256), lds, s, S, nh,
                        (const unsigned short*)qkv, (const unsigned short*)o,
                        (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv,

@@ -20,6 +20,14 @@ from ._ext import hip, ptr, stream_handle
 
 # split-K partials through a workspace + reduce pass (DTFX_SPLITK_WS=0: f32 atomics into the output)
 _SPLITK_WS = os.environ.get("DTFX_SPLITK_WS", "1") != "0"
+# 1x1 / stride-1 convolutions with 64 / 128 reduction channels on the streaming kernel
+# (csrc/kernels/conv1x1.hip); DTFX_CONV1X1=0: the implicit-GEMM path (A/B runs)
+_CONV1X1 = os.environ.get("DTFX_CONV1X1", "1") != "0"
+
+
+def _pointwise(KH, KW, stride, pad, M, K, N, w):
+    return (_CONV1X1 and KH == 1 and KW == 1 and stride == 1 and pad == 0 and w.stride(0) % 8 == 0
+            and hip().conv1x1_applies(M, K, N))
 
 BF16 = torch.bfloat16
 
@@ -91,6 +99,20 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
         hip().colpart_reduce(part.shape[1], Cout, ptr(part[0]), ptr(part[1]), ptr(colsum),
                              ptr(colsq), stream_handle())
         return y
+    if residual is None and _pointwise(KH, KW, stride, pad, N * H * W, C, Cout, w):
+        # layer1 / layer2 expansions (64 -> 256, 128 -> 512): weights in registers, pixels
+        # streamed; one partial statistics row per persistent pixel block
+        M = N * H * W
+        ps = pq = None
+        if colsum is not None:
+            part = torch.empty(2, hip().conv1x1_rows(1, M, C, Cout), Cout, device=x.device)
+            ps, pq = part[0], part[1]
+        hip().conv1x1(1, M, C, Cout, ptr(x), ptr(w), w.stride(0), ptr(y), 0, 0, 0, 0, 0, ptr(ps),
+                      ptr(pq), stream_handle())
+        if colsum is not None:
+            hip().colpart_reduce(ps.shape[0], Cout, ptr(ps), ptr(pq), ptr(colsum), ptr(colsq),
+                                 stream_handle())
+        return y
     ps = pq = None
     if colsum is not None:
         rows = (N * OH * OW + 63) // 64  # one partial row per 64-row output slab
@@ -156,6 +178,23 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
         part = torch.empty(2, 8 * (N * H * W // 112), C, device=dy.device)
         hip().conv3x3_c64_dgrad(N, H, W, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(y), ptr(x),
                                 ptr(mean), ptr(rstd), ptr(part[0]), ptr(part[1]), stream_handle())
+        hip().colpart_reduce(part.shape[1], C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
+                             stream_handle())
+        return dx
+    if _pointwise(KH, KW, stride, pad, N * H * W, Cout, C, w):
+        # conv1's data gradient in layer1 / layer2 (64 / 128 -> 256 / 512 channels): the
+        # streaming 1x1 kernel, shortcut gradient, ReLU mask and BN reductions fused
+        M = N * H * W
+        if bn is None:
+            hip().conv1x1(2, M, Cout, C, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(residual), 0,
+                          0, 0, 0, 0, 0, stream_handle())
+            return dx
+        y, x, mean, rstd, sdy, sdx = bn
+        if y.shape != dx.shape or x.shape != dx.shape:
+            raise ValueError("fused BN backward: y and x must have the dgrad output's shape")
+        part = torch.empty(2, hip().conv1x1_rows(2, M, Cout, C), C, device=dy.device)
+        hip().conv1x1(2, M, Cout, C, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(residual), ptr(y),
+                      ptr(x), ptr(mean), ptr(rstd), ptr(part[0]), ptr(part[1]), stream_handle())
         hip().colpart_reduce(part.shape[1], C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
                              stream_handle())
         return dx

@@ -29,6 +29,11 @@ CONVS = [  # N, H, W, C, Cout, k, stride, pad
     (3, 60, 60, 256, 1024, 1, 1, 0),  # same, M = 10800: ragged 256-row block and 64-row slab
     (3, 60, 60, 64, 1024, 3, 1, 1),  # 3x3 forward on the 8-phase gather (ragged M)
     (4, 64, 64, 1024, 256, 3, 2, 1),  # stride-2 dgrad classes on the 8-phase gather
+    (2, 16, 16, 64, 256, 1, 1, 0),   # streaming 1x1 kernel (conv1x1.hip): forward K = 64
+    (2, 8, 8, 128, 512, 1, 1, 0),    # forward K = 128, two column blocks
+    (1, 8, 4, 64, 2048, 1, 1, 0),    # one 32-pixel tile, 8 column blocks, idle pixel blocks
+    (2, 16, 16, 256, 64, 1, 1, 0),   # dgrad K = 64 -> 256 channels
+    (2, 8, 8, 512, 128, 1, 1, 0),    # dgrad K = 128 -> 512 channels (16-pixel tiles)
 ]
 
 
@@ -72,6 +77,9 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, W, C, Co, k, s, p):
     (2, 28, 28, 128, 128, 3, 1, 1, False),  # 128-channel 3x3 kernel with the fused BN backward
     (4, 64, 64, 1024, 256, 3, 2, 1, True),  # 8-phase dgrad: per-slab BN columns, class rows
     (4, 64, 64, 1024, 256, 1, 1, 0, True),  # 8-phase 1x1 dgrad
+    (2, 16, 16, 256, 64, 1, 1, 0, True),   # streaming 1x1 dgrad (conv1x1.hip), K = 64
+    (2, 8, 8, 512, 128, 1, 1, 0, True),    # K = 128, two column blocks
+    (2, 16, 16, 256, 128, 1, 1, 0, False),  # K = 128 -> 256, no shortcut gradient
 ])
 def test_conv_dgrad_fused_batchnorm_backward(gpu, N, H, W, C, Co, k, s, p, with_res):
     """dgrad with BatchNorm backward's reductions in its epilogue (+ shortcut gradient, ReLU
@@ -157,3 +165,14 @@ def test_sgd_momentum_mixed(gpu):
         cnn.sgd_momentum_mixed(p, g, v, None, 0.1, 0.9, 1e-4, 0.5)
     assert torch.allclose(P.cpu(), p, atol=1e-6)
     assert torch.equal(pb.cpu(), P.cpu().to(BF))
+
+
+@pytest.mark.parametrize("N,H,W,C,Co", [(2, 16, 16, 256, 64), (2, 8, 8, 512, 128)])
+def test_conv1x1_dgrad_residual_only(gpu, N, H, W, C, Co):
+    """The first bottleneck's conv1 dgrad: the shortcut gradient added, no BN fused."""
+    w = _r(Co, C, seed=21, scale=C ** -0.5).to(BF)
+    dy = _r(N, H, W, Co, seed=22).to(BF)
+    res = _r(N, H, W, C, seed=23).to(BF)
+    dx = cnn.conv_dgrad(dy.to(gpu), w.to(gpu), (N, H, W, C), 1, 1, 1, 0, residual=res.to(gpu))
+    dxr = cnn.conv_dgrad(dy, w, (N, H, W, C), 1, 1, 1, 0, residual=res)
+    assert (dx.cpu().float() - dxr.float()).abs().max() < 3e-2 * dxr.float().abs().max()

@@ -3,6 +3,7 @@
 import pytest
 import torch
 
+from distributedtensorflowexample_amd.ops import _ext
 from distributedtensorflowexample_amd.ops import transformer as T
 
 pytestmark = pytest.mark.gpu
@@ -52,8 +53,9 @@ def test_embedding_fwd_bwd(gpu):
         assert torch.allclose(a.cpu(), b, atol=1e-3)
 
 
-@pytest.mark.parametrize("S,masked", [(128, False), (128, True), (77, True), (64, False)])
-def test_attention_fwd_bwd(gpu, S, masked):
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("S,masked", [(128, False), (128, True), (77, True), (64, False), (33, True)])
+def test_attention_fwd_bwd(gpu, S, masked, variant):
     B, nh = 3, 4
     qkv = _r(B * S, 3 * nh * 64, seed=10).to(BF)
     kmask = None
@@ -65,7 +67,13 @@ def test_attention_fwd_bwd(gpu, S, masked):
     assert (o.cpu().float() - orf.float()).abs().max() < 2e-2
     assert (lse.cpu().view(B, nh, -1)[..., :S] - lser.view(B, nh, -1)[..., :S]).abs().max() < 1e-3
     dout = _r(B * S, nh * 64, seed=11).to(BF)
-    dq = T.attn_bwd(qkv.to(gpu), o, dout.to(gpu), lse, B, S, nh, kmask.to(gpu) if masked else None)
+    hip = _ext.hip()
+    hip.attn_bwd_set_variant(variant)
+    try:
+        dq = T.attn_bwd(qkv.to(gpu), o, dout.to(gpu), lse, B, S, nh, kmask.to(gpu) if masked else None)
+        torch.cuda.synchronize()
+    finally:
+        hip.attn_bwd_set_variant(-1)
     dqr = T.attn_bwd(qkv, o.cpu(), dout, lse.cpu(), B, S, nh, kmask)
     err = (dq.cpu().float() - dqr.float()).abs().max().item()
     assert err < 3e-2 * max(1.0, dqr.float().abs().max().item()), err
