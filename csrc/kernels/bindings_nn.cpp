@@ -45,7 +45,7 @@ bool conv3x3_c128_applies(int, int, int, int, int, int, int, int);
 bool conv1x1_applies(int, int, int);
 int conv1x1_rows(int, int, int, int);
 void conv1x1_launch(int, int, int, int, const void*, const void*, int, void*, const void*,
-                    const void*, const void*, const float*, const float*, float*, float*,
+                    const void*, const void*, const float*, const float*, float*, float*, void*,
                     hipStream_t);
 void conv3x3_c128_launch(int, int, int, int, const void*, const void*, int, void*, void*,
                          const void*, const void*, const float*, const float*, float*, float*,
@@ -254,11 +254,11 @@ void register_nn(py::module_& m) {
   m.def("conv1x1_rows", &dtfx::conv1x1_rows, "(mode, M, K, N): partial statistics rows a launch writes");
   m.def("conv1x1", [](int mode, int M, int K, int N, uintptr_t x, uintptr_t w, int ldw,
                       uintptr_t y, uintptr_t res, uintptr_t relu_y, uintptr_t bn_x, uintptr_t mean,
-                      uintptr_t rstd, uintptr_t ps, uintptr_t pq, uintptr_t s) {
+                      uintptr_t rstd, uintptr_t ps, uintptr_t pq, uintptr_t wt, uintptr_t s) {
     dtfx::conv1x1_launch(mode, M, K, N, P<const void>(x), P<const void>(w), ldw, P<void>(y),
                          P<const void>(res), P<const void>(relu_y), P<const void>(bn_x),
                          P<const float>(mean), P<const float>(rstd), P<float>(ps), P<float>(pq),
-                         S(s));
+                         P<void>(wt), S(s));
   });
   m.def("conv3x3_c128_applies", &dtfx::conv3x3_c128_applies,
         "the 128-channel 3x3 kernel handles this conv (stride 1, pad 1, H % 4, W % 28)");

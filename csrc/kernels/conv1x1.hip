@@ -1,23 +1,21 @@
-// 1x1 / stride 1 convolutions with 64 or 128 reduction channels and >= 256 output channels
-// (ResNet-50's layer1 / layer2 expansions: conv3 and layer1's downsample forward, 64 -> 256
-// and 128 -> 512; conv1's data gradient, 64 -> 256 and 128 -> 256 / 512), NHWC bf16, as a
-// streaming product: persistent blocks, the weights held in REGISTERS for the block's life,
-// per 32-pixel tile only the pixels' K channels read (prefetched a tile ahead) and the
-// output written, with the BatchNorm work fused:
+// 1x1 / stride 1 convolutions with 64, 128 or 256 reduction channels and 256 * 2^i output
+// channels (ResNet-50's expansions: conv3 and layer1's downsample forward, 64 -> 256,
+// 128 -> 512, 256 -> 1024; conv1's data gradient, 64 / 128 / 256 -> 256 ... 1024), NHWC
+// bf16, as a streaming product: persistent blocks, the weights held in REGISTERS for the
+// block's life, per pixel tile only the pixels' K channels read and the output written, with
+// the BatchNorm work fused:
 //   forward:  y = x W^T, partial rows of sum(y) / sum(y^2) per output channel;
 //   dgrad:    de = (dy W + residual) * (relu_y > 0), partial rows of sum(de) and
 //             sum(de * xhat) (xhat = (bn_x - mean) * rstd, formed at the end from
 //             sum(de * bn_x) - mean * sum(de)), for bn_bwd_apply.
 // These are memory-bound products (K = 64: 2 FLOP per output byte): on the implicit-GEMM
-// tile they ran at 2.6-3.5 TB/s (layer1 conv3 forward 195 us against 79 us of HBM traffic)
-// because every 128 x 128 block waited on its one K tile's load before its epilogue could
-// stream; here nothing waits on a barrier and every wave keeps a tile of loads in flight.
+// tile they ran at 2.4-3.5 TB/s (layer1 conv3 forward 216 us against 79 us of HBM traffic);
+// here 4.1-6.1 TB/s (profiles/r2/conv1x1_streaming.txt).
 //
 // The product is computed transposed, D[channel][pixel] = W[channel][:] . x[pixel][:], so
 // an MFMA lane's 4 accumulator rows are 4 CONSECUTIVE channels of one pixel: outputs and side
 // inputs move as 8-B vectors of NHWC rows, and a lane's statistics stay its own 4 channels
-// for the whole block (one shuffle reduction at the end).  Wave w owns 32 channels (2 MFMA
-// row tiles) of the block's 256; all 8 waves read the same x fragments (L1 hits).
+// for the whole block.  Compute wave w owns 32 channels (2 MFMA row tiles) of the block's 256.
 #include "common.h"
 
 #include <algorithm>
@@ -32,7 +30,6 @@ typedef short bf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NTW = 2, NW = 8;
 constexpr int NC = NW * NTW * 16;  // 256 channels per block
-constexpr int TM = 32;             // pixels per tile (16 for the 128-channel dgrad: registers)
 
 __device__ __forceinline__ unsigned short tobf(float f) {
   __bf16 b = (__bf16)f;
@@ -42,157 +39,24 @@ __device__ __forceinline__ float bf(short v) {
   return __uint_as_float((unsigned)(unsigned short)v << 16);
 }
 
-// DG = false: x = input [M][K], w = weights [N][ldw] (row n: the K input channels).
-// DG = true:  x = dy [M][K], w = weights [K][ldw] (row k = output channel, N input channels).
-template <int K, bool DG>
-__global__ __launch_bounds__(512, 4) void conv1x1_kernel(
-    int M, int N, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
-    int ldw, unsigned short* __restrict__ y, const unsigned short* __restrict__ res,
-    const unsigned short* __restrict__ relu_y, const unsigned short* __restrict__ bn_x,
-    const float* __restrict__ bn_mean, const float* __restrict__ bn_rstd, float* __restrict__ ps,
-    float* __restrict__ pq) {
-  constexpr int KK = K / 32, MT = (K == 128 && DG) ? 1 : 2, TMK = 16 * MT;
-  const int nbn = N / NC, PB = gridDim.x / nbn;
-  // blocks b and b + 8 sit on one XCD: the column blocks of a pixel block share its x in L2
-  const int b = blockIdx.x, i8 = b >> 3;
-  const int cb = i8 % nbn, pb = (i8 / nbn) * 8 + (b & 7);
-  const int tid = threadIdx.x, lane = tid & 63, cl = lane & 15, g = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int c0 = cb * NC + wave * (NTW * 16);
-  bf16x8 wf[NTW][KK];  // A operand: row = channel c0 + 16 j + cl, k = 32 kk + 8 g .. + 7
-#pragma unroll
-  for (int j = 0; j < NTW; ++j)
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      const int n = c0 + 16 * j + cl, k = 32 * kk + 8 * g;
-      if constexpr (!DG) {
-        wf[j][kk] = *(const bf16x8*)(w + (size_t)n * ldw + k);
-      } else {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) wf[j][kk][u] = (short)w[(size_t)(k + u) * ldw + n];
-      }
-    }
-  const bool stats = ps != nullptr;
-  float s1[NTW][4], s2[NTW][4];
-#pragma unroll
-  for (int j = 0; j < NTW; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
-  const int T = M / TMK;
-  // B operand: pixel tt * TMK + 16 i + cl, k = 32 kk + 8 g .. + 7
-  auto load_x = [&](int tt, bf16x8 (&f)[MT][KK]) {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk)
-        f[i][kk] = *(const bf16x8*)(x + (size_t)(tt * TMK + 16 * i + cl) * K + 32 * kk + 8 * g);
-  };
-  bf16x8 xf[MT][KK];
-  if (pb < T) load_x(pb, xf);
-  for (int t = pb; t < T; t += PB) {
-    // this tile's side inputs (dgrad), then the next tile's pixels: both in flight during
-    // the MFMAs and ahead of this tile's stores
-    bf16x4 rv[NTW][MT], yv[NTW][MT], xv[NTW][MT];
-    if constexpr (DG) {
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          const size_t off = (size_t)(t * TMK + 16 * i + cl) * N + c0 + 16 * j + 4 * g;
-          if (res) rv[j][i] = *(const bf16x4*)(res + off);
-          if (relu_y) yv[j][i] = *(const bf16x4*)(relu_y + off);
-          if (stats) xv[j][i] = *(const bf16x4*)(bn_x + off);
-        }
-    }
-    const bool more = t + PB < T;
-    bf16x8 xn[MT][KK];
-    if (more) load_x(t + PB, xn);
-    f32x4 acc[NTW][MT];
-#pragma unroll
-    for (int j = 0; j < NTW; ++j)
-#pragma unroll
-      for (int i = 0; i < MT; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[i][kk], acc[j][i], 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < NTW; ++j)
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const size_t off = (size_t)(t * TMK + 16 * i + cl) * N + c0 + 16 * j + 4 * g;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = acc[j][i][r];
-          if constexpr (DG) {
-            if (res) v += bf(rv[j][i][r]);
-            if (relu_y && !(bf(yv[j][i][r]) > 0.f)) v = 0.f;
-          }
-          o[r] = (short)tobf(v);
-          if constexpr (DG) {
-            const float d = bf(o[r]);
-            s1[j][r] += d;
-            s2[j][r] += d * (stats ? bf(xv[j][i][r]) : 0.f);
-          } else {
-            s1[j][r] += v;
-            s2[j][r] += v * v;
-          }
-        }
-        *(bf16x4*)(y + off) = o;
-      }
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk) xf[i][kk] = xn[i][kk];
-    }
-  }
-  if (!stats) return;
-  // lanes cl = 0..15 hold the same 4 channels for 16 pixels: sum them
-#pragma unroll
-  for (int j = 0; j < NTW; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int m = 1; m < 16; m <<= 1) {
-        s1[j][r] += __shfl_xor(s1[j][r], m);
-        s2[j][r] += __shfl_xor(s2[j][r], m);
-      }
-    }
-  if (cl == 0) {
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int ch = c0 + 16 * j + 4 * g;
-      f32x4 a, q;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        a[r] = s1[j][r];
-        q[r] = DG ? bn_rstd[ch + r] * (s2[j][r] - bn_mean[ch + r] * s1[j][r]) : s2[j][r];
-      }
-      *(f32x4*)(ps + (size_t)pb * N + ch) = a;
-      *(f32x4*)(pq + (size_t)pb * N + ch) = q;
-    }
-  }
-}
-
 // Forward with a loader wave: wave NW (the ninth) only moves 64-pixel x tiles into a ring of
 // 3 LDS buffers (global_load_lds, counted vmcnt), the 8 compute waves only read LDS and store.
 // A wave that waits on a load also waits for every store it issued before that load (one
 // in-order vmcnt counter), so when the compute waves fetched their own pixels each held at
 // most a tile of stores in flight: ~5 us per 32-pixel tile, 2.2 TB/s.  Here nothing behind
 // the stores waits on memory.  x rows in LDS: 16-B chunk c of row r at c ^ swz(r) (K = 64:
-// 128-B rows, swz = (r >> 1) & 7; K = 128: 256-B rows, swz = r & 15): the 16 rows a fragment
-// read touches land on distinct bank groups.
+// 128-B rows, swz = (r >> 1) & 7; K >= 128: swz = r & 15): the 16 rows a fragment read
+// touches land on distinct bank groups.
 typedef __attribute__((address_space(3))) void lds_void;
 constexpr int NBUF = 3;
 constexpr int OPITCH = NC * 2 + 16;  // output staging row (bytes): 16-B skew per pixel
 template <int K>
-constexpr int ftm() {  // pixels per tile: 64 (K = 64) / 32 (K = 128: LDS for 2 blocks per CU)
-  return K == 64 ? 64 : 32;
+constexpr int ftm() {  // forward pixels per tile: LDS for 2 blocks per CU (1 for K = 256)
+  return K == 128 ? 32 : 64;
+}
+template <int K>
+constexpr int fbpc() {  // forward blocks per CU: K = 256 needs 64 VGPRs of weights
+  return K == 256 ? 1 : 2;
 }
 
 template <int K>
@@ -201,7 +65,7 @@ __device__ __forceinline__ int xswz(int r) {
 }
 
 template <int K>
-__global__ __launch_bounds__(576, 5) void conv1x1_fwd_kernel(
+__global__ __launch_bounds__(576, fbpc<K>() == 2 ? 5 : 3) void conv1x1_fwd_kernel(
     int M, int N, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
     int ldw, unsigned short* __restrict__ y, float* __restrict__ ps, float* __restrict__ pq) {
   constexpr int FTM = ftm<K>(), KK = K / 32, MT = FTM / 16, CPR = K / 8;  // chunks per row
@@ -262,7 +126,7 @@ __global__ __launch_bounds__(576, 5) void conv1x1_fwd_kernel(
   for (int it = 0; it < nmy; ++it) {
     const char* xs = sm + (it % NBUF) * TB;
     const int p0 = (pb + it * PB) * FTM;
-#pragma unroll(K == 64 ? MT : 1)
+#pragma unroll K == 64 ? MT : 1
     for (int i = 0; i < MT; ++i) {
       bf16x8 xf[KK];
 #pragma unroll
@@ -329,9 +193,15 @@ __global__ __launch_bounds__(576, 5) void conv1x1_fwd_kernel(
 // every output written as 16-B chunks of whole 512-B row slices, and nothing that stores waits
 // on a load.  Thread t always owns channels 8 (t & 31) .. + 7 of the slice: its statistics
 // are summed over the block's pixels in registers and reduced across waves once at the end.
-constexpr int DTM = 16, DBUF = 4;
+constexpr int DTM = 16;
 constexpr int SPITCH = NC * 4 + 16;  // f32 staging row (bytes), 16-B skew per pixel
+template <int K, bool RES, bool BN>
+constexpr int dgrad_ring() {
+  constexpr int nqt = DTM * K * 2 / 1024 + ((RES ? 1 : 0) + (BN ? 2 : 0)) * (DTM * NC * 2 / 1024);
+  return 2 * nqt <= 63 ? 4 : 3;
+}
 
+// w here is the transposed weight copy wt [N][K] (transpose_bf16_kernel).
 template <int K, bool RES, bool BN>
 __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
     int M, int N, const unsigned short* __restrict__ dy, const unsigned short* __restrict__ w,
@@ -342,9 +212,11 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
   constexpr int KK = K / 32, CPR = K / 8;
   constexpr int DYB = DTM * K * 2, SB = DTM * NC * 2, NSIDE = (RES ? 1 : 0) + (BN ? 2 : 0);
   constexpr int STAGE = DYB + NSIDE * SB, NQD = DYB / 1024, NQS = SB / 1024;
-  constexpr int NQT = NQD + NSIDE * NQS;  // DMA instructions per tile (<= 28)
+  constexpr int NQT = NQD + NSIDE * NQS;  // DMA instructions per tile (<= 32)
+  // ring depth: vmcnt holds at most 63 in flight, so 2 younger tiles only while 2 NQT <= 63
+  constexpr int DB = dgrad_ring<K, RES, BN>(), D = DB - 1;
   extern __shared__ __attribute__((aligned(16))) char sm[];
-  char* stg = sm + DBUF * STAGE;
+  char* stg = sm + DB * STAGE;
   const int nbn = N / NC, PB = gridDim.x / nbn;
   const int b = blockIdx.x, i8 = b >> 3;
   const int cb = i8 % nbn, pb = (i8 / nbn) * 8 + (b & 7);
@@ -355,7 +227,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
   if (wave == NW) {
     auto issue = [&](int it) {
       const int tile = pb + it * PB;
-      char* d = sm + (it % DBUF) * STAGE;
+      char* d = sm + (it % DB) * STAGE;
 #pragma unroll
       for (int q = 0; q < NQD; ++q) {
         const int P = q * 64 + lane, r = P / CPR, c = (P % CPR) ^ xswz<K>(r);
@@ -376,20 +248,18 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
         }
       }
     };
-    for (int it = 0; it < 3 && it < nmy; ++it) issue(it);
-    if (nmy >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NQT) : "memory");
-    else if (nmy == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQT) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // wait until the oldest outstanding tile landed, `younger` newer tiles still in flight
+    auto wait_oldest = [&](int younger) {
+      if (D >= 3 && younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D >= 3 ? 2 * NQT : 0) : "memory");
+      else if (younger >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    for (int it = 0; it < D && it < nmy; ++it) issue(it);
+    wait_oldest(min(D, nmy) - 1);
     __syncthreads();
     for (int it = 0; it < nmy; ++it) {
-      if (it + 3 < nmy) {
-        issue(it + 3);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NQT) : "memory");  // tile it + 1 landed
-      } else if (it + 2 < nmy) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQT) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (it + D < nmy) issue(it + D);
+      wait_oldest(min(D, nmy - 1 - it) - 1);  // tile it + 1 landed
       __syncthreads();  // (the compute waves' staging barrier)
       __syncthreads();
     }
@@ -397,22 +267,19 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
     return;
   }
   const int c0 = wave * (NTW * 16);  // the wave's channels inside the slice
-  bf16x8 wf[NTW][KK];                // A operand: W^T[n][k] = w[k][n]
+  bf16x8 wf[NTW][KK];                // A operand: W^T[n][k], rows of the transposed copy wt
 #pragma unroll
   for (int j = 0; j < NTW; ++j)
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      const int n = cb * NC + c0 + 16 * j + cl, k = 32 * kk + 8 * g;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) wf[j][kk][u] = (short)w[(size_t)(k + u) * ldw + n];
-    }
+    for (int kk = 0; kk < KK; ++kk)
+      wf[j][kk] = *(const bf16x8*)(w + (size_t)(cb * NC + c0 + 16 * j + cl) * K + 32 * kk + 8 * g);
   float s1[8], s2[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) s1[u] = s2[u] = 0.f;
   const int ep = tid >> 5, ec = tid & 31;  // epilogue: pixel, 16-B chunk of the slice
   __syncthreads();  // tile 0 in LDS
   for (int it = 0; it < nmy; ++it) {
-    const char* buf = sm + (it % DBUF) * STAGE;
+    const char* buf = sm + (it % DB) * STAGE;
     const int p0 = (pb + it * PB) * DTM;
     bf16x8 xf[KK];
 #pragma unroll
@@ -489,108 +356,127 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
   }
 }
 
+// dst[c][r] = src[r][c] for a rows x cols bf16 block (ld_src >= cols): 32 x 32 tiles via LDS.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(int rows, int cols,
+                                                            const unsigned short* __restrict__ src,
+                                                            int ld_src, unsigned short* __restrict__ dst) {
+  __shared__ unsigned short t[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    t[i][tx] = r < rows && c < cols ? src[(size_t)r * ld_src + c] : 0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < cols && r < rows) dst[(size_t)c * rows + r] = t[tx][i];
+  }
+}
+
 }  // namespace pw
 
 bool conv1x1_applies(int M, int K, int N) {
-  const int nbn = N / pw::NC;  // column blocks: a power of two <= 8 (512 / nbn pixel blocks)
-  return (K == 64 || K == 128) && N % pw::NC == 0 && (nbn & (nbn - 1)) == 0 && nbn <= 8 &&
-         M % pw::TM == 0 && M > 0;
+  const int nbn = N / pw::NC;  // column blocks: a power of two <= 8 (the XCD pairing)
+  return (K == 64 || K == 128 || K == 256) && N % pw::NC == 0 && (nbn & (nbn - 1)) == 0 &&
+         nbn <= 8 && M % 64 == 0 && M > 0;
 }
 
-static bool conv1x1_loader() {  // DTFX_CONV1X1_LOADER=0: the kernels without the loader wave
-  static const bool on = [] {
-    const char* e = std::getenv("DTFX_CONV1X1_LOADER");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
+// Persistent blocks of a launch: 1 or 2 per CU (256 CUs), a multiple of 8 pixel blocks.
+static int conv1x1_blocks(int mode, int K) {
+  return mode == 2 || K == 256 ? 256 : 512;
 }
 
 // Partial statistics rows a launch of this mode writes ([rows][N] each of ps / pq).
 int conv1x1_rows(int mode, int M, int K, int N) {
-  (void)K;
-  const int nbn = N / pw::NC;
-  if (conv1x1_loader() && mode == 2 && M % pw::DTM == 0) return 256 / nbn;  // 1 block per CU
-  return 512 / nbn;
+  (void)M;
+  return conv1x1_blocks(mode, K) / (N / pw::NC);
+}
+
+template <int K>
+static void conv1x1_fwd_go(dim3 grid, int M, int N, const void* x, const void* w, int ldw, void* y,
+                           float* ps, float* pq, hipStream_t s) {
+  using namespace pw;
+  const size_t lds = (size_t)NBUF * ftm<K>() * K * 2 + (size_t)ftm<K>() * OPITCH;
+  static bool attr = false;
+  if (!attr) {
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_fwd_kernel<K>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(conv1x1_fwd_kernel<K>, grid, dim3(576), lds, s, M, N, (const unsigned short*)x,
+                     (const unsigned short*)w, ldw, (unsigned short*)y, ps, pq);
+}
+
+template <int K, bool RES, bool BN>
+static void conv1x1_dgrad_go(dim3 grid, int M, int N, const void* dy, const void* w, int ldw,
+                             void* dx, const void* res, const void* relu_y, const void* bn_x,
+                             const float* mean, const float* rstd, float* ps, float* pq,
+                             hipStream_t s) {
+  using namespace pw;
+  const size_t lds =
+      (size_t)dgrad_ring<K, RES, BN>() * (DTM * K * 2 + ((RES ? 1 : 0) + (BN ? 2 : 0)) * DTM * NC * 2) +
+      (size_t)DTM * SPITCH;
+  static bool attr = false;
+  if (!attr) {
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_dgrad_kernel<K, RES, BN>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv1x1_dgrad_kernel<K, RES, BN>), grid, dim3(576), lds, s, M, N,
+                     (const unsigned short*)dy, (const unsigned short*)w, ldw, (unsigned short*)dx,
+                     (const unsigned short*)res, (const unsigned short*)relu_y,
+                     (const unsigned short*)bn_x, mean, rstd, ps, pq);
+}
+
+template <int K>
+static void conv1x1_dgrad_pick(dim3 grid, int M, int N, const void* dy, const void* w, int ldw,
+                               void* dx, const void* res, const void* relu_y, const void* bn_x,
+                               const float* mean, const float* rstd, float* ps, float* pq,
+                               hipStream_t s) {
+  if (res && ps)
+    conv1x1_dgrad_go<K, true, true>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s);
+  else if (res)
+    conv1x1_dgrad_go<K, true, false>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s);
+  else if (ps)
+    conv1x1_dgrad_go<K, false, true>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s);
+  else
+    conv1x1_dgrad_go<K, false, false>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s);
 }
 
 // mode 1: forward (x [M][K], w [N][ldw]); mode 2: data gradient (x = dy [M][K], w [K][ldw],
-// optional residual, relu_y (mask), bn_x / mean / rstd (statistics)).  ps / pq (optional):
-// conv1x1_rows() partial rows of N floats each.
+// optional residual; with ps / pq the ReLU mask relu_y and the BN statistics of bn_x / mean /
+// rstd).  ps / pq (optional): conv1x1_rows() partial rows of N floats each.  wt (dgrad): an
+// N x K bf16 workspace for the transposed weights.
 void conv1x1_launch(int mode, int M, int K, int N, const void* x, const void* w, int ldw, void* y,
                     const void* res, const void* relu_y, const void* bn_x, const float* mean,
-                    const float* rstd, float* ps, float* pq, hipStream_t s) {
+                    const float* rstd, float* ps, float* pq, void* wt, hipStream_t s) {
   using namespace pw;
   if (!conv1x1_applies(M, K, N)) throw std::runtime_error("conv1x1: unsupported shape");
   if (ldw % 8 || (mode == 1 ? ldw < K : ldw < N) ||
-      (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) & 15) ||
-      (((uintptr_t)res | (uintptr_t)relu_y | (uintptr_t)bn_x) & 7))
-    throw std::runtime_error("conv1x1: ldw % 8, ldw >= reduction row, aligned tensors");
+      (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y | (uintptr_t)res | (uintptr_t)relu_y |
+        (uintptr_t)bn_x) & 15))
+    throw std::runtime_error("conv1x1: ldw % 8, ldw >= reduction row, 16-B aligned tensors");
   if ((ps != nullptr) != (pq != nullptr) ||
-      (mode == 2 && ps && (!bn_x || !mean || !rstd)))
-    throw std::runtime_error("conv1x1: statistics need ps, pq (and for dgrad bn_x, mean, rstd)");
-  const int nbn = N / NC;
-  // 2 blocks of 8 waves per CU; the pixel-block count a multiple of 8 (XCD pairing)
-  const int PB = 512 / nbn;
-  const dim3 grid(PB * nbn), blk(512);
-#define DTFX_PW_LAUNCH(KV, DGV)                                                                 \
-  hipLaunchKernelGGL((conv1x1_kernel<KV, DGV>), grid, blk, 0, s, M, N, (const unsigned short*)x, \
-                     (const unsigned short*)w, ldw, (unsigned short*)y,                           \
-                     (const unsigned short*)res, (const unsigned short*)relu_y,                   \
-                     (const unsigned short*)bn_x, mean, rstd, ps, pq)
-  const bool loader = conv1x1_loader();
-  if (mode == 2 && loader && M % DTM == 0) {
-    const bool res_ = res != nullptr, bn_ = ps != nullptr;
-    if (bn_ && !relu_y) throw std::runtime_error("conv1x1 dgrad: statistics need relu_y");
-    const size_t lds = (size_t)DBUF * (DTM * K * 2 + ((res_ ? 1 : 0) + (bn_ ? 2 : 0)) * DTM * NC * 2) +
-                       (size_t)DTM * SPITCH;
-    const dim3 g2(256 / nbn * nbn);
-#define DTFX_PW_DG(KV, RV, BV)                                                                  \
-  do {                                                                                          \
-    static bool attr_ = false;                                                                  \
-    if (!attr_) {                                                                               \
-      DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_dgrad_kernel<KV, RV, BV>,         \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); \
-      attr_ = true;                                                                             \
-    }                                                                                           \
-    hipLaunchKernelGGL((conv1x1_dgrad_kernel<KV, RV, BV>), g2, dim3(576), lds, s, M, N,         \
-                       (const unsigned short*)x, (const unsigned short*)w, ldw,                 \
-                       (unsigned short*)y, (const unsigned short*)res,                          \
-                       (const unsigned short*)relu_y, (const unsigned short*)bn_x, mean, rstd,  \
-                       ps, pq);                                                                 \
-  } while (0)
-    if (K == 64) {
-      if (res_ && bn_) DTFX_PW_DG(64, true, true);
-      else if (res_) DTFX_PW_DG(64, true, false);
-      else if (bn_) DTFX_PW_DG(64, false, true);
-      else DTFX_PW_DG(64, false, false);
-    } else {
-      if (res_ && bn_) DTFX_PW_DG(128, true, true);
-      else if (res_) DTFX_PW_DG(128, true, false);
-      else if (bn_) DTFX_PW_DG(128, false, true);
-      else DTFX_PW_DG(128, false, false);
-    }
-#undef DTFX_PW_DG
-  } else if (mode == 1 && loader && M % (K == 64 ? ftm<64>() : ftm<128>()) == 0) {
-    const int ft = K == 64 ? ftm<64>() : ftm<128>();
-    const size_t lds = (size_t)NBUF * ft * K * 2 + (size_t)ft * OPITCH;
-    if (K == 64)
-      hipLaunchKernelGGL(conv1x1_fwd_kernel<64>, grid, dim3(576), lds, s, M, N,
-                         (const unsigned short*)x, (const unsigned short*)w, ldw,
-                         (unsigned short*)y, ps, pq);
-    else
-      hipLaunchKernelGGL(conv1x1_fwd_kernel<128>, grid, dim3(576), lds, s, M, N,
-                         (const unsigned short*)x, (const unsigned short*)w, ldw,
-                         (unsigned short*)y, ps, pq);
-  } else if (mode == 1) {
-    if (K == 64) DTFX_PW_LAUNCH(64, false);
-    else DTFX_PW_LAUNCH(128, false);
+      (mode == 2 && ps && (!relu_y || !bn_x || !mean || !rstd)))
+    throw std::runtime_error("conv1x1: statistics need ps, pq (and for dgrad relu_y, bn_x, mean, rstd)");
+  if (mode == 2 && relu_y && !ps)
+    throw std::runtime_error("conv1x1: the ReLU mask comes with the BN statistics");
+  const dim3 grid(conv1x1_blocks(mode, K));
+  if (mode == 1) {
+    if (K == 64) conv1x1_fwd_go<64>(grid, M, N, x, w, ldw, y, ps, pq, s);
+    else if (K == 128) conv1x1_fwd_go<128>(grid, M, N, x, w, ldw, y, ps, pq, s);
+    else conv1x1_fwd_go<256>(grid, M, N, x, w, ldw, y, ps, pq, s);
   } else if (mode == 2) {
-    if (K == 64) DTFX_PW_LAUNCH(64, true);
-    else DTFX_PW_LAUNCH(128, true);
+    if (!wt || ((uintptr_t)wt & 15)) throw std::runtime_error("conv1x1 dgrad: 16-B aligned wt workspace");
+    hipLaunchKernelGGL(transpose_bf16_kernel, dim3(N / 32, K / 32), dim3(256), 0, s, K, N,
+                       (const unsigned short*)w, ldw, (unsigned short*)wt);
+    w = wt;
+    if (K == 64) conv1x1_dgrad_pick<64>(grid, M, N, x, w, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s);
+    else if (K == 128) conv1x1_dgrad_pick<128>(grid, M, N, x, w, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s);
+    else conv1x1_dgrad_pick<256>(grid, M, N, x, w, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s);
   } else {
     throw std::runtime_error("conv1x1: mode 1 (forward) or 2 (dgrad)");
   }
-#undef DTFX_PW_LAUNCH
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

@@ -20,7 +20,7 @@ from ._ext import hip, ptr, stream_handle
 
 # split-K partials through a workspace + reduce pass (DTFX_SPLITK_WS=0: f32 atomics into the output)
 _SPLITK_WS = os.environ.get("DTFX_SPLITK_WS", "1") != "0"
-# 1x1 / stride-1 convolutions with 64 / 128 reduction channels on the streaming kernel
+# 1x1 / stride-1 convolutions with 64 / 128 / 256 reduction channels on the streaming kernels
 # (csrc/kernels/conv1x1.hip); DTFX_CONV1X1=0: the implicit-GEMM path (A/B runs)
 _CONV1X1 = os.environ.get("DTFX_CONV1X1", "1") != "0"
 
@@ -108,7 +108,7 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
             part = torch.empty(2, hip().conv1x1_rows(1, M, C, Cout), Cout, device=x.device)
             ps, pq = part[0], part[1]
         hip().conv1x1(1, M, C, Cout, ptr(x), ptr(w), w.stride(0), ptr(y), 0, 0, 0, 0, 0, ptr(ps),
-                      ptr(pq), stream_handle())
+                      ptr(pq), 0, stream_handle())
         if colsum is not None:
             hip().colpart_reduce(ps.shape[0], Cout, ptr(ps), ptr(pq), ptr(colsum), ptr(colsq),
                                  stream_handle())
@@ -185,16 +185,18 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
         # conv1's data gradient in layer1 / layer2 (64 / 128 -> 256 / 512 channels): the
         # streaming 1x1 kernel, shortcut gradient, ReLU mask and BN reductions fused
         M = N * H * W
+        wt = torch.empty(C, Cout, device=dy.device, dtype=BF16)  # transposed weights
         if bn is None:
             hip().conv1x1(2, M, Cout, C, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(residual), 0,
-                          0, 0, 0, 0, 0, stream_handle())
+                          0, 0, 0, 0, 0, ptr(wt), stream_handle())
             return dx
         y, x, mean, rstd, sdy, sdx = bn
         if y.shape != dx.shape or x.shape != dx.shape:
             raise ValueError("fused BN backward: y and x must have the dgrad output's shape")
         part = torch.empty(2, hip().conv1x1_rows(2, M, Cout, C), C, device=dy.device)
         hip().conv1x1(2, M, Cout, C, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(residual), ptr(y),
-                      ptr(x), ptr(mean), ptr(rstd), ptr(part[0]), ptr(part[1]), stream_handle())
+                      ptr(x), ptr(mean), ptr(rstd), ptr(part[0]), ptr(part[1]), ptr(wt),
+                      stream_handle())
         hip().colpart_reduce(part.shape[1], C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
                              stream_handle())
         return dx

@@ -25,13 +25,15 @@ CONVS = [  # N, H, W, C, Cout, k, stride, pad
     (2, 15, 13, 64, 128, 3, 2, 1),   # stride-2 dgrad: phase classes of unequal size
     (2, 14, 14, 64, 64, 3, 2, 1),    # stride-2 dgrad on the 256x64 tile
     (2, 13, 15, 128, 64, 1, 2, 0),   # 1x1 stride 2: three of four classes have no taps
-    (4, 64, 64, 256, 1024, 1, 1, 0),  # 1x1 stride 1 on the 8-phase plain GEMM
+    (4, 64, 64, 256, 1024, 1, 1, 0),  # 1x1 stride 1, K = 256: the streaming kernel
     (3, 60, 60, 256, 1024, 1, 1, 0),  # same, M = 10800: ragged 256-row block and 64-row slab
     (3, 60, 60, 64, 1024, 3, 1, 1),  # 3x3 forward on the 8-phase gather (ragged M)
     (4, 64, 64, 1024, 256, 3, 2, 1),  # stride-2 dgrad classes on the 8-phase gather
     (2, 16, 16, 64, 256, 1, 1, 0),   # streaming 1x1 kernel (conv1x1.hip): forward K = 64
     (2, 8, 8, 128, 512, 1, 1, 0),    # forward K = 128, two column blocks
-    (1, 8, 4, 64, 2048, 1, 1, 0),    # one 32-pixel tile, 8 column blocks, idle pixel blocks
+    (1, 8, 8, 64, 2048, 1, 1, 0),    # one 64-pixel tile, 8 column blocks, idle pixel blocks
+    (2, 8, 8, 256, 1024, 1, 1, 0),   # forward K = 256 (one block per CU)
+    (2, 8, 8, 1024, 256, 1, 1, 0),   # dgrad K = 256 -> 1024 channels
     (2, 16, 16, 256, 64, 1, 1, 0),   # dgrad K = 64 -> 256 channels
     (2, 8, 8, 512, 128, 1, 1, 0),    # dgrad K = 128 -> 512 channels (16-pixel tiles)
 ]
@@ -76,7 +78,8 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, W, C, Co, k, s, p):
     (2, 8, 56, 64, 64, 3, 1, 1, False),    # 64-channel 3x3 kernel with the fused BN backward
     (2, 28, 28, 128, 128, 3, 1, 1, False),  # 128-channel 3x3 kernel with the fused BN backward
     (4, 64, 64, 1024, 256, 3, 2, 1, True),  # 8-phase dgrad: per-slab BN columns, class rows
-    (4, 64, 64, 1024, 256, 1, 1, 0, True),  # 8-phase 1x1 dgrad
+    (3, 60, 60, 1024, 256, 1, 1, 0, True),  # 8-phase 1x1 dgrad (M % 64 != 0: not streamed)
+    (4, 64, 64, 1024, 256, 1, 1, 0, True),  # streaming 1x1 dgrad, K = 256, 4 column blocks
     (2, 16, 16, 256, 64, 1, 1, 0, True),   # streaming 1x1 dgrad (conv1x1.hip), K = 64
     (2, 8, 8, 512, 128, 1, 1, 0, True),    # K = 128, two column blocks
     (2, 16, 16, 256, 128, 1, 1, 0, False),  # K = 128 -> 256, no shortcut gradient
@@ -167,7 +170,8 @@ def test_sgd_momentum_mixed(gpu):
     assert torch.equal(pb.cpu(), P.cpu().to(BF))
 
 
-@pytest.mark.parametrize("N,H,W,C,Co", [(2, 16, 16, 256, 64), (2, 8, 8, 512, 128)])
+@pytest.mark.parametrize("N,H,W,C,Co", [(2, 16, 16, 256, 64), (2, 8, 8, 512, 128),
+                                         (2, 8, 8, 1024, 256)])
 def test_conv1x1_dgrad_residual_only(gpu, N, H, W, C, Co):
     """The first bottleneck's conv1 dgrad: the shortcut gradient added, no BN fused."""
     w = _r(Co, C, seed=21, scale=C ** -0.5).to(BF)
