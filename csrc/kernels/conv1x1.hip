@@ -356,6 +356,169 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
   }
 }
 
+// Narrow products: 64 or 128 output channels from 256 or 512 reduction channels (ResNet-50's
+// reductions: conv1 forward 256 -> 64 / 128 and 512 -> 128, conv3's data gradient into conv2's
+// 64 / 128 channels with conv2's BatchNorm backward fused).  Same loader-wave / LDS-ring scheme
+// with one block per CU owning ALL N channels: compute wave w takes MFMA row tile w % NT and
+// K part w / NT (KS = 8 / NT parts, the parts' f32 products summed in the staged epilogue), so
+// the N x K weights (32-128 KB) sit in the 8 waves' registers.
+template <int K, int N_, bool DG>
+constexpr int ntm() {  // pixels per tile (LDS: 3-4 ring stages + the f32 staging)
+  return DG ? (N_ == 64 ? 32 : 16) : (N_ == 64 ? 64 : 32);
+}
+template <int K, int N_, bool DG>
+constexpr int nqt_narrow() {  // DMA instructions per tile
+  return ntm<K, N_, DG>() * K * 2 / 1024 + (DG ? 2 * ntm<K, N_, DG>() * N_ * 2 / 1024 : 0);
+}
+
+template <int K, int N_, bool DG>
+__global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
+    int M, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
+    unsigned short* __restrict__ y, const unsigned short* __restrict__ relu_y,
+    const unsigned short* __restrict__ bn_x, const float* __restrict__ bn_mean,
+    const float* __restrict__ bn_rstd, float* __restrict__ ps, float* __restrict__ pq) {
+  constexpr int NT = N_ / 16, KS = 8 / NT, KKW = K / 32 / KS, CPR = K / 8, NCH = N_ / 8;
+  constexpr int TM = ntm<K, N_, DG>(), MT = TM / 16;
+  constexpr int XB = TM * K * 2, SB = TM * N_ * 2, STAGE = XB + (DG ? 2 * SB : 0);
+  constexpr int NQX = XB / 1024, NQS = SB / 1024, NQT = nqt_narrow<K, N_, DG>();
+  constexpr int DB = 2 * NQT <= 63 ? 4 : 3, D = DB - 1;
+  constexpr int PITCH = N_ * 4 + 16;           // f32 staging row (bytes)
+  constexpr int NE = TM * NCH;                 // epilogue chunks per tile
+  constexpr int EP = (NE + 511) / 512;         // epilogue passes
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* stg = sm + DB * STAGE;                 // [KS][TM][PITCH]
+  const int PB = gridDim.x, pb = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, cl = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T = M / TM;
+  const int nmy = pb < T ? (T - pb + PB - 1) / PB : 0;
+  if (wave == NW) {
+    auto issue = [&](int it) {
+      const int tile = pb + it * PB;
+      char* d = sm + (it % DB) * STAGE;
+#pragma unroll
+      for (int q = 0; q < NQX; ++q) {
+        const int P = q * 64 + lane, r = P / CPR, c = (P % CPR) ^ xswz<K>(r);
+        const unsigned short* src = x + ((size_t)tile * TM + r) * K + c * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(d + q * 1024), 16, 0, 0);
+      }
+      if constexpr (DG) {
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+          const unsigned short* side = si == 0 ? relu_y : bn_x;
+#pragma unroll
+          for (int q = 0; q < NQS; ++q) {
+            const int P = q * 64 + lane;  // row-major [TM][N_] in 16-B chunks
+            const unsigned short* src = side + (size_t)tile * TM * N_ + P * 8;
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (lds_void*)(d + XB + si * SB + q * 1024), 16, 0, 0);
+          }
+        }
+      }
+    };
+    auto wait_oldest = [&](int younger) {
+      if (D >= 3 && younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D >= 3 ? 2 * NQT : 0) : "memory");
+      else if (younger >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    for (int it = 0; it < D && it < nmy; ++it) issue(it);
+    wait_oldest(min(D, nmy) - 1);
+    __syncthreads();
+    for (int it = 0; it < nmy; ++it) {
+      if (it + D < nmy) issue(it + D);
+      wait_oldest(min(D, nmy - 1 - it) - 1);  // tile it + 1 landed
+      __syncthreads();
+      __syncthreads();
+    }
+    __syncthreads();  // (the statistics reduction)
+    return;
+  }
+  const int nt = wave % NT, part = wave / NT, kk0 = part * KKW;
+  bf16x8 wf[KKW];  // A operand rows: channel 16 nt + cl (forward: w [N][ldw]; dgrad: wt [N][K])
+#pragma unroll
+  for (int kk = 0; kk < KKW; ++kk)
+    wf[kk] = *(const bf16x8*)(w + (size_t)(16 * nt + cl) * K + 32 * (kk0 + kk) + 8 * g);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s1[u] = s2[u] = 0.f;
+  __syncthreads();  // tile 0 in LDS
+  for (int it = 0; it < nmy; ++it) {
+    const char* buf = sm + (it % DB) * STAGE;
+    const int p0 = (pb + it * PB) * TM;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int r = 16 * i + cl;
+#pragma unroll
+      for (int kk = 0; kk < KKW; ++kk) {
+        const bf16x8 xf = *(const bf16x8*)(buf + r * (K * 2) + (((4 * (kk0 + kk) + g) ^ xswz<K>(r)) << 4));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kk], xf, acc, 0, 0, 0);
+      }
+      *(f32x4*)(stg + (part * TM + r) * PITCH + (16 * nt + 4 * g) * 4) = acc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < EP; ++q) {
+      const int e = q * 512 + tid;
+      if (NE % 512 == 0 || e < NE) {
+        const int p = e / NCH, c = e % NCH;
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const f32x4 a0 = *(const f32x4*)(stg + (ks * TM + p) * PITCH + c * 32);
+          const f32x4 a1 = *(const f32x4*)(stg + (ks * TM + p) * PITCH + c * 32 + 16);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            v[u] += a0[u];
+            v[4 + u] += a1[u];
+          }
+        }
+        bf16x8 o;
+        if constexpr (DG) {
+          const bf16x8 y8 = *(const bf16x8*)(buf + XB + p * (N_ * 2) + c * 16);
+          const bf16x8 x8 = *(const bf16x8*)(buf + XB + SB + p * (N_ * 2) + c * 16);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            o[u] = (short)tobf(bf(y8[u]) > 0.f ? v[u] : 0.f);
+            const float d = bf(o[u]);
+            s1[u] += d;
+            s2[u] += d * bf(x8[u]);
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            o[u] = (short)tobf(v[u]);
+            s1[u] += v[u];
+            s2[u] += v[u] * v[u];
+          }
+        }
+        *(bf16x8*)(y + (size_t)(p0 + p) * N_ + c * 8) = o;
+      }
+    }
+    __syncthreads();
+  }
+  // statistics: thread tid owns channels 8 (tid % NCH) .. + 7; sum the 512 / NCH owners
+  float* red = (float*)sm;  // the ring is idle now: [512][16]
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    red[tid * 16 + u] = s1[u];
+    red[tid * 16 + 8 + u] = s2[u];
+  }
+  __syncthreads();
+  if (tid < N_) {
+    const int c = tid >> 3, u = tid & 7;
+    float a = 0.f, q = 0.f;
+    for (int r = c; r < 512; r += NCH) {
+      a += red[r * 16 + u];
+      q += red[r * 16 + 8 + u];
+    }
+    ps[(size_t)pb * N_ + tid] = a;
+    pq[(size_t)pb * N_ + tid] = DG ? bn_rstd[tid] * (q - bn_mean[tid] * a) : q;
+  }
+}
+
 // dst[c][r] = src[r][c] for a rows x cols bf16 block (ld_src >= cols): 32 x 32 tiles via LDS.
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(int rows, int cols,
                                                             const unsigned short* __restrict__ src,
@@ -375,10 +538,20 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(int rows, int cols,
 
 }  // namespace pw
 
+static bool conv1x1_narrow(int K, int N) {
+  static const bool on = [] {  // DTFX_CONV1X1_NARROW=0: reductions stay on the implicit GEMM
+    const char* e = std::getenv("DTFX_CONV1X1_NARROW");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on && ((K == 256 && (N == 64 || N == 128)) || (K == 512 && N == 128));
+}
+
 bool conv1x1_applies(int M, int K, int N) {
+  if (M <= 0 || M % 64) return false;
+  if (conv1x1_narrow(K, N)) return true;
   const int nbn = N / pw::NC;  // column blocks: a power of two <= 8 (the XCD pairing)
   return (K == 64 || K == 128 || K == 256) && N % pw::NC == 0 && (nbn & (nbn - 1)) == 0 &&
-         nbn <= 8 && M % 64 == 0 && M > 0;
+         nbn <= 8;
 }
 
 // Persistent blocks of a launch: 1 or 2 per CU (256 CUs), a multiple of 8 pixel blocks.
@@ -389,7 +562,30 @@ static int conv1x1_blocks(int mode, int K) {
 // Partial statistics rows a launch of this mode writes ([rows][N] each of ps / pq).
 int conv1x1_rows(int mode, int M, int K, int N) {
   (void)M;
+  if (conv1x1_narrow(K, N)) return 256;
   return conv1x1_blocks(mode, K) / (N / pw::NC);
+}
+
+template <int K, int N_, bool DG>
+static void conv1x1_narrow_go(int M, const void* x, const void* w, void* y, const void* relu_y,
+                              const void* bn_x, const float* mean, const float* rstd, float* ps,
+                              float* pq, hipStream_t s) {
+  using namespace pw;
+  constexpr int TM = ntm<K, N_, DG>(), NQT = nqt_narrow<K, N_, DG>();
+  constexpr int DB = 2 * NQT <= 63 ? 4 : 3;
+  const size_t lds = (size_t)DB * (TM * K * 2 + (DG ? 2 * TM * N_ * 2 : 0)) +
+                     (size_t)(8 / (N_ / 16)) * TM * (N_ * 4 + 16);
+  static_assert((size_t)DB * (TM * K * 2 + (DG ? 2 * TM * N_ * 2 : 0)) >= 512 * 16 * 4,
+                "the statistics reduction reuses the ring");
+  static bool attr = false;
+  if (!attr) {
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_narrow_kernel<K, N_, DG>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv1x1_narrow_kernel<K, N_, DG>), dim3(256), dim3(576), lds, s, M,
+                     (const unsigned short*)x, (const unsigned short*)w, (unsigned short*)y,
+                     (const unsigned short*)relu_y, (const unsigned short*)bn_x, mean, rstd, ps, pq);
 }
 
 template <int K>
@@ -461,6 +657,31 @@ void conv1x1_launch(int mode, int M, int K, int N, const void* x, const void* w,
     throw std::runtime_error("conv1x1: statistics need ps, pq (and for dgrad relu_y, bn_x, mean, rstd)");
   if (mode == 2 && relu_y && !ps)
     throw std::runtime_error("conv1x1: the ReLU mask comes with the BN statistics");
+  if (conv1x1_narrow(K, N)) {
+    // one partial statistics row per block, always written (the model's reductions all feed
+    // a BatchNorm); dgrad: the mask / statistics are required, no shortcut gradient
+    if (!ps || (mode == 1 && ldw != K) || (mode == 2 && (res || !relu_y)) || (mode != 1 && mode != 2))
+      throw std::runtime_error("conv1x1 narrow: statistics required, ldw == K (forward), "
+                               "no residual and relu_y given (dgrad)");
+    const void* wv = w;
+    if (mode == 2) {
+      if (!wt || ((uintptr_t)wt & 15)) throw std::runtime_error("conv1x1 dgrad: 16-B aligned wt workspace");
+      hipLaunchKernelGGL(transpose_bf16_kernel, dim3((N + 31) / 32, K / 32), dim3(256), 0, s, K, N,
+                         (const unsigned short*)w, ldw, (unsigned short*)wt);
+      wv = wt;
+    }
+#define DTFX_PW_NARROW(KV, NV)                                                                  \
+  do {                                                                                          \
+    if (mode == 1) conv1x1_narrow_go<KV, NV, false>(M, x, wv, y, relu_y, bn_x, mean, rstd, ps, pq, s); \
+    else conv1x1_narrow_go<KV, NV, true>(M, x, wv, y, relu_y, bn_x, mean, rstd, ps, pq, s);     \
+  } while (0)
+    if (K == 256 && N == 64) DTFX_PW_NARROW(256, 64);
+    else if (K == 256) DTFX_PW_NARROW(256, 128);
+    else DTFX_PW_NARROW(512, 128);
+#undef DTFX_PW_NARROW
+    DTFX_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const dim3 grid(conv1x1_blocks(mode, K));
   if (mode == 1) {
     if (K == 64) conv1x1_fwd_go<64>(grid, M, N, x, w, ldw, y, ps, pq, s);

@@ -25,9 +25,14 @@ _SPLITK_WS = os.environ.get("DTFX_SPLITK_WS", "1") != "0"
 _CONV1X1 = os.environ.get("DTFX_CONV1X1", "1") != "0"
 
 
-def _pointwise(KH, KW, stride, pad, M, K, N, w):
-    return (_CONV1X1 and KH == 1 and KW == 1 and stride == 1 and pad == 0 and w.stride(0) % 8 == 0
-            and hip().conv1x1_applies(M, K, N))
+def _pointwise(KH, KW, stride, pad, M, K, N, w, stats, residual=None):
+    """The streaming 1x1 kernels take this product: wide outputs (N >= 256, any epilogue) or
+    the narrow reductions (N = 64 / 128: BN statistics required, no shortcut gradient)."""
+    if not (_CONV1X1 and KH == 1 and KW == 1 and stride == 1 and pad == 0 and w.stride(0) % 8 == 0):
+        return False
+    if N < 256 and (not stats or residual is not None):
+        return False
+    return hip().conv1x1_applies(M, K, N)
 
 BF16 = torch.bfloat16
 
@@ -99,9 +104,10 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
         hip().colpart_reduce(part.shape[1], Cout, ptr(part[0]), ptr(part[1]), ptr(colsum),
                              ptr(colsq), stream_handle())
         return y
-    if residual is None and _pointwise(KH, KW, stride, pad, N * H * W, C, Cout, w):
-        # layer1 / layer2 expansions (64 -> 256, 128 -> 512): weights in registers, pixels
-        # streamed; one partial statistics row per persistent pixel block
+    if residual is None and _pointwise(KH, KW, stride, pad, N * H * W, C, Cout, w, colsum is not None):
+        # the 1x1 expansions (64 -> 256 ... 256 -> 1024) and reductions (256 -> 64 / 128,
+        # 512 -> 128): weights in registers, pixels streamed; one partial statistics row per
+        # persistent pixel block
         M = N * H * W
         ps = pq = None
         if colsum is not None:
@@ -181,9 +187,10 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
         hip().colpart_reduce(part.shape[1], C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
                              stream_handle())
         return dx
-    if _pointwise(KH, KW, stride, pad, N * H * W, Cout, C, w):
-        # conv1's data gradient in layer1 / layer2 (64 / 128 -> 256 / 512 channels): the
-        # streaming 1x1 kernel, shortcut gradient, ReLU mask and BN reductions fused
+    if _pointwise(KH, KW, stride, pad, N * H * W, Cout, C, w, bn is not None, residual):
+        # conv1's data gradient (64 / 128 / 256 -> 256 ... 1024 channels, + shortcut gradient)
+        # and conv3's (256 / 512 -> 64 / 128): the streaming 1x1 kernels, ReLU mask and BN
+        # reductions fused
         M = N * H * W
         wt = torch.empty(C, Cout, device=dy.device, dtype=BF16)  # transposed weights
         if bn is None:

@@ -36,6 +36,7 @@ CONVS = [  # N, H, W, C, Cout, k, stride, pad
     (2, 8, 8, 1024, 256, 1, 1, 0),   # dgrad K = 256 -> 1024 channels
     (2, 16, 16, 256, 64, 1, 1, 0),   # dgrad K = 64 -> 256 channels
     (2, 8, 8, 512, 128, 1, 1, 0),    # dgrad K = 128 -> 512 channels (16-pixel tiles)
+    (2, 8, 8, 256, 128, 1, 1, 0),    # narrow forward 256 -> 128 (the two above: 256 -> 64, 512 -> 128)
 ]
 
 
@@ -83,6 +84,10 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, W, C, Co, k, s, p):
     (2, 16, 16, 256, 64, 1, 1, 0, True),   # streaming 1x1 dgrad (conv1x1.hip), K = 64
     (2, 8, 8, 512, 128, 1, 1, 0, True),    # K = 128, two column blocks
     (2, 16, 16, 256, 128, 1, 1, 0, False),  # K = 128 -> 256, no shortcut gradient
+    (2, 16, 16, 64, 256, 1, 1, 0, False),  # narrow dgrad 256 -> 64 with the BN backward
+    (2, 8, 8, 128, 512, 1, 1, 0, False),   # narrow dgrad 512 -> 128
+    (2, 8, 8, 128, 256, 1, 1, 0, False),   # narrow dgrad 256 -> 128
+    (2, 8, 8, 128, 512, 1, 1, 0, True),    # narrow shape + shortcut gradient: implicit GEMM
 ])
 def test_conv_dgrad_fused_batchnorm_backward(gpu, N, H, W, C, Co, k, s, p, with_res):
     """dgrad with BatchNorm backward's reductions in its epilogue (+ shortcut gradient, ReLU

@@ -2,7 +2,7 @@
 
     python tools/probes/conv_one.py PASS N H W C Cout k stride pad [reps]
 PASS: fwd (with the fused BN statistics) | dgrad (fused BN backward + shortcut gradient when
-the geometry keeps the shape) | wgrad.  Prints the per-call device time."""
+the geometry keeps the shape) | dgradbn (fused BN backward only) | wgrad.  Prints the per-call device time."""
 import json
 import os
 import sys
@@ -32,8 +32,9 @@ def main():
     dw = torch.zeros(Co, ld, device=dev)
     if ps == "fwd":
         fn = lambda: CN.conv_fwd(x, w, k, k, s, p, colsum=cs, colsq=cq)  # noqa: E731
-    elif ps == "dgrad":
-        fn = lambda: CN.conv_dgrad(dy, w, x.shape, k, k, s, p, residual=x,  # noqa: E731
+    elif ps in ("dgrad", "dgradbn"):
+        res = x if ps == "dgrad" else None
+        fn = lambda: CN.conv_dgrad(dy, w, x.shape, k, k, s, p, residual=res,  # noqa: E731
                                    bn=(x, x, mean, rstd, sdy, sdx))
     else:
         fn = lambda: CN.conv_wgrad(dy, x, dw, k, k, s, p)  # noqa: E731
