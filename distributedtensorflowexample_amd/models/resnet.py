@@ -137,6 +137,12 @@ class ResNet50:
             self._stats[name] = (self._stats_flat[off:off + cout],
                                  self._stats_flat[off + cout:off + 2 * cout])
             off += 2 * cout
+        # weight gradients on a second HIP stream (set by the trainer): each only needs its
+        # conv's output gradient and saved input, so it overlaps the data-gradient / BatchNorm
+        # chain.  ``wgrad_sync_buckets``: join before every gradient-bucket hook (sync DP).
+        self.wgrad_stream = None
+        self.wgrad_sync_buckets = True
+        self._keep = []  # operands the side stream still reads
 
     # conv + fused BN statistics + finalize
     def _conv_bn(self, name, x):
@@ -198,6 +204,7 @@ class ResNet50:
             on_bucket_ready(len(P.buckets) - 1)
         dx = CN.avgpool_bwd(dpool, x.shape)
         bucket = len(P.buckets) - 2
+        ws = self.wgrad_stream
         dx_is_de = False  # dx already dL/d(BN output) of the block's conv3 (fused reductions)
         for i in range(len(blocks) - 1, -1, -1):
             pre, x_in, (c1, m1, r1, a1), (c2, m2, r2, a2), (c3, m3, r3), ds, out = blocks[i]
@@ -209,6 +216,8 @@ class ResNet50:
                                  out, dout_is_de=dx_is_de, fuse_prev=fuse)
             dx_is_de = fuse is not None
             if on_bucket_ready is not None:
+                if ws is not None and self.wgrad_sync_buckets:
+                    torch.cuda.current_stream(dx.device).wait_stream(ws)
                 on_bucket_ready(bucket)
             bucket -= 1
         da = CN.maxpool_bwd(dx, idx, saved["conv1"][4].shape)
@@ -217,6 +226,9 @@ class ResNet50:
                           P.G("conv1.bn.beta"), relu=True, grads_zeroed=True)
         _, cin, cout, k, s, p = self.specs["conv1"]
         CN.conv_wgrad(dc, img, P.G("conv1.weight"), k, k, s, p, beta=1.0)
+        if ws is not None:  # join: every gradient final on the main stream
+            torch.cuda.current_stream(dc.device).wait_stream(ws)
+            self._keep.clear()
         if on_bucket_ready is not None:
             on_bucket_ready(0)
         return loss, acc
@@ -241,7 +253,14 @@ class ResNet50:
     def _wgrad_dgrad(self, name, dc, x_in, residual=None, need_dx=True, bn=None):
         P = self.params
         _, cin, cout, k, s, p = self.specs[name]
-        CN.conv_wgrad(dc, x_in, P.G(name + ".weight"), k, k, s, p, beta=1.0)
+        ws = self.wgrad_stream
+        if ws is None:
+            CN.conv_wgrad(dc, x_in, P.G(name + ".weight"), k, k, s, p, beta=1.0)
+        else:  # weight gradient beside the data gradient (operands kept alive until the join)
+            ws.wait_stream(torch.cuda.current_stream(dc.device))
+            with torch.cuda.stream(ws):
+                CN.conv_wgrad(dc, x_in, P.G(name + ".weight"), k, k, s, p, beta=1.0)
+            self._keep.append((dc, x_in))
         if not need_dx:
             return None
         return CN.conv_dgrad(dc, P.W(name + ".weight"), x_in.shape, k, k, s, p, residual=residual,

@@ -8,6 +8,8 @@ has no counterpart (it trains an MLP with async PS, worker.py:71-79).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..models.resnet import STAGES, ResNet50, synthetic_imagenet
@@ -30,6 +32,13 @@ class ResNetTrainer:
             TR.cast_bf16(p.master, p.bf)
         self.comm_stream = (torch.cuda.Stream(self.device)
                             if (self.device.type == "cuda" and overlap and self.world > 1) else None)
+        # DTFX_RESNET_WSTREAM=1: weight gradients on a second stream (models/resnet.py).  Off:
+        # the persistent convolution kernels size their grids for the whole chip, and blocks
+        # queued behind a side-stream kernel stretch their tail (10264 vs 10524 img/s, two
+        # interleaved rounds, batch 256)
+        if self.device.type == "cuda" and os.environ.get("DTFX_RESNET_WSTREAM", "0") == "1":
+            self.model.wgrad_stream = torch.cuda.Stream(self.device)
+            self.model.wgrad_sync_buckets = self.world > 1
         self.data = synthetic_imagenet(batch, device, image_size, seed=data_seed,
                                        num_classes=num_classes)
         self.graph = None
