@@ -114,11 +114,13 @@ def main():
     ap.add_argument("--max_graph_steps", type=int, default=1024,
                     help="max steps per hipGraph (graphs are epoch-aligned)")
     ap.add_argument("--no_graph", action="store_true")
-    ap.add_argument("--launch", choices=["auto", "graph", "host"], default="auto",
+    ap.add_argument("--launch", choices=["auto", "graph", "host", "persistent"], default="auto",
                     help="MLP, 1 GPU: how the timed steps are issued -- graph = hipGraph "
                          "replays, host = the C++ host loop launching both kernels of every "
-                         "step (no graph-submission latency), auto = time both on K steps "
-                         "before the timed region and use the faster")
+                         "step (no graph-submission latency), persistent = ALL K steps in one "
+                         "launch of the persistent kernel (workgroups hand data to each other "
+                         "as epoch-tagged granules), auto = time the candidates on min(K, 2000) "
+                         "steps before the timed region and use the fastest")
     ap.add_argument("--comm", choices=["auto", "native", "xgmi", "torch"], default="auto",
                     help="native: the framework's C++ RCCL communicator (gloo control plane); "
                          "xgmi: one-shot peer-memory all-reduce over xGMI (small buckets); "
@@ -256,20 +258,36 @@ def main():
     # though both timed 8.3-8.4 on a 200-step probe).
     launch = "graph" if use_graph else "eager"
     a.launch_probe = None
-    if use_graph and tr.host_loop_ok and (a.launch == "host" or
-                                          (a.launch == "auto" and a.steps <= 200)):
-        kp = a.steps
+    if a.launch == "persistent" and not tr.persistent_ok:
+        sys.exit("--launch persistent: single GPU, batch <= 128 only")
+    cands = []
+    if use_graph and tr.host_loop_ok and a.launch == "auto":
+        cands = ["graph"] + (["host"] if a.steps <= 200 else []) + (
+            ["persistent"] if tr.persistent_ok else [])
+    if a.launch == "host" and tr.host_loop_ok:
+        launch = "host"
+    if a.launch == "persistent":
+        launch = "persistent"
+    if launch in ("host", "persistent") or len(cands) > 1:
+        kp = min(a.steps, 2000)
 
         def run_k(mode):
             if mode == "host":
                 tr.run_launched(kp)
+            elif mode == "persistent":
+                tr.run_persistent(kp)
             else:
                 tr.run(kp)
             tr.flush()
 
-        probe = {"graph": [], "host": []}
-        tr.run_launched(max(a.warmup, 8))  # warm the direct-launch path
-        for _ in range(3 if a.launch == "auto" else 0):
+        probe = {m: [] for m in cands}
+        if tr.host_loop_ok:
+            tr.run_launched(max(a.warmup, 8))  # warm the direct-launch path
+        if tr.persistent_ok and (launch == "persistent" or "persistent" in cands):
+            tr.run_persistent(max(a.warmup, 8))  # first launch: granule buffer + code object
+            tr.check()
+            tr.run(1, use_graph=False)
+        for _ in range(3 if cands else 0):
             for mode in probe:
                 if mode == "graph":
                     tr.prepare(kp)
@@ -279,14 +297,15 @@ def main():
                 torch.cuda.synchronize()
                 probe[mode].append((time.perf_counter() - t_0) * 1e6 / kp)
                 tr.run(1, use_graph=False)  # pending update again, as after the warmup
-        if a.launch == "host":
-            launch = "host"
-        else:
+        if cands:
+            tr.check()
             med = {m: sorted(v)[len(v) // 2] for m, v in probe.items()}
             launch = min(med, key=med.get)
             a.launch_probe = {m: round(v, 3) for m, v in med.items()}
     if launch == "graph":
         tr.prepare(a.steps)
+    if launch == "persistent":
+        tr.flush()  # the warmup's pending update lands before the clock (it is not a timed step)
     pre_steps = tr.global_step()
     if barrier:
         barrier()
@@ -294,6 +313,8 @@ def main():
     t0 = time.perf_counter()
     if launch == "host":
         tr.run_launched(a.steps)
+    elif launch == "persistent":
+        tr.run_persistent(a.steps)  # every update applied inside the launch
     else:
         tr.run(a.steps, use_graph)
     tr.flush()  # the last step's deferred update is part of the timed work
@@ -301,6 +322,7 @@ def main():
     if barrier:
         barrier()
     elapsed = time.perf_counter() - t0
+    tr.check()  # raises if a persistent-engine hand-off ever timed out
     for c in ((comm, fused_comm, factor_comm) if world > 1 else ()):
         if hasattr(c, "check"):
             c.check()  # raises if an xGMI exchange ever timed out
@@ -347,7 +369,8 @@ def main():
                 "hipgraph": launch == "graph",
                 "launch": launch,
                 "engine": getattr(a, "engine_kind", "allreduce" if allreduce else "single"),
-                "launches_per_step": 2 if tr.pipelined else 3,
+                "launches_per_step": (round(1.0 / a.steps, 6) if launch == "persistent"
+                                      else 2 if tr.pipelined else 3),
             },
             "comm_probe_us": getattr(a, "comm_probe", None),
             "engine_probe_us_per_step": getattr(a, "engine_probe", None),

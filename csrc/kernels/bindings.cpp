@@ -28,6 +28,12 @@ void mlp_fwdapply_launch(const float*, float*, float, const float*, const float*
 void mlp_head2_launch(const float*, const int*, float*, int, hipStream_t);
 void mlp_run_pipelined_launch(float*, float*, int, int, float, const float*, const int*, int, int,
                               int, float*, int*, float*, int, int, hipStream_t);
+long long mlp_persistent_ll_words();
+int mlp_persistent_blocks();
+int mlp_persistent_trace_steps();
+void mlp_persistent_launch(float*, const float*, const int*, int, int, int, float, unsigned,
+                           unsigned long long*, int*, float*, int, int, long long,
+                           unsigned long long*, hipStream_t);
 void calib_launch(int, int, int, const int*, const float*, float*, hipStream_t);
 void clock_probe_launch(int, int, unsigned long long*, float*, hipStream_t);
 void gemm_f32_launch(bool, bool, int, int, int, float, const float*, int, const float*, int,
@@ -103,6 +109,22 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("p0"), py::arg("p1"), py::arg("cur"), py::arg("pending"), py::arg("lr"), py::arg("x"),
      py::arg("labels"), py::arg("nbatches"), py::arg("pos"), py::arg("n"), py::arg("ws"),
      py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"));
+  m.def("mlp_persistent_ll_words", &dtfx::mlp_persistent_ll_words);
+  m.def("mlp_persistent_blocks", &dtfx::mlp_persistent_blocks);
+  m.def("mlp_persistent_trace_steps", &dtfx::mlp_persistent_trace_steps);
+  m.def("mlp_persistent", [](uintptr_t p, uintptr_t x, uintptr_t lab, int nbatches, int pos,
+                             int steps, float lr, unsigned ebase, uintptr_t ll, uintptr_t ctr,
+                             uintptr_t stats, int ring, int B, long long ticks, uintptr_t s,
+                             uintptr_t trace) {
+    py::gil_scoped_release nogil;
+    dtfx::mlp_persistent_launch(P<float>(p), P<const float>(x), P<const int>(lab), nbatches, pos,
+                                steps, lr, ebase, P<unsigned long long>(ll), P<int>(ctr),
+                                P<float>(stats), ring, B, ticks, P<unsigned long long>(trace),
+                                S(s));
+  }, py::arg("p"), py::arg("x"), py::arg("labels"), py::arg("nbatches"), py::arg("pos"),
+     py::arg("steps"), py::arg("lr"), py::arg("ebase"), py::arg("ll"), py::arg("ctr"),
+     py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("ticks"), py::arg("stream"),
+     py::arg("trace") = 0);
   m.def("gemm_f32", [](bool ta, bool tb, int M, int N, int K, float alpha, uintptr_t A, int lda,
                        uintptr_t B, int ldb, float beta, uintptr_t C, int ldc, uintptr_t bias,
                        int act, uintptr_t aux, int ldaux, bool act_grad, uintptr_t s) {

@@ -98,6 +98,8 @@ class FusedMLPTrainer:
         self.max_graph_steps = int(max_graph_steps)
         self._graphs = {}
         self._pool = None
+        self._ll = None   # granule buffer of the persistent engine (allocated on first use)
+        self._ebase = 0   # epoch base of its next launch
 
     # -- state --------------------------------------------------------------
     @property
@@ -258,6 +260,46 @@ class FusedMLPTrainer:
         self.pos = (self.pos + steps) % self.nbatches
         self.cur ^= steps & 1
         self.pending = True
+
+    # -- persistent single-launch engine (csrc/kernels/mlp_persistent.hip) ----------------
+    @property
+    def persistent_ok(self):
+        """The plain single-GPU step with batch <= 128 can run as ONE persistent launch."""
+        return self.host_loop_ok and self.B <= 128
+
+    def run_persistent(self, steps, timeout_s=2.0, trace=None):
+        """``steps`` complete SGD steps (every update applied, nothing left pending) in ONE
+        launch: 105 co-resident workgroups hand z1 partials / backprop factors / small
+        parameters to each other as epoch-tagged 8-byte granules instead of ending a kernel.
+        Same trajectory as the pipelined two-launch step (to f32 rounding).  ``timeout_s`` bounds every in-kernel
+        wait; a timed-out run raises at the next ``check()``.  ``trace``: optional int64
+        [blocks, trace_steps, 8] buffer of in-kernel s_memrealtime stamps (probe only)."""
+        from ..ops._ext import hip, ptr, stream_handle
+
+        steps = int(steps)
+        if not self.persistent_ok:
+            raise RuntimeError("run_persistent: single-GPU step with batch <= 128 only")
+        if steps <= 0:
+            return
+        self.flush()  # a pending pipelined update is applied first (params exact)
+        h = hip()
+        if self._ll is None or self._ebase + steps + 2 >= 2 ** 32:
+            self._ll = torch.zeros(int(h.mlp_persistent_ll_words()), dtype=torch.int64,
+                                   device=self.device)
+            self._ebase = 0
+        ws = self.ws
+        h.mlp_persistent(ptr(self.bufs[self.cur]), ptr(self.x), ptr(self.labels), self.nbatches,
+                         self.pos, steps, self.lr, self._ebase, ptr(self._ll), ptr(ws.ctr),
+                         ptr(ws.stats), ws.stats_ring, self.B, int(timeout_s * 1e8),
+                         stream_handle(), 0 if trace is None else ptr(trace))
+        self._ebase += steps + 1
+        self.pos = (self.pos + steps) % self.nbatches
+
+    def check(self):
+        """Raise if an in-kernel wait of the persistent engine ever timed out."""
+        if self._ll is not None and int(self._ll[-32].item()) != 0:
+            raise RuntimeError("persistent MLP engine: an in-kernel hand-off timed out "
+                               "(parameters are not valid)")
 
     def run(self, steps, use_graph=True, lead=0):
         """Run ``steps`` training steps (epoch-aligned hipGraph replays).  ``lead`` > 0 (single

@@ -293,3 +293,72 @@ def test_host_loop_matches_graph_replay(gpu):
         assert runs[mode][1] == runs["graph"][1] == 23
         assert torch.equal(runs[mode][2], runs["graph"][2]), mode
         assert runs[mode][3] == runs["graph"][3] == 23 % 13
+
+
+@pytest.mark.parametrize("B", [100, 64, 128, 7])
+def test_persistent_trainer_matches_pipelined(gpu, B):
+    """The persistent single-launch engine (workgroups hand z1 partials, backprop factors and
+    small parameters to each other as epoch-tagged granules) runs the same SGD trajectory as
+    the two-launch pipelined step -- parameters within f32 rounding (the compiler may contract
+    a different product of a dot into an FMA), identical global_step, matching loss/accuracy
+    records -- across several launches (the epoch base advances), an epoch wrap of the
+    dataset and a switch back to the pipelined path."""
+    from distributedtensorflowexample_amd.train.fused_mlp import FusedMLPTrainer
+
+    nb, lr = 5, 0.3
+    p, x, y = _mlp_setup(gpu, B, nb, seed=5)
+    p.mul_(0.1)
+    tp = FusedMLPTrainer(p, x, y, B, lr)
+    tq = FusedMLPTrainer(p, x, y, B, lr)
+    assert tq.persistent_ok
+    tp.run(7, use_graph=False)
+    tp.flush()
+    tq.run_persistent(7)
+    torch.cuda.synchronize()
+    tq.check()
+    assert tq.global_step() == tp.global_step() == 7
+    assert tq.pos == tp.pos
+    d = (tq.params - tp.params).abs().max().item()
+    assert d < 1e-6, d
+    tp.run(13, use_graph=False)
+    for k in (6, 1, 4):
+        tq.run_persistent(k)
+    tq.run(2, use_graph=False)  # back on the pipelined path
+    tp.flush()
+    tq.flush()
+    torch.cuda.synchronize()
+    tq.check()
+    assert tq.global_step() == tp.global_step() == 20
+    d = (tq.params - tp.params).abs().max().item()
+    assert d < 2e-6, d
+    assert torch.allclose(tq.stats_range(0, 20), tp.stats_range(0, 20), atol=1e-5)
+    # and against the float64 reference
+    ref = p.double().cpu()
+    xr, yr = x.double().cpu(), y.cpu()
+    for s in range(20):
+        sl = slice((s % nb) * B, (s % nb + 1) * B)
+        g, _, _ = mlp_step.reference_step(ref, xr[sl], yr[sl])
+        ref = ref - lr * g
+    assert (tq.params.double().cpu() - ref).abs().max().item() < 1e-4
+
+
+def test_persistent_trainer_long_run(gpu):
+    """2000 steps in one persistent launch (epoch parity planes reused 1000 times, 20 dataset
+    wraps) track 2000 pipelined steps."""
+    from distributedtensorflowexample_amd.data.synthetic import mnist_like_device
+    from distributedtensorflowexample_amd.models.mlp import init_params
+    from distributedtensorflowexample_amd.train.fused_mlp import FusedMLPTrainer
+
+    p = init_params(gpu, seed=7)
+    x, y = mnist_like_device(10000, seed=8, device=gpu)
+    tp = FusedMLPTrainer(p, x, y, 100, 0.001)
+    tq = FusedMLPTrainer(p, x, y, 100, 0.001)
+    tp.run(2000)
+    tp.flush()
+    tq.run_persistent(2000)
+    torch.cuda.synchronize()
+    tq.check()
+    assert tq.global_step() == tp.global_step() == 2000
+    d = (tq.params - tp.params).abs().max().item()
+    assert d < 1e-4, d
+    assert torch.allclose(tq.stats_range(1000, 2000), tp.stats_range(1000, 2000), atol=1e-4)
