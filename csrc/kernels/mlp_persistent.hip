@@ -9,21 +9,25 @@
 // ONE agent-scope store (sc1) and polled with agent-scope loads until the epoch matches.  No
 // grid barrier, no fence, no flag: a consumer waits exactly for the words it reads.
 //
-// Grid (105 workgroups x 256 threads, all co-resident: 1 per CU needed of 256 CUs):
+// Grid (105 + B workgroups x 256 threads, all co-resident: 1 per CU needed of 256 CUs):
 //   blocks [0, 98): W1 block (jt, ks) OWNS W1t[jt*16 .. +16][ks*56 .. +56] for the whole
 //     launch: the tile lives in LDS (+ each lane's 4 master values in registers); the W1
 //     gradient is never materialised and W1 never leaves the block until the final store.
 //     step t:  (t > 0) wait for dz1 of step t-1 (rows x this block's 16 hidden units) ->
 //              LDS; dW1^T tile = dz1^T . x(t-1) (f32 MFMA, K = batch); W1 -= lr * g;
-//              z1 partial of every row over the block's 56 features -> SLAB granules;
-//              wave 3 then runs the head of row `blockIdx.x` (wave 2: row + 105).
+//              z1 partial of every row over the block's 56 features -> SLAB granules.
 //   blocks [98, 105): small block jt owns W2t[:, jt*16 .. +16], b1[jt*16 .. +16] (and b2,
 //     the loss/accuracy record and global_step for jt == 0) in registers; step t:
-//              (t > 0) dW2 / db1 / db2 of step t-1 from the HEAD granules of every row,
-//              update, publish the new values as SP granules (epoch of step t).
-//   head (one wave per batch row): waits for its row's 14 SLAB partials and the SP
-//     granules, z1 -> h -> logits -> softmax / xent / argmax -> dlogits -> dz1; publishes
-//     {dz1, h, dlogits, (loss, correct)} of the row as HEAD granules.
+//              (t > 0) dW2 / db1 / db2 of step t-1 from the HEAD granules of every row
+//              (batch split over the 4 waves), update, publish the new values as SP
+//              granules (epoch of step t).
+//   blocks [105, 105 + B): head of batch row bid - 105 (4 waves): waits for its row's 14
+//     SLAB partials and the SP granules, z1 -> h -> logits -> softmax / xent / argmax ->
+//     dlogits -> dz1; publishes {dz1, h, dlogits, (loss, correct)} as HEAD granules.
+//   Heads have workgroups of their own because a wave's load cannot be consumed before
+//   every OLDER store of that wave is acknowledged (gfx9 counts loads and stores in one
+//   vmcnt): a W1 wave that published its slab and then ran a head stalled ~2 us on its own
+//   write-through stores before it could use the head's data (trace probe).
 //
 // Epochs: step t of a launch tags its words with ebase + 1 + t (the host advances ebase by
 // steps + 1 per launch, so a stale word from any earlier launch never matches).  Two parity
@@ -63,14 +67,30 @@ constexpr long long SLAB_PAR = (long long)KS * MAXB * SLAB_ROW;
 constexpr int HEAD_ROW = 256;                                 // per row: dz1 | h | dl | stat
 constexpr int HDZ = 0, HHB = 128, HDL = 232, HST = 248;
 constexpr long long HEAD_PAR = (long long)MAXB * HEAD_ROW;
-constexpr int SP_PAR = 1152;                                  // b1 [0,100) W2t [100,1100) b2
+constexpr int SP_REP = 1152;                                  // b1 [0,100) W2t [100,1100) b2
 constexpr int SP_W2 = 100, SP_B2 = 1100;
+// Every head reads ALL small parameters; with one copy a hundred waves' agent-scope loads of
+// the same 9 KB queued on the few memory channels holding it (trace probe: 3.7 us from the
+// last publish to the heads' data), so the small blocks publish NREP copies and head row b
+// reads copy b % NREP.
+constexpr int NREP = 8;
+constexpr int SP_PAR = NREP * SP_REP;
 constexpr long long OFF_SLAB = 0;
 constexpr long long OFF_HEAD = OFF_SLAB + 2 * SLAB_PAR;
 constexpr long long OFF_SP = OFF_HEAD + 2 * HEAD_PAR;
 constexpr long long OFF_ERR = OFF_SP + 2 * SP_PAR;
 constexpr long long LL_WORDS = OFF_ERR + 32;
 constexpr int TRACE_STEPS = 64;
+// representative word polled before the full load of a wait (-1: poll every word at once)
+#ifndef DTFX_REP_HEAD
+#define DTFX_REP_HEAD -1
+#endif
+#ifndef DTFX_REP_SMALL
+#define DTFX_REP_SMALL -1
+#endif
+#ifndef DTFX_REP_W1
+#define DTFX_REP_W1 -1
+#endif
 
 static_assert(NPARAM == 79510, "parameter count of worker.py:50-53");
 static_assert(KS * KW == D && HDL + 16 <= HST && HST + 2 <= HEAD_ROW, "layout");
@@ -83,7 +103,7 @@ struct Args {
   int* ctr;                 // global_step
   float* stats;             // [ring][2] loss / accuracy per step
   long long ticks;          // wait bound (s_memrealtime ticks)
-  u64* trace;               // optional [NBLK][TRACE_STEPS][8] s_memrealtime stamps (probe)
+  u64* trace;               // optional [NBLK][TRACE_STEPS][12] s_memrealtime stamps (probe)
   float lr;
   unsigned ebase;
   int nbatches, pos0, steps, B, ring;
@@ -96,10 +116,18 @@ __device__ __forceinline__ void st_ll(u64* p, float v, unsigned e) {
 __device__ __forceinline__ u64 ld_ll(const u64* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for every vector
+// memory op in flight (s_waitcnt vmcnt(0)): after a phase that published granules with
+// write-through stores it stalled ~2 us until they were acknowledged (trace probe), which no
+// consumer here needs -- cross-workgroup data is tagged, cross-wave data goes through LDS.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // probe stamp k of (block, step t) by lane 0 of the calling wave
 __device__ __forceinline__ void stamp(const Args& a, int t, int k) {
   if (a.trace != nullptr && t < TRACE_STEPS && (threadIdx.x & 63) == 0)
-    a.trace[((size_t)blockIdx.x * TRACE_STEPS + t) * 8 + k] = __builtin_amdgcn_s_memrealtime();
+    a.trace[((size_t)blockIdx.x * TRACE_STEPS + t) * 12 + k] = __builtin_amdgcn_s_memrealtime();
 }
 __device__ __forceinline__ float4 f4(const float* p) {
   return *reinterpret_cast<const float4*>(p);
@@ -128,7 +156,7 @@ __device__ __forceinline__ void ll_wait(Addr addr, int rep, unsigned e, const Ar
     }
     return false;
   };
-  if (!fail) {
+  if (!fail && rep >= 0) {
     const u64* pr = addr(rep);
     if (pr) {
       for (int it = 1; (unsigned)(ld_ll(pr) >> 32) != e; ++it) {
@@ -161,56 +189,64 @@ __device__ __forceinline__ void ll_wait(Addr addr, int rep, unsigned e, const Ar
 }
 
 // ---------------------------------------------------------------------------------------
-// head of batch row `row`, step t (one wave): mlp_head_kernel<false, false, 0, KS2> math
+// head of batch row `row`, step t, by the 4 waves of a workgroup (mlp_head_kernel math):
+// wave w owns hidden units j = 25w + (lane & 31) (lanes with lane & 31 >= 25 idle); half
+// h2 = lane >> 5 sums slab planes ks = 7 h2 .. 7 h2 + 6 and holds W2t rows c = 5 h2 .. +4.
+// A one-wave head had to pull 60 granule words per lane (30 KB per wave: ~5 us of agent-scope
+// loads); split four ways a wave pulls 23.  The 10 partial logits of each wave meet in LDS
+// (red, double-buffered by step parity).  Called by every wave of the block (barrier inside).
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void head_row(const Args& a, int row, int t, int lane, bool& fail) {
+__device__ __forceinline__ float swap32_add(float v) {  // v + v of lane ^ 32
+  const int x = __float_as_int(v);
+  auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return __int_as_float(r[0]) + __int_as_float(r[1]);
+}
+
+__device__ __forceinline__ void head_row(const Args& a, int row, int t, int wave, int lane,
+                                         float (*red)[16], bool& fail) {
   const unsigned e = a.ebase + 1u + (unsigned)t;
   const int bidx = (a.pos0 + t) % a.nbatches;
   const int y = a.labels[(size_t)bidx * a.B + row];
-  const u64* slab = a.ll + OFF_SLAB + (e & 1) * SLAB_PAR + (size_t)row * SLAB_ROW;
-  const u64* sp = a.ll + OFF_SP + (e & 1) * SP_PAR;
-  // words: [0, 28) slab[ks][j_u], [28, 48) W2t[c][j_u], [48, 50) b1[j_u], [50, 60) b2[c]
-  stamp(a, t, 5);
-  float v[60];
-  ll_wait<60>(
+  const int h2 = lane >> 5, jl = lane & 31;
+  const bool jv = jl < 25;
+  const int j = 25 * wave + (jv ? jl : 0);
+  const u64* slab = a.ll + OFF_SLAB + (e & 1) * SLAB_PAR + (size_t)row * SLAB_ROW + j;
+  const u64* sp = a.ll + OFF_SP + (e & 1) * SP_PAR + (row % NREP) * SP_REP;
+  // words: [0, 7) slab[7 h2 + k][j], [7, 12) W2t[5 h2 + k][j], [12] b1[j], [13, 23) b2[c]
+  if (wave == 3) stamp(a, t, 5);
+  float v[23];
+  ll_wait<23>(
       [&](int i) -> const u64* {
-        if (i < 28) {
-          const int u = i / KS, ks = i % KS, j = lane + 64 * u;
-          return j < H ? slab + (size_t)ks * MAXB * SLAB_ROW + j : nullptr;
-        }
-        if (i < 48) {
-          const int u = (i - 28) / C, c = (i - 28) % C, j = lane + 64 * u;
-          return j < H ? sp + SP_W2 + c * H + j : nullptr;
-        }
-        if (i < 50) {
-          const int j = lane + 64 * (i - 48);
-          return j < H ? sp + j : nullptr;
-        }
-        return sp + SP_B2 + (i - 50);
+        if (i < 7) return jv ? slab + (size_t)(7 * h2 + i) * MAXB * SLAB_ROW : nullptr;
+        if (i < 12) return jv ? sp + SP_W2 + (5 * h2 + i - 7) * H + j : nullptr;
+        if (i == 12) return jv ? sp + j : nullptr;
+        return sp + SP_B2 + (i - 13);
       },
-      KS - 1, e, a, v, fail);
-  stamp(a, t, 6);
-  float zs[2], hv[2], w2[2][C], b2v[C];
-  bool jv[2];
+      DTFX_REP_HEAD, e, a, v, fail);
+  stamp(a, t, wave == 3 ? 6 : 8 + wave);
+  float zp = 0.f;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    jv[u] = lane + 64 * u < H;
-    zs[u] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) zs[u] += v[u * KS + ks];
-#pragma unroll
-    for (int c = 0; c < C; ++c) w2[u][c] = v[28 + u * C + c];
-  }
-#pragma unroll
-  for (int c = 0; c < C; ++c) b2v[c] = v[50 + c];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) hv[u] = jv[u] ? sigmoidf_(zs[u] + v[48 + u]) : 0.f;
+  for (int k = 0; k < 7; ++k) zp += v[k];
+  const float z = swap32_add(zp);  // planes 0..6 + planes 7..13
+  const float hv = jv ? sigmoidf_(z + v[12]) : 0.f;
   float lg[C];
 #pragma unroll
-  for (int c = 0; c < C; ++c) lg[c] = hv[0] * w2[0][c] + hv[1] * w2[1][c];
+  for (int c = 0; c < C; ++c) {
+    const bool mine = (c >= 5 * h2) && (c < 5 * h2 + 5);
+    const float w2 = v[7 + (c - 5 * h2 >= 0 && c - 5 * h2 < 5 ? c - 5 * h2 : 0)];
+    lg[c] = mine ? hv * w2 : 0.f;
+  }
   wave_sum_n(lg);
+  float* rw = red[(t & 1) * 4 + wave];
+  float mine_l = 0.f;
 #pragma unroll
-  for (int c = 0; c < C; ++c) lg[c] += b2v[c];
+  for (int c = 0; c < C; ++c) mine_l = lane == c ? lg[c] : mine_l;
+  if (lane < C) rw[lane] = mine_l;
+  lds_barrier();
+  if (wave == 3) stamp(a, t, 11);
+  const float (*rr)[16] = red + (t & 1) * 4;
+#pragma unroll
+  for (int c = 0; c < C; ++c) lg[c] = ((rr[0][c] + rr[1][c]) + (rr[2][c] + rr[3][c])) + v[13 + c];
   float m = lg[0];
   int am = 0;
 #pragma unroll
@@ -226,27 +262,31 @@ __device__ __forceinline__ void head_row(const Args& a, int row, int t, int lane
     dl[c] = (__expf(lg[c] - m) * inv - (c == y ? 1.f : 0.f)) * invB;
     ly = (c == y) ? lg[c] : ly;
   }
+  float dhp = 0.f;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    float dlc = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) dlc = (c == 5 * h2 + k) ? dl[c] : dlc;
+    dhp += dlc * v[7 + k];
+  }
+  const float dh = swap32_add(dhp);
   u64* hd = a.ll + OFF_HEAD + (e & 1) * HEAD_PAR + (size_t)row * HEAD_ROW;
+  if (jv) {
+    if (h2 == 0) st_ll(hd + HDZ + j, dh * hv * (1.f - hv), e);
+    else st_ll(hd + HHB + j, hv, e);
+  }
+  if (wave == 0) {
+    float mydl = 0.f;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int j = lane + 64 * u;
-    if (j < H) {
-      float dh = 0.f;
-#pragma unroll
-      for (int c = 0; c < C; ++c) dh += dl[c] * w2[u][c];
-      st_ll(hd + HDZ + j, dh * hv[u] * (1.f - hv[u]), e);
-      st_ll(hd + HHB + j, hv[u], e);
+    for (int c = 0; c < C; ++c) mydl = (lane == c) ? dl[c] : mydl;
+    if (lane < C) st_ll(hd + HDL + lane, mydl, e);
+    if (lane == 0) {
+      st_ll(hd + HST, m + __logf(se) - ly, e);  // xent of this row
+      st_ll(hd + HST + 1, (am == y) ? 1.f : 0.f, e);
     }
   }
-  float mydl = 0.f;
-#pragma unroll
-  for (int c = 0; c < C; ++c) mydl = (lane == c) ? dl[c] : mydl;
-  if (lane < C) st_ll(hd + HDL + lane, mydl, e);
-  if (lane == 0) {
-    st_ll(hd + HST, m + __logf(se) - ly, e);  // xent of this row
-    st_ll(hd + HST + 1, (am == y) ? 1.f : 0.f, e);
-  }
-  stamp(a, t, 7);
+  if (wave == 3) stamp(a, t, 7);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -262,15 +302,19 @@ __global__ __launch_bounds__(256) void mlp_persistent_kernel(Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, r = lane & 15, q = lane >> 4;
   const int bid = blockIdx.x;
-  // head rows of this block: wave 3 -> row bid, wave 2 -> row bid + NBLK
-  const int hrow = wave == 3 ? bid : (wave == 2 ? bid + NBLK : B);
-  const bool has_head = hrow < B;
   bool fail = false;
+
+  if (bid >= NBLK) {
+    // ===================== head block: batch row bid - NBLK ===========================
+    __shared__ float red[8][16];  // per-wave partial logits, [step parity][wave][c]
+    for (int t = 0; t < a.steps; ++t) head_row(a, bid - NBLK, t, wave, lane, red, fail);
+    return;
+  }
 
   if (bid >= NW1) {
     // ===================== small-parameter block jt ===================================
     const int jt = bid - NW1;
-    if (wave >= 2 && jt != 0 && !(wave == 3 && has_head)) return;
+    const bool upd = wave < 2 || (wave == 2 && jt == 0);  // waves owning parameters
     // owned values: wave 0 W2t[c = q*4+i][j = jt*16+r]; wave 1 b1[j = jt*16+q*4+i] (r == 0);
     // wave 2 (jt == 0) b2[c = q*4+i] (r == 0).  sp index: position in the SP plane
     int spi[4];
@@ -302,80 +346,97 @@ __global__ __launch_bounds__(256) void mlp_persistent_kernel(Args a) {
       u64* sp = a.ll + OFF_SP + (e0 & 1) * SP_PAR;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (own[i]) st_ll(sp + spi[i], pv[i], e0);
+        if (own[i])
+#pragma unroll
+          for (int c = 0; c < NREP; ++c) st_ll(sp + c * SP_REP + spi[i], pv[i], e0);
     }
-    if (wave == 3 && has_head) head_row(a, hrow, 0, lane, fail);
+    // The batch (K of every product) is split over the 4 waves -- wave w takes row groups
+    // g = w, w + 4 -- so each wave pulls at most 28 granule words per lane instead of one wave
+    // pulling 56 (its ~28 KB of agent-scope loads sat on the critical path: every head waits
+    // for these parameters).  Products per wave (MFMA 16x16x4, lane l: A[l&15][k], B[k][l&15]):
+    //   P0 dW2^T[c][j] = sum_b dl[b][c] h[b][jt*16+j]   P1 db1[jt*16+i] = sum_b dz1[b][jt*16+i]
+    //   P2 db2[c] = sum_b dl[b][c] (jt == 0)
+    // Partials meet in LDS (double-buffered by step parity) and the owners add them in wave
+    // order.  Wave 3 of jt == 0 also folds the loss / accuracy record of the step.
+    __shared__ f32x4 part[2][4][3][64];
+    const bool hv_ok = jt * 16 + r < H;
     for (int t = 1; t <= a.steps; ++t) {
       const unsigned ep = a.ebase + (unsigned)t;  // HEAD granules of step t-1
       const u64* hd = a.ll + OFF_HEAD + (ep & 1) * HEAD_PAR;
-      if (wave < 3) {
-        // A operand: wave 0 / 2 dl[b][c = r]; wave 1 dz1[b][jt*16 + r].  B: wave 0 h[b][jt*16+r]
-        const int acol = wave == 1 ? HDZ + jt * 16 + r : HDL + r;
-        const bool aval = wave == 1 ? (jt * 16 + r < H) : (r < C);
-        const bool bval = jt * 16 + r < H;
-        // one wait for both operands: [0, 4*MAXG) A, [4*MAXG, 8*MAXG) B (wave 0 only)
-        constexpr int NA = MAXG * 4;
-        float v[2 * NA];
-        if (wave == 0) stamp(a, t, 0);
-        ll_wait<2 * NA>(
-            [&](int i) -> const u64* {
-              const int k = i < NA ? i : i - NA;
-              const int b = (k >> 2) * 16 + q * 4 + (k & 3);
-              if ((k >> 2) >= NG || b >= B) return nullptr;
-              if (i < NA) return aval ? hd + (size_t)b * HEAD_ROW + acol : nullptr;
-              return wave == 0 && bval ? hd + (size_t)b * HEAD_ROW + HHB + jt * 16 + r : nullptr;
-            },
-            0, ep, a, v, fail);
-        if (wave == 0) stamp(a, t, 1);
-        if (wave != 0) {
+      if (wave == 0) stamp(a, t, 0);
+      // words: [0, 8) dl[b][r], [8, 16) h[b][jt*16+r], [16, 24) dz1[b][jt*16+r] for the 2 x 4
+      // rows b = g*16 + q*4 + e of groups g = wave, wave + 4; [24, 28) stat words (rows lane,
+      // lane + 64) for wave 3 of jt == 0
+      float v[28];
+      ll_wait<28>(
+          [&](int i) -> const u64* {
+            if (i >= 24) {
+              const int b = lane + 64 * ((i - 24) >> 1);
+              return wave == 3 && jt == 0 && b < B ? hd + (size_t)b * HEAD_ROW + HST + (i & 1)
+                                                   : nullptr;
+            }
+            const int k = i & 7, g = wave + 4 * (k >> 2);
+            const int b = g * 16 + q * 4 + (k & 3);
+            if (g >= NG || b >= B) return nullptr;
+            const u64* row = hd + (size_t)b * HEAD_ROW;
+            if (i < 8) return r < C ? row + HDL + r : nullptr;
+            if (i < 16) return hv_ok ? row + HHB + jt * 16 + r : nullptr;
+            return hv_ok ? row + HDZ + jt * 16 + r : nullptr;
+          },
+          DTFX_REP_SMALL, ep, a, v, fail);
+      if (wave == 0) stamp(a, t, 1);
+      f32x4 p0 = {0, 0, 0, 0}, p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0};
 #pragma unroll
-          for (int i = NA; i < 2 * NA; ++i) v[i] = 1.f;
-        }
-        f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+      for (int h = 0; h < 2; ++h) {
+        if (wave + 4 * h < NG) {
 #pragma unroll
-        for (int g = 0; g < MAXG; ++g) {
-          if (g < NG) {
-            acc0 = mfma16x16x4(v[g * 4 + 0], v[NA + g * 4 + 0], acc0);
-            acc1 = mfma16x16x4(v[g * 4 + 1], v[NA + g * 4 + 1], acc1);
-            acc0 = mfma16x16x4(v[g * 4 + 2], v[NA + g * 4 + 2], acc0);
-            acc1 = mfma16x16x4(v[g * 4 + 3], v[NA + g * 4 + 3], acc1);
+          for (int e = 0; e < 4; ++e) {
+            p0 = mfma16x16x4(v[h * 4 + e], v[8 + h * 4 + e], p0);
+            p1 = mfma16x16x4(v[16 + h * 4 + e], 1.f, p1);
+            if (jt == 0) p2 = mfma16x16x4(v[h * 4 + e], 1.f, p2);
           }
+        }
+      }
+      f32x4(&pp)[4][3][64] = part[t & 1];
+      pp[wave][0][lane] = p0;
+      pp[wave][1][lane] = p1;
+      pp[wave][2][lane] = p2;
+      lds_barrier();
+      if (upd) {
+        f32x4 g = {0, 0, 0, 0};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const f32x4 o = pp[w][wave][lane];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) g[i] += o[i];
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (!fail) pv[i] = pv[i] - a.lr * (acc0[i] + acc1[i]);
+          if (!fail) pv[i] = pv[i] - a.lr * g[i];
         if (t < a.steps) {
           const unsigned e = a.ebase + 1u + (unsigned)t;
           u64* sp = a.ll + OFF_SP + (e & 1) * SP_PAR;
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            if (own[i]) st_ll(sp + spi[i], pv[i], e);
+            if (own[i])
+#pragma unroll
+              for (int c = 0; c < NREP; ++c) st_ll(sp + c * SP_REP + spi[i], pv[i], e);
           if (wave == 0) stamp(a, t, 2);
         }
-      } else {
-        if (jt == 0) {  // loss / accuracy record of step t-1
-          float sv[4];
-          ll_wait<4>(
-              [&](int i) -> const u64* {
-                const int b = lane + 64 * (i >> 1);
-                return b < B ? hd + (size_t)b * HEAD_ROW + HST + (i & 1) : nullptr;
-              },
-              0, ep, a, sv, fail);
-          const float l = wave_sum(sv[0] + sv[2]), ac = wave_sum(sv[1] + sv[3]);
-          if (lane == 0 && a.stats) {
-            float* st = a.stats + (size_t)((ctr0 + t - 1) % a.ring) * 2;
-            st[0] = l / (float)B;
-            st[1] = ac / (float)B;
-          }
+      } else if (wave == 3 && jt == 0) {  // loss / accuracy record of step t-1
+        const float l = wave_sum(v[24] + v[26]), ac = wave_sum(v[25] + v[27]);
+        if (lane == 0 && a.stats) {
+          float* st = a.stats + (size_t)((ctr0 + t - 1) % a.ring) * 2;
+          st[0] = l / (float)B;
+          st[1] = ac / (float)B;
         }
-        if (has_head && t < a.steps) head_row(a, hrow, t, lane, fail);
       }
     }
-    if (wave < 3) {
+    if (upd) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (own[i]) a.p[OFF_B1 + spi[i]] = pv[i];
-    } else if (jt == 0 && lane == 0) {
+    } else if (wave == 3 && jt == 0 && lane == 0) {
       *a.ctr = ctr0 + a.steps;
     }
     return;
@@ -445,12 +506,12 @@ __global__ __launch_bounds__(256) void mlp_persistent_kernel(Args a) {
             const int b = (tid >> 4) + 16 * k;
             return b < B && jvalid ? hd + (size_t)b * HEAD_ROW + jl : nullptr;
           },
-          0, ep, a, dz, fail);
+          DTFX_REP_W1, ep, a, dz, fail);
       if (wave == 0) stamp(a, t, 1);
 #pragma unroll
       for (int k = 0; k < NL; ++k) Dz[jl][(tid >> 4) + 16 * k] = dz[k];
       if (fail) abort_flag = 1;
-      __syncthreads();
+      lds_barrier();
       if (abort_flag) break;
       if (wave == 0) stamp(a, t, 2);
       f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
@@ -479,7 +540,7 @@ __global__ __launch_bounds__(256) void mlp_persistent_kernel(Args a) {
         break;
       }
     }
-    __syncthreads();  // Wt of step t complete
+    lds_barrier();  // Wt of step t complete
     if (abort_flag) break;
     if (wave == 0) stamp(a, t, 3);
     // ---- phase B: z1 partial of row tiles rt = wave, wave + 4 over the block's features ---
@@ -513,10 +574,6 @@ __global__ __launch_bounds__(256) void mlp_persistent_kernel(Args a) {
       }
     }
     if (wave == 0) stamp(a, t, 4);
-    if (has_head) {
-      head_row(a, hrow, t, lane, fail);
-      if (fail) abort_flag = 1;
-    }
   }
 }
 
@@ -542,9 +599,9 @@ void mlp_persistent_launch(float* p, const float* x, const int* labels, int nbat
     throw std::runtime_error("mlp_persistent: x must be 16-byte aligned");
   Args a{p, x, labels, ll, ctr, stats, ticks, trace, lr, ebase, nbatches, pos, steps, B, ring};
   if ((B + 15) / 16 == 7)
-    hipLaunchKernelGGL(mlp_persistent_kernel<7>, dim3(NBLK), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(mlp_persistent_kernel<7>, dim3(NBLK + B), dim3(256), 0, stream, a);
   else
-    hipLaunchKernelGGL(mlp_persistent_kernel<0>, dim3(NBLK), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(mlp_persistent_kernel<0>, dim3(NBLK + B), dim3(256), 0, stream, a);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

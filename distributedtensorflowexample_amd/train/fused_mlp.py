@@ -273,7 +273,7 @@ class FusedMLPTrainer:
         parameters to each other as epoch-tagged 8-byte granules instead of ending a kernel.
         Same trajectory as the pipelined two-launch step (to f32 rounding).  ``timeout_s`` bounds every in-kernel
         wait; a timed-out run raises at the next ``check()``.  ``trace``: optional int64
-        [blocks, trace_steps, 8] buffer of in-kernel s_memrealtime stamps (probe only)."""
+        [blocks, trace_steps, 12] buffer of in-kernel s_memrealtime stamps (probe only)."""
         from ..ops._ext import hip, ptr, stream_handle
 
         steps = int(steps)

@@ -30,15 +30,15 @@ def main():
     x, y = mnist_like_device(55000, seed=100, device=dev)
     tr = FusedMLPTrainer(p, x, y, 100, 0.001)
     tr.run_persistent(100)
-    nblk, ts = hip().mlp_persistent_blocks(), hip().mlp_persistent_trace_steps()
-    trace = torch.zeros(nblk, ts, 8, dtype=torch.int64, device=dev)
+    nblk, ts = hip().mlp_persistent_blocks() + 100, hip().mlp_persistent_trace_steps()
+    trace = torch.zeros(nblk, ts, 12, dtype=torch.int64, device=dev)
     tr.run_persistent(ts + 1, trace=trace)
     torch.cuda.synchronize()
     tr.check()
     T = trace.cpu().double() * 0.01  # ticks -> us
     nw1 = 98
-    W, S = T[:nw1], T[nw1:]
-    hb = list(range(100))  # head rows 0..99 -> blocks 0..99, wave 3
+    W, S = T[:nw1], T[nw1:nw1 + 7]
+    hb = list(range(nw1 + 7, nw1 + 107))  # head blocks (row = block - 105)
     out = {}
     steps = range(8, ts - 1)
     out["period"] = med([W[:, t + 1, 3].median().item() - W[:, t, 3].median().item() for t in steps])
@@ -49,7 +49,11 @@ def main():
     H = T[hb]
     out["head_wait"] = med([(H[:, t, 6] - H[:, t, 5]).median().item() for t in steps])
     out["head_compute_store"] = med([(H[:, t, 7] - H[:, t, 6]).median().item() for t in steps])
-    out["head_start_after_own_slab"] = med([(H[:nw1, t, 5] - W[:, t, 4]).median().item() for t in steps])
+    for w in range(3):
+        out["head_wave%d_got_minus_wave3" % w] = med(
+            [(H[:, t, 8 + w] - H[:, t, 6]).median().item() for t in steps])
+    out["head_sync_to_stored"] = med([(H[:, t, 7] - H[:, t, 11]).median().item() for t in steps])
+    out["head_wave3_got_to_sync"] = med([(H[:, t, 11] - H[:, t, 6]).median().item() for t in steps])
     # hand-offs: last producer done -> consumer sees data
     out["slab_last_store_to_head_got_med"] = med(
         [(H[:, t, 6] - W[:, t, 4].max()).median().item() for t in steps])
