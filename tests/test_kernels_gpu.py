@@ -362,3 +362,27 @@ def test_persistent_trainer_long_run(gpu):
     d = (tq.params - tp.params).abs().max().item()
     assert d < 1e-4, d
     assert torch.allclose(tq.stats_range(1000, 2000), tp.stats_range(1000, 2000), atol=1e-4)
+
+
+def test_persistent_trainer_error_word_drains_and_raises(gpu):
+    """A raised error word (what a timed-out hand-off leaves) makes every wait of the next
+    persistent launch give up after a few polls: the grid drains quickly and check() raises."""
+    import time
+
+    from distributedtensorflowexample_amd.data.synthetic import mnist_like_device
+    from distributedtensorflowexample_amd.models.mlp import init_params
+    from distributedtensorflowexample_amd.train.fused_mlp import FusedMLPTrainer
+
+    p = init_params(gpu, seed=9)
+    x, y = mnist_like_device(1000, seed=9, device=gpu)
+    tr = FusedMLPTrainer(p, x, y, 100, 0.01)
+    tr.run_persistent(5)
+    torch.cuda.synchronize()
+    tr.check()
+    tr._ll[-32] = 1  # the sticky error word
+    t0 = time.perf_counter()
+    tr.run_persistent(200, timeout_s=0.5)
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 10.0
+    with pytest.raises(RuntimeError):
+        tr.check()
