@@ -57,6 +57,7 @@ void act_fwd_launch(long long, int, const float*, float*, hipStream_t);
 void register_rccl(py::module_& m);
 void register_nn(py::module_& m);
 void register_xgmi(py::module_& m);
+void register_gpu_ps(py::module_& m);
 
 template <typename T>
 static inline T* P(uintptr_t a) { return reinterpret_cast<T*>(a); }
@@ -187,6 +188,7 @@ PYBIND11_MODULE(_hip, m) {
   register_rccl(m);
   register_nn(m);
   register_xgmi(m);
+  register_gpu_ps(m);
   m.def("device_count", []() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -184,6 +184,10 @@ def define_reference_flags(flag_values=FLAGS):
     DEFINE_float("save_model_secs", 30.0, "Chief checkpoint interval (Supervisor)", fv)
     DEFINE_float("save_summaries_secs", 30.0, "Chief step-rate summary interval", fv)
     DEFINE_boolean("use_locking", False, "Serialize PS updates per variable", fv)
+    DEFINE_string("ps_device", "cpu",
+                  "cpu: variables on the TCP parameter server (the reference) | gpu: variables "
+                  "in one GPU-resident store on the chief worker's GPU, IPC-mapped by every "
+                  "worker (pull / apply / global_step over xGMI; async PS only)", fv)
     DEFINE_integer("seed", 0, "Parameter init seed", fv)
     DEFINE_string("model", "mlp", "mlp (the reference) | bert | resnet50 (north-star configs)", fv)
     DEFINE_string("model_config", "base", "base | tiny (tiny = CPU-sized variant of bert/resnet50)",

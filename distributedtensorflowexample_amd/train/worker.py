@@ -76,9 +76,23 @@ class Worker:
         self.lr = float(flags.learning_rate)
         self.use_fused = self.device.type == "cuda" and 1 <= self.batch_size <= mlp_step.MAX_BATCH
 
-        # global variables on the ps (replica_device_setter(num_ps), worker.py:24-32)
-        self.store = PSVariableStore(server.target, GLOBAL_SPECS,
-                                     setter=replica_device_setter(len(server.target)))
+        # global variables on the ps (replica_device_setter(num_ps), worker.py:24-32), or with
+        # --ps_device gpu in one GPU-resident store on the chief's GPU (parallel/gpu_ps.py)
+        self.gpu_ps = str(getattr(flags, "ps_device", "cpu")) == "gpu"
+        if self.gpu_ps:
+            if not self.use_fused:
+                raise ValueError("--ps_device gpu needs a GPU worker and 1 <= batch_size <= %d"
+                                 % mlp_step.MAX_BATCH)
+            if bool(getattr(flags, "sync_replicas", False)):
+                raise ValueError("--sync_replicas runs on the TCP parameter server "
+                                 "(--ps_device cpu)")
+            from ..parallel.gpu_ps import GpuPSStore
+
+            self.store = GpuPSStore(server.target, self.device, int(flags.num_workers),
+                                    setter=replica_device_setter(len(server.target)))
+        else:
+            self.store = PSVariableStore(server.target, GLOBAL_SPECS,
+                                         setter=replica_device_setter(len(server.target)))
         # local replica (worker.py:34-40): one flat buffer on this worker's device
         self.params = torch.zeros(mlp_step.NPARAM, device=self.device)
         self.grad = torch.zeros_like(self.params)
@@ -126,6 +140,20 @@ class Worker:
         tfg = {k: t.contiguous() for k, t in flat_to_tf_vars(g.cpu()).items()}
         return tfg, float(loss), float(acc)
 
+    def compute_device(self, batch_x, batch_y):
+        """Local forward/backward with the gradient left in ``self.grad`` on the device (GPU
+        parameter store: nothing crosses to the host but the loss / accuracy record)."""
+        y = np.asarray(batch_y)
+        labels = y.argmax(1) if y.ndim == 2 else y
+        self.xb.copy_(torch.from_numpy(np.ascontiguousarray(batch_x, np.float32)))
+        self.yb.copy_(torch.from_numpy(labels.astype(np.int32)))
+        mlp_step.step_grad(self.params, self.xb, self.yb, self.ws, self.grad)
+
+    def step_record(self):
+        """(loss, accuracy) the last compute_device step recorded on the device."""
+        loss, acc = self.ws.stats[(self.ws.global_step() - 1) % self.ws.stats_ring].tolist()
+        return float(loss), float(acc)
+
     def accuracy(self, images, labels):
         """worker.py:87-90 on the local replica."""
         x = torch.from_numpy(np.ascontiguousarray(images, np.float32)).to(self.device)
@@ -166,6 +194,36 @@ class Worker:
             # the mean of replicas_to_aggregate gradients and advances global_step
             local_step = self.store.read_int("global/global_step") if sync else 0
             while not sv.should_stop():
+                if self.gpu_ps:
+                    # the same four ops on the device, stream-ordered: pull (peer read), local
+                    # forward/backward, remote ApplyGradientDescent (peer read-modify-write),
+                    # AssignAdd on global_step (system-scope atomic; returns the old value)
+                    self.store.pull_into(self.params)
+                    batch_x, batch_y = dataset.train.next_batch(self.batch_size)
+                    self.compute_device(batch_x, batch_y)
+                    self.store.push_apply_flat(self.grad, self.lr,
+                                               bool(getattr(fl, "use_locking", False)))
+                    step = self.store.fetch_add("global/global_step", 1)
+                    cost, acc = self.step_record()
+                    self.summary_writer.add_scalars({"loss": cost, "accuracy": acc}, step)
+                    history.append((step, cost, acc))
+                    local_steps += 1
+                    if step % log_every == 0 and step != 0:
+                        elapsed = time.time() - start_time
+                        self.log("step: {}\t| cost: {}\t| speed: {}step/sec".format(
+                            step, cost, float((step - start_step) / max(elapsed, 1e-9))))
+                        start_time = time.time()
+                        start_step = step
+                    if step % eval_every == 0:
+                        self.log("test accuracy: {}".format(
+                            self.accuracy(dataset.test.images, dataset.test.labels)))
+                    if step >= fl.training_steps:
+                        break
+                    if max_steps is not None and local_steps >= max_steps:
+                        break
+                    if stop_after_secs is not None and time.time() - t_begin > stop_after_secs:
+                        break
+                    continue
                 self.sync_op()
                 batch_x, batch_y = dataset.train.next_batch(self.batch_size)
                 grads, cost, acc = self.compute(batch_x, batch_y)
@@ -193,4 +251,6 @@ class Worker:
                     break
                 if stop_after_secs is not None and time.time() - t_begin > stop_after_secs:
                     break
+        if self.gpu_ps:
+            self.store.close()  # the chief frees the store once every other worker detached
         return history

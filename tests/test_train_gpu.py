@@ -105,3 +105,125 @@ def test_mirrored_gpu_periodic_checkpoints_do_not_perturb_training(gpu, tmp_path
     assert out["busy"][1] > out["quiet"][1] >= 1, (out["busy"][1], out["quiet"][1])
     assert out["busy"][2] == {"MainThread"}, out["busy"][2]
     assert torch.equal(out["busy"][0], out["quiet"][0])
+
+
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_gpu_parameter_store_single_worker_matches_tcp_ps(gpu, tmp_path):
+    """--ps_device gpu (variables in one GPU-resident store, pull / apply / global_step on the
+    device): with one worker, async PS is plain SGD, so the run tracks the TCP parameter
+    server's run step for step; restore-or-init and the TF-layout checkpoint work through the
+    GPU store."""
+    from distributedtensorflowexample_amd.cluster import Server
+    from distributedtensorflowexample_amd.data.mnist import read_data_sets
+    from distributedtensorflowexample_amd.train.saver import latest_checkpoint, load_checkpoint
+    from distributedtensorflowexample_amd.train.worker import Worker
+
+    hists = {}
+    for dev in ("cpu", "gpu"):
+        port = _free_port()
+        spec = {"ps": ["127.0.0.1:%d" % port], "worker": ["127.0.0.1:1"]}
+        ps = Server(spec, "ps", 0)
+        try:
+            fl = _flags(tmp_path / dev, ps_device=dev, num_workers=1, training_steps=150,
+                        eval_every=10 ** 9, save_model_secs=0.2)
+            w = Worker("worker", 0, Server(spec, "worker", 0), fl, device="cuda",
+                       log=lambda *_: None)
+            assert w.gpu_ps == (dev == "gpu")
+            hists[dev] = w.learn(read_data_sets(seed=0))
+        finally:
+            ps.stop()
+    hc, hg = hists["cpu"], hists["gpu"]
+    assert [h[0] for h in hg] == [h[0] for h in hc] == list(range(151))
+    for (_, lc, ac), (_, lg, ag) in zip(hc, hg):
+        assert abs(lc - lg) < 1e-3 * max(1.0, abs(lc))
+    # checkpoint round trip through the GPU store (TF names / layouts), restore, readiness
+    import torch
+
+    port = _free_port()
+    spec = {"ps": ["127.0.0.1:%d" % port], "worker": ["127.0.0.1:1"]}
+    ps = Server(spec, "ps", 0)
+    try:
+        fl = _flags(tmp_path / "ck", ps_device="gpu", num_workers=1)
+        w = Worker("worker", 0, Server(spec, "worker", 0), fl, device="cuda",
+                   log=lambda *_: None)
+        w.store.create()
+        assert len(w.store.uninitialized()) == 5
+        w.init_op()
+        assert w.store.uninitialized() == []
+        w.store.fetch_add("global/global_step", 7)
+        prefix = w.saver.save(None, str(tmp_path / "ck" / "model.ckpt"),
+                              global_step=w.store.read_int("global/global_step"),
+                              variables=w.store.read_all())
+        assert latest_checkpoint(str(tmp_path / "ck")) == prefix
+        v = {k: torch.as_tensor(t) for k, t in load_checkpoint(prefix).items()}
+        assert tuple(v["global/dense/kernel"].shape) == (784, 100)
+        assert int(v["global/global_step"]) == 7
+        v2 = {k: (t * 2 if k != "global/global_step" else t + 5) for k, t in v.items()}
+        w.store.assign(v2)
+        back = w.store.read_all()
+        for k in v:
+            assert torch.equal(torch.as_tensor(back[k]).to(v2[k].dtype), v2[k]), k
+        w.store.close()
+    finally:
+        ps.stop()
+
+
+def _gpu_ps_worker(task, port, logdir, q):
+    import torch
+
+    from distributedtensorflowexample_amd.cluster import Server
+    from distributedtensorflowexample_amd.data.mnist import read_data_sets
+    from distributedtensorflowexample_amd.train.worker import Worker
+
+    try:
+        torch.cuda.set_device(0)
+        spec = {"ps": ["127.0.0.1:%d" % port], "worker": ["127.0.0.1:1", "127.0.0.1:2"]}
+        import pathlib
+
+        fl = _flags(pathlib.Path(logdir), ps_device="gpu", num_workers=2, training_steps=400,
+                    eval_every=10 ** 9, learning_rate=0.05)
+        w = Worker("worker", task, Server(spec, "worker", task), fl, device="cuda",
+                   log=lambda *_: None)
+        h = w.learn(read_data_sets(seed=task))
+        q.put((task, len(h), h[0][1], h[-1][1], h[-1][0], None))
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        q.put((task, 0, 0.0, 0.0, 0, repr(e)))
+
+
+def test_gpu_parameter_store_two_worker_processes(gpu, tmp_path):
+    """Chief + one more worker process (sharing the GPU, as run_single_gpu.sh does) train
+    asynchronously through the chief's GPU-resident store: both map it, global_step is shared
+    (each step's fetch_add returns a distinct old value), the loss falls, and the chief frees
+    the store only after the other worker detached."""
+    import multiprocessing as mp
+
+    from distributedtensorflowexample_amd.cluster import Server
+
+    port = _free_port()
+    ps = Server({"ps": ["127.0.0.1:%d" % port], "worker": ["127.0.0.1:1", "127.0.0.1:2"]},
+                "ps", 0)
+    try:
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        procs = [ctx.Process(target=_gpu_ps_worker, args=(t, port, str(tmp_path), q))
+                 for t in (0, 1)]
+        for p in procs:
+            p.start()
+        res = sorted(q.get(timeout=180) for _ in procs)
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        ps.stop()
+    for task, n, l0, l1, last, err in res:
+        assert err is None, err
+        assert n > 0 and l1 < l0, (task, n, l0, l1)
+    assert sum(r[1] for r in res) >= 400 - 2  # the shared global_step reached training_steps
+    assert max(r[4] for r in res) >= 399

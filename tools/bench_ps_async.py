@@ -7,6 +7,7 @@ reports cluster samples/sec = speed (global steps/sec, worker.py:144-146)
 x batch_size -- exactly what the reference prints.
 
     python tools/bench_ps_async.py --num_workers 2 --steps 20000
+    python tools/bench_ps_async.py --num_workers 2 --steps 20000 --ps_device gpu
 """
 import argparse
 import glob
@@ -30,6 +31,9 @@ def main():
     ap.add_argument("--log_every", type=int, default=1000)
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--base_port", type=int, default=24222)
+    ap.add_argument("--ps_device", choices=["cpu", "gpu"], default="cpu",
+                    help="cpu: the reference's TCP parameter server; gpu: variables in the "
+                         "chief's GPU-resident store (parallel/gpu_ps.py)")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp(prefix="psbench")
     rc = launch_ps(a.num_workers, a.num_gpus, None, 1, cpu=a.cpu, base_port=a.base_port,
@@ -37,7 +41,7 @@ def main():
                    extra=["--training_steps", str(a.steps), "--log_every", str(a.log_every),
                           "--eval_every", str(10 ** 9), "--logdir", os.path.join(tmp, "m"),
                           "--save_model_secs", "1e9", "--save_summaries_secs", "1e9",
-                          "--batch_size", str(a.batch_size)])
+                          "--batch_size", str(a.batch_size), "--ps_device", a.ps_device])
     speeds = []
     for p in glob.glob(os.path.join(tmp, "logs", "worker*.log")):
         for m in re.finditer(r"step: (\d+)\t\| cost: [^|]+\| speed: ([0-9.eE+-]+)step/sec",
@@ -52,6 +56,7 @@ def main():
                       "value": round(sps * a.batch_size, 1), "unit": "samples/sec",
                       "global_steps_per_sec": round(sps, 1), "num_workers": a.num_workers,
                       "num_gpus": a.num_gpus, "device": "cpu" if a.cpu else "MI355X",
+                      "ps_device": a.ps_device,
                       "steps": a.steps, "rc": rc, "n_speed_samples": len(speeds)}))
     return 0
 
