@@ -142,16 +142,27 @@ class Worker:
 
     def compute_device(self, batch_x, batch_y):
         """Local forward/backward with the gradient left in ``self.grad`` on the device (GPU
-        parameter store: nothing crosses to the host but the loss / accuracy record)."""
+        parameter store: nothing crosses to the host but the loss / accuracy record).  The
+        batch goes through pinned staging buffers (asynchronous H2D), and the record's ring
+        slot comes from a host mirror of the kernel's step counter (no read-back)."""
+        if not hasattr(self, "_xs"):
+            self._xs = torch.empty(self.batch_size, D, pin_memory=True)
+            self._ys = torch.empty(self.batch_size, dtype=torch.int32, pin_memory=True)
+            self._rec = self.ws.global_step()
         y = np.asarray(batch_y)
         labels = y.argmax(1) if y.ndim == 2 else y
-        self.xb.copy_(torch.from_numpy(np.ascontiguousarray(batch_x, np.float32)))
-        self.yb.copy_(torch.from_numpy(labels.astype(np.int32)))
+        torch.cuda.current_stream(self.device).synchronize()  # staging free (previous copy)
+        self._xs.numpy()[...] = batch_x
+        self._ys.numpy()[...] = labels
+        self.xb.copy_(self._xs, non_blocking=True)
+        self.yb.copy_(self._ys, non_blocking=True)
         mlp_step.step_grad(self.params, self.xb, self.yb, self.ws, self.grad)
+        self._rec_slot = self._rec % self.ws.stats_ring
+        self._rec += 1
 
     def step_record(self):
         """(loss, accuracy) the last compute_device step recorded on the device."""
-        loss, acc = self.ws.stats[(self.ws.global_step() - 1) % self.ws.stats_ring].tolist()
+        loss, acc = self.ws.stats[self._rec_slot].tolist()
         return float(loss), float(acc)
 
     def accuracy(self, images, labels):

@@ -192,7 +192,9 @@ def _gpu_ps_worker(task, port, logdir, q):
         w = Worker("worker", task, Server(spec, "worker", task), fl, device="cuda",
                    log=lambda *_: None)
         h = w.learn(read_data_sets(seed=task))
-        q.put((task, len(h), h[0][1], h[-1][1], h[-1][0], None))
+        first = sum(c for _, c, _ in h[:10]) / len(h[:10])
+        last = sum(c for _, c, _ in h[-10:]) / len(h[-10:])
+        q.put((task, len(h), first, last, h[-1][0], None))
     except Exception as e:  # noqa: BLE001 - reported to the parent
         q.put((task, 0, 0.0, 0.0, 0, repr(e)))
 
