@@ -175,6 +175,13 @@ class Worker:
 
     # -- training loop (worker.py:105-159) ------------------------------------
     def learn(self, dataset, max_steps=None, stop_after_secs=None):
+        try:
+            return self._learn(dataset, max_steps, stop_after_secs)
+        finally:
+            if self.gpu_ps:  # also on an exception: peers must not outlive the owner's store
+                self.store.close()  # the chief frees it once every other worker detached
+
+    def _learn(self, dataset, max_steps=None, stop_after_secs=None):
         fl = self.flags
         sv = Supervisor(is_chief=self.is_chief, logdir=fl.logdir, saver=self.saver,
                         summary_writer=self.summary_writer, ready_op=self.store.uninitialized,
@@ -262,6 +269,4 @@ class Worker:
                     break
                 if stop_after_secs is not None and time.time() - t_begin > stop_after_secs:
                     break
-        if self.gpu_ps:
-            self.store.close()  # the chief frees the store once every other worker detached
         return history
