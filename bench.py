@@ -119,8 +119,9 @@ def main():
                          "replays, host = the C++ host loop launching both kernels of every "
                          "step (no graph-submission latency), persistent = ALL K steps in one "
                          "launch of the persistent kernel (workgroups hand data to each other "
-                         "as epoch-tagged granules), auto = time the candidates on min(K, 2000) "
-                         "steps before the timed region and use the fastest")
+                         "as epoch-tagged granules; measured slower, explicit only), auto = "
+                         "time graph / host on min(K, 2000) steps before the timed region and "
+                         "use the faster")
     ap.add_argument("--comm", choices=["auto", "native", "xgmi", "torch"], default="auto",
                     help="native: the framework's C++ RCCL communicator (gloo control plane); "
                          "xgmi: one-shot peer-memory all-reduce over xGMI (small buckets); "
@@ -260,10 +261,12 @@ def main():
     a.launch_probe = None
     if a.launch == "persistent" and not tr.persistent_ok:
         sys.exit("--launch persistent: single GPU, batch <= 128 only")
+    # The persistent engine (--launch persistent) is not an auto candidate: it measured
+    # 9.0-9.2 us/step against the graph's 8.2 on every box (profiles/r2/persistent/), so
+    # probing it would only lengthen the startup.
     cands = []
     if use_graph and tr.host_loop_ok and a.launch == "auto":
-        cands = ["graph"] + (["host"] if a.steps <= 200 else []) + (
-            ["persistent"] if tr.persistent_ok else [])
+        cands = ["graph"] + (["host"] if a.steps <= 200 else [])
     if a.launch == "host" and tr.host_loop_ok:
         launch = "host"
     if a.launch == "persistent":
