@@ -386,3 +386,34 @@ def test_persistent_trainer_error_word_drains_and_raises(gpu):
     assert time.perf_counter() - t0 < 10.0
     with pytest.raises(RuntimeError):
         tr.check()
+
+
+@pytest.mark.parametrize("locking", [False, True])
+def test_gpu_param_store_kernels(gpu, locking):
+    """GPU parameter store primitives (csrc/kernels/gpu_ps.*) against a float64 reference:
+    pull into a local replica, ApplyGradientDescent (plain lock-free RMW, or f32 atomics with
+    use_locking), global_step fetch-add returning the old value, host read / write."""
+    from distributedtensorflowexample_amd.ops._ext import hip, stream_handle
+
+    n = mlp_step.NPARAM
+    st = hip().GpuParamStore(gpu.index or 0, n, True)
+    try:
+        p0 = _rand(n, dev="cpu", seed=11)
+        g = _rand(n, dev=gpu, seed=12)
+        st.write(p0.data_ptr(), 0, n * 4)
+        s = stream_handle(gpu)
+        for _ in range(3):
+            st.push_apply(g.data_ptr(), 0.25, locking, s)
+        local = torch.zeros(n, device=gpu)
+        st.pull(local.data_ptr(), s)
+        torch.cuda.synchronize()
+        ref = p0.double() - 3 * 0.25 * g.double().cpu()
+        assert (local.double().cpu() - ref).abs().max().item() < 1e-5
+        back = torch.empty(n)
+        st.read(back.data_ptr(), 0, n * 4)
+        assert torch.equal(back, local.cpu())
+        assert st.fetch_add(0, 1, s) == 0
+        assert st.fetch_add(0, 5, s) == 1
+        assert st.fetch_add(0, 0, s) == 6
+    finally:
+        st.close()
