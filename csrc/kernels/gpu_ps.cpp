@@ -23,7 +23,8 @@ namespace dtfx {
 
 void gps_pull_launch(float*, const float*, long long, hipStream_t);
 void gps_apply_launch(float*, const float*, float, long long, bool, hipStream_t);
-void gps_fetch_add_launch(unsigned long long*, long long, unsigned long long*, hipStream_t);
+void gps_fetch_add_launch(unsigned long long*, long long, unsigned long long*, const float*, int,
+                          hipStream_t);
 
 class GpuParamStore {
  public:
@@ -40,8 +41,8 @@ class GpuParamStore {
       GPS_CHECK(hipExtMallocWithFlags(&base_, bytes_, hipDeviceMallocUncached));
       GPS_CHECK(hipMemset(base_, 0, bytes_));
     }
-    GPS_CHECK(hipHostMalloc(&host_word_, 8, hipHostMallocDefault));
-    GPS_CHECK(hipMalloc(&dev_word_, 8));
+    GPS_CHECK(hipHostMalloc(&host_word_, 64, hipHostMallocDefault));
+    GPS_CHECK(hipMalloc(&dev_word_, 64));
   }
   ~GpuParamStore() { close(); }
 
@@ -78,14 +79,18 @@ class GpuParamStore {
 
   // control word `slot` += delta on the device (system-scope atomic); returns the old value
   long long fetch_add(int slot, long long delta, uintptr_t stream) {
-    if (slot < 0 || slot >= kCtrlWords) throw std::runtime_error("gpu_ps: bad control slot");
-    py::gil_scoped_release nogil;
-    std::lock_guard<std::mutex> lock(mu_);  // one staging word: the saver thread calls too
-    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    gps_fetch_add_launch(ctrl() + slot, delta, dev_word_, s);
-    GPS_CHECK(hipMemcpyAsync(host_word_, dev_word_, 8, hipMemcpyDeviceToHost, s));
-    GPS_CHECK(hipStreamSynchronize(s));
-    return (long long)*host_word_;
+    return fetch_add_impl(slot, delta, stream, 0, 0, nullptr);
+  }
+
+  // the same, also reading back `nextra` (<= 14) f32 words at device address `extra` in the
+  // same copy: (old value, [floats])
+  py::tuple fetch_add_read(int slot, long long delta, uintptr_t stream, uintptr_t extra,
+                           int nextra) {
+    float vals[14];
+    const long long old = fetch_add_impl(slot, delta, stream, extra, nextra, vals);
+    py::list l;
+    for (int i = 0; i < nextra; ++i) l.append(vals[i]);
+    return py::make_tuple(old, l);
   }
 
   // synchronous host <-> store copies (init / restore / checkpoint); offsets in bytes
@@ -124,6 +129,21 @@ class GpuParamStore {
   }
 
  private:
+  long long fetch_add_impl(int slot, long long delta, uintptr_t stream, uintptr_t extra,
+                           int nextra, float* vals) {
+    if (slot < 0 || slot >= kCtrlWords) throw std::runtime_error("gpu_ps: bad control slot");
+    if (nextra < 0 || nextra > 14) throw std::runtime_error("gpu_ps: at most 14 extra words");
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> lock(mu_);  // one staging buffer: the saver thread calls too
+    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    gps_fetch_add_launch(ctrl() + slot, delta, dev_word_, reinterpret_cast<const float*>(extra),
+                         nextra, s);
+    GPS_CHECK(hipMemcpyAsync(host_word_, dev_word_, 8 + 4 * nextra, hipMemcpyDeviceToHost, s));
+    GPS_CHECK(hipStreamSynchronize(s));
+    if (vals) std::memcpy(vals, host_word_ + 1, 4 * nextra);
+    return (long long)*host_word_;
+  }
+
   void* base() const {
     if (!base_) throw std::runtime_error("gpu_ps: store not allocated / opened");
     return base_;
@@ -161,6 +181,8 @@ void register_gpu_ps(py::module_& m) {
            py::arg("locking"), py::arg("stream"))
       .def("fetch_add", &dtfx::GpuParamStore::fetch_add, py::arg("slot"), py::arg("delta"),
            py::arg("stream"))
+      .def("fetch_add_read", &dtfx::GpuParamStore::fetch_add_read, py::arg("slot"),
+           py::arg("delta"), py::arg("stream"), py::arg("extra"), py::arg("nextra"))
       .def("read", &dtfx::GpuParamStore::read)
       .def("write", &dtfx::GpuParamStore::write)
       .def("ctrl_offset", &dtfx::GpuParamStore::ctrl_offset)

@@ -53,11 +53,15 @@ __global__ __launch_bounds__(256) void gps_apply_kernel(float* __restrict__ p,
   }
 }
 
+// out[0] = old counter value; out[1 ..] = `nextra` f32 words copied from `extra` (the
+// worker's loss / accuracy record of the step), so one read-back serves both
 __global__ void gps_fetch_add_kernel(unsigned long long* ctr, long long delta,
-                                     unsigned long long* out) {
+                                     unsigned long long* out, const float* extra, int nextra) {
   if (threadIdx.x == 0)
     *out = __hip_atomic_fetch_add(ctr, (unsigned long long)delta, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_SYSTEM);
+  if ((int)threadIdx.x < nextra)
+    reinterpret_cast<float*>(out + 1)[threadIdx.x] = extra[threadIdx.x];
 }
 
 }  // namespace gps
@@ -85,8 +89,10 @@ void gps_apply_launch(float* p, const float* g, float lr, long long n, bool lock
 }
 
 void gps_fetch_add_launch(unsigned long long* ctr, long long delta, unsigned long long* out,
-                          hipStream_t s) {
-  hipLaunchKernelGGL(gps::gps_fetch_add_kernel, dim3(1), dim3(64), 0, s, ctr, delta, out);
+                          const float* extra, int nextra, hipStream_t s) {
+  if (nextra < 0 || nextra > 14) throw std::runtime_error("gpu_ps: at most 14 extra words");
+  hipLaunchKernelGGL(gps::gps_fetch_add_kernel, dim3(1), dim3(64), 0, s, ctr, delta, out, extra,
+                     nextra);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

@@ -155,6 +155,13 @@ class GpuPSStore:
             raise KeyError(name)
         return self._ctrl(STEP_SLOT, delta)
 
+    def fetch_add_record(self, record, delta=1):
+        """global_step fetch-add that also reads back ``record`` (a small f32 device tensor:
+        the step's loss / accuracy) in the same copy -- one host round trip per step."""
+        old, vals = self._st.fetch_add_read(STEP_SLOT, int(delta), stream_handle(self.device),
+                                            record.data_ptr(), record.numel())
+        return int(old), vals
+
     def read_int(self, name):
         return self.fetch_add(name, 0)
 

@@ -221,8 +221,9 @@ class Worker:
                     self.compute_device(batch_x, batch_y)
                     self.store.push_apply_flat(self.grad, self.lr,
                                                bool(getattr(fl, "use_locking", False)))
-                    step = self.store.fetch_add("global/global_step", 1)
-                    cost, acc = self.step_record()
+                    # counter_op + the step's loss / accuracy record: one read-back
+                    step, (cost, acc) = self.store.fetch_add_record(
+                        self.ws.stats[self._rec_slot])
                     self.summary_writer.add_scalars({"loss": cost, "accuracy": acc}, step)
                     history.append((step, cost, acc))
                     local_steps += 1

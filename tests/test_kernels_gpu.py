@@ -415,5 +415,8 @@ def test_gpu_param_store_kernels(gpu, locking):
         assert st.fetch_add(0, 1, s) == 0
         assert st.fetch_add(0, 5, s) == 1
         assert st.fetch_add(0, 0, s) == 6
+        rec = torch.tensor([1.5, 0.25], device=gpu)
+        old, vals = st.fetch_add_read(0, 1, s, rec.data_ptr(), 2)
+        assert old == 6 and vals == [1.5, 0.25] and st.fetch_add(0, 0, s) == 7
     finally:
         st.close()
