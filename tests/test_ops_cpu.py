@@ -67,3 +67,26 @@ def test_init_cpu_distributions():
     assert t.abs().max() <= 2.0
     init.fill_(t, "uniform", 2.0, 3.0, seed=2)
     assert 2.0 <= t.min() and t.max() < 3.0
+
+
+def test_gpu_store_layout_round_trip():
+    """The GPU parameter store keeps the fused kernels' flat layout (W stored [out, in]); its
+    TF-layout boundary (assign / pull / read_all) round-trips every variable exactly."""
+    import torch
+
+    from distributedtensorflowexample_amd.ops import mlp_step
+    from distributedtensorflowexample_amd.parallel.gpu_ps import _flat_from_tf, _tf_from_flat
+
+    g = torch.Generator().manual_seed(3)
+    tf = {"global/dense/kernel": torch.randn(784, 100, generator=g),
+          "global/dense/bias": torch.randn(100, generator=g),
+          "global/dense_1/kernel": torch.randn(100, 10, generator=g),
+          "global/dense_1/bias": torch.randn(10, generator=g)}
+    flat = _flat_from_tf(tf, torch.zeros(mlp_step.NPARAM))
+    W1t, _, W2t, _ = mlp_step.unflatten(flat)
+    assert torch.equal(W1t, tf["global/dense/kernel"].t())
+    assert torch.equal(W2t, tf["global/dense_1/kernel"].t())
+    back = _tf_from_flat(flat)
+    for k, v in tf.items():
+        assert torch.equal(back[k], v), k
+        assert back[k].is_contiguous()
