@@ -81,16 +81,6 @@ constexpr long long OFF_SP = OFF_HEAD + 2 * HEAD_PAR;
 constexpr long long OFF_ERR = OFF_SP + 2 * SP_PAR;
 constexpr long long LL_WORDS = OFF_ERR + 32;
 constexpr int TRACE_STEPS = 64;
-// representative word polled before the full load of a wait (-1: poll every word at once)
-#ifndef DTFX_REP_HEAD
-#define DTFX_REP_HEAD -1
-#endif
-#ifndef DTFX_REP_SMALL
-#define DTFX_REP_SMALL -1
-#endif
-#ifndef DTFX_REP_W1
-#define DTFX_REP_W1 -1
-#endif
 
 static_assert(NPARAM == 79510, "parameter count of worker.py:50-53");
 static_assert(KS * KW == D && HDL + 16 <= HST && HST + 2 <= HEAD_ROW, "layout");
@@ -133,15 +123,13 @@ __device__ __forceinline__ float4 f4(const float* p) {
   return *reinterpret_cast<const float4*>(p);
 }
 
-// Waits until every word addr(i) (nullptr = absent: value 0) carries epoch e.  While the
-// producers have not written yet, only ONE representative word addr(rep) is polled (one load
-// per poll round instead of N: a hundred waves each re-polling 60 stale words per round
-// flooded the memory system the producers' stores go through); then every word is loaded
-// together and only stale ones are re-polled.  On timeout or a raised error word, sets `fail`
-// (and the error word) and returns zeros.
+// Waits until every word addr(i) (nullptr = absent: value 0) carries epoch e: every word is
+// loaded together and only stale ones are re-polled (polling one representative word first
+// measured slower: it adds a round trip once the data lands, profiles/r2/persistent/).  On
+// timeout or a raised error word, sets `fail` (and the error word) and returns zeros.
 template <int N, class Addr>
-__device__ __forceinline__ void ll_wait(Addr addr, int rep, unsigned e, const Args& a,
-                                        float (&out)[N], bool& fail) {
+__device__ __forceinline__ void ll_wait(Addr addr, unsigned e, const Args& a, float (&out)[N],
+                                        bool& fail) {
   u64 w[N];
   const u64 ready_word = (u64)e << 32;
   long long t0 = -1;
@@ -156,15 +144,6 @@ __device__ __forceinline__ void ll_wait(Addr addr, int rep, unsigned e, const Ar
     }
     return false;
   };
-  if (!fail && rep >= 0) {
-    const u64* pr = addr(rep);
-    if (pr) {
-      for (int it = 1; (unsigned)(ld_ll(pr) >> 32) != e; ++it) {
-        if (expired(it)) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-  }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const u64* p = addr(i);
@@ -222,7 +201,7 @@ __device__ __forceinline__ void head_row(const Args& a, int row, int t, int wave
         if (i == 12) return jv ? sp + j : nullptr;
         return sp + SP_B2 + (i - 13);
       },
-      DTFX_REP_HEAD, e, a, v, fail);
+      e, a, v, fail);
   stamp(a, t, wave == 3 ? 6 : 8 + wave);
   float zp = 0.f;
 #pragma unroll
@@ -383,7 +362,7 @@ __global__ __launch_bounds__(256) void mlp_persistent_kernel(Args a) {
             if (i < 16) return hv_ok ? row + HHB + jt * 16 + r : nullptr;
             return hv_ok ? row + HDZ + jt * 16 + r : nullptr;
           },
-          DTFX_REP_SMALL, ep, a, v, fail);
+          ep, a, v, fail);
       if (wave == 0) stamp(a, t, 1);
       f32x4 p0 = {0, 0, 0, 0}, p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0};
 #pragma unroll
@@ -506,7 +485,7 @@ __global__ __launch_bounds__(256) void mlp_persistent_kernel(Args a) {
             const int b = (tid >> 4) + 16 * k;
             return b < B && jvalid ? hd + (size_t)b * HEAD_ROW + jl : nullptr;
           },
-          DTFX_REP_W1, ep, a, dz, fail);
+          ep, a, dz, fail);
       if (wave == 0) stamp(a, t, 1);
 #pragma unroll
       for (int k = 0; k < NL; ++k) Dz[jl][(tid >> 4) + 16 * k] = dz[k];
