@@ -26,7 +26,9 @@ namespace dtfx {
 
 class XgmiAllReduce {
  public:
-  XgmiAllReduce(int rank, int world, int device, long long max_numel, const std::string& protocol)
+  // own_slots = false: the slot regions are supplied by open_local() (test harness).
+  XgmiAllReduce(int rank, int world, int device, long long max_numel, const std::string& protocol,
+                bool own_slots = true)
       : rank_(rank), world_(world), device_(device), S_((max_numel + 63) / 64 * 64) {
     if (protocol == "flag") mode_ = -1;
     else if (protocol == "ll") mode_ = XG_LL_PULL;
@@ -43,8 +45,10 @@ class XgmiAllReduce {
     data_bytes_ = mode_ < 0 ? (long long)sizeof(float) * 2 * S_ : xgmi_ll_bytes(mode_, world, S_);
     bytes_ = data_bytes_ + sizeof(unsigned) * XG_MAX_WORLD * XG_BLOCKS;
     bytes_ = (bytes_ + (2u << 20) - 1) / (2u << 20) * (2u << 20);
-    XG_CHECK(hipExtMallocWithFlags(&base_, bytes_, hipDeviceMallocUncached));
-    XG_CHECK(hipMemset(base_, 0, bytes_));
+    if (own_slots) {
+      XG_CHECK(hipExtMallocWithFlags(&base_, bytes_, hipDeviceMallocUncached));
+      XG_CHECK(hipMemset(base_, 0, bytes_));
+    }
     XG_CHECK(hipMalloc(&epochs_, sizeof(unsigned) * XG_BLOCKS + sizeof(int)));
     XG_CHECK(hipMemset(epochs_, 0, sizeof(unsigned) * XG_BLOCKS + sizeof(int)));
     err_ = (int*)(epochs_ + XG_BLOCKS);
@@ -56,6 +60,24 @@ class XgmiAllReduce {
     }
   }
   ~XgmiAllReduce() { close(); }
+
+  size_t region_bytes() const { return bytes_; }
+  long long slot_stride() const { return S_; }
+
+  // Test harness ("peer buffers that are local allocations"): every rank's slot
+  // region is a caller-owned allocation of region_bytes() on THIS device, so one process can
+  // run any rank's kernels of any world size with the other ranks' words pre-staged.  The
+  // kernels and the layout are exactly those of open(); only the pointers' origin differs.
+  void open_local(const std::vector<uintptr_t>& regions) {
+    if ((int)regions.size() != world_) throw std::runtime_error("xgmi: need one region per rank");
+    if (base_) throw std::runtime_error("xgmi: open_local() is for communicators without slots");
+    for (int j = 0; j < world_; ++j) {
+      if (!regions[j] || (regions[j] & 255)) throw std::runtime_error("xgmi: region must be 256-B aligned");
+      peers_.data[j] = (float*)regions[j];
+      peers_.flags[j] = (unsigned*)((char*)regions[j] + data_bytes_);
+    }
+    ready_ = true;
+  }
 
   py::bytes handle() {
     hipIpcMemHandle_t h;
@@ -208,6 +230,12 @@ void register_xgmi(py::module_& m) {
       .def(py::init<int, int, int, long long, const std::string&>(), py::arg("rank"),
            py::arg("world"), py::arg("device"), py::arg("max_numel"),
            py::arg("protocol") = "ll")
+      .def(py::init<int, int, int, long long, const std::string&, bool>(), py::arg("rank"),
+           py::arg("world"), py::arg("device"), py::arg("max_numel"), py::arg("protocol"),
+           py::arg("own_slots"))
+      .def("region_bytes", &dtfx::XgmiAllReduce::region_bytes)
+      .def("slot_stride", &dtfx::XgmiAllReduce::slot_stride)
+      .def("open_local", &dtfx::XgmiAllReduce::open_local)
       .def("handle", &dtfx::XgmiAllReduce::handle)
       .def("open", &dtfx::XgmiAllReduce::open)
       .def("all_reduce", &dtfx::XgmiAllReduce::all_reduce, py::arg("g"), py::arg("n"),

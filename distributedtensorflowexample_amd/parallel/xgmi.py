@@ -50,6 +50,40 @@ class XgmiComm:
             raise RuntimeError("xgmi: ranks %s could not export their buffers" % missing)
         self._h.open(handles)
 
+    @classmethod
+    def with_local_peers(cls, rank, world_size, max_numel, regions=None, device=None,
+                         protocol="push", timeout_s=2.0):
+        """Test harness ("peer buffers that are local allocations"): a communicator
+        for ``rank`` of a ``world_size``-rank job whose peer slot regions are plain allocations
+        on this device -- ``regions`` (one int64 tensor per rank, ``region_words`` long) or new
+        zeroed ones.  The kernels and the slot layout are those of a real communicator; one
+        process can therefore run ANY rank's kernels of ANY world size, with the other ranks'
+        words staged into the regions by the caller.  Returns (comm, regions)."""
+        self = cls.__new__(cls)
+        self.rank, self.world_size = int(rank), int(world_size)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None
+                                   else torch.device(device).index)
+        self.timeout_s = float(timeout_s)
+        self.max_numel = int(max_numel)
+        self.protocol = protocol
+        self._h = hip().XgmiAllReduce(self.rank, self.world_size, self.device.index,
+                                      self.max_numel, protocol, False)
+        words = self._h.region_bytes() // 8
+        if regions is None:
+            regions = [torch.zeros(words, dtype=torch.int64, device=self.device)
+                       for _ in range(self.world_size)]
+        if len(regions) != self.world_size or any(
+                r.dtype != torch.int64 or r.numel() < words or not r.is_cuda for r in regions):
+            raise ValueError("need %d int64 device regions of >= %d words" % (world_size, words))
+        self._h.open_local([r.data_ptr() for r in regions])
+        self.regions = regions
+        return self, regions
+
+    @property
+    def slot_stride(self):
+        """Elements per slot (S): the stride of the LL slot layout (``docs/COMM.md``)."""
+        return self._h.slot_stride()
+
     def allreduce_sum_(self, t):
         if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
             raise ValueError("XgmiComm: contiguous f32 GPU tensors only")

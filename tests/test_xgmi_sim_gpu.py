@@ -1,0 +1,509 @@
+"""Every xGMI kernel instantiation for world 2..8 (and the flag protocol up to 16),
+executed on ONE GPU with simulated peers.
+
+SURVEY §4 ("peer buffers that are local allocations, so the kernel path is identical and
+only the pointer origin differs"): ``XgmiComm.with_local_peers`` builds the communicator of
+rank r of a W-rank job whose W slot regions are plain allocations on cuda:0.  Before each
+launch the test stages, into those regions, exactly the words the W-1 peers would have
+written for that round (value + epoch, in the slot of the epoch's parity); the launch then
+runs the real kernel of rank r (template instantiation XW = W) and must
+
+  * finish without a timed-out wait (every word it waits for is there),
+  * produce the rank-ordered sum / gathered factors / SGD update of a float64 reference
+    (exact where the kernel only sums staged f32 values in rank order), and
+  * leave in every peer's region exactly the words a real peer would receive.
+
+Two rounds per case cover both slot parities and the device-side epoch advance.  The
+rank-to-rank protocol itself (concurrent ranks racing on parities) is exercised by the
+multi-process tests in test_xgmi_gpu.py and the shared-GPU rehearsal (scripts/gpu_rehearsal.sh).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+WORLDS = [2, 3, 4, 5, 6, 7, 8]
+XG_BLOCKS = 256
+MASK32 = 0xFFFFFFFF
+
+
+def _words(v, epoch):
+    """{f32 value, u32 epoch} LL words (int64) of a float32 tensor."""
+    bits = v.contiguous().view(torch.int32).to(torch.int64) & MASK32
+    return bits | (int(epoch) << 32)
+
+
+def _vals(w):
+    return (w & MASK32).to(torch.int32).view(torch.float32)
+
+
+def _epochs(w):
+    return (w >> 32) & MASK32
+
+
+def _ordered_sum(vals):
+    """float32 sum in rank order starting from 0 -- what every kernel computes."""
+    acc = torch.zeros_like(vals[0])
+    for v in vals:
+        acc = acc + v
+    return acc
+
+
+def _ranks(world):
+    return sorted({0, world // 2, world - 1})
+
+
+# ---------------------------------------------------------------------------------------
+# stand-alone all-reduce: LL pull / push / push2 and the flag protocol
+# ---------------------------------------------------------------------------------------
+def _stage_and_check_allreduce(proto, world, rank, n, dev):
+    from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+    comm, regs = XgmiComm.with_local_peers(rank, world, n, device=dev, protocol=proto)
+    S = comm.slot_stride
+    g = torch.Generator().manual_seed(100 * world + rank)
+    for epoch in (1, 2):  # parity 1 then 0
+        par = epoch & 1
+        vals = [torch.randn(n, generator=g) * (j + 1) for j in range(world)]
+        exp = _ordered_sum(vals)
+        vd = [v.to(dev) for v in vals]
+        if proto == "ll":  # each rank publishes into its OWN [2][S] slot; readers pull
+            for j in range(world):
+                if j != rank:
+                    regs[j][par * S:par * S + n] = _words(vd[j], epoch)
+        elif proto == "push":  # slot(dst, src) = [(par * W + src) * S]
+            for j in range(world):
+                if j != rank:
+                    o = (par * world + j) * S
+                    regs[rank][o:o + n] = _words(vd[j], epoch)
+        elif proto == "push2":
+            shard = (n + world - 1) // world
+            s0, s1 = rank * shard, min(n, (rank + 1) * shard)
+            for j in range(world):  # reduce-scatter: peers' shares of MY shard
+                if j != rank:
+                    o = (par * world + j) * S
+                    regs[rank][o + s0:o + s1] = _words(vd[j][s0:s1], epoch)
+            res = (2 * world + par) * S  # all-gather: owners' sums of THEIR shards
+            full = _words(exp.to(dev), epoch)
+            regs[rank][res:res + n] = full
+        else:  # flag: f32 slots [2][S] + flags [W][XG_BLOCKS] per rank
+            for j in range(world):
+                if j != rank:
+                    regs[j].view(torch.float32)[par * S:par * S + n] = vd[j]
+                    fl = regs[rank].view(torch.int32)[2 * S + j * XG_BLOCKS:
+                                                      2 * S + (j + 1) * XG_BLOCKS]
+                    fl.fill_(epoch)
+        t = vd[rank].clone()
+        torch.cuda.synchronize()
+        comm.allreduce_sum_(t)
+        comm.check()
+        assert torch.equal(t.cpu(), exp), (proto, world, rank, epoch,
+                                           float((t.cpu() - exp).abs().max()))
+        # float64 sanity of the same sum
+        ref = torch.stack([v.double() for v in vals]).sum(0)
+        assert float((t.cpu().double() - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
+        # what the peers received
+        mine = _words(vd[rank], epoch)
+        if proto == "ll":
+            assert torch.equal(regs[rank][par * S:par * S + n], mine)
+        elif proto == "push":
+            for j in range(world):
+                if j != rank:
+                    o = (par * world + rank) * S
+                    assert torch.equal(regs[j][o:o + n], mine), (j, epoch)
+        elif proto == "push2":
+            shard = (n + world - 1) // world
+            for o_rank in range(world):
+                if o_rank == rank:
+                    continue
+                a0, a1 = o_rank * shard, min(n, (o_rank + 1) * shard)
+                o = (par * world + rank) * S
+                assert torch.equal(regs[o_rank][o + a0:o + a1], mine[a0:a1]), (o_rank, epoch)
+                s0, s1 = rank * shard, min(n, (rank + 1) * shard)
+                res = (2 * world + par) * S
+                assert torch.equal(regs[o_rank][res + s0:res + s1],
+                                   _words(exp[s0:s1].to(dev), epoch)), (o_rank, epoch)
+        else:
+            assert torch.equal(regs[rank].view(torch.float32)[par * S:par * S + n], vd[rank])
+            for j in range(world):
+                f = regs[j].view(torch.int32)[2 * S + rank * XG_BLOCKS:
+                                              2 * S + (rank + 1) * XG_BLOCKS]
+                assert bool((f == epoch).all()), (j, epoch)
+    comm.destroy()
+
+
+@pytest.mark.parametrize("world", WORLDS)
+@pytest.mark.parametrize("proto", ["ll", "push", "push2"])
+def test_ll_allreduce_simulated_peers(gpu, proto, world):
+    for rank in _ranks(world):
+        for n in (79510, 1021):  # the MLP gradient; a size that is not a multiple of W or 4
+            _stage_and_check_allreduce(proto, world, rank, n, gpu)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5, 8, 12, 16])
+def test_flag_allreduce_simulated_peers(gpu, world):
+    for rank in _ranks(world):
+        _stage_and_check_allreduce("flag", world, rank, 79510, gpu)
+        _stage_and_check_allreduce("flag", world, rank, 1021, gpu)
+
+
+# ---------------------------------------------------------------------------------------
+# MLP data-parallel engines: fused (3-launch), fused2 (pipelined), factor, factor2
+# ---------------------------------------------------------------------------------------
+def _setup(dev, B, seed):
+    from distributedtensorflowexample_amd.data.synthetic import mnist_like_device
+    from distributedtensorflowexample_amd.models.mlp import init_params
+    from distributedtensorflowexample_amd.ops import mlp_step
+
+    p = init_params(dev, seed=seed, stddev=0.3)
+    x, y = mnist_like_device(B, seed=seed + 1, device=dev)
+    ws = mlp_step.StepWorkspace(B, dev)
+    return p, x, y, ws
+
+
+def _ws_views(ws):
+    from distributedtensorflowexample_amd.ops import mlp_step
+
+    B = ws.B
+    BP = (B + 15) // 16 * 16
+    HP = mlp_step.HP
+    o = 14 * BP * HP
+    hbuf = ws.buf[o:o + BP * HP].view(BP, HP)
+    o += BP * HP
+    dz1T = ws.buf[o:o + HP * BP].view(HP, BP)
+    return hbuf, dz1T, BP
+
+
+def _plain_fwd_head(p, x, y, ws):
+    """3-launch layout: K1 (7 slabs) + plain head -> factors of (p, x) in ws."""
+    from distributedtensorflowexample_amd.ops._ext import hip, ptr, stream_handle
+
+    h, s = hip(), stream_handle()
+    h.mlp_fwd(ptr(p), 0, 0.0, 0, ptr(x), ptr(ws.buf), ws.B, s)
+    h.mlp_head(ptr(p), 0, 0.0, 0, ptr(y), ptr(ws.buf), ws.B, s)
+
+
+def _pipelined_fwd_head(p, x, y, ws):
+    """Pipelined layout (14 slabs): copy-only fwdapply + head2 -> factors of (p, x) in ws."""
+    from distributedtensorflowexample_amd.ops._ext import hip, ptr, stream_handle
+
+    h, s = hip(), stream_handle()
+    tmp = p.clone()
+    h.mlp_fwdapply(ptr(p), ptr(tmp), 0.0, ptr(x), ptr(x), ptr(ws.buf), ptr(ws.ctr), 0,
+                   ws.stats_ring, ws.B, 0, s)
+    h.mlp_head2(ptr(tmp), ptr(y), ptr(ws.buf), ws.B, s)
+
+
+def _ref_grad(p, x, y):
+    from distributedtensorflowexample_amd.ops import mlp_step
+
+    g, _, _ = mlp_step.reference_step(p.double().cpu(), x.double().cpu(), y.cpu())
+    return g
+
+
+def _ref_dz1(p, x, y):
+    from distributedtensorflowexample_amd.ops import mlp_step
+
+    pd, xd = p.double().cpu(), x.double().cpu()
+    W1t, b1, W2t, b2 = mlp_step.unflatten(pd)
+    h, logits = mlp_step.reference_forward(pd, xd)
+    prob = torch.softmax(logits, 1)
+    dl = (prob - torch.nn.functional.one_hot(y.cpu().long(), 10).double()) / x.shape[0]
+    return ((dl @ W2t) * h * (1 - h))  # [B, H]
+
+
+def _stage_param_words(comm, regs, peer_vals, epoch, lo, hi):
+    """Peers' LL words for parameter offsets [lo, hi) into MY push slots."""
+    S, W, r = comm.slot_stride, comm.world_size, comm.rank
+    par = epoch & 1
+    for q in range(W):
+        if q != r:
+            o = (par * W + q) * S
+            regs[r][o + lo:o + hi] = _words(peer_vals[q][lo:hi].to(regs[r].device), epoch)
+
+
+def _check_pushed(comm, regs, own_ref, epoch, lo, hi, tol):
+    """Every peer received MY words for [lo, hi) in slot (parity, me), with this epoch."""
+    S, W, r = comm.slot_stride, comm.world_size, comm.rank
+    par = epoch & 1
+    for j in range(W):
+        if j == r:
+            continue
+        o = (par * W + r) * S
+        w = regs[j][o + lo:o + hi].cpu()
+        assert bool((_epochs(w) == epoch).all()), ("epoch", j, epoch)
+        err = float((_vals(w).double() - own_ref[lo:hi]).abs().max())
+        assert err <= tol, ("pushed value", j, epoch, err)
+
+
+def _peer_grads(world, rank, seed, scale):
+    from distributedtensorflowexample_amd.ops import mlp_step
+
+    g = torch.Generator().manual_seed(seed)
+    return [None if q == rank else torch.randn(mlp_step.NPARAM, generator=g) * scale
+            for q in range(world)]
+
+
+def _expected_update(own, peers, rank):
+    tot = torch.zeros_like(own)
+    for q, v in enumerate(peers):
+        tot += own if q == rank else v.double()
+    return tot
+
+
+def _engine_cases():
+    cases = [(w, w - 1, 100) for w in WORLDS]
+    cases += [(w, 0, 100) for w in (3, 8)]
+    cases += [(w, w // 2, 64) for w in (2, 5, 8)]  # generic (NGT = 0) instantiations
+    return cases
+
+
+@pytest.mark.parametrize("world,rank,B", _engine_cases())
+def test_fused_wgrad_exchange_simulated_peers(gpu, world, rank, B):
+    """mlp_wgrad_kernel<.., XW>: 3-launch fused engine (exchange in the wgrad epilogue)."""
+    from distributedtensorflowexample_amd.ops import mlp_step
+    from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+    p, x, y, ws = _setup(gpu, B, 10 * world + rank)
+    comm, regs = XgmiComm.with_local_peers(rank, world, mlp_step.NPARAM, device=gpu)
+    _plain_fwd_head(p, x, y, ws)
+    own = _ref_grad(p, x, y)
+    lr = 0.5
+    cur = p.double().cpu()
+    for epoch in (1, 2):
+        peers = _peer_grads(world, rank, 7 * epoch + world, 0.05)
+        _stage_param_words(comm, regs, peers, epoch, 0, mlp_step.NPARAM)
+        torch.cuda.synchronize()
+        comm.mlp_wgrad(p, lr, x, ws)
+        comm.check()
+        cur = cur - lr * _expected_update(own, peers, rank)
+        err = float((p.double().cpu() - cur).abs().max())
+        assert err <= 2e-5, (epoch, err)
+        _check_pushed(comm, regs, own, epoch, 0, mlp_step.NPARAM, 2e-6)
+    assert ws.global_step() == 2
+    comm.destroy()
+
+
+@pytest.mark.parametrize("world,rank,B", _engine_cases())
+def test_fused2_fwdapply_exchange_simulated_peers(gpu, world, rank, B):
+    """mlp_fwdapply_kernel<NGT, XW>: pipelined fused engine (step t-1's exchange + apply fused
+    with step t's forward)."""
+    from distributedtensorflowexample_amd.data.synthetic import mnist_like_device
+    from distributedtensorflowexample_amd.ops import mlp_step
+    from distributedtensorflowexample_amd.ops._ext import hip, ptr, stream_handle
+    from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+    p_old, x_prev, y_prev, ws = _setup(gpu, B, 20 * world + rank)
+    x, y = mnist_like_device(B, seed=999 + rank, device=gpu)
+    comm, regs = XgmiComm.with_local_peers(rank, world, mlp_step.NPARAM, device=gpu)
+    lr = 0.5
+    bufs = [p_old, torch.empty_like(p_old)]
+    batches = [(x_prev, y_prev), (x, y)]
+    _pipelined_fwd_head(p_old, x_prev, y_prev, ws)
+    cur = 0
+    for epoch in (1, 2):
+        xp, yp = batches[(epoch - 1) % 2]
+        xn, yn = batches[epoch % 2]
+        po, pn = bufs[cur], bufs[cur ^ 1]
+        own = _ref_grad(po, xp, yp)
+        peers = _peer_grads(world, rank, 11 * epoch + world, 0.05)
+        _stage_param_words(comm, regs, peers, epoch, 0, mlp_step.NPARAM)
+        exp = po.double().cpu() - lr * _expected_update(own, peers, rank)
+        torch.cuda.synchronize()
+        comm.mlp_fwdapply(po, pn, lr, xp, xn, ws, True)
+        hip().mlp_head2(ptr(pn), ptr(yn), ptr(ws.buf), ws.B, stream_handle())
+        comm.check()
+        err = float((pn.double().cpu() - exp).abs().max())
+        assert err <= 2e-5, (epoch, err)
+        _check_pushed(comm, regs, own, epoch, 0, mlp_step.NPARAM, 2e-6)
+        # step t's forward ran on the UPDATED parameters
+        hbuf, _, _ = _ws_views(ws)
+        h_ref, _ = mlp_step.reference_forward(pn.double().cpu(), xn.double().cpu())
+        herr = float((hbuf[:B, :100].double().cpu() - h_ref).abs().max())
+        assert herr <= 1e-4, (epoch, herr)
+        cur ^= 1
+    assert ws.global_step() == 2
+    comm.destroy()
+
+
+@pytest.mark.parametrize("nslab", [7, 14])
+@pytest.mark.parametrize("world,rank,B", _engine_cases())
+def test_factor_head_allgather_simulated_peers(gpu, world, rank, B, nslab):
+    """mlp_head_kernel<.., XW, NSLAB>: all-gather of the backprop factors dz1 into dz1A."""
+    from distributedtensorflowexample_amd.ops import mlp_step
+    from distributedtensorflowexample_amd.ops._ext import hip, ptr, stream_handle
+    from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+    p, x, y, ws = _setup(gpu, B, 30 * world + rank)
+    comm, regs = XgmiComm.with_local_peers(rank, world, mlp_step.NPARAM, device=gpu)
+    BP = (B + 15) // 16 * 16
+    HP = mlp_step.HP
+    plane = HP * BP
+    dz1A = torch.zeros(world, HP, BP, device=gpu)
+    own = _ref_dz1(p, x, y)  # [B, H]
+    S, par_w = comm.slot_stride, world
+    g = torch.Generator().manual_seed(5 + world)
+    for epoch in (1, 2):
+        par = epoch & 1
+        peer = {}
+        for q in range(world):
+            if q == rank:
+                continue
+            v = torch.zeros(HP, BP)
+            v[:100, :B] = torch.randn(100, B, generator=g)
+            peer[q] = v
+            o = (par * par_w + q) * S
+            regs[rank][o:o + plane] = _words(v.reshape(-1).to(gpu), epoch)
+        torch.cuda.synchronize()
+        if nslab == 7:
+            hip().mlp_fwd(ptr(p), 0, 0.0, 0, ptr(x), ptr(ws.buf), ws.B, stream_handle())
+        else:
+            tmp = p.clone()
+            hip().mlp_fwdapply(ptr(p), ptr(tmp), 0.0, ptr(x), ptr(x), ptr(ws.buf), ptr(ws.ctr),
+                               0, ws.stats_ring, ws.B, 0, stream_handle())
+        comm.mlp_head(p, y, ws, dz1A, nslab=nslab)
+        comm.check()
+        got = dz1A.cpu()
+        for q in range(world):
+            if q == rank:
+                err = float((got[q, :100, :B].double() - own.t()).abs().max())
+                assert err <= 1e-5, (epoch, err)
+            else:
+                assert torch.equal(got[q, :100, :B], peer[q][:100, :B]), (epoch, q)
+        # every peer received my factors for (j < 100, row < B)
+        for j in range(world):
+            if j == rank:
+                continue
+            o = (par * world + rank) * S
+            w = regs[j][o:o + plane].cpu().view(HP, BP)[:100, :B]
+            assert bool((_epochs(w) == epoch).all()), (j, epoch)
+            assert float((_vals(w).double() - own.t()).abs().max()) <= 1e-5
+    comm.destroy()
+
+
+def _factor_inputs(world, rank, B, dev, seed):
+    from distributedtensorflowexample_amd.data.synthetic import mnist_like_device
+    from distributedtensorflowexample_amd.ops import mlp_step
+
+    BP = (B + 15) // 16 * 16
+    x_all = torch.stack([mnist_like_device(B, seed=seed + q, device=dev)[0]
+                         for q in range(world)]).contiguous()
+    g = torch.Generator().manual_seed(seed)
+    dz1A = torch.zeros(world, mlp_step.HP, BP)
+    dz1A[:, :100, :B] = torch.randn(world, 100, B, generator=g) * 0.01
+    return x_all, dz1A.to(dev)
+
+
+def _global_w1_grad(dz1A, x_all, B):
+    W = x_all.shape[0]
+    g = torch.zeros(100, 784, dtype=torch.float64)
+    for q in range(W):
+        g += dz1A[q, :100, :B].double().cpu() @ x_all[q].double().cpu()
+    return g.reshape(-1)
+
+
+@pytest.mark.parametrize("world,rank,B", _engine_cases())
+def test_factor_wgrad_simulated_peers(gpu, world, rank, B):
+    """mlp_wgrad_factor_kernel<XW, NGT>: global dW1 from every rank's factors and batch, small
+    parameters exchanged (LL push)."""
+    from distributedtensorflowexample_amd.ops import mlp_step
+    from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+    p, _, y, ws = _setup(gpu, B, 40 * world + rank)
+    x_all, dz1A = _factor_inputs(world, rank, B, gpu, 77 + world)
+    x = x_all[rank]
+    comm, regs = XgmiComm.with_local_peers(rank, world, mlp_step.NPARAM, device=gpu)
+    _plain_fwd_head(p, x, y, ws)
+    own = _ref_grad(p, x, y)
+    gW1 = _global_w1_grad(dz1A, x_all, B)
+    lr = 0.5
+    cur = p.double().cpu()
+    lo = mlp_step.OFF_B1
+    for epoch in (1, 2):
+        peers = _peer_grads(world, rank, 13 * epoch + world, 0.05)
+        _stage_param_words(comm, regs, peers, epoch, lo, mlp_step.NPARAM)
+        torch.cuda.synchronize()
+        comm.mlp_wgrad_factor(p, lr, x, x_all.stride(0), dz1A, ws)
+        comm.check()
+        upd = _expected_update(own, peers, rank)
+        upd[:lo] = gW1
+        cur = cur - lr * upd
+        err = float((p.double().cpu() - cur).abs().max())
+        assert err <= 2e-5, (epoch, err)
+        _check_pushed(comm, regs, own, epoch, lo, mlp_step.NPARAM, 2e-6)
+    assert ws.global_step() == 2
+    comm.destroy()
+
+
+@pytest.mark.parametrize("world,rank,B", _engine_cases())
+def test_factor2_fwdapply_simulated_peers(gpu, world, rank, B):
+    """mlp_fwdapply_factor_kernel<XW, NGT>: pipelined factor engine (global W1 update of step
+    t-1 from every rank's factors and previous batch, small parameters exchanged, fused with
+    step t's forward)."""
+    from distributedtensorflowexample_amd.data.synthetic import mnist_like_device
+    from distributedtensorflowexample_amd.ops import mlp_step
+    from distributedtensorflowexample_amd.ops._ext import hip, ptr, stream_handle
+    from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+    p_old, _, y_prev, ws = _setup(gpu, B, 50 * world + rank)
+    x_all, dz1A = _factor_inputs(world, rank, B, gpu, 91 + world)
+    x_prev = x_all[rank]
+    x, y = mnist_like_device(B, seed=555 + rank, device=gpu)
+    comm, regs = XgmiComm.with_local_peers(rank, world, mlp_step.NPARAM, device=gpu)
+    lr = 0.5
+    lo = mlp_step.OFF_B1
+    _pipelined_fwd_head(p_old, x_prev, y_prev, ws)
+    own = _ref_grad(p_old, x_prev, y_prev)
+    gW1 = _global_w1_grad(dz1A, x_all, B)
+    p_new = torch.empty_like(p_old)
+    peers = _peer_grads(world, rank, 17 + world, 0.05)
+    _stage_param_words(comm, regs, peers, 1, lo, mlp_step.NPARAM)
+    torch.cuda.synchronize()
+    comm.mlp_fwdapply_factor(p_old, p_new, lr, x_prev, x, x_all.stride(0), dz1A, ws, True)
+    hip().mlp_head2(ptr(p_new), ptr(y), ptr(ws.buf), ws.B, stream_handle())
+    comm.check()
+    upd = _expected_update(own, peers, rank)
+    upd[:lo] = gW1
+    exp = p_old.double().cpu() - lr * upd
+    err = float((p_new.double().cpu() - exp).abs().max())
+    assert err <= 2e-5, err
+    _check_pushed(comm, regs, own, 1, lo, mlp_step.NPARAM, 2e-6)
+    hbuf, _, _ = _ws_views(ws)
+    h_ref, _ = mlp_step.reference_forward(p_new.double().cpu(), x.double().cpu())
+    assert float((hbuf[:B, :100].double().cpu() - h_ref).abs().max()) <= 1e-4
+    # second round (parity 0): the factors of (p_new, x) now sit in ws
+    own2 = _ref_grad(p_new, x, y)
+    x_all2, dz1A2 = _factor_inputs(world, rank, B, gpu, 191 + world)
+    x_all2[rank] = x
+    gW1b = _global_w1_grad(dz1A2, x_all2, B)
+    peers2 = _peer_grads(world, rank, 19 + world, 0.05)
+    _stage_param_words(comm, regs, peers2, 2, lo, mlp_step.NPARAM)
+    p3 = torch.empty_like(p_old)
+    torch.cuda.synchronize()
+    comm.mlp_fwdapply_factor(p_new, p3, lr, x_all2[rank], x, x_all2.stride(0), dz1A2, ws, True)
+    comm.check()
+    upd2 = _expected_update(own2, peers2, rank)
+    upd2[:lo] = gW1b
+    exp2 = p_new.double().cpu() - lr * upd2
+    assert float((p3.double().cpu() - exp2).abs().max()) <= 2e-5
+    _check_pushed(comm, regs, own2, 2, lo, mlp_step.NPARAM, 2e-6)
+    assert ws.global_step() == 2
+    comm.destroy()
+
+
+def test_timeout_when_a_peer_word_is_missing(gpu):
+    """A word a peer never wrote is a bounded wait, reported through the error word (no hang)."""
+    from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+    world, rank, n = 8, 3, 4096
+    comm, regs = XgmiComm.with_local_peers(rank, world, n, device=gpu, protocol="push",
+                                           timeout_s=0.05)
+    S = comm.slot_stride
+    for j in range(world):
+        if j not in (rank, 6):  # peer 6 never publishes
+            o = (1 * world + j) * S
+            regs[rank][o:o + n] = _words(torch.ones(n, device=gpu), 1)
+    t = torch.ones(n, device=gpu)
+    comm.allreduce_sum_(t)
+    assert comm.failed()
+    comm.destroy()
