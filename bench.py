@@ -194,12 +194,14 @@ def main():
         else:
             comm = _native_comm(world, rank, dev, mlp_numel())
         rendezvous = comm  # RCCL communicator kept for the timing barrier
+        # shared-GPU rehearsal: the peers time-share one device, so an xGMI wait lasts longer
+        tmo = 60.0 if SHARED_GPU else 2.0
         if a.comm != "torch":
             if a.comm in ("xgmi", "auto"):
                 from distributedtensorflowexample_amd.parallel.select import pick_small_allreduce
                 from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
 
-                comm, probe = pick_small_allreduce(comm, a.comm, world, rank, dev)
+                comm, probe = pick_small_allreduce(comm, a.comm, world, rank, dev, timeout_s=tmo)
                 a.comm_probe = probe
                 a.comm = ("xgmi-" + comm.protocol) if isinstance(comm, XgmiComm) else "native"
             if a.engine != "allreduce":
@@ -208,7 +210,7 @@ def main():
 
                 kind, c, eprobe = pick_mlp_engine(params, x, y, a.batch_size, a.learning_rate,
                                                   comm, world, rank, dev, mode=a.engine,
-                                                  x_all=x_all)
+                                                  x_all=x_all, timeout_s=tmo)
                 a.engine_probe = eprobe
                 if kind in ("fused", "fused2"):
                     fused_comm, a.comm = c, "xgmi-fused-push"

@@ -62,10 +62,17 @@ constexpr uint32_t kNoVar = 0xffffffffu;
 enum DType : uint8_t { DT_F32 = 0, DT_I64 = 1 };
 
 // ---------------------------------------------------------------- io helpers
+// A lost ps connection (peer closed, reset, or -- with an rpc timeout -- silent for too long):
+// raised to Python as ConnectionError, so a worker whose ps died exits instead of retrying.
+struct PSConnectionLost : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
 bool read_full(int fd, void* buf, size_t n) {
   char* p = static_cast<char*>(buf);
   while (n) {
     const ssize_t r = ::recv(fd, p, n, 0);
+    if (r < 0 && errno == EINTR) continue;
     if (r <= 0) return false;
     p += r;
     n -= static_cast<size_t>(r);
@@ -76,6 +83,7 @@ bool write_full(int fd, const void* buf, size_t n) {
   const char* p = static_cast<const char*>(buf);
   while (n) {
     const ssize_t r = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (r < 0 && errno == EINTR) continue;
     if (r <= 0) return false;
     p += r;
     n -= static_cast<size_t>(r);
@@ -221,6 +229,7 @@ class PSServer {
     d["bytes_out"] = bytes_out_.load();
     d["sync_rounds"] = sync_rounds_.load();
     d["sync_stale"] = sync_stale_.load();
+    d["sync_withdrawn"] = sync_withdrawn_.load();
     return d;
   }
 
@@ -425,7 +434,7 @@ class PSServer {
     for (uint32_t k = 0; k < n; ++k) vs[k] = var(ids[k] = r.get<uint32_t>());
     Var* stepv = step_id == kNoVar ? nullptr : var(step_id);
     std::unique_lock<std::mutex> lk(sync_mu_);
-    if (sync_gen_ < 0 || (sync_count_ == 0 && local_step > sync_gen_))
+    if (sync_gen_ < 0 || (sync_pending_.empty() && local_step > sync_gen_))
       sync_gen_ = local_step;  // first round of a (fresh or restored) job: adopt its step
     if (local_step < sync_gen_) {  // stale: its round was applied without it
       ++sync_stale_;
@@ -436,41 +445,54 @@ class PSServer {
     if (local_step > sync_gen_)
       throw std::runtime_error("ps: sync push from step " + std::to_string(local_step) +
                                " while round " + std::to_string(sync_gen_) + " is open");
+    // this push's gradients are kept apart until its round closes: a push whose wait times
+    // out is withdrawn EXACTLY (its entry removed), so a retried push is not counted twice and
+    // a round never applies an abandoned gradient
+    SyncPush mine;
+    mine.token = ++sync_tokens_;
     for (uint32_t k = 0; k < n; ++k) {
       Var* v = vs[k];
       if (v->dtype != DT_F32) throw std::runtime_error("ps: sync push to a non-float variable");
       const char* g = r.take(v->nbytes());
-      std::vector<float>& a = sync_acc_[ids[k]];
-      if (a.size() != v->count) a.assign(v->count, 0.f);
-      for (size_t i = 0; i < v->count; ++i) {
-        float gi;
-        std::memcpy(&gi, g + 4 * i, 4);
-        a[i] += gi;
-      }
+      std::vector<float> gv(v->count);
+      std::memcpy(gv.data(), g, v->nbytes());
+      mine.grads.emplace_back(ids[k], std::move(gv));
     }
+    sync_pending_.push_back(std::move(mine));
+    const uint64_t token = sync_pending_.back().token;
     const int64_t round = sync_gen_;
-    if (++sync_count_ >= static_cast<int>(R)) {
-      // apply the mean of the round's R gradients (SyncReplicasOptimizer averages)
+    if (static_cast<int>(sync_pending_.size()) >= static_cast<int>(R)) {
+      // apply the mean of the round's R gradients (SyncReplicasOptimizer averages), summed in
+      // arrival order
+      std::map<uint32_t, std::vector<float>> acc;
+      for (const SyncPush& sp : sync_pending_)
+        for (const auto& kv : sp.grads) {
+          std::vector<float>& a = acc[kv.first];
+          if (a.empty()) a.assign(kv.second.size(), 0.f);
+          for (size_t i = 0; i < a.size(); ++i) a[i] += kv.second[i];
+        }
       const float scale = lr / static_cast<float>(R);
-      for (auto& kv : sync_acc_) {
+      for (auto& kv : acc) {
         Var* v = var(kv.first);
         std::lock_guard<std::mutex> vl(v->mu);
         float* p = v->f.data();
-        for (size_t i = 0; i < kv.second.size(); ++i) {
-          p[i] -= scale * kv.second[i];
-          kv.second[i] = 0.f;
-        }
+        for (size_t i = 0; i < kv.second.size(); ++i) p[i] -= scale * kv.second[i];
       }
-      sync_count_ = 0;
+      sync_pending_.clear();
       ++sync_gen_;
       ++sync_rounds_;
       if (stepv) stepv->i.store(sync_gen_);
       sync_cv_.notify_all();
     } else if (!sync_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms),
                                   [&] { return sync_gen_ > round || !running_; })) {
+      const size_t have = sync_pending_.size();
+      sync_pending_.erase(std::remove_if(sync_pending_.begin(), sync_pending_.end(),
+                                         [&](const SyncPush& sp) { return sp.token == token; }),
+                          sync_pending_.end());
+      ++sync_withdrawn_;
       throw std::runtime_error("ps: sync round " + std::to_string(round) + " timed out with " +
-                               std::to_string(sync_count_) + " of " + std::to_string(R) +
-                               " replicas");
+                               std::to_string(have) + " of " + std::to_string(R) +
+                               " replicas (this push was withdrawn)");
     }
     if (sync_gen_ <= round) throw std::runtime_error("ps: server stopped during a sync round");
     w.put<int64_t>(sync_gen_);
@@ -491,16 +513,26 @@ class PSServer {
   std::mutex sync_mu_;
   std::condition_variable sync_cv_;
   int64_t sync_gen_ = -1;
-  int sync_count_ = 0;
-  std::map<uint32_t, std::vector<float>> sync_acc_;
-  std::atomic<uint64_t> sync_rounds_{0}, sync_stale_{0};
+  struct SyncPush {
+    uint64_t token = 0;
+    std::vector<std::pair<uint32_t, std::vector<float>>> grads;
+  };
+  std::vector<SyncPush> sync_pending_;  // the open round's pushes, in arrival order
+  uint64_t sync_tokens_ = 0;
+  std::atomic<uint64_t> sync_rounds_{0}, sync_stale_{0}, sync_withdrawn_{0};
 };
 
 // ---------------------------------------------------------------- client
 class PSClient {
  public:
-  PSClient(std::vector<std::string> addrs, double connect_timeout_s) : addrs_(std::move(addrs)) {
-    for (auto& a : addrs_) fds_.push_back(connect_to(a, connect_timeout_s));
+  // rpc_timeout_s > 0: a ps that stays silent that long on a request counts as lost (a hung or
+  // stopped ps ends the worker instead of blocking it forever); 0 = wait indefinitely.
+  PSClient(std::vector<std::string> addrs, double connect_timeout_s, double rpc_timeout_s = 0.0)
+      : addrs_(std::move(addrs)), rpc_timeout_s_(rpc_timeout_s) {
+    for (auto& a : addrs_) {
+      fds_.push_back(connect_to(a, connect_timeout_s));
+      set_timeout(fds_.back(), rpc_timeout_s_);
+    }
   }
   ~PSClient() { close(); }
 
@@ -568,6 +600,7 @@ class PSClient {
     // drain EVERY task's response before reporting a failure: an unread reply would stay
     // queued on its socket and answer the next call on that connection
     std::string first_error;
+    bool lost = false;
     for (size_t t = 0; t < per.size(); ++t) {
       if (per[t].empty()) continue;
       try {
@@ -578,10 +611,14 @@ class PSClient {
           std::memcpy(reinterpret_cast<void*>(ptrs[k]), resp.data() + off, sizes[k]);
           off += sizes[k];
         }
+      } catch (const PSConnectionLost& e) {
+        if (first_error.empty()) first_error = e.what();
+        lost = true;
       } catch (const std::exception& e) {
         if (first_error.empty()) first_error = e.what();
       }
     }
+    if (lost) throw PSConnectionLost(first_error);
     if (!first_error.empty()) throw std::runtime_error(first_error);
   }
   // push gradients (f32) and apply var -= lr * grad on the owning ps tasks
@@ -605,14 +642,19 @@ class PSClient {
       send(static_cast<int>(t), w.b);
     }
     std::string first_error;  // drain every task's reply first (see pull)
+      bool lost = false;
     for (size_t t = 0; t < per.size(); ++t) {
       if (per[t].empty()) continue;
       try {
         recv(static_cast<int>(t));
+      } catch (const PSConnectionLost& e) {
+        if (first_error.empty()) first_error = e.what();
+        lost = true;
       } catch (const std::exception& e) {
         if (first_error.empty()) first_error = e.what();
       }
     }
+    if (lost) throw PSConnectionLost(first_error);
     if (!first_error.empty()) throw std::runtime_error(first_error);
   }
   // Synchronous-replicas push (see SYNC_PUSH): every task gets its variables' gradients; the
@@ -633,6 +675,18 @@ class PSClient {
       for (size_t k = 0; k < hs.size(); ++k) per[task_of(hs[k])].push_back(k);
       const size_t step_task = task_of(step_handle);
       const uint32_t tmo = static_cast<uint32_t>(std::min(timeout_s, 4.0e6) * 1000.0);
+      // the ps holds this reply until the round closes (up to timeout_s): the rpc timeout
+      // covers the silence AFTER that wait, restored on every exit path
+      struct Extend {
+        PSClient* c;
+        double secs;
+        Extend(PSClient* c_, double s_) : c(c_), secs(s_) {
+          if (c->rpc_timeout_s_ > 0) for (int fd : c->fds_) set_timeout(fd, secs + c->rpc_timeout_s_);
+        }
+        ~Extend() {
+          if (c->rpc_timeout_s_ > 0) for (int fd : c->fds_) set_timeout(fd, c->rpc_timeout_s_);
+        }
+      } extend(this, timeout_s);
       std::vector<bool> sent(fds_.size(), false);
       for (size_t t = 0; t < per.size(); ++t) {
         if (per[t].empty() && t != step_task) continue;
@@ -650,6 +704,7 @@ class PSClient {
         sent[t] = true;
       }
       std::string first_error;  // drain every task's reply first (see pull)
+      bool lost = false;
       for (size_t t = 0; t < per.size(); ++t) {
         if (!sent[t]) continue;
         try {
@@ -659,11 +714,15 @@ class PSClient {
           const bool a = r.get<uint8_t>() != 0;
           if (t == step_task || round < 0) round = g;
           applied = applied && a;
+        } catch (const PSConnectionLost& e) {
+          if (first_error.empty()) first_error = e.what();
+          lost = true;
         } catch (const std::exception& e) {
           if (first_error.empty()) first_error = e.what();
         }
       }
-      if (!first_error.empty()) throw std::runtime_error(first_error);
+      if (lost) throw PSConnectionLost(first_error);
+    if (!first_error.empty()) throw std::runtime_error(first_error);
     }
     return py::make_tuple(round, applied);
   }
@@ -729,6 +788,15 @@ class PSClient {
     if (s == "int64" || s == "int32") return DT_I64;
     throw std::runtime_error("ps: unsupported dtype " + s);
   }
+  static void set_timeout(int fd, double secs) {
+    timeval tv{};
+    if (secs > 0) {
+      tv.tv_sec = static_cast<time_t>(secs);
+      tv.tv_usec = static_cast<suseconds_t>((secs - static_cast<double>(tv.tv_sec)) * 1e6);
+    }
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+  }
   static int connect_to(const std::string& addr, double timeout_s) {
     const auto c = addr.rfind(':');
     if (c == std::string::npos) throw std::runtime_error("ps: bad address " + addr);
@@ -758,15 +826,15 @@ class PSClient {
       throw std::runtime_error("ps: bad task");
     const uint32_t len = static_cast<uint32_t>(payload.size());
     if (!write_full(fds_[task], &len, 4) || !write_full(fds_[task], payload.data(), payload.size()))
-      throw std::runtime_error("ps: connection to " + addrs_[task] + " lost (send)");
+      throw PSConnectionLost("ps: connection to " + addrs_[task] + " lost (send)");
   }
   std::string recv(int task) {
     uint32_t len;
     if (!read_full(fds_[task], &len, 4))
-      throw std::runtime_error("ps: connection to " + addrs_[task] + " lost (recv)");
+      throw PSConnectionLost("ps: connection to " + addrs_[task] + " lost (recv)");
     std::string resp(len, '\0');
     if (!read_full(fds_[task], &resp[0], len))
-      throw std::runtime_error("ps: connection to " + addrs_[task] + " lost (recv body)");
+      throw PSConnectionLost("ps: connection to " + addrs_[task] + " lost (recv body)");
     if (resp.empty()) throw std::runtime_error("ps: empty response");
     if (resp[0] != 0) throw std::runtime_error(resp.substr(1));
     return resp.substr(1);
@@ -783,6 +851,7 @@ class PSClient {
   }
 
   std::vector<std::string> addrs_;
+  double rpc_timeout_s_ = 0.0;
   std::vector<int> fds_;
   std::mutex mu_;  // one request/response exchange at a time (shared by Python threads)
 };
@@ -790,6 +859,7 @@ class PSClient {
 }  // namespace
 
 void register_ps(py::module_& m) {
+  py::register_exception<PSConnectionLost>(m, "PSConnectionLost", PyExc_ConnectionError);
   py::class_<PSServer>(m, "PSServer")
       .def(py::init<const std::string&, int>(), py::arg("host") = "127.0.0.1", py::arg("port") = 0)
       .def("start", &PSServer::start)
@@ -799,8 +869,8 @@ void register_ps(py::module_& m) {
       .def("stats", &PSServer::stats)
       .def_property_readonly("port", &PSServer::port);
   py::class_<PSClient>(m, "PSClient")
-      .def(py::init<std::vector<std::string>, double>(), py::arg("addresses"),
-           py::arg("connect_timeout") = 60.0)
+      .def(py::init<std::vector<std::string>, double, double>(), py::arg("addresses"),
+           py::arg("connect_timeout") = 60.0, py::arg("rpc_timeout") = 0.0)
       .def("create", &PSClient::create, py::arg("name"), py::arg("dtype"), py::arg("shape"),
            py::arg("task"))
       .def("lookup", &PSClient::lookup, py::arg("name"), py::arg("task"))

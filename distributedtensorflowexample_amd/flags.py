@@ -184,6 +184,9 @@ def define_reference_flags(flag_values=FLAGS):
     DEFINE_float("save_model_secs", 30.0, "Chief checkpoint interval (Supervisor)", fv)
     DEFINE_float("save_summaries_secs", 30.0, "Chief step-rate summary interval", fv)
     DEFINE_boolean("use_locking", False, "Serialize PS updates per variable", fv)
+    DEFINE_float("ps_timeout_secs", 0.0,
+                 "Worker: a ps silent this long on a request counts as lost and the worker "
+                 "exits non-zero (0: wait indefinitely; a dead ps is detected at once)", fv)
     DEFINE_string("ps_device", "cpu",
                   "cpu: variables on the TCP parameter server (the reference) | gpu: variables "
                   "in one GPU-resident store on the chief worker's GPU, IPC-mapped by every "

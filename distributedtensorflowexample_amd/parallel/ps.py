@@ -46,8 +46,11 @@ class PSVariableStore:
     'int64'.  Float variables are exchanged through pinned host buffers.
     """
 
-    def __init__(self, ps_addresses, specs, connect_timeout=120.0, setter=None):
-        self.client = host().PSClient(list(ps_addresses), float(connect_timeout))
+    def __init__(self, ps_addresses, specs, connect_timeout=120.0, setter=None, rpc_timeout=0.0):
+        # a lost ps raises ConnectionError (host().PSConnectionLost) from any call; rpc_timeout
+        # > 0 also counts a ps that stays silent that long as lost
+        self.client = host().PSClient(list(ps_addresses), float(connect_timeout),
+                                      float(rpc_timeout))
         self.specs = [(n, tuple(int(d) for d in s), dt) for n, s, dt in specs]
         self.setter = setter or replica_device_setter(len(ps_addresses))
         self.handles = {}
@@ -74,7 +77,7 @@ class PSVariableStore:
                 try:
                     self.handles[n] = self.client.lookup(n, self.setter(i))
                     break
-                except RuntimeError:
+                except RuntimeError:  # not created yet (a lost ps is a ConnectionError)
                     if time.time() - t0 > timeout:
                         raise TimeoutError("ps variable %s never created" % n)
                     time.sleep(poll)

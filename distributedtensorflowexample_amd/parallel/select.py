@@ -28,7 +28,7 @@ def xgmi_protocols(world):
 
 
 def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_key="dtfx/xgmi/0",
-                         protocols=None):
+                         protocols=None, timeout_s=2.0):
     """MLP gradient all-reduce backend.  Every candidate xGMI protocol (``xgmi_protocols``)
     that can be created on every rank and agrees with RCCL on ten random gradients is timed
     against RCCL inside captured hipGraphs (max over ranks, interleaved, best of three); mode
@@ -47,7 +47,7 @@ def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_k
         xg, err = None, ""
         try:
             xg = XgmiComm(rank, world, n, device=dev, key="%s/%s" % (xgmi_key, proto),
-                          protocol=proto)
+                          protocol=proto, timeout_s=timeout_s)
         except Exception as e:  # no IPC / peer mapping on this node
             err = repr(e)
             print("[bench] rank %d: xgmi-%s: %s" % (rank, proto, err), file=sys.stderr)
@@ -59,18 +59,22 @@ def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_k
             continue
         g = torch.Generator(device="cpu").manual_seed(1000 + rank)
         ok = True
-        try:
-            for it in range(10):  # fresh random gradients: both backends must agree every time
-                base = torch.randn(n, generator=g).to(dev) * (1 + it)
-                ra, xa = base.clone(), base.clone()
-                rccl.allreduce_sum_(ra)
-                torch.cuda.synchronize()
-                dist.barrier()
+        # Every rank issues the SAME sequence of collectives whatever happens locally: a rank
+        # that left this loop early (a timed-out wait raising on it but not on a peer) would
+        # leave its peers blocked in the next RCCL call.  Timeouts are read without raising
+        # (failed()) and the verdict is agreed on after all ten rounds.
+        for it in range(10):  # fresh random gradients: both backends must agree every time
+            base = torch.randn(n, generator=g).to(dev) * (1 + it)
+            ra, xa = base.clone(), base.clone()
+            rccl.allreduce_sum_(ra)
+            torch.cuda.synchronize()
+            dist.barrier()
+            try:
                 xg.allreduce_sum_(xa)
-                xg.check()
-                ok &= bool(((ra - xa).abs().max() <= 1e-5 * ra.abs().max()).item())
-        except Exception as e:
-            ok, err = False, repr(e)
+                bad = xg.failed()
+            except Exception as e:  # noqa: BLE001 - host-side launch error: same on every call
+                bad, err = True, repr(e)
+            ok &= not bad and bool(((ra - xa).abs().max() <= 1e-5 * ra.abs().max()).item())
         if agree(ok):
             cands["xgmi-" + proto] = xg
         else:
@@ -132,7 +136,8 @@ def pick_small_allreduce(rccl, mode, world, rank, dev, iters=200, n=None, xgmi_k
 
 
 def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mode="auto",
-                    xgmi_key="dtfx/xgmi/fused", verify_steps=20, time_steps=400, x_all=None):
+                    xgmi_key="dtfx/xgmi/fused", verify_steps=20, time_steps=400, x_all=None,
+                    timeout_s=2.0):
     """Data-parallel engine of the fused MLP trainer, one of
       ``("allreduce", ar_comm)`` -- flat gradient, separate all-reduce launch, deferred apply;
       ``("fused", XgmiComm)``   -- gradient exchange inside the weight-gradient kernel;
@@ -170,7 +175,7 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
         c, err = None, ""
         try:
             c = XgmiComm(rank, world, mlp_step.NPARAM, device=dev, key="%s/%s" % (xgmi_key, kind),
-                         protocol="push")
+                         protocol="push", timeout_s=timeout_s)
         except Exception as e:
             err = repr(e)
             print("[bench] rank %d: %s xgmi engine: %s" % (rank, kind, err), file=sys.stderr)
@@ -200,20 +205,24 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
     pa = ta.flush().clone()
     trainers = {"allreduce": ta}
     for kind in list(comms):
+        # the control-plane collectives below run on every rank whatever happened locally
+        # (an exception on one rank must not leave the others waiting in a broadcast)
         ok, err = True, ""
+        chk = torch.full((1,), float("nan"), dtype=torch.float64)
         try:
             tk = make(kind)
             tk.run(verify_steps, use_graph=False)
-            comms[kind].check()
             pk = tk.flush()
+            if comms[kind].failed():  # a timed-out in-kernel wait (no raise: see above)
+                ok, err = False, "xGMI exchange timed out waiting for a peer"
             tol = 1e-4 * (1.0 + float(pa.abs().max()))
-            ok = bool(((pk - pa).abs().max() <= tol).item())
+            ok &= bool(((pk - pa).abs().max() <= tol).item())
             chk = pk.double().sum().reshape(1).cpu()  # replicas must stay bit-identical
-            ref = chk.clone()
-            dist.broadcast(ref, 0)
-            ok &= bool(torch.equal(chk, ref))
         except Exception as e:
             ok, err = False, repr(e)
+        ref = chk.clone()
+        dist.broadcast(ref, 0)
+        ok &= bool(torch.equal(chk, ref))
         if agree(ok):
             trainers[kind] = tk
         else:

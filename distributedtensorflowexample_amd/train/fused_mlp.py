@@ -135,6 +135,25 @@ class FusedMLPTrainer:
             self.pending = False
         return self.bufs[self.cur]
 
+    def snapshot(self):
+        """Parameters after every step run so far (a pending update included) as a NEW
+        tensor, WITHOUT changing the trainer: no peer exchange starts and the replicas' update
+        sequence is untouched, so one rank alone may call it (chief-only checkpoints and
+        evals).  The all-reduce engine's pending gradient is already reduced: applied to a
+        copy.  A pending update of the pipelined exchange engines needs every rank's
+        exchange: raises (call flush() on every rank instead)."""
+        p = self.bufs[self.cur]
+        if not self.pending:
+            return p.clone()
+        if not self.pipelined:
+            out = p.clone()
+            optim.sgd_(out, self.grad, self.lr / self.world_size)
+            return out
+        if self.world_size == 1:
+            return self.flush().clone()
+        raise RuntimeError("snapshot(): the pending update is a peer exchange; flush() on "
+                           "every rank first")
+
     def load_params(self, p):
         self.bufs[self.cur].copy_(p)
         self.pending = False

@@ -42,16 +42,28 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
     use_gpu = torch.cuda.is_available() and flags.device != "cpu"
     if world > 1 and not dist.is_initialized():
         dist.init_process_group("gloo")  # control plane; tensors over RCCL on GPU
+    shared_gpu = os.environ.get("DTFX_SHARED_GPU") == "1"
     if use_gpu:
+        # DTFX_SHARED_GPU=1 (rehearsal on a one-GPU box only): every rank on device 0 and an
+        # xGMI-IPC communicator in place of RCCL, which refuses two ranks on one GPU
+        local = 0 if shared_gpu else local
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-        comm = NativeComm.from_process_group() if world > 1 else None
+        comm = None
+        if world > 1 and shared_gpu:
+            from ..parallel.xgmi import XgmiComm
+
+            comm = XgmiComm(rank, world, mlp_step.NPARAM, device=dev, key="dtfx/mirrored/shared",
+                            protocol="push", timeout_s=120.0)
+        elif world > 1:
+            comm = NativeComm.from_process_group()
         if getattr(flags, "zero1", False) and world > 1:
             # the fused GPU engines exchange gradients inside their kernels; a 1/N-sharded
             # update of a 318 KB model would only add two collectives per step
             raise ValueError("--zero1 is implemented on the autograd (CPU) mirrored path; the "
                              "fused GPU MLP engines replicate the update")
-        if comm is not None and os.environ.get("DTFX_MLP_COMM", "auto") != "rccl":
+        if (comm is not None and not shared_gpu
+                and os.environ.get("DTFX_MLP_COMM", "auto") != "rccl"):
             # the 318 KB gradient is latency bound: xGMI one-shot when verified and faster
             from ..parallel.select import pick_small_allreduce
 
@@ -90,7 +102,8 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
                                      for q in range(world)]).to(dev).contiguous()
                 tr_x, tr_y = x_all[rank], tr_y[:n]
             kind, c, _ = pick_mlp_engine(params, tr_x.to(dev), tr_y.to(dev), B,
-                                         flags.learning_rate, comm, world, rank, dev, x_all=x_all)
+                                         flags.learning_rate, comm, world, rank, dev, x_all=x_all,
+                                         mode=os.environ.get("DTFX_MLP_ENGINE", "auto"))
             fused = c if kind in ("fused", "fused2") else None
             factor = c if kind in ("factor", "factor2") else None
             pipe = kind not in ("fused", "factor")  # fused2 / factor2: two-launch variants
@@ -99,7 +112,12 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
                              else None, world_size=world, fused_comm=fused, factor_comm=factor,
                              x_all=x_all if factor is not None else None, rank=rank,
                              pipeline=pipe if comm is not None else True)
-        get_params = lambda: tr.flush().clone()  # noqa: E731
+        # tr.snapshot() never starts a peer exchange on ONE rank and never changes the
+        # replicas' update sequence (the all-reduce engine's pending gradient is applied to a
+        # copy); the pipelined exchange engines have nothing pending at the checkpoint /
+        # eval / replica-check points, because the loop below reads each chunk's stats on
+        # EVERY rank (stats_range flushes there, collectively)
+        get_params = tr.snapshot
         step_fn = None
     else:
         model = mlp_model.MnistMLP(flat=params)

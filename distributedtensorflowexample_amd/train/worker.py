@@ -92,7 +92,9 @@ class Worker:
                                     setter=replica_device_setter(len(server.target)))
         else:
             self.store = PSVariableStore(server.target, GLOBAL_SPECS,
-                                         setter=replica_device_setter(len(server.target)))
+                                         setter=replica_device_setter(len(server.target)),
+                                         rpc_timeout=float(getattr(flags, "ps_timeout_secs", 0)
+                                                           or 0))
         # local replica (worker.py:34-40): one flat buffer on this worker's device
         self.params = torch.zeros(mlp_step.NPARAM, device=self.device)
         self.grad = torch.zeros_like(self.params)

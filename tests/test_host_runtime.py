@@ -264,6 +264,26 @@ def test_ps_sync_replicas_rounds(h):
         # a round that never completes fails after its timeout instead of hanging
         with pytest.raises(RuntimeError, match="timed out"):
             st0.sync_push({"a": torch.ones(64), "b": torch.ones(3)}, 0.5, 3, 12, timeout_s=0.3)
+        # ... and its gradient is withdrawn: retrying the same step (twice more, timing out
+        # again) and then completing the round with two other replicas applies the mean of
+        # exactly three gradients, the retry counted once
+        with pytest.raises(RuntimeError, match="withdrawn"):
+            st0.sync_push({"a": torch.ones(64), "b": torch.ones(3)}, 0.5, 3, 12, timeout_s=0.3)
+        assert sum(s.stats()["sync_withdrawn"] for s in servers) == 4  # 2 pushes x 2 tasks
+        outs = {}
+
+        def push(k, val):
+            st = PSVariableStore(addrs, specs).lookup()
+            outs[k] = st.sync_push({"a": torch.full((64,), val), "b": torch.full((3,), val)},
+                                   0.5, 3, 12, timeout_s=30)
+            st.close()
+
+        ts = [threading.Thread(target=push, args=(k, v)) for k, v in enumerate((1.0, 4.0, 7.0))]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        assert all(o == (13, True) for o in outs.values()), outs
+        v = st0.read_all()
+        assert torch.allclose(v["a"], torch.full((64,), -5.0 - 0.5 * 4.0))  # mean (1+4+7)/3
         st0.close()
     finally:
         for s in servers:
