@@ -322,7 +322,8 @@ def main():
         tr.run_persistent(a.steps)  # every update applied inside the launch
     else:
         tr.run(a.steps, use_graph)
-    tr.flush()  # the last step's deferred update is part of the timed work
+    if launch != "persistent":  # (the persistent launch leaves nothing pending)
+        tr.flush()  # the last step's deferred update is part of the timed work
     torch.cuda.synchronize()
     if barrier:
         barrier()

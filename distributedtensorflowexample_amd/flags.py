@@ -192,7 +192,12 @@ def define_reference_flags(flag_values=FLAGS):
                   "in one GPU-resident store on the chief worker's GPU, IPC-mapped by every "
                   "worker (pull / apply / global_step over xGMI; async PS only)", fv)
     DEFINE_integer("seed", 0, "Parameter init seed", fv)
-    DEFINE_string("model", "mlp", "mlp (the reference) | bert | resnet50 (north-star configs)", fv)
+    DEFINE_string("model", "mlp", "mlp (the reference) | bert | resnet50 (north-star configs); "
+                  "async PS: mlp | softmax (softmax regression)", fv)
+    DEFINE_string("hidden_units", "", "async PS, --model mlp: hidden layer widths, e.g. 256,128 "
+                  "(default: the reference's 100)", fv)
+    DEFINE_string("activation", "sigmoid", "async PS, --model mlp: hidden activation "
+                  "(sigmoid | relu)", fv)
     DEFINE_string("model_config", "base", "base | tiny (tiny = CPU-sized variant of bert/resnet50)",
                   fv)
     DEFINE_integer("seq_len", 128, "BERT sequence length", fv)

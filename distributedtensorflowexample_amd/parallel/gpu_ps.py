@@ -9,9 +9,16 @@ same semantics (lock-free apply unless ``use_locking``, ``fetch_add`` returning 
 other worker maps it over IPC, so a pull is a peer read and an apply a peer read-modify-write
 over xGMI, issued from the worker's own stream with no host copy of parameters or gradients.
 
-The TCP parameter server stays the control plane only: it carries the allocation's IPC handle
-and a detach counter (the owner frees the memory only after every other worker detached, so
-no peer is ever left with a dangling mapping).  Checkpoint / restore / readiness read and
+The TCP parameter server stays the control plane only: it carries the allocation's IPC handle,
+a detach counter (the owner frees the memory only after every other worker detached, so
+no peer is ever left with a dangling mapping; a peer that never detaches within the close
+timeout leaves the allocation alive until the owner's process exits) and a store generation.
+
+Failure semantics differ from the reference's in one respect: the variables live in the
+CHIEF's process, not on the ps task, so a chief failure loses them (a restarted chief
+restores the last checkpoint into a NEW store).  The chief bumps the generation at every
+``create()``; the other workers compare it periodically (``check_generation``) and exit
+non-zero instead of training on a stale mapping.  Checkpoint / restore / readiness read and
 write the GPU store (``read_all`` / ``assign`` / ``uninitialized``), so the Supervisor and
 Saver work unchanged.
 
@@ -31,6 +38,7 @@ from .ps import PSVariableStore
 
 HANDLE = "gpu_ps/ipc_handle"
 DETACHED = "gpu_ps/detached"
+GENERATION = "gpu_ps/generation"
 STEP_SLOT, INIT_SLOT = 0, 1
 
 
@@ -65,8 +73,11 @@ class GpuPSStore:
         nbytes = hip().GpuParamStore.handle_size()
         self._hwords = nbytes // 4
         self.ctl = PSVariableStore(ps_addresses, [(HANDLE, (self._hwords,), "float32"),
-                                                  (DETACHED, (), "int64")],
+                                                  (DETACHED, (), "int64"),
+                                                  (GENERATION, (), "int64")],
                                    connect_timeout=connect_timeout, setter=setter)
+        self.generation = None
+        self._kept_alive = None  # an allocation a peer never detached from (owner)
         self.n = mlp_step.NPARAM
         self._st = None
         self._owner = False
@@ -80,6 +91,7 @@ class GpuPSStore:
         self._owner = True
         h = np.frombuffer(self._st.handle(), dtype=np.float32).copy()
         self.ctl.assign({DETACHED: 0})
+        self.generation = self.ctl.fetch_add(GENERATION, 1) + 1
         self.ctl.assign({HANDLE: torch.from_numpy(h)})
         return self
 
@@ -95,9 +107,20 @@ class GpuPSStore:
             if time.time() - t0 > timeout:
                 raise TimeoutError("gpu_ps: the chief never published the store")
             time.sleep(poll)
+        self.generation = self.ctl.read_int(GENERATION)
         self._st = hip().GpuParamStore(self.device.index or 0, self.n, False)
         self._st.open(h)
         return self
+
+    def check_generation(self):
+        """Non-chief: raise if the chief re-created the store since ``lookup`` (its process
+        restarted: this worker's mapping no longer holds the global variables)."""
+        if self._owner or self.generation is None:
+            return
+        g = self.ctl.read_int(GENERATION)
+        if g != self.generation:
+            raise RuntimeError("gpu_ps: the chief re-created the parameter store (generation "
+                               "%d -> %d); this worker's mapping is stale" % (self.generation, g))
 
     def _ctrl(self, slot, delta):
         return int(self._st.fetch_add(slot, int(delta), stream_handle(self.device)))
@@ -171,16 +194,31 @@ class GpuPSStore:
         return out
 
     def close(self, timeout=60.0, poll=0.05):
-        """Detach (non-owner) or wait for every other worker to detach, then free (owner)."""
+        """Detach (non-owner) or wait for every other worker to detach, then free (owner).
+
+        Owner: the published handle is cleared FIRST, so a worker that looks the store up
+        late fails cleanly instead of mapping memory about to be freed.  If some peer has not
+        detached within ``timeout`` seconds the allocation is NOT freed (a peer may still be
+        pulling or applying through its mapping): it stays alive until this process exits,
+        with a warning."""
         if self._st is None:
             return
         torch.cuda.synchronize(self.device)
         if self._owner:
+            self.ctl.assign({HANDLE: torch.zeros(self._hwords)})
             t0 = time.time()
             while (self.ctl.read_int(DETACHED) < self.num_workers - 1
                    and time.time() - t0 < timeout):
                 time.sleep(poll)
-            self._st.close()
+            missing = self.num_workers - 1 - self.ctl.read_int(DETACHED)
+            if missing > 0:
+                import warnings
+
+                warnings.warn("gpu_ps: %d worker(s) never detached within %.0f s; the store "
+                              "stays allocated until this process exits" % (missing, timeout))
+                self._kept_alive = self._st
+            else:
+                self._st.close()
         else:
             self._st.close()
             self.ctl.fetch_add(DETACHED, 1)

@@ -100,6 +100,7 @@ class FusedMLPTrainer:
         self._pool = None
         self._ll = None   # granule buffer of the persistent engine (allocated on first use)
         self._ebase = 0   # epoch base of its next launch
+        self._unchecked = False  # a persistent launch whose hand-offs were not verified yet
 
     # -- state --------------------------------------------------------------
     @property
@@ -109,14 +110,23 @@ class FusedMLPTrainer:
             self.fused_comm is not None or self.factor_comm is not None
             or (self.allreduce is None and self.world_size == 1))
 
+    def _verified(self):
+        """Raise before parameters or stats of a persistent launch whose in-kernel hand-off
+        timed out are used (that launch writes zeros instead of valid parameters)."""
+        if self._unchecked:
+            self._unchecked = False
+            self.check()
+
     @property
     def params(self):
         """Current parameters (excludes a pending, not yet applied gradient)."""
+        self._verified()
         return self.bufs[self.cur]
 
     def flush(self):
         """Apply the pending update in place (DP: p -= lr/N * grad; pipelined: the last
         step's factors)."""
+        self._verified()
         if self.pending:
             if self.pipelined and self.factor_comm is not None:
                 xp, _ = self.batch((self.pos - 1) % self.nbatches)
@@ -142,6 +152,7 @@ class FusedMLPTrainer:
         evals).  The all-reduce engine's pending gradient is already reduced: applied to a
         copy.  A pending update of the pipelined exchange engines needs every rank's
         exchange: raises (call flush() on every rank instead)."""
+        self._verified()
         p = self.bufs[self.cur]
         if not self.pending:
             return p.clone()
@@ -313,6 +324,7 @@ class FusedMLPTrainer:
                          stream_handle(), 0 if trace is None else ptr(trace))
         self._ebase += steps + 1
         self.pos = (self.pos + steps) % self.nbatches
+        self._unchecked = True
 
     def check(self):
         """Raise if an in-kernel wait of the persistent engine ever timed out."""
@@ -363,6 +375,7 @@ class FusedMLPTrainer:
     # -- observability ------------------------------------------------------
     def stats(self, step=None):
         """(loss, accuracy) recorded by the kernel for ``step`` (default: last)."""
+        self._verified()
         if self.pipelined and self.pending:
             self.flush()  # the last step's record is written by its apply
         s = (self.global_step() - 1) if step is None else int(step)
@@ -371,6 +384,7 @@ class FusedMLPTrainer:
 
     def stats_range(self, start, end):
         """Loss/accuracy for steps [start, end) as a CPU tensor [n, 2]."""
+        self._verified()
         if self.pipelined and self.pending:
             self.flush()
         ring = self.ws.stats_ring

@@ -27,22 +27,29 @@ import time
 import numpy as np
 import torch
 
-from ..models import mlp as mlp_model
-from ..ops import mlp_step
+from .. import variables as vs
+from ..models.dense import make_ps_model
+from ..ops import mlp_step, nn
 from ..parallel.ps import PSVariableStore, replica_device_setter
 from ..utils.summary import FileWriter
 from .saver import FastSaver
 from .supervisor import Supervisor
 
 D, H, C = mlp_step.D, mlp_step.H, mlp_step.C
-GLOBAL_SPECS = [
-    ("global/dense/kernel", (D, H), "float32"),
-    ("global/dense/bias", (H,), "float32"),
-    ("global/dense_1/kernel", (H, C), "float32"),
-    ("global/dense_1/bias", (C,), "float32"),
-    ("global/global_step", (), "int64"),
-]
-TRAINABLE = [n for n, _, dt in GLOBAL_SPECS if dt == "float32"]
+
+
+def build_worker_variables(model, registry):
+    """worker.py:24-40: the global replica + global_step under ``global`` (on the ps), the
+    local replica under ``local`` (this worker's device; never saved).  Returns the
+    registry's ``get_vars('global', False)`` -- ps variables and saver var list -- and
+    ``get_vars('global')`` -- the trainable ones gradients are paired with (worker.py:76-77)."""
+    with registry.as_default():
+        with vs.variable_scope("global"):
+            model.build_variables()
+            vs.create_global_step()
+        with vs.variable_scope("local"):
+            model.build_variables()
+        return vs.get_vars("global", False), vs.get_vars("global")
 
 
 def tf_vars_to_flat(v, out):
@@ -74,15 +81,25 @@ class Worker:
         self.is_chief = self.task_index == 0
         self.batch_size = int(flags.batch_size)
         self.lr = float(flags.learning_rate)
-        self.use_fused = self.device.type == "cuda" and 1 <= self.batch_size <= mlp_step.MAX_BATCH
+        # the model declares its variables; everything below is derived from the registry
+        # (get_vars, utils.py:3-8) as in the reference: ps variables, gradient pairing, pull,
+        # init op and the saver's var list
+        self.model = make_ps_model(getattr(flags, "model", "mlp"),
+                                   getattr(flags, "hidden_units", ""),
+                                   getattr(flags, "activation", None))
+        self.registry = vs.VariableRegistry()
+        self.global_vars, self.trainable = build_worker_variables(self.model, self.registry)
+        self.step_name = next(v.name for v in self.global_vars if v.name.endswith("global_step"))
+        self.use_fused = (self.model.is_reference_mlp and self.device.type == "cuda"
+                          and 1 <= self.batch_size <= mlp_step.MAX_BATCH)
 
         # global variables on the ps (replica_device_setter(num_ps), worker.py:24-32), or with
         # --ps_device gpu in one GPU-resident store on the chief's GPU (parallel/gpu_ps.py)
         self.gpu_ps = str(getattr(flags, "ps_device", "cpu")) == "gpu"
         if self.gpu_ps:
             if not self.use_fused:
-                raise ValueError("--ps_device gpu needs a GPU worker and 1 <= batch_size <= %d"
-                                 % mlp_step.MAX_BATCH)
+                raise ValueError("--ps_device gpu needs the reference MLP on a GPU worker and "
+                                 "1 <= batch_size <= %d" % mlp_step.MAX_BATCH)
             if bool(getattr(flags, "sync_replicas", False)):
                 raise ValueError("--sync_replicas runs on the TCP parameter server "
                                  "(--ps_device cpu)")
@@ -91,39 +108,47 @@ class Worker:
             self.store = GpuPSStore(server.target, self.device, int(flags.num_workers),
                                     setter=replica_device_setter(len(server.target)))
         else:
-            self.store = PSVariableStore(server.target, GLOBAL_SPECS,
+            self.store = PSVariableStore(server.target, [v.spec for v in self.global_vars],
                                          setter=replica_device_setter(len(server.target)),
                                          rpc_timeout=float(getattr(flags, "ps_timeout_secs", 0)
                                                            or 0))
-        # local replica (worker.py:34-40): one flat buffer on this worker's device
-        self.params = torch.zeros(mlp_step.NPARAM, device=self.device)
-        self.grad = torch.zeros_like(self.params)
+        # local replica (worker.py:34-40): the fused MLP keeps one flat buffer on this
+        # worker's device; other models a list of [out, in] kernels / biases
         if self.use_fused:
+            self.params = torch.zeros(mlp_step.NPARAM, device=self.device)
+            self.grad = torch.zeros_like(self.params)
             self.ws = mlp_step.StepWorkspace(self.batch_size, self.device)
             self.grad_host = torch.empty(mlp_step.NPARAM, pin_memory=True)
             self.xb = torch.empty(self.batch_size, D, device=self.device)
             self.yb = torch.empty(self.batch_size, dtype=torch.int32, device=self.device)
+        else:
+            self.local = self.model.new_local(self.device)
+        self._test = None  # device-resident test set of the eval op (uploaded once)
         self.summary_writer = FileWriter(flags.logdir + "_%d" % self.task_index)
         # FastSaver over get_vars('global', False) (worker.py:102-103)
-        self.saver = FastSaver({n: None for n, _, _ in GLOBAL_SPECS}, assign=self.store.assign)
+        self.saver = FastSaver({v.name: None for v in self.global_vars}, assign=self.store.assign)
 
     # -- graph pieces (as ops) ---------------------------------------------
     def init_op(self):
-        """global_init_op: W ~ N(0, 1), b = 0, global_step = 0 (worker.py:51-53, 98-99)."""
-        p = mlp_model.init_params("cpu", seed=int(getattr(self.flags, "seed", 0)))
-        v = {k: t.contiguous() for k, t in flat_to_tf_vars(p).items()}
-        v["global/global_step"] = 0
-        self.store.assign(v)
+        """global_init_op over get_vars('global', False) (worker.py:98-99): kernels
+        N(0, 1), biases 0, global_step 0 -- each variable's declared initializer."""
+        seed = int(getattr(self.flags, "seed", 0))
+        self.store.assign({v.name: (0 if v.dtype != "float32" else v.initial_value(seed, i))
+                           for i, v in enumerate(self.global_vars)})
 
     def sync_op(self):
-        """worker.py:81-85: local <- global."""
+        """worker.py:81-85: local <- global for every trainable variable."""
         vals = self.store.pull()
         with torch.no_grad():
-            dev = {k: t.to(self.device, non_blocking=True) for k, t in vals.items()}
-            tf_vars_to_flat(dev, self.params)
+            if self.use_fused:
+                dev = {k: t.to(self.device, non_blocking=True) for k, t in vals.items()}
+                tf_vars_to_flat(dev, self.params)
+            else:
+                self.model.load_local(self.local, [vals[v.name] for v in self.trainable])
 
     def compute(self, batch_x, batch_y):
-        """Local forward/backward -> (grads in TF layout on CPU, loss, accuracy)."""
+        """Local forward/backward -> (grads {global name: TF-layout CPU tensor}, loss,
+        accuracy): the reference's zip(get_vars('global'), local gradients) pairing."""
         y = np.asarray(batch_y)
         labels = y.argmax(1) if y.ndim == 2 else y
         if self.use_fused and batch_x.shape[0] == self.batch_size:
@@ -134,13 +159,27 @@ class Worker:
             self.grad_host.copy_(self.grad)
             loss, acc = self.ws.stats[(self.ws.global_step() - 1) % self.ws.stats_ring].tolist()
             g = self.grad_host
-        else:
+        elif self.use_fused or self.model.is_reference_mlp:
             x = torch.from_numpy(np.ascontiguousarray(batch_x, np.float32))
-            g, loss_t, acc_t = mlp_step.reference_step(self.params.cpu(), x,
-                                                       torch.from_numpy(labels))
+            p = self.params.cpu() if hasattr(self, "params") else self._flat_local()
+            g, loss_t, acc_t = mlp_step.reference_step(p, x, torch.from_numpy(labels))
             loss, acc = float(loss_t), float(acc_t)
+        else:
+            x = torch.from_numpy(np.ascontiguousarray(batch_x, np.float32)).to(self.device)
+            lab = torch.from_numpy(labels.astype(np.int64)).to(self.device)
+            gs, loss, acc = self.model.grads(self.local, x, lab)
+            return ({v.name: t.cpu().contiguous() for v, t in zip(self.trainable, gs)},
+                    float(loss), float(acc))
         tfg = {k: t.contiguous() for k, t in flat_to_tf_vars(g.cpu()).items()}
         return tfg, float(loss), float(acc)
+
+    def _flat_local(self):
+        """Reference MLP on a non-fused device: the local replica as the flat layout."""
+        p = torch.empty(mlp_step.NPARAM)
+        W1t, b1, W2t, b2 = mlp_step.unflatten(p)
+        for dst, src in zip((W1t, b1, W2t, b2), self.local):
+            dst.copy_(src)
+        return p
 
     def compute_device(self, batch_x, batch_y):
         """Local forward/backward with the gradient left in ``self.grad`` on the device (GPU
@@ -168,12 +207,23 @@ class Worker:
         return float(loss), float(acc)
 
     def accuracy(self, images, labels):
-        """worker.py:87-90 on the local replica."""
-        x = torch.from_numpy(np.ascontiguousarray(images, np.float32)).to(self.device)
-        _, logits = mlp_step.reference_forward(self.params, x)
-        y = np.asarray(labels)
-        y = y.argmax(1) if y.ndim == 2 else y
-        return float((logits.argmax(1).cpu().numpy() == y).mean())
+        """worker.py:87-90,150-154 on the local replica: the 10k-image test accuracy.  The
+        test set is uploaded once and stays resident; on the GPU the forward is the
+        hand-written GEMM with the bias + sigmoid epilogue fused (nn.gemm / nn.dense)."""
+        if self._test is None or self._test[0] is not images:
+            x = torch.from_numpy(np.ascontiguousarray(images, np.float32)).to(self.device)
+            y = np.asarray(labels)
+            y = torch.from_numpy(y.argmax(1) if y.ndim == 2 else y).to(self.device)
+            self._test = (images, x, y)
+        _, x, y = self._test
+        with torch.no_grad():
+            if self.use_fused:
+                W1t, b1, W2t, b2 = mlp_step.unflatten(self.params)
+                h = nn.gemm(x, W1t, trans_b=True, bias=b1, act="sigmoid")
+                logits = nn.gemm(h, W2t, trans_b=True, bias=b2)
+            else:
+                logits = self.model.logits(self.local, x)
+            return float((logits.argmax(1) == y).float().mean())
 
     # -- training loop (worker.py:105-159) ------------------------------------
     def learn(self, dataset, max_steps=None, stop_after_secs=None):
@@ -187,7 +237,7 @@ class Worker:
         fl = self.flags
         sv = Supervisor(is_chief=self.is_chief, logdir=fl.logdir, saver=self.saver,
                         summary_writer=self.summary_writer, ready_op=self.store.uninitialized,
-                        global_step=lambda: self.store.read_int("global/global_step"),
+                        global_step=lambda: self.store.read_int(self.step_name),
                         save_model_secs=getattr(fl, "save_model_secs", 30),
                         save_summaries_secs=getattr(fl, "save_summaries_secs", 30),
                         init_op=self.init_op, local_init_op=None,
@@ -212,7 +262,7 @@ class Worker:
             # --sync_replicas (TF's SyncReplicasOptimizer): this worker's local step is the
             # global step it read; each push joins that step's round on the ps, which applies
             # the mean of replicas_to_aggregate gradients and advances global_step
-            local_step = self.store.read_int("global/global_step") if sync else 0
+            local_step = self.store.read_int(self.step_name) if sync else 0
             while not sv.should_stop():
                 if self.gpu_ps:
                     # the same four ops on the device, stream-ordered: pull (peer read), local
@@ -229,6 +279,8 @@ class Worker:
                     self.summary_writer.add_scalars({"loss": cost, "accuracy": acc}, step)
                     history.append((step, cost, acc))
                     local_steps += 1
+                    if local_steps % 1000 == 0:
+                        self.store.check_generation()  # the chief's store was not replaced
                     if step % log_every == 0 and step != 0:
                         elapsed = time.time() - start_time
                         self.log("step: {}\t| cost: {}\t| speed: {}step/sec".format(
@@ -253,7 +305,7 @@ class Worker:
                     local_step, _ = self.store.sync_push(grads, self.lr, replicas, local_step)
                 else:
                     self.store.push_apply(grads, self.lr, bool(getattr(fl, "use_locking", False)))
-                    step = self.store.fetch_add("global/global_step", 1)  # counter_op; old value
+                    step = self.store.fetch_add(self.step_name, 1)  # counter_op; old value
                 self.summary_writer.add_scalars({"loss": cost, "accuracy": acc}, step)
                 history.append((step, cost, acc))
                 local_steps += 1
