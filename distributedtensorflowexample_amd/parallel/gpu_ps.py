@@ -91,7 +91,11 @@ class GpuPSStore:
         self._owner = True
         h = np.frombuffer(self._st.handle(), dtype=np.float32).copy()
         self.ctl.assign({DETACHED: 0})
-        self.generation = self.ctl.fetch_add(GENERATION, 1) + 1
+        if GENERATION in self.ctl.uninitialized():  # first store of this ps
+            self.ctl.assign({GENERATION: 1})
+            self.generation = 1
+        else:  # a restarted chief: a new store generation
+            self.generation = self.ctl.fetch_add(GENERATION, 1) + 1
         self.ctl.assign({HANDLE: torch.from_numpy(h)})
         return self
 
@@ -196,8 +200,9 @@ class GpuPSStore:
     def close(self, timeout=60.0, poll=0.05):
         """Detach (non-owner) or wait for every other worker to detach, then free (owner).
 
-        Owner: the published handle is cleared FIRST, so a worker that looks the store up
-        late fails cleanly instead of mapping memory about to be freed.  If some peer has not
+        Owner: once the wait ends the published handle is cleared BEFORE anything is freed,
+        so a worker that looks the store up later fails cleanly instead of mapping memory
+        about to be freed (one that joins during the wait trains and detaches).  If some peer has not
         detached within ``timeout`` seconds the allocation is NOT freed (a peer may still be
         pulling or applying through its mapping): it stays alive until this process exits,
         with a warning."""
@@ -205,11 +210,12 @@ class GpuPSStore:
             return
         torch.cuda.synchronize(self.device)
         if self._owner:
-            self.ctl.assign({HANDLE: torch.zeros(self._hwords)})
             t0 = time.time()
             while (self.ctl.read_int(DETACHED) < self.num_workers - 1
                    and time.time() - t0 < timeout):
                 time.sleep(poll)
+            # late lookups from here on find no handle and fail cleanly
+            self.ctl.assign({HANDLE: torch.zeros(self._hwords)})
             missing = self.num_workers - 1 - self.ctl.read_int(DETACHED)
             if missing > 0:
                 import warnings
