@@ -92,6 +92,20 @@ def _timing_barrier(comm, local):
     return dist.barrier
 
 
+def _large_bucket_comm(a, comm, world, rank, dev, max_numel):
+    """BERT / ResNet gradient buckets: RCCL, or (``--comm auto``, N > 1) RCCL with the buckets
+    where the xGMI bandwidth-mode two-shot measured faster routed to it
+    (parallel/select.py::pick_large_allreduce, probe recorded in the JSON)."""
+    a.comm_probe = None
+    if world < 2 or world > 8 or SHARED_GPU or a.comm != "auto" or comm is None:
+        return comm
+    from distributedtensorflowexample_amd.parallel.select import HybridComm, pick_large_allreduce
+
+    c, a.comm_probe = pick_large_allreduce(comm, world, rank, dev, max_numel)
+    a.comm = "rccl+xgmi-bw" if isinstance(c, HybridComm) else "native"
+    return c
+
+
 def main():
     if os.environ.get("DTFX_WATCHDOG_S"):  # debugging aid: dump every thread's stack, then exit
         import faulthandler
@@ -148,7 +162,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.comm == "auto" and (a.model != "mlp" or world == 1):
+    if a.comm == "auto" and world == 1:
         a.comm = "native"
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
@@ -402,10 +416,11 @@ def bench_bert(a, world, rank, local, dev):
 
         comm = _native_comm(world, rank, dev, 160 << 20) if a.comm != "torch" else TorchComm()
     cfg = BertConfig.base() if a.bert_config == "base" else BertConfig.tiny()
+    rendezvous, comm = comm, _large_bucket_comm(a, comm, world, rank, dev, 24 << 20)
     tr = BertTrainer(cfg, a.bert_batch, a.seq_len, dev, comm=comm, data_seed=17 + rank)
     use_graph = not a.no_graph
     tr.run(a.warmup, use_graph)
-    barrier = _timing_barrier(comm, local) if world > 1 else None
+    barrier = _timing_barrier(rendezvous, local) if world > 1 else None
     if barrier:
         barrier()
     torch.cuda.synchronize()
@@ -430,8 +445,8 @@ def bench_bert(a, world, rank, local, dev):
             "value": round(seqs, 1), "unit": "sequences/sec", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic (random token ids / masked positions, device-resident), "
-                    "random-init weights",
+            "data": "synthetic MLM (Markov-chain token ids, 15% masked: 80% [MASK] / 10% "
+                    "random / 10% kept; 8 device-resident batches rotated), random-init weights",
             "config": {"model": "BERT-%s MLM (L%d H%d A%d, vocab %d)" % (
                 a.bert_config, cfg.layers, cfg.hidden, cfg.heads, cfg.vocab_size),
                 "global_batch": a.bert_batch * world, "per_gpu_batch": a.bert_batch,
@@ -439,6 +454,7 @@ def bench_bert(a, world, rank, local, dev):
                 "comm": _comm_label(a) if world > 1 else "none", "hipgraph": use_graph,
                 "optimizer": "AdamW (fused, f32 master)"},
             "model_tflops_per_gpu": round(tr.flops_per_step() / (ms * 1e-3) / 1e12, 1),
+            "comm_probe_us": getattr(a, "comm_probe", None),
             "final_loss": round(loss, 4), "final_mlm_acc": round(acc, 4),
         }), flush=True)
     if world > 1:
@@ -454,10 +470,11 @@ def bench_resnet(a, world, rank, local, dev):
         from distributedtensorflowexample_amd.parallel.comm import TorchComm
 
         comm = _native_comm(world, rank, dev, 32 << 20) if a.comm != "torch" else TorchComm()
+    rendezvous, comm = comm, _large_bucket_comm(a, comm, world, rank, dev, 8 << 20)
     tr = ResNetTrainer(a.resnet_batch, dev, comm=comm, image_size=a.image_size, data_seed=rank)
     use_graph = not a.no_graph
     tr.run(a.warmup, use_graph)
-    barrier = _timing_barrier(comm, local) if world > 1 else None
+    barrier = _timing_barrier(rendezvous, local) if world > 1 else None
     if barrier:
         barrier()
     torch.cuda.synchronize()
@@ -486,6 +503,7 @@ def bench_resnet(a, world, rank, local, dev):
                        "global_batch": a.resnet_batch * world, "per_gpu_batch": a.resnet_batch,
                        "seq_len": None, "parallelism": "dp%d" % world,
                        "comm": _comm_label(a) if world > 1 else "none", "hipgraph": use_graph},
+            "comm_probe_us": getattr(a, "comm_probe", None),
             "final_loss": round(loss, 4), "final_train_acc": round(acc, 4),
         }), flush=True)
     if world > 1:

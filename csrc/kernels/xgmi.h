@@ -17,10 +17,15 @@ void xgmi_allreduce_launch(float* g, long long n, int rank, int world, long long
                            const XgPeers& peers, unsigned* epochs, int* err, long long ticks,
                            hipStream_t stream);
 
-enum { XG_LL_PULL = 0, XG_LL_PUSH = 1, XG_LL_PUSH2 = 2 };
+enum { XG_LL_PULL = 0, XG_LL_PUSH = 1, XG_LL_PUSH2 = 2, XG_BW = 3 };
 
-// bytes of one rank's LL data region (the flag array follows it)
+// bytes of one rank's LL / BW data region (the flag array follows it)
 long long xgmi_ll_bytes(int mode, int world, long long S);
+
+// bandwidth-mode two-shot all-reduce for large buckets (f32 payload + release flags)
+void xgmi_bw_launch(float* g, long long n, int rank, int world, long long S, const XgPeers& peers,
+                    unsigned* epochs, int* err, long long ticks, hipStream_t stream,
+                    int blocks = XG_BLOCKS);
 
 void xgmi_ll_launch(int mode, float* g, long long n, int rank, int world, long long S,
                     const XgPeers& peers, unsigned* epochs, int* err, long long ticks,

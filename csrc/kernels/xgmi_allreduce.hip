@@ -26,6 +26,7 @@
 #include "xgmi.h"
 #include "xgmi_ll.h"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace dtfx {
@@ -83,8 +84,14 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(float* __restrict__
     if (t == 0) atomicExch(err, 1);
     return;  // g keeps the local gradient; the host sees err and raises
   }
-  // acquire: no load of peer data above this point, none served by a stale cache line
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // acquire: no load of peer data above this point, none served by a stale cache line.
+  // ONE lane per block (buffer_inv sc1 invalidates the CU's whole L1), the block held by a
+  // barrier until it completed
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
   // 4) sum the world slices in rank order (identical on every rank) into g
   for (long long i = lo + t; i < hi; i += blockDim.x) {
     f32x4 acc = ((const f32x4*)(peers.data[0] + par))[i];
@@ -194,9 +201,181 @@ __global__ __launch_bounds__(256) void xgmi_ll_kernel(float* __restrict__ g, lon
   if (t == 0) epochs[b] = epoch;
 }
 
+// ---------------------------------------------------------------------------
+// BW: bandwidth-mode two-shot all-reduce for LARGE buckets (BERT / ResNet gradients),
+// f32 payload (no epoch inside the data: every byte on the links is gradient) and
+// per-(phase, source, block) release flags.  Each rank owns chunk r = [r*cs, (r+1)*cs) of
+// the buffer (cs = ceil(n / W), float4-aligned):
+//   1) reduce-scatter: rank r stores its share of EVERY peer's chunk straight into that
+//      peer's receive slot rs(q, par, r) -- remote writes over the W-1 xGMI links in
+//      parallel -- then raises flag (0, r, b) at every peer;
+//   2) once the W-1 flags of its chunk are up, the owner sums the W contributions in rank
+//      order (bit-identical on every rank), keeps the result and stores it into every
+//      peer's gather region ag(q, par) (remote writes again), then raises flag (1, r, b);
+//   3) once the W-1 gather flags are up, every rank copies the other owners' chunks from
+//      its local gather region into g.
+// Per link and direction: 2 (W-1)/W * n * 4 bytes -- a ring's volume, but moved over all
+// W-1 links at once instead of one.  Block b handles sub-range b of every chunk; flags are
+// epoch counters owned by block b (device-resident epochs: graph replays advance them),
+// slots alternate by epoch parity (the flag protocol's argument: a rank reaches epoch e+2
+// only after every peer finished epoch e).  Every wait is bounded (s_memrealtime).
+// Region of one rank (floats): rs [2][W][CS] | ag [2][S]; flags [2 phases][W][XG_BLOCKS].
+// ---------------------------------------------------------------------------
+__host__ __device__ inline long long xg_bw_cs(long long S, int W) {
+  return ((S + W - 1) / W + 3) / 4 * 4;
+}
+
+template <int W>
+__global__ __launch_bounds__(512) void xgmi_bw_kernel(float* __restrict__ g, long long n, int rank,
+                                                      long long S, XgPeers peers,
+                                                      unsigned* __restrict__ epochs,
+                                                      int* __restrict__ err, long long ticks) {
+  __shared__ unsigned s_epoch;
+  __shared__ int s_fail;
+  const int b = blockIdx.x, t = threadIdx.x, nt = blockDim.x, nb = gridDim.x;
+  if (t == 0) {
+    s_epoch = epochs[b] + 1;
+    s_fail = 0;
+  }
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  const long long par = epoch & 1u;
+  const long long CS = xg_bw_cs(S, W);             // slot capacity of one chunk
+  const long long cs = ((n + W - 1) / W + 3) / 4 * 4;  // this call's chunk length
+  const long long per = ((cs + nb - 1) / nb + 3) / 4 * 4;
+  const long long lo = b * per;                    // sub-range [lo, hi) of every chunk
+  // elements of chunk c in this block's sub-range (<= 0: none)
+  auto chunk_hi = [&](int c) { return min(min(per, cs - lo), n - c * cs - lo); };
+  auto rs = [&](int q, int src) { return peers.data[q] + (par * W + src) * CS; };
+  auto ag = [&](int q) { return peers.data[q] + 2 * W * CS + par * S; };
+  auto flag = [&](int q, int phase, int src) {
+    return peers.flags[q] + (phase * W + src) * XG_BLOCKS + b;
+  };
+  // consumer: the W-1 polls, then ONE agent-scope acquire per block -- buffer_inv sc1
+  // invalidates the whole CU's L1, so one lane suffices (every thread of the 256 512-thread
+  // blocks fencing cost ~28 us per call, docs/COMM.md) -- and a barrier that holds the
+  // block until it has completed
+  auto wait_flags = [&](int phase) {
+    if (t < W && t != rank) {
+      const unsigned* f = flag(rank, phase, t);
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+          s_fail = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  };
+  // producer: every thread's stores acknowledged, then ONE system-scope release per block
+  // (with the explicit vmcnt wait the compiler may otherwise drop, MI355X_MICROARCH.md
+  // "Compiler hazard") and relaxed flag stores to the W-1 peers
+  auto raise_flags = [&](int phase) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int q = 0; q < W; ++q)
+        if (q != rank)
+          __hip_atomic_store(flag(q, phase, rank), epoch, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  };
+  // 1) reduce-scatter sends: my share of chunk q -> rs(q, par, me), all peers interleaved
+  //    so every link carries traffic at once
+  for (int k = 1; k < W; ++k) {
+    const int q = (rank + k) % W;
+    const long long m = chunk_hi(q);
+    if (m <= 0) continue;
+    const f32x4* src = (const f32x4*)(g + q * cs + lo);
+    f32x4* dst = (f32x4*)(rs(q, rank) + lo);
+    const long long m4 = m >> 2;
+    for (long long i = t; i < m4; i += nt) dst[i] = src[i];
+    for (long long i = 4 * m4 + t; i < m; i += nt) rs(q, rank)[lo + i] = g[q * cs + lo + i];
+  }
+  raise_flags(0);
+  wait_flags(0);
+  if (s_fail) {
+    if (t == 0) atomicExch(err, 1);
+    return;
+  }
+  // 2) owner: rank-ordered sum of my chunk's sub-range, kept in g and pushed to every peer
+  {
+    const long long m = chunk_hi(rank);
+    if (m > 0) {
+      float* mine = g + rank * cs + lo;
+      const long long m4 = m >> 2;
+      for (long long i = t; i < m4; i += nt) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          const f32x4 v = j == rank ? ((const f32x4*)mine)[i] : ((const f32x4*)(rs(rank, j) + lo))[i];
+          acc += v;
+        }
+        ((f32x4*)mine)[i] = acc;
+#pragma unroll
+        for (int k = 1; k < W; ++k) ((f32x4*)(ag((rank + k) % W) + rank * cs + lo))[i] = acc;
+      }
+      for (long long i = 4 * m4 + t; i < m; i += nt) {
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < W; ++j) acc += j == rank ? mine[i] : rs(rank, j)[lo + i];
+        mine[i] = acc;
+#pragma unroll
+        for (int k = 1; k < W; ++k) ag((rank + k) % W)[rank * cs + lo + i] = acc;
+      }
+    }
+  }
+  raise_flags(1);
+  wait_flags(1);
+  if (s_fail) {
+    if (t == 0) atomicExch(err, 1);
+    return;
+  }
+  // 3) all-gather receives: the other owners' chunks from my gather region
+  for (int k = 1; k < W; ++k) {
+    const int c = (rank + k) % W;
+    const long long m = chunk_hi(c);
+    if (m <= 0) continue;
+    const f32x4* src = (const f32x4*)(ag(rank) + c * cs + lo);
+    f32x4* dst = (f32x4*)(g + c * cs + lo);
+    const long long m4 = m >> 2;
+    for (long long i = t; i < m4; i += nt) dst[i] = src[i];
+    for (long long i = 4 * m4 + t; i < m; i += nt) g[c * cs + lo + i] = ag(rank)[c * cs + lo + i];
+  }
+  __syncthreads();
+  if (t == 0) epochs[b] = epoch;
+}
+
 long long xgmi_ll_bytes(int mode, int world, long long S) {
   if (mode == XG_LL_PULL) return 8LL * 2 * S;
+  if (mode == XG_BW) return 4LL * (2LL * world * xg_bw_cs(S, world) + 2 * S);
   return 8LL * (2LL * world * S + 2 * S);
+}
+
+void xgmi_bw_launch(float* g, long long n, int rank, int world, long long S, const XgPeers& peers,
+                    unsigned* epochs, int* err, long long ticks, hipStream_t stream, int blocks) {
+  const dim3 grid(blocks), block(512);
+#define DTFX_BW(WW)                                                                          \
+  case WW:                                                                                   \
+    hipLaunchKernelGGL((xgmi_bw_kernel<WW>), grid, block, 0, stream, g, n, rank, S, peers,   \
+                       epochs, err, ticks);                                                  \
+    break;
+  switch (world) {
+    DTFX_BW(1) DTFX_BW(2) DTFX_BW(3) DTFX_BW(4) DTFX_BW(5) DTFX_BW(6) DTFX_BW(7) DTFX_BW(8)
+    default:
+      throw std::runtime_error("xgmi bw protocol: world must be <= 8");
+  }
+#undef DTFX_BW
+  DTFX_HIP_CHECK(hipGetLastError());
 }
 
 void xgmi_ll_launch(int mode, float* g, long long n, int rank, int world, long long S,

@@ -34,8 +34,9 @@ class XgmiAllReduce {
     else if (protocol == "ll") mode_ = XG_LL_PULL;
     else if (protocol == "push") mode_ = XG_LL_PUSH;
     else if (protocol == "push2") mode_ = XG_LL_PUSH2;
-    else throw std::runtime_error("xgmi: protocol must be flag|ll|push|push2");
-    if (mode_ >= 0 && world > 8) throw std::runtime_error("xgmi: LL protocols support world <= 8");
+    else if (protocol == "bw") mode_ = XG_BW;
+    else throw std::runtime_error("xgmi: protocol must be flag|ll|push|push2|bw");
+    if (mode_ >= 0 && world > 8) throw std::runtime_error("xgmi: LL / bw protocols support world <= 8");
     if (world < 1 || world > XG_MAX_WORLD) throw std::runtime_error("xgmi: world must be 1..16");
     XG_CHECK(hipSetDevice(device));
     // ONE fine-grained uncached (MTYPE UC) allocation: data slots [2][S] f32 followed by the
@@ -62,6 +63,12 @@ class XgmiAllReduce {
   ~XgmiAllReduce() { close(); }
 
   size_t region_bytes() const { return bytes_; }
+  // bandwidth protocol: workgroups per call (<= XG_BLOCKS).  Fewer leave more CUs to the
+  // backward kernels an overlapped all-reduce runs beside; every rank must use the same.
+  void set_bw_blocks(int nb) {
+    if (nb < 1 || nb > XG_BLOCKS) throw std::runtime_error("xgmi: bw blocks must be 1..256");
+    bw_blocks_ = nb;
+  }
   long long slot_stride() const { return S_; }
 
   // Test harness ("peer buffers that are local allocations"): every rank's slot
@@ -112,7 +119,10 @@ class XgmiAllReduce {
     if (n > S_) throw std::runtime_error("xgmi: buffer larger than max_numel");
     if (g & 15) throw std::runtime_error("xgmi: buffer must be 16-byte aligned");
     const long long ticks = (long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
-    if (mode_ >= 0)
+    if (mode_ == XG_BW)
+      xgmi_bw_launch((float*)g, n, rank_, world_, S_, peers_, epochs_, err_, ticks,
+                     (hipStream_t)stream, bw_blocks_);
+    else if (mode_ >= 0)
       xgmi_ll_launch(mode_, (float*)g, n, rank_, world_, S_, peers_, epochs_, err_, ticks,
                      (hipStream_t)stream);
     else
@@ -211,7 +221,8 @@ class XgmiAllReduce {
  private:
   int rank_, world_, device_;
   long long S_;
-  int mode_ = -1;  // -1: flag protocol, else XG_LL_*
+  int mode_ = -1;  // -1: flag protocol, else XG_LL_* / XG_BW
+  int bw_blocks_ = XG_BLOCKS;
   long long data_bytes_ = 0;
   size_t bytes_ = 0;
   void* base_ = nullptr;
@@ -234,6 +245,7 @@ void register_xgmi(py::module_& m) {
            py::arg("world"), py::arg("device"), py::arg("max_numel"), py::arg("protocol"),
            py::arg("own_slots"))
       .def("region_bytes", &dtfx::XgmiAllReduce::region_bytes)
+      .def("set_bw_blocks", &dtfx::XgmiAllReduce::set_bw_blocks)
       .def("slot_stride", &dtfx::XgmiAllReduce::slot_stride)
       .def("open_local", &dtfx::XgmiAllReduce::open_local)
       .def("handle", &dtfx::XgmiAllReduce::handle)

@@ -309,18 +309,50 @@ class BertMLM:
                       gscale=gscale, step_ptr=step_ptr)
 
 
-def synthetic_mlm_batch(cfg: BertConfig, batch, seq, device, max_pred=None, seed=0, pad_to=64):
-    """Random token ids / segments / masked positions + labels of the MLM shape.
+MASK_ID = 103  # "[MASK]" in the BERT uncased vocabulary
 
-    Returns (ids, tt, mask_pos, labels, n_valid); the masked-position list is
-    padded to a multiple of ``pad_to`` with (position 0, label -100) rows."""
+
+def _markov_tokens(cfg, n, seq, g, sub_vocab=4096, fanout=4):
+    """Token sequences of a sparse first-order Markov chain over a sub-vocabulary: every
+    token has ``fanout`` possible successors with skewed probabilities, so a masked token
+    is partly predictable from its left neighbour (an MLM signal the model can learn, with
+    accuracy well below 1), unlike uniformly random ids."""
+    V = min(sub_vocab, cfg.vocab_size - 1000)
+    vocab = torch.randperm(cfg.vocab_size - 1000, generator=g)[:V] + 1000  # skip specials
+    succ = torch.randint(0, V, (V, fanout), generator=g)
+    probs = torch.tensor([0.55, 0.25, 0.12, 0.08][:fanout])
+    cur = torch.randint(0, V, (n,), generator=g)
+    out = torch.empty(n, seq, dtype=torch.long)
+    for t in range(seq):
+        out[:, t] = cur
+        pick = torch.multinomial(probs, n, replacement=True, generator=g)
+        cur = succ[cur, pick]
+    return vocab[out].to(torch.int32)
+
+
+def synthetic_mlm_batch(cfg: BertConfig, batch, seq, device, max_pred=None, seed=0, pad_to=64):
+    """One masked-LM batch of the pre-training shape (BERT's recipe on synthetic text).
+
+    Token ids come from a sparse Markov chain (``_markov_tokens``); 15 % of the positions
+    (``max_pred``) are selected per sequence and their ORIGINAL ids become the labels; the
+    inputs at those positions are replaced by ``[MASK]`` 80 % of the time, a random id
+    10 %, kept 10 %.  Returns (ids, tt, mask_pos, labels, n_valid); the masked-position
+    list is padded to a multiple of ``pad_to`` with (position 0, label -100) rows."""
     g = torch.Generator().manual_seed(seed)
     max_pred = max_pred or max(1, round(0.15 * seq))
-    ids = torch.randint(0, cfg.vocab_size, (batch, seq), generator=g, dtype=torch.int32)
+    ids = _markov_tokens(cfg, batch, seq, g) if cfg.vocab_size > 2000 else torch.randint(
+        1000 if cfg.vocab_size > 1100 else 0, cfg.vocab_size, (batch, seq), generator=g,
+        dtype=torch.int32)
     tt = (torch.arange(seq)[None, :] >= seq // 2).to(torch.int32).expand(batch, seq).contiguous()
     pos = torch.stack([torch.randperm(seq, generator=g)[:max_pred] for _ in range(batch)])
     flat = (pos + torch.arange(batch)[:, None] * seq).reshape(-1)
-    labels = torch.randint(0, cfg.vocab_size, (flat.numel(),), generator=g, dtype=torch.int32)
+    ids_flat = ids.reshape(-1)
+    labels = ids_flat[flat].clone()
+    r = torch.rand(flat.numel(), generator=g)
+    rand_ids = torch.randint(0, cfg.vocab_size, (flat.numel(),), generator=g, dtype=torch.int32)
+    mask_id = MASK_ID if cfg.vocab_size > MASK_ID else 0
+    ids_flat[flat] = torch.where(r < 0.8, torch.full_like(labels, mask_id),
+                                 torch.where(r < 0.9, rand_ids, labels))
     n_valid = flat.numel()
     pad = (-n_valid) % pad_to
     if pad:
@@ -328,6 +360,15 @@ def synthetic_mlm_batch(cfg: BertConfig, batch, seq, device, max_pred=None, seed
         labels = torch.cat([labels, torch.full((pad,), -100, dtype=torch.int32)])
     dev = torch.device(device)
     return ids.to(dev), tt.to(dev), flat.to(dev), labels.to(dev), n_valid
+
+
+def synthetic_mlm_pool(cfg: BertConfig, nbatches, batch, seq, device, seed=0, pad_to=64):
+    """``nbatches`` device-resident batches of ``synthetic_mlm_batch`` stacked on a leading
+    axis (a rotating dataset: the trainer copies batch k into its step's static buffers)."""
+    bs = [synthetic_mlm_batch(cfg, batch, seq, "cpu", seed=seed * 7919 + k, pad_to=pad_to)
+          for k in range(nbatches)]
+    dev = torch.device(device)
+    return tuple(torch.stack([b[i] for b in bs]).to(dev) for i in range(4)), bs[0][4]
 
 
 # ---------------------------------------------------------------------------

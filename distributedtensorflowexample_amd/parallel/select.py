@@ -268,3 +268,141 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
     if best == "allreduce":
         return "allreduce", ar_comm, probe
     return best, comms[best], probe
+
+
+class HybridComm:
+    """RCCL communicator with the large f32 all-reduces routed to the xGMI bandwidth-mode
+    two-shot (protocol "bw") where ``pick_large_allreduce`` measured it faster: tensors with
+    ``lo <= numel <= bw.max_numel``, 16-byte aligned, f32 and contiguous.  Everything else
+    (other collectives, dtypes, sizes) goes to RCCL.  Every rank holds the same ``lo``, so
+    both communicators see the same call sequence on every rank; both are graph-capturable.
+    """
+
+    def __init__(self, rccl, bw, lo):
+        self.rccl, self.bw, self.lo = rccl, bw, int(lo)
+        self.rank, self.world_size = rccl.rank, rccl.world_size
+        self.device = getattr(rccl, "device", bw.device)
+
+    def _use_bw(self, t):
+        return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+                and self.lo <= t.numel() <= self.bw.max_numel and t.data_ptr() % 16 == 0)
+
+    def allreduce_sum_(self, t):
+        return self.bw.allreduce_sum_(t) if self._use_bw(t) else self.rccl.allreduce_sum_(t)
+
+    def allreduce_avg_(self, t):
+        if self._use_bw(t):
+            self.bw.allreduce_sum_(t)
+            return t.div_(self.world_size)
+        return self.rccl.allreduce_avg_(t)
+
+    def check(self):
+        self.bw.check()
+
+    def failed(self):
+        return self.bw.failed()
+
+    def __getattr__(self, name):  # broadcast_, reduce_scatter, all_gather, barrier, ...
+        return getattr(self.rccl, name)
+
+    def destroy(self):
+        self.bw.destroy()
+
+
+def pick_large_allreduce(rccl, world, rank, dev, max_numel, sizes=None, iters=10,
+                         xgmi_key="dtfx/xgmi/bw", timeout_s=2.0, bw_blocks=None):
+    """Bucketed all-reduce backend for the large gradients (BERT / ResNet buckets): the xGMI
+    bandwidth-mode two-shot is created on every rank (or not at all), verified against RCCL
+    on random buckets, and timed against RCCL inside captured hipGraphs at each size in
+    ``sizes`` (max over ranks, best of three).  Returns ``(HybridComm, probe)`` routing every
+    bucket of at least the smallest size from which bw won at every larger probed size, or
+    ``(rccl, probe)`` when it never wins.  The same decision on every rank."""
+    max_numel = int(max_numel)
+    sizes = [s for s in (sizes or (1 << 18, 1 << 20, 1 << 22, 7 << 20, 1 << 24))
+             if s <= max_numel] or [max_numel]
+
+    def agree(ok):
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    bw, err = None, ""
+    try:
+        bw = XgmiComm(rank, world, max_numel, device=dev, key=xgmi_key, protocol="bw",
+                      timeout_s=timeout_s, bw_blocks=bw_blocks)
+    except Exception as e:  # no IPC / peer mapping on this node
+        err = repr(e)
+    if not agree(bw is not None):
+        if bw is not None:
+            bw.destroy()
+        if rank == 0:
+            print("[bench] xgmi-bw unavailable (%s): RCCL for every bucket" % err, file=sys.stderr)
+        return rccl, None
+    g = torch.Generator(device="cpu").manual_seed(2000 + rank)
+    ok = True
+    for n in (sizes[0] + 3, sizes[-1]):  # (a ragged size too) -- same collectives on every rank
+        base = (torch.randn(n, generator=g) * (1 + rank)).to(dev)
+        ra, xa = base.clone(), base.clone()
+        rccl.allreduce_sum_(ra)
+        torch.cuda.synchronize()
+        dist.barrier()
+        try:
+            bw.allreduce_sum_(xa)
+            bad = bw.failed()
+        except Exception as e:  # noqa: BLE001
+            bad, err = True, repr(e)
+        ok &= not bad and bool(((ra - xa).abs().max() <= 1e-5 * ra.abs().max()).item())
+        del base, ra, xa
+    if not agree(ok):
+        if rank == 0:
+            print("[bench] xgmi-bw failed verification (%s): RCCL" % err, file=sys.stderr)
+        bw.destroy()
+        return rccl, None
+
+    def timed(c, buf):
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            c.allreduce_sum_(buf)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for _ in range(iters):
+                c.allreduce_sum_(buf)
+        gr.replay()
+        torch.cuda.synchronize()
+        best = float("inf")
+        for _ in range(3):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            gr.replay()
+            torch.cuda.synchronize()
+            dt = torch.tensor([(time.perf_counter() - t0) / iters * 1e6], dtype=torch.float64)
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            best = min(best, float(dt.item()))
+        return best
+
+    probe = {}
+    for n in sizes:
+        buf = torch.zeros(n, device=dev)
+        probe[n] = {"rccl": round(timed(rccl, buf), 1), "bw": round(timed(bw, buf), 1)}
+        del buf
+    if not agree(not bw.failed()):
+        probe["bw_timed_out"] = True
+        bw.destroy()
+        return rccl, probe
+    lo = None
+    for n in reversed(sizes):  # smallest size from which bw wins at every larger size
+        if probe[n]["bw"] < probe[n]["rccl"]:
+            lo = n
+        else:
+            break
+    if rank == 0:
+        print("[bench] large all-reduce probe (us/call, max over ranks): %s -> %s"
+              % (probe, "xgmi-bw from %d elements" % lo if lo else "rccl"), file=sys.stderr)
+    if lo is None:
+        bw.destroy()
+        return rccl, probe
+    return HybridComm(rccl, bw, lo), probe

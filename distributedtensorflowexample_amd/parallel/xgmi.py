@@ -1,13 +1,15 @@
-"""xGMI one-shot all-reduce communicator (small buckets; opt-in).
+"""xGMI peer-memory all-reduce communicators: LL one-/two-shot for small buckets and the
+bandwidth-mode two-shot ("bw") for large ones; ``HybridComm`` routes by bucket size.
 
 Wraps ``csrc/kernels/xgmi_allreduce.hip`` / ``xgmi_comm.cpp``: every rank
 exports an uncached IPC slot, the handles are exchanged through the
 torch.distributed TCP store, and each ``allreduce_sum_`` is ONE kernel that
 publishes, flags and sums straight from peer memory over the direct xGMI
 links (protocol: ``docs/COMM.md``).  Graph-capturable (epochs live on the
-device).  Only f32, and only up to ``max_numel`` elements: it exists for the
-latency-bound 318 KB gradient of the MNIST MLP; RCCL (``comm.NativeComm``)
-remains the default and the path for large buckets.
+device).  Only f32, and only up to ``max_numel`` elements.  The LL protocols exist for the
+latency-bound 318 KB gradient of the MNIST MLP; the "bw" protocol (f32 payload, per-block
+release flags, all W-1 links at once) for large buckets, where it is selected against RCCL
+per bucket size at startup (``select.pick_large_allreduce`` -> ``select.HybridComm``).
 """
 from __future__ import annotations
 
@@ -19,7 +21,7 @@ from ..ops import hip
 
 class XgmiComm:
     def __init__(self, rank, world_size, max_numel, device=None, store=None,
-                 key="dtfx/xgmi/0", timeout_s=2.0, protocol=None):
+                 key="dtfx/xgmi/0", timeout_s=2.0, protocol=None, bw_blocks=None):
         self.rank, self.world_size = int(rank), int(world_size)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None
                                    else torch.device(device).index)
@@ -49,10 +51,12 @@ class XgmiComm:
             self._h.close()
             raise RuntimeError("xgmi: ranks %s could not export their buffers" % missing)
         self._h.open(handles)
+        if bw_blocks is not None:
+            self._h.set_bw_blocks(int(bw_blocks))
 
     @classmethod
     def with_local_peers(cls, rank, world_size, max_numel, regions=None, device=None,
-                         protocol="push", timeout_s=2.0):
+                         protocol="push", timeout_s=2.0, bw_blocks=None):
         """Test harness ("peer buffers that are local allocations"): a communicator
         for ``rank`` of a ``world_size``-rank job whose peer slot regions are plain allocations
         on this device -- ``regions`` (one int64 tensor per rank, ``region_words`` long) or new
@@ -76,6 +80,8 @@ class XgmiComm:
                 r.dtype != torch.int64 or r.numel() < words or not r.is_cuda for r in regions):
             raise ValueError("need %d int64 device regions of >= %d words" % (world_size, words))
         self._h.open_local([r.data_ptr() for r in regions])
+        if bw_blocks is not None:
+            self._h.set_bw_blocks(int(bw_blocks))
         self.regions = regions
         return self, regions
 

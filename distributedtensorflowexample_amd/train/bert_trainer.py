@@ -20,13 +20,13 @@ import os
 
 import torch
 
-from ..models.bert import BertConfig, BertMLM, synthetic_mlm_batch
+from ..models.bert import BertConfig, BertMLM, synthetic_mlm_pool
 from ..ops import optim as OPT
 
 
 class BertTrainer:
     def __init__(self, cfg: BertConfig, batch, seq, device, comm=None, lr=1e-4, seed=0,
-                 overlap=True, weight_decay=0.01, data_seed=None):
+                 overlap=True, weight_decay=0.01, data_seed=None, data_batches=8):
         self.cfg, self.batch, self.seq = cfg, batch, seq
         self.device = torch.device(device)
         self.comm = comm
@@ -44,8 +44,11 @@ class BertTrainer:
         if self.gpu and os.environ.get("DTFX_BERT_WSTREAM", "1") != "0":
             self.model.wgrad_stream = torch.cuda.Stream(self.device)
             self.model.wgrad_sync_buckets = self.world > 1
-        self.data = synthetic_mlm_batch(cfg, batch, seq, device,
-                                        seed=(data_seed if data_seed is not None else 17))
+        # a rotating dataset of `data_batches` device-resident MLM batches: before every step
+        # (eager or graph replay) batch k is copied into the static buffers the step reads
+        self.pool, nv = synthetic_mlm_pool(cfg, data_batches, batch, seq, device,
+                                           seed=(data_seed if data_seed is not None else 17))
+        self.data = tuple(t[0].clone() for t in self.pool) + (nv,)
         # the embedding bucket (0) is the LAST gradient backward produces: its all-reduce
         # (94 MB of f32 word-embedding gradient for BERT-base) is the one exchange that
         # nothing overlaps, so AdamW of every other bucket runs while it is in flight
@@ -87,7 +90,13 @@ class BertTrainer:
         OPT.counter_add_(self.step_t, 1)
         return loss, acc
 
+    def _load_batch(self):
+        k = self.step_count % self.pool[0].shape[0]
+        for dst, src in zip(self.data[:4], self.pool):
+            dst.copy_(src[k], non_blocking=True)
+
     def step(self, use_graph=False):
+        self._load_batch()
         if not use_graph:
             self.last = self._step_body()
         elif self.graph is None:

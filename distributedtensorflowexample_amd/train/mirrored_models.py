@@ -42,6 +42,13 @@ def train_model_mirrored(flags, log=print):
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         comm = NativeComm.from_process_group() if world > 1 else None
+        if comm is not None and 2 <= world <= 8 and os.environ.get("DTFX_COMM_LARGE", "auto") == "auto":
+            # large gradient buckets: RCCL, or the xGMI bandwidth-mode two-shot from the bucket
+            # size where it measured faster (the same decision on every rank)
+            from ..parallel.select import pick_large_allreduce
+
+            comm, _ = pick_large_allreduce(comm, world, rank, dev,
+                                           (24 << 20) if flags.model == "bert" else (8 << 20))
     else:
         dev = torch.device("cpu")
         comm = TorchComm() if world > 1 else None

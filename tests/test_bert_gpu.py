@@ -59,7 +59,7 @@ def test_bert_base_step_runs(gpu):
 def test_bert_fits_fixed_batch(gpu):
     from distributedtensorflowexample_amd.train.bert_trainer import BertTrainer
 
-    tr = BertTrainer(BertConfig.tiny(), 8, 128, gpu, lr=2e-3)
+    tr = BertTrainer(BertConfig.tiny(), 8, 128, gpu, lr=2e-3, data_batches=1)
     tr.run(1)
     l0, _ = tr.stats()
     tr.run(30, use_graph=True)

@@ -242,3 +242,55 @@ def test_factor_mlp_exchange_matches_allreduce_engine(gpu, world, B, pipeline):
         p.join(60)
     for r, ok, msg in res:
         assert ok, (r, msg)
+
+
+def _large_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from distributedtensorflowexample_amd.parallel.select import HybridComm, pick_large_allreduce
+        from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+        # stand-in for RCCL (two ranks cannot share a GPU under RCCL): the flag protocol
+        ref = XgmiComm(rank, world, 1 << 22, device="cuda:0", key="dtfx/xgmi/lref",
+                       protocol="flag", timeout_s=30.0)
+        comm, probe = pick_large_allreduce(ref, world, rank, torch.device("cuda:0"), 1 << 22,
+                                           sizes=(1 << 18, 1 << 21), timeout_s=30.0)
+        ok = probe is not None and all(("bw" in v and "rccl" in v) for k, v in probe.items()
+                                       if k != "bw_timed_out")
+        g = torch.Generator().manual_seed(9)
+        for n in (1000, 1 << 18, (1 << 21) + 5, 3 << 20):  # routed by size, ragged included
+            vals = [torch.randn(n, generator=g) for _ in range(world)]
+            t = vals[rank].cuda()
+            comm.allreduce_sum_(t)
+            torch.cuda.synchronize()
+            exp = vals[0] + vals[1]
+            ok &= bool((t.cpu() - exp).abs().max() <= 1e-5)
+        if isinstance(comm, HybridComm):
+            comm.check()
+        q.put((rank, ok, str(probe)))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+
+        q.put((rank, False, traceback.format_exc()[-1500:]))
+
+
+def test_large_bucket_selection_two_ranks(gpu):
+    """pick_large_allreduce on two ranks sharing the GPU: the bandwidth-mode two-shot is
+    created, verified and timed against the reference communicator per bucket size, and the
+    returned communicator (HybridComm or the reference) sums buckets of every size exactly."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_large_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    for r, ok, msg in res:
+        assert ok, (r, msg)

@@ -507,3 +507,65 @@ def test_timeout_when_a_peer_word_is_missing(gpu):
     comm.allreduce_sum_(t)
     assert comm.failed()
     comm.destroy()
+
+
+# ---------------------------------------------------------------------------------------
+# bandwidth-mode two-shot all-reduce (large buckets): f32 payload + per-block release flags
+# ---------------------------------------------------------------------------------------
+def _bw_check(world, rank, n, S_numel, dev):
+    from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+    comm, regs = XgmiComm.with_local_peers(rank, world, S_numel, device=dev, protocol="bw")
+    S = comm.slot_stride
+    CS = ((S + world - 1) // world + 3) // 4 * 4
+    cs = ((n + world - 1) // world + 3) // 4 * 4
+    flags0 = 2 * world * CS + 2 * S  # int32 index of the flag array
+    m = [max(0, min(cs, n - c * cs)) for c in range(world)]
+    g = torch.Generator().manual_seed(31 * world + rank + n)
+    for epoch in (1, 2, 3):
+        par = epoch & 1
+        vals = [torch.randn(n, generator=g) * (j + 1) for j in range(world)]
+        exp = _ordered_sum(vals)
+        vd = [v.to(dev) for v in vals]
+        ed = exp.to(dev)
+        f = regs[rank].view(torch.float32)
+        fl = regs[rank].view(torch.int32)
+        for j in range(world):
+            if j == rank:
+                continue
+            o = (par * world + j) * CS
+            f[o:o + m[rank]] = vd[j][rank * cs:rank * cs + m[rank]]
+            fl[flags0 + (0 * world + j) * XG_BLOCKS:flags0 + (0 * world + j + 1) * XG_BLOCKS] = epoch
+            fl[flags0 + (1 * world + j) * XG_BLOCKS:flags0 + (1 * world + j + 1) * XG_BLOCKS] = epoch
+        ag = 2 * world * CS + par * S
+        for c in range(world):
+            if c != rank:
+                f[ag + c * cs:ag + c * cs + m[c]] = ed[c * cs:c * cs + m[c]]
+        t = vd[rank].clone()
+        torch.cuda.synchronize()
+        comm.allreduce_sum_(t)
+        comm.check()
+        assert torch.equal(t.cpu(), exp), (world, rank, n, epoch,
+                                           float((t.cpu() - exp).abs().max()))
+        for q in range(world):  # what every peer received from me
+            if q == rank:
+                continue
+            fq, flq = regs[q].view(torch.float32), regs[q].view(torch.int32)
+            o = (par * world + rank) * CS
+            assert torch.equal(fq[o:o + m[q]], vd[rank][q * cs:q * cs + m[q]]), (q, epoch)
+            assert torch.equal(fq[ag + rank * cs:ag + rank * cs + m[rank]],
+                               ed[rank * cs:rank * cs + m[rank]]), (q, epoch)
+            for ph in (0, 1):
+                a = flags0 + (ph * world + rank) * XG_BLOCKS
+                assert bool((flq[a:a + XG_BLOCKS] == epoch).all()), (q, ph, epoch)
+    comm.destroy()
+
+
+@pytest.mark.parametrize("world", WORLDS)
+def test_bw_allreduce_simulated_peers(gpu, world):
+    for rank in _ranks(world):
+        # a BERT-layer-sized bucket, a size that is not a multiple of W * 4 or of the block
+        # split, and a bucket smaller than the communicator's capacity
+        for n, cap in ((7 * 1024 * 1024 + 13, 7 * 1024 * 1024 + 13), (100003, 100003),
+                       (5000, 1 << 20)):
+            _bw_check(world, rank, n, cap, gpu)
