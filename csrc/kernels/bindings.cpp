@@ -26,6 +26,9 @@ long long mlp_workspace_floats(int);
 void mlp_fwdapply_launch(const float*, float*, float, const float*, const float*, float*, int*,
                          float*, int, int, int, hipStream_t);
 void mlp_head2_launch(const float*, const int*, float*, int, hipStream_t);
+void mlp_pipelined_trace_launch(const float*, float*, float, const float*, const float*,
+                                const int*, float*, int*, float*, int, int, hipStream_t,
+                                unsigned long long*, unsigned long long*);
 void mlp_run_pipelined_launch(float*, float*, int, int, float, const float*, const int*, int, int,
                               int, float*, int*, float*, int, int, hipStream_t);
 long long mlp_persistent_ll_words();
@@ -96,6 +99,16 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("p_old"), py::arg("p_new"), py::arg("lr"), py::arg("x_prev"), py::arg("x"),
      py::arg("ws"), py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"),
      py::arg("stats_on"), py::arg("stream"));
+  m.def("mlp_pipelined_trace", [](uintptr_t p_old, uintptr_t p_new, float lr, uintptr_t x_prev,
+                                   uintptr_t x, uintptr_t lab, uintptr_t ws, uintptr_t ctr,
+                                   uintptr_t stats, int ring, int B, uintptr_t s, uintptr_t trf,
+                                   uintptr_t trh) {
+    dtfx::mlp_pipelined_trace_launch(P<const float>(p_old), P<float>(p_new), lr,
+                                     P<const float>(x_prev), P<const float>(x), P<const int>(lab),
+                                     P<float>(ws), P<int>(ctr), P<float>(stats), ring, B, S(s),
+                                     reinterpret_cast<unsigned long long*>(trf),
+                                     reinterpret_cast<unsigned long long*>(trh));
+  });
   m.def("mlp_head2", [](uintptr_t p, uintptr_t lab, uintptr_t ws, int B, uintptr_t s) {
     dtfx::mlp_head2_launch(P<const float>(p), P<const int>(lab), P<float>(ws), B, S(s));
   }, py::arg("p"), py::arg("labels"), py::arg("ws"), py::arg("B"), py::arg("stream"));

@@ -572,11 +572,17 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
 // exchanged in LL words with the XW - 1 peers (xg_exchange, epoch slot bid*4 + wave) and
 // summed in rank order before the apply -- the all-reduce of the 3-launch fused engine,
 // moved into the next step's first launch (2 launches per data-parallel step).
-template <int NGT, int XW = 0>
+// TRACE (probe builds, tools/probes/mlp_pipelined_trace.py): per wave, s_memrealtime stamps
+// 0 entry, 1 phase-A operands landed, 2 W1 tile applied (after the barrier), 3 slab stored;
+// small-parameter blocks: 0 entry, 3 done.  tr: [blocks * 4 waves][4].
+template <int NGT, int XW = 0, bool TRACE = false>
 __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
     const float* __restrict__ x_prev, const float* __restrict__ x, Bufs w, int* __restrict__ ctr,
-    float* __restrict__ stats, int stats_ring, int B, int stats_on, MlpXg xg) {
+    float* __restrict__ stats, int stats_ring, int B, int stats_on, MlpXg xg,
+    unsigned long long* __restrict__ tr = nullptr) {
+  unsigned long long* trw = TRACE ? tr + (size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 : nullptr;
+  if (TRACE) trace_stamp(trw, 0);
   const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
   const int NG = NGT > 0 ? NGT : BP / 16;
   const int RT = (B + 15) >> 4;
@@ -588,6 +594,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     const int jt = bid - HT * KS2;
     wgrad_small<true, NGT, XW>(jt, wave, lane, MLP_XG_SMALL_EPOCH + jt * 4 + wave, p_new, lr,
                                nullptr, w, ctr, stats, stats_ring, B, xg, p_old, stats_on);
+    if (TRACE) trace_stamp(trw, 3);
     return;
   }
   constexpr int LW = KW2 + 4;  // LDS row pitch (floats)
@@ -639,6 +646,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
       pw[i] = p_old[OFF_W1 + (size_t)(j < H ? j : H - 1) * D + fc];
     }
     __builtin_amdgcn_sched_barrier(0);  // all loads in flight together
+    if (TRACE) trace_stamp(trw, 1);
     f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
     for (int g = 0; g < MAXG; ++g) {
@@ -679,6 +687,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     }
   }
   __syncthreads();
+  if (TRACE) trace_stamp(trw, 2);
 
   // ---- phase B: z1 partial over the block's 56 features, row tiles rt = wave, wave + 4, ..
   // lane (r, q): A = x[rt*16 + r][f0 + 16g + 4q + e], B = Wt[r][16g + 4q + e]; group 3 has
@@ -719,6 +728,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) out[(size_t)i * HP] = acc0[i] + acc1[i];
   }
+  if (TRACE) trace_stamp(trw, 3);
 }
 
 
@@ -1189,6 +1199,23 @@ void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const fl
   }
 #undef DTFX_FXW
 #undef DTFX_FX
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// Probe: one pipelined step with in-kernel stamps in both launches (trf: 105 * 4 * 4,
+// trh: B * 4 entries); batch 100 only.
+void mlp_pipelined_trace_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
+                                const float* x, const int* labels, float* ws, int* ctr,
+                                float* stats, int stats_ring, int B, hipStream_t stream,
+                                unsigned long long* trf, unsigned long long* trh) {
+  using namespace mlp;
+  check_b(B);
+  if ((B + 15) / 16 != 7) throw std::runtime_error("mlp_pipelined_trace: batch 97..112 only");
+  const Bufs w = make_bufs(ws, B);
+  hipLaunchKernelGGL((mlp_fwdapply_kernel<7, 0, true>), dim3(HT * KS2 + HT), dim3(256), 0, stream,
+                     p_old, p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B, 1, MlpXg{}, trf);
+  hipLaunchKernelGGL((mlp_head_kernel<false, true, 0, KS2>), dim3(B), dim3(64), 0, stream, p_new,
+                     p_new, 0.f, nullptr, labels, w, B, trh, MlpXg{}, nullptr);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
