@@ -657,6 +657,94 @@ class PSClient {
     if (lost) throw PSConnectionLost(first_error);
     if (!first_error.empty()) throw std::runtime_error(first_error);
   }
+  // One worker step's ps traffic in ONE network round trip per task: push + apply (this
+  // worker's gradients), fetch_add on global_step, and the pull of the parameters for the next
+  // step, pipelined on each task's connection.  The ps serves a connection's requests in
+  // order, so it applies the push, then advances the step, then reads the variables --
+  // exactly the reference's train_op -> counter_op -> sync_op sequence (worker.py:135-141,
+  // 131), three round trips there.  Returns the old step value.
+  int64_t push_step_pull(std::vector<int64_t> hs, std::vector<uintptr_t> ptrs,
+                         std::vector<size_t> sizes, float lr, bool locking, int64_t step_h,
+                         int64_t delta, std::vector<int64_t> phs, std::vector<uintptr_t> pptrs,
+                         std::vector<size_t> psizes) {
+    if (hs.size() != ptrs.size() || hs.size() != sizes.size() || phs.size() != pptrs.size() ||
+        phs.size() != psizes.size())
+      throw std::runtime_error("ps push_step_pull: argument lengths differ");
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> lk(mu_);
+    const size_t T = fds_.size(), step_task = task_of(step_h);
+    std::vector<std::vector<size_t>> per(T), pper(T);
+    for (size_t k = 0; k < hs.size(); ++k) per[task_of(hs[k])].push_back(k);
+    for (size_t k = 0; k < phs.size(); ++k) pper[task_of(phs[k])].push_back(k);
+    for (size_t t = 0; t < T; ++t) {
+      std::string batch;  // the task's requests, framed, sent with one write
+      auto frame = [&](const Writer& w) {
+        const uint32_t len = static_cast<uint32_t>(w.b.size());
+        batch.append(reinterpret_cast<const char*>(&len), 4);
+        batch.append(w.b);
+      };
+      if (!per[t].empty()) {
+        Writer w;
+        w.put<uint8_t>(OP_PUSH_APPLY);
+        w.put<float>(lr);
+        w.put<uint8_t>(locking ? 1 : 0);
+        w.put<uint32_t>(static_cast<uint32_t>(per[t].size()));
+        for (size_t k : per[t]) w.put<uint32_t>(static_cast<uint32_t>(hs[k]));
+        for (size_t k : per[t]) w.raw(reinterpret_cast<const void*>(ptrs[k]), sizes[k]);
+        frame(w);
+      }
+      if (t == step_task) {
+        Writer w;
+        w.put<uint8_t>(OP_FETCH_ADD);
+        w.put<uint32_t>(static_cast<uint32_t>(step_h));
+        w.put<int64_t>(delta);
+        frame(w);
+      }
+      if (!pper[t].empty()) {
+        Writer w;
+        w.put<uint8_t>(OP_PULL);
+        w.put<uint32_t>(static_cast<uint32_t>(pper[t].size()));
+        for (size_t k : pper[t]) w.put<uint32_t>(static_cast<uint32_t>(phs[k]));
+        frame(w);
+      }
+      if (!batch.empty() && !write_full(fds_[t], batch.data(), batch.size()))
+        throw PSConnectionLost("ps: connection to " + addrs_[t] + " lost (send)");
+    }
+    int64_t old = -1;
+    std::string first_error;  // drain every reply first (see pull)
+    bool lost = false;
+    for (size_t t = 0; t < T; ++t) {
+      const int n_req = (per[t].empty() ? 0 : 1) + (t == step_task ? 1 : 0) + (pper[t].empty() ? 0 : 1);
+      for (int q = 0; q < n_req; ++q) {
+        try {
+          std::string resp = recv(static_cast<int>(t));
+          const bool is_push = q == 0 && !per[t].empty();
+          const bool is_step = t == step_task && q == (per[t].empty() ? 0 : 1);
+          if (is_push) continue;
+          if (is_step) {
+            Reader r{resp.data(), resp.data() + resp.size()};
+            old = r.get<int64_t>();
+            continue;
+          }
+          size_t off = 0;
+          for (size_t k : pper[t]) {
+            if (off + psizes[k] > resp.size()) throw std::runtime_error("ps pull: short response");
+            std::memcpy(reinterpret_cast<void*>(pptrs[k]), resp.data() + off, psizes[k]);
+            off += psizes[k];
+          }
+        } catch (const PSConnectionLost& e) {
+          if (first_error.empty()) first_error = e.what();
+          lost = true;
+          break;  // nothing more arrives on a lost connection
+        } catch (const std::exception& e) {
+          if (first_error.empty()) first_error = e.what();
+        }
+      }
+    }
+    if (lost) throw PSConnectionLost(first_error);
+    if (!first_error.empty()) throw std::runtime_error(first_error);
+    return old;
+  }
   // Synchronous-replicas push (see SYNC_PUSH): every task gets its variables' gradients; the
   // task holding `step_handle` (global_step) advances it with each applied round.  Returns
   // (round after the push -- the new global step --, applied (False: dropped as stale)).
@@ -882,6 +970,10 @@ void register_ps(py::module_& m) {
            py::arg("sizes"), py::arg("lr"), py::arg("replicas_to_aggregate"),
            py::arg("local_step"), py::arg("step_handle"), py::arg("timeout_s") = 600.0)
       .def("fetch_add", &PSClient::fetch_add)
+      .def("push_step_pull", &PSClient::push_step_pull, py::arg("handles"), py::arg("ptrs"),
+           py::arg("sizes"), py::arg("lr"), py::arg("use_locking"), py::arg("step_handle"),
+           py::arg("delta"), py::arg("pull_handles"), py::arg("pull_ptrs"),
+           py::arg("pull_sizes"))
       .def("uninitialized", &PSClient::uninitialized)
       .def("list_vars", &PSClient::list_vars)
       .def("ping", &PSClient::ping)

@@ -184,6 +184,10 @@ def define_reference_flags(flag_values=FLAGS):
     DEFINE_float("save_model_secs", 30.0, "Chief checkpoint interval (Supervisor)", fv)
     DEFINE_float("save_summaries_secs", 30.0, "Chief step-rate summary interval", fv)
     DEFINE_boolean("use_locking", False, "Serialize PS updates per variable", fv)
+    DEFINE_boolean("ps_fused_rpc", True,
+                   "Worker: push + global_step increment + the next step's pull in one "
+                   "pipelined round trip per ps task (False: three round trips, as the "
+                   "reference's three session runs)", fv)
     DEFINE_float("ps_timeout_secs", 0.0,
                  "Worker: a ps silent this long on a request counts as lost and the worker "
                  "exits non-zero (0: wait indefinitely; a dead ps is detected at once)", fv)

@@ -116,6 +116,26 @@ class PSVariableStore:
         self.client.push_apply([self.handles[n] for n in names], [g.data_ptr() for g in gs],
                                [g.numel() * 4 for g in gs], float(lr), bool(use_locking))
 
+    def push_step_pull(self, grads, lr, use_locking=False, step_name="global/global_step",
+                       names=None):
+        """train_op + counter_op + the next step's sync_op in ONE round trip per ps task
+        (pipelined requests, served in order): ``var -= lr * grad``, ``global_step += 1``,
+        then the float variables pulled into the pinned buffers.  Returns (old step,
+        {name: pulled tensor})."""
+        gnames = list(grads)
+        gs = [grads[n] for n in gnames]
+        for g in gs:
+            if g.dtype != torch.float32 or g.device.type != "cpu" or not g.is_contiguous():
+                raise ValueError("push_step_pull needs contiguous f32 CPU tensors")
+        pnames = names or self._float_names
+        bs = [self.bufs[n] for n in pnames]
+        old = self.client.push_step_pull(
+            [self.handles[n] for n in gnames], [g.data_ptr() for g in gs],
+            [g.numel() * 4 for g in gs], float(lr), bool(use_locking), self.handles[step_name],
+            1, [self.handles[n] for n in pnames], [b.data_ptr() for b in bs],
+            [b.numel() * 4 for b in bs])
+        return int(old), {n: b for n, b in zip(pnames, bs)}
+
     def sync_push(self, grads, lr, replicas_to_aggregate, local_step,
                   step_name="global/global_step", timeout_s=600.0):
         """Synchronous replicas (tf.train.SyncReplicasOptimizer): push this worker's

@@ -138,7 +138,9 @@ class Worker:
 
     def sync_op(self):
         """worker.py:81-85: local <- global for every trainable variable."""
-        vals = self.store.pull()
+        self._assign_local(self.store.pull())
+
+    def _assign_local(self, vals):
         with torch.no_grad():
             if self.use_fused:
                 dev = {k: t.to(self.device, non_blocking=True) for k, t in vals.items()}
@@ -263,6 +265,8 @@ class Worker:
             # global step it read; each push joins that step's round on the ps, which applies
             # the mean of replicas_to_aggregate gradients and advances global_step
             local_step = self.store.read_int(self.step_name) if sync else 0
+            fused_rpc = bool(getattr(fl, "ps_fused_rpc", True)) and not self.gpu_ps
+            pulled = False  # the parameters for the next step already came with the last push
             while not sv.should_stop():
                 if self.gpu_ps:
                     # the same four ops on the device, stream-ordered: pull (peer read), local
@@ -297,12 +301,20 @@ class Worker:
                     if stop_after_secs is not None and time.time() - t_begin > stop_after_secs:
                         break
                     continue
-                self.sync_op()
+                if not pulled:
+                    self.sync_op()
                 batch_x, batch_y = dataset.train.next_batch(self.batch_size)
                 grads, cost, acc = self.compute(batch_x, batch_y)
                 if sync:
                     step = local_step
                     local_step, _ = self.store.sync_push(grads, self.lr, replicas, local_step)
+                elif fused_rpc:
+                    # train_op, counter_op and the NEXT step's sync_op in one round trip
+                    # (pipelined on the ps connection, served in the reference's order)
+                    step, vals = self.store.push_step_pull(
+                        grads, self.lr, bool(getattr(fl, "use_locking", False)), self.step_name)
+                    self._assign_local(vals)
+                    pulled = True
                 else:
                     self.store.push_apply(grads, self.lr, bool(getattr(fl, "use_locking", False)))
                     step = self.store.fetch_add(self.step_name, 1)  # counter_op; old value

@@ -322,3 +322,33 @@ def test_sync_replicas_optimizer_api(h, ps):
     assert opt.apply_gradients([(torch.ones(8), "w")]) == 4
     opt.local_step = 3  # a backup replica still on step 3
     assert opt.apply_gradients([(torch.ones(8), "w")]) == 4 and opt.dropped == 1
+
+
+def test_ps_push_step_pull_one_round_trip(h):
+    """push_step_pull: the pipelined push + fetch_add + pull over two ps tasks is served in
+    the reference's order (apply, then step, then read): the pulled values include this
+    push's update and the old step comes back."""
+    import torch
+
+    from distributedtensorflowexample_amd.parallel.ps import PSVariableStore
+
+    servers = [h.PSServer("127.0.0.1", 0) for _ in range(2)]
+    for s in servers:
+        s.start()
+    try:
+        addrs = ["127.0.0.1:%d" % s.port for s in servers]
+        specs = [("a", (1000,), "float32"), ("b", (7,), "float32"),
+                 ("global/global_step", (), "int64")]
+        st = PSVariableStore(addrs, specs).create()
+        st.assign({"a": np.ones(1000), "b": np.full(7, 2.0), "global/global_step": 41})
+        for k in range(3):
+            old, vals = st.push_step_pull({"a": torch.full((1000,), 1.0),
+                                           "b": torch.full((7,), 4.0)}, 0.25)
+            assert old == 41 + k
+            assert torch.allclose(vals["a"], torch.full((1000,), 1.0 - 0.25 * (k + 1)))
+            assert torch.allclose(vals["b"], torch.full((7,), 2.0 - 1.0 * (k + 1)))
+        assert st.read_int("global/global_step") == 44
+        st.close()
+    finally:
+        for s in servers:
+            s.stop()

@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--ps_device", choices=["cpu", "gpu"], default="cpu",
                     help="cpu: the reference's TCP parameter server; gpu: variables in the "
                          "chief's GPU-resident store (parallel/gpu_ps.py)")
+    ap.add_argument("--rpc", choices=["fused", "separate"], default="fused",
+                    help="fused: push + step + next pull in one pipelined round trip per ps "
+                         "task; separate: the reference's three round trips per step")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp(prefix="psbench")
     rc = launch_ps(a.num_workers, a.num_gpus, None, 1, cpu=a.cpu, base_port=a.base_port,
@@ -41,7 +44,8 @@ def main():
                    extra=["--training_steps", str(a.steps), "--log_every", str(a.log_every),
                           "--eval_every", str(10 ** 9), "--logdir", os.path.join(tmp, "m"),
                           "--save_model_secs", "1e9", "--save_summaries_secs", "1e9",
-                          "--batch_size", str(a.batch_size), "--ps_device", a.ps_device])
+                          "--batch_size", str(a.batch_size), "--ps_device", a.ps_device,
+                          "--ps_fused_rpc=%s" % ("true" if a.rpc == "fused" else "false")])
     speeds = []
     for p in glob.glob(os.path.join(tmp, "logs", "worker*.log")):
         for m in re.finditer(r"step: (\d+)\t\| cost: [^|]+\| speed: ([0-9.eE+-]+)step/sec",
@@ -56,7 +60,7 @@ def main():
                       "value": round(sps * a.batch_size, 1), "unit": "samples/sec",
                       "global_steps_per_sec": round(sps, 1), "num_workers": a.num_workers,
                       "num_gpus": a.num_gpus, "device": "cpu" if a.cpu else "MI355X",
-                      "ps_device": a.ps_device,
+                      "ps_device": a.ps_device, "rpc": a.rpc,
                       "steps": a.steps, "rc": rc, "n_speed_samples": len(speeds)}))
     return 0
 
