@@ -118,9 +118,16 @@ class Worker:
             self.params = torch.zeros(mlp_step.NPARAM, device=self.device)
             self.grad = torch.zeros_like(self.params)
             self.ws = mlp_step.StepWorkspace(self.batch_size, self.device)
-            self.grad_host = torch.empty(mlp_step.NPARAM, pin_memory=True)
             self.xb = torch.empty(self.batch_size, D, device=self.device)
             self.yb = torch.empty(self.batch_size, dtype=torch.int32, device=self.device)
+            # the gradient leaves the GPU already in TF layout (transposed on the device) plus
+            # the step's loss / accuracy record: ONE D2H copy per step into pinned memory
+            n = mlp_step.NPARAM
+            self._gtf_dev = torch.empty(n + 2, device=self.device)
+            self.grad_host = torch.empty(n + 2, pin_memory=True)
+            self._xs = torch.empty(self.batch_size, D, pin_memory=True)
+            self._ys = torch.empty(self.batch_size, dtype=torch.int32, pin_memory=True)
+            self._rec = None  # host mirror of the kernels' step counter (stats ring slot)
         else:
             self.local = self.model.new_local(self.device)
         self._test = None  # device-resident test set of the eval op (uploaded once)
@@ -154,13 +161,34 @@ class Worker:
         y = np.asarray(batch_y)
         labels = y.argmax(1) if y.ndim == 2 else y
         if self.use_fused and batch_x.shape[0] == self.batch_size:
-            self.xb.copy_(torch.from_numpy(np.ascontiguousarray(batch_x, np.float32)),
-                          non_blocking=False)
-            self.yb.copy_(torch.from_numpy(labels.astype(np.int32)))
+            stream = torch.cuda.current_stream(self.device)
+            stream.synchronize()  # the pinned staging buffers are free (previous step's copies)
+            self._xs.numpy()[...] = batch_x
+            self._ys.numpy()[...] = labels
+            self.xb.copy_(self._xs, non_blocking=True)
+            self.yb.copy_(self._ys, non_blocking=True)
+            rec = self.ws.global_step() if self._rec is None else self._rec
             mlp_step.step_grad(self.params, self.xb, self.yb, self.ws, self.grad)
-            self.grad_host.copy_(self.grad)
-            loss, acc = self.ws.stats[(self.ws.global_step() - 1) % self.ws.stats_ring].tolist()
-            g = self.grad_host
+            self._rec = rec + 1
+            n = mlp_step.NPARAM
+            src = flat_to_tf_vars(self.grad)  # device views (kernels transposed)
+            off = 0
+            for k in ("global/dense/kernel", "global/dense/bias", "global/dense_1/kernel",
+                      "global/dense_1/bias"):
+                t = src[k]
+                self._gtf_dev[off:off + t.numel()].view(t.shape).copy_(t)
+                off += t.numel()
+            self._gtf_dev[n:n + 2].copy_(self.ws.stats[rec % self.ws.stats_ring])
+            self.grad_host.copy_(self._gtf_dev, non_blocking=True)
+            stream.synchronize()
+            loss, acc = self.grad_host[n:n + 2].tolist()
+            tfg, off = {}, 0
+            for k, shape in (("global/dense/kernel", (D, H)), ("global/dense/bias", (H,)),
+                             ("global/dense_1/kernel", (H, C)), ("global/dense_1/bias", (C,))):
+                m = int(np.prod(shape))
+                tfg[k] = self.grad_host[off:off + m].view(shape)
+                off += m
+            return tfg, float(loss), float(acc)
         elif self.use_fused or self.model.is_reference_mlp:
             x = torch.from_numpy(np.ascontiguousarray(batch_x, np.float32))
             p = self.params.cpu() if hasattr(self, "params") else self._flat_local()
@@ -188,9 +216,7 @@ class Worker:
         parameter store: nothing crosses to the host but the loss / accuracy record).  The
         batch goes through pinned staging buffers (asynchronous H2D), and the record's ring
         slot comes from a host mirror of the kernel's step counter (no read-back)."""
-        if not hasattr(self, "_xs"):
-            self._xs = torch.empty(self.batch_size, D, pin_memory=True)
-            self._ys = torch.empty(self.batch_size, dtype=torch.int32, pin_memory=True)
+        if self._rec is None:
             self._rec = self.ws.global_step()
         y = np.asarray(batch_y)
         labels = y.argmax(1) if y.ndim == 2 else y
