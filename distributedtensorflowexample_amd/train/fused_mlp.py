@@ -331,6 +331,7 @@ class FusedMLPTrainer:
         if self._ll is not None and int(self._ll[-32].item()) != 0:
             raise RuntimeError("persistent MLP engine: an in-kernel hand-off timed out "
                                "(parameters are not valid)")
+        self._unchecked = False  # verified
 
     def run(self, steps, use_graph=True, lead=0):
         """Run ``steps`` training steps (epoch-aligned hipGraph replays).  ``lead`` > 0 (single
