@@ -61,17 +61,26 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
   return __builtin_bit_cast(unsigned short, b);
 }
 
-// GELU (tanh form) and its derivative on fast_tanh: epilogue VALU work per output element
-// is ~10 instructions instead of libm tanhf's ~40 (measured: it set the time of the
-// GELU-grad dgrad GEMM of BERT's FFN).
-__device__ __forceinline__ float gelu_f(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.f + fast_tanh(k0 * (x + k1 * x * x * x)));
+// GELU (tanh form) and its derivative, as sigmoids: 0.5 (1 + tanh(u)) = sigmoid(2u), so
+//   gelu(x)  = x * s,  s = 1 / (1 + 2^(-x (A + B x^2)))   (A, B: 2 sqrt(2/pi) (1, 0.044715),
+//                                                           pre-scaled by log2(e))
+//   gelu'(x) = s + x s (1 - s) (2u)',  (2u)' = C (1 + 3 * 0.044715 x^2)
+// One v_exp_f32 (base 2, no range reduction) + one v_rcp_f32 and 5-6 plain VALU per element
+// -- the tanh form took ~13 (epilogue VALU is exposed: BERT's FFN1 forward lost 13 % of its
+// GEMM rate to the GELU math, tools/gemm_cfg_ab.py "ffn1_fwd_gelu_noaux" vs "ffn1_fwd_bias").
+// Saturates: 2^(+large) = inf -> s = 0 (x -> -inf gives -0), 2^(-large) = 0 -> s = 1.
+__device__ __forceinline__ float gelu_sig(float x) {
+  constexpr float A = 2.302208198f;   // 2 * sqrt(2 / pi) * log2(e)
+  constexpr float B = 0.1029432397f;  // A * 0.044715
+  const float t = x * __builtin_fmaf(B, x * x, A);
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-t));
 }
+__device__ __forceinline__ float gelu_f(float x) { return x * gelu_sig(x); }
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float th = fast_tanh(k0 * (x + k1 * x * x * x));
-  return 0.5f * (1.f + th) + 0.5f * x * (1.f - th * th) * k0 * (1.f + 3.f * k1 * x * x);
+  constexpr float C = 1.5957691216f;   // 2 * sqrt(2 / pi)
+  constexpr float D = 0.2140644640f;   // C * 3 * 0.044715
+  const float s = gelu_sig(x);
+  return __builtin_fmaf(x * s * (1.f - s), __builtin_fmaf(D, x * x, C), s);
 }
 
 // Convolution as implicit GEMM (NHWC bf16 activations, weights [Cout][KH][KW][Cin]).
@@ -802,6 +811,19 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
       __builtin_amdgcn_wave_barrier();
       continue;
     }
+    // the bias of this lane's 8 columns: the same for the slab's 4 row groups, loaded once
+    float bn[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) bn[u] = 0.f;
+    if (e.bias) {
+      const int nb = n0 + c0 + (lane & 7) * 8;
+      if ((lane & 7) * 8 < SLW && nb + 8 <= N) {
+        *(f32x4*)&bn[0] = *(const f32x4*)&e.bias[nb];
+        *(f32x4*)&bn[4] = *(const f32x4*)&e.bias[nb + 4];
+      } else if ((lane & 7) * 8 < SLW) {
+        for (int u = 0; u < 8 && nb + u < N; ++u) bn[u] = e.bias[nb + u];
+      }
+    }
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
@@ -811,19 +833,8 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
       *(f32x4*)&v[0] = *(const f32x4*)&ep[rr * EP_LD + cg];
       *(f32x4*)&v[4] = *(const f32x4*)&ep[rr * EP_LD + cg + 4];
       if (!live[it]) continue;
-      float bn[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) bn[u] = 0.f;
-      if (e.bias) {
-        if (full[it]) {
-          *(f32x4*)&bn[0] = *(const f32x4*)&e.bias[n];
-          *(f32x4*)&bn[4] = *(const f32x4*)&e.bias[n + 4];
-        } else {
-          for (int u = 0; u < 8 && n + u < N; ++u) bn[u] = e.bias[n + u];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = e.alpha * v[u] + bn[u];
+      for (int u = 0; u < 8; ++u) v[u] = __builtin_fmaf(e.alpha, v[u], bn[u]);
       if (full[it]) {
         if (e.aux_out) {
           bf16x8 o;

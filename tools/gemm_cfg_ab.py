@@ -41,6 +41,11 @@ def main():
     shapes = [  # (name, M, N, K, ta, tb, epilogue)
         ("qkv_fwd", T, 2304, 768, False, True, None), ("out_fwd", T, 768, 768, False, True, None),
         ("ffn1_fwd_gelu", T, 3072, 768, False, True, "gelu"),
+        # epilogue cost split of the GELU shapes (same GEMM, epilogue variants)
+        ("ffn1_fwd_plain", T, 3072, 768, False, True, None),
+        ("ffn1_fwd_bias", T, 3072, 768, False, True, "bias"),
+        ("ffn1_fwd_gelu_noaux", T, 3072, 768, False, True, "gelu_noaux"),
+        ("ffn2_dgrad_plain", T, 3072, 768, False, False, None),
         ("ffn2_fwd", T, 768, 3072, False, True, None),
         ("qkv_dgrad", T, 768, 2304, False, False, None), ("ffn1_dgrad", T, 768, 3072, False, False, None),
         ("ffn2_dgrad_gelu", T, 3072, 768, False, False, "gelu_grad"),
@@ -64,6 +69,12 @@ def main():
         elif epi == "gelu":
             kw = dict(bias=torch.zeros(N, device=dev), act="gelu",
                       aux_out=torch.empty(M, N, device=dev, dtype=torch.bfloat16),
+                      out=torch.empty(M, N, device=dev, dtype=torch.bfloat16))
+        elif epi == "bias":
+            kw = dict(bias=torch.zeros(N, device=dev),
+                      out=torch.empty(M, N, device=dev, dtype=torch.bfloat16))
+        elif epi == "gelu_noaux":
+            kw = dict(bias=torch.zeros(N, device=dev), act="gelu",
                       out=torch.empty(M, N, device=dev, dtype=torch.bfloat16))
         elif epi == "gelu_grad":
             kw = dict(act_grad="gelu", aux_in=torch.zeros(M, N, device=dev, dtype=torch.bfloat16),
