@@ -23,6 +23,7 @@ void mlp_head_launch(const float*, const float*, float, float*, const int*, floa
 void mlp_wgrad_launch(float*, float, float*, const float*, float*, int*, float*, int, int,
                       hipStream_t, unsigned long long*);
 long long mlp_workspace_floats(int);
+void mlp_tf_layout_launch(const float*, float*, int, const float*, int, hipStream_t);
 void mlp_fwdapply_launch(const float*, float*, float, const float*, const float*, float*, int*,
                          float*, int, int, int, hipStream_t);
 void mlp_head2_launch(const float*, const int*, float*, int, hipStream_t);
@@ -71,6 +72,11 @@ PYBIND11_MODULE(_hip, m) {
   m.attr("ARCH") = "gfx950";
 
   m.def("mlp_workspace_floats", &dtfx::mlp_workspace_floats);
+  m.def("mlp_tf_layout", [](uintptr_t src, uintptr_t dst, int to_tf, uintptr_t xsrc, int extra,
+                            uintptr_t s) {
+    dtfx::mlp_tf_layout_launch(P<const float>(src), P<float>(dst), to_tf, P<const float>(xsrc),
+                               extra, S(s));
+  });
   m.def("mlp_fwd", [](uintptr_t p_old, uintptr_t grad, float lr, uintptr_t p_new, uintptr_t x,
                       uintptr_t ws, int B, uintptr_t s, uintptr_t tr) {
     dtfx::mlp_fwd_launch(P<const float>(p_old), P<const float>(grad), lr, P<float>(p_new),

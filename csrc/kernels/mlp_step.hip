@@ -978,6 +978,42 @@ static mlp::Bufs make_bufs(float* ws, int B) {
   return b;
 }
 
+// TF checkpoint layout <-> the kernels' flat layout of the MLP parameters / gradients (the
+// async-PS wire format is TF's: worker.py:27-31 kernels [in, out]).  The four segments sit at
+// the same offsets in both (78400 | 100 | 1000 | 10); only the kernels are transposed.
+// to_tf = 1: flat -> TF (+ `extra` floats copied from `xsrc` after NPARAM: the step's loss /
+// accuracy record rides along in the same D2H copy); 0: TF -> flat.
+__global__ __launch_bounds__(256) void mlp_tf_layout_kernel(const float* __restrict__ src,
+                                                            float* __restrict__ dst, int to_tf,
+                                                            const float* __restrict__ xsrc,
+                                                            int extra) {
+  using namespace mlp;
+  const int i = blockIdx.x * 256 + threadIdx.x;  // destination index
+  if (i < NPARAM) {
+    int j = i;  // source index
+    if (i < OFF_B1) {  // W1: TF [784][100] <-> flat [100][784]
+      j = to_tf ? (i % H) * D + i / H : (i % D) * H + i / D;
+    } else if (i >= OFF_W2 && i < OFF_B2) {  // W2: TF [100][10] <-> flat [10][100]
+      const int k = i - OFF_W2;
+      j = OFF_W2 + (to_tf ? (k % C) * H + k / C : (k % H) * C + k / H);
+    }
+    dst[i] = src[j];
+  } else if (to_tf && i < NPARAM + extra) {
+    dst[i] = xsrc[i - NPARAM];
+  }
+}
+
+void mlp_tf_layout_launch(const float* src, float* dst, int to_tf, const float* xsrc, int extra,
+                          hipStream_t stream) {
+  using namespace mlp;
+  if (extra < 0 || extra > 64 || (extra && !xsrc))
+    throw std::runtime_error("mlp_tf_layout: 0..64 extra floats with a source");
+  const int n = NPARAM + (to_tf ? extra : 0);
+  hipLaunchKernelGGL(mlp_tf_layout_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, src, dst,
+                     to_tf, xsrc, to_tf ? extra : 0);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
 long long mlp_workspace_floats(int B) {
   using namespace mlp;
   const long long BP = ((B + 15) / 16) * 16;

@@ -229,6 +229,39 @@ def step_grad(p_old, x, labels, ws: StepWorkspace, grad, prev_grad=None, lr=0.0,
     return p_new if prev_grad is not None else p_old
 
 
+def to_tf_layout(flat, out, record=None):
+    """Flat kernel layout -> TF checkpoint layout (kernels [in, out]) as ONE concatenated buffer
+    [W1 784x100 | b1 | W2 100x10 | b2] (same segment offsets), optionally followed by the
+    floats of ``record`` (e.g. the step's loss / accuracy) -- one launch on the GPU."""
+    extra = 0 if record is None else record.numel()
+    if out.numel() < NPARAM + extra:
+        raise ValueError("output too small")
+    if flat.is_cuda:
+        hip().mlp_tf_layout(ptr(flat), ptr(out), 1, ptr(record), extra, stream_handle())
+        return out
+    W1t, b1, W2t, b2 = unflatten(flat)
+    out[OFF_W1:OFF_B1].view(D, H).copy_(W1t.t())
+    out[OFF_B1:OFF_W2].copy_(b1)
+    out[OFF_W2:OFF_B2].view(H, C).copy_(W2t.t())
+    out[OFF_B2:NPARAM].copy_(b2)
+    if extra:
+        out[NPARAM:NPARAM + extra].copy_(record.reshape(-1))
+    return out
+
+
+def from_tf_layout(tf, flat):
+    """Inverse of ``to_tf_layout`` (the first NPARAM floats of ``tf``)."""
+    if flat.is_cuda:
+        hip().mlp_tf_layout(ptr(tf), ptr(flat), 0, 0, 0, stream_handle())
+        return flat
+    W1t, b1, W2t, b2 = unflatten(flat)
+    W1t.copy_(tf[OFF_W1:OFF_B1].view(D, H).t())
+    b1.copy_(tf[OFF_B1:OFF_W2])
+    W2t.copy_(tf[OFF_W2:OFF_B2].view(H, C).t())
+    b2.copy_(tf[OFF_B2:NPARAM])
+    return flat
+
+
 def reference_forward(p, x):
     W1t, b1, W2t, b2 = unflatten(p)
     h = torch.sigmoid(x @ W1t.t() + b1)

@@ -55,12 +55,16 @@ class PSVariableStore:
         self.setter = setter or replica_device_setter(len(ps_addresses))
         self.handles = {}
         pin = torch.cuda.is_available()
-        self.bufs = {}
+        # the float variables' pinned pull buffers are views of ONE allocation, in spec order
+        # (``flat``): a worker moves a whole pull to its device with a single copy
+        self._float_names = [n for n, _, dt in self.specs if dt == "float32"]
+        sizes = {n: int(np.prod(s)) if s else 1 for n, s, dt in self.specs if dt == "float32"}
+        self.flat = torch.empty(sum(sizes.values()), dtype=torch.float32, pin_memory=pin)
+        self.bufs, off = {}, 0
         for n, s, dt in self.specs:
             if dt == "float32":
-                b = torch.empty(s, dtype=torch.float32, pin_memory=pin)
-                self.bufs[n] = b
-        self._float_names = [n for n, _, dt in self.specs if dt == "float32"]
+                self.bufs[n] = self.flat[off:off + sizes[n]].view(s)
+                off += sizes[n]
 
     # -- bring-up ----------------------------------------------------------
     def create(self):
@@ -163,8 +167,13 @@ class PSVariableStore:
         return self.fetch_add(name, 0)
 
     def read_all(self):
-        """{name: CPU tensor} snapshot of every variable (the chief's Saver)."""
-        out = {n: b.clone() for n, b in self.pull().items()}
+        """{name: CPU tensor} snapshot of every variable (the chief's Saver).  Pulled into
+        buffers of its own: the saver thread never writes the pull buffers the training loop
+        is copying to its device."""
+        names = self._float_names
+        out = {n: torch.empty_like(self.bufs[n]) for n in names}
+        self.client.pull([self.handles[n] for n in names], [out[n].data_ptr() for n in names],
+                         [out[n].numel() * 4 for n in names])
         for n, s, dt in self.specs:
             if dt != "float32":
                 out[n] = torch.tensor(self.read_int(n), dtype=torch.int32)

@@ -149,7 +149,16 @@ class Worker:
 
     def _assign_local(self, vals):
         with torch.no_grad():
-            if self.use_fused:
+            flat = getattr(self.store, "flat", None)
+            if (self.use_fused and flat is not None and flat.numel() == mlp_step.NPARAM
+                    and all(vals[k].data_ptr() == self.store.bufs[k].data_ptr() for k in vals)):
+                # the pull landed in the store's one pinned buffer (TF layout, spec order):
+                # one H2D copy + one layout kernel
+                if not hasattr(self, "_ptf_dev"):
+                    self._ptf_dev = torch.empty(mlp_step.NPARAM, device=self.device)
+                self._ptf_dev.copy_(flat, non_blocking=True)
+                mlp_step.from_tf_layout(self._ptf_dev, self.params)
+            elif self.use_fused:
                 dev = {k: t.to(self.device, non_blocking=True) for k, t in vals.items()}
                 tf_vars_to_flat(dev, self.params)
             else:
@@ -171,14 +180,8 @@ class Worker:
             mlp_step.step_grad(self.params, self.xb, self.yb, self.ws, self.grad)
             self._rec = rec + 1
             n = mlp_step.NPARAM
-            src = flat_to_tf_vars(self.grad)  # device views (kernels transposed)
-            off = 0
-            for k in ("global/dense/kernel", "global/dense/bias", "global/dense_1/kernel",
-                      "global/dense_1/bias"):
-                t = src[k]
-                self._gtf_dev[off:off + t.numel()].view(t.shape).copy_(t)
-                off += t.numel()
-            self._gtf_dev[n:n + 2].copy_(self.ws.stats[rec % self.ws.stats_ring])
+            # TF layout + the loss / accuracy record in one launch, then one D2H copy
+            mlp_step.to_tf_layout(self.grad, self._gtf_dev, self.ws.stats[rec % self.ws.stats_ring])
             self.grad_host.copy_(self._gtf_dev, non_blocking=True)
             stream.synchronize()
             loss, acc = self.grad_host[n:n + 2].tolist()
