@@ -21,6 +21,10 @@ timeout -k 10 200 python bench.py --model resnet50 > "$OUT/bench_resnet.json" 2>
 tail -1 "$OUT/bench_resnet.json" | cut -c 1-180
 timeout -k 10 240 python -u tools/probes/resnet_layers.py > "$OUT/resnet_layers.jsonl" 2>&1 || exit 1
 tail -1 "$OUT/resnet_layers.jsonl"
+step ps_async
+timeout -k 10 200 python tools/bench_ps_async.py --num_workers 2 --steps 40000 > "$OUT/ps_async_w2.json" 2>/dev/null || exit 1
+timeout -k 10 200 python tools/bench_ps_async.py --num_workers 2 --steps 40000 --ps_device gpu > "$OUT/ps_async_gpu_w2.json" 2>/dev/null || exit 1
+cut -c 1-160 "$OUT/ps_async_w2.json" "$OUT/ps_async_gpu_w2.json"
 step prof
 cd /tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/mprof" -o run -- python "$R/bench.py" --steps 2000 --warmup 200 > "$OUT/mprof.log" 2>&1 || exit 1

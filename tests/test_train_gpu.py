@@ -187,7 +187,9 @@ def _gpu_ps_worker(task, port, logdir, q, ready=None):
         spec = {"ps": ["127.0.0.1:%d" % port], "worker": ["127.0.0.1:1", "127.0.0.1:2"]}
         import pathlib
 
-        fl = _flags(pathlib.Path(logdir), ps_device="gpu", num_workers=2, training_steps=4000,
+        # 20k shared steps (~2 s at ~12 k steps/s): long enough that the other worker's first
+        # step (kernel loads, first launches) lands well before the chief alone finishes
+        fl = _flags(pathlib.Path(logdir), ps_device="gpu", num_workers=2, training_steps=20000,
                     eval_every=10 ** 9, learning_rate=0.05)
         w = Worker("worker", task, Server(spec, "worker", task), fl, device="cuda",
                    log=lambda *_: None)
@@ -234,5 +236,5 @@ def test_gpu_parameter_store_two_worker_processes(gpu, tmp_path):
     for task, n, l0, l1, last, err in res:
         assert err is None, err
         assert n >= 20 and l1 < l0, (task, n, l0, l1)  # both workers trained (~12 k steps/s)
-    assert sum(r[1] for r in res) >= 4000 - 2  # the shared global_step reached training_steps
-    assert max(r[4] for r in res) >= 3999
+    assert sum(r[1] for r in res) >= 20000 - 2  # the shared global_step reached training_steps
+    assert max(r[4] for r in res) >= 19999
