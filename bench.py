@@ -142,7 +142,8 @@ def main():
                          "auto (MLP, N>1): verify xgmi against RCCL, time both, use the faster; "
                          "torch: torch.distributed nccl(=RCCL) process group")
     ap.add_argument("--engine",
-                    choices=["auto", "fused", "fused2", "factor", "factor2", "allreduce"],
+                    choices=["auto", "fused", "fused2", "fused2x", "factor", "factor2",
+                             "allreduce"],
                     default="auto",
                     help="MLP, N>1: fused = gradient exchange inside the backward kernel (xGMI LL "
                          "push); factor = sufficient-factor exchange (dz1 all-gathered in the "
@@ -226,11 +227,11 @@ def main():
                                                   comm, world, rank, dev, mode=a.engine,
                                                   x_all=x_all, timeout_s=tmo)
                 a.engine_probe = eprobe
-                if kind in ("fused", "fused2"):
+                if kind in ("fused", "fused2", "fused2x"):
                     fused_comm, a.comm = c, "xgmi-fused-push"
                 elif kind in ("factor", "factor2"):
                     factor_comm, a.comm = c, "xgmi-factor-allgather"
-                a.engine_pipeline = kind in ("fused2", "factor2")
+                a.engine_pipeline = kind in ("fused2", "fused2x", "factor2")
                 a.engine_kind = kind
         if factor_comm is None:
             x_all = None

@@ -339,9 +339,57 @@ __device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const 
       if (d != me) xgll::store((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + off[i], wd);
   }
   auto local = [&](int j) { return (const u64*)xg.peers.data[me] + (par * XW + j) * xg.S; };
+  if (!fail) xgll::gather_sum_n<XW, 4>(local, off, ok, me, ep, v, xg.ticks, fail);
+}
+
+// Two-shot form of xg_exchange (reduce-scatter + all-gather inside the wave): element i of
+// lane l (hidden row 4 q + i of the tile, q = l / 16) is owned by rank (q + 4 i) % XW -- the
+// same on every rank, and one owner per 16-lane row segment, so every push below writes whole
+// 128-byte runs.  (1) a non-owned value goes to its owner only (slot (par, me) of the owner),
+// (2) the owner sums the XW contributions in rank order and pushes the sum into every peer's
+// result region (2 XW + par) -- the push layout's last two slots --, (3) a non-owned element
+// waits for its owner's sum.  Per rank 2 (XW-1)/XW words per element cross the links instead
+// of XW-1 (at 8 ranks 1.75 vs 7), for one more dependent hop.  Every rank pushes before it
+// waits in each phase: no wait cycle.
+template <int XW>
+__device__ __forceinline__ void xg_exchange2(const MlpXg& xg, unsigned ep, const size_t (&off)[4],
+                                             const bool (&ok)[4], float (&v)[4], bool& fail,
+                                             int lane) {
+  using xgll::u64;
+  const long long par = ep & 1u;
+  const int me = xg.rank;
+  const int q = lane >> 4;
+  int own[4];
+  bool mine[4], other[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (ok[i] && !fail) v[i] = xgll::gather_sum<XW>(local, (long long)off[i], me, ep, v[i], xg.ticks, fail);
+  for (int i = 0; i < 4; ++i) {
+    own[i] = (q + 4 * i) % XW;
+    mine[i] = ok[i] && own[i] == me;
+    other[i] = ok[i] && own[i] != me;
+  }
+  auto slot = [&](int dst, int src) { return (u64*)xg.peers.data[dst] + (par * XW + src) * xg.S; };
+  auto result = [&](int dst) { return (u64*)xg.peers.data[dst] + (2 * XW + par) * xg.S; };
+  // uniform loop over destinations, per-lane predicate: a per-lane peer index would turn the
+  // kernel-argument pointer table into a private (scratch) array
+#pragma unroll
+  for (int d = 0; d < XW; ++d) {
+    if (d == me) continue;
+    u64* dst = slot(d, me);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (other[i] && own[i] == d) xgll::store(dst + off[i], xgll::word(v[i], ep));
+  }
+  auto local = [&](int j) { return (const u64*)slot(me, j); };
+  if (!fail) xgll::gather_sum_n<XW, 4>(local, off, mine, me, ep, v, xg.ticks, fail);
+#pragma unroll
+  for (int d = 0; d < XW; ++d) {
+    if (d == me) continue;
+    u64* dst = result(d);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (mine[i]) xgll::store(dst + off[i], xgll::word(v[i], ep));
+  }
+  if (!fail) xgll::wait_n<4>(result(me), off, other, ep, v, xg.ticks, fail);
 }
 
 // Small parameters of hidden tile jt (one product per wave), shared by mlp_wgrad_kernel and
@@ -575,7 +623,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
 // TRACE (probe builds, tools/probes/mlp_pipelined_trace.py): per wave, s_memrealtime stamps
 // 0 entry, 1 phase-A operands landed, 2 W1 tile applied (after the barrier), 3 slab stored;
 // small-parameter blocks: 0 entry, 3 done.  tr: [blocks * 4 waves][4].
-template <int NGT, int XW = 0, bool TRACE = false>
+template <int NGT, int XW = 0, bool TRACE = false, bool TWO = false>
 __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
     const float* __restrict__ x_prev, const float* __restrict__ x, Bufs w, int* __restrict__ ctr,
@@ -670,7 +718,8 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         okw[i] = cv && j < H;
         offw[i] = OFF_W1 + (size_t)(j < H ? j : 0) * D + fc;
       }
-      xg_exchange<XW>(xg, ep, offw, okw, gv, fail);
+      if constexpr (TWO) xg_exchange2<XW>(xg, ep, offw, okw, gv, fail, lane);
+      else xg_exchange<XW>(xg, ep, offw, okw, gv, fail);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1210,7 +1259,8 @@ void mlp_fwdapply_launch(const float* p_old, float* p_new, float lr, const float
 // mlp_head2_launch.  lr already divided by the world size.
 void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
                             const float* x, float* ws, int* ctr, float* stats, int stats_ring,
-                            int B, int stats_on, hipStream_t stream, const MlpXg& xg, int world) {
+                            int B, int stats_on, hipStream_t stream, const MlpXg& xg, int world,
+                            int two_shot) {
   using namespace mlp;
   check_b(B);
   if (!p_old || !p_new || p_old == p_new || !x_prev || !x || !ctr)
@@ -1220,9 +1270,14 @@ void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const fl
   static_assert(HT * KS2 * 4 <= MLP_XG_SMALL_EPOCH, "W1 epoch slots overlap the small ones");
   const Bufs w = make_bufs(ws, B);
   dim3 grid(HT * KS2 + HT), block(256);
-#define DTFX_FX(WW, NGT)                                                                     \
-  hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, WW>), grid, block, 0, stream, p_old, p_new, lr, \
-                     x_prev, x, w, ctr, stats, stats_ring, B, stats_on, xg)
+#define DTFX_FX(WW, NGT)                                                                      \
+  if (two_shot)                                                                               \
+    hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, WW, false, true>), grid, block, 0, stream,    \
+                       p_old, p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B, stats_on, xg, \
+                       nullptr);                                                              \
+  else                                                                                        \
+    hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, WW>), grid, block, 0, stream, p_old, p_new,   \
+                       lr, x_prev, x, w, ctr, stats, stats_ring, B, stats_on, xg, nullptr)
 #define DTFX_FXW(WW)                        \
   case WW:                                  \
     if ((B + 15) / 16 == 7) DTFX_FX(WW, 7); \

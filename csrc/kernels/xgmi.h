@@ -67,9 +67,12 @@ void mlp_wgrad_factor_launch(float* p, float lr, const float* x, long long xstri
 
 // Pipelined fused engine: step t-1's local W1/W2/b gradient tiles exchanged and applied
 // (p_old -> p_new) in the launch that runs step t's forward; the head is the plain one.
+// two_shot: the W1 tiles' exchange as reduce-scatter + all-gather (xg_exchange2): 2 (W-1)/W
+// words per element per rank instead of W-1 (needs the push layout's result region)
 void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
                             const float* x, float* ws, int* ctr, float* stats, int stats_ring,
-                            int B, int stats_on, hipStream_t stream, const MlpXg& xg, int world);
+                            int B, int stats_on, hipStream_t stream, const MlpXg& xg, int world,
+                            int two_shot = 0);
 
 void mlp_wgrad_xg_launch(float* p, float lr, const float* x, float* ws, int* ctr, float* stats,
                          int stats_ring, int B, hipStream_t stream, const MlpXg& xg, int world);

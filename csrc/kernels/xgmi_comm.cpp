@@ -182,12 +182,12 @@ class XgmiAllReduce {
   // Pipelined fused engine: exchange + apply of step t-1 fused with step t's forward.
   void mlp_fwdapply(uintptr_t p_old, uintptr_t p_new, float lr, uintptr_t x_prev, uintptr_t x,
                     uintptr_t ws, uintptr_t ctr, uintptr_t stats, int ring, int B, int stats_on,
-                    uintptr_t stream, double timeout_s) {
+                    uintptr_t stream, double timeout_s, int two_shot) {
     if (!ready_) throw std::runtime_error("xgmi: open() the peer handles first");
     if (mode_ != XG_LL_PUSH) throw std::runtime_error("xgmi: the fused MLP exchange needs protocol push");
     mlp_fwdapply_xg_launch((const float*)p_old, (float*)p_new, lr, (const float*)x_prev,
                            (const float*)x, (float*)ws, (int*)ctr, (float*)stats, ring, B,
-                           stats_on, (hipStream_t)stream, mlp_xg(timeout_s), world_);
+                           stats_on, (hipStream_t)stream, mlp_xg(timeout_s), world_, two_shot);
   }
 
   void mlp_wgrad_factor(uintptr_t p, float lr, uintptr_t x, long long xstride, uintptr_t dz1A,
@@ -198,6 +198,14 @@ class XgmiAllReduce {
     mlp_wgrad_factor_launch((float*)p, lr, (const float*)x, xstride, (const float*)dz1A,
                             (float*)ws, (int*)ctr, (float*)stats, ring, B, (hipStream_t)stream,
                             mlp_xg(timeout_s), world_);
+  }
+
+  // Probe / test hook: every exchange-epoch counter back to 0 on `stream` (the next call of
+  // any kernel of this communicator uses epoch 1 again).  Only meaningful with simulated peers
+  // (open_local), whose words the caller stages for that epoch.
+  void reset_epochs(uintptr_t stream) {
+    XG_CHECK(hipMemsetAsync(epochs_, 0, sizeof(unsigned) * XG_BLOCKS, (hipStream_t)stream));
+    XG_CHECK(hipMemsetAsync(mlp_epochs_, 0, sizeof(unsigned) * MLP_XG_EPOCHS, (hipStream_t)stream));
   }
 
   int error() {
@@ -265,11 +273,12 @@ void register_xgmi(py::module_& m) {
       .def("mlp_fwdapply", &dtfx::XgmiAllReduce::mlp_fwdapply, py::arg("p_old"),
            py::arg("p_new"), py::arg("lr"), py::arg("x_prev"), py::arg("x"), py::arg("ws"),
            py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stats_on"),
-           py::arg("stream"), py::arg("timeout_s") = 2.0)
+           py::arg("stream"), py::arg("timeout_s") = 2.0, py::arg("two_shot") = 0)
       .def("mlp_wgrad_factor", &dtfx::XgmiAllReduce::mlp_wgrad_factor, py::arg("p"),
            py::arg("lr"), py::arg("x"), py::arg("xstride"), py::arg("dz1A"), py::arg("ws"),
            py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"),
            py::arg("timeout_s") = 2.0)
       .def("error", &dtfx::XgmiAllReduce::error)
+      .def("reset_epochs", &dtfx::XgmiAllReduce::reset_epochs)
       .def("close", &dtfx::XgmiAllReduce::close);
 }

@@ -84,6 +84,77 @@ __device__ __forceinline__ void gather_all(Base base, long long i, int rank, uns
   for (int j = 0; j < W; ++j) out[j] = j == rank ? own : __uint_as_float((unsigned)w[j]);
 }
 
+// gather_sum over N elements of a lane at once: every first load of the N x (W-1) words is
+// issued before the first wait, so the N round trips overlap instead of serialising (the MLP
+// exchange epilogues hold 4 elements per lane).  v[n] holds the own value on entry and the
+// rank-ordered sum on return for act[n]; inactive elements are left as they are.
+template <int W, int N, class Base>
+__device__ __forceinline__ void gather_sum_n(Base base, const size_t (&off)[N], const bool (&act)[N],
+                                             int rank, unsigned epoch, float (&v)[N],
+                                             long long ticks, bool& fail) {
+  const u64 done = (u64)epoch << 32;
+  u64 w[N][W];
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int j = 0; j < W; ++j) w[n][j] = (act[n] && j != rank) ? load(base(j) + off[n]) : done;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ready = true;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+        if ((unsigned)(w[n][j] >> 32) != epoch) {
+          ready = false;
+          w[n][j] = load(base(j) + off[n]);
+        }
+    if (ready) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      fail = true;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    if (!act[n]) continue;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc += j == rank ? v[n] : __uint_as_float((unsigned)w[n][j]);
+    v[n] = acc;
+  }
+}
+
+// wait_one over N words at once (first loads issued together); v[n] = the word's value.
+template <int N>
+__device__ __forceinline__ void wait_n(const u64* p, const size_t (&off)[N], const bool (&act)[N],
+                                       unsigned epoch, float (&v)[N], long long ticks, bool& fail) {
+  const u64 done = (u64)epoch << 32;
+  u64 w[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) w[n] = act[n] ? load(p + off[n]) : done;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ready = true;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+      if ((unsigned)(w[n] >> 32) != epoch) {
+        ready = false;
+        w[n] = load(p + off[n]);
+      }
+    if (ready) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      fail = true;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+    if (act[n]) v[n] = __uint_as_float((unsigned)w[n]);
+}
+
 __device__ __forceinline__ float wait_one(const u64* p, unsigned epoch, long long ticks,
                                           bool& fail) {
   u64 w = load(p);

@@ -144,6 +144,9 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
       ``("fused2", XgmiComm)``  -- the same exchange in the two-launch pipelined step (step
                                    t-1's local gradient tiles exchanged and applied inside
                                    step t's forward launch);
+      ``("fused2x", XgmiComm)`` -- fused2 with the W1 tiles exchanged two-shot (each element
+                                   reduced by one owner rank and broadcast back: 2 (W-1)/W
+                                   words per element per rank instead of W-1; world >= 3);
       ``("factor", XgmiComm)``  -- sufficient-factor exchange: the backprop factors dz1 are
                                    all-gathered inside the head kernel and every rank forms
                                    the global W1 gradient from them and every rank's batch
@@ -164,8 +167,11 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
 
     if world < 2 or world > 8 or mode == "allreduce":
         return "allreduce", ar_comm, None
-    kinds = {"auto": ["fused", "fused2", "factor", "factor2"], "fused": ["fused"],
-             "fused2": ["fused2"], "factor": ["factor"], "factor2": ["factor2"]}[mode]
+    kinds = {"auto": ["fused", "fused2", "fused2x", "factor", "factor2"], "fused": ["fused"],
+             "fused2": ["fused2"], "fused2x": ["fused2x"], "factor": ["factor"],
+             "factor2": ["factor2"]}[mode]
+    if world < 3:  # two-shot moves no fewer words than one-shot at 2 ranks, for one more hop
+        kinds = [k for k in kinds if k != "fused2x"]
     if x_all is None:
         kinds = [k for k in kinds if not k.startswith("factor")]
     if batch_size > 128:
@@ -179,6 +185,8 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
         except Exception as e:
             err = repr(e)
             print("[bench] rank %d: %s xgmi engine: %s" % (rank, kind, err), file=sys.stderr)
+        if c is not None and kind == "fused2x":
+            c.two_shot = True
         if agree(c is not None):
             comms[kind] = c
         else:
@@ -190,9 +198,9 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
         return "allreduce", ar_comm, None
 
     def make(kind):
-        if kind in ("fused", "fused2"):  # fused2: the two-launch pipelined variant
+        if kind in ("fused", "fused2", "fused2x"):  # fused2 / fused2x: two-launch pipelined
             return FusedMLPTrainer(params, x, y, batch_size, lr, world_size=world,
-                                   fused_comm=comms[kind], pipeline=kind == "fused2")
+                                   fused_comm=comms[kind], pipeline=kind != "fused")
         if kind in ("factor", "factor2"):  # factor2: the two-launch pipelined variant
             return FusedMLPTrainer(params, None, y, batch_size, lr, world_size=world,
                                    factor_comm=comms[kind], x_all=x_all, rank=rank,

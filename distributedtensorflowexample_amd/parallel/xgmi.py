@@ -27,6 +27,9 @@ class XgmiComm:
                                    else torch.device(device).index)
         self.timeout_s = float(timeout_s)
         self.max_numel = int(max_numel)
+        # fused MLP engine: exchange the W1 gradient tiles two-shot (reduce-scatter +
+        # all-gather inside the kernel) instead of one-shot (set by the engine selection)
+        self.two_shot = False
         # "ll": 8-byte {value, epoch} words (no flag round trip; world <= 8); "flag": slots +
         # per-block epoch flags (any world <= 16)
         self.protocol = protocol or ("ll" if self.world_size <= 8 else "flag")
@@ -70,6 +73,7 @@ class XgmiComm:
         self.timeout_s = float(timeout_s)
         self.max_numel = int(max_numel)
         self.protocol = protocol
+        self.two_shot = False
         self._h = hip().XgmiAllReduce(self.rank, self.world_size, self.device.index,
                                       self.max_numel, protocol, False)
         words = self._h.region_bytes() // 8
@@ -141,7 +145,7 @@ class XgmiComm:
                              ptr(x_prev if apply else x), ptr(x), ptr(ws.buf), ptr(ws.ctr),
                              ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B,
                              1 if apply else 0, torch.cuda.current_stream().cuda_stream,
-                             self.timeout_s)
+                             self.timeout_s, 1 if self.two_shot else 0)
 
     def mlp_wgrad_factor(self, p, lr, x, xstride, dz1A, ws, stats=True):
         """Factor engine: global dW1 from the gathered factors and every rank's batch

@@ -104,7 +104,7 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
             kind, c, _ = pick_mlp_engine(params, tr_x.to(dev), tr_y.to(dev), B,
                                          flags.learning_rate, comm, world, rank, dev, x_all=x_all,
                                          mode=os.environ.get("DTFX_MLP_ENGINE", "auto"))
-            fused = c if kind in ("fused", "fused2") else None
+            fused = c if kind in ("fused", "fused2", "fused2x") else None
             factor = c if kind in ("factor", "factor2") else None
             pipe = kind not in ("fused", "factor")  # fused2 / factor2: two-launch variants
         tr = FusedMLPTrainer(params, tr_x, tr_y, B, flags.learning_rate,

@@ -32,19 +32,26 @@ def test_kill_and_resume(tmp_path, model, step_key):
     else:
         args = common + ["--training_steps", "8000", "--learning_rate", "0.01"]
     p = _run(args, str(tmp_path / "a.log"))
-    killed_at = None
-    t0 = time.time()
-    while time.time() - t0 < 120:
-        ck = latest_checkpoint(logdir)
-        if ck and int(load_checkpoint(ck)[step_key]) > 0:
-            killed_at = int(load_checkpoint(ck)[step_key])
-            break
-        time.sleep(0.2)
-    p.send_signal(signal.SIGKILL)
-    p.wait(30)
-    assert killed_at is not None, open(str(tmp_path / "a.log")).read()[-2000:]
-    q = _run(args, str(tmp_path / "b.log"))
-    assert q.wait(300) == 0, open(str(tmp_path / "b.log")).read()[-2000:]
+    q = None
+    try:
+        killed_at = None
+        t0 = time.time()
+        while time.time() - t0 < 120:
+            ck = latest_checkpoint(logdir)
+            if ck and int(load_checkpoint(ck)[step_key]) > 0:
+                killed_at = int(load_checkpoint(ck)[step_key])
+                break
+            time.sleep(0.2)
+        p.send_signal(signal.SIGKILL)
+        p.wait(30)
+        assert killed_at is not None, open(str(tmp_path / "a.log")).read()[-2000:]
+        q = _run(args, str(tmp_path / "b.log"))
+        assert q.wait(300) == 0, open(str(tmp_path / "b.log")).read()[-2000:]
+    finally:  # no orphaned trainer on a failed assertion
+        for r in (p, q):
+            if r is not None and r.poll() is None:
+                r.kill()
+                r.wait(30)
     final = int(load_checkpoint(latest_checkpoint(logdir))[step_key])
     assert final == int(args[args.index("--training_steps") + 1])
     log_b = open(str(tmp_path / "b.log")).read()

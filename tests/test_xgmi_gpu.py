@@ -118,7 +118,7 @@ def test_auto_selection_path(gpu):
         assert ok, (r, msg)
 
 
-def _fused_worker(rank, world, port, q, pipeline):
+def _fused_worker(rank, world, port, q, pipeline, two_shot=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -132,6 +132,7 @@ def _fused_worker(rank, world, port, q, pipeline):
         params = init_params(dev, seed=7)
         x, y = mnist_like_device(2000, seed=50 + rank, device=dev)  # per-rank data
         fc = XgmiComm(rank, world, params.numel(), device=dev, key="f/push", protocol="push")
+        fc.two_shot = two_shot
         ref = XgmiComm(rank, world, params.numel(), device=dev, key="f/ll", protocol="ll")
         lr = 0.05
         tf = FusedMLPTrainer(params, x, y, 100, lr, world_size=world, fused_comm=fc,
@@ -160,15 +161,17 @@ def _fused_worker(rank, world, port, q, pipeline):
         q.put((rank, False, repr(e)))
 
 
-@pytest.mark.parametrize("world,pipeline", [(2, False), (3, False), (2, True), (3, True)])
-def test_fused_mlp_exchange_matches_allreduce_engine(gpu, world, pipeline):
+@pytest.mark.parametrize("world,pipeline,two_shot", [(2, False, False), (3, False, False),
+                                                     (2, True, False), (3, True, False),
+                                                     (3, True, True), (4, True, True)])
+def test_fused_mlp_exchange_matches_allreduce_engine(gpu, world, pipeline, two_shot):
     """The gradient exchange fused into the MLP backward kernel (pipeline: into the next
     step's forward launch) gives the same SGD trajectory as the separate all-reduce engine,
     and bit-identical replicas."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_fused_worker, args=(r, world, port, q, pipeline))
+    procs = [ctx.Process(target=_fused_worker, args=(r, world, port, q, pipeline, two_shot))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -569,3 +569,85 @@ def test_bw_allreduce_simulated_peers(gpu, world):
         for n, cap in ((7 * 1024 * 1024 + 13, 7 * 1024 * 1024 + 13), (100003, 100003),
                        (5000, 1 << 20)):
             _bw_check(world, rank, n, cap, gpu)
+
+
+def _w1_owner(off, world):
+    """Owner rank of W1 element ``off`` in the two-shot exchange of mlp_fwdapply_kernel<.., XW,
+    .., TWO> (lane (q, r) of a phase-A wave holds hidden j = jt*16 + 4q + i, feature
+    ks*56 + 16w + r; owner = (q + 4 i) % XW)."""
+    hl = (off // 784) % 16
+    return (hl // 4 + 4 * (hl % 4)) % world
+
+
+@pytest.mark.parametrize("world,rank", [(3, 2), (4, 1), (5, 0), (8, 7), (8, 3)])
+def test_fused2_two_shot_exchange_simulated_peers(gpu, world, rank):
+    """mlp_fwdapply_kernel<7, XW, false, true>: the W1 tiles' exchange as reduce-scatter +
+    all-gather (owned elements: gather + rank-ordered sum + broadcast; the others: push to the
+    owner, then take its sum); small parameters one-shot."""
+    from distributedtensorflowexample_amd.data.synthetic import mnist_like_device
+    from distributedtensorflowexample_amd.ops import mlp_step
+    from distributedtensorflowexample_amd.ops._ext import hip, ptr, stream_handle
+    from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+    B = 100
+    p_old, x_prev, y_prev, ws = _setup(gpu, B, 60 * world + rank)
+    x, y = mnist_like_device(B, seed=777 + rank, device=gpu)
+    comm, regs = XgmiComm.with_local_peers(rank, world, mlp_step.NPARAM, device=gpu)
+    comm.two_shot = True
+    S = comm.slot_stride
+    n1 = mlp_step.OFF_B1
+    owner = torch.tensor([_w1_owner(o, world) for o in range(n1)])
+    mine = owner == rank
+    lr = 0.5
+    bufs = [p_old, torch.empty_like(p_old)]
+    batches = [(x_prev, y_prev), (x, y)]
+    _pipelined_fwd_head(p_old, x_prev, y_prev, ws)
+    g = torch.Generator().manual_seed(world * 31 + rank)
+    cur = 0
+    for epoch in (1, 2):
+        par = epoch & 1
+        xp, yp = batches[(epoch - 1) % 2]
+        xn, yn = batches[epoch % 2]
+        po, pn = bufs[cur], bufs[cur ^ 1]
+        own = _ref_grad(po, xp, yp)
+        peers = _peer_grads(world, rank, 23 * epoch + world, 0.05)
+        # small parameters: one-shot slots, every peer
+        _stage_param_words(comm, regs, peers, epoch, n1, mlp_step.NPARAM)
+        # W1, owned: the peers' contributions; not owned: the owner's (arbitrary) sum
+        for q in range(world):
+            if q != rank:
+                o = (par * world + q) * S
+                w = _words(peers[q][:n1].to(gpu), epoch)
+                sl = regs[rank][o:o + n1]
+                sl[mine.to(gpu)] = w[mine.to(gpu)]
+        owners_sum = torch.randn(n1, generator=g) * 0.07
+        res = (2 * world + par) * S
+        rw = _words(owners_sum.to(gpu), epoch)
+        sl = regs[rank][res:res + n1]
+        sl[(~mine).to(gpu)] = rw[(~mine).to(gpu)]
+        tot = _expected_update(own, peers, rank)
+        exp = po.double().cpu() - lr * tot
+        exp[:n1][~mine] = po.double().cpu()[:n1][~mine] - lr * owners_sum.double()[~mine]
+        torch.cuda.synchronize()
+        comm.mlp_fwdapply(po, pn, lr, xp, xn, ws, True)
+        hip().mlp_head2(ptr(pn), ptr(yn), ptr(ws.buf), ws.B, stream_handle())
+        comm.check()
+        err = float((pn.double().cpu() - exp).abs().max())
+        assert err <= 2e-5, (epoch, err)
+        # pushes: my share of every non-owned element went to its owner only; my sums of the
+        # owned ones to every peer's result region
+        for d in range(world):
+            if d == rank:
+                continue
+            o = (par * world + rank) * S
+            wv = regs[d][o:o + n1].cpu()
+            to_d = owner == d
+            assert bool((_epochs(wv[to_d]) == epoch).all()), ("contribution epoch", d)
+            assert float((_vals(wv[to_d]).double() - own[:n1][to_d]).abs().max()) <= 2e-6
+            rv = regs[d][res:res + n1].cpu()
+            assert bool((_epochs(rv[mine]) == epoch).all()), ("result epoch", d)
+            got = _vals(rv[mine]).double()
+            assert float((got - tot[:n1][mine]).abs().max()) <= 2e-5
+        _check_pushed(comm, regs, own, epoch, n1, mlp_step.NPARAM, 2e-6)
+        cur ^= 1
+    comm.destroy()
