@@ -45,6 +45,13 @@ def _pump(proc, name, logf, quiet):
             sys.stdout.flush()
 
 
+def _cpu_threads(nproc):
+    """OMP_NUM_THREADS for one of nproc CPU-device tasks on this host: the user's setting, else
+    a fair share of the cores (torch's default of every core per process oversubscribes the
+    host nproc-fold and the gloo/TCP tasks stall one another)."""
+    return os.environ.get("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // max(1, nproc))))
+
+
 class Cluster:
     def __init__(self, log_dir, quiet=False):
         self.log_dir = log_dir
@@ -114,7 +121,8 @@ def launch_ps(num_workers=2, num_gpus=1, gpu_ids=None, num_ps=1, extra=(), log_d
         n = "worker%d" % i
         env = {} if cpu else {"HIP_VISIBLE_DEVICES": str(gpu_ids[i % len(gpu_ids)])}
         if cpu:
-            env.update({"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": ""})
+            env.update({"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": "",
+                        "OMP_NUM_THREADS": _cpu_threads(num_workers)})
         cl.spawn(n, ["--job_name", "worker", "--task_index", str(i)] + common, env)
         w_names.append(n)
     try:
@@ -128,12 +136,16 @@ def launch_mirrored(nproc=1, extra=(), log_dir="launch_logs", timeout=None, quie
     port = _free_port()
     cl = Cluster(log_dir, quiet)
     names = []
+    ex = list(extra)
+    cpu = "--device" in ex and ex.index("--device") + 1 < len(ex) and ex[ex.index("--device") + 1] == "cpu"
     for r in range(nproc):
         n = "rank%d" % r
-        cl.spawn(n, ["--strategy", "mirrored"] + list(extra),
-                 {"RANK": str(r), "WORLD_SIZE": str(nproc), "LOCAL_RANK": str(r),
-                  "LOCAL_WORLD_SIZE": str(nproc), "MASTER_ADDR": "127.0.0.1",
-                  "MASTER_PORT": str(port)})
+        env = {"RANK": str(r), "WORLD_SIZE": str(nproc), "LOCAL_RANK": str(r),
+               "LOCAL_WORLD_SIZE": str(nproc), "MASTER_ADDR": "127.0.0.1",
+               "MASTER_PORT": str(port)}
+        if cpu:
+            env["OMP_NUM_THREADS"] = _cpu_threads(nproc)
+        cl.spawn(n, ["--strategy", "mirrored"] + ex, env)
         names.append(n)
     try:
         rc = cl.wait(names, timeout)

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _run(args, log):
     return subprocess.Popen([sys.executable, os.path.join(ROOT, "main.py")] + args,
                             stdout=open(log, "w"), stderr=subprocess.STDOUT, cwd=ROOT,
-                            env=dict(os.environ, HIP_VISIBLE_DEVICES=""))
+                            env=dict(os.environ, HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2"))
 
 
 @pytest.mark.parametrize("model,step_key", [("mlp", "global/global_step"),
