@@ -25,6 +25,10 @@ void bn_finalize_launch(int, long long, const float*, const float*, float, float
                         float*, float, hipStream_t);
 void bn_apply_launch(long long, int, const void*, const float*, const float*, const float*,
                      const float*, const void*, int, void*, hipStream_t);
+void bn_apply_stats_launch(long long, int, const void*, const float*, const float*, float, float*,
+                           float*, float*, float*, float, const float*, const float*, const void*,
+                           int, void*, const float*, const float*, const float*, const float*,
+                           float*, float*, float*, float*, hipStream_t);
 void bn_bwd_launch(long long, int, const void*, const void*, const void*, const float*, const float*,
                    const float*, int, float*, float*, float*, void*, void*, hipStream_t);
 long long bn_bwd_scratch_rows(long long, int);
@@ -208,6 +212,19 @@ void register_nn(py::module_& m) {
     dtfx::bn_apply_launch(M, C, P<const void>(x), P<const float>(mean), P<const float>(rstd),
                           P<const float>(g), P<const float>(b), P<const void>(res), relu, P<void>(y),
                           S(s));
+  });
+  m.def("bn_apply_stats", [](long long M, int C, uintptr_t x, uintptr_t sum, uintptr_t sq, float eps,
+                             uintptr_t mean, uintptr_t rstd, uintptr_t run_mean, uintptr_t run_var,
+                             float momentum, uintptr_t g, uintptr_t b, uintptr_t res, int relu,
+                             uintptr_t y, uintptr_t sum2, uintptr_t sq2, uintptr_t g2, uintptr_t b2,
+                             uintptr_t mean2, uintptr_t rstd2, uintptr_t run_mean2,
+                             uintptr_t run_var2, uintptr_t s) {
+    dtfx::bn_apply_stats_launch(M, C, P<const void>(x), P<const float>(sum), P<const float>(sq), eps,
+                                P<float>(mean), P<float>(rstd), P<float>(run_mean), P<float>(run_var),
+                                momentum, P<const float>(g), P<const float>(b), P<const void>(res),
+                                relu, P<void>(y), P<const float>(sum2), P<const float>(sq2),
+                                P<const float>(g2), P<const float>(b2), P<float>(mean2),
+                                P<float>(rstd2), P<float>(run_mean2), P<float>(run_var2), S(s));
   });
   m.def("bn_bwd", [](long long M, int C, uintptr_t dy, uintptr_t yout, uintptr_t x, uintptr_t mean,
                      uintptr_t rstd, uintptr_t g, int relu, uintptr_t sdy, uintptr_t sdyxh,

@@ -100,7 +100,50 @@ __global__ void bn_finalize_kernel(int C, float inv_m, float unbias, const float
 // up to 2048: 256 % (C / 8) == 0) each thread keeps ONE channel group for its whole
 // grid-stride walk, so its 8 coefficients pairs are loaded once (not 32 scalar loads and
 // a 64-bit modulo per 16-B chunk), and the walk keeps 4 chunks in flight.
-template <int U>
+//
+// Fused finalize (st.ssum != null, the forward's training-mode path): the batch statistics
+// come in as the column sums ssum / ssq of the conv epilogue, every thread forms mean / rstd
+// of its own channels exactly as bn_finalize_kernel does, and block 0 stores mean / rstd (for
+// the backward) and updates the running statistics -- one launch per BatchNorm instead of
+// finalize + apply (ResNet-50: 53 launches of ~5 us per step).
+// A second set (st2.ssum != null) normalises the residual with ITS own batch statistics and
+// affine (gamma2 / beta2) before the add: a bottleneck's output relu(bn3(c3) + bn_ds(cds)) in
+// one pass over c3 and the raw downsample conv output cds -- the normalised shortcut is never
+// written and read back (the downsample backward only needs cds and its mean / rstd).
+struct BnStats {
+  const float* ssum;
+  const float* ssq;
+  float inv_m, eps, unbias, momentum;
+  float* mean_out;
+  float* rstd_out;
+  float* run_mean;
+  float* run_var;
+  const float* gamma2;  // st2 only: the residual BN's affine
+  const float* beta2;
+};
+__device__ __forceinline__ void bn_store_stats(const BnStats& st, int c, float mu, float rs) {
+  st.mean_out[c] = mu;
+  st.rstd_out[c] = rs;
+  if (st.run_mean) {
+    const float var = fmaxf(st.ssq[c] * st.inv_m - mu * mu, 0.f);
+    st.run_mean[c] = st.momentum * st.run_mean[c] + (1.f - st.momentum) * mu;
+    st.run_var[c] = st.momentum * st.run_var[c] + (1.f - st.momentum) * var * st.unbias;
+  }
+}
+template <bool STATS>
+__device__ __forceinline__ void bn_coef(const BnStats& st, const float* mean, const float* rstd, int c,
+                                        float& mu, float& rs) {
+  if (STATS) {
+    mu = st.ssum[c] * st.inv_m;
+    rs = rsqrtf(fmaxf(st.ssq[c] * st.inv_m - mu * mu, 0.f) + st.eps);
+  } else {
+    mu = mean[c];
+    rs = rstd[c];
+  }
+}
+// (STATS / RBN are template parameters: as run-time flags the per-element residual branch and
+// the coefficient loads ended up inside the streaming loop -- 4x slower)
+template <int U, bool STATS, bool RBN>
 __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
                                                        const unsigned short* __restrict__ x,
                                                        const float* __restrict__ mean,
@@ -108,19 +151,41 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta,
                                                        const unsigned short* __restrict__ res,
-                                                       int relu, unsigned short* __restrict__ y) {
+                                                       int relu, unsigned short* __restrict__ y,
+                                                       BnStats st, BnStats st2) {
   const int cg = C >> 3;
   const long long n8 = M * cg;
   const long long stride = (long long)gridDim.x * blockDim.x;
   const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr bool rbn = RBN;  // residual normalised by its own BN (res: raw conv output)
+  if (STATS && blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float mu, rs;
+      bn_coef<STATS>(st, mean, rstd, c, mu, rs);
+      bn_store_stats(st, c, mu, rs);
+      if (rbn) {
+        bn_coef<true>(st2, nullptr, nullptr, c, mu, rs);
+        bn_store_stats(st2, c, mu, rs);
+      }
+    }
+  }
   if (stride % cg == 0) {
     const int c0 = (int)(i0 % cg) * 8;
-    float sc[8], sh[8];
+    float sc[8], sh[8], sc2[8], sh2[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int c = c0 + u;
-      sc[u] = rstd[c] * gamma[c];
-      sh[u] = beta[c] - mean[c] * sc[u];
+      float mu, rs;
+      bn_coef<STATS>(st, mean, rstd, c, mu, rs);
+      sc[u] = rs * gamma[c];
+      sh[u] = beta[c] - mu * sc[u];
+      sc2[u] = 1.f;
+      sh2[u] = 0.f;
+      if (rbn) {
+        bn_coef<true>(st2, nullptr, nullptr, c, mu, rs);
+        sc2[u] = rs * st2.gamma2[c];
+        sh2[u] = st2.beta2[c] - mu * sc2[u];
+      }
     }
     for (long long ib = i0; ib < n8; ib += U * stride) {
       bf16x8 xv[U], rv[U];
@@ -141,7 +206,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           float o = v[u] * sc[u] + sh[u];
-          if (res) o += r[u];
+          if (res) o += rbn ? r[u] * sc2[u] + sh2[u] : r[u];
           if (relu) o = fmaxf(o, 0.f);
           v[u] = o;
         }
@@ -158,8 +223,15 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int c = c0 + u;
-      float o = (v[u] - mean[c]) * rstd[c] * gamma[c] + beta[c];
-      if (res) o += r[u];
+      float mu, rs;
+      bn_coef<STATS>(st, mean, rstd, c, mu, rs);
+      float o = (v[u] - mu) * rs * gamma[c] + beta[c];
+      if (res && rbn) {
+        bn_coef<true>(st2, nullptr, nullptr, c, mu, rs);
+        o += (r[u] - mu) * rs * st2.gamma2[c] + st2.beta2[c];
+      } else if (res) {
+        o += r[u];
+      }
       if (relu) o = fmaxf(o, 0.f);
       v[u] = o;
     }
@@ -521,9 +593,33 @@ void bn_apply_launch(long long M, int C, const void* x, const float* mean, const
                      const float* gamma, const float* beta, const void* res, int relu, void* y,
                      hipStream_t st) {
   if (C % 8) throw std::runtime_error("bn_apply: C % 8 != 0");
-  hipLaunchKernelGGL((bn_apply_kernel<kEwU>), dim3(grid_once(M * C / 8, kEwU)), dim3(256), 0, st,
-                     M, C, (const unsigned short*)x, mean, rstd, gamma, beta,
-                     (const unsigned short*)res, relu, (unsigned short*)y);
+  hipLaunchKernelGGL((bn_apply_kernel<kEwU, false, false>), dim3(grid_once(M * C / 8, kEwU)), dim3(256),
+                     0, st, M, C, (const unsigned short*)x, mean, rstd, gamma, beta,
+                     (const unsigned short*)res, relu, (unsigned short*)y, BnStats{}, BnStats{});
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// Training-mode forward BatchNorm in one launch: statistics from the column sums s / q
+// (sum, sum of squares over M rows), mean / rstd written for the backward, running
+// statistics updated (momentum, unbiased variance), y = act(bn(x) [+ res]).  With s2 set the
+// residual is a raw conv output normalised by its own statistics s2 / q2 and affine g2 / b2
+// (mean2 / rstd2 / running2 written likewise): y = act(bn(x) + bn2(res)).
+void bn_apply_stats_launch(long long M, int C, const void* x, const float* s, const float* q,
+                           float eps, float* mean, float* rstd, float* run_mean, float* run_var,
+                           float momentum, const float* gamma, const float* beta, const void* res,
+                           int relu, void* y, const float* s2, const float* q2, const float* g2,
+                           const float* b2, float* mean2, float* rstd2, float* run_mean2,
+                           float* run_var2, hipStream_t stream) {
+  if (C % 8) throw std::runtime_error("bn_apply: C % 8 != 0");
+  if (s2 && (!res || !q2 || !g2 || !b2 || !mean2 || !rstd2))
+    throw std::runtime_error("bn_apply_stats: residual BN needs res, q2, gamma2, beta2, mean2, rstd2");
+  const float inv_m = 1.f / (float)M, unbias = M > 1 ? (float)M / (float)(M - 1) : 1.f;
+  BnStats bs{s, q, inv_m, eps, unbias, momentum, mean, rstd, run_mean, run_var, nullptr, nullptr};
+  BnStats bs2{s2, q2, inv_m, eps, unbias, momentum, mean2, rstd2, run_mean2, run_var2, g2, b2};
+  auto k = s2 ? bn_apply_kernel<kEwU, true, true> : bn_apply_kernel<kEwU, true, false>;
+  hipLaunchKernelGGL(k, dim3(grid_once(M * C / 8, kEwU)), dim3(256), 0, stream, M, C,
+                     (const unsigned short*)x, (const float*)nullptr, (const float*)nullptr, gamma,
+                     beta, (const unsigned short*)res, relu, (unsigned short*)y, bs, bs2);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

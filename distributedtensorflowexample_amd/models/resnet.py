@@ -144,21 +144,21 @@ class ResNet50:
         self.wgrad_sync_buckets = True
         self._keep = []  # operands the side stream still reads
 
-    # conv + fused BN statistics + finalize
+    # conv + fused BN statistics (column sums in the conv epilogue)
     def _conv_bn(self, name, x):
         _, cin, cout, k, s, p = self.specs[name]
         P = self.params
         cs, cq = self._stats[name]
         y = CN.conv_fwd(x, P.W(name + ".weight"), k, k, s, p, colsum=cs, colsq=cq)
-        M = y.numel() // cout
-        rm, rv = P.running[name]
-        mean, rstd = CN.bn_finalize(cs, cq, M, self.eps, rm, rv)
-        return y, mean, rstd
+        return y, (cs, cq, y.numel() // cout)
 
-    def _bn_apply(self, name, y, mean, rstd, residual=None, relu=True):
+    # finalize (mean / rstd, running statistics) + apply (+ residual, ReLU) in one launch
+    def _bn_apply(self, name, y, st, residual=None, relu=True, res_bn=None):
         P = self.params
-        return CN.bn_apply(y, mean, rstd, P.P(name + ".bn.gamma"), P.P(name + ".bn.beta"),
-                           residual, relu)
+        cs, cq, M = st
+        rm, rv = P.running[name]
+        return CN.bn_apply_stats(y, cs, cq, M, P.P(name + ".bn.gamma"), P.P(name + ".bn.beta"),
+                                 residual, relu, self.eps, rm, rv, res_bn=res_bn)
 
     def forward_backward(self, images, labels, on_bucket_ready=None):
         """images: NHWC bf16 [N, H, W, 8]; labels int32 [N].  Returns (loss, accuracy)."""
@@ -167,27 +167,33 @@ class ResNet50:
         P.grad.zero_()
         self._stats_flat.zero_()  # every BN's (sum, sum of squares) accumulators, one memset
         saved = {}
-        c, m, r = self._conv_bn("conv1", images)
-        a = self._bn_apply("conv1", c, m, r)
+        c, st = self._conv_bn("conv1", images)
+        a, m, r = self._bn_apply("conv1", c, st)
         saved["conv1"] = (images, c, m, r, a)
         x, idx = CN.maxpool_fwd(a)
         blocks = []
-        for si, (w, nb, st) in enumerate(P.stages):
+        for si, (w, nb, st_) in enumerate(P.stages):
             for b in range(nb):
                 pre = "layer%d.%d." % (si + 1, b)
                 x_in = x
-                c1, m1, r1 = self._conv_bn(pre + "conv1", x_in)
-                a1 = self._bn_apply(pre + "conv1", c1, m1, r1)
-                c2, m2, r2 = self._conv_bn(pre + "conv2", a1)
-                a2 = self._bn_apply(pre + "conv2", c2, m2, r2)
-                c3, m3, r3 = self._conv_bn(pre + "conv3", a2)
+                c1, s1 = self._conv_bn(pre + "conv1", x_in)
+                a1, m1, r1 = self._bn_apply(pre + "conv1", c1, s1)
+                c2, s2 = self._conv_bn(pre + "conv2", a1)
+                a2, m2, r2 = self._bn_apply(pre + "conv2", c2, s2)
+                c3, s3 = self._conv_bn(pre + "conv3", a2)
                 if b == 0:
-                    cs_, ms, rs = self._conv_bn(pre + "downsample", x_in)
-                    sc = self._bn_apply(pre + "downsample", cs_, ms, rs, relu=False)
+                    # out = relu(bn3(c3) + bn_ds(downsample(x))) in one pass: the normalised
+                    # shortcut is never materialised
+                    cs_, sds = self._conv_bn(pre + "downsample", x_in)
+                    rm, rv = P.running[pre + "downsample"]
+                    nd = pre + "downsample.bn."
+                    out, m3, r3, ms, rs = self._bn_apply(
+                        pre + "conv3", c3, s3, residual=cs_, relu=True,
+                        res_bn=(sds[0], sds[1], P.P(nd + "gamma"), P.P(nd + "beta"), rm, rv))
                     ds = (cs_, ms, rs)
                 else:
-                    sc, ds = x_in, None
-                out = self._bn_apply(pre + "conv3", c3, m3, r3, residual=sc, relu=True)
+                    ds = None
+                    out, m3, r3 = self._bn_apply(pre + "conv3", c3, s3, residual=x_in, relu=True)
                 blocks.append((pre, x_in, (c1, m1, r1, a1), (c2, m2, r2, a2), (c3, m3, r3), ds, out))
                 x = out
         pooled = CN.avgpool_fwd(x)                               # [N, 2048]

@@ -305,6 +305,40 @@ def bn_apply(x, mean, rstd, gamma, beta, residual=None, relu=True):
     return y
 
 
+def bn_apply_stats(x, s, q, M, gamma, beta, residual=None, relu=True, eps=1e-5, run_mean=None,
+                   run_var=None, momentum=0.9, res_bn=None):
+    """Training-mode forward BatchNorm from the conv epilogue's column sums ``s`` / ``q``
+    (sum, sum of squares over ``M`` rows): ``bn_finalize`` + ``bn_apply`` in one launch on
+    the GPU (mean / rstd formed per thread, block 0 stores them and updates the running
+    statistics).  ``res_bn = (s2, q2, gamma2, beta2, run_mean2, run_var2)``: ``residual`` is
+    a raw conv output normalised by its own statistics before the add (a bottleneck's
+    downsample shortcut, never materialised).  Returns (y, mean, rstd) or, with ``res_bn``,
+    (y, mean, rstd, mean2, rstd2)."""
+    if not x.is_cuda:
+        mean, rstd = bn_finalize(s, q, M, eps, run_mean, run_var, momentum)
+        extra = ()
+        if res_bn is not None:
+            s2, q2, g2, b2, rm2, rv2 = res_bn
+            m2, r2 = bn_finalize(s2, q2, M, eps, rm2, rv2, momentum)
+            residual = bn_apply(residual, m2, r2, g2, b2, relu=False)
+            extra = (m2, r2)
+        return (bn_apply(x, mean, rstd, gamma, beta, residual, relu), mean, rstd) + extra
+    C = x.shape[-1]
+    mean = torch.empty(C, device=x.device)
+    rstd = torch.empty(C, device=x.device)
+    y = torch.empty_like(x)
+    s2 = q2 = g2 = b2 = rm2 = rv2 = m2 = r2 = None
+    if res_bn is not None:
+        s2, q2, g2, b2, rm2, rv2 = res_bn
+        m2 = torch.empty(C, device=x.device)
+        r2 = torch.empty(C, device=x.device)
+    hip().bn_apply_stats(x.numel() // C, C, ptr(x), ptr(s), ptr(q), float(eps), ptr(mean), ptr(rstd),
+                         ptr(run_mean), ptr(run_var), float(momentum), ptr(gamma), ptr(beta),
+                         ptr(residual), int(relu), ptr(y), ptr(s2), ptr(q2), ptr(g2), ptr(b2),
+                         ptr(m2), ptr(r2), ptr(rm2), ptr(rv2), stream_handle())
+    return (y, mean, rstd) if res_bn is None else (y, mean, rstd, m2, r2)
+
+
 def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, relu=True, want_dres=False,
            grads_zeroed=False):
     """Backward of y = act(bn(x) [+ res]).  Accumulates dgamma/dbeta; returns (dx, dres)

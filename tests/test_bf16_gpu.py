@@ -157,7 +157,15 @@ def test_gemm_8phase_epilogues_and_splitk(cfg8, gpu):
     cs = torch.zeros(N, device=gpu)
     yb = bf16.gemm(x, w, False, True, colsum=cs)
     assert (cs - yb.float().sum(0)).abs().max().item() < 2e-2 * M ** 0.5
-    # split-K weight gradient on the 8-phase tile
+    # activation gradient (GELU') + f32 accumulation into C (beta = 1)
+    pre = _rand(M, N, dev=gpu, seed=18, scale=2.0)
+    c0 = torch.randn(M, N, device=gpu)
+    c = c0.clone()
+    bf16.gemm(x, w, False, True, act_grad="gelu", aux_in=pre, out=c, beta=1.0)
+    u2 = pre.float().requires_grad_()
+    gg, = torch.autograd.grad(torch.nn.functional.gelu(u2, approximate="tanh").sum(), u2)
+    assert (c - (c0 + (x.float() @ w.float().t()) * gg)).abs().max().item() < 1e-3 * K ** 0.5
+    # split-K weight gradient on the large tile
     T = 4096
     dy = _rand(T, 512, dev=gpu, seed=16)
     xx = _rand(T, 256, dev=gpu, seed=17)

@@ -147,6 +147,45 @@ def test_batchnorm_fwd_bwd(gpu):
     assert torch.allclose(db.cpu(), dbr, atol=1e-2, rtol=1e-3)
 
 
+@pytest.mark.parametrize("C", [64, 96, 2048])  # 96: the general (per-element channel) path
+def test_batchnorm_apply_from_sums(gpu, C):
+    """Fused finalize + apply (bn_apply_stats): mean / rstd / running statistics and the output
+    match bn_finalize + bn_apply on the CPU; with res_bn the residual (a raw conv output) is
+    normalised by its own statistics and affine before the add."""
+    N, H, W = 4, 7, 9
+    M = N * H * W
+    x = _r(N, H, W, C, seed=20, scale=2).to(BF) + 1
+    r = _r(N, H, W, C, seed=21, scale=3).to(BF) - 0.5
+    g1, b1 = _r(C, seed=22) * 0.1 + 1, _r(C, seed=23) * 0.1
+    g2, b2 = _r(C, seed=24) * 0.1 + 1, _r(C, seed=25) * 0.1
+    xf, rf = x.float().reshape(M, C), r.float().reshape(M, C)
+    s1, q1, s2, q2 = xf.sum(0), (xf * xf).sum(0), rf.sum(0), (rf * rf).sum(0)
+    # single BN, residual added as is
+    rm, rv = torch.zeros(C), torch.ones(C)
+    yr, mr, rr = cnn.bn_apply_stats(x, s1, q1, M, g1, b1, r, True, 1e-5, rm, rv)
+    rmg, rvg = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    y, m, rs = cnn.bn_apply_stats(x.to(gpu), s1.to(gpu), q1.to(gpu), M, g1.to(gpu), b1.to(gpu),
+                                  r.to(gpu), True, 1e-5, rmg, rvg)
+    assert torch.allclose(m.cpu(), mr, atol=1e-5) and torch.allclose(rs.cpu(), rr, rtol=1e-4)
+    assert torch.allclose(rmg.cpu(), rm, atol=1e-5) and torch.allclose(rvg.cpu(), rv, rtol=1e-4)
+    # (one bf16 ulp of outputs up to ~6)
+    assert (y.cpu().float() - yr.float()).abs().max() < 1e-2 * yr.float().abs().max() + 1e-2
+    # residual through its own BN (the downsample shortcut of a bottleneck)
+    rm1, rv1, rm2, rv2 = torch.zeros(C), torch.ones(C), torch.zeros(C), torch.ones(C)
+    yr, mr, rr, mr2, rr2 = cnn.bn_apply_stats(x, s1, q1, M, g1, b1, r, True, 1e-5, rm1, rv1,
+                                              res_bn=(s2, q2, g2, b2, rm2, rv2))
+    dev = [t.to(gpu) for t in (rm1.new_zeros(C), rv1.new_ones(C), rm2.new_zeros(C), rv2.new_ones(C))]
+    y, m, rs, m2, r2 = cnn.bn_apply_stats(
+        x.to(gpu), s1.to(gpu), q1.to(gpu), M, g1.to(gpu), b1.to(gpu), r.to(gpu), True, 1e-5, dev[0],
+        dev[1], res_bn=(s2.to(gpu), q2.to(gpu), g2.to(gpu), b2.to(gpu), dev[2], dev[3]))
+    for a, b in ((m, mr), (m2, mr2), (dev[0], rm1), (dev[2], rm2)):
+        assert torch.allclose(a.cpu(), b, atol=1e-5)
+    for a, b in ((rs, rr), (r2, rr2), (dev[1], rv1), (dev[3], rv2)):
+        assert torch.allclose(a.cpu(), b, rtol=1e-4)
+    # (the CPU reference rounds the normalised shortcut to bf16 before the add)
+    assert (y.cpu().float() - yr.float()).abs().max() < 2e-2 * yr.float().abs().max() + 1e-2
+
+
 def test_pools(gpu):
     x = _r(2, 15, 16, 64, seed=9).to(BF)
     y, idx = cnn.maxpool_fwd(x.to(gpu))
