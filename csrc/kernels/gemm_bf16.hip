@@ -1125,9 +1125,23 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
     }
     const bool use_ws = splitk > 1 && splitk_ws_ok(ws, ws_floats, splitk, M, Nn, out, ldo);
     if (use_ws) e.ws = ws;
-    launch_cfg<3, true, false, true>(choose_cfg(M, Nn, splitk, 3), dim3(1, splitk, 1), M, Nn, K,
-                                     (const unsigned short*)a, Cout, (const unsigned short*)b, 0,
-                                     out, ldo, e, 0LL, 0LL, 0LL, d, stream);
+    static const bool plain1x1w = [] {  // DTFX_CONV1X1_WGRAD_GEMM=0: 1x1 wgrads on the gather path
+      const char* v = getenv("DTFX_CONV1X1_WGRAD_GEMM");
+      return v ? atoi(v) != 0 : true;
+    }();
+    if (plain1x1w && KH == 1 && KW == 1 && stride == 1 && pad == 0 && K % gb::BK == 0) {
+      // a 1x1 stride-1 weight gradient is the plain product dW[co][ci] = sum_p dy[p][co] x[p][ci]
+      // (A^T B, both operands k-strided): staged by the plain glds loader instead of the
+      // im2col gather, whose per-lane pixel / tap address math (4 float divmods per 16-B
+      // chunk) ran these at 370-430 TFLOP/s (profiles/r3/evidence/resnet_layers.jsonl)
+      launch_cfg<0, true, false, true>(choose_cfg(M, Nn, splitk, 0, true), dim3(1, splitk, 1), M, Nn,
+                                       K, (const unsigned short*)a, Cout, (const unsigned short*)b, C,
+                                       out, ldo, e, 0LL, 0LL, 0LL, d, stream);
+    } else {
+      launch_cfg<3, true, false, true>(choose_cfg(M, Nn, splitk, 3), dim3(1, splitk, 1), M, Nn, K,
+                                       (const unsigned short*)a, Cout, (const unsigned short*)b, 0,
+                                       out, ldo, e, 0LL, 0LL, 0LL, d, stream);
+    }
     if (use_ws) splitk_reduce(M, Nn, splitk, ws, (float*)out, ldo, beta, stream);
   } else {
     throw std::runtime_error("conv_bf16: mode must be 1 (fwd), 2 (dgrad) or 3 (wgrad)");
