@@ -15,6 +15,7 @@ tail -1 "$OUT/bench_mlp_k20.json" | cut -c 1-160; tail -1 "$OUT/bench_mlp.json" 
 step bert
 timeout -k 10 200 python bench.py --model bert > "$OUT/bench_bert.json" 2>&1 || exit 1
 timeout -k 10 200 python bench.py --model bert --bert_batch 32 --seq_len 512 > "$OUT/bench_bert512.json" 2>&1 || exit 1
+timeout -k 10 200 python bench.py --model bert --bert_batch 256 > "$OUT/bench_bert_b256.json" 2>&1 || exit 1
 tail -1 "$OUT/bench_bert.json" | cut -c 1-180; tail -1 "$OUT/bench_bert512.json" | cut -c 1-180
 step resnet
 timeout -k 10 200 python bench.py --model resnet50 > "$OUT/bench_resnet.json" 2>&1 || exit 1
