@@ -163,58 +163,68 @@ __global__ __launch_bounds__(NC <= 2 ? 512 : 256) void layernorm_bwd_kernel(
   }
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(T, r0 + rows_per_block);
-  bf16x8 xb[NC], yb[NC], rb[NC];
-  float mean = 0.f, rstd = 0.f;
-  auto load = [&](int row) {
+  // Two rows in flight per wave beyond the one being reduced (register double buffer, two
+  // rows per trip so the buffer index stays literal): with one, every row waited out most of
+  // a memory round trip (the kernel ran at ~1/2 of its HBM bound at the BERT shape).
+  bf16x8 xb[2][NC], yb[2][NC], rb[2][NC];
+  float mb[2] = {0.f, 0.f}, rsb[2] = {0.f, 0.f};
+  auto load = [&](int p, int row) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int ch = min(lane + 64 * c, nch - 1);  // clamped: masked at use
-      xb[c] = *(const bf16x8*)(x + (size_t)row * H + ch * 8);
-      yb[c] = *(const bf16x8*)(dy + (size_t)row * H + ch * 8);
-      if (dres) rb[c] = *(const bf16x8*)(dres + (size_t)row * H + ch * 8);
+      xb[p][c] = *(const bf16x8*)(x + (size_t)row * H + ch * 8);
+      yb[p][c] = *(const bf16x8*)(dy + (size_t)row * H + ch * 8);
+      if (dres) rb[p][c] = *(const bf16x8*)(dres + (size_t)row * H + ch * 8);
     }
-    mean = mean_in[row];
-    rstd = rstd_in[row];
+    mb[p] = mean_in[row];
+    rsb[p] = rstd_in[row];
   };
-  int row = r0 + wave;
-  if (row < r1) load(row);
-  for (; row < r1; row += NWV) {
-    float xh[NC][8], g[NC][8], dyv[NC][8], rv[NC][8];
-    float s1 = 0.f, s2 = 0.f;
-    const float mu = mean, rs = rstd;
+  const int first = r0 + wave;
+  const int nrows = first < r1 ? (r1 - first + NWV - 1) / NWV : 0;  // rows of this wave
+  if (nrows > 0) load(0, first);
+  if (nrows > 1) load(1, first + NWV);
+  for (int i = 0; i < nrows; i += 2) {
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const bool ok = lane + 64 * c < nch;
-      float xv[8];
-      unpack8(xb[c], xv);
-      unpack8(yb[c], dyv[c]);
-      if (dres) unpack8(rb[c], rv[c]);
+    for (int p = 0; p < 2; ++p) {
+      if (i + p >= nrows) break;
+      const int row = first + (i + p) * NWV;
+      float xh[NC][8], g[NC][8], dyv[NC][8], rv[NC][8];
+      float s1 = 0.f, s2 = 0.f;
+      const float mu = mb[p], rs = rsb[p];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (!ok) dyv[c][u] = 0.f;
-        xh[c][u] = (xv[u] - mu) * rs;
-        g[c][u] = dyv[c][u] * gm[c][u];
-        s1 += g[c][u];
-        s2 += g[c][u] * xh[c][u];
-        dg[c][u] += dyv[c][u] * xh[c][u];
-        db[c][u] += dyv[c][u];
-      }
-    }
-    if (row + NWV < r1) load(row + NWV);  // next row in flight during the reductions
-    s1 = wave_sum(s1) / H;
-    s2 = wave_sum(s2) / H;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int ch = lane + 64 * c;
-      if (ch < nch) {
-        float o[8];
+      for (int c = 0; c < NC; ++c) {
+        const bool ok = lane + 64 * c < nch;
+        float xv[8];
+        unpack8(xb[p][c], xv);
+        unpack8(yb[p][c], dyv[c]);
+        if (dres) unpack8(rb[p][c], rv[c]);
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          o[u] = rs * (g[c][u] - s1 - xh[c][u] * s2);
-          if (dres) o[u] += rv[c][u];
-          ds[c][u] += o[u];
+          if (!ok) dyv[c][u] = 0.f;
+          xh[c][u] = (xv[u] - mu) * rs;
+          g[c][u] = dyv[c][u] * gm[c][u];
+          s1 += g[c][u];
+          s2 += g[c][u] * xh[c][u];
+          dg[c][u] += dyv[c][u] * xh[c][u];
+          db[c][u] += dyv[c][u];
         }
-        *(bf16x8*)(dx + (size_t)row * H + ch * 8) = pack8(o);
+      }
+      if (i + p + 2 < nrows) load(p, row + 2 * NWV);  // in flight during the reductions
+      s1 = wave_sum(s1) / H;
+      s2 = wave_sum(s2) / H;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ch = lane + 64 * c;
+        if (ch < nch) {
+          float o[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            o[u] = rs * (g[c][u] - s1 - xh[c][u] * s2);
+            if (dres) o[u] += rv[c][u];
+            ds[c][u] += o[u];
+          }
+          *(bf16x8*)(dx + (size_t)row * H + ch * 8) = pack8(o);
+        }
       }
     }
   }
@@ -1070,7 +1080,7 @@ void layernorm_bwd_launch(int T, int H, const void* dy, const void* x, const flo
   check_h(H);
   if (T <= 0) return;
   // BERT 16384 rows: 256 blocks (measured 16: 54 us, 32: 35, 64: 31, 128: 38 -- atomics vs
-  // parallelism).  DTFX_LN_RPB overrides (sweeps).
+  // parallelism; with two rows in flight per wave 32: 33.9, 64: 26.5, 128: 29.8 us).  DTFX_LN_RPB overrides (sweeps).
   static const int rpb_env = [] {
     const char* e = getenv("DTFX_LN_RPB");
     return e ? atoi(e) : 0;
