@@ -48,6 +48,7 @@
 #include "common.h"
 #include "xgmi_ll.h"
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -62,7 +63,8 @@ constexpr int KW = D / KS;     // 112 = 7 groups of 16
 constexpr int FT = D / 16;     // 49 feature tiles (dW1)
 constexpr int KS2 = 14;        // K slices of the pipelined step's fused apply+forward launch
 constexpr int KW2 = D / KS2;   // 56 features = 3.5 MFMA groups of 16
-constexpr int NSLAB_MAX = KS2; // slab planes in the workspace
+constexpr int KS3 = 28;        // ... the single-GPU form: 28 slices of 28 features (203 blocks)
+constexpr int NSLAB_MAX = KS3; // slab planes in the workspace
 constexpr int OFF_W1 = 0;
 constexpr int OFF_B1 = H * D;
 constexpr int OFF_W2 = OFF_B1 + H;
@@ -623,7 +625,14 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
 // TRACE (probe builds, tools/probes/mlp_pipelined_trace.py): per wave, s_memrealtime stamps
 // 0 entry, 1 phase-A operands landed, 2 W1 tile applied (after the barrier), 3 slab stored;
 // small-parameter blocks: 0 entry, 3 done.  tr: [blocks * 4 waves][4].
-template <int NGT, int XW = 0, bool TRACE = false, bool TWO = false>
+// KSX: K slices (blocks per hidden tile).  KS2 = 14 (56 features, 105 blocks, every
+// data-parallel engine); KS3 = 28 for the single-GPU step: 203 blocks on the 256 CUs instead of
+// 105, phase A's K (the batch) split over two waves per 16-column group (partials added
+// through LDS) and phase B's z1 partial over 28 features -- per wave 14 + 8..16 f32 MFMAs
+// instead of 28 + 16..32.  f32 MFMAs issue at 32 cycles each on one SIMD, so with one wave
+// per SIMD the MFMA issue itself set the two phases' length (profiles/r3/mlp_trace/pmc.md:
+// 41 % of the waves' cycles were issue stalls).
+template <int NGT, int XW = 0, bool TRACE = false, bool TWO = false, int KSX = KS2>
 __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
     const float* __restrict__ x_prev, const float* __restrict__ x, Bufs w, int* __restrict__ ctr,
@@ -637,22 +646,29 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
   constexpr int MAXG = NGT > 0 ? NGT : MAXB / 16;
+  constexpr int KWX = D / KSX;            // features per block
+  constexpr int NCG = (KWX + 15) / 16;     // 16-column groups of the W1 tile (4 or 2)
+  constexpr int KSP = 4 / NCG;             // phase-A K splits (waves per column group)
+  constexpr int G2 = (KWX + 15) / 16;      // phase-B 16-feature groups
+  static_assert(KSX * KWX == D && KWX % 4 == 0 && NCG * KSP == 4, "K slicing");
+  static_assert(XW == 0 || KSX == KS2, "the exchange engines use the 14-slice layout");
   const int bid = blockIdx.x;
-  if (bid >= HT * KS2) {
-    const int jt = bid - HT * KS2;
+  if (bid >= HT * KSX) {
+    const int jt = bid - HT * KSX;
     wgrad_small<true, NGT, XW>(jt, wave, lane, MLP_XG_SMALL_EPOCH + jt * 4 + wave, p_new, lr,
                                nullptr, w, ctr, stats, stats_ring, B, xg, p_old, stats_on);
     if (TRACE) trace_stamp(trw, 3);
     return;
   }
-  constexpr int LW = KW2 + 4;  // LDS row pitch (floats)
+  constexpr int LW = KWX + 4;  // LDS row pitch (floats)
   __shared__ float Wt[16][LW];
-  const int jt = bid / KS2, ks = bid % KS2;
-  const int f0 = ks * KW2;
+  __shared__ float Kred[KSP > 1 ? NCG : 1][64][4];  // phase-A K-split partials
+  const int jt = bid / KSX, ks = bid % KSX;
+  const int f0 = ks * KWX;
   // phase B's x rows are independent of phase A: requested first, so the whole launch
   // makes one memory round trip (B <= 128 -> at most 2 row tiles per wave held here)
   constexpr int RTW = 2;
-  float4 xa[RTW][4];
+  float4 xa[RTW][G2];
   float rmv[RTW];
 #pragma unroll
   for (int t = 0; t < RTW; ++t) {
@@ -660,54 +676,69 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     const float* xr = x + (size_t)(row < B ? row : B - 1) * D + f0;
     rmv[t] = row < B ? 1.f : 0.f;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G2; ++g) {
       const int k = 16 * g + 4 * q;
-      xa[t][g] = f4(xr + (k < KW2 ? k : 0));
+      xa[t][g] = f4(xr + (k < KWX ? k : 0));
     }
   }
 
-  // ---- phase A: this wave's 16 x 16 slice of the updated W1 tile ---------------------
+  // ---- phase A: this wave's 16 x 16 slice of the updated W1 tile (K split sp of KSP) -----
   {
-    const int fl = wave * 16 + r;           // feature within the 56-wide slice
-    const bool cv = fl < KW2;               // wave 3: 8 live columns
-    const int fc = f0 + (cv ? fl : KW2 - 1);
+    const int cgp = wave % NCG, sp = wave / NCG;
+    const int fl = cgp * 16 + r;            // feature within the block's slice
+    const bool cv = fl < KWX;               // (14 slices: wave 3 has 8 live columns)
+    const int fc = f0 + (cv ? fl : KWX - 1);
     const float* a = w.dz1T + (size_t)(jt * 16 + r) * BP + q * 4;
     const float* xc = x_prev + fc;
-    float4 av[MAXG];
-    float xv[MAXG][4];
-    float pw[4];
+    constexpr int GPS = (MAXG + KSP - 1) / KSP;  // batch groups per K split
+    const int g0 = sp * GPS;
+    float4 av[GPS];
+    float xv[GPS][4];
+    float pw[4] = {0.f, 0.f, 0.f, 0.f};
     const unsigned ep = XW > 0 ? xg.epochs[bid * 4 + wave] + 1 : 0u;
 #pragma unroll
-    for (int g = 0; g < MAXG; ++g) {
+    for (int gg = 0; gg < GPS; ++gg) {
+      const int g = g0 + gg;
       if (g < NG) {
-        av[g] = f4(a + g * 16);
+        av[gg] = f4(a + g * 16);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int b = g * 16 + q * 4 + e;  // rows >= B: dz1T is zero there
-          xv[g][e] = xc[(size_t)(b < B ? b : B - 1) * D];
+          xv[gg][e] = xc[(size_t)(b < B ? b : B - 1) * D];
         }
       }
     }
+    if (sp == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = jt * 16 + q * 4 + i;
-      pw[i] = p_old[OFF_W1 + (size_t)(j < H ? j : H - 1) * D + fc];
+      for (int i = 0; i < 4; ++i) {
+        const int j = jt * 16 + q * 4 + i;
+        pw[i] = p_old[OFF_W1 + (size_t)(j < H ? j : H - 1) * D + fc];
+      }
     }
     __builtin_amdgcn_sched_barrier(0);  // all loads in flight together
     if (TRACE) trace_stamp(trw, 1);
     f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
-    for (int g = 0; g < MAXG; ++g) {
-      if (g < NG) {
-        acc0 = mfma16x16x4(av[g].x, xv[g][0], acc0);
-        acc1 = mfma16x16x4(av[g].y, xv[g][1], acc1);
-        acc0 = mfma16x16x4(av[g].z, xv[g][2], acc0);
-        acc1 = mfma16x16x4(av[g].w, xv[g][3], acc1);
+    for (int gg = 0; gg < GPS; ++gg) {
+      if (g0 + gg < NG) {
+        acc0 = mfma16x16x4(av[gg].x, xv[gg][0], acc0);
+        acc1 = mfma16x16x4(av[gg].y, xv[gg][1], acc1);
+        acc0 = mfma16x16x4(av[gg].z, xv[gg][2], acc0);
+        acc1 = mfma16x16x4(av[gg].w, xv[gg][3], acc1);
       }
     }
     float gv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) gv[i] = acc0[i] + acc1[i];
+    if constexpr (KSP > 1) {  // the later K split's partial joins split 0 (fixed order)
+      if (sp > 0)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Kred[cgp][lane][i] = gv[i];
+      __syncthreads();
+      if (sp == 0)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gv[i] += Kred[cgp][lane][i];
+    }
     bool fail = false;
     if constexpr (XW > 0) {
       size_t offw[4];
@@ -721,13 +752,15 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
       if constexpr (TWO) xg_exchange2<XW>(xg, ep, offw, okw, gv, fail, lane);
       else xg_exchange<XW>(xg, ep, offw, okw, gv, fail);
     }
+    if (sp == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int hl = q * 4 + i, j = jt * 16 + hl;
-      const float v = fail ? pw[i] : pw[i] - lr * gv[i];  // timed out: keep W1 (err raised)
-      if (cv) {
-        Wt[hl][fl] = j < H ? v : 0.f;  // padded hidden rows contribute exact zeros
-        if (j < H) p_new[OFF_W1 + (size_t)j * D + f0 + fl] = v;
+      for (int i = 0; i < 4; ++i) {
+        const int hl = q * 4 + i, j = jt * 16 + hl;
+        const float v = fail ? pw[i] : pw[i] - lr * gv[i];  // timed out: keep W1 (err raised)
+        if (cv) {
+          Wt[hl][fl] = j < H ? v : 0.f;  // padded hidden rows contribute exact zeros
+          if (j < H) p_new[OFF_W1 + (size_t)j * D + f0 + fl] = v;
+        }
       }
     }
     if constexpr (XW > 0) {
@@ -738,36 +771,36 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
   __syncthreads();
   if (TRACE) trace_stamp(trw, 2);
 
-  // ---- phase B: z1 partial over the block's 56 features, row tiles rt = wave, wave + 4, ..
-  // lane (r, q): A = x[rt*16 + r][f0 + 16g + 4q + e], B = Wt[r][16g + 4q + e]; group 3 has
-  // 8 live features (q < 2)
-  float4 wb[4];
+  // ---- phase B: z1 partial over the block's KWX features, row tiles rt = wave, wave + 4,
+  // ..  lane (r, q): A = x[rt*16 + r][f0 + 16g + 4q + e], B = Wt[r][16g + 4q + e]; the last
+  // group is partly live (14 slices: 8 features, q < 2; 28 slices: 12, q < 3)
+  float4 wb[G2];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
+  for (int g = 0; g < G2; ++g) {
     const int k = 16 * g + 4 * q;
-    wb[g] = k < KW2 ? *reinterpret_cast<const float4*>(&Wt[r][k]) : float4{0.f, 0.f, 0.f, 0.f};
+    wb[g] = k < KWX ? *reinterpret_cast<const float4*>(&Wt[r][k]) : float4{0.f, 0.f, 0.f, 0.f};
   }
   for (int rt = wave, t = 0; rt < RT; rt += 4, ++t) {
-    float4 xg[4];
+    float4 xg[G2];
     float rm;
     if (t < RTW) {  // prefetched (wave-uniform)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) xg[g] = t == 0 ? xa[0][g] : xa[1][g];
+      for (int g = 0; g < G2; ++g) xg[g] = t == 0 ? xa[0][g] : xa[1][g];
       rm = t == 0 ? rmv[0] : rmv[1];
     } else {        // B > 128: later row tiles load here
       const int row = rt * 16 + r;
       const float* xr = x + (size_t)(row < B ? row : B - 1) * D + f0;
       rm = row < B ? 1.f : 0.f;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < G2; ++g) {
         const int k = 16 * g + 4 * q;
-        xg[g] = f4(xr + (k < KW2 ? k : 0));
+        xg[g] = f4(xr + (k < KWX ? k : 0));
       }
     }
     f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      // (wb is zero for the dead half of group 3, so no mask is needed on xg there)
+    for (int g = 0; g < G2; ++g) {
+      // (wb is zero for the dead part of the last group, so no mask is needed on xg there)
       acc0 = mfma16x16x4(xg[g].x * rm, wb[g].x, acc0);
       acc1 = mfma16x16x4(xg[g].y * rm, wb[g].y, acc1);
       acc0 = mfma16x16x4(xg[g].z * rm, wb[g].z, acc0);
@@ -1235,7 +1268,17 @@ void mlp_wgrad_factor_launch(float* p, float lr, const float* x, long long xstri
 }
 
 
-// Pipelined single-GPU step (see mlp_fwdapply_kernel): K1' then the head over KS2 slabs.
+// K slices of the single-GPU pipelined step (fwdapply + head agree on it): KS3 = 28, or
+// DTFX_MLP_KS=14 for the layout of the data-parallel engines (A/B runs).
+static int mlp_single_ks() {
+  static const int ks = [] {
+    const char* e = std::getenv("DTFX_MLP_KS");
+    return e && std::atoi(e) == 14 ? 14 : 28;
+  }();
+  return ks;
+}
+
+// Pipelined single-GPU step (see mlp_fwdapply_kernel): K1' then the head over the K slabs.
 void mlp_fwdapply_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
                          const float* x, float* ws, int* ctr, float* stats, int stats_ring, int B,
                          int stats_on, hipStream_t stream) {
@@ -1245,13 +1288,26 @@ void mlp_fwdapply_launch(const float* p_old, float* p_new, float lr, const float
     throw std::runtime_error("mlp_fwdapply: needs distinct ping-pong buffers, both batches, ctr");
   if (stats && stats_ring < 1) throw std::runtime_error("mlp_fwdapply: stats_ring < 1");
   const Bufs w = make_bufs(ws, B);
-  dim3 grid(HT * KS2 + HT), block(256);
-  if ((B + 15) / 16 == 7)
-    hipLaunchKernelGGL((mlp_fwdapply_kernel<7>), grid, block, 0, stream, p_old, p_new, lr, x_prev,
-                       x, w, ctr, stats, stats_ring, B, stats_on, MlpXg{});
-  else
-    hipLaunchKernelGGL((mlp_fwdapply_kernel<0>), grid, block, 0, stream, p_old, p_new, lr, x_prev,
-                       x, w, ctr, stats, stats_ring, B, stats_on, MlpXg{});
+  const bool rt7 = (B + 15) / 16 == 7;
+  if (mlp_single_ks() == KS3) {
+    dim3 grid(HT * KS3 + HT), block(256);
+    if (rt7)
+      hipLaunchKernelGGL((mlp_fwdapply_kernel<7, 0, false, false, KS3>), grid, block, 0, stream, p_old,
+                         p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B, stats_on, MlpXg{},
+                         nullptr);
+    else
+      hipLaunchKernelGGL((mlp_fwdapply_kernel<0, 0, false, false, KS3>), grid, block, 0, stream, p_old,
+                         p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B, stats_on, MlpXg{},
+                         nullptr);
+  } else {
+    dim3 grid(HT * KS2 + HT), block(256);
+    if (rt7)
+      hipLaunchKernelGGL((mlp_fwdapply_kernel<7>), grid, block, 0, stream, p_old, p_new, lr, x_prev,
+                         x, w, ctr, stats, stats_ring, B, stats_on, MlpXg{});
+    else
+      hipLaunchKernelGGL((mlp_fwdapply_kernel<0>), grid, block, 0, stream, p_old, p_new, lr, x_prev,
+                         x, w, ctr, stats, stats_ring, B, stats_on, MlpXg{});
+  }
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
@@ -1314,8 +1370,12 @@ void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipSt
   using namespace mlp;
   check_b(B);
   const Bufs w = make_bufs(ws, B);
-  hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS2>), dim3(B), dim3(64), 0, stream, p, p,
-                     0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr);
+  if (mlp_single_ks() == KS3)
+    hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS3>), dim3(B), dim3(64), 0, stream, p, p,
+                       0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr);
+  else
+    hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS2>), dim3(B), dim3(64), 0, stream, p, p,
+                       0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
@@ -1340,6 +1400,7 @@ void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float 
   float* bufs[2] = {p0, p1};
   const size_t xb = (size_t)B * D;
   const bool rt7 = (B + 15) / 16 == 7;
+  const bool ks3 = mlp_single_ks() == KS3;
   for (int i = 0; i < n; ++i) {
     const int prev = (pos + nbatches - 1) % nbatches;
     const float* xcur = x + (size_t)pos * xb;
@@ -1348,15 +1409,29 @@ void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float 
     float* pn = bufs[cur ^ 1];
     const float l = pending ? lr : 0.f;  // (pending doubles as the kernel's "apply / record
                                          //  the previous step" flag, as in step_pipelined)
-    if (rt7)
-      hipLaunchKernelGGL((mlp_fwdapply_kernel<7>), dim3(HT * KS2 + HT), dim3(256), 0, stream, po,
-                         pn, l, xprev, xcur, w, ctr, stats, stats_ring, B, pending, MlpXg{});
-    else
-      hipLaunchKernelGGL((mlp_fwdapply_kernel<0>), dim3(HT * KS2 + HT), dim3(256), 0, stream, po,
-                         pn, l, xprev, xcur, w, ctr, stats, stats_ring, B, pending, MlpXg{});
-    hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS2>), dim3(B), dim3(64), 0, stream, pn,
-                       pn, 0.f, nullptr, labels + (size_t)pos * B, w, B, nullptr, MlpXg{},
-                       nullptr);
+    if (ks3) {
+      if (rt7)
+        hipLaunchKernelGGL((mlp_fwdapply_kernel<7, 0, false, false, KS3>), dim3(HT * KS3 + HT),
+                           dim3(256), 0, stream, po, pn, l, xprev, xcur, w, ctr, stats, stats_ring,
+                           B, pending, MlpXg{}, nullptr);
+      else
+        hipLaunchKernelGGL((mlp_fwdapply_kernel<0, 0, false, false, KS3>), dim3(HT * KS3 + HT),
+                           dim3(256), 0, stream, po, pn, l, xprev, xcur, w, ctr, stats, stats_ring,
+                           B, pending, MlpXg{}, nullptr);
+      hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS3>), dim3(B), dim3(64), 0, stream, pn,
+                         pn, 0.f, nullptr, labels + (size_t)pos * B, w, B, nullptr, MlpXg{},
+                         nullptr);
+    } else {
+      if (rt7)
+        hipLaunchKernelGGL((mlp_fwdapply_kernel<7>), dim3(HT * KS2 + HT), dim3(256), 0, stream, po,
+                           pn, l, xprev, xcur, w, ctr, stats, stats_ring, B, pending, MlpXg{});
+      else
+        hipLaunchKernelGGL((mlp_fwdapply_kernel<0>), dim3(HT * KS2 + HT), dim3(256), 0, stream, po,
+                           pn, l, xprev, xcur, w, ctr, stats, stats_ring, B, pending, MlpXg{});
+      hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS2>), dim3(B), dim3(64), 0, stream, pn,
+                         pn, 0.f, nullptr, labels + (size_t)pos * B, w, B, nullptr, MlpXg{},
+                         nullptr);
+    }
     cur ^= 1;
     pending = 1;
     pos = (pos + 1) % nbatches;

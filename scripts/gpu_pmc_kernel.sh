@@ -12,12 +12,14 @@ for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONF
   timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d "$OUT/p$i" -o run -- python $R/$PMC_CMD > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   f=$(find "$OUT/p$i" -name "*counter_collection.csv" | head -1)
   [ -n "$f" ] && python - "$f" "${KFILTER:-}" <<'PY'
-import csv, sys, collections
+import csv, sys, collections, re
 rows = list(csv.DictReader(open(sys.argv[1])))
 agg = collections.defaultdict(float); n = collections.Counter()
 for r in rows:
     if sys.argv[2] not in r.get("Kernel_Name", ""): continue
-    agg[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]] += 1
-for k in sorted(agg): print("%-28s %16.0f  (%d dispatch rows)" % (k, agg[k], n[k]))
+    kn = re.sub(r"\(.*$", "", r["Kernel_Name"]).replace("void ", "").replace("dtfx::", "")[:60]
+    key = (kn, r["Counter_Name"])
+    agg[key] += float(r["Counter_Value"]); n[key] += 1
+for k in sorted(agg): print("%-60s %-26s %16.0f  (%d dispatch rows)" % (k[0], k[1], agg[k], n[k]))
 PY
 done
