@@ -26,7 +26,8 @@ long long mlp_workspace_floats(int);
 void mlp_tf_layout_launch(const float*, float*, int, const float*, int, hipStream_t);
 void mlp_fwdapply_launch(const float*, float*, float, const float*, const float*, float*, int*,
                          float*, int, int, int, hipStream_t);
-void mlp_head2_launch(const float*, const int*, float*, int, hipStream_t);
+void mlp_head2_launch(const float*, const int*, float*, int, hipStream_t, int);
+int mlp_single_ks_query();
 void mlp_pipelined_trace_launch(const float*, float*, float, const float*, const float*,
                                 const int*, float*, int*, float*, int, int, hipStream_t,
                                 unsigned long long*, unsigned long long*);
@@ -105,6 +106,8 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("p_old"), py::arg("p_new"), py::arg("lr"), py::arg("x_prev"), py::arg("x"),
      py::arg("ws"), py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"),
      py::arg("stats_on"), py::arg("stream"));
+  m.def("mlp_single_ks", &dtfx::mlp_single_ks_query,
+        "K slices of the single-GPU pipelined MLP step (28, or 14 with DTFX_MLP_KS=14)");
   m.def("mlp_pipelined_trace", [](uintptr_t p_old, uintptr_t p_new, float lr, uintptr_t x_prev,
                                    uintptr_t x, uintptr_t lab, uintptr_t ws, uintptr_t ctr,
                                    uintptr_t stats, int ring, int B, uintptr_t s, uintptr_t trf,
@@ -115,9 +118,12 @@ PYBIND11_MODULE(_hip, m) {
                                      reinterpret_cast<unsigned long long*>(trf),
                                      reinterpret_cast<unsigned long long*>(trh));
   });
-  m.def("mlp_head2", [](uintptr_t p, uintptr_t lab, uintptr_t ws, int B, uintptr_t s) {
-    dtfx::mlp_head2_launch(P<const float>(p), P<const int>(lab), P<float>(ws), B, S(s));
-  }, py::arg("p"), py::arg("labels"), py::arg("ws"), py::arg("B"), py::arg("stream"));
+  m.def("mlp_head2", [](uintptr_t p, uintptr_t lab, uintptr_t ws, int B, uintptr_t s, int nslab) {
+    dtfx::mlp_head2_launch(P<const float>(p), P<const int>(lab), P<float>(ws), B, S(s), nslab);
+  }, py::arg("p"), py::arg("labels"), py::arg("ws"), py::arg("B"), py::arg("stream"),
+     py::arg("nslab") = 0,
+     "head of the 2-launch step; nslab: slabs the first launch wrote (0: the single-GPU "
+     "step's, 14: every data-parallel engine's)");
   m.def("mlp_run_pipelined", [](uintptr_t p0, uintptr_t p1, int cur, int pending, float lr,
                                 uintptr_t x, uintptr_t lab, int nbatches, int pos, int n,
                                 uintptr_t ws, uintptr_t ctr, uintptr_t stats, int ring, int B,

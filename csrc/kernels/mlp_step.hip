@@ -178,21 +178,37 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
   const unsigned ep = XW > 0 ? xg.epochs[MLP_XG_HEAD_EPOCH + row] + 1 : 0u;
   const bool publish = APPLY && row == 0;
 
-  // All loads first, unconditional (j clamped to < H), masked afterwards.
+  // All loads first, unconditional (clamped), masked afterwards.  Lane l owns the ADJACENT
+  // hidden units 2l, 2l + 1 (lanes 0..49), so every per-unit operand -- the NSLAB partial
+  // z1 slabs, b1, the 10 W2 columns -- arrives as one 8-B load per pair: 49 load
+  // instructions per lane instead of 88 (more than the 63 a wave can keep in flight:
+  // the 28-slab step waited out a second round trip here).
   float hv[2], w2[2][C], zs[2], b1v[2], b2v[C];
   int jj[2];
   bool jv[2];
+  const int j0 = min(2 * lane, H - 2);  // (H even: j0, j0 + 1 always a valid, aligned pair)
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int j = lane + 64 * u;
-    jv[u] = j < H;
-    jj[u] = jv[u] ? j : H - 1;
+    jv[u] = 2 * lane + u < H;
+    jj[u] = j0 + u;
     zs[u] = 0.f;
+  }
 #pragma unroll
-    for (int s = 0; s < NSLAB; ++s) zs[u] += w.slab[((size_t)s * BP + row) * HP + jj[u]];
-    b1v[u] = p_old[OFF_B1 + jj[u]];
+  for (int s = 0; s < NSLAB; ++s) {
+    const float2 v = *reinterpret_cast<const float2*>(&w.slab[((size_t)s * BP + row) * HP + j0]);
+    zs[0] += v.x;
+    zs[1] += v.y;
+  }
+  {
+    const float2 v = *reinterpret_cast<const float2*>(&p_old[OFF_B1 + j0]);
+    b1v[0] = v.x;
+    b1v[1] = v.y;
+  }
 #pragma unroll
-    for (int c = 0; c < C; ++c) w2[u][c] = p_old[OFF_W2 + c * H + jj[u]];
+  for (int c = 0; c < C; ++c) {
+    const float2 v = *reinterpret_cast<const float2*>(&p_old[OFF_W2 + c * H + j0]);
+    w2[0][c] = v.x;
+    w2[1][c] = v.y;
   }
 #pragma unroll
   for (int c = 0; c < C; ++c) b2v[c] = p_old[OFF_B2 + c];
@@ -267,7 +283,7 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
   float dzv[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int j = lane + 64 * u;
+    const int j = 2 * lane + u;
     dzv[u] = 0.f;
     if (j < H) {
       float dh = 0.f;
@@ -283,7 +299,7 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     const int me = xg.rank;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {  // push first: every peer's wait overlaps ours
-      const int j = lane + 64 * u;
+      const int j = 2 * lane + u;
       if (j < H) {
         const long long off = (long long)j * BP + row;
         const u64 wd = xgll::word(dzv[u], ep);
@@ -296,7 +312,7 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     bool fail = false;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int j = lane + 64 * u;
+      const int j = 2 * lane + u;
       if (j < H) {
         const long long off = (long long)j * BP + row;
         float vals[XW];
@@ -1349,8 +1365,9 @@ void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const fl
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
-// Probe: one pipelined step with in-kernel stamps in both launches (trf: 105 * 4 * 4,
-// trh: B * 4 entries); batch 100 only.
+// Probe: one pipelined step with in-kernel stamps in both launches (trf: (7 * ks + 7) * 4 * 4
+// with ks = mlp_single_ks_query(), trh: B * 4 entries); batch 100 only.
+int mlp_single_ks_query() { return mlp_single_ks(); }
 void mlp_pipelined_trace_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
                                 const float* x, const int* labels, float* ws, int* ctr,
                                 float* stats, int stats_ring, int B, hipStream_t stream,
@@ -1359,18 +1376,31 @@ void mlp_pipelined_trace_launch(const float* p_old, float* p_new, float lr, cons
   check_b(B);
   if ((B + 15) / 16 != 7) throw std::runtime_error("mlp_pipelined_trace: batch 97..112 only");
   const Bufs w = make_bufs(ws, B);
-  hipLaunchKernelGGL((mlp_fwdapply_kernel<7, 0, true>), dim3(HT * KS2 + HT), dim3(256), 0, stream,
-                     p_old, p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B, 1, MlpXg{}, trf);
-  hipLaunchKernelGGL((mlp_head_kernel<false, true, 0, KS2>), dim3(B), dim3(64), 0, stream, p_new,
-                     p_new, 0.f, nullptr, labels, w, B, trh, MlpXg{}, nullptr);
+  if (mlp_single_ks() == KS3) {
+    hipLaunchKernelGGL((mlp_fwdapply_kernel<7, 0, true, false, KS3>), dim3(HT * KS3 + HT), dim3(256),
+                       0, stream, p_old, p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B, 1,
+                       MlpXg{}, trf);
+    hipLaunchKernelGGL((mlp_head_kernel<false, true, 0, KS3>), dim3(B), dim3(64), 0, stream, p_new,
+                       p_new, 0.f, nullptr, labels, w, B, trh, MlpXg{}, nullptr);
+  } else {
+    hipLaunchKernelGGL((mlp_fwdapply_kernel<7, 0, true>), dim3(HT * KS2 + HT), dim3(256), 0, stream,
+                       p_old, p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B, 1, MlpXg{}, trf);
+    hipLaunchKernelGGL((mlp_head_kernel<false, true, 0, KS2>), dim3(B), dim3(64), 0, stream, p_new,
+                       p_new, 0.f, nullptr, labels, w, B, trh, MlpXg{}, nullptr);
+  }
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
-void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipStream_t stream) {
+// nslab: the K slabs the first launch wrote -- 0: the single-GPU step's (mlp_single_ks());
+// the data-parallel engines' first launches (fused, fused2x, factor) always write KS2 = 14.
+void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipStream_t stream,
+                      int nslab) {
   using namespace mlp;
   check_b(B);
+  if (nslab == 0) nslab = mlp_single_ks();
+  if (nslab != KS2 && nslab != KS3) throw std::runtime_error("mlp_head2: nslab must be 0, 14 or 28");
   const Bufs w = make_bufs(ws, B);
-  if (mlp_single_ks() == KS3)
+  if (nslab == KS3)
     hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS3>), dim3(B), dim3(64), 0, stream, p, p,
                        0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr);
   else

@@ -35,6 +35,9 @@ NPARAM = OFF_B2 + C
 MAX_BATCH = 256
 
 
+# partial z1 slabs the data-parallel engines' first launch writes (their K slicing)
+XG_SLABS = 14
+
 def unflatten(p):
     """Views (W1t [H,D], b1 [H], W2t [C,H], b2 [C]) into a flat buffer."""
     return (p[OFF_W1:OFF_B1].view(H, D), p[OFF_B1:OFF_W2], p[OFF_W2:OFF_B2].view(C, H),
@@ -96,8 +99,8 @@ def step_pipelined(p_old, p_new, x_prev, x, labels, ws: StepWorkspace, lr, apply
     """Two-launch single-GPU step: ``mlp_fwdapply`` applies the PREVIOUS step's SGD update
     (from the factors dz1/h/dlogits the last head left in ``ws`` and the previous batch
     ``x_prev``; W1 never materialises a gradient) reading ``p_old`` and writing ``p_new``,
-    and runs this step's forward on the updated W1; ``mlp_head`` (14 partial slabs)
-    finishes the step.  ``apply=False`` (nothing pending): a plain copy + forward.  The
+    and runs this step's forward on the updated W1; ``mlp_head2`` (28 partial z1 slabs:
+    the single-GPU K slicing, ``hip().mlp_single_ks()``) finishes the step.  ``apply=False`` (nothing pending): a plain copy + forward.  The
     last step's update stays pending until ``flush_pipelined``."""
     _check(x, labels, ws.B)
     _check(x_prev, None, ws.B)
@@ -146,7 +149,7 @@ def step_xgmi_pipelined(p_old, p_new, x_prev, x, labels, ws: StepWorkspace, lr, 
     if p_old.data_ptr() == p_new.data_ptr():
         raise ValueError("the pipelined step needs distinct ping-pong buffers")
     comm.mlp_fwdapply(p_old, p_new, lr, x_prev, x, ws, apply, stats)
-    hip().mlp_head2(ptr(p_new), ptr(labels), ptr(ws.buf), ws.B, stream_handle())
+    hip().mlp_head2(ptr(p_new), ptr(labels), ptr(ws.buf), ws.B, stream_handle(), XG_SLABS)
 
 
 def flush_xgmi(p_old, p_new, x_prev, ws: StepWorkspace, lr, comm, stats=True):

@@ -167,7 +167,10 @@ def _ws_views(ws):
     B = ws.B
     BP = (B + 15) // 16 * 16
     HP = mlp_step.HP
-    o = 14 * BP * HP
+    # workspace = [slab planes][BP][HP] | hbuf | dz1T | dlT [16][BP] | rowstat [2 BP]; the
+    # number of slab planes (the largest K slicing of any first launch) from its size
+    planes = (ws.buf.numel() - 2 * BP * HP - 18 * BP) // (BP * HP)
+    o = planes * BP * HP
     hbuf = ws.buf[o:o + BP * HP].view(BP, HP)
     o += BP * HP
     dz1T = ws.buf[o:o + HP * BP].view(HP, BP)
@@ -184,7 +187,7 @@ def _plain_fwd_head(p, x, y, ws):
 
 
 def _pipelined_fwd_head(p, x, y, ws):
-    """Pipelined layout (14 slabs): copy-only fwdapply + head2 -> factors of (p, x) in ws."""
+    """Single-GPU pipelined layout: copy-only fwdapply + head2 -> factors of (p, x) in ws."""
     from distributedtensorflowexample_amd.ops._ext import hip, ptr, stream_handle
 
     h, s = hip(), stream_handle()
@@ -311,7 +314,7 @@ def test_fused2_fwdapply_exchange_simulated_peers(gpu, world, rank, B):
         exp = po.double().cpu() - lr * _expected_update(own, peers, rank)
         torch.cuda.synchronize()
         comm.mlp_fwdapply(po, pn, lr, xp, xn, ws, True)
-        hip().mlp_head2(ptr(pn), ptr(yn), ptr(ws.buf), ws.B, stream_handle())
+        hip().mlp_head2(ptr(pn), ptr(yn), ptr(ws.buf), ws.B, stream_handle(), 14)
         comm.check()
         err = float((pn.double().cpu() - exp).abs().max())
         assert err <= 2e-5, (epoch, err)
@@ -460,7 +463,7 @@ def test_factor2_fwdapply_simulated_peers(gpu, world, rank, B):
     _stage_param_words(comm, regs, peers, 1, lo, mlp_step.NPARAM)
     torch.cuda.synchronize()
     comm.mlp_fwdapply_factor(p_old, p_new, lr, x_prev, x, x_all.stride(0), dz1A, ws, True)
-    hip().mlp_head2(ptr(p_new), ptr(y), ptr(ws.buf), ws.B, stream_handle())
+    hip().mlp_head2(ptr(p_new), ptr(y), ptr(ws.buf), ws.B, stream_handle(), 14)
     comm.check()
     upd = _expected_update(own, peers, rank)
     upd[:lo] = gW1
@@ -630,7 +633,7 @@ def test_fused2_two_shot_exchange_simulated_peers(gpu, world, rank):
         exp[:n1][~mine] = po.double().cpu()[:n1][~mine] - lr * owners_sum.double()[~mine]
         torch.cuda.synchronize()
         comm.mlp_fwdapply(po, pn, lr, xp, xn, ws, True)
-        hip().mlp_head2(ptr(pn), ptr(yn), ptr(ws.buf), ws.B, stream_handle())
+        hip().mlp_head2(ptr(pn), ptr(yn), ptr(ws.buf), ws.B, stream_handle(), 14)
         comm.check()
         err = float((pn.double().cpu() - exp).abs().max())
         assert err <= 2e-5, (epoch, err)

@@ -3,9 +3,10 @@ s_memrealtime stamps (100 MHz; every stamp waits for the wave's outstanding memo
 marks "everything issued before has landed").
 
 Steps 100 and 101 of a 200-step hipGraph chain run the traced kernels (same code, stamps
-added): mlp_fwdapply_kernel<7, 0, true> (98 W1-tile blocks x 4 waves: 0 entry, 1 phase-A
-operands landed, 2 W1 tile applied + barrier, 3 slab stored; 7 small-parameter blocks: 0, 3)
-and mlp_head_kernel<.., KS2> (100 one-wave blocks: 0 entry, 1 operands landed, 2 compute
+added): mlp_fwdapply_kernel<7, 0, true, .., KS> (7 x KS W1-tile blocks x 4 waves: 0 entry,
+1 phase-A operands landed, 2 W1 tile applied + barrier, 3 slab stored; 7 small-parameter
+blocks: 0, 3; KS = 28, or 14 with DTFX_MLP_KS=14) and mlp_head_kernel<.., KS> (100 one-wave
+blocks: 0 entry, 1 operands landed, 2 compute
 done, 3 stores landed).  Prints per-phase medians / maxima and the kernel-to-kernel gaps
 (the dependent-launch boundaries a single-launch design would have to beat).
 
@@ -22,7 +23,7 @@ from distributedtensorflowexample_amd.models.mlp import init_params  # noqa: E40
 from distributedtensorflowexample_amd.ops import hip, mlp_step  # noqa: E402
 from distributedtensorflowexample_amd.ops._ext import ptr, stream_handle  # noqa: E402
 
-NB_W1, NB_SMALL = 98, 7
+NB_SMALL = 7
 
 
 def phases(t, cols):
@@ -39,6 +40,7 @@ def phases(t, cols):
 def main():
     dev = torch.device("cuda:0")
     h = hip()
+    NB_W1 = 7 * h.mlp_single_ks()
     B, nb = 100, 550
     p = [init_params(dev, 0), torch.empty(mlp_step.NPARAM, device=dev)]
     x = torch.rand(nb * B, 784, device=dev)
@@ -113,7 +115,7 @@ def main():
         g2.replay()
     e1.record()
     torch.cuda.synchronize()
-    out = {"traced_step_replays": reps,
+    out = {"k_slices": NB_W1 // 7, "traced_step_replays": reps,
            "untraced_us_per_step": round(e0.elapsed_time(e1) * 1e3 / 1000, 3)}
     print(json.dumps(out, indent=1))
 
