@@ -25,7 +25,7 @@ void mlp_wgrad_launch(float*, float, float*, const float*, float*, int*, float*,
 long long mlp_workspace_floats(int);
 void mlp_tf_layout_launch(const float*, float*, int, const float*, int, hipStream_t);
 void mlp_fwdapply_launch(const float*, float*, float, const float*, const float*, float*, int*,
-                         float*, int, int, int, hipStream_t);
+                         float*, int, int, int, hipStream_t, int);
 void mlp_head2_launch(const float*, const int*, float*, int, hipStream_t, int);
 int mlp_single_ks_query();
 void mlp_pipelined_trace_launch(const float*, float*, float, const float*, const float*,
@@ -99,13 +99,14 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"), py::arg("trace") = 0);
   m.def("mlp_fwdapply", [](uintptr_t p_old, uintptr_t p_new, float lr, uintptr_t x_prev,
                            uintptr_t x, uintptr_t ws, uintptr_t ctr, uintptr_t stats, int ring,
-                           int B, int stats_on, uintptr_t s) {
+                           int B, int stats_on, uintptr_t s, int ks) {
     dtfx::mlp_fwdapply_launch(P<const float>(p_old), P<float>(p_new), lr, P<const float>(x_prev),
                               P<const float>(x), P<float>(ws), P<int>(ctr), P<float>(stats), ring,
-                              B, stats_on, S(s));
+                              B, stats_on, S(s), ks);
   }, py::arg("p_old"), py::arg("p_new"), py::arg("lr"), py::arg("x_prev"), py::arg("x"),
      py::arg("ws"), py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"),
-     py::arg("stats_on"), py::arg("stream"));
+     py::arg("stats_on"), py::arg("stream"), py::arg("ks") = 0,
+     "first launch of the 2-launch step; ks: K slices (0: the single-GPU setting, 14, 28)");
   m.def("mlp_single_ks", &dtfx::mlp_single_ks_query,
         "K slices of the single-GPU pipelined MLP step (28, or 14 with DTFX_MLP_KS=14)");
   m.def("mlp_pipelined_trace", [](uintptr_t p_old, uintptr_t p_new, float lr, uintptr_t x_prev,

@@ -1297,7 +1297,7 @@ static int mlp_single_ks() {
 // Pipelined single-GPU step (see mlp_fwdapply_kernel): K1' then the head over the K slabs.
 void mlp_fwdapply_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
                          const float* x, float* ws, int* ctr, float* stats, int stats_ring, int B,
-                         int stats_on, hipStream_t stream) {
+                         int stats_on, hipStream_t stream, int ks) {
   using namespace mlp;
   check_b(B);
   if (!p_old || !p_new || p_old == p_new || !x_prev || !x || !ctr)
@@ -1305,7 +1305,9 @@ void mlp_fwdapply_launch(const float* p_old, float* p_new, float lr, const float
   if (stats && stats_ring < 1) throw std::runtime_error("mlp_fwdapply: stats_ring < 1");
   const Bufs w = make_bufs(ws, B);
   const bool rt7 = (B + 15) / 16 == 7;
-  if (mlp_single_ks() == KS3) {
+  if (ks == 0) ks = mlp_single_ks();
+  if (ks != KS2 && ks != KS3) throw std::runtime_error("mlp_fwdapply: ks must be 0, 14 or 28");
+  if (ks == KS3) {
     dim3 grid(HT * KS3 + HT), block(256);
     if (rt7)
       hipLaunchKernelGGL((mlp_fwdapply_kernel<7, 0, false, false, KS3>), grid, block, 0, stream, p_old,

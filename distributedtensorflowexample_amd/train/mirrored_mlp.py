@@ -40,8 +40,7 @@ def _dist_env():
 def train_mirrored(flags, dataset, log=print, max_steps=None):
     rank, world, local = _dist_env()
     use_gpu = torch.cuda.is_available() and flags.device != "cpu"
-    own_pg = world > 1 and not dist.is_initialized()  # (a caller's group stays the caller's)
-    if own_pg:
+    if world > 1 and not dist.is_initialized():
         dist.init_process_group("gloo")  # control plane; tensors over RCCL on GPU
     shared_gpu = os.environ.get("DTFX_SHARED_GPU") == "1"
     if use_gpu:
@@ -248,12 +247,15 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
                 break
         if is_chief:
             sv.save_checkpoint()
-    out = history, get_params()
-    if own_pg:
-        # orderly teardown: every rank (the chief's final checkpoint included) reaches here
-        # before any process group goes away -- a rank that exited while the store-hosting
-        # chief was still tearing down its gloo group died in std::terminate at interpreter
-        # exit now and then (tests/test_cluster_e2e.py, frequent checkpoints)
+    return history, get_params()
+
+
+def shutdown_mirrored():
+    """Orderly end of a mirrored run (the CLI's, main.py): every rank -- the chief's final
+    checkpoint included -- reaches a barrier before any process group goes away.  A rank that
+    exited while the store-hosting chief was still tearing its gloo group down died in
+    std::terminate at interpreter exit now and then (tests/test_cluster_e2e.py, frequent
+    checkpoints)."""
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
-    return out

@@ -52,10 +52,12 @@ def main(argv=None):
         train_model_mirrored(FLAGS)
         return 0
     if FLAGS.strategy == "mirrored":
-        from distributedtensorflowexample_amd.train.mirrored_mlp import train_mirrored
+        from distributedtensorflowexample_amd.train.mirrored_mlp import (shutdown_mirrored,
+                                                                         train_mirrored)
 
         mnist = read_data_sets(FLAGS.data_dir or None, one_hot=True, seed=FLAGS.seed)
         train_mirrored(FLAGS, mnist)
+        shutdown_mirrored()
         return 0
     if FLAGS.strategy != "ps_async":
         raise SystemExit("unknown --strategy %r" % FLAGS.strategy)

@@ -361,9 +361,9 @@ def test_factor_head_allgather_simulated_peers(gpu, world, rank, B, nslab):
         if nslab == 7:
             hip().mlp_fwd(ptr(p), 0, 0.0, 0, ptr(x), ptr(ws.buf), ws.B, stream_handle())
         else:
-            tmp = p.clone()
+            tmp = p.clone()  # (a first launch with the factor engines' 14-slice layout)
             hip().mlp_fwdapply(ptr(p), ptr(tmp), 0.0, ptr(x), ptr(x), ptr(ws.buf), ptr(ws.ctr),
-                               0, ws.stats_ring, ws.B, 0, stream_handle())
+                               0, ws.stats_ring, ws.B, 0, stream_handle(), ks=nslab)
         comm.mlp_head(p, y, ws, dz1A, nslab=nslab)
         comm.check()
         got = dz1A.cpu()
