@@ -293,7 +293,7 @@ def main():
 
         def run_k(mode):
             if mode == "host":
-                tr.run_launched(kp)
+                tr.run_launched(kp, flush=True)  # (the flush launched by the same call)
             elif mode == "persistent":
                 tr.run_persistent(kp)
             else:
@@ -332,7 +332,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if launch == "host":
-        tr.run_launched(a.steps)
+        tr.run_launched(a.steps, flush=True)  # the last step's update: one more launch, same call
     elif launch == "persistent":
         tr.run_persistent(a.steps)  # every update applied inside the launch
     else:

@@ -32,7 +32,9 @@ void mlp_pipelined_trace_launch(const float*, float*, float, const float*, const
                                 const int*, float*, int*, float*, int, int, hipStream_t,
                                 unsigned long long*, unsigned long long*);
 void mlp_run_pipelined_launch(float*, float*, int, int, float, const float*, const int*, int, int,
-                              int, float*, int*, float*, int, int, hipStream_t);
+                              int, float*, int*, float*, int, int, hipStream_t, int);
+void mlp_apply_launch(const float*, float*, float, const float*, float*, int*, float*, int, int,
+                      hipStream_t);
 long long mlp_persistent_ll_words();
 int mlp_persistent_blocks();
 int mlp_persistent_trace_steps();
@@ -128,14 +130,20 @@ PYBIND11_MODULE(_hip, m) {
   m.def("mlp_run_pipelined", [](uintptr_t p0, uintptr_t p1, int cur, int pending, float lr,
                                 uintptr_t x, uintptr_t lab, int nbatches, int pos, int n,
                                 uintptr_t ws, uintptr_t ctr, uintptr_t stats, int ring, int B,
-                                uintptr_t s) {
+                                uintptr_t s, int flush) {
     py::gil_scoped_release nogil;
     dtfx::mlp_run_pipelined_launch(P<float>(p0), P<float>(p1), cur, pending, lr, P<const float>(x),
                                    P<const int>(lab), nbatches, pos, n, P<float>(ws), P<int>(ctr),
-                                   P<float>(stats), ring, B, S(s));
+                                   P<float>(stats), ring, B, S(s), flush);
   }, py::arg("p0"), py::arg("p1"), py::arg("cur"), py::arg("pending"), py::arg("lr"), py::arg("x"),
      py::arg("labels"), py::arg("nbatches"), py::arg("pos"), py::arg("n"), py::arg("ws"),
-     py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"));
+     py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"),
+     py::arg("flush") = 0);
+  m.def("mlp_apply", [](uintptr_t p_old, uintptr_t p_new, float lr, uintptr_t x_prev, uintptr_t ws,
+                        uintptr_t ctr, uintptr_t stats, int ring, int B, uintptr_t s) {
+    dtfx::mlp_apply_launch(P<const float>(p_old), P<float>(p_new), lr, P<const float>(x_prev),
+                           P<float>(ws), P<int>(ctr), P<float>(stats), ring, B, S(s));
+  });
   m.def("mlp_persistent_ll_words", &dtfx::mlp_persistent_ll_words);
   m.def("mlp_persistent_blocks", &dtfx::mlp_persistent_blocks);
   m.def("mlp_persistent_trace_steps", &dtfx::mlp_persistent_trace_steps);

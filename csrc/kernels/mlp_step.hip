@@ -648,7 +648,9 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
 // instead of 28 + 16..32.  f32 MFMAs issue at 32 cycles each on one SIMD, so with one wave
 // per SIMD the MFMA issue itself set the two phases' length (profiles/r3/mlp_trace/pmc.md:
 // 41 % of the waves' cycles were issue stalls).
-template <int NGT, int XW = 0, bool TRACE = false, bool TWO = false, int KSX = KS2>
+// FWD = false (mlp_apply_launch: the pending update of the last pipelined step, the flush):
+// phase A and the small parameters only -- no forward, no x loads.
+template <int NGT, int XW = 0, bool TRACE = false, bool TWO = false, int KSX = KS2, bool FWD = true>
 __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
     const float* __restrict__ x_prev, const float* __restrict__ x, Bufs w, int* __restrict__ ctr,
@@ -687,7 +689,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
   float4 xa[RTW][G2];
   float rmv[RTW];
 #pragma unroll
-  for (int t = 0; t < RTW; ++t) {
+  for (int t = 0; t < (FWD ? RTW : 0); ++t) {
     const int row = (wave + 4 * t) * 16 + r;
     const float* xr = x + (size_t)(row < B ? row : B - 1) * D + f0;
     rmv[t] = row < B ? 1.f : 0.f;
@@ -774,7 +776,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         const int hl = q * 4 + i, j = jt * 16 + hl;
         const float v = fail ? pw[i] : pw[i] - lr * gv[i];  // timed out: keep W1 (err raised)
         if (cv) {
-          Wt[hl][fl] = j < H ? v : 0.f;  // padded hidden rows contribute exact zeros
+          if (FWD) Wt[hl][fl] = j < H ? v : 0.f;  // padded hidden rows contribute exact zeros
           if (j < H) p_new[OFF_W1 + (size_t)j * D + f0 + fl] = v;
         }
       }
@@ -784,6 +786,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
       if (fail) atomicExch(xg.err, 1);
     }
   }
+  if constexpr (!FWD) return;
   __syncthreads();
   if (TRACE) trace_stamp(trw, 2);
 
@@ -1329,6 +1332,35 @@ void mlp_fwdapply_launch(const float* p_old, float* p_new, float lr, const float
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+// The pending update of the last single-GPU pipelined step (the flush): W1 from step t's
+// factors and its small parameters, p_old -> p_new, with step t's loss / accuracy record and
+// global_step += 1 -- the first launch's apply half alone (mlp_fwdapply_kernel<.., FWD =
+// false>, the single-GPU K slicing), ~half the MFMAs per wave of the 3-launch step's
+// mlp_wgrad_kernel.
+void mlp_apply_launch(const float* p_old, float* p_new, float lr, const float* x_prev, float* ws,
+                      int* ctr, float* stats, int stats_ring, int B, hipStream_t stream) {
+  using namespace mlp;
+  check_b(B);
+  if (!p_old || !p_new || p_old == p_new || !x_prev || !ctr)
+    throw std::runtime_error("mlp_apply: needs distinct ping-pong buffers, the batch, ctr");
+  if (stats && stats_ring < 1) throw std::runtime_error("mlp_apply: stats_ring < 1");
+  const Bufs w = make_bufs(ws, B);
+  const bool rt7 = (B + 15) / 16 == 7;
+#define DTFX_AP(NGT, KSV)                                                                       \
+  hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, 0, false, false, KSV, false>), dim3(HT * KSV + HT), \
+                     dim3(256), 0, stream, p_old, p_new, lr, x_prev, x_prev, w, ctr, stats,        \
+                     stats_ring, B, 1, MlpXg{}, nullptr)
+  if (mlp_single_ks() == KS3) {
+    if (rt7) DTFX_AP(7, KS3);
+    else DTFX_AP(0, KS3);
+  } else {
+    if (rt7) DTFX_AP(7, KS2);
+    else DTFX_AP(0, KS2);
+  }
+#undef DTFX_AP
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
 // Pipelined fused data-parallel step, first launch (mlp_fwdapply_kernel<.., XW>); the head is
 // mlp_head2_launch.  lr already divided by the world size.
 void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
@@ -1418,10 +1450,12 @@ void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipSt
 // one by one while the host keeps queueing ahead (host ~2 us per launch < ~4 us of GPU time
 // per launch), so a short run starts at once.  Returns nothing: the caller advances its host
 // mirrors (batch position, parity, pending) by n.
+// flush != 0: the pending update of the last step is applied by one more launch
+// (mlp_apply_launch, into the other buffer: the parity then moves by n + 1).
 void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float lr,
                               const float* x, const int* labels, int nbatches, int pos, int n,
                               float* ws, int* ctr, float* stats, int stats_ring, int B,
-                              hipStream_t stream) {
+                              hipStream_t stream, int flush) {
   using namespace mlp;
   check_b(B);
   if (!p0 || !p1 || p0 == p1 || !x || !labels || !ctr || nbatches < 1 || pos < 0 ||
@@ -1467,6 +1501,11 @@ void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float 
     cur ^= 1;
     pending = 1;
     pos = (pos + 1) % nbatches;
+  }
+  if (flush && pending) {  // the last step's pending update: bufs[cur] -> bufs[cur ^ 1]
+    const int prev = (pos + nbatches - 1) % nbatches;
+    mlp_apply_launch(bufs[cur], bufs[cur ^ 1], lr, x + (size_t)prev * xb, ws, ctr, stats,
+                     stats_ring, B, stream);
   }
   DTFX_HIP_CHECK(hipGetLastError());
 }

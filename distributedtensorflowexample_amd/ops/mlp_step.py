@@ -114,12 +114,14 @@ def step_pipelined(p_old, p_new, x_prev, x, labels, ws: StepWorkspace, lr, apply
     h.mlp_head2(ptr(p_new), ptr(labels), ptr(ws.buf), ws.B, s)
 
 
-def flush_pipelined(p, x_prev, ws: StepWorkspace, lr, stats=True):
-    """Apply the pending update of the last pipelined step in place (the 3-launch step's
-    weight-gradient kernel in direct mode: same factors, same batch)."""
+def flush_pipelined(p_old, p_new, x_prev, ws: StepWorkspace, lr, stats=True):
+    """Apply the pending update of the last pipelined step, ``p_old`` -> ``p_new`` (the
+    ping-pong pair; the caller flips its parity): the apply half of ``mlp_fwdapply`` alone
+    (same factors, same batch, same K slicing), with the step's stats record."""
     _check(x_prev, None, ws.B)
-    _check_flat(p)
-    hip().mlp_wgrad(ptr(p), float(lr), 0, ptr(x_prev), ptr(ws.buf), ptr(ws.ctr),
+    _check_flat(p_old)
+    _check_flat(p_new)
+    hip().mlp_apply(ptr(p_old), ptr(p_new), float(lr), ptr(x_prev), ptr(ws.buf), ptr(ws.ctr),
                     ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B, stream_handle())
 
 

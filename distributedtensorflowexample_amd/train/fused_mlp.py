@@ -101,6 +101,7 @@ class FusedMLPTrainer:
         self._ll = None   # granule buffer of the persistent engine (allocated on first use)
         self._ebase = 0   # epoch base of its next launch
         self._unchecked = False  # a persistent launch whose hand-offs were not verified yet
+        self._host_args = None   # run_launched's cached launcher and buffer addresses
 
     # -- state --------------------------------------------------------------
     @property
@@ -139,7 +140,9 @@ class FusedMLPTrainer:
                 self.cur ^= 1
             elif self.pipelined:
                 xp, _ = self.batch((self.pos - 1) % self.nbatches)
-                mlp_step.flush_pipelined(self.bufs[self.cur], xp, self.ws, self.lr)
+                mlp_step.flush_pipelined(self.bufs[self.cur], self.bufs[self.cur ^ 1], xp, self.ws,
+                                         self.lr)
+                self.cur ^= 1
             else:
                 optim.sgd_(self.bufs[self.cur], self.grad, self.lr / self.world_size)
             self.pending = False
@@ -272,24 +275,34 @@ class FusedMLPTrainer:
         return (self.pipelined and self.world_size == 1 and self.fused_comm is None
                 and self.factor_comm is None and self.allreduce is None)
 
-    def run_launched(self, steps):
+    def run_launched(self, steps, flush=False):
         """``steps`` pipelined single-GPU steps issued by ONE C++ call (kernel launches, no
-        graph): no ~15 us graph-submission latency before the first kernel."""
-        from ..ops._ext import hip, ptr, stream_handle
-
+        graph): no ~15 us graph-submission latency before the first kernel.  ``flush``: the
+        last step's update is applied by the same call (one more launch, as ``flush()``).
+        The buffer addresses are read once: a short timed region (bench.py --steps 20) pays
+        the Python side of this call before its first kernel starts."""
         steps = int(steps)
         if not self.host_loop_ok:
             raise RuntimeError("run_launched: single-GPU pipelined step only")
         if steps <= 0:
+            if flush:
+                self.flush()
             return
-        ws = self.ws
-        hip().mlp_run_pipelined(ptr(self.bufs[0]), ptr(self.bufs[1]), self.cur,
-                                1 if self.pending else 0, self.lr, ptr(self.x), ptr(self.labels),
-                                self.nbatches, self.pos, steps, ptr(ws.buf), ptr(ws.ctr),
-                                ptr(ws.stats), ws.stats_ring, self.B, stream_handle())
+        a = self._host_args
+        if a is None:
+            from ..ops._ext import hip, ptr
+
+            ws = self.ws
+            a = self._host_args = (hip().mlp_run_pipelined, ptr(self.bufs[0]), ptr(self.bufs[1]),
+                                   ptr(self.x), ptr(self.labels), ptr(ws.buf), ptr(ws.ctr),
+                                   ptr(ws.stats), ws.stats_ring)
+        fn, p0, p1, xp, lp, wb, wc, wst, ring = a
+        fn(p0, p1, self.cur, 1 if self.pending else 0, self.lr, xp, lp, self.nbatches, self.pos,
+           steps, wb, wc, wst, ring, self.B, torch.cuda.current_stream(self.device).cuda_stream,
+           1 if flush else 0)
         self.pos = (self.pos + steps) % self.nbatches
-        self.cur ^= steps & 1
-        self.pending = True
+        self.cur ^= (steps + (1 if flush else 0)) & 1
+        self.pending = not flush
 
     # -- persistent single-launch engine (csrc/kernels/mlp_persistent.hip) ----------------
     @property

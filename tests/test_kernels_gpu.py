@@ -274,7 +274,7 @@ def test_host_loop_matches_graph_replay(gpu):
     p = init_params(gpu, seed=3)
     x, y = mnist_like_device(1300, seed=4, device=gpu)  # 13 batches: runs wrap the epoch
     runs = {}
-    for mode in ("graph", "host", "lead"):
+    for mode in ("graph", "host", "host_flush", "lead"):
         tr = FusedMLPTrainer(p, x, y, 100, 0.05)
         if mode == "graph":
             tr.run(3)
@@ -282,13 +282,17 @@ def test_host_loop_matches_graph_replay(gpu):
         elif mode == "host":
             tr.run_launched(3)
             tr.run_launched(20)
+        elif mode == "host_flush":  # the flush launched by the same call (bench.py's timed region)
+            tr.run_launched(3)
+            tr.run_launched(20, flush=True)
+            assert not tr.pending
         else:
             tr.run(3)
             tr.prepare(20, lead=4)
             tr.run(20, lead=4)
         st = tr.stats_range(0, 23).clone()
         runs[mode] = (tr.flush().clone(), tr.global_step(), st, tr.pos)
-    for mode in ("host", "lead"):
+    for mode in ("host", "host_flush", "lead"):
         assert torch.equal(runs[mode][0], runs["graph"][0]), mode
         assert runs[mode][1] == runs["graph"][1] == 23
         assert torch.equal(runs[mode][2], runs["graph"][2]), mode
