@@ -16,6 +16,7 @@ void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const v
 void colsum_bf16_launch(const void*, int, int, int, float*, float, hipStream_t);
 long long gemm_bf16_ws_floats(bool, bool, int, int, int, int, float);
 long long conv_wgrad_ws_floats(int, int, int, int, int, int, int, int, int);
+long long conv_splitk_ws_floats(int, int, int, int, int, int, int, int, int, int);
 void conv_bf16_launch(int, int, int, int, int, int, int, int, int, int, const void*, const void*, int,
                       void*, float, const void*, float*, float*, int, hipStream_t, const void*,
                       const void*, const float*, const float*, float*, long long);
@@ -116,6 +117,9 @@ void register_nn(py::module_& m) {
      py::arg("ws_floats") = 0);
   m.def("gemm_bf16_ws_floats", &dtfx::gemm_bf16_ws_floats,
         "f32 elements of split-K workspace gemm_bf16 would use (0: no split-K)");
+  m.def("conv_splitk_ws_floats", &dtfx::conv_splitk_ws_floats,
+        "f32 elements of split-K workspace a forward (mode 1) / stride-1 data-gradient (mode 2) "
+        "conv_bf16 would use (0: no split-K)");
   m.def("conv_wgrad_ws_floats", &dtfx::conv_wgrad_ws_floats,
         "f32 elements of split-K workspace a conv weight gradient would use (0: no split-K)");
   m.def("colsum_bf16", [](uintptr_t G, int M, int N, int ldg, uintptr_t out, float beta,

@@ -898,6 +898,102 @@ static void splitk_reduce(int M, int N, int S, const float* ws, float* C, int ld
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+// Epilogue of a split-K convolution (fwd / stride-1 dgrad with few output tiles, see
+// conv_splitk): y = sum_s ws[s] (split order) (+ residual) (* (relu_y > 0)) -> bf16, and the
+// BatchNorm statistics of one partial row per 64-row slab, exactly as the GEMM epilogue
+// writes them (fwd: sum / sum of squares of the f32 values; dgrad with bn_x: sum of the
+// stored bf16 values and of value * xhat).  Block: 64 rows x 256 columns, thread = 8 columns
+// x 8 rows (row lane rl = rows rl, rl + 8, ...); the 8 row lanes meet in LDS.
+__global__ __launch_bounds__(256) void conv_splitk_epi_kernel(
+    int M, int N, int S, const float* __restrict__ ws, unsigned short* __restrict__ y, int ldc,
+    const unsigned short* __restrict__ res, const unsigned short* __restrict__ relu_y,
+    const unsigned short* __restrict__ bn_x, const float* __restrict__ bn_mean,
+    const float* __restrict__ bn_rstd, float* __restrict__ psum, float* __restrict__ psq) {
+  __shared__ float red[2][8][257];
+  const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int n = blockIdx.x * 256 + cg * 8, m0 = blockIdx.y * 64;
+  const bool live_n = n < N;  // (N % 8 == 0)
+  const size_t plane = (size_t)M * N;
+  float cs[8], cq[8], mu[8], rs[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
+  if (bn_x && live_n) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      mu[u] = bn_mean[n + u];
+      rs[u] = bn_rstd[n + u];
+    }
+  }
+  if (live_n) {
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + rl + 8 * i;
+      if (m >= M) break;
+      const float* w = ws + (size_t)m * N + n;
+      float v[8];
+      *(f32x4*)&v[0] = *(const f32x4*)w;
+      *(f32x4*)&v[4] = *(const f32x4*)(w + 4);
+      for (int sp = 1; sp < S; ++sp) {
+        const f32x4 a = *(const f32x4*)(w + sp * plane), b = *(const f32x4*)(w + sp * plane + 4);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[u] += a[u];
+          v[u + 4] += b[u];
+        }
+      }
+      const size_t o = (size_t)m * ldc + n;
+      if (res) {
+        const bf16x8 r = *(const bf16x8*)&res[o];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r[u]);
+      }
+      if (relu_y) {
+        const bf16x8 a = *(const bf16x8*)&relu_y[o];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] *= bf2f((unsigned short)a[u]) > 0.f ? 1.f : 0.f;
+      }
+      bf16x8 out;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) out[u] = (short)f2bf(v[u]);
+      if (psum) {
+        if (bn_x) {
+          const bf16x8 xq = *(const bf16x8*)&bn_x[o];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float vr = bf2f((unsigned short)out[u]);
+            cs[u] += vr;
+            cq[u] += vr * (bf2f((unsigned short)xq[u]) - mu[u]) * rs[u];
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            cs[u] += v[u];
+            cq[u] += v[u] * v[u];
+          }
+        }
+      }
+      *(bf16x8*)&y[o] = out;
+    }
+  }
+  if (!psum) return;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    red[0][rl][cg * 8 + u] = cs[u];
+    red[1][rl][cg * 8 + u] = cq[u];
+  }
+  __syncthreads();
+  const int c = threadIdx.x, nc = blockIdx.x * 256 + c;
+  if (nc < N) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      a += red[0][r][c];
+      b += red[1][r][c];
+    }
+    psum[(size_t)blockIdx.y * N + nc] = a;
+    psq[(size_t)blockIdx.y * N + nc] = b;
+  }
+}
+
 // Split-K factor of a GEMM (splitk <= 0: auto) and its tile configuration.
 static int gemm_splitk(bool ta, bool out_f32, int M, int N, int K, int splitk, int batch, float beta,
                        bool plain_epilogue, int* cfg_out) {
@@ -1009,6 +1105,35 @@ static bool conv_ph8(int M, int N, int K, int zdim, int src_ch, long long src_el
          choose_cfg(M, N, zdim, 0) == 5;
 }
 
+// Split-K of a forward / stride-1 data-gradient convolution on the 8-phase tile: the layer4
+// shapes (M = 12544 pixels x 512 channels, K = 2048 .. 4608) have 98 256x256 tiles for 256 CUs,
+// so the 128x128 tile (392 blocks) was chosen and ran them at 450-510 TFLOP/s.  Two K splits on
+// the 8-phase tile (196 blocks, >= 8 K tiles each) + conv_splitk_epi_kernel instead.  1: none.
+// DTFX_CONV_SPLITK=0 disables (A/B runs).
+int conv_splitk(int mode, int N, int H, int W, int C, int Cout, int KH, int KW, int stride,
+                int pad) {
+  static const bool on = [] {
+    const char* v = getenv("DTFX_CONV_SPLITK");
+    return v ? atoi(v) != 0 : true;
+  }();
+  if (!on || gemm_cfg_env() >= 0 || (mode != 1 && !(mode == 2 && stride == 1))) return 1;
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  const int M = mode == 1 ? N * OH * OW : N * H * W, Nn = mode == 1 ? Cout : C;
+  const int K = KH * KW * (mode == 1 ? C : Cout), src_ch = mode == 1 ? C : Cout;
+  const long long src_elems = (long long)N * (mode == 1 ? H * W * C : OH * OW * Cout);
+  if (src_ch % 64 || Nn % 8 || src_elems * 2 >= 0x7fffffffLL) return 1;
+  const int tiles = ((M + 255) / 256) * ((Nn + 255) / 256), nkt = K / gb::BK;
+  if (tiles > 128) return 1;
+  return std::max(1, std::min(256 / tiles, nkt / 8));
+}
+long long conv_splitk_ws_floats(int mode, int N, int H, int W, int C, int Cout, int KH, int KW,
+                                int stride, int pad) {
+  const int s = conv_splitk(mode, N, H, W, C, Cout, KH, KW, stride, pad);
+  if (s <= 1) return 0;
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  return (long long)s * (mode == 1 ? (long long)N * OH * OW * Cout : (long long)N * H * W * C);
+}
+
 // Split-K of a conv weight gradient (M = Cout, N = KH*KW*C, K = pixels): one wave of the 512
 // resident 128x128 slots (see gemm_splitk)
 static int conv_wgrad_splitk(int M, int Nn, int K) {
@@ -1071,6 +1196,22 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
         return;
       }
     }
+    const int sk = conv_splitk(1, N, H, W, C, Cout, KH, KW, stride, pad);
+    if (sk > 1 && ws && ws_floats >= (long long)sk * M * Nn && ((uintptr_t)ws & 15) == 0 &&
+        (colsum != nullptr) == (colsq != nullptr)) {
+      GemmEpi ep{};
+      ep.alpha = 1.f;
+      ep.ws = ws;
+      launch_cfg<1, false, true, true>(5, dim3(1, sk, 1), M, Nn, K, (const unsigned short*)a, 0,
+                                       (const unsigned short*)b, ldw, ws, Nn, ep, 0LL, 0LL, 0LL, d,
+                                       stream);
+      hipLaunchKernelGGL(conv_splitk_epi_kernel, dim3((Nn + 255) / 256, (M + 63) / 64), dim3(256), 0,
+                         stream, M, Nn, sk, ws, (unsigned short*)out, Cout,
+                         (const unsigned short*)residual, nullptr, nullptr, nullptr, nullptr, colsum,
+                         colsq);
+      DTFX_HIP_CHECK(hipGetLastError());
+      return;
+    }
     const int cfg1 = conv_ph8(M, Nn, K, 1, C, (long long)N * H * W * C) ? 5 : choose_cfg(M, Nn, 1, 1);
     launch_cfg<1, false, true, false>(cfg1, dim3(1, 1, 1), M, Nn, K,
                                       (const unsigned short*)a, 0, (const unsigned short*)b, ldw,
@@ -1105,6 +1246,23 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
       const size_t bytes = sizeof(float) * (size_t)s * s * d.prc * C;
       if (colsum) DTFX_HIP_CHECK(hipMemsetAsync(colsum, 0, bytes, stream));
       if (colsq) DTFX_HIP_CHECK(hipMemsetAsync(colsq, 0, bytes, stream));
+    }
+    const int sk = conv_splitk(2, N, H, W, C, Cout, KH, KW, stride, pad);
+    if (sk > 1 && ws && ws_floats >= (long long)sk * M * Nn && ((uintptr_t)ws & 15) == 0 &&
+        (!e.col_partial || (colsum && colsq))) {
+      GemmEpi ep{};
+      ep.alpha = 1.f;
+      ep.ws = ws;
+      launch_cfg<2, false, false, true>(5, dim3(1, sk, 1), M, Nn, K, (const unsigned short*)a, 0,
+                                        (const unsigned short*)b, d.wld, ws, Nn, ep, 0LL, 0LL, 0LL,
+                                        d, stream);
+      hipLaunchKernelGGL(conv_splitk_epi_kernel, dim3((Nn + 255) / 256, (M + 63) / 64), dim3(256), 0,
+                         stream, M, Nn, sk, ws, (unsigned short*)out, C,
+                         (const unsigned short*)residual, (const unsigned short*)relu_y,
+                         (const unsigned short*)bn_x, bn_mean, bn_rstd,
+                         e.col_partial ? colsum : nullptr, e.col_partial ? colsq : nullptr);
+      DTFX_HIP_CHECK(hipGetLastError());
+      return;
     }
     const int cfg2 = conv_ph8(M, Nn, ((KH + s - 1) / s) * ((KW + s - 1) / s) * Cout, s * s, Cout, (long long)N * OH * OW * Cout)
                          ? 5 : choose_cfg(M, Nn, s * s, 2);

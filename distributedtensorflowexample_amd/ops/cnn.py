@@ -124,8 +124,12 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
         rows = (N * OH * OW + 63) // 64  # one partial row per 64-row output slab
         part = torch.empty(2, rows, Cout, device=x.device)
         ps, pq = part[0], part[1]
+    # few output tiles over a deep K (layer4): split-K partials + an epilogue pass
+    nws = hip().conv_splitk_ws_floats(1, N, H, W, C, Cout, KH, KW, stride, pad)
+    ws = torch.empty(nws, device=x.device) if nws else None
     hip().conv_bf16(1, N, H, W, C, Cout, KH, KW, stride, pad, ptr(x), ptr(w), w.stride(0), ptr(y),
-                    0.0, ptr(residual), ptr(ps), ptr(pq), 0, stream_handle())
+                    0.0, ptr(residual), ptr(ps), ptr(pq), 0, stream_handle(), ws=ptr(ws),
+                    ws_floats=nws)
     if colsum is not None:
         hip().colpart_reduce(ps.shape[0], Cout, ptr(ps), ptr(pq), ptr(colsum), ptr(colsq),
                              stream_handle())
@@ -207,9 +211,12 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
         hip().colpart_reduce(part.shape[1], C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
                              stream_handle())
         return dx
+    nws = hip().conv_splitk_ws_floats(2, N, H, W, C, Cout, KH, KW, stride, pad)
+    ws = torch.empty(nws, device=dy.device) if nws else None  # split-K partials (layer4)
     if bn is None:
         hip().conv_bf16(2, N, H, W, C, Cout, KH, KW, stride, pad, ptr(dy), ptr(w), w.stride(0),
-                        ptr(dx), 0.0, ptr(residual), 0, 0, 0, stream_handle())
+                        ptr(dx), 0.0, ptr(residual), 0, 0, 0, stream_handle(), ws=ptr(ws),
+                        ws_floats=nws)
         return dx
     y, x, mean, rstd, sdy, sdx = bn
     if y.shape != dx.shape or x.shape != dx.shape:
@@ -221,7 +228,8 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
     part = torch.empty(2, rows, C, device=dy.device)
     hip().conv_bf16(2, N, H, W, C, Cout, KH, KW, stride, pad, ptr(dy), ptr(w), w.stride(0),
                     ptr(dx), 0.0, ptr(residual), ptr(part[0]), ptr(part[1]), 0, stream_handle(),
-                    relu_y=ptr(y), bn_x=ptr(x), bn_mean=ptr(mean), bn_rstd=ptr(rstd))
+                    relu_y=ptr(y), bn_x=ptr(x), bn_mean=ptr(mean), bn_rstd=ptr(rstd), ws=ptr(ws),
+                    ws_floats=nws)
     hip().colpart_reduce(rows, C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx), stream_handle())
     return dx
 

@@ -37,6 +37,9 @@ CONVS = [  # N, H, W, C, Cout, k, stride, pad
     (2, 16, 16, 256, 64, 1, 1, 0),   # dgrad K = 64 -> 256 channels
     (2, 8, 8, 512, 128, 1, 1, 0),    # dgrad K = 128 -> 512 channels (16-pixel tiles)
     (2, 8, 8, 256, 128, 1, 1, 0),    # narrow forward 256 -> 128 (the two above: 256 -> 64, 512 -> 128)
+    (4, 14, 14, 256, 256, 3, 1, 1),  # few tiles, deep K: split-K fwd / dgrad + epilogue pass
+    (2, 7, 7, 512, 512, 3, 1, 1),    # ResNet layer4 conv2 shape: M = 98 (ragged 64-row slab)
+    (2, 7, 7, 2048, 512, 1, 1, 0),   # layer4 conv1 (1x1, K = 2048), split-K forward
 ]
 
 
@@ -88,8 +91,12 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, W, C, Co, k, s, p):
     (2, 8, 8, 128, 512, 1, 1, 0, False),   # narrow dgrad 512 -> 128
     (2, 8, 8, 128, 256, 1, 1, 0, False),   # narrow dgrad 256 -> 128
     (2, 8, 8, 128, 512, 1, 1, 0, True),    # narrow shape + shortcut gradient: implicit GEMM
+    (4, 14, 14, 256, 256, 3, 1, 1, True),  # split-K dgrad: BN backward in the epilogue pass
+    (2, 7, 7, 512, 512, 3, 1, 1, False),   # layer4 conv2 shape, ragged last statistics slab
+    (2, 7, 7, 512, 2048, 1, 1, 0, True),   # layer4 conv3 dgrad (K = 2048) + shortcut gradient
 ])
 def test_conv_dgrad_fused_batchnorm_backward(gpu, N, H, W, C, Co, k, s, p, with_res):
+    """(The last three cases take the split-K path: cnn.hip conv_splitk > 1.)"""
     """dgrad with BatchNorm backward's reductions in its epilogue (+ shortcut gradient, ReLU
     mask) and the apply-only BN kernel == dgrad, then the two-pass bn_bwd (f32 CPU path)."""
     c = _r(N, H, W, C, seed=11, scale=2).to(BF) + 0.5      # BN input (a conv output)

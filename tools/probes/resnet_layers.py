@@ -6,7 +6,7 @@ it, i.e. every conv except the stem and the down-sampling projection) and weight
 and reports time, TFLOP/s, the minimum HBM traffic and the roofline bound
 max(FLOP / 2.3 PF/s, bytes / 6.5 TB/s).  One JSON line per (layer, pass), then totals.
 
-    python tools/probes/resnet_layers.py [--batch 256] [--reps 20]
+    python tools/probes/resnet_layers.py [--batch 256] [--reps 20]   (env ONLY=layer4,layer3.0)
 """
 import argparse
 import json
@@ -53,6 +53,9 @@ def main():
         OH, OW = CN.out_hw(H, H, k, s, p)
         if name != "conv1" and name.endswith("conv2"):
             size = OH
+        only = os.environ.get("ONLY")  # comma list of layer-name prefixes (A/B runs)
+        if only and not name.startswith(tuple(only.split(","))):
+            continue
         x = torch.randn(N, H, H, cin, device=dev).to(BF16)
         w = (torch.randn(cout, CN.kpad(k, k, cin), device=dev) * 0.05).to(BF16)
         dy = torch.randn(N, OH, OW, cout, device=dev).to(BF16)
