@@ -5,6 +5,9 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd); OUT=$R/gpurun_out/ev; mkdir -p "$OUT"; export TMPDIR=/tmp
 step() { echo "== $1"; }
+# PART=1: tests + benches, PART=2: ps benches + profiles (two gpurun calls), default: all
+PART=${PART:-all}
+if [ "$PART" != 2 ]; then
 step tests
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
 tail -1 "$OUT/pytest_gpu.log"
@@ -22,6 +25,8 @@ timeout -k 10 200 python bench.py --model resnet50 > "$OUT/bench_resnet.json" 2>
 tail -1 "$OUT/bench_resnet.json" | cut -c 1-180
 timeout -k 10 240 python -u tools/probes/resnet_layers.py > "$OUT/resnet_layers.jsonl" 2>&1 || exit 1
 tail -1 "$OUT/resnet_layers.jsonl"
+fi
+[ "$PART" = 1 ] && exit 0
 step ps_async
 timeout -k 10 200 python tools/bench_ps_async.py --num_workers 2 --steps 40000 > "$OUT/ps_async_w2.json" 2>/dev/null || exit 1
 timeout -k 10 200 python tools/bench_ps_async.py --num_workers 2 --steps 40000 --ps_device gpu > "$OUT/ps_async_gpu_w2.json" 2>/dev/null || exit 1
