@@ -135,6 +135,53 @@ class FlatParams:
         edges = [0] + lay0 + [head0, self.numel]
         self.buckets = [(edges[i], edges[i + 1]) for i in range(len(edges) - 1)]
 
+        self._zero_views = None
+
+    # weight gradients that exactly one GEMM writes per step (beta = 0): never zeroed
+    @staticmethod
+    def overwritten(name):
+        return name.startswith("encoder/") and name.endswith("/kernel") or \
+            name == "cls/predictions/transform/dense/kernel"
+
+    def zero_grad(self):
+        """Zero the gradient slots that the backward ACCUMULATES into (embeddings, biases,
+        LayerNorm parameters -- atomics / beta = 1 epilogues) and the alignment padding; the
+        GEMM-written weight gradients (``overwritten``) are skipped: 85 of the 110 M slots
+        of BERT-base, ~0.34 GB of stores per step.  The per-layer ranges repeat at the layer
+        stride, so each becomes ONE strided view over all layers: a handful of launches."""
+        if self._zero_views is None:
+            keep, ranges, pos = [], [], 0
+            for name, shape, _ in self.layout:
+                if self.overwritten(name):
+                    off = self.offsets[name][0]
+                    keep.append((off, off + math.prod(shape)))
+            for a, b in sorted(keep):
+                if a > pos:
+                    ranges.append((pos, a))
+                pos = b
+            if pos < self.numel:
+                ranges.append((pos, self.numel))
+            lay = [self.offsets["encoder/layer_%d/attention/qkv/kernel" % l][0]
+                   for l in range(self.cfg.layers)]
+            stride = lay[1] - lay[0] if len(lay) > 1 else 0
+            periodic = len(lay) > 1 and all(lay[i + 1] - lay[i] == stride for i in range(len(lay) - 1))
+            rs, views = set(ranges), []
+            for a, b in ranges:
+                if (a, b) not in rs:
+                    continue  # already covered by a strided view
+                rel = a - lay[0]
+                if periodic and 0 <= rel < stride and all(
+                        (lay[l] + rel, lay[l] + rel + b - a) in rs for l in range(len(lay))):
+                    views.append(self.grad.as_strided((len(lay), b - a), (stride, 1), a))
+                    for l in range(len(lay)):
+                        rs.discard((lay[l] + rel, lay[l] + rel + b - a))
+                else:
+                    views.append(self.grad[a:b])
+                    rs.discard((a, b))
+            self._zero_views = views
+        for v in self._zero_views:
+            v.zero_()
+
     def view(self, flat, name):
         off, shape = self.offsets[name]
         return flat[off:off + math.prod(shape)].view(shape)
@@ -198,7 +245,7 @@ class BertMLM:
         if seq > cfg.max_pos:
             raise ValueError("sequence length %d exceeds max_pos %d" % (seq, cfg.max_pos))
         Tn = batch * seq
-        p.grad.zero_()
+        p.zero_grad()
         ids_f, tt_f = ids.reshape(-1), tt.reshape(-1)
         x0, h, me, re = TR.embed_ln_fwd(ids_f, tt_f, p.W("embeddings/word_embeddings"),
                                         p.W("embeddings/position_embeddings"),
@@ -234,7 +281,7 @@ class BertMLM:
                               p.G("cls/predictions/transform/LayerNorm/gamma"),
                               p.G("cls/predictions/transform/LayerNorm/beta"))
         dut = TR.act_grad(dt, ut, "gelu")
-        B16.gemm(dut, hm, True, False, out=p.G("cls/predictions/transform/dense/kernel"), beta=1.0)
+        B16.gemm(dut, hm, True, False, out=p.G("cls/predictions/transform/dense/kernel"), beta=0.0)
         B16.colsum(dut, out=p.G("cls/predictions/transform/dense/bias"), beta=1.0)
         dhm = B16.gemm(dut, p.W("cls/predictions/transform/dense/kernel"))
         if on_bucket_ready is not None:
@@ -244,13 +291,13 @@ class BertMLM:
         # ---- backward: encoder
         ws, keep = self.wgrad_stream, []  # keep: operands the side stream still reads
 
-        def wgrad(dy, xin, name):
+        def wgrad(dy, xin, name):  # the only writer of these slots: beta = 0 (zero_grad skips them)
             if ws is None:
-                B16.gemm(dy, xin, True, False, out=p.G(name), beta=1.0)
+                B16.gemm(dy, xin, True, False, out=p.G(name), beta=0.0)
                 return
             ws.wait_stream(torch.cuda.current_stream(dy.device))
             with torch.cuda.stream(ws):
-                B16.gemm(dy, xin, True, False, out=p.G(name), beta=1.0)
+                B16.gemm(dy, xin, True, False, out=p.G(name), beta=0.0)
             keep.append((dy, xin))
 
         for l in reversed(range(cfg.layers)):
