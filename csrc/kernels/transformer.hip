@@ -534,13 +534,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = mma(a, lfrag<false>(Vs, LDQ, 16 * j, 32 * kk, lane), o[j]);
     }
+    // through this wave's own P rows (consumed by the products above): 2 16-B stores per
+    // lane instead of 16 2-byte stores
+    char* stg = Ps + (size_t)r0 * LDP;
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = r0 + rg + r;
-      if (row < S)
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          out[((size_t)b * S + row) * Hd + h * D + 16 * j + cl] = tobf(o[j][r]);
+      for (int j = 0; j < 4; ++j)
+        *(unsigned short*)(stg + (rg + r) * LDP + (16 * j + cl) * 2) = tobf(o[j][r]);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = lane + 64 * u, row = r0 + (c >> 3), ch = c & 7;
+      const bf16x8 v = *(const bf16x8*)(stg + (c >> 3) * LDP + ch * 16);
+      if (row < S) *(bf16x8*)(out + ((size_t)b * S + row) * Hd + h * D + ch * 8) = v;
     }
   }
 }
@@ -659,18 +667,28 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_kernel(
         aq[j] = mma(dsr, lfrag<false>(Ks, LDQ, 16 * j, 32 * kk, lane), aq[j]);
       }
     }
+    // each 16 x 64 tile goes through this wave's rows of the V image (no longer read after
+    // the barrier above) and leaves as 16-B chunks: 6 global stores per lane instead of 48
+    // 2-byte stores
+    char* stg = Vs + (size_t)k0 * LDQ;
+    auto put = [&](const f32x4 (&acc)[4], float mul, unsigned short* dst) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = k0 + rg + r;
-      if (row < S)
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const size_t off = (size_t)row * ld + 16 * j + cl;
-          dv[off] = tobf(av[j][r]);
-          dk[off] = tobf(ak[j][r] * scale);
-          dq[off] = tobf(aq[j][r] * scale);
-        }
-    }
+        for (int j = 0; j < 4; ++j)
+          *(unsigned short*)(stg + (rg + r) * LDQ + (16 * j + cl) * 2) = tobf(acc[j][r] * mul);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = lane + 64 * u, row = k0 + (c >> 3), ch = c & 7;
+        const bf16x8 v = *(const bf16x8*)(stg + (c >> 3) * LDQ + ch * 16);
+        if (row < S) *(bf16x8*)(dst + (size_t)row * ld + ch * 8) = v;
+      }
+      __builtin_amdgcn_wave_barrier();  // read back before the next tile overwrites the rows
+    };
+    put(av, 1.f, dv);
+    put(ak, scale, dk);
+    put(aq, scale, dq);
     if (dbias) {  // fused qkv bias gradient: column sums over this wave's 16 rows
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
