@@ -634,15 +634,16 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
 // lr = 0 / stats_on = 0 (the first step after a flush): a pure copy p_old -> p_new.
 // Removes one dependent kernel boundary and one cold-load phase per step vs the 3-launch
 // step (fwd / head / wgrad).
-// XW > 0 (pipelined FUSED data-parallel engine): each wave's local 16x16 gradient slice is
-// exchanged in LL words with the XW - 1 peers (xg_exchange, epoch slot bid*4 + wave) and
-// summed in rank order before the apply -- the all-reduce of the 3-launch fused engine,
+// XW > 0 (pipelined FUSED data-parallel engine, launched with KSX = KS3): each 16x16 local
+// gradient slice (summed over the two K-split waves) is exchanged by its K-split-0 wave in LL
+// words with the XW - 1 peers (xg_exchange, epoch slot bid * NCG + column group) and summed
+// in rank order before the apply -- the all-reduce of the 3-launch fused engine,
 // moved into the next step's first launch (2 launches per data-parallel step).
 // TRACE (probe builds, tools/probes/mlp_pipelined_trace.py): per wave, s_memrealtime stamps
 // 0 entry, 1 phase-A operands landed, 2 W1 tile applied (after the barrier), 3 slab stored;
 // small-parameter blocks: 0 entry, 3 done.  tr: [blocks * 4 waves][4].
-// KSX: K slices (blocks per hidden tile).  KS2 = 14 (56 features, 105 blocks, every
-// data-parallel engine); KS3 = 28 for the single-GPU step: 203 blocks on the 256 CUs instead of
+// KSX: K slices (blocks per hidden tile).  KS2 = 14 (56 features, 105 blocks: the factor
+// engine's layout); KS3 = 28 for the single-GPU step and the fused engines: 203 blocks on the 256 CUs instead of
 // 105, phase A's K (the batch) split over two waves per 16-column group (partials added
 // through LDS) and phase B's z1 partial over 28 features -- per wave 14 + 8..16 f32 MFMAs
 // instead of 28 + 16..32.  f32 MFMAs issue at 32 cycles each on one SIMD, so with one wave
@@ -669,7 +670,6 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
   constexpr int KSP = 4 / NCG;             // phase-A K splits (waves per column group)
   constexpr int G2 = (KWX + 15) / 16;      // phase-B 16-feature groups
   static_assert(KSX * KWX == D && KWX % 4 == 0 && NCG * KSP == 4, "K slicing");
-  static_assert(XW == 0 || KSX == KS2, "the exchange engines use the 14-slice layout");
   const int bid = blockIdx.x;
   if (bid >= HT * KSX) {
     const int jt = bid - HT * KSX;
@@ -713,7 +713,9 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     float4 av[GPS];
     float xv[GPS][4];
     float pw[4] = {0.f, 0.f, 0.f, 0.f};
-    const unsigned ep = XW > 0 ? xg.epochs[bid * 4 + wave] + 1 : 0u;
+    // exchange-epoch slot of this 16 x 16 slice (the K split 0 wave exchanges the summed tile)
+    const int eslot = bid * NCG + cgp;
+    const unsigned ep = XW > 0 ? xg.epochs[eslot] + 1 : 0u;
 #pragma unroll
     for (int gg = 0; gg < GPS; ++gg) {
       const int g = g0 + gg;
@@ -758,7 +760,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         for (int i = 0; i < 4; ++i) gv[i] += Kred[cgp][lane][i];
     }
     bool fail = false;
-    if constexpr (XW > 0) {
+    if constexpr (XW > 0) if (sp == 0) {
       size_t offw[4];
       bool okw[4];
 #pragma unroll
@@ -781,8 +783,8 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         }
       }
     }
-    if constexpr (XW > 0) {
-      if (lane == 0) xg.epochs[bid * 4 + wave] = ep;
+    if constexpr (XW > 0) if (sp == 0) {
+      if (lane == 0) xg.epochs[eslot] = ep;
       if (fail) atomicExch(xg.err, 1);
     }
   }
@@ -1373,17 +1375,19 @@ void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const fl
     throw std::runtime_error("mlp_fwdapply_xg: needs distinct ping-pong buffers, both batches, ctr");
   if (stats && stats_ring < 1) throw std::runtime_error("mlp_fwdapply_xg: stats_ring < 1");
   if (xg.S < NPARAM) throw std::runtime_error("mlp_fwdapply_xg: exchange slots smaller than the model");
-  static_assert(HT * KS2 * 4 <= MLP_XG_SMALL_EPOCH, "W1 epoch slots overlap the small ones");
+  // 28 K slices (as the single-GPU step): 196 W1 blocks x 2 column groups of epoch slots
+  static_assert(HT * KS3 * 2 <= MLP_XG_SMALL_EPOCH, "W1 epoch slots overlap the small ones");
   const Bufs w = make_bufs(ws, B);
-  dim3 grid(HT * KS2 + HT), block(256);
+  dim3 grid(HT * KS3 + HT), block(256);
 #define DTFX_FX(WW, NGT)                                                                      \
   if (two_shot)                                                                               \
-    hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, WW, false, true>), grid, block, 0, stream,    \
-                       p_old, p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B, stats_on, xg, \
-                       nullptr);                                                              \
+    hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, WW, false, true, KS3>), grid, block, 0,       \
+                       stream, p_old, p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B,      \
+                       stats_on, xg, nullptr);                                                \
   else                                                                                        \
-    hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, WW>), grid, block, 0, stream, p_old, p_new,   \
-                       lr, x_prev, x, w, ctr, stats, stats_ring, B, stats_on, xg, nullptr)
+    hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, WW, false, false, KS3>), grid, block, 0,      \
+                       stream, p_old, p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B,      \
+                       stats_on, xg, nullptr)
 #define DTFX_FXW(WW)                        \
   case WW:                                  \
     if ((B + 15) / 16 == 7) DTFX_FX(WW, 7); \
@@ -1426,7 +1430,7 @@ void mlp_pipelined_trace_launch(const float* p_old, float* p_new, float lr, cons
 }
 
 // nslab: the K slabs the first launch wrote -- 0: the single-GPU step's (mlp_single_ks());
-// the data-parallel engines' first launches (fused, fused2x, factor) always write KS2 = 14.
+// the fused2 / fused2x first launch writes KS3 = 28, the factor engine's KS2 = 14.
 void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipStream_t stream,
                       int nslab) {
   using namespace mlp;

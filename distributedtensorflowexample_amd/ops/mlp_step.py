@@ -36,7 +36,7 @@ MAX_BATCH = 256
 
 
 # partial z1 slabs the data-parallel engines' first launch writes (their K slicing)
-XG_SLABS = 14
+XG_SLABS = 28
 
 def unflatten(p):
     """Views (W1t [H,D], b1 [H], W2t [C,H], b2 [C]) into a flat buffer."""

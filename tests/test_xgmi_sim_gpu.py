@@ -314,7 +314,7 @@ def test_fused2_fwdapply_exchange_simulated_peers(gpu, world, rank, B):
         exp = po.double().cpu() - lr * _expected_update(own, peers, rank)
         torch.cuda.synchronize()
         comm.mlp_fwdapply(po, pn, lr, xp, xn, ws, True)
-        hip().mlp_head2(ptr(pn), ptr(yn), ptr(ws.buf), ws.B, stream_handle(), 14)
+        hip().mlp_head2(ptr(pn), ptr(yn), ptr(ws.buf), ws.B, stream_handle(), mlp_step.XG_SLABS)
         comm.check()
         err = float((pn.double().cpu() - exp).abs().max())
         assert err <= 2e-5, (epoch, err)
@@ -633,7 +633,7 @@ def test_fused2_two_shot_exchange_simulated_peers(gpu, world, rank):
         exp[:n1][~mine] = po.double().cpu()[:n1][~mine] - lr * owners_sum.double()[~mine]
         torch.cuda.synchronize()
         comm.mlp_fwdapply(po, pn, lr, xp, xn, ws, True)
-        hip().mlp_head2(ptr(pn), ptr(yn), ptr(ws.buf), ws.B, stream_handle(), 14)
+        hip().mlp_head2(ptr(pn), ptr(yn), ptr(ws.buf), ws.B, stream_handle(), mlp_step.XG_SLABS)
         comm.check()
         err = float((pn.double().cpu() - exp).abs().max())
         assert err <= 2e-5, (epoch, err)

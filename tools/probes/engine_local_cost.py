@@ -91,13 +91,13 @@ def main():
         def fused2():
             reset()
             comm.mlp_fwdapply(p[0], p[1], 1e-4, x_all[r][:B], x_all[r][B:], ws, True)
-            h.mlp_head2(ptr(p[1]), ptr(yc), ptr(ws.buf), B, stream_handle(), 14)
+            h.mlp_head2(ptr(p[1]), ptr(yc), ptr(ws.buf), B, stream_handle(), mlp_step.XG_SLABS)
 
         def fused2x():
             comm.two_shot = True
             reset()
             comm.mlp_fwdapply(p[0], p[1], 1e-4, x_all[r][:B], x_all[r][B:], ws, True)
-            h.mlp_head2(ptr(p[1]), ptr(yc), ptr(ws.buf), B, stream_handle(), 14)
+            h.mlp_head2(ptr(p[1]), ptr(yc), ptr(ws.buf), B, stream_handle(), mlp_step.XG_SLABS)
             comm.two_shot = False
 
         def factor2():
