@@ -707,8 +707,8 @@ class PSClient {
         for (size_t k : pper[t]) w.put<uint32_t>(static_cast<uint32_t>(phs[k]));
         frame(w);
       }
-      if (!batch.empty() && !write_full(fds_[t], batch.data(), batch.size()))
-        throw PSConnectionLost("ps: connection to " + addrs_[t] + " lost (send)");
+      check_usable();
+      if (!batch.empty() && !write_full(fds_[t], batch.data(), batch.size())) lost(static_cast<int>(t), "send");
     }
     int64_t old = -1;
     std::string first_error;  // drain every reply first (see pull)
@@ -909,20 +909,37 @@ class PSClient {
       std::this_thread::sleep_for(std::chrono::milliseconds(50));  // ps not up yet (run_*.sh sleep 1)
     }
   }
+  // A lost or timed-out connection (SO_RCVTIMEO can fire in the middle of a frame) makes the
+  // whole client unusable: every socket is closed, so a later call -- e.g. the Supervisor's
+  // saver thread on the same client -- can never read the late or partial reply of the
+  // abandoned request as its own response; it throws PSConnectionLost at once instead.
+  [[noreturn]] void lost(int task, const char* what) {
+    if (broken_.empty()) broken_ = "ps: connection to " + addrs_[task] + " lost (" + what + ")";
+    for (int& fd : fds_)
+      if (fd >= 0) {
+        ::close(fd);
+        fd = -1;
+      }
+    throw PSConnectionLost(broken_);
+  }
+  void check_usable() const {
+    if (!broken_.empty())
+      throw PSConnectionLost("ps: client unusable after an earlier connection loss: " + broken_);
+  }
   void send(int task, const std::string& payload) {
+    check_usable();
     if (task < 0 || task >= static_cast<int>(fds_.size()) || fds_[task] < 0)
       throw std::runtime_error("ps: bad task");
     const uint32_t len = static_cast<uint32_t>(payload.size());
     if (!write_full(fds_[task], &len, 4) || !write_full(fds_[task], payload.data(), payload.size()))
-      throw PSConnectionLost("ps: connection to " + addrs_[task] + " lost (send)");
+      lost(task, "send");
   }
   std::string recv(int task) {
+    check_usable();
     uint32_t len;
-    if (!read_full(fds_[task], &len, 4))
-      throw PSConnectionLost("ps: connection to " + addrs_[task] + " lost (recv)");
+    if (!read_full(fds_[task], &len, 4)) lost(task, "recv");
     std::string resp(len, '\0');
-    if (!read_full(fds_[task], &resp[0], len))
-      throw PSConnectionLost("ps: connection to " + addrs_[task] + " lost (recv body)");
+    if (!read_full(fds_[task], &resp[0], len)) lost(task, "recv body");
     if (resp.empty()) throw std::runtime_error("ps: empty response");
     if (resp[0] != 0) throw std::runtime_error(resp.substr(1));
     return resp.substr(1);
@@ -941,6 +958,7 @@ class PSClient {
   std::vector<std::string> addrs_;
   double rpc_timeout_s_ = 0.0;
   std::vector<int> fds_;
+  std::string broken_;  // set by the first connection loss (see lost())
   std::mutex mu_;  // one request/response exchange at a time (shared by Python threads)
 };
 

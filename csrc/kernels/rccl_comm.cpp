@@ -65,6 +65,22 @@ class RcclComm {
       comm_ = nullptr;
     }
   }
+  // Fail-fast teardown (parallel/watchdog.py): called from a watchdog thread while the
+  // training thread may be blocked on a stream whose RCCL kernels wait for a dead peer.
+  // ncclCommAbort makes those kernels return and frees the communicator; every later
+  // collective on this object raises.
+  void abort() {
+    ncclComm_t c = comm_;
+    comm_ = nullptr;
+    if (c) ncclCommAbort(c);
+  }
+  // ncclSuccess (0) while healthy; an RCCL error code once a remote failure / abort was seen.
+  int async_error() const {
+    if (!comm_) return static_cast<int>(ncclInvalidUsage);
+    ncclResult_t r = ncclSuccess;
+    if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return static_cast<int>(ncclInternalError);
+    return static_cast<int>(r);
+  }
   ncclComm_t get() const {
     if (!comm_) throw std::runtime_error("rccl: communicator destroyed");
     return comm_;
@@ -156,6 +172,8 @@ void register_rccl(py::module_& m) {
       .def("broadcast", &RcclComm::broadcast)
       .def("all_to_all", &RcclComm::all_to_all)
       .def("destroy", &RcclComm::destroy)
+      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
+      .def("async_error", &RcclComm::async_error)
       .def_property_readonly("nranks", &RcclComm::nranks)
       .def_property_readonly("rank", &RcclComm::rank);
 }

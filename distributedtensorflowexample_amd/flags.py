@@ -218,6 +218,12 @@ def define_reference_flags(flag_values=FLAGS):
                    "than --num_workers makes the slowest workers backups)", fv)
     DEFINE_boolean("zero1", False, "Autograd sync-DP path: shard the optimizer update over the "
                    "replicas (ZeRO-1: reduce-scatter, owner update, all-gather)", fv)
+    DEFINE_float("dist_timeout_secs", 300.0,
+                 "Sync DP: timeout of the gloo control-plane collectives (torch's default is "
+                 "30 min); a rank whose peer died raises after at most this long", fv)
+    DEFINE_float("peer_timeout_secs", 60.0,
+                 "Sync DP fail-fast watchdog: a peer whose store heartbeat stalls this long is "
+                 "lost -- RCCL is aborted and the rank exits with code 75 (0 = off)", fv)
     DEFINE_integer("check_replicas_every", 0,
                    "Sync DP debug check (SURVEY 5.2): every N steps compare every replica's "
                    "parameters with rank 0's and stop if they are not bit-identical (0 = off)", fv)

@@ -73,16 +73,38 @@ class Cluster:
         self._threads.append(t)
         return p
 
-    def wait(self, names, timeout=None):
+    def wait(self, names, timeout=None, fail_fast=False, poll=0.1, grace=10.0):
+        """Wait for ``names``; {name: returncode, None if still running at ``timeout``}.
+
+        ``fail_fast`` (sync DP): every task is polled, and as soon as one exits non-zero the
+        others are stopped (SIGTERM, SIGKILL after ``grace`` s) -- a synchronous job cannot
+        make progress without every rank, and a rank blocked in a collective with a dead
+        peer would otherwise hold the launcher until ``timeout``."""
         t0 = time.time()
-        rc = {}
-        for n in names:
-            left = None if timeout is None else max(0.1, timeout - (time.time() - t0))
-            try:
-                rc[n] = self.procs[n].wait(left)
-            except subprocess.TimeoutExpired:
-                rc[n] = None
-        return rc
+        if not fail_fast:
+            rc = {}
+            for n in names:
+                left = None if timeout is None else max(0.1, timeout - (time.time() - t0))
+                try:
+                    rc[n] = self.procs[n].wait(left)
+                except subprocess.TimeoutExpired:
+                    rc[n] = None
+            return rc
+        while True:
+            rc = {n: self.procs[n].poll() for n in names}
+            failed = [n for n in names if rc[n] not in (None, 0)]
+            if failed:
+                alive = [n for n in names if rc[n] is None]
+                if alive:
+                    print("launch: %s exited with %s; stopping %s" % (
+                        failed[0], rc[failed[0]], ", ".join(alive)), file=sys.stderr, flush=True)
+                    self.terminate(alive, grace)
+                return {n: self.procs[n].poll() for n in names}
+            if all(v is not None for v in rc.values()):
+                return rc
+            if timeout is not None and time.time() - t0 > timeout:
+                return rc
+            time.sleep(poll)
 
     def terminate(self, names, grace=10.0):
         for n in names:
@@ -148,7 +170,7 @@ def launch_mirrored(nproc=1, extra=(), log_dir="launch_logs", timeout=None, quie
         cl.spawn(n, ["--strategy", "mirrored"] + ex, env)
         names.append(n)
     try:
-        rc = cl.wait(names, timeout)
+        rc = cl.wait(names, timeout, fail_fast=True)
     finally:
         cl.terminate([n for n in cl.procs if cl.procs[n].poll() is None])
     return rc

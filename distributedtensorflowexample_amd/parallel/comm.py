@@ -156,6 +156,14 @@ class NativeComm:
     def destroy(self):
         self._comm.destroy()
 
+    def abort(self):
+        """ncclCommAbort: unblock RCCL kernels waiting on a dead peer (watchdog teardown)."""
+        self._comm.abort()
+
+    def failed(self):
+        """RCCL reported an asynchronous error (a remote failure or an abort)."""
+        return self._comm.async_error() != 0
+
 
 def make_comm(kind="auto", group=None):
     """``native`` (C++ RCCL), ``torch`` (torch.distributed) or ``auto``."""

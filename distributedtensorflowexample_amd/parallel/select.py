@@ -281,9 +281,12 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
 class HybridComm:
     """RCCL communicator with the large f32 all-reduces routed to the xGMI bandwidth-mode
     two-shot (protocol "bw") where ``pick_large_allreduce`` measured it faster: tensors with
-    ``lo <= numel <= bw.max_numel``, 16-byte aligned, f32 and contiguous.  Everything else
-    (other collectives, dtypes, sizes) goes to RCCL.  Every rank holds the same ``lo``, so
-    both communicators see the same call sequence on every rank; both are graph-capturable.
+    ``lo <= numel <= bw.max_numel``, f32 and contiguous.  Everything else (other collectives,
+    dtypes, sizes) goes to RCCL.  The route depends only on properties every rank shares
+    (dtype, numel, ``lo``) -- never on a per-rank property such as the address -- so both
+    communicators see the same call sequence on every rank; both are graph-capturable.  A
+    routed tensor that is not 16-byte aligned goes through an aligned copy instead of
+    silently switching one rank to RCCL (which would leave its peers waiting in the kernel).
     """
 
     def __init__(self, rccl, bw, lo):
@@ -292,15 +295,25 @@ class HybridComm:
         self.device = getattr(rccl, "device", bw.device)
 
     def _use_bw(self, t):
-        return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
-                and self.lo <= t.numel() <= self.bw.max_numel and t.data_ptr() % 16 == 0)
+        if not (t.is_cuda and t.dtype == torch.float32 and self.lo <= t.numel() <= self.bw.max_numel):
+            return False
+        if not t.is_contiguous():
+            raise ValueError("HybridComm: a routed all-reduce tensor must be contiguous")
+        return True
+
+    def _bw_sum(self, t):
+        if t.data_ptr() % 16 == 0:
+            return self.bw.allreduce_sum_(t)
+        tmp = t.clone()  # fresh allocations are 512-byte aligned
+        self.bw.allreduce_sum_(tmp)
+        return t.copy_(tmp)
 
     def allreduce_sum_(self, t):
-        return self.bw.allreduce_sum_(t) if self._use_bw(t) else self.rccl.allreduce_sum_(t)
+        return self._bw_sum(t) if self._use_bw(t) else self.rccl.allreduce_sum_(t)
 
     def allreduce_avg_(self, t):
         if self._use_bw(t):
-            self.bw.allreduce_sum_(t)
+            self._bw_sum(t)
             return t.div_(self.world_size)
         return self.rccl.allreduce_avg_(t)
 
@@ -308,7 +321,7 @@ class HybridComm:
         self.bw.check()
 
     def failed(self):
-        return self.bw.failed()
+        return self.bw.failed() or bool(getattr(self.rccl, "failed", lambda: False)())
 
     def __getattr__(self, name):  # broadcast_, reduce_scatter, all_gather, barrier, ...
         return getattr(self.rccl, name)
@@ -318,13 +331,20 @@ class HybridComm:
 
 
 def pick_large_allreduce(rccl, world, rank, dev, max_numel, sizes=None, iters=10,
-                         xgmi_key="dtfx/xgmi/bw", timeout_s=2.0, bw_blocks=None):
+                         xgmi_key="dtfx/xgmi/bw", timeout_s=2.0, bw_blocks=None,
+                         train_timeout_s=120.0):
     """Bucketed all-reduce backend for the large gradients (BERT / ResNet buckets): the xGMI
     bandwidth-mode two-shot is created on every rank (or not at all), verified against RCCL
     on random buckets, and timed against RCCL inside captured hipGraphs at each size in
     ``sizes`` (max over ranks, best of three).  Returns ``(HybridComm, probe)`` routing every
     bucket of at least the smallest size from which bw won at every larger probed size, or
-    ``(rccl, probe)`` when it never wins.  The same decision on every rank."""
+    ``(rccl, probe)`` when it never wins.  The same decision on every rank.
+
+    ``timeout_s`` bounds the in-kernel peer waits of the probe; the returned communicator
+    waits up to ``train_timeout_s`` (a rank that is away for seconds -- the chief writing a
+    checkpoint, first-step graph capture -- must not time its peers out: a timed-out
+    two-shot leaves the bucket partly reduced, where RCCL would simply have blocked).
+    Trainers still poll ``failed()`` collectively (``check_comm_collective``)."""
     max_numel = int(max_numel)
     sizes = [s for s in (sizes or (1 << 18, 1 << 20, 1 << 22, 7 << 20, 1 << 24))
              if s <= max_numel] or [max_numel]
@@ -413,4 +433,20 @@ def pick_large_allreduce(rccl, world, rank, dev, max_numel, sizes=None, iters=10
     if lo is None:
         bw.destroy()
         return rccl, probe
+    bw.timeout_s = float(train_timeout_s)  # read at every launch / graph capture from here on
     return HybridComm(rccl, bw, lo), probe
+
+
+def check_comm_collective(comm, where=""):
+    """Raise on EVERY rank if the xGMI communicator of ANY rank latched a timed-out in-kernel
+    wait (its buffer then holds a partial reduction and the replicas have diverged).  A
+    collective over the gloo control plane, so every rank must call it at the same step."""
+    failed = getattr(comm, "failed", None)
+    bad = bool(failed()) if callable(failed) else False
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([1 if bad else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        bad = bool(t.item())
+    if bad:
+        raise RuntimeError("xGMI all-reduce timed out waiting for a peer%s: replicas are no "
+                           "longer identical" % ((" (" + where + ")") if where else ""))

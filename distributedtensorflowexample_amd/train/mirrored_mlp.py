@@ -22,6 +22,7 @@ import torch.distributed as dist
 from ..models import mlp as mlp_model
 from ..ops import mlp_step, nn, optim
 from ..parallel.comm import NativeComm, TorchComm
+from ..parallel.watchdog import init_process_group_with_timeout, maybe_inject_fault, watch_peers
 from ..optim import GradientDescentOptimizer
 from ..parallel.mirrored import DistributedDataParallel
 from ..parallel.sharded import ShardedOptimizer
@@ -41,7 +42,8 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
     rank, world, local = _dist_env()
     use_gpu = torch.cuda.is_available() and flags.device != "cpu"
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group("gloo")  # control plane; tensors over RCCL on GPU
+        init_process_group_with_timeout(  # control plane; tensors over RCCL on GPU
+            "gloo", getattr(flags, "dist_timeout_secs", None))
     shared_gpu = os.environ.get("DTFX_SHARED_GPU") == "1"
     if use_gpu:
         # DTFX_SHARED_GPU=1 (rehearsal on a one-GPU box only): every rank on device 0 and an
@@ -198,17 +200,27 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
         return float((logits.argmax(1).cpu().numpy() == test_y).mean())
 
     history = []
-    with sv.managed_session():
+    # fail-fast: a rank whose peer died aborts its communicator and exits (non-zero)
+    with watch_peers(comm, float(getattr(flags, "peer_timeout_secs", 60.0) or 0.0)), \
+            sv.managed_session():
         if world > 1 and sv.restored_from is not None:
             pass  # chief-only restore: other ranks broadcast below
         if world > 1:  # replicas start identical (restored or initialised on the chief)
             p = get_params()
             if comm is not None:
                 comm.broadcast_(p, 0)
+            # ... at the chief's global step (a restored chief resumes mid-run; the other
+            # ranks must run exactly as many steps, or they wait in a collective forever)
+            s = torch.tensor([global_step()], dtype=torch.int64)
+            dist.broadcast(s, 0)
+            s = int(s.item())
             if use_gpu:
                 tr.load_params(p)
+                tr.ws.set_global_step(s)
+                tr.pos = s % tr.nbatches
             else:
                 model.flat.data.copy_(p)
+                state["pos"] = s
         chunk = int(flags.log_every)
         state["step"] = global_step()
         start_time, start_step = time.time(), state["step"]
@@ -224,6 +236,7 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
                 stats = torch.tensor([step_fn() for _ in range(n)])
             step = global_step()
             state["step"] = step
+            maybe_inject_fault(rank, step)
             if writer is not None:
                 writer.add_scalar_series(["loss", "accuracy"], range(s0, s0 + n), stats.tolist())
             cost = float(stats[-1, 0])

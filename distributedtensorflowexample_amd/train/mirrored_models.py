@@ -23,6 +23,8 @@ import torch
 import torch.distributed as dist
 
 from ..parallel.comm import NativeComm, TorchComm
+from ..parallel.watchdog import init_process_group_with_timeout, maybe_inject_fault, watch_peers
+from ..parallel.select import check_comm_collective
 from ..utils.summary import FileWriter
 from .saver import FastSaver
 from .supervisor import Supervisor
@@ -37,7 +39,8 @@ def train_model_mirrored(flags, log=print):
     rank, world, local = _dist_env()
     use_gpu = torch.cuda.is_available() and flags.device != "cpu"
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group("gloo")
+        init_process_group_with_timeout(  # control plane; tensors over RCCL on GPU
+            "gloo", getattr(flags, "dist_timeout_secs", None))
     if use_gpu:
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
@@ -98,7 +101,9 @@ def train_model_mirrored(flags, log=print):
                     save_summaries_secs=flags.save_summaries_secs, save_variables=save_vars,
                     checkpoint_on_main_thread=True)  # never read parameters mid-step
     steps_total = int(flags.training_steps)
-    with sv.managed_session():
+    # fail-fast: a rank whose peer died aborts its communicator and exits (non-zero)
+    with watch_peers(comm, float(getattr(flags, "peer_timeout_secs", 60.0) or 0.0)), \
+            sv.managed_session():
         if is_chief and sv.restored_from is not None:
             log("Restored %s (global_step %d)" % (sv.restored_from, global_step()))
         if world > 1:  # every replica starts from the chief's parameters and step
@@ -116,13 +121,24 @@ def train_model_mirrored(flags, log=print):
             tr.step(use_graph)
             state["step"] += 1
             step = global_step()
+            maybe_inject_fault(rank, step)
             k = int(getattr(flags, "check_replicas_every", 0) or 0)
             if k > 0 and world > 1 and step % k == 0:
                 from ..parallel.mirrored import assert_replicas_identical
 
                 assert_replicas_identical(comm, model.params.master, world, step)
+            logstep = step % int(flags.log_every) == 0 or step == steps_total
+            if world > 1 and use_gpu:
+                # a timed-out xGMI bucket all-reduce leaves diverged replicas: stop on every
+                # rank at the next log step (same step everywhere: a collective check), and
+                # never let the chief checkpoint parameters its own comm reports as partial
+                if logstep:
+                    check_comm_collective(comm, "step %d" % step)
+                elif is_chief and sv.checkpoint_pending() and getattr(comm, "failed", None) \
+                        and comm.failed():
+                    raise RuntimeError("xGMI all-reduce timed out before a checkpoint")
             sv.service()  # a requested checkpoint, between steps
-            if step % int(flags.log_every) == 0 or step == steps_total:
+            if logstep:
                 loss, acc = tr.stats()
                 if writer is not None:
                     writer.add_scalars({"loss": loss, "accuracy": acc}, step)

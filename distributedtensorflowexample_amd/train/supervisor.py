@@ -55,15 +55,22 @@ class Coordinator:
 
 
 class _LoopThread(threading.Thread):
-    def __init__(self, coord, period, fn, name):
+    """TF's ``LooperThread`` with a timer: with ``run_at_start`` the first call happens when
+    the thread starts ("next timer time starts as now"), which is why a TF chief writes
+    ``model.ckpt-<start step>`` right after init/restore; later calls every ``period`` s."""
+
+    def __init__(self, coord, period, fn, name, run_at_start=False):
         super().__init__(name=name, daemon=True)
         self.coord, self.period, self.fn = coord, float(period), fn
+        self.run_at_start = bool(run_at_start)
         self._halt = threading.Event()
 
     def run(self):
+        nxt = time.time() + (0.0 if self.run_at_start else self.period)
         while not self.coord.should_stop() and not self._halt.is_set():
-            if self._halt.wait(self.period):
+            if self._halt.wait(max(nxt - time.time(), 0.0)):
                 break
+            nxt += self.period
             try:
                 self.fn()
             except Exception as e:  # report, keep training (TF logs and continues)
@@ -138,6 +145,10 @@ class Supervisor:
         return self.saver.save(None, self.save_path, global_step=step,
                                variables=self.save_variables() if self.save_variables else None)
 
+    def checkpoint_pending(self):
+        """A main-thread checkpoint was requested and not yet written."""
+        return self._ckpt_request.is_set()
+
     def service(self):
         """Run requested main-thread services (``checkpoint_on_main_thread``): call between
         training steps.  Returns the checkpoint path when one was written."""
@@ -150,7 +161,7 @@ class Supervisor:
         if self.saver is not None and self.save_model_secs and self.save_path:
             fn = self._ckpt_request.set if self.checkpoint_on_main_thread else self.save_checkpoint
             self._threads.append(_LoopThread(self.coord, self.save_model_secs, fn,
-                                             "SVTimerCheckpointThread"))
+                                             "SVTimerCheckpointThread", run_at_start=True))
         if self.summary_writer is not None and self.save_summaries_secs and self.global_step:
             state = {"t": time.time(), "s": self._step()}
 
