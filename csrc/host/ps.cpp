@@ -667,83 +667,44 @@ class PSClient {
                          std::vector<size_t> sizes, float lr, bool locking, int64_t step_h,
                          int64_t delta, std::vector<int64_t> phs, std::vector<uintptr_t> pptrs,
                          std::vector<size_t> psizes) {
-    if (hs.size() != ptrs.size() || hs.size() != sizes.size() || phs.size() != pptrs.size() ||
-        phs.size() != psizes.size())
-      throw std::runtime_error("ps push_step_pull: argument lengths differ");
     py::gil_scoped_release nogil;
     std::lock_guard<std::mutex> lk(mu_);
-    const size_t T = fds_.size(), step_task = task_of(step_h);
-    std::vector<std::vector<size_t>> per(T), pper(T);
-    for (size_t k = 0; k < hs.size(); ++k) per[task_of(hs[k])].push_back(k);
-    for (size_t k = 0; k < phs.size(); ++k) pper[task_of(phs[k])].push_back(k);
-    for (size_t t = 0; t < T; ++t) {
-      std::string batch;  // the task's requests, framed, sent with one write
-      auto frame = [&](const Writer& w) {
-        const uint32_t len = static_cast<uint32_t>(w.b.size());
-        batch.append(reinterpret_cast<const char*>(&len), 4);
-        batch.append(w.b);
-      };
-      if (!per[t].empty()) {
-        Writer w;
-        w.put<uint8_t>(OP_PUSH_APPLY);
-        w.put<float>(lr);
-        w.put<uint8_t>(locking ? 1 : 0);
-        w.put<uint32_t>(static_cast<uint32_t>(per[t].size()));
-        for (size_t k : per[t]) w.put<uint32_t>(static_cast<uint32_t>(hs[k]));
-        for (size_t k : per[t]) w.raw(reinterpret_cast<const void*>(ptrs[k]), sizes[k]);
-        frame(w);
-      }
-      if (t == step_task) {
-        Writer w;
-        w.put<uint8_t>(OP_FETCH_ADD);
-        w.put<uint32_t>(static_cast<uint32_t>(step_h));
-        w.put<int64_t>(delta);
-        frame(w);
-      }
-      if (!pper[t].empty()) {
-        Writer w;
-        w.put<uint8_t>(OP_PULL);
-        w.put<uint32_t>(static_cast<uint32_t>(pper[t].size()));
-        for (size_t k : pper[t]) w.put<uint32_t>(static_cast<uint32_t>(phs[k]));
-        frame(w);
-      }
-      check_usable();
-      if (!batch.empty() && !write_full(fds_[t], batch.data(), batch.size())) lost(static_cast<int>(t), "send");
+    psp_send(hs, ptrs, sizes, lr, locking, step_h, delta, phs, pptrs, psizes);
+    return psp_recv();
+  }
+  // The same exchange split in two (train/worker.py): ``begin`` sends every request and
+  // returns at once; the ps applies the push, advances the step and reads the parameters
+  // while the caller prepares its next batch; ``end`` receives the replies (the pulled
+  // parameters land in ``pptrs``) and returns the old step.  The client's lock is held from
+  // begin to end (same thread), so no other request can interleave on the connections; every
+  // begin must be followed by end (the Python side calls it in a ``finally``).
+  void push_step_pull_begin(std::vector<int64_t> hs, std::vector<uintptr_t> ptrs,
+                            std::vector<size_t> sizes, float lr, bool locking, int64_t step_h,
+                            int64_t delta, std::vector<int64_t> phs, std::vector<uintptr_t> pptrs,
+                            std::vector<size_t> psizes) {
+    py::gil_scoped_release nogil;
+    mu_.lock();
+    try {
+      if (psp_.active) throw std::runtime_error("ps push_step_pull_begin: an exchange is already open");
+      psp_send(hs, ptrs, sizes, lr, locking, step_h, delta, phs, pptrs, psizes);
+    } catch (...) {
+      psp_.active = false;
+      mu_.unlock();
+      throw;
     }
-    int64_t old = -1;
-    std::string first_error;  // drain every reply first (see pull)
-    bool lost = false;
-    for (size_t t = 0; t < T; ++t) {
-      const int n_req = (per[t].empty() ? 0 : 1) + (t == step_task ? 1 : 0) + (pper[t].empty() ? 0 : 1);
-      for (int q = 0; q < n_req; ++q) {
-        try {
-          std::string resp = recv(static_cast<int>(t));
-          const bool is_push = q == 0 && !per[t].empty();
-          const bool is_step = t == step_task && q == (per[t].empty() ? 0 : 1);
-          if (is_push) continue;
-          if (is_step) {
-            Reader r{resp.data(), resp.data() + resp.size()};
-            old = r.get<int64_t>();
-            continue;
-          }
-          size_t off = 0;
-          for (size_t k : pper[t]) {
-            if (off + psizes[k] > resp.size()) throw std::runtime_error("ps pull: short response");
-            std::memcpy(reinterpret_cast<void*>(pptrs[k]), resp.data() + off, psizes[k]);
-            off += psizes[k];
-          }
-        } catch (const PSConnectionLost& e) {
-          if (first_error.empty()) first_error = e.what();
-          lost = true;
-          break;  // nothing more arrives on a lost connection
-        } catch (const std::exception& e) {
-          if (first_error.empty()) first_error = e.what();
-        }
+    psp_.active = true;
+  }
+  int64_t push_step_pull_end() {
+    py::gil_scoped_release nogil;
+    if (!psp_.active) throw std::runtime_error("ps push_step_pull_end without begin");
+    struct Unlock {
+      PSClient* c;
+      ~Unlock() {
+        c->psp_.active = false;
+        c->mu_.unlock();
       }
-    }
-    if (lost) throw PSConnectionLost(first_error);
-    if (!first_error.empty()) throw std::runtime_error(first_error);
-    return old;
+    } unlock{this};
+    return psp_recv();
   }
   // Synchronous-replicas push (see SYNC_PUSH): every task gets its variables' gradients; the
   // task holding `step_handle` (global_step) advances it with each applied round.  Returns
@@ -871,6 +832,110 @@ class PSClient {
   }
 
  private:
+  // push_step_pull, send half (mu_ held by the caller): per task, the push + apply of its
+  // gradients, the fetch_add on global_step (its task only) and the pull of its variables,
+  // framed back to back and written with one call.  The reply plan stays in psp_.
+  void psp_send(const std::vector<int64_t>& hs, const std::vector<uintptr_t>& ptrs,
+                const std::vector<size_t>& sizes, float lr, bool locking, int64_t step_h,
+                int64_t delta, const std::vector<int64_t>& phs, const std::vector<uintptr_t>& pptrs,
+                const std::vector<size_t>& psizes) {
+    if (hs.size() != ptrs.size() || hs.size() != sizes.size() || phs.size() != pptrs.size() ||
+        phs.size() != psizes.size())
+      throw std::runtime_error("ps push_step_pull: argument lengths differ");
+    check_usable();
+    const size_t T = fds_.size();
+    psp_.step_task = task_of(step_h);
+    psp_.per.assign(T, {});
+    psp_.pper.assign(T, {});
+    psp_.pptrs = pptrs;
+    psp_.psizes = psizes;
+    auto& per = psp_.per;
+    auto& pper = psp_.pper;
+    for (size_t k = 0; k < hs.size(); ++k) per[task_of(hs[k])].push_back(k);
+    for (size_t k = 0; k < phs.size(); ++k) pper[task_of(phs[k])].push_back(k);
+    for (size_t t = 0; t < T; ++t) {
+      std::string batch;  // the task's requests, framed, sent with one write
+      auto frame = [&](const Writer& w) {
+        const uint32_t len = static_cast<uint32_t>(w.b.size());
+        batch.append(reinterpret_cast<const char*>(&len), 4);
+        batch.append(w.b);
+      };
+      if (!per[t].empty()) {
+        Writer w;
+        w.put<uint8_t>(OP_PUSH_APPLY);
+        w.put<float>(lr);
+        w.put<uint8_t>(locking ? 1 : 0);
+        w.put<uint32_t>(static_cast<uint32_t>(per[t].size()));
+        for (size_t k : per[t]) w.put<uint32_t>(static_cast<uint32_t>(hs[k]));
+        for (size_t k : per[t]) w.raw(reinterpret_cast<const void*>(ptrs[k]), sizes[k]);
+        frame(w);
+      }
+      if (t == psp_.step_task) {
+        Writer w;
+        w.put<uint8_t>(OP_FETCH_ADD);
+        w.put<uint32_t>(static_cast<uint32_t>(step_h));
+        w.put<int64_t>(delta);
+        frame(w);
+      }
+      if (!pper[t].empty()) {
+        Writer w;
+        w.put<uint8_t>(OP_PULL);
+        w.put<uint32_t>(static_cast<uint32_t>(pper[t].size()));
+        for (size_t k : pper[t]) w.put<uint32_t>(static_cast<uint32_t>(phs[k]));
+        frame(w);
+      }
+      check_usable();
+      if (!batch.empty() && !write_full(fds_[t], batch.data(), batch.size())) lost(static_cast<int>(t), "send");
+    }
+  }
+  // push_step_pull, receive half: drains every reply (see pull) and returns the old step.
+  int64_t psp_recv() {
+    const size_t T = fds_.size(), step_task = psp_.step_task;
+    const auto& per = psp_.per;
+    const auto& pper = psp_.pper;
+    int64_t old = -1;
+    std::string first_error;
+    bool lost_conn = false;
+    for (size_t t = 0; t < T; ++t) {
+      const int n_req = (per[t].empty() ? 0 : 1) + (t == step_task ? 1 : 0) + (pper[t].empty() ? 0 : 1);
+      for (int q = 0; q < n_req; ++q) {
+        try {
+          std::string resp = recv(static_cast<int>(t));
+          const bool is_push = q == 0 && !per[t].empty();
+          const bool is_step = t == step_task && q == (per[t].empty() ? 0 : 1);
+          if (is_push) continue;
+          if (is_step) {
+            Reader r{resp.data(), resp.data() + resp.size()};
+            old = r.get<int64_t>();
+            continue;
+          }
+          size_t off = 0;
+          for (size_t k : pper[t]) {
+            if (off + psp_.psizes[k] > resp.size()) throw std::runtime_error("ps pull: short response");
+            std::memcpy(reinterpret_cast<void*>(psp_.pptrs[k]), resp.data() + off, psp_.psizes[k]);
+            off += psp_.psizes[k];
+          }
+        } catch (const PSConnectionLost& e) {
+          if (first_error.empty()) first_error = e.what();
+          lost_conn = true;
+          break;  // nothing more arrives on a lost connection
+        } catch (const std::exception& e) {
+          if (first_error.empty()) first_error = e.what();
+        }
+      }
+    }
+    if (lost_conn) throw PSConnectionLost(first_error);
+    if (!first_error.empty()) throw std::runtime_error(first_error);
+    return old;
+  }
+  struct PendingPSP {
+    bool active = false;
+    size_t step_task = 0;
+    std::vector<std::vector<size_t>> per, pper;
+    std::vector<uintptr_t> pptrs;
+    std::vector<size_t> psizes;
+  } psp_;
+
   static uint8_t dt(const std::string& s) {
     if (s == "float32") return DT_F32;
     if (s == "int64" || s == "int32") return DT_I64;
@@ -992,6 +1057,11 @@ void register_ps(py::module_& m) {
            py::arg("sizes"), py::arg("lr"), py::arg("use_locking"), py::arg("step_handle"),
            py::arg("delta"), py::arg("pull_handles"), py::arg("pull_ptrs"),
            py::arg("pull_sizes"))
+      .def("push_step_pull_begin", &PSClient::push_step_pull_begin, py::arg("handles"),
+           py::arg("ptrs"), py::arg("sizes"), py::arg("lr"), py::arg("use_locking"),
+           py::arg("step_handle"), py::arg("delta"), py::arg("pull_handles"),
+           py::arg("pull_ptrs"), py::arg("pull_sizes"))
+      .def("push_step_pull_end", &PSClient::push_step_pull_end)
       .def("uninitialized", &PSClient::uninitialized)
       .def("list_vars", &PSClient::list_vars)
       .def("ping", &PSClient::ping)

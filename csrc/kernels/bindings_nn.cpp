@@ -12,7 +12,7 @@ void attn_bwd_set_variant(int);
 void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const void*, int, void*,
                       int, float, float, const float*, int, const void*, void*, int, const void*,
                       int, int, int, int, long long, long long, long long,
-                      float*, hipStream_t, float*, long long);
+                      float*, hipStream_t, float*, long long, bool);
 void colsum_bf16_launch(const void*, int, int, int, float*, float, hipStream_t);
 long long gemm_bf16_ws_floats(bool, bool, int, int, int, int, float);
 long long conv_wgrad_ws_floats(int, int, int, int, int, int, int, int, int);
@@ -74,7 +74,7 @@ void attn_fwd_launch(int, int, int, const void*, void*, float*, const float*, fl
 void attn_bwd_launch(int, int, int, const void*, const void*, const void*, const float*,
                      const float*, float, void*, float*, hipStream_t);
 void adam_mixed_launch(long long, float*, const float*, float*, float*, void*, float, float, float,
-                       float, float, float, const int*, int, hipStream_t);
+                       float, float, float, const int*, int, hipStream_t, const long long*, int);
 void cast_f32_bf16_launch(long long, const float*, void*, hipStream_t);
 void act_grad_bf16_launch(long long, int, const void*, const void*, void*, hipStream_t);
 void flash_fwd_launch(int, int, int, const void*, void*, float*, int, const float*, float,
@@ -101,12 +101,12 @@ void register_nn(py::module_& m) {
                         uintptr_t bias, int act, uintptr_t aux_in, uintptr_t aux_out, int ld_aux,
                         uintptr_t residual, int ld_res, int act_grad, int splitk, int batch, long long sA,
                         long long sB, long long sC, uintptr_t colsum, uintptr_t s, uintptr_t ws,
-                        long long ws_floats) {
+                        long long ws_floats, bool defer_reduce) {
     dtfx::gemm_bf16_launch(ta, tb, out_f32, M, N, K, P<const void>(A), lda, P<const void>(B), ldb,
                            P<void>(C), ldc, alpha, beta, P<const float>(bias), act,
                            P<const void>(aux_in), P<void>(aux_out), ld_aux, P<const void>(residual),
                            ld_res, act_grad, splitk, batch, sA, sB, sC,
-                           P<float>(colsum), S(s), P<float>(ws), ws_floats);
+                           P<float>(colsum), S(s), P<float>(ws), ws_floats, defer_reduce);
   }, py::arg("ta"), py::arg("tb"), py::arg("out_f32"), py::arg("M"), py::arg("N"), py::arg("K"),
      py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"),
      py::arg("alpha") = 1.f, py::arg("beta") = 0.f, py::arg("bias") = 0, py::arg("act") = 0,
@@ -114,7 +114,7 @@ void register_nn(py::module_& m) {
      py::arg("residual") = 0, py::arg("ld_res") = 0, py::arg("act_grad") = 0,
      py::arg("splitk") = 0, py::arg("batch") = 1, py::arg("sA") = 0, py::arg("sB") = 0,
      py::arg("sC") = 0, py::arg("colsum") = 0, py::arg("stream") = 0, py::arg("ws") = 0,
-     py::arg("ws_floats") = 0);
+     py::arg("ws_floats") = 0, py::arg("defer_reduce") = false);
   m.def("gemm_bf16_ws_floats", &dtfx::gemm_bf16_ws_floats,
         "f32 elements of split-K workspace gemm_bf16 would use (0: no split-K)");
   m.def("conv_splitk_ws_floats", &dtfx::conv_splitk_ws_floats,
@@ -166,11 +166,15 @@ void register_nn(py::module_& m) {
   });
   m.def("adam_mixed", [](long long n, uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v,
                          uintptr_t pb, float lr, float b1, float b2, float eps, float wd,
-                         float gscale, uintptr_t step_ptr, int step, uintptr_t s) {
+                         float gscale, uintptr_t step_ptr, int step, uintptr_t s, uintptr_t segs,
+                         int nseg) {
     dtfx::adam_mixed_launch(n, P<float>(p), P<const float>(g), P<float>(mm), P<float>(v),
                             P<void>(pb), lr, b1, b2, eps, wd, gscale, P<const int>(step_ptr), step,
-                            S(s));
-  });
+                            S(s), P<const long long>(segs), nseg);
+  }, py::arg("n"), py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pb"),
+     py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"),
+     py::arg("gscale"), py::arg("step_ptr"), py::arg("step"), py::arg("stream"),
+     py::arg("segs") = 0, py::arg("nseg") = 0);
   m.def("cast_f32_bf16", [](long long n, uintptr_t x, uintptr_t y, uintptr_t s) {
     dtfx::cast_f32_bf16_launch(n, P<const float>(x), P<void>(y), S(s));
   });

@@ -882,6 +882,49 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S,
   }
 }
 
+// Few splits (S <= 8: the BERT weight gradients, S = 3 / 4 / 14 -> 14 takes the lane-split
+// kernel above): one thread per float4 output, all S plane loads issued before the first add,
+// two outputs per thread (grid-stride, 8..16 loads in flight) -- the one-load-per-lane shape
+// above left 3 of 4 lanes' latency exposed at S = 3 (1.2 TB/s, 31 us for the 28 MB of the
+// FFN weight gradients).  Sum order s = 0, 1, .. (the same as the lane-split kernel for S <= L).
+template <int SMAX>
+__global__ __launch_bounds__(256) void splitk_reduce_few_kernel(int M, int N, int S,
+                                                                const float* __restrict__ ws,
+                                                                float* __restrict__ C, int ldc,
+                                                                float beta) {
+  const int nq = N >> 2;
+  const long long total = (long long)M * nq;
+  const size_t plane = (size_t)M * N;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += 2 * stride) {
+    f32x4 v[2][SMAX];
+    int m[2], n[2];
+    bool live[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long long j = i + u * stride;
+      live[u] = j < total;
+      m[u] = live[u] ? (int)(j / nq) : 0;
+      n[u] = live[u] ? (int)(j - (long long)m[u] * nq) * 4 : 0;
+      const float* w = ws + (size_t)m[u] * N + n[u];
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s)
+        if (s < S && live[u]) v[u][s] = __builtin_nontemporal_load((const f32x4*)(w + s * plane));
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!live[u]) continue;
+      f32x4 a = v[u][0];
+#pragma unroll
+      for (int s = 1; s < SMAX; ++s)
+        if (s < S) a += v[u][s];
+      float* c = C + (size_t)m[u] * ldc + n[u];
+      if (beta != 0.f) a += beta * *(const f32x4*)c;
+      *(f32x4*)c = a;
+    }
+  }
+}
+
 // Split-K through the partial workspace when it fits (else f32 atomics into a pre-zeroed /
 // accumulating C).  Returns true when the caller must NOT pre-zero C.
 static bool splitk_ws_ok(float* ws, long long ws_floats, int splitk, int M, int N, void* C, int ldc) {
@@ -890,6 +933,14 @@ static bool splitk_ws_ok(float* ws, long long ws_floats, int splitk, int M, int 
 }
 static void splitk_reduce(int M, int N, int S, const float* ws, float* C, int ldc, float beta,
                           hipStream_t stream) {
+  if (S <= 8) {
+    const long long n4 = (long long)M * (N / 4);
+    const long long blocks = std::min<long long>((n4 + 511) / 512, 2048);
+    hipLaunchKernelGGL(splitk_reduce_few_kernel<8>, dim3((unsigned)blocks), dim3(256), 0, stream,
+                       M, N, S, ws, C, ldc, beta);
+    DTFX_HIP_CHECK(hipGetLastError());
+    return;
+  }
   int L = 1;
   while (L < S && L < 16) L <<= 1;
   const long long n = (long long)M * (N / 4), cpb = 256 / L;
@@ -1030,7 +1081,7 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
                       const float* bias, int act, const void* aux_in, void* aux_out, int ld_aux,
                       const void* residual, int ld_res, int act_grad, int splitk, int batch,
                       long long sA, long long sB, long long sC, float* colsum,
-                      hipStream_t stream, float* ws, long long ws_floats) {
+                      hipStream_t stream, float* ws, long long ws_floats, bool defer_reduce) {
   if (M <= 0 || N <= 0 || batch <= 0) return;
   if (batch > 1 && (bias || aux_in || aux_out || residual || colsum))
     throw std::runtime_error("gemm_bf16: batched GEMM supports alpha/beta/act epilogues only");
@@ -1068,6 +1119,11 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
             ld_aux, (const unsigned short*)residual, ld_res, act_grad, colsum, nullptr, 0};
   const bool use_ws = splitk > 1 && splitk_ws_ok(ws, ws_floats, splitk, M, N, C, ldc);
   if (use_ws) e.ws = ws;
+  // defer_reduce: the caller consumes the split planes itself (the BERT optimizer sums them,
+  // adam_mixed_launch with segments) -- C is not written when the GEMM splits
+  if (defer_reduce && splitk > 1 && !use_ws)
+    throw std::runtime_error("gemm_bf16: defer_reduce needs a workspace of splitk * M * N floats");
+  const bool reduce = use_ws && !defer_reduce;
   const dim3 gyz(1, splitk, batch);
   auto* Au = (const unsigned short*)A;
   auto* Bu = (const unsigned short*)B;
@@ -1075,7 +1131,7 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   if (ta == TA_ && tb == TB_ && out_f32 == F_) {                                               \
     launch_cfg<0, TA_, TB_, F_>(cfg, gyz, M, N, K, Au, lda, Bu, ldb, C, ldc, e, sA, sB, sC,    \
                                 ConvDesc{}, stream);                                           \
-    if (use_ws) splitk_reduce(M, N, splitk, ws, (float*)C, ldc, beta, stream);                 \
+    if (reduce) splitk_reduce(M, N, splitk, ws, (float*)C, ldc, beta, stream);                 \
     return;                                                                                    \
   }
   DTFX_GB(false, true, false)

@@ -940,6 +940,75 @@ __global__ __launch_bounds__(256) void adam_mixed_kernel(
   }
 }
 
+// The same AdamW with the weight gradients of some flat ranges ("segments") left as split-K
+// partial planes by their GEMMs (gemm_bf16_launch defer_reduce): the split planes are summed
+// here, in split order, instead of by a reduce pass that writes the gradient only for this
+// kernel to read it back.  Used when nothing sits between the weight gradient and the
+// optimizer (one GPU: no all-reduce).  Segment k (int64 x 5, sorted by start, disjoint):
+// {lo4, hi4 (float4 indices into the flat buffer), partial planes (f32 pointer), plane
+// stride in float4s, S}.  A lane finds its segment by binary search in LDS (<= 128 entries).
+constexpr int kAdamMaxSegs = 128;
+__global__ __launch_bounds__(256) void adam_mixed_segs_kernel(
+    long long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+    float* __restrict__ v, unsigned short* __restrict__ pb, float lr, float b1, float b2,
+    float eps, float wd, float gscale, const int* __restrict__ step_ptr, int step,
+    const long long* __restrict__ segs, int nseg) {
+  __shared__ long long s_lo[kAdamMaxSegs], s_hi[kAdamMaxSegs], s_pl[kAdamMaxSegs];
+  __shared__ const f32x4* s_w[kAdamMaxSegs];
+  __shared__ int s_S[kAdamMaxSegs];
+  for (int k = threadIdx.x; k < nseg; k += blockDim.x) {
+    s_lo[k] = segs[5 * k];
+    s_hi[k] = segs[5 * k + 1];
+    s_w[k] = (const f32x4*)segs[5 * k + 2];
+    s_pl[k] = segs[5 * k + 3];
+    s_S[k] = (int)segs[5 * k + 4];
+  }
+  __syncthreads();
+  const int t = step_ptr ? *step_ptr : step;
+  const float bc1 = 1.f - powf(b1, (float)t), bc2 = 1.f - powf(b2, (float)t);
+  const float step_size = lr / bc1, rbc2 = rsqrtf(bc2);
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    // last segment with lo <= i
+    int lo = 0, hi = nseg - 1, k = -1;
+    while (lo <= hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_lo[mid] <= i) {
+        k = mid;
+        lo = mid + 1;
+      } else {
+        hi = mid - 1;
+      }
+    }
+    f32x4 gv;
+    if (k >= 0 && i < s_hi[k]) {
+      const f32x4* w = s_w[k] + (i - s_lo[k]);
+      const long long pl = s_pl[k];
+      const int S = s_S[k];
+      gv = w[0];
+      for (int q = 1; q < S; ++q) gv += w[q * pl];
+    } else {
+      gv = ((const f32x4*)g)[i];
+    }
+    f32x4 pv = ((f32x4*)p)[i], mv = ((f32x4*)m)[i], vv = ((f32x4*)v)[i];
+    bf16x4 o;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float gg = gv[u] * gscale;
+      mv[u] = b1 * mv[u] + (1.f - b1) * gg;
+      vv[u] = b2 * vv[u] + (1.f - b2) * gg * gg;
+      pv[u] -= lr * wd * pv[u];
+      pv[u] -= step_size * mv[u] / (sqrtf(vv[u]) * rbc2 + eps);
+      o[u] = (short)tobf(pv[u]);
+    }
+    ((f32x4*)p)[i] = pv;
+    ((f32x4*)m)[i] = mv;
+    ((f32x4*)v)[i] = vv;
+    if (pb) ((bf16x4*)pb)[i] = o;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // MLM loss: softmax cross-entropy over a large vocabulary, one 256-thread block
 // per row.  Pass 1: online (max, sum-exp) + argmax over float4 loads; pass 2:
@@ -1219,11 +1288,21 @@ void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, cons
 
 void adam_mixed_launch(long long n, float* p, const float* g, float* m, float* v, void* pb,
                        float lr, float b1, float b2, float eps, float wd, float gscale,
-                       const int* step_ptr, int step, hipStream_t s) {
+                       const int* step_ptr, int step, hipStream_t s, const long long* segs,
+                       int nseg) {
   if (n % 4) throw std::runtime_error("adam_mixed: n must be a multiple of 4");
   if (n <= 0) return;
+  if (nseg < 0 || nseg > kAdamMaxSegs || (nseg && !segs))
+    throw std::runtime_error("adam_mixed: 0..128 segments with a table");
   long long blocks = (n / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
+  if (nseg) {
+    hipLaunchKernelGGL(adam_mixed_segs_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g,
+                       m, v, (unsigned short*)pb, lr, b1, b2, eps, wd, gscale, step_ptr, step,
+                       segs, nseg);
+    DTFX_HIP_CHECK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(adam_mixed_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
                      (unsigned short*)pb, lr, b1, b2, eps, wd, gscale, step_ptr, step);
   DTFX_HIP_CHECK(hipGetLastError());

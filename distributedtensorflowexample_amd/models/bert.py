@@ -212,6 +212,8 @@ class BertMLM:
         # slots).  ``wgrad_sync_buckets``: join before every gradient-bucket hook (sync DP).
         self.wgrad_stream = None
         self.wgrad_sync_buckets = True
+        self._parts = {}     # weight name -> split-K partial planes (enable_splitk_fold)
+        self._segs = None    # their AdamW segment table
 
     # ------------------------------------------------------------------ forward
     def _layer_fwd(self, l, x, batch, seq, kmask):
@@ -291,13 +293,15 @@ class BertMLM:
         # ---- backward: encoder
         ws, keep = self.wgrad_stream, []  # keep: operands the side stream still reads
 
+        parts = self._parts
+
         def wgrad(dy, xin, name):  # the only writer of these slots: beta = 0 (zero_grad skips them)
             if ws is None:
-                B16.gemm(dy, xin, True, False, out=p.G(name), beta=0.0)
+                B16.gemm(dy, xin, True, False, out=p.G(name), beta=0.0, partials=parts.get(name))
                 return
             ws.wait_stream(torch.cuda.current_stream(dy.device))
             with torch.cuda.stream(ws):
-                B16.gemm(dy, xin, True, False, out=p.G(name), beta=0.0)
+                B16.gemm(dy, xin, True, False, out=p.G(name), beta=0.0, partials=parts.get(name))
             keep.append((dy, xin))
 
         for l in reversed(range(cfg.layers)):
@@ -346,14 +350,59 @@ class BertMLM:
         return B16.gemm(dqkv, p.W(pre + "attention/qkv/kernel"), residual=da)
 
     # ------------------------------------------------------------------ optimizer
+    ENCODER_WEIGHTS = ("attention/qkv/kernel", "attention/output/dense/kernel",
+                       "intermediate/dense/kernel", "output/dense/kernel")
+
+    def enable_splitk_fold(self, tokens):
+        """Leave the encoder weight gradients as split-K partial planes and let AdamW sum them
+        (one GPU only: with data parallelism the bucket all-reduce needs the reduced gradient).
+        Removes the reduce pass of each split weight-gradient GEMM -- it wrote the f32 gradient
+        (28 MB for an FFN weight at seq 128 x batch 128) only for AdamW to read it back.
+        ``tokens``: the weight gradients' K (batch x seq).  The planes cost S x the gradient's
+        memory (~1.4 GB for BERT-base; 288 GB of HBM).  ``p.grad`` no longer holds these
+        gradients: :meth:`materialize_grads` sums them there on demand (tests, debugging)."""
+        if not self.device.type == "cuda":
+            return 0
+        p, rows = self.params, []
+        for l in range(self.cfg.layers):
+            for w in self.ENCODER_WEIGHTS:
+                name = "encoder/layer_%d/%s" % (l, w)
+                off, (M, N) = p.offsets[name]
+                S = B16.splitk_planes(M, N, int(tokens))
+                if S <= 1:
+                    continue
+                buf = torch.zeros(S * M * N, device=self.device)
+                self._parts[name] = buf
+                rows.append((off // 4, (off + M * N) // 4, buf.data_ptr(), (M * N) // 4, S))
+        rows.sort()
+        if len(rows) > 128:
+            raise ValueError("enable_splitk_fold: at most 128 split weight gradients")
+        self._segs = (torch.tensor(rows, dtype=torch.int64, device=self.device)
+                      if rows else None)
+        return len(rows)
+
+    def materialize_grads(self):
+        """Sum every folded weight gradient's planes into ``params.grad`` (split order)."""
+        p = self.params
+        for name, buf in self._parts.items():
+            g = p.G(name)
+            S = buf.numel() // g.numel()
+            planes = buf.view(S, *g.shape)
+            acc = planes[0].clone()
+            for s in range(1, S):
+                acc += planes[s]
+            g.copy_(acc)
+
     def adam_step(self, lr, step, gscale=1.0, wd=0.01, step_ptr=None, lo=0, hi=None):
         """Fused AdamW over the flat range [lo, hi) (default: every parameter); ranges split
         at bucket edges (ALIGN-aligned) give bit-identical results to one launch."""
         p = self.params
         hi = p.numel if hi is None else hi
+        if self._segs is not None and (lo, hi) != (0, p.numel):
+            raise ValueError("adam_step: the split-K fold runs over the whole buffer at once")
         sl = slice(lo, hi)
         TR.adam_mixed(p.master[sl], p.grad[sl], p.m[sl], p.v[sl], p.bf[sl], lr, step, wd=wd,
-                      gscale=gscale, step_ptr=step_ptr)
+                      gscale=gscale, step_ptr=step_ptr, segs=self._segs)
 
 
 MASK_ID = 103  # "[MASK]" in the BERT uncased vocabulary

@@ -45,7 +45,7 @@ def _check(t, name, dtype=torch.bfloat16):
 
 def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=None, aux_in=None,
          act_grad=None, residual=None, out=None, out_dtype=torch.bfloat16, alpha=1.0, beta=0.0, splitk=0,
-         colsum=None):
+         colsum=None, partials=None):
     """``out = epi(alpha * op(a) @ op(b))``, bf16 operands, f32 accumulate.
 
     Epilogue order: ``+bias`` -> ``aux_out = v`` (pre-activation, bf16) ->
@@ -55,6 +55,9 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
     gradients: few output tiles, deep K), combining with f32 atomics.
     ``colsum`` (f32 [N]) accumulates the column sums of the final values
     (a fused bias gradient of the produced activation gradient).
+    ``partials`` (f32, >= ``splitk_planes(..) * M * N`` elements): a split-K GEMM leaves its
+    S partial planes there and does NOT write ``out`` (no reduce pass): the caller sums them
+    (``transformer.adam_mixed(.., segs=..)``).  Unsplit GEMMs write ``out`` as usual.
     """
     act_i = ACT[act]
     ag_i = ACT[act_grad]
@@ -137,7 +140,17 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
     ws, nws = None, 0
     plain = (bias is None and act_i == 0 and ag_i == 0 and residual is None and aux_out is None
              and colsum is None)
-    if out.dtype == torch.float32 and plain and _SPLITK_WS:
+    defer = False
+    if partials is not None:
+        nws = hip().gemm_bf16_ws_floats(bool(trans_a), out.dtype == torch.float32, M, N, K,
+                                        int(splitk), float(beta)) if plain else 0
+        if nws:
+            if not (partials.is_cuda and partials.dtype == torch.float32
+                    and partials.is_contiguous() and partials.numel() >= nws):
+                raise ValueError("gemm_bf16: partials must be a contiguous f32 GPU buffer of "
+                                 ">= %d elements" % nws)
+            ws, nws, defer = partials, partials.numel(), True
+    elif out.dtype == torch.float32 and plain and _SPLITK_WS:
         # split-K partials go to a workspace and one reduce pass (plain stores instead of f32
         # atomics, which run at the memory side at ~1.3 TB/s chip-wide)
         nws = hip().gemm_bf16_ws_floats(bool(trans_a), True, M, N, K, int(splitk), float(beta))
@@ -148,8 +161,15 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
                     float(alpha), float(beta), ptr(bias), act_i, ptr(aux_in), ptr(aux_out),
                     aux.stride(0) if aux is not None else 0, ptr(residual),
                     residual.stride(0) if residual is not None else 0, ag_i, int(splitk),
-                    colsum=ptr(colsum), stream=stream_handle(), ws=ptr(ws), ws_floats=nws)
+                    colsum=ptr(colsum), stream=stream_handle(), ws=ptr(ws), ws_floats=nws,
+                    defer_reduce=defer)
     return out
+
+
+def splitk_planes(M, N, K, trans_a=True, beta=0.0):
+    """Split-K planes an f32-output plain GEMM of this shape runs with (1: not split)."""
+    nws = hip().gemm_bf16_ws_floats(bool(trans_a), True, M, N, K, 0, float(beta))
+    return max(1, nws // (M * N)) if nws else 1
 
 
 def bmm(a, b, trans_a=False, trans_b=False, *, out=None, out_dtype=torch.bfloat16, alpha=1.0,

@@ -140,6 +140,32 @@ class PSVariableStore:
             [b.numel() * 4 for b in bs])
         return int(old), {n: b for n, b in zip(pnames, bs)}
 
+    def push_step_pull_begin(self, grads, lr, use_locking=False, step_name="global/global_step",
+                             names=None):
+        """Split-phase :meth:`push_step_pull`: send the push, the step increment and the pull,
+        return at once (the ps works while the caller stages its next batch).  Must be
+        followed by :meth:`push_step_pull_end` on the same thread (no other call on this
+        store in between)."""
+        gnames = list(grads)
+        gs = [grads[n] for n in gnames]
+        for g in gs:
+            if g.dtype != torch.float32 or g.device.type != "cpu" or not g.is_contiguous():
+                raise ValueError("push_step_pull needs contiguous f32 CPU tensors")
+        pnames = names or self._float_names
+        bs = [self.bufs[n] for n in pnames]
+        self.client.push_step_pull_begin(
+            [self.handles[n] for n in gnames], [g.data_ptr() for g in gs],
+            [g.numel() * 4 for g in gs], float(lr), bool(use_locking), self.handles[step_name],
+            1, [self.handles[n] for n in pnames], [b.data_ptr() for b in bs],
+            [b.numel() * 4 for b in bs])
+        self._psp_names = pnames
+
+    def push_step_pull_end(self):
+        """-> (old step, {name: pulled tensor}) of the exchange :meth:`push_step_pull_begin`
+        opened."""
+        old = self.client.push_step_pull_end()
+        return int(old), {n: self.bufs[n] for n in self._psp_names}
+
     def sync_push(self, grads, lr, replicas_to_aggregate, local_step,
                   step_name="global/global_step", timeout_s=600.0):
         """Synchronous replicas (tf.train.SyncReplicasOptimizer): push this worker's

@@ -44,6 +44,11 @@ class BertTrainer:
         if self.gpu and os.environ.get("DTFX_BERT_WSTREAM", "1") != "0":
             self.model.wgrad_stream = torch.cuda.Stream(self.device)
             self.model.wgrad_sync_buckets = self.world > 1
+        if (self.gpu and self.world == 1 and os.environ.get("DTFX_BERT_FOLD", "1") != "0"
+                and (batch * seq) % 64 == 0):
+            # one GPU: no all-reduce between the weight gradients and AdamW -> AdamW sums the
+            # split-K planes itself (no reduce pass per split weight-gradient GEMM)
+            self.model.enable_splitk_fold(batch * seq)
         # a rotating dataset of `data_batches` device-resident MLM batches: before every step
         # (eager or graph replay) batch k is copied into the static buffers the step reads
         self.pool, nv = synthetic_mlm_pool(cfg, data_batches, batch, seq, device,

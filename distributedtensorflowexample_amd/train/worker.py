@@ -38,38 +38,71 @@ from .supervisor import Supervisor
 D, H, C = mlp_step.D, mlp_step.H, mlp_step.C
 
 
-def build_worker_variables(model, registry):
+def build_worker_variables(model, registry, global_scope="global", local_scope="local"):
     """worker.py:24-40: the global replica + global_step under ``global`` (on the ps), the
     local replica under ``local`` (this worker's device; never saved).  Returns the
     registry's ``get_vars('global', False)`` -- ps variables and saver var list -- and
     ``get_vars('global')`` -- the trainable ones gradients are paired with (worker.py:76-77)."""
     with registry.as_default():
-        with vs.variable_scope("global"):
+        with vs.variable_scope(global_scope):
             model.build_variables()
             vs.create_global_step()
-        with vs.variable_scope("local"):
+        with vs.variable_scope(local_scope):
             model.build_variables()
-        return vs.get_vars("global", False), vs.get_vars("global")
+        return vs.get_vars(global_scope, False), vs.get_vars(global_scope)
 
 
-def tf_vars_to_flat(v, out):
+# the reference's names (worker.py:27-31 + tf.layers.dense naming): the sync-DP checkpoints
+REFERENCE_MLP_NAMES = ("global/dense/kernel", "global/dense/bias", "global/dense_1/kernel",
+                       "global/dense_1/bias")
+# TF-layout shapes of the fused step's flat buffer, in its order (ops/mlp_step.py)
+FUSED_TF_SHAPES = ((D, H), (H,), (H, C), (C,))
+
+
+def fused_tf_names(trainable):
+    """Names of the fused MLP step's four TF-layout tensors, taken from the registry's
+    trainable collection the way the reference pairs gradients with variables: by position
+    (``zip(get_vars('global'), gvs)``, worker.py:76-77; collection order = creation order).
+    Raises unless the collection is exactly the 784-100-10 kernel/bias sequence."""
+    shapes = tuple(tuple(v.shape) for v in trainable)
+    if shapes != FUSED_TF_SHAPES:
+        raise ValueError("fused MLP layout needs trainable variables shaped %s, got %s"
+                         % (FUSED_TF_SHAPES, shapes))
+    return tuple(v.name for v in trainable)
+
+
+def tf_vars_to_flat(v, out, names=REFERENCE_MLP_NAMES):
     """TF-layout {name: tensor} -> flat internal buffer (W stored [out, in])."""
     W1t, b1, W2t, b2 = mlp_step.unflatten(out)
-    W1t.copy_(v["global/dense/kernel"].t())
-    b1.copy_(v["global/dense/bias"])
-    W2t.copy_(v["global/dense_1/kernel"].t())
-    b2.copy_(v["global/dense_1/bias"])
+    k1, c1, k2, c2 = names
+    W1t.copy_(v[k1].t())
+    b1.copy_(v[c1])
+    W2t.copy_(v[k2].t())
+    b2.copy_(v[c2])
     return out
 
 
-def flat_to_tf_vars(p):
+def flat_to_tf_vars(p, names=REFERENCE_MLP_NAMES):
     W1t, b1, W2t, b2 = mlp_step.unflatten(p)
-    return {"global/dense/kernel": W1t.t(), "global/dense/bias": b1,
-            "global/dense_1/kernel": W2t.t(), "global/dense_1/bias": b2}
+    k1, c1, k2, c2 = names
+    return {k1: W1t.t(), c1: b1, k2: W2t.t(), c2: b2}
+
+
+def split_tf_flat(flat, names):
+    """Views of a TF-layout flat buffer (the order of ``names`` / FUSED_TF_SHAPES)."""
+    out, off = {}, 0
+    for k, shape in zip(names, FUSED_TF_SHAPES):
+        m = 1
+        for d in shape:
+            m *= d
+        out[k] = flat[off:off + m].view(shape)
+        off += m
+    return out
 
 
 class Worker:
-    def __init__(self, job_name, task_index, server, flags, device=None, log=print):
+    def __init__(self, job_name, task_index, server, flags, device=None, log=print,
+                 global_scope="global"):
         self.job_name = job_name
         self.task_index = int(task_index)
         self.server = server
@@ -88,10 +121,14 @@ class Worker:
                                    getattr(flags, "hidden_units", ""),
                                    getattr(flags, "activation", None))
         self.registry = vs.VariableRegistry()
-        self.global_vars, self.trainable = build_worker_variables(self.model, self.registry)
+        self.global_vars, self.trainable = build_worker_variables(self.model, self.registry,
+                                                                  global_scope)
         self.step_name = next(v.name for v in self.global_vars if v.name.endswith("global_step"))
         self.use_fused = (self.model.is_reference_mlp and self.device.type == "cuda"
                           and 1 <= self.batch_size <= mlp_step.MAX_BATCH)
+        # the fused layout's tensor names come from the registry (never literals)
+        self.fused_names = (fused_tf_names(self.trainable) if self.model.is_reference_mlp
+                            else None)
 
         # global variables on the ps (replica_device_setter(num_ps), worker.py:24-32), or with
         # --ps_device gpu in one GPU-resident store on the chief's GPU (parallel/gpu_ps.py)
@@ -128,6 +165,7 @@ class Worker:
             self._xs = torch.empty(self.batch_size, D, pin_memory=True)
             self._ys = torch.empty(self.batch_size, dtype=torch.int32, pin_memory=True)
             self._rec = None  # host mirror of the kernels' step counter (stats ring slot)
+            self._staged = False  # a batch staged by stage() and not consumed yet
         else:
             self.local = self.model.new_local(self.device)
         self._test = None  # device-resident test set of the eval op (uploaded once)
@@ -160,22 +198,36 @@ class Worker:
                 mlp_step.from_tf_layout(self._ptf_dev, self.params)
             elif self.use_fused:
                 dev = {k: t.to(self.device, non_blocking=True) for k, t in vals.items()}
-                tf_vars_to_flat(dev, self.params)
+                tf_vars_to_flat(dev, self.params, self.fused_names)
             else:
                 self.model.load_local(self.local, [vals[v.name] for v in self.trainable])
 
-    def compute(self, batch_x, batch_y):
+    def stage(self, batch_x, batch_y):
+        """Fused GPU worker: the batch -> pinned staging buffers -> asynchronous H2D into the
+        device batch.  Called while the previous step's push/pull is in flight on the ps
+        (``push_step_pull_begin``), so the host copy leaves the critical path.  The staging
+        buffers are free: every compute ends with a stream wait that covers their last H2D."""
+        if not (self.use_fused and batch_x.shape[0] == self.batch_size):
+            return False
+        y = np.asarray(batch_y)
+        self._xs.numpy()[...] = batch_x
+        self._ys.numpy()[...] = y.argmax(1) if y.ndim == 2 else y
+        self.xb.copy_(self._xs, non_blocking=True)
+        self.yb.copy_(self._ys, non_blocking=True)
+        self._staged = True
+        return True
+
+    def compute(self, batch_x, batch_y, staged=False):
         """Local forward/backward -> (grads {global name: TF-layout CPU tensor}, loss,
-        accuracy): the reference's zip(get_vars('global'), local gradients) pairing."""
+        accuracy): the reference's zip(get_vars('global'), local gradients) pairing.
+        ``staged``: the batch is already on its way to the device (:meth:`stage`)."""
         y = np.asarray(batch_y)
         labels = y.argmax(1) if y.ndim == 2 else y
         if self.use_fused and batch_x.shape[0] == self.batch_size:
             stream = torch.cuda.current_stream(self.device)
-            stream.synchronize()  # the pinned staging buffers are free (previous step's copies)
-            self._xs.numpy()[...] = batch_x
-            self._ys.numpy()[...] = labels
-            self.xb.copy_(self._xs, non_blocking=True)
-            self.yb.copy_(self._ys, non_blocking=True)
+            if not (staged and self._staged):
+                self.stage(batch_x, batch_y)
+            self._staged = False
             rec = self.ws.global_step() if self._rec is None else self._rec
             mlp_step.step_grad(self.params, self.xb, self.yb, self.ws, self.grad)
             self._rec = rec + 1
@@ -185,13 +237,7 @@ class Worker:
             self.grad_host.copy_(self._gtf_dev, non_blocking=True)
             stream.synchronize()
             loss, acc = self.grad_host[n:n + 2].tolist()
-            tfg, off = {}, 0
-            for k, shape in (("global/dense/kernel", (D, H)), ("global/dense/bias", (H,)),
-                             ("global/dense_1/kernel", (H, C)), ("global/dense_1/bias", (C,))):
-                m = int(np.prod(shape))
-                tfg[k] = self.grad_host[off:off + m].view(shape)
-                off += m
-            return tfg, float(loss), float(acc)
+            return split_tf_flat(self.grad_host, self.fused_names), float(loss), float(acc)
         elif self.use_fused or self.model.is_reference_mlp:
             x = torch.from_numpy(np.ascontiguousarray(batch_x, np.float32))
             p = self.params.cpu() if hasattr(self, "params") else self._flat_local()
@@ -203,7 +249,7 @@ class Worker:
             gs, loss, acc = self.model.grads(self.local, x, lab)
             return ({v.name: t.cpu().contiguous() for v, t in zip(self.trainable, gs)},
                     float(loss), float(acc))
-        tfg = {k: t.contiguous() for k, t in flat_to_tf_vars(g.cpu()).items()}
+        tfg = {k: t.contiguous() for k, t in flat_to_tf_vars(g.cpu(), self.fused_names).items()}
         return tfg, float(loss), float(acc)
 
     def _flat_local(self):
@@ -296,6 +342,9 @@ class Worker:
             local_step = self.store.read_int(self.step_name) if sync else 0
             fused_rpc = bool(getattr(fl, "ps_fused_rpc", True)) and not self.gpu_ps
             pulled = False  # the parameters for the next step already came with the last push
+            next_gen_check = time.time() + 0.5
+            nxt = None  # the next batch, drawn (and staged) during the last exchange
+            split_rpc = hasattr(self.store, "push_step_pull_begin")
             while not sv.should_stop():
                 if self.gpu_ps:
                     # the same four ops on the device, stream-ordered: pull (peer read), local
@@ -312,8 +361,10 @@ class Worker:
                     self.summary_writer.add_scalars({"loss": cost, "accuracy": acc}, step)
                     history.append((step, cost, acc))
                     local_steps += 1
-                    if local_steps % 1000 == 0:
-                        self.store.check_generation()  # the chief's store was not replaced
+                    now = time.time()
+                    if now >= next_gen_check:  # the chief's store was not replaced: checked on
+                        next_gen_check = now + 0.5  # a time interval (one ps RPC), not a step count
+                        self.store.check_generation()
                     if step % log_every == 0 and step != 0:
                         elapsed = time.time() - start_time
                         self.log("step: {}\t| cost: {}\t| speed: {}step/sec".format(
@@ -332,14 +383,31 @@ class Worker:
                     continue
                 if not pulled:
                     self.sync_op()
-                batch_x, batch_y = dataset.train.next_batch(self.batch_size)
-                grads, cost, acc = self.compute(batch_x, batch_y)
+                if nxt is None:
+                    batch_x, batch_y = dataset.train.next_batch(self.batch_size)
+                    staged = False
+                else:
+                    (batch_x, batch_y), staged, nxt = nxt, True, None
+                grads, cost, acc = self.compute(batch_x, batch_y, staged=staged)
                 if sync:
                     step = local_step
                     local_step, _ = self.store.sync_push(grads, self.lr, replicas, local_step)
-                elif fused_rpc:
+                elif fused_rpc and split_rpc:
                     # train_op, counter_op and the NEXT step's sync_op in one round trip
-                    # (pipelined on the ps connection, served in the reference's order)
+                    # (pipelined on the ps connection, served in the reference's order),
+                    # split in two: the next batch is drawn and staged to the device while
+                    # the ps applies / counts / reads.  Per-worker order stays pull ->
+                    # compute -> push -> step (worker.py:129-141)
+                    self.store.push_step_pull_begin(
+                        grads, self.lr, bool(getattr(fl, "use_locking", False)), self.step_name)
+                    try:
+                        nxt = dataset.train.next_batch(self.batch_size)
+                        self.stage(*nxt)
+                    finally:
+                        step, vals = self.store.push_step_pull_end()
+                    self._assign_local(vals)
+                    pulled = True
+                elif fused_rpc:
                     step, vals = self.store.push_step_pull(
                         grads, self.lr, bool(getattr(fl, "use_locking", False)), self.step_name)
                     self._assign_local(vals)

@@ -97,3 +97,60 @@ def test_bert_dp_adam_waits_for_each_bucket_reduction(gpu):
     split = tr.model.params.buckets[1][0]
     for part in (d[split:], d[:split]):  # body (overlapped AdamW), embeddings (after the rest)
         assert (part < -0.9 * lr).float().mean().item() > 0.999
+
+
+def test_gemm_partials_sum_to_reduced_gradient(gpu):
+    """``gemm(.., partials=buf)``: a split weight-gradient GEMM leaves its S planes (split
+    order) and does not touch ``out``; their sum equals the reduce-pass result."""
+    from distributedtensorflowexample_amd.ops import bf16 as B16
+
+    g = torch.Generator().manual_seed(5)
+    for M, N, K in ((768, 3072, 16384), (128, 128, 4096), (768, 768, 16384)):
+        dy = (torch.randn(K, M, generator=g) * 0.1).to(gpu, torch.bfloat16)
+        x = (torch.randn(K, N, generator=g) * 0.1).to(gpu, torch.bfloat16)
+        S = B16.splitk_planes(M, N, K)
+        assert S > 1, (M, N, K)
+        ref = B16.gemm(dy, x, True, False, out=torch.empty(M, N, device=gpu), beta=0.0)
+        out = torch.full((M, N), 7.0, device=gpu)
+        parts = torch.zeros(S * M * N, device=gpu)
+        B16.gemm(dy, x, True, False, out=out, beta=0.0, partials=parts)
+        torch.cuda.synchronize()
+        assert bool((out == 7.0).all())           # not written
+        acc = parts.view(S, M, N)[0].clone()
+        for s in range(1, S):
+            acc += parts.view(S, M, N)[s]
+        exact = dy.float().t() @ x.float()
+        tol = 2e-3 * exact.abs().max().item()
+        assert (acc - ref).abs().max().item() <= 1e-6 * exact.abs().max().item() + 1e-7
+        assert (acc - exact).abs().max().item() <= tol
+
+
+def test_bert_splitk_fold_matches_reduce_path(gpu, monkeypatch):
+    """One-GPU AdamW summing the split-K planes itself (enable_splitk_fold) trains like the
+    reduce-pass path: same loss, parameters within the f32-atomics tolerance of the
+    eager/graph comparison above."""
+    from distributedtensorflowexample_amd.train.bert_trainer import BertTrainer
+
+    cfg = BertConfig.tiny()
+    monkeypatch.setenv("DTFX_BERT_FOLD", "0")
+    a = BertTrainer(cfg, 32, 128, gpu, lr=1e-3)
+    monkeypatch.setenv("DTFX_BERT_FOLD", "1")
+    b = BertTrainer(cfg, 32, 128, gpu, lr=1e-3)
+    assert a.model._segs is None and b.model._segs is not None
+    assert b.model._segs.shape[0] == 4 * cfg.layers
+    a.run(3, use_graph=False)
+    b.run(3, use_graph=True)
+    d = (a.model.params.master - b.model.params.master).abs()
+    assert (d <= 2e-5).float().mean() > 0.99
+    assert d.max() <= 3 * 1e-3 * 1.01
+    la, _ = a.stats()
+    lb, _ = b.stats()
+    assert abs(la - lb) < 1e-3 * abs(la)
+    # the folded gradients, materialised, match the reduce path's gradients of one step
+    a.run(1, use_graph=False)
+    b.run(1, use_graph=False)
+    b.model.materialize_grads()
+    for name in b.model._parts:
+        ga, gb = a.model.params.G(name).flatten(), b.model.params.G(name).flatten()
+        cos = torch.dot(ga, gb) / (ga.norm() * gb.norm() + 1e-30)
+        assert cos > 0.999, (name, cos.item())

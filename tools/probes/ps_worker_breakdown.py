@@ -27,6 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3000)
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--mode", choices=["serial", "pipelined"], default="pipelined")
     a = ap.parse_args()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -43,26 +44,54 @@ def main():
     w.store.create()
     w.init_op()
     w.sync_op()
-    t = {k: [] for k in ("next_batch", "compute", "push_step_pull", "assign_local", "summary",
-                         "total")}
+    if a.mode == "serial":  # round-3 loop: every phase on the critical path, in sequence
+        keys = ("next_batch", "compute", "push_step_pull", "assign_local", "summary", "total")
+    else:  # Worker's loop now: next batch drawn + staged while the ps works
+        keys = ("compute", "rpc_begin", "stage_next", "rpc_end", "assign_local", "summary",
+                "total")
+    t = {k: [] for k in keys}
+    nxt = None
     for i in range(a.steps):
-        t0 = time.perf_counter()
-        bx, by = data.train.next_batch(100)
-        t1 = time.perf_counter()
-        grads, cost, acc = w.compute(bx, by)
-        t2 = time.perf_counter()
-        step, vals = w.store.push_step_pull(grads, w.lr, False, w.step_name)
-        t3 = time.perf_counter()
-        w._assign_local(vals)
-        if w.device.type == "cuda":
-            torch.cuda.synchronize()
-        t4 = time.perf_counter()
-        w.summary_writer.add_scalars({"loss": cost, "accuracy": acc}, step)
-        t5 = time.perf_counter()
+        if a.mode == "serial":
+            t0 = time.perf_counter()
+            bx, by = data.train.next_batch(100)
+            t1 = time.perf_counter()
+            grads, cost, acc = w.compute(bx, by)
+            t2 = time.perf_counter()
+            step, vals = w.store.push_step_pull(grads, w.lr, False, w.step_name)
+            t3 = time.perf_counter()
+            w._assign_local(vals)
+            if w.device.type == "cuda":
+                torch.cuda.synchronize()
+            t4 = time.perf_counter()
+            w.summary_writer.add_scalars({"loss": cost, "accuracy": acc}, step)
+            t5 = time.perf_counter()
+            ds = (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t5 - t0)
+        else:
+            t0 = time.perf_counter()
+            if nxt is None:
+                bx, by = data.train.next_batch(100)
+                grads, cost, acc = w.compute(bx, by)
+            else:
+                grads, cost, acc = w.compute(*nxt, staged=True)
+            t1 = time.perf_counter()
+            w.store.push_step_pull_begin(grads, w.lr, False, w.step_name)
+            t2 = time.perf_counter()
+            nxt = data.train.next_batch(100)
+            w.stage(*nxt)
+            t3 = time.perf_counter()
+            step, vals = w.store.push_step_pull_end()
+            t4 = time.perf_counter()
+            w._assign_local(vals)
+            t5 = time.perf_counter()
+            w.summary_writer.add_scalars({"loss": cost, "accuracy": acc}, step)
+            t6 = time.perf_counter()
+            ds = (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t6 - t5, t6 - t0)
         if i >= 200:
-            for k, d in zip(t, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t5 - t0)):
+            for k, d in zip(t, ds):
                 t[k].append(d * 1e6)
     out = {k: round(statistics.median(v), 1) for k, v in t.items()}
+    out["mode"] = a.mode
     out["steps_per_sec_one_worker"] = round(1e6 / out["total"], 1)
     print(json.dumps(out))
     w.summary_writer.close()
