@@ -320,7 +320,13 @@ def main():
         if cands:
             tr.check()
             med = {m: sorted(v)[len(v) // 2] for m, v in probe.items()}
-            launch = min(med, key=med.get)
+            if world > 1:  # the same choice on every rank: max over ranks of each median
+                names = sorted(med)
+                t = torch.tensor([med[m] for m in names], dtype=torch.float64)
+                t = t if a.comm != "torch" else t.to(dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                med = dict(zip(names, t.cpu().tolist()))
+            launch = min(med, key=lambda m: (med[m], m))
             a.launch_probe = {m: round(v, 3) for m, v in med.items()}
     if launch == "graph":
         tr.prepare(a.steps)

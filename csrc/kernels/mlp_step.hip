@@ -360,53 +360,79 @@ __device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const 
   if (!fail) xgll::gather_sum_n<XW, 4>(local, off, ok, me, ep, v, xg.ticks, fail);
 }
 
-// Two-shot form of xg_exchange (reduce-scatter + all-gather inside the wave): element i of
-// lane l (hidden row 4 q + i of the tile, q = l / 16) is owned by rank (q + 4 i) % XW -- the
-// same on every rank, and one owner per 16-lane row segment, so every push below writes whole
-// 128-byte runs.  (1) a non-owned value goes to its owner only (slot (par, me) of the owner),
-// (2) the owner sums the XW contributions in rank order and pushes the sum into every peer's
-// result region (2 XW + par) -- the push layout's last two slots --, (3) a non-owned element
-// waits for its owner's sum.  Per rank 2 (XW-1)/XW words per element cross the links instead
-// of XW-1 (at 8 ranks 1.75 vs 7), for one more dependent hop.  Every rank pushes before it
-// waits in each phase: no wait cycle.
+// Two-shot form of xg_exchange (reduce-scatter + all-gather inside the wave).  Element set i
+// of the wave (the lane's element i; 64 lanes x 4 sets per exchanging wave) is owned by rank
+// (eslot * 4 + i) % XW: WAVE-UNIFORM, the same on every rank, and balanced over the ranks
+// across the launch's waves.  (1) every non-owned element goes to its owner only (slot
+// (par, me) of the owner), (2) the owner sums the XW contributions in rank order and pushes
+// the sum into every peer's result region (2 XW + par) -- the push layout's last two slots --,
+// (3) a non-owned element waits for its owner's sum.  Per rank 2 (XW-1)/XW words per element
+// cross the links instead of XW-1 (at 8 ranks 1.75 vs 7), for one more dependent hop.  Every
+// rank pushes before it waits in each phase: no wait cycle.
+// Uniform ownership (round 4) replaced a per-lane one ((lane / 16 + 4 i) % XW): with that, a
+// wave issued all 4 x (XW-1) predicated gather loads and 4 x (XW-1) predicated stores per phase
+// whatever it owned (at 8 ranks 16 of 64 lanes did the gathers); now a wave issues (XW-1) loads
+// per OWNED set (<= 1 set from 4 ranks up) and one store per element -- the first hop at
+// 8 ranks measured 3.2 us of the 4.7 us exchange (tools/probes/engine_trace.py).
 template <int XW>
 __device__ __forceinline__ void xg_exchange2(const MlpXg& xg, unsigned ep, const size_t (&off)[4],
                                              const bool (&ok)[4], float (&v)[4], bool& fail,
-                                             int lane) {
+                                             int eslot, unsigned long long* trw = nullptr) {
   using xgll::u64;
   const long long par = ep & 1u;
   const int me = xg.rank;
-  const int q = lane >> 4;
+  constexpr int NO = (4 + XW - 1) / XW;  // most sets a wave can own
   int own[4];
-  bool mine[4], other[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    own[i] = (q + 4 * i) % XW;
-    mine[i] = ok[i] && own[i] == me;
-    other[i] = ok[i] && own[i] != me;
-  }
+  for (int i = 0; i < 4; ++i) own[i] = __builtin_amdgcn_readfirstlane((eslot * 4 + i) % XW);
   auto slot = [&](int dst, int src) { return (u64*)xg.peers.data[dst] + (par * XW + src) * xg.S; };
   auto result = [&](int dst) { return (u64*)xg.peers.data[dst] + (2 * XW + par) * xg.S; };
-  // uniform loop over destinations, per-lane predicate: a per-lane peer index would turn the
-  // kernel-argument pointer table into a private (scratch) array
+  // (1) each non-owned element to its owner: a wave-uniform destination per set (the
+  // branch over d is scalar, so the pointer table stays in SGPRs)
 #pragma unroll
-  for (int d = 0; d < XW; ++d) {
-    if (d == me) continue;
-    u64* dst = slot(d, me);
+  for (int i = 0; i < 4; ++i) {
+    if (own[i] == me) continue;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (other[i] && own[i] == d) xgll::store(dst + off[i], xgll::word(v[i], ep));
+    for (int d = 0; d < XW; ++d)
+      if (d == own[i] && ok[i]) xgll::store(slot(d, me) + off[i], xgll::word(v[i], ep));
+  }
+  // the owned sets, compacted (uniform indices; selects instead of register-array indexing)
+  int no = 0, idx[NO];
+#pragma unroll
+  for (int k = 0; k < NO; ++k) idx[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (own[i] == me && no < NO) idx[no++] = i;
+  size_t offo[NO];
+  bool acto[NO];
+  float vo[NO];
+#pragma unroll
+  for (int k = 0; k < NO; ++k) {
+    const int j = idx[k];
+    offo[k] = j == 0 ? off[0] : j == 1 ? off[1] : j == 2 ? off[2] : off[3];
+    acto[k] = k < no && (j == 0 ? ok[0] : j == 1 ? ok[1] : j == 2 ? ok[2] : ok[3]);
+    vo[k] = j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
   }
   auto local = [&](int j) { return (const u64*)slot(me, j); };
-  if (!fail) xgll::gather_sum_n<XW, 4>(local, off, mine, me, ep, v, xg.ticks, fail);
+  if (no > 0 && !fail) xgll::gather_sum_n<XW, NO>(local, offo, acto, me, ep, vo, xg.ticks, fail);
+  if (trw) trace_stamp(trw, 5);  // probe builds: the owned sums are complete
+  // (2) the owned sums to every peer's result region
 #pragma unroll
-  for (int d = 0; d < XW; ++d) {
-    if (d == me) continue;
-    u64* dst = result(d);
+  for (int k = 0; k < NO; ++k) {
+    if (k >= no) break;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (mine[i]) xgll::store(dst + off[i], xgll::word(v[i], ep));
+    for (int d = 0; d < XW; ++d)
+      if (d != me && acto[k]) xgll::store(result(d) + offo[k], xgll::word(vo[k], ep));
+    const int j = idx[k];
+    if (j == 0) v[0] = vo[k];
+    else if (j == 1) v[1] = vo[k];
+    else if (j == 2) v[2] = vo[k];
+    else v[3] = vo[k];
   }
+  // (3) the non-owned elements: their owners' sums
+  bool other[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) other[i] = ok[i] && own[i] != me;
   if (!fail) xgll::wait_n<4>(result(me), off, other, ep, v, xg.ticks, fail);
 }
 
@@ -657,7 +683,11 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     const float* __restrict__ x_prev, const float* __restrict__ x, Bufs w, int* __restrict__ ctr,
     float* __restrict__ stats, int stats_ring, int B, int stats_on, MlpXg xg,
     unsigned long long* __restrict__ tr = nullptr) {
-  unsigned long long* trw = TRACE ? tr + (size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 : nullptr;
+  // stamps per wave: 0 entry, 1 phase-A operands landed, 2 W1 tile applied + barrier, 3 slab
+  // stored; with XW > 0 also 4 local gradient slice ready (exchange starts), 5 two-shot: the
+  // owned sums done (first hop), 6 exchange done -- 8 slots per wave then
+  constexpr int TRN = XW > 0 ? 8 : 4;
+  unsigned long long* trw = TRACE ? tr + (size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * TRN : nullptr;
   if (TRACE) trace_stamp(trw, 0);
   const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
   const int NG = NGT > 0 ? NGT : BP / 16;
@@ -769,8 +799,10 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         okw[i] = cv && j < H;
         offw[i] = OFF_W1 + (size_t)(j < H ? j : 0) * D + fc;
       }
-      if constexpr (TWO) xg_exchange2<XW>(xg, ep, offw, okw, gv, fail, lane);
+      if (TRACE) trace_stamp(trw, 4);
+      if constexpr (TWO) xg_exchange2<XW>(xg, ep, offw, okw, gv, fail, eslot, TRACE ? trw : nullptr);
       else xg_exchange<XW>(xg, ep, offw, okw, gv, fail);
+      if (TRACE) trace_stamp(trw, 6);
     }
     if (sp == 0) {
 #pragma unroll
@@ -1368,7 +1400,7 @@ void mlp_apply_launch(const float* p_old, float* p_new, float lr, const float* x
 void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
                             const float* x, float* ws, int* ctr, float* stats, int stats_ring,
                             int B, int stats_on, hipStream_t stream, const MlpXg& xg, int world,
-                            int two_shot) {
+                            int two_shot, unsigned long long* trace) {
   using namespace mlp;
   check_b(B);
   if (!p_old || !p_new || p_old == p_new || !x_prev || !x || !ctr)
@@ -1379,6 +1411,28 @@ void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const fl
   static_assert(HT * KS3 * 2 <= MLP_XG_SMALL_EPOCH, "W1 epoch slots overlap the small ones");
   const Bufs w = make_bufs(ws, B);
   dim3 grid(HT * KS3 + HT), block(256);
+  if (trace) {  // probe builds (tools/probes/engine_trace.py): [blocks * 4 waves][8] stamps
+    if ((B + 15) / 16 != 7) throw std::runtime_error("mlp_fwdapply_xg trace: batch 97..112 only");
+#define DTFX_FXT(WW)                                                                            \
+  case WW:                                                                                      \
+    if (two_shot)                                                                               \
+      hipLaunchKernelGGL((mlp_fwdapply_kernel<7, WW, true, true, KS3>), grid, block, 0, stream,  \
+                         p_old, p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B, stats_on, xg, \
+                         trace);                                                                \
+    else                                                                                        \
+      hipLaunchKernelGGL((mlp_fwdapply_kernel<7, WW, true, false, KS3>), grid, block, 0, stream, \
+                         p_old, p_new, lr, x_prev, x, w, ctr, stats, stats_ring, B, stats_on, xg, \
+                         trace);                                                                \
+    break;
+    switch (world) {
+      DTFX_FXT(2) DTFX_FXT(4) DTFX_FXT(8)
+      default:
+        throw std::runtime_error("mlp_fwdapply_xg trace: world 2, 4 or 8");
+    }
+#undef DTFX_FXT
+    DTFX_HIP_CHECK(hipGetLastError());
+    return;
+  }
 #define DTFX_FX(WW, NGT)                                                                      \
   if (two_shot)                                                                               \
     hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, WW, false, true, KS3>), grid, block, 0,       \
@@ -1545,4 +1599,38 @@ void mlp_fwdapply_factor_launch(const float* p_old, float* p_new, float lr, cons
 #undef DTFX_FF
   DTFX_HIP_CHECK(hipGetLastError());
 }
+// Async-PS worker step (train/worker.py, the reference's hot loop worker.py:131-137) in ONE
+// host call: the staged batch (pinned host -> device), the parameters pulled by the last
+// push/step/pull exchange (pinned host, TF layout -> device flat layout; skipped when
+// pulled_host is null), forward + backward writing the flat gradient, the gradient in TF
+// layout with the step's loss / accuracy record appended (-> pinned host), and a wait for the
+// stream.  Replaces ~10 Python-issued copies / launches / syncs per step; the caller releases
+// the GIL for the call.  Host buffers must be pinned (hipHostMalloc'd); *_dev are device staging
+// buffers of NPARAM + 2 floats.
+void mlp_ps_worker_step(float* p, const float* pulled_host, float* pull_dev, const float* x_host,
+                        const int* y_host, float* x_dev, int* y_dev, float* grad, float* ws,
+                        int* ctr, float* stats, int stats_ring, const float* record, int B,
+                        float* grad_dev, float* grad_host, hipStream_t s) {
+  using namespace mlp;
+  check_b(B);
+  if (!p || !x_host || !y_host || !x_dev || !y_dev || !grad || !ws || !ctr || !grad_dev ||
+      !grad_host || (pulled_host && !pull_dev) || (record && !stats))
+    throw std::runtime_error("mlp_ps_worker_step: missing buffer");
+  DTFX_HIP_CHECK(hipMemcpyAsync(x_dev, x_host, sizeof(float) * (size_t)B * D,
+                                hipMemcpyHostToDevice, s));
+  DTFX_HIP_CHECK(hipMemcpyAsync(y_dev, y_host, sizeof(int) * (size_t)B, hipMemcpyHostToDevice, s));
+  if (pulled_host) {
+    DTFX_HIP_CHECK(hipMemcpyAsync(pull_dev, pulled_host, sizeof(float) * NPARAM,
+                                  hipMemcpyHostToDevice, s));
+    mlp_tf_layout_launch(pull_dev, p, 0, nullptr, 0, s);
+  }
+  mlp_fwd_launch(p, nullptr, 0.f, nullptr, x_dev, ws, B, s, nullptr);
+  mlp_head_launch(p, nullptr, 0.f, nullptr, y_dev, ws, B, s, nullptr);
+  mlp_wgrad_launch(nullptr, 0.f, grad, x_dev, ws, ctr, stats, stats_ring, B, s, nullptr);
+  mlp_tf_layout_launch(grad, grad_dev, 1, record, record ? 2 : 0, s);
+  DTFX_HIP_CHECK(hipMemcpyAsync(grad_host, grad_dev, sizeof(float) * (NPARAM + (record ? 2 : 0)),
+                                hipMemcpyDeviceToHost, s));
+  DTFX_HIP_CHECK(hipStreamSynchronize(s));
+}
+
 }  // namespace dtfx

@@ -72,9 +72,12 @@ void mlp_wgrad_factor_launch(float* p, float lr, const float* x, long long xstri
 void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const float* x_prev,
                             const float* x, float* ws, int* ctr, float* stats, int stats_ring,
                             int B, int stats_on, hipStream_t stream, const MlpXg& xg, int world,
-                            int two_shot = 0);
+                            int two_shot = 0, unsigned long long* trace = nullptr);
 
 void mlp_wgrad_xg_launch(float* p, float lr, const float* x, float* ws, int* ctr, float* stats,
                          int stats_ring, int B, hipStream_t stream, const MlpXg& xg, int world);
+// plain head of the pipelined step (mlp_step.hip); nslab = 28 after the fused engines' launch
+void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipStream_t stream,
+                      int nslab);
 
 }  // namespace dtfx

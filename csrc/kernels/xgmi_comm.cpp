@@ -182,12 +182,68 @@ class XgmiAllReduce {
   // Pipelined fused engine: exchange + apply of step t-1 fused with step t's forward.
   void mlp_fwdapply(uintptr_t p_old, uintptr_t p_new, float lr, uintptr_t x_prev, uintptr_t x,
                     uintptr_t ws, uintptr_t ctr, uintptr_t stats, int ring, int B, int stats_on,
-                    uintptr_t stream, double timeout_s, int two_shot) {
+                    uintptr_t stream, double timeout_s, int two_shot, uintptr_t trace) {
     if (!ready_) throw std::runtime_error("xgmi: open() the peer handles first");
     if (mode_ != XG_LL_PUSH) throw std::runtime_error("xgmi: the fused MLP exchange needs protocol push");
     mlp_fwdapply_xg_launch((const float*)p_old, (float*)p_new, lr, (const float*)x_prev,
                            (const float*)x, (float*)ws, (int*)ctr, (float*)stats, ring, B,
-                           stats_on, (hipStream_t)stream, mlp_xg(timeout_s), world_, two_shot);
+                           stats_on, (hipStream_t)stream, mlp_xg(timeout_s), world_, two_shot,
+                           (unsigned long long*)trace);
+  }
+
+  // Host loop of the pipelined exchange engines (FusedMLPTrainer.run_launched, data-parallel
+  // form of mlp_run_pipelined_launch): n two-launch steps of kind 0 fused2 / 1 fused2x /
+  // 2 factor2 over the device-resident batches, issued by ONE call -- no graph submission
+  // (the ~17 us fixed cost of a replay that a driver-sized K = 20 run feels) and no Python per
+  // step.  Same launches, arguments and order as step_xgmi_pipelined / step_factor_pipelined;
+  // flush: the last step's pending update too (flush_xgmi / flush_factor).  x: this rank's
+  // batches (factor2: its slice of x_all, the peers' at +- xstride).
+  void mlp_run_engine(int kind, uintptr_t p0, uintptr_t p1, int cur, int pending, float lr,
+                      uintptr_t x, long long xstride, uintptr_t labels, int nbatches, int pos,
+                      int n, uintptr_t ws, uintptr_t ctr, uintptr_t stats, int ring, int B,
+                      uintptr_t dz1A, uintptr_t stream, double timeout_s, int flush) {
+    if (!ready_) throw std::runtime_error("xgmi: open() the peer handles first");
+    if (mode_ != XG_LL_PUSH) throw std::runtime_error("xgmi: the MLP engines need protocol push");
+    if (kind < 0 || kind > 2 || !p0 || !p1 || p0 == p1 || !x || !labels || !ctr || nbatches < 1 ||
+        pos < 0 || pos >= nbatches || n < 0 || (kind == 2 && !dz1A))
+      throw std::runtime_error("mlp_run_engine: bad kind / buffers / position / count");
+    const MlpXg xg = mlp_xg(timeout_s);
+    hipStream_t s = (hipStream_t)stream;
+    float* bufs[2] = {(float*)p0, (float*)p1};
+    const float* xs = (const float*)x;
+    const int* lab = (const int*)labels;
+    const size_t xb = (size_t)B * 784;
+    for (int i = 0; i < n; ++i) {
+      const int prev = (pos + nbatches - 1) % nbatches;
+      const float* xcur = xs + (size_t)pos * xb;
+      const float* xprev = pending ? xs + (size_t)prev * xb : xcur;
+      const float l = pending ? lr : 0.f;
+      float* po = bufs[cur];
+      float* pn = bufs[cur ^ 1];
+      if (kind == 2) {
+        mlp_fwdapply_factor_launch(po, pn, l, xprev, xcur, xstride, (const float*)dz1A,
+                                   (float*)ws, (int*)ctr, (float*)stats, ring, B, pending, s, xg,
+                                   world_);
+        mlp_head_xg_launch(pn, lab + (size_t)pos * B, (float*)ws, (float*)dz1A, B, s, xg,
+                           world_, 14);
+      } else {
+        mlp_fwdapply_xg_launch(po, pn, l, xprev, xcur, (float*)ws, (int*)ctr, (float*)stats,
+                               ring, B, pending, s, xg, world_, kind);
+        mlp_head2_launch(pn, lab + (size_t)pos * B, (float*)ws, B, s, 28);
+      }
+      cur ^= 1;
+      pending = 1;
+      pos = (pos + 1) % nbatches;
+    }
+    if (flush && pending) {
+      const float* xp = xs + (size_t)((pos + nbatches - 1) % nbatches) * xb;
+      if (kind == 2)  // in place
+        mlp_wgrad_factor_launch(bufs[cur], lr, xp, xstride, (const float*)dz1A, (float*)ws,
+                                (int*)ctr, (float*)stats, ring, B, s, xg, world_);
+      else            // bufs[cur] -> bufs[cur ^ 1]
+        mlp_fwdapply_xg_launch(bufs[cur], bufs[cur ^ 1], lr, xp, xp, (float*)ws, (int*)ctr,
+                               (float*)stats, ring, B, 1, s, xg, world_, kind);
+    }
   }
 
   void mlp_wgrad_factor(uintptr_t p, float lr, uintptr_t x, long long xstride, uintptr_t dz1A,
@@ -273,11 +329,18 @@ void register_xgmi(py::module_& m) {
       .def("mlp_fwdapply", &dtfx::XgmiAllReduce::mlp_fwdapply, py::arg("p_old"),
            py::arg("p_new"), py::arg("lr"), py::arg("x_prev"), py::arg("x"), py::arg("ws"),
            py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stats_on"),
-           py::arg("stream"), py::arg("timeout_s") = 2.0, py::arg("two_shot") = 0)
+           py::arg("stream"), py::arg("timeout_s") = 2.0, py::arg("two_shot") = 0,
+           py::arg("trace") = 0)
       .def("mlp_wgrad_factor", &dtfx::XgmiAllReduce::mlp_wgrad_factor, py::arg("p"),
            py::arg("lr"), py::arg("x"), py::arg("xstride"), py::arg("dz1A"), py::arg("ws"),
            py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"),
            py::arg("timeout_s") = 2.0)
+      .def("mlp_run_engine", &dtfx::XgmiAllReduce::mlp_run_engine, py::arg("kind"),
+           py::arg("p0"), py::arg("p1"), py::arg("cur"), py::arg("pending"), py::arg("lr"),
+           py::arg("x"), py::arg("xstride"), py::arg("labels"), py::arg("nbatches"),
+           py::arg("pos"), py::arg("n"), py::arg("ws"), py::arg("ctr"), py::arg("stats"),
+           py::arg("ring"), py::arg("B"), py::arg("dz1A"), py::arg("stream"),
+           py::arg("timeout_s"), py::arg("flush"))
       .def("error", &dtfx::XgmiAllReduce::error)
       .def("reset_epochs", &dtfx::XgmiAllReduce::reset_epochs)
       .def("close", &dtfx::XgmiAllReduce::close);

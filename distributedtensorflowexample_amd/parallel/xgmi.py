@@ -135,17 +135,19 @@ class XgmiComm:
                                     ws.stats_ring, ws.B, 1 if apply else 0,
                                     torch.cuda.current_stream().cuda_stream, self.timeout_s)
 
-    def mlp_fwdapply(self, p_old, p_new, lr, x_prev, x, ws, apply, stats=True):
+    def mlp_fwdapply(self, p_old, p_new, lr, x_prev, x, ws, apply, stats=True, trace=None):
         """Pipelined fused engine, first launch: step t-1's local gradient tiles (from the
         factors its head left in ``ws`` and ``x_prev``) exchanged with the peers, summed in
-        rank order and applied ``p_old`` -> ``p_new``, fused with step t's forward."""
+        rank order and applied ``p_old`` -> ``p_new``, fused with step t's forward.
+        ``trace``: int64 [blocks * 4, 8] in-kernel stamp buffer (probe builds, world 2/4/8)."""
         from ..ops._ext import ptr
 
         self._h.mlp_fwdapply(ptr(p_old), ptr(p_new), float(lr) if apply else 0.0,
                              ptr(x_prev if apply else x), ptr(x), ptr(ws.buf), ptr(ws.ctr),
                              ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B,
                              1 if apply else 0, torch.cuda.current_stream().cuda_stream,
-                             self.timeout_s, 1 if self.two_shot else 0)
+                             self.timeout_s, 1 if self.two_shot else 0,
+                             0 if trace is None else ptr(trace))
 
     def mlp_wgrad_factor(self, p, lr, x, xstride, dz1A, ws, stats=True):
         """Factor engine: global dW1 from the gathered factors and every rank's batch

@@ -271,9 +271,15 @@ class FusedMLPTrainer:
 
     @property
     def host_loop_ok(self):
-        """The plain single-GPU pipelined step can be issued by the C++ host loop."""
-        return (self.pipelined and self.world_size == 1 and self.fused_comm is None
-                and self.factor_comm is None and self.allreduce is None)
+        """The step can be issued by a C++ host loop: the plain single-GPU pipelined step
+        (``mlp_run_pipelined``) or a pipelined exchange engine -- fused2 / fused2x / factor2
+        (``XgmiComm`` ``mlp_run_engine``)."""
+        if not self.pipelined or self.allreduce is not None:
+            return False
+        if self.world_size == 1:
+            return self.fused_comm is None and self.factor_comm is None
+        c = self.fused_comm if self.fused_comm is not None else self.factor_comm
+        return c is not None and hasattr(getattr(c, "_h", None), "mlp_run_engine")
 
     def run_launched(self, steps, flush=False):
         """``steps`` pipelined single-GPU steps issued by ONE C++ call (kernel launches, no
@@ -283,11 +289,13 @@ class FusedMLPTrainer:
         the Python side of this call before its first kernel starts."""
         steps = int(steps)
         if not self.host_loop_ok:
-            raise RuntimeError("run_launched: single-GPU pipelined step only")
+            raise RuntimeError("run_launched: pipelined single-GPU step or exchange engine only")
         if steps <= 0:
             if flush:
                 self.flush()
             return
+        if self.world_size > 1:
+            return self._run_launched_engine(steps, flush)
         a = self._host_args
         if a is None:
             from ..ops._ext import hip, ptr
@@ -304,11 +312,35 @@ class FusedMLPTrainer:
         self.cur ^= (steps + (1 if flush else 0)) & 1
         self.pending = not flush
 
+    def _run_launched_engine(self, steps, flush):
+        """run_launched for the pipelined exchange engines: every rank issues the same steps
+        from one C++ call (the in-kernel exchanges pair them up across ranks)."""
+        from ..ops._ext import ptr
+
+        factor = self.factor_comm is not None
+        comm = self.factor_comm if factor else self.fused_comm
+        kind = 2 if factor else (1 if getattr(comm, "two_shot", False) else 0)
+        a = self._host_args
+        if a is None:
+            ws = self.ws
+            a = self._host_args = (comm._h.mlp_run_engine, ptr(self.bufs[0]), ptr(self.bufs[1]),
+                                   ptr(self.x), ptr(self.labels), ptr(ws.buf), ptr(ws.ctr),
+                                   ptr(ws.stats), ws.stats_ring,
+                                   ptr(self.dz1A) if factor else 0)
+        fn, p0, p1, xp, lp, wb, wc, wst, ring, dz = a
+        fn(kind, p0, p1, self.cur, 1 if self.pending else 0, self.lr / self.world_size, xp,
+           int(self.xstride), lp, self.nbatches, self.pos, steps, wb, wc, wst, ring, self.B, dz,
+           torch.cuda.current_stream(self.device).cuda_stream, float(comm.timeout_s),
+           1 if flush else 0)
+        self.pos = (self.pos + steps) % self.nbatches
+        self.cur ^= (steps + (1 if (flush and not factor) else 0)) & 1
+        self.pending = not flush
+
     # -- persistent single-launch engine (csrc/kernels/mlp_persistent.hip) ----------------
     @property
     def persistent_ok(self):
         """The plain single-GPU step with batch <= 128 can run as ONE persistent launch."""
-        return self.host_loop_ok and self.B <= 128
+        return self.host_loop_ok and self.world_size == 1 and self.B <= 128
 
     def run_persistent(self, steps, timeout_s=2.0, trace=None):
         """``steps`` complete SGD steps (every update applied, nothing left pending) in ONE

@@ -166,6 +166,10 @@ class Worker:
             self._ys = torch.empty(self.batch_size, dtype=torch.int32, pin_memory=True)
             self._rec = None  # host mirror of the kernels' step counter (stats ring slot)
             self._staged = False  # a batch staged by stage() and not consumed yet
+            # parameters of the last exchange waiting in the store's pinned pull buffer: the
+            # next compute() lands them (H2D + layout) in the same native call as its step
+            self._pull_pending = False
+            self._pull_dev = torch.empty(mlp_step.NPARAM, device=self.device)
         else:
             self.local = self.model.new_local(self.device)
         self._test = None  # device-resident test set of the eval op (uploaded once)
@@ -184,36 +188,42 @@ class Worker:
     def sync_op(self):
         """worker.py:81-85: local <- global for every trainable variable."""
         self._assign_local(self.store.pull())
+        self._land_pull()  # the explicit sync op lands at once (the fused RPC path defers)
 
     def _assign_local(self, vals):
         with torch.no_grad():
             flat = getattr(self.store, "flat", None)
             if (self.use_fused and flat is not None and flat.numel() == mlp_step.NPARAM
+                    and flat.is_pinned()
                     and all(vals[k].data_ptr() == self.store.bufs[k].data_ptr() for k in vals)):
-                # the pull landed in the store's one pinned buffer (TF layout, spec order):
-                # one H2D copy + one layout kernel
-                if not hasattr(self, "_ptf_dev"):
-                    self._ptf_dev = torch.empty(mlp_step.NPARAM, device=self.device)
-                self._ptf_dev.copy_(flat, non_blocking=True)
-                mlp_step.from_tf_layout(self._ptf_dev, self.params)
+                # the pull landed in the store's one pinned buffer (TF layout, spec order): the
+                # next compute() copies + converts it in its native call (_land_pull otherwise)
+                self._pull_pending = True
             elif self.use_fused:
                 dev = {k: t.to(self.device, non_blocking=True) for k, t in vals.items()}
                 tf_vars_to_flat(dev, self.params, self.fused_names)
             else:
                 self.model.load_local(self.local, [vals[v.name] for v in self.trainable])
 
+    def _land_pull(self):
+        """Apply a pending pull to the device parameters now (one H2D + one layout kernel):
+        before anything but compute() reads ``self.params``."""
+        if self.use_fused and self._pull_pending:
+            self._pull_dev.copy_(self.store.flat, non_blocking=True)
+            mlp_step.from_tf_layout(self._pull_dev, self.params)
+            self._pull_pending = False
+
     def stage(self, batch_x, batch_y):
-        """Fused GPU worker: the batch -> pinned staging buffers -> asynchronous H2D into the
-        device batch.  Called while the previous step's push/pull is in flight on the ps
-        (``push_step_pull_begin``), so the host copy leaves the critical path.  The staging
-        buffers are free: every compute ends with a stream wait that covers their last H2D."""
+        """Fused GPU worker: the batch -> pinned staging buffers (the H2D copies are issued by
+        the next compute()'s native call).  Called while the previous step's push/pull is in
+        flight on the ps (``push_step_pull_begin``), so the host copy leaves the critical path.
+        The staging buffers are free: every compute ends with a stream wait that covers their
+        last H2D."""
         if not (self.use_fused and batch_x.shape[0] == self.batch_size):
             return False
         y = np.asarray(batch_y)
         self._xs.numpy()[...] = batch_x
         self._ys.numpy()[...] = y.argmax(1) if y.ndim == 2 else y
-        self.xb.copy_(self._xs, non_blocking=True)
-        self.yb.copy_(self._ys, non_blocking=True)
         self._staged = True
         return True
 
@@ -224,22 +234,29 @@ class Worker:
         y = np.asarray(batch_y)
         labels = y.argmax(1) if y.ndim == 2 else y
         if self.use_fused and batch_x.shape[0] == self.batch_size:
-            stream = torch.cuda.current_stream(self.device)
+            from ..ops._ext import hip, ptr, stream_handle
+
             if not (staged and self._staged):
                 self.stage(batch_x, batch_y)
             self._staged = False
             rec = self.ws.global_step() if self._rec is None else self._rec
-            mlp_step.step_grad(self.params, self.xb, self.yb, self.ws, self.grad)
             self._rec = rec + 1
             n = mlp_step.NPARAM
-            # TF layout + the loss / accuracy record in one launch, then one D2H copy
-            mlp_step.to_tf_layout(self.grad, self._gtf_dev, self.ws.stats[rec % self.ws.stats_ring])
-            self.grad_host.copy_(self._gtf_dev, non_blocking=True)
-            stream.synchronize()
+            ws = self.ws
+            # ONE native call: batch + pulled parameters in, forward/backward, the TF-layout
+            # gradient + this step's loss / accuracy record out, stream wait (GIL released)
+            hip().mlp_ps_worker_step(
+                ptr(self.params), ptr(self.store.flat) if self._pull_pending else 0,
+                ptr(self._pull_dev), ptr(self._xs), ptr(self._ys), ptr(self.xb), ptr(self.yb),
+                ptr(self.grad), ptr(ws.buf), ptr(ws.ctr), ptr(ws.stats), ws.stats_ring,
+                ptr(ws.stats) + 8 * (rec % ws.stats_ring), self.batch_size, ptr(self._gtf_dev),
+                ptr(self.grad_host), stream_handle(self.device))
+            self._pull_pending = False
             loss, acc = self.grad_host[n:n + 2].tolist()
             return split_tf_flat(self.grad_host, self.fused_names), float(loss), float(acc)
         elif self.use_fused or self.model.is_reference_mlp:
             x = torch.from_numpy(np.ascontiguousarray(batch_x, np.float32))
+            self._land_pull()
             p = self.params.cpu() if hasattr(self, "params") else self._flat_local()
             g, loss_t, acc_t = mlp_step.reference_step(p, x, torch.from_numpy(labels))
             loss, acc = float(loss_t), float(acc_t)
@@ -293,6 +310,7 @@ class Worker:
             y = torch.from_numpy(y.argmax(1) if y.ndim == 2 else y).to(self.device)
             self._test = (images, x, y)
         _, x, y = self._test
+        self._land_pull()
         with torch.no_grad():
             if self.use_fused:
                 W1t, b1, W2t, b2 = mlp_step.unflatten(self.params)

@@ -118,7 +118,7 @@ def test_auto_selection_path(gpu):
         assert ok, (r, msg)
 
 
-def _fused_worker(rank, world, port, q, pipeline, two_shot=False):
+def _fused_worker(rank, world, port, q, pipeline, two_shot=False, host=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -145,6 +145,13 @@ def _fused_worker(rank, world, port, q, pipeline, two_shot=False):
         ta.run(7, use_graph=False)
         ta.flush()
         ta.run(33, use_graph=True)
+        total = 40
+        if host:  # the C++ host loop (mlp_run_engine), with and without its own flush
+            assert tf.host_loop_ok
+            tf.run_launched(11)
+            tf.run_launched(9, flush=True)
+            ta.run(20, use_graph=False)
+            total = 60
         fc.check()
         ref.check()
         pf, pa = tf.flush(), ta.flush()
@@ -153,7 +160,7 @@ def _fused_worker(rank, world, port, q, pipeline, two_shot=False):
         chk = pf.double().sum().reshape(1).cpu()
         r0 = chk.clone()
         dist.broadcast(r0, 0)
-        ok = err <= 1e-4 and moved > 1e-3 and torch.equal(chk, r0) and tf.global_step() == 40
+        ok = err <= 1e-4 and moved > 1e-3 and torch.equal(chk, r0) and tf.global_step() == total
         q.put((rank, ok, "err %.3g moved %.3g step %d" % (err, moved, tf.global_step())))
         dist.barrier()
         dist.destroy_process_group()
@@ -161,17 +168,20 @@ def _fused_worker(rank, world, port, q, pipeline, two_shot=False):
         q.put((rank, False, repr(e)))
 
 
-@pytest.mark.parametrize("world,pipeline,two_shot", [(2, False, False), (3, False, False),
-                                                     (2, True, False), (3, True, False),
-                                                     (3, True, True), (4, True, True)])
-def test_fused_mlp_exchange_matches_allreduce_engine(gpu, world, pipeline, two_shot):
+@pytest.mark.parametrize("world,pipeline,two_shot,host", [
+    (2, False, False, False), (3, False, False, False), (2, True, False, False),
+    (3, True, False, False), (3, True, True, False), (4, True, True, False),
+    (2, True, False, True), (3, True, True, True)])
+def test_fused_mlp_exchange_matches_allreduce_engine(gpu, world, pipeline, two_shot, host):
     """The gradient exchange fused into the MLP backward kernel (pipeline: into the next
     step's forward launch) gives the same SGD trajectory as the separate all-reduce engine,
-    and bit-identical replicas."""
+    and bit-identical replicas -- eager, graph-replayed and (host) issued by the C++ host
+    loop."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_fused_worker, args=(r, world, port, q, pipeline, two_shot))
+    procs = [ctx.Process(target=_fused_worker, args=(r, world, port, q, pipeline, two_shot,
+                                                     host))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -182,7 +192,7 @@ def test_fused_mlp_exchange_matches_allreduce_engine(gpu, world, pipeline, two_s
         assert ok, (r, msg)
 
 
-def _factor_worker(rank, world, port, q, B, pipeline):
+def _factor_worker(rank, world, port, q, B, pipeline, host=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -211,6 +221,13 @@ def _factor_worker(rank, world, port, q, B, pipeline):
         tf.run(33, use_graph=True)   # graph replays (device-side epochs), crosses an epoch
         ta.run(7, use_graph=False)
         ta.run(33, use_graph=True)
+        total = 40
+        if host:  # the C++ host loop (mlp_run_engine), with and without its own flush
+            assert tf.host_loop_ok
+            tf.run_launched(11)
+            tf.run_launched(9, flush=True)
+            ta.run(20, use_graph=False)
+            total = 60
         fc.check()
         ref.check()
         pf, pa = tf.flush(), ta.flush()
@@ -219,7 +236,7 @@ def _factor_worker(rank, world, port, q, B, pipeline):
         chk = pf.double().sum().reshape(1).cpu()
         r0 = chk.clone()
         dist.broadcast(r0, 0)
-        ok = err <= 1e-4 and moved > 1e-3 and torch.equal(chk, r0) and tf.global_step() == 40
+        ok = err <= 1e-4 and moved > 1e-3 and torch.equal(chk, r0) and tf.global_step() == total
         q.put((rank, ok, "err %.3g moved %.3g step %d" % (err, moved, tf.global_step())))
         dist.barrier()
         dist.destroy_process_group()
@@ -227,16 +244,17 @@ def _factor_worker(rank, world, port, q, B, pipeline):
         q.put((rank, False, repr(e)))
 
 
-@pytest.mark.parametrize("world,B,pipeline", [(2, 100, False), (3, 100, False), (2, 64, False),
-                                               (2, 100, True), (3, 100, True), (2, 64, True)])
-def test_factor_mlp_exchange_matches_allreduce_engine(gpu, world, B, pipeline):
+@pytest.mark.parametrize("world,B,pipeline,host", [
+    (2, 100, False, False), (3, 100, False, False), (2, 64, False, False),
+    (2, 100, True, False), (3, 100, True, False), (2, 64, True, False), (2, 100, True, True)])
+def test_factor_mlp_exchange_matches_allreduce_engine(gpu, world, B, pipeline, host):
     """Sufficient-factor engine (dz1 all-gathered in the head kernel, global W1 gradient
     formed on every rank from every rank's batch) follows the all-reduce engine's SGD
     trajectory, with bit-identical replicas."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_factor_worker, args=(r, world, port, q, B, pipeline))
+    procs = [ctx.Process(target=_factor_worker, args=(r, world, port, q, B, pipeline, host))
              for r in range(world)]
     for p in procs:
         p.start()
