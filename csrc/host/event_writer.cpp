@@ -232,6 +232,7 @@ py::dict parse_event(py::bytes b) {
       out["wall_time"] = d;
     } else if (f == 2 && w == 0) out["step"] = static_cast<int64_t>(r.varint());
     else if (f == 3 && w == 2) out["file_version"] = r.bytes();
+    else if (f == 4 && w == 2) out["graph_def"] = py::bytes(r.bytes());
     else if (f == 5 && w == 2) {
       const std::string sbuf = r.bytes();
       pb::Reader sr(sbuf);

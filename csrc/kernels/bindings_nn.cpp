@@ -74,7 +74,8 @@ void attn_fwd_launch(int, int, int, const void*, void*, float*, const float*, fl
 void attn_bwd_launch(int, int, int, const void*, const void*, const void*, const float*,
                      const float*, float, void*, float*, hipStream_t);
 void adam_mixed_launch(long long, float*, const float*, float*, float*, void*, float, float, float,
-                       float, float, float, const int*, int, hipStream_t, const long long*, int);
+                       float, float, float, const int*, int, hipStream_t, const long long*, int,
+                       long long);
 void cast_f32_bf16_launch(long long, const float*, void*, hipStream_t);
 void act_grad_bf16_launch(long long, int, const void*, const void*, void*, hipStream_t);
 void flash_fwd_launch(int, int, int, const void*, void*, float*, int, const float*, float,
@@ -167,14 +168,14 @@ void register_nn(py::module_& m) {
   m.def("adam_mixed", [](long long n, uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v,
                          uintptr_t pb, float lr, float b1, float b2, float eps, float wd,
                          float gscale, uintptr_t step_ptr, int step, uintptr_t s, uintptr_t segs,
-                         int nseg) {
+                         int nseg, long long base4) {
     dtfx::adam_mixed_launch(n, P<float>(p), P<const float>(g), P<float>(mm), P<float>(v),
                             P<void>(pb), lr, b1, b2, eps, wd, gscale, P<const int>(step_ptr), step,
-                            S(s), P<const long long>(segs), nseg);
+                            S(s), P<const long long>(segs), nseg, base4);
   }, py::arg("n"), py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pb"),
      py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"),
      py::arg("gscale"), py::arg("step_ptr"), py::arg("step"), py::arg("stream"),
-     py::arg("segs") = 0, py::arg("nseg") = 0);
+     py::arg("segs") = 0, py::arg("nseg") = 0, py::arg("base4") = 0);
   m.def("cast_f32_bf16", [](long long n, uintptr_t x, uintptr_t y, uintptr_t s) {
     dtfx::cast_f32_bf16_launch(n, P<const float>(x), P<void>(y), S(s));
   });

@@ -342,14 +342,14 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
 // NGT > 0: batch padded to NGT*16 rows at compile time (branch-free loads);
 // NGT == 0: generic (runtime NG, guarded loops).
 // XW > 0: fused xGMI gradient exchange over XW ranks before the (direct) apply.
-template <int XW>
-__device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const size_t (&off)[4],
-                                            const bool (&ok)[4], float (&v)[4], bool& fail) {
+template <int XW, int N = 4>
+__device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const size_t (&off)[N],
+                                            const bool (&ok)[N], float (&v)[N], bool& fail) {
   using xgll::u64;
   const long long par = ep & 1u;
   const int me = xg.rank;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < N; ++i) {
     if (!ok[i]) continue;
     const u64 wd = xgll::word(v[i], ep);
 #pragma unroll
@@ -357,83 +357,67 @@ __device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const 
       if (d != me) xgll::store((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + off[i], wd);
   }
   auto local = [&](int j) { return (const u64*)xg.peers.data[me] + (par * XW + j) * xg.S; };
-  if (!fail) xgll::gather_sum_n<XW, 4>(local, off, ok, me, ep, v, xg.ticks, fail);
+  if (!fail) xgll::gather_sum_n<XW, N>(local, off, ok, me, ep, v, xg.ticks, fail);
 }
 
-// Two-shot form of xg_exchange (reduce-scatter + all-gather inside the wave).  Element set i
-// of the wave (the lane's element i; 64 lanes x 4 sets per exchanging wave) is owned by rank
-// (eslot * 4 + i) % XW: WAVE-UNIFORM, the same on every rank, and balanced over the ranks
-// across the launch's waves.  (1) every non-owned element goes to its owner only (slot
-// (par, me) of the owner), (2) the owner sums the XW contributions in rank order and pushes
-// the sum into every peer's result region (2 XW + par) -- the push layout's last two slots --,
-// (3) a non-owned element waits for its owner's sum.  Per rank 2 (XW-1)/XW words per element
-// cross the links instead of XW-1 (at 8 ranks 1.75 vs 7), for one more dependent hop.  Every
-// rank pushes before it waits in each phase: no wait cycle.
-// Uniform ownership (round 4) replaced a per-lane one ((lane / 16 + 4 i) % XW): with that, a
-// wave issued all 4 x (XW-1) predicated gather loads and 4 x (XW-1) predicated stores per phase
-// whatever it owned (at 8 ranks 16 of 64 lanes did the gathers); now a wave issues (XW-1) loads
-// per OWNED set (<= 1 set from 4 ranks up) and one store per element -- the first hop at
-// 8 ranks measured 3.2 us of the 4.7 us exchange (tools/probes/engine_trace.py).
-template <int XW>
-__device__ __forceinline__ void xg_exchange2(const MlpXg& xg, unsigned ep, const size_t (&off)[4],
-                                             const bool (&ok)[4], float (&v)[4], bool& fail,
-                                             int eslot, unsigned long long* trw = nullptr) {
+// Two-shot form of xg_exchange (reduce-scatter + all-gather inside the wave): element i of
+// lane l (hidden row 4 q + i of the tile, q = l / 16) is owned by rank (q + 4 i) % XW -- the
+// same on every rank, and one owner per 16-lane row segment, so every push below writes whole
+// 128-byte runs.  (1) a non-owned value goes to its owner only (slot (par, me) of the owner),
+// (2) the owner sums the XW contributions in rank order and pushes the sum into every peer's
+// result region (2 XW + par) -- the push layout's last two slots --, (3) a non-owned element
+// waits for its owner's sum.  Per rank 2 (XW-1)/XW words per element cross the links instead
+// of XW-1 (at 8 ranks 1.75 vs 7), for one more dependent hop.  Every rank pushes before it
+// waits in each phase: no wait cycle.
+// Tried (round 4, tools/probes/engine_trace.py): wave-uniform owners ((eslot * 4 + i) % XW,
+// every owned set's gather in full 64-lane instructions, 4x fewer load instructions).  The
+// median wave's exchange at 8 ranks fell 4.7 -> 1.8 us, but the owning waves then carried all
+// of the gather transactions, the launch's span grew 8.2 -> 9.0 us and the step's local cost
+// 11.8 -> 12.6 us (W = 4: 10.1 -> 10.7): the per-lane owners keep every wave's share of the
+// uncached-memory transactions equal, which is what bounds the phase.
+// N < 4: the lane's elements i0 .. i0 + N - 1 of the four (the exchange split over the
+// K-split waves of mlp_fwdapply_kernel); ownership is by the element index i either way.
+template <int XW, int N = 4>
+__device__ __forceinline__ void xg_exchange2(const MlpXg& xg, unsigned ep, const size_t (&off)[N],
+                                             const bool (&ok)[N], float (&v)[N], bool& fail,
+                                             int lane, unsigned long long* trw = nullptr,
+                                             int i0 = 0) {
   using xgll::u64;
   const long long par = ep & 1u;
   const int me = xg.rank;
-  constexpr int NO = (4 + XW - 1) / XW;  // most sets a wave can own
-  int own[4];
+  const int q = lane >> 4;
+  int own[N];
+  bool mine[N], other[N];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) own[i] = __builtin_amdgcn_readfirstlane((eslot * 4 + i) % XW);
+  for (int i = 0; i < N; ++i) {
+    own[i] = (q + 4 * (i0 + i)) % XW;
+    mine[i] = ok[i] && own[i] == me;
+    other[i] = ok[i] && own[i] != me;
+  }
   auto slot = [&](int dst, int src) { return (u64*)xg.peers.data[dst] + (par * XW + src) * xg.S; };
   auto result = [&](int dst) { return (u64*)xg.peers.data[dst] + (2 * XW + par) * xg.S; };
-  // (1) each non-owned element to its owner: a wave-uniform destination per set (the
-  // branch over d is scalar, so the pointer table stays in SGPRs)
+  // uniform loop over destinations, per-lane predicate: a per-lane peer index would turn the
+  // kernel-argument pointer table into a private (scratch) array
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (own[i] == me) continue;
+  for (int d = 0; d < XW; ++d) {
+    if (d == me) continue;
+    u64* dst = slot(d, me);
 #pragma unroll
-    for (int d = 0; d < XW; ++d)
-      if (d == own[i] && ok[i]) xgll::store(slot(d, me) + off[i], xgll::word(v[i], ep));
-  }
-  // the owned sets, compacted (uniform indices; selects instead of register-array indexing)
-  int no = 0, idx[NO];
-#pragma unroll
-  for (int k = 0; k < NO; ++k) idx[k] = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (own[i] == me && no < NO) idx[no++] = i;
-  size_t offo[NO];
-  bool acto[NO];
-  float vo[NO];
-#pragma unroll
-  for (int k = 0; k < NO; ++k) {
-    const int j = idx[k];
-    offo[k] = j == 0 ? off[0] : j == 1 ? off[1] : j == 2 ? off[2] : off[3];
-    acto[k] = k < no && (j == 0 ? ok[0] : j == 1 ? ok[1] : j == 2 ? ok[2] : ok[3]);
-    vo[k] = j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
+    for (int i = 0; i < N; ++i)
+      if (other[i] && own[i] == d) xgll::store(dst + off[i], xgll::word(v[i], ep));
   }
   auto local = [&](int j) { return (const u64*)slot(me, j); };
-  if (no > 0 && !fail) xgll::gather_sum_n<XW, NO>(local, offo, acto, me, ep, vo, xg.ticks, fail);
+  if (!fail) xgll::gather_sum_n<XW, N>(local, off, mine, me, ep, v, xg.ticks, fail);
   if (trw) trace_stamp(trw, 5);  // probe builds: the owned sums are complete
-  // (2) the owned sums to every peer's result region
 #pragma unroll
-  for (int k = 0; k < NO; ++k) {
-    if (k >= no) break;
+  for (int d = 0; d < XW; ++d) {
+    if (d == me) continue;
+    u64* dst = result(d);
 #pragma unroll
-    for (int d = 0; d < XW; ++d)
-      if (d != me && acto[k]) xgll::store(result(d) + offo[k], xgll::word(vo[k], ep));
-    const int j = idx[k];
-    if (j == 0) v[0] = vo[k];
-    else if (j == 1) v[1] = vo[k];
-    else if (j == 2) v[2] = vo[k];
-    else v[3] = vo[k];
+    for (int i = 0; i < N; ++i)
+      if (mine[i]) xgll::store(dst + off[i], xgll::word(v[i], ep));
   }
-  // (3) the non-owned elements: their owners' sums
-  bool other[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) other[i] = ok[i] && own[i] != me;
-  if (!fail) xgll::wait_n<4>(result(me), off, other, ep, v, xg.ticks, fail);
+  if (!fail) xgll::wait_n<N>(result(me), off, other, ep, v, xg.ticks, fail);
 }
 
 // Small parameters of hidden tile jt (one product per wave), shared by mlp_wgrad_kernel and
@@ -758,9 +742,15 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         }
       }
     }
-    if (sp == 0) {
+    // SPLITX (exchange engines, two K-split waves per column group): BOTH waves finish half of
+    // the slice -- wave sp joins, exchanges and applies elements 2 sp, 2 sp + 1 of each lane --
+    // so the exchange's uncached-memory transactions are spread over all 4 waves of the block
+    // (the exchange bounds the phase at 4-8 ranks, tools/probes/engine_trace.py)
+    constexpr bool SPLITX = XW > 0 && KSP == 2;
+    if (SPLITX || sp == 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        if (SPLITX && (i >> 1) != sp) continue;
         const int j = jt * 16 + q * 4 + i;
         pw[i] = p_old[OFF_W1 + (size_t)(j < H ? j : H - 1) * D + fc];
       }
@@ -780,7 +770,16 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     float gv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) gv[i] = acc0[i] + acc1[i];
-    if constexpr (KSP > 1) {  // the later K split's partial joins split 0 (fixed order)
+    if constexpr (SPLITX) {  // hand the other wave its half: element i goes to wave i / 2
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if ((i >> 1) != sp) Kred[cgp][lane][i] = gv[i];
+      __syncthreads();
+      // split 0 + split 1 either way (IEEE addition commutes: the same bits on every rank)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if ((i >> 1) == sp) gv[i] += Kred[cgp][lane][i];
+    } else if constexpr (KSP > 1) {  // the later K split's partial joins split 0 (fixed order)
       if (sp > 0)
 #pragma unroll
         for (int i = 0; i < 4; ++i) Kred[cgp][lane][i] = gv[i];
@@ -790,7 +789,38 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         for (int i = 0; i < 4; ++i) gv[i] += Kred[cgp][lane][i];
     }
     bool fail = false;
-    if constexpr (XW > 0) if (sp == 0) {
+    if constexpr (SPLITX) {
+      size_t offw[2];
+      bool okw[2];
+      float g2[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int i = 2 * sp + e;
+        const int j = jt * 16 + q * 4 + i;
+        okw[e] = cv && j < H;
+        offw[e] = OFF_W1 + (size_t)(j < H ? j : 0) * D + fc;
+        g2[e] = sp == 0 ? gv[e] : gv[2 + e];
+      }
+      if (TRACE) trace_stamp(trw, 4);
+      if constexpr (TWO)
+        xg_exchange2<XW, 2>(xg, ep, offw, okw, g2, fail, lane, TRACE ? trw : nullptr, 2 * sp);
+      else
+        xg_exchange<XW, 2>(xg, ep, offw, okw, g2, fail);
+      if (TRACE) trace_stamp(trw, 6);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int i = 2 * sp + e;
+        const int hl = q * 4 + i, j = jt * 16 + hl;
+        const float pv = sp == 0 ? pw[e] : pw[2 + e];
+        const float v = fail ? pv : pv - lr * g2[e];  // timed out: keep W1 (err raised)
+        if (cv) {
+          if (FWD) Wt[hl][fl] = j < H ? v : 0.f;  // padded hidden rows contribute exact zeros
+          if (j < H) p_new[OFF_W1 + (size_t)j * D + f0 + fl] = v;
+        }
+      }
+      if (sp == 0 && lane == 0) xg.epochs[eslot] = ep;
+      if (fail) atomicExch(xg.err, 1);
+    } else if constexpr (XW > 0) if (sp == 0) {
       size_t offw[4];
       bool okw[4];
 #pragma unroll
@@ -800,11 +830,11 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         offw[i] = OFF_W1 + (size_t)(j < H ? j : 0) * D + fc;
       }
       if (TRACE) trace_stamp(trw, 4);
-      if constexpr (TWO) xg_exchange2<XW>(xg, ep, offw, okw, gv, fail, eslot, TRACE ? trw : nullptr);
+      if constexpr (TWO) xg_exchange2<XW>(xg, ep, offw, okw, gv, fail, lane, TRACE ? trw : nullptr);
       else xg_exchange<XW>(xg, ep, offw, okw, gv, fail);
       if (TRACE) trace_stamp(trw, 6);
     }
-    if (sp == 0) {
+    if (!SPLITX && sp == 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int hl = q * 4 + i, j = jt * 16 + hl;
@@ -815,7 +845,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         }
       }
     }
-    if constexpr (XW > 0) if (sp == 0) {
+    if constexpr (XW > 0 && !SPLITX) if (sp == 0) {
       if (lane == 0) xg.epochs[eslot] = ep;
       if (fail) atomicExch(xg.err, 1);
     }

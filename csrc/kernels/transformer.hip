@@ -952,13 +952,15 @@ __global__ __launch_bounds__(256) void adam_mixed_segs_kernel(
     long long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
     float* __restrict__ v, unsigned short* __restrict__ pb, float lr, float b1, float b2,
     float eps, float wd, float gscale, const int* __restrict__ step_ptr, int step,
-    const long long* __restrict__ segs, int nseg) {
+    const long long* __restrict__ segs, int nseg, long long base4) {
   __shared__ long long s_lo[kAdamMaxSegs], s_hi[kAdamMaxSegs], s_pl[kAdamMaxSegs];
   __shared__ const f32x4* s_w[kAdamMaxSegs];
   __shared__ int s_S[kAdamMaxSegs];
+  // segment bounds are absolute float4 indices of the whole flat buffer; this launch covers
+  // [base4, base4 + n / 4) of it (a bucket's range)
   for (int k = threadIdx.x; k < nseg; k += blockDim.x) {
-    s_lo[k] = segs[5 * k];
-    s_hi[k] = segs[5 * k + 1];
+    s_lo[k] = segs[5 * k] - base4;
+    s_hi[k] = segs[5 * k + 1] - base4;
     s_w[k] = (const f32x4*)segs[5 * k + 2];
     s_pl[k] = segs[5 * k + 3];
     s_S[k] = (int)segs[5 * k + 4];
@@ -1289,7 +1291,7 @@ void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, cons
 void adam_mixed_launch(long long n, float* p, const float* g, float* m, float* v, void* pb,
                        float lr, float b1, float b2, float eps, float wd, float gscale,
                        const int* step_ptr, int step, hipStream_t s, const long long* segs,
-                       int nseg) {
+                       int nseg, long long base4) {
   if (n % 4) throw std::runtime_error("adam_mixed: n must be a multiple of 4");
   if (n <= 0) return;
   if (nseg < 0 || nseg > kAdamMaxSegs || (nseg && !segs))
@@ -1299,7 +1301,7 @@ void adam_mixed_launch(long long n, float* p, const float* g, float* m, float* v
   if (nseg) {
     hipLaunchKernelGGL(adam_mixed_segs_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g,
                        m, v, (unsigned short*)pb, lr, b1, b2, eps, wd, gscale, step_ptr, step,
-                       segs, nseg);
+                       segs, nseg, base4);
     DTFX_HIP_CHECK(hipGetLastError());
     return;
   }

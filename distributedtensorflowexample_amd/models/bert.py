@@ -379,7 +379,25 @@ class BertMLM:
             raise ValueError("enable_splitk_fold: at most 128 split weight gradients")
         self._segs = (torch.tensor(rows, dtype=torch.int64, device=self.device)
                       if rows else None)
+        # per-bucket tables (adam_step over one bucket's range): built once, graph-safe
+        self._seg_rows = rows
+        self._bucket_segs = {}
         return len(rows)
+
+    def _segs_for(self, lo, hi):
+        if self._segs is None:
+            return None
+        if (lo, hi) == (0, self.params.numel):
+            return self._segs
+        key = (lo, hi)
+        if key not in self._bucket_segs:
+            rows = [r for r in self._seg_rows if r[0] * 4 >= lo and r[1] * 4 <= hi]
+            if any(r[0] * 4 < hi and r[1] * 4 > lo and not (r[0] * 4 >= lo and r[1] * 4 <= hi)
+                   for r in self._seg_rows):
+                raise ValueError("adam_step: range [%d, %d) cuts a folded gradient" % key)
+            self._bucket_segs[key] = (torch.tensor(rows, dtype=torch.int64, device=self.device)
+                                      if rows else None)
+        return self._bucket_segs[key]
 
     def materialize_grads(self):
         """Sum every folded weight gradient's planes into ``params.grad`` (split order)."""
@@ -398,11 +416,9 @@ class BertMLM:
         at bucket edges (ALIGN-aligned) give bit-identical results to one launch."""
         p = self.params
         hi = p.numel if hi is None else hi
-        if self._segs is not None and (lo, hi) != (0, p.numel):
-            raise ValueError("adam_step: the split-K fold runs over the whole buffer at once")
         sl = slice(lo, hi)
         TR.adam_mixed(p.master[sl], p.grad[sl], p.m[sl], p.v[sl], p.bf[sl], lr, step, wd=wd,
-                      gscale=gscale, step_ptr=step_ptr, segs=self._segs)
+                      gscale=gscale, step_ptr=step_ptr, segs=self._segs_for(lo, hi), base=lo)
 
 
 MASK_ID = 103  # "[MASK]" in the BERT uncased vocabulary

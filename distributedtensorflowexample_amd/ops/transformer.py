@@ -205,10 +205,11 @@ def attn_bwd(qkv, o, dout, lse, batch, seq, nh, kmask=None, scale=None, dbias=No
 
 # ---------------------------------------------------------------- optimizer / casts
 def adam_mixed(p, g, m, v, pb, lr, step, b1=0.9, b2=0.999, eps=1e-6, wd=0.01, gscale=1.0,
-               step_ptr=None, segs=None):
+               step_ptr=None, segs=None, base=0):
     """AdamW on an f32 master buffer; refreshes the bf16 working copy ``pb``.  ``segs``
     (int64 [nseg, 5] on the GPU, see ``BertMLM.enable_splitk_fold``): flat ranges whose
-    gradient is read as the sum of split-K partial planes instead of from ``g``."""
+    gradient is read as the sum of split-K partial planes instead of from ``g``; their bounds
+    are offsets into the whole flat buffer, of which ``p``... start at element ``base``."""
     if segs is not None and not p.is_cuda:
         raise ValueError("adam_mixed: segments are a GPU path")
     if not p.is_cuda:
@@ -228,7 +229,8 @@ def adam_mixed(p, g, m, v, pb, lr, step, b1=0.9, b2=0.999, eps=1e-6, wd=0.01, gs
         raise ValueError("adam_mixed: segs must be a contiguous int64 [nseg, 5] GPU tensor")
     hip().adam_mixed(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(pb), float(lr), float(b1),
                      float(b2), float(eps), float(wd), float(gscale), ptr(step_ptr), int(step),
-                     stream_handle(), ptr(segs), 0 if segs is None else int(segs.shape[0]))
+                     stream_handle(), ptr(segs), 0 if segs is None else int(segs.shape[0]),
+                     int(base) // 4)
 
 
 def cast_bf16(x, out=None):

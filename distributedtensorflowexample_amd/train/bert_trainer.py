@@ -58,14 +58,30 @@ class BertTrainer:
         # (94 MB of f32 word-embedding gradient for BERT-base) is the one exchange that
         # nothing overlaps, so AdamW of every other bucket runs while it is in flight
         self._body_reduced = (torch.cuda.Event() if self.comm_stream is not None else None)
+        # one GPU: nothing sits between a bucket's last gradient and its AdamW, so each
+        # bucket's AdamW runs on a third stream as soon as the bucket is final -- the
+        # (memory-bound) optimizer of layer l overlaps the (MFMA-bound) backward of layers
+        # < l instead of running after the whole backward
+        self.opt_stream = (torch.cuda.Stream(self.device)
+                           if (self.gpu and self.world == 1
+                               and os.environ.get("DTFX_BERT_OPT_OVERLAP", "1") != "0") else None)
+        self._adam_kw = None
         self.step_t = torch.ones(1, dtype=torch.int32, device=self.device)  # Adam step (device side)
         self.step_count = 0
         self.graph = None
         self.last = None
 
-    # gradient bucket ready -> all-reduce on the comm stream
+    # gradient bucket ready -> all-reduce on the comm stream (one GPU: its AdamW)
     def _on_bucket(self, i):
         if self.world == 1:
+            if self.opt_stream is not None and i != 0:  # the embeddings' AdamW: after the join
+                lo, hi = self.model.params.buckets[i]
+                cur = torch.cuda.current_stream(self.device)
+                self.opt_stream.wait_stream(cur)
+                if self.model.wgrad_stream is not None:  # the bucket's weight gradients
+                    self.opt_stream.wait_stream(self.model.wgrad_stream)
+                with torch.cuda.stream(self.opt_stream):
+                    self.model.adam_step(self.lr, 0, lo=lo, hi=hi, **self._adam_kw)
             return
         lo, hi = self.model.params.buckets[i]
         view = self.model.params.grad[lo:hi]
@@ -80,10 +96,16 @@ class BertTrainer:
 
     def _step_body(self):
         ids, tt, pos, lab, nv = self.data
+        kw = dict(gscale=1.0 / self.world, wd=self.wd, step_ptr=self.step_t)
+        self._adam_kw = kw
         loss, acc = self.model.forward_backward(ids, tt, pos, lab, n_valid=nv,
                                                 on_bucket_ready=self._on_bucket)
-        kw = dict(gscale=1.0 / self.world, wd=self.wd, step_ptr=self.step_t)
-        if self.comm_stream is not None:
+        if self.opt_stream is not None:
+            cur = torch.cuda.current_stream(self.device)
+            lo, hi = self.model.params.buckets[0]
+            self.model.adam_step(self.lr, 0, lo=lo, hi=hi, **kw)  # embeddings, last bucket
+            cur.wait_stream(self.opt_stream)                      # every other bucket's AdamW
+        elif self.comm_stream is not None:
             cur = torch.cuda.current_stream(self.device)
             split = self.model.params.buckets[1][0]  # [0, split): embeddings bucket
             cur.wait_event(self._body_reduced)

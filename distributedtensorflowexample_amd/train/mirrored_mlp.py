@@ -38,6 +38,18 @@ def _dist_env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def _mlp_graph(batch, lr):
+    """The reference MLP's graph for the chief's Supervisor (names from a variable registry
+    built like the async worker's, utils/graph.py)."""
+    from .. import variables as vs
+    from ..models.dense import make_ps_model
+    from ..utils.graph import reference_mlp_graph
+    from .worker import build_worker_variables
+
+    gv, tv = build_worker_variables(make_ps_model("mlp", "", None), vs.VariableRegistry())
+    return reference_mlp_graph(gv, tv, 0, batch_size=batch, learning_rate=lr)
+
+
 def train_mirrored(flags, dataset, log=print, max_steps=None):
     rank, world, local = _dist_env()
     use_gpu = torch.cuda.is_available() and flags.device != "cpu"
@@ -187,7 +199,7 @@ def train_mirrored(flags, dataset, log=print, max_steps=None):
                     saver=saver if is_chief else None, summary_writer=writer,
                     global_step=published_step, save_model_secs=flags.save_model_secs,
                     save_summaries_secs=flags.save_summaries_secs, save_variables=save_vars,
-                    checkpoint_on_main_thread=True)
+                    checkpoint_on_main_thread=True, graph=_mlp_graph(B, flags.learning_rate))
 
     test_x = torch.from_numpy(dataset.test.images).float().to(dev)
     test_y = dataset.test.labels.argmax(1) if dataset.test.labels.ndim == 2 else dataset.test.labels

@@ -3,7 +3,8 @@
 What the reference relies on (worker.py:107-123):
 
 * chief (task 0): restore the latest checkpoint in ``logdir`` or run
-  ``init_op``; then ``local_init_op``; start a checkpoint thread
+  ``init_op``; then ``local_init_op``; write the graph (``graph.pbtxt`` in
+  ``logdir`` + a ``graph_def`` event); start a checkpoint thread
   (``save_model_secs``) and a ``global_step/sec`` summary thread
   (``save_summaries_secs``);
 * non-chief: poll ``ready_op`` (the list of uninitialized global variables)
@@ -85,7 +86,7 @@ class Supervisor:
                  ready_op=None, global_step=None, save_model_secs=600, save_summaries_secs=120,
                  init_op=None, local_init_op=None, recovery_wait_secs=30, save_variables=None,
                  checkpoint_basename="model.ckpt", ready_timeout_secs=None, final_checkpoint=False,
-                 checkpoint_on_main_thread=False):
+                 checkpoint_on_main_thread=False, graph=None):
         self.is_chief = bool(is_chief)
         self.logdir = logdir
         self.saver = saver
@@ -102,6 +103,7 @@ class Supervisor:
         self.ready_timeout_secs = ready_timeout_secs
         self.final_checkpoint = final_checkpoint
         self.checkpoint_on_main_thread = bool(checkpoint_on_main_thread)
+        self.graph = graph  # utils.graph.GraphDefBuilder: written by the chief at start
         self._ckpt_request = threading.Event()
         self.coord = Coordinator()
         self._threads = []
@@ -157,7 +159,20 @@ class Supervisor:
             return self.save_checkpoint()
         return None
 
+    def write_graph(self):
+        """TF's Supervisor (chief): ``graph.pbtxt`` into ``logdir`` and the GraphDef through the
+        summary writer (TensorBoard's Graphs tab)."""
+        if self.graph is None:
+            return
+        if self.logdir:
+            os.makedirs(self.logdir, exist_ok=True)
+            with open(os.path.join(self.logdir, "graph.pbtxt"), "w") as f:
+                f.write(self.graph.to_pbtxt())
+        if self.summary_writer is not None and hasattr(self.summary_writer, "add_graph"):
+            self.summary_writer.add_graph(self.graph)
+
     def start_standard_services(self):
+        self.write_graph()
         if self.saver is not None and self.save_model_secs and self.save_path:
             fn = self._ckpt_request.set if self.checkpoint_on_main_thread else self.save_checkpoint
             self._threads.append(_LoopThread(self.coord, self.save_model_secs, fn,

@@ -320,6 +320,16 @@ class Worker:
                 logits = self.model.logits(self.local, x)
             return float((logits.argmax(1) == y).float().mean())
 
+    def graph_def(self):
+        """The reference graph over this worker's registry variables (utils/graph.py), or None
+        for models without the reference MLP's layer structure."""
+        if len(self.trainable) % 2:
+            return None
+        from ..utils.graph import reference_mlp_graph
+
+        return reference_mlp_graph(self.global_vars, self.trainable, self.task_index,
+                                   learning_rate=self.lr)
+
     # -- training loop (worker.py:105-159) ------------------------------------
     def learn(self, dataset, max_steps=None, stop_after_secs=None):
         try:
@@ -336,7 +346,8 @@ class Worker:
                         save_model_secs=getattr(fl, "save_model_secs", 30),
                         save_summaries_secs=getattr(fl, "save_summaries_secs", 30),
                         init_op=self.init_op, local_init_op=None,
-                        recovery_wait_secs=1.0, save_variables=self.store.read_all)
+                        recovery_wait_secs=1.0, save_variables=self.store.read_all,
+                        graph=self.graph_def())
         if self.is_chief:
             self.store.create()
         else:

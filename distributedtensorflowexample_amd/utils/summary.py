@@ -46,6 +46,15 @@ class FileWriter:
         else:
             self._w.add_summary(bytes(summary), step)
 
+    def add_graph(self, graph_def):
+        """``FileWriter.add_graph``: one Event carrying the serialized GraphDef (bytes, or a
+        ``utils.graph.GraphDefBuilder``), shown by TensorBoard's Graphs tab."""
+        from .graph import graph_event
+
+        if hasattr(graph_def, "to_bytes"):
+            graph_def = graph_def.to_bytes()
+        self._w.add_event(graph_event(bytes(graph_def)))
+
     def add_scalars(self, values, global_step):
         self._w.add_scalars({str(k): float(v) for k, v in values.items()}, int(global_step))
 
@@ -68,6 +77,7 @@ class FileWriter:
 
 
 def read_events(path):
-    """[{'step', 'wall_time', 'scalars': {...}}] of an event file (tests/tools)."""
+    """[{'step', 'wall_time', 'scalars': {...}, 'graph_def'?: bytes}] of an event file
+    (tests/tools)."""
     h = host()
     return [h.parse_event(r) for r in h.read_records(path)]

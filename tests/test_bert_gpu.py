@@ -154,3 +154,25 @@ def test_bert_splitk_fold_matches_reduce_path(gpu, monkeypatch):
         ga, gb = a.model.params.G(name).flatten(), b.model.params.G(name).flatten()
         cos = torch.dot(ga, gb) / (ga.norm() * gb.norm() + 1e-30)
         assert cos > 0.999, (name, cos.item())
+
+
+def test_bert_overlapped_adam_matches_one_launch(gpu, monkeypatch):
+    """One GPU: each bucket's AdamW on a third stream as soon as the bucket is final (overlapping
+    the rest of the backward) gives the one-launch-after-backward result."""
+    from distributedtensorflowexample_amd.train.bert_trainer import BertTrainer
+
+    cfg = BertConfig.tiny()
+    monkeypatch.setenv("DTFX_BERT_OPT_OVERLAP", "0")
+    a = BertTrainer(cfg, 32, 128, gpu, lr=1e-3)
+    monkeypatch.setenv("DTFX_BERT_OPT_OVERLAP", "1")
+    b = BertTrainer(cfg, 32, 128, gpu, lr=1e-3)
+    assert a.opt_stream is None and b.opt_stream is not None
+    a.run(3, use_graph=False)
+    b.run(3, use_graph=True)
+    d = (a.model.params.master - b.model.params.master).abs()
+    assert (d <= 2e-5).float().mean() > 0.99
+    assert d.max() <= 3 * 1e-3 * 1.01
+    assert int(a.step_t.item()) == int(b.step_t.item()) == 4
+    la, _ = a.stats()
+    lb, _ = b.stats()
+    assert abs(la - lb) < 1e-3 * abs(la)

@@ -57,6 +57,10 @@ def test_async_ps_cluster_cpu(tmp_path):
     assert sorted(v) == ["global/dense/bias", "global/dense/kernel", "global/dense_1/bias",
                          "global/dense_1/kernel", "global/global_step"]
     assert tuple(v["global/dense/kernel"].shape) == (784, 100)
+    # the chief wrote the graph (TF Supervisor): graph.pbtxt in logdir + a graph_def event
+    assert open(logdir + "/graph.pbtxt").read().count('op: "ApplyGradientDescent"') == 4
+    ev0 = read_events(glob.glob(logdir + "_0/events.out.tfevents.*")[0])
+    assert sum("graph_def" in e for e in ev0) == 1
     # per-worker TensorBoard files with loss/accuracy every step
     for t in (0, 1):
         ev = read_events(glob.glob(logdir + "_%d/events.out.tfevents.*" % t)[0])

@@ -576,14 +576,10 @@ def test_bw_allreduce_simulated_peers(gpu, world):
 
 def _w1_owner(off, world):
     """Owner rank of W1 element ``off`` in the two-shot exchange of mlp_fwdapply_kernel<.., XW,
-    .., TWO, 28 slices>: lane (q, r) of the exchanging wave of column group cgp in block
-    bid = jt * 28 + ks holds hidden j = jt*16 + 4q + i, feature ks*28 + 16 cgp + r; the set i
-    of the wave is owned by rank (eslot * 4 + i) % XW with eslot = bid * 2 + cgp."""
-    j, f = off // 784, off % 784
-    jt, i = j // 16, (j % 16) % 4
-    ks, cgp = f // 28, (f % 28) // 16
-    eslot = (jt * 28 + ks) * 2 + cgp
-    return (eslot * 4 + i) % world
+    .., TWO> (lane (q, r) of a phase-A wave holds hidden j = jt*16 + 4q + i, feature
+    ks*56 + 16w + r; owner = (q + 4 i) % XW)."""
+    hl = (off // 784) % 16
+    return (hl // 4 + 4 * (hl % 4)) % world
 
 
 @pytest.mark.parametrize("world,rank", [(3, 2), (4, 1), (5, 0), (8, 7), (8, 3)])
