@@ -34,6 +34,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -87,6 +88,27 @@ bool write_full(int fd, const void* buf, size_t n) {
     if (r <= 0) return false;
     p += r;
     n -= static_cast<size_t>(r);
+  }
+  return true;
+}
+// Gather-write of several buffers (sendmsg over iovecs, partial writes resumed): the push's
+// gradient bytes go from the caller's (pinned) memory straight into the socket, without first
+// being copied into a request string.
+bool writev_full(int fd, std::vector<iovec>& iov) {
+  size_t i = 0;
+  while (i < iov.size()) {
+    msghdr m{};
+    m.msg_iov = iov.data() + i;
+    m.msg_iovlen = std::min<size_t>(iov.size() - i, 1024);
+    const ssize_t r = ::sendmsg(fd, &m, MSG_NOSIGNAL);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    size_t n = static_cast<size_t>(r);
+    while (i < iov.size() && n >= iov[i].iov_len) n -= iov[i++].iov_len;
+    if (n) {
+      iov[i].iov_base = static_cast<char*>(iov[i].iov_base) + n;
+      iov[i].iov_len -= n;
+    }
   }
   return true;
 }
@@ -854,22 +876,33 @@ class PSClient {
     for (size_t k = 0; k < hs.size(); ++k) per[task_of(hs[k])].push_back(k);
     for (size_t k = 0; k < phs.size(); ++k) pper[task_of(phs[k])].push_back(k);
     for (size_t t = 0; t < T; ++t) {
-      std::string batch;  // the task's requests, framed, sent with one write
-      auto frame = [&](const Writer& w) {
-        const uint32_t len = static_cast<uint32_t>(w.b.size());
-        batch.append(reinterpret_cast<const char*>(&len), 4);
-        batch.append(w.b);
-      };
+      // the task's requests, framed, sent with ONE gather-write: the headers from small
+      // strings, the gradient payload straight from the caller's buffers (no copy)
+      std::vector<std::string> hdrs;
+      hdrs.reserve(3);
+      std::vector<iovec> iov;
       if (!per[t].empty()) {
+        size_t payload = 0;
+        for (size_t k : per[t]) payload += sizes[k];
         Writer w;
         w.put<uint8_t>(OP_PUSH_APPLY);
         w.put<float>(lr);
         w.put<uint8_t>(locking ? 1 : 0);
         w.put<uint32_t>(static_cast<uint32_t>(per[t].size()));
         for (size_t k : per[t]) w.put<uint32_t>(static_cast<uint32_t>(hs[k]));
-        for (size_t k : per[t]) w.raw(reinterpret_cast<const void*>(ptrs[k]), sizes[k]);
-        frame(w);
+        const uint32_t len = static_cast<uint32_t>(w.b.size() + payload);
+        hdrs.emplace_back(reinterpret_cast<const char*>(&len), 4);
+        hdrs.back().append(w.b);
+        iov.push_back({const_cast<char*>(hdrs.back().data()), hdrs.back().size()});
+        for (size_t k : per[t])
+          if (sizes[k]) iov.push_back({reinterpret_cast<void*>(ptrs[k]), sizes[k]});
       }
+      std::string tail;  // fetch_add + pull frames
+      auto frame = [&](const Writer& w) {
+        const uint32_t len = static_cast<uint32_t>(w.b.size());
+        tail.append(reinterpret_cast<const char*>(&len), 4);
+        tail.append(w.b);
+      };
       if (t == psp_.step_task) {
         Writer w;
         w.put<uint8_t>(OP_FETCH_ADD);
@@ -884,9 +917,32 @@ class PSClient {
         for (size_t k : pper[t]) w.put<uint32_t>(static_cast<uint32_t>(phs[k]));
         frame(w);
       }
+      if (!tail.empty()) iov.push_back({const_cast<char*>(tail.data()), tail.size()});
       check_usable();
-      if (!batch.empty() && !write_full(fds_[t], batch.data(), batch.size())) lost(static_cast<int>(t), "send");
+      if (!iov.empty() && !writev_full(fds_[t], iov)) lost(static_cast<int>(t), "send");
     }
+  }
+  // A pull reply read straight into the destination buffers (status byte, then the variables'
+  // bytes in request order): no intermediate response string.
+  void recv_pull_into(int task, const std::vector<size_t>& ks) {
+    check_usable();
+    uint32_t len;
+    if (!read_full(fds_[task], &len, 4)) lost(task, "recv");
+    if (len < 1) throw std::runtime_error("ps: empty response");
+    uint8_t status;
+    if (!read_full(fds_[task], &status, 1)) lost(task, "recv body");
+    size_t want = 0;
+    for (size_t k : ks) want += psp_.psizes[k];
+    if (status != 0 || len - 1 != want) {  // an error string (or an unexpected size): drain it
+      std::string rest(len - 1, '\0');
+      if (len > 1 && !read_full(fds_[task], &rest[0], len - 1)) lost(task, "recv body");
+      if (status != 0) throw std::runtime_error(rest);
+      throw std::runtime_error("ps pull: response size mismatch");
+    }
+    for (size_t k : ks)
+      if (psp_.psizes[k] && !read_full(fds_[task], reinterpret_cast<void*>(psp_.pptrs[k]),
+                                       psp_.psizes[k]))
+        lost(task, "recv body");
   }
   // push_step_pull, receive half: drains every reply (see pull) and returns the old step.
   int64_t psp_recv() {
@@ -900,21 +956,16 @@ class PSClient {
       const int n_req = (per[t].empty() ? 0 : 1) + (t == step_task ? 1 : 0) + (pper[t].empty() ? 0 : 1);
       for (int q = 0; q < n_req; ++q) {
         try {
-          std::string resp = recv(static_cast<int>(t));
           const bool is_push = q == 0 && !per[t].empty();
           const bool is_step = t == step_task && q == (per[t].empty() ? 0 : 1);
-          if (is_push) continue;
-          if (is_step) {
-            Reader r{resp.data(), resp.data() + resp.size()};
-            old = r.get<int64_t>();
+          if (!is_push && !is_step) {  // the pull: straight into the caller's buffers
+            recv_pull_into(static_cast<int>(t), pper[t]);
             continue;
           }
-          size_t off = 0;
-          for (size_t k : pper[t]) {
-            if (off + psp_.psizes[k] > resp.size()) throw std::runtime_error("ps pull: short response");
-            std::memcpy(reinterpret_cast<void*>(psp_.pptrs[k]), resp.data() + off, psp_.psizes[k]);
-            off += psp_.psizes[k];
-          }
+          std::string resp = recv(static_cast<int>(t));
+          if (is_push) continue;
+          Reader r{resp.data(), resp.data() + resp.size()};
+          old = r.get<int64_t>();
         } catch (const PSConnectionLost& e) {
           if (first_error.empty()) first_error = e.what();
           lost_conn = true;
