@@ -23,6 +23,7 @@ void mlp_head_launch(const float*, const float*, float, float*, const int*, floa
 void mlp_wgrad_launch(float*, float, float*, const float*, float*, int*, float*, int, int,
                       hipStream_t, unsigned long long*);
 long long mlp_workspace_floats(int);
+void mlp_ps_stage(const float*, const int*, float*, int*, int, hipStream_t);
 void mlp_ps_worker_step(float*, const float*, float*, const float*, const int*, float*, int*,
                         float*, float*, int*, float*, int, const float*, int, float*, float*,
                         hipStream_t);
@@ -96,6 +97,11 @@ PYBIND11_MODULE(_hip, m) {
   }, py::call_guard<py::gil_scoped_release>(),
      "async-PS worker step: staged batch + pulled params (TF layout) in, TF-layout gradient "
      "+ loss/accuracy record out, one call (train/worker.py)");
+  m.def("mlp_ps_stage", [](uintptr_t x_host, uintptr_t y_host, uintptr_t x_dev, uintptr_t y_dev,
+                           int B, uintptr_t s) {
+    dtfx::mlp_ps_stage(P<const float>(x_host), P<const int>(y_host), P<float>(x_dev),
+                       P<int>(y_dev), B, S(s));
+  });
   m.def("mlp_fwd", [](uintptr_t p_old, uintptr_t grad, float lr, uintptr_t p_new, uintptr_t x,
                       uintptr_t ws, int B, uintptr_t s, uintptr_t tr) {
     dtfx::mlp_fwd_launch(P<const float>(p_old), P<const float>(grad), lr, P<float>(p_new),

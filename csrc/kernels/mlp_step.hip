@@ -1643,12 +1643,14 @@ void mlp_ps_worker_step(float* p, const float* pulled_host, float* pull_dev, con
                         float* grad_dev, float* grad_host, hipStream_t s) {
   using namespace mlp;
   check_b(B);
-  if (!p || !x_host || !y_host || !x_dev || !y_dev || !grad || !ws || !ctr || !grad_dev ||
+  if (!p || (x_host && !y_host) || !x_dev || !y_dev || !grad || !ws || !ctr || !grad_dev ||
       !grad_host || (pulled_host && !pull_dev) || (record && !stats))
     throw std::runtime_error("mlp_ps_worker_step: missing buffer");
-  DTFX_HIP_CHECK(hipMemcpyAsync(x_dev, x_host, sizeof(float) * (size_t)B * D,
-                                hipMemcpyHostToDevice, s));
-  DTFX_HIP_CHECK(hipMemcpyAsync(y_dev, y_host, sizeof(int) * (size_t)B, hipMemcpyHostToDevice, s));
+  if (x_host) {  // (null: already staged by mlp_ps_stage while the last exchange was in flight)
+    DTFX_HIP_CHECK(hipMemcpyAsync(x_dev, x_host, sizeof(float) * (size_t)B * D,
+                                  hipMemcpyHostToDevice, s));
+    DTFX_HIP_CHECK(hipMemcpyAsync(y_dev, y_host, sizeof(int) * (size_t)B, hipMemcpyHostToDevice, s));
+  }
   if (pulled_host) {
     DTFX_HIP_CHECK(hipMemcpyAsync(pull_dev, pulled_host, sizeof(float) * NPARAM,
                                   hipMemcpyHostToDevice, s));
@@ -1663,4 +1665,14 @@ void mlp_ps_worker_step(float* p, const float* pulled_host, float* pull_dev, con
   DTFX_HIP_CHECK(hipStreamSynchronize(s));
 }
 
+
+// The next batch's H2D copies (pinned host -> device), issued while the previous step's
+// push/step/pull exchange is on the wire; mlp_ps_worker_step then runs with x_host = null.
+void mlp_ps_stage(const float* x_host, const int* y_host, float* x_dev, int* y_dev, int B,
+                  hipStream_t s) {
+  check_b(B);
+  DTFX_HIP_CHECK(hipMemcpyAsync(x_dev, x_host, sizeof(float) * (size_t)B * mlp::D,
+                                hipMemcpyHostToDevice, s));
+  DTFX_HIP_CHECK(hipMemcpyAsync(y_dev, y_host, sizeof(int) * (size_t)B, hipMemcpyHostToDevice, s));
+}
 }  // namespace dtfx

@@ -58,13 +58,14 @@ class BertTrainer:
         # (94 MB of f32 word-embedding gradient for BERT-base) is the one exchange that
         # nothing overlaps, so AdamW of every other bucket runs while it is in flight
         self._body_reduced = (torch.cuda.Event() if self.comm_stream is not None else None)
-        # one GPU: nothing sits between a bucket's last gradient and its AdamW, so each
-        # bucket's AdamW runs on a third stream as soon as the bucket is final -- the
-        # (memory-bound) optimizer of layer l overlaps the (MFMA-bound) backward of layers
-        # < l instead of running after the whole backward
+        # one GPU, DTFX_BERT_OPT_OVERLAP=1 (opt-in): each bucket's AdamW on a third stream as
+        # soon as the bucket is final, overlapping the backward of the layers below.  Measured
+        # SLOWER (bench.py --model bert: 7,779-7,801 vs 7,859-7,870 seq/s, same box,
+        # profiles/r4/bert/): the memory-bound AdamW blocks take CUs and HBM bandwidth from the
+        # dgrad / wgrad GEMMs on the critical path, costing more than the 0.66 ms it hides
         self.opt_stream = (torch.cuda.Stream(self.device)
                            if (self.gpu and self.world == 1
-                               and os.environ.get("DTFX_BERT_OPT_OVERLAP", "1") != "0") else None)
+                               and os.environ.get("DTFX_BERT_OPT_OVERLAP", "0") == "1") else None)
         self._adam_kw = None
         self.step_t = torch.ones(1, dtype=torch.int32, device=self.device)  # Adam step (device side)
         self.step_count = 0

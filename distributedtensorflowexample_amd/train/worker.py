@@ -214,16 +214,20 @@ class Worker:
             self._pull_pending = False
 
     def stage(self, batch_x, batch_y):
-        """Fused GPU worker: the batch -> pinned staging buffers (the H2D copies are issued by
-        the next compute()'s native call).  Called while the previous step's push/pull is in
-        flight on the ps (``push_step_pull_begin``), so the host copy leaves the critical path.
-        The staging buffers are free: every compute ends with a stream wait that covers their
-        last H2D."""
+        """Fused GPU worker: the batch -> pinned staging buffers -> asynchronous H2D into the
+        device batch (one native call).  Called while the previous step's push/pull is in
+        flight on the ps (``push_step_pull_begin``), so the host copy and the transfer leave the
+        critical path.  The staging buffers are free: every compute ends with a stream wait
+        that covers their last H2D."""
         if not (self.use_fused and batch_x.shape[0] == self.batch_size):
             return False
+        from ..ops._ext import hip, ptr, stream_handle
+
         y = np.asarray(batch_y)
         self._xs.numpy()[...] = batch_x
         self._ys.numpy()[...] = y.argmax(1) if y.ndim == 2 else y
+        hip().mlp_ps_stage(ptr(self._xs), ptr(self._ys), ptr(self.xb), ptr(self.yb),
+                           self.batch_size, stream_handle(self.device))
         self._staged = True
         return True
 
@@ -247,7 +251,7 @@ class Worker:
             # gradient + this step's loss / accuracy record out, stream wait (GIL released)
             hip().mlp_ps_worker_step(
                 ptr(self.params), ptr(self.store.flat) if self._pull_pending else 0,
-                ptr(self._pull_dev), ptr(self._xs), ptr(self._ys), ptr(self.xb), ptr(self.yb),
+                ptr(self._pull_dev), 0, 0, ptr(self.xb), ptr(self.yb),  # batch: staged
                 ptr(self.grad), ptr(ws.buf), ptr(ws.ctr), ptr(ws.stats), ws.stats_ring,
                 ptr(ws.stats) + 8 * (rec % ws.stats_ring), self.batch_size, ptr(self._gtf_dev),
                 ptr(self.grad_host), stream_handle(self.device))

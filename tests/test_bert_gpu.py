@@ -162,8 +162,8 @@ def test_bert_overlapped_adam_matches_one_launch(gpu, monkeypatch):
     from distributedtensorflowexample_amd.train.bert_trainer import BertTrainer
 
     cfg = BertConfig.tiny()
-    monkeypatch.setenv("DTFX_BERT_OPT_OVERLAP", "0")
-    a = BertTrainer(cfg, 32, 128, gpu, lr=1e-3)
+    monkeypatch.delenv("DTFX_BERT_OPT_OVERLAP", raising=False)
+    a = BertTrainer(cfg, 32, 128, gpu, lr=1e-3)  # default: AdamW after the backward
     monkeypatch.setenv("DTFX_BERT_OPT_OVERLAP", "1")
     b = BertTrainer(cfg, 32, 128, gpu, lr=1e-3)
     assert a.opt_stream is None and b.opt_stream is not None
