@@ -46,6 +46,8 @@
 // mlp_wgrad after it has used the value as the stats-ring index; no other
 // thread of any launch touches it.
 #include "common.h"
+#include <mutex>
+#include <map>
 #include "xgmi_ll.h"
 
 #include <cstdlib>
@@ -441,28 +443,39 @@ __device__ __forceinline__ void wgrad_small(int jt, int wave, int lane, int eidx
   // ---- small parameters of hidden tile jt: one product per wave -----------
   //   wave 0: dW2^T[:, jt] = dlT . h[:, jt]   wave 1: db1[jt] = dz1T[jt] . 1
   //   wave 2: db2 = dlT . 1 (jt == 0)         wave 3: loss/accuracy (jt == 0)
+  // With an exchange (XW > 0), the dW2 product is formed by waves 0 AND 2, each exchanging
+  // and applying half of every lane's elements (the exchange's uncached-memory transactions
+  // bound these blocks, as in mlp_fwdapply_kernel's split exchange), and db2 moves to wave 3
+  // after the loss / accuracy record.
+  const bool SPLIT = XW > 0 && (xg.split & 2);
+  int role = wave;  // 0 / 2 (SPLIT): dW2 (halves), 1: db1, 2 (!SPLIT): db2, 3: stats (+ db2)
   if (wave == 3) {
-    if (jt != 0 || !stats_on) return;
-    float l = 0.f, a = 0.f;
-    for (int b = lane; b < B; b += 64) {
-      l += w.rowstat[2 * b];
-      a += w.rowstat[2 * b + 1];
-    }
-    l = wave_sum(l);
-    a = wave_sum(a);
-    if (lane == 0) {
-      const int step = *ctr;  // this thread is the only reader/writer of ctr
-      if (stats) {
-        float* st = stats + (size_t)(step % stats_ring) * 2;
-        st[0] = l / (float)B;
-        st[1] = a / (float)B;
+    if (jt != 0) return;
+    if (stats_on) {
+      float l = 0.f, a = 0.f;
+      for (int b = lane; b < B; b += 64) {
+        l += w.rowstat[2 * b];
+        a += w.rowstat[2 * b + 1];
       }
-      *ctr = step + 1;
+      l = wave_sum(l);
+      a = wave_sum(a);
+      if (lane == 0) {
+        const int step = *ctr;  // this thread is the only reader/writer of ctr
+        if (stats) {
+          float* st = stats + (size_t)(step % stats_ring) * 2;
+          st[0] = l / (float)B;
+          st[1] = a / (float)B;
+        }
+        *ctr = step + 1;
+      }
     }
-    return;
+    if (!SPLIT) return;
+    role = 4;  // db2
   }
-  if (wave == 2 && jt != 0) return;
-  const float* A = (wave == 1) ? w.dz1T + (size_t)(jt * 16 + r) * BP + q * 4
+  if (!SPLIT && wave == 2 && jt != 0) return;
+  const bool dw2 = role == 0 || (SPLIT && role == 2);
+  const bool db2 = role == 4 || (!SPLIT && role == 2);
+  const float* A = (role == 1) ? w.dz1T + (size_t)(jt * 16 + r) * BP + q * 4
                                : w.dlT + (size_t)r * BP + q * 4;
   const float* hb = w.hbuf + jt * 16 + r;
   const unsigned ep = XW > 0 ? xg.epochs[eidx] + 1 : 0u;
@@ -471,7 +484,7 @@ __device__ __forceinline__ void wgrad_small(int jt, int wave, int lane, int eidx
 #pragma unroll
   for (int g = 0; g < MAXG; ++g)
     if (g < NG) av[g] = f4(A + g * 16);
-  if (wave == 0) {  // one uniform branch around the whole B-operand load block
+  if (dw2) {  // one uniform branch around the whole B-operand load block
 #pragma unroll
     for (int g = 0; g < MAXG; ++g)
       if (g < NG)
@@ -491,21 +504,22 @@ __device__ __forceinline__ void wgrad_small(int jt, int wave, int lane, int eidx
   float pv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    if (wave == 0) {  // C[c = q*4+i][j = jt*16 + r] -> dW2t[c][j]
+    if (dw2) {  // C[c = q*4+i][j = jt*16 + r] -> dW2t[c][j]; SPLIT: wave 0 i < 2, wave 2 i >= 2
       const int c = q * 4 + i, j = jt * 16 + r;
-      ok[i] = c < C && j < H;
-      off[i] = OFF_W2 + (ok[i] ? c * H + j : 0);
-    } else if (wave == 1) {  // C[j = jt*16 + q*4+i][*] -> db1[j]
+      ok[i] = c < C && j < H && (!SPLIT || (i >> 1) == (role >> 1));
+      off[i] = OFF_W2 + (c < C && j < H ? c * H + j : 0);
+    } else if (role == 1) {  // C[j = jt*16 + q*4+i][*] -> db1[j]
       const int j = jt * 16 + q * 4 + i;
       ok[i] = r == 0 && j < H;
       off[i] = OFF_B1 + (j < H ? j : 0);
-    } else {  // C[c = q*4+i][*] -> db2[c]
+    } else {  // db2: C[c = q*4+i][*] -> db2[c]
       const int c = q * 4 + i;
       ok[i] = r == 0 && c < C;
       off[i] = OFF_B2 + (c < C ? c : 0);
     }
     if (DIRECT) pv[i] = p_src[off[i]];
   }
+  (void)db2;
   __builtin_amdgcn_sched_barrier(0);
   // NB: padded batch columns of dz1T/dlT are zero, so multiplying by 1 is exact.
   f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
@@ -522,7 +536,24 @@ __device__ __forceinline__ void wgrad_small(int jt, int wave, int lane, int eidx
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[i] = acc0[i] + acc1[i];
   bool fail = false;
-  if constexpr (XW > 0) xg_exchange<XW>(xg, ep, off, ok, v, fail);
+  if constexpr (XW > 0) {
+    if (SPLIT && dw2) {  // this wave's half: elements 2 (role / 2) + e of every lane
+      const bool hi = role == 2;  // (selects: no dynamically indexed register arrays)
+      size_t o2[2] = {hi ? off[2] : off[0], hi ? off[3] : off[1]};
+      bool k2[2] = {hi ? ok[2] : ok[0], hi ? ok[3] : ok[1]};
+      float v2[2] = {hi ? v[2] : v[0], hi ? v[3] : v[1]};
+      xg_exchange<XW, 2>(xg, ep, o2, k2, v2, fail);
+      if (hi) {
+        v[2] = v2[0];
+        v[3] = v2[1];
+      } else {
+        v[0] = v2[0];
+        v[1] = v2[1];
+      }
+    } else {
+      xg_exchange<XW>(xg, ep, off, ok, v, fail);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (ok[i] && !fail) {
@@ -746,7 +777,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     // the slice -- wave sp joins, exchanges and applies elements 2 sp, 2 sp + 1 of each lane --
     // so the exchange's uncached-memory transactions are spread over all 4 waves of the block
     // (the exchange bounds the phase at 4-8 ranks, tools/probes/engine_trace.py)
-    constexpr bool SPLITX = XW > 0 && KSP == 2;
+    const bool SPLITX = XW > 0 && KSP == 2 && (xg.split & 1);
     if (SPLITX || sp == 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -770,7 +801,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     float gv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) gv[i] = acc0[i] + acc1[i];
-    if constexpr (SPLITX) {  // hand the other wave its half: element i goes to wave i / 2
+    if (SPLITX) {  // hand the other wave its half: element i goes to wave i / 2
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if ((i >> 1) != sp) Kred[cgp][lane][i] = gv[i];
@@ -789,7 +820,8 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         for (int i = 0; i < 4; ++i) gv[i] += Kred[cgp][lane][i];
     }
     bool fail = false;
-    if constexpr (SPLITX) {
+    if constexpr (XW > 0) {
+    if (SPLITX) {
       size_t offw[2];
       bool okw[2];
       float g2[2];
@@ -820,7 +852,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
       }
       if (sp == 0 && lane == 0) xg.epochs[eslot] = ep;
       if (fail) atomicExch(xg.err, 1);
-    } else if constexpr (XW > 0) if (sp == 0) {
+    } else if (sp == 0) {
       size_t offw[4];
       bool okw[4];
 #pragma unroll
@@ -834,6 +866,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
       else xg_exchange<XW>(xg, ep, offw, okw, gv, fail);
       if (TRACE) trace_stamp(trw, 6);
     }
+    }  // XW > 0
     if (!SPLITX && sp == 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -845,7 +878,7 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         }
       }
     }
-    if constexpr (XW > 0 && !SPLITX) if (sp == 0) {
+    if (XW > 0 && !SPLITX && sp == 0) {
       if (lane == 0) xg.epochs[eslot] = ep;
       if (fail) atomicExch(xg.err, 1);
     }
@@ -1166,6 +1199,25 @@ __global__ __launch_bounds__(256) void mlp_tf_layout_kernel(const float* __restr
   } else if (to_tf && i < NPARAM + extra) {
     dst[i] = xsrc[i - NPARAM];
   }
+}
+
+// TF layout -> flat layout iterating over the SOURCE (TF) index: consecutive threads read
+// consecutive words (the source may be host memory read over the host link, where the
+// destination-major walk of mlp_tf_layout_kernel would issue 4-byte reads 400 bytes apart)
+// and scatter into device memory.
+__global__ __launch_bounds__(256) void mlp_from_tf_src_major_kernel(const float* __restrict__ src,
+                                                                    float* __restrict__ dst) {
+  using namespace mlp;
+  const int k = blockIdx.x * 256 + threadIdx.x;  // source (TF) index
+  if (k >= NPARAM) return;
+  int i = k;  // destination (flat) index
+  if (k < OFF_B1) {  // TF W1 [784][100] -> flat W1t [100][784]
+    i = (k % H) * D + k / H;
+  } else if (k >= OFF_W2 && k < OFF_B2) {  // TF W2 [100][10] -> flat W2t [10][100]
+    const int m = k - OFF_W2;
+    i = OFF_W2 + (m % C) * H + m / C;
+  }
+  dst[i] = src[k];
 }
 
 void mlp_tf_layout_launch(const float* src, float* dst, int to_tf, const float* xsrc, int extra,
@@ -1637,6 +1689,27 @@ void mlp_fwdapply_factor_launch(const float* p_old, float* p_new, float lr, cons
 // stream.  Replaces ~10 Python-issued copies / launches / syncs per step; the caller releases
 // the GIL for the call.  Host buffers must be pinned (hipHostMalloc'd); *_dev are device staging
 // buffers of NPARAM + 2 floats.
+// Device address of a pinned host buffer when the runtime maps it into the GPU's address
+// space (hipHostMalloc'd memory: the kernels then read / write it over the host link
+// directly), else null and the caller moves it with a DMA copy.  Looked up per buffer once.
+static const void* mapped_device_ptr(const void* host) {
+  static std::mutex mu;
+  static std::map<const void*, const void*> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(host);
+  if (it != cache.end()) return it->second;
+  hipPointerAttribute_t a{};
+  const void* d = nullptr;
+  if (hipPointerGetAttributes(&a, host) == hipSuccess) {
+    if (a.type == hipMemoryTypeHost && a.devicePointer) d = a.devicePointer;
+  } else {
+    (void)hipGetLastError();  // not a HIP allocation: clear the sticky error
+  }
+  if (getenv("DTFX_PS_NO_ZERO_COPY")) d = nullptr;
+  cache[host] = d;
+  return d;
+}
+
 void mlp_ps_worker_step(float* p, const float* pulled_host, float* pull_dev, const float* x_host,
                         const int* y_host, float* x_dev, int* y_dev, float* grad, float* ws,
                         int* ctr, float* stats, int stats_ring, const float* record, int B,
@@ -1651,17 +1724,32 @@ void mlp_ps_worker_step(float* p, const float* pulled_host, float* pull_dev, con
                                   hipMemcpyHostToDevice, s));
     DTFX_HIP_CHECK(hipMemcpyAsync(y_dev, y_host, sizeof(int) * (size_t)B, hipMemcpyHostToDevice, s));
   }
+  // zero copy where the pinned buffers are device-mapped: the layout kernels read the pulled
+  // parameters from / write the gradient to host memory themselves -- no DMA copy (each has
+  // a setup latency of several us on top of the transfer) and two fewer queue entries
+  const float* pulled_map = pulled_host ? (const float*)mapped_device_ptr(pulled_host) : nullptr;
+  float* grad_map = (float*)mapped_device_ptr(grad_host);
   if (pulled_host) {
-    DTFX_HIP_CHECK(hipMemcpyAsync(pull_dev, pulled_host, sizeof(float) * NPARAM,
-                                  hipMemcpyHostToDevice, s));
-    mlp_tf_layout_launch(pull_dev, p, 0, nullptr, 0, s);
+    if (pulled_map) {
+      hipLaunchKernelGGL(mlp_from_tf_src_major_kernel, dim3((NPARAM + 255) / 256), dim3(256), 0,
+                         s, pulled_map, p);
+      DTFX_HIP_CHECK(hipGetLastError());
+    } else {
+      DTFX_HIP_CHECK(hipMemcpyAsync(pull_dev, pulled_host, sizeof(float) * NPARAM,
+                                    hipMemcpyHostToDevice, s));
+      mlp_tf_layout_launch(pull_dev, p, 0, nullptr, 0, s);
+    }
   }
   mlp_fwd_launch(p, nullptr, 0.f, nullptr, x_dev, ws, B, s, nullptr);
   mlp_head_launch(p, nullptr, 0.f, nullptr, y_dev, ws, B, s, nullptr);
   mlp_wgrad_launch(nullptr, 0.f, grad, x_dev, ws, ctr, stats, stats_ring, B, s, nullptr);
-  mlp_tf_layout_launch(grad, grad_dev, 1, record, record ? 2 : 0, s);
-  DTFX_HIP_CHECK(hipMemcpyAsync(grad_host, grad_dev, sizeof(float) * (NPARAM + (record ? 2 : 0)),
-                                hipMemcpyDeviceToHost, s));
+  if (grad_map) {
+    mlp_tf_layout_launch(grad, grad_map, 1, record, record ? 2 : 0, s);
+  } else {
+    mlp_tf_layout_launch(grad, grad_dev, 1, record, record ? 2 : 0, s);
+    DTFX_HIP_CHECK(hipMemcpyAsync(grad_host, grad_dev, sizeof(float) * (NPARAM + (record ? 2 : 0)),
+                                  hipMemcpyDeviceToHost, s));
+  }
   DTFX_HIP_CHECK(hipStreamSynchronize(s));
 }
 

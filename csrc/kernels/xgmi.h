@@ -42,6 +42,9 @@ struct MlpXg {
   unsigned* epochs;     // one counter per (block, wave) of the kernel, device resident
   int* err;             // set on a timed-out wait
   long long ticks;      // wait bound in s_memrealtime ticks (100 MHz)
+  // exchange work split (DTFX_XG_SPLIT, default 3): bit 0 -- mlp_fwdapply_kernel's W1 slices
+  // over both K-split waves; bit 1 -- the small parameters' dW2 over two waves (A/B probes)
+  int split;
 };
 constexpr int MLP_XG_EPOCHS = 1024;
 // epoch slots of the factor engine (mlp_head_kernel<.., XW> rows / mlp_wgrad_factor_kernel's

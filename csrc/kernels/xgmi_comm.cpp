@@ -5,6 +5,7 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -155,6 +156,8 @@ class XgmiAllReduce {
     xg.epochs = mlp_epochs_;
     xg.err = err_;
     xg.ticks = (long long)(timeout_s * 1e8);
+    const char* sp = getenv("DTFX_XG_SPLIT");
+    xg.split = sp ? atoi(sp) : 3;
     return xg;
   }
 

@@ -39,9 +39,20 @@ def med_max(d):
     return [round(float(d.median()), 3), round(float(d.max()), 3)]
 
 
-def summarize(t, xw):
-    """t: int64 [waves, 8] (xw) or [waves, 4] stamps in 10 ns ticks."""
+def summarize(t, xw, n_small_waves=7 * 4):
+    """t: int64 [waves, 8] (xw) or [waves, 4] stamps in 10 ns ticks; the last
+    ``n_small_waves`` rows are the small-parameter blocks (dW2 / db1 / db2 + stats)."""
     t = t.double()
+    small = t[-n_small_waves:]
+    small = small[small[:, 0] > 0]
+    w1 = t[:-n_small_waves]
+    w1 = w1[w1[:, 0] > 0]
+    extra = {}
+    if small.numel():
+        extra["small_blocks"] = med_max((small[:, 3] - small[:, 0]) / 100.0)
+        extra["small_end_after_w1_end_us"] = round(float((small[:, 3].max() - w1[:, 3].max())
+                                                         / 100.0), 3)
+    extra["w1_span_us"] = round(float((w1[:, 3].max() - w1[:, 0].min()) / 100.0), 3)
     live = t[:, 0] > 0
     t = t[live]
     us = lambda a, b: (t[:, b] - t[:, a]) / 100.0  # noqa: E731
@@ -61,6 +72,7 @@ def summarize(t, xw):
         out["apply_barrier"] = med_max(us(6, 2)[ex])
     else:
         out["phaseA_apply_barrier"] = med_max(us(1, 2)[t[:, 2] > 0])
+    out.update(extra)
     return out
 
 
