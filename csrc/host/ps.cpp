@@ -556,7 +556,10 @@ class PSClient {
       set_timeout(fds_.back(), rpc_timeout_s_);
     }
   }
-  ~PSClient() { close(); }
+  ~PSClient() {
+    close();
+    stop_sender();
+  }
 
   void close() {
     // (waits for an exchange another thread has in flight; that thread holds mu_ without
@@ -708,8 +711,18 @@ class PSClient {
     mu_.lock();
     try {
       if (psp_.active) throw std::runtime_error("ps push_step_pull_begin: an exchange is already open");
+      check_usable();
+      start_sender();
+      psp_async_ = true;  // plan only; the sender thread writes it
       psp_send(hs, ptrs, sizes, lr, locking, step_h, delta, phs, pptrs, psizes);
+      psp_async_ = false;
+      {
+        std::lock_guard<std::mutex> lk(smu_);
+        send_state_.store(1, std::memory_order_release);
+      }
+      scv_.notify_one();
     } catch (...) {
+      psp_async_ = false;
       psp_.active = false;
       mu_.unlock();
       throw;
@@ -726,6 +739,11 @@ class PSClient {
         c->mu_.unlock();
       }
     } unlock{this};
+    // the sender thread's write of this exchange must be complete (spin: it is usually done)
+    while (send_state_.load(std::memory_order_acquire) == 1) __builtin_ia32_pause();
+    send_state_.store(0, std::memory_order_relaxed);
+    check_usable();
+    if (send_bad_ >= 0) lost(send_bad_, "send");
     return psp_recv();
   }
   // Synchronous-replicas push (see SYNC_PUSH): every task gets its variables' gradients; the
@@ -875,12 +893,15 @@ class PSClient {
     auto& pper = psp_.pper;
     for (size_t k = 0; k < hs.size(); ++k) per[task_of(hs[k])].push_back(k);
     for (size_t k = 0; k < phs.size(); ++k) pper[task_of(phs[k])].push_back(k);
+    psp_.hdrs.assign(T, std::string());
+    psp_.tails.assign(T, std::string());
+    psp_.iov.assign(T, {});
     for (size_t t = 0; t < T; ++t) {
       // the task's requests, framed, sent with ONE gather-write: the headers from small
-      // strings, the gradient payload straight from the caller's buffers (no copy)
-      std::vector<std::string> hdrs;
-      hdrs.reserve(3);
-      std::vector<iovec> iov;
+      // strings, the gradient payload straight from the caller's buffers (no copy).  The plan
+      // lives in psp_ until it is sent (inline, or by the sender thread: psp_begin_async)
+      std::string& hdr = psp_.hdrs[t];
+      std::vector<iovec>& iov = psp_.iov[t];
       if (!per[t].empty()) {
         size_t payload = 0;
         for (size_t k : per[t]) payload += sizes[k];
@@ -891,13 +912,13 @@ class PSClient {
         w.put<uint32_t>(static_cast<uint32_t>(per[t].size()));
         for (size_t k : per[t]) w.put<uint32_t>(static_cast<uint32_t>(hs[k]));
         const uint32_t len = static_cast<uint32_t>(w.b.size() + payload);
-        hdrs.emplace_back(reinterpret_cast<const char*>(&len), 4);
-        hdrs.back().append(w.b);
-        iov.push_back({const_cast<char*>(hdrs.back().data()), hdrs.back().size()});
+        hdr.assign(reinterpret_cast<const char*>(&len), 4);
+        hdr.append(w.b);
+        iov.push_back({const_cast<char*>(hdr.data()), hdr.size()});
         for (size_t k : per[t])
           if (sizes[k]) iov.push_back({reinterpret_cast<void*>(ptrs[k]), sizes[k]});
       }
-      std::string tail;  // fetch_add + pull frames
+      std::string& tail = psp_.tails[t];  // fetch_add + pull frames
       auto frame = [&](const Writer& w) {
         const uint32_t len = static_cast<uint32_t>(w.b.size());
         tail.append(reinterpret_cast<const char*>(&len), 4);
@@ -918,9 +939,58 @@ class PSClient {
         frame(w);
       }
       if (!tail.empty()) iov.push_back({const_cast<char*>(tail.data()), tail.size()});
-      check_usable();
-      if (!iov.empty() && !writev_full(fds_[t], iov)) lost(static_cast<int>(t), "send");
     }
+    if (!psp_async_) psp_write();
+  }
+  // The planned writes (the caller's thread, or the sender thread; mu_ held by the exchange).
+  // Returns the index of a task whose connection failed, or -1.
+  int psp_write_tasks() {
+    for (size_t t = 0; t < psp_.iov.size(); ++t)
+      if (!psp_.iov[t].empty() && !writev_full(fds_[t], psp_.iov[t])) return static_cast<int>(t);
+    return -1;
+  }
+  void psp_write() {
+    check_usable();
+    const int bad = psp_write_tasks();
+    if (bad >= 0) lost(bad, "send");
+  }
+  // Sender thread of the split-phase exchange (push_step_pull_begin with a background send):
+  // the request bytes -- 318 KB of gradient for the reference MLP -- are copied into the
+  // socket by this thread while the caller stages its next batch; push_step_pull_end waits
+  // for it.  It spins briefly between exchanges (they come every ~0.1 ms), then sleeps.
+  void sender_loop() {
+    while (true) {
+      int spins = 0;
+      while (send_state_.load(std::memory_order_acquire) != 1) {
+        if (sender_stop_.load(std::memory_order_acquire)) return;
+        if (++spins < 20000) {
+          __builtin_ia32_pause();
+        } else {
+          std::unique_lock<std::mutex> lk(smu_);
+          scv_.wait_for(lk, std::chrono::milliseconds(5), [this] {
+            return send_state_.load(std::memory_order_acquire) == 1 ||
+                   sender_stop_.load(std::memory_order_acquire);
+          });
+          spins = 0;
+        }
+      }
+      send_bad_ = psp_write_tasks();
+      send_state_.store(2, std::memory_order_release);
+    }
+  }
+  void start_sender() {
+    if (sender_.joinable()) return;
+    sender_stop_.store(false, std::memory_order_release);
+    sender_ = std::thread([this] { sender_loop(); });
+  }
+  void stop_sender() {
+    if (!sender_.joinable()) return;
+    {
+      std::lock_guard<std::mutex> lk(smu_);
+      sender_stop_.store(true, std::memory_order_release);
+    }
+    scv_.notify_all();
+    sender_.join();
   }
   // A pull reply read straight into the destination buffers (status byte, then the variables'
   // bytes in request order): no intermediate response string.
@@ -985,7 +1055,16 @@ class PSClient {
     std::vector<std::vector<size_t>> per, pper;
     std::vector<uintptr_t> pptrs;
     std::vector<size_t> psizes;
+    std::vector<std::string> hdrs, tails;  // the planned writes' own bytes, per task
+    std::vector<std::vector<iovec>> iov;
   } psp_;
+  bool psp_async_ = false;
+  std::thread sender_;
+  std::mutex smu_;
+  std::condition_variable scv_;
+  std::atomic<int> send_state_{0};  // 0 idle, 1 planned (sender writes), 2 written
+  int send_bad_ = -1;
+  std::atomic<bool> sender_stop_{false};
 
   static uint8_t dt(const std::string& s) {
     if (s == "float32") return DT_F32;
