@@ -66,6 +66,12 @@ constexpr int FT = D / 16;     // 49 feature tiles (dW1)
 constexpr int KS2 = 14;        // K slices of the pipelined step's fused apply+forward launch
 constexpr int KW2 = D / KS2;   // 56 features = 3.5 MFMA groups of 16
 constexpr int KS3 = 28;        // ... the single-GPU form: 28 slices of 28 features (203 blocks)
+// 16-byte LL layout of the one-shot split exchange (mlp_fwdapply_kernel<.., XW, .., TWO =
+// false> with DTFX_XG_SPLIT bit 0): word pair of (exchange slot, K-split wave, lane) at
+// XG_W1_BASE + ((eslot * 2 + sp) * 64 + lane) * 2 -- past the parameter-offset region of
+// the small parameters; a communicator needs XG_SLOT_WORDS words per slot for it.
+constexpr long long XG_W1_BASE = 79616;
+constexpr long long XG_SLOT_WORDS = XG_W1_BASE + (long long)HT * KS3 * 2 * 2 * 64 * 2;
 constexpr int NSLAB_MAX = KS3; // slab planes in the workspace
 constexpr int OFF_W1 = 0;
 constexpr int OFF_B1 = H * D;
@@ -377,6 +383,54 @@ __device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const 
 // of the gather transactions, the launch's span grew 8.2 -> 9.0 us and the step's local cost
 // 11.8 -> 12.6 us (W = 4: 10.1 -> 10.7): the per-lane owners keep every wave's share of the
 // uncached-memory transactions equal, which is what bounds the phase.
+// One-shot exchange of a lane's TWO elements as one 16-byte word pair {v0, epoch, v1, epoch}
+// per peer (a single dwordx4 store / load instead of two 8-byte LL accesses: half the memory
+// instructions and requests of the wave, and 16-byte fabric writes on real xGMI).  Each 8-byte
+// half still carries its own epoch, so a reader never accepts a value of another epoch even if
+// the pair were observed as two 8-byte halves.  `woff`: this (slot, wave, lane)'s pair in the
+// XG_W1_BASE layout -- the same on every rank; both words are always written and gathered.
+template <int XW>
+__device__ __forceinline__ void xg_exchange16(const MlpXg& xg, unsigned ep, long long woff,
+                                              float (&v)[2], bool& fail) {
+  using xgll::u64;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const long long par = ep & 1u;
+  const int me = xg.rank;
+  const u32x4 out = {__float_as_uint(v[0]), ep, __float_as_uint(v[1]), ep};
+#pragma unroll
+  for (int d = 0; d < XW; ++d)
+    if (d != me) *(u32x4*)((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + woff) = out;
+  u32x4 w[XW];
+#pragma unroll
+  for (int j = 0; j < XW; ++j)
+    if (j != me)
+      w[j] = *(volatile u32x4*)((const u64*)xg.peers.data[me] + (par * XW + j) * xg.S + woff);
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ready = true;
+#pragma unroll
+    for (int j = 0; j < XW; ++j)
+      if (j != me && (w[j].y != ep || w[j].w != ep)) {
+        ready = false;
+        w[j] = *(volatile u32x4*)((const u64*)xg.peers.data[me] + (par * XW + j) * xg.S + woff);
+      }
+    if (ready) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xg.ticks) {
+      fail = true;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  float a0 = 0.f, a1 = 0.f;  // rank-ordered sums: the same bits on every rank
+#pragma unroll
+  for (int j = 0; j < XW; ++j) {
+    a0 += j == me ? v[0] : __uint_as_float(w[j].x);
+    a1 += j == me ? v[1] : __uint_as_float(w[j].z);
+  }
+  v[0] = a0;
+  v[1] = a1;
+}
+
 // N < 4: the lane's elements i0 .. i0 + N - 1 of the four (the exchange split over the
 // K-split waves of mlp_fwdapply_kernel); ownership is by the element index i either way.
 template <int XW, int N = 4>
@@ -837,7 +891,8 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
       if constexpr (TWO)
         xg_exchange2<XW, 2>(xg, ep, offw, okw, g2, fail, lane, TRACE ? trw : nullptr, 2 * sp);
       else
-        xg_exchange<XW, 2>(xg, ep, offw, okw, g2, fail);
+        xg_exchange16<XW>(xg, ep, XG_W1_BASE + ((long long)(eslot * 2 + sp) * 64 + lane) * 2,
+                          g2, fail);
       if (TRACE) trace_stamp(trw, 6);
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -1489,6 +1544,10 @@ void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const fl
     throw std::runtime_error("mlp_fwdapply_xg: needs distinct ping-pong buffers, both batches, ctr");
   if (stats && stats_ring < 1) throw std::runtime_error("mlp_fwdapply_xg: stats_ring < 1");
   if (xg.S < NPARAM) throw std::runtime_error("mlp_fwdapply_xg: exchange slots smaller than the model");
+  if (!two_shot && (xg.split & 1) && xg.S < XG_SLOT_WORDS)
+    throw std::runtime_error("mlp_fwdapply_xg: the one-shot split exchange needs slots of "
+                             "mlp_step.XG_SLOT_WORDS words (create the communicator with that "
+                             "max_numel)");
   // 28 K slices (as the single-GPU step): 196 W1 blocks x 2 column groups of epoch slots
   static_assert(HT * KS3 * 2 <= MLP_XG_SMALL_EPOCH, "W1 epoch slots overlap the small ones");
   const Bufs w = make_bufs(ws, B);

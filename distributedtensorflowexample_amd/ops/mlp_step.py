@@ -37,6 +37,27 @@ MAX_BATCH = 256
 
 # partial z1 slabs the data-parallel engines' first launch writes (their K slicing)
 XG_SLABS = 28
+# 16-byte LL layout of the fused engines' one-shot split exchange (csrc/kernels/mlp_step.hip,
+# xg_exchange16): a communicator for fused2 needs slots of XG_SLOT_WORDS words
+XG_W1_BASE = 79616
+XG_SLOT_WORDS = XG_W1_BASE + 7 * 28 * 2 * 2 * 64 * 2
+
+
+def xg_w1_pair_offsets():
+    """Slot word offset of every W1 element (flat [100][784] order) in the 16-byte layout:
+    element (hidden j, feature f) is lane (4 q + ..) r of K-split wave sp = i // 2 of column
+    group cgp of block (jt, ks), word e = i % 2 of its pair (j = 16 jt + 4 q + i, f = 28 ks +
+    16 cgp + r)."""
+    j = torch.arange(H).view(H, 1).expand(H, D)
+    f = torch.arange(D).view(1, D).expand(H, D)
+    jt, hl = j // 16, j % 16
+    q, i = hl // 4, hl % 4
+    ks, fl = f // 28, f % 28
+    cgp, r = fl // 16, fl % 16
+    eslot = (jt * 28 + ks) * 2 + cgp
+    sp, e = i // 2, i % 2
+    lane = q * 16 + r
+    return (XG_W1_BASE + ((eslot * 2 + sp) * 64 + lane) * 2 + e).reshape(-1)
 
 def unflatten(p):
     """Views (W1t [H,D], b1 [H], W2t [C,H], b2 [C]) into a flat buffer."""

@@ -180,7 +180,8 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
     for kind in kinds:
         c, err = None, ""
         try:
-            c = XgmiComm(rank, world, mlp_step.NPARAM, device=dev, key="%s/%s" % (xgmi_key, kind),
+            c = XgmiComm(rank, world, max(mlp_step.NPARAM, mlp_step.XG_SLOT_WORDS), device=dev,
+                         key="%s/%s" % (xgmi_key, kind),
                          protocol="push", timeout_s=timeout_s)
         except Exception as e:
             err = repr(e)

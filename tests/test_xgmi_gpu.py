@@ -131,7 +131,10 @@ def _fused_worker(rank, world, port, q, pipeline, two_shot=False, host=False):
         dev = torch.device("cuda:0")
         params = init_params(dev, seed=7)
         x, y = mnist_like_device(2000, seed=50 + rank, device=dev)  # per-rank data
-        fc = XgmiComm(rank, world, params.numel(), device=dev, key="f/push", protocol="push")
+        from distributedtensorflowexample_amd.ops import mlp_step
+
+        fc = XgmiComm(rank, world, mlp_step.XG_SLOT_WORDS, device=dev, key="f/push",
+                      protocol="push")
         fc.two_shot = two_shot
         ref = XgmiComm(rank, world, params.numel(), device=dev, key="f/ll", protocol="ll")
         lr = 0.05

@@ -298,11 +298,16 @@ def test_fused2_fwdapply_exchange_simulated_peers(gpu, world, rank, B):
 
     p_old, x_prev, y_prev, ws = _setup(gpu, B, 20 * world + rank)
     x, y = mnist_like_device(B, seed=999 + rank, device=gpu)
-    comm, regs = XgmiComm.with_local_peers(rank, world, mlp_step.NPARAM, device=gpu)
+    comm, regs = XgmiComm.with_local_peers(rank, world, mlp_step.XG_SLOT_WORDS, device=gpu)
     lr = 0.5
     bufs = [p_old, torch.empty_like(p_old)]
     batches = [(x_prev, y_prev), (x, y)]
     _pipelined_fwd_head(p_old, x_prev, y_prev, ws)
+    # W1 travels in the 16-byte pair layout (xg_exchange16): every pair word of the region is
+    # written by every peer (padding lanes too), so stage the whole region, then the real ones
+    w1map = mlp_step.xg_w1_pair_offsets().to(gpu)
+    n1, S = mlp_step.OFF_B1, comm.slot_stride
+    reg_lo, reg_hi = mlp_step.XG_W1_BASE, mlp_step.XG_SLOT_WORDS
     cur = 0
     for epoch in (1, 2):
         xp, yp = batches[(epoch - 1) % 2]
@@ -310,7 +315,14 @@ def test_fused2_fwdapply_exchange_simulated_peers(gpu, world, rank, B):
         po, pn = bufs[cur], bufs[cur ^ 1]
         own = _ref_grad(po, xp, yp)
         peers = _peer_grads(world, rank, 11 * epoch + world, 0.05)
-        _stage_param_words(comm, regs, peers, epoch, 0, mlp_step.NPARAM)
+        _stage_param_words(comm, regs, peers, epoch, n1, mlp_step.NPARAM)  # small: by offset
+        par = epoch & 1
+        for q in range(world):
+            if q != rank:
+                o = (par * world + q) * S
+                regs[rank][o + reg_lo:o + reg_hi] = _words(torch.zeros(reg_hi - reg_lo,
+                                                                        device=gpu), epoch)
+                regs[rank][o + w1map] = _words(peers[q][:n1].to(gpu), epoch)
         exp = po.double().cpu() - lr * _expected_update(own, peers, rank)
         torch.cuda.synchronize()
         comm.mlp_fwdapply(po, pn, lr, xp, xn, ws, True)
@@ -318,7 +330,12 @@ def test_fused2_fwdapply_exchange_simulated_peers(gpu, world, rank, B):
         comm.check()
         err = float((pn.double().cpu() - exp).abs().max())
         assert err <= 2e-5, (epoch, err)
-        _check_pushed(comm, regs, own, epoch, 0, mlp_step.NPARAM, 2e-6)
+        _check_pushed(comm, regs, own, epoch, n1, mlp_step.NPARAM, 2e-6)
+        for j in range(world):  # my W1 words reached every peer, in the pair layout
+            if j != rank:
+                w = regs[j][(par * world + rank) * S + w1map].cpu()
+                assert bool((_epochs(w) == epoch).all()), ("epoch", j, epoch)
+                assert float((_vals(w).double() - own[:n1]).abs().max()) <= 2e-6
         # step t's forward ran on the UPDATED parameters
         hbuf, _, _ = _ws_views(ws)
         h_ref, _ = mlp_step.reference_forward(pn.double().cpu(), xn.double().cpu())

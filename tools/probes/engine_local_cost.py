@@ -70,7 +70,7 @@ def main():
     out["single_gpu_2launch_us"] = round(graph_us(single, dev), 2)
     for W in (2, 4, 8):
         r = W - 1
-        comm, regs = XgmiComm.with_local_peers(r, W, mlp_step.NPARAM, device=dev,
+        comm, regs = XgmiComm.with_local_peers(r, W, mlp_step.XG_SLOT_WORDS, device=dev,
                                                protocol="push", timeout_s=1.0)
         S = comm.slot_stride
         word = (1 << 32) | int(torch.tensor([1e-3]).view(torch.int32).item())

@@ -50,6 +50,15 @@ def summarize(t, xw, n_small_waves=7 * 4):
     extra = {}
     if small.numel():
         extra["small_blocks"] = med_max((small[:, 3] - small[:, 0]) / 100.0)
+        # per wave role (row % 4): 0 dW2 (half), 1 db1, 2 dW2 half / db2, 3 stats (+ db2)
+        sm = t[-n_small_waves:]
+        for wv in range(4):
+            rows = sm[wv::4]
+            rows = rows[rows[:, 0] > 0]
+            if rows.numel():
+                extra["small_wave%d" % wv] = med_max((rows[:, 3] - rows[:, 0]) / 100.0)
+                extra["small_wave%d_start_after_first_us" % wv] = round(
+                    float((rows[:, 0].min() - t[t[:, 0] > 0][:, 0].min()) / 100.0), 3)
         extra["small_end_after_w1_end_us"] = round(float((small[:, 3].max() - w1[:, 3].max())
                                                          / 100.0), 3)
     extra["w1_span_us"] = round(float((w1[:, 3].max() - w1[:, 0].min()) / 100.0), 3)
@@ -99,7 +108,7 @@ def main():
     out["single"] = summarize(trf.cpu(), False)
     for W in (2, 4, 8):
         r = W - 1
-        comm, regs = XgmiComm.with_local_peers(r, W, mlp_step.NPARAM, device=dev,
+        comm, regs = XgmiComm.with_local_peers(r, W, mlp_step.XG_SLOT_WORDS, device=dev,
                                                protocol="push", timeout_s=1.0)
         S = comm.slot_stride
         word = (1 << 32) | int(torch.tensor([1e-3]).view(torch.int32).item())

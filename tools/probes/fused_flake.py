@@ -27,7 +27,8 @@ def worker(rank, world, port, reps):
     dev = torch.device("cuda:0")
     params = init_params(dev, seed=7)
     x, y = mnist_like_device(2000, seed=50 + rank, device=dev)
-    fc = XgmiComm(rank, world, params.numel(), device=dev, key="p/fused", protocol="push")
+    fc = XgmiComm(rank, world, mlp_step.XG_SLOT_WORDS, device=dev, key="p/fused",
+                  protocol="push")
     c_flag = XgmiComm(rank, world, params.numel(), device=dev, key="p/flag", protocol="flag")
     c_push = XgmiComm(rank, world, params.numel(), device=dev, key="p/push", protocol="push")
     for rep in range(reps):
