@@ -8,6 +8,9 @@ step() { echo "== $1"; }
 # PART=1: tests + benches, PART=2: ps benches + profiles (two gpurun calls), default: all
 PART=${PART:-all}
 if [ "$PART" != 2 ]; then
+step smoke
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 1; }
+tail -1 "$OUT/smoke.log"
 step tests
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
 tail -1 "$OUT/pytest_gpu.log"
@@ -28,7 +31,10 @@ tail -1 "$OUT/resnet_layers.jsonl"
 fi
 [ "$PART" = 1 ] && exit 0
 step ps_async
+timeout -k 10 200 python tools/probes/ps_worker_breakdown.py > "$OUT/ps_worker_breakdown.json" 2>&1 || exit 1
+timeout -k 10 200 python tools/probes/engine_local_cost.py > "$OUT/engine_local_cost.json" 2>&1 || exit 1
 timeout -k 10 200 python tools/bench_ps_async.py --num_workers 2 --steps 40000 > "$OUT/ps_async_w2.json" 2>/dev/null || exit 1
+timeout -k 10 200 python tools/bench_ps_async.py --num_workers 8 --steps 40000 > "$OUT/ps_async_w8.json" 2>/dev/null || exit 1
 timeout -k 10 200 python tools/bench_ps_async.py --num_workers 2 --steps 40000 --ps_device gpu > "$OUT/ps_async_gpu_w2.json" 2>/dev/null || exit 1
 cut -c 1-160 "$OUT/ps_async_w2.json" "$OUT/ps_async_gpu_w2.json"
 step prof
