@@ -591,6 +591,26 @@ __device__ __forceinline__ void wgrad_small(int jt, int wave, int lane, int eidx
   for (int i = 0; i < 4; ++i) v[i] = acc0[i] + acc1[i];
   bool fail = false;
   if constexpr (XW > 0) {
+    if (SPLIT && (role == 1 || role == 4)) {
+      // db1 / db2: the product against ones replicates every value over the 16 lanes of its
+      // row group, so lane r < 4 of group q takes element i = r alone -- ONE element per lane
+      // (W-1 stores, W-1 loads) instead of four with one live lane in sixteen (the traced
+      // tail of these blocks: 6.4 us at 8 ranks, profiles/r4/engine_trace/)
+      const int is = r & 3;
+      auto sel = [&](auto (&a)[4]) { return is == 0 ? a[0] : is == 1 ? a[1] : is == 2 ? a[2] : a[3]; };
+      const bool live = r < 4 && (role == 1 ? (jt * 16 + q * 4 + is < H) : (q * 4 + is < C));
+      size_t o1[1] = {sel(off)};
+      bool k1[1] = {live};
+      float v1[1] = {sel(v)};
+      xg_exchange<XW, 1>(xg, ep, o1, k1, v1, fail);
+      if (live && !fail) {
+        if (DIRECT) p[o1[0]] = sel(pv) - lr * v1[0];
+        else grad[o1[0]] = v1[0];
+      }
+      if (lane == 0) xg.epochs[eidx] = ep;
+      if (fail) atomicExch(xg.err, 1);
+      return;
+    }
     if (SPLIT && dw2) {  // this wave's half: elements 2 (role / 2) + e of every lane
       const bool hi = role == 2;  // (selects: no dynamically indexed register arrays)
       size_t o2[2] = {hi ? off[2] : off[0], hi ? off[3] : off[1]};
