@@ -52,10 +52,25 @@ int conv1x1_rows(int, int, int, int);
 void conv1x1_launch(int, int, int, int, const void*, const void*, int, void*, const void*,
                     const void*, const void*, const float*, const float*, float*, float*, void*,
                     hipStream_t);
+bool conv1x1_pro_applies(int, int, int);
+void conv1x1_pro_launch(int, int, int, int, const void*, const void*, const float*, void*,
+                        const void*, int, void*, const void*, const void*, const float*,
+                        const float*, float*, float*, void*, hipStream_t);
+void bn_fwd_coef_launch(long long, int, const float*, const float*, float, float*, float*, float*,
+                        float*, float, const float*, const float*, const float*, const float*,
+                        const float*, const float*, float*, float*, float*, float*, float*,
+                        hipStream_t);
+void bn_bwd_coef_launch(long long, int, const float*, const float*, const float*, const float*,
+                        const float*, float*, hipStream_t);
 void conv3x3_c128_launch(int, int, int, int, const void*, const void*, int, void*, void*,
                          const void*, const void*, const float*, const float*, float*, float*,
                          hipStream_t);
 void maxpool_fwd_launch(int, int, int, int, const void*, void*, void*, hipStream_t);
+void maxpool_bn_fwd_launch(int, int, int, int, const void*, const float*, void*, void*, hipStream_t);
+int maxpool_bn_bwd_rows(int, int, int, int);
+void maxpool_bn_bwd_launch(int, int, int, int, const void*, const void*, const void*, const float*,
+                           const float*, const float*, const float*, float*, float*, float*,
+                           float*, void*, hipStream_t);
 void maxpool_bwd_launch(int, int, int, int, const void*, const void*, void*, hipStream_t);
 void avgpool_fwd_launch(int, int, int, const void*, void*, hipStream_t);
 void avgpool_bwd_launch(int, int, int, const void*, void*, hipStream_t);
@@ -285,6 +300,49 @@ void register_nn(py::module_& m) {
                          P<const void>(res), P<const void>(relu_y), P<const void>(bn_x),
                          P<const float>(mean), P<const float>(rstd), P<float>(ps), P<float>(pq),
                          P<void>(wt), S(s));
+  });
+  m.def("conv1x1_pro_applies", &dtfx::conv1x1_pro_applies,
+        "(M, K, N): the narrow 1x1 kernel with the BatchNorm prologue takes this product");
+  m.def("conv1x1_pro", [](int mode, int M, int K, int N, uintptr_t s0, uintptr_t s1, uintptr_t coef,
+                          uintptr_t xo, uintptr_t w, int ldw, uintptr_t y, uintptr_t relu_y,
+                          uintptr_t bn_x, uintptr_t mean, uintptr_t rstd, uintptr_t ps, uintptr_t pq,
+                          uintptr_t wt, uintptr_t s) {
+    dtfx::conv1x1_pro_launch(mode, M, K, N, P<const void>(s0), P<const void>(s1),
+                             P<const float>(coef), P<void>(xo), P<const void>(w), ldw, P<void>(y),
+                             P<const void>(relu_y), P<const void>(bn_x), P<const float>(mean),
+                             P<const float>(rstd), P<float>(ps), P<float>(pq), P<void>(wt), S(s));
+  });
+  m.def("bn_fwd_coef", [](long long M, int C, uintptr_t sum, uintptr_t sq, float eps, uintptr_t mean,
+                          uintptr_t rstd, uintptr_t run_mean, uintptr_t run_var, float momentum,
+                          uintptr_t g, uintptr_t b, uintptr_t sum2, uintptr_t sq2, uintptr_t g2,
+                          uintptr_t b2, uintptr_t mean2, uintptr_t rstd2, uintptr_t run_mean2,
+                          uintptr_t run_var2, uintptr_t coef, uintptr_t s) {
+    dtfx::bn_fwd_coef_launch(M, C, P<const float>(sum), P<const float>(sq), eps, P<float>(mean),
+                             P<float>(rstd), P<float>(run_mean), P<float>(run_var), momentum,
+                             P<const float>(g), P<const float>(b), P<const float>(sum2),
+                             P<const float>(sq2), P<const float>(g2), P<const float>(b2),
+                             P<float>(mean2), P<float>(rstd2), P<float>(run_mean2),
+                             P<float>(run_var2), P<float>(coef), S(s));
+  });
+  m.def("bn_bwd_coef", [](long long M, int C, uintptr_t mean, uintptr_t rstd, uintptr_t g,
+                          uintptr_t sdy, uintptr_t sdyxh, uintptr_t coef, uintptr_t s) {
+    dtfx::bn_bwd_coef_launch(M, C, P<const float>(mean), P<const float>(rstd), P<const float>(g),
+                             P<const float>(sdy), P<const float>(sdyxh), P<float>(coef), S(s));
+  });
+  m.def("maxpool_bn_fwd", [](int N, int H, int W, int C, uintptr_t x, uintptr_t fcoef, uintptr_t y,
+                             uintptr_t idx, uintptr_t s) {
+    dtfx::maxpool_bn_fwd_launch(N, H, W, C, P<const void>(x), P<const float>(fcoef), P<void>(y),
+                                P<void>(idx), S(s));
+  });
+  m.def("maxpool_bn_bwd_rows", &dtfx::maxpool_bn_bwd_rows);
+  m.def("maxpool_bn_bwd", [](int N, int H, int W, int C, uintptr_t dy, uintptr_t idx, uintptr_t x,
+                             uintptr_t fcoef, uintptr_t mean, uintptr_t rstd, uintptr_t g,
+                             uintptr_t sdy, uintptr_t sdyxh, uintptr_t scratch, uintptr_t bcoef,
+                             uintptr_t dx, uintptr_t s) {
+    dtfx::maxpool_bn_bwd_launch(N, H, W, C, P<const void>(dy), P<const void>(idx), P<const void>(x),
+                                P<const float>(fcoef), P<const float>(mean), P<const float>(rstd),
+                                P<const float>(g), P<float>(sdy), P<float>(sdyxh),
+                                P<float>(scratch), P<float>(bcoef), P<void>(dx), S(s));
   });
   m.def("conv3x3_c128_applies", &dtfx::conv3x3_c128_applies,
         "the 128-channel 3x3 kernel handles this conv (stride 1, pad 1, H % 4, W % 28)");

@@ -239,6 +239,50 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
   }
 }
 
+// Per-channel coefficients of the 1x1 kernels' BatchNorm prologue (conv1x1.hip, PRO):
+// op = (s0 a + c) + (s1 b + d), coef = [a | b | c | d] f32 [4][C].
+// Forward: exactly bn_apply_kernel<STATS>'s terms (a = rstd gamma, c = beta - mean a; residual
+// b = 1, d = 0, or its own BN b = rstd2 gamma2, d = beta2 - mean2 b), and the kernel's block-0
+// duty (mean / rstd for the backward, running statistics).
+__global__ __launch_bounds__(256) void bn_fwd_coef_kernel(int C, BnStats st, BnStats st2,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, int rbn,
+                                                          float* __restrict__ coef) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float mu, rs;
+  bn_coef<true>(st, nullptr, nullptr, c, mu, rs);
+  bn_store_stats(st, c, mu, rs);
+  const float a = rs * gamma[c];
+  float b = 1.f, d = 0.f;
+  if (rbn) {
+    float mu2, rs2;
+    bn_coef<true>(st2, nullptr, nullptr, c, mu2, rs2);
+    bn_store_stats(st2, c, mu2, rs2);
+    b = rs2 * st2.gamma2[c];
+    d = st2.beta2[c] - mu2 * b;
+  }
+  coef[c] = a;
+  coef[C + c] = b;
+  coef[2 * C + c] = beta[c] - mu * a;
+  coef[3 * C + c] = d;
+}
+// Backward: bn_bwd_apply_kernel's affine form dx = A de + K1 x + K0 (s0 = de, s1 = x).
+__global__ __launch_bounds__(256) void bn_bwd_coef_kernel(int C, const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ sum_dy,
+                                                          const float* __restrict__ sum_dyxh,
+                                                          float inv_m, float* __restrict__ coef) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float A = gamma[c] * rstd[c], s1 = sum_dy[c] * inv_m, s2 = sum_dyxh[c] * inv_m;
+  coef[c] = A;
+  coef[C + c] = -A * rstd[c] * s2;
+  coef[2 * C + c] = 0.f;
+  coef[3 * C + c] = -A * s1 + A * rstd[c] * s2 * mean[c];
+}
+
 // Backward reductions: dy_eff = dy * (y > 0 if relu); per block, sums over its rows of
 // dy_eff and dy_eff * xhat per channel, reduced in LDS and written as ONE partial row per
 // block ([blocks][C], no atomics); colpart_reduce finishes the column sums.
@@ -504,6 +548,210 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int N, int H, int W, i
   }
 }
 
+// ---- the ResNet stem's BatchNorm fused into its max pool ----------------------------------
+// The stem output a = relu(bn(c)) (N x 112 x 112 x 64, 205 M elements at batch 256) is only
+// read by the pool, so it is never written: the forward pools relu(c * A + B) formed per tap
+// (bf16-rounded exactly as bn_apply_kernel stores it: the same maxima and argmax taps), and the
+// backward re-gathers the pool gradient per input pixel twice -- once for BatchNorm backward's
+// two reductions (ReLU mask recomputed from c with the forward's own arithmetic), once for the
+// apply -- instead of writing da and reading da, a and c in two more passes
+// (bn_bwd_reduce + bn_bwd_apply).  fcoef / bcoef: bn_fwd_coef / bn_bwd_coef rows [4][C].
+__device__ __forceinline__ float bn_relu_bf(float v, float a, float b) {
+  return bf(tobf(fmaxf(v * a + b, 0.f)));
+}
+__global__ __launch_bounds__(256) void maxpool_bn_fwd_kernel(int N, int H, int W, int C, int OH, int OW,
+                                                             const unsigned short* __restrict__ x,
+                                                             const float* __restrict__ fcoef,
+                                                             unsigned short* __restrict__ y,
+                                                             unsigned char* __restrict__ idx) {
+  const int cg = C >> 3;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= OW * cg) return;
+  const int ow = j / cg, g = j - ow * cg;
+  float sa[8], sb[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    sa[u] = fcoef[g * 8 + u];
+    sb[u] = fcoef[2 * C + g * 8 + u];
+  }
+  for (int row = blockIdx.y; row < N * OH; row += gridDim.y) {
+    const int n = row / OH, oh = row - n * OH;
+    float best[8];
+    unsigned char bi[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { best[u] = -INFINITY; bi[u] = 0; }
+    bf16x8 v[9];
+    bool ok[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ih = oh * 2 - 1 + t / 3, iw = ow * 2 - 1 + t % 3;
+      ok[t] = ih >= 0 && ih < H && iw >= 0 && iw < W;
+      if (ok[t]) v[t] = *(const bf16x8*)(x + (((size_t)n * H + ih) * W + iw) * C + g * 8);
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (!ok[t]) continue;
+      float f[8];
+      unpack8(v[t], f);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float a = bn_relu_bf(f[u], sa[u], sb[u]);
+        if (a > best[u]) { best[u] = a; bi[u] = (unsigned char)t; }
+      }
+    }
+    const size_t o = ((size_t)row * OW + ow) * cg + g;
+    ((bf16x8*)y)[o] = pack8(best);
+    uint2 pk;
+    pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((unsigned)bi[3] << 24);
+    pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((unsigned)bi[7] << 24);
+    ((uint2*)idx)[o] = pk;
+  }
+}
+
+// The pool gradient of input pixel (n, ih, iw), channels 8 g .. + 7 (maxpool_bwd_kernel's
+// gather), rounded to bf16 as maxpool_bwd stores it.
+__device__ __forceinline__ void maxpool_grad8(int n, int ih, int iw, int g, int cg, int OH, int OW,
+                                              const unsigned short* __restrict__ dy,
+                                              const unsigned char* __restrict__ idx, float* out) {
+  int khc[2], ohc[2], kwc[2], owc[2];
+  bool okh[2], okw[2];
+  if (ih & 1) {
+    khc[0] = 0; ohc[0] = (ih + 1) >> 1; okh[0] = ohc[0] < OH;
+    khc[1] = 2; ohc[1] = (ih - 1) >> 1; okh[1] = true;
+  } else {
+    khc[0] = 1; ohc[0] = ih >> 1; okh[0] = ohc[0] < OH;
+    khc[1] = 1; ohc[1] = 0; okh[1] = false;
+  }
+  if (iw & 1) {
+    kwc[0] = 0; owc[0] = (iw + 1) >> 1; okw[0] = owc[0] < OW;
+    kwc[1] = 2; owc[1] = (iw - 1) >> 1; okw[1] = true;
+  } else {
+    kwc[0] = 1; owc[0] = iw >> 1; okw[0] = owc[0] < OW;
+    kwc[1] = 1; owc[1] = 0; okw[1] = false;
+  }
+  uint2 pk[2][2];
+  bf16x8 dv[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (okh[a] && okw[c]) {
+        const size_t o = (((size_t)n * OH + ohc[a]) * OW + owc[c]) * cg + g;
+        pk[a][c] = ((const uint2*)idx)[o];
+        dv[a][c] = ((const bf16x8*)dy)[o];
+      }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) out[u] = 0.f;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (!(okh[a] && okw[c])) continue;
+      float d[8];
+      unpack8(dv[a][c], d);
+      const unsigned tap = khc[a] * 3 + kwc[c];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const unsigned w = q < 4 ? pk[a][c].x : pk[a][c].y;
+        if (((w >> (8 * (q & 3))) & 0xFF) == tap) out[q] += d[q];
+      }
+    }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) out[u] = bf(tobf(out[u]));
+}
+
+// Pass 1: per block, sums of de = da * (bn(c) > 0) and de * xhat over its rows; one partial row
+// per block (blockIdx.y * gridDim.x + blockIdx.x), the threads of a channel group meet in LDS.
+__global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_kernel(
+    int N, int H, int W, int C, int OH, int OW, const unsigned short* __restrict__ dy,
+    const unsigned char* __restrict__ idx, const unsigned short* __restrict__ x,
+    const float* __restrict__ fcoef, const float* __restrict__ mean, const float* __restrict__ rstd,
+    float* __restrict__ part_dy, float* __restrict__ part_dyxh) {
+  __shared__ float red[256][17];
+  const int cg = C >> 3;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const bool live = j < W * cg;
+  const int iw = live ? j / cg : 0, g = live ? j - iw * cg : 0;
+  float sa[8], sb[8], mu[8], rs[8], s1[8], s2[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    sa[u] = fcoef[g * 8 + u];
+    sb[u] = fcoef[2 * C + g * 8 + u];
+    mu[u] = mean[g * 8 + u];
+    rs[u] = rstd[g * 8 + u];
+    s1[u] = s2[u] = 0.f;
+  }
+  if (live) {
+    for (int row = blockIdx.y; row < N * H; row += gridDim.y) {
+      const int n = row / H, ih = row - n * H;
+      const bf16x8 xv = ((const bf16x8*)x)[((size_t)row * W + iw) * cg + g];
+      float da[8], xf[8];
+      maxpool_grad8(n, ih, iw, g, cg, OH, OW, dy, idx, da);
+      unpack8(xv, xf);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float de = xf[u] * sa[u] + sb[u] > 0.f ? da[u] : 0.f;
+        s1[u] += de;
+        s2[u] += de * (xf[u] - mu[u]) * rs[u];
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    red[threadIdx.x][u] = live ? s1[u] : 0.f;
+    red[threadIdx.x][8 + u] = live ? s2[u] : 0.f;
+  }
+  __syncthreads();
+  // channel c = 8 g + u: threads t with (blockIdx.x * 256 + t) % cg == g (256 % cg == 0)
+  const size_t prow = (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * C;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int gg = c >> 3, u = c & 7;
+    const int t0 = ((gg - (blockIdx.x * 256) % cg) % cg + cg) % cg;
+    float a = 0.f, b = 0.f;
+    for (int t = t0; t < 256; t += cg) {
+      a += red[t][u];
+      b += red[t][8 + u];
+    }
+    part_dy[prow + c] = a;
+    part_dyxh[prow + c] = b;
+  }
+}
+
+// Pass 2: dc = A de + K1 c + K0 (bn_bwd_apply_kernel's affine form) from the re-gathered pool
+// gradient and the recomputed mask.
+__global__ __launch_bounds__(256) void maxpool_bn_bwd_apply_kernel(
+    int N, int H, int W, int C, int OH, int OW, const unsigned short* __restrict__ dy,
+    const unsigned char* __restrict__ idx, const unsigned short* __restrict__ x,
+    const float* __restrict__ fcoef, const float* __restrict__ bcoef, unsigned short* __restrict__ dx) {
+  const int cg = C >> 3;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= W * cg) return;
+  const int iw = j / cg, g = j - iw * cg;
+  float sa[8], sb[8], ka[8], k1[8], k0[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    sa[u] = fcoef[g * 8 + u];
+    sb[u] = fcoef[2 * C + g * 8 + u];
+    ka[u] = bcoef[g * 8 + u];
+    k1[u] = bcoef[C + g * 8 + u];
+    k0[u] = bcoef[3 * C + g * 8 + u];
+  }
+  for (int row = blockIdx.y; row < N * H; row += gridDim.y) {
+    const int n = row / H, ih = row - n * H;
+    const size_t o = ((size_t)row * W + iw) * cg + g;
+    const bf16x8 xv = ((const bf16x8*)x)[o];
+    float da[8], xf[8], r[8];
+    maxpool_grad8(n, ih, iw, g, cg, OH, OW, dy, idx, da);
+    unpack8(xv, xf);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float de = xf[u] * sa[u] + sb[u] > 0.f ? da[u] : 0.f;
+      r[u] = ka[u] * de + k1[u] * xf[u] + k0[u];
+    }
+    ((bf16x8*)dx)[o] = pack8(r);
+  }
+}
+
 // global average pool: x [N][HW][C] -> y [N][C] (bf16); thread per (n, c)
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(int N, int HW, int C,
                                                           const unsigned short* __restrict__ x,
@@ -623,6 +871,33 @@ void bn_apply_stats_launch(long long M, int C, const void* x, const float* s, co
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+// Coefficients for conv1x1_pro_launch (mode 1): the training-mode BatchNorm of x (column sums
+// s / q over M rows, affine gamma / beta) plus the residual term (s2 set: a raw conv output
+// with its own BN), mean / rstd (and mean2 / rstd2) stored, running statistics updated --
+// bn_apply_stats_launch's bookkeeping, with the elementwise pass left to the consumer conv.
+void bn_fwd_coef_launch(long long M, int C, const float* s, const float* q, float eps, float* mean,
+                        float* rstd, float* run_mean, float* run_var, float momentum,
+                        const float* gamma, const float* beta, const float* s2, const float* q2,
+                        const float* g2, const float* b2, float* mean2, float* rstd2,
+                        float* run_mean2, float* run_var2, float* coef, hipStream_t stream) {
+  if (s2 && (!q2 || !g2 || !b2 || !mean2 || !rstd2))
+    throw std::runtime_error("bn_fwd_coef: residual BN needs q2, gamma2, beta2, mean2, rstd2");
+  const float inv_m = 1.f / (float)M, unbias = M > 1 ? (float)M / (float)(M - 1) : 1.f;
+  BnStats bs{s, q, inv_m, eps, unbias, momentum, mean, rstd, run_mean, run_var, nullptr, nullptr};
+  BnStats bs2{s2, q2, inv_m, eps, unbias, momentum, mean2, rstd2, run_mean2, run_var2, g2, b2};
+  hipLaunchKernelGGL(bn_fwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, C, bs, bs2,
+                     gamma, beta, s2 ? 1 : 0, coef);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+// Coefficients for conv1x1_pro_launch (mode 2): BatchNorm backward's apply half from the final
+// reductions (as bn_bwd_apply_launch).
+void bn_bwd_coef_launch(long long M, int C, const float* mean, const float* rstd, const float* gamma,
+                        const float* sum_dy, const float* sum_dyxh, float* coef, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, C, mean, rstd,
+                     gamma, sum_dy, sum_dyxh, 1.f / (float)M, coef);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
 // sum_dy / sum_dyxh (f32 [C]) are ACCUMULATED (+=): pass zeroed buffers, or the
 // (zeroed) dbeta / dgamma gradient slots themselves -- they are exactly these sums.
 // scratch: f32 [2 * bn_bwd_scratch_rows(M, C)][C].
@@ -688,6 +963,43 @@ void maxpool_bwd_launch(int N, int H, int W, int C, const void* dy, const void* 
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((W * (C / 8) + 255) / 256, rows), dim3(256), 0, st, N,
                      H, W, C, OH, OW, (const unsigned short*)dy, (const unsigned char*)idx,
                      (unsigned short*)dx);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// The stem's BatchNorm + ReLU + 3x3/2 max pool (see maxpool_bn_fwd_kernel).
+void maxpool_bn_fwd_launch(int N, int H, int W, int C, const void* x, const float* fcoef, void* y,
+                           void* idx, hipStream_t st) {
+  if (C % 8 || 256 % (C / 8)) throw std::runtime_error("maxpool_bn: C % 8 != 0, 256 % (C / 8) == 0");
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const int rows = std::min(N * OH, 65535);
+  hipLaunchKernelGGL(maxpool_bn_fwd_kernel, dim3((OW * (C / 8) + 255) / 256, rows), dim3(256), 0, st,
+                     N, H, W, C, OH, OW, (const unsigned short*)x, fcoef, (unsigned short*)y,
+                     (unsigned char*)idx);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+// Partial-row count of maxpool_bn_bwd's reduce pass ([rows][C] each of part_dy / part_dyxh).
+int maxpool_bn_bwd_rows(int N, int H, int W, int C) {
+  return ((W * (C / 8) + 255) / 256) * std::min(N * H, 256);
+}
+// Backward: BatchNorm backward's reductions (ACCUMULATED into sum_dy / sum_dyxh -- the zeroed
+// dbeta / dgamma slots) and its apply, each over the re-gathered pool gradient; dx = dL/dc.
+void maxpool_bn_bwd_launch(int N, int H, int W, int C, const void* dy, const void* idx,
+                           const void* x, const float* fcoef, const float* mean, const float* rstd,
+                           const float* gamma, float* sum_dy, float* sum_dyxh, float* scratch,
+                           float* bcoef, void* dx, hipStream_t st) {
+  if (C % 8 || 256 % (C / 8)) throw std::runtime_error("maxpool_bn: C % 8 != 0, 256 % (C / 8) == 0");
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const int gx = (W * (C / 8) + 255) / 256, gy = std::min(N * H, 256);
+  const int R = gx * gy;
+  hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, N, H, W, C, OH, OW,
+                     (const unsigned short*)dy, (const unsigned char*)idx,
+                     (const unsigned short*)x, fcoef, mean, rstd, scratch, scratch + (size_t)R * C);
+  DTFX_HIP_CHECK(hipGetLastError());
+  colpart_reduce_launch(R, C, scratch, scratch + (size_t)R * C, sum_dy, sum_dyxh, st);
+  bn_bwd_coef_launch((long long)N * H * W, C, mean, rstd, gamma, sum_dy, sum_dyxh, bcoef, st);
+  hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel, dim3(gx, std::min(N * H, 65535)), dim3(256), 0, st,
+                     N, H, W, C, OH, OW, (const unsigned short*)dy, (const unsigned char*)idx,
+                     (const unsigned short*)x, fcoef, (const float*)bcoef, (unsigned short*)dx);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

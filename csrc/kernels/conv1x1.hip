@@ -362,26 +362,48 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
 // with one block per CU owning ALL N channels: compute wave w takes MFMA row tile w % NT and
 // K part w / NT (KS = 8 / NT parts, the parts' f32 products summed in the staged epilogue), so
 // the N x K weights (32-128 KB) sit in the 8 waves' registers.
-template <int K, int N_, bool DG>
+//
+// PRO (BatchNorm prologue): the reduction operand is not read from memory as is but formed per
+// tile from TWO [M][K] sources and per-channel coefficients, op = (s0 a + c) + (s1 b + d)
+// (coef = [a | b | c | d], f32 [4][K]):
+//   PRO 1 (forward, + ReLU): s0 = conv3 output c3, s1 = the shortcut (b = 1, d = 0) or the raw
+//         downsample output (its own BN as b, d): op = the bottleneck output
+//         relu(bn3(c3) + shortcut), which is also written to xo -- the next block's conv1 forms
+//         its input itself instead of a separate bn_apply pass writing it and conv1 reading it
+//         back (one full read of the 4w-channel block output fewer per block);
+//   PRO 2 (data gradient): s0 = dL/d(BN3 output) de3, s1 = c3: op = BN3's dL/dc3 (the affine
+//         form of bn_bwd_apply), written to xo for conv3's weight gradient -- the bn_bwd_apply
+//         pass (read de3 + c3, write dc3) and this kernel's read of dc3 become one pass.
+// The 8 compute waves transform the landed tile in place in LDS (thread t owns one 16-B chunk
+// column, so its 8 channels' coefficients stay in registers), one barrier, then the MFMAs read
+// it as before.  The loader wave moves both sources (twice the tile bytes: half the pixels per
+// tile).
+template <int K, int N_, bool DG, int PRO = 0>
 constexpr int ntm() {  // pixels per tile (LDS: 3-4 ring stages + the f32 staging)
-  return DG ? (N_ == 64 ? 32 : 16) : (N_ == 64 ? 64 : 32);
+  return PRO ? ((K == 512 || (DG && N_ == 128)) ? 16 : 32) : DG ? (N_ == 64 ? 32 : 16) : (N_ == 64 ? 64 : 32);
 }
-template <int K, int N_, bool DG>
+template <int K, int N_, bool DG, int PRO = 0>
 constexpr int nqt_narrow() {  // DMA instructions per tile
-  return ntm<K, N_, DG>() * K * 2 / 1024 + (DG ? 2 * ntm<K, N_, DG>() * N_ * 2 / 1024 : 0);
+  return ntm<K, N_, DG, PRO>() * K * 2 * (PRO ? 2 : 1) / 1024 +
+         (DG ? 2 * ntm<K, N_, DG, PRO>() * N_ * 2 / 1024 : 0);
 }
 
-template <int K, int N_, bool DG>
+template <int K, int N_, bool DG, int PRO>
 __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
     int M, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
     unsigned short* __restrict__ y, const unsigned short* __restrict__ relu_y,
     const unsigned short* __restrict__ bn_x, const float* __restrict__ bn_mean,
-    const float* __restrict__ bn_rstd, float* __restrict__ ps, float* __restrict__ pq) {
+    const float* __restrict__ bn_rstd, float* __restrict__ ps, float* __restrict__ pq,
+    const unsigned short* __restrict__ src1, const float* __restrict__ coef,
+    unsigned short* __restrict__ xo) {
   constexpr int NT = N_ / 16, KS = 8 / NT, KKW = K / 32 / KS, CPR = K / 8, NCH = N_ / 8;
-  constexpr int TM = ntm<K, N_, DG>(), MT = TM / 16;
-  constexpr int XB = TM * K * 2, SB = TM * N_ * 2, STAGE = XB + (DG ? 2 * SB : 0);
-  constexpr int NQX = XB / 1024, NQS = SB / 1024, NQT = nqt_narrow<K, N_, DG>();
+  constexpr int TM = ntm<K, N_, DG, PRO>(), MT = TM / 16;
+  constexpr int XB = TM * K * 2, SB = TM * N_ * 2;
+  constexpr int XS = XB * (PRO ? 2 : 1);  // side tiles (relu_y, bn_x) after the source tile(s)
+  constexpr int STAGE = XS + (DG ? 2 * SB : 0);
+  constexpr int NQX = XB / 1024, NQS = SB / 1024, NQT = nqt_narrow<K, N_, DG, PRO>();
   constexpr int DB = 2 * NQT <= 63 ? 4 : 3, D = DB - 1;
+  static_assert(!PRO || (512 % CPR == 0 && TM % (512 / CPR) == 0), "PRO: whole chunk columns");
   constexpr int PITCH = N_ * 4 + 16;           // f32 staging row (bytes)
   constexpr int NE = TM * NCH;                 // epilogue chunks per tile
   constexpr int EP = (NE + 511) / 512;         // epilogue passes
@@ -402,6 +424,14 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
         const unsigned short* src = x + ((size_t)tile * TM + r) * K + c * 8;
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(d + q * 1024), 16, 0, 0);
       }
+      if constexpr (PRO != 0) {  // the second source, same swizzled image
+#pragma unroll
+        for (int q = 0; q < NQX; ++q) {
+          const int P = q * 64 + lane, r = P / CPR, c = (P % CPR) ^ xswz<K>(r);
+          const unsigned short* src = src1 + ((size_t)tile * TM + r) * K + c * 8;
+          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(d + XB + q * 1024), 16, 0, 0);
+        }
+      }
       if constexpr (DG) {
 #pragma unroll
         for (int si = 0; si < 2; ++si) {
@@ -411,7 +441,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
             const int P = q * 64 + lane;  // row-major [TM][N_] in 16-B chunks
             const unsigned short* src = side + (size_t)tile * TM * N_ + P * 8;
             __builtin_amdgcn_global_load_lds((const void*)src,
-                                             (lds_void*)(d + XB + si * SB + q * 1024), 16, 0, 0);
+                                             (lds_void*)(d + XS + si * SB + q * 1024), 16, 0, 0);
           }
         }
       }
@@ -425,6 +455,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
     wait_oldest(min(D, nmy) - 1);
     __syncthreads();
     for (int it = 0; it < nmy; ++it) {
+      if constexpr (PRO != 0) asm volatile("s_barrier" ::: "memory");  // (the transform's barrier)
       if (it + D < nmy) issue(it + D);
       wait_oldest(min(D, nmy - 1 - it) - 1);  // tile it + 1 landed
       __syncthreads();
@@ -441,10 +472,42 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
   float s1[8], s2[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) s1[u] = s2[u] = 0.f;
+  // PRO: thread tid transforms chunk column tcc of rows tr0 + j * RPP
+  constexpr int RPP = PRO ? 512 / CPR : 1, NPASS = PRO ? TM / RPP : 0;
+  const int tcc = tid % CPR, tr0 = tid / CPR;
+  float ca[8], cb[8], cc[8], cd[8];
+  if constexpr (PRO != 0) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ca[u] = coef[tcc * 8 + u];
+      cb[u] = coef[K + tcc * 8 + u];
+      cc[u] = coef[2 * K + tcc * 8 + u];
+      cd[u] = coef[3 * K + tcc * 8 + u];
+    }
+  }
   __syncthreads();  // tile 0 in LDS
   for (int it = 0; it < nmy; ++it) {
-    const char* buf = sm + (it % DB) * STAGE;
+    char* buf = sm + (it % DB) * STAGE;
     const int p0 = (pb + it * PB) * TM;
+    if constexpr (PRO != 0) {
+#pragma unroll
+      for (int j = 0; j < NPASS; ++j) {
+        const int r = tr0 + j * RPP, off = r * (K * 2) + ((tcc ^ xswz<K>(r)) << 4);
+        const bf16x8 a8 = *(const bf16x8*)(buf + off);
+        const bf16x8 b8 = *(const bf16x8*)(buf + XB + off);
+        bf16x8 o8;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          float o = bf(a8[u]) * ca[u] + cc[u];  // (bn_apply_kernel's order: bn(s0), then + s1 term)
+          o += bf(b8[u]) * cb[u] + cd[u];
+          if (PRO == 1) o = fmaxf(o, 0.f);
+          o8[u] = (short)tobf(o);
+        }
+        *(bf16x8*)(buf + off) = o8;
+        if (xo) *(bf16x8*)(xo + (size_t)(p0 + r) * K + tcc * 8) = o8;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -477,8 +540,8 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
         }
         bf16x8 o;
         if constexpr (DG) {
-          const bf16x8 y8 = *(const bf16x8*)(buf + XB + p * (N_ * 2) + c * 16);
-          const bf16x8 x8 = *(const bf16x8*)(buf + XB + SB + p * (N_ * 2) + c * 16);
+          const bf16x8 y8 = *(const bf16x8*)(buf + XS + p * (N_ * 2) + c * 16);
+          const bf16x8 x8 = *(const bf16x8*)(buf + XS + SB + p * (N_ * 2) + c * 16);
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             o[u] = (short)tobf(bf(y8[u]) > 0.f ? v[u] : 0.f);
@@ -566,26 +629,28 @@ int conv1x1_rows(int mode, int M, int K, int N) {
   return conv1x1_blocks(mode, K) / (N / pw::NC);
 }
 
-template <int K, int N_, bool DG>
+template <int K, int N_, bool DG, int PRO = 0>
 static void conv1x1_narrow_go(int M, const void* x, const void* w, void* y, const void* relu_y,
                               const void* bn_x, const float* mean, const float* rstd, float* ps,
-                              float* pq, hipStream_t s) {
+                              float* pq, hipStream_t s, const void* s1 = nullptr,
+                              const float* coef = nullptr, void* xo = nullptr) {
   using namespace pw;
-  constexpr int TM = ntm<K, N_, DG>(), NQT = nqt_narrow<K, N_, DG>();
+  constexpr int TM = ntm<K, N_, DG, PRO>(), NQT = nqt_narrow<K, N_, DG, PRO>();
   constexpr int DB = 2 * NQT <= 63 ? 4 : 3;
-  const size_t lds = (size_t)DB * (TM * K * 2 + (DG ? 2 * TM * N_ * 2 : 0)) +
-                     (size_t)(8 / (N_ / 16)) * TM * (N_ * 4 + 16);
-  static_assert((size_t)DB * (TM * K * 2 + (DG ? 2 * TM * N_ * 2 : 0)) >= 512 * 16 * 4,
-                "the statistics reduction reuses the ring");
+  constexpr size_t ring = (size_t)DB * (TM * K * 2 * (PRO ? 2 : 1) + (DG ? 2 * TM * N_ * 2 : 0));
+  constexpr size_t lds = ring + (size_t)(8 / (N_ / 16)) * TM * (N_ * 4 + 16);
+  static_assert(ring >= 512 * 16 * 4, "the statistics reduction reuses the ring");
+  static_assert(lds <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_narrow_kernel<K, N_, DG>,
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_narrow_kernel<K, N_, DG, PRO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL((conv1x1_narrow_kernel<K, N_, DG>), dim3(256), dim3(576), lds, s, M,
+  hipLaunchKernelGGL((conv1x1_narrow_kernel<K, N_, DG, PRO>), dim3(256), dim3(576), lds, s, M,
                      (const unsigned short*)x, (const unsigned short*)w, (unsigned short*)y,
-                     (const unsigned short*)relu_y, (const unsigned short*)bn_x, mean, rstd, ps, pq);
+                     (const unsigned short*)relu_y, (const unsigned short*)bn_x, mean, rstd, ps, pq,
+                     (const unsigned short*)s1, coef, (unsigned short*)xo);
 }
 
 template <int K>
@@ -698,6 +763,50 @@ void conv1x1_launch(int mode, int M, int K, int N, const void* x, const void* w,
   } else {
     throw std::runtime_error("conv1x1: mode 1 (forward) or 2 (dgrad)");
   }
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// The narrow products with the BatchNorm prologue (PRO, see conv1x1_narrow_kernel):
+//  mode 1: op = relu((s0 a + c) + (s1 b + d)) written to xo, y = op W^T + statistics rows;
+//  mode 2: op = (s0 a + c) + (s1 b + d) written to xo (may be null), y = de = (op W) * (relu_y
+//          > 0) + the BN-backward statistics rows of bn_x / mean / rstd.
+// coef: f32 [4][K] (bn_fwd_coef / bn_bwd_coef in cnn.hip).  One partial statistics row per block
+// (conv1x1_rows(), 256).
+bool conv1x1_pro_applies(int M, int K, int N) {
+  return M > 0 && M % 64 == 0 && conv1x1_narrow(K, N);
+}
+void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const void* s1,
+                        const float* coef, void* xo, const void* w, int ldw, void* y,
+                        const void* relu_y, const void* bn_x, const float* mean, const float* rstd,
+                        float* ps, float* pq, void* wt, hipStream_t s) {
+  using namespace pw;
+  if (!conv1x1_pro_applies(M, K, N)) throw std::runtime_error("conv1x1_pro: unsupported shape");
+  if (!s0 || !s1 || !coef || !ps || !pq || (mode == 1 && (!xo || ldw != K)) ||
+      (mode == 2 && (!relu_y || !bn_x || !mean || !rstd || !wt)) || (mode != 1 && mode != 2))
+    throw std::runtime_error("conv1x1_pro: sources, coefficients and statistics required; forward: "
+                             "xo and ldw == K; dgrad: relu_y, bn_x, mean, rstd and wt");
+  if (ldw % 8 || (((uintptr_t)s0 | (uintptr_t)s1 | (uintptr_t)xo | (uintptr_t)w | (uintptr_t)y |
+                   (uintptr_t)relu_y | (uintptr_t)bn_x | (uintptr_t)wt | (uintptr_t)coef) & 15))
+    throw std::runtime_error("conv1x1_pro: ldw % 8, 16-B aligned tensors");
+  const void* wv = w;
+  if (mode == 2) {
+    hipLaunchKernelGGL(transpose_bf16_kernel, dim3((N + 31) / 32, K / 32), dim3(256), 0, s, K, N,
+                       (const unsigned short*)w, ldw, (unsigned short*)wt);
+    wv = wt;
+  }
+#define DTFX_PW_PRO(KV, NV)                                                                     \
+  do {                                                                                          \
+    if (mode == 1)                                                                              \
+      conv1x1_narrow_go<KV, NV, false, 1>(M, s0, wv, y, nullptr, nullptr, nullptr, nullptr, ps, pq, \
+                                          s, s1, coef, xo);                                     \
+    else                                                                                        \
+      conv1x1_narrow_go<KV, NV, true, 2>(M, s0, wv, y, relu_y, bn_x, mean, rstd, ps, pq, s, s1, \
+                                         coef, xo);                                             \
+  } while (0)
+  if (K == 256 && N == 64) DTFX_PW_PRO(256, 64);
+  else if (K == 256) DTFX_PW_PRO(256, 128);
+  else DTFX_PW_PRO(512, 128);
+#undef DTFX_PW_PRO
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

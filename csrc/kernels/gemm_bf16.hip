@@ -127,13 +127,15 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   const int nk = max(0, min(per, nk_all - kt0));
   RowState rs;
   if (NBUF != 8 && (MODE == 1 || MODE == 2)) conv_rows<NW, BM / 8 / NW>(cd, MODE, M, m0, wave, lane, rs);
+  Im2colCols ics;  // MODE 3: the lane's gathered columns, decoded once
+  if constexpr (MODE == 3) im2col_cols<NW>(cd, n0, wave, lane, ics);
   auto stage_all = [&](int buf, int kt) {
     char* base = smem + buf * BUF_BYTES;
     const int k0 = (kt0 + kt) * BK;
     if (MODE == 1 || MODE == 2) stage_a_conv<NW, BM / 8 / NW>(cd, MODE, rs, A, k0, base, wave, lane);
     else stage<!TA, BM, NW>(A, lda, m0, a_max, k0, base, wave, lane, K - 1);
     if (MODE == 2) stage_b_wtap<NW, BN>(cd, B, n0, k0, base + TILE_A, wave, lane);
-    else if (MODE == 3) stage_b_im2col<NW>(cd, B, K, n0, k0, base + TILE_A, wave, lane);
+    else if (MODE == 3) stage_b_im2col_h<NW>(cd, B, K, k0, ics, base + TILE_A, wave, lane);
     else stage<TB, BN, NW>(B, ldb, n0, b_max, k0, base + TILE_A, wave, lane, K - 1);
   };
   auto compute = [&](int buf) {

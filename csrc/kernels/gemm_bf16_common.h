@@ -259,28 +259,54 @@ __device__ __forceinline__ void stage_b_wtap(const ConvDesc& d, const unsigned s
   }
 }
 
-// B tile for wgrad (k-strided image [64 pixels][128 j]): im2col(x)[p][j = (kh, kw, ci)]
+// B tile for wgrad (k-strided image [64 pixels][128 j]): im2col(x)[p][j = (kh, kw, ci)].
+// The column half of the gather is hoisted out of the K loop: a lane's 16-B
+// chunk always covers the same 8 columns j (its k-row kr and swizzled chunk are fixed), so
+// (tap, ci) -> (kh - pad, kw - pad, ci) is decoded ONCE per block (im2col_cols) and each K tile
+// only decodes its pixels (2 fdivmods per chunk instead of 4).
+struct Im2colCols {
+  int ci[4], dh[4], dw[4];  // channel offset, kh - pad, kw - pad of the lane's i-th chunk
+  int jok;                  // bit i: the chunk's columns are inside KH * KW * C
+};
 template <int NW>
-__device__ __forceinline__ void stage_b_im2col(const ConvDesc& d, const unsigned short* __restrict__ x,
-                                               int NP, int n0, int k0, char* lds_tile, int wave,
-                                               int lane) {
-  const int ohw = d.OH * d.OW;
-  const float iohw = 1.f / ohw, iow = 1.f / d.OW, ikw = 1.f / d.KW, ic = 1.f / d.C;
+__device__ __forceinline__ void im2col_cols(const ConvDesc& d, int n0, int wave, int lane, Im2colCols& s) {
+  static_assert(16 / NW <= 4, "Im2colCols holds 4 chunks per lane");
+  const float ikw = 1.f / d.KW, ic = 1.f / d.C;
   const int jtot = d.KH * d.KW * d.C;
+  s.jok = 0;
 #pragma unroll
   for (int i = 0; i < 16 / NW; ++i) {
     const int blk = i * NW + wave;
     const int kr = blk * 4 + (lane >> 4);
     const int c = (lane & 15) ^ swz_tr(kr);
-    const int p = k0 + kr, j = n0 + c * 8;
-    int n, rem, oh, ow, tap, ci, kh, kw;
-    fdivmod(min(p, NP - 1), ohw, iohw, n, rem);
-    fdivmod(rem, d.OW, iow, oh, ow);
+    const int j = n0 + c * 8;
+    int tap, ci, kh, kw;
     fdivmod(min(j, jtot - 8), d.C, ic, tap, ci);
     fdivmod(tap, d.KW, ikw, kh, kw);
-    const int yy = oh * d.stride - d.pad + kh, xx = ow * d.stride - d.pad + kw;
-    const bool ok = p < NP && j < jtot && yy >= 0 && yy < d.H && xx >= 0 && xx < d.W;
-    const unsigned short* g = ok ? x + ((size_t)(n * d.H + yy) * d.W + xx) * d.C + ci : g_zero16;
+    s.ci[i] = ci;
+    s.dh[i] = kh - d.pad;
+    s.dw[i] = kw - d.pad;
+    s.jok |= (j < jtot ? 1 : 0) << i;
+  }
+}
+template <int NW>
+__device__ __forceinline__ void stage_b_im2col_h(const ConvDesc& d, const unsigned short* __restrict__ x,
+                                                 int NP, int k0, const Im2colCols& s, char* lds_tile,
+                                                 int wave, int lane) {
+  const int ohw = d.OH * d.OW;
+  const float iohw = 1.f / ohw, iow = 1.f / d.OW;
+#pragma unroll
+  for (int i = 0; i < 16 / NW; ++i) {
+    const int blk = i * NW + wave;
+    const int kr = blk * 4 + (lane >> 4);
+    const int p = k0 + kr;
+    int n, rem, oh, ow;
+    fdivmod(min(p, NP - 1), ohw, iohw, n, rem);
+    fdivmod(rem, d.OW, iow, oh, ow);
+    const int yy = oh * d.stride + s.dh[i], xx = ow * d.stride + s.dw[i];
+    const bool ok = p < NP && ((s.jok >> i) & 1) && (unsigned)yy < (unsigned)d.H &&
+                    (unsigned)xx < (unsigned)d.W;
+    const unsigned short* g = ok ? x + ((size_t)(n * d.H + yy) * d.W + xx) * d.C + s.ci[i] : g_zero16;
     __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(lds_tile + blk * 1024), 16, 0, 0);
   }
 }

@@ -11,7 +11,11 @@ MI355X-first design:
   matrix cores (``ops.cnn.conv_*``: the im2col/col2im gathers run inside the
   GEMM's LDS staging) and the forward convolution's epilogue also produces
   the BatchNorm batch statistics (sum and sum of squares per channel), so BN
-  costs one finalize + one fused apply(+residual +ReLU) pass;
+  costs one finalize + one fused apply(+residual +ReLU) pass -- or none of its
+  own where the consumer forms it: a bottleneck's output relu(bn3(c3) + shortcut)
+  inside the next block's narrow 1x1 conv1 (``_finish_block``), BN3's backward
+  apply inside conv3's narrow data gradient (``_block_bwd``), and the stem's
+  relu(bn(c)) inside the max pool, forward and backward (never stored);
 * flat f32 master / bf16 working copy / f32 gradient / momentum buffers with
   64-element aligned slots; one all-reduce bucket per bottleneck block,
   released as soon as that block's backward finishes;
@@ -22,6 +26,7 @@ MI355X-first design:
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -32,6 +37,8 @@ from ..ops import transformer as TR
 
 BF16 = torch.bfloat16
 ALIGN = 64
+# the stem's BatchNorm + ReLU fused into its max pool (DTFX_STEM_POOL_BN=0: separate passes)
+_STEM_POOL_BN = os.environ.get("DTFX_STEM_POOL_BN", "1") != "0"
 STAGES = [(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)]  # (width, blocks, stride)
 IN_CH = 8          # 3 image channels + 5 zero channels
 NUM_CLASSES = 1000
@@ -168,34 +175,36 @@ class ResNet50:
         self._stats_flat.zero_()  # every BN's (sum, sum of squares) accumulators, one memset
         saved = {}
         c, st = self._conv_bn("conv1", images)
-        a, m, r = self._bn_apply("conv1", c, st)
-        saved["conv1"] = (images, c, m, r, a)
-        x, idx = CN.maxpool_fwd(a)
+        if c.is_cuda and _STEM_POOL_BN:
+            # the stem's relu(bn(c)) is formed inside the pool and never stored
+            rm, rv = P.running["conv1"]
+            x, idx, m, r, fco = CN.bn_maxpool_fwd(c, st[0], st[1], st[2], P.P("conv1.bn.gamma"),
+                                                  P.P("conv1.bn.beta"), self.eps, rm, rv)
+            saved["conv1"] = (images, c, m, r, None, fco)
+        else:
+            a, m, r = self._bn_apply("conv1", c, st)
+            saved["conv1"] = (images, c, m, r, a, None)
+            x, idx = CN.maxpool_fwd(a)
         blocks = []
+        pend = None  # the previous block, its output not formed yet (see _finish_block)
         for si, (w, nb, st_) in enumerate(P.stages):
             for b in range(nb):
                 pre = "layer%d.%d." % (si + 1, b)
-                x_in = x
-                c1, s1 = self._conv_bn(pre + "conv1", x_in)
+                if pend is None:
+                    x_in = x
+                    c1, s1 = self._conv_bn(pre + "conv1", x_in)
+                else:
+                    x_in, c1, s1 = self._finish_block(blocks, pend, pre + "conv1")
                 a1, m1, r1 = self._bn_apply(pre + "conv1", c1, s1)
                 c2, s2 = self._conv_bn(pre + "conv2", a1)
                 a2, m2, r2 = self._bn_apply(pre + "conv2", c2, s2)
                 c3, s3 = self._conv_bn(pre + "conv3", a2)
-                if b == 0:
-                    # out = relu(bn3(c3) + bn_ds(downsample(x))) in one pass: the normalised
-                    # shortcut is never materialised
-                    cs_, sds = self._conv_bn(pre + "downsample", x_in)
-                    rm, rv = P.running[pre + "downsample"]
-                    nd = pre + "downsample.bn."
-                    out, m3, r3, ms, rs = self._bn_apply(
-                        pre + "conv3", c3, s3, residual=cs_, relu=True,
-                        res_bn=(sds[0], sds[1], P.P(nd + "gamma"), P.P(nd + "beta"), rm, rv))
-                    ds = (cs_, ms, rs)
-                else:
-                    ds = None
-                    out, m3, r3 = self._bn_apply(pre + "conv3", c3, s3, residual=x_in, relu=True)
-                blocks.append((pre, x_in, (c1, m1, r1, a1), (c2, m2, r2, a2), (c3, m3, r3), ds, out))
-                x = out
+                # (first block: the downsample conv of the same input; its BatchNorm is applied
+                # with bn3's, the normalised shortcut is never materialised)
+                dsc = self._conv_bn(pre + "downsample", x_in) if b == 0 else None
+                blocks.append([pre, x_in, (c1, m1, r1, a1), (c2, m2, r2, a2), None, None, None])
+                pend = (len(blocks) - 1, c3, s3, dsc)
+        x, _, _ = self._finish_block(blocks, pend, None)
         pooled = CN.avgpool_fwd(x)                               # [N, 2048]
         logits = B16.gemm(pooled, P.W("fc.weight"), False, True, bias=P.P("fc.bias"),
                           out_dtype=torch.float32)                # [N, 1024]
@@ -226,10 +235,14 @@ class ResNet50:
                     torch.cuda.current_stream(dx.device).wait_stream(ws)
                 on_bucket_ready(bucket)
             bucket -= 1
-        da = CN.maxpool_bwd(dx, idx, saved["conv1"][4].shape)
-        img, c, m, r, a = saved["conv1"]
-        dc, _ = CN.bn_bwd(da, a, c, m, r, P.P("conv1.bn.gamma"), P.G("conv1.bn.gamma"),
-                          P.G("conv1.bn.beta"), relu=True, grads_zeroed=True)
+        img, c, m, r, a, fco = saved["conv1"]
+        if a is None:
+            dc = CN.maxpool_bn_bwd(dx, idx, c, m, r, P.P("conv1.bn.gamma"), P.P("conv1.bn.beta"),
+                                   fco, P.G("conv1.bn.gamma"), P.G("conv1.bn.beta"))
+        else:
+            da = CN.maxpool_bwd(dx, idx, a.shape)
+            dc, _ = CN.bn_bwd(da, a, c, m, r, P.P("conv1.bn.gamma"), P.G("conv1.bn.gamma"),
+                              P.G("conv1.bn.beta"), relu=True, grads_zeroed=True)
         _, cin, cout, k, s, p = self.specs["conv1"]
         CN.conv_wgrad(dc, img, P.G("conv1.weight"), k, k, s, p, beta=1.0)
         if ws is not None:  # join: every gradient final on the main stream
@@ -238,6 +251,47 @@ class ResNet50:
         if on_bucket_ready is not None:
             on_bucket_ready(0)
         return loss, acc
+
+    def _finish_block(self, blocks, pend, next_conv):
+        """Form block ``pend``'s output ``out = relu(bn3(c3) + shortcut)`` (shortcut: the
+        block input, or bn_ds(downsample conv output) for a first block) and, with
+        ``next_conv`` (the next block's conv1, 1x1 / stride 1), that conv's output.  When the
+        narrow 1x1 kernel takes the product, ``out`` is formed inside its prologue
+        (``CN.bn_out_conv1x1``: one pass over c3 and the shortcut instead of a bn_apply pass and
+        the conv's read of its result); otherwise bn_apply then the conv.  Fills the block's
+        (c3, mean, rstd), downsample and output entries.  Returns (out, c1, c1 statistics)."""
+        i, c3, s3, dsc = pend
+        P = self.params
+        pre = blocks[i][0]
+        name = pre + "conv3"
+        res_bn = None
+        residual = blocks[i][1]
+        if dsc is not None:
+            residual, sds = dsc
+            rm, rv = P.running[pre + "downsample"]
+            nd = pre + "downsample.bn."
+            res_bn = (sds[0], sds[1], P.P(nd + "gamma"), P.P(nd + "beta"), rm, rv)
+        c1 = s1 = None
+        if next_conv is not None and CN.bn_prologue_applies(c3, c3.shape[-1],
+                                                            self.specs[next_conv][2]):
+            cout = self.specs[next_conv][2]
+            cs, cq, M = s3
+            ncs, ncq = self._stats[next_conv]
+            rm3, rv3 = P.running[name]
+            r = CN.bn_out_conv1x1(c3, cs, cq, M, P.P(name + ".bn.gamma"), P.P(name + ".bn.beta"),
+                                  residual, P.W(next_conv + ".weight"), ncs, ncq, self.eps, rm3,
+                                  rv3, res_bn=res_bn)
+            out, c1, stats = r[0], r[1], r[2:]
+            s1 = (ncs, ncq, c1.numel() // cout)
+        else:
+            r = self._bn_apply(name, c3, s3, residual=residual, relu=True, res_bn=res_bn)
+            out, stats = r[0], r[1:]
+            if next_conv is not None:
+                c1, s1 = self._conv_bn(next_conv, out)
+        blocks[i][4] = (c3, stats[0], stats[1])
+        blocks[i][5] = (residual, stats[2], stats[3]) if dsc is not None else None
+        blocks[i][6] = out
+        return out, c1, s1
 
     def _bn_bwd(self, name, dy, y, x, mean, rstd, relu=True, want_dres=False):
         P = self.params
@@ -279,18 +333,32 @@ class ResNet50:
         ``fuse_prev = (bn name, y, (c, mean, rstd))``: the BatchNorm that produced this block's
         input; its reductions are fused into this block's last dgrad (whose result is then
         that BN's output gradient)."""
+        P = self.params
+        n3 = pre + "conv3"
+        # conv3's data gradient (a narrow 1x1 product) forms dc3 = BN3-backward(de3) in its
+        # prologue when it can: one pass over de3 and c3 (dc3 written for the weight gradient)
+        pro = dout_is_de and CN.bn_prologue_applies(c3, c3.shape[-1], a2.shape[-1])
+        dc3 = None
         if dout_is_de:
             dres = dout
-            dc3 = self._bn_apply_bwd(pre + "conv3", dout, c3, m3, r3)
+            if not pro:
+                dc3 = self._bn_apply_bwd(n3, dout, c3, m3, r3)
         else:
-            dc3, dres = self._bn_bwd(pre + "conv3", dout, out, c3, m3, r3, relu=True, want_dres=True)
+            dc3, dres = self._bn_bwd(n3, dout, out, c3, m3, r3, relu=True, want_dres=True)
         if ds is not None:
             cs_, ms, rs = ds
             dcs, _ = self._bn_bwd(pre + "downsample", dres, None, cs_, ms, rs, relu=False)
             dshort = self._wgrad_dgrad(pre + "downsample", dcs, x_in)
         else:
             dshort = dres
-        de2 = self._wgrad_dgrad(pre + "conv3", dc3, a2, bn=self._bn_fused(pre + "conv2", a2, c2, m2, r2))
+        bn2 = self._bn_fused(pre + "conv2", a2, c2, m2, r2)
+        if pro:
+            de2, dc3 = CN.bn_in_conv1x1_dgrad(dout, c3, m3, r3, P.P(n3 + ".bn.gamma"),
+                                              P.G(n3 + ".bn.beta"), P.G(n3 + ".bn.gamma"),
+                                              P.W(n3 + ".weight"), bn2)
+            self._wgrad_dgrad(n3, dc3, a2, need_dx=False)
+        else:
+            de2 = self._wgrad_dgrad(n3, dc3, a2, bn=bn2)
         dc2 = self._bn_apply_bwd(pre + "conv2", de2, c2, m2, r2)
         de1 = self._wgrad_dgrad(pre + "conv2", dc2, a1, bn=self._bn_fused(pre + "conv1", a1, c1, m1, r1))
         dc1 = self._bn_apply_bwd(pre + "conv1", de1, c1, m1, r1)

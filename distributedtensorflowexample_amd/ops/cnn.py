@@ -250,6 +250,100 @@ def bn_bwd_apply(de, x, mean, rstd, gamma, sum_dy, sum_dyxh):
     return dx
 
 
+def bn_prologue_applies(x, K, N):
+    """True when a 1x1 / stride-1 product over ``x``'s pixels reducing K channels to N runs on
+    the narrow kernel with the BatchNorm prologue (:func:`bn_out_conv1x1`: K = the block
+    output's channels, N = the next conv's; :func:`bn_in_conv1x1_dgrad`: K = the conv's output
+    channels, N = its input channels).  ``DTFX_BN_PROLOGUE=0`` keeps the separate passes."""
+    if not (x.is_cuda and _CONV1X1 and _BN_PRO):
+        return False
+    return bool(hip().conv1x1_pro_applies(x.numel() // x.shape[-1], K, N))
+
+
+_BN_PRO = os.environ.get("DTFX_BN_PROLOGUE", "1") != "0"
+
+
+def bn_out_conv1x1(c, s, q, M, gamma, beta, residual, w, colsum, colsq, eps=1e-5, run_mean=None,
+                   run_var=None, momentum=0.9, res_bn=None):
+    """A bottleneck's output and the next 1x1 conv in one pass over the conv3 output.
+
+    ``out = relu(bn(c) + shortcut)`` (training-mode BatchNorm of ``c`` from its column sums
+    ``s`` / ``q`` over ``M`` rows; shortcut = ``residual``, or -- ``res_bn = (s2, q2, gamma2,
+    beta2, run_mean2, run_var2)`` -- ``residual`` normalised by its own BatchNorm), then
+    ``y = out W^T`` (1x1, stride 1) with y's BatchNorm statistics accumulated into
+    ``colsum`` / ``colsq``.  GPU: ``bn_fwd_coef`` + the narrow 1x1 kernel's prologue
+    (csrc/kernels/conv1x1.hip, PRO 1), which writes ``out`` as it forms the product's operand --
+    the separate ``bn_apply`` pass and the conv's read of its result become one pass.
+    Returns (out, y, mean, rstd) or, with ``res_bn``, (out, y, mean, rstd, mean2, rstd2)."""
+    if not c.is_cuda:
+        r = bn_apply_stats(c, s, q, M, gamma, beta, residual, True, eps, run_mean, run_var,
+                           momentum, res_bn=res_bn)
+        y = conv_fwd(r[0], w, 1, 1, 1, 0, colsum=colsum, colsq=colsq)
+        return (r[0], y) + tuple(r[1:])
+    K = c.shape[-1]
+    Nout = w.shape[0]
+    Mrows = c.numel() // K
+    dev = c.device
+    st = torch.empty(4 if res_bn is not None else 2, K, device=dev)
+    coef = torch.empty(4, K, device=dev)
+    s2 = q2 = g2 = b2 = rm2 = rv2 = None
+    if res_bn is not None:
+        s2, q2, g2, b2, rm2, rv2 = res_bn
+    hip().bn_fwd_coef(int(M), K, ptr(s), ptr(q), float(eps), ptr(st[0]), ptr(st[1]), ptr(run_mean),
+                      ptr(run_var), float(momentum), ptr(gamma), ptr(beta), ptr(s2), ptr(q2),
+                      ptr(g2), ptr(b2), ptr(st[2] if res_bn is not None else None),
+                      ptr(st[3] if res_bn is not None else None), ptr(rm2), ptr(rv2), ptr(coef),
+                      stream_handle())
+    out = torch.empty_like(c)
+    y = torch.empty(*c.shape[:-1], Nout, device=dev, dtype=BF16)
+    part = torch.empty(2, hip().conv1x1_rows(1, Mrows, K, Nout), Nout, device=dev)
+    hip().conv1x1_pro(1, Mrows, K, Nout, ptr(c), ptr(residual), ptr(coef), ptr(out), ptr(w),
+                      w.stride(0), ptr(y), 0, 0, 0, 0, ptr(part[0]), ptr(part[1]), 0,
+                      stream_handle())
+    hip().colpart_reduce(part.shape[1], Nout, ptr(part[0]), ptr(part[1]), ptr(colsum), ptr(colsq),
+                         stream_handle())
+    if res_bn is None:
+        return out, y, st[0], st[1]
+    return out, y, st[0], st[1], st[2], st[3]
+
+
+def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn, want_dc=True):
+    """BatchNorm backward's apply half and the data gradient of the 1x1 conv that produced the
+    BatchNorm's input, in one pass.
+
+    ``de`` = dL/d(BN output) with the final reductions ``sum_dy`` / ``sum_dyxh`` (see
+    :func:`conv_dgrad`'s ``bn``), ``c`` = the BN input (this conv's output): the conv's output
+    gradient ``dc = bn_bwd_apply(de, c, ...)`` is formed inside the narrow dgrad kernel's
+    prologue (PRO 2) and written out when ``want_dc`` (the weight gradient reads it); the
+    product is ``conv_dgrad(dc, w, bn=bn)`` with the fused BatchNorm backward of the conv's
+    own input (``bn = (y, x, mean, rstd, sum_dy, sum_dyxh)``, required).  Returns (dx, dc)."""
+    if not de.is_cuda:
+        dc = bn_bwd_apply(de, c, mean, rstd, gamma, sum_dy, sum_dyxh)
+        N, H, W, _ = c.shape
+        dx = conv_dgrad(dc, w, (N, H, W, w.shape[1]), 1, 1, 1, 0, bn=bn)
+        return dx, dc
+    K = c.shape[-1]          # the conv's output channels (the BN's)
+    Cin = w.shape[1]
+    M = c.numel() // K
+    y, x, bmean, brstd, sdy, sdx = bn
+    dev = c.device
+    coef = torch.empty(4, K, device=dev)
+    hip().bn_bwd_coef(M, K, ptr(mean), ptr(rstd), ptr(gamma), ptr(sum_dy), ptr(sum_dyxh),
+                      ptr(coef), stream_handle())
+    dc = torch.empty_like(c) if want_dc else None
+    dx = torch.empty(*c.shape[:-1], Cin, device=dev, dtype=BF16)
+    if y.shape != dx.shape or x.shape != dx.shape:
+        raise ValueError("fused BN backward: y and x must have the dgrad output's shape")
+    wt = torch.empty(Cin, K, device=dev, dtype=BF16)
+    part = torch.empty(2, hip().conv1x1_rows(2, M, K, Cin), Cin, device=dev)
+    hip().conv1x1_pro(2, M, K, Cin, ptr(de), ptr(c), ptr(coef), ptr(dc), ptr(w), w.stride(0),
+                      ptr(dx), ptr(y), ptr(x), ptr(bmean), ptr(brstd), ptr(part[0]), ptr(part[1]),
+                      ptr(wt), stream_handle())
+    hip().colpart_reduce(part.shape[1], Cin, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
+                         stream_handle())
+    return dx, dc
+
+
 def conv_wgrad(dy, x, dw, KH, KW, stride, pad, beta=1.0):
     """dw[:, :KH*KW*C] (f32 [Cout, ldw]) (+)= dL/dW."""
     N, H, W, C = x.shape
@@ -399,6 +493,51 @@ def maxpool_fwd(x):
     idx = torch.empty(N, OH, OW, C, device=x.device, dtype=torch.uint8)
     hip().maxpool_fwd(N, H, W, C, ptr(x), ptr(y), ptr(idx), stream_handle())
     return y, idx
+
+
+def bn_maxpool_fwd(c, s, q, M, gamma, beta, eps=1e-5, run_mean=None, run_var=None,
+                   momentum=0.9):
+    """The ResNet stem's ``maxpool(relu(bn(c)))`` (training-mode BatchNorm from c's column sums
+    ``s`` / ``q`` over ``M`` rows) without materialising ``relu(bn(c))``.
+    Returns (y, idx, mean, rstd, fcoef); ``fcoef`` (GPU: the [4][C] BatchNorm coefficients,
+    CPU: None) goes to :func:`maxpool_bn_bwd`."""
+    if not c.is_cuda:
+        a, mean, rstd = bn_apply_stats(c, s, q, M, gamma, beta, None, True, eps, run_mean, run_var,
+                                       momentum)
+        y, idx = maxpool_fwd(a)
+        return y, idx, mean, rstd, None
+    N, H, W, C = c.shape
+    OH, OW = out_hw(H, W, 3, 2, 1)
+    st = torch.empty(2, C, device=c.device)
+    fcoef = torch.empty(4, C, device=c.device)
+    hip().bn_fwd_coef(int(M), C, ptr(s), ptr(q), float(eps), ptr(st[0]), ptr(st[1]), ptr(run_mean),
+                      ptr(run_var), float(momentum), ptr(gamma), ptr(beta), 0, 0, 0, 0, 0, 0, 0, 0,
+                      ptr(fcoef), stream_handle())
+    y = torch.empty(N, OH, OW, C, device=c.device, dtype=BF16)
+    idx = torch.empty(N, OH, OW, C, device=c.device, dtype=torch.uint8)
+    hip().maxpool_bn_fwd(N, H, W, C, ptr(c), ptr(fcoef), ptr(y), ptr(idx), stream_handle())
+    return y, idx, st[0], st[1], fcoef
+
+
+def maxpool_bn_bwd(dy, idx, c, mean, rstd, gamma, beta, fcoef, dgamma, dbeta):
+    """Backward of :func:`bn_maxpool_fwd`: dL/dc from the pool's output gradient ``dy``;
+    dgamma / dbeta are the (per-step zeroed) gradient slots, which receive BatchNorm backward's
+    two sums.  GPU: two passes that each re-gather the pool gradient per input pixel (sums,
+    then the apply) -- the dense pool gradient and ``relu(bn(c))`` are never read or written."""
+    if not c.is_cuda:
+        a = bn_apply(c, mean, rstd, gamma, beta, None, relu=True)
+        da = maxpool_bwd(dy, idx, c.shape)
+        dc, _ = bn_bwd(da, a, c, mean, rstd, gamma, dgamma, dbeta, relu=True, grads_zeroed=True)
+        return dc
+    N, H, W, C = c.shape
+    rows = hip().maxpool_bn_bwd_rows(N, H, W, C)
+    scratch = torch.empty(2 * rows * C, device=c.device)
+    bcoef = torch.empty(4, C, device=c.device)
+    dc = torch.empty_like(c)
+    hip().maxpool_bn_bwd(N, H, W, C, ptr(dy), ptr(idx), ptr(c), ptr(fcoef), ptr(mean), ptr(rstd),
+                         ptr(gamma), ptr(dbeta), ptr(dgamma), ptr(scratch), ptr(bcoef), ptr(dc),
+                         stream_handle())
+    return dc
 
 
 def maxpool_bwd(dy, idx, x_shape):

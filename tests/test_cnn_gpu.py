@@ -231,3 +231,129 @@ def test_conv1x1_dgrad_residual_only(gpu, N, H, W, C, Co):
     dx = cnn.conv_dgrad(dy.to(gpu), w.to(gpu), (N, H, W, C), 1, 1, 1, 0, residual=res.to(gpu))
     dxr = cnn.conv_dgrad(dy, w, (N, H, W, C), 1, 1, 1, 0, residual=res)
     assert (dx.cpu().float() - dxr.float()).abs().max() < 3e-2 * dxr.float().abs().max()
+
+
+@pytest.mark.parametrize("N,H,W,K,Co,ds", [
+    (2, 16, 16, 256, 64, False),   # layer1 block output -> next conv1 (256 -> 64)
+    (2, 16, 16, 256, 64, True),    # first block: shortcut through the downsample BN
+    (4, 8, 8, 256, 128, True),     # layer1 -> layer2.0 conv1 (256 -> 128)
+    (4, 8, 8, 512, 128, False),    # layer2 block output -> next conv1 (512 -> 128), 16-pixel tiles
+    (3, 16, 20, 512, 128, True),   # M = 960: tiles spread unevenly over the 256 blocks
+])
+def test_bn_out_conv1x1_prologue(gpu, N, H, W, K, Co, ds):
+    """The bottleneck output relu(bn3(c3) + shortcut) formed inside the next 1x1 conv's prologue
+    (conv1x1.hip PRO 1) == bn_apply_stats then conv_fwd (f32 CPU path): the block output, the
+    conv output, its statistics, mean / rstd and the running statistics."""
+    M = N * H * W
+    c = _r(N, H, W, K, seed=31, scale=2).to(BF) + 0.5
+    r = _r(N, H, W, K, seed=32, scale=1.5).to(BF) - 0.25
+    g1, b1 = _r(K, seed=33) * 0.1 + 1, _r(K, seed=34) * 0.1
+    g2, b2 = _r(K, seed=35) * 0.1 + 1, _r(K, seed=36) * 0.1
+    cf, rf = c.float().reshape(M, K), r.float().reshape(M, K)
+    s, q, s2, q2 = cf.sum(0), (cf * cf).sum(0), rf.sum(0), (rf * rf).sum(0)
+    w = _r(Co, K, seed=37, scale=K ** -0.5).to(BF)
+
+    def run(dev):
+        t = lambda v: v.to(dev)  # noqa: E731
+        cs, cq = torch.zeros(Co, device=dev), torch.zeros(Co, device=dev)
+        run_st = [torch.zeros(K, device=dev), torch.ones(K, device=dev),
+                  torch.zeros(K, device=dev), torch.ones(K, device=dev)]
+        res_bn = (t(s2), t(q2), t(g2), t(b2), run_st[2], run_st[3]) if ds else None
+        out = cnn.bn_out_conv1x1(t(c), t(s), t(q), M, t(g1), t(b1), t(r), t(w), cs, cq, 1e-5,
+                                 run_st[0], run_st[1], res_bn=res_bn)
+        return [v.cpu() for v in out] + [cs.cpu(), cq.cpu()] + [v.cpu() for v in run_st]
+
+    got, ref = run(gpu), run("cpu")
+    assert len(got) == len(ref) == (12 if ds else 10)
+    o, orf = got[0].float(), ref[0].float()
+    # (the CPU reference rounds the normalised shortcut to bf16 before the add)
+    assert (o - orf).abs().max() < 2e-2 * orf.abs().max() + 1e-2
+    assert ((o == 0) == (orf == 0)).float().mean() > 0.995          # ReLU
+    y, yr = got[1].float(), ref[1].float()
+    assert (y - yr).abs().max() < 3e-2 * yr.abs().max()
+    for a, b in zip(got[2:], ref[2:]):  # mean / rstd (x2), column sums, running statistics
+        assert torch.allclose(a, b, rtol=2e-2, atol=1e-2 * float(b.abs().max()) + 1e-4)
+    # the GPU prologue against the GPU's own two-pass path: the same block output
+    rb = (s2.to(gpu), q2.to(gpu), g2.to(gpu), b2.to(gpu), None, None) if ds else None
+    two = cnn.bn_apply_stats(c.to(gpu), s.to(gpu), q.to(gpu), M, g1.to(gpu), b1.to(gpu),
+                             r.to(gpu), True, 1e-5, res_bn=rb)
+    d = (two[0].cpu().float() - o).abs()
+    assert (d <= 2 ** -7 * o.abs() + 1e-6).all()  # at most one bf16 rounding apart
+
+
+@pytest.mark.parametrize("N,H,W,Cin,K", [
+    (2, 16, 16, 64, 256),    # layer1 conv3 data gradient (256 -> 64)
+    (4, 8, 8, 128, 512),     # layer2 conv3 (512 -> 128, 16-pixel tiles)
+    (3, 16, 20, 64, 256),    # M = 960
+])
+def test_bn_in_conv1x1_dgrad_prologue(gpu, N, H, W, Cin, K):
+    """BN3-backward's apply half formed inside conv3's narrow dgrad prologue (conv1x1.hip PRO 2)
+    == bn_bwd_apply then the dgrad with conv2's fused BN reductions (f32 CPU path): dL/dc3
+    (written for the weight gradient), de2 and conv2's BN sums."""
+    M = N * H * W
+    c3 = _r(N, H, W, K, seed=41, scale=2).to(BF) + 0.5
+    c3f = c3.float().reshape(M, K)
+    m3, r3 = cnn.bn_finalize(c3f.sum(0), (c3f * c3f).sum(0), M)
+    g3 = _r(K, seed=42) * 0.1 + 1
+    de3 = _r(N, H, W, K, seed=43).to(BF)
+    d3 = de3.float().reshape(M, K)
+    sdy3, sdx3 = d3.sum(0), (d3 * (c3f - m3) * r3).sum(0)
+    c2 = _r(N, H, W, Cin, seed=44, scale=2).to(BF) + 0.5
+    c2f = c2.float().reshape(M, Cin)
+    m2, r2 = cnn.bn_finalize(c2f.sum(0), (c2f * c2f).sum(0), M)
+    g2, b2 = _r(Cin, seed=45) * 0.1 + 1, _r(Cin, seed=46) * 0.1
+    y2 = cnn.bn_apply(c2, m2, r2, g2, b2, None, relu=True)
+    w3 = _r(K, Cin, seed=47, scale=Cin ** -0.5).to(BF)
+
+    def run(dev):
+        t = lambda v: v.to(dev)  # noqa: E731
+        sdy2, sdx2 = torch.zeros(Cin, device=dev), torch.zeros(Cin, device=dev)
+        dx, dc = cnn.bn_in_conv1x1_dgrad(t(de3), t(c3), t(m3), t(r3), t(g3), t(sdy3), t(sdx3),
+                                         t(w3), (t(y2), t(c2), t(m2), t(r2), sdy2, sdx2))
+        return dx.cpu().float(), dc.cpu().float(), sdy2.cpu(), sdx2.cpu()
+
+    (dx, dc, a, b), (dxr, dcr, ar, br) = run(gpu), run("cpu")
+    assert (dc - dcr).abs().max() < 2e-2 * dcr.abs().max()
+    assert (dx - dxr).abs().max() < 3e-2 * dxr.abs().max()
+    assert ((dx == 0) == (dxr == 0)).float().mean() > 0.995    # conv2's ReLU mask
+    assert torch.allclose(a, ar, atol=0.05 * float(ar.abs().max()) + 1e-2, rtol=2e-2)
+    assert torch.allclose(b, br, atol=0.05 * float(br.abs().max()) + 1e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 16, 16), (3, 15, 17)])   # odd sizes: clipped windows
+def test_stem_bn_maxpool_fused(gpu, N, H, W):
+    """The stem's maxpool(relu(bn(c))) with relu(bn(c)) never stored (maxpool_bn_fwd_kernel) and
+    its two-pass backward (re-gathered pool gradient: BatchNorm sums, then the apply) == the
+    separate bn_apply_stats / maxpool / maxpool_bwd / bn_bwd passes (f32 CPU path)."""
+    C = 64
+    M = N * H * W
+    c = _r(N, H, W, C, seed=51, scale=2).to(BF) + 0.25
+    cf = c.float().reshape(M, C)
+    s, q = cf.sum(0), (cf * cf).sum(0)
+    g, b = _r(C, seed=52) * 0.1 + 1, _r(C, seed=53) * 0.1
+
+    def run(dev, idx_bwd=None):
+        t = lambda v: v.to(dev)  # noqa: E731
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        y, idx, m, r, fco = cnn.bn_maxpool_fwd(t(c), t(s), t(q), M, t(g), t(b), 1e-5, rm, rv)
+        if idx_bwd is not None:  # the backward of both paths routes through the same taps
+            idx = t(idx_bwd)
+        dy = _r(*y.shape, seed=54).to(BF).to(dev)
+        dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        dc = cnn.maxpool_bn_bwd(dy, idx, t(c), m, r, t(g), t(b), fco, dg, db)
+        return [v.cpu() for v in (y, idx, m, r, rm, rv, dc, dg, db)]
+
+    (y, idx, m, r, rm, rv, dc, dg, db) = run(gpu)
+    (yr, idxr, mr, rr, rmr, rvr, dcr, dgr, dbr) = run("cpu", idx)
+    # (same bf16 activations inside every window: identical maxima and argmax taps, bar ties
+    # created by one-ulp differences in the normalisation)
+    assert (y.float() - yr.float()).abs().max() < 1e-2 * yr.float().abs().max() + 1e-2
+    yr2, idxr2 = cnn.maxpool_fwd(cnn.bn_apply(c, mr, rr, g, b, None, relu=True))
+    assert (idx == idxr2).float().mean() > 0.99
+    for a_, b_ in ((m, mr), (rm, rmr)):
+        assert torch.allclose(a_, b_, atol=1e-5)
+    for a_, b_ in ((r, rr), (rv, rvr)):
+        assert torch.allclose(a_, b_, rtol=1e-4)
+    assert (dc.float() - dcr.float()).abs().max() < 4e-2 * dcr.float().abs().max()
+    assert torch.allclose(db, dbr, atol=0.05 * float(dbr.abs().max()) + 1e-2, rtol=2e-2)
+    assert torch.allclose(dg, dgr, atol=0.05 * float(dgr.abs().max()) + 1e-2, rtol=2e-2)
