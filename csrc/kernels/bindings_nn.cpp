@@ -52,10 +52,10 @@ int conv1x1_rows(int, int, int, int);
 void conv1x1_launch(int, int, int, int, const void*, const void*, int, void*, const void*,
                     const void*, const void*, const float*, const float*, float*, float*, void*,
                     hipStream_t);
-bool conv1x1_pro_applies(int, int, int);
+bool conv1x1_pro_applies(int, int, int, int);
 void conv1x1_pro_launch(int, int, int, int, const void*, const void*, const float*, void*,
-                        const void*, int, void*, const void*, const void*, const float*,
-                        const float*, float*, float*, void*, hipStream_t);
+                        const void*, int, void*, const void*, const void*, const void*,
+                        const float*, const float*, float*, float*, void*, hipStream_t);
 void bn_fwd_coef_launch(long long, int, const float*, const float*, float, float*, float*, float*,
                         float*, float, const float*, const float*, const float*, const float*,
                         const float*, const float*, float*, float*, float*, float*, float*,
@@ -70,7 +70,7 @@ void maxpool_bn_fwd_launch(int, int, int, int, const void*, const float*, void*,
 int maxpool_bn_bwd_rows(int, int, int, int);
 void maxpool_bn_bwd_launch(int, int, int, int, const void*, const void*, const void*, const float*,
                            const float*, const float*, const float*, float*, float*, float*,
-                           float*, void*, hipStream_t);
+                           void*, void*, hipStream_t);
 void maxpool_bwd_launch(int, int, int, int, const void*, const void*, void*, hipStream_t);
 void avgpool_fwd_launch(int, int, int, const void*, void*, hipStream_t);
 void avgpool_bwd_launch(int, int, int, const void*, void*, hipStream_t);
@@ -302,15 +302,16 @@ void register_nn(py::module_& m) {
                          P<void>(wt), S(s));
   });
   m.def("conv1x1_pro_applies", &dtfx::conv1x1_pro_applies,
-        "(M, K, N): the narrow 1x1 kernel with the BatchNorm prologue takes this product");
+        "(mode, M, K, N): a 1x1 kernel with the BatchNorm prologue takes this product");
   m.def("conv1x1_pro", [](int mode, int M, int K, int N, uintptr_t s0, uintptr_t s1, uintptr_t coef,
-                          uintptr_t xo, uintptr_t w, int ldw, uintptr_t y, uintptr_t relu_y,
-                          uintptr_t bn_x, uintptr_t mean, uintptr_t rstd, uintptr_t ps, uintptr_t pq,
-                          uintptr_t wt, uintptr_t s) {
+                          uintptr_t xo, uintptr_t w, int ldw, uintptr_t y, uintptr_t res,
+                          uintptr_t relu_y, uintptr_t bn_x, uintptr_t mean, uintptr_t rstd,
+                          uintptr_t ps, uintptr_t pq, uintptr_t wt, uintptr_t s) {
     dtfx::conv1x1_pro_launch(mode, M, K, N, P<const void>(s0), P<const void>(s1),
                              P<const float>(coef), P<void>(xo), P<const void>(w), ldw, P<void>(y),
-                             P<const void>(relu_y), P<const void>(bn_x), P<const float>(mean),
-                             P<const float>(rstd), P<float>(ps), P<float>(pq), P<void>(wt), S(s));
+                             P<const void>(res), P<const void>(relu_y), P<const void>(bn_x),
+                             P<const float>(mean), P<const float>(rstd), P<float>(ps), P<float>(pq),
+                             P<void>(wt), S(s));
   });
   m.def("bn_fwd_coef", [](long long M, int C, uintptr_t sum, uintptr_t sq, float eps, uintptr_t mean,
                           uintptr_t rstd, uintptr_t run_mean, uintptr_t run_var, float momentum,
@@ -337,12 +338,12 @@ void register_nn(py::module_& m) {
   m.def("maxpool_bn_bwd_rows", &dtfx::maxpool_bn_bwd_rows);
   m.def("maxpool_bn_bwd", [](int N, int H, int W, int C, uintptr_t dy, uintptr_t idx, uintptr_t x,
                              uintptr_t fcoef, uintptr_t mean, uintptr_t rstd, uintptr_t g,
-                             uintptr_t sdy, uintptr_t sdyxh, uintptr_t scratch, uintptr_t bcoef,
+                             uintptr_t sdy, uintptr_t sdyxh, uintptr_t scratch, uintptr_t de,
                              uintptr_t dx, uintptr_t s) {
     dtfx::maxpool_bn_bwd_launch(N, H, W, C, P<const void>(dy), P<const void>(idx), P<const void>(x),
                                 P<const float>(fcoef), P<const float>(mean), P<const float>(rstd),
                                 P<const float>(g), P<float>(sdy), P<float>(sdyxh),
-                                P<float>(scratch), P<float>(bcoef), P<void>(dx), S(s));
+                                P<float>(scratch), P<void>(de), P<void>(dx), S(s));
   });
   m.def("conv3x3_c128_applies", &dtfx::conv3x3_c128_applies,
         "the 128-channel 3x3 kernel handles this conv (stride 1, pad 1, H % 4, W % 28)");

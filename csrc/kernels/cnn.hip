@@ -551,11 +551,13 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int N, int H, int W, i
 // ---- the ResNet stem's BatchNorm fused into its max pool ----------------------------------
 // The stem output a = relu(bn(c)) (N x 112 x 112 x 64, 205 M elements at batch 256) is only
 // read by the pool, so it is never written: the forward pools relu(c * A + B) formed per tap
-// (bf16-rounded exactly as bn_apply_kernel stores it: the same maxima and argmax taps), and the
-// backward re-gathers the pool gradient per input pixel twice -- once for BatchNorm backward's
-// two reductions (ReLU mask recomputed from c with the forward's own arithmetic), once for the
-// apply -- instead of writing da and reading da, a and c in two more passes
-// (bn_bwd_reduce + bn_bwd_apply).  fcoef / bcoef: bn_fwd_coef / bn_bwd_coef rows [4][C].
+// (bf16-rounded exactly as bn_apply_kernel stores it: the same maxima and argmax taps).  The
+// backward gathers the pool gradient per input pixel, masks it with the ReLU recomputed from c
+// (the forward's own arithmetic), reduces BatchNorm backward's two sums and writes de in ONE
+// pass; the apply is the streaming bn_bwd_apply over de and c.  (Before: maxpool_bwd writing
+// da, then bn_bwd reading da, a and c twice.  A version that re-gathered the pool gradient in
+// the apply pass instead of writing de ran 610 us against ~500 for the separate passes: the
+// gather runs well below streaming rate.)  fcoef: bn_fwd_coef rows [4][C].
 __device__ __forceinline__ float bn_relu_bf(float v, float a, float b) {
   return bf(tobf(fmaxf(v * a + b, 0.f)));
 }
@@ -660,13 +662,14 @@ __device__ __forceinline__ void maxpool_grad8(int n, int ih, int iw, int g, int 
   for (int u = 0; u < 8; ++u) out[u] = bf(tobf(out[u]));
 }
 
-// Pass 1: per block, sums of de = da * (bn(c) > 0) and de * xhat over its rows; one partial row
-// per block (blockIdx.y * gridDim.x + blockIdx.x), the threads of a channel group meet in LDS.
+// de = da * (bn(c) > 0) written, and per block the sums of de and de * xhat over its rows: one
+// partial row per block (blockIdx.y * gridDim.x + blockIdx.x), the threads of a channel group
+// meet in LDS.
 __global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_kernel(
     int N, int H, int W, int C, int OH, int OW, const unsigned short* __restrict__ dy,
     const unsigned char* __restrict__ idx, const unsigned short* __restrict__ x,
     const float* __restrict__ fcoef, const float* __restrict__ mean, const float* __restrict__ rstd,
-    float* __restrict__ part_dy, float* __restrict__ part_dyxh) {
+    float* __restrict__ part_dy, float* __restrict__ part_dyxh, unsigned short* __restrict__ de_out) {
   __shared__ float red[256][17];
   const int cg = C >> 3;
   const int j = blockIdx.x * 256 + threadIdx.x;
@@ -684,16 +687,19 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_kernel(
   if (live) {
     for (int row = blockIdx.y; row < N * H; row += gridDim.y) {
       const int n = row / H, ih = row - n * H;
-      const bf16x8 xv = ((const bf16x8*)x)[((size_t)row * W + iw) * cg + g];
+      const size_t o = ((size_t)row * W + iw) * cg + g;
+      const bf16x8 xv = ((const bf16x8*)x)[o];
       float da[8], xf[8];
       maxpool_grad8(n, ih, iw, g, cg, OH, OW, dy, idx, da);
       unpack8(xv, xf);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const float de = xf[u] * sa[u] + sb[u] > 0.f ? da[u] : 0.f;
+        da[u] = de;
         s1[u] += de;
         s2[u] += de * (xf[u] - mu[u]) * rs[u];
       }
+      ((bf16x8*)de_out)[o] = pack8(da);
     }
   }
 #pragma unroll
@@ -714,41 +720,6 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_kernel(
     }
     part_dy[prow + c] = a;
     part_dyxh[prow + c] = b;
-  }
-}
-
-// Pass 2: dc = A de + K1 c + K0 (bn_bwd_apply_kernel's affine form) from the re-gathered pool
-// gradient and the recomputed mask.
-__global__ __launch_bounds__(256) void maxpool_bn_bwd_apply_kernel(
-    int N, int H, int W, int C, int OH, int OW, const unsigned short* __restrict__ dy,
-    const unsigned char* __restrict__ idx, const unsigned short* __restrict__ x,
-    const float* __restrict__ fcoef, const float* __restrict__ bcoef, unsigned short* __restrict__ dx) {
-  const int cg = C >> 3;
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= W * cg) return;
-  const int iw = j / cg, g = j - iw * cg;
-  float sa[8], sb[8], ka[8], k1[8], k0[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    sa[u] = fcoef[g * 8 + u];
-    sb[u] = fcoef[2 * C + g * 8 + u];
-    ka[u] = bcoef[g * 8 + u];
-    k1[u] = bcoef[C + g * 8 + u];
-    k0[u] = bcoef[3 * C + g * 8 + u];
-  }
-  for (int row = blockIdx.y; row < N * H; row += gridDim.y) {
-    const int n = row / H, ih = row - n * H;
-    const size_t o = ((size_t)row * W + iw) * cg + g;
-    const bf16x8 xv = ((const bf16x8*)x)[o];
-    float da[8], xf[8], r[8];
-    maxpool_grad8(n, ih, iw, g, cg, OH, OW, dy, idx, da);
-    unpack8(xv, xf);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float de = xf[u] * sa[u] + sb[u] > 0.f ? da[u] : 0.f;
-      r[u] = ka[u] * de + k1[u] * xf[u] + k0[u];
-    }
-    ((bf16x8*)dx)[o] = pack8(r);
   }
 }
 
@@ -977,30 +948,31 @@ void maxpool_bn_fwd_launch(int N, int H, int W, int C, const void* x, const floa
                      (unsigned char*)idx);
   DTFX_HIP_CHECK(hipGetLastError());
 }
-// Partial-row count of maxpool_bn_bwd's reduce pass ([rows][C] each of part_dy / part_dyxh).
+// Partial-row count of maxpool_bn_bwd's reduce pass ([rows][C] each of part_dy / part_dyxh):
+// ~7 input rows per thread at ResNet-50's 256 x 112 rows -- one row per block would write
+// 115 k partial rows, 112 rows per thread left the pass latency-bound (242 us).
+static int maxpool_bn_bwd_gy(int N, int H) { return std::min(N * H, 4096); }
 int maxpool_bn_bwd_rows(int N, int H, int W, int C) {
-  return ((W * (C / 8) + 255) / 256) * std::min(N * H, 256);
+  return ((W * (C / 8) + 255) / 256) * maxpool_bn_bwd_gy(N, H);
 }
-// Backward: BatchNorm backward's reductions (ACCUMULATED into sum_dy / sum_dyxh -- the zeroed
-// dbeta / dgamma slots) and its apply, each over the re-gathered pool gradient; dx = dL/dc.
+// Backward: de (the masked pool gradient, written to `de`) with BatchNorm backward's sums
+// ACCUMULATED into sum_dy / sum_dyxh (the zeroed dbeta / dgamma slots), then the apply
+// dx = dL/dc over de and c (bn_bwd_apply_kernel).
 void maxpool_bn_bwd_launch(int N, int H, int W, int C, const void* dy, const void* idx,
                            const void* x, const float* fcoef, const float* mean, const float* rstd,
                            const float* gamma, float* sum_dy, float* sum_dyxh, float* scratch,
-                           float* bcoef, void* dx, hipStream_t st) {
+                           void* de, void* dx, hipStream_t st) {
   if (C % 8 || 256 % (C / 8)) throw std::runtime_error("maxpool_bn: C % 8 != 0, 256 % (C / 8) == 0");
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  const int gx = (W * (C / 8) + 255) / 256, gy = std::min(N * H, 256);
+  const int gx = (W * (C / 8) + 255) / 256, gy = maxpool_bn_bwd_gy(N, H);
   const int R = gx * gy;
   hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, N, H, W, C, OH, OW,
                      (const unsigned short*)dy, (const unsigned char*)idx,
-                     (const unsigned short*)x, fcoef, mean, rstd, scratch, scratch + (size_t)R * C);
+                     (const unsigned short*)x, fcoef, mean, rstd, scratch, scratch + (size_t)R * C,
+                     (unsigned short*)de);
   DTFX_HIP_CHECK(hipGetLastError());
   colpart_reduce_launch(R, C, scratch, scratch + (size_t)R * C, sum_dy, sum_dyxh, st);
-  bn_bwd_coef_launch((long long)N * H * W, C, mean, rstd, gamma, sum_dy, sum_dyxh, bcoef, st);
-  hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel, dim3(gx, std::min(N * H, 65535)), dim3(256), 0, st,
-                     N, H, W, C, OH, OW, (const unsigned short*)dy, (const unsigned char*)idx,
-                     (const unsigned short*)x, fcoef, (const float*)bcoef, (unsigned short*)dx);
-  DTFX_HIP_CHECK(hipGetLastError());
+  bn_bwd_apply_launch((long long)N * H * W, C, de, x, mean, rstd, gamma, sum_dy, sum_dyxh, dx, st);
 }
 
 void avgpool_fwd_launch(int N, int HW, int C, const void* x, void* y, hipStream_t st) {

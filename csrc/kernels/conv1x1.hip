@@ -64,10 +64,14 @@ __device__ __forceinline__ int xswz(int r) {
   return K == 64 ? (r >> 1) & 7 : r & 15;
 }
 
-template <int K>
+// PRO 3: the x tile is formed as relu(x a + c) in LDS before the MFMAs (the BatchNorm + ReLU
+// of the conv that produced x, coef rows 0 and 2 of bn_fwd_coef) and written to xo by the
+// first column block: the BN's output is written once and never read back for this product.
+template <int K, int PRO = 0>
 __global__ __launch_bounds__(576, fbpc<K>() == 2 ? 5 : 3) void conv1x1_fwd_kernel(
     int M, int N, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
-    int ldw, unsigned short* __restrict__ y, float* __restrict__ ps, float* __restrict__ pq) {
+    int ldw, unsigned short* __restrict__ y, float* __restrict__ ps, float* __restrict__ pq,
+    const float* __restrict__ coef, unsigned short* __restrict__ xo) {
   constexpr int FTM = ftm<K>(), KK = K / 32, MT = FTM / 16, CPR = K / 8;  // chunks per row
   constexpr int TB = FTM * K * 2, NQ = TB / 1024;  // tile bytes, DMA rounds per tile
   extern __shared__ __attribute__((aligned(16))) char sm[];
@@ -99,6 +103,7 @@ __global__ __launch_bounds__(576, fbpc<K>() == 2 ? 5 : 3) void conv1x1_fwd_kerne
     }
     __syncthreads();
     for (int it = 0; it < nmy; ++it) {
+      if constexpr (PRO != 0) asm volatile("s_barrier" ::: "memory");  // (the transform's barrier)
       if (it + 2 < nmy) {
         issue(it + 2);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ) : "memory");  // tile it + 1 landed
@@ -122,10 +127,39 @@ __global__ __launch_bounds__(576, fbpc<K>() == 2 ? 5 : 3) void conv1x1_fwd_kerne
   for (int j = 0; j < NTW; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+  // PRO: thread tid transforms chunk column tcc of rows tr0 + j * RPP; the coefficient rows
+  // a / c sit in LDS after the output staging (in registers they pushed the two-blocks-per-CU
+  // variants past 96 VGPRs into scratch)
+  constexpr int RPP = 512 / CPR, NPASS = FTM / RPP;
+  const int tcc = tid % CPR, tr0 = tid / CPR;
+  float* ctab = (float*)(stg + FTM * OPITCH);  // [2][K]
+  if constexpr (PRO != 0) {
+    for (int i = tid; i < K; i += NW * 64) {
+      ctab[i] = coef[i];
+      ctab[K + i] = coef[2 * K + i];
+    }
+  }
   __syncthreads();  // tile 0 in LDS
   for (int it = 0; it < nmy; ++it) {
-    const char* xs = sm + (it % NBUF) * TB;
+    char* xs = sm + (it % NBUF) * TB;
     const int p0 = (pb + it * PB) * FTM;
+    if constexpr (PRO != 0) {
+#pragma unroll
+      for (int j = 0; j < NPASS; ++j) {
+        const int r = tr0 + j * RPP, off = r * (K * 2) + ((tcc ^ xswz<K>(r)) << 4);
+        const bf16x8 a8 = *(const bf16x8*)(xs + off);
+        const f32x4 a0 = *(const f32x4*)(ctab + tcc * 8), a1 = *(const f32x4*)(ctab + tcc * 8 + 4);
+        const f32x4 c0_ = *(const f32x4*)(ctab + K + tcc * 8), c1_ = *(const f32x4*)(ctab + K + tcc * 8 + 4);
+        const float ca[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        const float cc[8] = {c0_[0], c0_[1], c0_[2], c0_[3], c1_[0], c1_[1], c1_[2], c1_[3]};
+        bf16x8 o8;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o8[u] = (short)tobf(fmaxf(bf(a8[u]) * ca[u] + cc[u], 0.f));
+        *(bf16x8*)(xs + off) = o8;
+        if (xo && cb == 0) *(bf16x8*)(xo + (size_t)(p0 + r) * K + tcc * 8) = o8;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
 #pragma unroll K == 64 ? MT : 1
     for (int i = 0; i < MT; ++i) {
       bf16x8 xf[KK];
@@ -195,26 +229,32 @@ __global__ __launch_bounds__(576, fbpc<K>() == 2 ? 5 : 3) void conv1x1_fwd_kerne
 // are summed over the block's pixels in registers and reduced across waves once at the end.
 constexpr int DTM = 16;
 constexpr int SPITCH = NC * 4 + 16;  // f32 staging row (bytes), 16-B skew per pixel
-template <int K, bool RES, bool BN>
+template <int K, bool RES, bool BN, int PRO = 0>
 constexpr int dgrad_ring() {
-  constexpr int nqt = DTM * K * 2 / 1024 + ((RES ? 1 : 0) + (BN ? 2 : 0)) * (DTM * NC * 2 / 1024);
+  constexpr int nqt = DTM * K * 2 * (PRO ? 2 : 1) / 1024 +
+                      ((RES ? 1 : 0) + (BN ? 2 : 0)) * (DTM * NC * 2 / 1024);
   return 2 * nqt <= 63 ? 4 : 3;
 }
 
 // w here is the transposed weight copy wt [N][K] (transpose_bf16_kernel).
-template <int K, bool RES, bool BN>
+// PRO 2: dy is formed per tile as s0 a + (s1 b + d) from dy and src1 (BatchNorm backward's
+// apply of the BN behind this conv, as in conv1x1_narrow_kernel; bn_bwd_coef's c row is zero)
+// and written to xo by the first column block.
+template <int K, bool RES, bool BN, int PRO = 0>
 __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
     int M, int N, const unsigned short* __restrict__ dy, const unsigned short* __restrict__ w,
     int ldw, unsigned short* __restrict__ dx, const unsigned short* __restrict__ res,
     const unsigned short* __restrict__ relu_y, const unsigned short* __restrict__ bn_x,
     const float* __restrict__ bn_mean, const float* __restrict__ bn_rstd, float* __restrict__ ps,
-    float* __restrict__ pq) {
+    float* __restrict__ pq, const unsigned short* __restrict__ src1 = nullptr,
+    const float* __restrict__ coef = nullptr, unsigned short* __restrict__ xo = nullptr) {
   constexpr int KK = K / 32, CPR = K / 8;
   constexpr int DYB = DTM * K * 2, SB = DTM * NC * 2, NSIDE = (RES ? 1 : 0) + (BN ? 2 : 0);
-  constexpr int STAGE = DYB + NSIDE * SB, NQD = DYB / 1024, NQS = SB / 1024;
-  constexpr int NQT = NQD + NSIDE * NQS;  // DMA instructions per tile (<= 32)
+  constexpr int DYS = DYB * (PRO ? 2 : 1);  // side tiles after the source tile(s)
+  constexpr int STAGE = DYS + NSIDE * SB, NQD = DYB / 1024, NQS = SB / 1024;
+  constexpr int NQT = NQD * (PRO ? 2 : 1) + NSIDE * NQS;  // DMA instructions per tile
   // ring depth: vmcnt holds at most 63 in flight, so 2 younger tiles only while 2 NQT <= 63
-  constexpr int DB = dgrad_ring<K, RES, BN>(), D = DB - 1;
+  constexpr int DB = dgrad_ring<K, RES, BN, PRO>(), D = DB - 1;
   extern __shared__ __attribute__((aligned(16))) char sm[];
   char* stg = sm + DB * STAGE;
   const int nbn = N / NC, PB = gridDim.x / nbn;
@@ -233,6 +273,10 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
         const int P = q * 64 + lane, r = P / CPR, c = (P % CPR) ^ xswz<K>(r);
         const unsigned short* src = dy + ((size_t)tile * DTM + r) * K + c * 8;
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(d + q * 1024), 16, 0, 0);
+        if constexpr (PRO != 0) {
+          const unsigned short* src2 = src1 + ((size_t)tile * DTM + r) * K + c * 8;
+          __builtin_amdgcn_global_load_lds((const void*)src2, (lds_void*)(d + DYB + q * 1024), 16, 0, 0);
+        }
       }
       const unsigned short* sides[3] = {res, relu_y, bn_x};
 #pragma unroll
@@ -244,7 +288,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
           const int r = 2 * q + (lane >> 5), c = lane & 31;
           const unsigned short* src = sides[si] + ((size_t)tile * DTM + r) * N + cb * NC + c * 8;
           __builtin_amdgcn_global_load_lds((const void*)src,
-                                           (lds_void*)(d + DYB + slot * SB + q * 1024), 16, 0, 0);
+                                           (lds_void*)(d + DYS + slot * SB + q * 1024), 16, 0, 0);
         }
       }
     };
@@ -258,6 +302,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
     wait_oldest(min(D, nmy) - 1);
     __syncthreads();
     for (int it = 0; it < nmy; ++it) {
+      if constexpr (PRO != 0) asm volatile("s_barrier" ::: "memory");  // (the transform's barrier)
       if (it + D < nmy) issue(it + D);
       wait_oldest(min(D, nmy - 1 - it) - 1);  // tile it + 1 landed
       __syncthreads();  // (the compute waves' staging barrier)
@@ -265,6 +310,17 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
     }
     __syncthreads();  // (the statistics reduction's barrier)
     return;
+  }
+  // PRO: thread tid < DTM * CPR transforms chunk tid % CPR of row tid / CPR
+  const int tcc = tid % CPR, tr = tid / CPR;
+  float ca[8], cb_[8], cd[8];  // (coef row 2 is zero for BatchNorm backward: not held)
+  if constexpr (PRO != 0) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ca[u] = coef[tcc * 8 + u];
+      cb_[u] = coef[K + tcc * 8 + u];
+      cd[u] = coef[3 * K + tcc * 8 + u];
+    }
   }
   const int c0 = wave * (NTW * 16);  // the wave's channels inside the slice
   bf16x8 wf[NTW][KK];                // A operand: W^T[n][k], rows of the transposed copy wt
@@ -279,8 +335,25 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
   const int ep = tid >> 5, ec = tid & 31;  // epilogue: pixel, 16-B chunk of the slice
   __syncthreads();  // tile 0 in LDS
   for (int it = 0; it < nmy; ++it) {
-    const char* buf = sm + (it % DB) * STAGE;
+    char* buf = sm + (it % DB) * STAGE;
     const int p0 = (pb + it * PB) * DTM;
+    if constexpr (PRO != 0) {
+      if (tid < DTM * CPR) {
+        const int off = tr * (K * 2) + ((tcc ^ xswz<K>(tr)) << 4);
+        const bf16x8 a8 = *(const bf16x8*)(buf + off);
+        const bf16x8 b8 = *(const bf16x8*)(buf + DYB + off);
+        bf16x8 o8;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          float o = bf(a8[u]) * ca[u];
+          o += bf(b8[u]) * cb_[u] + cd[u];
+          o8[u] = (short)tobf(o);
+        }
+        *(bf16x8*)(buf + off) = o8;
+        if (xo && cb == 0) *(bf16x8*)(xo + (size_t)(p0 + tr) * K + tcc * 8) = o8;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
     bf16x8 xf[KK];
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk)
@@ -300,14 +373,14 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
       float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
       const int so = ep * (NC * 2) + ec * 16;
       if constexpr (RES) {
-        const bf16x8 r8 = *(const bf16x8*)(buf + DYB + so);
+        const bf16x8 r8 = *(const bf16x8*)(buf + DYS + so);
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] += bf(r8[u]);
       }
       bf16x8 o;
       if constexpr (BN) {
-        const bf16x8 y8 = *(const bf16x8*)(buf + DYB + (RES ? 1 : 0) * SB + so);
-        const bf16x8 x8 = *(const bf16x8*)(buf + DYB + (RES ? 2 : 1) * SB + so);
+        const bf16x8 y8 = *(const bf16x8*)(buf + DYS + (RES ? 1 : 0) * SB + so);
+        const bf16x8 x8 = *(const bf16x8*)(buf + DYS + (RES ? 2 : 1) * SB + so);
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           o[u] = (short)tobf(bf(y8[u]) > 0.f ? v[u] : 0.f);
@@ -653,55 +726,65 @@ static void conv1x1_narrow_go(int M, const void* x, const void* w, void* y, cons
                      (const unsigned short*)s1, coef, (unsigned short*)xo);
 }
 
-template <int K>
+template <int K, int PRO = 0>
 static void conv1x1_fwd_go(dim3 grid, int M, int N, const void* x, const void* w, int ldw, void* y,
-                           float* ps, float* pq, hipStream_t s) {
+                           float* ps, float* pq, hipStream_t s, const float* coef = nullptr,
+                           void* xo = nullptr) {
   using namespace pw;
-  const size_t lds = (size_t)NBUF * ftm<K>() * K * 2 + (size_t)ftm<K>() * OPITCH;
+  const size_t lds = (size_t)NBUF * ftm<K>() * K * 2 + (size_t)ftm<K>() * OPITCH +
+                     (PRO ? (size_t)2 * K * 4 : 0);
   static bool attr = false;
   if (!attr) {
-    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_fwd_kernel<K>,
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_fwd_kernel<K, PRO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL(conv1x1_fwd_kernel<K>, grid, dim3(576), lds, s, M, N, (const unsigned short*)x,
-                     (const unsigned short*)w, ldw, (unsigned short*)y, ps, pq);
+  hipLaunchKernelGGL((conv1x1_fwd_kernel<K, PRO>), grid, dim3(576), lds, s, M, N,
+                     (const unsigned short*)x, (const unsigned short*)w, ldw, (unsigned short*)y, ps,
+                     pq, coef, (unsigned short*)xo);
 }
 
-template <int K, bool RES, bool BN>
+template <int K, bool RES, bool BN, int PRO = 0>
 static void conv1x1_dgrad_go(dim3 grid, int M, int N, const void* dy, const void* w, int ldw,
                              void* dx, const void* res, const void* relu_y, const void* bn_x,
                              const float* mean, const float* rstd, float* ps, float* pq,
-                             hipStream_t s) {
+                             hipStream_t s, const void* src1 = nullptr,
+                             const float* coef = nullptr, void* xo = nullptr) {
   using namespace pw;
   const size_t lds =
-      (size_t)dgrad_ring<K, RES, BN>() * (DTM * K * 2 + ((RES ? 1 : 0) + (BN ? 2 : 0)) * DTM * NC * 2) +
+      (size_t)dgrad_ring<K, RES, BN, PRO>() *
+          (DTM * K * 2 * (PRO ? 2 : 1) + ((RES ? 1 : 0) + (BN ? 2 : 0)) * DTM * NC * 2) +
       (size_t)DTM * SPITCH;
+  static_assert(PRO == 0 || (size_t)dgrad_ring<K, RES, BN, PRO>() *
+                                    (DTM * K * 2 * 2 + ((RES ? 1 : 0) + (BN ? 2 : 0)) * DTM * NC * 2) +
+                                (size_t)DTM * SPITCH <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_dgrad_kernel<K, RES, BN>,
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_dgrad_kernel<K, RES, BN, PRO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL((conv1x1_dgrad_kernel<K, RES, BN>), grid, dim3(576), lds, s, M, N,
+  hipLaunchKernelGGL((conv1x1_dgrad_kernel<K, RES, BN, PRO>), grid, dim3(576), lds, s, M, N,
                      (const unsigned short*)dy, (const unsigned short*)w, ldw, (unsigned short*)dx,
                      (const unsigned short*)res, (const unsigned short*)relu_y,
-                     (const unsigned short*)bn_x, mean, rstd, ps, pq);
+                     (const unsigned short*)bn_x, mean, rstd, ps, pq, (const unsigned short*)src1,
+                     coef, (unsigned short*)xo);
 }
 
-template <int K>
+template <int K, int PRO = 0>
 static void conv1x1_dgrad_pick(dim3 grid, int M, int N, const void* dy, const void* w, int ldw,
                                void* dx, const void* res, const void* relu_y, const void* bn_x,
                                const float* mean, const float* rstd, float* ps, float* pq,
-                               hipStream_t s) {
+                               hipStream_t s, const void* src1 = nullptr,
+                               const float* coef = nullptr, void* xo = nullptr) {
   if (res && ps)
-    conv1x1_dgrad_go<K, true, true>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s);
+    conv1x1_dgrad_go<K, true, true, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo);
   else if (res)
-    conv1x1_dgrad_go<K, true, false>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s);
+    conv1x1_dgrad_go<K, true, false, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo);
   else if (ps)
-    conv1x1_dgrad_go<K, false, true>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s);
+    conv1x1_dgrad_go<K, false, true, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo);
   else
-    conv1x1_dgrad_go<K, false, false>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s);
+    conv1x1_dgrad_go<K, false, false, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo);
 }
 
 // mode 1: forward (x [M][K], w [N][ldw]); mode 2: data gradient (x = dy [M][K], w [K][ldw],
@@ -766,27 +849,39 @@ void conv1x1_launch(int mode, int M, int K, int N, const void* x, const void* w,
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
-// The narrow products with the BatchNorm prologue (PRO, see conv1x1_narrow_kernel):
-//  mode 1: op = relu((s0 a + c) + (s1 b + d)) written to xo, y = op W^T + statistics rows;
-//  mode 2: op = (s0 a + c) + (s1 b + d) written to xo (may be null), y = de = (op W) * (relu_y
-//          > 0) + the BN-backward statistics rows of bn_x / mean / rstd.
-// coef: f32 [4][K] (bn_fwd_coef / bn_bwd_coef in cnn.hip).  One partial statistics row per block
-// (conv1x1_rows(), 256).
-bool conv1x1_pro_applies(int M, int K, int N) {
-  return M > 0 && M % 64 == 0 && conv1x1_narrow(K, N);
+// The 1x1 products with a BatchNorm prologue (PRO; coef: f32 [4][K] from bn_fwd_coef /
+// bn_bwd_coef in cnn.hip), op = the product's reduction operand formed per tile:
+//  mode 1 (narrow forward):  op = relu((s0 a + c) + (s1 b + d)) -> xo; y = op W^T + statistics
+//          rows (a bottleneck output inside the next conv1);
+//  mode 2 (data gradient):   op = (s0 a + c) + (s1 b + d) -> xo (may be null); narrow: y = de
+//          = (op W) * (relu_y > 0) + BN-backward rows of bn_x / mean / rstd; wide: as
+//          conv1x1_launch mode 2 (+ residual, optional BN);
+//  mode 3 (wide forward):    op = relu(s0 a + c) -> xo; y = op W^T + statistics rows (a BN +
+//          ReLU inside the following expansion conv).
+// Partial statistics rows: conv1x1_rows().
+bool conv1x1_pro_applies(int mode, int M, int K, int N) {
+  if (M <= 0 || M % 64) return false;
+  const bool narrow = conv1x1_narrow(K, N);
+  if (mode == 1) return narrow;
+  if (mode == 3) return !narrow && conv1x1_applies(M, K, N);
+  return mode == 2 && conv1x1_applies(M, K, N);
 }
 void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const void* s1,
                         const float* coef, void* xo, const void* w, int ldw, void* y,
-                        const void* relu_y, const void* bn_x, const float* mean, const float* rstd,
-                        float* ps, float* pq, void* wt, hipStream_t s) {
+                        const void* res, const void* relu_y, const void* bn_x, const float* mean,
+                        const float* rstd, float* ps, float* pq, void* wt, hipStream_t s) {
   using namespace pw;
-  if (!conv1x1_pro_applies(M, K, N)) throw std::runtime_error("conv1x1_pro: unsupported shape");
-  if (!s0 || !s1 || !coef || !ps || !pq || (mode == 1 && (!xo || ldw != K)) ||
-      (mode == 2 && (!relu_y || !bn_x || !mean || !rstd || !wt)) || (mode != 1 && mode != 2))
-    throw std::runtime_error("conv1x1_pro: sources, coefficients and statistics required; forward: "
-                             "xo and ldw == K; dgrad: relu_y, bn_x, mean, rstd and wt");
+  if (!conv1x1_pro_applies(mode, M, K, N)) throw std::runtime_error("conv1x1_pro: unsupported shape");
+  const bool narrow = conv1x1_narrow(K, N);
+  if (!s0 || !coef || (mode != 3 && !s1) || ((mode == 1 || mode == 3) && (!xo || !ps || !pq)) ||
+      (mode == 1 && ldw != K) || (mode == 2 && !wt) ||
+      (mode == 2 && narrow && (!relu_y || !bn_x || !mean || !rstd || !ps || res)) ||
+      ((ps != nullptr) != (pq != nullptr)) || (mode == 2 && ps && (!relu_y || !bn_x || !mean || !rstd)))
+    throw std::runtime_error("conv1x1_pro: sources, coefficients, statistics (and for the data "
+                             "gradient wt, relu_y, bn_x, mean, rstd) required");
   if (ldw % 8 || (((uintptr_t)s0 | (uintptr_t)s1 | (uintptr_t)xo | (uintptr_t)w | (uintptr_t)y |
-                   (uintptr_t)relu_y | (uintptr_t)bn_x | (uintptr_t)wt | (uintptr_t)coef) & 15))
+                   (uintptr_t)res | (uintptr_t)relu_y | (uintptr_t)bn_x | (uintptr_t)wt |
+                   (uintptr_t)coef) & 15))
     throw std::runtime_error("conv1x1_pro: ldw % 8, 16-B aligned tensors");
   const void* wv = w;
   if (mode == 2) {
@@ -794,6 +889,7 @@ void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const voi
                        (const unsigned short*)w, ldw, (unsigned short*)wt);
     wv = wt;
   }
+  if (narrow) {
 #define DTFX_PW_PRO(KV, NV)                                                                     \
   do {                                                                                          \
     if (mode == 1)                                                                              \
@@ -803,10 +899,22 @@ void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const voi
       conv1x1_narrow_go<KV, NV, true, 2>(M, s0, wv, y, relu_y, bn_x, mean, rstd, ps, pq, s, s1, \
                                          coef, xo);                                             \
   } while (0)
-  if (K == 256 && N == 64) DTFX_PW_PRO(256, 64);
-  else if (K == 256) DTFX_PW_PRO(256, 128);
-  else DTFX_PW_PRO(512, 128);
+    if (K == 256 && N == 64) DTFX_PW_PRO(256, 64);
+    else if (K == 256) DTFX_PW_PRO(256, 128);
+    else DTFX_PW_PRO(512, 128);
 #undef DTFX_PW_PRO
+  } else {
+    const dim3 grid(conv1x1_blocks(mode == 3 ? 1 : 2, K));
+    if (mode == 3) {
+      if (K == 64) conv1x1_fwd_go<64, 3>(grid, M, N, s0, w, ldw, y, ps, pq, s, coef, xo);
+      else if (K == 128) conv1x1_fwd_go<128, 3>(grid, M, N, s0, w, ldw, y, ps, pq, s, coef, xo);
+      else conv1x1_fwd_go<256, 3>(grid, M, N, s0, w, ldw, y, ps, pq, s, coef, xo);
+    } else {
+      if (K == 64) conv1x1_dgrad_pick<64, 2>(grid, M, N, s0, wv, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s, s1, coef, xo);
+      else if (K == 128) conv1x1_dgrad_pick<128, 2>(grid, M, N, s0, wv, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s, s1, coef, xo);
+      else conv1x1_dgrad_pick<256, 2>(grid, M, N, s0, wv, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s, s1, coef, xo);
+    }
+  }
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

@@ -197,8 +197,7 @@ class ResNet50:
                     x_in, c1, s1 = self._finish_block(blocks, pend, pre + "conv1")
                 a1, m1, r1 = self._bn_apply(pre + "conv1", c1, s1)
                 c2, s2 = self._conv_bn(pre + "conv2", a1)
-                a2, m2, r2 = self._bn_apply(pre + "conv2", c2, s2)
-                c3, s3 = self._conv_bn(pre + "conv3", a2)
+                a2, m2, r2, c3, s3 = self._bn_relu_conv(pre + "conv2", c2, s2, pre + "conv3")
                 # (first block: the downsample conv of the same input; its BatchNorm is applied
                 # with bn3's, the normalised shortcut is never materialised)
                 dsc = self._conv_bn(pre + "downsample", x_in) if b == 0 else None
@@ -252,6 +251,24 @@ class ResNet50:
             on_bucket_ready(0)
         return loss, acc
 
+    def _bn_relu_conv(self, name, c, st, next_conv):
+        """``a = relu(bn(c))`` and the 1x1 expansion ``next_conv`` of it: one pass over c on the
+        wide 1x1 kernel's prologue (``CN.bn_relu_conv1x1``) when it takes the product, else
+        bn_apply then the conv.  Returns (a, mean, rstd, y, y statistics)."""
+        P = self.params
+        cout = self.specs[next_conv][2]
+        if CN.bn_prologue_applies(c, c.shape[-1], cout, 3):
+            cs, cq, M = st
+            ncs, ncq = self._stats[next_conv]
+            rm, rv = P.running[name]
+            a, y, m, r = CN.bn_relu_conv1x1(c, cs, cq, M, P.P(name + ".bn.gamma"),
+                                            P.P(name + ".bn.beta"), P.W(next_conv + ".weight"),
+                                            ncs, ncq, self.eps, rm, rv)
+            return a, m, r, y, (ncs, ncq, y.numel() // cout)
+        a, m, r = self._bn_apply(name, c, st)
+        y, sy = self._conv_bn(next_conv, a)
+        return a, m, r, y, sy
+
     def _finish_block(self, blocks, pend, next_conv):
         """Form block ``pend``'s output ``out = relu(bn3(c3) + shortcut)`` (shortcut: the
         block input, or bn_ds(downsample conv output) for a first block) and, with
@@ -273,7 +290,7 @@ class ResNet50:
             res_bn = (sds[0], sds[1], P.P(nd + "gamma"), P.P(nd + "beta"), rm, rv)
         c1 = s1 = None
         if next_conv is not None and CN.bn_prologue_applies(c3, c3.shape[-1],
-                                                            self.specs[next_conv][2]):
+                                                            self.specs[next_conv][2], 1):
             cout = self.specs[next_conv][2]
             cs, cq, M = s3
             ncs, ncq = self._stats[next_conv]
@@ -337,7 +354,7 @@ class ResNet50:
         n3 = pre + "conv3"
         # conv3's data gradient (a narrow 1x1 product) forms dc3 = BN3-backward(de3) in its
         # prologue when it can: one pass over de3 and c3 (dc3 written for the weight gradient)
-        pro = dout_is_de and CN.bn_prologue_applies(c3, c3.shape[-1], a2.shape[-1])
+        pro = dout_is_de and CN.bn_prologue_applies(c3, c3.shape[-1], a2.shape[-1], 2)
         dc3 = None
         if dout_is_de:
             dres = dout
@@ -361,12 +378,20 @@ class ResNet50:
             de2 = self._wgrad_dgrad(n3, dc3, a2, bn=bn2)
         dc2 = self._bn_apply_bwd(pre + "conv2", de2, c2, m2, r2)
         de1 = self._wgrad_dgrad(pre + "conv2", dc2, a1, bn=self._bn_fused(pre + "conv1", a1, c1, m1, r1))
-        dc1 = self._bn_apply_bwd(pre + "conv1", de1, c1, m1, r1)
+        n1 = pre + "conv1"
         bn = None
         if fuse_prev is not None:
             name, y, (c, m, r) = fuse_prev
             bn = self._bn_fused(name, y, c, m, r)
-        return self._wgrad_dgrad(pre + "conv1", dc1, x_in, residual=dshort, bn=bn)
+        if CN.bn_prologue_applies(c1, c1.shape[-1], x_in.shape[-1], 2):
+            # BN1's backward apply inside conv1's data gradient (dc1 written for the wgrad)
+            dx, dc1 = CN.bn_in_conv1x1_dgrad(de1, c1, m1, r1, P.P(n1 + ".bn.gamma"),
+                                             P.G(n1 + ".bn.beta"), P.G(n1 + ".bn.gamma"),
+                                             P.W(n1 + ".weight"), bn, residual=dshort)
+            self._wgrad_dgrad(n1, dc1, x_in, need_dx=False)
+            return dx
+        dc1 = self._bn_apply_bwd(n1, de1, c1, m1, r1)
+        return self._wgrad_dgrad(n1, dc1, x_in, residual=dshort, bn=bn)
 
     def sgd_step(self, lr, momentum=0.9, wd=5e-5, gscale=1.0):
         p = self.params

@@ -250,17 +250,24 @@ def bn_bwd_apply(de, x, mean, rstd, gamma, sum_dy, sum_dyxh):
     return dx
 
 
-def bn_prologue_applies(x, K, N):
+def bn_prologue_applies(x, K, N, mode):
     """True when a 1x1 / stride-1 product over ``x``'s pixels reducing K channels to N runs on
-    the narrow kernel with the BatchNorm prologue (:func:`bn_out_conv1x1`: K = the block
-    output's channels, N = the next conv's; :func:`bn_in_conv1x1_dgrad`: K = the conv's output
-    channels, N = its input channels).  ``DTFX_BN_PROLOGUE=0`` keeps the separate passes."""
+    a 1x1 kernel with the BatchNorm prologue: mode 1 :func:`bn_out_conv1x1` (K = the block
+    output's channels, N = the next conv's), mode 2 :func:`bn_in_conv1x1_dgrad` (K = the conv's
+    output channels, N = its input channels), mode 3 :func:`bn_relu_conv1x1`.
+    ``DTFX_BN_PROLOGUE=0`` keeps the separate passes (A/B runs); the wide-kernel variants
+    (mode 3, and mode 2 on a non-narrow shape) follow ``DTFX_BN_PROLOGUE_WIDE``."""
     if not (x.is_cuda and _CONV1X1 and _BN_PRO):
         return False
-    return bool(hip().conv1x1_pro_applies(x.numel() // x.shape[-1], K, N))
+    M = x.numel() // x.shape[-1]
+    if not hip().conv1x1_pro_applies(mode, M, K, N):
+        return False
+    narrow = bool(hip().conv1x1_pro_applies(1, M, K, N))
+    return narrow or _BN_PRO_WIDE
 
 
 _BN_PRO = os.environ.get("DTFX_BN_PROLOGUE", "1") != "0"
+_BN_PRO_WIDE = os.environ.get("DTFX_BN_PROLOGUE_WIDE", "1") != "0"
 
 
 def bn_out_conv1x1(c, s, q, M, gamma, beta, residual, w, colsum, colsq, eps=1e-5, run_mean=None,
@@ -298,7 +305,7 @@ def bn_out_conv1x1(c, s, q, M, gamma, beta, residual, w, colsum, colsq, eps=1e-5
     y = torch.empty(*c.shape[:-1], Nout, device=dev, dtype=BF16)
     part = torch.empty(2, hip().conv1x1_rows(1, Mrows, K, Nout), Nout, device=dev)
     hip().conv1x1_pro(1, Mrows, K, Nout, ptr(c), ptr(residual), ptr(coef), ptr(out), ptr(w),
-                      w.stride(0), ptr(y), 0, 0, 0, 0, ptr(part[0]), ptr(part[1]), 0,
+                      w.stride(0), ptr(y), 0, 0, 0, 0, 0, ptr(part[0]), ptr(part[1]), 0,
                       stream_handle())
     hip().colpart_reduce(part.shape[1], Nout, ptr(part[0]), ptr(part[1]), ptr(colsum), ptr(colsq),
                          stream_handle())
@@ -307,40 +314,75 @@ def bn_out_conv1x1(c, s, q, M, gamma, beta, residual, w, colsum, colsq, eps=1e-5
     return out, y, st[0], st[1], st[2], st[3]
 
 
-def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn, want_dc=True):
+def bn_relu_conv1x1(c, s, q, M, gamma, beta, w, colsum, colsq, eps=1e-5, run_mean=None,
+                    run_var=None, momentum=0.9):
+    """``a = relu(bn(c))`` (training-mode BatchNorm from c's column sums) and the 1x1 / stride-1
+    expansion conv ``y = a W^T`` in one pass over ``c``: the wide 1x1 kernel's prologue (PRO 3)
+    forms ``a`` in LDS, writes it once (the backward reads it) and feeds it to the MFMAs -- the
+    bn_apply pass and the conv's read of its result become one.  y's BatchNorm statistics are
+    accumulated into ``colsum`` / ``colsq``.  Returns (a, y, mean, rstd)."""
+    if not c.is_cuda:
+        a, mean, rstd = bn_apply_stats(c, s, q, M, gamma, beta, None, True, eps, run_mean, run_var,
+                                       momentum)
+        return a, conv_fwd(a, w, 1, 1, 1, 0, colsum=colsum, colsq=colsq), mean, rstd
+    K = c.shape[-1]
+    Nout = w.shape[0]
+    Mrows = c.numel() // K
+    st = torch.empty(2, K, device=c.device)
+    coef = torch.empty(4, K, device=c.device)
+    hip().bn_fwd_coef(int(M), K, ptr(s), ptr(q), float(eps), ptr(st[0]), ptr(st[1]), ptr(run_mean),
+                      ptr(run_var), float(momentum), ptr(gamma), ptr(beta), 0, 0, 0, 0, 0, 0, 0, 0,
+                      ptr(coef), stream_handle())
+    a = torch.empty_like(c)
+    y = torch.empty(*c.shape[:-1], Nout, device=c.device, dtype=BF16)
+    part = torch.empty(2, hip().conv1x1_rows(1, Mrows, K, Nout), Nout, device=c.device)
+    hip().conv1x1_pro(3, Mrows, K, Nout, ptr(c), 0, ptr(coef), ptr(a), ptr(w), w.stride(0), ptr(y),
+                      0, 0, 0, 0, 0, ptr(part[0]), ptr(part[1]), 0, stream_handle())
+    hip().colpart_reduce(part.shape[1], Nout, ptr(part[0]), ptr(part[1]), ptr(colsum), ptr(colsq),
+                         stream_handle())
+    return a, y, st[0], st[1]
+
+
+def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, want_dc=True,
+                        residual=None):
     """BatchNorm backward's apply half and the data gradient of the 1x1 conv that produced the
     BatchNorm's input, in one pass.
 
     ``de`` = dL/d(BN output) with the final reductions ``sum_dy`` / ``sum_dyxh`` (see
     :func:`conv_dgrad`'s ``bn``), ``c`` = the BN input (this conv's output): the conv's output
-    gradient ``dc = bn_bwd_apply(de, c, ...)`` is formed inside the narrow dgrad kernel's
-    prologue (PRO 2) and written out when ``want_dc`` (the weight gradient reads it); the
-    product is ``conv_dgrad(dc, w, bn=bn)`` with the fused BatchNorm backward of the conv's
-    own input (``bn = (y, x, mean, rstd, sum_dy, sum_dyxh)``, required).  Returns (dx, dc)."""
+    gradient ``dc = bn_bwd_apply(de, c, ...)`` is formed inside the 1x1 dgrad kernel's prologue
+    (PRO 2) and written out when ``want_dc`` (the weight gradient reads it); the product is
+    ``conv_dgrad(dc, w, residual=residual, bn=bn)`` -- with ``bn = (y, x, mean, rstd, sum_dy,
+    sum_dyxh)`` the fused BatchNorm backward of the conv's own input (required on the narrow
+    kernels).  Returns (dx, dc)."""
     if not de.is_cuda:
         dc = bn_bwd_apply(de, c, mean, rstd, gamma, sum_dy, sum_dyxh)
         N, H, W, _ = c.shape
-        dx = conv_dgrad(dc, w, (N, H, W, w.shape[1]), 1, 1, 1, 0, bn=bn)
+        dx = conv_dgrad(dc, w, (N, H, W, w.shape[1]), 1, 1, 1, 0, residual=residual, bn=bn)
         return dx, dc
     K = c.shape[-1]          # the conv's output channels (the BN's)
     Cin = w.shape[1]
     M = c.numel() // K
-    y, x, bmean, brstd, sdy, sdx = bn
     dev = c.device
     coef = torch.empty(4, K, device=dev)
     hip().bn_bwd_coef(M, K, ptr(mean), ptr(rstd), ptr(gamma), ptr(sum_dy), ptr(sum_dyxh),
                       ptr(coef), stream_handle())
     dc = torch.empty_like(c) if want_dc else None
     dx = torch.empty(*c.shape[:-1], Cin, device=dev, dtype=BF16)
-    if y.shape != dx.shape or x.shape != dx.shape:
-        raise ValueError("fused BN backward: y and x must have the dgrad output's shape")
     wt = torch.empty(Cin, K, device=dev, dtype=BF16)
-    part = torch.empty(2, hip().conv1x1_rows(2, M, K, Cin), Cin, device=dev)
+    y = x = bmean = brstd = sdy = sdx = part = None
+    if bn is not None:
+        y, x, bmean, brstd, sdy, sdx = bn
+        if y.shape != dx.shape or x.shape != dx.shape:
+            raise ValueError("fused BN backward: y and x must have the dgrad output's shape")
+        part = torch.empty(2, hip().conv1x1_rows(2, M, K, Cin), Cin, device=dev)
     hip().conv1x1_pro(2, M, K, Cin, ptr(de), ptr(c), ptr(coef), ptr(dc), ptr(w), w.stride(0),
-                      ptr(dx), ptr(y), ptr(x), ptr(bmean), ptr(brstd), ptr(part[0]), ptr(part[1]),
+                      ptr(dx), ptr(residual), ptr(y), ptr(x), ptr(bmean), ptr(brstd),
+                      ptr(None if part is None else part[0]), ptr(None if part is None else part[1]),
                       ptr(wt), stream_handle())
-    hip().colpart_reduce(part.shape[1], Cin, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
-                         stream_handle())
+    if part is not None:
+        hip().colpart_reduce(part.shape[1], Cin, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
+                             stream_handle())
     return dx, dc
 
 
@@ -522,8 +564,9 @@ def bn_maxpool_fwd(c, s, q, M, gamma, beta, eps=1e-5, run_mean=None, run_var=Non
 def maxpool_bn_bwd(dy, idx, c, mean, rstd, gamma, beta, fcoef, dgamma, dbeta):
     """Backward of :func:`bn_maxpool_fwd`: dL/dc from the pool's output gradient ``dy``;
     dgamma / dbeta are the (per-step zeroed) gradient slots, which receive BatchNorm backward's
-    two sums.  GPU: two passes that each re-gather the pool gradient per input pixel (sums,
-    then the apply) -- the dense pool gradient and ``relu(bn(c))`` are never read or written."""
+    two sums.  GPU: one pass gathers the pool gradient, masks it with the ReLU recomputed from
+    ``c``, reduces the sums and writes ``de``; the streaming apply reads ``de`` and ``c``
+    (``relu(bn(c))`` is never read or written)."""
     if not c.is_cuda:
         a = bn_apply(c, mean, rstd, gamma, beta, None, relu=True)
         da = maxpool_bwd(dy, idx, c.shape)
@@ -532,10 +575,10 @@ def maxpool_bn_bwd(dy, idx, c, mean, rstd, gamma, beta, fcoef, dgamma, dbeta):
     N, H, W, C = c.shape
     rows = hip().maxpool_bn_bwd_rows(N, H, W, C)
     scratch = torch.empty(2 * rows * C, device=c.device)
-    bcoef = torch.empty(4, C, device=c.device)
+    de = torch.empty_like(c)
     dc = torch.empty_like(c)
     hip().maxpool_bn_bwd(N, H, W, C, ptr(dy), ptr(idx), ptr(c), ptr(fcoef), ptr(mean), ptr(rstd),
-                         ptr(gamma), ptr(dbeta), ptr(dgamma), ptr(scratch), ptr(bcoef), ptr(dc),
+                         ptr(gamma), ptr(dbeta), ptr(dgamma), ptr(scratch), ptr(de), ptr(dc),
                          stream_handle())
     return dc
 

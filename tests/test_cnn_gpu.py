@@ -281,15 +281,20 @@ def test_bn_out_conv1x1_prologue(gpu, N, H, W, K, Co, ds):
     assert (d <= 2 ** -7 * o.abs() + 1e-6).all()  # at most one bf16 rounding apart
 
 
-@pytest.mark.parametrize("N,H,W,Cin,K", [
-    (2, 16, 16, 64, 256),    # layer1 conv3 data gradient (256 -> 64)
-    (4, 8, 8, 128, 512),     # layer2 conv3 (512 -> 128, 16-pixel tiles)
-    (3, 16, 20, 64, 256),    # M = 960
+@pytest.mark.parametrize("N,H,W,Cin,K,with_res,with_bn", [
+    (2, 16, 16, 64, 256, False, True),    # layer1 conv3 data gradient (narrow 256 -> 64)
+    (4, 8, 8, 128, 512, False, True),     # layer2 conv3 (narrow 512 -> 128, 16-pixel tiles)
+    (3, 16, 20, 64, 256, False, True),    # M = 960
+    (2, 16, 16, 256, 64, True, True),     # layer1 conv1 (wide 64 -> 256, + shortcut gradient)
+    (2, 16, 16, 256, 64, True, False),    # first block's conv1: shortcut only, no BN behind
+    (2, 8, 8, 512, 128, True, True),      # layer2 conv1 (two column blocks: xo from one)
+    (2, 8, 8, 1024, 256, True, True),     # layer3 conv1 (four column blocks)
 ])
-def test_bn_in_conv1x1_dgrad_prologue(gpu, N, H, W, Cin, K):
-    """BN3-backward's apply half formed inside conv3's narrow dgrad prologue (conv1x1.hip PRO 2)
-    == bn_bwd_apply then the dgrad with conv2's fused BN reductions (f32 CPU path): dL/dc3
-    (written for the weight gradient), de2 and conv2's BN sums."""
+def test_bn_in_conv1x1_dgrad_prologue(gpu, N, H, W, Cin, K, with_res, with_bn):
+    """A BatchNorm's backward apply formed inside the dgrad prologue of the 1x1 conv feeding it
+    (conv1x1.hip PRO 2: narrow conv3 / wide conv1 products) == bn_bwd_apply then the dgrad with
+    the fused BN reductions of the conv's own input and the shortcut gradient (f32 CPU path):
+    dL/dc (written for the weight gradient), the dgrad output and the input BN's sums."""
     M = N * H * W
     c3 = _r(N, H, W, K, seed=41, scale=2).to(BF) + 0.5
     c3f = c3.float().reshape(M, K)
@@ -304,18 +309,22 @@ def test_bn_in_conv1x1_dgrad_prologue(gpu, N, H, W, Cin, K):
     g2, b2 = _r(Cin, seed=45) * 0.1 + 1, _r(Cin, seed=46) * 0.1
     y2 = cnn.bn_apply(c2, m2, r2, g2, b2, None, relu=True)
     w3 = _r(K, Cin, seed=47, scale=Cin ** -0.5).to(BF)
+    res = _r(N, H, W, Cin, seed=48).to(BF) if with_res else None
 
     def run(dev):
-        t = lambda v: v.to(dev)  # noqa: E731
+        t = lambda v: None if v is None else v.to(dev)  # noqa: E731
         sdy2, sdx2 = torch.zeros(Cin, device=dev), torch.zeros(Cin, device=dev)
+        bn = (t(y2), t(c2), t(m2), t(r2), sdy2, sdx2) if with_bn else None
         dx, dc = cnn.bn_in_conv1x1_dgrad(t(de3), t(c3), t(m3), t(r3), t(g3), t(sdy3), t(sdx3),
-                                         t(w3), (t(y2), t(c2), t(m2), t(r2), sdy2, sdx2))
+                                         t(w3), bn, residual=t(res))
         return dx.cpu().float(), dc.cpu().float(), sdy2.cpu(), sdx2.cpu()
 
     (dx, dc, a, b), (dxr, dcr, ar, br) = run(gpu), run("cpu")
     assert (dc - dcr).abs().max() < 2e-2 * dcr.abs().max()
     assert (dx - dxr).abs().max() < 3e-2 * dxr.abs().max()
-    assert ((dx == 0) == (dxr == 0)).float().mean() > 0.995    # conv2's ReLU mask
+    if not with_bn:
+        return
+    assert ((dx == 0) == (dxr == 0)).float().mean() > 0.995    # the input BN's ReLU mask
     assert torch.allclose(a, ar, atol=0.05 * float(ar.abs().max()) + 1e-2, rtol=2e-2)
     assert torch.allclose(b, br, atol=0.05 * float(br.abs().max()) + 1e-2, rtol=2e-2)
 
@@ -357,3 +366,35 @@ def test_stem_bn_maxpool_fused(gpu, N, H, W):
     assert (dc.float() - dcr.float()).abs().max() < 4e-2 * dcr.float().abs().max()
     assert torch.allclose(db, dbr, atol=0.05 * float(dbr.abs().max()) + 1e-2, rtol=2e-2)
     assert torch.allclose(dg, dgr, atol=0.05 * float(dgr.abs().max()) + 1e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("N,H,W,K,Co", [
+    (2, 16, 16, 64, 256),     # layer1 conv2 BN -> conv3 (64 -> 256)
+    (2, 8, 8, 128, 512),      # layer2 (two column blocks: a written by one)
+    (2, 8, 8, 256, 1024),     # layer3 (four column blocks, one block per CU)
+    (3, 16, 20, 64, 256),     # M = 960: ragged tiles over the persistent blocks
+])
+def test_bn_relu_conv1x1_prologue(gpu, N, H, W, K, Co):
+    """relu(bn(c)) formed inside the wide 1x1 forward kernel's prologue (conv1x1.hip PRO 3) and
+    written once == bn_apply_stats then conv_fwd (f32 CPU path)."""
+    M = N * H * W
+    c = _r(N, H, W, K, seed=61, scale=2).to(BF) + 0.5
+    cf = c.float().reshape(M, K)
+    s_, q_ = cf.sum(0), (cf * cf).sum(0)
+    g, b = _r(K, seed=62) * 0.1 + 1, _r(K, seed=63) * 0.1
+    w = _r(Co, K, seed=64, scale=K ** -0.5).to(BF)
+
+    def run(dev):
+        t = lambda v: v.to(dev)  # noqa: E731
+        cs, cq = torch.zeros(Co, device=dev), torch.zeros(Co, device=dev)
+        rm, rv = torch.zeros(K, device=dev), torch.ones(K, device=dev)
+        a, y, m, r = cnn.bn_relu_conv1x1(t(c), t(s_), t(q_), M, t(g), t(b), t(w), cs, cq, 1e-5, rm, rv)
+        return [v.cpu() for v in (a, y, m, r, cs, cq, rm, rv)]
+
+    got, ref = run(gpu), run("cpu")
+    a, ar = got[0].float(), ref[0].float()
+    d = (a - ar).abs()
+    assert (d <= 2 ** -7 * ar.abs() + 1e-6).all()  # at most one bf16 rounding apart
+    assert (got[1].float() - ref[1].float()).abs().max() < 3e-2 * ref[1].float().abs().max()
+    for x_, y_ in zip(got[2:], ref[2:]):
+        assert torch.allclose(x_, y_, rtol=2e-2, atol=1e-2 * float(y_.abs().max()) + 1e-4)
