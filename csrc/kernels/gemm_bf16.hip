@@ -66,9 +66,8 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   constexpr int NWN = NBUF == 8 ? 4 : BN / 64, NW = NBUF == 8 ? 8 : (BM / WM) * NWN;
   constexpr int TM = WM / 16;                      // 16-row MFMA tiles per wave
   constexpr int NQN = BN / 2, SW = NQN / 2;        // 8-phase: B half width, wave slab width
-  static_assert(BN_ == 128 || MODE == 0 || MODE == 1 || (MODE == 2 && BN_ == 64) ||
-                    (NBUF == 8 && MODE != 3),
-                "gathered B operands need BN = 128 (dgrad: or 64)");
+  static_assert(BN_ == 128 || MODE == 0 || MODE == 1 || (MODE == 2 && BN_ == 64) || NBUF == 8,
+                "gathered B operands need BN = 128 (dgrad: or 64) or the 8-phase tile");
   constexpr int TILE_A = BM * BK * 2, TILE_B = BN * BK * 2, BUF_BYTES = TILE_A + TILE_B;
   constexpr int LPT = (BM / 8) / NW + (BN / 8) / NW;  // glds per thread per K tile
   // strided batch over blockIdx.z (attention's per-(batch, head) products)
@@ -248,6 +247,44 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
       return (co0 * ldb + tap * cd.C) * 2;
     };
     const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7fffffff, 0x00020000);
+    // MODE 3 (weight gradient) B = im2col(x) [64 pixels][256 columns j = (kh, kw, ci)]: a lane's
+    // two loads per half image keep their k-rows and swizzled chunks, so their columns decode
+    // ONCE here (wdh / wdw / wci, per half and load); each K tile decodes only its pixels.
+    // Padding taps and pixels past K point past the buffer (the hardware returns zeros).
+    int wdh[4] = {0, 0, 0, 0}, wdw[4] = {0, 0, 0, 0}, wci[4] = {0, 0, 0, 0}, wjok = 0;
+    if constexpr (MODE == 3) {
+      const int jtot = cd.KH * cd.KW * cd.C;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int kr = ((q & 1) * NW + wave) * 4 + (lane >> 4);
+        const int j = n0 + (q >> 1) * NQN + (((lane & 15) ^ swz_tr(kr)) << 3);
+        int tap, ci, kh, kw;
+        fdivmod(min(j, jtot - 8), cd.C, 1.f / cd.C, tap, ci);
+        fdivmod(tap, cd.KW, 1.f / cd.KW, kh, kw);
+        wdh[q] = kh - cd.pad;
+        wdw[q] = kw - cd.pad;
+        wci[q] = ci;
+        wjok |= (j < jtot ? 1 : 0) << q;
+      }
+    }
+    auto wg_stage_b = [&](int buf, int which, int kt) {
+      const int k0 = (kt0 + kt) * BK, ohw = cd.OH * cd.OW;
+      char* d_ = smem + (buf * 4 + which) * 16384;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int q = (which - 2) * 2 + i;
+        const int kr = (i * NW + wave) * 4 + (lane >> 4), p = k0 + kr;
+        int n, rem, oh, ow;
+        fdivmod(min(p, K - 1), ohw, 1.f / ohw, n, rem);
+        fdivmod(rem, cd.OW, 1.f / cd.OW, oh, ow);
+        const int yy = oh * cd.stride + wdh[q], xx = ow * cd.stride + wdw[q];
+        const bool ok = p < K && ((wjok >> q) & 1) && (unsigned)yy < (unsigned)cd.H &&
+                        (unsigned)xx < (unsigned)cd.W;
+        const int vo = ok ? (((n * cd.H + yy) * cd.W + xx) * cd.C + wci[q]) * 2 : (int)0x80000000;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(d_ + (i * NW + wave) * 1024), 16, vo,
+                                                 0, 0, 0);
+      }
+    };
     auto voff = [&](bool isA, int which, int i) -> int {
       const bool kc = isA ? !TA : TB;
       const int ld = isA ? lda : ldb, omax = isA ? a_max : b_max;
@@ -270,6 +307,10 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   do {                                                                                          \
     if constexpr (CONV8 && (WHICH) < 2) {                                                       \
       conv_stage_a((BUF), (WHICH), (KT));                                                       \
+      break;                                                                                    \
+    }                                                                                           \
+    if constexpr (MODE == 3 && (WHICH) >= 2) {                                                  \
+      wg_stage_b((BUF), (WHICH), (KT));                                                         \
       break;                                                                                    \
     }                                                                                           \
     const int k0_ = (kt0 + (KT)) * BK;                                                          \
@@ -832,16 +873,18 @@ static void launch_cfg(int cfg, dim3 grid_yz, int M, int N, int K, const unsigne
       return;
     }
   }
-  if constexpr (MODE == 1 || MODE == 2) {
+  if constexpr (MODE == 1 || MODE == 2 || MODE == 3) {
     if (cfg == 5) {
       launch_one<MODE, TA, TB, F, 256, 8, 256>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
                                                d, stream);
       return;
     }
-    if (cfg == 4) {
-      launch_one<MODE, TA, TB, F, 256, 2, 64>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
-                                              d, stream);
-      return;
+    if constexpr (MODE != 3) {
+      if (cfg == 4) {
+        launch_one<MODE, TA, TB, F, 256, 2, 64>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB,
+                                                sC, d, stream);
+        return;
+      }
     }
   }
   if (cfg == 1)
@@ -1192,17 +1235,41 @@ long long conv_splitk_ws_floats(int mode, int N, int H, int W, int C, int Cout, 
   return (long long)s * (mode == 1 ? (long long)N * OH * OW * Cout : (long long)N * H * W * C);
 }
 
+// A gathered (3x3 / strided) weight gradient on the 8-phase 256x256 tile: >= 256 output
+// channels (a 128-channel output would leave half the tile idle), whole 64-pixel K tiles (the
+// dy^T operand is not range-checked) and a source < 2 GB (32-bit buffer offsets).  On the
+// 128x128 tile these ran at 470-530 TFLOP/s (LDS-bound: 2 x 8 KB of fragments per 128x128x64
+// step).  DTFX_CONV_WGRAD_PH8=0 keeps them there (A/B runs).
+static bool conv_wgrad_ph8(int M, int Nn, int K, long long src_elems) {
+  static const bool on = [] {
+    const char* v = getenv("DTFX_CONV_WGRAD_PH8");
+    return v ? atoi(v) != 0 : true;
+  }();
+  return on && gemm_cfg_env() < 0 && M >= 256 && K % gb::BK == 0 && Nn >= 256 &&
+         src_elems * 2 < 0x7fffffffLL;
+}
 // Split-K of a conv weight gradient (M = Cout, N = KH*KW*C, K = pixels): one wave of the 512
-// resident 128x128 slots (see gemm_splitk)
-static int conv_wgrad_splitk(int M, int Nn, int K) {
-  const int tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
+// resident 128x128 slots (see gemm_splitk), or of the 256 8-phase blocks (>= 8 K tiles each)
+static int conv_wgrad_splitk(int M, int Nn, int K, bool ph8 = false) {
   const int nkt = (K + 63) / 64;
+  if (ph8) {
+    const int tiles = ((M + 255) / 256) * ((Nn + 255) / 256);
+    return tiles < 256 ? std::max(1, std::min(256 / tiles, nkt / 8)) : 1;
+  }
+  const int tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
   return tiles < 256 ? std::max(1, std::min(512 / tiles, nkt / 4)) : 1;
+}
+static bool conv_wgrad_ph8_for(int N, int H, int W, int C, int Cout, int KH, int KW, int stride,
+                               int pad) {
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  const bool gathered = !(KH == 1 && KW == 1 && stride == 1 && pad == 0);
+  return gathered && conv_wgrad_ph8(Cout, KH * KW * C, N * OH * OW, (long long)N * H * W * C);
 }
 long long conv_wgrad_ws_floats(int N, int H, int W, int C, int Cout, int KH, int KW, int stride,
                                int pad) {
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
-  const int Nn = KH * KW * C, s = conv_wgrad_splitk(Cout, Nn, N * OH * OW);
+  const bool ph8 = conv_wgrad_ph8_for(N, H, W, C, Cout, KH, KW, stride, pad);
+  const int Nn = KH * KW * C, s = conv_wgrad_splitk(Cout, Nn, N * OH * OW, ph8);
   return s > 1 ? (long long)s * Cout * Nn : 0;
 }
 
@@ -1331,7 +1398,8 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
     if (residual || colsum || colsq || relu_y || bn_x)
       throw std::runtime_error("conv_bf16: wgrad has no epilogue options");
     M = Cout; Nn = KH * KW * C; K = N * OH * OW;
-    if (splitk <= 0) splitk = conv_wgrad_splitk(M, Nn, K);
+    const bool ph8 = conv_wgrad_ph8_for(N, H, W, C, Cout, KH, KW, stride, pad);
+    if (splitk <= 0) splitk = conv_wgrad_splitk(M, Nn, K, ph8);
     const int ldo = ldw > 0 ? ldw : Nn;  // dW row stride (the padded fwd weight layout)
     if (ldo < Nn || ldo % 8) throw std::runtime_error("conv_bf16: wgrad ld must be >= KH*KW*C, % 8");
     if (splitk > 1) {
@@ -1354,7 +1422,7 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
                                        K, (const unsigned short*)a, Cout, (const unsigned short*)b, C,
                                        out, ldo, e, 0LL, 0LL, 0LL, d, stream);
     } else {
-      launch_cfg<3, true, false, true>(choose_cfg(M, Nn, splitk, 3), dim3(1, splitk, 1), M, Nn, K,
+      launch_cfg<3, true, false, true>(ph8 ? 5 : choose_cfg(M, Nn, splitk, 3), dim3(1, splitk, 1), M, Nn, K,
                                        (const unsigned short*)a, Cout, (const unsigned short*)b, 0,
                                        out, ldo, e, 0LL, 0LL, 0LL, d, stream);
     }

@@ -40,6 +40,9 @@ CONVS = [  # N, H, W, C, Cout, k, stride, pad
     (4, 14, 14, 256, 256, 3, 1, 1),  # few tiles, deep K: split-K fwd / dgrad + epilogue pass
     (2, 7, 7, 512, 512, 3, 1, 1),    # ResNet layer4 conv2 shape: M = 98 (ragged 64-row slab)
     (2, 7, 7, 2048, 512, 1, 1, 0),   # layer4 conv1 (1x1, K = 2048), split-K forward
+    (4, 16, 16, 256, 512, 3, 1, 1),  # 3x3 weight gradient on the 8-phase tile (Cout >= 256)
+    (4, 32, 32, 256, 256, 3, 2, 1),  # same, stride 2 (layer3.0's shape class)
+    (8, 8, 8, 512, 512, 3, 1, 1),    # layer4 conv2 class: 8-phase wgrad, 2 x 18 tiles, split K
 ]
 
 
