@@ -38,7 +38,7 @@ bool stem_conv_applies(int, int, int, int, int, int, int, int);
 void stem_conv_fwd_launch(int, int, int, const void*, const void*, int, void*, float*, float*,
                           hipStream_t);
 void stem_conv_wgrad_launch(int, int, int, const void*, const void*, float*, int, float,
-                            hipStream_t);
+                            hipStream_t, const void*, const float*);
 bool conv3x3_c64_applies(int, int, int, int, int, int, int, int);
 void conv3x3_c64_fwd_launch(int, int, int, const void*, const void*, int, void*, float*, float*,
                             hipStream_t);
@@ -70,7 +70,7 @@ void maxpool_bn_fwd_launch(int, int, int, int, const void*, const float*, void*,
 int maxpool_bn_bwd_rows(int, int, int, int);
 void maxpool_bn_bwd_launch(int, int, int, int, const void*, const void*, const void*, const float*,
                            const float*, const float*, const float*, float*, float*, float*,
-                           void*, void*, hipStream_t);
+                           void*, void*, float*, hipStream_t);
 void maxpool_bwd_launch(int, int, int, int, const void*, const void*, void*, hipStream_t);
 void avgpool_fwd_launch(int, int, int, const void*, void*, hipStream_t);
 void avgpool_bwd_launch(int, int, int, const void*, void*, hipStream_t);
@@ -267,10 +267,11 @@ void register_nn(py::module_& m) {
                                P<float>(ps), P<float>(pq), S(s));
   });
   m.def("stem_conv_wgrad", [](int N, int H, int W, uintptr_t x, uintptr_t dy, uintptr_t dw, int ldw,
-                              float beta, uintptr_t s) {
+                              float beta, uintptr_t s, uintptr_t bnx, uintptr_t coef) {
     dtfx::stem_conv_wgrad_launch(N, H, W, P<const void>(x), P<const void>(dy), P<float>(dw), ldw,
-                                 beta, S(s));
-  });
+                                 beta, S(s), P<const void>(bnx), P<const float>(coef));
+  }, py::arg("N"), py::arg("H"), py::arg("W"), py::arg("x"), py::arg("dy"), py::arg("dw"),
+     py::arg("ldw"), py::arg("beta"), py::arg("stream"), py::arg("bnx") = 0, py::arg("coef") = 0);
   m.def("conv3x3_c64_applies", &dtfx::conv3x3_c64_applies,
         "the 64-channel 3x3 kernel handles this conv (stride 1, pad 1, H % 4, W % 28)");
   m.def("conv3x3_c64_fwd", [](int N, int H, int W, uintptr_t x, uintptr_t w, int ldw, uintptr_t y,
@@ -339,11 +340,11 @@ void register_nn(py::module_& m) {
   m.def("maxpool_bn_bwd", [](int N, int H, int W, int C, uintptr_t dy, uintptr_t idx, uintptr_t x,
                              uintptr_t fcoef, uintptr_t mean, uintptr_t rstd, uintptr_t g,
                              uintptr_t sdy, uintptr_t sdyxh, uintptr_t scratch, uintptr_t de,
-                             uintptr_t dx, uintptr_t s) {
+                             uintptr_t dx, uintptr_t bcoef, uintptr_t s) {
     dtfx::maxpool_bn_bwd_launch(N, H, W, C, P<const void>(dy), P<const void>(idx), P<const void>(x),
                                 P<const float>(fcoef), P<const float>(mean), P<const float>(rstd),
                                 P<const float>(g), P<float>(sdy), P<float>(sdyxh),
-                                P<float>(scratch), P<void>(de), P<void>(dx), S(s));
+                                P<float>(scratch), P<void>(de), P<void>(dx), P<float>(bcoef), S(s));
   });
   m.def("conv3x3_c128_applies", &dtfx::conv3x3_c128_applies,
         "the 128-channel 3x3 kernel handles this conv (stride 1, pad 1, H % 4, W % 28)");

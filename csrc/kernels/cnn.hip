@@ -957,11 +957,11 @@ int maxpool_bn_bwd_rows(int N, int H, int W, int C) {
 }
 // Backward: de (the masked pool gradient, written to `de`) with BatchNorm backward's sums
 // ACCUMULATED into sum_dy / sum_dyxh (the zeroed dbeta / dgamma slots), then the apply
-// dx = dL/dc over de and c (bn_bwd_apply_kernel).
+// dx = dL/dc over de and c (bn_bwd_apply_kernel) -- or, with dx null, only its coefficients.
 void maxpool_bn_bwd_launch(int N, int H, int W, int C, const void* dy, const void* idx,
                            const void* x, const float* fcoef, const float* mean, const float* rstd,
                            const float* gamma, float* sum_dy, float* sum_dyxh, float* scratch,
-                           void* de, void* dx, hipStream_t st) {
+                           void* de, void* dx, float* bcoef, hipStream_t st) {
   if (C % 8 || 256 % (C / 8)) throw std::runtime_error("maxpool_bn: C % 8 != 0, 256 % (C / 8) == 0");
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
   const int gx = (W * (C / 8) + 255) / 256, gy = maxpool_bn_bwd_gy(N, H);
@@ -972,7 +972,10 @@ void maxpool_bn_bwd_launch(int N, int H, int W, int C, const void* dy, const voi
                      (unsigned short*)de);
   DTFX_HIP_CHECK(hipGetLastError());
   colpart_reduce_launch(R, C, scratch, scratch + (size_t)R * C, sum_dy, sum_dyxh, st);
-  bn_bwd_apply_launch((long long)N * H * W, C, de, x, mean, rstd, gamma, sum_dy, sum_dyxh, dx, st);
+  // dx == null: the consumer forms dL/dc itself (the stem weight gradient's prologue) from the
+  // apply coefficients, written to bcoef
+  if (dx) bn_bwd_apply_launch((long long)N * H * W, C, de, x, mean, rstd, gamma, sum_dy, sum_dyxh, dx, st);
+  else bn_bwd_coef_launch((long long)N * H * W, C, mean, rstd, gamma, sum_dy, sum_dyxh, bcoef, st);
 }
 
 void avgpool_fwd_launch(int N, int HW, int C, const void* x, void* y, hipStream_t st) {

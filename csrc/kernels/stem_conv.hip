@@ -167,9 +167,16 @@ __device__ __forceinline__ bf16x8 tr_pair(const char* a0, const char* a1) {
   return v;
 }
 
+// PRO: dy is the gradient at the stem BatchNorm's output (the masked pool gradient de) and the
+// conv output gradient is formed as it is staged, dc = A de + K1 c + K0 (bn_bwd_apply_kernel's
+// affine form; coef rows 0, 1, 3 of bn_bwd_coef, c = bnx, the BN input): the apply pass that
+// wrote dc and this kernel's read of it become one read of de and c.  A thread's four dy chunks
+// share one channel chunk (tid & 7), so its coefficients stay in registers.
+template <bool PRO>
 __global__ __launch_bounds__(256, 1) void stem_conv_wgrad_kernel(
     int N, int H, int W, int OH, int OW, const unsigned short* __restrict__ x,
-    const unsigned short* __restrict__ dy, float* __restrict__ dw, int ldw) {
+    const unsigned short* __restrict__ dy, float* __restrict__ dw, int ldw,
+    const unsigned short* __restrict__ bnx, const float* __restrict__ coef) {
   extern __shared__ __attribute__((aligned(16))) char sm[];
   char* Ds = sm;             // [128 px][64 co] bf16, 144-B rows
   char* Ps = sm + 128 * DP;  // [21][37] pixels x 8 channels
@@ -185,7 +192,17 @@ __global__ __launch_bounds__(256, 1) void stem_conv_wgrad_kernel(
     for (int j = 0; j < 7; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // dy tile and input patch of tile tt into registers, issued one tile ahead (in flight
   // during the previous tile's MFMAs)
-  bf16x8 dv[4], pv[4];
+  bf16x8 dv[4], pv[4], cv[4];
+  float ka[8], k1[8], k0[8];
+  if constexpr (PRO) {
+    const int cc = (tid & 7) * 8;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ka[u] = coef[cc + u];
+      k1[u] = coef[COUT + cc + u];
+      k0[u] = coef[3 * COUT + cc + u];
+    }
+  }
   auto load_tile = [&](int tt) {
     const int n = tt / tiles_img, r = tt - n * tiles_img;
     const int oh0 = (r / tiles_w) * TH, ow0 = (r % tiles_w) * TW;
@@ -193,7 +210,9 @@ __global__ __launch_bounds__(256, 1) void stem_conv_wgrad_kernel(
 #pragma unroll
     for (int k = 0; k < 4; ++k) {  // dy tile: 128 px x 8 chunks; patch: 777 pixels
       const int e = tid + 256 * k, px = e >> 3, c = e & 7;
-      dv[k] = *(const bf16x8*)(dy + (((size_t)n * OH + oh0 + (px >> 4)) * OW + ow0 + (px & 15)) * COUT + c * 8);
+      const size_t o = (((size_t)n * OH + oh0 + (px >> 4)) * OW + ow0 + (px & 15)) * COUT + c * 8;
+      dv[k] = *(const bf16x8*)(dy + o);
+      if constexpr (PRO) cv[k] = *(const bf16x8*)(bnx + o);
       const int pr = e / PC, pc = e - pr * PC, ih = ih0 + pr, iw = iw0 + pc;
       pv[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (e < PR * PC && ih >= 0 && ih < H && iw >= 0 && iw < W)
@@ -206,7 +225,17 @@ __global__ __launch_bounds__(256, 1) void stem_conv_wgrad_kernel(
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int e = tid + 256 * k, px = e >> 3, c = e & 7;
-      *(bf16x8*)(Ds + px * DP + c * 16) = dv[k];
+      bf16x8 d8 = dv[k];
+      if constexpr (PRO) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float de = __uint_as_float((unsigned)(unsigned short)dv[k][u] << 16);
+          const float xf = __uint_as_float((unsigned)(unsigned short)cv[k][u] << 16);
+          const __bf16 o = (__bf16)(ka[u] * de + k1[u] * xf + k0[u]);
+          d8[u] = (short)__builtin_bit_cast(unsigned short, o);
+        }
+      }
+      *(bf16x8*)(Ds + px * DP + c * 16) = d8;
       if (e < PR * PC) *(bf16x8*)(Ps + e * 16) = pv[k];
     }
     __syncthreads();
@@ -260,13 +289,17 @@ bool stem_conv_applies(int H, int W, int C, int Cout, int KH, int KW, int stride
 
 // dw (f32 [64][ldw], the first 392 columns) (+)= the stem's weight gradient: beta 1
 // accumulates, beta 0 overwrites.
+// With bnx / coef (bn_bwd_coef rows [4][64]): dy is the gradient at the stem BatchNorm's
+// output and the conv output gradient is formed on the fly (see stem_conv_wgrad_kernel).
 void stem_conv_wgrad_launch(int N, int H, int W, const void* x, const void* dy, float* dw, int ldw,
-                            float beta, hipStream_t s) {
+                            float beta, hipStream_t s, const void* bnx, const float* coef) {
   using namespace stem;
   if (!stem_conv_applies(H, W, CIN, COUT, KS, KS, STR, PAD))
     throw std::runtime_error("stem_conv: unsupported geometry");
-  if (ldw < KS * KS * CIN || (((uintptr_t)x | (uintptr_t)dy) & 15))
+  if (ldw < KS * KS * CIN || (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)bnx) & 15))
     throw std::runtime_error("stem_conv_wgrad: ld >= 392 and 16-B aligned inputs");
+  if ((bnx != nullptr) != (coef != nullptr))
+    throw std::runtime_error("stem_conv_wgrad: the BN prologue needs both bnx and coef");
   if (beta != 0.f && beta != 1.f) throw std::runtime_error("stem_conv_wgrad: beta must be 0 or 1");
   if (beta == 0.f)
     DTFX_HIP_CHECK(hipMemset2DAsync(dw, sizeof(float) * ldw, 0, sizeof(float) * KS * KS * CIN,
@@ -275,8 +308,9 @@ void stem_conv_wgrad_launch(int N, int H, int W, const void* x, const void* dy, 
   const int tiles = N * (OH / TH) * (OW / TW);
   const size_t lds = 128 * DP + P_BYTES;
   const int blocks = std::min(tiles, 256);  // one persistent block per CU: 28 accumulator tiles
-  hipLaunchKernelGGL(stem_conv_wgrad_kernel, dim3(blocks), dim3(256), lds, s, N, H, W, OH, OW,
-                     (const unsigned short*)x, (const unsigned short*)dy, dw, ldw);
+  auto k = bnx ? stem_conv_wgrad_kernel<true> : stem_conv_wgrad_kernel<false>;
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, s, N, H, W, OH, OW, (const unsigned short*)x,
+                     (const unsigned short*)dy, dw, ldw, (const unsigned short*)bnx, coef);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

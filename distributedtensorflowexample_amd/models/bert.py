@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 
 import torch
 
@@ -38,6 +39,12 @@ from ..ops import init as I
 from ..ops import transformer as TR
 
 BF16 = torch.bfloat16
+# DTFX_BERT_WGRAD_BATCH=1: a layer's weight gradients issued to the side stream together after
+# its data-gradient chain (one cross-stream edge per layer instead of per GEMM).  Measured
+# slower, 7,715-7,726 vs 7,916-7,925 seq/s (profiles/r4/bert/wgrad_batch_ab): the per-GEMM
+# edges cost ~15 us of idle GPU each, but starting each weight gradient as soon as its operand
+# exists overlaps more of the data-gradient chain.
+_WGRAD_BATCH = os.environ.get("DTFX_BERT_WGRAD_BATCH", "0") == "1"
 ALIGN = 64
 
 
@@ -294,18 +301,34 @@ class BertMLM:
         ws, keep = self.wgrad_stream, []  # keep: operands the side stream still reads
 
         parts = self._parts
+        pending = []  # (dy, x, name) of the layer being differentiated (batched wgrad issue)
 
         def wgrad(dy, xin, name):  # the only writer of these slots: beta = 0 (zero_grad skips them)
             if ws is None:
                 B16.gemm(dy, xin, True, False, out=p.G(name), beta=0.0, partials=parts.get(name))
+                return
+            if _WGRAD_BATCH:
+                pending.append((dy, xin, name))
                 return
             ws.wait_stream(torch.cuda.current_stream(dy.device))
             with torch.cuda.stream(ws):
                 B16.gemm(dy, xin, True, False, out=p.G(name), beta=0.0, partials=parts.get(name))
             keep.append((dy, xin))
 
+        def flush_wgrads():  # (DTFX_BERT_WGRAD_BATCH=1 only)
+            if not pending:
+                return
+            ws.wait_stream(torch.cuda.current_stream(pending[0][0].device))
+            with torch.cuda.stream(ws):
+                for dy, xin, name in pending:
+                    B16.gemm(dy, xin, True, False, out=p.G(name), beta=0.0,
+                             partials=parts.get(name))
+            keep.extend((dy, xin) for dy, xin, _ in pending)
+            pending.clear()
+
         for l in reversed(range(cfg.layers)):
             dh = self._layer_bwd(l, dh, saved[l], batch, seq, kmask, wgrad)
+            flush_wgrads()
             saved[l] = None
             if on_bucket_ready is not None:
                 if ws is not None and self.wgrad_sync_buckets:

@@ -235,15 +235,23 @@ class ResNet50:
                 on_bucket_ready(bucket)
             bucket -= 1
         img, c, m, r, a, fco = saved["conv1"]
-        if a is None:
+        _, cin, cout, k, s, p = self.specs["conv1"]
+        if a is None and CN.stem_wgrad_bn_applies(img, cout, k, s, p):
+            # the stem weight gradient forms dL/dc from de and c as it stages them
+            de, bco = CN.maxpool_bn_bwd(dx, idx, c, m, r, P.P("conv1.bn.gamma"),
+                                        P.P("conv1.bn.beta"), fco, P.G("conv1.bn.gamma"),
+                                        P.G("conv1.bn.beta"), apply=False)
+            CN.conv_wgrad(de, img, P.G("conv1.weight"), k, k, s, p, beta=1.0, bn_in=(c, bco))
+            dc = de
+        elif a is None:
             dc = CN.maxpool_bn_bwd(dx, idx, c, m, r, P.P("conv1.bn.gamma"), P.P("conv1.bn.beta"),
                                    fco, P.G("conv1.bn.gamma"), P.G("conv1.bn.beta"))
+            CN.conv_wgrad(dc, img, P.G("conv1.weight"), k, k, s, p, beta=1.0)
         else:
             da = CN.maxpool_bwd(dx, idx, a.shape)
             dc, _ = CN.bn_bwd(da, a, c, m, r, P.P("conv1.bn.gamma"), P.G("conv1.bn.gamma"),
                               P.G("conv1.bn.beta"), relu=True, grads_zeroed=True)
-        _, cin, cout, k, s, p = self.specs["conv1"]
-        CN.conv_wgrad(dc, img, P.G("conv1.weight"), k, k, s, p, beta=1.0)
+            CN.conv_wgrad(dc, img, P.G("conv1.weight"), k, k, s, p, beta=1.0)
         if ws is not None:  # join: every gradient final on the main stream
             torch.cuda.current_stream(dc.device).wait_stream(ws)
             self._keep.clear()

@@ -386,10 +386,33 @@ def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, 
     return dx, dc
 
 
-def conv_wgrad(dy, x, dw, KH, KW, stride, pad, beta=1.0):
-    """dw[:, :KH*KW*C] (f32 [Cout, ldw]) (+)= dL/dW."""
+def stem_wgrad_bn_applies(x, Cout, k, stride, pad):
+    """The stem weight-gradient kernel (with its BatchNorm prologue) takes this conv of x
+    (``DTFX_STEM_WGRAD_BN=0``: the separate apply pass, A/B runs)."""
+    N, H, W, C = x.shape
+    return (x.is_cuda and _STEM_WGRAD_BN
+            and bool(hip().stem_conv_applies(H, W, C, Cout, k, k, stride, pad)))
+
+
+_STEM_WGRAD_BN = os.environ.get("DTFX_STEM_WGRAD_BN", "1") != "0"
+
+
+def conv_wgrad(dy, x, dw, KH, KW, stride, pad, beta=1.0, bn_in=None):
+    """dw[:, :KH*KW*C] (f32 [Cout, ldw]) (+)= dL/dW.
+
+    ``bn_in = (c, bcoef)`` (the ResNet stem only, see :func:`maxpool_bn_bwd`): ``dy`` is the
+    gradient at the BatchNorm output behind this conv and the conv output gradient is formed
+    as the kernel stages it, ``dc = bn_bwd_apply(dy, c)`` with the coefficients ``bcoef``."""
     N, H, W, C = x.shape
     Cout = dy.shape[-1]
+    if bn_in is not None:
+        if not (dy.is_cuda and hip().stem_conv_applies(H, W, C, Cout, KH, KW, stride, pad)
+                and beta in (0.0, 1.0)):
+            raise ValueError("conv_wgrad: the BatchNorm prologue is the stem kernel's (GPU)")
+        c, bcoef = bn_in
+        hip().stem_conv_wgrad(N, H, W, ptr(x), ptr(dy), ptr(dw), dw.stride(0), float(beta),
+                              stream_handle(), bnx=ptr(c), coef=ptr(bcoef))
+        return dw
     if not dy.is_cuda:
         g = torch.nn.grad.conv2d_weight(_nchw(x), (Cout, C, KH, KW), _nchw(dy), stride=stride,
                                         padding=pad)
@@ -561,12 +584,14 @@ def bn_maxpool_fwd(c, s, q, M, gamma, beta, eps=1e-5, run_mean=None, run_var=Non
     return y, idx, st[0], st[1], fcoef
 
 
-def maxpool_bn_bwd(dy, idx, c, mean, rstd, gamma, beta, fcoef, dgamma, dbeta):
+def maxpool_bn_bwd(dy, idx, c, mean, rstd, gamma, beta, fcoef, dgamma, dbeta, apply=True):
     """Backward of :func:`bn_maxpool_fwd`: dL/dc from the pool's output gradient ``dy``;
     dgamma / dbeta are the (per-step zeroed) gradient slots, which receive BatchNorm backward's
     two sums.  GPU: one pass gathers the pool gradient, masks it with the ReLU recomputed from
     ``c``, reduces the sums and writes ``de``; the streaming apply reads ``de`` and ``c``
-    (``relu(bn(c))`` is never read or written)."""
+    (``relu(bn(c))`` is never read or written).  ``apply=False`` (GPU): return ``(de,
+    bcoef)`` instead of dL/dc -- the stem weight gradient forms dL/dc itself
+    (:func:`conv_wgrad` ``bn_in``)."""
     if not c.is_cuda:
         a = bn_apply(c, mean, rstd, gamma, beta, None, relu=True)
         da = maxpool_bwd(dy, idx, c.shape)
@@ -576,11 +601,12 @@ def maxpool_bn_bwd(dy, idx, c, mean, rstd, gamma, beta, fcoef, dgamma, dbeta):
     rows = hip().maxpool_bn_bwd_rows(N, H, W, C)
     scratch = torch.empty(2 * rows * C, device=c.device)
     de = torch.empty_like(c)
-    dc = torch.empty_like(c)
+    dc = torch.empty_like(c) if apply else None
+    bcoef = None if apply else torch.empty(4, C, device=c.device)
     hip().maxpool_bn_bwd(N, H, W, C, ptr(dy), ptr(idx), ptr(c), ptr(fcoef), ptr(mean), ptr(rstd),
                          ptr(gamma), ptr(dbeta), ptr(dgamma), ptr(scratch), ptr(de), ptr(dc),
-                         stream_handle())
-    return dc
+                         ptr(bcoef), stream_handle())
+    return dc if apply else (de, bcoef)
 
 
 def maxpool_bwd(dy, idx, x_shape):

@@ -401,3 +401,35 @@ def test_bn_relu_conv1x1_prologue(gpu, N, H, W, K, Co):
     assert (got[1].float() - ref[1].float()).abs().max() < 3e-2 * ref[1].float().abs().max()
     for x_, y_ in zip(got[2:], ref[2:]):
         assert torch.allclose(x_, y_, rtol=2e-2, atol=1e-2 * float(y_.abs().max()) + 1e-4)
+
+
+def test_stem_wgrad_bn_prologue(gpu):
+    """The stem weight gradient forming dL/dc = bn_bwd_apply(de, c) as it stages its dy tile
+    (stem_conv_wgrad_kernel<true>, coefficients from maxpool_bn_bwd(apply=False)) == the apply
+    pass then the plain stem weight gradient."""
+    N, H, W = 2, 32, 32   # stem: 7x7 / 2 -> 16 x 16, 64 channels
+    img = _r(N, H, W, 8, seed=71).to(BF)
+    img[..., 3:] = 0
+    w = torch.zeros(64, cnn.kpad(7, 7, 8))
+    w[:, :392] = _r(64, 392, seed=72, scale=392 ** -0.5)
+    w = w.to(BF)
+    g_ = lambda t: t.to(gpu)  # noqa: E731
+    C = 64
+    cs, cq = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
+    c = cnn.conv_fwd(g_(img), g_(w), 7, 7, 2, 3, colsum=cs, colsq=cq)
+    M = c.numel() // C
+    gam, bet = g_(_r(C, seed=73) * 0.1 + 1), g_(_r(C, seed=74) * 0.1)
+    y, idx, m, r, fco = cnn.bn_maxpool_fwd(c, cs, cq, M, gam, bet)
+    dy = g_(_r(*y.shape, seed=75).to(BF))
+    dg1, db1 = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
+    dg2, db2 = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
+    dc = cnn.maxpool_bn_bwd(dy, idx, c, m, r, gam, bet, fco, dg1, db1)
+    ref = torch.zeros(64, w.shape[1], device=gpu)
+    cnn.conv_wgrad(dc, g_(img), ref, 7, 7, 2, 3, beta=1.0)
+    de, bco = cnn.maxpool_bn_bwd(dy, idx, c, m, r, gam, bet, fco, dg2, db2, apply=False)
+    got = torch.zeros(64, w.shape[1], device=gpu)
+    assert cnn.stem_wgrad_bn_applies(g_(img), 64, 7, 2, 3)
+    cnn.conv_wgrad(de, g_(img), got, 7, 7, 2, 3, beta=1.0, bn_in=(c, bco))
+    assert torch.allclose(dg1, dg2) and torch.allclose(db1, db2)
+    # (both form the same bf16 dc; the f32 atomics sum in different orders)
+    assert (got - ref).abs().max() < 1e-3 * ref.abs().max()
