@@ -611,10 +611,18 @@ __global__ __launch_bounds__(256) void maxpool_bn_fwd_kernel(int N, int H, int W
 }
 
 // The pool gradient of input pixel (n, ih, iw), channels 8 g .. + 7 (maxpool_bwd_kernel's
-// gather), rounded to bf16 as maxpool_bwd stores it.
-__device__ __forceinline__ void maxpool_grad8(int n, int ih, int iw, int g, int cg, int OH, int OW,
-                                              const unsigned short* __restrict__ dy,
-                                              const unsigned char* __restrict__ idx, float* out) {
+// gather), rounded to bf16 as maxpool_bwd stores it.  Branch-free: the (at most 2 x 2)
+// candidate windows are loaded from clamped in-range addresses and masked afterwards, so a
+// caller's two rows' loads can all be in flight together.
+struct PoolCand {
+  uint2 pk[2][2];
+  bf16x8 dv[2][2];
+  unsigned tap[2][2];  // the window tap this pixel is, or 0xFF for no window
+};
+__device__ __forceinline__ void maxpool_grad8_load(int n, int ih, int iw, int g, int cg, int OH,
+                                                   int OW, const unsigned short* __restrict__ dy,
+                                                   const unsigned char* __restrict__ idx,
+                                                   PoolCand& pc) {
   int khc[2], ohc[2], kwc[2], owc[2];
   bool okh[2], okw[2];
   if (ih & 1) {
@@ -631,31 +639,30 @@ __device__ __forceinline__ void maxpool_grad8(int n, int ih, int iw, int g, int 
     kwc[0] = 1; owc[0] = iw >> 1; okw[0] = owc[0] < OW;
     kwc[1] = 1; owc[1] = 0; okw[1] = false;
   }
-  uint2 pk[2][2];
-  bf16x8 dv[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-      if (okh[a] && okw[c]) {
-        const size_t o = (((size_t)n * OH + ohc[a]) * OW + owc[c]) * cg + g;
-        pk[a][c] = ((const uint2*)idx)[o];
-        dv[a][c] = ((const bf16x8*)dy)[o];
-      }
+    for (int c = 0; c < 2; ++c) {
+      const bool ok = okh[a] && okw[c];
+      const size_t o = (((size_t)n * OH + min(ohc[a], OH - 1)) * OW + min(owc[c], OW - 1)) * cg + g;
+      pc.pk[a][c] = ((const uint2*)idx)[o];
+      pc.dv[a][c] = ((const bf16x8*)dy)[o];
+      pc.tap[a][c] = ok ? (unsigned)(khc[a] * 3 + kwc[c]) : 0xFFu;
+    }
+}
+__device__ __forceinline__ void maxpool_grad8_sum(const PoolCand& pc, float* out) {
 #pragma unroll
   for (int u = 0; u < 8; ++u) out[u] = 0.f;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      if (!(okh[a] && okw[c])) continue;
       float d[8];
-      unpack8(dv[a][c], d);
-      const unsigned tap = khc[a] * 3 + kwc[c];
+      unpack8(pc.dv[a][c], d);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const unsigned w = q < 4 ? pk[a][c].x : pk[a][c].y;
-        if (((w >> (8 * (q & 3))) & 0xFF) == tap) out[q] += d[q];
+        const unsigned w = q < 4 ? pc.pk[a][c].x : pc.pk[a][c].y;
+        if (((w >> (8 * (q & 3))) & 0xFF) == pc.tap[a][c]) out[q] += d[q];
       }
     }
 #pragma unroll
@@ -685,21 +692,37 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_kernel(
     s1[u] = s2[u] = 0.f;
   }
   if (live) {
-    for (int row = blockIdx.y; row < N * H; row += gridDim.y) {
-      const int n = row / H, ih = row - n * H;
-      const size_t o = ((size_t)row * W + iw) * cg + g;
-      const bf16x8 xv = ((const bf16x8*)x)[o];
-      float da[8], xf[8];
-      maxpool_grad8(n, ih, iw, g, cg, OH, OW, dy, idx, da);
-      unpack8(xv, xf);
+    // two rows per iteration, every load of both issued before the first use
+    const int NH = N * H, gy = gridDim.y;
+    for (int row = blockIdx.y; row < NH; row += 2 * gy) {
+      int rr[2];
+      rr[0] = row;
+      rr[1] = row + gy < NH ? row + gy : row;  // (a duplicate row: loaded, not stored / summed)
+      PoolCand pc[2];
+      bf16x8 xv[2];
+      size_t o[2];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float de = xf[u] * sa[u] + sb[u] > 0.f ? da[u] : 0.f;
-        da[u] = de;
-        s1[u] += de;
-        s2[u] += de * (xf[u] - mu[u]) * rs[u];
+      for (int k = 0; k < 2; ++k) {
+        const int n = rr[k] / H, ih = rr[k] - n * H;
+        o[k] = ((size_t)rr[k] * W + iw) * cg + g;
+        xv[k] = ((const bf16x8*)x)[o[k]];
+        maxpool_grad8_load(n, ih, iw, g, cg, OH, OW, dy, idx, pc[k]);
       }
-      ((bf16x8*)de_out)[o] = pack8(da);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (k == 1 && row + gy >= NH) break;
+        float da[8], xf[8];
+        maxpool_grad8_sum(pc[k], da);
+        unpack8(xv[k], xf);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float de = xf[u] * sa[u] + sb[u] > 0.f ? da[u] : 0.f;
+          da[u] = de;
+          s1[u] += de;
+          s2[u] += de * (xf[u] - mu[u]) * rs[u];
+        }
+        ((bf16x8*)de_out)[o[k]] = pack8(da);
+      }
     }
   }
 #pragma unroll

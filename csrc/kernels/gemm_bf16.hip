@@ -438,6 +438,12 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   // are not there: f32 outputs, and the 8-phase dgrad with the fused BatchNorm backward
   // (3 side inputs beside 128 accumulators) -- those load at use.
   constexpr bool PREF = !OUT_F32 && !(NBUF == 8 && MODE == 2);
+  // The 8-phase dgrad loads its side inputs per slab right after the slab's accumulators went
+  // to LDS (their registers are free then): one memory round trip per 32-row slab.  Loaded at
+  // use, each of the slab's 4 row groups waited on two dependent round trips (aux / residual,
+  // then bn_x and the BN mean / rstd) -- ~25 us of exposed latency per block on the ResNet-50
+  // layer3 / layer4 data gradients (3x3: 100 us against the forward's 75).
+  constexpr bool LATE = NBUF == 8 && MODE == 2 && !OUT_F32;
   float* ep = (float*)smem + wave * (32 * EP_LD);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
   float cs[8], cq[8];  // fused column sums / sums of squares of this lane's 8 columns
@@ -489,6 +495,9 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
         }
     }
   };
+  // (unrolled for the late prefetch: a slab's accumulators are then known dead once they are in
+  // LDS, and its side inputs take their registers)
+#pragma unroll LATE ? 4 : 1
   for (int h = 0; h < WM / 32; ++h) {
     const int r0 = slab_r0(h), c0 = slab_c0(h);
     // (8-phase: consecutive slabs alternate between the two column halves)
@@ -529,6 +538,24 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             ep[((t & 1) * 16 + row_l + r) * EP_LD + j * 16 + col_l] = acc[t][j][r];
+    if constexpr (LATE) {
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int ns = full[it] ? nn[it] : 0;
+        if (e.act_grad) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)pm[it] * e.ld_aux + ns];
+        if (e.residual) r8[it] = *(const bf16x8*)&e.residual[(size_t)pm[it] * e.ld_res + ns];
+        if (e.bn_x) x8[it] = *(const bf16x8*)&e.bn_x[(size_t)pm[it] * ldc + ns];
+      }
+      if (e.bn_x) {  // the lane's 8 columns are the same for the slab's 4 row groups
+        const int nb = n0 + c0 + (lane & 7) * 8;
+        if ((lane & 7) * 8 < SLW && nb + 8 <= N) {
+          *(f32x4*)&bmu[0] = *(const f32x4*)&e.bn_mean[nb];
+          *(f32x4*)&bmu[4] = *(const f32x4*)&e.bn_mean[nb + 4];
+          *(f32x4*)&brs[0] = *(const f32x4*)&e.bn_rstd[nb];
+          *(f32x4*)&brs[4] = *(const f32x4*)&e.bn_rstd[nb + 4];
+        }
+      }
+    }
     __builtin_amdgcn_wave_barrier();
     if (OUT_F32 && gridDim.y > 1) {
       // split-K partial: alpha only; hardware f32 atomics, one 256-B row segment per
@@ -582,12 +609,12 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           for (int u = 0; u < 8; ++u) v[u] = fmaxf(v[u], 0.f);
         }
         if (MODE != 0 && e.residual) {  // convolutions: shortcut gradient before the mask
-          if (!PREF) r8[it] = *(const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n];
+          if (!PREF && !LATE) r8[it] = *(const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[it][u]);
         }
         if (e.act_grad) {
-          if (!PREF) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)mp * e.ld_aux + n];
+          if (!PREF && !LATE) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)mp * e.ld_aux + n];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             const float uu = bf2f((unsigned short)a8[it][u]);
@@ -603,7 +630,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           if (MODE == 2 && !OUT_F32 && e.bn_x) {
             // statistics of the VALUES STORED (bf16-rounded), as a separate reduction over
             // the output tensor would see them
-            if (!PREF) {  // load at use: x, and the BN mean / rstd of the 8 columns
+            if (!PREF && !LATE) {  // load at use: x, and the BN mean / rstd of the 8 columns
               x8[it] = *(const bf16x8*)&e.bn_x[mp * ldc + n];
               *(f32x4*)&bmu[0] = *(const f32x4*)&e.bn_mean[n];
               *(f32x4*)&bmu[4] = *(const f32x4*)&e.bn_mean[n + 4];
