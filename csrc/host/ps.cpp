@@ -276,14 +276,20 @@ class PSServer {
   }
 
   void serve(int fd) {
-    std::string req, resp;
+    // Request and reply buffers live for the connection: a fresh 318 KB reply string per pull
+    // was an mmap'd allocation (above malloc's mmap threshold) whose pages the kernel zeroed
+    // and faulted in on every request, and the reply was then copied once more behind its
+    // header -- both on the ps's critical path, which bounds the async cluster's step rate.
+    std::string req;
+    std::vector<iovec> iov(2);
+    Writer w;
     while (running_) {
       uint32_t len;
       if (!read_full(fd, &len, 4)) break;
       req.resize(len);
       if (!read_full(fd, &req[0], len)) break;
       bytes_in_ += len + 4;
-      Writer w;
+      w.b.clear();
       uint8_t status = 0;
       try {
         handle(req, w);
@@ -291,13 +297,16 @@ class PSServer {
         status = 1;
         w.b = e.what();
       }
+      char hdr[5];
       const uint32_t rl = static_cast<uint32_t>(w.b.size() + 1);
-      resp.clear();
-      resp.append(reinterpret_cast<const char*>(&rl), 4);
-      resp.push_back(static_cast<char>(status));
-      resp.append(w.b);
-      bytes_out_ += resp.size();
-      if (!write_full(fd, resp.data(), resp.size())) break;
+      std::memcpy(hdr, &rl, 4);
+      hdr[4] = static_cast<char>(status);
+      bytes_out_ += 5 + w.b.size();
+      iov.resize(2);
+      iov[0] = iovec{hdr, 5};
+      iov[1] = iovec{const_cast<char*>(w.b.data()), w.b.size()};
+      if (w.b.empty()) iov.resize(1);
+      if (!writev_full(fd, iov)) break;
     }
     // deregister before closing: stop() shuts down the fds in conns_, and a closed fd number
     // can be reused by any other socket of the process
