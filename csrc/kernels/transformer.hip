@@ -716,6 +716,186 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_kernel(
   }
 }
 
+// Persistent attention backward: one block per CU walks (sequence, head) pairs; the NEXT
+// pair's Q, K, V, dO and O are loaded into registers while the current pair computes (the
+// per-block form waited out its 80 KB of loads, then computed: ~14 us per pair at BERT-base
+// seq 128 for ~1 us of MFMA work, one resident block per CU).  The same math and LDS layout as
+// attn_bwd_kernel<8>; rowsum(dO * O) comes from the prefetched registers.
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 1) void attn_bwd_persist_kernel(
+    int S, int nh, int npairs, const unsigned short* __restrict__ qkv,
+    const unsigned short* __restrict__ o, const unsigned short* __restrict__ dout,
+    const float* __restrict__ lse, const float* __restrict__ kmask, float scale,
+    unsigned short* __restrict__ dqkv, float* __restrict__ dbias) {
+  using namespace at;
+  constexpr int NT = NW * 64, RPW = SP / NW, NI = RPW / 16, PER = SP * 8 / NT;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* Qs = sm;
+  char* Ks = sm + QB;
+  char* Vs = sm + 2 * QB;
+  char* dOs = sm + 3 * QB;
+  char* Ps = sm + 4 * QB;
+  char* dSs = Ps + PB;
+  float* Dr = (float*)(dSs + PB);
+  const int Hd = nh * D, ld = 3 * Hd;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int cl = lane & 15, rg = (lane >> 4) * 4;
+  // prefetch registers: [tensor Q K V dO O][chunk k]; thread chunk i = tid + NT k: row i >> 3,
+  // 16-B column chunk i & 7
+  bf16x8 pf[5][PER];
+  auto prefetch = [&](int pair) {
+    const int b = pair / nh, h = pair % nh;
+    const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
+    const unsigned short* src[5] = {base, base + Hd, base + 2 * Hd,
+                                    dout + (size_t)b * S * Hd + h * D, o + (size_t)b * S * Hd + h * D};
+    const int lds_[5] = {ld, ld, ld, Hd, Hd};
+#pragma unroll
+    for (int n = 0; n < 5; ++n)
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = threadIdx.x + NT * k, r = i >> 3, c = i & 7;
+        pf[n][k] = *(const bf16x8*)(src[n] + (size_t)min(r, S - 1) * lds_[n] + c * 8);
+      }
+  };
+  int pair = blockIdx.x;
+  if (pair < npairs) prefetch(pair);
+  for (; pair < npairs; pair += gridDim.x) {
+    const int b = pair / nh, h = pair % nh;
+    __syncthreads();  // the previous pair's LDS reads are done
+    {
+      char* const dst[4] = {Qs, Ks, Vs, dOs};
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = threadIdx.x + NT * k, r = i >> 3, c = i & 7;
+        float dsum = 0.f;
+        if (r < S) {
+          float ov[8], dv[8];
+          unpack8(pf[4][k], ov);
+          unpack8(pf[3][k], dv);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) dsum += ov[u] * dv[u];
+        }
+        // the 8 chunks of a row sit in 8 consecutive lanes
+        dsum += __shfl_xor(dsum, 1);
+        dsum += __shfl_xor(dsum, 2);
+        dsum += __shfl_xor(dsum, 4);
+        if (c == 0) Dr[r] = dsum;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          bf16x8 v = pf[n][k];
+          if (r >= S) v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+          *(bf16x8*)(dst[n] + r * LDQ + c * 16) = v;
+        }
+      }
+    }
+    if (pair + (int)gridDim.x < npairs) prefetch(pair + gridDim.x);  // in flight below
+    __syncthreads();
+    const float* L = lse + ((size_t)b * nh + h) * SP;
+    float km[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int key = 16 * j + cl;
+      km[j] = key < S ? (kmask ? kmask[(size_t)b * S + key] : 0.f) : -INFINITY;
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int r0 = RPW * wave + 16 * i;
+      f32x4 sacc[8], dp[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sacc[j] = dp[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 aq = lfrag<true>(Qs, LDQ, r0, 32 * kk, lane);
+        const bf16x8 ado = lfrag<true>(dOs, LDQ, r0, 32 * kk, lane);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sacc[j] = mma(aq, lfrag<true>(Ks, LDQ, 16 * j, 32 * kk, lane), sacc[j]);
+          dp[j] = mma(ado, lfrag<true>(Vs, LDQ, 16 * j, 32 * kk, lane), dp[j]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + rg + r;
+        const bool live = row < S;
+        const float lr = live ? L[row] : 0.f, dr = Dr[row];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float pv = live ? __expf(sacc[j][r] * scale + km[j] - lr) : 0.f;
+          const float ds = pv * (dp[j][r] - dr);
+          *(unsigned short*)(Ps + row * LDP + (16 * j + cl) * 2) = tobf(pv);
+          *(unsigned short*)(dSs + row * LDP + (16 * j + cl) * 2) = tobf(ds);
+        }
+      }
+    }
+    __syncthreads();
+    unsigned short* dq = dqkv + (size_t)b * S * ld + h * D;
+    unsigned short* dk = dq + Hd;
+    unsigned short* dv = dq + 2 * Hd;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int k0 = RPW * wave + 16 * i;
+      f32x4 av[4], ak[4], aq[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) av[j] = ak[j] = aq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const bf16x8 pT = lfrag<false>(Ps, LDP, k0, 32 * kk, lane);
+        const bf16x8 dsT = lfrag<false>(dSs, LDP, k0, 32 * kk, lane);
+        const bf16x8 dsr = lfrag<true>(dSs, LDP, k0, 32 * kk, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          av[j] = mma(pT, lfrag<false>(dOs, LDQ, 16 * j, 32 * kk, lane), av[j]);
+          ak[j] = mma(dsT, lfrag<false>(Qs, LDQ, 16 * j, 32 * kk, lane), ak[j]);
+          aq[j] = mma(dsr, lfrag<false>(Ks, LDQ, 16 * j, 32 * kk, lane), aq[j]);
+        }
+      }
+      char* stg = Vs + (size_t)k0 * LDQ;  // this wave's V rows: consumed above
+      auto put = [&](const f32x4 (&acc)[4], float mul, unsigned short* dst) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            *(unsigned short*)(stg + (rg + r) * LDQ + (16 * j + cl) * 2) = tobf(acc[j][r] * mul);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = lane + 64 * u, row = k0 + (c >> 3), ch = c & 7;
+          const bf16x8 v = *(const bf16x8*)(stg + (c >> 3) * LDQ + ch * 16);
+          if (row < S) *(bf16x8*)(dst + (size_t)row * ld + ch * 8) = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+      };
+      put(av, 1.f, dv);
+      put(ak, scale, dk);
+      put(aq, scale, dq);
+      if (dbias) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float sq = 0.f, sk = 0.f, sv = 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            sq += aq[j][r];
+            sk += ak[j][r];
+            sv += av[j][r];
+          }
+          sq += __shfl_xor(sq, 16);
+          sq += __shfl_xor(sq, 32);
+          sk += __shfl_xor(sk, 16);
+          sk += __shfl_xor(sk, 32);
+          sv += __shfl_xor(sv, 16);
+          sv += __shfl_xor(sv, 32);
+          if (lane < 16) {
+            const int c = h * D + 16 * j + cl;
+            unsafeAtomicAdd(dbias + c, sq * scale);
+            unsafeAtomicAdd(dbias + Hd + c, sk * scale);
+            unsafeAtomicAdd(dbias + 2 * Hd + c, sv);
+          }
+        }
+      }
+    }
+  }
+}
+
 // Attention backward in two query halves: the same math as attn_bwd_kernel with 72 KB of LDS
 // instead of 141 KB, so two blocks share a CU (the first version's single resident block
 // left every global-load and barrier latency exposed: 69 us at BERT-base's seq 128 against
@@ -1234,7 +1414,8 @@ void attn_fwd_launch(int Bn, int S, int nh, const void* qkv, void* out, float* l
 }
 
 // Attention-backward kernel: -1 = from the environment, 0: attn_bwd_kernel<8>,
-// 1: attn_bwd_kernel<4>, 2: attn_bwd_half_kernel (tests run every variant in one process).
+// 1: attn_bwd_kernel<4>, 2: attn_bwd_half_kernel, 3: attn_bwd_persist_kernel, 4: the same on a
+// 3-block grid (tests run every variant in one process).
 static int g_attn_bwd_variant = -1;
 void attn_bwd_set_variant(int v) { g_attn_bwd_variant = v; }
 
@@ -1263,8 +1444,31 @@ void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, cons
     const char* e = std::getenv("DTFX_ATTN_BWD_HALF");
     return e && std::atoi(e) == 1;
   }();
-  const int var = g_attn_bwd_variant >= 0 ? g_attn_bwd_variant : half ? 2 : nw == 4 ? 1 : 0;
-  if (var == 2) {
+  // DTFX_ATTN_BWD_PERSIST=1: the persistent kernel (grid: DTFX_ATTN_BWD_BLOCKS, default one
+  // block per CU)
+  static const bool persist = [] {
+    const char* e = std::getenv("DTFX_ATTN_BWD_PERSIST");
+    return e && std::atoi(e) == 1;
+  }();
+  const int var = g_attn_bwd_variant >= 0 ? g_attn_bwd_variant : persist ? 3 : half ? 2 : nw == 4 ? 1 : 0;
+  if (var == 3 || var == 4) {
+    // 4 waves: one per SIMD with up to 512 registers each -- the 8-wave form's 40 prefetch
+    // registers spilled
+    static bool pattr = false;
+    if (!pattr) {
+      DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_persist_kernel<4>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      pattr = true;
+    }
+    static const int blocks = [] {
+      const char* e = std::getenv("DTFX_ATTN_BWD_BLOCKS");
+      return e && std::atoi(e) > 0 ? std::atoi(e) : 256;
+    }();
+    const int np = Bn * nh, nb = var == 4 ? 3 : blocks;  // 4: a 3-block grid (tests: many pairs per block)
+    hipLaunchKernelGGL(attn_bwd_persist_kernel<4>, dim3(std::min(np, nb)), dim3(256), lds, s, S, nh,
+                       np, (const unsigned short*)qkv, (const unsigned short*)o,
+                       (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv, dbias);
+  } else if (var == 2) {
     static bool hattr = false;
     if (!hattr) {
       DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_half_kernel,

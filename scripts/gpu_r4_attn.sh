@@ -1,0 +1,14 @@
+# persistent attention backward: tests, standalone timing of every variant, BERT A/B
+set -o pipefail
+mkdir -p gpurun_out/attn
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_transformer_gpu.py tests/test_bert_gpu.py > gpurun_out/attn/t.log 2>&1 || exit 1
+timeout -k 10 120 python tools/probes/attn_one.py 20 > gpurun_out/attn/one_default.json 2>&1 || exit 1
+DTFX_ATTN_BWD_PERSIST=1 timeout -k 10 120 python tools/probes/attn_one.py 20 > gpurun_out/attn/one_persist.json 2>&1 || exit 1
+DTFX_ATTN_BWD_PERSIST=1 DTFX_ATTN_BWD_BLOCKS=128 timeout -k 10 120 python tools/probes/attn_one.py 20 > gpurun_out/attn/one_persist128.json 2>&1 || exit 1
+DTFX_ATTN_BWD_HALF=1 timeout -k 10 120 python tools/probes/attn_one.py 20 > gpurun_out/attn/one_half.json 2>&1 || exit 1
+for r in 1 2; do
+  timeout -k 10 300 python bench.py --model bert > gpurun_out/attn/bert_default_$r.json 2>/dev/null || exit 1
+  DTFX_ATTN_BWD_PERSIST=1 timeout -k 10 300 python bench.py --model bert > gpurun_out/attn/bert_persist_$r.json 2>/dev/null || exit 1
+  DTFX_ATTN_BWD_PERSIST=1 DTFX_ATTN_BWD_BLOCKS=128 timeout -k 10 300 python bench.py --model bert > gpurun_out/attn/bert_persist128_$r.json 2>/dev/null || exit 1
+done
+echo done

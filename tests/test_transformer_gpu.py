@@ -53,7 +53,7 @@ def test_embedding_fwd_bwd(gpu):
         assert torch.allclose(a.cpu(), b, atol=1e-3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])  # 3 / 4: persistent (4: 3 blocks, 4 pairs each)
 @pytest.mark.parametrize("S,masked", [(128, False), (128, True), (77, True), (64, False), (33, True)])
 def test_attention_fwd_bwd(gpu, S, masked, variant):
     B, nh = 3, 4
