@@ -630,18 +630,29 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_kernel(
         dp[j] = mma(ado, lfrag<true>(Vs, LDQ, 16 * j, 32 * kk, lane), dp[j]);
       }
     }
+    // P and dS are stored TRANSPOSED ([key][query]): a lane's 4 accumulator rows are 4
+    // consecutive queries of one key, one 8-B store each (the row-major 2-B stores were a
+    // quarter of the kernel's LDS instructions and most of its bank-conflict cycles)
+    float lr[4], dr[4];
+    bool live[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = r0 + rg + r;
-      const bool live = row < S;
-      const float lr = live ? L[row] : 0.f, dr = Dr[row];
+      live[r] = row < S;
+      lr[r] = live[r] ? L[row] : 0.f;
+      dr[r] = Dr[row];
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float p = live ? __expf(s[j][r] * scale + km[j] - lr) : 0.f;
-        const float ds = p * (dp[j][r] - dr);
-        *(unsigned short*)(Ps + row * LDP + (16 * j + cl) * 2) = tobf(p);
-        *(unsigned short*)(dSs + row * LDP + (16 * j + cl) * 2) = tobf(ds);
+    for (int j = 0; j < 8; ++j) {
+      bf16x4 p4, d4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = live[r] ? __expf(s[j][r] * scale + km[j] - lr[r]) : 0.f;
+        p4[r] = (short)tobf(p);
+        d4[r] = (short)tobf(p * (dp[j][r] - dr[r]));
       }
+      *(bf16x4*)(Ps + (16 * j + cl) * LDP + (r0 + rg) * 2) = p4;
+      *(bf16x4*)(dSs + (16 * j + cl) * LDP + (r0 + rg) * 2) = d4;
     }
   }
   __syncthreads();
@@ -657,9 +668,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_kernel(
     for (int j = 0; j < 4; ++j) av[j] = ak[j] = aq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      const bf16x8 pT = lfrag<false>(Ps, LDP, k0, 32 * kk, lane);
-      const bf16x8 dsT = lfrag<false>(dSs, LDP, k0, 32 * kk, lane);
-      const bf16x8 dsr = lfrag<true>(dSs, LDP, k0, 32 * kk, lane);
+      const bf16x8 pT = lfrag<true>(Ps, LDP, k0, 32 * kk, lane);    // (P^T, dS^T stored)
+      const bf16x8 dsT = lfrag<true>(dSs, LDP, k0, 32 * kk, lane);
+      const bf16x8 dsr = lfrag<false>(dSs, LDP, k0, 32 * kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         av[j] = mma(pT, lfrag<false>(dOs, LDQ, 16 * j, 32 * kk, lane), av[j]);
@@ -813,18 +824,26 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_persist_kernel(
           dp[j] = mma(ado, lfrag<true>(Vs, LDQ, 16 * j, 32 * kk, lane), dp[j]);
         }
       }
+      float lr[4], dr[4];
+      bool live[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = r0 + rg + r;
-        const bool live = row < S;
-        const float lr = live ? L[row] : 0.f, dr = Dr[row];
+        live[r] = row < S;
+        lr[r] = live[r] ? L[row] : 0.f;
+        dr[r] = Dr[row];
+      }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float pv = live ? __expf(sacc[j][r] * scale + km[j] - lr) : 0.f;
-          const float ds = pv * (dp[j][r] - dr);
-          *(unsigned short*)(Ps + row * LDP + (16 * j + cl) * 2) = tobf(pv);
-          *(unsigned short*)(dSs + row * LDP + (16 * j + cl) * 2) = tobf(ds);
+      for (int j = 0; j < 8; ++j) {  // P^T, dS^T: one 8-B store per key (see attn_bwd_kernel)
+        bf16x4 p4, d4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = live[r] ? __expf(sacc[j][r] * scale + km[j] - lr[r]) : 0.f;
+          p4[r] = (short)tobf(pv);
+          d4[r] = (short)tobf(pv * (dp[j][r] - dr[r]));
         }
+        *(bf16x4*)(Ps + (16 * j + cl) * LDP + (r0 + rg) * 2) = p4;
+        *(bf16x4*)(dSs + (16 * j + cl) * LDP + (r0 + rg) * 2) = d4;
       }
     }
     __syncthreads();
@@ -839,9 +858,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_persist_kernel(
       for (int j = 0; j < 4; ++j) av[j] = ak[j] = aq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8 pT = lfrag<false>(Ps, LDP, k0, 32 * kk, lane);
-        const bf16x8 dsT = lfrag<false>(dSs, LDP, k0, 32 * kk, lane);
-        const bf16x8 dsr = lfrag<true>(dSs, LDP, k0, 32 * kk, lane);
+        const bf16x8 pT = lfrag<true>(Ps, LDP, k0, 32 * kk, lane);
+        const bf16x8 dsT = lfrag<true>(dSs, LDP, k0, 32 * kk, lane);
+        const bf16x8 dsr = lfrag<false>(dSs, LDP, k0, 32 * kk, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           av[j] = mma(pT, lfrag<false>(dOs, LDQ, 16 * j, 32 * kk, lane), av[j]);
@@ -1445,7 +1464,10 @@ void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, cons
     return e && std::atoi(e) == 1;
   }();
   // DTFX_ATTN_BWD_PERSIST=1: the persistent kernel (grid: DTFX_ATTN_BWD_BLOCKS, default one
-  // block per CU)
+  // block per CU).  Measured slower: 84 us standalone vs 68 for the 8-wave per-pair kernel (128
+  // blocks: 144 us), BERT 7,922-7,947 vs 7,960-8,003 seq/s (profiles/r4/bert/attn_persist/):
+  // the pairs are not load-latency-bound but bound inside their compute phases (~11 us per
+  // pair per CU against ~1 us of MFMA work), which one wave per SIMD hides worse.
   static const bool persist = [] {
     const char* e = std::getenv("DTFX_ATTN_BWD_PERSIST");
     return e && std::atoi(e) == 1;
