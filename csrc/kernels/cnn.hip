@@ -918,6 +918,7 @@ void bn_bwd_launch(long long M, int C, const void* dy, const void* yout, const v
                      (const unsigned short*)x, mean, rstd, relu, part_dy, part_dyxh);
   DTFX_HIP_CHECK(hipGetLastError());
   colpart_reduce_launch((int)blocks, C, part_dy, part_dyxh, sum_dy, sum_dyxh, st);
+  if (!dx && !dres) return;  // reductions only (the apply runs in a consumer's prologue)
   hipLaunchKernelGGL(bn_bwd_apply_kernel<kEwU>, dim3(grid_once(M * C / 8, kEwU)), dim3(256), 0, st, M, C,
                      (const unsigned short*)dy, (const unsigned short*)yout,
                      (const unsigned short*)x, mean, rstd, gamma, sum_dy, sum_dyxh, relu,

@@ -451,6 +451,13 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
 // column, so its 8 channels' coefficients stay in registers), one barrier, then the MFMAs read
 // it as before.  The loader wave moves both sources (twice the tile bytes: half the pixels per
 // tile).
+//   PRO 4 (plain data gradient): PRO 2's operand without a BatchNorm behind the conv's input --
+//         no ReLU mask, no side tiles, no statistics (the stride-1 downsample conv of ResNet's
+//         first block: its own BN's backward apply in the prologue).
+template <bool DG, int PRO>
+constexpr bool nside() {  // the data gradient's relu_y / bn_x side tiles ride along
+  return DG && PRO != 4;
+}
 template <int K, int N_, bool DG, int PRO = 0>
 constexpr int ntm() {  // pixels per tile (LDS: 3-4 ring stages + the f32 staging)
   return PRO ? ((K == 512 || (DG && N_ == 128)) ? 16 : 32) : DG ? (N_ == 64 ? 32 : 16) : (N_ == 64 ? 64 : 32);
@@ -458,7 +465,7 @@ constexpr int ntm() {  // pixels per tile (LDS: 3-4 ring stages + the f32 stagin
 template <int K, int N_, bool DG, int PRO = 0>
 constexpr int nqt_narrow() {  // DMA instructions per tile
   return ntm<K, N_, DG, PRO>() * K * 2 * (PRO ? 2 : 1) / 1024 +
-         (DG ? 2 * ntm<K, N_, DG, PRO>() * N_ * 2 / 1024 : 0);
+         (nside<DG, PRO>() ? 2 * ntm<K, N_, DG, PRO>() * N_ * 2 / 1024 : 0);
 }
 
 template <int K, int N_, bool DG, int PRO>
@@ -473,7 +480,8 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
   constexpr int TM = ntm<K, N_, DG, PRO>(), MT = TM / 16;
   constexpr int XB = TM * K * 2, SB = TM * N_ * 2;
   constexpr int XS = XB * (PRO ? 2 : 1);  // side tiles (relu_y, bn_x) after the source tile(s)
-  constexpr int STAGE = XS + (DG ? 2 * SB : 0);
+  constexpr bool SIDE = nside<DG, PRO>();
+  constexpr int STAGE = XS + (SIDE ? 2 * SB : 0);
   constexpr int NQX = XB / 1024, NQS = SB / 1024, NQT = nqt_narrow<K, N_, DG, PRO>();
   constexpr int DB = 2 * NQT <= 63 ? 4 : 3, D = DB - 1;
   static_assert(!PRO || (512 % CPR == 0 && TM % (512 / CPR) == 0), "PRO: whole chunk columns");
@@ -505,7 +513,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
           __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(d + XB + q * 1024), 16, 0, 0);
         }
       }
-      if constexpr (DG) {
+      if constexpr (SIDE) {
 #pragma unroll
         for (int si = 0; si < 2; ++si) {
           const unsigned short* side = si == 0 ? relu_y : bn_x;
@@ -534,7 +542,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
       __syncthreads();
       __syncthreads();
     }
-    __syncthreads();  // (the statistics reduction)
+    if constexpr (!DG || SIDE) __syncthreads();  // (the statistics reduction)
     return;
   }
   const int nt = wave % NT, part = wave / NT, kk0 = part * KKW;
@@ -612,7 +620,10 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
           }
         }
         bf16x8 o;
-        if constexpr (DG) {
+        if constexpr (DG && !SIDE) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) o[u] = (short)tobf(v[u]);
+        } else if constexpr (DG) {
           const bf16x8 y8 = *(const bf16x8*)(buf + XS + p * (N_ * 2) + c * 16);
           const bf16x8 x8 = *(const bf16x8*)(buf + XS + SB + p * (N_ * 2) + c * 16);
 #pragma unroll
@@ -635,6 +646,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
     }
     __syncthreads();
   }
+  if constexpr (DG && !SIDE) return;
   // statistics: thread tid owns channels 8 (tid % NCH) .. + 7; sum the 512 / NCH owners
   float* red = (float*)sm;  // the ring is idle now: [512][16]
 #pragma unroll
@@ -710,7 +722,7 @@ static void conv1x1_narrow_go(int M, const void* x, const void* w, void* y, cons
   using namespace pw;
   constexpr int TM = ntm<K, N_, DG, PRO>(), NQT = nqt_narrow<K, N_, DG, PRO>();
   constexpr int DB = 2 * NQT <= 63 ? 4 : 3;
-  constexpr size_t ring = (size_t)DB * (TM * K * 2 * (PRO ? 2 : 1) + (DG ? 2 * TM * N_ * 2 : 0));
+  constexpr size_t ring = (size_t)DB * (TM * K * 2 * (PRO ? 2 : 1) + (nside<DG, PRO>() ? 2 * TM * N_ * 2 : 0));
   constexpr size_t lds = ring + (size_t)(8 / (N_ / 16)) * TM * (N_ * 4 + 16);
   static_assert(ring >= 512 * 16 * 4, "the statistics reduction reuses the ring");
   static_assert(lds <= 160 * 1024, "LDS");
@@ -875,7 +887,7 @@ void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const voi
   const bool narrow = conv1x1_narrow(K, N);
   if (!s0 || !coef || (mode != 3 && !s1) || ((mode == 1 || mode == 3) && (!xo || !ps || !pq)) ||
       (mode == 1 && ldw != K) || (mode == 2 && !wt) ||
-      (mode == 2 && narrow && (!relu_y || !bn_x || !mean || !rstd || !ps || res)) ||
+      (mode == 2 && narrow && res) || (mode == 2 && !ps && narrow && (relu_y || bn_x)) ||
       ((ps != nullptr) != (pq != nullptr)) || (mode == 2 && ps && (!relu_y || !bn_x || !mean || !rstd)))
     throw std::runtime_error("conv1x1_pro: sources, coefficients, statistics (and for the data "
                              "gradient wt, relu_y, bn_x, mean, rstd) required");
@@ -895,9 +907,12 @@ void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const voi
     if (mode == 1)                                                                              \
       conv1x1_narrow_go<KV, NV, false, 1>(M, s0, wv, y, nullptr, nullptr, nullptr, nullptr, ps, pq, \
                                           s, s1, coef, xo);                                     \
-    else                                                                                        \
+    else if (ps)                                                                                \
       conv1x1_narrow_go<KV, NV, true, 2>(M, s0, wv, y, relu_y, bn_x, mean, rstd, ps, pq, s, s1, \
                                          coef, xo);                                             \
+    else                                                                                        \
+      conv1x1_narrow_go<KV, NV, true, 4>(M, s0, wv, y, nullptr, nullptr, nullptr, nullptr,      \
+                                         nullptr, nullptr, s, s1, coef, xo);                    \
   } while (0)
     if (K == 256 && N == 64) DTFX_PW_PRO(256, 64);
     else if (K == 256) DTFX_PW_PRO(256, 128);

@@ -39,6 +39,7 @@ BF16 = torch.bfloat16
 ALIGN = 64
 # the stem's BatchNorm + ReLU fused into its max pool (DTFX_STEM_POOL_BN=0: separate passes)
 _STEM_POOL_BN = os.environ.get("DTFX_STEM_POOL_BN", "1") != "0"
+_DS_PRO = os.environ.get("DTFX_DS_PROLOGUE", "1") != "0"  # stride-1 downsample BN apply in its dgrad
 STAGES = [(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)]  # (width, blocks, stride)
 IN_CH = 8          # 3 image channels + 5 zero channels
 NUM_CLASSES = 1000
@@ -318,10 +319,10 @@ class ResNet50:
         blocks[i][6] = out
         return out, c1, s1
 
-    def _bn_bwd(self, name, dy, y, x, mean, rstd, relu=True, want_dres=False):
+    def _bn_bwd(self, name, dy, y, x, mean, rstd, relu=True, want_dres=False, apply=True):
         P = self.params
         return CN.bn_bwd(dy, y, x, mean, rstd, P.P(name + ".bn.gamma"), P.G(name + ".bn.gamma"),
-                         P.G(name + ".bn.beta"), relu, want_dres, grads_zeroed=True)
+                         P.G(name + ".bn.beta"), relu, want_dres, grads_zeroed=True, apply=apply)
 
     def _bn_fused(self, name, y, x, mean, rstd):
         """``bn`` argument of CN.conv_dgrad: BatchNorm ``name`` (input x, post-ReLU output y)
@@ -372,8 +373,19 @@ class ResNet50:
             dc3, dres = self._bn_bwd(n3, dout, out, c3, m3, r3, relu=True, want_dres=True)
         if ds is not None:
             cs_, ms, rs = ds
-            dcs, _ = self._bn_bwd(pre + "downsample", dres, None, cs_, ms, rs, relu=False)
-            dshort = self._wgrad_dgrad(pre + "downsample", dcs, x_in)
+            nd = pre + "downsample"
+            if _DS_PRO and self.specs[nd][4] == 1 and CN.bn_prologue_applies(cs_, cs_.shape[-1],
+                                                                 x_in.shape[-1], 2):
+                # stride-1 downsample (layer1.0): its BN's reductions, then the apply inside the
+                # narrow data gradient's prologue (dcs written for the weight gradient)
+                self._bn_bwd(nd, dres, None, cs_, ms, rs, relu=False, apply=False)
+                dshort, dcs = CN.bn_in_conv1x1_dgrad(dres, cs_, ms, rs, P.P(nd + ".bn.gamma"),
+                                                     P.G(nd + ".bn.beta"), P.G(nd + ".bn.gamma"),
+                                                     P.W(nd + ".weight"))
+                self._wgrad_dgrad(nd, dcs, x_in, need_dx=False)
+            else:
+                dcs, _ = self._bn_bwd(nd, dres, None, cs_, ms, rs, relu=False)
+                dshort = self._wgrad_dgrad(nd, dcs, x_in)
         else:
             dshort = dres
         bn2 = self._bn_fused(pre + "conv2", a2, c2, m2, r2)

@@ -353,8 +353,8 @@ def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, 
     gradient ``dc = bn_bwd_apply(de, c, ...)`` is formed inside the 1x1 dgrad kernel's prologue
     (PRO 2) and written out when ``want_dc`` (the weight gradient reads it); the product is
     ``conv_dgrad(dc, w, residual=residual, bn=bn)`` -- with ``bn = (y, x, mean, rstd, sum_dy,
-    sum_dyxh)`` the fused BatchNorm backward of the conv's own input (required on the narrow
-    kernels).  Returns (dx, dc)."""
+    sum_dyxh)`` the fused BatchNorm backward of the conv's own input (optional: without it
+    the narrow kernels run the plain data gradient, PRO 4).  Returns (dx, dc)."""
     if not de.is_cuda:
         dc = bn_bwd_apply(de, c, mean, rstd, gamma, sum_dy, sum_dyxh)
         N, H, W, _ = c.shape
@@ -507,9 +507,11 @@ def bn_apply_stats(x, s, q, M, gamma, beta, residual=None, relu=True, eps=1e-5, 
 
 
 def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, relu=True, want_dres=False,
-           grads_zeroed=False):
+           grads_zeroed=False, apply=True):
     """Backward of y = act(bn(x) [+ res]).  Accumulates dgamma/dbeta; returns (dx, dres)
     where dres = dy * act'(y) is the gradient of the residual input (if requested).
+    ``apply=False`` (GPU, no ReLU): only the reductions -- the caller forms dx in a consumer's
+    prologue (:func:`bn_in_conv1x1_dgrad`); returns (None, None).
 
     ``grads_zeroed=True`` (the model's per-step zeroed gradient slots) lets the GPU kernels
     reduce straight into dgamma / dbeta -- they are exactly sum(dy_eff * xhat) / sum(dy_eff)
@@ -530,9 +532,11 @@ def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, relu=True, want_dres=Fals
     else:
         sums = torch.zeros(2, C, device=x.device)
         sdy, sdx = sums[0], sums[1]
+    if not apply and (relu or want_dres):
+        raise ValueError("bn_bwd(apply=False): reductions of an un-masked gradient only")
     rows = hip().bn_bwd_scratch_rows(M, C)
     scratch = torch.empty(2 * rows * C, device=x.device)
-    dx = torch.empty_like(x)
+    dx = torch.empty_like(x) if apply else None
     dres = torch.empty_like(x) if want_dres else None
     hip().bn_bwd(M, C, ptr(dy), ptr(y), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), int(relu),
                  ptr(sdy), ptr(sdx), ptr(scratch), ptr(dx), ptr(dres), stream_handle())

@@ -288,6 +288,8 @@ def test_bn_out_conv1x1_prologue(gpu, N, H, W, K, Co, ds):
     (2, 16, 16, 64, 256, False, True),    # layer1 conv3 data gradient (narrow 256 -> 64)
     (4, 8, 8, 128, 512, False, True),     # layer2 conv3 (narrow 512 -> 128, 16-pixel tiles)
     (3, 16, 20, 64, 256, False, True),    # M = 960
+    (2, 16, 16, 64, 256, False, False),   # layer1.0 downsample (narrow, plain: PRO 4)
+    (4, 8, 8, 128, 512, False, False),    # narrow 512 -> 128 plain
     (2, 16, 16, 256, 64, True, True),     # layer1 conv1 (wide 64 -> 256, + shortcut gradient)
     (2, 16, 16, 256, 64, True, False),    # first block's conv1: shortcut only, no BN behind
     (2, 8, 8, 512, 128, True, True),      # layer2 conv1 (two column blocks: xo from one)
