@@ -14,8 +14,12 @@
 // and transposed, W'[ci][tap][co] = W[co][8 - tap][ci]: conv3x3_c128_flip builds W' once per
 // call into a workspace, then the same kernel runs with the BN-backward epilogue.
 //
-// 8 waves: wave w owns output channel block w (of 16) and all 7 pixel groups (of 16): 7 MFMA
-// tiles, 8 LDS fragment reads per k-group.
+// 8 waves: wave w owns output channels 32 (w & 3) .. + 31 and input-channel half w >> 2 (the K
+// split) for all 7 pixel groups (of 16): 14 MFMA tiles, per k-group 7 A + 2 B fragment reads for
+// 14 MFMAs.  The first version (wave = 16 output channels x the whole K: 7 A + 1 B reads per 7
+// MFMAs) was LDS-bandwidth-bound at ~2.3x its MFMA time (every A fragment read fed one MFMA).
+// The two K halves are summed through LDS after the last tap: wave (cb, 0) finalises pixel
+// groups 0-3, wave (cb, 1) groups 4-6, each writing the other's groups first.
 #include "common.h"
 
 #include <algorithm>
@@ -33,7 +37,9 @@ constexpr int P_BYTES = PH * PW * C * 2;                          // 46080
 constexpr int PCH = PH * PW * NCH;                                // 2880 patch chunks
 constexpr int WT_PITCH = C * 2 + 16;                              // 272 B per weight row
 constexpr int WT_BYTES = C * WT_PITCH;                            // 34816 per tap slice
-constexpr int LDS = P_BYTES + 2 * WT_BYTES;                       // 115712
+constexpr int R_BYTES = 4 * 2 * 7 * 64 * 16;                       // K-half partials 57344
+constexpr int S_BYTES = R_BYTES > P_BYTES ? R_BYTES : P_BYTES;     // patch / partials / staging
+constexpr int LDS = S_BYTES + 2 * WT_BYTES;                       // 126976
 
 __device__ __forceinline__ unsigned short tobf(float f) {
   __bf16 b = (__bf16)f;
@@ -58,12 +64,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c128_kernel(
     const float* __restrict__ bn_rstd, float* __restrict__ psum, float* __restrict__ psq) {
   extern __shared__ __attribute__((aligned(16))) char sm[];
   char* Ps = sm;
-  char* Wt = sm + P_BYTES;  // [2][128 co][272 B]
+  char* Wt = sm + S_BYTES;  // [2][128 co][272 B]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tiles_w = W / TW, tiles_img = (H / TH) * tiles_w, tiles = N * tiles_img;
   const int cl = lane & 15, g = lane >> 4;
-  const int cb = wave;
+  const int cb = wave & 3, kh = wave >> 2;  // 32 output channels, input-channel half
   bf16x8 pv[6], wv[4];
   auto load_patch = [&](int tt) {
     const int n = tt / tiles_img, r = tt - n * tiles_img;
@@ -116,54 +122,98 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c128_kernel(
     __syncthreads();
     const bool more = t + (int)gridDim.x < tiles;
     if (more) load_patch(t + gridDim.x);
-    f32x4 acc[7];
+    f32x4 acc[7][2];
 #pragma unroll
-    for (int i = 0; i < 7; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 7; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
       const bool next_w = tap < 8 || more;
       if (next_w) load_w(tap < 8 ? tap + 1 : 0);
-      const int kh = tap / 3, kw = tap - kh * 3;
+      const int th = tap / 3, tw = tap - th * 3;
       const char* wb = Wt + buf * WT_BYTES;
 #pragma unroll
-      for (int kq = 0; kq < 4; ++kq) {
-        const int chunk = kq * 4 + g;
-        const bf16x8 b = *(const bf16x8*)(wb + (16 * cb + cl) * WT_PITCH + (kq * 32 + 8 * g) * 2);
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int kq = 2 * kh + k2, chunk = kq * 4 + g;
+        const bf16x8 b0 = *(const bf16x8*)(wb + (32 * cb + cl) * WT_PITCH + (kq * 32 + 8 * g) * 2);
+        const bf16x8 b1 = *(const bf16x8*)(wb + (32 * cb + 16 + cl) * WT_PITCH + (kq * 32 + 8 * g) * 2);
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
-          const int q = pq[i] + kh * PW + kw;
+          const int q = pq[i] + th * PW + tw;
           const bf16x8 a = *(const bf16x8*)(Ps + q * 256 + ((chunk ^ (q & 15)) << 4));
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
+          acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b0, acc[i][0], 0, 0, 0);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, acc[i][1], 0, 0, 0);
         }
       }
       if (next_w) store_w(buf ^ 1);
       __syncthreads();  // the next slice is in; every wave is done with this one
       buf ^= 1;
     }
-    if (!DGRAD) {  // BN statistics of the f32 values: partial row t, this wave's 16 channels
-      float s = 0.f, sq = 0.f;
+    // data gradient: the epilogue's side inputs requested now, in flight during the reduction
+    const int ec = tid & 15;
+    const bool fused = DGRAD && relu_y != nullptr;
+    bf16x8 ysv[4], xsv[4];
+    if (fused) {
 #pragma unroll
-      for (int i = 0; i < 7; ++i)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          s += acc[i][rr];
-          sq += acc[i][rr] * acc[i][rr];
+      for (int k = 0; k < 4; ++k) {
+        const int e = tid + 512 * k, p = e >> 4;
+        if (e < NPX * NCH) {
+          const size_t go = (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8;
+          ysv[k] = *(const bf16x8*)(relu_y + go);
+          xsv[k] = *(const bf16x8*)(bn_x + go);
         }
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
-      sq += __shfl_xor(sq, 16);
-      sq += __shfl_xor(sq, 32);
-      if (g == 0) {
-        const size_t o = (size_t)t * C + 16 * cb + cl;
-        psum[o] = s;
-        psq[o] = sq;
       }
     }
-    // output staging in the patch region (every wave passed the last tap's barrier)
+    // K halves: write the partner's pixel groups, then add the partner's partials of ours
+    f32x4* red = (f32x4*)sm;  // [cb][j][group][lane]
 #pragma unroll
     for (int i = 0; i < 7; ++i)
+      if ((i < 4) != (kh == 0))
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        *(unsigned short*)(Ps + (16 * i + 4 * g + rr) * 256 + (16 * cb + cl) * 2) = tobf(acc[i][rr]);
+        for (int j = 0; j < 2; ++j) red[((cb * 2 + j) * 7 + i) * 64 + lane] = acc[i][j];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+      if ((i < 4) == (kh == 0))
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const f32x4 o = red[((cb * 2 + j) * 7 + i) * 64 + lane];
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) acc[i][j][rr] += o[rr];
+        }
+    __syncthreads();  // partials consumed: the region takes the output staging
+    if (!DGRAD) {  // BN statistics of the f32 values: partial row 2 t + kh (this wave's groups)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float s = 0.f, sq = 0.f;
+#pragma unroll
+        for (int i = 0; i < 7; ++i)
+          if ((i < 4) == (kh == 0))
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              s += acc[i][j][rr];
+              sq += acc[i][j][rr] * acc[i][j][rr];
+            }
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        sq += __shfl_xor(sq, 16);
+        sq += __shfl_xor(sq, 32);
+        if (g == 0) {
+          const size_t o = (size_t)(2 * t + kh) * C + 32 * cb + 16 * j + cl;
+          psum[o] = s;
+          psq[o] = sq;
+        }
+      }
+    }
+    // output staging in the patch region
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+      if ((i < 4) == (kh == 0))
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            *(unsigned short*)(Ps + (16 * i + 4 * g + rr) * 256 + (32 * cb + 16 * j + cl) * 2) =
+                tobf(acc[i][j][rr]);
     __syncthreads();
     if (!DGRAD) {
 #pragma unroll
@@ -176,8 +226,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c128_kernel(
     } else {
       // BN backward: de = dx * (relu_y > 0); sum(de), sum(de * xhat) for this thread's chunk
       // (ec = tid & 15 for every k), reduced over the wave, one partial row per wave and tile
-      const int ec = tid & 15;
-      const bool fused = relu_y != nullptr;
       float cs[8], cq[8], mu[8], rs[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -192,7 +240,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c128_kernel(
         const size_t go = (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8;
         bf16x8 o = *(const bf16x8*)(Ps + p * 256 + ec * 16);
         if (fused) {
-          const bf16x8 yv = *(const bf16x8*)(relu_y + go), xv = *(const bf16x8*)(bn_x + go);
+          const bf16x8 yv = ysv[k], xv = xsv[k];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             const bool pos = bf(yv[u]) > 0.f;
@@ -232,7 +280,7 @@ bool conv3x3_c128_applies(int H, int W, int C, int Cout, int KH, int KW, int str
          H % c3b::TH == 0 && W % c3b::TW == 0;
 }
 
-// mode 1: y = conv(x, w), psum / psq partial statistic rows [tiles][128];
+// mode 1: y = conv(x, w), psum / psq partial statistic rows [2 * tiles][128];
 // mode 2: y = dx of dy = x (w flipped into wf, [128][1152] bf16 workspace), with relu_y given
 //         the fused BN backward, psum / psq partial rows [8 * tiles][128]
 // (tiles = N * H * W / 112)

@@ -3,15 +3,16 @@
 // rows, reduced by colpart_reduce).
 //
 // The stem's scheme (stem_conv.hip) applied to layer1: all 64 x 576 weights stay in LDS for a
-// persistent block's life, and per 4 x 28-pixel output tile the 6 x 30-pixel input patch is
+// persistent block's life, and per 8 x 28-pixel output tile the 10 x 30-pixel input patch is
 // staged ONCE (prefetched a tile ahead into registers), so the MFMA A fragments of every tap
 // are read from the patch at the tap's offset instead of re-gathering each input pixel nine
 // times through L2 (the implicit GEMM's 256x64 tile: 181 us per call at batch 256, against
 // ~32 us of HBM traffic).  Patch pixels are 128-B rows of 8 16-B channel chunks, chunk c of
 // pixel q stored at c ^ (q & 7): the 16 lanes of a fragment read 16 consecutive pixels.
 //
-// k-group kg = (tap kg / 2, channel half kg % 2): 18 groups of 32.  8 waves: wave w owns
-// output channels 16 (w & 3) .. + 15 and pixel groups (of 16) 0-3 (w < 4) or 4-6.
+// k-group kg = (tap kg / 2, channel half kg % 2): 18 groups of 32; the wave layout of the
+// forward / data gradient is at conv3x3_c64_kernel, the weight gradient's at its kernel (which
+// keeps 4 x 28 tiles).
 #include "common.h"
 
 #include <algorithm>
@@ -28,114 +29,235 @@ constexpr int WP = 584;                                          // weight row p
 constexpr int W_BYTES = C * WP * 2;                              // 74752
 constexpr int P_BYTES = PH * PW * 128;                           // 23040 (output staging too)
 constexpr int PCH = PH * PW * 8;                                 // 1440 patch chunks
+// forward / data gradient: 8 x 28 output tiles (10 x 30 patch), K-half partials in LDS
+constexpr int TH2 = 8, NPX2 = TH2 * TW;                          // 224 = 14 groups of 16
+constexpr int PCH2 = (TH2 + 2) * PW * 8;                         // 2400 patch chunks
+constexpr int R_BYTES = 2 * 2 * 2 * 7 * 64 * 16;                 // 57344 (> the 38400-B patch)
 
 __device__ __forceinline__ unsigned short tobf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(unsigned short, b);
 }
 
-__global__ __launch_bounds__(512, 1) void conv3x3_c64_fwd_kernel(
+// Forward (DGRAD false) and data gradient (DGRAD true) on 8 x 28-pixel output tiles (14
+// pixel groups of 16, a 10 x 30 input patch).  8 waves: wave w owns output channels
+// 32 (w & 1) .. + 31, input-channel half (w >> 1) & 1 (the K split: k-groups 2 tap + half)
+// and pixel groups 7 (w >> 2) .. + 6: per k-group 7 A + 2 B fragment reads for 14 MFMAs.  The
+// first version (wave = 16 output channels x the whole K x 4 or 3 groups of a 4 x 28 tile:
+// 4 A + 1 B reads per 4 MFMAs, and a 4 / 3 group imbalance) was bound by LDS bandwidth at
+// ~2.6x its MFMA time.  The K halves are summed through LDS after the last k-group: of each
+// pair, the half-0 wave finalises groups 0-3 and the half-1 wave groups 4-6 of its seven.
+//
+// The data gradient of a stride-1 3x3 conv is the forward conv of dy with the kernel flipped
+// and transposed, W'[ci][tap][co] = W[co][8 - tap][ci] (built while the block loads its
+// resident weights); with relu_y the BatchNorm backward is fused as the GEMM path's epilogue:
+// de = dx * (relu_y > 0) and sum(de), sum(de * xhat) (xhat from bn_x, mean, rstd) as partial
+// rows, one per wave and tile ([8 * tiles][64]); relu_y / bn_x may be null (plain dgrad).
+// Forward: the output's BatchNorm statistics (f32 values) as partial rows [4 * tiles][64].
+template <bool DGRAD>
+__global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(
     int N, int H, int W, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
-    int ldw, unsigned short* __restrict__ y, float* __restrict__ psum, float* __restrict__ psq) {
+    int ldw, unsigned short* __restrict__ y, const unsigned short* __restrict__ relu_y,
+    const unsigned short* __restrict__ bn_x, const float* __restrict__ bn_mean,
+    const float* __restrict__ bn_rstd, float* __restrict__ psum, float* __restrict__ psq) {
   extern __shared__ __attribute__((aligned(16))) char sm[];
   char* Ws = sm;
-  char* Ps = sm + W_BYTES;
+  char* Ps = sm + W_BYTES;  // patch, then the K-half partials, then the output staging
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  for (int i = tid; i < C * 72; i += 512) {  // weights [64 co][576 k], once
-    const int co = i / 72, c = i - co * 72;
-    *(bf16x8*)(Ws + co * WP * 2 + c * 16) = *(const bf16x8*)(w + (size_t)co * ldw + c * 8);
+  if (!DGRAD) {
+    for (int i = tid; i < C * 72; i += 512) {  // weights [64 co][576 k], once
+      const int co = i / 72, c = i - co * 72;
+      *(bf16x8*)(Ws + co * WP * 2 + c * 16) = *(const bf16x8*)(w + (size_t)co * ldw + c * 8);
+    }
+  } else {
+    for (int i = tid; i < C * 72; i += 512) {  // W'[ci][tap * 64 + co8 * 8 .. + 7], once
+      const int ci = i / 72, rem = i - ci * 72, tap = rem >> 3, co8 = rem & 7;
+      bf16x8 v;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = (short)w[(size_t)(co8 * 8 + u) * ldw + (8 - tap) * C + ci];
+      *(bf16x8*)(Ws + ci * WP * 2 + rem * 16) = v;
+    }
   }
-  const int tiles_w = W / TW, tiles_img = (H / TH) * tiles_w, tiles = N * tiles_img;
+  const int tiles_w = W / TW, tiles_img = (H / TH2) * tiles_w, tiles = N * tiles_img;
   const int cl = lane & 15, g = lane >> 4;
-  const int cb = wave & 3;                         // output channel block
-  const int g0 = wave < 4 ? 0 : 4, ng = wave < 4 ? 4 : 3;  // pixel groups of this wave
-  bf16x8 v[3];  // patch chunks of the next tile: 1440 / 512 -> 3 per thread
+  const int cb = wave & 1, kh = (wave >> 1) & 1, ph = wave >> 2;
+  const bool fused = DGRAD && relu_y != nullptr;
+  const int ec = tid & 7;  // the 8-channel chunk this thread handles in the epilogue
+  float mu[8], rs[8];
+  if (fused) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      mu[u] = bn_mean[ec * 8 + u];
+      rs[u] = bn_rstd[ec * 8 + u];
+    }
+  }
+  bf16x8 v[5];  // patch chunks of the next tile: 2400 / 512 -> 5 per thread
   auto load_patch = [&](int tt) {
     const int n = tt / tiles_img, r = tt - n * tiles_img;
-    const int ih0 = (r / tiles_w) * TH - 1, iw0 = (r % tiles_w) * TW - 1;
+    const int ih0 = (r / tiles_w) * TH2 - 1, iw0 = (r % tiles_w) * TW - 1;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 5; ++k) {
       const int e = tid + 512 * k, q = e >> 3, c = e & 7, pr = q / PW, pc = q - pr * PW;
       const int ih = ih0 + pr, iw = iw0 + pc;
       v[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (e < PCH && ih >= 0 && ih < H && iw >= 0 && iw < W)
+      if (e < PCH2 && ih >= 0 && ih < H && iw >= 0 && iw < W)
         v[k] = *(const bf16x8*)(x + (((size_t)n * H + ih) * W + iw) * C + c * 8);
     }
   };
+  // this lane's pixel in each of its groups: patch pixel of tap (0, 0)
+  int pq[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int p = 16 * (7 * ph + i) + cl;
+    pq[i] = (p / TW) * PW + (p % TW);
+  }
   if (blockIdx.x < tiles) load_patch(blockIdx.x);
   for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
     const int n = t / tiles_img, r = t - n * tiles_img;
-    const int oh0 = (r / tiles_w) * TH, ow0 = (r % tiles_w) * TW;
-    __syncthreads();  // the previous tile's output staging is done
+    const int oh0 = (r / tiles_w) * TH2, ow0 = (r % tiles_w) * TW;
+    __syncthreads();  // the previous tile's output staging is consumed
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 5; ++k) {
       const int e = tid + 512 * k, q = e >> 3, c = e & 7;
-      if (e < PCH) *(bf16x8*)(Ps + q * 128 + ((c ^ (q & 7)) << 4)) = v[k];
+      if (e < PCH2) *(bf16x8*)(Ps + q * 128 + ((c ^ (q & 7)) << 4)) = v[k];
     }
     __syncthreads();
     if (t + (int)gridDim.x < tiles) load_patch(t + gridDim.x);
-    // this lane's pixel in each of its groups: patch pixel of tap (0, 0)
-    int pq[4];
+    f32x4 acc[7][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = 16 * (g0 + i) + cl;
-      pq[i] = (p / TW) * PW + (p % TW);
+    for (int i = 0; i < 7; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int chunk = kh * 4 + g;
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const int th = tap / 3, tw = tap - th * 3, kg = 2 * tap + kh;
+      const bf16x8 b0 = *(const bf16x8*)(Ws + (32 * cb + cl) * WP * 2 + (32 * kg + 8 * g) * 2);
+      const bf16x8 b1 = *(const bf16x8*)(Ws + (32 * cb + 16 + cl) * WP * 2 + (32 * kg + 8 * g) * 2);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const int q = pq[i] + th * PW + tw;
+        const bf16x8 a = *(const bf16x8*)(Ps + q * 128 + ((chunk ^ (q & 7)) << 4));
+        acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b0, acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, acc[i][1], 0, 0, 0);
+      }
     }
-    f32x4 acc[4];
+    // data gradient: the epilogue's side inputs requested now, in flight during the reduction
+    bf16x8 ysv[4], xsv[4];
+    if (fused) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-    for (int kg = 0; kg < 18; ++kg) {
-      const int tap = kg >> 1, kh = tap / 3, kw = tap - kh * 3, chunk = (kg & 1) * 4 + g;
-      const bf16x8 b = *(const bf16x8*)(Ws + (16 * cb + cl) * WP * 2 + (32 * kg + 8 * g) * 2);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (i < ng) {
-          const int q = pq[i] + kh * PW + kw;
-          const bf16x8 a = *(const bf16x8*)(Ps + q * 128 + ((chunk ^ (q & 7)) << 4));
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
+      for (int k = 0; k < 4; ++k) {
+        const int e = tid + 512 * k, p = e >> 3;
+        if (e < NPX2 * 8) {
+          const size_t go = (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8;
+          ysv[k] = *(const bf16x8*)(relu_y + go);
+          xsv[k] = *(const bf16x8*)(bn_x + go);
         }
       }
     }
-    // BN statistics (f32 values): lane (cl, g) holds channel 16 cb + cl of pixels 4 g + rr
-    {
-      float s = 0.f, sq = 0.f;
+    __syncthreads();  // every wave is done with the patch
+    // K halves: write the partner's pixel groups, then add the partner's partials of ours
+    f32x4* red = (f32x4*)Ps;  // [ph][cb][j][group][lane]
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (i < ng)
+    for (int i = 0; i < 7; ++i)
+      if ((i < 4) != (kh == 0))
 #pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            s += acc[i][rr];
-            sq += acc[i][rr] * acc[i][rr];
-          }
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
-      sq += __shfl_xor(sq, 16);
-      sq += __shfl_xor(sq, 32);
-      if (g == 0) {  // partial row 2 t + (pixel half), channels of this wave's block
-        const size_t o = (size_t)(2 * t + (wave >> 2)) * C + 16 * cb + cl;
-        psum[o] = s;
-        psq[o] = sq;
+        for (int j = 0; j < 2; ++j) red[(((ph * 2 + cb) * 2 + j) * 7 + i) * 64 + lane] = acc[i][j];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+      if ((i < 4) == (kh == 0))
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const f32x4 o = red[(((ph * 2 + cb) * 2 + j) * 7 + i) * 64 + lane];
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) acc[i][j][rr] += o[rr];
+        }
+    __syncthreads();  // partials consumed: the region takes the output staging
+    if (!DGRAD) {  // partial row 4 t + 2 ph + kh: this wave's finalised groups
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float s = 0.f, sq = 0.f;
+#pragma unroll
+        for (int i = 0; i < 7; ++i)
+          if ((i < 4) == (kh == 0))
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              s += acc[i][j][rr];
+              sq += acc[i][j][rr] * acc[i][j][rr];
+            }
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        sq += __shfl_xor(sq, 16);
+        sq += __shfl_xor(sq, 32);
+        if (g == 0) {
+          const size_t o = (size_t)(4 * t + 2 * ph + kh) * C + 32 * cb + 16 * j + cl;
+          psum[o] = s;
+          psq[o] = sq;
+        }
       }
     }
-    __syncthreads();  // every wave is done with the patch: stage the output there
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (i < ng)
+    for (int i = 0; i < 7; ++i)
+      if ((i < 4) == (kh == 0))
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          *(unsigned short*)(Ps + (16 * (g0 + i) + 4 * g + rr) * 128 + (16 * cb + cl) * 2) =
-              tobf(acc[i][rr]);
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            *(unsigned short*)(Ps + (16 * (7 * ph + i) + 4 * g + rr) * 128 + (32 * cb + 16 * j + cl) * 2) =
+                tobf(acc[i][j][rr]);
     __syncthreads();
-    for (int e = tid; e < NPX * 8; e += 512) {  // 112 px x 8 chunks, 16-B coalesced stores
-      const int p = e >> 3, c = e & 7;
-      const int oh = oh0 + p / TW, ow = ow0 + p % TW;
-      *(bf16x8*)(y + (((size_t)n * H + oh) * W + ow) * C + c * 8) = *(const bf16x8*)(Ps + p * 128 + c * 16);
+    if (!DGRAD) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // 224 px x 8 chunks, 16-B coalesced stores
+        const int e = tid + 512 * k, p = e >> 3, c = e & 7;
+        if (e < NPX2 * 8)
+          *(bf16x8*)(y + (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + c * 8) =
+              *(const bf16x8*)(Ps + p * 128 + c * 16);
+      }
+    } else {
+      float cs[8], cq[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = tid + 512 * k, p = e >> 3;
+        if (e >= NPX2 * 8) continue;
+        bf16x8 o = *(const bf16x8*)(Ps + p * 128 + ec * 16);
+        if (fused) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float yy = __uint_as_float((unsigned)(unsigned short)ysv[k][u] << 16);
+            const float d = yy > 0.f ? __uint_as_float((unsigned)(unsigned short)o[u] << 16) : 0.f;
+            o[u] = yy > 0.f ? o[u] : (short)0;
+            const float xx = __uint_as_float((unsigned)(unsigned short)xsv[k][u] << 16);
+            cs[u] += d;
+            cq[u] += d * (xx - mu[u]) * rs[u];
+          }
+        }
+        *(bf16x8*)(y + (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8) = o;
+      }
+      if (fused) {  // lanes of one chunk: lane & 7 equal -> partial row of this wave
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          cs[u] += __shfl_xor(cs[u], 8);
+          cs[u] += __shfl_xor(cs[u], 16);
+          cs[u] += __shfl_xor(cs[u], 32);
+          cq[u] += __shfl_xor(cq[u], 8);
+          cq[u] += __shfl_xor(cq[u], 16);
+          cq[u] += __shfl_xor(cq[u], 32);
+        }
+        if (lane < 8) {
+          const size_t o = (size_t)(8 * t + wave) * C + ec * 8;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            psum[o + u] = cs[u];
+            psq[o + u] = cq[u];
+          }
+        }
+      }
     }
   }
 }
-
 
 // Weight gradient dW[co][k] (+)= sum_p dy[p][co] * x[p + tap][ci], k = tap * 64 + ci: per
 // 4 x 28 tile the dy tile (112 px x 64 co, 144-B rows) and the input patch are staged once
@@ -252,163 +374,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_wgrad_kernel(
 }
 
 
-// Data gradient with BatchNorm backward fused: dx = conv3x3(dy, W') with W'[ci][tap][co] =
-// W[co][8 - tap][ci] (a stride-1 3x3 data gradient is the forward conv of dy with the kernel
-// flipped and transposed; built while the block loads its resident weights), then, as the
-// GEMM path's fused epilogue, de = dx * (relu_y > 0) and the BN's sum(de), sum(de * xhat)
-// (xhat from bn_x, mean, rstd) as partial rows, one per wave and tile ([8 * tiles][64]).
-// relu_y / bn_x may be null (plain dgrad, no statistics).
-__global__ __launch_bounds__(512, 1) void conv3x3_c64_dgrad_kernel(
-    int N, int H, int W, const unsigned short* __restrict__ dy, const unsigned short* __restrict__ w,
-    int ldw, unsigned short* __restrict__ dx, const unsigned short* __restrict__ relu_y,
-    const unsigned short* __restrict__ bn_x, const float* __restrict__ bn_mean,
-    const float* __restrict__ bn_rstd, float* __restrict__ psum, float* __restrict__ psq) {
-  extern __shared__ __attribute__((aligned(16))) char sm[];
-  char* Ws = sm;
-  char* Ps = sm + W_BYTES;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  for (int i = tid; i < C * 72; i += 512) {  // W'[ci][tap * 64 + co8 * 8 .. + 7], once
-    const int ci = i / 72, rem = i - ci * 72, tap = rem >> 3, co8 = rem & 7;
-    bf16x8 v;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = (short)w[(size_t)(co8 * 8 + u) * ldw + (8 - tap) * C + ci];
-    *(bf16x8*)(Ws + ci * WP * 2 + rem * 16) = v;
-  }
-  const int tiles_w = W / TW, tiles_img = (H / TH) * tiles_w, tiles = N * tiles_img;
-  const int cl = lane & 15, g = lane >> 4;
-  const int cb = wave & 3;
-  const int g0 = wave < 4 ? 0 : 4, ng = wave < 4 ? 4 : 3;
-  const bool fused = relu_y != nullptr;
-  const int ec = tid & 7;  // the 8-channel chunk this thread handles in the epilogue
-  float mu[8], rs[8];
-  if (fused) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      mu[u] = bn_mean[ec * 8 + u];
-      rs[u] = bn_rstd[ec * 8 + u];
-    }
-  }
-  bf16x8 v[3];
-  auto load_patch = [&](int tt) {
-    const int n = tt / tiles_img, r = tt - n * tiles_img;
-    const int ih0 = (r / tiles_w) * TH - 1, iw0 = (r % tiles_w) * TW - 1;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int e = tid + 512 * k, q = e >> 3, c = e & 7, pr = q / PW, pc = q - pr * PW;
-      const int ih = ih0 + pr, iw = iw0 + pc;
-      v[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (e < PCH && ih >= 0 && ih < H && iw >= 0 && iw < W)
-        v[k] = *(const bf16x8*)(dy + (((size_t)n * H + ih) * W + iw) * C + c * 8);
-    }
-  };
-  if (blockIdx.x < tiles) load_patch(blockIdx.x);
-  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
-    const int n = t / tiles_img, r = t - n * tiles_img;
-    const int oh0 = (r / tiles_w) * TH, ow0 = (r % tiles_w) * TW;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int e = tid + 512 * k, q = e >> 3, c = e & 7;
-      if (e < PCH) *(bf16x8*)(Ps + q * 128 + ((c ^ (q & 7)) << 4)) = v[k];
-    }
-    __syncthreads();
-    if (t + (int)gridDim.x < tiles) load_patch(t + gridDim.x);
-    // the epilogue's side inputs of this tile, in flight during the MFMAs
-    bf16x8 yv[2], xv[2];
-    if (fused) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int e = tid + 512 * k, p = e >> 3;
-        const size_t o = (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8;
-        if (e < NPX * 8) {
-          yv[k] = *(const bf16x8*)(relu_y + o);
-          xv[k] = *(const bf16x8*)(bn_x + o);
-        }
-      }
-    }
-    int pq[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = 16 * (g0 + i) + cl;
-      pq[i] = (p / TW) * PW + (p % TW);
-    }
-    f32x4 acc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-    for (int kg = 0; kg < 18; ++kg) {
-      const int tap = kg >> 1, kh = tap / 3, kw = tap - kh * 3, chunk = (kg & 1) * 4 + g;
-      const bf16x8 b = *(const bf16x8*)(Ws + (16 * cb + cl) * WP * 2 + (32 * kg + 8 * g) * 2);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (i < ng) {
-          const int q = pq[i] + kh * PW + kw;
-          const bf16x8 a = *(const bf16x8*)(Ps + q * 128 + ((chunk ^ (q & 7)) << 4));
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
-        }
-      }
-    }
-    __syncthreads();  // every wave is done with the patch: stage the output there
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (i < ng)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          *(unsigned short*)(Ps + (16 * (g0 + i) + 4 * g + rr) * 128 + (16 * cb + cl) * 2) =
-              tobf(acc[i][rr]);
-    __syncthreads();
-    float cs[8], cq[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int e = tid + 512 * k, p = e >> 3;
-      if (e >= NPX * 8) continue;
-      bf16x8 o = *(const bf16x8*)(Ps + p * 128 + ec * 16);
-      if (fused) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const float yy = __uint_as_float((unsigned)(unsigned short)yv[k][u] << 16);
-          const float d = yy > 0.f ? __uint_as_float((unsigned)(unsigned short)o[u] << 16) : 0.f;
-          o[u] = yy > 0.f ? o[u] : (short)0;
-          const float xx = __uint_as_float((unsigned)(unsigned short)xv[k][u] << 16);
-          cs[u] += d;
-          cq[u] += d * (xx - mu[u]) * rs[u];
-        }
-      }
-      *(bf16x8*)(dx + (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8) = o;
-    }
-    if (fused) {  // lanes of one chunk: lane & 7 equal -> partial row of this wave
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        cs[u] += __shfl_xor(cs[u], 8);
-        cs[u] += __shfl_xor(cs[u], 16);
-        cs[u] += __shfl_xor(cs[u], 32);
-        cq[u] += __shfl_xor(cq[u], 8);
-        cq[u] += __shfl_xor(cq[u], 16);
-        cq[u] += __shfl_xor(cq[u], 32);
-      }
-      if (lane < 8) {
-        const size_t o = (size_t)(8 * t + wave) * C + ec * 8;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          psum[o + u] = cs[u];
-          psq[o + u] = cq[u];
-        }
-      }
-    }
-  }
-}
-
 }  // namespace c3
 
 bool conv3x3_c64_applies(int H, int W, int C, int Cout, int KH, int KW, int stride, int pad) {
   return C == c3::C && Cout == c3::C && KH == 3 && KW == 3 && stride == 1 && pad == 1 &&
-         H % c3::TH == 0 && W % c3::TW == 0;
+         H % c3::TH2 == 0 && W % c3::TW == 0;
 }
 
-// dx (+ fused BN backward when relu_y is given: psum / psq partial rows [8 * tiles][64])
+// dx (+ fused BN backward when relu_y is given: psum / psq partial rows [8 * tiles][64],
+// tiles = N*H*W / 224)
 void conv3x3_c64_dgrad_launch(int N, int H, int W, const void* dy, const void* w, int ldw, void* dx,
                               const void* relu_y, const void* bn_x, const float* bn_mean,
                               const float* bn_rstd, float* psum, float* psq, hipStream_t s) {
@@ -419,16 +393,16 @@ void conv3x3_c64_dgrad_launch(int N, int H, int W, const void* dy, const void* w
     throw std::runtime_error("conv3x3_c64_dgrad: ld >= 576 and 16-B aligned tensors");
   if (relu_y && (!bn_x || !bn_mean || !bn_rstd || !psum || !psq))
     throw std::runtime_error("conv3x3_c64_dgrad: fused BN backward needs bn_x, mean, rstd, partials");
-  const int tiles = N * (H / TH) * (W / TW);
-  const size_t lds = W_BYTES + P_BYTES;
+  const int tiles = N * (H / TH2) * (W / TW);
+  const size_t lds = W_BYTES + R_BYTES;
   static bool attr = false;
   if (!attr) {
-    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_c64_dgrad_kernel,
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_c64_kernel<true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
   const int blocks = std::min(tiles, 256);
-  hipLaunchKernelGGL(conv3x3_c64_dgrad_kernel, dim3(blocks), dim3(512), lds, s, N, H, W,
+  hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3(blocks), dim3(512), lds, s, N, H, W,
                      (const unsigned short*)dy, (const unsigned short*)w, ldw, (unsigned short*)dx,
                      (const unsigned short*)relu_y, (const unsigned short*)bn_x, bn_mean, bn_rstd,
                      psum, psq);
@@ -455,7 +429,7 @@ void conv3x3_c64_wgrad_launch(int N, int H, int W, const void* x, const void* dy
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
-// y = conv3x3(x, w), psum / psq: partial statistic rows [2 * tiles][64] (tiles = N*H*W / 112)
+// y = conv3x3(x, w), psum / psq: partial statistic rows [4 * tiles][64] (tiles = N*H*W / 224)
 void conv3x3_c64_fwd_launch(int N, int H, int W, const void* x, const void* w, int ldw, void* y,
                             float* psum, float* psq, hipStream_t s) {
   using namespace c3;
@@ -463,18 +437,18 @@ void conv3x3_c64_fwd_launch(int N, int H, int W, const void* x, const void* w, i
     throw std::runtime_error("conv3x3_c64: unsupported geometry");
   if (ldw < 9 * C || ldw % 8 || (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) & 15))
     throw std::runtime_error("conv3x3_c64: weights need ld >= 576 (% 8), 16-B aligned tensors");
-  const int tiles = N * (H / TH) * (W / TW);
-  const size_t lds = W_BYTES + P_BYTES;
+  const int tiles = N * (H / TH2) * (W / TW);
+  const size_t lds = W_BYTES + R_BYTES;
   static bool attr = false;
   if (!attr) {
-    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_c64_fwd_kernel,
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_c64_kernel<false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
   const int blocks = std::min(tiles, 256);
-  hipLaunchKernelGGL(conv3x3_c64_fwd_kernel, dim3(blocks), dim3(512), lds, s, N, H, W,
+  hipLaunchKernelGGL(conv3x3_c64_kernel<false>, dim3(blocks), dim3(512), lds, s, N, H, W,
                      (const unsigned short*)x, (const unsigned short*)w, ldw, (unsigned short*)y,
-                     psum, psq);
+                     nullptr, nullptr, nullptr, nullptr, psum, psq);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

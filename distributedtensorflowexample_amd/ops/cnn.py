@@ -87,8 +87,8 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
     if (colsum is not None and residual is None
             and hip().conv3x3_c128_applies(H, W, C, Cout, KH, KW, stride, pad)):
         # layer2's 128-channel 3x3 conv: csrc/kernels/conv3x3_c128.hip (input patch staged
-        # once per 4 x 28 output tile, weights streamed one tap at a time); 1 row per tile
-        part = torch.empty(2, N * OH * OW // 112, Cout, device=x.device)
+        # once per 4 x 28 output tile, weights streamed one tap at a time); 2 rows per tile
+        part = torch.empty(2, 2 * (N * OH * OW // 112), Cout, device=x.device)
         hip().conv3x3_c128(1, N, H, W, ptr(x), ptr(w), w.stride(0), ptr(y), 0, 0, 0, 0, 0,
                            ptr(part[0]), ptr(part[1]), stream_handle())
         hip().colpart_reduce(part.shape[1], Cout, ptr(part[0]), ptr(part[1]), ptr(colsum),
@@ -97,8 +97,8 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
     if (colsum is not None and residual is None
             and hip().conv3x3_c64_applies(H, W, C, Cout, KH, KW, stride, pad)):
         # layer1's 64-channel 3x3 conv: csrc/kernels/conv3x3_c64.hip (weights resident in
-        # LDS, input patch staged once per 4 x 28 output tile); 2 partial rows per tile
-        part = torch.empty(2, 2 * (N * OH * OW // 112), Cout, device=x.device)
+        # LDS, input patch staged once per 8 x 28 output tile); 4 partial rows per tile
+        part = torch.empty(2, 4 * (N * OH * OW // 224), Cout, device=x.device)
         hip().conv3x3_c64_fwd(N, H, W, ptr(x), ptr(w), w.stride(0), ptr(y), ptr(part[0]),
                               ptr(part[1]), stream_handle())
         hip().colpart_reduce(part.shape[1], Cout, ptr(part[0]), ptr(part[1]), ptr(colsum),
@@ -179,13 +179,13 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
         return dx
     if residual is None and hip().conv3x3_c64_applies(H, W, C, Cout, KH, KW, stride, pad):
         # layer1's 64-channel 3x3 conv: csrc/kernels/conv3x3_c64.hip (dy patch staged once
-        # per 4 x 28 tile, flipped weights resident in LDS, BN backward in the epilogue)
+        # per 8 x 28 tile, flipped weights resident in LDS, BN backward in the epilogue)
         if bn is None:
             hip().conv3x3_c64_dgrad(N, H, W, ptr(dy), ptr(w), w.stride(0), ptr(dx), 0, 0, 0, 0,
                                     0, 0, stream_handle())
             return dx
         y, x, mean, rstd, sdy, sdx = bn
-        part = torch.empty(2, 8 * (N * H * W // 112), C, device=dy.device)
+        part = torch.empty(2, 8 * (N * H * W // 224), C, device=dy.device)
         hip().conv3x3_c64_dgrad(N, H, W, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(y), ptr(x),
                                 ptr(mean), ptr(rstd), ptr(part[0]), ptr(part[1]), stream_handle())
         hip().colpart_reduce(part.shape[1], C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),

@@ -21,6 +21,7 @@ CONVS = [  # N, H, W, C, Cout, k, stride, pad
     (2, 32, 32, 8, 64, 7, 2, 3),     # the stem kernel (stem_conv.hip): one 16x16 output image
     (3, 48, 64, 8, 64, 7, 2, 3),     # stem kernel, 3 x 2 x 3 tiles per image and batch
     (2, 8, 56, 64, 64, 3, 1, 1),     # the 64-channel 3x3 kernel (conv3x3_c64.hip), 4 tiles
+    (3, 16, 28, 64, 64, 3, 1, 1),    # same, 6 tiles of 8 x 28 (two tile rows per image)
     (2, 28, 28, 128, 128, 3, 1, 1),  # the 128-channel 3x3 kernel (conv3x3_c128.hip), 14 tiles
     (2, 15, 13, 64, 128, 3, 2, 1),   # stride-2 dgrad: phase classes of unequal size
     (2, 14, 14, 64, 64, 3, 2, 1),    # stride-2 dgrad on the 256x64 tile
@@ -83,6 +84,7 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, W, C, Co, k, s, p):
     (2, 15, 13, 64, 128, 3, 2, 1, True),   # unequal classes: zeroed partial rows
     (2, 13, 15, 128, 64, 1, 2, 0, True),   # empty classes: residual + mask only
     (2, 8, 56, 64, 64, 3, 1, 1, False),    # 64-channel 3x3 kernel with the fused BN backward
+    (3, 16, 28, 64, 64, 3, 1, 1, False),   # same, 6 tiles
     (2, 28, 28, 128, 128, 3, 1, 1, False),  # 128-channel 3x3 kernel with the fused BN backward
     (4, 64, 64, 1024, 256, 3, 2, 1, True),  # 8-phase dgrad: per-slab BN columns, class rows
     (3, 60, 60, 1024, 256, 1, 1, 0, True),  # 8-phase 1x1 dgrad (M % 64 != 0: not streamed)
