@@ -45,7 +45,7 @@ void conv3x3_c64_fwd_launch(int, int, int, const void*, const void*, int, void*,
 void conv3x3_c64_wgrad_launch(int, int, int, const void*, const void*, float*, int, float,
                               hipStream_t);
 void conv3x3_c64_dgrad_launch(int, int, int, const void*, const void*, int, void*, const void*,
-                              const void*, const float*, const float*, float*, float*, hipStream_t);
+                              const void*, const float*, const float*, float*, float*, void*, hipStream_t);
 bool conv3x3_c128_applies(int, int, int, int, int, int, int, int);
 bool conv1x1_applies(int, int, int);
 int conv1x1_rows(int, int, int, int);
@@ -286,11 +286,12 @@ void register_nn(py::module_& m) {
   });
   m.def("conv3x3_c64_dgrad", [](int N, int H, int W, uintptr_t dy, uintptr_t w, int ldw,
                                 uintptr_t dx, uintptr_t relu_y, uintptr_t bn_x, uintptr_t mean,
-                                uintptr_t rstd, uintptr_t ps, uintptr_t pq, uintptr_t s) {
+                                uintptr_t rstd, uintptr_t ps, uintptr_t pq, uintptr_t wf, uintptr_t s) {
     dtfx::conv3x3_c64_dgrad_launch(N, H, W, P<const void>(dy), P<const void>(w), ldw, P<void>(dx),
                                    P<const void>(relu_y), P<const void>(bn_x), P<const float>(mean),
-                                   P<const float>(rstd), P<float>(ps), P<float>(pq), S(s));
-  });
+                                   P<const float>(rstd), P<float>(ps), P<float>(pq), P<void>(wf),
+                                   S(s));
+  }, "wf: [64][576] bf16 workspace for the flipped weights");
   m.def("conv1x1_applies", &dtfx::conv1x1_applies,
         "(M, K, N): the streaming 1x1 kernel takes this product (K 64 / 128, N = 256 * 2^i)");
   m.def("conv1x1_rows", &dtfx::conv1x1_rows, "(mode, M, K, N): partial statistics rows a launch writes");

@@ -4,11 +4,11 @@
 //
 // conv3x3_c64.hip's staged patch with the weights STREAMED: the 128 x 1152 weights (295 KB) do
 // not fit in LDS, so a persistent block keeps one 6 x 30-pixel input patch (4 x 28 output
-// tile, 46 KB, prefetched a tile ahead into registers) and double-buffers the 128 x 128 weight
+// tile, 48 KB, prefetched a tile ahead into registers) and double-buffers the 128 x 128 weight
 // slice of one tap at a time (34 KB each, the next tap's slice loaded into registers during the
 // current tap's MFMAs).  Every input
-// pixel is read from HBM / L2 once per tile instead of once per tap.  Patch pixels are 256-B
-// rows of 16 16-B channel chunks, chunk c of pixel q stored at c ^ (q & 15).
+// pixel is read from HBM / L2 once per tile instead of once per tap.  Patch pixels are 272-B
+// rows (256 B of channels + 16 B pad).
 //
 // The data gradient of a stride-1 3x3 conv is the forward conv of dy with the kernel flipped
 // and transposed, W'[ci][tap][co] = W[co][8 - tap][ci]: conv3x3_c128_flip builds W' once per
@@ -33,7 +33,8 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int C = 128, TH = 4, TW = 28, PH = TH + 2, PW = TW + 2;  // 6 x 30 patch
 constexpr int NPX = TH * TW;                                      // 112 = 7 groups of 16
 constexpr int NCH = C / 8;                                        // 16 chunks per pixel
-constexpr int P_BYTES = PH * PW * C * 2;                          // 46080
+constexpr int PP = C * 2 + 16;                                    // patch pixel pitch 272 B
+constexpr int P_BYTES = PH * PW * PP;                             // 48960
 constexpr int PCH = PH * PW * NCH;                                // 2880 patch chunks
 constexpr int WT_PITCH = C * 2 + 16;                              // 272 B per weight row
 constexpr int WT_BYTES = C * WT_PITCH;                            // 34816 per tap slice
@@ -71,13 +72,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c128_kernel(
   const int cl = lane & 15, g = lane >> 4;
   const int cb = wave & 3, kh = wave >> 2;  // 32 output channels, input-channel half
   bf16x8 pv[6], wv[4];
+  int lpr[6], lpc[6];  // patch rows / columns of this thread's chunks (tile-invariant)
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int q = (tid + 512 * k) >> 4;
+    lpr[k] = q / PW;
+    lpc[k] = q - lpr[k] * PW;
+  }
   auto load_patch = [&](int tt) {
     const int n = tt / tiles_img, r = tt - n * tiles_img;
     const int ih0 = (r / tiles_w) * TH - 1, iw0 = (r % tiles_w) * TW - 1;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      const int e = tid + 512 * k, q = e >> 4, c = e & 15, pr = q / PW, pc = q - pr * PW;
-      const int ih = ih0 + pr, iw = iw0 + pc;
+      const int e = tid + 512 * k, c = e & 15;
+      const int ih = ih0 + lpr[k], iw = iw0 + lpc[k];
       pv[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (e < PCH && ih >= 0 && ih < H && iw >= 0 && iw < W)
         pv[k] = *(const bf16x8*)(x + (((size_t)n * H + ih) * W + iw) * C + c * 8);
@@ -97,12 +105,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c128_kernel(
       *(bf16x8*)(Wt + buf * WT_BYTES + co * WT_PITCH + c * 16) = wv[k];
     }
   };
-  // this lane's pixel in each of its groups: patch pixel of tap (0, 0)
-  int pq[7];
+  // A fragment addresses of tap (0, 0): this lane's pixel in each group, its chunk of input
+  // half kh.  Patch pixels are 272-B rows (16 consecutive pixels: 16 distinct 16-B bank
+  // slots), so a tap is one uniform offset and a k-group an immediate.
+  int abase[7];
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     const int p = 16 * i + cl;
-    pq[i] = (p / TW) * PW + (p % TW);
+    abase[i] = ((p / TW) * PW + (p % TW)) * PP + (8 * kh + g) * 16;
   }
   int buf = 0;
   if (blockIdx.x < tiles) {
@@ -117,7 +127,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c128_kernel(
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const int e = tid + 512 * k, q = e >> 4, c = e & 15;
-      if (e < PCH) *(bf16x8*)(Ps + q * 256 + ((c ^ (q & 15)) << 4)) = pv[k];
+      if (e < PCH) *(bf16x8*)(Ps + q * PP + c * 16) = pv[k];
     }
     __syncthreads();
     const bool more = t + (int)gridDim.x < tiles;
@@ -125,21 +135,35 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c128_kernel(
     f32x4 acc[7][2];
 #pragma unroll
     for (int i = 0; i < 7; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // data gradient: the epilogue's side inputs, requested with the last tap (in flight during
+    // its MFMAs and the K-half reduction)
+    const int ec = tid & 15;
+    const bool fused = DGRAD && relu_y != nullptr;
+    bf16x8 ysv[4], xsv[4];
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
       const bool next_w = tap < 8 || more;
       if (next_w) load_w(tap < 8 ? tap + 1 : 0);
-      const int th = tap / 3, tw = tap - th * 3;
-      const char* wb = Wt + buf * WT_BYTES;
+      if (fused && tap == 8) {  // after the weight loads: their wait leaves these in flight
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int e = tid + 512 * k, p = e >> 4;
+          if (e < NPX * NCH) {
+            const size_t go = (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8;
+            ysv[k] = *(const bf16x8*)(relu_y + go);
+            xsv[k] = *(const bf16x8*)(bn_x + go);
+          }
+        }
+      }
+      const int th = tap / 3, tw = tap - th * 3, toff = (th * PW + tw) * PP;
+      const char* wb = Wt + buf * WT_BYTES + (32 * cb + cl) * WT_PITCH + (64 * kh + 8 * g) * 2;
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2) {
-        const int kq = 2 * kh + k2, chunk = kq * 4 + g;
-        const bf16x8 b0 = *(const bf16x8*)(wb + (32 * cb + cl) * WT_PITCH + (kq * 32 + 8 * g) * 2);
-        const bf16x8 b1 = *(const bf16x8*)(wb + (32 * cb + 16 + cl) * WT_PITCH + (kq * 32 + 8 * g) * 2);
+        const bf16x8 b0 = *(const bf16x8*)(wb + k2 * 64);
+        const bf16x8 b1 = *(const bf16x8*)(wb + 16 * WT_PITCH + k2 * 64);
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
-          const int q = pq[i] + th * PW + tw;
-          const bf16x8 a = *(const bf16x8*)(Ps + q * 256 + ((chunk ^ (q & 15)) << 4));
+          const bf16x8 a = *(const bf16x8*)(Ps + abase[i] + toff + k2 * 64);
           acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b0, acc[i][0], 0, 0, 0);
           acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, acc[i][1], 0, 0, 0);
         }
@@ -147,21 +171,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c128_kernel(
       if (next_w) store_w(buf ^ 1);
       __syncthreads();  // the next slice is in; every wave is done with this one
       buf ^= 1;
-    }
-    // data gradient: the epilogue's side inputs requested now, in flight during the reduction
-    const int ec = tid & 15;
-    const bool fused = DGRAD && relu_y != nullptr;
-    bf16x8 ysv[4], xsv[4];
-    if (fused) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int e = tid + 512 * k, p = e >> 4;
-        if (e < NPX * NCH) {
-          const size_t go = (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8;
-          ysv[k] = *(const bf16x8*)(relu_y + go);
-          xsv[k] = *(const bf16x8*)(bn_x + go);
-        }
-      }
     }
     // K halves: write the partner's pixel groups, then add the partner's partials of ours
     f32x4* red = (f32x4*)sm;  // [cb][j][group][lane]

@@ -32,7 +32,8 @@ constexpr int PCH = PH * PW * 8;                                 // 1440 patch c
 // forward / data gradient: 8 x 28 output tiles (10 x 30 patch), K-half partials in LDS
 constexpr int TH2 = 8, NPX2 = TH2 * TW;                          // 224 = 14 groups of 16
 constexpr int PCH2 = (TH2 + 2) * PW * 8;                         // 2400 patch chunks
-constexpr int R_BYTES = 2 * 2 * 2 * 7 * 64 * 16;                 // 57344 (> the 38400-B patch)
+constexpr int PP2 = 144;                                         // patch pixel pitch (bytes)
+constexpr int R_BYTES = 2 * 2 * 2 * 7 * 64 * 16;                 // 57344 (> the 43200-B patch)
 
 __device__ __forceinline__ unsigned short tobf(float f) {
   __bf16 b = (__bf16)f;
@@ -49,11 +50,20 @@ __device__ __forceinline__ unsigned short tobf(float f) {
 // pair, the half-0 wave finalises groups 0-3 and the half-1 wave groups 4-6 of its seven.
 //
 // The data gradient of a stride-1 3x3 conv is the forward conv of dy with the kernel flipped
-// and transposed, W'[ci][tap][co] = W[co][8 - tap][ci] (built while the block loads its
-// resident weights); with relu_y the BatchNorm backward is fused as the GEMM path's epilogue:
+// and transposed, W'[ci][tap][co] = W[co][8 - tap][ci] (conv3x3_c64_flip_kernel, once per call
+// into a workspace: each block building it with 2-byte gathers cost ~15 us); with relu_y the BatchNorm backward is fused as the GEMM path's epilogue:
 // de = dx * (relu_y > 0) and sum(de), sum(de * xhat) (xhat from bn_x, mean, rstd) as partial
 // rows, one per wave and tile ([8 * tiles][64]); relu_y / bn_x may be null (plain dgrad).
 // Forward: the output's BatchNorm statistics (f32 values) as partial rows [4 * tiles][64].
+// W' [ci][tap * 64 + co] = W [co][(8 - tap) * 64 + ci]
+__global__ __launch_bounds__(256) void conv3x3_c64_flip_kernel(const unsigned short* __restrict__ w,
+                                                               int ldw, unsigned short* __restrict__ wf) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // output element
+  if (i >= C * 9 * C) return;
+  const int ci = i / (9 * C), rem = i - ci * 9 * C, tap = rem / C, co = rem - tap * C;
+  wf[i] = w[(size_t)co * ldw + (8 - tap) * C + ci];
+}
+
 template <bool DGRAD>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(
     int N, int H, int W, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
@@ -65,19 +75,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(
   char* Ps = sm + W_BYTES;  // patch, then the K-half partials, then the output staging
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (!DGRAD) {
-    for (int i = tid; i < C * 72; i += 512) {  // weights [64 co][576 k], once
-      const int co = i / 72, c = i - co * 72;
-      *(bf16x8*)(Ws + co * WP * 2 + c * 16) = *(const bf16x8*)(w + (size_t)co * ldw + c * 8);
-    }
-  } else {
-    for (int i = tid; i < C * 72; i += 512) {  // W'[ci][tap * 64 + co8 * 8 .. + 7], once
-      const int ci = i / 72, rem = i - ci * 72, tap = rem >> 3, co8 = rem & 7;
-      bf16x8 v;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = (short)w[(size_t)(co8 * 8 + u) * ldw + (8 - tap) * C + ci];
-      *(bf16x8*)(Ws + ci * WP * 2 + rem * 16) = v;
-    }
+  for (int i = tid; i < C * 72; i += 512) {  // weights [64 co][576 k] (dgrad: W'), once
+    const int co = i / 72, c = i - co * 72;
+    *(bf16x8*)(Ws + co * WP * 2 + c * 16) = *(const bf16x8*)(w + (size_t)co * ldw + c * 8);
   }
   const int tiles_w = W / TW, tiles_img = (H / TH2) * tiles_w, tiles = N * tiles_img;
   const int cl = lane & 15, g = lane >> 4;
@@ -93,25 +93,35 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(
     }
   }
   bf16x8 v[5];  // patch chunks of the next tile: 2400 / 512 -> 5 per thread
+  int lpr[5], lpc[5];  // their patch rows / columns (tile-invariant)
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int q = (tid + 512 * k) >> 3;
+    lpr[k] = q / PW;
+    lpc[k] = q - lpr[k] * PW;
+  }
   auto load_patch = [&](int tt) {
     const int n = tt / tiles_img, r = tt - n * tiles_img;
     const int ih0 = (r / tiles_w) * TH2 - 1, iw0 = (r % tiles_w) * TW - 1;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-      const int e = tid + 512 * k, q = e >> 3, c = e & 7, pr = q / PW, pc = q - pr * PW;
-      const int ih = ih0 + pr, iw = iw0 + pc;
+      const int e = tid + 512 * k, c = e & 7;
+      const int ih = ih0 + lpr[k], iw = iw0 + lpc[k];
       v[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (e < PCH2 && ih >= 0 && ih < H && iw >= 0 && iw < W)
         v[k] = *(const bf16x8*)(x + (((size_t)n * H + ih) * W + iw) * C + c * 8);
     }
   };
-  // this lane's pixel in each of its groups: patch pixel of tap (0, 0)
-  int pq[7];
+  // A fragment addresses of tap (0, 0): this lane's pixel in each of its groups, its chunk.
+  // Patch pixels are 144-B rows (16 consecutive pixels: 16 distinct 16-B bank slots), so a
+  // tap's offset is a compile-time immediate of the LDS read.
+  int abase[7];
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     const int p = 16 * (7 * ph + i) + cl;
-    pq[i] = (p / TW) * PW + (p % TW);
+    abase[i] = ((p / TW) * PW + (p % TW)) * PP2 + (kh * 4 + g) * 16;
   }
+  const int bbase = (32 * cb + cl) * WP * 2 + (32 * kh + 8 * g) * 2;
   if (blockIdx.x < tiles) load_patch(blockIdx.x);
   for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
     const int n = t / tiles_img, r = t - n * tiles_img;
@@ -120,28 +130,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       const int e = tid + 512 * k, q = e >> 3, c = e & 7;
-      if (e < PCH2) *(bf16x8*)(Ps + q * 128 + ((c ^ (q & 7)) << 4)) = v[k];
+      if (e < PCH2) *(bf16x8*)(Ps + q * PP2 + c * 16) = v[k];
     }
     __syncthreads();
     if (t + (int)gridDim.x < tiles) load_patch(t + gridDim.x);
-    f32x4 acc[7][2];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int chunk = kh * 4 + g;
-#pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
-      const int th = tap / 3, tw = tap - th * 3, kg = 2 * tap + kh;
-      const bf16x8 b0 = *(const bf16x8*)(Ws + (32 * cb + cl) * WP * 2 + (32 * kg + 8 * g) * 2);
-      const bf16x8 b1 = *(const bf16x8*)(Ws + (32 * cb + 16 + cl) * WP * 2 + (32 * kg + 8 * g) * 2);
-#pragma unroll
-      for (int i = 0; i < 7; ++i) {
-        const int q = pq[i] + th * PW + tw;
-        const bf16x8 a = *(const bf16x8*)(Ps + q * 128 + ((chunk ^ (q & 7)) << 4));
-        acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b0, acc[i][0], 0, 0, 0);
-        acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, acc[i][1], 0, 0, 0);
-      }
-    }
-    // data gradient: the epilogue's side inputs requested now, in flight during the reduction
+    // data gradient: the epilogue's side inputs requested now, in flight during the MFMAs
     bf16x8 ysv[4], xsv[4];
     if (fused) {
 #pragma unroll
@@ -152,6 +145,21 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(
           ysv[k] = *(const bf16x8*)(relu_y + go);
           xsv[k] = *(const bf16x8*)(bn_x + go);
         }
+      }
+    }
+    f32x4 acc[7][2];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int th = tap / 3, tw = tap - th * 3;
+      const bf16x8 b0 = *(const bf16x8*)(Ws + bbase + tap * 128);
+      const bf16x8 b1 = *(const bf16x8*)(Ws + bbase + 16 * WP * 2 + tap * 128);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const bf16x8 a = *(const bf16x8*)(Ps + abase[i] + (th * PW + tw) * PP2);
+        acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b0, acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, acc[i][1], 0, 0, 0);
       }
     }
     __syncthreads();  // every wave is done with the patch
@@ -385,12 +393,13 @@ bool conv3x3_c64_applies(int H, int W, int C, int Cout, int KH, int KW, int stri
 // tiles = N*H*W / 224)
 void conv3x3_c64_dgrad_launch(int N, int H, int W, const void* dy, const void* w, int ldw, void* dx,
                               const void* relu_y, const void* bn_x, const float* bn_mean,
-                              const float* bn_rstd, float* psum, float* psq, hipStream_t s) {
+                              const float* bn_rstd, float* psum, float* psq, void* wf, hipStream_t s) {
   using namespace c3;
   if (!conv3x3_c64_applies(H, W, C, C, 3, 3, 1, 1))
     throw std::runtime_error("conv3x3_c64: unsupported geometry");
-  if (ldw < 9 * C || (((uintptr_t)dy | (uintptr_t)dx | (uintptr_t)relu_y | (uintptr_t)bn_x) & 15))
-    throw std::runtime_error("conv3x3_c64_dgrad: ld >= 576 and 16-B aligned tensors");
+  if (ldw < 9 * C || !wf ||
+      (((uintptr_t)dy | (uintptr_t)dx | (uintptr_t)relu_y | (uintptr_t)bn_x | (uintptr_t)wf) & 15))
+    throw std::runtime_error("conv3x3_c64_dgrad: ld >= 576, a [64][576] bf16 workspace wf, 16-B aligned tensors");
   if (relu_y && (!bn_x || !bn_mean || !bn_rstd || !psum || !psq))
     throw std::runtime_error("conv3x3_c64_dgrad: fused BN backward needs bn_x, mean, rstd, partials");
   const int tiles = N * (H / TH2) * (W / TW);
@@ -402,8 +411,10 @@ void conv3x3_c64_dgrad_launch(int N, int H, int W, const void* dy, const void* w
     attr = true;
   }
   const int blocks = std::min(tiles, 256);
+  hipLaunchKernelGGL(conv3x3_c64_flip_kernel, dim3((C * 9 * C + 255) / 256), dim3(256), 0, s,
+                     (const unsigned short*)w, ldw, (unsigned short*)wf);
   hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3(blocks), dim3(512), lds, s, N, H, W,
-                     (const unsigned short*)dy, (const unsigned short*)w, ldw, (unsigned short*)dx,
+                     (const unsigned short*)dy, (const unsigned short*)wf, 9 * C, (unsigned short*)dx,
                      (const unsigned short*)relu_y, (const unsigned short*)bn_x, bn_mean, bn_rstd,
                      psum, psq);
   DTFX_HIP_CHECK(hipGetLastError());

@@ -179,15 +179,18 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
         return dx
     if residual is None and hip().conv3x3_c64_applies(H, W, C, Cout, KH, KW, stride, pad):
         # layer1's 64-channel 3x3 conv: csrc/kernels/conv3x3_c64.hip (dy patch staged once
-        # per 8 x 28 tile, flipped weights resident in LDS, BN backward in the epilogue)
+        # per 8 x 28 tile, flipped weights (a workspace) resident in LDS, BN backward in the
+        # epilogue)
+        wf = torch.empty(C, 9 * Cout, device=dy.device, dtype=BF16)
         if bn is None:
             hip().conv3x3_c64_dgrad(N, H, W, ptr(dy), ptr(w), w.stride(0), ptr(dx), 0, 0, 0, 0,
-                                    0, 0, stream_handle())
+                                    0, 0, ptr(wf), stream_handle())
             return dx
         y, x, mean, rstd, sdy, sdx = bn
         part = torch.empty(2, 8 * (N * H * W // 224), C, device=dy.device)
         hip().conv3x3_c64_dgrad(N, H, W, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(y), ptr(x),
-                                ptr(mean), ptr(rstd), ptr(part[0]), ptr(part[1]), stream_handle())
+                                ptr(mean), ptr(rstd), ptr(part[0]), ptr(part[1]), ptr(wf),
+                                stream_handle())
         hip().colpart_reduce(part.shape[1], C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
                              stream_handle())
         return dx
