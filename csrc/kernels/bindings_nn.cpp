@@ -55,7 +55,8 @@ void conv1x1_launch(int, int, int, int, const void*, const void*, int, void*, co
 bool conv1x1_pro_applies(int, int, int, int);
 void conv1x1_pro_launch(int, int, int, int, const void*, const void*, const float*, void*,
                         const void*, int, void*, const void*, const void*, const void*,
-                        const float*, const float*, float*, float*, void*, hipStream_t);
+                        const float*, const float*, float*, float*, void*, hipStream_t,
+                        int = 0, int = 0);
 void bn_fwd_coef_launch(long long, int, const float*, const float*, float, float*, float*, float*,
                         float*, float, const float*, const float*, const float*, const float*,
                         const float*, const float*, float*, float*, float*, float*, float*,
@@ -308,13 +309,19 @@ void register_nn(py::module_& m) {
   m.def("conv1x1_pro", [](int mode, int M, int K, int N, uintptr_t s0, uintptr_t s1, uintptr_t coef,
                           uintptr_t xo, uintptr_t w, int ldw, uintptr_t y, uintptr_t res,
                           uintptr_t relu_y, uintptr_t bn_x, uintptr_t mean, uintptr_t rstd,
-                          uintptr_t ps, uintptr_t pq, uintptr_t wt, uintptr_t s) {
+                          uintptr_t ps, uintptr_t pq, uintptr_t wt, uintptr_t s, int res_h,
+                          int res_w) {
     dtfx::conv1x1_pro_launch(mode, M, K, N, P<const void>(s0), P<const void>(s1),
                              P<const float>(coef), P<void>(xo), P<const void>(w), ldw, P<void>(y),
                              P<const void>(res), P<const void>(relu_y), P<const void>(bn_x),
                              P<const float>(mean), P<const float>(rstd), P<float>(ps), P<float>(pq),
-                             P<void>(wt), S(s));
-  });
+                             P<void>(wt), S(s), res_h, res_w);
+  }, py::arg("mode"), py::arg("M"), py::arg("K"), py::arg("N"), py::arg("s0"), py::arg("s1"),
+     py::arg("coef"), py::arg("xo"), py::arg("w"), py::arg("ldw"), py::arg("y"), py::arg("res"),
+     py::arg("relu_y"), py::arg("bn_x"), py::arg("mean"), py::arg("rstd"), py::arg("ps"),
+     py::arg("pq"), py::arg("wt"), py::arg("s"), py::arg("res_h") = 0, py::arg("res_w") = 0,
+     "res_h / res_w (mode 2, wide): the residual is a stride-2 conv's data gradient stored "
+     "compact [pixels / 4][N] for an res_h x res_w grid (zero at odd rows / columns)");
   m.def("bn_fwd_coef", [](long long M, int C, uintptr_t sum, uintptr_t sq, float eps, uintptr_t mean,
                           uintptr_t rstd, uintptr_t run_mean, uintptr_t run_var, float momentum,
                           uintptr_t g, uintptr_t b, uintptr_t sum2, uintptr_t sq2, uintptr_t g2,

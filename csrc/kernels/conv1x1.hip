@@ -229,6 +229,8 @@ __global__ __launch_bounds__(576, fbpc<K>() == 2 ? 5 : 3) void conv1x1_fwd_kerne
 // are summed over the block's pixels in registers and reduced across waves once at the end.
 constexpr int DTM = 16;
 constexpr int SPITCH = NC * 4 + 16;  // f32 staging row (bytes), 16-B skew per pixel
+// the DMA source of a stride-2 residual's zero pixels (one 512-B channel slice)
+__device__ __attribute__((aligned(16))) unsigned short g_zero_slice[NC];
 template <int K, bool RES, bool BN, int PRO = 0>
 constexpr int dgrad_ring() {
   constexpr int nqt = DTM * K * 2 * (PRO ? 2 : 1) / 1024 +
@@ -247,7 +249,8 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
     const unsigned short* __restrict__ relu_y, const unsigned short* __restrict__ bn_x,
     const float* __restrict__ bn_mean, const float* __restrict__ bn_rstd, float* __restrict__ ps,
     float* __restrict__ pq, const unsigned short* __restrict__ src1 = nullptr,
-    const float* __restrict__ coef = nullptr, unsigned short* __restrict__ xo = nullptr) {
+    const float* __restrict__ coef = nullptr, unsigned short* __restrict__ xo = nullptr,
+    int rs_h = 0, int rs_w = 0) {
   constexpr int KK = K / 32, CPR = K / 8;
   constexpr int DYB = DTM * K * 2, SB = DTM * NC * 2, NSIDE = (RES ? 1 : 0) + (BN ? 2 : 0);
   constexpr int DYS = DYB * (PRO ? 2 : 1);  // side tiles after the source tile(s)
@@ -279,6 +282,19 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
         }
       }
       const unsigned short* sides[3] = {res, relu_y, bn_x};
+      // stride-2 residual: the tile's first pixel (n0, h0, w0), once per tile (DTM <= rs_w, so
+      // the tile's pixels sit on at most two grid rows: per pixel one compare instead of the
+      // four integer divisions -- those made the loader wave the bottleneck, +110 us per call)
+      int rw0 = 0, rh0 = 0, rn0 = 0;
+      if (RES && rs_w) {
+        const int m0 = tile * DTM;
+        const int hq0 = (int)((float)m0 * (1.f / (float)rs_w));  // exact: m0 < 2^24
+        const int hq = hq0 - (hq0 * rs_w > m0) + ((hq0 + 1) * rs_w <= m0);
+        rw0 = m0 - hq * rs_w;
+        rn0 = (int)((float)hq * (1.f / (float)rs_h));
+        rn0 = rn0 - (rn0 * rs_h > hq) + ((rn0 + 1) * rs_h <= hq);
+        rh0 = hq - rn0 * rs_h;
+      }
 #pragma unroll
       for (int si = 0; si < 3; ++si) {
         if ((si == 0 && !RES) || (si > 0 && !BN)) continue;
@@ -287,6 +303,17 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
         for (int q = 0; q < NQS; ++q) {
           const int r = 2 * q + (lane >> 5), c = lane & 31;
           const unsigned short* src = sides[si] + ((size_t)tile * DTM + r) * N + cb * NC + c * 8;
+          if (si == 0 && rs_w) {  // stride-2 residual: stored compact, zero at odd rows / columns
+            int ww = rw0 + r, hh = rh0, nn = rn0;
+            if (ww >= rs_w) {
+              ww -= rs_w;
+              if (++hh == rs_h) hh = 0, ++nn;
+            }
+            src = ((hh | ww) & 1)
+                      ? g_zero_slice + c * 8
+                      : res + ((((size_t)nn * (rs_h >> 1) + (hh >> 1)) * (rs_w >> 1)) + (ww >> 1)) *
+                                    N + cb * NC + c * 8;
+          }
           __builtin_amdgcn_global_load_lds((const void*)src,
                                            (lds_void*)(d + DYS + slot * SB + q * 1024), 16, 0, 0);
         }
@@ -761,7 +788,8 @@ static void conv1x1_dgrad_go(dim3 grid, int M, int N, const void* dy, const void
                              void* dx, const void* res, const void* relu_y, const void* bn_x,
                              const float* mean, const float* rstd, float* ps, float* pq,
                              hipStream_t s, const void* src1 = nullptr,
-                             const float* coef = nullptr, void* xo = nullptr) {
+                             const float* coef = nullptr, void* xo = nullptr, int rs_h = 0,
+                             int rs_w = 0) {
   using namespace pw;
   const size_t lds =
       (size_t)dgrad_ring<K, RES, BN, PRO>() *
@@ -780,7 +808,7 @@ static void conv1x1_dgrad_go(dim3 grid, int M, int N, const void* dy, const void
                      (const unsigned short*)dy, (const unsigned short*)w, ldw, (unsigned short*)dx,
                      (const unsigned short*)res, (const unsigned short*)relu_y,
                      (const unsigned short*)bn_x, mean, rstd, ps, pq, (const unsigned short*)src1,
-                     coef, (unsigned short*)xo);
+                     coef, (unsigned short*)xo, rs_h, rs_w);
 }
 
 template <int K, int PRO = 0>
@@ -788,15 +816,16 @@ static void conv1x1_dgrad_pick(dim3 grid, int M, int N, const void* dy, const vo
                                void* dx, const void* res, const void* relu_y, const void* bn_x,
                                const float* mean, const float* rstd, float* ps, float* pq,
                                hipStream_t s, const void* src1 = nullptr,
-                               const float* coef = nullptr, void* xo = nullptr) {
+                               const float* coef = nullptr, void* xo = nullptr, int rs_h = 0,
+                               int rs_w = 0) {
   if (res && ps)
-    conv1x1_dgrad_go<K, true, true, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo);
+    conv1x1_dgrad_go<K, true, true, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo, rs_h, rs_w);
   else if (res)
-    conv1x1_dgrad_go<K, true, false, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo);
+    conv1x1_dgrad_go<K, true, false, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo, rs_h, rs_w);
   else if (ps)
-    conv1x1_dgrad_go<K, false, true, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo);
+    conv1x1_dgrad_go<K, false, true, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo, rs_h, rs_w);
   else
-    conv1x1_dgrad_go<K, false, false, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo);
+    conv1x1_dgrad_go<K, false, false, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo, rs_h, rs_w);
 }
 
 // mode 1: forward (x [M][K], w [N][ldw]); mode 2: data gradient (x = dy [M][K], w [K][ldw],
@@ -881,8 +910,13 @@ bool conv1x1_pro_applies(int mode, int M, int K, int N) {
 void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const void* s1,
                         const float* coef, void* xo, const void* w, int ldw, void* y,
                         const void* res, const void* relu_y, const void* bn_x, const float* mean,
-                        const float* rstd, float* ps, float* pq, void* wt, hipStream_t s) {
+                        const float* rstd, float* ps, float* pq, void* wt, hipStream_t s,
+                        int res_h, int res_w) {
   using namespace pw;
+  if (res_w && (mode != 2 || !res || conv1x1_narrow(K, N) || res_h <= 0 || res_h % 2 ||
+                res_w % 2 || res_w < pw::DTM || M % (res_h * res_w) || M >= (1 << 24)))
+    throw std::runtime_error("conv1x1_pro: a stride-2 (compact) residual needs the wide data "
+                             "gradient and even res_h / res_w dividing the pixels");
   if (!conv1x1_pro_applies(mode, M, K, N)) throw std::runtime_error("conv1x1_pro: unsupported shape");
   const bool narrow = conv1x1_narrow(K, N);
   if (!s0 || !coef || (mode != 3 && !s1) || ((mode == 1 || mode == 3) && (!xo || !ps || !pq)) ||
@@ -925,9 +959,9 @@ void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const voi
       else if (K == 128) conv1x1_fwd_go<128, 3>(grid, M, N, s0, w, ldw, y, ps, pq, s, coef, xo);
       else conv1x1_fwd_go<256, 3>(grid, M, N, s0, w, ldw, y, ps, pq, s, coef, xo);
     } else {
-      if (K == 64) conv1x1_dgrad_pick<64, 2>(grid, M, N, s0, wv, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s, s1, coef, xo);
-      else if (K == 128) conv1x1_dgrad_pick<128, 2>(grid, M, N, s0, wv, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s, s1, coef, xo);
-      else conv1x1_dgrad_pick<256, 2>(grid, M, N, s0, wv, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s, s1, coef, xo);
+      if (K == 64) conv1x1_dgrad_pick<64, 2>(grid, M, N, s0, wv, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s, s1, coef, xo, res_h, res_w);
+      else if (K == 128) conv1x1_dgrad_pick<128, 2>(grid, M, N, s0, wv, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s, s1, coef, xo, res_h, res_w);
+      else conv1x1_dgrad_pick<256, 2>(grid, M, N, s0, wv, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s, s1, coef, xo, res_h, res_w);
     }
   }
   DTFX_HIP_CHECK(hipGetLastError());

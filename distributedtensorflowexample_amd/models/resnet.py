@@ -40,6 +40,7 @@ ALIGN = 64
 # the stem's BatchNorm + ReLU fused into its max pool (DTFX_STEM_POOL_BN=0: separate passes)
 _STEM_POOL_BN = os.environ.get("DTFX_STEM_POOL_BN", "1") != "0"
 _DS_PRO = os.environ.get("DTFX_DS_PROLOGUE", "1") != "0"  # stride-1 downsample BN apply in its dgrad
+_DS_COMPACT = os.environ.get("DTFX_DS_COMPACT", "1") != "0"  # stride-2 downsample dgrad kept compact
 STAGES = [(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)]  # (width, blocks, stride)
 IN_CH = 8          # 3 image channels + 5 zero channels
 NUM_CLASSES = 1000
@@ -336,6 +337,13 @@ class ResNet50:
         return CN.bn_bwd_apply(de, x, mean, rstd, P.P(name + ".bn.gamma"), P.G(name + ".bn.beta"),
                                P.G(name + ".bn.gamma"))
 
+    def _conv1_pro_wide(self, pre, c1, x_in):
+        """conv1's data gradient runs on the wide 1x1 kernel with the BN prologue (the path
+        that can read a compact stride-2 residual)."""
+        K, N = c1.shape[-1], x_in.shape[-1]
+        return (CN.bn_prologue_applies(c1, K, N, 2)
+                and not CN.hip().conv1x1_pro_applies(1, c1.numel() // K, K, N))
+
     def _wgrad_dgrad(self, name, dc, x_in, residual=None, need_dx=True, bn=None):
         P = self.params
         _, cin, cout, k, s, p = self.specs[name]
@@ -365,6 +373,7 @@ class ResNet50:
         # prologue when it can: one pass over de3 and c3 (dc3 written for the weight gradient)
         pro = dout_is_de and CN.bn_prologue_applies(c3, c3.shape[-1], a2.shape[-1], 2)
         dc3 = None
+        short_s2 = False  # dshort stored compact (stride-2 downsample, see below)
         if dout_is_de:
             dres = dout
             if not pro:
@@ -383,6 +392,21 @@ class ResNet50:
                                                      P.G(nd + ".bn.beta"), P.G(nd + ".bn.gamma"),
                                                      P.W(nd + ".weight"))
                 self._wgrad_dgrad(nd, dcs, x_in, need_dx=False)
+            elif (_DS_COMPACT and self.specs[nd][4] == 2 and self._conv1_pro_wide(pre, c1, x_in)
+                  and x_in.shape[1] % 2 == 0 and x_in.shape[2] % 2 == 0
+                  and x_in.shape[2] >= 16 and x_in.numel() // x_in.shape[-1] < (1 << 24)):
+                # stride-2 downsample: its data gradient lives at the even rows / columns only,
+                # so it stays compact [N, H/2, W/2, Cin] (a stride-1 1x1 product on the
+                # subsampled grid) and conv1's wide data gradient reads it as a stride-2
+                # residual -- no full-resolution tensor of mostly zeros written and read back
+                dcs, _ = self._bn_bwd(nd, dres, None, cs_, ms, rs, relu=False)
+                self._wgrad_dgrad(nd, dcs, x_in, need_dx=False)
+                # (a plain [pixels, Cout] x [Cout, Cin] GEMM: 118 / 68 us at layer2.0 / 3.0
+                # against 167 / 100 on the conv data-gradient path, tools/probes/ds_compact_gemm.py)
+                n_, h_, w_, cin = x_in.shape
+                dshort = B16.gemm(dcs.view(-1, dcs.shape[-1]), P.W(nd + ".weight")).view(
+                    n_, h_ // 2, w_ // 2, cin)
+                short_s2 = True
             else:
                 dcs, _ = self._bn_bwd(nd, dres, None, cs_, ms, rs, relu=False)
                 dshort = self._wgrad_dgrad(nd, dcs, x_in)
@@ -407,9 +431,11 @@ class ResNet50:
             # BN1's backward apply inside conv1's data gradient (dc1 written for the wgrad)
             dx, dc1 = CN.bn_in_conv1x1_dgrad(de1, c1, m1, r1, P.P(n1 + ".bn.gamma"),
                                              P.G(n1 + ".bn.beta"), P.G(n1 + ".bn.gamma"),
-                                             P.W(n1 + ".weight"), bn, residual=dshort)
+                                             P.W(n1 + ".weight"), bn, residual=dshort,
+                                             residual_s2=short_s2)
             self._wgrad_dgrad(n1, dc1, x_in, need_dx=False)
             return dx
+        assert not short_s2
         dc1 = self._bn_apply_bwd(n1, de1, c1, m1, r1)
         return self._wgrad_dgrad(n1, dc1, x_in, residual=dshort, bn=bn)
 

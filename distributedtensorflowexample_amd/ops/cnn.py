@@ -347,7 +347,7 @@ def bn_relu_conv1x1(c, s, q, M, gamma, beta, w, colsum, colsq, eps=1e-5, run_mea
 
 
 def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, want_dc=True,
-                        residual=None):
+                        residual=None, residual_s2=False):
     """BatchNorm backward's apply half and the data gradient of the 1x1 conv that produced the
     BatchNorm's input, in one pass.
 
@@ -357,8 +357,18 @@ def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, 
     (PRO 2) and written out when ``want_dc`` (the weight gradient reads it); the product is
     ``conv_dgrad(dc, w, residual=residual, bn=bn)`` -- with ``bn = (y, x, mean, rstd, sum_dy,
     sum_dyxh)`` the fused BatchNorm backward of the conv's own input (optional: without it
-    the narrow kernels run the plain data gradient, PRO 4).  Returns (dx, dc)."""
+    the narrow kernels run the plain data gradient, PRO 4).  ``residual_s2`` (wide kernels): the
+    residual is a stride-2 1x1 conv's data gradient stored compact, ``[N, H / 2, W / 2, Cin]``
+    (zero at odd rows / columns of the full grid -- never materialised).  Returns (dx, dc)."""
+    if residual is not None and residual_s2:
+        N_, H_, W_, _ = c.shape
+        if tuple(residual.shape) != (N_, H_ // 2, W_ // 2, w.shape[1]) or H_ % 2 or W_ % 2:
+            raise ValueError("residual_s2: residual must be [N, H/2, W/2, Cin] of an even grid")
     if not de.is_cuda:
+        if residual is not None and residual_s2:
+            full = torch.zeros(*c.shape[:-1], w.shape[1], dtype=residual.dtype)
+            full[:, ::2, ::2] = residual
+            residual = full
         dc = bn_bwd_apply(de, c, mean, rstd, gamma, sum_dy, sum_dyxh)
         N, H, W, _ = c.shape
         dx = conv_dgrad(dc, w, (N, H, W, w.shape[1]), 1, 1, 1, 0, residual=residual, bn=bn)
@@ -379,10 +389,11 @@ def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, 
         if y.shape != dx.shape or x.shape != dx.shape:
             raise ValueError("fused BN backward: y and x must have the dgrad output's shape")
         part = torch.empty(2, hip().conv1x1_rows(2, M, K, Cin), Cin, device=dev)
+    rh, rw = (c.shape[1], c.shape[2]) if residual is not None and residual_s2 else (0, 0)
     hip().conv1x1_pro(2, M, K, Cin, ptr(de), ptr(c), ptr(coef), ptr(dc), ptr(w), w.stride(0),
                       ptr(dx), ptr(residual), ptr(y), ptr(x), ptr(bmean), ptr(brstd),
                       ptr(None if part is None else part[0]), ptr(None if part is None else part[1]),
-                      ptr(wt), stream_handle())
+                      ptr(wt), stream_handle(), res_h=rh, res_w=rw)
     if part is not None:
         hip().colpart_reduce(part.shape[1], Cin, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
                              stream_handle())

@@ -336,6 +336,49 @@ def test_bn_in_conv1x1_dgrad_prologue(gpu, N, H, W, Cin, K, with_res, with_bn):
     assert torch.allclose(b, br, atol=0.05 * float(br.abs().max()) + 1e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("N,H,W,Cin,K", [
+    (2, 16, 16, 256, 128),   # layer2.0 conv1's data gradient + the downsample's (56 -> 28)
+    (2, 6, 16, 512, 256),    # layer3.0 class (two column blocks; a tile spans two grid rows)
+])
+def test_bn_in_conv1x1_dgrad_compact_residual(gpu, N, H, W, Cin, K):
+    """A stride-2 1x1 conv's data gradient kept compact [N, H/2, W/2, Cin] and read by the
+    wide dgrad kernel as a residual that is zero at odd rows / columns (conv1x1.hip rs_h /
+    rs_w) == the same residual expanded to full resolution (f32 CPU path)."""
+    M = N * H * W
+    c1 = _r(N, H, W, K, seed=61, scale=2).to(BF) + 0.5
+    c1f = c1.float().reshape(M, K)
+    m1, r1 = cnn.bn_finalize(c1f.sum(0), (c1f * c1f).sum(0), M)
+    g1 = _r(K, seed=62) * 0.1 + 1
+    de1 = _r(N, H, W, K, seed=63).to(BF)
+    d1 = de1.float().reshape(M, K)
+    sdy1, sdx1 = d1.sum(0), (d1 * (c1f - m1) * r1).sum(0)
+    cx = _r(N, H, W, Cin, seed=64, scale=2).to(BF) + 0.5
+    cxf = cx.float().reshape(M, Cin)
+    mx, rx = cnn.bn_finalize(cxf.sum(0), (cxf * cxf).sum(0), M)
+    yx = cnn.bn_apply(cx, mx, rx, _r(Cin, seed=65) * 0.1 + 1, _r(Cin, seed=66) * 0.1, None,
+                      relu=True)
+    w1 = _r(K, Cin, seed=67, scale=Cin ** -0.5).to(BF)
+    rc = _r(N, H // 2, W // 2, Cin, seed=68).to(BF)
+    full = torch.zeros(N, H, W, Cin, dtype=BF)
+    full[:, ::2, ::2] = rc
+
+    def run(dev, res, s2):
+        t = lambda v: v.to(dev)  # noqa: E731
+        sdy, sdx = torch.zeros(Cin, device=dev), torch.zeros(Cin, device=dev)
+        dx, _ = cnn.bn_in_conv1x1_dgrad(t(de1), t(c1), t(m1), t(r1), t(g1), t(sdy1), t(sdx1),
+                                        t(w1), (t(yx), t(cx), t(mx), t(rx), sdy, sdx),
+                                        residual=t(res), residual_s2=s2)
+        return dx.cpu().float(), sdy.cpu(), sdx.cpu()
+
+    dx, a, b = run(gpu, rc, True)
+    dxr, ar, br = run("cpu", full, False)
+    assert (dx - dxr).abs().max() < 3e-2 * dxr.abs().max()
+    assert torch.allclose(a, ar, atol=0.05 * float(ar.abs().max()) + 1e-2, rtol=2e-2)
+    assert torch.allclose(b, br, atol=0.05 * float(br.abs().max()) + 1e-2, rtol=2e-2)
+    dxg, _, _ = run(gpu, full, False)   # the full-resolution residual on the same kernel
+    assert (dx - dxg).abs().max() <= 1e-6 + 2 ** -7 * dxg.abs().max()
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 16, 16), (3, 15, 17)])   # odd sizes: clipped windows
 def test_stem_bn_maxpool_fused(gpu, N, H, W):
     """The stem's maxpool(relu(bn(c))) with relu(bn(c)) never stored (maxpool_bn_fwd_kernel) and
