@@ -35,6 +35,7 @@ void bn_bwd_launch(long long, int, const void*, const void*, const void*, const 
 long long bn_bwd_scratch_rows(long long, int);
 void colpart_reduce_launch(int, int, const float*, const float*, float*, float*, hipStream_t);
 bool stem_conv_applies(int, int, int, int, int, int, int, int);
+int stem_conv_fwd_rows(int, int, int);
 void stem_conv_fwd_launch(int, int, int, const void*, const void*, int, void*, float*, float*,
                           hipStream_t);
 void stem_conv_wgrad_launch(int, int, int, const void*, const void*, float*, int, float,
@@ -260,6 +261,8 @@ void register_nn(py::module_& m) {
                         P<void>(dres), S(s));
   });
   m.def("bn_bwd_scratch_rows", &dtfx::bn_bwd_scratch_rows);
+  m.def("stem_conv_fwd_rows", &dtfx::stem_conv_fwd_rows,
+        "(N, OH, OW): partial statistics rows stem_conv_fwd writes ([rows][64] each)");
   m.def("stem_conv_applies", &dtfx::stem_conv_applies,
         "the ResNet stem kernel handles this conv (7x7/2, pad 3, 8 -> 64 channels, OH % 8, OW % 16)");
   m.def("stem_conv_fwd", [](int N, int H, int W, uintptr_t x, uintptr_t w, int ldw, uintptr_t y,

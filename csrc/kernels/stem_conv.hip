@@ -36,6 +36,18 @@ __device__ __forceinline__ unsigned short tobf(float f) {
   return __builtin_bit_cast(unsigned short, b);
 }
 
+// Forward tiles: 16 x 16 output pixels, wave w owns output rows 4w..4w+3 (4 A fragments of
+// 16 pixels) x 64 channels (4 B fragments): 8 LDS fragment reads per 16 MFMAs (the first
+// version's 8 x 16 tiles with 2 rows per wave read 6 per 8 and were LDS-bound).  The 37 x 37
+// input patch is stored column-parity-major ([row][even columns | odd columns]) so the 16
+// lanes of a fragment, which read every second patch column, hit 16 consecutive 16-B slots.
+// A last tile row of an OH % 16 != 0 image is partial: rows >= OH are masked.
+constexpr int FTH = 16;                                        // forward output tile rows
+constexpr int FPR = (FTH - 1) * STR + KS;                      // 37 patch rows
+constexpr int FPH = (PC + 1) / 2;                              // 19 even-column slots per row
+constexpr int FPP = 2 * FPH;                                   // 38 slots per patch row
+constexpr int FP_BYTES = FPR * FPP * 16;                       // 22496 (output staging: 16 KB)
+
 __global__ __launch_bounds__(256, 2) void stem_conv_fwd_kernel(
     int N, int H, int W, int OH, int OW, const unsigned short* __restrict__ x,
     const unsigned short* __restrict__ w, int ldw, unsigned short* __restrict__ y,
@@ -50,71 +62,78 @@ __global__ __launch_bounds__(256, 2) void stem_conv_fwd_kernel(
     const int co = i / 56, c = i - co * 56;
     *(bf16x8*)(Ws + co * WP * 2 + c * 16) = *(const bf16x8*)(w + (size_t)co * ldw + c * 8);
   }
-  const int tiles_w = OW / TW, tiles_img = (OH / TH) * tiles_w;
+  const int tiles_w = OW / TW, tiles_h = (OH + FTH - 1) / FTH, tiles_img = tiles_h * tiles_w;
   const int tiles = N * tiles_img;
   const int cl = lane & 15, g = lane >> 4;
-  // input patch of tile tt into registers (zero outside the image): 777 16-B pixels, 4 per
+  // input patch of tile tt into registers (zero outside the image): 1369 16-B pixels, 6 per
   // thread -- issued one tile ahead, so the loads are in flight during the MFMAs
-  bf16x8 v[4];
+  bf16x8 v[6];
+  int pslot[6];  // LDS slot of each (tile-invariant)
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int p = tid + 256 * k, pr = p / PC, pc = p - pr * PC;
+    pslot[k] = p < FPR * PC ? pr * FPP + (pc & 1) * FPH + (pc >> 1) : -1;
+  }
   auto load_patch = [&](int tt) {
     const int n = tt / tiles_img, r = tt - n * tiles_img;
-    const int ih0 = (r / tiles_w) * TH * STR - PAD, iw0 = (r % tiles_w) * TW * STR - PAD;
+    const int ih0 = (r / tiles_w) * FTH * STR - PAD, iw0 = (r % tiles_w) * TW * STR - PAD;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 6; ++k) {
       const int p = tid + 256 * k, pr = p / PC, pc = p - pr * PC;
       const int ih = ih0 + pr, iw = iw0 + pc;
       v[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (p < PR * PC && ih >= 0 && ih < H && iw >= 0 && iw < W)
+      if (p < FPR * PC && ih >= 0 && ih < H && iw >= 0 && iw < W)
         v[k] = *(const bf16x8*)(x + (((size_t)n * H + ih) * W + iw) * CIN);
     }
   };
   if (blockIdx.x < tiles) load_patch(blockIdx.x);
   for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
     const int n = t / tiles_img, r = t - n * tiles_img;
-    const int oh0 = (r / tiles_w) * TH, ow0 = (r % tiles_w) * TW;
+    const int oh0 = (r / tiles_w) * FTH, ow0 = (r % tiles_w) * TW;
     __syncthreads();  // the previous tile's output staging (same LDS) is done
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int p = tid + 256 * k;
-      if (p < PR * PC) *(bf16x8*)(Ps + p * 16) = v[k];
-    }
+    for (int k = 0; k < 6; ++k)
+      if (pslot[k] >= 0) *(bf16x8*)(Ps + pslot[k] * 16) = v[k];
     __syncthreads();
     if (t + (int)gridDim.x < tiles) load_patch(t + gridDim.x);
-    f32x4 acc[2][4];
+    f32x4 acc[4][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int kg = 0; kg < NKG; ++kg) {
       const int tap = 4 * kg + g, kh = tap / KS, kw = tap - kh * KS;
-      bf16x8 a[2], b[4];
+      // this lane's pixel: output row 4 wave + i, column cl -> patch row 2 (4 wave + i) + kh,
+      // column 2 cl + kw (parity kw & 1, slot cl + kw / 2)
+      const int abase = ((8 * wave + kh) * FPP + (kw & 1) * FPH + cl + (kw >> 1)) * 16;
+      bf16x8 a[4], b[4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {  // this lane's pixel: output row 2 wave + i, column cl
-        const int pr = (2 * wave + i) * STR + kh, pc = cl * STR + kw;
-        a[i] = tap < KS * KS ? *(const bf16x8*)(Ps + (pr * PC + pc) * 16)
+      for (int i = 0; i < 4; ++i)
+        a[i] = tap < KS * KS ? *(const bf16x8*)(Ps + abase + i * 2 * FPP * 16)
                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         b[j] = *(const bf16x8*)(Ws + (16 * j + cl) * WP * 2 + (32 * kg + 8 * g) * 2);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    // BN statistics of the f32 values: lane (cl, g) holds channel 16 j + cl of pixels 4 g + r
-    const int prow = t * 4 + wave;  // one partial row per wave (32 pixels)
+    // BN statistics of the f32 values: lane (cl, g) holds channel 16 j + cl of pixels 4 g + rr
+    // of output row 4 wave + i; rows past OH (a partial last tile row) are masked
+    const int prow = t * 4 + wave;  // one partial row per wave (64 pixels)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float s = 0.f, q = 0.f;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 4; ++i)
+        if (oh0 + 4 * wave + i < OH)
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          s += acc[i][j][rr];
-          q += acc[i][j][rr] * acc[i][j][rr];
-        }
+          for (int rr = 0; rr < 4; ++rr) {
+            s += acc[i][j][rr];
+            q += acc[i][j][rr] * acc[i][j][rr];
+          }
       s += __shfl_xor(s, 16);
       s += __shfl_xor(s, 32);
       q += __shfl_xor(q, 16);
@@ -125,22 +144,27 @@ __global__ __launch_bounds__(256, 2) void stem_conv_fwd_kernel(
       }
     }
     __syncthreads();  // every wave is done reading the patch: reuse it for the output
-    char* st = Ps + wave * 4096;  // [32 px][64 co] bf16, 128-B rows (px = 16 i + column)
+    char* st = Ps + wave * 4096;  // [32 px][64 co] bf16, 128-B rows: two rows per pass
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int h = 0; h < 2; ++h) {
+      if (h) __builtin_amdgcn_wave_barrier();  // (the first pass's reads are done)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          *(unsigned short*)(st + (16 * i + 4 * g + rr) * 128 + (16 * j + cl) * 2) =
-              tobf(acc[i][j][rr]);
-    __builtin_amdgcn_wave_barrier();
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {  // 32 px x 8 chunks: 4 per lane, 16 B each, coalesced rows
-      const int e = lane + 64 * k, px = e >> 3, c = e & 7;
-      const int oh = oh0 + 2 * wave + (px >> 4), ow = ow0 + (px & 15);
-      *(bf16x8*)(y + (((size_t)n * OH + oh) * OW + ow) * COUT + c * 8) =
-          *(const bf16x8*)(st + px * 128 + c * 16);
+          for (int rr = 0; rr < 4; ++rr)
+            *(unsigned short*)(st + (16 * i + 4 * g + rr) * 128 + (16 * j + cl) * 2) =
+                tobf(acc[2 * h + i][j][rr]);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // 32 px x 8 chunks: 4 per lane, 16 B each, coalesced rows
+        const int e = lane + 64 * k, px = e >> 3, c = e & 7;
+        const int oh = oh0 + 4 * wave + 2 * h + (px >> 4), ow = ow0 + (px & 15);
+        if (oh < OH)
+          *(bf16x8*)(y + (((size_t)n * OH + oh) * OW + ow) * COUT + c * 8) =
+              *(const bf16x8*)(st + px * 128 + c * 16);
+      }
     }
   }
 }
@@ -314,6 +338,11 @@ void stem_conv_wgrad_launch(int N, int H, int W, const void* x, const void* dy, 
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+// psum / psq: stem_conv_fwd_rows() partial rows of 64 floats each
+int stem_conv_fwd_rows(int N, int OH, int OW) {
+  return N * ((OH + stem::FTH - 1) / stem::FTH) * (OW / stem::TW) * 4;
+}
+
 void stem_conv_fwd_launch(int N, int H, int W, const void* x, const void* w, int ldw, void* y,
                           float* psum, float* psq, hipStream_t s) {
   using namespace stem;
@@ -322,8 +351,10 @@ void stem_conv_fwd_launch(int N, int H, int W, const void* x, const void* w, int
   if (ldw < 56 * 8 || ldw % 8 || (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) & 15))
     throw std::runtime_error("stem_conv: weights need ld >= 448 (% 8), 16-B aligned tensors");
   const int OH = (H + 2 * PAD - KS) / STR + 1, OW = (W + 2 * PAD - KS) / STR + 1;
-  const int tiles = N * (OH / TH) * (OW / TW);
-  const size_t lds = W_BYTES + P_BYTES;
+  const int tiles = N * ((OH + FTH - 1) / FTH) * (OW / TW);
+  const size_t lds = W_BYTES + FP_BYTES;
+  static_assert(FP_BYTES >= 4 * 4096, "output staging");
+  static_assert(2 * (W_BYTES + FP_BYTES) <= 160 * 1024, "two blocks per CU");
   static bool attr = false;
   if (!attr) {
     DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)stem_conv_fwd_kernel,

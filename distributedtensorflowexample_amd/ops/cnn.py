@@ -77,8 +77,8 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
     if (colsum is not None and residual is None
             and hip().stem_conv_applies(H, W, C, Cout, KH, KW, stride, pad)):
         # the ResNet stem (7x7/2, 8 -> 64 channels): csrc/kernels/stem_conv.hip, input patch
-        # staged once per 8 x 16 output tile; one partial statistics row per 32 pixels
-        part = torch.empty(2, N * OH * OW // 32, Cout, device=x.device)
+        # staged once per 16 x 16 output tile; one partial statistics row per 64 pixels
+        part = torch.empty(2, hip().stem_conv_fwd_rows(N, OH, OW), Cout, device=x.device)
         hip().stem_conv_fwd(N, H, W, ptr(x), ptr(w), w.stride(0), ptr(y), ptr(part[0]),
                             ptr(part[1]), stream_handle())
         hip().colpart_reduce(part.shape[1], Cout, ptr(part[0]), ptr(part[1]), ptr(colsum),
