@@ -53,7 +53,7 @@ namespace dtfx {
 // 256x256: 8 waves of 128x64; 256x64 (conv fwd with 64 output channels): 4 waves of 64x64
 // stacked along M, 2 blocks/CU -- no MFMA work on a 128-wide tile's dead half).  NBUF = LDS stages (2: next tile in flight during
 // compute; 3: two tiles in flight, counted vmcnt + raw barrier).
-template <int MODE, bool TA, bool TB, bool OUT_F32, int BM_, int NBUF, int BN_>
+template <int MODE, bool TA, bool TB, bool OUT_F32, int BM_, int NBUF, int BN_, bool F1 = false>
 __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
                              (BM_ == 128 || BN_ == 64) && NBUF == 2 ? 2 : 1) void gemm_bf16_kernel(
     int M, int N, int K, const unsigned short* __restrict__ A, int lda,
@@ -208,6 +208,12 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
     const int a_bytes = CONV8 ? (int)min((long long)cd.N * csh * csw * cch * 2, 0x7fffffffLL) : 0x7fffffff;
     const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
     int cpb[4] = {0, 0, 0, 0}, cyx[4] = {0, 0, 0, 0};  // per A row (half * 2 + i): pixel base, y0 << 16 | x0
+    // F1 (its own instantiation, cfg 7): a 1x1 / stride-1 / pad-0 convolution (forward, or the
+    // data gradient's single phase class).  Every row reads its own pixel for every K tile, so
+    // the row's byte offset is final at setup (cpb holds it) and a K tile is the uniform
+    // soffset alone: no per-tile tap decode (scalar divisions + per-load address math left
+    // these products 34-46 % behind the plain GEMM on the same tile; a runtime branch for it
+    // slowed the 3x3 instantiation: profiles/r4/resnet_fast1_negative/)
     if constexpr (CONV8) {
       const int PW = MODE == 1 ? cd.OW : cd.Wc, PHW = MODE == 1 ? cd.OH * cd.OW : cd.Hc * cd.Wc;
 #pragma unroll
@@ -220,9 +226,22 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
         const int x0 = MODE == 1 ? px * cd.stride - cd.pad : px + cd.ox;
         cpb[r] = (n * csh + y0) * csw + x0;
         cyx[r] = (y0 << 16) | (x0 & 0xffff);
+        if constexpr (F1) {
+          const int row = ((r & 1) * NW + wave) * 8 + (lane >> 3);
+          cpb[r] = m < M ? cpb[r] * cch * 2 + (((lane & 7) ^ swz_kc(row)) << 4) : (int)0x80000000;
+        }
       }
     }
     auto conv_stage_a = [&](int buf, int which, int kt) {
+      if constexpr (F1) {
+        const int k0f = (kt0 + kt) * BK;
+        char* df = smem + (buf * 4 + which) * 16384;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(df + (i * NW + wave) * 1024), 16,
+                                                   cpb[which * 2 + i], k0f * 2, 0, 0);
+        return;
+      }
       const int k0 = (kt0 + kt) * BK, tap = k0 / cch, ch0 = k0 - tap * cch;
       const int tw_ = MODE == 1 ? cd.KW : max(cd.nkw, 1);
       const int th = tap / tw_, tw = tap - th * tw_;
@@ -241,6 +260,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
     };
     // MODE 2 B (weights, k-strided [64 co][ci] image): row co0 + kr of the tap's column block
     auto wtap_soff = [&](int kt) {
+      if constexpr (F1) return (kt0 + kt) * BK * ldb * 2;  // tap 0: weight row k0
       const int k0 = (kt0 + kt) * BK, ctap = k0 / cd.K, co0 = k0 - ctap * cd.K;
       const int th = ctap / max(cd.nkw, 1), tw = ctap - th * cd.nkw;
       const int tap = (cd.kh0 + cd.stride * th) * cd.KW + cd.kw0 + cd.stride * tw;
@@ -842,7 +862,7 @@ static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
   return 0;
 }
 
-template <int MODE, bool TA, bool TB, bool F, int BM_, int NBUF, int BN_ = 128>
+template <int MODE, bool TA, bool TB, bool F, int BM_, int NBUF, int BN_ = 128, bool F1 = false>
 static void launch_one(dim3 grid_yz, int M, int N, int K, const unsigned short* A, int lda,
                        const unsigned short* B, int ldb, void* C, int ldc, const GemmEpi& e,
                        long long sA, long long sB, long long sC, const ConvDesc& d,
@@ -853,7 +873,7 @@ static void launch_one(dim3 grid_yz, int M, int N, int K, const unsigned short* 
   static bool attr = false;
   if (!attr) {
     DTFX_HIP_CHECK(hipFuncSetAttribute(
-        (const void*)gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF, BN_>,
+        (const void*)gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF, BN_, F1>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
@@ -872,7 +892,7 @@ static void launch_one(dim3 grid_yz, int M, int N, int K, const unsigned short* 
     const size_t ep = (size_t)(threads / 64) * 32 * 68 * 4;
     lds_launch = stage > ep ? stage : ep;
   }
-  hipLaunchKernelGGL((gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF, BN_>),
+  hipLaunchKernelGGL((gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF, BN_, F1>),
                      dim3(tiles, grid_yz.y, grid_yz.z), dim3(threads), lds_launch, stream, M, N, K, A, lda,
                      B, ldb, C, ldc, e, sA, sB, sC, d);
   DTFX_HIP_CHECK(hipGetLastError());
@@ -897,6 +917,13 @@ static void launch_cfg(int cfg, dim3 grid_yz, int M, int N, int K, const unsigne
     if (cfg == 3) {
       launch_one<MODE, TA, TB, F, 256, 2, 256>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
                                                d, stream);
+      return;
+    }
+  }
+  if constexpr (MODE == 1 || MODE == 2) {
+    if (cfg == 7) {  // the 8-phase tile with the 1x1 / stride-1 staging (F1)
+      launch_one<MODE, TA, TB, F, 256, 8, 256, true>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA,
+                                                     sB, sC, d, stream);
       return;
     }
   }
@@ -1233,6 +1260,15 @@ static bool conv_ph8(int M, int N, int K, int zdim, int src_ch, long long src_el
          choose_cfg(M, N, zdim, 0) == 5;
 }
 
+// cfg 5 -> 7 for a 1x1 / stride-1 / pad-0 convolution (the F1 staging; DTFX_CONV_F1=0: off)
+static int conv_f1(int cfg, int KH, int KW, int stride, int pad) {
+  static const bool on = [] {
+    const char* v = getenv("DTFX_CONV_F1");
+    return v ? atoi(v) != 0 : true;
+  }();
+  return on && cfg == 5 && KH == 1 && KW == 1 && stride == 1 && pad == 0 ? 7 : cfg;
+}
+
 // Split-K of a forward / stride-1 data-gradient convolution on the 8-phase tile: the layer4
 // shapes (M = 12544 pixels x 512 channels, K = 2048 .. 4608) have 98 256x256 tiles for 256 CUs,
 // so the 128x128 tile (392 blocks) was chosen and ran them at 450-510 TFLOP/s.  Two K splits on
@@ -1354,7 +1390,7 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
       GemmEpi ep{};
       ep.alpha = 1.f;
       ep.ws = ws;
-      launch_cfg<1, false, true, true>(5, dim3(1, sk, 1), M, Nn, K, (const unsigned short*)a, 0,
+      launch_cfg<1, false, true, true>(conv_f1(5, KH, KW, stride, pad), dim3(1, sk, 1), M, Nn, K, (const unsigned short*)a, 0,
                                        (const unsigned short*)b, ldw, ws, Nn, ep, 0LL, 0LL, 0LL, d,
                                        stream);
       hipLaunchKernelGGL(conv_splitk_epi_kernel, dim3((Nn + 255) / 256, (M + 63) / 64), dim3(256), 0,
@@ -1365,7 +1401,7 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
       return;
     }
     const int cfg1 = conv_ph8(M, Nn, K, 1, C, (long long)N * H * W * C) ? 5 : choose_cfg(M, Nn, 1, 1);
-    launch_cfg<1, false, true, false>(cfg1, dim3(1, 1, 1), M, Nn, K,
+    launch_cfg<1, false, true, false>(conv_f1(cfg1, KH, KW, stride, pad), dim3(1, 1, 1), M, Nn, K,
                                       (const unsigned short*)a, 0, (const unsigned short*)b, ldw,
                                       out, Cout, e, 0LL, 0LL, 0LL, d, stream);
   } else if (mode == 2) {
@@ -1405,7 +1441,7 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
       GemmEpi ep{};
       ep.alpha = 1.f;
       ep.ws = ws;
-      launch_cfg<2, false, false, true>(5, dim3(1, sk, 1), M, Nn, K, (const unsigned short*)a, 0,
+      launch_cfg<2, false, false, true>(conv_f1(5, KH, KW, stride, pad), dim3(1, sk, 1), M, Nn, K, (const unsigned short*)a, 0,
                                         (const unsigned short*)b, d.wld, ws, Nn, ep, 0LL, 0LL, 0LL,
                                         d, stream);
       hipLaunchKernelGGL(conv_splitk_epi_kernel, dim3((Nn + 255) / 256, (M + 63) / 64), dim3(256), 0,
@@ -1418,7 +1454,7 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
     }
     const int cfg2 = conv_ph8(M, Nn, ((KH + s - 1) / s) * ((KW + s - 1) / s) * Cout, s * s, Cout, (long long)N * OH * OW * Cout)
                          ? 5 : choose_cfg(M, Nn, s * s, 2);
-    launch_cfg<2, false, false, false>(cfg2, dim3(1, 1, s * s), M, Nn, K,
+    launch_cfg<2, false, false, false>(conv_f1(cfg2, KH, KW, stride, pad), dim3(1, 1, s * s), M, Nn, K,
                                        (const unsigned short*)a, 0, (const unsigned short*)b, d.wld,
                                        out, C, e, 0LL, 0LL, 0LL, d, stream);
   } else if (mode == 3) {
