@@ -10,6 +10,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from distributedtensorflowexample_amd.models.bert import BertConfig  # noqa: E402
 from distributedtensorflowexample_amd.ops import bf16 as B16, hip  # noqa: E402
 
 
@@ -28,17 +29,18 @@ def timeit(fn, iters=20):
 def main():
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
+    V = BertConfig().vocab_padded  # the model's padded vocabulary (row stride % 8 == 0)
     for M in (2432, 2458, 4915):
         x = torch.randn(M, 768, device=dev).to(torch.bfloat16)
-        E = torch.randn(30522, 768, device=dev).mul_(0.02).to(torch.bfloat16)
-        b = torch.zeros(30522, device=dev)
-        res = {"M": M, "N": 30522, "K": 768}
+        E = torch.randn(V, 768, device=dev).mul_(0.02).to(torch.bfloat16)
+        b = torch.zeros(V, device=dev)
+        res = {"M": M, "N": V, "K": 768}
         for cfg in (-1, 0, 5, 6):
             hip().gemm_bf16_set_cfg(cfg)
             us = timeit(lambda: B16.gemm(x, E, False, True, bias=b, out_dtype=torch.float32))
             res["us_cfg%d" % cfg if cfg >= 0 else "us_auto"] = round(us, 1)
         hip().gemm_bf16_set_cfg(-1)
-        res["tflops_auto"] = round(2 * M * 30522 * 768 / res["us_auto"] * 1e-6, 1)
+        res["tflops_auto"] = round(2 * M * V * 768 / res["us_auto"] * 1e-6, 1)
         print(json.dumps(res), flush=True)
 
 
