@@ -42,7 +42,7 @@ void stem_conv_wgrad_launch(int, int, int, const void*, const void*, float*, int
                             hipStream_t, const void*, const float*);
 bool conv3x3_c64_applies(int, int, int, int, int, int, int, int);
 void conv3x3_c64_fwd_launch(int, int, int, const void*, const void*, int, void*, float*, float*,
-                            hipStream_t);
+                            hipStream_t, const float* = nullptr, void* = nullptr);
 void conv3x3_c64_wgrad_launch(int, int, int, const void*, const void*, float*, int, float,
                               hipStream_t);
 void conv3x3_c64_dgrad_launch(int, int, int, const void*, const void*, int, void*, const void*,
@@ -279,10 +279,12 @@ void register_nn(py::module_& m) {
   m.def("conv3x3_c64_applies", &dtfx::conv3x3_c64_applies,
         "the 64-channel 3x3 kernel handles this conv (stride 1, pad 1, H % 4, W % 28)");
   m.def("conv3x3_c64_fwd", [](int N, int H, int W, uintptr_t x, uintptr_t w, int ldw, uintptr_t y,
-                              uintptr_t ps, uintptr_t pq, uintptr_t s) {
+                              uintptr_t ps, uintptr_t pq, uintptr_t s, uintptr_t coef, uintptr_t xo) {
     dtfx::conv3x3_c64_fwd_launch(N, H, W, P<const void>(x), P<const void>(w), ldw, P<void>(y),
-                                 P<float>(ps), P<float>(pq), S(s));
-  });
+                                 P<float>(ps), P<float>(pq), S(s), P<const float>(coef), P<void>(xo));
+  }, py::arg("N"), py::arg("H"), py::arg("W"), py::arg("x"), py::arg("w"), py::arg("ldw"),
+     py::arg("y"), py::arg("ps"), py::arg("pq"), py::arg("s"), py::arg("coef") = 0,
+     py::arg("xo") = 0, "coef / xo: relu(bn(x)) formed in the patch staging and written to xo");
   m.def("conv3x3_c64_wgrad", [](int N, int H, int W, uintptr_t x, uintptr_t dy, uintptr_t dw,
                                 int ldw, float beta, uintptr_t s) {
     dtfx::conv3x3_c64_wgrad_launch(N, H, W, P<const void>(x), P<const void>(dy), P<float>(dw), ldw,

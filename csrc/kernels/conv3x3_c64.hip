@@ -64,12 +64,18 @@ __global__ __launch_bounds__(256) void conv3x3_c64_flip_kernel(const unsigned sh
   wf[i] = w[(size_t)co * ldw + (8 - tap) * C + ci];
 }
 
-template <bool DGRAD>
+// PRO (forward): x is the raw output c of the previous conv and the patch is formed as
+// relu(c a + b) per channel (coef rows 0 / 2 of bn_fwd_coef) while it is staged; in-image
+// pixels only (the zero padding stays zero), and each tile writes its own (interior) pixels of
+// the result to xo once -- the backward reads it.  The bn_apply pass that wrote it and this
+// kernel's read of it become one read of c.
+template <bool DGRAD, bool PRO = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(
     int N, int H, int W, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
     int ldw, unsigned short* __restrict__ y, const unsigned short* __restrict__ relu_y,
     const unsigned short* __restrict__ bn_x, const float* __restrict__ bn_mean,
-    const float* __restrict__ bn_rstd, float* __restrict__ psum, float* __restrict__ psq) {
+    const float* __restrict__ bn_rstd, float* __restrict__ psum, float* __restrict__ psq,
+    const float* __restrict__ coef = nullptr, unsigned short* __restrict__ xo = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char sm[];
   char* Ws = sm;
   char* Ps = sm + W_BYTES;  // patch, then the K-half partials, then the output staging
@@ -90,6 +96,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(
     for (int u = 0; u < 8; ++u) {
       mu[u] = bn_mean[ec * 8 + u];
       rs[u] = bn_rstd[ec * 8 + u];
+    }
+  }
+  float pa[8], pc_[8];  // PRO: this thread's channels (chunk tid & 7) scale / shift
+  if constexpr (PRO) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      pa[u] = coef[ec * 8 + u];
+      pc_[u] = coef[2 * C + ec * 8 + u];
     }
   }
   bf16x8 v[5];  // patch chunks of the next tile: 2400 / 512 -> 5 per thread
@@ -130,7 +144,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       const int e = tid + 512 * k, q = e >> 3, c = e & 7;
-      if (e < PCH2) *(bf16x8*)(Ps + q * PP2 + c * 16) = v[k];
+      if (e < PCH2) {
+        bf16x8 o = v[k];
+        if constexpr (PRO) {
+          const int ih = oh0 - 1 + lpr[k], iw = ow0 - 1 + lpc[k];
+          if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              o[u] = (short)tobf(fmaxf(__uint_as_float((unsigned)(unsigned short)v[k][u] << 16) * pa[u] + pc_[u], 0.f));
+            if (lpr[k] >= 1 && lpr[k] <= TH2 && lpc[k] >= 1 && lpc[k] <= TW)  // this tile's own pixel
+              *(bf16x8*)(xo + (((size_t)n * H + ih) * W + iw) * C + c * 8) = o;
+          }
+        }
+        *(bf16x8*)(Ps + q * PP2 + c * 16) = o;
+      }
     }
     __syncthreads();
     if (t + (int)gridDim.x < tiles) load_patch(t + gridDim.x);
@@ -441,25 +468,32 @@ void conv3x3_c64_wgrad_launch(int N, int H, int W, const void* x, const void* dy
 }
 
 // y = conv3x3(x, w), psum / psq: partial statistic rows [4 * tiles][64] (tiles = N*H*W / 224)
+// coef / xo (both or neither): x is the previous conv's raw output and relu(bn(x)) (coef: the
+// [4][64] bn_fwd_coef rows) is formed as the patch is staged and written to xo.
 void conv3x3_c64_fwd_launch(int N, int H, int W, const void* x, const void* w, int ldw, void* y,
-                            float* psum, float* psq, hipStream_t s) {
+                            float* psum, float* psq, hipStream_t s, const float* coef, void* xo) {
   using namespace c3;
   if (!conv3x3_c64_applies(H, W, C, C, 3, 3, 1, 1))
     throw std::runtime_error("conv3x3_c64: unsupported geometry");
-  if (ldw < 9 * C || ldw % 8 || (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) & 15))
+  if (ldw < 9 * C || ldw % 8 || (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y | (uintptr_t)xo) & 15))
     throw std::runtime_error("conv3x3_c64: weights need ld >= 576 (% 8), 16-B aligned tensors");
+  if ((coef != nullptr) != (xo != nullptr))
+    throw std::runtime_error("conv3x3_c64: the BN prologue needs both coef and xo");
   const int tiles = N * (H / TH2) * (W / TW);
   const size_t lds = W_BYTES + R_BYTES;
   static bool attr = false;
   if (!attr) {
     DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_c64_kernel<false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_c64_kernel<false, true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
   const int blocks = std::min(tiles, 256);
-  hipLaunchKernelGGL(conv3x3_c64_kernel<false>, dim3(blocks), dim3(512), lds, s, N, H, W,
-                     (const unsigned short*)x, (const unsigned short*)w, ldw, (unsigned short*)y,
-                     nullptr, nullptr, nullptr, nullptr, psum, psq);
+  auto k = coef ? conv3x3_c64_kernel<false, true> : conv3x3_c64_kernel<false, false>;
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, s, N, H, W, (const unsigned short*)x,
+                     (const unsigned short*)w, ldw, (unsigned short*)y, nullptr, nullptr, nullptr,
+                     nullptr, psum, psq, coef, (unsigned short*)xo);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

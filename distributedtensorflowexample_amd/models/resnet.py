@@ -197,8 +197,19 @@ class ResNet50:
                     c1, s1 = self._conv_bn(pre + "conv1", x_in)
                 else:
                     x_in, c1, s1 = self._finish_block(blocks, pend, pre + "conv1")
-                a1, m1, r1 = self._bn_apply(pre + "conv1", c1, s1)
-                c2, s2 = self._conv_bn(pre + "conv2", a1)
+                n2 = pre + "conv2"
+                if CN.bn_relu_conv3x3_applies(c1, P.W(n2 + ".weight")) and self.specs[n2][4] == 1:
+                    # layer1: relu(bn1(c1)) formed in the 64-channel 3x3 kernel's patch staging
+                    cs, cq, M1 = s1
+                    ncs, ncq = self._stats[n2]
+                    rm, rv = P.running[pre + "conv1"]
+                    a1, c2, m1, r1 = CN.bn_relu_conv3x3(
+                        c1, cs, cq, M1, P.P(pre + "conv1.bn.gamma"), P.P(pre + "conv1.bn.beta"),
+                        P.W(n2 + ".weight"), ncs, ncq, self.eps, rm, rv)
+                    s2 = (ncs, ncq, c2.numel() // c2.shape[-1])
+                else:
+                    a1, m1, r1 = self._bn_apply(pre + "conv1", c1, s1)
+                    c2, s2 = self._conv_bn(n2, a1)
                 a2, m2, r2, c3, s3 = self._bn_relu_conv(pre + "conv2", c2, s2, pre + "conv3")
                 # (first block: the downsample conv of the same input; its BatchNorm is applied
                 # with bn3's, the normalised shortcut is never materialised)

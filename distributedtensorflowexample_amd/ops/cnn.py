@@ -346,6 +346,48 @@ def bn_relu_conv1x1(c, s, q, M, gamma, beta, w, colsum, colsq, eps=1e-5, run_mea
     return a, y, st[0], st[1]
 
 
+def bn_relu_conv3x3_applies(c, w):
+    """The 64-channel 3x3 kernel (with its BatchNorm + ReLU prologue) takes ``conv(relu(bn(c)))``
+    for these shapes.  Opt-in (``DTFX_BN_PROLOGUE_C64=1``): in the ResNet-50 step it measured
+    11,742-11,752 vs 11,753-11,769 img/s for the separate bn_apply pass (interleaved, one box,
+    ``profiles/r4/resnet_c64pro/``) -- the transform and the scattered writes of ``a`` sit in the
+    kernel's staging phase, which the 64-channel forward cannot hide."""
+    N, H, W, C = c.shape
+    return (c.is_cuda and _BN_PRO and _BN_PRO_C64 and w.shape[0] == C
+            and bool(hip().conv3x3_c64_applies(H, W, C, C, 3, 3, 1, 1)))
+
+
+_BN_PRO_C64 = os.environ.get("DTFX_BN_PROLOGUE_C64", "0") == "1"
+
+
+def bn_relu_conv3x3(c, s, q, M, gamma, beta, w, colsum, colsq, eps=1e-5, run_mean=None,
+                    run_var=None, momentum=0.9):
+    """``a = relu(bn(c))`` (training-mode BatchNorm from c's column sums) and the 3x3 / stride-1
+    / pad-1 conv ``y = conv(a, w)`` with y's BatchNorm statistics accumulated into ``colsum`` /
+    ``colsq``, in one pass over ``c`` (GPU: ``conv3x3_c64.hip``'s prologue forms ``a`` as the
+    input patch is staged and writes each tile's own pixels of it once).  Returns
+    (a, y, mean, rstd)."""
+    if not c.is_cuda:
+        a, mean, rstd = bn_apply_stats(c, s, q, M, gamma, beta, None, True, eps, run_mean, run_var,
+                                       momentum)
+        return a, conv_fwd(a, w, 3, 3, 1, 1, colsum=colsum, colsq=colsq), mean, rstd
+    N, H, W, K = c.shape
+    Cout = w.shape[0]
+    st = torch.empty(2, K, device=c.device)
+    coef = torch.empty(4, K, device=c.device)
+    hip().bn_fwd_coef(int(M), K, ptr(s), ptr(q), float(eps), ptr(st[0]), ptr(st[1]), ptr(run_mean),
+                      ptr(run_var), float(momentum), ptr(gamma), ptr(beta), 0, 0, 0, 0, 0, 0, 0, 0,
+                      ptr(coef), stream_handle())
+    a = torch.empty_like(c)
+    y = torch.empty(N, H, W, Cout, device=c.device, dtype=BF16)
+    part = torch.empty(2, 4 * (N * H * W // 224), Cout, device=c.device)
+    hip().conv3x3_c64_fwd(N, H, W, ptr(c), ptr(w), w.stride(0), ptr(y), ptr(part[0]),
+                          ptr(part[1]), stream_handle(), coef=ptr(coef), xo=ptr(a))
+    hip().colpart_reduce(part.shape[1], Cout, ptr(part[0]), ptr(part[1]), ptr(colsum), ptr(colsq),
+                         stream_handle())
+    return a, y, st[0], st[1]
+
+
 def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, want_dc=True,
                         residual=None, residual_s2=False):
     """BatchNorm backward's apply half and the data gradient of the 1x1 conv that produced the

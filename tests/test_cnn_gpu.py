@@ -379,6 +379,35 @@ def test_bn_in_conv1x1_dgrad_compact_residual(gpu, N, H, W, Cin, K):
     assert (dx - dxg).abs().max() <= 1e-6 + 2 ** -7 * dxg.abs().max()
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 8, 56), (3, 16, 28)])
+def test_bn_relu_conv3x3_c64_prologue(gpu, N, H, W):
+    """relu(bn(c)) formed in the 64-channel 3x3 kernel's patch staging (conv3x3_c64.hip PRO),
+    written once to a, then the conv with its output statistics == bn_apply_stats then conv_fwd
+    (f32 CPU path): a, y, the column sums, mean / rstd and the running statistics."""
+    C = 64
+    M = N * H * W
+    c = _r(N, H, W, C, seed=71, scale=2).to(BF) + 0.25
+    cf = c.float().reshape(M, C)
+    s, q = cf.sum(0), (cf * cf).sum(0)
+    g, b = _r(C, seed=72) * 0.1 + 1, _r(C, seed=73) * 0.1
+    w = (_r(C, 9 * C, seed=74, scale=(9 * C) ** -0.5)).to(BF)
+
+    def run(dev):
+        t = lambda v: v.to(dev)  # noqa: E731
+        cs, cq = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        a, y, m, r = cnn.bn_relu_conv3x3(t(c), t(s), t(q), M, t(g), t(b), t(w), cs, cq, 1e-5,
+                                         rm, rv)
+        return [v.cpu().float() for v in (a, y, cs, cq, m, r, rm, rv)]
+
+    got, ref = run(gpu), run("cpu")
+    a, y = got[0], got[1]
+    assert (a - ref[0]).abs().max() <= 2 ** -7 * ref[0].abs().max() + 1e-6
+    assert (y - ref[1]).abs().max() < 3e-2 * ref[1].abs().max()
+    for x_, r_ in zip(got[2:], ref[2:]):
+        assert torch.allclose(x_, r_, rtol=1e-2, atol=1e-2 * float(r_.abs().max()) + 1e-5)
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 16, 16), (3, 15, 17)])   # odd sizes: clipped windows
 def test_stem_bn_maxpool_fused(gpu, N, H, W):
     """The stem's maxpool(relu(bn(c))) with relu(bn(c)) never stored (maxpool_bn_fwd_kernel) and
