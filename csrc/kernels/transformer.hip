@@ -1455,13 +1455,14 @@ void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, cons
     const char* e = std::getenv("DTFX_ATTN_BWD_WAVES");
     return e && std::atoi(e) == 4 ? 4 : 8;
   }();
-  // DTFX_ATTN_BWD_HALF=1: the two-blocks-per-CU kernel.  Alone it is 18 % faster (BERT-base
-  // shape, batch 128: 56 vs 69 us), but in the BERT step it runs beside the weight-gradient
-  // GEMMs of the second stream and both take 94 us there (rocprofv3, same box); end to end
-  // 7892 vs 7924 seq/s over 3 interleaved rounds, so it stays opt-in.
+  // The two-blocks-per-CU kernel (default; DTFX_ATTN_BWD_HALF=0: the 8-wave one).  Alone it is
+  // 14-18 % faster (BERT-base shape, batch 128: 56.9 vs 66.3 us).  Beside the weight-gradient
+  // GEMMs of a second stream it lost that (round 3: 7892 vs 7924 seq/s); with the one-GPU BERT
+  // step now issuing its weight gradients in order (train/bert_trainer.py) it gains: 7,903-7,919
+  // -> 8,034-8,055 seq/s interleaved (profiles/r4/bert/half_nows/).
   static const bool half = [] {
     const char* e = std::getenv("DTFX_ATTN_BWD_HALF");
-    return e && std::atoi(e) == 1;
+    return !(e && std::atoi(e) == 0);
   }();
   // DTFX_ATTN_BWD_PERSIST=1: the persistent kernel (grid: DTFX_ATTN_BWD_BLOCKS, default one
   // block per CU).  Measured slower: 84 us standalone vs 68 for the 8-wave per-pair kernel (128
