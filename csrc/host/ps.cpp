@@ -566,14 +566,33 @@ class PSClient {
     }
   }
   ~PSClient() {
-    close();
+    if (psp_.active) {
+      // an exchange whose end() never came (mu_ still held by its thread, maybe this one):
+      // nobody can finish it, so do not wait for mu_ -- wake the sender, join it, then close
+      for (int fd : fds_)
+        if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
+      stop_sender();
+      close_fds();
+      return;
+    }
+    if (PyGILState_Check()) {  // (Python dealloc): never wait for mu_ while holding the GIL
+      py::gil_scoped_release nogil;
+      close();
+    } else {
+      close();
+    }
     stop_sender();
   }
 
+  // Bound with the GIL released (py::call_guard): an exchange that another thread has open
+  // (push_step_pull_begin .. end) holds mu_ while that thread runs Python WITH the GIL
+  // (next_batch, stage) before it calls end(); waiting for mu_ here with the GIL held would
+  // deadlock both threads.  Without the GIL, close() simply waits for that end().
   void close() {
-    // (waits for an exchange another thread has in flight; that thread holds mu_ without
-    // the GIL and releases mu_ before re-taking the GIL, so this cannot deadlock)
     std::lock_guard<std::mutex> lk(mu_);
+    close_fds();
+  }
+  void close_fds() {
     for (int& fd : fds_)
       if (fd >= 0) {
         ::close(fd);
@@ -1205,6 +1224,6 @@ void register_ps(py::module_& m) {
       .def("list_vars", &PSClient::list_vars)
       .def("ping", &PSClient::ping)
       .def("shutdown_server", &PSClient::shutdown_server)
-      .def("close", &PSClient::close)
+      .def("close", &PSClient::close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("num_tasks", &PSClient::num_tasks);
 }

@@ -305,30 +305,35 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     using xgll::u64;
     const long long par = ep & 1u, plane = (long long)HP * BP;
     const int me = xg.rank;
+    auto local = [&](int q) { return (const u64*)xg.peers.data[me] + (par * XW + q) * xg.S; };
+    size_t offs[2];
+    bool act[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {  // push first: every peer's wait overlaps ours
-      const int j = 2 * lane + u;
-      if (j < H) {
-        const long long off = (long long)j * BP + row;
+    for (int u = 0; u < 2; ++u) {
+      act[u] = 2 * lane + u < H;
+      offs[u] = (size_t)(act[u] ? 2 * lane + u : 0) * BP + row;
+    }
+    // first polls, then the pushes (xgll::first_loads: one vmcnt for both); every peer's
+    // wait still overlaps ours
+    u64 wq[2][XW];
+    xgll::first_loads<XW, 2>(local, offs, act, me, ep, wq);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (act[u]) {
         const u64 wd = xgll::word(dzv[u], ep);
 #pragma unroll
         for (int d = 0; d < XW; ++d)
-          if (d != me) xgll::store((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + off, wd);
+          if (d != me) xgll::store((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + offs[u], wd);
       }
     }
-    auto local = [&](int q) { return (const u64*)xg.peers.data[me] + (par * XW + q) * xg.S; };
     bool fail = false;
+    float vals[2][XW];
+    xgll::finish_all_n<XW, 2>(local, offs, act, me, ep, wq, dzv, vals, xg.ticks, fail);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int j = 2 * lane + u;
-      if (j < H) {
-        const long long off = (long long)j * BP + row;
-        float vals[XW];
-        xgll::gather_all<XW>(local, off, me, ep, dzv[u], xg.ticks, vals, fail);
+    for (int u = 0; u < 2; ++u)
+      if (act[u])
 #pragma unroll
-        for (int q = 0; q < XW; ++q) dz1A[q * plane + off] = vals[q];
-      }
-    }
+        for (int q = 0; q < XW; ++q) dz1A[q * plane + offs[u]] = vals[u][q];
     if (lane == 0) xg.epochs[MLP_XG_HEAD_EPOCH + row] = ep;
     if (fail) atomicExch(xg.err, 1);
   }
@@ -356,6 +361,9 @@ __device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const 
   using xgll::u64;
   const long long par = ep & 1u;
   const int me = xg.rank;
+  auto local = [&](int j) { return (const u64*)xg.peers.data[me] + (par * XW + j) * xg.S; };
+  u64 w[N][XW];  // first polls before the pushes (xgll::first_loads: one vmcnt for both)
+  xgll::first_loads<XW, N>(local, off, ok, me, ep, w);
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     if (!ok[i]) continue;
@@ -364,8 +372,7 @@ __device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const 
     for (int d = 0; d < XW; ++d)
       if (d != me) xgll::store((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + off[i], wd);
   }
-  auto local = [&](int j) { return (const u64*)xg.peers.data[me] + (par * XW + j) * xg.S; };
-  if (!fail) xgll::gather_sum_n<XW, N>(local, off, ok, me, ep, v, xg.ticks, fail);
+  if (!fail) xgll::finish_sum_n<XW, N>(local, off, ok, me, ep, w, v, xg.ticks, fail);
 }
 
 // Two-shot form of xg_exchange (reduce-scatter + all-gather inside the wave): element i of
@@ -397,14 +404,14 @@ __device__ __forceinline__ void xg_exchange16(const MlpXg& xg, unsigned ep, long
   const long long par = ep & 1u;
   const int me = xg.rank;
   const u32x4 out = {__float_as_uint(v[0]), ep, __float_as_uint(v[1]), ep};
-#pragma unroll
-  for (int d = 0; d < XW; ++d)
-    if (d != me) *(u32x4*)((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + woff) = out;
-  u32x4 w[XW];
+  u32x4 w[XW];  // first polls before the pushes (xgll::first_loads: one vmcnt for both)
 #pragma unroll
   for (int j = 0; j < XW; ++j)
     if (j != me)
       w[j] = *(volatile u32x4*)((const u64*)xg.peers.data[me] + (par * XW + j) * xg.S + woff);
+#pragma unroll
+  for (int d = 0; d < XW; ++d)
+    if (d != me) *(u32x4*)((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + woff) = out;
   const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
   for (;;) {
     bool ready = true;
@@ -431,6 +438,93 @@ __device__ __forceinline__ void xg_exchange16(const MlpXg& xg, unsigned ep, long
   v[1] = a1;
 }
 
+// Two-shot form of xg_exchange16 (fused2x, round 5): a lane's TWO elements travel as one
+// 16-byte word pair in the XG_W1_BASE layout (`woff`, as the one-shot) and the PAIR has one
+// owner rank, (q + 4 sp) % XW -- the same on every rank; at 8 ranks the 8 (q, sp) classes of a
+// column group are the 8 owners.  (1) a non-owner lane pushes its pair to the owner's slot
+// (parity, me); (2) an owner lane gathers the XW - 1 peers' pairs, sums each element in rank
+// order and pushes the sums into every peer's result region (2 XW + parity); (3) a non-owner
+// lane waits for its owner's sums.  Per hop one 16-byte store / load per lane and peer instead
+// of two 8-byte LL accesses to two owners (per-element owners, xg_exchange2), and every poll
+// is issued before the hop's own pushes (xgll::first_loads: stores and loads share one
+// in-order vmcnt).  Each 8-byte half carries the epoch, as in xg_exchange16.
+template <int XW>
+__device__ __forceinline__ void xg_exchange2p(const MlpXg& xg, unsigned ep, long long woff,
+                                              float (&v)[2], bool& fail, int lane, int sp,
+                                              unsigned long long* trw = nullptr) {
+  using xgll::u64;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const long long par = ep & 1u;
+  const int me = xg.rank;
+  const int own = ((lane >> 4) + 4 * sp) % XW;
+  const bool mine = own == me;
+  auto slot = [&](int dst, int src) {
+    return (u32x4*)((u64*)xg.peers.data[dst] + (par * XW + src) * xg.S + woff);
+  };
+  auto result = [&](int dst) { return (u32x4*)((u64*)xg.peers.data[dst] + (2 * XW + par) * xg.S + woff); };
+  auto ready2 = [&](const u32x4& w) { return w.y == ep && w.w == ep; };
+  // ---- hop 1: owners' first polls, then the non-owners' push to their owner
+  u32x4 w[XW];
+#pragma unroll
+  for (int j = 0; j < XW; ++j)
+    if (mine && j != me) w[j] = *(volatile u32x4*)slot(me, j);
+  const u32x4 out = {__float_as_uint(v[0]), ep, __float_as_uint(v[1]), ep};
+  // uniform loop over destinations, per-lane predicate: a per-lane peer index would turn the
+  // kernel-argument pointer table into a private (scratch) array
+#pragma unroll
+  for (int d = 0; d < XW; ++d)
+    if (d != me && own == d) *slot(d, me) = out;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  if (mine) {
+    for (;;) {
+      bool ready = true;
+#pragma unroll
+      for (int j = 0; j < XW; ++j)
+        if (j != me && !ready2(w[j])) {
+          ready = false;
+          w[j] = *(volatile u32x4*)slot(me, j);
+        }
+      if (ready) break;
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xg.ticks) {
+        fail = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    float a0 = 0.f, a1 = 0.f;  // rank-ordered sums: the same bits on every rank
+#pragma unroll
+    for (int j = 0; j < XW; ++j) {
+      a0 += j == me ? v[0] : __uint_as_float(w[j].x);
+      a1 += j == me ? v[1] : __uint_as_float(w[j].z);
+    }
+    v[0] = a0;
+    v[1] = a1;
+  }
+  if (trw) trace_stamp(trw, 5);  // probe builds: the owned sums are complete
+  // ---- hop 2: non-owners' first poll of the result, then the owners' broadcast
+  u32x4 r = {0u, 0u, 0u, 0u};
+  if (!mine) r = *(volatile u32x4*)result(me);
+  if (mine && !fail) {
+    const u32x4 sum = {__float_as_uint(v[0]), ep, __float_as_uint(v[1]), ep};
+#pragma unroll
+    for (int d = 0; d < XW; ++d)
+      if (d != me) *result(d) = sum;
+  }
+  if (!mine) {
+    const long long t1 = (long long)__builtin_amdgcn_s_memrealtime();
+    while (!ready2(r)) {
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t1 > xg.ticks) {
+        fail = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      r = *(volatile u32x4*)result(me);
+    }
+    v[0] = __uint_as_float(r.x);
+    v[1] = __uint_as_float(r.z);
+  }
+}
+
 // N < 4: the lane's elements i0 .. i0 + N - 1 of the four (the exchange split over the
 // K-split waves of mlp_fwdapply_kernel); ownership is by the element index i either way.
 template <int XW, int N = 4>
@@ -452,6 +546,10 @@ __device__ __forceinline__ void xg_exchange2(const MlpXg& xg, unsigned ep, const
   }
   auto slot = [&](int dst, int src) { return (u64*)xg.peers.data[dst] + (par * XW + src) * xg.S; };
   auto result = [&](int dst) { return (u64*)xg.peers.data[dst] + (2 * XW + par) * xg.S; };
+  auto local = [&](int j) { return (const u64*)slot(me, j); };
+  // each hop issues its first polls before its pushes (xgll::first_loads: one vmcnt for both)
+  u64 w1[N][XW];
+  xgll::first_loads<XW, N>(local, off, mine, me, ep, w1);
   // uniform loop over destinations, per-lane predicate: a per-lane peer index would turn the
   // kernel-argument pointer table into a private (scratch) array
 #pragma unroll
@@ -462,9 +560,10 @@ __device__ __forceinline__ void xg_exchange2(const MlpXg& xg, unsigned ep, const
     for (int i = 0; i < N; ++i)
       if (other[i] && own[i] == d) xgll::store(dst + off[i], xgll::word(v[i], ep));
   }
-  auto local = [&](int j) { return (const u64*)slot(me, j); };
-  if (!fail) xgll::gather_sum_n<XW, N>(local, off, mine, me, ep, v, xg.ticks, fail);
+  if (!fail) xgll::finish_sum_n<XW, N>(local, off, mine, me, ep, w1, v, xg.ticks, fail);
   if (trw) trace_stamp(trw, 5);  // probe builds: the owned sums are complete
+  u64 w2[N];
+  xgll::first_loads1<N>(result(me), off, other, ep, w2);
 #pragma unroll
   for (int d = 0; d < XW; ++d) {
     if (d == me) continue;
@@ -473,7 +572,7 @@ __device__ __forceinline__ void xg_exchange2(const MlpXg& xg, unsigned ep, const
     for (int i = 0; i < N; ++i)
       if (mine[i]) xgll::store(dst + off[i], xgll::word(v[i], ep));
   }
-  if (!fail) xgll::wait_n<N>(result(me), off, other, ep, v, xg.ticks, fail);
+  if (!fail) xgll::finish_wait_n<N>(result(me), off, other, ep, w2, v, xg.ticks, fail);
 }
 
 // Small parameters of hidden tile jt (one product per wave), shared by mlp_wgrad_kernel and
@@ -908,9 +1007,13 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         g2[e] = sp == 0 ? gv[e] : gv[2 + e];
       }
       if (TRACE) trace_stamp(trw, 4);
-      if constexpr (TWO)
-        xg_exchange2<XW, 2>(xg, ep, offw, okw, g2, fail, lane, TRACE ? trw : nullptr, 2 * sp);
-      else
+      if constexpr (TWO) {
+        if (xg.split & 4)  // (DTFX_XG_SPLIT bit 2: the round-4 per-element owners, A/B runs)
+          xg_exchange2<XW, 2>(xg, ep, offw, okw, g2, fail, lane, TRACE ? trw : nullptr, 2 * sp);
+        else
+          xg_exchange2p<XW>(xg, ep, XG_W1_BASE + ((long long)(eslot * 2 + sp) * 64 + lane) * 2,
+                            g2, fail, lane, sp, TRACE ? trw : nullptr);
+      } else
         xg_exchange16<XW>(xg, ep, XG_W1_BASE + ((long long)(eslot * 2 + sp) * 64 + lane) * 2,
                           g2, fail);
       if (TRACE) trace_stamp(trw, 6);
@@ -1010,12 +1113,21 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
 // mlp_fwdapply_kernel structure with the W1 update formed from EVERY rank's factors:
 //   g = sum_q dz1A[q][jt]^T . x_q(t-1)   (K = XW * BP, the all-gathered factors of step
 //   t-1 and every rank's resident batch), W1new = W1old - lr * g,
-// then step t's forward on W1new.  1024-thread blocks: wave (c, s) owns column slice c
-// (16 of the tile's 56 features) and K split s of 4; the 4 partial slices are added in
-// split order through LDS (identical order on every rank: bit-identical replicas).
-// Small-parameter blocks exchange dW2/db1/db2 partials of step t-1 as in the 3-launch
-// factor engine (waves 0..3 of the block).  The head of step t all-gathers dz1 into dz1A
-// (mlp_head_kernel<.., XW, KS2>).
+// then step t's forward on W1new.  The single-GPU step's 28-feature K slices (196 W1
+// blocks): 512-thread blocks, wave (c, s) owns column group c (16 + 12 live features) and
+// K split s of 4; the 4 partial slices are added in split order through LDS (identical order
+// on every rank: bit-identical replicas).  At 8 ranks the global W1 gradient is 8 x the
+// 1-GPU step's MFMA work (K = 800), so it must be spread over the chip and issue all of its
+// loads in ONE round trip: a wave's K share (XW * 7 / 4 batch groups of 16 rows, 14 at 8
+// ranks) is requested at once (CH groups per round), and the seven hidden tiles of a K slice
+// -- which read the same x columns of every rank's batch, the one large fresh read -- run on
+// one XCD (block b on XCD b % 8; speed only), so each XCD's L2 fetches its slices' x once.
+// The first version (14 slices, 98 blocks, 4 load rounds, slices scattered over the XCDs)
+// cost 21.2 us per step at 8 ranks against 7.3 for the 1-GPU step (round-4 local cost).
+// Small-parameter blocks exchange dW2/db1/db2 partials of step t-1 as in the 3-launch factor
+// engine (waves 0..3 of the block).  The head of step t all-gathers dz1 into dz1A
+// (mlp_head_kernel<.., XW, KS3>).
+constexpr int FX_SLOTS = (KS3 + 7) / 8 * HT;  // block slots per XCD (4 slice rows x 7 tiles)
 template <int XW, int NGT>
 __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
     const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
@@ -1028,37 +1140,41 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
   const int bid = blockIdx.x;
-  if (bid >= HT * KS2) {
+  if (bid >= 8 * FX_SLOTS) {
+    const int jt = bid - 8 * FX_SLOTS;
     if (wave < 4)
-      wgrad_small<true, NGT, XW>(bid - HT * KS2, wave, lane,
-                                 MLP_XG_SMALL_EPOCH + (bid - HT * KS2) * 4 + wave, p_new, lr,
+      wgrad_small<true, NGT, XW>(jt, wave, lane, MLP_XG_SMALL_EPOCH + jt * 4 + wave, p_new, lr,
                                  nullptr, w, ctr, stats, stats_ring, B, xg, p_old, stats_on);
     return;
   }
-  constexpr int LW = KW2 + 4;
+  // block -> (hidden tile jt, K slice ks) with ks % 8 == the block's XCD
+  const int xcd = bid & 7, s8 = bid >> 3;
+  const int jt = s8 % HT, ks = (s8 / HT) * 8 + xcd;
+  if (ks >= KS3) return;  // (whole block: the slots past the 28 slices)
+  constexpr int KWX = D / KS3;  // 28 features
+  constexpr int LW = KWX + 4;
   __shared__ float Wt[16][LW];
-  __shared__ f32x4 red[4][64];
-  const int jt = bid / KS2, ks = bid % KS2;
-  const int f0 = ks * KW2;
+  __shared__ f32x4 red[2][3][64];
+  const int f0 = ks * KWX;
   const int me = xg.rank;
   // phase B's x rows (wave w < RT owns row tile w; B <= 128): requested first
-  float4 xa[4];
+  float4 xa[2];
   const int rowB = wave * 16 + r;
   const float rmB = rowB < B ? 1.f : 0.f;
   if (wave < RT) {
     const float* xr = x + (size_t)(rowB < B ? rowB : B - 1) * D + f0;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < 2; ++g) {
       const int k = 16 * g + 4 * q;
-      xa[g] = f4(xr + (k < KW2 ? k : 0));
+      xa[g] = f4(xr + (k < KWX ? k : 0));
     }
   }
-  // ---- phase A: slice c, K split s (2 splits) ------------------------------------------
-  const int c = wave & 3, sp = wave >> 2;
+  // ---- phase A: column group c, K split sp (4 splits) -----------------------------------
+  const int c = wave & 1, sp = wave >> 1;
   const int fl = c * 16 + r;
-  const bool cv = fl < KW2;
-  const int fc = f0 + (cv ? fl : KW2 - 1);
-  const int G = XW * NG, per = (G + 1) / 2;
+  const bool cv = fl < KWX;
+  const int fc = f0 + (cv ? fl : KWX - 1);
+  const int G = XW * NG, per = (G + 3) / 4;
   const int g0 = sp * per, g1 = min(G, g0 + per);
   float pw[4];
   if (sp == 0) {
@@ -1069,7 +1185,8 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
     }
   }
   f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-  constexpr int CH = 7;
+  // one round at 8 ranks x 7 groups (14 per split); more only for batches > 112 rows
+  constexpr int CH = (XW * (NGT > 0 ? NGT : 7) + 3) / 4;
   for (int c0 = g0; c0 < g1; c0 += CH) {
     float4 av[CH];
     float xv[CH][4];
@@ -1087,7 +1204,7 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
         }
       }
     }
-    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);  // the round's loads in flight together
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       if (c0 + i < g1) {
@@ -1101,12 +1218,15 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
   f32x4 part;
 #pragma unroll
   for (int i = 0; i < 4; ++i) part[i] = acc0[i] + acc1[i];
-  if (sp > 0) red[c][lane] = part;
+  if (sp > 0) red[c][sp - 1][lane] = part;
   __syncthreads();
   if (sp == 0) {
-    const f32x4 o = red[c][lane];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) part[i] += o[i];
+    for (int k = 0; k < 3; ++k) {  // split order: the same bits on every rank
+      const f32x4 o = red[c][k][lane];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[i] += o[i];
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int hl = q * 4 + i, j = jt * 16 + hl;
@@ -1118,17 +1238,18 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
     }
   }
   __syncthreads();
-  // ---- phase B: z1 partial of row tile `wave` over the block's 56 features ----------
+  // ---- phase B: z1 partial of row tile `wave` over the block's 28 features -------------
   if (wave >= RT) return;
-  float4 wb[4];
+  float4 wb[2];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
+  for (int g = 0; g < 2; ++g) {
     const int k = 16 * g + 4 * q;
-    wb[g] = k < KW2 ? *reinterpret_cast<const float4*>(&Wt[r][k]) : float4{0.f, 0.f, 0.f, 0.f};
+    wb[g] = k < KWX ? *reinterpret_cast<const float4*>(&Wt[r][k]) : float4{0.f, 0.f, 0.f, 0.f};
   }
   f32x4 o0 = {0, 0, 0, 0}, o1 = {0, 0, 0, 0};
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
+  for (int g = 0; g < 2; ++g) {
+    // (wb is zero for the dead part of the last group, so no mask is needed on xa there)
     o0 = mfma16x16x4(xa[g].x * rmB, wb[g].x, o0);
     o1 = mfma16x16x4(xa[g].y * rmB, wb[g].y, o1);
     o0 = mfma16x16x4(xa[g].z * rmB, wb[g].z, o0);
@@ -1426,7 +1547,7 @@ void mlp_head_xg_launch(const float* p, const int* labels, float* ws, float* dz1
                         hipStream_t stream, const MlpXg& xg, int world, int nslab) {
   using namespace mlp;
   check_b(B);
-  if (nslab != KS && nslab != KS2) throw std::runtime_error("mlp_head_xg: nslab must be 7 or 14");
+  if (nslab != KS && nslab != KS3) throw std::runtime_error("mlp_head_xg: nslab must be 7 or 28");
   if (xg.S < (long long)HP * (((B + 15) / 16) * 16))
     throw std::runtime_error("mlp_head_xg: exchange slots smaller than the factor plane");
   const Bufs w = make_bufs(ws, B);
@@ -1436,7 +1557,7 @@ void mlp_head_xg_launch(const float* p, const int* labels, float* ws, float* dz1
       hipLaunchKernelGGL((mlp_head_kernel<false, false, WW>), dim3(B), dim3(64), 0, stream, p, \
                          p, 0.f, nullptr, labels, w, B, nullptr, xg, dz1A);                    \
     else                                                                                       \
-      hipLaunchKernelGGL((mlp_head_kernel<false, false, WW, KS2>), dim3(B), dim3(64), 0, stream, \
+      hipLaunchKernelGGL((mlp_head_kernel<false, false, WW, KS3>), dim3(B), dim3(64), 0, stream, \
                          p, p, 0.f, nullptr, labels, w, B, nullptr, xg, dz1A);                 \
     break;
   switch (world) {
@@ -1564,10 +1685,10 @@ void mlp_fwdapply_xg_launch(const float* p_old, float* p_new, float lr, const fl
     throw std::runtime_error("mlp_fwdapply_xg: needs distinct ping-pong buffers, both batches, ctr");
   if (stats && stats_ring < 1) throw std::runtime_error("mlp_fwdapply_xg: stats_ring < 1");
   if (xg.S < NPARAM) throw std::runtime_error("mlp_fwdapply_xg: exchange slots smaller than the model");
-  if (!two_shot && (xg.split & 1) && xg.S < XG_SLOT_WORDS)
-    throw std::runtime_error("mlp_fwdapply_xg: the one-shot split exchange needs slots of "
-                             "mlp_step.XG_SLOT_WORDS words (create the communicator with that "
-                             "max_numel)");
+  if ((xg.split & 1) && !(two_shot && (xg.split & 4)) && xg.S < XG_SLOT_WORDS)
+    throw std::runtime_error("mlp_fwdapply_xg: the split exchange's 16-byte pair layout needs "
+                             "slots of mlp_step.XG_SLOT_WORDS words (create the communicator "
+                             "with that max_numel)");
   // 28 K slices (as the single-GPU step): 196 W1 blocks x 2 column groups of epoch slots
   static_assert(HT * KS3 * 2 <= MLP_XG_SMALL_EPOCH, "W1 epoch slots overlap the small ones");
   const Bufs w = make_bufs(ws, B);
@@ -1741,7 +1862,7 @@ void mlp_fwdapply_factor_launch(const float* p_old, float* p_new, float lr, cons
     throw std::runtime_error("mlp_fwdapply_factor: needs ping-pong buffers, batches, ctr, dz1A");
   if (xg.S < NPARAM) throw std::runtime_error("mlp_fwdapply_factor: exchange slots too small");
   const Bufs w = make_bufs(ws, B);
-  dim3 grid(HT * KS2 + HT), block(512);
+  dim3 grid(8 * FX_SLOTS + HT), block(512);
 #define DTFX_FF(WW, NGT)                                                                       \
   hipLaunchKernelGGL((mlp_fwdapply_factor_kernel<WW, NGT>), grid, block, 0, stream, p_old,     \
                      p_new, lr, x_prev, x, xstride, dz1A, w, ctr, stats, stats_ring, B,        \

@@ -13,8 +13,11 @@
 #include <pybind11/pybind11.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <memory>
+#include <thread>
 #include <stdexcept>
 #include <string>
 
@@ -55,60 +58,80 @@ class RcclComm {
     ncclUniqueId id;
     std::memcpy(&id, s.data(), sizeof(id));
     if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("rccl: hipSetDevice failed");
-    check(ncclCommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
+    ncclComm_t c = nullptr;
+    check(ncclCommInitRank(&c, nranks, id, rank), "ncclCommInitRank");
+    comm_.store(c, std::memory_order_release);
   }
   ~RcclComm() { destroy(); }
 
   void destroy() {
-    if (comm_) {
-      ncclCommDestroy(comm_);
-      comm_ = nullptr;
-    }
+    ncclComm_t c = comm_.exchange(nullptr);
+    if (c) ncclCommDestroy(c);
   }
   // Fail-fast teardown (parallel/watchdog.py): called from a watchdog thread while the
   // training thread may be blocked on a stream whose RCCL kernels wait for a dead peer.
   // ncclCommAbort makes those kernels return and frees the communicator; every later
-  // collective on this object raises.
+  // collective on this object raises.  The pointer is swapped out atomically (no new call
+  // can pick it up) and the abort waits, bounded, for calls already inside RCCL on another
+  // thread (`Use` guards) to leave, so it does not free a communicator under an enqueue.
   void abort() {
-    ncclComm_t c = comm_;
-    comm_ = nullptr;
-    if (c) ncclCommAbort(c);
+    ncclComm_t c = comm_.exchange(nullptr);
+    if (!c) return;
+    const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(2);
+    while (inflight_.load(std::memory_order_acquire) > 0 && std::chrono::steady_clock::now() < until)
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    ncclCommAbort(c);
   }
   // ncclSuccess (0) while healthy; an RCCL error code once a remote failure / abort was seen.
-  int async_error() const {
-    if (!comm_) return static_cast<int>(ncclInvalidUsage);
+  int async_error() {
+    Use u(this);
+    if (!u.c) return static_cast<int>(ncclInvalidUsage);
     ncclResult_t r = ncclSuccess;
-    if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return static_cast<int>(ncclInternalError);
+    if (ncclCommGetAsyncError(u.c, &r) != ncclSuccess) return static_cast<int>(ncclInternalError);
     return static_cast<int>(r);
   }
-  ncclComm_t get() const {
-    if (!comm_) throw std::runtime_error("rccl: communicator destroyed");
-    return comm_;
-  }
+  // A call's hold on the communicator: counted in inflight_ for abort() to wait on.
+  struct Use {
+    RcclComm* o;
+    ncclComm_t c;
+    explicit Use(RcclComm* o_) : o(o_) {
+      o->inflight_.fetch_add(1, std::memory_order_acq_rel);
+      c = o->comm_.load(std::memory_order_acquire);
+    }
+    ~Use() { o->inflight_.fetch_sub(1, std::memory_order_acq_rel); }
+    ncclComm_t get() const {
+      if (!c) throw std::runtime_error("rccl: communicator destroyed");
+      return c;
+    }
+  };
 
   void all_reduce(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt,
                   const std::string& op, uintptr_t stream) {
+    Use u(this);
     check(ncclAllReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
-                        dtype_of(dt), op_of(op), get(), reinterpret_cast<hipStream_t>(stream)),
+                        dtype_of(dt), op_of(op), u.get(), reinterpret_cast<hipStream_t>(stream)),
           "ncclAllReduce");
   }
   void reduce_scatter(uintptr_t send, uintptr_t recv, size_t recv_count, const std::string& dt,
                       const std::string& op, uintptr_t stream) {
+    Use u(this);
     check(ncclReduceScatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv),
-                            recv_count, dtype_of(dt), op_of(op), get(),
+                            recv_count, dtype_of(dt), op_of(op), u.get(),
                             reinterpret_cast<hipStream_t>(stream)),
           "ncclReduceScatter");
   }
   void all_gather(uintptr_t send, uintptr_t recv, size_t send_count, const std::string& dt,
                   uintptr_t stream) {
+    Use u(this);
     check(ncclAllGather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv),
-                        send_count, dtype_of(dt), get(), reinterpret_cast<hipStream_t>(stream)),
+                        send_count, dtype_of(dt), u.get(), reinterpret_cast<hipStream_t>(stream)),
           "ncclAllGather");
   }
   void broadcast(uintptr_t send, uintptr_t recv, size_t count, const std::string& dt, int root,
                  uintptr_t stream) {
+    Use u(this);
     check(ncclBroadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
-                        dtype_of(dt), root, get(), reinterpret_cast<hipStream_t>(stream)),
+                        dtype_of(dt), root, u.get(), reinterpret_cast<hipStream_t>(stream)),
           "ncclBroadcast");
   }
   void all_to_all(uintptr_t send, uintptr_t recv, size_t count_per_rank, const std::string& dt,
@@ -116,7 +139,8 @@ class RcclComm {
     // grouped send/recv: rank r's slice i goes to rank i
     const ncclDataType_t t = dtype_of(dt);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    ncclComm_t c = get();
+    Use u(this);
+    ncclComm_t c = u.get();
     check(ncclGroupStart(), "ncclGroupStart");
     // the group is ALWAYS closed: an error inside it is recorded and raised after
     // ncclGroupEnd, so the next collective is never merged into an unfinished group
@@ -145,7 +169,8 @@ class RcclComm {
   int rank() const { return rank_; }
 
  private:
-  ncclComm_t comm_ = nullptr;
+  std::atomic<ncclComm_t> comm_{nullptr};
+  std::atomic<int> inflight_{0};
   int nranks_, rank_;
 };
 

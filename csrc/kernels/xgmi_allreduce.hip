@@ -235,9 +235,13 @@ __global__ __launch_bounds__(512) void xgmi_bw_kernel(float* __restrict__ g, lon
   const int b = blockIdx.x, t = threadIdx.x, nt = blockDim.x, nb = gridDim.x;
   if (t == 0) {
     s_epoch = epochs[b] + 1;
-    s_fail = 0;
+    // a communicator that already timed out (a peer is gone) is broken for good: calls queued
+    // behind the timed-out one leave at once instead of each waiting `ticks` again, so the
+    // stream drains within one timeout (the peer watchdog's drain window, parallel/watchdog.py)
+    s_fail = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  if (s_fail) return;
   const unsigned epoch = s_epoch;
   const long long par = epoch & 1u;
   const long long CS = xg_bw_cs(S, W);             // slot capacity of one chunk

@@ -228,7 +228,7 @@ class XgmiAllReduce {
                                    (float*)ws, (int*)ctr, (float*)stats, ring, B, pending, s, xg,
                                    world_);
         mlp_head_xg_launch(pn, lab + (size_t)pos * B, (float*)ws, (float*)dz1A, B, s, xg,
-                           world_, 14);
+                           world_, 28);
       } else {
         mlp_fwdapply_xg_launch(po, pn, l, xprev, xcur, (float*)ws, (int*)ctr, (float*)stats,
                                ring, B, pending, s, xg, world_, kind);

@@ -88,6 +88,81 @@ __device__ __forceinline__ void gather_all(Base base, long long i, int rank, uns
 // issued before the first wait, so the N round trips overlap instead of serialising (the MLP
 // exchange epilogues hold 4 elements per lane).  v[n] holds the own value on entry and the
 // rank-ordered sum on return for act[n]; inactive elements are left as they are.
+//
+// Split form (first_loads + finish_sum_n): the exchanges issue their first polls BEFORE their
+// own pushes.  CDNA counts a wave's stores and loads in ONE in-order vmcnt, so a load issued
+// after a store cannot be consumed until that store is acknowledged -- for a push into a
+// peer's memory a full round trip, paid on top of the peer data's own one-way arrival.
+template <int W, int N, class Base>
+__device__ __forceinline__ void first_loads(Base base, const size_t (&off)[N], const bool (&act)[N],
+                                            int rank, unsigned epoch, u64 (&w)[N][W]) {
+  const u64 done = (u64)epoch << 32;
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int j = 0; j < W; ++j) w[n][j] = (act[n] && j != rank) ? load(base(j) + off[n]) : done;
+}
+template <int W, int N, class Base>
+__device__ __forceinline__ void finish_sum_n(Base base, const size_t (&off)[N],
+                                             const bool (&act)[N], int rank, unsigned epoch,
+                                             u64 (&w)[N][W], float (&v)[N], long long ticks,
+                                             bool& fail) {
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ready = true;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+        if ((unsigned)(w[n][j] >> 32) != epoch) {
+          ready = false;
+          w[n][j] = load(base(j) + off[n]);
+        }
+    if (ready) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      fail = true;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    if (!act[n]) continue;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc += j == rank ? v[n] : __uint_as_float((unsigned)w[n][j]);
+    v[n] = acc;
+  }
+}
+// All-gather counterpart of finish_sum_n: out[n][j] = peer j's value (out[n][rank] = own[n]).
+template <int W, int N, class Base>
+__device__ __forceinline__ void finish_all_n(Base base, const size_t (&off)[N],
+                                             const bool (&act)[N], int rank, unsigned epoch,
+                                             u64 (&w)[N][W], const float (&own)[N],
+                                             float (&out)[N][W], long long ticks, bool& fail) {
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ready = true;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+        if ((unsigned)(w[n][j] >> 32) != epoch) {
+          ready = false;
+          w[n][j] = load(base(j) + off[n]);
+        }
+    if (ready) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      fail = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int j = 0; j < W; ++j) out[n][j] = j == rank ? own[n] : __uint_as_float((unsigned)w[n][j]);
+}
 template <int W, int N, class Base>
 __device__ __forceinline__ void gather_sum_n(Base base, const size_t (&off)[N], const bool (&act)[N],
                                              int rank, unsigned epoch, float (&v)[N],
@@ -124,6 +199,39 @@ __device__ __forceinline__ void gather_sum_n(Base base, const size_t (&off)[N], 
     for (int j = 0; j < W; ++j) acc += j == rank ? v[n] : __uint_as_float((unsigned)w[n][j]);
     v[n] = acc;
   }
+}
+
+// wait_n in split form (first polls issued before the caller's pushes, see first_loads).
+template <int N>
+__device__ __forceinline__ void first_loads1(const u64* p, const size_t (&off)[N], const bool (&act)[N],
+                                             unsigned epoch, u64 (&w)[N]) {
+  const u64 done = (u64)epoch << 32;
+#pragma unroll
+  for (int n = 0; n < N; ++n) w[n] = act[n] ? load(p + off[n]) : done;
+}
+template <int N>
+__device__ __forceinline__ void finish_wait_n(const u64* p, const size_t (&off)[N],
+                                              const bool (&act)[N], unsigned epoch, u64 (&w)[N],
+                                              float (&v)[N], long long ticks, bool& fail) {
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ready = true;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+      if ((unsigned)(w[n] >> 32) != epoch) {
+        ready = false;
+        w[n] = load(p + off[n]);
+      }
+    if (ready) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      fail = true;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+    if (act[n]) v[n] = __uint_as_float((unsigned)w[n]);
 }
 
 // wait_one over N words at once (first loads issued together); v[n] = the word's value.

@@ -220,6 +220,7 @@ class BertMLM:
         self.wgrad_stream = None
         self.wgrad_sync_buckets = True
         self._parts = {}     # weight name -> split-K partial planes (enable_splitk_fold)
+        self._fold_tokens = None  # the weight gradients' K those planes were sized for
         self._segs = None    # their AdamW segment table
 
     # ------------------------------------------------------------------ forward
@@ -254,6 +255,10 @@ class BertMLM:
         if seq > cfg.max_pos:
             raise ValueError("sequence length %d exceeds max_pos %d" % (seq, cfg.max_pos))
         Tn = batch * seq
+        if self._parts and Tn != self._fold_tokens:
+            raise ValueError("forward_backward: split-K fold was enabled for %d tokens, this "
+                             "batch has %d (call enable_splitk_fold again or disable it)"
+                             % (self._fold_tokens, Tn))
         p.zero_grad()
         ids_f, tt_f = ids.reshape(-1), tt.reshape(-1)
         x0, h, me, re = TR.embed_ln_fwd(ids_f, tt_f, p.W("embeddings/word_embeddings"),
@@ -387,6 +392,8 @@ class BertMLM:
         if not self.device.type == "cuda":
             return 0
         p, rows = self.params, []
+        self._parts = {}
+        self._fold_tokens = int(tokens)
         for l in range(self.cfg.layers):
             for w in self.ENCODER_WEIGHTS:
                 name = "encoder/layer_%d/%s" % (l, w)

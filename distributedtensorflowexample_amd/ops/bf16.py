@@ -55,9 +55,10 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
     gradients: few output tiles, deep K), combining with f32 atomics.
     ``colsum`` (f32 [N]) accumulates the column sums of the final values
     (a fused bias gradient of the produced activation gradient).
-    ``partials`` (f32, >= ``splitk_planes(..) * M * N`` elements): a split-K GEMM leaves its
-    S partial planes there and does NOT write ``out`` (no reduce pass): the caller sums them
-    (``transformer.adam_mixed(.., segs=..)``).  Unsplit GEMMs write ``out`` as usual.
+    ``partials`` (f32, exactly ``splitk_planes(..) * M * N`` elements): the split-K GEMM leaves
+    its S partial planes there and does NOT write ``out`` (no reduce pass): the caller sums them
+    (``transformer.adam_mixed(.., segs=..)``).  A GEMM whose split differs from the buffer's
+    plane count (or that does not split) raises instead of leaving stale planes.
     """
     act_i = ACT[act]
     ag_i = ACT[act_grad]
@@ -144,12 +145,16 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
     if partials is not None:
         nws = hip().gemm_bf16_ws_floats(bool(trans_a), out.dtype == torch.float32, M, N, K,
                                         int(splitk), float(beta)) if plain else 0
-        if nws:
-            if not (partials.is_cuda and partials.dtype == torch.float32
-                    and partials.is_contiguous() and partials.numel() >= nws):
-                raise ValueError("gemm_bf16: partials must be a contiguous f32 GPU buffer of "
-                                 ">= %d elements" % nws)
-            ws, nws, defer = partials, partials.numel(), True
+        # the caller sums exactly partials.numel() // (M*N) planes: a GEMM that does not
+        # split (nws == 0) or splits into another plane count would leave stale planes there
+        if nws != partials.numel():
+            raise ValueError("gemm_bf16: this (%d, %d, K=%d) GEMM leaves %d split-K partial "
+                             "floats but partials holds %d (split-K fold set up for another "
+                             "shape?)" % (M, N, K, nws, partials.numel()))
+        if not (partials.is_cuda and partials.dtype == torch.float32
+                and partials.is_contiguous()):
+            raise ValueError("gemm_bf16: partials must be a contiguous f32 GPU buffer")
+        ws, defer = partials, True
     elif out.dtype == torch.float32 and plain and _SPLITK_WS:
         # split-K partials go to a workspace and one reduce pass (plain stores instead of f32
         # atomics, which run at the memory side at ~1.3 TB/s chip-wide)

@@ -41,6 +41,15 @@ XG_SLABS = 28
 # xg_exchange16): a communicator for fused2 needs slots of XG_SLOT_WORDS words
 XG_W1_BASE = 79616
 XG_SLOT_WORDS = XG_W1_BASE + 7 * 28 * 2 * 2 * 64 * 2
+# z1 slabs of the factor engines' first launch (mlp_fwdapply_factor_kernel's K slicing)
+FACTOR_SLABS = 28
+
+
+def engine_slot_words(kind):
+    """Words per slot of a data-parallel engine's communicator: the pipelined fused engines'
+    W1 exchange (one-shot fused2, two-shot fused2x) moves 16-byte word pairs in a layout past
+    the parameter-offset region (XG_SLOT_WORDS); the others exchange at parameter offsets."""
+    return XG_SLOT_WORDS if kind in ("fused2", "fused2x") else NPARAM
 
 
 def xg_w1_pair_offsets():
@@ -222,7 +231,7 @@ def step_factor_pipelined(p_old, p_new, x_prev, x, labels, ws: StepWorkspace, lr
     if dz1A.numel() < comm.world_size * factor_plane(ws.B):
         raise ValueError("dz1A must hold world * 112 * BP f32 values")
     comm.mlp_fwdapply_factor(p_old, p_new, lr, x_prev, x, xstride, dz1A, ws, apply, stats)
-    comm.mlp_head(p_new, labels, ws, dz1A, nslab=14)
+    comm.mlp_head(p_new, labels, ws, dz1A, nslab=FACTOR_SLABS)
 
 
 def flush_factor(p, x_prev, ws: StepWorkspace, lr, comm, dz1A, xstride, stats=True):

@@ -180,7 +180,7 @@ def pick_mlp_engine(params, x, y, batch_size, lr, ar_comm, world, rank, dev, mod
     for kind in kinds:
         c, err = None, ""
         try:
-            c = XgmiComm(rank, world, max(mlp_step.NPARAM, mlp_step.XG_SLOT_WORDS), device=dev,
+            c = XgmiComm(rank, world, mlp_step.engine_slot_words(kind), device=dev,
                          key="%s/%s" % (xgmi_key, kind),
                          protocol="push", timeout_s=timeout_s)
         except Exception as e:
@@ -333,7 +333,7 @@ class HybridComm:
 
 def pick_large_allreduce(rccl, world, rank, dev, max_numel, sizes=None, iters=10,
                          xgmi_key="dtfx/xgmi/bw", timeout_s=2.0, bw_blocks=None,
-                         train_timeout_s=120.0):
+                         train_timeout_s=None, peer_timeout_s=60.0):
     """Bucketed all-reduce backend for the large gradients (BERT / ResNet buckets): the xGMI
     bandwidth-mode two-shot is created on every rank (or not at all), verified against RCCL
     on random buckets, and timed against RCCL inside captured hipGraphs at each size in
@@ -345,7 +345,16 @@ def pick_large_allreduce(rccl, world, rank, dev, max_numel, sizes=None, iters=10
     waits up to ``train_timeout_s`` (a rank that is away for seconds -- the chief writing a
     checkpoint, first-step graph capture -- must not time its peers out: a timed-out
     two-shot leaves the bucket partly reduced, where RCCL would simply have blocked).
-    Trainers still poll ``failed()`` collectively (``check_comm_collective``)."""
+    Trainers still poll ``failed()`` collectively (``check_comm_collective``).
+
+    Default ``train_timeout_s``: ``min(120, peer_timeout_s)``.  The peer watchdog
+    (``--peer_timeout_secs``) declares a silent peer lost after ``peer_timeout_s``, drains for
+    10 s and ends the process; a two-shot waiting on that peer must have left the GPU by then,
+    and once one call timed out the calls queued behind it exit at entry (the kernel reads
+    the communicator's error word first), so the stream drains within one timeout."""
+    if train_timeout_s is None:
+        train_timeout_s = min(120.0, float(peer_timeout_s)) if peer_timeout_s and peer_timeout_s > 0 \
+            else 120.0
     max_numel = int(max_numel)
     sizes = [s for s in (sizes or (1 << 18, 1 << 20, 1 << 22, 7 << 20, 1 << 24))
              if s <= max_numel] or [max_numel]

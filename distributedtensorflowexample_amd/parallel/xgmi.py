@@ -116,7 +116,7 @@ class XgmiComm:
     def mlp_head(self, p, labels, ws, dz1A, nslab=7):
         """Factor engine: MLP head launch that also all-gathers every rank's backprop factors
         dz1 into ``dz1A`` [world, 112, BP] (protocol "push"); see ``ops.mlp_step.step_factor``.
-        ``nslab``: partial-z1 planes left by the forward (7: 3-launch, 14: pipelined)."""
+        ``nslab``: partial-z1 planes left by the forward (7: 3-launch, 28: pipelined)."""
         from ..ops._ext import ptr
 
         self._h.mlp_head(ptr(p), ptr(labels), ptr(ws.buf), ptr(dz1A), ws.B,
@@ -186,3 +186,56 @@ class XgmiComm:
 
     def destroy(self):
         self._h.close()
+
+
+class SimulatedPeersComm:
+    """Rank 0 of a ``world_size``-rank data-parallel job on ONE GPU, for timing the DP shape of
+    a training step: every all-reduce runs the real bandwidth-mode
+    two-shot kernel (``xgmi_bw_kernel<W>``, protocol "bw") of rank 0 over simulated local
+    peers -- its reduce-scatter stores into the W-1 "peer" receive slots, the owner sum over
+    W contributions and the all-gather copies, all in this GPU's HBM, every peer flag
+    pre-raised (``XgmiComm.with_local_peers``).  So a trainer driven with it runs its world > 1
+    path exactly (comm stream, bucket hooks, no split-K fold, side-stream defaults, 1/W
+    scaling) and its comm kernels compete with the backward for CUs and HBM as on a node --
+    minus the link time, which this cannot show.  The peers' slots hold zeros, so the
+    "global" gradient is this rank's own (the numerics stay those of one rank).
+
+    Buckets above ``max_numel`` elements are reduced in ``max_numel`` pieces."""
+
+    def __init__(self, world_size, max_numel, device=None, bw_blocks=None, timeout_s=5.0):
+        self.rank, self.world_size = 0, int(world_size)
+        self.comm, regs = XgmiComm.with_local_peers(0, self.world_size, int(max_numel),
+                                                    device=device, protocol="bw",
+                                                    timeout_s=timeout_s, bw_blocks=bw_blocks)
+        self.device = self.comm.device
+        self.max_numel = int(max_numel)
+        W, S = self.world_size, self.comm.slot_stride
+        CS = ((S + W - 1) // W + 3) // 4 * 4
+        f0 = 2 * W * CS + 2 * S  # the flag array, past the data slots (xgmi_ll_bytes, XG_BW)
+        for r in regs:  # every flag any call could wait for: already raised (epoch 0x7fffffff)
+            r.view(torch.int32)[f0:f0 + 2 * W * 256] = 0x7FFFFFFF
+        self.regions = regs
+
+    def allreduce_sum_(self, t):
+        flat = t.view(-1)
+        for lo in range(0, flat.numel(), self.max_numel):
+            self.comm.allreduce_sum_(flat[lo:lo + self.max_numel])
+        return t
+
+    def allreduce_avg_(self, t):
+        return self.allreduce_sum_(t).div_(self.world_size)
+
+    def broadcast_(self, t, root=0):
+        return t  # rank 0 is the root: its values are the broadcast values
+
+    def barrier(self):
+        torch.cuda.synchronize(self.device)
+
+    def failed(self):
+        return self.comm.failed()
+
+    def check(self):
+        self.comm.check()
+
+    def destroy(self):
+        self.comm.destroy()

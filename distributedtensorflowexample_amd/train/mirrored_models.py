@@ -50,8 +50,9 @@ def train_model_mirrored(flags, log=print):
             # size where it measured faster (the same decision on every rank)
             from ..parallel.select import pick_large_allreduce
 
-            comm, _ = pick_large_allreduce(comm, world, rank, dev,
-                                           (24 << 20) if flags.model == "bert" else (8 << 20))
+            comm, _ = pick_large_allreduce(
+                comm, world, rank, dev, (24 << 20) if flags.model == "bert" else (8 << 20),
+                peer_timeout_s=float(getattr(flags, "peer_timeout_secs", 60.0) or 0.0))
     else:
         dev = torch.device("cpu")
         comm = TorchComm() if world > 1 else None

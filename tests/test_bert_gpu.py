@@ -134,6 +134,7 @@ def test_bert_splitk_fold_matches_reduce_path(gpu, monkeypatch):
     cfg = BertConfig.tiny()
     monkeypatch.setenv("DTFX_BERT_FOLD", "0")
     a = BertTrainer(cfg, 32, 128, gpu, lr=1e-3)
+    a.init_master = a.model.params.master.clone()
     monkeypatch.setenv("DTFX_BERT_FOLD", "1")
     b = BertTrainer(cfg, 32, 128, gpu, lr=1e-3)
     assert a.model._segs is None and b.model._segs is not None
@@ -142,7 +143,11 @@ def test_bert_splitk_fold_matches_reduce_path(gpu, monkeypatch):
     b.run(3, use_graph=True)
     d = (a.model.params.master - b.model.params.master).abs()
     assert (d <= 2e-5).float().mean() > 0.99
-    assert d.max() <= 3 * 1e-3 * 1.01
+    # (an elementwise max bound is vacuous here: 3 AdamW steps at lr 1e-3 move a parameter at
+    # most ~3e-3, and a near-zero gradient's sign may legitimately differ between the two
+    # summation orders) -- the moved parameters as a whole must agree to f32-rounding level
+    moved = (a.model.params.master - a.init_master).abs()
+    assert d.sum() <= 1e-3 * moved.sum()
     la, _ = a.stats()
     lb, _ = b.stats()
     assert abs(la - lb) < 1e-3 * abs(la)
@@ -156,6 +161,29 @@ def test_bert_splitk_fold_matches_reduce_path(gpu, monkeypatch):
         assert cos > 0.999, (name, cos.item())
 
 
+def test_bert_splitk_fold_rejects_other_token_count(gpu, monkeypatch):
+    """The fold's planes are sized for one token count: a step with another batch x seq (whose
+    weight-gradient GEMMs would split differently, or not at all) must raise, not let AdamW
+    sum stale planes."""
+    from distributedtensorflowexample_amd.models.bert import synthetic_mlm_batch
+    from distributedtensorflowexample_amd.ops import bf16 as B16
+
+    cfg = BertConfig.tiny()
+    m = BertMLM(cfg, gpu)
+    assert m.enable_splitk_fold(32 * 128) > 0
+    ids, tt, pos, lab, nv = synthetic_mlm_batch(cfg, 8, 128, gpu)
+    with pytest.raises(ValueError, match="split-K fold"):
+        m.forward_backward(ids, tt, pos, lab, n_valid=nv)
+    # the GEMM-level guard: a partials buffer sized for another plane count
+    name = next(iter(m._parts))
+    W = m.params.G(name)
+    M, N = W.shape
+    dy = torch.randn(8 * 128, M, device=gpu).to(torch.bfloat16)
+    x = torch.randn(8 * 128, N, device=gpu).to(torch.bfloat16)
+    with pytest.raises(ValueError, match="partial"):
+        B16.gemm(dy, x, True, False, out=W, beta=0.0, partials=m._parts[name])
+
+
 def test_bert_overlapped_adam_matches_one_launch(gpu, monkeypatch):
     """One GPU: each bucket's AdamW on a third stream as soon as the bucket is final (overlapping
     the rest of the backward) gives the one-launch-after-backward result."""
@@ -164,6 +192,7 @@ def test_bert_overlapped_adam_matches_one_launch(gpu, monkeypatch):
     cfg = BertConfig.tiny()
     monkeypatch.delenv("DTFX_BERT_OPT_OVERLAP", raising=False)
     a = BertTrainer(cfg, 32, 128, gpu, lr=1e-3)  # default: AdamW after the backward
+    a.init_master = a.model.params.master.clone()
     monkeypatch.setenv("DTFX_BERT_OPT_OVERLAP", "1")
     b = BertTrainer(cfg, 32, 128, gpu, lr=1e-3)
     assert a.opt_stream is None and b.opt_stream is not None
@@ -171,7 +200,11 @@ def test_bert_overlapped_adam_matches_one_launch(gpu, monkeypatch):
     b.run(3, use_graph=True)
     d = (a.model.params.master - b.model.params.master).abs()
     assert (d <= 2e-5).float().mean() > 0.99
-    assert d.max() <= 3 * 1e-3 * 1.01
+    # (an elementwise max bound is vacuous here: 3 AdamW steps at lr 1e-3 move a parameter at
+    # most ~3e-3, and a near-zero gradient's sign may legitimately differ between the two
+    # summation orders) -- the moved parameters as a whole must agree to f32-rounding level
+    moved = (a.model.params.master - a.init_master).abs()
+    assert d.sum() <= 1e-3 * moved.sum()
     assert int(a.step_t.item()) == int(b.step_t.item()) == 4
     la, _ = a.stats()
     lb, _ = b.stats()

@@ -346,7 +346,7 @@ def test_fused2_fwdapply_exchange_simulated_peers(gpu, world, rank, B):
     comm.destroy()
 
 
-@pytest.mark.parametrize("nslab", [7, 14])
+@pytest.mark.parametrize("nslab", [7, 28])
 @pytest.mark.parametrize("world,rank,B", _engine_cases())
 def test_factor_head_allgather_simulated_peers(gpu, world, rank, B, nslab):
     """mlp_head_kernel<.., XW, NSLAB>: all-gather of the backprop factors dz1 into dz1A."""
@@ -378,7 +378,7 @@ def test_factor_head_allgather_simulated_peers(gpu, world, rank, B, nslab):
         if nslab == 7:
             hip().mlp_fwd(ptr(p), 0, 0.0, 0, ptr(x), ptr(ws.buf), ws.B, stream_handle())
         else:
-            tmp = p.clone()  # (a first launch with the factor engines' 14-slice layout)
+            tmp = p.clone()  # (a first launch with the factor engines' 28-slice layout)
             hip().mlp_fwdapply(ptr(p), ptr(tmp), 0.0, ptr(x), ptr(x), ptr(ws.buf), ptr(ws.ctr),
                                0, ws.stats_ring, ws.B, 0, stream_handle(), ks=nslab)
         comm.mlp_head(p, y, ws, dz1A, nslab=nslab)
@@ -480,7 +480,7 @@ def test_factor2_fwdapply_simulated_peers(gpu, world, rank, B):
     _stage_param_words(comm, regs, peers, 1, lo, mlp_step.NPARAM)
     torch.cuda.synchronize()
     comm.mlp_fwdapply_factor(p_old, p_new, lr, x_prev, x, x_all.stride(0), dz1A, ws, True)
-    hip().mlp_head2(ptr(p_new), ptr(y), ptr(ws.buf), ws.B, stream_handle(), 14)
+    hip().mlp_head2(ptr(p_new), ptr(y), ptr(ws.buf), ws.B, stream_handle(), mlp_step.FACTOR_SLABS)
     comm.check()
     upd = _expected_update(own, peers, rank)
     upd[:lo] = gW1
@@ -591,19 +591,22 @@ def test_bw_allreduce_simulated_peers(gpu, world):
             _bw_check(world, rank, n, cap, gpu)
 
 
-def _w1_owner(off, world):
-    """Owner rank of W1 element ``off`` in the two-shot exchange of mlp_fwdapply_kernel<.., XW,
-    .., TWO> (lane (q, r) of a phase-A wave holds hidden j = jt*16 + 4q + i, feature
-    ks*56 + 16w + r; owner = (q + 4 i) % XW)."""
-    hl = (off // 784) % 16
-    return (hl // 4 + 4 * (hl % 4)) % world
+def _pair_owner(words, world):
+    """Owner rank of a word of the 16-byte pair layout in the pair two-shot exchange
+    (xg_exchange2p): pair (eslot, sp, lane) is owned by (lane // 16 + 4 sp) % world."""
+    from distributedtensorflowexample_amd.ops import mlp_step
+
+    pi = (words - mlp_step.XG_W1_BASE) // 2
+    lane, sp = pi % 64, (pi // 64) % 2
+    return (lane // 16 + 4 * sp) % world
 
 
-@pytest.mark.parametrize("world,rank", [(3, 2), (4, 1), (5, 0), (8, 7), (8, 3)])
+@pytest.mark.parametrize("world,rank", [(2, 1), (3, 2), (4, 1), (5, 0), (6, 4), (7, 6), (8, 7),
+                                        (8, 3)])
 def test_fused2_two_shot_exchange_simulated_peers(gpu, world, rank):
     """mlp_fwdapply_kernel<7, XW, false, true>: the W1 tiles' exchange as reduce-scatter +
-    all-gather (owned elements: gather + rank-ordered sum + broadcast; the others: push to the
-    owner, then take its sum); small parameters one-shot."""
+    all-gather of 16-byte word pairs (xg_exchange2p; owned pairs: gather + rank-ordered sum +
+    broadcast; the others: push to the owner, then take its sums); small parameters one-shot."""
     from distributedtensorflowexample_amd.data.synthetic import mnist_like_device
     from distributedtensorflowexample_amd.ops import mlp_step
     from distributedtensorflowexample_amd.ops._ext import hip, ptr, stream_handle
@@ -612,12 +615,17 @@ def test_fused2_two_shot_exchange_simulated_peers(gpu, world, rank):
     B = 100
     p_old, x_prev, y_prev, ws = _setup(gpu, B, 60 * world + rank)
     x, y = mnist_like_device(B, seed=777 + rank, device=gpu)
-    comm, regs = XgmiComm.with_local_peers(rank, world, mlp_step.NPARAM, device=gpu)
+    comm, regs = XgmiComm.with_local_peers(rank, world, mlp_step.engine_slot_words("fused2x"),
+                                           device=gpu)
     comm.two_shot = True
     S = comm.slot_stride
     n1 = mlp_step.OFF_B1
-    owner = torch.tensor([_w1_owner(o, world) for o in range(n1)])
+    w1map = mlp_step.xg_w1_pair_offsets()
+    owner = _pair_owner(w1map, world)
     mine = owner == rank
+    reg = torch.arange(mlp_step.XG_W1_BASE, mlp_step.XG_SLOT_WORDS)
+    reg_mine = _pair_owner(reg, world) == rank
+    w1g, mg = w1map.to(gpu), mine.to(gpu)
     lr = 0.5
     bufs = [p_old, torch.empty_like(p_old)]
     batches = [(x_prev, y_prev), (x, y)]
@@ -633,18 +641,17 @@ def test_fused2_two_shot_exchange_simulated_peers(gpu, world, rank):
         peers = _peer_grads(world, rank, 23 * epoch + world, 0.05)
         # small parameters: one-shot slots, every peer
         _stage_param_words(comm, regs, peers, epoch, n1, mlp_step.NPARAM)
-        # W1, owned: the peers' contributions; not owned: the owner's (arbitrary) sum
+        # W1, owned pairs: the peers' contributions (padding words: zeros of this epoch);
+        # not owned: the owner's (arbitrary) sums in my result region
         for q in range(world):
             if q != rank:
                 o = (par * world + q) * S
-                w = _words(peers[q][:n1].to(gpu), epoch)
-                sl = regs[rank][o:o + n1]
-                sl[mine.to(gpu)] = w[mine.to(gpu)]
+                regs[rank][o + reg] = _words(torch.zeros(reg.numel(), device=gpu), epoch)
+                regs[rank][o + w1g[mg]] = _words(peers[q][:n1].to(gpu)[mg], epoch)
         owners_sum = torch.randn(n1, generator=g) * 0.07
         res = (2 * world + par) * S
-        rw = _words(owners_sum.to(gpu), epoch)
-        sl = regs[rank][res:res + n1]
-        sl[(~mine).to(gpu)] = rw[(~mine).to(gpu)]
+        regs[rank][res + reg] = _words(torch.zeros(reg.numel(), device=gpu), epoch)
+        regs[rank][res + w1g[~mg]] = _words(owners_sum.to(gpu)[~mg], epoch)
         tot = _expected_update(own, peers, rank)
         exp = po.double().cpu() - lr * tot
         exp[:n1][~mine] = po.double().cpu()[:n1][~mine] - lr * owners_sum.double()[~mine]
@@ -654,20 +661,23 @@ def test_fused2_two_shot_exchange_simulated_peers(gpu, world, rank):
         comm.check()
         err = float((pn.double().cpu() - exp).abs().max())
         assert err <= 2e-5, (epoch, err)
-        # pushes: my share of every non-owned element went to its owner only; my sums of the
-        # owned ones to every peer's result region
+        # pushes: my pairs went to their owner only; my sums of the owned pairs to every
+        # peer's result region
         for d in range(world):
             if d == rank:
                 continue
             o = (par * world + rank) * S
-            wv = regs[d][o:o + n1].cpu()
             to_d = owner == d
+            wv = regs[d][o + w1g].cpu()
             assert bool((_epochs(wv[to_d]) == epoch).all()), ("contribution epoch", d)
             assert float((_vals(wv[to_d]).double() - own[:n1][to_d]).abs().max()) <= 2e-6
-            rv = regs[d][res:res + n1].cpu()
+            rv = regs[d][res + w1g].cpu()
             assert bool((_epochs(rv[mine]) == epoch).all()), ("result epoch", d)
             got = _vals(rv[mine]).double()
             assert float((got - tot[:n1][mine]).abs().max()) <= 2e-5
+            # padding words of my owned pairs were broadcast too (every owner lane pushes)
+            rr = regs[d][res + reg].cpu()
+            assert bool((_epochs(rr[reg_mine]) == epoch).all()), ("result padding", d)
         _check_pushed(comm, regs, own, epoch, n1, mlp_step.NPARAM, 2e-6)
         cur ^= 1
     comm.destroy()

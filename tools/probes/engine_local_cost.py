@@ -68,66 +68,72 @@ def main():
         h.mlp_head2(ptr(p[1]), ptr(yc), ptr(ws.buf), B, stream_handle())
 
     out["single_gpu_2launch_us"] = round(graph_us(single, dev), 2)
+    engines = [e for e in os.environ.get("ENGINES", "fused2,fused2x,factor2,fused,factor").split(",") if e]
     for W in (2, 4, 8):
         r = W - 1
-        comm, regs = XgmiComm.with_local_peers(r, W, mlp_step.XG_SLOT_WORDS, device=dev,
-                                               protocol="push", timeout_s=1.0)
-        S = comm.slot_stride
-        word = (1 << 32) | int(torch.tensor([1e-3]).view(torch.int32).item())
-        for q in range(W):
-            if q != r:
-                o = (1 * W + q) * S  # parity 1 = epoch 1
-                regs[r][o:o + S] = word
-        regs[r][(2 * W + 1) * S:(2 * W + 2) * S] = word  # two-shot results (parity 1)
         x_all = torch.stack([mnist_like_device(2 * B, seed=10 + q, device=dev)[0]
                              for q in range(W)]).contiguous()
         dz1A = torch.zeros(W * mlp_step.factor_plane(B), device=dev)
         xs = x_all.stride(0)
-        hx = comm._h
-
-        def reset():
-            hx.reset_epochs(stream_handle())
-
-        def fused2():
-            reset()
-            comm.mlp_fwdapply(p[0], p[1], 1e-4, x_all[r][:B], x_all[r][B:], ws, True)
-            h.mlp_head2(ptr(p[1]), ptr(yc), ptr(ws.buf), B, stream_handle(), mlp_step.XG_SLABS)
-
-        def fused2x():
-            comm.two_shot = True
-            reset()
-            comm.mlp_fwdapply(p[0], p[1], 1e-4, x_all[r][:B], x_all[r][B:], ws, True)
-            h.mlp_head2(ptr(p[1]), ptr(yc), ptr(ws.buf), B, stream_handle(), mlp_step.XG_SLABS)
-            comm.two_shot = False
-
-        def factor2():
-            reset()
-            comm.mlp_fwdapply_factor(p[0], p[1], 1e-4, x_all[r][:B], x_all[r][B:], xs, dz1A, ws,
-                                     True)
-            comm.mlp_head(p[1], yc, ws, dz1A, nslab=14)
-
-        def fused():
-            reset()
-            h.mlp_fwd(ptr(p[0]), 0, 0.0, 0, ptr(xc), ptr(ws.buf), B, stream_handle())
-            h.mlp_head(ptr(p[0]), 0, 0.0, 0, ptr(yc), ptr(ws.buf), B, stream_handle())
-            comm.mlp_wgrad(p[0], 1e-4, xc, ws)
-
-        def factor():
-            reset()
-            h.mlp_fwd(ptr(p[0]), 0, 0.0, 0, ptr(x_all[r][B:]), ptr(ws.buf), B, stream_handle())
-            comm.mlp_head(p[0], yc, ws, dz1A, nslab=7)
-            comm.mlp_wgrad_factor(p[0], 1e-4, x_all[r][B:], xs, dz1A, ws)
-
-        t_reset = graph_us(reset, dev)
         res = {}
-        for name, fn in (("fused2", fused2), ("fused2x", fused2x), ("factor2", factor2),
-                         ("fused", fused),
-                         ("factor", factor)):
+        for name in engines:
+            # each engine's communicator has the slot size the selector gives it
+            # (mlp_step.engine_slot_words); "<engine>@big" forces the fused2 pair layout's size
+            kind, _, big = name.partition("@")
+            words = mlp_step.XG_SLOT_WORDS if big else mlp_step.engine_slot_words(kind)
+            comm, regs = XgmiComm.with_local_peers(r, W, words, device=dev, protocol="push",
+                                                   timeout_s=1.0)
+            S = comm.slot_stride
+            word = (1 << 32) | int(torch.tensor([1e-3]).view(torch.int32).item())
+            for q in range(W):
+                if q != r:
+                    o = (1 * W + q) * S  # parity 1 = epoch 1
+                    regs[r][o:o + S] = word
+            regs[r][(2 * W + 1) * S:(2 * W + 2) * S] = word  # two-shot results (parity 1)
+            hx = comm._h
+
+            def reset():
+                hx.reset_epochs(stream_handle())
+
+            def fused2():
+                reset()
+                comm.mlp_fwdapply(p[0], p[1], 1e-4, x_all[r][:B], x_all[r][B:], ws, True)
+                h.mlp_head2(ptr(p[1]), ptr(yc), ptr(ws.buf), B, stream_handle(), mlp_step.XG_SLABS)
+
+            def fused2x():
+                comm.two_shot = True
+                reset()
+                comm.mlp_fwdapply(p[0], p[1], 1e-4, x_all[r][:B], x_all[r][B:], ws, True)
+                h.mlp_head2(ptr(p[1]), ptr(yc), ptr(ws.buf), B, stream_handle(), mlp_step.XG_SLABS)
+                comm.two_shot = False
+
+            def factor2():
+                reset()
+                comm.mlp_fwdapply_factor(p[0], p[1], 1e-4, x_all[r][:B], x_all[r][B:], xs, dz1A,
+                                         ws, True)
+                comm.mlp_head(p[1], yc, ws, dz1A, nslab=mlp_step.FACTOR_SLABS)
+
+            def fused():
+                reset()
+                h.mlp_fwd(ptr(p[0]), 0, 0.0, 0, ptr(xc), ptr(ws.buf), B, stream_handle())
+                h.mlp_head(ptr(p[0]), 0, 0.0, 0, ptr(yc), ptr(ws.buf), B, stream_handle())
+                comm.mlp_wgrad(p[0], 1e-4, xc, ws)
+
+            def factor():
+                reset()
+                h.mlp_fwd(ptr(p[0]), 0, 0.0, 0, ptr(x_all[r][B:]), ptr(ws.buf), B, stream_handle())
+                comm.mlp_head(p[0], yc, ws, dz1A, nslab=7)
+                comm.mlp_wgrad_factor(p[0], 1e-4, x_all[r][B:], xs, dz1A, ws)
+
+            fn = {"fused2": fused2, "fused2x": fused2x, "factor2": factor2, "fused": fused,
+                  "factor": factor}[kind]
+            t_reset = graph_us(reset, dev)
             res[name] = round(graph_us(fn, dev) - t_reset, 2)
-        comm.check()
-        res["epoch_reset_us"] = round(t_reset, 2)
+            comm.check()
+            res.setdefault("epoch_reset_us", round(t_reset, 2))
+            comm.destroy()
+            del regs
         out["world%d" % W] = res
-        comm.destroy()
     print(json.dumps(out, indent=1))
 
 
