@@ -41,6 +41,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -159,8 +160,19 @@ __attribute__((noinline)) void dtfx_racy_read(Writer& w, const float* p, size_t 
   w.raw(p, nbytes);
 }
 // g: the gradient bytes inside the request buffer (no alignment guarantee: loaded by memcpy)
-__attribute__((noinline)) void dtfx_hogwild_apply(float* p, const char* g, size_t n, float lr) {
-  for (size_t i = 0; i < n; ++i) {
+// first: where this apply starts (it wraps around).  Every connection thread starts at its own
+// offset (PSServer::serve), so concurrent Hogwild applies of several workers walk different
+// cache lines at any moment instead of chasing each other through the same ones (each line
+// then bounces between the cores once per apply rather than once per competing thread).
+__attribute__((noinline)) void dtfx_hogwild_apply(float* p, const char* g, size_t n, float lr,
+                                                  size_t first = 0) {
+  first = n ? first % n : 0;
+  for (size_t i = first; i < n; ++i) {
+    float gi;
+    std::memcpy(&gi, g + 4 * i, 4);
+    p[i] -= lr * gi;
+  }
+  for (size_t i = 0; i < first; ++i) {
     float gi;
     std::memcpy(&gi, g + 4 * i, 4);
     p[i] -= lr * gi;
@@ -275,7 +287,10 @@ class PSServer {
     return vars_[id].get();
   }
 
+  // this connection thread's Hogwild start offset, in eighths of a variable (dtfx_hogwild_apply)
+  static thread_local size_t rot_;
   void serve(int fd) {
+    rot_ = static_cast<size_t>(conn_seq_.fetch_add(1)) % 8;
     // Request and reply buffers live for the connection: a fresh 318 KB reply string per pull
     // was an mmap'd allocation (above malloc's mmap threshold) whose pages the kernel zeroed
     // and faulted in on every request, and the reply was then copied once more behind its
@@ -407,7 +422,7 @@ class PSServer {
           } else {
             // Hogwild, as ApplyGradientDescent(use_locking=False): concurrent
             // workers may interleave element updates.
-            dtfx_hogwild_apply(p, g, cnt, lr);
+            dtfx_hogwild_apply(p, g, cnt, lr, rot_ * cnt / 8 / 16 * 16);
           }
         }
         break;
@@ -536,6 +551,7 @@ class PSServer {
   std::atomic<bool> running_{false}, shutdown_req_{false};
   std::thread acc_;
   std::mutex cmu_, vmu_;
+  std::atomic<int> conn_seq_{0};
   std::vector<int> conns_;
   std::vector<std::thread> threads_;
   std::vector<std::unique_ptr<Var>> vars_;
@@ -552,6 +568,8 @@ class PSServer {
   uint64_t sync_tokens_ = 0;
   std::atomic<uint64_t> sync_rounds_{0}, sync_stale_{0}, sync_withdrawn_{0};
 };
+
+thread_local size_t PSServer::rot_ = 0;
 
 // ---------------------------------------------------------------- client
 class PSClient {
@@ -986,12 +1004,22 @@ class PSClient {
   // the request bytes -- 318 KB of gradient for the reference MLP -- are copied into the
   // socket by this thread while the caller stages its next batch; push_step_pull_end waits
   // for it.  It spins briefly between exchanges (they come every ~0.1 ms), then sleeps.
+  // Spins before the sender sleeps (DTFX_PS_SENDER_SPINS, default 20000): several workers per
+  // host each spinning a sender thread compete with the ps threads for the CPU share.
+  static int sender_spins() {
+    static const int n = [] {
+      const char* e = getenv("DTFX_PS_SENDER_SPINS");
+      return e ? std::max(0, atoi(e)) : 20000;
+    }();
+    return n;
+  }
   void sender_loop() {
+    const int max_spins = sender_spins();
     while (true) {
       int spins = 0;
       while (send_state_.load(std::memory_order_acquire) != 1) {
         if (sender_stop_.load(std::memory_order_acquire)) return;
-        if (++spins < 20000) {
+        if (++spins < max_spins) {
           __builtin_ia32_pause();
         } else {
           std::unique_lock<std::mutex> lk(smu_);

@@ -171,17 +171,25 @@ __global__ __launch_bounds__(64) void mlp_fwd_kernel(
 // ---------------------------------------------------------------------------
 // XW > 0 (factor exchange, MlpXg in xgmi.h): the row's dz1 values are also pushed as LL
 // words into slot (parity, me) of every peer and every peer's values for the same (j, row)
-// are gathered from local memory into dz1A [XW][HP][BP] -- the all-gather of the backprop
+// are gathered from local memory into dz1A [XW][BP][HP] -- the all-gather of the backprop
 // factors that mlp_wgrad_factor_kernel turns into the global weight gradient.
 template <bool APPLY, bool TRACE, int XW = 0, int NSLAB = KS>
 __global__ __launch_bounds__(64) void mlp_head_kernel(
     const float* __restrict__ p_old, const float* __restrict__ grad, float lr,
     float* __restrict__ p_new, const int* __restrict__ labels, Bufs w, int B,
-    unsigned long long* __restrict__ tr, MlpXg xg, float* __restrict__ dz1A) {
+    unsigned long long* __restrict__ tr, MlpXg xg, float* __restrict__ dz1A,
+    const float* __restrict__ x_next = nullptr) {
   static_assert(XW == 0 || (!APPLY && !TRACE), "the factor exchange runs the direct step");
   if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 0);
   const int BP = ((B + 15) >> 4) * 16;
   const int row = blockIdx.x, lane = threadIdx.x;
+  // x_next (the next step's batch, pipelined single-GPU step): one dword per 128-B line of
+  // its row `row` is read here and only checked at the very end, so the row sits in the
+  // memory-side cache when the next launch's forward reads it (instead of an HBM miss on its
+  // first round trip); nothing waits for it before the head's own work is done
+  unsigned pf = 0u;
+  if (x_next != nullptr && lane < (D + 31) / 32)
+    pf = __float_as_uint(x_next[(size_t)row * D + lane * 32]);
   const int y = labels[row];
   const unsigned ep = XW > 0 ? xg.epochs[MLP_XG_HEAD_EPOCH + row] + 1 : 0u;
   const bool publish = APPLY && row == 0;
@@ -302,38 +310,55 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     }
   }
   if constexpr (XW > 0) {
+    // the row's 100 factors travel as 50 16-byte word pairs {dz(2l), ep, dz(2l+1), ep} at
+    // word row * HP + 2l of slot (parity, me) -- a wave's pushes and polls are contiguous
+    // 800-B runs, one store / load per lane and peer -- and land in dz1A [XW][BP][HP] row-major
+    // (one 8-byte store per lane and rank).  Each 8-byte half carries the epoch (as
+    // xg_exchange16); every poll is issued before the pushes (xgll::first_loads).
     using xgll::u64;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const long long par = ep & 1u, plane = (long long)HP * BP;
     const int me = xg.rank;
-    auto local = [&](int q) { return (const u64*)xg.peers.data[me] + (par * XW + q) * xg.S; };
-    size_t offs[2];
-    bool act[2];
+    const bool act = lane < H / 2;
+    const long long woff = (long long)row * HP + 2 * (act ? lane : 0);
+    auto slot = [&](int dst, int src) {
+      return (u32x4*)((u64*)xg.peers.data[dst] + (par * XW + src) * xg.S + woff);
+    };
+    u32x4 wq[XW];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      act[u] = 2 * lane + u < H;
-      offs[u] = (size_t)(act[u] ? 2 * lane + u : 0) * BP + row;
-    }
-    // first polls, then the pushes (xgll::first_loads: one vmcnt for both); every peer's
-    // wait still overlaps ours
-    u64 wq[2][XW];
-    xgll::first_loads<XW, 2>(local, offs, act, me, ep, wq);
+    for (int q = 0; q < XW; ++q)
+      if (act && q != me) wq[q] = *(volatile u32x4*)slot(me, q);
+    if (act) {
+      const u32x4 out = {__float_as_uint(dzv[0]), ep, __float_as_uint(dzv[1]), ep};
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (act[u]) {
-        const u64 wd = xgll::word(dzv[u], ep);
-#pragma unroll
-        for (int d = 0; d < XW; ++d)
-          if (d != me) xgll::store((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + offs[u], wd);
-      }
+      for (int d = 0; d < XW; ++d)
+        if (d != me) *slot(d, me) = out;
     }
     bool fail = false;
-    float vals[2][XW];
-    xgll::finish_all_n<XW, 2>(local, offs, act, me, ep, wq, dzv, vals, xg.ticks, fail);
+    if (act) {
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        bool ready = true;
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-      if (act[u])
+        for (int q = 0; q < XW; ++q)
+          if (q != me && (wq[q].y != ep || wq[q].w != ep)) {
+            ready = false;
+            wq[q] = *(volatile u32x4*)slot(me, q);
+          }
+        if (ready) break;
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xg.ticks) {
+          fail = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
 #pragma unroll
-        for (int q = 0; q < XW; ++q) dz1A[q * plane + offs[u]] = vals[u][q];
+      for (int q = 0; q < XW; ++q) {
+        const float2 v = q == me ? make_float2(dzv[0], dzv[1])
+                                 : make_float2(__uint_as_float(wq[q].x), __uint_as_float(wq[q].z));
+        *reinterpret_cast<float2*>(&dz1A[q * plane + woff]) = v;
+      }
+    }
     if (lane == 0) xg.epochs[MLP_XG_HEAD_EPOCH + row] = ep;
     if (fail) atomicExch(xg.err, 1);
   }
@@ -346,6 +371,8 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     w.rowstat[2 * row] = m + __logf(se) - ly;  // xent of this row
     w.rowstat[2 * row + 1] = (am == y) ? 1.f : 0.f;
   }
+  // consume the prefetch (a signalling-NaN pattern no finite input has: never taken)
+  if (x_next != nullptr && pf == 0x7FBADBADu) w.rowstat[2 * row + 1] = 0.f;
   if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 3);
 }
 
@@ -456,7 +483,11 @@ __device__ __forceinline__ void xg_exchange2p(const MlpXg& xg, unsigned ep, long
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   const long long par = ep & 1u;
   const int me = xg.rank;
-  const int own = ((lane >> 4) + 4 * sp) % XW;
+  // owner class of the pair: (q + 4 sp) % XW -- at 8 ranks one rank owns one (q, sp) row of
+  // a column group.  DTFX_XG_SPLIT bit 3 (A/B runs): (q + 4 (sp ^ h)) % XW, h = the lane's half
+  // of its 16-lane row, so a rank owns half a row in EACH of the two waves
+  const int h = (xg.split & 8) ? ((lane >> 3) & 1) : 0;
+  const int own = ((lane >> 4) + 4 * (sp ^ h)) % XW;
   const bool mine = own == me;
   auto slot = [&](int dst, int src) {
     return (u32x4*)((u64*)xg.peers.data[dst] + (par * XW + src) * xg.S + woff);
@@ -1127,8 +1158,15 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
 // Small-parameter blocks exchange dW2/db1/db2 partials of step t-1 as in the 3-launch factor
 // engine (waves 0..3 of the block).  The head of step t all-gathers dz1 into dz1A
 // (mlp_head_kernel<.., XW, KS3>).
+// LDSX (DTFX_FACTOR_LDS=1): the block's x slab of every rank's previous batch -- XW * BP rows
+// x 28 features -- is staged into LDS once with 16-byte loads (12-13 per thread), and each
+// wave reads its B operands from there (4 ds_read_b32 per batch group) instead of issuing 4
+// 4-byte global loads per group (56 per lane at 8 ranks).  Rows of 36 floats: the four
+// 16-lane row groups of a read land on disjoint bank quarters.  Padded batch rows hold row
+// B - 1 (finite; dz1A is zero there).
 constexpr int FX_SLOTS = (KS3 + 7) / 8 * HT;  // block slots per XCD (4 slice rows x 7 tiles)
-template <int XW, int NGT>
+constexpr int FX_PITCH = 36;                  // LDS row pitch of the staged x slab (floats)
+template <int XW, int NGT, bool LDSX = false>
 __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
     const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
     const float* __restrict__ x_prev, const float* __restrict__ x, long long xstride,
@@ -1187,7 +1225,46 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
   f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
   // one round at 8 ranks x 7 groups (14 per split); more only for batches > 112 rows
   constexpr int CH = (XW * (NGT > 0 ? NGT : 7) + 3) / 4;
-  for (int c0 = g0; c0 < g1; c0 += CH) {
+  if constexpr (LDSX) {
+    constexpr int ROWS = XW * (NGT > 0 ? NGT * 16 : MAXB / 2);  // B <= 128 here
+    __shared__ float xs[ROWS * FX_PITCH];
+    {  // stage: row rr = rank q's batch row b (q = rr / BP), 7 float4 per row
+      const int nrow = XW * BP;
+      for (int i = threadIdx.x; i < nrow * 7; i += 512) {
+        const int rr = i / 7, c4 = i - rr * 7;
+        const int qq = rr / BP, b = rr - qq * BP;
+        const float* src = x_prev + (long long)(qq - me) * xstride + (size_t)(b < B ? b : B - 1) * D +
+                           f0 + 4 * c4;
+        *reinterpret_cast<float4*>(&xs[rr * FX_PITCH + 4 * c4]) = f4(src);
+      }
+    }
+    constexpr int CHL = (XW * (NGT > 0 ? NGT : MAXB / 32) + 3) / 4;  // >= per: one round
+    float4 av[CHL];
+#pragma unroll
+    for (int i = 0; i < CHL; ++i) {
+      const int g = g0 + i;
+      if (g < g1) {
+        const int qq = g / NG, gg = g - qq * NG;
+        const float* a = dz1A + ((size_t)qq * BP + gg * 16 + q * 4) * HP + jt * 16 + r;
+        av[i] = make_float4(a[0], a[HP], a[2 * HP], a[3 * HP]);
+      }
+    }
+    __syncthreads();
+    const int fcl = cv ? fl : KWX - 1;  // the lane's column in the slab
+#pragma unroll
+    for (int i = 0; i < CHL; ++i) {
+      const int g = g0 + i;
+      if (g < g1) {
+        const int qq = g / NG, gg = g - qq * NG;
+        const float* xr = &xs[(qq * BP + gg * 16 + q * 4) * FX_PITCH + fcl];
+        acc0 = mfma16x16x4(av[i].x, xr[0], acc0);
+        acc1 = mfma16x16x4(av[i].y, xr[FX_PITCH], acc1);
+        acc0 = mfma16x16x4(av[i].z, xr[2 * FX_PITCH], acc0);
+        acc1 = mfma16x16x4(av[i].w, xr[3 * FX_PITCH], acc1);
+      }
+    }
+  }
+  for (int c0 = g0; c0 < (LDSX ? g0 : g1); c0 += CH) {
     float4 av[CH];
     float xv[CH][4];
 #pragma unroll
@@ -1195,7 +1272,8 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
       const int g = c0 + i;
       if (g < g1) {  // wave-uniform
         const int qq = g / NG, gg = g - qq * NG;
-        av[i] = f4(dz1A + ((size_t)qq * HP + jt * 16 + r) * BP + gg * 16 + q * 4);
+        const float* a = dz1A + ((size_t)qq * BP + gg * 16 + q * 4) * HP + jt * 16 + r;
+        av[i] = make_float4(a[0], a[HP], a[2 * HP], a[3 * HP]);
         const float* xq = x_prev + (long long)(qq - me) * xstride + fc;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1262,7 +1340,7 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
 
 // ---------------------------------------------------------------------------
 // K3, factor engine (sufficient-factor exchange, world XW): the backprop factors dz1 of
-// every rank were all-gathered by mlp_head_kernel<.., XW> into dz1A [XW][HP][BP], and every
+// every rank were all-gathered by mlp_head_kernel<.., XW> into dz1A [XW][BP][HP], and every
 // rank holds every rank's (deterministic, device-resident) batch, so each rank computes the
 // GLOBAL dW1^T = sum_q dz1_q^T . x_q itself (K = XW * BP) and applies it -- the 313 KB W1
 // gradient never crosses xGMI; only the 1,110 small-parameter gradients are exchanged
@@ -1316,7 +1394,8 @@ __global__ __launch_bounds__(256) void mlp_wgrad_factor_kernel(
       const int g = c0 + i;
       if (g < g1) {  // wave-uniform
         const int qq = g / NG, gg = g - qq * NG;
-        av[i] = f4(dz1A + ((size_t)qq * HP + jt * 16 + r) * BP + gg * 16 + q4 * 4);
+        const float* a = dz1A + ((size_t)qq * BP + gg * 16 + q4 * 4) * HP + jt * 16 + r;
+        av[i] = make_float4(a[0], a[HP], a[2 * HP], a[3 * HP]);
         const float* xq = x + (long long)(qq - me) * xstride + kt * 16 + r;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1768,7 +1847,7 @@ void mlp_pipelined_trace_launch(const float* p_old, float* p_new, float lr, cons
 // nslab: the K slabs the first launch wrote -- 0: the single-GPU step's (mlp_single_ks());
 // the fused2 / fused2x first launch writes KS3 = 28, the factor engine's KS2 = 14.
 void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipStream_t stream,
-                      int nslab) {
+                      int nslab, const float* x_next) {
   using namespace mlp;
   check_b(B);
   if (nslab == 0) nslab = mlp_single_ks();
@@ -1776,11 +1855,20 @@ void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipSt
   const Bufs w = make_bufs(ws, B);
   if (nslab == KS3)
     hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS3>), dim3(B), dim3(64), 0, stream, p, p,
-                       0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr);
+                       0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr, x_next);
   else
     hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS2>), dim3(B), dim3(64), 0, stream, p, p,
                        0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr);
   DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// DTFX_MLP_PREFETCH=1: the head of step t touches step t+1's batch (mlp_head_kernel x_next).
+static bool mlp_prefetch_next() {
+  static const bool on = [] {
+    const char* e = std::getenv("DTFX_MLP_PREFETCH");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
 }
 
 // n pipelined single-GPU steps issued from ONE host call (no Python, no hipGraph): step i
@@ -1807,9 +1895,11 @@ void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float 
   const size_t xb = (size_t)B * D;
   const bool rt7 = (B + 15) / 16 == 7;
   const bool ks3 = mlp_single_ks() == KS3;
+  const bool pref = mlp_prefetch_next();
   for (int i = 0; i < n; ++i) {
     const int prev = (pos + nbatches - 1) % nbatches;
     const float* xcur = x + (size_t)pos * xb;
+    const float* xnext = pref && i + 1 < n ? x + (size_t)((pos + 1) % nbatches) * xb : nullptr;
     const float* xprev = pending ? x + (size_t)prev * xb : xcur;
     const float* po = bufs[cur];
     float* pn = bufs[cur ^ 1];
@@ -1826,7 +1916,7 @@ void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float 
                            B, pending, MlpXg{}, nullptr);
       hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS3>), dim3(B), dim3(64), 0, stream, pn,
                          pn, 0.f, nullptr, labels + (size_t)pos * B, w, B, nullptr, MlpXg{},
-                         nullptr);
+                         nullptr, xnext);
     } else {
       if (rt7)
         hipLaunchKernelGGL((mlp_fwdapply_kernel<7>), dim3(HT * KS2 + HT), dim3(256), 0, stream, po,
@@ -1863,10 +1953,21 @@ void mlp_fwdapply_factor_launch(const float* p_old, float* p_new, float lr, cons
   if (xg.S < NPARAM) throw std::runtime_error("mlp_fwdapply_factor: exchange slots too small");
   const Bufs w = make_bufs(ws, B);
   dim3 grid(8 * FX_SLOTS + HT), block(512);
+  static const bool ldsx = [] {
+    const char* e = std::getenv("DTFX_FACTOR_LDS");
+    return e && std::atoi(e) != 0;
+  }();
 #define DTFX_FF(WW, NGT)                                                                       \
-  hipLaunchKernelGGL((mlp_fwdapply_factor_kernel<WW, NGT>), grid, block, 0, stream, p_old,     \
-                     p_new, lr, x_prev, x, xstride, dz1A, w, ctr, stats, stats_ring, B,        \
-                     stats_on, xg)
+  do {                                                                                         \
+    if (ldsx)                                                                                  \
+      hipLaunchKernelGGL((mlp_fwdapply_factor_kernel<WW, NGT, true>), grid, block, 0, stream,  \
+                         p_old, p_new, lr, x_prev, x, xstride, dz1A, w, ctr, stats, stats_ring, \
+                         B, stats_on, xg);                                                     \
+    else                                                                                       \
+      hipLaunchKernelGGL((mlp_fwdapply_factor_kernel<WW, NGT>), grid, block, 0, stream, p_old, \
+                         p_new, lr, x_prev, x, xstride, dz1A, w, ctr, stats, stats_ring, B,    \
+                         stats_on, xg);                                                        \
+  } while (0)
 #define DTFX_FFW(WW)                                 \
   case WW:                                           \
     if ((B + 15) / 16 == 7) DTFX_FF(WW, 7);          \

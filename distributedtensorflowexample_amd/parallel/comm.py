@@ -173,3 +173,14 @@ def make_comm(kind="auto", group=None):
     if kind == "native":
         return NativeComm.from_process_group(group)
     return TorchComm(group)
+
+
+def make_comm_stream(device):
+    """The stream the gradient-bucket all-reduces run on (overlapping the backward).
+    ``DTFX_COMM_PRIORITY``: its HIP stream priority (torch's convention: lower = higher
+    priority; ``torch.cuda.Stream.priority_range()``); unset: the default priority.  Measured
+    on the simulated world-8 step (tools/probes/dp_sim.py)."""
+    prio = os.environ.get("DTFX_COMM_PRIORITY")
+    if prio is None or prio == "":
+        return torch.cuda.Stream(device)
+    return torch.cuda.Stream(device, priority=int(prio))

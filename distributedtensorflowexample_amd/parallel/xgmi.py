@@ -115,7 +115,7 @@ class XgmiComm:
 
     def mlp_head(self, p, labels, ws, dz1A, nslab=7):
         """Factor engine: MLP head launch that also all-gathers every rank's backprop factors
-        dz1 into ``dz1A`` [world, 112, BP] (protocol "push"); see ``ops.mlp_step.step_factor``.
+        dz1 into ``dz1A`` [world, BP, 112] (row-major; protocol "push"); see ``ops.mlp_step.step_factor``.
         ``nslab``: partial-z1 planes left by the forward (7: 3-launch, 28: pipelined)."""
         from ..ops._ext import ptr
 

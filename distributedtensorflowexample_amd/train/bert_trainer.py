@@ -40,7 +40,10 @@ class BertTrainer:
 
             TR.cast_bf16(p.master, p.bf)
         self.gpu = self.device.type == "cuda"
-        self.comm_stream = torch.cuda.Stream(self.device) if (self.gpu and overlap and self.world > 1) else None
+        from ..parallel.comm import make_comm_stream
+
+        self.comm_stream = (make_comm_stream(self.device) if (self.gpu and overlap and self.world > 1)
+                            else None)
         # weight gradients on a second stream: on one GPU the step measured 1.7 % faster without
         # it once the attention backward ran two blocks per CU (7,903-7,919 -> 8,034-8,055
         # seq/s, profiles/r4/bert/half_nows/), so it is the multi-GPU default only;

@@ -30,7 +30,9 @@ class ResNetTrainer:
 
             comm.broadcast_(p.master, 0)
             TR.cast_bf16(p.master, p.bf)
-        self.comm_stream = (torch.cuda.Stream(self.device)
+        from ..parallel.comm import make_comm_stream
+
+        self.comm_stream = (make_comm_stream(self.device)
                             if (self.device.type == "cuda" and overlap and self.world > 1) else None)
         # DTFX_RESNET_WSTREAM=1: weight gradients on a second stream (models/resnet.py).  Off:
         # the persistent convolution kernels size their grids for the whole chip, and blocks

@@ -81,8 +81,10 @@ def main(argv=None):
         server = Server(cluster, job_name="ps", task_index=FLAGS.task_index)
         server.join()
     elif FLAGS.job_name == "worker":
+        from distributedtensorflowexample_amd.config import apply_hip_schedule
         from distributedtensorflowexample_amd.train.worker import Worker
 
+        apply_hip_schedule()  # DTFX_HIP_SCHED (before the first GPU call)
         mnist = read_data_sets(FLAGS.data_dir or None, one_hot=True)
         config = ConfigProto(gpu_options=gpu_options)
         server = Server(cluster, job_name="worker", task_index=FLAGS.task_index, config=config)

@@ -359,7 +359,7 @@ def test_factor_head_allgather_simulated_peers(gpu, world, rank, B, nslab):
     BP = (B + 15) // 16 * 16
     HP = mlp_step.HP
     plane = HP * BP
-    dz1A = torch.zeros(world, HP, BP, device=gpu)
+    dz1A = torch.zeros(world, BP, HP, device=gpu)  # [rank][batch row][hidden]
     own = _ref_dz1(p, x, y)  # [B, H]
     S, par_w = comm.slot_stride, world
     g = torch.Generator().manual_seed(5 + world)
@@ -369,8 +369,8 @@ def test_factor_head_allgather_simulated_peers(gpu, world, rank, B, nslab):
         for q in range(world):
             if q == rank:
                 continue
-            v = torch.zeros(HP, BP)
-            v[:100, :B] = torch.randn(100, B, generator=g)
+            v = torch.zeros(BP, HP)  # the slot's word layout: row * HP + hidden
+            v[:B, :100] = torch.randn(B, 100, generator=g)
             peer[q] = v
             o = (par * par_w + q) * S
             regs[rank][o:o + plane] = _words(v.reshape(-1).to(gpu), epoch)
@@ -386,18 +386,18 @@ def test_factor_head_allgather_simulated_peers(gpu, world, rank, B, nslab):
         got = dz1A.cpu()
         for q in range(world):
             if q == rank:
-                err = float((got[q, :100, :B].double() - own.t()).abs().max())
+                err = float((got[q, :B, :100].double() - own).abs().max())
                 assert err <= 1e-5, (epoch, err)
             else:
-                assert torch.equal(got[q, :100, :B], peer[q][:100, :B]), (epoch, q)
-        # every peer received my factors for (j < 100, row < B)
+                assert torch.equal(got[q, :B, :100], peer[q][:B, :100]), (epoch, q)
+        # every peer received my factors for (row < B, j < 100)
         for j in range(world):
             if j == rank:
                 continue
             o = (par * world + rank) * S
-            w = regs[j][o:o + plane].cpu().view(HP, BP)[:100, :B]
+            w = regs[j][o:o + plane].cpu().view(BP, HP)[:B, :100]
             assert bool((_epochs(w) == epoch).all()), (j, epoch)
-            assert float((_vals(w).double() - own.t()).abs().max()) <= 1e-5
+            assert float((_vals(w).double() - own).abs().max()) <= 1e-5
     comm.destroy()
 
 
@@ -409,8 +409,8 @@ def _factor_inputs(world, rank, B, dev, seed):
     x_all = torch.stack([mnist_like_device(B, seed=seed + q, device=dev)[0]
                          for q in range(world)]).contiguous()
     g = torch.Generator().manual_seed(seed)
-    dz1A = torch.zeros(world, mlp_step.HP, BP)
-    dz1A[:, :100, :B] = torch.randn(world, 100, B, generator=g) * 0.01
+    dz1A = torch.zeros(world, BP, mlp_step.HP)  # [rank][batch row][hidden], row-major
+    dz1A[:, :B, :100] = torch.randn(world, B, 100, generator=g) * 0.01
     return x_all, dz1A.to(dev)
 
 
@@ -418,7 +418,7 @@ def _global_w1_grad(dz1A, x_all, B):
     W = x_all.shape[0]
     g = torch.zeros(100, 784, dtype=torch.float64)
     for q in range(W):
-        g += dz1A[q, :100, :B].double().cpu() @ x_all[q].double().cpu()
+        g += dz1A[q, :B, :100].double().cpu().t() @ x_all[q].double().cpu()
     return g.reshape(-1)
 
 

@@ -10,6 +10,8 @@ fold).  Against the 1-GPU step, each switch A/B'd in the same process, interleav
   dp            world W, trainer defaults, bw kernel on all 256 workgroups
   dp_null       world W, all-reduce a no-op (the DP-mode trainer changes alone)
   dp_bw128 / 64 the bw kernel on 128 / 64 workgroups (fewer CUs taken from the backward)
+  dp_prio_hi    the comm stream at the highest HIP stream priority (default: the lowest,
+                the compute stream's)
   BERT: dp_nows (no weight-gradient stream), 1gpu_nofold (the 1-GPU step without the fold)
   ResNet: dp_ws (weight gradients on a side stream)
 
@@ -52,6 +54,8 @@ def make(model, variant, world, dev, a):
         env["DTFX_BERT_FOLD"] = "0"
     if variant == "dp_ws":
         env["DTFX_RESNET_WSTREAM"] = "1"
+    if variant == "dp_prio_hi":
+        env["DTFX_COMM_PRIORITY"] = str(torch.cuda.Stream.priority_range()[1])
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -93,9 +97,10 @@ def main():
     if a.variants:
         variants = a.variants.split(",")
     elif a.model == "bert":
-        variants = ["1gpu", "dp", "dp_null", "dp_nows", "dp_bw128", "dp_bw64", "1gpu_nofold"]
+        variants = ["1gpu", "dp", "dp_null", "dp_nows", "dp_bw128", "dp_bw64", "dp_prio_hi",
+                    "1gpu_nofold"]
     else:
-        variants = ["1gpu", "dp", "dp_null", "dp_bw128", "dp_bw64", "dp_ws"]
+        variants = ["1gpu", "dp", "dp_null", "dp_bw128", "dp_bw64", "dp_prio_hi", "dp_ws"]
     trainers = {}
     for v in variants:
         tr = make(a.model, v, a.world, dev, a)

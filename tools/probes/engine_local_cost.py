@@ -125,8 +125,22 @@ def main():
                 comm.mlp_head(p[0], yc, ws, dz1A, nslab=7)
                 comm.mlp_wgrad_factor(p[0], 1e-4, x_all[r][B:], xs, dz1A, ws)
 
+            def factor2_fwd():  # the factor engine's first launch + the plain head
+                reset()
+                comm.mlp_fwdapply_factor(p[0], p[1], 1e-4, x_all[r][:B], x_all[r][B:], xs, dz1A,
+                                         ws, True)
+                h.mlp_head2(ptr(p[1]), ptr(yc), ptr(ws.buf), B, stream_handle(),
+                            mlp_step.FACTOR_SLABS)
+
+            def factor2_head():  # the 1-GPU first launch + the factor engine's head
+                reset()
+                h.mlp_fwdapply(ptr(p[0]), ptr(p[1]), 1e-4, ptr(x_all[r][:B]), ptr(x_all[r][B:]),
+                               ptr(ws.buf), ptr(ws.ctr), ptr(ws.stats), ws.stats_ring, B, 1,
+                               stream_handle())
+                comm.mlp_head(p[1], yc, ws, dz1A, nslab=mlp_step.FACTOR_SLABS)
+
             fn = {"fused2": fused2, "fused2x": fused2x, "factor2": factor2, "fused": fused,
-                  "factor": factor}[kind]
+                  "factor": factor, "factor2_fwd": factor2_fwd, "factor2_head": factor2_head}[kind]
             t_reset = graph_us(reset, dev)
             res[name] = round(graph_us(fn, dev) - t_reset, 2)
             comm.check()
