@@ -30,7 +30,7 @@ void mlp_ps_worker_step(float*, const float*, float*, const float*, const int*, 
 void mlp_tf_layout_launch(const float*, float*, int, const float*, int, hipStream_t);
 void mlp_fwdapply_launch(const float*, float*, float, const float*, const float*, float*, int*,
                          float*, int, int, int, hipStream_t, int);
-void mlp_head2_launch(const float*, const int*, float*, int, hipStream_t, int, const float*);
+void mlp_head2_launch(const float*, const int*, float*, int, hipStream_t, int);
 int mlp_single_ks_query();
 void mlp_pipelined_trace_launch(const float*, float*, float, const float*, const float*,
                                 const int*, float*, int*, float*, int, int, hipStream_t,
@@ -143,12 +143,10 @@ PYBIND11_MODULE(_hip, m) {
                                      reinterpret_cast<unsigned long long*>(trf),
                                      reinterpret_cast<unsigned long long*>(trh));
   });
-  m.def("mlp_head2", [](uintptr_t p, uintptr_t lab, uintptr_t ws, int B, uintptr_t s, int nslab,
-                        uintptr_t x_next) {
-    dtfx::mlp_head2_launch(P<const float>(p), P<const int>(lab), P<float>(ws), B, S(s), nslab,
-                           P<const float>(x_next));
+  m.def("mlp_head2", [](uintptr_t p, uintptr_t lab, uintptr_t ws, int B, uintptr_t s, int nslab) {
+    dtfx::mlp_head2_launch(P<const float>(p), P<const int>(lab), P<float>(ws), B, S(s), nslab);
   }, py::arg("p"), py::arg("labels"), py::arg("ws"), py::arg("B"), py::arg("stream"),
-     py::arg("nslab") = 0, py::arg("x_next") = 0,
+     py::arg("nslab") = 0,
      "head of the 2-launch step; nslab: slabs the first launch wrote (0: the single-GPU "
      "step's, 14: every data-parallel engine's)");
   m.def("mlp_run_pipelined", [](uintptr_t p0, uintptr_t p1, int cur, int pending, float lr,

@@ -177,19 +177,11 @@ template <bool APPLY, bool TRACE, int XW = 0, int NSLAB = KS>
 __global__ __launch_bounds__(64) void mlp_head_kernel(
     const float* __restrict__ p_old, const float* __restrict__ grad, float lr,
     float* __restrict__ p_new, const int* __restrict__ labels, Bufs w, int B,
-    unsigned long long* __restrict__ tr, MlpXg xg, float* __restrict__ dz1A,
-    const float* __restrict__ x_next = nullptr) {
+    unsigned long long* __restrict__ tr, MlpXg xg, float* __restrict__ dz1A) {
   static_assert(XW == 0 || (!APPLY && !TRACE), "the factor exchange runs the direct step");
   if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 0);
   const int BP = ((B + 15) >> 4) * 16;
   const int row = blockIdx.x, lane = threadIdx.x;
-  // x_next (the next step's batch, pipelined single-GPU step): one dword per 128-B line of
-  // its row `row` is read here and only checked at the very end, so the row sits in the
-  // memory-side cache when the next launch's forward reads it (instead of an HBM miss on its
-  // first round trip); nothing waits for it before the head's own work is done
-  unsigned pf = 0u;
-  if (x_next != nullptr && lane < (D + 31) / 32)
-    pf = __float_as_uint(x_next[(size_t)row * D + lane * 32]);
   const int y = labels[row];
   const unsigned ep = XW > 0 ? xg.epochs[MLP_XG_HEAD_EPOCH + row] + 1 : 0u;
   const bool publish = APPLY && row == 0;
@@ -316,23 +308,23 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     // (one 8-byte store per lane and rank).  Each 8-byte half carries the epoch (as
     // xg_exchange16); every poll is issued before the pushes (xgll::first_loads).
     using xgll::u64;
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    using xgll::u32x4;
     const long long par = ep & 1u, plane = (long long)HP * BP;
-    const int me = xg.rank;
+    const int me = xgll::uniform(xg.rank);
     const bool act = lane < H / 2;
     const long long woff = (long long)row * HP + 2 * (act ? lane : 0);
     auto slot = [&](int dst, int src) {
-      return (u32x4*)((u64*)xg.peers.data[dst] + (par * XW + src) * xg.S + woff);
+      return xgll::uniform_ptr((u64*)xg.peers.data[dst]) + (par * XW + src) * xg.S + woff;
     };
     u32x4 wq[XW];
 #pragma unroll
     for (int q = 0; q < XW; ++q)
-      if (act && q != me) wq[q] = *(volatile u32x4*)slot(me, q);
+      if (act && q != me) wq[q] = xgll::load_pair(slot(me, q));
     if (act) {
       const u32x4 out = {__float_as_uint(dzv[0]), ep, __float_as_uint(dzv[1]), ep};
 #pragma unroll
       for (int d = 0; d < XW; ++d)
-        if (d != me) *slot(d, me) = out;
+        if (d != me) *(u32x4*)slot(d, me) = out;
     }
     bool fail = false;
     if (act) {
@@ -343,7 +335,7 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
         for (int q = 0; q < XW; ++q)
           if (q != me && (wq[q].y != ep || wq[q].w != ep)) {
             ready = false;
-            wq[q] = *(volatile u32x4*)slot(me, q);
+            wq[q] = xgll::load_pair(slot(me, q));
           }
         if (ready) break;
         if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xg.ticks) {
@@ -371,8 +363,6 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     w.rowstat[2 * row] = m + __logf(se) - ly;  // xent of this row
     w.rowstat[2 * row + 1] = (am == y) ? 1.f : 0.f;
   }
-  // consume the prefetch (a signalling-NaN pattern no finite input has: never taken)
-  if (x_next != nullptr && pf == 0x7FBADBADu) w.rowstat[2 * row + 1] = 0.f;
   if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 3);
 }
 
@@ -387,7 +377,7 @@ __device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const 
                                             const bool (&ok)[N], float (&v)[N], bool& fail) {
   using xgll::u64;
   const long long par = ep & 1u;
-  const int me = xg.rank;
+  const int me = xgll::uniform(xg.rank);
   auto local = [&](int j) { return (const u64*)xg.peers.data[me] + (par * XW + j) * xg.S; };
   u64 w[N][XW];  // first polls before the pushes (xgll::first_loads: one vmcnt for both)
   xgll::first_loads<XW, N>(local, off, ok, me, ep, w);
@@ -422,23 +412,28 @@ __device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const 
 // instructions and requests of the wave, and 16-byte fabric writes on real xGMI).  Each 8-byte
 // half still carries its own epoch, so a reader never accepts a value of another epoch even if
 // the pair were observed as two 8-byte halves.  `woff`: this (slot, wave, lane)'s pair in the
-// XG_W1_BASE layout -- the same on every rank; both words are always written and gathered.
+// XG_W1_BASE layout -- the same on every rank.  `live` = false (a pair of padding columns /
+// hidden rows, the same on every rank): neither pushed nor gathered -- 22 % of the layout's
+// pairs, so the links carry live parameters only (78,400 of 100,352 words).
 template <int XW>
 __device__ __forceinline__ void xg_exchange16(const MlpXg& xg, unsigned ep, long long woff,
-                                              float (&v)[2], bool& fail) {
+                                              float (&v)[2], bool& fail, bool live = true) {
   using xgll::u64;
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  using xgll::u32x4;
   const long long par = ep & 1u;
-  const int me = xg.rank;
+  const int me = xgll::uniform(xg.rank);
+  const u64* mine = xgll::uniform_ptr((const u64*)xg.peers.data[me]) + woff;
   const u32x4 out = {__float_as_uint(v[0]), ep, __float_as_uint(v[1]), ep};
   u32x4 w[XW];  // first polls before the pushes (xgll::first_loads: one vmcnt for both)
 #pragma unroll
-  for (int j = 0; j < XW; ++j)
-    if (j != me)
-      w[j] = *(volatile u32x4*)((const u64*)xg.peers.data[me] + (par * XW + j) * xg.S + woff);
+  for (int j = 0; j < XW; ++j) {
+    w[j] = u32x4{0u, ep, 0u, ep};
+    if (live && j != me) w[j] = xgll::load_pair(mine + (par * XW + j) * xg.S);
+  }
 #pragma unroll
   for (int d = 0; d < XW; ++d)
-    if (d != me) *(u32x4*)((u64*)xg.peers.data[d] + (par * XW + me) * xg.S + woff) = out;
+    if (live && d != me)
+      *(u32x4*)(xgll::uniform_ptr((u64*)xg.peers.data[d]) + (par * XW + me) * xg.S + woff) = out;
   const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
   for (;;) {
     bool ready = true;
@@ -446,7 +441,7 @@ __device__ __forceinline__ void xg_exchange16(const MlpXg& xg, unsigned ep, long
     for (int j = 0; j < XW; ++j)
       if (j != me && (w[j].y != ep || w[j].w != ep)) {
         ready = false;
-        w[j] = *(volatile u32x4*)((const u64*)xg.peers.data[me] + (par * XW + j) * xg.S + woff);
+        w[j] = xgll::load_pair(mine + (par * XW + j) * xg.S);
       }
     if (ready) break;
     if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xg.ticks) {
@@ -475,36 +470,37 @@ __device__ __forceinline__ void xg_exchange16(const MlpXg& xg, unsigned ep, long
 // of two 8-byte LL accesses to two owners (per-element owners, xg_exchange2), and every poll
 // is issued before the hop's own pushes (xgll::first_loads: stores and loads share one
 // in-order vmcnt).  Each 8-byte half carries the epoch, as in xg_exchange16.
+// `live` as in xg_exchange16: a dead pair is neither pushed, gathered nor broadcast.
 template <int XW>
 __device__ __forceinline__ void xg_exchange2p(const MlpXg& xg, unsigned ep, long long woff,
                                               float (&v)[2], bool& fail, int lane, int sp,
-                                              unsigned long long* trw = nullptr) {
+                                              unsigned long long* trw = nullptr,
+                                              bool live = true) {
   using xgll::u64;
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  using xgll::u32x4;
   const long long par = ep & 1u;
-  const int me = xg.rank;
+  const int me = xgll::uniform(xg.rank);
   // owner class of the pair: (q + 4 sp) % XW -- at 8 ranks one rank owns one (q, sp) row of
   // a column group.  DTFX_XG_SPLIT bit 3 (A/B runs): (q + 4 (sp ^ h)) % XW, h = the lane's half
   // of its 16-lane row, so a rank owns half a row in EACH of the two waves
   const int h = (xg.split & 8) ? ((lane >> 3) & 1) : 0;
   const int own = ((lane >> 4) + 4 * (sp ^ h)) % XW;
-  const bool mine = own == me;
-  auto slot = [&](int dst, int src) {
-    return (u32x4*)((u64*)xg.peers.data[dst] + (par * XW + src) * xg.S + woff);
-  };
-  auto result = [&](int dst) { return (u32x4*)((u64*)xg.peers.data[dst] + (2 * XW + par) * xg.S + woff); };
+  const bool mine = live && own == me, other = live && own != me;
+  auto base = [&](int dst) { return xgll::uniform_ptr((u64*)xg.peers.data[dst]); };
+  auto slot = [&](int dst, int src) { return base(dst) + (par * XW + src) * xg.S + woff; };
+  auto result = [&](int dst) { return base(dst) + (2 * XW + par) * xg.S + woff; };
   auto ready2 = [&](const u32x4& w) { return w.y == ep && w.w == ep; };
   // ---- hop 1: owners' first polls, then the non-owners' push to their owner
   u32x4 w[XW];
 #pragma unroll
   for (int j = 0; j < XW; ++j)
-    if (mine && j != me) w[j] = *(volatile u32x4*)slot(me, j);
+    if (mine && j != me) w[j] = xgll::load_pair(slot(me, j));
   const u32x4 out = {__float_as_uint(v[0]), ep, __float_as_uint(v[1]), ep};
   // uniform loop over destinations, per-lane predicate: a per-lane peer index would turn the
   // kernel-argument pointer table into a private (scratch) array
 #pragma unroll
   for (int d = 0; d < XW; ++d)
-    if (d != me && own == d) *slot(d, me) = out;
+    if (other && own == d) *(u32x4*)slot(d, me) = out;
   const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
   if (mine) {
     for (;;) {
@@ -513,7 +509,7 @@ __device__ __forceinline__ void xg_exchange2p(const MlpXg& xg, unsigned ep, long
       for (int j = 0; j < XW; ++j)
         if (j != me && !ready2(w[j])) {
           ready = false;
-          w[j] = *(volatile u32x4*)slot(me, j);
+          w[j] = xgll::load_pair(slot(me, j));
         }
       if (ready) break;
       if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xg.ticks) {
@@ -534,14 +530,14 @@ __device__ __forceinline__ void xg_exchange2p(const MlpXg& xg, unsigned ep, long
   if (trw) trace_stamp(trw, 5);  // probe builds: the owned sums are complete
   // ---- hop 2: non-owners' first poll of the result, then the owners' broadcast
   u32x4 r = {0u, 0u, 0u, 0u};
-  if (!mine) r = *(volatile u32x4*)result(me);
+  if (other) r = xgll::load_pair(result(me));
   if (mine && !fail) {
     const u32x4 sum = {__float_as_uint(v[0]), ep, __float_as_uint(v[1]), ep};
 #pragma unroll
     for (int d = 0; d < XW; ++d)
-      if (d != me) *result(d) = sum;
+      if (d != me) *(u32x4*)result(d) = sum;
   }
-  if (!mine) {
+  if (other) {
     const long long t1 = (long long)__builtin_amdgcn_s_memrealtime();
     while (!ready2(r)) {
       if ((long long)__builtin_amdgcn_s_memrealtime() - t1 > xg.ticks) {
@@ -549,7 +545,7 @@ __device__ __forceinline__ void xg_exchange2p(const MlpXg& xg, unsigned ep, long
         break;
       }
       __builtin_amdgcn_s_sleep(1);
-      r = *(volatile u32x4*)result(me);
+      r = xgll::load_pair(result(me));
     }
     v[0] = __uint_as_float(r.x);
     v[1] = __uint_as_float(r.z);
@@ -565,7 +561,7 @@ __device__ __forceinline__ void xg_exchange2(const MlpXg& xg, unsigned ep, const
                                              int i0 = 0) {
   using xgll::u64;
   const long long par = ep & 1u;
-  const int me = xg.rank;
+  const int me = xgll::uniform(xg.rank);
   const int q = lane >> 4;
   int own[N];
   bool mine[N], other[N];
@@ -575,8 +571,12 @@ __device__ __forceinline__ void xg_exchange2(const MlpXg& xg, unsigned ep, const
     mine[i] = ok[i] && own[i] == me;
     other[i] = ok[i] && own[i] != me;
   }
-  auto slot = [&](int dst, int src) { return (u64*)xg.peers.data[dst] + (par * XW + src) * xg.S; };
-  auto result = [&](int dst) { return (u64*)xg.peers.data[dst] + (2 * XW + par) * xg.S; };
+  auto slot = [&](int dst, int src) {
+    return xgll::uniform_ptr((u64*)xg.peers.data[dst]) + (par * XW + src) * xg.S;
+  };
+  auto result = [&](int dst) {
+    return xgll::uniform_ptr((u64*)xg.peers.data[dst]) + (2 * XW + par) * xg.S;
+  };
   auto local = [&](int j) { return (const u64*)slot(me, j); };
   // each hop issues its first polls before its pushes (xgll::first_loads: one vmcnt for both)
   u64 w1[N][XW];
@@ -1038,15 +1038,17 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
         g2[e] = sp == 0 ? gv[e] : gv[2 + e];
       }
       if (TRACE) trace_stamp(trw, 4);
+      // the pair's two hidden rows j, j + 1 (j even, H even: both live or both padding)
+      const bool plive = cv && jt * 16 + q * 4 + 2 * sp < H;
       if constexpr (TWO) {
         if (xg.split & 4)  // (DTFX_XG_SPLIT bit 2: the round-4 per-element owners, A/B runs)
           xg_exchange2<XW, 2>(xg, ep, offw, okw, g2, fail, lane, TRACE ? trw : nullptr, 2 * sp);
         else
           xg_exchange2p<XW>(xg, ep, XG_W1_BASE + ((long long)(eslot * 2 + sp) * 64 + lane) * 2,
-                            g2, fail, lane, sp, TRACE ? trw : nullptr);
+                            g2, fail, lane, sp, TRACE ? trw : nullptr, plive);
       } else
         xg_exchange16<XW>(xg, ep, XG_W1_BASE + ((long long)(eslot * 2 + sp) * 64 + lane) * 2,
-                          g2, fail);
+                          g2, fail, plive);
       if (TRACE) trace_stamp(trw, 6);
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -1145,33 +1147,35 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
 //   g = sum_q dz1A[q][jt]^T . x_q(t-1)   (K = XW * BP, the all-gathered factors of step
 //   t-1 and every rank's resident batch), W1new = W1old - lr * g,
 // then step t's forward on W1new.  The single-GPU step's 28-feature K slices (196 W1
-// blocks): 512-thread blocks, wave (c, s) owns column group c (16 + 12 live features) and
-// K split s of 4; the 4 partial slices are added in split order through LDS (identical order
-// on every rank: bit-identical replicas).  At 8 ranks the global W1 gradient is 8 x the
-// 1-GPU step's MFMA work (K = 800), so it must be spread over the chip and issue all of its
-// loads in ONE round trip: a wave's K share (XW * 7 / 4 batch groups of 16 rows, 14 at 8
-// ranks) is requested at once (CH groups per round), and the seven hidden tiles of a K slice
+// blocks): 1024-thread blocks, wave (c, s) owns column group c (16 + 12 live features) and
+// K split s of fx_kspl = 8 (generic batches: 512 threads, 4 splits); the partial slices are
+// added in split order through LDS
+// (identical order on every rank: bit-identical replicas).  At 8 ranks the global W1 gradient
+// is 8 x the 1-GPU step's MFMA work (K = 800), so it must be spread over the chip and issue
+// all of its loads in ONE round trip: a wave's K share (XW * 7 / 8 batch groups of 16 rows, 7
+// at 8 ranks) is requested at once (CH groups per round), and the seven hidden tiles of a K slice
 // -- which read the same x columns of every rank's batch, the one large fresh read -- run on
 // one XCD (block b on XCD b % 8; speed only), so each XCD's L2 fetches its slices' x once.
 // The first version (14 slices, 98 blocks, 4 load rounds, slices scattered over the XCDs)
 // cost 21.2 us per step at 8 ranks against 7.3 for the 1-GPU step (round-4 local cost).
+// Measured and not kept (round 5): the block's x slab of all ranks staged in LDS with 16-byte
+// loads instead of per-lane 4-byte gathers (first launch + plain head 10.9-11.1 -> 11.8-12.1
+// us at 8 ranks: the staging round trip then sits in front of every MFMA).
 // Small-parameter blocks exchange dW2/db1/db2 partials of step t-1 as in the 3-launch factor
 // engine (waves 0..3 of the block).  The head of step t all-gathers dz1 into dz1A
 // (mlp_head_kernel<.., XW, KS3>).
-// LDSX (DTFX_FACTOR_LDS=1): the block's x slab of every rank's previous batch -- XW * BP rows
-// x 28 features -- is staged into LDS once with 16-byte loads (12-13 per thread), and each
-// wave reads its B operands from there (4 ds_read_b32 per batch group) instead of issuing 4
-// 4-byte global loads per group (56 per lane at 8 ranks).  Rows of 36 floats: the four
-// 16-lane row groups of a read land on disjoint bank quarters.  Padded batch rows hold row
-// B - 1 (finite; dz1A is zero there).
 constexpr int FX_SLOTS = (KS3 + 7) / 8 * HT;  // block slots per XCD (4 slice rows x 7 tiles)
-constexpr int FX_PITCH = 36;                  // LDS row pitch of the staged x slab (floats)
-template <int XW, int NGT, bool LDSX = false>
-__global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
+// phase-A K splits: 8 (1024-thread blocks, 16 waves, 4 per SIMD) for the batch <= 112
+// instantiations; the generic ones keep 4 (512 threads: their small-parameter waves hold
+// 16 batch groups of operands, which 4 waves per SIMD would spill)
+template <int NGT> constexpr int fx_kspl() { return NGT > 0 ? 8 : 4; }
+template <int XW, int NGT>
+__global__ __launch_bounds__(128 * fx_kspl<NGT>()) void mlp_fwdapply_factor_kernel(
     const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
     const float* __restrict__ x_prev, const float* __restrict__ x, long long xstride,
     const float* __restrict__ dz1A, Bufs w, int* __restrict__ ctr, float* __restrict__ stats,
     int stats_ring, int B, int stats_on, MlpXg xg) {
+  constexpr int FX_KSPL = fx_kspl<NGT>();
   const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
   const int NG = NGT > 0 ? NGT : BP / 16;
   const int RT = (B + 15) >> 4;
@@ -1192,9 +1196,9 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
   constexpr int KWX = D / KS3;  // 28 features
   constexpr int LW = KWX + 4;
   __shared__ float Wt[16][LW];
-  __shared__ f32x4 red[2][3][64];
+  __shared__ f32x4 red[2][FX_KSPL - 1][64];
   const int f0 = ks * KWX;
-  const int me = xg.rank;
+  const int me = xgll::uniform(xg.rank);
   // phase B's x rows (wave w < RT owns row tile w; B <= 128): requested first
   float4 xa[2];
   const int rowB = wave * 16 + r;
@@ -1207,12 +1211,12 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
       xa[g] = f4(xr + (k < KWX ? k : 0));
     }
   }
-  // ---- phase A: column group c, K split sp (4 splits) -----------------------------------
+  // ---- phase A: column group c, K split sp (FX_KSPL splits) ------------------------------
   const int c = wave & 1, sp = wave >> 1;
   const int fl = c * 16 + r;
   const bool cv = fl < KWX;
   const int fc = f0 + (cv ? fl : KWX - 1);
-  const int G = XW * NG, per = (G + 3) / 4;
+  const int G = XW * NG, per = (G + FX_KSPL - 1) / FX_KSPL;
   const int g0 = sp * per, g1 = min(G, g0 + per);
   float pw[4];
   if (sp == 0) {
@@ -1223,48 +1227,9 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
     }
   }
   f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-  // one round at 8 ranks x 7 groups (14 per split); more only for batches > 112 rows
-  constexpr int CH = (XW * (NGT > 0 ? NGT : 7) + 3) / 4;
-  if constexpr (LDSX) {
-    constexpr int ROWS = XW * (NGT > 0 ? NGT * 16 : MAXB / 2);  // B <= 128 here
-    __shared__ float xs[ROWS * FX_PITCH];
-    {  // stage: row rr = rank q's batch row b (q = rr / BP), 7 float4 per row
-      const int nrow = XW * BP;
-      for (int i = threadIdx.x; i < nrow * 7; i += 512) {
-        const int rr = i / 7, c4 = i - rr * 7;
-        const int qq = rr / BP, b = rr - qq * BP;
-        const float* src = x_prev + (long long)(qq - me) * xstride + (size_t)(b < B ? b : B - 1) * D +
-                           f0 + 4 * c4;
-        *reinterpret_cast<float4*>(&xs[rr * FX_PITCH + 4 * c4]) = f4(src);
-      }
-    }
-    constexpr int CHL = (XW * (NGT > 0 ? NGT : MAXB / 32) + 3) / 4;  // >= per: one round
-    float4 av[CHL];
-#pragma unroll
-    for (int i = 0; i < CHL; ++i) {
-      const int g = g0 + i;
-      if (g < g1) {
-        const int qq = g / NG, gg = g - qq * NG;
-        const float* a = dz1A + ((size_t)qq * BP + gg * 16 + q * 4) * HP + jt * 16 + r;
-        av[i] = make_float4(a[0], a[HP], a[2 * HP], a[3 * HP]);
-      }
-    }
-    __syncthreads();
-    const int fcl = cv ? fl : KWX - 1;  // the lane's column in the slab
-#pragma unroll
-    for (int i = 0; i < CHL; ++i) {
-      const int g = g0 + i;
-      if (g < g1) {
-        const int qq = g / NG, gg = g - qq * NG;
-        const float* xr = &xs[(qq * BP + gg * 16 + q * 4) * FX_PITCH + fcl];
-        acc0 = mfma16x16x4(av[i].x, xr[0], acc0);
-        acc1 = mfma16x16x4(av[i].y, xr[FX_PITCH], acc1);
-        acc0 = mfma16x16x4(av[i].z, xr[2 * FX_PITCH], acc0);
-        acc1 = mfma16x16x4(av[i].w, xr[3 * FX_PITCH], acc1);
-      }
-    }
-  }
-  for (int c0 = g0; c0 < (LDSX ? g0 : g1); c0 += CH) {
+  // one round at 8 ranks x 7 groups (7 per split); more only for batches > 112 rows
+  constexpr int CH = (XW * (NGT > 0 ? NGT : 7) + FX_KSPL - 1) / FX_KSPL;
+  for (int c0 = g0; c0 < g1; c0 += CH) {
     float4 av[CH];
     float xv[CH][4];
 #pragma unroll
@@ -1300,7 +1265,7 @@ __global__ __launch_bounds__(512) void mlp_fwdapply_factor_kernel(
   __syncthreads();
   if (sp == 0) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {  // split order: the same bits on every rank
+    for (int k = 0; k < FX_KSPL - 1; ++k) {  // split order: the same bits on every rank
       const f32x4 o = red[c][k][lane];
 #pragma unroll
       for (int i = 0; i < 4; ++i) part[i] += o[i];
@@ -1375,7 +1340,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_factor_kernel(
   __shared__ f32x4 red[3][64];
   const int G = XW * NG, per = (G + 3) / 4;
   const int g0 = wave * per, g1 = min(G, g0 + per);
-  const int me = xg.rank;
+  const int me = xgll::uniform(xg.rank);
   float pw[4];
   if (wave == 0) {
 #pragma unroll
@@ -1847,7 +1812,7 @@ void mlp_pipelined_trace_launch(const float* p_old, float* p_new, float lr, cons
 // nslab: the K slabs the first launch wrote -- 0: the single-GPU step's (mlp_single_ks());
 // the fused2 / fused2x first launch writes KS3 = 28, the factor engine's KS2 = 14.
 void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipStream_t stream,
-                      int nslab, const float* x_next) {
+                      int nslab) {
   using namespace mlp;
   check_b(B);
   if (nslab == 0) nslab = mlp_single_ks();
@@ -1855,20 +1820,11 @@ void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipSt
   const Bufs w = make_bufs(ws, B);
   if (nslab == KS3)
     hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS3>), dim3(B), dim3(64), 0, stream, p, p,
-                       0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr, x_next);
+                       0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr);
   else
     hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS2>), dim3(B), dim3(64), 0, stream, p, p,
                        0.f, nullptr, labels, w, B, nullptr, MlpXg{}, nullptr);
   DTFX_HIP_CHECK(hipGetLastError());
-}
-
-// DTFX_MLP_PREFETCH=1: the head of step t touches step t+1's batch (mlp_head_kernel x_next).
-static bool mlp_prefetch_next() {
-  static const bool on = [] {
-    const char* e = std::getenv("DTFX_MLP_PREFETCH");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
 }
 
 // n pipelined single-GPU steps issued from ONE host call (no Python, no hipGraph): step i
@@ -1895,11 +1851,9 @@ void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float 
   const size_t xb = (size_t)B * D;
   const bool rt7 = (B + 15) / 16 == 7;
   const bool ks3 = mlp_single_ks() == KS3;
-  const bool pref = mlp_prefetch_next();
   for (int i = 0; i < n; ++i) {
     const int prev = (pos + nbatches - 1) % nbatches;
     const float* xcur = x + (size_t)pos * xb;
-    const float* xnext = pref && i + 1 < n ? x + (size_t)((pos + 1) % nbatches) * xb : nullptr;
     const float* xprev = pending ? x + (size_t)prev * xb : xcur;
     const float* po = bufs[cur];
     float* pn = bufs[cur ^ 1];
@@ -1916,7 +1870,7 @@ void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float 
                            B, pending, MlpXg{}, nullptr);
       hipLaunchKernelGGL((mlp_head_kernel<false, false, 0, KS3>), dim3(B), dim3(64), 0, stream, pn,
                          pn, 0.f, nullptr, labels + (size_t)pos * B, w, B, nullptr, MlpXg{},
-                         nullptr, xnext);
+                         nullptr);
     } else {
       if (rt7)
         hipLaunchKernelGGL((mlp_fwdapply_kernel<7>), dim3(HT * KS2 + HT), dim3(256), 0, stream, po,
@@ -1952,22 +1906,12 @@ void mlp_fwdapply_factor_launch(const float* p_old, float* p_new, float lr, cons
     throw std::runtime_error("mlp_fwdapply_factor: needs ping-pong buffers, batches, ctr, dz1A");
   if (xg.S < NPARAM) throw std::runtime_error("mlp_fwdapply_factor: exchange slots too small");
   const Bufs w = make_bufs(ws, B);
-  dim3 grid(8 * FX_SLOTS + HT), block(512);
-  static const bool ldsx = [] {
-    const char* e = std::getenv("DTFX_FACTOR_LDS");
-    return e && std::atoi(e) != 0;
-  }();
+  dim3 grid(8 * FX_SLOTS + HT);
 #define DTFX_FF(WW, NGT)                                                                       \
-  do {                                                                                         \
-    if (ldsx)                                                                                  \
-      hipLaunchKernelGGL((mlp_fwdapply_factor_kernel<WW, NGT, true>), grid, block, 0, stream,  \
-                         p_old, p_new, lr, x_prev, x, xstride, dz1A, w, ctr, stats, stats_ring, \
-                         B, stats_on, xg);                                                     \
-    else                                                                                       \
-      hipLaunchKernelGGL((mlp_fwdapply_factor_kernel<WW, NGT>), grid, block, 0, stream, p_old, \
-                         p_new, lr, x_prev, x, xstride, dz1A, w, ctr, stats, stats_ring, B,    \
-                         stats_on, xg);                                                        \
-  } while (0)
+  hipLaunchKernelGGL((mlp_fwdapply_factor_kernel<WW, NGT>), grid, dim3(128 * fx_kspl<NGT>()), 0, \
+                     stream, p_old,                                                            \
+                     p_new, lr, x_prev, x, xstride, dz1A, w, ctr, stats, stats_ring, B,        \
+                     stats_on, xg)
 #define DTFX_FFW(WW)                                 \
   case WW:                                           \
     if ((B + 15) / 16 == 7) DTFX_FF(WW, 7);          \

@@ -81,6 +81,6 @@ void mlp_wgrad_xg_launch(float* p, float lr, const float* x, float* ws, int* ctr
                          int stats_ring, int B, hipStream_t stream, const MlpXg& xg, int world);
 // plain head of the pipelined step (mlp_step.hip); nslab = 28 after the fused engines' launch
 void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipStream_t stream,
-                      int nslab, const float* x_next = nullptr);
+                      int nslab);
 
 }  // namespace dtfx

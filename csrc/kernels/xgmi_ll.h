@@ -24,6 +24,29 @@ __device__ __forceinline__ u64 load(const u64* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A 16-byte LL word pair {v0, epoch, v1, epoch} read as TWO relaxed system-scope 8-byte loads
+// (each half carries its own epoch).  Not a `volatile` 16-byte load: LLVM completes every
+// volatile access before the next one (an `s_waitcnt vmcnt(0)` after each, and a FLAT load
+// here), which turned a wave's W - 1 polls into W - 1 serial memory round trips.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 load_pair(const u64* p) {
+  const u64 a = load(p), b = load(p + 1);
+  return u32x4{(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+}
+
+// A wave-uniform value made provably uniform (scalar registers): the peer pointer table and
+// the rank come from a kernel-argument struct passed by reference into device helpers, where
+// the compiler otherwise may index it with a vector register (a per-lane load of the pointer
+// and an s_waitcnt vmcnt(0) before every peer access).
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const u64 v = (u64)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (T*)(((u64)hi << 32) | lo);
+}
+
 // Loads word i of every peer j != rank from base(j) and re-polls the stale ones; returns
 // the rank-ordered sum with `own` at position `rank` (identical on every rank), or sets
 // fail after `ticks` of s_memrealtime (100 MHz).

@@ -68,3 +68,105 @@ def apply_hip_schedule(mode=None):
     if rc != 0:
         raise RuntimeError("hipSetDeviceFlags(%s) failed: %d" % (mode, rc))
     return _HIP_SCHED[mode]
+
+
+# ---------------------------------------------------------------------------------------------
+# NUMA placement of the async-PS cluster's host processes (--cpu_affinity numa).  Measured
+# (tools/probes/ps_capacity.py, 2-socket box, profiles/r5/ps/): the ps alone served 8 clients
+# at 5.9K round trips/s with its threads free to roam both sockets and 59K pinned to one node.
+
+
+def numa_nodes():
+    """{node: [cpu, ...]} from sysfs ({} where it says nothing)."""
+    out = {}
+    base = "/sys/devices/system/node"
+    try:
+        names = os.listdir(base)
+    except OSError:
+        return out
+    for d in names:
+        if not (d.startswith("node") and d[4:].isdigit()):
+            continue
+        try:
+            cl = open(os.path.join(base, d, "cpulist")).read().strip()
+        except OSError:
+            continue
+        cpus = []
+        for part in cl.split(","):
+            if not part:
+                continue
+            lo, _, hi = part.partition("-")
+            cpus.extend(range(int(lo), int(hi or lo) + 1))
+        out[int(d[4:])] = cpus
+    return out
+
+
+def _pci_numa_node(domain, bus, dev, fn=0):
+    try:
+        n = int(open("/sys/bus/pci/devices/%04x:%02x:%02x.%x/numa_node"
+                     % (domain, bus, dev, fn)).read())
+        return n if n >= 0 else None
+    except (OSError, ValueError):
+        return None
+
+
+def gpu_numa_node(device_index=0):
+    """NUMA node of a visible GPU (the worker process, which uses the GPU anyway)."""
+    try:
+        import torch
+
+        p = torch.cuda.get_device_properties(device_index)
+        return _pci_numa_node(p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+    except Exception:  # noqa: BLE001 - best effort
+        return None
+
+
+def first_gpu_numa_node_sysfs():
+    """Node of the first GPU in the KFD topology, without touching the GPU (the ps process)."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = sorted(os.listdir(base), key=lambda v: int(v) if v.isdigit() else 1 << 30)
+    except OSError:
+        return None
+    for n in nodes:
+        try:
+            props = dict(l.split() for l in open(os.path.join(base, n, "properties"))
+                         if len(l.split()) == 2)
+        except (OSError, ValueError):
+            continue
+        if int(props.get("simd_count", "0")) <= 0:
+            continue
+        loc, dom = int(props.get("location_id", "0")), int(props.get("domain", "0"))
+        return _pci_numa_node(dom, loc >> 8, (loc >> 3) & 31, loc & 7)
+    return None
+
+
+def pin_to_numa_node(node, count=0, offset=0):
+    """Restrict this process (and the threads it starts) to allowed CPUs of ``node``: all of
+    them (``count`` 0), or ``count`` of them from position ``offset`` of the node's sorted list
+    (physical cores first; wraps).  Returns the CPU list, or None (unknown node / nothing
+    allowed there: left as it was)."""
+    if node is None:
+        return None
+    allowed = os.sched_getaffinity(0)
+    cpus = [c for c in sorted(numa_nodes().get(int(node), [])) if c in allowed]
+    if not cpus:
+        return None
+    if count > 0:
+        cpus = [cpus[(offset + k) % len(cpus)] for k in range(min(count, len(cpus)))]
+    os.sched_setaffinity(0, cpus)
+    return cpus
+
+
+# --cpu_affinity numa layout: ps task t on 8 consecutive cores (one shared-L3 core complex on
+# the EPYC hosts of this pool), worker i on 2 cores after the ps tasks' -- the cluster's
+# processes packed on one socket instead of spread by the scheduler over 256 CPUs
+PS_CPUS, WORKER_CPUS = 8, 2
+
+
+def ps_cpu_slot(task_index):
+    return PS_CPUS, PS_CPUS * int(task_index)
+
+
+def worker_cpu_slot(task_index, num_ps):
+    return WORKER_CPUS, PS_CPUS * int(num_ps) + WORKER_CPUS * int(task_index)

@@ -127,14 +127,7 @@ def step_direct(p, x, labels, ws: StepWorkspace, lr, stats=True):
                 ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B, s)
 
 
-# DTFX_MLP_PREFETCH=1: the head of step t touches step t+1's batch rows so they sit in the
-# memory-side cache when step t+1's forward reads them (mlp_head_kernel x_next; the C++ host
-# loop reads the same variable)
-PREFETCH_NEXT = os.environ.get("DTFX_MLP_PREFETCH", "0") not in ("", "0")
-
-
-def step_pipelined(p_old, p_new, x_prev, x, labels, ws: StepWorkspace, lr, apply, stats=True,
-                   x_next=None):
+def step_pipelined(p_old, p_new, x_prev, x, labels, ws: StepWorkspace, lr, apply, stats=True):
     """Two-launch single-GPU step: ``mlp_fwdapply`` applies the PREVIOUS step's SGD update
     (from the factors dz1/h/dlogits the last head left in ``ws`` and the previous batch
     ``x_prev``; W1 never materialises a gradient) reading ``p_old`` and writing ``p_new``,
@@ -150,8 +143,7 @@ def step_pipelined(p_old, p_new, x_prev, x, labels, ws: StepWorkspace, lr, apply
     h.mlp_fwdapply(ptr(p_old), ptr(p_new), float(lr) if apply else 0.0,
                    ptr(x_prev if apply else x), ptr(x), ptr(ws.buf), ptr(ws.ctr),
                    ptr(ws.stats) if stats else 0, ws.stats_ring, ws.B, 1 if apply else 0, s)
-    h.mlp_head2(ptr(p_new), ptr(labels), ptr(ws.buf), ws.B, s, 0,
-                ptr(x_next) if x_next is not None else 0)
+    h.mlp_head2(ptr(p_new), ptr(labels), ptr(ws.buf), ws.B, s)
 
 
 def flush_pipelined(p_old, p_new, x_prev, ws: StepWorkspace, lr, stats=True):

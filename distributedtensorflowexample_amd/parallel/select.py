@@ -332,7 +332,7 @@ class HybridComm:
 
 
 def pick_large_allreduce(rccl, world, rank, dev, max_numel, sizes=None, iters=10,
-                         xgmi_key="dtfx/xgmi/bw", timeout_s=2.0, bw_blocks=None,
+                         xgmi_key="dtfx/xgmi/bw", timeout_s=2.0, bw_blocks=128,
                          train_timeout_s=None, peer_timeout_s=60.0):
     """Bucketed all-reduce backend for the large gradients (BERT / ResNet buckets): the xGMI
     bandwidth-mode two-shot is created on every rank (or not at all), verified against RCCL
@@ -346,6 +346,11 @@ def pick_large_allreduce(rccl, world, rank, dev, max_numel, sizes=None, iters=10
     checkpoint, first-step graph capture -- must not time its peers out: a timed-out
     two-shot leaves the bucket partly reduced, where RCCL would simply have blocked).
     Trainers still poll ``failed()`` collectively (``check_comm_collective``).
+
+    ``bw_blocks`` (default 128 of the kernel's 256 workgroups): the two-shot runs BESIDE the
+    backward on the comm stream, and fewer workgroups take fewer CUs from it -- the simulated
+    world-8 step (tools/probes/dp_sim.py, profiles/r5/dp_sim/) ran BERT-base +7.4 % over the
+    1-GPU step with 128 against +8.5 % with 256 (+8.0 % with 64), ResNet-50 +5.7 % against +6.5 %.
 
     Default ``train_timeout_s``: ``min(120, peer_timeout_s)``.  The peer watchdog
     (``--peer_timeout_secs``) declares a silent peer lost after ``peer_timeout_s``, drains for

@@ -214,9 +214,8 @@ class FusedMLPTrainer:
             return
         if self.pipelined:
             xp, _ = self.batch((self.pos - 2) % self.nbatches)  # pos already advanced
-            xn = self.batch(self.pos)[0] if mlp_step.PREFETCH_NEXT else None
             mlp_step.step_pipelined(self.bufs[self.cur], self.bufs[self.cur ^ 1], xp, xb, yb,
-                                    self.ws, self.lr, apply=self.pending, x_next=xn)
+                                    self.ws, self.lr, apply=self.pending)
             self.cur ^= 1
             self.pending = True
             return

@@ -76,6 +76,12 @@ def main(argv=None):
     gpu_options = GPUOptions(per_process_gpu_memory_fraction=fraction)
 
     if FLAGS.job_name == "ps":
+        if getattr(FLAGS, "cpu_affinity", "none") == "numa":
+            from distributedtensorflowexample_amd.config import (first_gpu_numa_node_sysfs,
+                                                                 pin_to_numa_node, ps_cpu_slot)
+
+            node = FLAGS.numa_node if FLAGS.numa_node >= 0 else first_gpu_numa_node_sysfs()
+            pin_to_numa_node(0 if node is None else node, *ps_cpu_slot(FLAGS.task_index))
         # Quirk decided: the ps does not load MNIST; it serves
         # until a client asks it to shut down (or it is signalled).
         server = Server(cluster, job_name="ps", task_index=FLAGS.task_index)
@@ -85,6 +91,15 @@ def main(argv=None):
         from distributedtensorflowexample_amd.train.worker import Worker
 
         apply_hip_schedule()  # DTFX_HIP_SCHED (before the first GPU call)
+        if getattr(FLAGS, "cpu_affinity", "none") == "numa":
+            from distributedtensorflowexample_amd.config import (first_gpu_numa_node_sysfs,
+                                                                 pin_to_numa_node,
+                                                                 worker_cpu_slot)
+
+            # the ps tasks' node (the same rule), so the workers' cores follow the ps tasks'
+            node = FLAGS.numa_node if FLAGS.numa_node >= 0 else first_gpu_numa_node_sysfs()
+            pin_to_numa_node(0 if node is None else node,
+                             *worker_cpu_slot(FLAGS.task_index, FLAGS.num_ps))
         mnist = read_data_sets(FLAGS.data_dir or None, one_hot=True)
         config = ConfigProto(gpu_options=gpu_options)
         server = Server(cluster, job_name="worker", task_index=FLAGS.task_index, config=config)

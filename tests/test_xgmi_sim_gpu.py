@@ -303,8 +303,8 @@ def test_fused2_fwdapply_exchange_simulated_peers(gpu, world, rank, B):
     bufs = [p_old, torch.empty_like(p_old)]
     batches = [(x_prev, y_prev), (x, y)]
     _pipelined_fwd_head(p_old, x_prev, y_prev, ws)
-    # W1 travels in the 16-byte pair layout (xg_exchange16): every pair word of the region is
-    # written by every peer (padding lanes too), so stage the whole region, then the real ones
+    # W1 travels in the 16-byte pair layout (xg_exchange16); pairs of padding columns / hidden
+    # rows do not travel: stage the whole region anyway (a superset), then the real words
     w1map = mlp_step.xg_w1_pair_offsets().to(gpu)
     n1, S = mlp_step.OFF_B1, comm.slot_stride
     reg_lo, reg_hi = mlp_step.XG_W1_BASE, mlp_step.XG_SLOT_WORDS
@@ -331,8 +331,12 @@ def test_fused2_fwdapply_exchange_simulated_peers(gpu, world, rank, B):
         err = float((pn.double().cpu() - exp).abs().max())
         assert err <= 2e-5, (epoch, err)
         _check_pushed(comm, regs, own, epoch, n1, mlp_step.NPARAM, 2e-6)
+        dead = torch.ones(reg_hi - reg_lo, dtype=torch.bool)
+        dead[w1map.cpu() - reg_lo] = False
         for j in range(world):  # my W1 words reached every peer, in the pair layout
             if j != rank:
+                pad = regs[j][(par * world + rank) * S + reg_lo:(par * world + rank) * S + reg_hi]
+                assert bool((_epochs(pad.cpu()[dead]) == 0).all())  # padding pairs never sent
                 w = regs[j][(par * world + rank) * S + w1map].cpu()
                 assert bool((_epochs(w) == epoch).all()), ("epoch", j, epoch)
                 assert float((_vals(w).double() - own[:n1]).abs().max()) <= 2e-6
@@ -624,7 +628,8 @@ def test_fused2_two_shot_exchange_simulated_peers(gpu, world, rank):
     owner = _pair_owner(w1map, world)
     mine = owner == rank
     reg = torch.arange(mlp_step.XG_W1_BASE, mlp_step.XG_SLOT_WORDS)
-    reg_mine = _pair_owner(reg, world) == rank
+    dead = torch.ones(reg.numel(), dtype=torch.bool)
+    dead[w1map - mlp_step.XG_W1_BASE] = False  # words of no W1 element (padding pairs)
     w1g, mg = w1map.to(gpu), mine.to(gpu)
     lr = 0.5
     bufs = [p_old, torch.empty_like(p_old)]
@@ -675,9 +680,11 @@ def test_fused2_two_shot_exchange_simulated_peers(gpu, world, rank):
             assert bool((_epochs(rv[mine]) == epoch).all()), ("result epoch", d)
             got = _vals(rv[mine]).double()
             assert float((got - tot[:n1][mine]).abs().max()) <= 2e-5
-            # padding words of my owned pairs were broadcast too (every owner lane pushes)
+            # pairs of padding columns / hidden rows never travel (neither pushed nor broadcast)
             rr = regs[d][res + reg].cpu()
-            assert bool((_epochs(rr[reg_mine]) == epoch).all()), ("result padding", d)
+            cc = regs[d][o + reg].cpu()
+            assert bool((_epochs(rr[dead]) == 0).all()), ("result padding", d)
+            assert bool((_epochs(cc[dead]) == 0).all()), ("contribution padding", d)
         _check_pushed(comm, regs, own, epoch, n1, mlp_step.NPARAM, 2e-6)
         cur ^= 1
     comm.destroy()

@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--rpc", choices=["fused", "separate"], default="fused",
                     help="fused: push + step + next pull in one pipelined round trip per ps "
                          "task; separate: the reference's three round trips per step")
+    ap.add_argument("--cpu_affinity", choices=["numa", "none"], default="numa",
+                    help="numa: every cluster process on one NUMA node's CPUs (main.py flag)")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp(prefix="psbench")
     rc = launch_ps(a.num_workers, a.num_gpus, None, 1, cpu=a.cpu, base_port=a.base_port,
@@ -45,7 +47,8 @@ def main():
                           "--eval_every", str(10 ** 9), "--logdir", os.path.join(tmp, "m"),
                           "--save_model_secs", "1e9", "--save_summaries_secs", "1e9",
                           "--batch_size", str(a.batch_size), "--ps_device", a.ps_device,
-                          "--ps_fused_rpc=%s" % ("true" if a.rpc == "fused" else "false")])
+                          "--ps_fused_rpc=%s" % ("true" if a.rpc == "fused" else "false"),
+                          "--cpu_affinity", a.cpu_affinity])
     speeds = []
     for p in glob.glob(os.path.join(tmp, "logs", "worker*.log")):
         for m in re.finditer(r"step: (\d+)\t\| cost: [^|]+\| speed: ([0-9.eE+-]+)step/sec",
@@ -60,7 +63,7 @@ def main():
                       "value": round(sps * a.batch_size, 1), "unit": "samples/sec",
                       "global_steps_per_sec": round(sps, 1), "num_workers": a.num_workers,
                       "num_gpus": a.num_gpus, "device": "cpu" if a.cpu else "MI355X",
-                      "ps_device": a.ps_device, "rpc": a.rpc,
+                      "ps_device": a.ps_device, "rpc": a.rpc, "cpu_affinity": a.cpu_affinity,
                       "steps": a.steps, "rc": rc, "n_speed_samples": len(speeds)}))
     return 0
 

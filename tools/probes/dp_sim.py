@@ -7,9 +7,10 @@ every world > 1 default of the trainer (BERT: weight gradients on a side stream,
 fold).  Against the 1-GPU step, each switch A/B'd in the same process, interleaved rounds:
 
   1gpu          comm None (the bench's step)
-  dp            world W, trainer defaults, bw kernel on all 256 workgroups
+  dp            world W, trainer defaults, the bw kernel on 128 workgroups (pick_large_allreduce's
+                default since round 5)
   dp_null       world W, all-reduce a no-op (the DP-mode trainer changes alone)
-  dp_bw128 / 64 the bw kernel on 128 / 64 workgroups (fewer CUs taken from the backward)
+  dp_bw256 / 64 the bw kernel on all 256 / on 64 workgroups
   dp_prio_hi    the comm stream at the highest HIP stream priority (default: the lowest,
                 the compute stream's)
   BERT: dp_nows (no weight-gradient stream), 1gpu_nofold (the 1-GPU step without the fold)
@@ -64,7 +65,7 @@ def make(model, variant, world, dev, a):
             if variant == "dp_null":
                 comm = NullComm(world)
             else:
-                blocks = {"dp_bw128": 128, "dp_bw64": 64}.get(variant)
+                blocks = {"dp_bw256": 256, "dp_bw64": 64}.get(variant, 128)
                 comm = SimulatedPeersComm(world, (24 << 20) if model == "bert" else (8 << 20),
                                           device=dev, bw_blocks=blocks)
         if model == "bert":
@@ -97,10 +98,10 @@ def main():
     if a.variants:
         variants = a.variants.split(",")
     elif a.model == "bert":
-        variants = ["1gpu", "dp", "dp_null", "dp_nows", "dp_bw128", "dp_bw64", "dp_prio_hi",
+        variants = ["1gpu", "dp", "dp_null", "dp_nows", "dp_bw256", "dp_bw64", "dp_prio_hi",
                     "1gpu_nofold"]
     else:
-        variants = ["1gpu", "dp", "dp_null", "dp_bw128", "dp_bw64", "dp_prio_hi", "dp_ws"]
+        variants = ["1gpu", "dp", "dp_null", "dp_bw256", "dp_bw64", "dp_prio_hi", "dp_ws"]
     trainers = {}
     for v in variants:
         tr = make(a.model, v, a.world, dev, a)
