@@ -2,6 +2,10 @@
 
     python tools/kernel_stats_diff.py A.csv STEPS_A B.csv STEPS_B [top]
 
+STEPS may be a number or ``k=<substring>``: the call count of the (first) kernel whose name
+contains the substring -- one that runs exactly once per step, so warm-up and capture steps
+are counted the same way in both runs.
+
 Prints us/step of every kernel in A and B and B - A, sorted by |B - A|, then the totals --
 e.g. the 1-GPU BERT step against its simulated world-8 data-parallel shape
 (tools/probes/dp_sim.py): which kernels the DP mode adds (the all-reduce) and which of the
@@ -12,13 +16,18 @@ import sys
 
 def load(path, steps):
     out = {}
-    for r in csv.DictReader(open(path)):
+    rows = list(csv.DictReader(open(path)))
+    if steps.startswith("k="):
+        steps = next(float(r["Calls"]) for r in rows if steps[2:] in r["Name"])
+        print("%s: %d steps" % (path, steps))
+    steps = float(steps)
+    for r in rows:
         out[r["Name"]] = out.get(r["Name"], 0.0) + float(r["TotalDurationNs"]) / 1e3 / steps
     return out
 
 
 def main():
-    a, sa, b, sb = sys.argv[1], float(sys.argv[2]), sys.argv[3], float(sys.argv[4])
+    a, sa, b, sb = sys.argv[1:5]
     top = int(sys.argv[5]) if len(sys.argv) > 5 else 25
     A, B = load(a, sa), load(b, sb)
     names = sorted(set(A) | set(B), key=lambda n: -abs(B.get(n, 0.0) - A.get(n, 0.0)))
