@@ -1187,8 +1187,24 @@ __global__ __launch_bounds__(256) void adam_mixed_segs_kernel(
       const f32x4* w = s_w[k] + (i - s_lo[k]);
       const long long pl = s_pl[k];
       const int S = s_S[k];
+      // the planes four at a time, loads first (a plain loop waited out one round trip per
+      // plane: 14 for the attention-output weights), added in split order
       gv = w[0];
-      for (int q = 1; q < S; ++q) gv += w[q * pl];
+      int q = 1;
+      for (; q + 3 < S; q += 4) {
+        const f32x4 a0 = w[q * pl], a1 = w[(q + 1) * pl], a2 = w[(q + 2) * pl], a3 = w[(q + 3) * pl];
+        gv += a0;
+        gv += a1;
+        gv += a2;
+        gv += a3;
+      }
+      if (q + 1 < S) {
+        const f32x4 a0 = w[q * pl], a1 = w[(q + 1) * pl];
+        gv += a0;
+        gv += a1;
+        q += 2;
+      }
+      if (q < S) gv += w[q * pl];
     } else {
       gv = ((const f32x4*)g)[i];
     }
