@@ -16,8 +16,13 @@ timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -1 "$OUT/pytest_gpu.log"
 step mlp
 timeout -k 10 120 python bench.py --steps 20 --warmup 5 > "$OUT/bench_mlp_k20.json" 2>&1 || exit 1
+timeout -k 10 120 python bench.py --steps 20 --warmup 5 > "$OUT/bench_mlp_k20_2.json" 2>&1 || exit 1
+timeout -k 10 120 python bench.py --steps 20 --warmup 5 > "$OUT/bench_mlp_k20_3.json" 2>&1 || exit 1
 timeout -k 10 200 python bench.py > "$OUT/bench_mlp.json" 2>&1 || exit 1
 tail -1 "$OUT/bench_mlp_k20.json" | cut -c 1-160; tail -1 "$OUT/bench_mlp.json" | cut -c 1-160
+step rehearsal
+DTFX_SHARED_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29655 bench.py --gpus 4 --steps 200 --warmup 20 > "$OUT/rehearsal_w4.log" 2>&1 || { tail -20 "$OUT/rehearsal_w4.log"; exit 1; }
+grep -h '^{' "$OUT/rehearsal_w4.log" | cut -c 1-160
 step bert
 timeout -k 10 200 python bench.py --model bert > "$OUT/bench_bert.json" 2>&1 || exit 1
 timeout -k 10 200 python bench.py --model bert --bert_batch 32 --seq_len 512 > "$OUT/bench_bert512.json" 2>&1 || exit 1
@@ -36,7 +41,8 @@ timeout -k 10 200 python tools/probes/engine_local_cost.py > "$OUT/engine_local_
 timeout -k 10 200 python tools/bench_ps_async.py --num_workers 2 --steps 40000 > "$OUT/ps_async_w2.json" 2>/dev/null || exit 1
 timeout -k 10 200 python tools/bench_ps_async.py --num_workers 8 --steps 40000 > "$OUT/ps_async_w8.json" 2>/dev/null || exit 1
 timeout -k 10 200 python tools/bench_ps_async.py --num_workers 2 --steps 40000 --ps_device gpu > "$OUT/ps_async_gpu_w2.json" 2>/dev/null || exit 1
-cut -c 1-160 "$OUT/ps_async_w2.json" "$OUT/ps_async_gpu_w2.json"
+timeout -k 10 200 python tools/bench_ps_async.py --num_workers 8 --steps 40000 --ps_device gpu > "$OUT/ps_async_gpu_w8.json" 2>/dev/null || exit 1
+cut -c 1-160 "$OUT/ps_async_w2.json" "$OUT/ps_async_w8.json" "$OUT/ps_async_gpu_w2.json" "$OUT/ps_async_gpu_w8.json"
 step prof
 cd /tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/mprof" -o run -- python "$R/bench.py" --steps 2000 --warmup 200 > "$OUT/mprof.log" 2>&1 || exit 1
