@@ -122,8 +122,10 @@ def gpu_numa_node(device_index=0):
 
 
 def first_gpu_numa_node_sysfs(base="/sys/class/kfd/kfd/topology/nodes",
-                              pci="/sys/bus/pci/devices"):
-    """Node of the first GPU in the KFD topology, without touching the GPU (the ps process)."""
+                              pci="/sys/bus/pci/devices", index=0):
+    """Node of the ``index``-th GPU of the KFD topology (the physical device numbering that
+    ``HIP_VISIBLE_DEVICES`` selects from), without touching the GPU: the ps process, and a
+    worker before its first GPU call (so the runtime's threads inherit the placement)."""
     try:
         nodes = sorted(os.listdir(base), key=lambda v: int(v) if v.isdigit() else 1 << 30)
     except OSError:
@@ -136,9 +138,24 @@ def first_gpu_numa_node_sysfs(base="/sys/class/kfd/kfd/topology/nodes",
             continue
         if int(props.get("simd_count", "0")) <= 0:
             continue
+        if index > 0:
+            index -= 1
+            continue
         loc, dom = int(props.get("location_id", "0")), int(props.get("domain", "0"))
         return _pci_numa_node(dom, loc >> 8, (loc >> 3) & 31, loc & 7, pci=pci)
     return None
+
+
+def visible_gpu_index(env=None):
+    """Physical index of the first GPU this process is given (``HIP_VISIBLE_DEVICES`` /
+    ``CUDA_VISIBLE_DEVICES``, as the launcher sets them per worker), 0 when unset or not a
+    plain index (UUIDs, empty)."""
+    env = os.environ if env is None else env
+    for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(k, "").split(",")[0].strip()
+        if v.isdigit():
+            return int(v)
+    return 0
 
 
 def pin_to_numa_node(node, count=0, offset=0):

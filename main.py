@@ -96,8 +96,11 @@ def main(argv=None):
                                                                  pin_to_numa_node,
                                                                  worker_cpu_slot)
 
-            # the ps tasks' node (the same rule), so the workers' cores follow the ps tasks'
-            node = FLAGS.numa_node if FLAGS.numa_node >= 0 else first_gpu_numa_node_sysfs()
+            from distributedtensorflowexample_amd.config import visible_gpu_index
+
+            # the node of this worker's GPU (the launcher's HIP_VISIBLE_DEVICES)
+            node = (FLAGS.numa_node if FLAGS.numa_node >= 0
+                    else first_gpu_numa_node_sysfs(index=visible_gpu_index()))
             pin_to_numa_node(0 if node is None else node,
                              *worker_cpu_slot(FLAGS.task_index, FLAGS.num_ps))
         mnist = read_data_sets(FLAGS.data_dir or None, one_hot=True)

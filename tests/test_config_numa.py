@@ -29,9 +29,23 @@ def test_first_gpu_numa_node_from_kfd_topology(tmp_path):
     _write(str(topo / "1" / "properties"), "simd_count 1024\nlocation_id %d\ndomain 0\n" % loc)
     _write(str(pci / "0000:75:00.0" / "numa_node"), "1\n")
     assert config.first_gpu_numa_node_sysfs(str(topo), str(pci)) == 1
+    # a second GPU (node 2 of the topology) on the other socket: index 1
+    loc2 = (0xf5 << 8)
+    _write(str(topo / "2" / "properties"), "simd_count 1024\nlocation_id %d\ndomain 0\n" % loc2)
+    _write(str(pci / "0000:f5:00.0" / "numa_node"), "0\n")
+    assert config.first_gpu_numa_node_sysfs(str(topo), str(pci), index=1) == 0
+    assert config.first_gpu_numa_node_sysfs(str(topo), str(pci), index=2) is None
     _write(str(pci / "0000:75:00.0" / "numa_node"), "-1\n")  # firmware says nothing
     assert config.first_gpu_numa_node_sysfs(str(topo), str(pci)) is None
     assert config.first_gpu_numa_node_sysfs(str(tmp_path / "none"), str(pci)) is None
+
+
+def test_visible_gpu_index():
+    assert config.visible_gpu_index({}) == 0
+    assert config.visible_gpu_index({"HIP_VISIBLE_DEVICES": "3"}) == 3
+    assert config.visible_gpu_index({"HIP_VISIBLE_DEVICES": "5,6"}) == 5
+    assert config.visible_gpu_index({"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": "2"}) == 2
+    assert config.visible_gpu_index({"HIP_VISIBLE_DEVICES": "GPU-1234abcd"}) == 0
 
 
 def test_cpu_slots_do_not_overlap():
