@@ -515,27 +515,6 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
         }
     }
   };
-  // PIPE (plain GEMMs on the 8-phase tile with ONE side input, aux_in or residual): the side
-  // input of slab h + 1 is requested while slab h is transposed and stored, so the epilogue
-  // waits for one memory round trip instead of one per slab (4 per tile; the BERT FFN2 data
-  // gradient's GELU' read of the pre-activation and the residual adds of the N = 768
-  // products).  Both side inputs: the per-slab loads below.
-  constexpr bool PIPE = PREF && NBUF == 8 && MODE == 0;
-  const bool pipe = PIPE && !e.no_pipe && ((e.act_grad != 0) != (e.residual != nullptr));
-  const unsigned short* side = e.act_grad ? e.aux_in : e.residual;
-  const int ld_side = e.act_grad ? e.ld_aux : e.ld_res;
-  bf16x8 pcur[4], pnxt[4];
-  auto side_issue = [&](int h, bf16x8 (&dst)[4]) {
-    const int r0 = slab_r0(h), c0 = slab_c0(h);
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int rr = it * 8 + (lane >> 3), cg = (lane & 7) * 8;
-      const int m = m0 + r0 + rr, n = n0 + c0 + cg;
-      const bool f = m < M && n + 8 <= N && cg < SLW;
-      dst[it] = *(const bf16x8*)&side[(size_t)(f ? m : 0) * ld_side + (f ? n : 0)];
-    }
-  };
-  if (pipe) side_issue(0, pcur);
   // (unrolled for the late prefetch: a slab's accumulators are then known dead once they are in
   // LDS, and its side inputs take their registers)
 #pragma unroll LATE ? 4 : 1
@@ -564,16 +543,12 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
         fdivmod(rem, cd.Wc, 1.f / cd.Wc, i, j);
         pm[it] = (nimg * cd.H + i * cd.stride + cd.ph) * cd.W + j * cd.stride + cd.pw;
       }
-      if (pipe) {
-        a8[it] = pcur[it];
-        r8[it] = pcur[it];
-      } else if (PREF) {
+      if (PREF) {
         if (e.act_grad) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)pm[it] * e.ld_aux + ns];
         if (e.residual) r8[it] = *(const bf16x8*)&e.residual[(size_t)pm[it] * e.ld_res + ns];
         if (MODE == 2 && e.bn_x) x8[it] = *(const bf16x8*)&e.bn_x[(size_t)pm[it] * ldc + ns];
       }
     }
-    if (pipe && h + 1 < WM / 32) side_issue(h + 1, pnxt);
     // static accumulator indices only (a runtime acc[2h+ii] index would put acc in scratch)
 #pragma unroll
     for (int t = 0; t < TM; ++t)
@@ -773,10 +748,6 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
         }
 #pragma unroll
       for (int u = 0; u < 8; ++u) cs[u] = cq[u] = 0.f;
-    }
-    if (pipe) {
-#pragma unroll
-      for (int it = 0; it < 4; ++it) pcur[it] = pnxt[it];
     }
   }
   if constexpr (NBUF == 8) {
@@ -1245,11 +1216,6 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   }
   GemmEpi e{alpha, beta, bias, act, (const unsigned short*)aux_in, (unsigned short*)aux_out,
             ld_aux, (const unsigned short*)residual, ld_res, act_grad, colsum, nullptr, 0};
-  static const int no_pipe = [] {
-    const char* v = getenv("DTFX_GEMM_EPI_PIPE");
-    return v && atoi(v) == 0 ? 1 : 0;
-  }();
-  e.no_pipe = no_pipe;
   const bool use_ws = splitk > 1 && splitk_ws_ok(ws, ws_floats, splitk, M, N, C, ldc);
   if (use_ws) e.ws = ws;
   // defer_reduce: the caller consumes the split planes itself (the BERT optimizer sums them,

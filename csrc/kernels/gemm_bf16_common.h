@@ -343,6 +343,5 @@ struct GemmEpi {
   // splitk_reduce folds them into C afterwards (f32 atomics run at the memory side, ~1.3 TB/s
   // chip-wide: a 512-block split-K wave adds ~34 MB, ~26 us, against ~6 us of plain stores)
   float* ws;
-  int no_pipe;  // 1: the epilogue's side inputs per slab, not pipelined (DTFX_GEMM_EPI_PIPE=0)
 };
 }  // namespace dtfx
