@@ -197,8 +197,10 @@ class SimulatedPeersComm:
     pre-raised (``XgmiComm.with_local_peers``).  So a trainer driven with it runs its world > 1
     path exactly (comm stream, bucket hooks, no split-K fold, side-stream defaults, 1/W
     scaling) and its comm kernels compete with the backward for CUs and HBM as on a node --
-    minus the link time, which this cannot show.  The peers' slots hold zeros, so the
-    "global" gradient is this rank's own (the numerics stay those of one rank).
+    minus the link time, which this cannot show.  The simulated peers never write: their
+    contributions and their reduced chunks read as zeros, so the result keeps only this rank's
+    own chunk (chunk 0 of W, unscaled) and zeros elsewhere -- a timing harness, not a
+    training one (``tests/test_xgmi_sim_gpu.py::test_simulated_peers_comm_shape``).
 
     Buckets above ``max_numel`` elements are reduced in ``max_numel`` pieces."""
 

@@ -688,3 +688,26 @@ def test_fused2_two_shot_exchange_simulated_peers(gpu, world, rank):
         _check_pushed(comm, regs, own, epoch, n1, mlp_step.NPARAM, 2e-6)
         cur ^= 1
     comm.destroy()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_simulated_peers_comm_shape(gpu, world):
+    """parallel.xgmi.SimulatedPeersComm (tools/probes/dp_sim.py): the real bandwidth-mode
+    two-shot of rank 0 over never-writing simulated peers -- its own chunk comes back as the
+    rank-ordered sum (own + zeros), every other chunk as zeros; buckets above max_numel go in
+    pieces; the flags were pre-raised, so nothing waits or fails."""
+    from distributedtensorflowexample_amd.parallel.xgmi import SimulatedPeersComm
+
+    n, cap = 10_000, 4_096
+    c = SimulatedPeersComm(world, cap, device=gpu)
+    g = torch.randn(n, device=gpu)
+    ref = g.clone()
+    c.allreduce_sum_(g)
+    torch.cuda.synchronize()
+    assert not c.failed()
+    for lo in range(0, n, cap):
+        piece, want = g[lo:lo + cap], ref[lo:lo + cap]
+        cs = ((piece.numel() + world - 1) // world + 3) // 4 * 4
+        assert torch.equal(piece[:cs], want[:cs])
+        assert not piece[cs:].any()
+    c.destroy()
