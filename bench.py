@@ -155,6 +155,11 @@ def main():
     ap.add_argument("--dp", action="store_true",
                     help="use the data-parallel path (gradient all-reduce) even on 1 GPU")
     a = ap.parse_args()
+    if os.environ.get("DTFX_STACKS_ON_USR1") == "1":  # (diagnostics: all threads' stacks)
+        import faulthandler
+        import signal
+
+        faulthandler.register(signal.SIGUSR1, all_threads=True)
     if a.steps is None:
         a.steps = {"mlp": 20000, "bert": 30, "resnet50": 20}[a.model]
     if a.warmup is None:
