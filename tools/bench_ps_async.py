@@ -41,6 +41,10 @@ def main():
                     help="numa: every cluster process on one NUMA node's CPUs (main.py flag)")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp(prefix="psbench")
+    import resource
+    import time
+
+    ru0, t0 = resource.getrusage(resource.RUSAGE_CHILDREN), time.perf_counter()
     rc = launch_ps(a.num_workers, a.num_gpus, None, 1, cpu=a.cpu, base_port=a.base_port,
                    log_dir=os.path.join(tmp, "logs"), quiet=True, timeout=1800,
                    extra=["--training_steps", str(a.steps), "--log_every", str(a.log_every),
@@ -49,6 +53,15 @@ def main():
                           "--batch_size", str(a.batch_size), "--ps_device", a.ps_device,
                           "--ps_fused_rpc=%s" % ("true" if a.rpc == "fused" else "false"),
                           "--cpu_affinity", a.cpu_affinity])
+    wall = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_CHILDREN)
+    cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    quota = None  # the cgroup's CPU allotment (cgroup v2 cpu.max: "quota period")
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     speeds = []
     for p in glob.glob(os.path.join(tmp, "logs", "worker*.log")):
         for m in re.finditer(r"step: (\d+)\t\| cost: [^|]+\| speed: ([0-9.eE+-]+)step/sec",
@@ -64,7 +77,12 @@ def main():
                       "global_steps_per_sec": round(sps, 1), "num_workers": a.num_workers,
                       "num_gpus": a.num_gpus, "device": "cpu" if a.cpu else "MI355X",
                       "ps_device": a.ps_device, "rpc": a.rpc, "cpu_affinity": a.cpu_affinity,
-                      "steps": a.steps, "rc": rc, "n_speed_samples": len(speeds)}))
+                      "steps": a.steps, "rc": rc, "n_speed_samples": len(speeds),
+                      # CPU time of the whole cluster over its wall time (ps + workers, start
+                      # to exit): the CPUs it kept busy, beside the cgroup's allotment
+                      "cluster_cpu_seconds": round(cpu_s, 1), "wall_seconds": round(wall, 1),
+                      "cpus_busy": round(cpu_s / wall, 2) if wall > 0 else None,
+                      "cgroup_cpus": quota}))
     return 0
 
 
