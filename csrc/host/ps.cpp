@@ -529,8 +529,9 @@ class PSServer {
       ++sync_rounds_;
       if (stepv) stepv->i.store(sync_gen_);
       sync_cv_.notify_all();
-    } else if (!sync_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms),
-                                  [&] { return sync_gen_ > round || !running_; })) {
+    } else if (!sync_cv_.wait_until(  // (system clock: visible to ThreadSanitizer, see sender_loop)
+                   lk, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms),
+                   [&] { return sync_gen_ > round || !running_; })) {
       const size_t have = sync_pending_.size();
       sync_pending_.erase(std::remove_if(sync_pending_.begin(), sync_pending_.end(),
                                          [&](const SyncPush& sp) { return sp.token == token; }),
@@ -1023,7 +1024,10 @@ class PSClient {
           __builtin_ia32_pause();
         } else {
           std::unique_lock<std::mutex> lk(smu_);
-          scv_.wait_for(lk, std::chrono::milliseconds(5), [this] {
+          // wait_until on the system clock: libstdc++'s wait_for (steady clock) goes through
+          // pthread_cond_clockwait, which ThreadSanitizer (GCC 11) does not intercept -- it then
+          // misses the unlock inside the wait and reports the next lock as a double lock
+          scv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(5), [this] {
             return send_state_.load(std::memory_order_acquire) == 1 ||
                    sender_stop_.load(std::memory_order_acquire);
           });
