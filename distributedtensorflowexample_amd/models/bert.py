@@ -45,6 +45,12 @@ BF16 = torch.bfloat16
 # edges cost ~15 us of idle GPU each, but starting each weight gradient as soon as its operand
 # exists overlaps more of the data-gradient chain.
 _WGRAD_BATCH = os.environ.get("DTFX_BERT_WGRAD_BATCH", "0") == "1"
+# DTFX_BERT_LIB_GEMM=1: the two layer GEMMs with no fused epilogue beyond a bias go to hipBLASLt
+# (torch.addmm / torch.mm): the QKV projection (N = 2304 over K = 768: 69 vs 82 us for this
+# repo's best tile) and the attention-output data gradient (26 vs 30 us); every GEMM with a
+# residual / GELU / column-sum epilogue measured faster here (tools/probes/blaslt_bert.py,
+# profiles/r5/blaslt/)
+_LIB_GEMM = os.environ.get("DTFX_BERT_LIB_GEMM", "1") == "1"
 ALIGN = 64
 
 
@@ -227,8 +233,11 @@ class BertMLM:
     def _layer_fwd(self, l, x, batch, seq, kmask):
         cfg, p = self.cfg, self.params
         pre = "encoder/layer_%d/" % l
-        qkv = B16.gemm(x, p.W(pre + "attention/qkv/kernel"), False, True,
-                       bias=p.P(pre + "attention/qkv/bias"))
+        if _LIB_GEMM:  # (bias from the bf16 working copy: hipBLASLt's bias epilogue wants C's type)
+            qkv = torch.addmm(p.W(pre + "attention/qkv/bias"), x, p.W(pre + "attention/qkv/kernel").t())
+        else:
+            qkv = B16.gemm(x, p.W(pre + "attention/qkv/kernel"), False, True,
+                           bias=p.P(pre + "attention/qkv/bias"))
         ctx, lse = TR.attn_fwd(qkv, batch, seq, cfg.heads, kmask)
         a = B16.gemm(ctx, p.W(pre + "attention/output/dense/kernel"), False, True,
                      bias=p.P(pre + "attention/output/dense/bias"), residual=x)
@@ -371,7 +380,10 @@ class BertMLM:
                               p.G(pre + "attention/output/LayerNorm/beta"),
                               dxsum=p.G(pre + "attention/output/dense/bias"))
         wgrad(da, ctx, pre + "attention/output/dense/kernel")
-        dctx = B16.gemm(da, p.W(pre + "attention/output/dense/kernel"))
+        if _LIB_GEMM:
+            dctx = torch.mm(da, p.W(pre + "attention/output/dense/kernel"))
+        else:
+            dctx = B16.gemm(da, p.W(pre + "attention/output/dense/kernel"))
         dqkv = TR.attn_bwd(qkv, ctx, dctx, lse, batch, seq, cfg.heads, kmask,
                            dbias=p.G(pre + "attention/qkv/bias"))
         wgrad(dqkv, x, pre + "attention/qkv/kernel")
