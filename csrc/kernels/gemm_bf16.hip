@@ -15,8 +15,10 @@
 //
 // Epilogue (all optional, in this order, f32):
 //   v = alpha*acc  (+ bias[n])  -> aux_out[m][n] = v (pre-activation, bf16)
-//   v = act(v)                   (gelu(tanh) / relu)
-//   v *= act'(aux_in[m][n])      (backward through an activation)
+//   v = act(v)                   (gelu(tanh) / relu; act 3: gelu, and aux_out receives
+//                                 gelu'(v) instead of v)
+//   v *= act'(aux_in[m][n])      (backward through an activation; act_grad 3: v *= aux_in,
+//                                 the derivative an act-3 forward stored)
 //   v += residual[m][n]          (bf16; convolutions: added BEFORE act', so a conv dgrad
 //                                 can emit dL/d(BN output) = (dgrad + shortcut) * relu'(y))
 //   v += beta * C_old            (f32 output only: gradient accumulation)
@@ -615,7 +617,16 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = __builtin_fmaf(e.alpha, v[u], bn[u]);
       if (full[it]) {
-        if (e.aux_out) {
+        if (e.act == 3) {
+          bf16x8 o;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            float gp;
+            v[u] = gelu_fg(v[u], gp);
+            o[u] = (short)f2bf(gp);
+          }
+          *(bf16x8*)&e.aux_out[(size_t)mp * e.ld_aux + n] = o;
+        } else if (e.aux_out) {
           bf16x8 o;
 #pragma unroll
           for (int u = 0; u < 8; ++u) o[u] = (short)f2bf(v[u]);
@@ -635,10 +646,15 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
         }
         if (e.act_grad) {
           if (!PREF && !LATE) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)mp * e.ld_aux + n];
+          if (e.act_grad == 3) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const float uu = bf2f((unsigned short)a8[it][u]);
-            v[u] *= (e.act_grad == 1) ? gelu_grad_f(uu) : (uu > 0.f ? 1.f : 0.f);
+            for (int u = 0; u < 8; ++u) v[u] *= bf2f((unsigned short)a8[it][u]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const float uu = bf2f((unsigned short)a8[it][u]);
+              v[u] *= (e.act_grad == 1) ? gelu_grad_f(uu) : (uu > 0.f ? 1.f : 0.f);
+            }
           }
         }
         if (MODE == 0 && e.residual) {
@@ -697,13 +713,19 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           }
         for (int u = 0; u < 8 && n + u < N; ++u) {
           float w = v[u];
-          if (e.aux_out) e.aux_out[(size_t)mp * e.ld_aux + n + u] = f2bf(w);
+          if (e.act == 3) {
+            float gp;
+            w = gelu_fg(w, gp);
+            e.aux_out[(size_t)mp * e.ld_aux + n + u] = f2bf(gp);
+          } else if (e.aux_out) {
+            e.aux_out[(size_t)mp * e.ld_aux + n + u] = f2bf(w);
+          }
           if (e.act == 1) w = gelu_f(w);
           else if (e.act == 2) w = fmaxf(w, 0.f);
           if (MODE != 0 && e.residual) w += bf2f(e.residual[(size_t)mp * e.ld_res + n + u]);
           if (e.act_grad) {
             const float uu = bf2f(e.aux_in[(size_t)mp * e.ld_aux + n + u]);
-            w *= (e.act_grad == 1) ? gelu_grad_f(uu) : (uu > 0.f ? 1.f : 0.f);
+            w *= (e.act_grad == 3) ? uu : (e.act_grad == 1) ? gelu_grad_f(uu) : (uu > 0.f ? 1.f : 0.f);
           }
           if (MODE == 0 && e.residual) w += bf2f(e.residual[(size_t)mp * e.ld_res + n + u]);
           if (MODE == 2 && !OUT_F32 && e.bn_x) {
@@ -1199,6 +1221,9 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
     throw std::runtime_error("gemm_bf16: residual must be 16-byte aligned with ld_res % 8 == 0");
   if (bias && ((uintptr_t)bias & 15)) throw std::runtime_error("gemm_bf16: bias must be 16-byte aligned");
   if (act_grad && !aux_in) throw std::runtime_error("gemm_bf16: act_grad needs aux_in");
+  if (act < 0 || act > 3 || act_grad < 0 || act_grad > 3)
+    throw std::runtime_error("gemm_bf16: act / act_grad must be 0..3");
+  if (act == 3 && !aux_out) throw std::runtime_error("gemm_bf16: act 3 stores gelu' in aux_out");
   const bool plain = !colsum && !bias && !act && !act_grad && !residual && !aux_out;
   int cfg;
   splitk = gemm_splitk(ta, out_f32, M, N, K, splitk, batch, beta, plain, &cfg);

@@ -41,6 +41,14 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   const float s = gelu_sig(x);
   return __builtin_fmaf(x * s * (1.f - s), __builtin_fmaf(D, x * x, C), s);
 }
+// gelu(x), with gelu'(x) from the same sigmoid (act 3: the forward stores the derivative, so the
+// backward epilogue is one multiply instead of a second exp + rcp per element)
+__device__ __forceinline__ float gelu_fg(float x, float& gp) {
+  constexpr float C = 1.5957691216f, D = 0.2140644640f;
+  const float s = gelu_sig(x), xs = x * s;
+  gp = __builtin_fmaf(xs * (1.f - s), __builtin_fmaf(D, x * x, C), s);
+  return xs;
+}
 
 // Convolution as implicit GEMM (NHWC bf16 activations, weights [Cout][KH][KW][Cin]).
 //   MODE 1 fwd   : C[pix][co]  = sum_k im2col(x)[pix][k] * W[co][k],   k = (kh, kw, ci)

@@ -51,6 +51,10 @@ _WGRAD_BATCH = os.environ.get("DTFX_BERT_WGRAD_BATCH", "0") == "1"
 # residual / GELU / column-sum epilogue measured faster here (tools/probes/blaslt_bert.py,
 # profiles/r5/blaslt/)
 _LIB_GEMM = os.environ.get("DTFX_BERT_LIB_GEMM", "1") == "1"
+# DTFX_BERT_GELU_DSAVE=1: the FFN input GEMM stores gelu'(u) (from the sigmoid its GELU computes
+# anyway) instead of the pre-activation u, so the FFN output dgrad's epilogue is one multiply
+# instead of a second exp + rcp + ~8 VALU per element
+_GELU_DSAVE = os.environ.get("DTFX_BERT_GELU_DSAVE", "1") == "1"
 ALIGN = 64
 
 
@@ -245,7 +249,8 @@ class BertMLM:
                                       p.P(pre + "attention/output/LayerNorm/beta"), cfg.eps)
         u = torch.empty(x.shape[0], cfg.ffn, device=x.device, dtype=BF16)
         g = B16.gemm(h1, p.W(pre + "intermediate/dense/kernel"), False, True,
-                     bias=p.P(pre + "intermediate/dense/bias"), act="gelu", aux_out=u)
+                     bias=p.P(pre + "intermediate/dense/bias"),
+                     act="gelu_dsave" if _GELU_DSAVE else "gelu", aux_out=u)
         f = B16.gemm(g, p.W(pre + "output/dense/kernel"), False, True,
                      bias=p.P(pre + "output/dense/bias"), residual=h1)
         out, m2, r2 = TR.layernorm_fwd(f, p.P(pre + "output/LayerNorm/gamma"),
@@ -371,7 +376,8 @@ class BertMLM:
                               p.G(pre + "output/LayerNorm/gamma"), p.G(pre + "output/LayerNorm/beta"),
                               dxsum=p.G(pre + "output/dense/bias"))
         wgrad(df, g, pre + "output/dense/kernel")
-        du = B16.gemm(df, p.W(pre + "output/dense/kernel"), act_grad="gelu", aux_in=u,
+        du = B16.gemm(df, p.W(pre + "output/dense/kernel"),  # (u: gelu'(u) under _GELU_DSAVE)
+                      act_grad="mul" if _GELU_DSAVE else "gelu", aux_in=u,
                       colsum=p.G(pre + "intermediate/dense/bias"))
         wgrad(du, h1, pre + "intermediate/dense/kernel")
         dh1 = B16.gemm(du, p.W(pre + "intermediate/dense/kernel"), residual=df)

@@ -20,6 +20,11 @@ from ._ext import hip, ptr, stream_handle
 _SPLITK_WS = os.environ.get("DTFX_SPLITK_WS", "1") != "0"
 
 ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2}
+# act "gelu_dsave" (3): GELU, and ``aux_out`` receives gelu'(pre-activation) instead of the
+# pre-activation; act_grad "mul" (3): ``v *= aux_in`` -- the backward of such a forward, one
+# multiply per element instead of recomputing the derivative (two transcendentals)
+ACT_FWD = dict(ACT, gelu_dsave=3)
+ACT_GRAD = dict(ACT, mul=3)
 
 
 def _gelu_ref(x):
@@ -50,7 +55,8 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
 
     Epilogue order: ``+bias`` -> ``aux_out = v`` (pre-activation, bf16) ->
     ``act`` -> ``*= act_grad'(aux_in)`` -> ``+residual`` -> ``+beta*out``.
-    ``act`` / ``act_grad`` in {None, "gelu", "relu"}.  ``splitk`` (0 = auto)
+    ``act`` in {None, "gelu", "relu", "gelu_dsave"}, ``act_grad`` in {None, "gelu", "relu",
+    "mul"} (``ACT_FWD`` / ``ACT_GRAD``).  ``splitk`` (0 = auto)
     splits K over workgroups for f32 outputs without epilogue (weight
     gradients: few output tiles, deep K), combining with f32 atomics.
     ``colsum`` (f32 [N]) accumulates the column sums of the final values
@@ -60,8 +66,10 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
     (``transformer.adam_mixed(.., segs=..)``).  A GEMM whose split differs from the buffer's
     plane count (or that does not split) raises instead of leaving stale planes.
     """
-    act_i = ACT[act]
-    ag_i = ACT[act_grad]
+    act_i = ACT_FWD[act]
+    ag_i = ACT_GRAD[act_grad]
+    if act_i == 3 and aux_out is None:
+        raise ValueError("gemm_bf16: act 'gelu_dsave' stores gelu' in aux_out")
     M = a.shape[1] if trans_a else a.shape[0]
     K = a.shape[0] if trans_a else a.shape[1]
     Kb = b.shape[1] if trans_b else b.shape[0]
@@ -76,15 +84,17 @@ def gemm(a, b, trans_a=False, trans_b=False, *, bias=None, act=None, aux_out=Non
         v = alpha * (A @ B)
         if bias is not None:
             v = v + bias.float()
-        if aux_out is not None:
+        if act_i == 3:
+            aux_out.copy_(_gelu_grad_ref(v))
+        elif aux_out is not None:
             aux_out.copy_(v)
-        if act_i == 1:
+        if act_i in (1, 3):
             v = _gelu_ref(v)
         elif act_i == 2:
             v = torch.relu(v)
         if ag_i:
             u = aux_in.float()
-            v = v * (_gelu_grad_ref(u) if ag_i == 1 else (u > 0).float())
+            v = v * (u if ag_i == 3 else _gelu_grad_ref(u) if ag_i == 1 else (u > 0).float())
         if residual is not None:
             v = v + residual.float()
         if colsum is not None:

@@ -81,6 +81,38 @@ def test_gemm_act_grad_and_beta(gpu):
     assert (r - (dy.float() @ w.float()) * (u.float() > 0)).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("cfg", [-1, 0, 5])
+@pytest.mark.parametrize("M,N,K", [(300, 260, 128), (1024, 1024, 256)])
+def test_gemm_gelu_dsave_and_mul(gpu, cfg, M, N, K):
+    # act "gelu_dsave": GELU output + gelu'(pre-activation) in aux_out (ragged N = 260 takes the
+    # per-element tail path); act_grad "mul": the backward multiplies by that stored derivative
+    from distributedtensorflowexample_amd.ops._ext import hip
+    x = _rand(M, K, dev=gpu, seed=13)
+    w = _rand(N, K, dev=gpu, seed=14, scale=0.3)
+    bias = torch.randn(N, device=gpu)
+    Np = (N + 7) // 8 * 8  # (row strides must be multiples of 8 elements)
+    gp = torch.empty(M, Np, device=gpu, dtype=torch.bfloat16)[:, :N]
+    y = torch.empty(M, Np, device=gpu)[:, :N]
+    hip().gemm_bf16_set_cfg(cfg)
+    try:
+        bf16.gemm(x, w, False, True, bias=bias, act="gelu_dsave", aux_out=gp, out=y)
+        u = x.float() @ w.float().t() + bias
+        assert (y - torch.nn.functional.gelu(u, approximate="tanh")).abs().max().item() < 1e-3
+        assert torch.allclose(gp.float(), bf16._gelu_grad_ref(u), rtol=1e-2, atol=1e-2)
+        dy = _rand(M, K, dev=gpu, seed=15)
+        w2 = _rand(K, N, dev=gpu, seed=16, scale=0.2)
+        if N % 8 == 0:
+            cs = torch.zeros(N, device=gpu)
+            d = bf16.gemm(dy, w2, act_grad="mul", aux_in=gp, out_dtype=torch.float32, colsum=cs)
+            ref = (dy.float() @ w2.float()) * gp.float()
+            assert (d - ref).abs().max().item() < 1e-3
+            assert (cs - ref.sum(0)).abs().max().item() < 1e-3 * M ** 0.5
+    finally:
+        hip().gemm_bf16_set_cfg(-1)
+    with pytest.raises(ValueError):
+        bf16.gemm(x, w, False, True, act="gelu_dsave")
+
+
 @pytest.mark.parametrize("M", [37, 5000])
 def test_colsum_bf16(gpu, M):
     g = _rand(M, 300, dev=gpu, seed=9)
