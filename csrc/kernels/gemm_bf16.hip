@@ -625,12 +625,12 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
             v[u] = gelu_fg(v[u], gp);
             o[u] = (short)f2bf(gp);
           }
-          *(bf16x8*)&e.aux_out[(size_t)mp * e.ld_aux + n] = o;
+          __builtin_nontemporal_store(o, (bf16x8*)&e.aux_out[(size_t)mp * e.ld_aux + n]);
         } else if (e.aux_out) {
           bf16x8 o;
 #pragma unroll
           for (int u = 0; u < 8; ++u) o[u] = (short)f2bf(v[u]);
-          *(bf16x8*)&e.aux_out[(size_t)mp * e.ld_aux + n] = o;
+          __builtin_nontemporal_store(o, (bf16x8*)&e.aux_out[(size_t)mp * e.ld_aux + n]);
         }
         if (e.act == 1) {
 #pragma unroll
@@ -703,7 +703,10 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           bf16x8 o;
 #pragma unroll
           for (int u = 0; u < 8; ++u) o[u] = (short)f2bf(v[u]);
-          *(bf16x8*)((unsigned short*)Cv + (size_t)mp * ldc + n) = o;
+          // non-temporal (streaming) stores for the bf16 outputs and aux: +2-3 % on every GEMM
+          // shape of tools/probes/gemm_k_sweep.py, BERT-base +0.8 %, ResNet-50 neutral
+          // (profiles/r5/gemm_nt/)
+          __builtin_nontemporal_store(o, (bf16x8*)((unsigned short*)Cv + (size_t)mp * ldc + n));
         }
       } else {
         if (MODE == 2 && !PREF && e.bn_x)
