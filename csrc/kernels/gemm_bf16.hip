@@ -586,7 +586,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
       for (int rr = 0; rr < 32; ++rr) {
         const int m = m0 + r0 + rr;
         if (m < M && n < N && lane < SLW)
-          if (e.ws) e.ws[((size_t)split * M + m) * N + n] = e.alpha * ep[rr * EP_LD + lane];
+          if (e.ws) __builtin_nontemporal_store(e.alpha * ep[rr * EP_LD + lane], &e.ws[((size_t)split * M + m) * N + n]);
           else unsafeAtomicAdd((float*)Cv + (size_t)m * ldc + n, e.alpha * ep[rr * EP_LD + lane]);
       }
       __builtin_amdgcn_wave_barrier();
@@ -697,8 +697,8 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
               v[u + 4] += e.beta * c1[u];
             }
           }
-          *(f32x4*)C = *(f32x4*)&v[0];
-          *(f32x4*)(C + 4) = *(f32x4*)&v[4];
+          __builtin_nontemporal_store(*(f32x4*)&v[0], (f32x4*)C);
+          __builtin_nontemporal_store(*(f32x4*)&v[4], (f32x4*)(C + 4));
         } else {
           bf16x8 o;
 #pragma unroll

@@ -1109,7 +1109,10 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
 
 // ---------------------------------------------------------------------------
 // Mixed-precision Adam(W): f32 master p, grad g, moments m, v; writes the bf16
-// working copy pb used by the GEMMs.  Grad scale folds the 1/world average.
+// working copy pb used by the GEMMs.  Grad scale folds the 1/world average.  p, m, v are
+// streamed (non-temporal: next read a whole step later), the bf16 copy is stored normally
+// (BERT-base +1.0 % together with the GEMMs' non-temporal f32 / split-K stores,
+// profiles/r5/gemm_nt/nt2/).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void adam_mixed_kernel(
     long long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
@@ -1132,9 +1135,9 @@ __global__ __launch_bounds__(256) void adam_mixed_kernel(
       pv[u] -= step_size * mv[u] / (sqrtf(vv[u]) * rbc2 + eps);
       o[u] = (short)tobf(pv[u]);
     }
-    ((f32x4*)p)[i] = pv;
-    ((f32x4*)m)[i] = mv;
-    ((f32x4*)v)[i] = vv;
+    __builtin_nontemporal_store(pv, (f32x4*)p + i);
+    __builtin_nontemporal_store(mv, (f32x4*)m + i);
+    __builtin_nontemporal_store(vv, (f32x4*)v + i);
     if (pb) ((bf16x4*)pb)[i] = o;
   }
 }
@@ -1208,7 +1211,8 @@ __global__ __launch_bounds__(256) void adam_mixed_segs_kernel(
     } else {
       gv = ((const f32x4*)g)[i];
     }
-    f32x4 pv = ((f32x4*)p)[i], mv = ((f32x4*)m)[i], vv = ((f32x4*)v)[i];
+    f32x4 pv = __builtin_nontemporal_load((f32x4*)p + i), mv = __builtin_nontemporal_load((f32x4*)m + i),
+          vv = __builtin_nontemporal_load((f32x4*)v + i);
     bf16x4 o;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1219,9 +1223,9 @@ __global__ __launch_bounds__(256) void adam_mixed_segs_kernel(
       pv[u] -= step_size * mv[u] / (sqrtf(vv[u]) * rbc2 + eps);
       o[u] = (short)tobf(pv[u]);
     }
-    ((f32x4*)p)[i] = pv;
-    ((f32x4*)m)[i] = mv;
-    ((f32x4*)v)[i] = vv;
+    __builtin_nontemporal_store(pv, (f32x4*)p + i);
+    __builtin_nontemporal_store(mv, (f32x4*)m + i);
+    __builtin_nontemporal_store(vv, (f32x4*)v + i);
     if (pb) ((bf16x4*)pb)[i] = o;
   }
 }
