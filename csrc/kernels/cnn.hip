@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
           if (relu) o = fmaxf(o, 0.f);
           v[u] = o;
         }
-        ((bf16x8*)y)[i] = pack8(v);
+        __builtin_nontemporal_store(pack8(v), (bf16x8*)y + (i));
       }
     }
     return;
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
       if (relu) o = fmaxf(o, 0.f);
       v[u] = o;
     }
-    ((bf16x8*)y)[i] = pack8(v);
+    __builtin_nontemporal_store(pack8(v), (bf16x8*)y + (i));
   }
 }
 
@@ -412,8 +412,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
           d[u] = de;
           o[u] = ka[u] * de + k1[u] * xf[u] + k0[u];
         }
-        ((bf16x8*)dx)[i] = pack8(o);
-        if (dres) ((bf16x8*)dres)[i] = pack8(d);
+        __builtin_nontemporal_store(pack8(o), (bf16x8*)dx + (i));
+        if (dres) __builtin_nontemporal_store(pack8(d), (bf16x8*)dres + (i));
       }
     }
     return;
@@ -432,8 +432,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       const float xh = (xv[u] - mean[c]) * rstd[c];
       o[u] = gamma[c] * rstd[c] * (de - sum_dy[c] * inv_m - xh * sum_dyxh[c] * inv_m);
     }
-    ((bf16x8*)dx)[i] = pack8(o);
-    if (dres) ((bf16x8*)dres)[i] = pack8(d);
+    __builtin_nontemporal_store(pack8(o), (bf16x8*)dx + (i));
+    if (dres) __builtin_nontemporal_store(pack8(d), (bf16x8*)dres + (i));
   }
 }
 
@@ -786,8 +786,8 @@ __global__ __launch_bounds__(256) void sgd_momentum_mixed_kernel(
       pv[u] -= lr * vv[u];
       op[u] = tobf(pv[u]);
     }
-    ((f32x4*)p)[i] = pv;
-    ((f32x4*)v)[i] = vv;
+    __builtin_nontemporal_store(pv, (f32x4*)p + (i));
+    __builtin_nontemporal_store(vv, (f32x4*)v + (i));
     if (pb) ((ushort4*)pb)[i] = o;
   }
 }

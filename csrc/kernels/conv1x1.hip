@@ -156,7 +156,7 @@ __global__ __launch_bounds__(576, fbpc<K>() == 2 ? 5 : 3) void conv1x1_fwd_kerne
 #pragma unroll
         for (int u = 0; u < 8; ++u) o8[u] = (short)tobf(fmaxf(bf(a8[u]) * ca[u] + cc[u], 0.f));
         *(bf16x8*)(xs + off) = o8;
-        if (xo && cb == 0) *(bf16x8*)(xo + (size_t)(p0 + r) * K + tcc * 8) = o8;
+        if (xo && cb == 0) __builtin_nontemporal_store(o8, (bf16x8*)(xo + (size_t)(p0 + r) * K + tcc * 8));
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
           o8[u] = (short)tobf(o);
         }
         *(bf16x8*)(buf + off) = o8;
-        if (xo && cb == 0) *(bf16x8*)(xo + (size_t)(p0 + tr) * K + tcc * 8) = o8;
+        if (xo && cb == 0) __builtin_nontemporal_store(o8, (bf16x8*)(xo + (size_t)(p0 + tr) * K + tcc * 8));
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
 #pragma unroll
         for (int u = 0; u < 8; ++u) o[u] = (short)tobf(v[u]);
       }
-      *(bf16x8*)(dx + (size_t)(p0 + ep) * N + cb * NC + ec * 8) = o;
+      __builtin_nontemporal_store(o, (bf16x8*)(dx + (size_t)(p0 + ep) * N + cb * NC + ec * 8));
     }
     __syncthreads();
   }
@@ -612,7 +612,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
           o8[u] = (short)tobf(o);
         }
         *(bf16x8*)(buf + off) = o8;
-        if (xo) *(bf16x8*)(xo + (size_t)(p0 + r) * K + tcc * 8) = o8;
+        if (xo) __builtin_nontemporal_store(o8, (bf16x8*)(xo + (size_t)(p0 + r) * K + tcc * 8));
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
@@ -668,7 +668,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
             s2[u] += v[u] * v[u];
           }
         }
-        *(bf16x8*)(y + (size_t)(p0 + p) * N_ + c * 8) = o;
+        __builtin_nontemporal_store(o, (bf16x8*)(y + (size_t)(p0 + p) * N_ + c * 8));
       }
     }
     __syncthreads();

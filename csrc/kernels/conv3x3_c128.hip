@@ -259,7 +259,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c128_kernel(
             cq[u] += d * (bf(xv[u]) - mu[u]) * rs[u];
           }
         }
-        *(bf16x8*)(y + go) = o;
+        __builtin_nontemporal_store(o, (bf16x8*)(y + go));
       }
       if (fused) {
 #pragma unroll

@@ -153,7 +153,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(
             for (int u = 0; u < 8; ++u)
               o[u] = (short)tobf(fmaxf(__uint_as_float((unsigned)(unsigned short)v[k][u] << 16) * pa[u] + pc_[u], 0.f));
             if (lpr[k] >= 1 && lpr[k] <= TH2 && lpc[k] >= 1 && lpc[k] <= TW)  // this tile's own pixel
-              *(bf16x8*)(xo + (((size_t)n * H + ih) * W + iw) * C + c * 8) = o;
+              __builtin_nontemporal_store(o, (bf16x8*)(xo + (((size_t)n * H + ih) * W + iw) * C + c * 8));
           }
         }
         *(bf16x8*)(Ps + q * PP2 + c * 16) = o;
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(
             cq[u] += d * (xx - mu[u]) * rs[u];
           }
         }
-        *(bf16x8*)(y + (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8) = o;
+        __builtin_nontemporal_store(o, (bf16x8*)(y + (((size_t)n * H + oh0 + p / TW) * W + ow0 + p % TW) * C + ec * 8));
       }
       if (fused) {  // lanes of one chunk: lane & 7 equal -> partial row of this wave
 #pragma unroll

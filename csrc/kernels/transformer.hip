@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         o[u] = (v[c][u] - mean) * rstd * gamma[ch * 8 + u] + beta[ch * 8 + u];
-      *(bf16x8*)(y + (size_t)row * H + ch * 8) = pack8(o);
+      __builtin_nontemporal_store(pack8(o), (bf16x8*)(y + (size_t)row * H + ch * 8));
     }
   }
   if (lane == 0) {
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(NC <= 2 ? 512 : 256) void layernorm_bwd_kernel(
             if (dres) o[u] += rv[c][u];
             ds[c][u] += o[u];
           }
-          *(bf16x8*)(dx + (size_t)row * H + ch * 8) = pack8(o);
+          __builtin_nontemporal_store(pack8(o), (bf16x8*)(dx + (size_t)row * H + ch * 8));
         }
       }
     }
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void embed_ln_fwd_kernel(
         v[c][u] = tobf_round(a[u] + b[u] + d[u]);
         s += v[c][u];
       }
-      *(bf16x8*)(xsum + (size_t)row * H + ch * 8) = pack8(v[c]);
+      __builtin_nontemporal_store(pack8(v[c]), (bf16x8*)(xsum + (size_t)row * H + ch * 8));
     }
   }
   const float mean = wave_sum(s) / H;
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256) void embed_ln_fwd_kernel(
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         o[u] = (v[c][u] - mean) * rstd * gamma[ch * 8 + u] + beta[ch * 8 + u];
-      *(bf16x8*)(y + (size_t)row * H + ch * 8) = pack8(o);
+      __builtin_nontemporal_store(pack8(o), (bf16x8*)(y + (size_t)row * H + ch * 8));
     }
   }
   if (lane == 0) {
@@ -1355,7 +1355,7 @@ __global__ __launch_bounds__(256) void act_grad_bf16_kernel(long long n8, int ac
       }
       a[k] *= d;
     }
-    ((bf16x8*)dx)[i] = pack8(a);
+    __builtin_nontemporal_store(pack8(a), (bf16x8*)dx + (i));
   }
 }
 
