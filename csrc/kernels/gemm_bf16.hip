@@ -1185,7 +1185,14 @@ static int gemm_splitk(bool ta, bool out_f32, int M, int N, int K, int splitk, i
   // 432 blocks 110 us vs x 2 (288, unbalanced) 146 us and x 4 (576, a second partial wave)
   // 154 us; 108 x 4 and 36 x 12 likewise the fastest of 1..16.
   if (batch == 1 && out_f32 && plain_epilogue && (beta == 0.f || beta == 1.f)) {
-    const int slots = cfg == 0 ? 512 : 256;
+    // DTFX_GEMM_TA8_SLOTS: block slots a weight gradient on the 8-phase tile splits for
+    // (DTFX_GEMM_TA8=1 A/B runs; fewer splits = fewer partial planes for the optimizer to read
+    // while the data gradients hold the rest of the chip)
+    static const int ta8_slots = [] {
+      const char* e = getenv("DTFX_GEMM_TA8_SLOTS");
+      return e ? std::max(1, atoi(e)) : 256;
+    }();
+    const int slots = cfg == 0 ? 512 : ta ? ta8_slots : 256;
     if (tiles < slots / 2) return std::max(1, std::min(slots / tiles, nkt / 8));
   }
   return 1;
