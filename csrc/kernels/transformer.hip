@@ -132,6 +132,78 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(
   }
 }
 
+// The same LayerNorm forward with R rows per wave, all R rows' loads issued before the first
+// row is reduced (one memory round trip per R rows instead of per row) and gamma / beta held in
+// registers; NC = ceil(H / 512) 8-column chunks per lane.
+template <int NC, int R>
+__global__ __launch_bounds__(256) void layernorm_fwd_rows_kernel(
+    int T, int H, const unsigned short* __restrict__ x, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, unsigned short* __restrict__ y,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row0 = (blockIdx.x * 4 + wave) * R;
+  if (row0 >= T) return;
+  const int nch = H >> 3;
+  bf16x8 raw[R][NC];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int rr = min(row0 + i, T - 1);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ch = min(lane + 64 * c, nch - 1);  // clamped: masked at use
+      raw[i][c] = *(const bf16x8*)(x + (size_t)rr * H + ch * 8);
+    }
+  }
+  float gm[NC][8], bt[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = min(lane + 64 * c, nch - 1);
+    *(f32x4*)&gm[c][0] = *(const f32x4*)(gamma + ch * 8);
+    *(f32x4*)&gm[c][4] = *(const f32x4*)(gamma + ch * 8 + 4);
+    *(f32x4*)&bt[c][0] = *(const f32x4*)(beta + ch * 8);
+    *(f32x4*)&bt[c][4] = *(const f32x4*)(beta + ch * 8 + 4);
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = row0 + i;
+    if (row >= T) break;
+    float v[NC][8];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      unpack8(raw[i][c], v[c]);
+      if (lane + 64 * c < nch)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[c][u];
+    }
+    const float mean = wave_sum(s) / H;
+    float s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (lane + 64 * c < nch)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float d = v[c][u] - mean;
+          s2 += d * d;
+        }
+    const float rstd = rsqrtf(wave_sum(s2) / H + eps);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o[u] = (v[c][u] - mean) * rstd * gm[c][u] + bt[c][u];
+        __builtin_nontemporal_store(pack8(o), (bf16x8*)(y + (size_t)row * H + ch * 8));
+      }
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
 // dgamma += sum dy * xhat, dbeta += sum dy (per block in registers, then atomics)
 // optional dres: dx += dres (the residual branch gradient, fused)
@@ -1377,8 +1449,29 @@ void layernorm_fwd_launch(int T, int H, const void* x, const float* gamma, const
                           float eps, void* y, float* mean, float* rstd, hipStream_t s) {
   check_h(H);
   if (T <= 0) return;
-  hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((T + 3) / 4), dim3(256), 0, s, T, H,
-                     (const unsigned short*)x, gamma, beta, eps, (unsigned short*)y, mean, rstd);
+  // rows per wave (DTFX_LN_FWD_ROWS=1: the one-row kernel, for A/B runs)
+  static const int rows = [] {
+    const char* e = getenv("DTFX_LN_FWD_ROWS");
+    return e ? atoi(e) : 4;
+  }();
+  const auto* xs = (const unsigned short*)x;
+  auto* ys = (unsigned short*)y;
+  const int nc = (H + 511) / 512;
+  if ((rows == 4 || rows == 2) && !(((uintptr_t)gamma | (uintptr_t)beta) & 15)) {  // (f32x4 gamma / beta)
+    const int per_block = 4 * rows;
+    const dim3 grid((T + per_block - 1) / per_block);
+#define DTFX_LNF(NC_, R_) \
+  hipLaunchKernelGGL((layernorm_fwd_rows_kernel<NC_, R_>), grid, dim3(256), 0, s, T, H, xs, gamma, beta, eps, ys, mean, rstd)
+    if (rows == 4) {
+      if (nc == 1) DTFX_LNF(1, 4); else if (nc == 2) DTFX_LNF(2, 4); else if (nc == 3) DTFX_LNF(3, 4); else DTFX_LNF(4, 4);
+    } else {
+      if (nc == 1) DTFX_LNF(1, 2); else if (nc == 2) DTFX_LNF(2, 2); else if (nc == 3) DTFX_LNF(3, 2); else DTFX_LNF(4, 2);
+    }
+#undef DTFX_LNF
+  } else {
+    hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((T + 3) / 4), dim3(256), 0, s, T, H, xs, gamma, beta, eps,
+                       ys, mean, rstd);
+  }
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

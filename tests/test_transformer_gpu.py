@@ -15,8 +15,9 @@ def _r(*shape, seed=0, scale=1.0):
     return (torch.randn(*shape, generator=g) * scale)
 
 
-def test_layernorm_fwd_bwd(gpu):
-    Tn, H = 300, 768
+@pytest.mark.parametrize("Tn,H", [(300, 768), (37, 136), (70, 2048), (129, 1000)])
+def test_layernorm_fwd_bwd(gpu, Tn, H):
+    # (row counts off the 16-row blocks of the 4-rows-per-wave forward; 1..4 column chunks)
     x = _r(Tn, H, seed=1).to(BF)
     gamma, beta = _r(H, seed=2) * 0.1 + 1, _r(H, seed=3) * 0.1
     y, mean, rstd = T.layernorm_fwd(x.to(gpu), gamma.to(gpu), beta.to(gpu))
