@@ -99,7 +99,7 @@ void flash_fwd_launch(int, int, int, const void*, void*, float*, int, const floa
                       hipStream_t);
 void flash_bwd_launch(int, int, int, const void*, const void*, const void*, const float*, int,
                       const float*, float, void*, float*, float*, hipStream_t);
-void mlm_xent_launch(int, int, const float*, int, const int*, float, float*, float*, void*, int,
+void mlm_xent_launch(int, int, const void*, bool, int, const int*, float, float*, float*, void*, int,
                      hipStream_t);
 }  // namespace dtfx
 
@@ -201,10 +201,13 @@ void register_nn(py::module_& m) {
     dtfx::act_grad_bf16_launch(n, act, P<const void>(dy), P<const void>(u), P<void>(dx), S(s));
   });
   m.def("mlm_xent", [](int N, int C, uintptr_t logits, int ldl, uintptr_t labels, float scale,
-                       uintptr_t loss, uintptr_t correct, uintptr_t dl, int ldd, uintptr_t s) {
-    dtfx::mlm_xent_launch(N, C, P<const float>(logits), ldl, P<const int>(labels), scale,
+                       uintptr_t loss, uintptr_t correct, uintptr_t dl, int ldd, uintptr_t s,
+                       bool logits_bf16) {
+    dtfx::mlm_xent_launch(N, C, P<const void>(logits), logits_bf16, ldl, P<const int>(labels), scale,
                           P<float>(loss), P<float>(correct), P<void>(dl), ldd, S(s));
-  });
+  }, py::arg("N"), py::arg("C"), py::arg("logits"), py::arg("ldl"), py::arg("labels"),
+     py::arg("scale"), py::arg("loss"), py::arg("correct"), py::arg("dl"), py::arg("ldd"),
+     py::arg("s"), py::arg("logits_bf16") = false);
   m.def("conv_bf16", [](int mode, int N, int H, int W, int C, int Cout, int KH, int KW, int stride,
                         int pad, uintptr_t a, uintptr_t b, int ldw, uintptr_t out, float beta,
                         uintptr_t residual, uintptr_t colsum, uintptr_t colsq, int splitk,

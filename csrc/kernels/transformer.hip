@@ -1308,7 +1308,18 @@ __global__ __launch_bounds__(256) void adam_mixed_segs_kernel(
 // dlogits = (softmax - onehot) * scale written directly as bf16 (the operand of
 // the decoder's dgrad/wgrad GEMMs).  Columns [C, ldd) of dlogits are zeroed.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void mlm_xent_kernel(int C, const float* __restrict__ logits,
+// logits f32 (LT = float) or bf16 (LT = unsigned short: half the bytes of the [Tm x vocab] product
+// written by the decoder GEMM and read here; the softmax math stays f32)
+__device__ __forceinline__ float xl1(const float* l, int c) { return l[c]; }
+__device__ __forceinline__ float xl1(const unsigned short* l, int c) { return bf(l[c]); }
+__device__ __forceinline__ f32x4 xl4(const float* l, int i) { return ((const f32x4*)l)[i]; }
+__device__ __forceinline__ f32x4 xl4(const unsigned short* l, int i) {
+  const bf16x4 b = ((const bf16x4*)l)[i];
+  return f32x4{bf((unsigned short)b[0]), bf((unsigned short)b[1]), bf((unsigned short)b[2]),
+               bf((unsigned short)b[3])};
+}
+template <typename LT>
+__global__ __launch_bounds__(256) void mlm_xent_kernel(int C, const LT* __restrict__ logits,
                                                        int ldl, const int* __restrict__ labels,
                                                        float scale, float* __restrict__ loss,
                                                        float* __restrict__ correct,
@@ -1316,7 +1327,7 @@ __global__ __launch_bounds__(256) void mlm_xent_kernel(int C, const float* __res
   __shared__ float sm_m[4], sm_s[4];
   __shared__ int sm_a[4];
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const float* l = logits + (size_t)row * ldl;
+  const LT* l = logits + (size_t)row * ldl;
   const int y = labels[row];
   float m = -INFINITY, sum = 0.f, best = -INFINITY;
   int am = 0x7fffffff;
@@ -1329,7 +1340,7 @@ __global__ __launch_bounds__(256) void mlm_xent_kernel(int C, const float* __res
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const int i = i0 + 256 * k;
-      v[k] = i < C4 ? ((const f32x4*)l)[i] : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      v[k] = i < C4 ? xl4(l, i) : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     }
     float lm = -INFINITY;
 #pragma unroll
@@ -1351,7 +1362,7 @@ __global__ __launch_bounds__(256) void mlm_xent_kernel(int C, const float* __res
         for (int u = 0; u < 4; ++u) sum += __expf(v[k][u] - m);  // -inf pads add 0
   }
   for (int c = 4 * C4 + t; c < C; c += 256) {
-    const float x = l[c];
+    const float x = xl1(l, c);
     if (x > best) { best = x; am = c; }
     if (x > m) { sum = (m == -INFINITY ? 0.f : sum * __expf(m - x)) + 1.f; m = x; }
     else sum += __expf(x - m);
@@ -1373,31 +1384,31 @@ __global__ __launch_bounds__(256) void mlm_xent_kernel(int C, const float* __res
   for (int w = 0; w < 4; ++w) Ssum += sm_m[w] == -INFINITY ? 0.f : sm_s[w] * __expf(sm_m[w] - M);
   // argmax across waves: recompute best value by index order
   int A = sm_a[0];
-  float Bv = l[A < C ? A : 0];
+  float Bv = xl1(l, A < C ? A : 0);
   for (int w = 1; w < 4; ++w) {
     const int a = sm_a[w];
     if (a < C) {
-      const float bv = l[a];
+      const float bv = xl1(l, a);
       if (bv > Bv || (bv == Bv && a < A)) { Bv = bv; A = a; }
     }
   }
   const bool valid = y >= 0 && y < C;
   const float lse = M + __logf(Ssum);
   if (t == 0) {
-    loss[row] = valid ? lse - l[y] : 0.f;
+    loss[row] = valid ? lse - xl1(l, y) : 0.f;
     correct[row] = (valid && A == y) ? 1.f : 0.f;
   }
   unsigned short* d = dl + (size_t)row * ldd;
   const float sc = valid ? scale : 0.f;
   for (int i = t; i < (ldd >> 2); i += 256) {
     const bool vec = 4 * i + 3 < C;  // (ldl % 4 == 0: the 16-B load is aligned)
-    const f32x4 lv = vec ? ((const f32x4*)l)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 lv = vec ? xl4(l, i) : f32x4{0.f, 0.f, 0.f, 0.f};
     bf16x4 o;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = 4 * i + u;
       float g = 0.f;
-      if (c < C) g = (__expf((vec ? lv[u] : l[c]) - lse) - (c == y ? 1.f : 0.f)) * sc;
+      if (c < C) g = (__expf((vec ? lv[u] : xl1(l, c)) - lse) - (c == y ? 1.f : 0.f)) * sc;
       o[u] = (short)tobf(g);
     }
     ((bf16x4*)d)[i] = o;
@@ -1650,13 +1661,18 @@ void adam_mixed_launch(long long n, float* p, const float* g, float* m, float* v
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
-void mlm_xent_launch(int N, int C, const float* logits, int ldl, const int* labels, float scale,
-                     float* loss, float* correct, void* dl, int ldd, hipStream_t s) {
+void mlm_xent_launch(int N, int C, const void* logits, bool logits_bf16, int ldl, const int* labels,
+                     float scale, float* loss, float* correct, void* dl, int ldd, hipStream_t s) {
   if (ldl % 4 || ldd % 4 || ldd < C || ldl < C)
     throw std::runtime_error("mlm_xent: ldl/ldd must be multiples of 4 and >= C");
   if (N <= 0) return;
-  hipLaunchKernelGGL(mlm_xent_kernel, dim3(N), dim3(256), 0, s, C, logits, ldl, labels, scale, loss,
-                     correct, (unsigned short*)dl, ldd);
+  if (logits_bf16)
+    hipLaunchKernelGGL(mlm_xent_kernel<unsigned short>, dim3(N), dim3(256), 0, s, C,
+                       (const unsigned short*)logits, ldl, labels, scale, loss, correct,
+                       (unsigned short*)dl, ldd);
+  else
+    hipLaunchKernelGGL(mlm_xent_kernel<float>, dim3(N), dim3(256), 0, s, C, (const float*)logits, ldl,
+                       labels, scale, loss, correct, (unsigned short*)dl, ldd);
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

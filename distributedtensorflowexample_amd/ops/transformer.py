@@ -263,8 +263,8 @@ def act_grad(dy, u, act="gelu"):
 
 
 def mlm_xent(logits, labels, n_classes, scale):
-    """Softmax cross-entropy over the first ``n_classes`` columns of f32 ``logits``
-    [N, ldl]; labels int32 (-100 = ignore).  Returns (loss_rows, correct_rows,
+    """Softmax cross-entropy over the first ``n_classes`` columns of f32 or bf16 ``logits``
+    [N, ldl] (f32 math either way); labels int32 (-100 = ignore).  Returns (loss_rows, correct_rows,
     dlogits bf16 [N, ldl] pre-scaled by ``scale``, zero beyond n_classes)."""
     N, ldl = logits.shape
     if not logits.is_cuda:
@@ -275,11 +275,11 @@ def mlm_xent(logits, labels, n_classes, scale):
         dl = torch.zeros(N, ldl, dtype=BF16)
         dl[:, :n_classes] = d.to(BF16)
         return loss, correct, dl
-    _contig(logits, "logits", torch.float32)
+    _contig(logits, "logits", logits.dtype if logits.dtype == BF16 else torch.float32)
     lab = labels.to(torch.int32).contiguous()
     loss = torch.empty(N, device=logits.device)
     correct = torch.empty(N, device=logits.device)
     dl = torch.empty(N, ldl, device=logits.device, dtype=BF16)
     hip().mlm_xent(N, n_classes, ptr(logits), ldl, ptr(lab), float(scale), ptr(loss), ptr(correct),
-                   ptr(dl), ldl, stream_handle())
+                   ptr(dl), ldl, stream_handle(), logits.dtype == BF16)
     return loss, correct, dl
