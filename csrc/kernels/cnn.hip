@@ -193,8 +193,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
       for (int k = 0; k < U; ++k) {
         const long long i = ib + k * stride;
         const long long ic = i < n8 ? i : i0;  // in-bounds dummy for the tail
-        xv[k] = ((const bf16x8*)x)[ic];
-        if (res) rv[k] = ((const bf16x8*)res)[ic];
+        xv[k] = __builtin_nontemporal_load((const bf16x8*)x + ic);
+        if (res) rv[k] = __builtin_nontemporal_load((const bf16x8*)res + ic);
       }
 #pragma unroll
       for (int k = 0; k < U; ++k) {
@@ -218,8 +218,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long long M, int C,
   for (long long i = i0; i < n8; i += stride) {  // general C
     const int c0 = (int)(i % cg) * 8;
     float v[8], r[8];
-    unpack8(((const bf16x8*)x)[i], v);
-    if (res) unpack8(((const bf16x8*)res)[i], r);
+    unpack8(__builtin_nontemporal_load((const bf16x8*)x + i), v);
+    if (res) unpack8(__builtin_nontemporal_load((const bf16x8*)res + i), r);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int c = c0 + u;
@@ -318,9 +318,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         for (int k = 0; k < U; ++k) {
           const long long r = rb + (long long)k * rpp;
           const long long i = (r < r1 ? r : r0 + rr) * cg + gg;  // in-bounds dummy row
-          dv[k] = ((const bf16x8*)dy)[i];
-          xq[k] = ((const bf16x8*)x)[i];
-          if (relu) yq[k] = ((const bf16x8*)yout)[i];
+          dv[k] = __builtin_nontemporal_load((const bf16x8*)dy + i);
+          xq[k] = __builtin_nontemporal_load((const bf16x8*)x + i);
+          if (relu) yq[k] = __builtin_nontemporal_load((const bf16x8*)yout + i);
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
@@ -394,9 +394,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       for (int k = 0; k < U; ++k) {
         const long long i = ib + k * stride;
         const long long ic = i < n8 ? i : i0;
-        dv[k] = ((const bf16x8*)dy)[ic];
-        xv[k] = ((const bf16x8*)x)[ic];
-        if (relu) yv[k] = ((const bf16x8*)yout)[ic];
+        dv[k] = __builtin_nontemporal_load((const bf16x8*)dy + ic);
+        xv[k] = __builtin_nontemporal_load((const bf16x8*)x + ic);
+        if (relu) yv[k] = __builtin_nontemporal_load((const bf16x8*)yout + ic);
       }
 #pragma unroll
       for (int k = 0; k < U; ++k) {
@@ -421,9 +421,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   for (long long i = i0; i < n8; i += stride) {  // general C
     const int c0 = (int)(i % cg) * 8;
     float d[8], xv[8], yv[8], o[8];
-    unpack8(((const bf16x8*)dy)[i], d);
-    unpack8(((const bf16x8*)x)[i], xv);
-    if (relu) unpack8(((const bf16x8*)yout)[i], yv);
+    unpack8(__builtin_nontemporal_load((const bf16x8*)dy + i), d);
+    unpack8(__builtin_nontemporal_load((const bf16x8*)x + i), xv);
+    if (relu) unpack8(__builtin_nontemporal_load((const bf16x8*)yout + i), yv);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int c = c0 + u;

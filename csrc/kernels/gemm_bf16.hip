@@ -546,8 +546,8 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
         pm[it] = (nimg * cd.H + i * cd.stride + cd.ph) * cd.W + j * cd.stride + cd.pw;
       }
       if (PREF) {
-        if (e.act_grad) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)pm[it] * e.ld_aux + ns];
-        if (e.residual) r8[it] = *(const bf16x8*)&e.residual[(size_t)pm[it] * e.ld_res + ns];
+        if (e.act_grad) a8[it] = __builtin_nontemporal_load((const bf16x8*)&e.aux_in[(size_t)pm[it] * e.ld_aux + ns]);
+        if (e.residual) r8[it] = __builtin_nontemporal_load((const bf16x8*)&e.residual[(size_t)pm[it] * e.ld_res + ns]);
         if (MODE == 2 && e.bn_x) x8[it] = *(const bf16x8*)&e.bn_x[(size_t)pm[it] * ldc + ns];
       }
     }
@@ -564,8 +564,8 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
         const int ns = full[it] ? nn[it] : 0;
-        if (e.act_grad) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)pm[it] * e.ld_aux + ns];
-        if (e.residual) r8[it] = *(const bf16x8*)&e.residual[(size_t)pm[it] * e.ld_res + ns];
+        if (e.act_grad) a8[it] = __builtin_nontemporal_load((const bf16x8*)&e.aux_in[(size_t)pm[it] * e.ld_aux + ns]);
+        if (e.residual) r8[it] = __builtin_nontemporal_load((const bf16x8*)&e.residual[(size_t)pm[it] * e.ld_res + ns]);
         if (e.bn_x) x8[it] = *(const bf16x8*)&e.bn_x[(size_t)pm[it] * ldc + ns];
       }
       if (e.bn_x) {  // the lane's 8 columns are the same for the slab's 4 row groups
@@ -640,12 +640,12 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           for (int u = 0; u < 8; ++u) v[u] = fmaxf(v[u], 0.f);
         }
         if (MODE != 0 && e.residual) {  // convolutions: shortcut gradient before the mask
-          if (!PREF && !LATE) r8[it] = *(const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n];
+          if (!PREF && !LATE) r8[it] = __builtin_nontemporal_load((const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n]);
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[it][u]);
         }
         if (e.act_grad) {
-          if (!PREF && !LATE) a8[it] = *(const bf16x8*)&e.aux_in[(size_t)mp * e.ld_aux + n];
+          if (!PREF && !LATE) a8[it] = __builtin_nontemporal_load((const bf16x8*)&e.aux_in[(size_t)mp * e.ld_aux + n]);
           if (e.act_grad == 3) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) v[u] *= bf2f((unsigned short)a8[it][u]);
@@ -658,7 +658,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
           }
         }
         if (MODE == 0 && e.residual) {
-          if (!PREF) r8[it] = *(const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n];
+          if (!PREF) r8[it] = __builtin_nontemporal_load((const bf16x8*)&e.residual[(size_t)mp * e.ld_res + n]);
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] += bf2f((unsigned short)r8[it][u]);
         }

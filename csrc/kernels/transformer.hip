@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void layernorm_fwd_rows_kernel(
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int ch = min(lane + 64 * c, nch - 1);  // clamped: masked at use
-      raw[i][c] = *(const bf16x8*)(x + (size_t)rr * H + ch * 8);
+      raw[i][c] = __builtin_nontemporal_load((const bf16x8*)(x + (size_t)rr * H + ch * 8));
     }
   }
   float gm[NC][8], bt[NC][8];
@@ -244,9 +244,9 @@ __global__ __launch_bounds__(NC <= 2 ? 512 : 256) void layernorm_bwd_kernel(
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int ch = min(lane + 64 * c, nch - 1);  // clamped: masked at use
-      xb[p][c] = *(const bf16x8*)(x + (size_t)row * H + ch * 8);
-      yb[p][c] = *(const bf16x8*)(dy + (size_t)row * H + ch * 8);
-      if (dres) rb[p][c] = *(const bf16x8*)(dres + (size_t)row * H + ch * 8);
+      xb[p][c] = __builtin_nontemporal_load((const bf16x8*)(x + (size_t)row * H + ch * 8));
+      yb[p][c] = __builtin_nontemporal_load((const bf16x8*)(dy + (size_t)row * H + ch * 8));
+      if (dres) rb[p][c] = __builtin_nontemporal_load((const bf16x8*)(dres + (size_t)row * H + ch * 8));
     }
     mb[p] = mean_in[row];
     rsb[p] = rstd_in[row];
@@ -1264,24 +1264,25 @@ __global__ __launch_bounds__(256) void adam_mixed_segs_kernel(
       const int S = s_S[k];
       // the planes four at a time, loads first (a plain loop waited out one round trip per
       // plane: 14 for the attention-output weights), added in split order
-      gv = w[0];
+      gv = __builtin_nontemporal_load(w);
       int q = 1;
       for (; q + 3 < S; q += 4) {
-        const f32x4 a0 = w[q * pl], a1 = w[(q + 1) * pl], a2 = w[(q + 2) * pl], a3 = w[(q + 3) * pl];
+        const f32x4 a0 = __builtin_nontemporal_load(w + q * pl), a1 = __builtin_nontemporal_load(w + (q + 1) * pl),
+                    a2 = __builtin_nontemporal_load(w + (q + 2) * pl), a3 = __builtin_nontemporal_load(w + (q + 3) * pl);
         gv += a0;
         gv += a1;
         gv += a2;
         gv += a3;
       }
       if (q + 1 < S) {
-        const f32x4 a0 = w[q * pl], a1 = w[(q + 1) * pl];
+        const f32x4 a0 = __builtin_nontemporal_load(w + q * pl), a1 = __builtin_nontemporal_load(w + (q + 1) * pl);
         gv += a0;
         gv += a1;
         q += 2;
       }
-      if (q < S) gv += w[q * pl];
+      if (q < S) gv += __builtin_nontemporal_load(w + q * pl);
     } else {
-      gv = ((const f32x4*)g)[i];
+      gv = __builtin_nontemporal_load((const f32x4*)g + i);
     }
     f32x4 pv = __builtin_nontemporal_load((f32x4*)p + i), mv = __builtin_nontemporal_load((f32x4*)m + i),
           vv = __builtin_nontemporal_load((f32x4*)v + i);
