@@ -45,11 +45,11 @@ BF16 = torch.bfloat16
 # edges cost ~15 us of idle GPU each, but starting each weight gradient as soon as its operand
 # exists overlaps more of the data-gradient chain.
 _WGRAD_BATCH = os.environ.get("DTFX_BERT_WGRAD_BATCH", "0") == "1"
-# DTFX_BERT_LIB_GEMM=1: the two layer GEMMs with no fused epilogue beyond a bias go to hipBLASLt
+# DTFX_BERT_LIB_GEMM=1: the GEMMs with no fused epilogue beyond a bias go to hipBLASLt
 # (torch.addmm / torch.mm): the QKV projection (N = 2304 over K = 768: 69 vs 82 us for this
-# repo's best tile) and the attention-output data gradient (26 vs 30 us); every GEMM with a
-# residual / GELU / column-sum epilogue measured faster here (tools/probes/blaslt_bert.py,
-# profiles/r5/blaslt/)
+# repo's best tile), the attention-output data gradient (26 vs 30 us) and the bf16 decoder
+# logits (121 vs 173 us); every GEMM with a residual / GELU / column-sum epilogue, and the
+# decoder's data gradient, measured faster here (tools/probes/blaslt_bert.py, profiles/r5/blaslt/)
 _LIB_GEMM = os.environ.get("DTFX_BERT_LIB_GEMM", "1") == "1"
 # DTFX_BERT_GELU_DSAVE=1: the FFN input GEMM stores gelu'(u) (from the sigmoid its GELU computes
 # anyway) instead of the pre-activation u, so the FFN output dgrad's epilogue is one multiply
@@ -299,8 +299,11 @@ class BertMLM:
         tn, mt, rt = TR.layernorm_fwd(t, p.P("cls/predictions/transform/LayerNorm/gamma"),
                                       p.P("cls/predictions/transform/LayerNorm/beta"), cfg.eps)
         E = p.W("embeddings/word_embeddings")
-        logits = B16.gemm(tn, E, False, True, bias=p.P("cls/predictions/output_bias"),
-                          out_dtype=BF16 if _BF16_LOGITS else torch.float32)
+        if _BF16_LOGITS and _LIB_GEMM:  # bias-only bf16 product: hipBLASLt 121 vs 173 us here
+            logits = torch.addmm(p.W("cls/predictions/output_bias"), tn, E.t())
+        else:
+            logits = B16.gemm(tn, E, False, True, bias=p.P("cls/predictions/output_bias"),
+                              out_dtype=BF16 if _BF16_LOGITS else torch.float32)
         Tm = tn.shape[0]
         scale = 1.0 / max(1, n_valid if n_valid is not None else Tm)
         loss_rows, correct, dlog_b = TR.mlm_xent(logits, mask_labels, cfg.vocab_size, scale)

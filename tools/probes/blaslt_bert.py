@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=128 * 128)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--head", action="store_true", help="the decoder GEMMs instead of the layer's")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     T, H, F = a.tokens, 768, 3072
@@ -57,6 +58,18 @@ def main():
         "out_dgrad": (lambda: B16.gemm(da, Wo), lambda: torch.mm(da, Wo)),
         "qkv_dgrad_res": (lambda: B16.gemm(dqkv, Wqkv, residual=da), lambda: torch.addmm(da, dqkv, Wqkv)),
     }
+    if a.head:  # the MLM decoder: masked rows x padded vocabulary
+        Tm, V = int(T * 0.15) // 64 * 64, 30528
+        tn, dlog, E = r(Tm, H), r(Tm, V), r(V, H)
+        bdec = r(V).float()
+        bdec16 = bdec.bfloat16()
+        from distributedtensorflowexample_amd.ops import transformer as TR
+        calls = {
+            "logits_bias_bf16": (lambda: B16.gemm(tn, E, False, True, bias=bdec),
+                                 lambda: torch.addmm(bdec16, tn, E.t())),
+            "decoder_dgrad_bf16": (lambda: TR.cast_bf16(B16.gemm(dlog, E, out_dtype=torch.float32)),
+                                   lambda: torch.mm(dlog, E)),
+        }
     for name, (ours, lt) in calls.items():
         err = (ours().float() - lt().float()).abs().max().item()
         to, tl = [], []
