@@ -69,6 +69,7 @@ def main():
                                  lambda: torch.addmm(bdec16, tn, E.t())),
             "decoder_dgrad_bf16": (lambda: TR.cast_bf16(B16.gemm(dlog, E, out_dtype=torch.float32)),
                                    lambda: torch.mm(dlog, E)),
+            "transform_dgrad": (lambda: B16.gemm(tn, Wo), lambda: torch.mm(tn, Wo)),
         }
     for name, (ours, lt) in calls.items():
         err = (ours().float() - lt().float()).abs().max().item()
