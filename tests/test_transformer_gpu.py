@@ -34,8 +34,9 @@ def test_layernorm_fwd_bwd(gpu, Tn, H):
     assert torch.allclose(db.cpu(), dbr, atol=1e-2, rtol=1e-3)
 
 
-def test_embedding_fwd_bwd(gpu):
-    B, S, H, V = 3, 40, 256, 1000
+@pytest.mark.parametrize("B", [3, 70])  # 70: the position / type gradient split over the batch
+def test_embedding_fwd_bwd(gpu, B):
+    S, H, V = 40, 256, 1000
     ids = torch.randint(0, V, (B * S,), dtype=torch.int32)
     tt = torch.randint(0, 2, (B * S,), dtype=torch.int32)
     word, pos, typ = _r(V, H, seed=6).to(BF), _r(64, H, seed=7).to(BF), _r(2, H, seed=8).to(BF)
