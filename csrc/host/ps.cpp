@@ -41,6 +41,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -50,6 +51,21 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+// Timed condition-variable wait.  Normal builds use the steady clock (immune to wall-clock
+// steps: NTP, a manual change).  ThreadSanitizer builds use the system clock: libstdc++'s
+// steady-clock wait goes through pthread_cond_clockwait, which TSan (GCC 11) does not
+// intercept -- it then misses the unlock inside the wait and reports the next lock as a
+// double lock (tools/sanitize_host.py).
+template <class Pred>
+static bool cv_wait_ms(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, long long ms,
+                       Pred pred) {
+#if defined(__SANITIZE_THREAD__)
+  return cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(ms), pred);
+#else
+  return cv.wait_for(lk, std::chrono::milliseconds(ms), pred);
+#endif
+}
 
 namespace py = pybind11;
 
@@ -529,9 +545,8 @@ class PSServer {
       ++sync_rounds_;
       if (stepv) stepv->i.store(sync_gen_);
       sync_cv_.notify_all();
-    } else if (!sync_cv_.wait_until(  // (system clock: visible to ThreadSanitizer, see sender_loop)
-                   lk, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms),
-                   [&] { return sync_gen_ > round || !running_; })) {
+    } else if (!cv_wait_ms(sync_cv_, lk, timeout_ms,
+                           [&] { return sync_gen_ > round || !running_; })) {
       const size_t have = sync_pending_.size();
       sync_pending_.erase(std::remove_if(sync_pending_.begin(), sync_pending_.end(),
                                          [&](const SyncPush& sp) { return sp.token == token; }),
@@ -586,12 +601,22 @@ class PSClient {
   }
   ~PSClient() {
     if (psp_.active) {
-      // an exchange whose end() never came (mu_ still held by its thread, maybe this one):
-      // nobody can finish it, so do not wait for mu_ -- wake the sender, join it, then close
+      // an exchange whose end() never came (mu_ still held by the thread that began it):
+      // nobody can finish it, so do not wait for mu_ -- wake the sender, join it, then close.
+      // If THIS thread began it, it owns mu_ and releases it here (a mutex must not be
+      // destroyed locked).  Another thread's open exchange is a caller bug: that thread
+      // would call end() on a freed client, so it is refused loudly instead.
+      if (psp_owner_ != std::this_thread::get_id()) {
+        fprintf(stderr, "PSClient destroyed while another thread has a push_step_pull "
+                        "exchange open; aborting\n");
+        std::abort();
+      }
       for (int fd : fds_)
         if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
       stop_sender();
       close_fds();
+      psp_.active = false;
+      mu_.unlock();
       return;
     }
     if (PyGILState_Check()) {  // (Python dealloc): never wait for mu_ while holding the GIL
@@ -774,6 +799,7 @@ class PSClient {
       mu_.unlock();
       throw;
     }
+    psp_owner_ = std::this_thread::get_id();
     psp_.active = true;
   }
   int64_t push_step_pull_end() {
@@ -1024,10 +1050,7 @@ class PSClient {
           __builtin_ia32_pause();
         } else {
           std::unique_lock<std::mutex> lk(smu_);
-          // wait_until on the system clock: libstdc++'s wait_for (steady clock) goes through
-          // pthread_cond_clockwait, which ThreadSanitizer (GCC 11) does not intercept -- it then
-          // misses the unlock inside the wait and reports the next lock as a double lock
-          scv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(5), [this] {
+          cv_wait_ms(scv_, lk, 5, [this] {
             return send_state_.load(std::memory_order_acquire) == 1 ||
                    sender_stop_.load(std::memory_order_acquire);
           });
@@ -1118,6 +1141,7 @@ class PSClient {
     std::vector<std::string> hdrs, tails;  // the planned writes' own bytes, per task
     std::vector<std::vector<iovec>> iov;
   } psp_;
+  std::thread::id psp_owner_;  // the thread holding mu_ for the open exchange
   bool psp_async_ = false;
   std::thread sender_;
   std::mutex smu_;

@@ -190,12 +190,16 @@ void register_rccl(py::module_& m) {
   py::class_<RcclComm>(m, "RcclComm")
       .def(py::init<py::bytes, int, int, int>(), py::arg("unique_id"), py::arg("nranks"),
            py::arg("rank"), py::arg("device"))
+      // the collectives touch no Python object: they run without the GIL, so a collective
+      // blocked inside RCCL (e.g. connecting to a dead peer) cannot keep the peer watchdog's
+      // thread from entering abort() -- whose Use/inflight guard then really waits for it
       .def("all_reduce", &RcclComm::all_reduce, py::arg("send"), py::arg("recv"), py::arg("count"),
-           py::arg("dtype") = "float32", py::arg("op") = "sum", py::arg("stream") = 0)
-      .def("reduce_scatter", &RcclComm::reduce_scatter)
-      .def("all_gather", &RcclComm::all_gather)
-      .def("broadcast", &RcclComm::broadcast)
-      .def("all_to_all", &RcclComm::all_to_all)
+           py::arg("dtype") = "float32", py::arg("op") = "sum", py::arg("stream") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("reduce_scatter", &RcclComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
+      .def("all_gather", &RcclComm::all_gather, py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())
+      .def("all_to_all", &RcclComm::all_to_all, py::call_guard<py::gil_scoped_release>())
       .def("destroy", &RcclComm::destroy)
       .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
       .def("async_error", &RcclComm::async_error)

@@ -229,16 +229,18 @@ template <int W>
 __global__ __launch_bounds__(512) void xgmi_bw_kernel(float* __restrict__ g, long long n, int rank,
                                                       long long S, XgPeers peers,
                                                       unsigned* __restrict__ epochs,
-                                                      int* __restrict__ err, long long ticks) {
+                                                      int* __restrict__ err, long long ticks,
+                                                      const int* __restrict__ abort_word) {
   __shared__ unsigned s_epoch;
   __shared__ int s_fail;
   const int b = blockIdx.x, t = threadIdx.x, nt = blockDim.x, nb = gridDim.x;
   if (t == 0) {
     s_epoch = epochs[b] + 1;
-    // a communicator that already timed out (a peer is gone) is broken for good: calls queued
-    // behind the timed-out one leave at once instead of each waiting `ticks` again, so the
-    // stream drains within one timeout (the peer watchdog's drain window, parallel/watchdog.py)
-    s_fail = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a communicator that already timed out (a peer is gone) or was aborted by the host is
+    // broken for good: calls queued behind the failed one leave at once instead of each waiting
+    // `ticks` again, so the stream drains within one timeout
+    s_fail = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+             __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
   if (s_fail) return;
@@ -263,10 +265,23 @@ __global__ __launch_bounds__(512) void xgmi_bw_kernel(float* __restrict__ g, lon
     if (t < W && t != rank) {
       const unsigned* f = flag(rank, phase, t);
       const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      long long t_ab = t0;
       while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+        const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+        if (now - t0 > ticks) {
           s_fail = 1;
           break;
+        }
+        // the host's abort word (pinned host memory, set by the peer watchdog's abort hook:
+        // XgmiComm.abort) is read once per ~1 ms of waiting -- a PCIe round trip per spin
+        // would slow the flag poll -- so an aborted job's waves leave the GPU within ~1 ms
+        // instead of at the end of a long training timeout
+        if (now - t_ab > 100000) {
+          t_ab = now;
+          if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+            s_fail = 1;
+            break;
+          }
         }
         __builtin_amdgcn_s_sleep(1);
       }
@@ -366,12 +381,14 @@ long long xgmi_ll_bytes(int mode, int world, long long S) {
 }
 
 void xgmi_bw_launch(float* g, long long n, int rank, int world, long long S, const XgPeers& peers,
-                    unsigned* epochs, int* err, long long ticks, hipStream_t stream, int blocks) {
+                    unsigned* epochs, int* err, long long ticks, hipStream_t stream, int blocks,
+                    const int* abort_word) {
+  if (!abort_word) throw std::runtime_error("xgmi bw protocol: needs the host abort word");
   const dim3 grid(blocks), block(512);
 #define DTFX_BW(WW)                                                                          \
   case WW:                                                                                   \
     hipLaunchKernelGGL((xgmi_bw_kernel<WW>), grid, block, 0, stream, g, n, rank, S, peers,   \
-                       epochs, err, ticks);                                                  \
+                       epochs, err, ticks, abort_word);                                      \
     break;
   switch (world) {
     DTFX_BW(1) DTFX_BW(2) DTFX_BW(3) DTFX_BW(4) DTFX_BW(5) DTFX_BW(6) DTFX_BW(7) DTFX_BW(8)

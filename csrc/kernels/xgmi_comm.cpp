@@ -54,6 +54,12 @@ class XgmiAllReduce {
     XG_CHECK(hipMalloc(&epochs_, sizeof(unsigned) * XG_BLOCKS + sizeof(int)));
     XG_CHECK(hipMemset(epochs_, 0, sizeof(unsigned) * XG_BLOCKS + sizeof(int)));
     err_ = (int*)(epochs_ + XG_BLOCKS);
+    // host-visible abort word (pinned, mapped): abort() sets it with a plain host store -- no
+    // HIP call, so the peer watchdog's thread can run it while the stream is blocked -- and
+    // the bandwidth kernel's peer waits read it (xgmi_bw_kernel)
+    XG_CHECK(hipHostMalloc((void**)&abort_host_, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+    *abort_host_ = 0;
+    XG_CHECK(hipHostGetDevicePointer((void**)&abort_dev_, abort_host_, 0));
     XG_CHECK(hipMalloc(&mlp_epochs_, sizeof(unsigned) * MLP_XG_EPOCHS));
     XG_CHECK(hipMemset(mlp_epochs_, 0, sizeof(unsigned) * MLP_XG_EPOCHS));
     for (int i = 0; i < XG_MAX_WORLD; ++i) {
@@ -122,7 +128,7 @@ class XgmiAllReduce {
     const long long ticks = (long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
     if (mode_ == XG_BW)
       xgmi_bw_launch((float*)g, n, rank_, world_, S_, peers_, epochs_, err_, ticks,
-                     (hipStream_t)stream, bw_blocks_);
+                     (hipStream_t)stream, bw_blocks_, abort_dev_);
     else if (mode_ >= 0)
       xgmi_ll_launch(mode_, (float*)g, n, rank_, world_, S_, peers_, epochs_, err_, ticks,
                      (hipStream_t)stream);
@@ -270,7 +276,13 @@ class XgmiAllReduce {
   int error() {
     int e = 0;
     XG_CHECK(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost));
-    return e;
+    return e | (abort_host_ && __atomic_load_n(abort_host_, __ATOMIC_RELAXED));
+  }
+
+  // Peer-watchdog hook: release every bandwidth-mode wait of this communicator (running or
+  // queued) within ~1 ms.  A plain store to pinned host memory, safe from any thread.
+  void abort() {
+    if (abort_host_) __atomic_store_n(abort_host_, 1, __ATOMIC_RELEASE);
   }
 
   void close() {
@@ -279,6 +291,8 @@ class XgmiAllReduce {
     if (base_) hipFree(base_);
     if (epochs_) hipFree(epochs_);
     if (mlp_epochs_) hipFree(mlp_epochs_);
+    if (abort_host_) hipHostFree(abort_host_);
+    abort_host_ = abort_dev_ = nullptr;
     base_ = nullptr;
     epochs_ = nullptr;
     mlp_epochs_ = nullptr;
@@ -296,6 +310,8 @@ class XgmiAllReduce {
   unsigned* epochs_ = nullptr;
   unsigned* mlp_epochs_ = nullptr;
   int* err_ = nullptr;
+  int* abort_host_ = nullptr;  // pinned host abort word and its device mapping
+  int* abort_dev_ = nullptr;
   XgPeers peers_;
   std::vector<void*> opened_;
   bool ready_ = false;
@@ -345,6 +361,7 @@ void register_xgmi(py::module_& m) {
            py::arg("ring"), py::arg("B"), py::arg("dz1A"), py::arg("stream"),
            py::arg("timeout_s"), py::arg("flush"))
       .def("error", &dtfx::XgmiAllReduce::error)
+      .def("abort", &dtfx::XgmiAllReduce::abort, py::call_guard<py::gil_scoped_release>())
       .def("reset_epochs", &dtfx::XgmiAllReduce::reset_epochs)
       .def("close", &dtfx::XgmiAllReduce::close);
 }

@@ -159,10 +159,13 @@ def visible_gpu_index(env=None):
 
 
 def pin_to_numa_node(node, count=0, offset=0):
-    """Restrict this process (and the threads it starts) to allowed CPUs of ``node``: all of
-    them (``count`` 0), or ``count`` of them from position ``offset`` of the node's sorted list
-    (physical cores first; wraps).  Returns the CPU list, or None (unknown node / nothing
-    allowed there: left as it was)."""
+    """Restrict the calling thread -- and every thread it starts afterwards, so call it before
+    the first GPU call (the HIP runtime's threads) -- to allowed CPUs of ``node``: all of them
+    (``count`` 0), or the ``count`` CPUs at positions ``offset`` .. ``offset + count - 1`` of
+    the node's sorted list.  A slot that does not fit on the node (a small node or cpuset: it
+    would wrap onto another process's cores, e.g. a worker onto the ps cores) is not pinned:
+    a warning, and the placement is left to the scheduler.  Returns the CPU list, or None
+    (unknown node / nothing allowed there / slot does not fit: left as it was)."""
     if node is None:
         return None
     allowed = os.sched_getaffinity(0)
@@ -170,14 +173,23 @@ def pin_to_numa_node(node, count=0, offset=0):
     if not cpus:
         return None
     if count > 0:
-        cpus = [cpus[(offset + k) % len(cpus)] for k in range(min(count, len(cpus)))]
+        if offset + count > len(cpus):
+            import sys
+
+            print("[affinity] NUMA node %d has %d usable CPUs; slot %d..%d does not fit: not "
+                  "pinned (--cpu_affinity none placement)" % (int(node), len(cpus), offset,
+                                                              offset + count - 1),
+                  file=sys.stderr, flush=True)
+            return None
+        cpus = cpus[offset:offset + count]
     os.sched_setaffinity(0, cpus)
     return cpus
 
 
 # --cpu_affinity numa layout: ps task t on 8 consecutive cores (one shared-L3 core complex on
-# the EPYC hosts of this pool), worker i on 2 cores after the ps tasks' -- the cluster's
-# processes packed on one socket instead of spread by the scheduler over 256 CPUs
+# the EPYC hosts of this pool) of GPU 0's node; worker i on 2 cores of ITS GPU's node, at the
+# offset after the ps tasks' cores (the same positions are left free on every node, so a worker
+# on GPU 0's node never lands on a ps core) -- instead of spread by the scheduler over 256 CPUs
 PS_CPUS, WORKER_CPUS = 8, 2
 
 

@@ -196,9 +196,10 @@ def define_reference_flags(flag_values=FLAGS):
                   "in one GPU-resident store on the chief worker's GPU, IPC-mapped by every "
                   "worker (pull / apply / global_step over xGMI; async PS only)", fv)
     DEFINE_string("cpu_affinity", "numa",
-                  "async PS: numa = the cluster's processes packed on ONE NUMA node (--numa_node, "
-                  "else GPU 0's node, else node 0): ps task t on 8 cores, worker i on 2 cores "
-                  "after them -- Hogwild applies and pulls of several connection threads "
+                  "async PS: numa = the ps tasks on GPU 0's NUMA node (--numa_node overrides), "
+                  "8 cores each; worker i on 2 cores of its OWN GPU's node, after the ps tasks' "
+                  "core positions; a slot that does not fit on its node is left unpinned "
+                  "(warning) -- Hogwild applies and pulls of several connection threads "
                   "scattered over two sockets bounce the same cache lines across the socket "
                   "link | none", fv)
     DEFINE_integer("numa_node", -1, "--cpu_affinity numa: the ps process's node (-1: auto)", fv)

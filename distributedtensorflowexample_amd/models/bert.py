@@ -45,12 +45,6 @@ BF16 = torch.bfloat16
 # edges cost ~15 us of idle GPU each, but starting each weight gradient as soon as its operand
 # exists overlaps more of the data-gradient chain.
 _WGRAD_BATCH = os.environ.get("DTFX_BERT_WGRAD_BATCH", "0") == "1"
-# DTFX_BERT_LIB_GEMM=1: the GEMMs with no fused epilogue beyond a bias go to hipBLASLt
-# (torch.addmm / torch.mm): the QKV projection (N = 2304 over K = 768: 69 vs 82 us for this
-# repo's best tile), the attention-output data gradient (26 vs 30 us) and the bf16 decoder
-# logits (121 vs 173 us); every GEMM with a residual / GELU / column-sum epilogue, and the
-# decoder's data gradient, measured faster here (tools/probes/blaslt_bert.py, profiles/r5/blaslt/)
-_LIB_GEMM = os.environ.get("DTFX_BERT_LIB_GEMM", "1") == "1"
 # DTFX_BERT_GELU_DSAVE=1: the FFN input GEMM stores gelu'(u) (from the sigmoid its GELU computes
 # anyway) instead of the pre-activation u, so the FFN output dgrad's epilogue is one multiply
 # instead of a second exp + rcp + ~8 VALU per element
@@ -244,11 +238,8 @@ class BertMLM:
     def _layer_fwd(self, l, x, batch, seq, kmask):
         cfg, p = self.cfg, self.params
         pre = "encoder/layer_%d/" % l
-        if _LIB_GEMM:  # (bias from the bf16 working copy: hipBLASLt's bias epilogue wants C's type)
-            qkv = torch.addmm(p.W(pre + "attention/qkv/bias"), x, p.W(pre + "attention/qkv/kernel").t())
-        else:
-            qkv = B16.gemm(x, p.W(pre + "attention/qkv/kernel"), False, True,
-                           bias=p.P(pre + "attention/qkv/bias"))
+        qkv = B16.gemm(x, p.W(pre + "attention/qkv/kernel"), False, True,
+                       bias=p.P(pre + "attention/qkv/bias"))
         ctx, lse = TR.attn_fwd(qkv, batch, seq, cfg.heads, kmask)
         a = B16.gemm(ctx, p.W(pre + "attention/output/dense/kernel"), False, True,
                      bias=p.P(pre + "attention/output/dense/bias"), residual=x)
@@ -299,11 +290,8 @@ class BertMLM:
         tn, mt, rt = TR.layernorm_fwd(t, p.P("cls/predictions/transform/LayerNorm/gamma"),
                                       p.P("cls/predictions/transform/LayerNorm/beta"), cfg.eps)
         E = p.W("embeddings/word_embeddings")
-        if _BF16_LOGITS and _LIB_GEMM:  # bias-only bf16 product: hipBLASLt 121 vs 173 us here
-            logits = torch.addmm(p.W("cls/predictions/output_bias"), tn, E.t())
-        else:
-            logits = B16.gemm(tn, E, False, True, bias=p.P("cls/predictions/output_bias"),
-                              out_dtype=BF16 if _BF16_LOGITS else torch.float32)
+        logits = B16.gemm(tn, E, False, True, bias=p.P("cls/predictions/output_bias"),
+                          out_dtype=BF16 if _BF16_LOGITS else torch.float32)
         Tm = tn.shape[0]
         scale = 1.0 / max(1, n_valid if n_valid is not None else Tm)
         loss_rows, correct, dlog_b = TR.mlm_xent(logits, mask_labels, cfg.vocab_size, scale)
@@ -396,10 +384,7 @@ class BertMLM:
                               p.G(pre + "attention/output/LayerNorm/beta"),
                               dxsum=p.G(pre + "attention/output/dense/bias"))
         wgrad(da, ctx, pre + "attention/output/dense/kernel")
-        if _LIB_GEMM:
-            dctx = torch.mm(da, p.W(pre + "attention/output/dense/kernel"))
-        else:
-            dctx = B16.gemm(da, p.W(pre + "attention/output/dense/kernel"))
+        dctx = B16.gemm(da, p.W(pre + "attention/output/dense/kernel"))
         dqkv = TR.attn_bwd(qkv, ctx, dctx, lse, batch, seq, cfg.heads, kmask,
                            dbias=p.G(pre + "attention/qkv/bias"))
         wgrad(dqkv, x, pre + "attention/qkv/kernel")

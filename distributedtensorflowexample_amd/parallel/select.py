@@ -324,6 +324,14 @@ class HybridComm:
     def failed(self):
         return self.bw.failed() or bool(getattr(self.rccl, "failed", lambda: False)())
 
+    def abort(self):
+        """Peer-watchdog hook: release the two-shot's peer waits (host abort word), then
+        abort the RCCL communicator."""
+        self.bw.abort()
+        ab = getattr(self.rccl, "abort", None)
+        if callable(ab):
+            ab()
+
     def __getattr__(self, name):  # broadcast_, reduce_scatter, all_gather, barrier, ...
         return getattr(self.rccl, name)
 
@@ -352,14 +360,16 @@ def pick_large_allreduce(rccl, world, rank, dev, max_numel, sizes=None, iters=10
     world-8 step (tools/probes/dp_sim.py, profiles/r5/dp_sim/) ran BERT-base +7.4 % over the
     1-GPU step with 128 against +8.5 % with 256 (+8.0 % with 64), ResNet-50 +5.7 % against +6.5 %.
 
-    Default ``train_timeout_s``: ``min(120, peer_timeout_s)``.  The peer watchdog
-    (``--peer_timeout_secs``) declares a silent peer lost after ``peer_timeout_s``, drains for
-    10 s and ends the process; a two-shot waiting on that peer must have left the GPU by then,
-    and once one call timed out the calls queued behind it exit at entry (the kernel reads
-    the communicator's error word first), so the stream drains within one timeout."""
+    Default ``train_timeout_s``: 120 s, independent of the peer watchdog's timeout, so a live
+    but slow peer (a chief writing a checkpoint while its heartbeats still flow) does not time
+    the two-shot out.  A peer that is really lost is the watchdog's job
+    (``--peer_timeout_secs``): its abort hook (``HybridComm.abort`` -> ``XgmiComm.abort``) sets
+    the communicator's host-visible abort word, which the kernel's peer waits poll about once
+    per millisecond, and calls queued behind read it at entry -- so the two-shot leaves the GPU
+    within the watchdog's drain window, before it ends the process.  ``peer_timeout_s`` is
+    accepted for compatibility and not used."""
     if train_timeout_s is None:
-        train_timeout_s = min(120.0, float(peer_timeout_s)) if peer_timeout_s and peer_timeout_s > 0 \
-            else 120.0
+        train_timeout_s = 120.0
     max_numel = int(max_numel)
     sizes = [s for s in (sizes or (1 << 18, 1 << 20, 1 << 22, 7 << 20, 1 << 24))
              if s <= max_numel] or [max_numel]

@@ -184,6 +184,14 @@ class XgmiComm:
         if self._h.error():
             raise RuntimeError("xGMI all-reduce timed out waiting for a peer")
 
+    def abort(self):
+        """Peer-watchdog abort hook: every bandwidth-mode peer wait of this communicator
+        (running or queued) gives up within ~1 ms and latches ``failed()``.  A host store to a
+        pinned word -- no HIP call, no GIL held in C++ -- so it is safe from the watchdog
+        thread while the stream is blocked in the kernel."""
+        if self._h is not None:
+            self._h.abort()
+
     def destroy(self):
         self._h.close()
 

@@ -43,6 +43,7 @@ import time
 import torch
 
 from ..ops import mlp_step, optim
+from ..ops._ext import stream_handle
 
 
 class FusedMLPTrainer:
@@ -303,11 +304,10 @@ class FusedMLPTrainer:
             ws = self.ws
             a = self._host_args = (hip().mlp_run_pipelined, ptr(self.bufs[0]), ptr(self.bufs[1]),
                                    ptr(self.x), ptr(self.labels), ptr(ws.buf), ptr(ws.ctr),
-                                   ptr(ws.stats), ws.stats_ring)
-        fn, p0, p1, xp, lp, wb, wc, wst, ring = a
+                                   ptr(ws.stats), ws.stats_ring, self.device.index)
+        fn, p0, p1, xp, lp, wb, wc, wst, ring, dix = a
         fn(p0, p1, self.cur, 1 if self.pending else 0, self.lr, xp, lp, self.nbatches, self.pos,
-           steps, wb, wc, wst, ring, self.B, torch.cuda.current_stream(self.device).cuda_stream,
-           1 if flush else 0)
+           steps, wb, wc, wst, ring, self.B, stream_handle(dix), 1 if flush else 0)
         self.pos = (self.pos + steps) % self.nbatches
         self.cur ^= (steps + (1 if flush else 0)) & 1
         self.pending = not flush
@@ -330,7 +330,7 @@ class FusedMLPTrainer:
         fn, p0, p1, xp, lp, wb, wc, wst, ring, dz = a
         fn(kind, p0, p1, self.cur, 1 if self.pending else 0, self.lr / self.world_size, xp,
            int(self.xstride), lp, self.nbatches, self.pos, steps, wb, wc, wst, ring, self.B, dz,
-           torch.cuda.current_stream(self.device).cuda_stream, float(comm.timeout_s),
+           stream_handle(self.device.index), float(comm.timeout_s),
            1 if flush else 0)
         self.pos = (self.pos + steps) % self.nbatches
         self.cur ^= (steps + (1 if (flush and not factor) else 0)) & 1

@@ -90,7 +90,8 @@ def main(argv=None):
         from distributedtensorflowexample_amd.config import apply_hip_schedule
         from distributedtensorflowexample_amd.train.worker import Worker
 
-        apply_hip_schedule()  # DTFX_HIP_SCHED (before the first GPU call)
+        # pinned first: the affinity of the calling thread is inherited by the threads started
+        # after it, so the HIP runtime's threads (apply_hip_schedule may start them) follow
         if getattr(FLAGS, "cpu_affinity", "none") == "numa":
             from distributedtensorflowexample_amd.config import (first_gpu_numa_node_sysfs,
                                                                  pin_to_numa_node,
@@ -103,6 +104,7 @@ def main(argv=None):
                     else first_gpu_numa_node_sysfs(index=visible_gpu_index()))
             pin_to_numa_node(0 if node is None else node,
                              *worker_cpu_slot(FLAGS.task_index, FLAGS.num_ps))
+        apply_hip_schedule()  # DTFX_HIP_SCHED (before the first GPU call)
         mnist = read_data_sets(FLAGS.data_dir or None, one_hot=True)
         config = ConfigProto(gpu_options=gpu_options)
         server = Server(cluster, job_name="worker", task_index=FLAGS.task_index, config=config)

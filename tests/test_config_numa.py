@@ -69,10 +69,11 @@ def test_pin_to_numa_node(monkeypatch):
     got = []
     monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: got.append(list(cpus)))
     assert config.pin_to_numa_node(1) == [4, 5, 6]        # allowed CPUs of the node only
-    assert config.pin_to_numa_node(0, count=2, offset=3) == [3, 0]  # wraps
+    assert config.pin_to_numa_node(0, count=2, offset=2) == [2, 3]  # a slot inside the node
+    assert config.pin_to_numa_node(0, count=2, offset=3) is None    # would wrap: not pinned
     assert config.pin_to_numa_node(None) is None
     assert config.pin_to_numa_node(5) is None            # unknown node: left alone
-    assert got == [[4, 5, 6], [3, 0]]
+    assert got == [[4, 5, 6], [2, 3]]
 
 
 def test_hip_schedule_modes(monkeypatch):
