@@ -1207,12 +1207,54 @@ long long gemm_bf16_ws_floats(bool ta, bool out_f32, int M, int N, int K, int sp
   return s > 1 ? (long long)s * M * N : 0;
 }
 
+static void gemm_bf16_launch_cfg(bool ta, bool tb, bool out_f32, int M, int N, int K, const void* A,
+                                 int lda, const void* B, int ldb, void* C, int ldc, float alpha,
+                                 float beta, const float* bias, int act, const void* aux_in,
+                                 void* aux_out, int ld_aux, const void* residual, int ld_res,
+                                 int act_grad, int splitk, int batch, long long sA, long long sB,
+                                 long long sC, float* colsum, hipStream_t stream, float* ws,
+                                 long long ws_floats, bool defer_reduce, int force_cfg);
+
+// Tail split of an 8-phase GEMM whose 256x256 tiles fill F >= 1 whole rounds of the 256 CUs
+// plus a sparse last one (<= half the CUs busy for a whole tile's time): the rows of the whole
+// rounds stay on the 8-phase tile, the remaining rows go to the 128x128 tile (two resident
+// blocks per CU, a quarter of the work per block), so the tail costs ~half a round instead of
+// a full one.  BERT-base's QKV projection (16384 x 2304, K = 768): 576 tiles = 2.25 rounds ->
+// 56 tile rows (504 tiles, 2 rounds) + 2048 rows x 2304 on 288 128x128 blocks.  Row-local
+// epilogues only (bias / act / aux / residual; column sums accumulate from both parts);
+// DTFX_GEMM_TAILSPLIT=0 turns it off.  Returns the rows left for the 8-phase part (M: none).
+static int gemm_tail_rows(int M, int N, int cfg, bool ta, int splitk, int batch) {
+  static const bool on = [] {
+    const char* e = getenv("DTFX_GEMM_TAILSPLIT");
+    return !(e && atoi(e) == 0);
+  }();
+  if (!on || cfg != 5 || ta || splitk > 1 || batch != 1) return M;
+  const int tm = (M + 255) / 256, tn = (N + 255) / 256;
+  const long long T = (long long)tm * tn;
+  const long long F = T / 256, R = T % 256;
+  if (F < 1 || R == 0 || R > 128) return M;
+  const int rows5 = (int)(F * 256 / tn) * 256;
+  return rows5 > 0 && rows5 < M ? rows5 : M;
+}
+
 void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const void* A, int lda,
                       const void* B, int ldb, void* C, int ldc, float alpha, float beta,
                       const float* bias, int act, const void* aux_in, void* aux_out, int ld_aux,
                       const void* residual, int ld_res, int act_grad, int splitk, int batch,
                       long long sA, long long sB, long long sC, float* colsum,
                       hipStream_t stream, float* ws, long long ws_floats, bool defer_reduce) {
+  gemm_bf16_launch_cfg(ta, tb, out_f32, M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, bias, act,
+                       aux_in, aux_out, ld_aux, residual, ld_res, act_grad, splitk, batch, sA, sB,
+                       sC, colsum, stream, ws, ws_floats, defer_reduce, -1);
+}
+
+static void gemm_bf16_launch_cfg(bool ta, bool tb, bool out_f32, int M, int N, int K, const void* A,
+                                 int lda, const void* B, int ldb, void* C, int ldc, float alpha,
+                                 float beta, const float* bias, int act, const void* aux_in,
+                                 void* aux_out, int ld_aux, const void* residual, int ld_res,
+                                 int act_grad, int splitk, int batch, long long sA, long long sB,
+                                 long long sC, float* colsum, hipStream_t stream, float* ws,
+                                 long long ws_floats, bool defer_reduce, int force_cfg) {
   if (M <= 0 || N <= 0 || batch <= 0) return;
   if (batch > 1 && (bias || aux_in || aux_out || residual || colsum))
     throw std::runtime_error("gemm_bf16: batched GEMM supports alpha/beta/act epilogues only");
@@ -1237,6 +1279,27 @@ void gemm_bf16_launch(bool ta, bool tb, bool out_f32, int M, int N, int K, const
   const bool plain = !colsum && !bias && !act && !act_grad && !residual && !aux_out;
   int cfg;
   splitk = gemm_splitk(ta, out_f32, M, N, K, splitk, batch, beta, plain, &cfg);
+  if (force_cfg >= 0) {
+    cfg = force_cfg;
+  } else {
+    const int rows5 = gemm_tail_rows(M, N, cfg, ta, splitk, batch);
+    if (rows5 < M) {
+      const size_t eb = out_f32 ? 4 : 2;
+      auto adv = [](const void* p, size_t bytes) -> const void* {
+        return p ? (const void*)((const char*)p + bytes) : nullptr;
+      };
+      gemm_bf16_launch_cfg(ta, tb, out_f32, rows5, N, K, A, lda, B, ldb, C, ldc, alpha, beta,
+                           bias, act, aux_in, aux_out, ld_aux, residual, ld_res, act_grad, 1, 1,
+                           0, 0, 0, colsum, stream, ws, ws_floats, defer_reduce, 5);
+      gemm_bf16_launch_cfg(ta, tb, out_f32, M - rows5, N, K, adv(A, (size_t)rows5 * lda * 2), lda,
+                           B, ldb, (void*)adv(C, (size_t)rows5 * ldc * eb), ldc, alpha, beta,
+                           bias, act, adv(aux_in, (size_t)rows5 * ld_aux * 2),
+                           (void*)adv(aux_out, (size_t)rows5 * ld_aux * 2), ld_aux,
+                           adv(residual, (size_t)rows5 * ld_res * 2), ld_res, act_grad, 1, 1, 0,
+                           0, 0, colsum, stream, ws, ws_floats, defer_reduce, 0);
+      return;
+    }
+  }
   if (splitk > 1) {
     if (batch > 1) throw std::runtime_error("gemm_bf16: split-K with batch > 1 is not supported");
     if (!out_f32 || bias || act || act_grad || residual || aux_out || colsum ||

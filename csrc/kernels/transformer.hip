@@ -487,10 +487,31 @@ constexpr int LDP = SP * 2 + 16;   // 272 B
 constexpr int QB = SP * LDQ;       // 18432 B
 constexpr int PB = SP * LDP;       // 34816 B
 
+// XOR-swizzled [rows][64] bf16 images with unpadded 128-B rows (attn_fwd_kernel,
+// attn_bwd_half_kernel): 16-B chunk c of row r sits at chunk c ^ swz(r).  Every image is read
+// both as rows (ds_read_b128, lfrag_sw<true>) and transposed (ds_read_b64_tr_b16,
+// lfrag_sw<false>); the 144-B padded rows were 2-way conflicted on both (the b128 group's rows
+// 4 and 13 on one slot, the tr read's rows q and q + 8 likewise: 36-41 % conflict cycles in
+// the BERT step's counters).  swz(r) (a linear map of r's low 4 bits, found by exhaustive
+// search over them) gives conflict-free b128 row reads -- each 16-lane group's rows {0-3,
+// 12-15} at chunk c and {4-11} at c ^ 1 land on 16 distinct slots -- and conflict-free tr reads
+// -- the rows {R..R+3, R+8..R+11} of a 32-lane half, two chunks each, on 16 distinct slots --
+// and keeps the P^T / dS^T 8-byte stores at 2-way, as before.
+constexpr int LDK = D * 2;         // 128 B
+constexpr int KB = SP * LDK;       // 16384 B
+__device__ __forceinline__ int swz(int r) {
+  return (__builtin_popcount(r & 15) & 1) | ((__builtin_popcount(r & 14) & 1) << 1) |
+         (((r >> 3) & 1) << 2);
+}
+// byte offset of element (row r, column col) of a swizzled image
+__device__ __forceinline__ int sw_off(int r, int col) {
+  return r * LDK + ((((col >> 3) ^ swz(r))) << 4) + (col & 7) * 2;
+}
+
 // Load N [S][64] head slices (row stride ld[i] elements) into LDS, zero rows >= S.  All
 // 4N 16-B loads of a thread are issued before the first LDS store (one memory round trip
 // instead of 4N dependent load -> store pairs).
-template <int N, int NT = 256>
+template <int N, int NT = 256, bool SWZ = false>
 __device__ __forceinline__ void load_heads(char* const (&dst)[N], const unsigned short* const (&src)[N],
                                            const int (&ld)[N], int S) {
   constexpr int PER = SP * 8 / NT;  // 16-B chunks per thread per head (NT threads)
@@ -508,8 +529,50 @@ __device__ __forceinline__ void load_heads(char* const (&dst)[N], const unsigned
     for (int k = 0; k < PER; ++k) {
       const int i = threadIdx.x + NT * k, r = i >> 3, c = i & 7;
       if (r >= S) v[n][k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      *(bf16x8*)(dst[n] + r * LDQ + c * 16) = v[n][k];
+      *(bf16x8*)(dst[n] + (SWZ ? r * LDK + ((c ^ swz(r)) << 4) : r * LDQ + c * 16)) = v[n][k];
     }
+}
+
+// lfrag over a swizzled image (same lane map as tf::lfrag).  swz is XOR-linear in the row's
+// low 4 bits and every fragment's first row is a multiple of 16 (row reads) or of 8 with the
+// lane's rows fixed modulo 16 (tr reads), so each lane's chunk XORs are constants computed once
+// (SwLane): a row read is one immediate offset, a tr read one XOR per fragment.
+struct SwLane {
+  int rr;  // row reads: the lane's byte offset for k0 = 0 (k0 = 32: ^ 64, since swz(r) < 8)
+  int tb;  // tr reads, lo row: row + in-chunk byte offset (k0, o0 excluded; hi row: + 4 rows)
+  int ct;  // tr reads, lo row: chunk XOR (hi row: ^ swz(4) = 3, swz being linear and the lo
+           // row's bit 2 clear)
+};
+__device__ __forceinline__ SwLane sw_lane(int lane) {
+  // (recomputed at each use from the lane id, a handful of VALU: the half backward sits at its
+  //  128-VGPR budget, and three long-lived registers more made it spill)
+  SwLane w;
+  const int l15 = lane & 15, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  w.rr = l15 * LDK + (((lane >> 4) ^ swz(l15)) << 4);
+  w.tb = (8 * g + q) * LDK + ((4 * p) & 7) * 2;
+  w.ct = (p >> 1) ^ swz(8 * (g & 1) + q);
+  return w;
+}
+template <bool KC>
+__device__ __forceinline__ bf16x8 lfrag_sw(const char* base, int o0, int k0, int lane) {
+  const SwLane w = sw_lane(lane);
+  if (KC) {  // k0 in {0, 32} (64-column images)
+    return *(const bf16x8*)(base + o0 * LDK + (w.rr ^ (k0 << 1)));
+  } else {   // o0 a multiple of 16, k0 of 32
+    // (the chunk XOR is formed at each read -- two VALU -- from an opaque copy of the lane's
+    //  row offset: hoisted, the 8 distinct (o0, lo / hi) offsets of a loop stay live and the
+    //  half backward, at its 128-VGPR budget, spilled)
+    int x = w.tb + (w.ct << 4);
+    asm volatile("" : "+v"(x));
+    const char* b = base + k0 * LDK;
+    bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(b + (x ^ (o0 << 1))));
+    bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_bf16x4*)(b + 4 * LDK + (x ^ (o0 << 1) ^ (3 << 4))));
+    bf16x8 v;
+    v.lo = lo;
+    v.hi = hi;
+    return v;
+  }
 }
 }  // namespace at
 
@@ -521,9 +584,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     float* __restrict__ lse, const float* __restrict__ kmask, float scale) {
   using namespace at;
   extern __shared__ __attribute__((aligned(16))) char sm[];
-  char* Ks = sm;
-  char* Vs = sm + QB;
-  char* Ps = sm + 2 * QB;
+  char* Ks = sm;  // swizzled images (at::swz)
+  char* Vs = sm + KB;
+  char* Ps = sm + 2 * KB;
   const int b = blockIdx.x / nh, h = blockIdx.x % nh;
   const int Hd = nh * D, ld = 3 * Hd;
   const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
@@ -544,7 +607,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     char* const dst[2] = {Ks, Vs};
     const unsigned short* const src[2] = {base + Hd, base + 2 * Hd};
     const int lds[2] = {ld, ld};
-    at::load_heads<2>(dst, src, lds, S);
+    at::load_heads<2, 256, true>(dst, src, lds, S);
   }
   __syncthreads();
 
@@ -564,7 +627,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     for (int kk = 0; kk < 2; ++kk) {
       const bf16x8 a = qf[i][kk];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = mma(a, lfrag<true>(Ks, LDQ, 16 * j, 32 * kk, lane), acc[j]);
+      for (int j = 0; j < 8; ++j) acc[j] = mma(a, lfrag_sw<true>(Ks, 16 * j, 32 * kk, lane), acc[j]);
     }
     // row softmax: row r0 + rg + r lives in the 16 lanes of this row group x 8 tiles
 #pragma unroll
@@ -604,7 +667,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     for (int kk = 0; kk < 4; ++kk) {
       const bf16x8 a = lfrag<true>(Ps, LDP, r0, 32 * kk, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = mma(a, lfrag<false>(Vs, LDQ, 16 * j, 32 * kk, lane), o[j]);
+      for (int j = 0; j < 4; ++j) o[j] = mma(a, lfrag_sw<false>(Vs, 16 * j, 32 * kk, lane), o[j]);
     }
     // through this wave's own P rows (consumed by the products above): 2 16-B stores per
     // lane instead of 16 2-byte stores
@@ -996,9 +1059,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_persist_kernel(
 // half.  P = exp(S * scale + mask - lse) needs no row maximum, so any tiling works.
 namespace atb {
 constexpr int HQ = 64;                  // queries per half
-constexpr int QH = HQ * at::LDQ;        // 9216 B
-constexpr int PT = at::SP * at::LDQ;    // [128 keys][64 queries] with 144-B rows: 18432 B
-constexpr int LDS = at::QB + 2 * QH + 2 * PT + HQ * 4;  // 73984
+constexpr int QH = HQ * at::LDK;        // 8192 B (swizzled images, at::swz)
+constexpr int PT = at::SP * at::LDK;    // [128 keys][64 queries], 128-B rows: 16384 B
+constexpr int LDS = at::KB + 2 * QH + 2 * PT + HQ * 4;  // 65792
 }  // namespace atb
 
 __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
@@ -1010,7 +1073,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
   using namespace atb;
   extern __shared__ __attribute__((aligned(16))) char sm[];
   char* Ks = sm;
-  char* Qh = Ks + QB;
+  char* Qh = Ks + KB;
   char* dOh = Qh + QH;
   char* PTs = dOh + QH;
   char* dSTs = PTs + PT;
@@ -1033,7 +1096,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int e = tid + 512 * k;
-      *(bf16x8*)(Ks + (e >> 3) * LDQ + (e & 7) * 16) = kv[k];
+      *(bf16x8*)(Ks + (e >> 3) * LDK + (((e & 7) ^ swz(e >> 3)) << 4)) = kv[k];
     }
   }
   const float* L = lse + ((size_t)b * nh + h) * SP;
@@ -1061,8 +1124,8 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
         dv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       }
       __syncthreads();  // the previous half's phase 2 is done with Q_h / dO_h / P^T / dS^T
-      *(bf16x8*)(Qh + r * LDQ + c * 16) = qv;
-      *(bf16x8*)(dOh + r * LDQ + c * 16) = dv;
+      *(bf16x8*)(Qh + r * LDK + ((c ^ swz(r)) << 4)) = qv;
+      *(bf16x8*)(dOh + r * LDK + ((c ^ swz(r)) << 4)) = dv;
       if (c == 0) Dr[r] = row < S ? d : 0.f;
       __syncthreads();
     }
@@ -1071,8 +1134,8 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
       bf16x8 aq[2], ado[2];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        aq[kk] = lfrag<true>(Qh, LDQ, 16 * qt, 32 * kk, lane);
-        ado[kk] = lfrag<true>(dOh, LDQ, 16 * qt, 32 * kk, lane);
+        aq[kk] = lfrag_sw<true>(Qh, 16 * qt, 32 * kk, lane);
+        ado[kk] = lfrag_sw<true>(dOh, 16 * qt, 32 * kk, lane);
       }
       float lr[4], dr[4];
       bool live[4];
@@ -1083,6 +1146,8 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
         lr[r] = live[r] ? L[row] : 0.f;
         dr[r] = Dr[ql];
       }
+      // the lane's P^T / dS^T store offset within a key tile (swz(16 kt + cl) = swz(cl))
+      const int poff = sw_off(cl, 16 * qt + rg);
 #pragma unroll 1
       for (int j = 0; j < 4; ++j) {
         const int kt = kt0 + j, key = 16 * kt + cl;
@@ -1092,7 +1157,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
         for (int kk = 0; kk < 2; ++kk) {
           bf16x8 vb = *(const bf16x8*)(base + 2 * Hd + (size_t)min(key, S - 1) * ld + 32 * kk + 8 * g);
           if (key >= S) vb = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-          sa = mma(aq[kk], lfrag<true>(Ks, LDQ, 16 * kt, 32 * kk, lane), sa);
+          sa = mma(aq[kk], lfrag_sw<true>(Ks, 16 * kt, 32 * kk, lane), sa);
           dp = mma(ado[kk], vb, dp);
         }
         bf16x4 pv, dsv;
@@ -1102,7 +1167,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
           pv[r] = (short)tobf(p);
           dsv[r] = (short)tobf(p * (dp[r] - dr[r]));
         }
-        const int off = key * LDQ + (16 * qt + rg) * 2;
+        const int off = kt * (16 * LDK) + poff;  // = sw_off(key, 16 qt + rg)
         *(bf16x4*)(PTs + off) = pv;
         *(bf16x4*)(dSTs + off) = dsv;
       }
@@ -1111,12 +1176,12 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
     // phase 2: dV += P^T dO_h, dK += dS^T Q_h (key tile `wave`); dQ_h = dS K
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 pT = lfrag<true>(PTs, LDQ, 16 * wave, 32 * kk, lane);
-      const bf16x8 dsT = lfrag<true>(dSTs, LDQ, 16 * wave, 32 * kk, lane);
+      const bf16x8 pT = lfrag_sw<true>(PTs, 16 * wave, 32 * kk, lane);
+      const bf16x8 dsT = lfrag_sw<true>(dSTs, 16 * wave, 32 * kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        av[j] = mma(pT, lfrag<false>(dOh, LDQ, 16 * j, 32 * kk, lane), av[j]);
-        ak[j] = mma(dsT, lfrag<false>(Qh, LDQ, 16 * j, 32 * kk, lane), ak[j]);
+        av[j] = mma(pT, lfrag_sw<false>(dOh, 16 * j, 32 * kk, lane), av[j]);
+        ak[j] = mma(dsT, lfrag_sw<false>(Qh, 16 * j, 32 * kk, lane), ak[j]);
       }
     }
     {
@@ -1125,10 +1190,10 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
       aq[0] = aq[1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8 dsr = lfrag<false>(dSTs, LDQ, 16 * qt, 32 * kk, lane);
+        const bf16x8 dsr = lfrag_sw<false>(dSTs, 16 * qt, 32 * kk, lane);
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
-          aq[jj] = mma(dsr, lfrag<false>(Ks, LDQ, 16 * (dt0 + jj), 32 * kk, lane), aq[jj]);
+          aq[jj] = mma(dsr, lfrag_sw<false>(Ks, 16 * (dt0 + jj), 32 * kk, lane), aq[jj]);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1545,7 +1610,7 @@ static void check_attn(int S, int nh) {
 void attn_fwd_launch(int Bn, int S, int nh, const void* qkv, void* out, float* lse,
                      const float* kmask, float scale, hipStream_t s) {
   check_attn(S, nh);
-  const size_t lds = 2 * at::QB + at::PB;
+  const size_t lds = 2 * at::KB + at::PB;
   static bool attr = false;
   if (!attr) {
     DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_kernel,

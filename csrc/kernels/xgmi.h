@@ -25,7 +25,7 @@ long long xgmi_ll_bytes(int mode, int world, long long S);
 // bandwidth-mode two-shot all-reduce for large buckets (f32 payload + release flags)
 void xgmi_bw_launch(float* g, long long n, int rank, int world, long long S, const XgPeers& peers,
                     unsigned* epochs, int* err, long long ticks, hipStream_t stream,
-                    int blocks, const int* abort_word);
+                    int blocks, const int* abort_word, int op = 0);
 
 void xgmi_ll_launch(int mode, float* g, long long n, int rank, int world, long long S,
                     const XgPeers& peers, unsigned* epochs, int* err, long long ticks,

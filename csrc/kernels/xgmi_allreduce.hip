@@ -220,12 +220,17 @@ __global__ __launch_bounds__(256) void xgmi_ll_kernel(float* __restrict__ g, lon
 // slots alternate by epoch parity (the flag protocol's argument: a rank reaches epoch e+2
 // only after every peer finished epoch e).  Every wait is bounded (s_memrealtime).
 // Region of one rank (floats): rs [2][W][CS] | ag [2][S]; flags [2 phases][W][XG_BLOCKS].
+// OP 0 is that all-reduce; the owner-sharded optimizer (ZeRO-1, train/bert_trainer.py) uses
+// its halves alone: OP 1 = reduce-scatter (step 1 and the owner sum, kept in g's chunk r,
+// nothing pushed), OP 2 = all-gather (g's chunk r is already final: step 2's push of it, then
+// step 3).  The epoch / parity argument holds for any sequence of the three: every call waits
+// on all peers' flags after its own writes and before its reads of the slots.
 // ---------------------------------------------------------------------------
 __host__ __device__ inline long long xg_bw_cs(long long S, int W) {
   return ((S + W - 1) / W + 3) / 4 * 4;
 }
 
-template <int W>
+template <int W, int OP>
 __global__ __launch_bounds__(512) void xgmi_bw_kernel(float* __restrict__ g, long long n, int rank,
                                                       long long S, XgPeers peers,
                                                       unsigned* __restrict__ epochs,
@@ -310,6 +315,7 @@ __global__ __launch_bounds__(512) void xgmi_bw_kernel(float* __restrict__ g, lon
   };
   // 1) reduce-scatter sends: my share of chunk q -> rs(q, par, me), all peers interleaved
   //    so every link carries traffic at once
+  if constexpr (OP != 2) {
   for (int k = 1; k < W; ++k) {
     const int q = (rank + k) % W;
     const long long m = chunk_hi(q);
@@ -326,7 +332,9 @@ __global__ __launch_bounds__(512) void xgmi_bw_kernel(float* __restrict__ g, lon
     if (t == 0) atomicExch(err, 1);
     return;
   }
+  }  // OP != 2
   // 2) owner: rank-ordered sum of my chunk's sub-range, kept in g and pushed to every peer
+  //    (OP 1: kept only; OP 2: my chunk is final already -- pushed only)
   {
     const long long m = chunk_hi(rank);
     if (m > 0) {
@@ -334,24 +342,41 @@ __global__ __launch_bounds__(512) void xgmi_bw_kernel(float* __restrict__ g, lon
       const long long m4 = m >> 2;
       for (long long i = t; i < m4; i += nt) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (OP == 2) {
+          acc = ((const f32x4*)mine)[i];
+        } else {
 #pragma unroll
-        for (int j = 0; j < W; ++j) {
-          const f32x4 v = j == rank ? ((const f32x4*)mine)[i] : ((const f32x4*)(rs(rank, j) + lo))[i];
-          acc += v;
+          for (int j = 0; j < W; ++j) {
+            const f32x4 v = j == rank ? ((const f32x4*)mine)[i] : ((const f32x4*)(rs(rank, j) + lo))[i];
+            acc += v;
+          }
+          ((f32x4*)mine)[i] = acc;
         }
-        ((f32x4*)mine)[i] = acc;
+        if constexpr (OP != 1) {
 #pragma unroll
-        for (int k = 1; k < W; ++k) ((f32x4*)(ag((rank + k) % W) + rank * cs + lo))[i] = acc;
+          for (int k = 1; k < W; ++k) ((f32x4*)(ag((rank + k) % W) + rank * cs + lo))[i] = acc;
+        }
       }
       for (long long i = 4 * m4 + t; i < m; i += nt) {
         float acc = 0.f;
+        if constexpr (OP == 2) {
+          acc = mine[i];
+        } else {
 #pragma unroll
-        for (int j = 0; j < W; ++j) acc += j == rank ? mine[i] : rs(rank, j)[lo + i];
-        mine[i] = acc;
+          for (int j = 0; j < W; ++j) acc += j == rank ? mine[i] : rs(rank, j)[lo + i];
+          mine[i] = acc;
+        }
+        if constexpr (OP != 1) {
 #pragma unroll
-        for (int k = 1; k < W; ++k) ag((rank + k) % W)[rank * cs + lo + i] = acc;
+          for (int k = 1; k < W; ++k) ag((rank + k) % W)[rank * cs + lo + i] = acc;
+        }
       }
     }
+  }
+  if constexpr (OP == 1) {
+    __syncthreads();
+    if (t == 0) epochs[b] = epoch;
+    return;
   }
   raise_flags(1);
   wait_flags(1);
@@ -382,13 +407,22 @@ long long xgmi_ll_bytes(int mode, int world, long long S) {
 
 void xgmi_bw_launch(float* g, long long n, int rank, int world, long long S, const XgPeers& peers,
                     unsigned* epochs, int* err, long long ticks, hipStream_t stream, int blocks,
-                    const int* abort_word) {
+                    const int* abort_word, int op) {
   if (!abort_word) throw std::runtime_error("xgmi bw protocol: needs the host abort word");
+  if (op < 0 || op > 2) throw std::runtime_error("xgmi bw protocol: op must be 0 (all-reduce), "
+                                                 "1 (reduce-scatter) or 2 (all-gather)");
   const dim3 grid(blocks), block(512);
 #define DTFX_BW(WW)                                                                          \
   case WW:                                                                                   \
-    hipLaunchKernelGGL((xgmi_bw_kernel<WW>), grid, block, 0, stream, g, n, rank, S, peers,   \
-                       epochs, err, ticks, abort_word);                                      \
+    if (op == 0)                                                                             \
+      hipLaunchKernelGGL((xgmi_bw_kernel<WW, 0>), grid, block, 0, stream, g, n, rank, S,     \
+                         peers, epochs, err, ticks, abort_word);                             \
+    else if (op == 1)                                                                        \
+      hipLaunchKernelGGL((xgmi_bw_kernel<WW, 1>), grid, block, 0, stream, g, n, rank, S,     \
+                         peers, epochs, err, ticks, abort_word);                             \
+    else                                                                                     \
+      hipLaunchKernelGGL((xgmi_bw_kernel<WW, 2>), grid, block, 0, stream, g, n, rank, S,     \
+                         peers, epochs, err, ticks, abort_word);                             \
     break;
   switch (world) {
     DTFX_BW(1) DTFX_BW(2) DTFX_BW(3) DTFX_BW(4) DTFX_BW(5) DTFX_BW(6) DTFX_BW(7) DTFX_BW(8)

@@ -128,13 +128,27 @@ class XgmiAllReduce {
     const long long ticks = (long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
     if (mode_ == XG_BW)
       xgmi_bw_launch((float*)g, n, rank_, world_, S_, peers_, epochs_, err_, ticks,
-                     (hipStream_t)stream, bw_blocks_, abort_dev_);
+                     (hipStream_t)stream, bw_blocks_, abort_dev_, 0);
     else if (mode_ >= 0)
       xgmi_ll_launch(mode_, (float*)g, n, rank_, world_, S_, peers_, epochs_, err_, ticks,
                      (hipStream_t)stream);
     else
       xgmi_allreduce_launch((float*)g, n, rank_, world_, S_, peers_, epochs_, err_, ticks,
                             (hipStream_t)stream);
+  }
+
+  // In-place halves of the bandwidth two-shot over g[0, n) (n a multiple of 4 x world, so
+  // rank r's chunk is exactly [r n / W, (r + 1) n / W)): op 1 reduce-scatter -- chunk r of g
+  // becomes the sum over ranks; op 2 all-gather -- every rank's chunk r lands in every g.
+  void shard_op(int op, uintptr_t g, long long n, uintptr_t stream, double timeout_s) {
+    if (!ready_) throw std::runtime_error("xgmi: open() the peer handles first");
+    if (mode_ != XG_BW) throw std::runtime_error("xgmi: reduce-scatter / all-gather need protocol bw");
+    if (op != 1 && op != 2) throw std::runtime_error("xgmi: shard op must be 1 or 2");
+    if (n > S_) throw std::runtime_error("xgmi: buffer larger than max_numel");
+    if (n % (4LL * world_)) throw std::runtime_error("xgmi: shard ops need n % (4 x world) == 0");
+    if (g & 15) throw std::runtime_error("xgmi: buffer must be 16-byte aligned");
+    xgmi_bw_launch((float*)g, n, rank_, world_, S_, peers_, epochs_, err_,
+                   (long long)(timeout_s * 1e8), (hipStream_t)stream, bw_blocks_, abort_dev_, op);
   }
 
   // MNIST-MLP weight-gradient kernel with the gradient exchange fused into its epilogue
@@ -360,6 +374,8 @@ void register_xgmi(py::module_& m) {
            py::arg("pos"), py::arg("n"), py::arg("ws"), py::arg("ctr"), py::arg("stats"),
            py::arg("ring"), py::arg("B"), py::arg("dz1A"), py::arg("stream"),
            py::arg("timeout_s"), py::arg("flush"))
+      .def("shard_op", &dtfx::XgmiAllReduce::shard_op, py::arg("op"), py::arg("g"), py::arg("n"),
+           py::arg("stream"), py::arg("timeout_s") = 2.0)
       .def("error", &dtfx::XgmiAllReduce::error)
       .def("abort", &dtfx::XgmiAllReduce::abort, py::call_guard<py::gil_scoped_release>())
       .def("reset_epochs", &dtfx::XgmiAllReduce::reset_epochs)

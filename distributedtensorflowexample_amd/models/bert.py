@@ -114,17 +114,29 @@ def param_layout(cfg: BertConfig):
 
 
 class FlatParams:
-    """Flat f32 master / bf16 copy / f32 grad / Adam moments with named views."""
+    """Flat f32 master / bf16 copy / f32 grad / Adam moments with named views.
 
-    def __init__(self, cfg: BertConfig, device, seed=0):
+    ``bucket_multiple`` (a multiple of ALIGN): every gradient bucket's length is padded to a
+    multiple of it -- the owner-sharded optimizer (``BertTrainer(zero1=True)``) splits each
+    bucket into world-size equal, ALIGN-aligned shards.  The padding stays zero."""
+
+    def __init__(self, cfg: BertConfig, device, seed=0, bucket_multiple=ALIGN):
         self.cfg = cfg
         self.layout = param_layout(cfg)
         self.offsets = {}
+        bm = int(bucket_multiple)
+        if bm < ALIGN or bm % ALIGN:
+            raise ValueError("bucket_multiple must be a positive multiple of %d" % ALIGN)
+        starts = {"encoder/layer_%d/attention/qkv/kernel" % l for l in range(cfg.layers)}
+        starts.add("cls/predictions/transform/dense/kernel")
         off = 0
         for name, shape, _ in self.layout:
+            if name in starts:  # a bucket edge: the previous bucket ends on a multiple
+                off = (off + bm - 1) // bm * bm
             n = math.prod(shape)
             self.offsets[name] = (off, shape)
             off += (n + ALIGN - 1) // ALIGN * ALIGN
+        off = (off + bm - 1) // bm * bm
         self.numel = off
         dev = torch.device(device)
         self.master = torch.zeros(off, device=dev)
@@ -220,10 +232,10 @@ class FlatParams:
 class BertMLM:
     """Explicit forward + backward of BERT MLM over the HIP ops."""
 
-    def __init__(self, cfg: BertConfig, device, seed=0):
+    def __init__(self, cfg: BertConfig, device, seed=0, bucket_multiple=ALIGN):
         self.cfg = cfg
         self.device = torch.device(device)
-        self.params = FlatParams(cfg, device, seed)
+        self.params = FlatParams(cfg, device, seed, bucket_multiple)
         # encoder weight gradients on a second HIP stream: they only need the layer's output
         # gradient and saved input, so they overlap the (independent) dgrad GEMMs -- whose
         # last wave is half empty at M = 16K tokens, N = 768 (768 tiles on 512 resident
@@ -256,11 +268,13 @@ class BertMLM:
         return out, (x, qkv, ctx, lse, a, m1, r1, h1, u, g, f, m2, r2)
 
     def forward_backward(self, ids, tt, mask_pos, mask_labels, kmask=None, on_bucket_ready=None,
-                         n_valid=None):
+                         n_valid=None, on_bucket_needed=None):
         """One MLM training step's forward + backward; gradients land in params.grad.
 
         ids, tt: int32 [B, S]; mask_pos: int64 flat token indices of the masked
-        positions [Tm]; mask_labels: int32 [Tm].  Returns (loss, accuracy) as
+        positions [Tm]; mask_labels: int32 [Tm].  ``on_bucket_needed(i)``: called before the
+        forward first reads bucket ``i``'s parameters (the owner-sharded optimizer's
+        all-gather of the previous update is waited for there).  Returns (loss, accuracy) as
         0-dim device tensors (no host sync)."""
         cfg, p = self.cfg, self.params
         batch, seq = ids.shape
@@ -272,6 +286,8 @@ class BertMLM:
                              "batch has %d (call enable_splitk_fold again or disable it)"
                              % (self._fold_tokens, Tn))
         p.zero_grad()
+        need = on_bucket_needed if on_bucket_needed is not None else (lambda i: None)
+        need(0)
         ids_f, tt_f = ids.reshape(-1), tt.reshape(-1)
         x0, h, me, re = TR.embed_ln_fwd(ids_f, tt_f, p.W("embeddings/word_embeddings"),
                                         p.W("embeddings/position_embeddings"),
@@ -280,9 +296,11 @@ class BertMLM:
                                         p.P("embeddings/LayerNorm/beta"), seq, cfg.eps)
         saved = []
         for l in range(cfg.layers):
+            need(l + 1)
             h, s = self._layer_fwd(l, h, batch, seq, kmask)
             saved.append(s)
         # ---- MLM head on the masked positions only
+        need(len(p.buckets) - 1)
         hm = h.index_select(0, mask_pos)
         ut = torch.empty(hm.shape, device=h.device, dtype=BF16)
         t = B16.gemm(hm, p.W("cls/predictions/transform/dense/kernel"), False, True,

@@ -318,6 +318,32 @@ class HybridComm:
             return t.div_(self.world_size)
         return self.rccl.allreduce_avg_(t)
 
+    def _shard_bw(self, full):
+        """Route an in-place reduce-scatter / all-gather over ``full`` to the two-shot's halves
+        (same size rule as the all-reduce; bf16 counted in f32 words)."""
+        if not (full.is_cuda and full.is_contiguous()):
+            return False
+        if full.dtype == torch.float32:
+            words = full.numel()
+        elif full.dtype == torch.bfloat16 and full.numel() % 2 == 0:
+            words = full.numel() // 2
+        else:
+            return False
+        return (self.lo <= words <= self.bw.max_numel and words % (4 * self.world_size) == 0
+                and full.data_ptr() % 16 == 0)
+
+    def reduce_scatter(self, out, inp):
+        if inp.dtype == torch.float32 and self._shard_bw(inp) and \
+                out.data_ptr() == inp.data_ptr() + self.rank * out.numel() * 4:
+            return self.bw.reduce_scatter(out, inp)
+        return self.rccl.reduce_scatter(out, inp)
+
+    def all_gather(self, out, inp):
+        if self._shard_bw(out) and \
+                inp.data_ptr() == out.data_ptr() + self.rank * inp.numel() * inp.element_size():
+            return self.bw.all_gather(out, inp)
+        return self.rccl.all_gather(out, inp)
+
     def check(self):
         self.bw.check()
 

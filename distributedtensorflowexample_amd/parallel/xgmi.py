@@ -103,6 +103,41 @@ class XgmiComm:
                            self.timeout_s)
         return t
 
+    def _shard_view(self, out, inp, dtype_ok=(torch.float32,)):
+        """(f32 word view of ``inp``, its word count) for an in-place shard op: ``out`` must be
+        this rank's chunk of ``inp`` (``inp[rank * n : (rank + 1) * n]``, n = out.numel()).
+        bf16 tensors travel as f32 words (all-gather only: the
+        kernel moves them, it does not sum them)."""
+        if inp.dtype not in dtype_ok or out.dtype != inp.dtype:
+            raise ValueError("XgmiComm shard op: dtype %s not supported here" % inp.dtype)
+        if not (inp.is_cuda and inp.is_contiguous() and out.is_contiguous()):
+            raise ValueError("XgmiComm shard op: contiguous GPU tensors only")
+        n = out.numel()
+        if inp.numel() != n * self.world_size or \
+                out.data_ptr() != inp.data_ptr() + self.rank * n * inp.element_size():
+            raise ValueError("XgmiComm shard op: out must be this rank's chunk of inp (in place)")
+        words = inp.view(torch.float32) if inp.dtype != torch.float32 else inp
+        if words.numel() % (4 * self.world_size) or words.numel() > self.max_numel:
+            raise ValueError("XgmiComm shard op: %d words (need a multiple of %d, <= %d)"
+                             % (words.numel(), 4 * self.world_size, self.max_numel))
+        return words
+
+    def reduce_scatter(self, out, inp):
+        """In-place reduce-scatter (protocol "bw"): ``out`` = this rank's chunk of ``inp``
+        receives the sum over ranks of that chunk."""
+        w = self._shard_view(out, inp)
+        self._h.shard_op(1, w.data_ptr(), w.numel(), torch.cuda.current_stream().cuda_stream,
+                         self.timeout_s)
+        return out
+
+    def all_gather(self, out, inp):
+        """In-place all-gather (protocol "bw"): every rank's chunk ``inp`` of ``out`` lands in
+        every rank's ``out``.  f32 or bf16 (moved as f32 words)."""
+        w = self._shard_view(inp, out, (torch.float32, torch.bfloat16))
+        self._h.shard_op(2, w.data_ptr(), w.numel(), torch.cuda.current_stream().cuda_stream,
+                         self.timeout_s)
+        return out
+
     def mlp_wgrad(self, p, lr, x, ws, stats=True):
         """MNIST-MLP weight-gradient launch with the gradient all-reduce fused into its
         epilogue (protocol "push"): ``p -= lr * sum over ranks of the gradient``; see
@@ -234,6 +269,28 @@ class SimulatedPeersComm:
 
     def allreduce_avg_(self, t):
         return self.allreduce_sum_(t).div_(self.world_size)
+
+    def _pieces(self, out, inp, esize_words):
+        """Split an in-place shard op over pieces of at most ``max_numel`` words whose
+        lengths are multiples of 4 x W words (timing harness: rank 0's chunk of each piece
+        stands in for its chunk of the whole)."""
+        flat = inp.view(-1)
+        step = max(4 * self.world_size, self.max_numel // (4 * self.world_size) * 4 * self.world_size)
+        step = int(step / esize_words)
+        for lo in range(0, flat.numel(), step):
+            piece = flat[lo:lo + step]
+            n = piece.numel() // self.world_size
+            yield piece[:n], piece
+
+    def reduce_scatter(self, out, inp):
+        for o, i in self._pieces(out, inp, 1.0):
+            self.comm.reduce_scatter(o, i)
+        return out
+
+    def all_gather(self, out, inp):
+        for i, o in self._pieces(inp, out, 0.5 if out.dtype == torch.bfloat16 else 1.0):
+            self.comm.all_gather(o, i)
+        return out
 
     def broadcast_(self, t, root=0):
         return t  # rank 0 is the root: its values are the broadcast values

@@ -10,6 +10,26 @@ f32 master weights and the bf16 working copy.  The whole step can be
 captured into one hipGraph (``use_graph``): the RCCL calls of the native
 communicator are graph-capturable.
 
+Owner-sharded optimizer (``zero1``, the world > 1 default; DTFX_BERT_ZERO1=0 turns it off):
+the reference applies every gradient ONCE, on the ps task that owns the variable
+(``apply_gradients`` colocated with the variable, worker.py:75-79, placed by
+``replica_device_setter``, worker.py:24-25).  Here every GPU owns an equal 1/W shard of each
+encoder-layer / head bucket (ZeRO-1):
+
+    backward      bucket i final -> reduce-scatter on the comm stream (half an all-reduce's
+                  bytes): this rank holds the summed gradient of its shard
+    after it      fused AdamW on the shard only (1/W of the work; Adam moments sized for
+                  the shard), in the order the buckets became ready
+    next step     all-gather of the shards (f32 master + bf16 working copy) on the comm
+                  stream at the start of the step; the forward of layer l waits only for
+                  bucket l's gather, so the gathers overlap the forward of the layers below
+
+The embedding bucket (the last one backward produces and the first one forward needs) stays
+all-reduced with a replicated AdamW: sharding it would expose its gather at the start of the
+forward.  Between steps the non-owned shards of ``params.master`` / ``params.bf`` are one
+update behind: ``sync_params()`` (a collective, every rank at the same step) completes them
+for checkpoints, evals and replica checks.
+
 Reference counterpart: the reference only has async-PS SGD of an MLP
 (worker.py:71-79, 129-159); this is the sync all-reduce design the
 BASELINE.json north star asks for, applied to BERT-base.
@@ -26,13 +46,19 @@ from ..ops import optim as OPT
 
 class BertTrainer:
     def __init__(self, cfg: BertConfig, batch, seq, device, comm=None, lr=1e-4, seed=0,
-                 overlap=True, weight_decay=0.01, data_seed=None, data_batches=8):
+                 overlap=True, weight_decay=0.01, data_seed=None, data_batches=8, zero1=None):
         self.cfg, self.batch, self.seq = cfg, batch, seq
         self.device = torch.device(device)
         self.comm = comm
         self.world = comm.world_size if comm is not None else 1
         self.lr, self.wd = lr, weight_decay
-        self.model = BertMLM(cfg, device, seed)
+        if zero1 is None:
+            zero1 = self.world > 1 and os.environ.get("DTFX_BERT_ZERO1", "1") != "0"
+        self.zero1 = bool(zero1) and self.world > 1
+        from ..models.bert import ALIGN
+
+        self.model = BertMLM(cfg, device, seed,
+                             bucket_multiple=ALIGN * (self.world if self.zero1 else 1))
         p = self.model.params
         if self.world > 1:  # replicas start identical (Philox init is seed-determined; broadcast anyway)
             comm.broadcast_(p.master, 0)
@@ -75,13 +101,115 @@ class BertTrainer:
                            if (self.gpu and self.world == 1
                                and os.environ.get("DTFX_BERT_OPT_OVERLAP", "0") == "1") else None)
         self._adam_kw = None
+        if self.zero1:
+            self._init_zero1()
         self.step_t = torch.ones(1, dtype=torch.int32, device=self.device)  # Adam step (device side)
         self.step_count = 0
         self.graph = None
         self.last = None
 
+    # -- owner-sharded optimizer (ZeRO-1) ------------------------------------------------
+    def _init_zero1(self):
+        p, W = self.model.params, self.world
+        r = self.comm.rank
+        self._shards = {}  # bucket -> (lo, hi, shard lo, shard hi, offset in the moment buffers)
+        off = 0
+        for b, (lo, hi) in enumerate(p.buckets):
+            if b == 0:
+                continue  # embeddings: all-reduced, replicated AdamW
+            n = (hi - lo) // W
+            self._shards[b] = (lo, hi, lo + r * n, lo + (r + 1) * n, off)
+            off += n
+        self._m_sh = torch.zeros(off, device=self.device)
+        self._v_sh = torch.zeros(off, device=self.device)
+        lo0, hi0 = p.buckets[0]
+        self._m_emb = torch.zeros(hi0 - lo0, device=self.device)
+        self._v_emb = torch.zeros(hi0 - lo0, device=self.device)
+        p.m = p.v = None  # the full-size moments are not kept: 1/W of them per rank
+        gpu = self.gpu
+        self._ev_rs = {b: (torch.cuda.Event() if gpu else None) for b in range(len(p.buckets))}
+        self._ev_ag = {b: (torch.cuda.Event() if gpu else None) for b in self._shards}
+
+    def _gather_bucket(self, b):
+        """All-gather bucket b's shards (f32 master + bf16 working copy) on the current stream."""
+        p = self.model.params
+        lo, hi, slo, shi, _ = self._shards[b]
+        self.comm.all_gather(p.master[lo:hi], p.master[slo:shi])
+        self.comm.all_gather(p.bf[lo:hi], p.bf[slo:shi])
+
+    def _zero1_gathers(self):
+        """Start of a step: the previous update's shards to every rank (comm stream)."""
+        if self.comm_stream is None:
+            for b in self._shards:
+                self._gather_bucket(b)
+            return
+        cur = torch.cuda.current_stream(self.device)
+        self.comm_stream.wait_stream(cur)
+        with torch.cuda.stream(self.comm_stream):
+            for b in sorted(self._shards):  # forward order: layers, then the head
+                self._gather_bucket(b)
+                self._ev_ag[b].record(self.comm_stream)
+
+    def _on_needed(self, b):
+        if self.comm_stream is not None and b in self._ev_ag:
+            torch.cuda.current_stream(self.device).wait_event(self._ev_ag[b])
+
+    def _zero1_bucket(self, i):
+        p = self.model.params
+        lo, hi = p.buckets[i]
+        g = p.grad[lo:hi]
+
+        def issue():
+            if i in self._shards:
+                _, _, slo, shi, _ = self._shards[i]
+                self.comm.reduce_scatter(p.grad[slo:shi], g)
+            else:
+                self.comm.allreduce_sum_(g)
+
+        if self.comm_stream is None:
+            issue()
+            return
+        self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.comm_stream):
+            issue()
+            self._ev_rs[i].record(self.comm_stream)
+
+    def _zero1_adam(self, kw):
+        """AdamW of this rank's shards (in the order their reduce-scatters were issued), then
+        the replicated embeddings."""
+        from ..ops import transformer as TR
+
+        p = self.model.params
+        cur = torch.cuda.current_stream(self.device) if self.comm_stream is not None else None
+        order = sorted(self._shards, reverse=True) + [0]
+        for b in order:
+            if cur is not None:
+                cur.wait_event(self._ev_rs[b])
+            if b == 0:
+                lo, hi = p.buckets[0]
+                m, v = self._m_emb, self._v_emb
+            else:
+                _, _, lo, hi, o = self._shards[b]
+                m, v = self._m_sh[o:o + hi - lo], self._v_sh[o:o + hi - lo]
+            TR.adam_mixed(p.master[lo:hi], p.grad[lo:hi], m, v, p.bf[lo:hi], self.lr, 0,
+                          wd=kw["wd"], gscale=kw["gscale"], step_ptr=kw["step_ptr"])
+        if cur is not None:
+            cur.wait_stream(self.comm_stream)
+
+    def sync_params(self):
+        """Complete the non-owned shards of the parameters after the last update (ZeRO-1): a
+        collective -- every rank calls it at the same step.  No-op without sharding."""
+        if not self.zero1:
+            return
+        for b in sorted(self._shards):
+            self._gather_bucket(b)
+        if self.gpu:
+            torch.cuda.current_stream(self.device).synchronize()
+
     # gradient bucket ready -> all-reduce on the comm stream (one GPU: its AdamW)
     def _on_bucket(self, i):
+        if self.zero1:
+            return self._zero1_bucket(i)
         if self.world == 1:
             if self.opt_stream is not None and i != 0:  # the embeddings' AdamW: after the join
                 lo, hi = self.model.params.buckets[i]
@@ -107,6 +235,14 @@ class BertTrainer:
         ids, tt, pos, lab, nv = self.data
         kw = dict(gscale=1.0 / self.world, wd=self.wd, step_ptr=self.step_t)
         self._adam_kw = kw
+        if self.zero1:
+            self._zero1_gathers()
+            loss, acc = self.model.forward_backward(ids, tt, pos, lab, n_valid=nv,
+                                                    on_bucket_ready=self._on_bucket,
+                                                    on_bucket_needed=self._on_needed)
+            self._zero1_adam(kw)
+            OPT.counter_add_(self.step_t, 1)
+            return loss, acc
         loss, acc = self.model.forward_backward(ids, tt, pos, lab, n_valid=nv,
                                                 on_bucket_ready=self._on_bucket)
         if self.opt_stream is not None:

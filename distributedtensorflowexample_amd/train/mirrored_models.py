@@ -57,17 +57,20 @@ def train_model_mirrored(flags, log=print):
         dev = torch.device("cpu")
         comm = TorchComm() if world > 1 else None
     is_chief = rank == 0
-    if getattr(flags, "zero1", False) and world > 1:
+    if getattr(flags, "zero1", False) and world > 1 and flags.model != "bert":
         raise ValueError("--zero1 is not implemented for --model %s (replicated fused "
-                         "optimizer); it applies to the autograd MLP path" % flags.model)
+                         "optimizer); it applies to bert and the autograd MLP path" % flags.model)
     tiny = flags.model_config == "tiny"
     if flags.model == "bert":
         from ..models import bert as M
         from .bert_trainer import BertTrainer
 
         cfg = M.BertConfig.tiny() if tiny else M.BertConfig.base()
+        # the owner-sharded AdamW is the world > 1 default (--zero1 keeps it on explicitly;
+        # DTFX_BERT_ZERO1=0 turns it off)
         tr = BertTrainer(cfg, flags.batch_size, flags.seq_len, dev, comm=comm,
-                         lr=flags.learning_rate, seed=flags.seed, data_seed=17 + rank)
+                         lr=flags.learning_rate, seed=flags.seed, data_seed=17 + rank,
+                         zero1=True if getattr(flags, "zero1", False) else None)
     elif flags.model == "resnet50":
         from ..models import resnet as M
         from .resnet_trainer import ResNetTrainer
@@ -124,11 +127,20 @@ def train_model_mirrored(flags, log=print):
             step = global_step()
             maybe_inject_fault(rank, step)
             k = int(getattr(flags, "check_replicas_every", 0) or 0)
+            logstep = step % int(flags.log_every) == 0 or step == steps_total
+            # owner-sharded optimizer: the other ranks' shards of the last update arrive with
+            # the next step's gathers; complete them (a collective: the same steps on every
+            # rank) wherever parameters are read -- replica checks and the chief's checkpoints,
+            # which then happen only at these steps
+            sharded = getattr(tr, "zero1", False)
+            synced = False
+            if sharded and (logstep or (k > 0 and step % k == 0)):
+                tr.sync_params()
+                synced = True
             if k > 0 and world > 1 and step % k == 0:
                 from ..parallel.mirrored import assert_replicas_identical
 
                 assert_replicas_identical(comm, model.params.master, world, step)
-            logstep = step % int(flags.log_every) == 0 or step == steps_total
             if world > 1 and use_gpu:
                 # a timed-out xGMI bucket all-reduce leaves diverged replicas: stop on every
                 # rank at the next log step (same step everywhere: a collective check), and
@@ -138,7 +150,8 @@ def train_model_mirrored(flags, log=print):
                 elif is_chief and sv.checkpoint_pending() and getattr(comm, "failed", None) \
                         and comm.failed():
                     raise RuntimeError("xGMI all-reduce timed out before a checkpoint")
-            sv.service()  # a requested checkpoint, between steps
+            if synced or not sharded:
+                sv.service()  # a requested checkpoint, between steps
             if logstep:
                 loss, acc = tr.stats()
                 if writer is not None:
@@ -148,6 +161,8 @@ def train_model_mirrored(flags, log=print):
                     log("step: {}\t| cost: {}\t| speed: {}step/sec".format(
                         step, loss, float((step - s0) / max(el, 1e-9))))
                     t0, s0 = time.time(), step
+        if getattr(tr, "zero1", False):
+            tr.sync_params()  # (every rank) the final checkpoint reads complete parameters
         if is_chief:
             sv.save_checkpoint()
     return global_step()

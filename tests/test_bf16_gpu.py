@@ -204,3 +204,29 @@ def test_gemm_8phase_epilogues_and_splitk(cfg8, gpu):
     out = torch.zeros(512, 256, device=gpu)
     bf16.gemm(dy, xx, True, False, out=out, splitk=4)
     assert (out - dy.float().t() @ xx.float()).abs().max().item() < 1e-4 * T ** 0.5
+
+
+@pytest.mark.parametrize("tb", [True, False])
+def test_gemm_tail_split_exact_and_epilogue(gpu, tb):
+    """An 8-phase GEMM with one sparse last round (tiles 17 x 16 = 272: one round + 16 tiles)
+    runs its last 256 rows on the 128x128 tile (gemm_tail_rows): exact on integers across the
+    seam, and the row-local epilogues (bias, GELU with aux, residual, column sums) land on the
+    right rows of both parts."""
+    M, N, K = 17 * 256, 16 * 256, 128
+    g = torch.Generator().manual_seed(11)
+    a = torch.randint(-3, 4, (M, K), generator=g).to(gpu, torch.bfloat16)
+    b = torch.randint(-3, 4, ((N, K) if tb else (K, N)), generator=g).to(gpu, torch.bfloat16)
+    y = bf16.gemm(a, b, False, tb, out_dtype=torch.float32)
+    assert torch.equal(y, _ref(a, b, False, tb))
+    x = _rand(M, K, dev=gpu, seed=12)
+    w = _rand(*((N, K) if tb else (K, N)), dev=gpu, seed=13, scale=0.3)
+    bias = torch.randn(N, device=gpu)
+    res = _rand(M, N, dev=gpu, seed=14)
+    aux = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    cs = torch.zeros(N, device=gpu)
+    yb = bf16.gemm(x, w, False, tb, bias=bias, act="gelu", aux_out=aux, residual=res, colsum=cs)
+    u = _ref(x, w, False, tb) + bias
+    ref = torch.nn.functional.gelu(u, approximate="tanh") + res.float()
+    assert torch.allclose(aux.float(), u, rtol=1e-2, atol=2e-2)
+    assert torch.allclose(yb.float(), ref, rtol=1e-2, atol=2e-2)
+    assert torch.allclose(cs, yb.float().sum(0), rtol=1e-3, atol=0.5)

@@ -26,7 +26,10 @@ def _make(kind, comm, rank):
         from distributedtensorflowexample_amd.models.bert import BertConfig
         from distributedtensorflowexample_amd.train.bert_trainer import BertTrainer
 
-        return BertTrainer(BertConfig.tiny(), 2, 32, "cpu", comm=comm, lr=1e-3, data_seed=10 + rank)
+        # (the all-reduce path; the owner-sharded optimizer, the world > 1 default, has its own
+        # test below)
+        return BertTrainer(BertConfig.tiny(), 2, 32, "cpu", comm=comm, lr=1e-3, data_seed=10 + rank,
+                           zero1=False)
     from distributedtensorflowexample_amd.train.resnet_trainer import ResNetTrainer
 
     return ResNetTrainer(2, "cpu", comm=comm, lr=0.05, image_size=32, stages=[(8, 1, 1), (16, 1, 2)],
@@ -70,3 +73,51 @@ def test_dp_replicas_identical_and_grad_is_shard_sum(kind):
         shard.append(tr.model.params.grad.clone())
     ref = shard[0] + shard[1]
     assert torch.allclose(res[0][1], ref, atol=1e-5, rtol=1e-4)
+
+
+def _zero1_worker(rank, world, port, q, zero1):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from distributedtensorflowexample_amd.models.bert import BertConfig
+    from distributedtensorflowexample_amd.parallel.comm import TorchComm
+    from distributedtensorflowexample_amd.train.bert_trainer import BertTrainer
+
+    tr = BertTrainer(BertConfig.tiny(), 2, 32, "cpu", comm=TorchComm(), lr=1e-3,
+                     data_seed=10 + rank, zero1=zero1)
+    tr.run(3)
+    tr.sync_params()
+    sd = {k: v.numpy().copy() for k, v in tr.model.params.state_dict().items()}
+    q.put((rank, sd, tr.model.params.master.numel(), tr.zero1))
+    dist.destroy_process_group()
+
+
+def _run(world, zero1):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_zero1_worker, args=(r, world, port, q, zero1))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (sd, n, z)) for r, sd, n, z in [q.get(timeout=300) for _ in range(world)])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bert_zero1_matches_replicated_adam(world):
+    """Owner-sharded AdamW (reduce-scatter -> AdamW on this rank's shard -> all-gather, the
+    reference's apply-once-on-the-owner, worker.py:75-79) against the replicated optimizer over
+    3 steps: every parameter to f32 rounding, replicas identical, bucket padding for W shards."""
+    sh = _run(world, True)
+    rep = _run(world, False)
+    assert all(z for _, _, z in sh.values()) and not any(z for _, _, z in rep.values())
+    assert sh[0][1] % (64 * world) == 0           # every bucket split into W aligned shards
+    for r in range(1, world):                     # replicas identical (sharded)
+        for k in sh[0][0]:
+            assert (sh[r][0][k] == sh[0][0][k]).all(), (r, k)
+    for k, v in rep[0][0].items():                # same trajectory as the replicated AdamW
+        d = abs(torch.from_numpy(sh[0][0][k]) - torch.from_numpy(v)).max().item()
+        assert d <= 1e-6 + 1e-5 * abs(torch.from_numpy(v)).max().item(), (k, d)

@@ -595,6 +595,75 @@ def test_bw_allreduce_simulated_peers(gpu, world):
             _bw_check(world, rank, n, cap, gpu)
 
 
+def _bw_shard_check(world, rank, n, dev, dtype):
+    """The bw kernel's halves (ZeRO-1): reduce-scatter -- chunk r of g becomes the rank-ordered
+    sum of every rank's chunk r, and each peer's receive slot holds my share of its chunk;
+    all-gather -- my chunk lands in every peer's gather region, and the peers' chunks staged in
+    mine land in g.  bf16 all-gathers travel as f32 words."""
+    from distributedtensorflowexample_amd.parallel.xgmi import XgmiComm
+
+    words = n if dtype == torch.float32 else n // 2
+    comm, regs = XgmiComm.with_local_peers(rank, world, words, device=dev, protocol="bw")
+    S = comm.slot_stride
+    CS = ((S + world - 1) // world + 3) // 4 * 4
+    cs = words // world
+    flags0 = 2 * world * CS + 2 * S
+    g = torch.Generator().manual_seed(17 * world + rank + n)
+    f = regs[rank].view(torch.float32)
+    fl = regs[rank].view(torch.int32)
+    ops = ("rs", "ag", "rs", "ag") if dtype == torch.float32 else ("ag", "ag")
+    for epoch, op in enumerate(ops, 1):  # (the device epoch advances once per call)
+        par = epoch & 1
+        ph = 0 if op == "rs" else 1
+        for j in range(world):
+            if j != rank:
+                fl[flags0 + (ph * world + j) * XG_BLOCKS:flags0 + (ph * world + j + 1) * XG_BLOCKS] = epoch
+        if op == "rs":
+            vals = [torch.randn(n, generator=g) * (j + 1) for j in range(world)]
+            exp = _ordered_sum([v[rank * cs:(rank + 1) * cs] for v in vals])
+            for j in range(world):
+                if j != rank:
+                    o = (par * world + j) * CS
+                    f[o:o + cs] = vals[j][rank * cs:(rank + 1) * cs].to(dev)
+            t = vals[rank].to(dev)
+            torch.cuda.synchronize()
+            comm.reduce_scatter(t[rank * cs:(rank + 1) * cs], t)
+            comm.check()
+            assert torch.equal(t[rank * cs:(rank + 1) * cs].cpu(), exp), (world, rank, epoch)
+            for q in range(world):
+                if q != rank:
+                    o = (par * world + rank) * CS
+                    assert torch.equal(regs[q].view(torch.float32)[o:o + cs].cpu(),
+                                       vals[rank][q * cs:(q + 1) * cs]), (q, epoch)
+        else:
+            full = (torch.randn(n, generator=g) * 3).to(dtype)
+            fw = full.view(torch.float32) if dtype != torch.float32 else full
+            ag = 2 * world * CS + par * S
+            for c in range(world):
+                if c != rank:
+                    f[ag + c * cs:ag + (c + 1) * cs] = fw[c * cs:(c + 1) * cs].to(dev)
+            t = torch.zeros(n, device=dev, dtype=dtype)
+            k = n // world
+            t[rank * k:(rank + 1) * k] = full[rank * k:(rank + 1) * k].to(dev)
+            torch.cuda.synchronize()
+            comm.all_gather(t, t[rank * k:(rank + 1) * k])
+            comm.check()
+            assert torch.equal(t.cpu(), full), (world, rank, epoch)
+            for q in range(world):
+                if q != rank:
+                    assert torch.equal(regs[q].view(torch.float32)[ag + rank * cs:ag + (rank + 1) * cs].cpu(),
+                                       fw[rank * cs:(rank + 1) * cs]), (q, epoch)
+    comm.destroy()
+
+
+@pytest.mark.parametrize("world", WORLDS)
+def test_bw_reduce_scatter_all_gather_simulated_peers(gpu, world):
+    for rank in _ranks(world):
+        for n in (64 * world * 1000, 64 * world * 3):
+            _bw_shard_check(world, rank, n, gpu, torch.float32)
+            _bw_shard_check(world, rank, n, gpu, torch.bfloat16)
+
+
 def _pair_owner(words, world):
     """Owner rank of a word of the 16-byte pair layout in the pair two-shot exchange
     (xg_exchange2p): pair (eslot, sp, lane) is owned by (lane // 16 + 4 sp) % world."""

@@ -8,7 +8,9 @@ fold).  Against the 1-GPU step, each switch A/B'd in the same process, interleav
 
   1gpu          comm None (the bench's step)
   dp            world W, trainer defaults, the bw kernel on 128 workgroups (pick_large_allreduce's
-                default since round 5)
+                default since round 5); BERT: the owner-sharded AdamW (reduce-scatter / shard
+                AdamW / all-gather halves of the bw kernel) since round 6
+  dp_rep        BERT: the replicated AdamW over all-reduced buckets (DTFX_BERT_ZERO1=0)
   dp_null       world W, all-reduce a no-op (the DP-mode trainer changes alone)
   dp_bw256 / 64 the bw kernel on all 256 / on 64 workgroups
   dp_prio_hi    the comm stream at the highest HIP stream priority (default: the lowest,
@@ -43,6 +45,12 @@ class NullComm:
     def allreduce_sum_(self, t):
         return t
 
+    def reduce_scatter(self, out, inp):
+        return out
+
+    def all_gather(self, out, inp):
+        return out
+
     def broadcast_(self, t, root=0):
         return t
 
@@ -51,6 +59,8 @@ def make(model, variant, world, dev, a):
     env = {}
     if variant == "dp_nows":
         env["DTFX_BERT_WSTREAM"] = "0"
+    if variant == "dp_rep":  # BERT: replicated AdamW over all-reduced buckets (rounds 4-5)
+        env["DTFX_BERT_ZERO1"] = "0"
     if variant == "1gpu_nofold":
         env["DTFX_BERT_FOLD"] = "0"
     if variant == "dp_ws":

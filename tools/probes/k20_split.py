@@ -41,7 +41,7 @@ def main():
     region = {k: [] for k in Ks}
     noflush = {k: [] for k in Ks}
     call = {k: [] for k in Ks}
-    waits = {"device": [], "stream": [], "event": []}
+    waits = {"device": [], "stream": [], "event": [], "stream+device": []}
     s = torch.cuda.current_stream()
     for _ in range(a.reps):
         for k in Ks:
@@ -61,6 +61,7 @@ def main():
             noflush[k].append((time.perf_counter() - t0) * 1e6)
         for how in waits:
             ev = torch.cuda.Event()
+            tr.run(1, use_graph=False)  # the same preamble as bench.py's timed region
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             tr.run_launched(20, flush=True)
@@ -68,11 +69,13 @@ def main():
                 torch.cuda.synchronize()
             elif how == "stream":
                 s.synchronize()
+            elif how == "stream+device":
+                s.synchronize()
+                torch.cuda.synchronize()
             else:
                 ev.record(s)
                 ev.synchronize()
             waits[how].append((time.perf_counter() - t0) * 1e6)
-            tr.run(1, use_graph=False)
     out = {"region_us": {k: round(med(v), 2) for k, v in region.items()},
            "region_noflush_us": {k: round(med(v), 2) for k, v in noflush.items()},
            "host_call_us": {k: round(med(v), 2) for k, v in call.items()},
