@@ -9,6 +9,7 @@ namespace py = pybind11;
 namespace dtfx {
 void gemm_bf16_set_cfg(int);
 void attn_bwd_set_variant(int);
+void attn_set_swizzle(int);
 void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const void*, int, void*,
                       int, float, float, const float*, int, const void*, void*, int, const void*,
                       int, int, int, int, long long, long long, long long,
@@ -108,6 +109,8 @@ static inline T* P(uintptr_t a) { return reinterpret_cast<T*>(a); }
 static inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 void register_nn(py::module_& m) {
+  m.def("attn_set_swizzle", &dtfx::attn_set_swizzle,
+        "attention LDS images: -1 = environment (DTFX_ATTN_SWZ), 0 = padded rows, 1 = swizzled");
   m.def("attn_bwd_set_variant", &dtfx::attn_bwd_set_variant,
         "force the attention-backward kernel (-1 = environment; 0: 8 waves, 1: 4 waves, "
         "2: two query halves, two blocks per CU)");

@@ -875,6 +875,22 @@ static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
       return e && atoi(e) == 1;
     }();
     if (use6 && est6 < est5 && est6 < est0 && N > 128) return 6;
+    // the 8-phase tile with its sparse last round's rows on the 128x128 tile (gemm_tail_rows):
+    // the whole rounds plus the tail's 128x128 rounds (BERT-base QKV: 2 + 0.53 against the
+    // 128x128 tile's 2.66 -- 746 vs 737 TFLOP/s, profiles/r6/probe2/)
+    if (zdim == 1 && !ta) {
+      const long long F = t3 / 256, R = t3 % 256;
+      const int tn = (N + 255) / 256;
+      if (F >= 1 && R > 0 && R <= 128) {
+        const int rows5 = (int)(F * 256 / tn) * 256;
+        if (rows5 > 0 && rows5 < M) {
+          const long long p5 = (long long)(rows5 / 256) * tn;
+          const long long tt = (long long)((M - rows5 + 127) / 128) * ((N + 127) / 128);
+          const double est5t = (double)((p5 + 255) / 256) + (double)((tt + 511) / 512) * 0.25 / 0.47;
+          if (est5t < est5 && est5t < est0) return 5;
+        }
+      }
+    }
     // (a 4-wave 256x256 tile with one 128 x 128 wave per SIMD -- hipBLASLt's pick for these
     // shapes -- measured slower in both its per-K-tile rate and its epilogue:
     // profiles/r3/bert_gemm/w4_tile.md, tools/probes/w4_bench.hip)

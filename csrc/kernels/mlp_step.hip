@@ -1702,6 +1702,27 @@ void mlp_apply_launch(const float* p_old, float* p_new, float lr, const float* x
   if (stats && stats_ring < 1) throw std::runtime_error("mlp_apply: stats_ring < 1");
   const Bufs w = make_bufs(ws, B);
   const bool rt7 = (B + 15) / 16 == 7;
+  // DTFX_MLP_FLUSH_FWD=1: the flush runs the steps' own instantiation (FWD = true, its forward
+  // over x_prev into the workspace slab, which the next step overwrites) instead of the
+  // apply-only one: A/B of whether the flush pays for a code object no step keeps hot
+  static const bool ffwd = [] {
+    const char* e = std::getenv("DTFX_MLP_FLUSH_FWD");
+    return e && std::atoi(e) == 1;
+  }();
+  if (ffwd) {
+    if (mlp_single_ks() == KS3) {
+      if (rt7)
+        hipLaunchKernelGGL((mlp_fwdapply_kernel<7, 0, false, false, KS3>), dim3(HT * KS3 + HT),
+                           dim3(256), 0, stream, p_old, p_new, lr, x_prev, x_prev, w, ctr, stats,
+                           stats_ring, B, 1, MlpXg{}, nullptr);
+      else
+        hipLaunchKernelGGL((mlp_fwdapply_kernel<0, 0, false, false, KS3>), dim3(HT * KS3 + HT),
+                           dim3(256), 0, stream, p_old, p_new, lr, x_prev, x_prev, w, ctr, stats,
+                           stats_ring, B, 1, MlpXg{}, nullptr);
+      DTFX_HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
 #define DTFX_AP(NGT, KSV)                                                                       \
   hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, 0, false, false, KSV, false>), dim3(HT * KSV + HT), \
                      dim3(256), 0, stream, p_old, p_new, lr, x_prev, x_prev, w, ctr, stats,        \

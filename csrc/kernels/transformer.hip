@@ -574,19 +574,36 @@ __device__ __forceinline__ bf16x8 lfrag_sw(const char* base, int o0, int k0, int
     return v;
   }
 }
+// The two image layouts behind one interface (SWZ: compile-time variant of the kernels below)
+template <bool SWZ>
+constexpr int img_pitch() { return SWZ ? LDK : LDQ; }
+template <bool SWZ>
+__device__ __forceinline__ int img_off(int r, int col) {
+  return SWZ ? sw_off(r, col) : r * LDQ + col * 2;
+}
+template <bool SWZ, bool KC>
+__device__ __forceinline__ bf16x8 img_frag(const char* base, int o0, int k0, int lane) {
+  if constexpr (SWZ) return lfrag_sw<KC>(base, o0, k0, lane);
+  else return tf::lfrag<KC>(base, LDQ, o0, k0, lane);
+}
 }  // namespace at
 
 // Q never goes through LDS: each wave's 32 query rows are only its own A operands, read
 // as MFMA fragments straight from global memory (issued before the K/V staging).  K, V
 // and P then take 70 KB of LDS: two blocks per CU.
+// SWZ (DTFX_ATTN_SWZ=1, opt-in): the K / V images XOR-swizzled (at::swz) instead of padded.
+// Conflict-free, but measured slower: LDS bank-conflict cycles 21.6 M -> 4.3 M on the probe,
+// 29.7 -> 31.0 us per call, BERT-base -0.3 % (profiles/r6/attn_swizzle/).
+template <bool SWZ>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     int S, int nh, const unsigned short* __restrict__ qkv, unsigned short* __restrict__ out,
     float* __restrict__ lse, const float* __restrict__ kmask, float scale) {
   using namespace at;
   extern __shared__ __attribute__((aligned(16))) char sm[];
-  char* Ks = sm;  // swizzled images (at::swz)
-  char* Vs = sm + KB;
-  char* Ps = sm + 2 * KB;
+  constexpr int IB = SP * img_pitch<SWZ>();  // bytes of one K / V image
+  char* Ks = sm;
+  char* Vs = sm + IB;
+  char* Ps = sm + 2 * IB;
   const int b = blockIdx.x / nh, h = blockIdx.x % nh;
   const int Hd = nh * D, ld = 3 * Hd;
   const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
@@ -607,7 +624,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     char* const dst[2] = {Ks, Vs};
     const unsigned short* const src[2] = {base + Hd, base + 2 * Hd};
     const int lds[2] = {ld, ld};
-    at::load_heads<2, 256, true>(dst, src, lds, S);
+    at::load_heads<2, 256, SWZ>(dst, src, lds, S);
   }
   __syncthreads();
 
@@ -627,7 +644,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     for (int kk = 0; kk < 2; ++kk) {
       const bf16x8 a = qf[i][kk];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = mma(a, lfrag_sw<true>(Ks, 16 * j, 32 * kk, lane), acc[j]);
+      for (int j = 0; j < 8; ++j) acc[j] = mma(a, img_frag<SWZ, true>(Ks, 16 * j, 32 * kk, lane), acc[j]);
     }
     // row softmax: row r0 + rg + r lives in the 16 lanes of this row group x 8 tiles
 #pragma unroll
@@ -667,7 +684,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     for (int kk = 0; kk < 4; ++kk) {
       const bf16x8 a = lfrag<true>(Ps, LDP, r0, 32 * kk, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = mma(a, lfrag_sw<false>(Vs, 16 * j, 32 * kk, lane), o[j]);
+      for (int j = 0; j < 4; ++j) o[j] = mma(a, img_frag<SWZ, false>(Vs, 16 * j, 32 * kk, lane), o[j]);
     }
     // through this wave's own P rows (consumed by the products above): 2 16-B stores per
     // lane instead of 16 2-byte stores
@@ -1059,11 +1076,16 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_persist_kernel(
 // half.  P = exp(S * scale + mask - lse) needs no row maximum, so any tiling works.
 namespace atb {
 constexpr int HQ = 64;                  // queries per half
-constexpr int QH = HQ * at::LDK;        // 8192 B (swizzled images, at::swz)
-constexpr int PT = at::SP * at::LDK;    // [128 keys][64 queries], 128-B rows: 16384 B
-constexpr int LDS = at::KB + 2 * QH + 2 * PT + HQ * 4;  // 65792
+template <bool SWZ> constexpr int QH() { return HQ * at::img_pitch<SWZ>(); }      // 9216 / 8192 B
+template <bool SWZ> constexpr int PT() { return at::SP * at::img_pitch<SWZ>(); }  // [128 keys][64 q]
+template <bool SWZ> constexpr int KIMG() { return at::SP * at::img_pitch<SWZ>(); }
+template <bool SWZ> constexpr int LDS() { return KIMG<SWZ>() + 2 * QH<SWZ>() + 2 * PT<SWZ>() + HQ * 4; }
 }  // namespace atb
 
+// SWZ (DTFX_ATTN_SWZ=1, opt-in): every image XOR-swizzled (at::swz): LDS bank-conflict cycles
+// 56.2 M -> 8.7 M and LDS-wait cycles 134 M -> 24 M on the probe, but 58.7-62.4 -> 61.1-63.2
+// us per call (profiles/r6/attn_swizzle/): the kernel is not LDS-bound.
+template <bool SWZ>
 __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
     int S, int nh, const unsigned short* __restrict__ qkv, const unsigned short* __restrict__ o,
     const unsigned short* __restrict__ dout, const float* __restrict__ lse,
@@ -1072,12 +1094,13 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
   using namespace at;
   using namespace atb;
   extern __shared__ __attribute__((aligned(16))) char sm[];
+  constexpr int P_ = img_pitch<SWZ>();
   char* Ks = sm;
-  char* Qh = Ks + KB;
-  char* dOh = Qh + QH;
-  char* PTs = dOh + QH;
-  char* dSTs = PTs + PT;
-  float* Dr = (float*)(dSTs + PT);
+  char* Qh = Ks + KIMG<SWZ>();
+  char* dOh = Qh + QH<SWZ>();
+  char* PTs = dOh + QH<SWZ>();
+  char* dSTs = PTs + PT<SWZ>();
+  float* Dr = (float*)(dSTs + PT<SWZ>());
   const int b = blockIdx.x / nh, h = blockIdx.x % nh;
   const int Hd = nh * D, ld = 3 * Hd;
   const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
@@ -1096,7 +1119,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int e = tid + 512 * k;
-      *(bf16x8*)(Ks + (e >> 3) * LDK + (((e & 7) ^ swz(e >> 3)) << 4)) = kv[k];
+      *(bf16x8*)(Ks + img_off<SWZ>(e >> 3, (e & 7) * 8)) = kv[k];
     }
   }
   const float* L = lse + ((size_t)b * nh + h) * SP;
@@ -1124,8 +1147,8 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
         dv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       }
       __syncthreads();  // the previous half's phase 2 is done with Q_h / dO_h / P^T / dS^T
-      *(bf16x8*)(Qh + r * LDK + ((c ^ swz(r)) << 4)) = qv;
-      *(bf16x8*)(dOh + r * LDK + ((c ^ swz(r)) << 4)) = dv;
+      *(bf16x8*)(Qh + img_off<SWZ>(r, c * 8)) = qv;
+      *(bf16x8*)(dOh + img_off<SWZ>(r, c * 8)) = dv;
       if (c == 0) Dr[r] = row < S ? d : 0.f;
       __syncthreads();
     }
@@ -1134,8 +1157,8 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
       bf16x8 aq[2], ado[2];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        aq[kk] = lfrag_sw<true>(Qh, 16 * qt, 32 * kk, lane);
-        ado[kk] = lfrag_sw<true>(dOh, 16 * qt, 32 * kk, lane);
+        aq[kk] = img_frag<SWZ, true>(Qh, 16 * qt, 32 * kk, lane);
+        ado[kk] = img_frag<SWZ, true>(dOh, 16 * qt, 32 * kk, lane);
       }
       float lr[4], dr[4];
       bool live[4];
@@ -1147,7 +1170,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
         dr[r] = Dr[ql];
       }
       // the lane's P^T / dS^T store offset within a key tile (swz(16 kt + cl) = swz(cl))
-      const int poff = sw_off(cl, 16 * qt + rg);
+      const int poff = img_off<SWZ>(cl, 16 * qt + rg);
 #pragma unroll 1
       for (int j = 0; j < 4; ++j) {
         const int kt = kt0 + j, key = 16 * kt + cl;
@@ -1157,7 +1180,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
         for (int kk = 0; kk < 2; ++kk) {
           bf16x8 vb = *(const bf16x8*)(base + 2 * Hd + (size_t)min(key, S - 1) * ld + 32 * kk + 8 * g);
           if (key >= S) vb = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-          sa = mma(aq[kk], lfrag_sw<true>(Ks, 16 * kt, 32 * kk, lane), sa);
+          sa = mma(aq[kk], img_frag<SWZ, true>(Ks, 16 * kt, 32 * kk, lane), sa);
           dp = mma(ado[kk], vb, dp);
         }
         bf16x4 pv, dsv;
@@ -1167,7 +1190,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
           pv[r] = (short)tobf(p);
           dsv[r] = (short)tobf(p * (dp[r] - dr[r]));
         }
-        const int off = kt * (16 * LDK) + poff;  // = sw_off(key, 16 qt + rg)
+        const int off = kt * (16 * P_) + poff;  // = img_off(key, 16 qt + rg)
         *(bf16x4*)(PTs + off) = pv;
         *(bf16x4*)(dSTs + off) = dsv;
       }
@@ -1176,12 +1199,12 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
     // phase 2: dV += P^T dO_h, dK += dS^T Q_h (key tile `wave`); dQ_h = dS K
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 pT = lfrag_sw<true>(PTs, 16 * wave, 32 * kk, lane);
-      const bf16x8 dsT = lfrag_sw<true>(dSTs, 16 * wave, 32 * kk, lane);
+      const bf16x8 pT = img_frag<SWZ, true>(PTs, 16 * wave, 32 * kk, lane);
+      const bf16x8 dsT = img_frag<SWZ, true>(dSTs, 16 * wave, 32 * kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        av[j] = mma(pT, lfrag_sw<false>(dOh, 16 * j, 32 * kk, lane), av[j]);
-        ak[j] = mma(dsT, lfrag_sw<false>(Qh, 16 * j, 32 * kk, lane), ak[j]);
+        av[j] = mma(pT, img_frag<SWZ, false>(dOh, 16 * j, 32 * kk, lane), av[j]);
+        ak[j] = mma(dsT, img_frag<SWZ, false>(Qh, 16 * j, 32 * kk, lane), ak[j]);
       }
     }
     {
@@ -1190,10 +1213,10 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
       aq[0] = aq[1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8 dsr = lfrag_sw<false>(dSTs, 16 * qt, 32 * kk, lane);
+        const bf16x8 dsr = img_frag<SWZ, false>(dSTs, 16 * qt, 32 * kk, lane);
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
-          aq[jj] = mma(dsr, lfrag_sw<false>(Ks, 16 * (dt0 + jj), 32 * kk, lane), aq[jj]);
+          aq[jj] = mma(dsr, img_frag<SWZ, false>(Ks, 16 * (dt0 + jj), 32 * kk, lane), aq[jj]);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1607,19 +1630,53 @@ static void check_attn(int S, int nh) {
   if (nh <= 0) throw std::runtime_error("attention: nh must be positive");
 }
 
-void attn_fwd_launch(int Bn, int S, int nh, const void* qkv, void* out, float* lse,
-                     const float* kmask, float scale, hipStream_t s) {
-  check_attn(S, nh);
-  const size_t lds = 2 * at::KB + at::PB;
+// Swizzled attention images (opt-in, measured slower: see attn_fwd_kernel): -1 = from the
+// environment (DTFX_ATTN_SWZ=1), 0 / 1 forced (tests run both in one process).
+static int g_attn_swz = -1;
+void attn_set_swizzle(int v) { g_attn_swz = v; }
+static bool attn_swz() {
+  static const bool env = [] {
+    const char* e = std::getenv("DTFX_ATTN_SWZ");
+    return e && std::atoi(e) == 1;
+  }();
+  return g_attn_swz >= 0 ? g_attn_swz == 1 : env;
+}
+
+template <bool SWZ>
+static void attn_fwd_launch_t(int Bn, int S, int nh, const void* qkv, void* out, float* lse,
+                              const float* kmask, float scale, hipStream_t s) {
+  const size_t lds = 2 * (size_t)at::SP * at::img_pitch<SWZ>() + at::PB;
   static bool attr = false;
   if (!attr) {
-    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_kernel,
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_kernel<SWZ>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(Bn * nh), dim3(256), lds, s, S, nh,
+  hipLaunchKernelGGL(attn_fwd_kernel<SWZ>, dim3(Bn * nh), dim3(256), lds, s, S, nh,
                      (const unsigned short*)qkv, (unsigned short*)out, lse, kmask, scale);
+}
+
+void attn_fwd_launch(int Bn, int S, int nh, const void* qkv, void* out, float* lse,
+                     const float* kmask, float scale, hipStream_t s) {
+  check_attn(S, nh);
+  if (attn_swz()) attn_fwd_launch_t<true>(Bn, S, nh, qkv, out, lse, kmask, scale, s);
+  else attn_fwd_launch_t<false>(Bn, S, nh, qkv, out, lse, kmask, scale, s);
   DTFX_HIP_CHECK(hipGetLastError());
+}
+
+template <bool SWZ>
+static void attn_bwd_half_launch(int Bn, int S, int nh, const void* qkv, const void* o,
+                                 const void* dout, const float* lse, const float* kmask,
+                                 float scale, void* dqkv, float* dbias, hipStream_t s) {
+  static bool hattr = false;
+  if (!hattr) {
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_half_kernel<SWZ>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, atb::LDS<SWZ>()));
+    hattr = true;
+  }
+  hipLaunchKernelGGL(attn_bwd_half_kernel<SWZ>, dim3(Bn * nh), dim3(512), atb::LDS<SWZ>(), s, S, nh,
+                     (const unsigned short*)qkv, (const unsigned short*)o,
+                     (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv, dbias);
 }
 
 // Attention-backward kernel: -1 = from the environment, 0: attn_bwd_kernel<8>,
@@ -1682,16 +1739,10 @@ void attn_bwd_launch(int Bn, int S, int nh, const void* qkv, const void* o, cons
                        np, (const unsigned short*)qkv, (const unsigned short*)o,
                        (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv, dbias);
   } else if (var == 2) {
-    static bool hattr = false;
-    if (!hattr) {
-      DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_half_kernel,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, atb::LDS));
-      hattr = true;
-    }
-    hipLaunchKernelGGL(attn_bwd_half_kernel, dim3(Bn * nh), dim3(512), atb::LDS, s, S, nh,
-                       (const unsigned short*)qkv, (const unsigned short*)o,
-                       (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv,
-                       dbias);
+    if (attn_swz())
+      attn_bwd_half_launch<true>(Bn, S, nh, qkv, o, dout, lse, kmask, scale, dqkv, dbias, s);
+    else
+      attn_bwd_half_launch<false>(Bn, S, nh, qkv, o, dout, lse, kmask, scale, dqkv, dbias, s);
   } else if (var == 1)
     hipLaunchKernelGGL(attn_bwd_kernel<4>, dim3(Bn * nh), dim3(256), lds, s, S, nh,
                        (const unsigned short*)qkv, (const unsigned short*)o,

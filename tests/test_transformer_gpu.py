@@ -55,7 +55,9 @@ def test_embedding_fwd_bwd(gpu, B):
         assert torch.allclose(a.cpu(), b, atol=1e-3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])  # 3 / 4: persistent (4: 3 blocks, 4 pairs each)
+# 3 / 4: persistent (4: 3 blocks, 4 pairs each); 5: the two-halves kernel and the forward with
+# the XOR-swizzled LDS images (opt-in DTFX_ATTN_SWZ=1)
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("S,masked", [(128, False), (128, True), (77, True), (64, False), (33, True)])
 def test_attention_fwd_bwd(gpu, S, masked, variant):
     B, nh = 3, 4
@@ -64,18 +66,20 @@ def test_attention_fwd_bwd(gpu, S, masked, variant):
     if masked:
         valid = torch.tensor([S, S - 5, S // 2])
         kmask = torch.where(torch.arange(S)[None, :] < valid[:, None], 0.0, -10000.0)
-    o, lse = T.attn_fwd(qkv.to(gpu), B, S, nh, kmask.to(gpu) if masked else None)
-    orf, lser = T.attn_fwd(qkv, B, S, nh, kmask)
-    assert (o.cpu().float() - orf.float()).abs().max() < 2e-2
-    assert (lse.cpu().view(B, nh, -1)[..., :S] - lser.view(B, nh, -1)[..., :S]).abs().max() < 1e-3
-    dout = _r(B * S, nh * 64, seed=11).to(BF)
     hip = _ext.hip()
-    hip.attn_bwd_set_variant(variant)
+    hip.attn_set_swizzle(1 if variant == 5 else 0)
     try:
+        o, lse = T.attn_fwd(qkv.to(gpu), B, S, nh, kmask.to(gpu) if masked else None)
+        orf, lser = T.attn_fwd(qkv, B, S, nh, kmask)
+        assert (o.cpu().float() - orf.float()).abs().max() < 2e-2
+        assert (lse.cpu().view(B, nh, -1)[..., :S] - lser.view(B, nh, -1)[..., :S]).abs().max() < 1e-3
+        dout = _r(B * S, nh * 64, seed=11).to(BF)
+        hip.attn_bwd_set_variant(2 if variant == 5 else variant)
         dq = T.attn_bwd(qkv.to(gpu), o, dout.to(gpu), lse, B, S, nh, kmask.to(gpu) if masked else None)
         torch.cuda.synchronize()
     finally:
         hip.attn_bwd_set_variant(-1)
+        hip.attn_set_swizzle(-1)
     dqr = T.attn_bwd(qkv, o.cpu(), dout, lse.cpu(), B, S, nh, kmask)
     err = (dq.cpu().float() - dqr.float()).abs().max().item()
     assert err < 3e-2 * max(1.0, dqr.float().abs().max().item()), err
