@@ -15,6 +15,8 @@ step tests
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
 tail -1 "$OUT/pytest_gpu.log"
 step mlp
+timeout -k 10 200 python tools/probes/k20_flush.py > "$OUT/k20_flush.json" 2>&1 || exit 1
+tail -1 "$OUT/k20_flush.json"
 timeout -k 10 120 python bench.py --steps 20 --warmup 5 > "$OUT/bench_mlp_k20.json" 2>&1 || exit 1
 timeout -k 10 120 python bench.py --steps 20 --warmup 5 > "$OUT/bench_mlp_k20_2.json" 2>&1 || exit 1
 timeout -k 10 120 python bench.py --steps 20 --warmup 5 > "$OUT/bench_mlp_k20_3.json" 2>&1 || exit 1
