@@ -168,6 +168,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("DTFX_BENCH_PIN") == "1":
+        # A/B knob: this rank's host thread (and the HIP runtime threads it starts) on one CPU
+        # of its GPU's NUMA node, chosen before the GPU is touched -- the MLP's short timed
+        # region issues ~40 launches from the host, so scheduler migrations show in it
+        from distributedtensorflowexample_amd.config import first_gpu_numa_node_sysfs, pin_to_numa_node
+
+        node = first_gpu_numa_node_sysfs(index=local)
+        pin_to_numa_node(0 if node is None else node, 1, 2 + 2 * local)
+    from distributedtensorflowexample_amd.config import apply_hip_schedule
+
+    apply_hip_schedule()  # DTFX_HIP_SCHED (unset: the runtime's default wait)
     if a.comm == "auto" and world == 1:
         a.comm = "native"
     if world != a.gpus:
