@@ -174,6 +174,10 @@ struct Reader {
 //  * Hogwild apply, ApplyGradientDescent(use_locking=False) (worker.py:79).
 __attribute__((noinline)) void dtfx_racy_read(Writer& w, const float* p, size_t nbytes) {
   w.raw(p, nbytes);
+  // not a tail call: the string append must run under THIS frame, or the sanitizer's stack
+  // (and its suppression by function name) loses it -- seen once as a reported race in
+  // std::string::_M_mutate called from handle()
+  asm volatile("" ::: "memory");
 }
 // g: the gradient bytes inside the request buffer (no alignment guarantee: loaded by memcpy)
 // first: where this apply starts (it wraps around).  Every connection thread starts at its own

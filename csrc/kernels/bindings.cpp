@@ -32,6 +32,7 @@ void mlp_fwdapply_launch(const float*, float*, float, const float*, const float*
                          float*, int, int, int, hipStream_t, int);
 void mlp_head2_launch(const float*, const int*, float*, int, hipStream_t, int);
 int mlp_single_ks_query();
+int mlp_set_flush_fused(int on);
 void mlp_pipelined_trace_launch(const float*, float*, float, const float*, const float*,
                                 const int*, float*, int*, float*, int, int, hipStream_t,
                                 unsigned long long*, unsigned long long*);
@@ -161,6 +162,10 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("labels"), py::arg("nbatches"), py::arg("pos"), py::arg("n"), py::arg("ws"),
      py::arg("ctr"), py::arg("stats"), py::arg("ring"), py::arg("B"), py::arg("stream"),
      py::arg("flush") = 0);
+  m.def("mlp_set_flush_fused", &dtfx::mlp_set_flush_fused,
+        "run_launched(.., flush=True): 1 = the last step's head and the flush in one launch "
+        "(mlp_head_flush_kernel; opt-in, measured slower), 0 = the flush as its own launch; "
+        "returns the previous setting");
   m.def("mlp_apply", [](uintptr_t p_old, uintptr_t p_new, float lr, uintptr_t x_prev, uintptr_t ws,
                         uintptr_t ctr, uintptr_t stats, int ring, int B, uintptr_t s) {
     dtfx::mlp_apply_launch(P<const float>(p_old), P<float>(p_new), lr, P<const float>(x_prev),

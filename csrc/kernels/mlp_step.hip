@@ -90,6 +90,8 @@ struct Bufs {            // workspace (zero-initialised once; padding stays 0)
   float* dz1T;           // [HP][BP]      dz1 transposed
   float* dlT;            // [16][BP]      dlogits transposed
   float* rowstat;        // [BP][2]       per-row (loss, correct)
+  int* sync;             // [4] handoff words of mlp_head_flush_kernel (0 between launches):
+                         //     [0] head rows done, [1] apply blocks done, [2] sticky timeout
 };
 
 __device__ __forceinline__ float4 f4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -173,15 +175,17 @@ __global__ __launch_bounds__(64) void mlp_fwd_kernel(
 // words into slot (parity, me) of every peer and every peer's values for the same (j, row)
 // are gathered from local memory into dz1A [XW][BP][HP] -- the all-gather of the backprop
 // factors that mlp_wgrad_factor_kernel turns into the global weight gradient.
+// (the body of one row's wave: mlp_head_kernel runs it as a one-wave block, the terminal
+// head + apply kernel of a launched region as one of four waves of a block)
 template <bool APPLY, bool TRACE, int XW = 0, int NSLAB = KS>
-__global__ __launch_bounds__(64) void mlp_head_kernel(
-    const float* __restrict__ p_old, const float* __restrict__ grad, float lr,
-    float* __restrict__ p_new, const int* __restrict__ labels, Bufs w, int B,
-    unsigned long long* __restrict__ tr, MlpXg xg, float* __restrict__ dz1A) {
+__device__ __forceinline__ void head_row(
+    const int row, const int lane, const float* __restrict__ p_old,
+    const float* __restrict__ grad, float lr, float* __restrict__ p_new,
+    const int* __restrict__ labels, const Bufs& w, int B, unsigned long long* __restrict__ tr,
+    const MlpXg& xg, float* __restrict__ dz1A) {
   static_assert(XW == 0 || (!APPLY && !TRACE), "the factor exchange runs the direct step");
-  if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 0);
+  if (TRACE) trace_stamp(tr, row * 4 + 0);
   const int BP = ((B + 15) >> 4) * 16;
-  const int row = blockIdx.x, lane = threadIdx.x;
   const int y = labels[row];
   const unsigned ep = XW > 0 ? xg.epochs[MLP_XG_HEAD_EPOCH + row] + 1 : 0u;
   const bool publish = APPLY && row == 0;
@@ -257,7 +261,7 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
       }
     }
   }
-  if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 1);
+  if (TRACE) trace_stamp(tr, row * 4 + 1);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     hv[u] = jv[u] ? sigmoidf_(zs[u] + b1v[u]) : 0.f;
@@ -354,7 +358,7 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     if (lane == 0) xg.epochs[MLP_XG_HEAD_EPOCH + row] = ep;
     if (fail) atomicExch(xg.err, 1);
   }
-  if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 2);
+  if (TRACE) trace_stamp(tr, row * 4 + 2);
   float mydl = 0.f;
 #pragma unroll
   for (int c = 0; c < C; ++c) mydl = (lane == c) ? dl[c] : mydl;
@@ -363,7 +367,16 @@ __global__ __launch_bounds__(64) void mlp_head_kernel(
     w.rowstat[2 * row] = m + __logf(se) - ly;  // xent of this row
     w.rowstat[2 * row + 1] = (am == y) ? 1.f : 0.f;
   }
-  if (TRACE) trace_stamp(tr, blockIdx.x * 4 + 3);
+  if (TRACE) trace_stamp(tr, row * 4 + 3);
+}
+
+template <bool APPLY, bool TRACE, int XW = 0, int NSLAB = KS>
+__global__ __launch_bounds__(64) void mlp_head_kernel(
+    const float* __restrict__ p_old, const float* __restrict__ grad, float lr,
+    float* __restrict__ p_new, const int* __restrict__ labels, Bufs w, int B,
+    unsigned long long* __restrict__ tr, MlpXg xg, float* __restrict__ dz1A) {
+  head_row<APPLY, TRACE, XW, NSLAB>(blockIdx.x, threadIdx.x, p_old, grad, lr, p_new, labels, w,
+                                     B, tr, xg, dz1A);
 }
 
 // ---------------------------------------------------------------------------
@@ -896,17 +909,19 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(
 // 41 % of the waves' cycles were issue stalls).
 // FWD = false (mlp_apply_launch: the pending update of the last pipelined step, the flush):
 // phase A and the small parameters only -- no forward, no x loads.
+// (the body of block `bid`: mlp_fwdapply_kernel runs it with bid = blockIdx.x, the terminal
+// head + apply kernel of a launched region with FWD = false on its apply blocks)
 template <int NGT, int XW = 0, bool TRACE = false, bool TWO = false, int KSX = KS2, bool FWD = true>
-__global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
-    const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
-    const float* __restrict__ x_prev, const float* __restrict__ x, Bufs w, int* __restrict__ ctr,
-    float* __restrict__ stats, int stats_ring, int B, int stats_on, MlpXg xg,
-    unsigned long long* __restrict__ tr = nullptr) {
+__device__ __forceinline__ void fwdapply_block(
+    const int bid, const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
+    const float* __restrict__ x_prev, const float* __restrict__ x, const Bufs& w,
+    int* __restrict__ ctr, float* __restrict__ stats, int stats_ring, int B, int stats_on,
+    const MlpXg& xg, unsigned long long* __restrict__ tr) {
   // stamps per wave: 0 entry, 1 phase-A operands landed, 2 W1 tile applied + barrier, 3 slab
   // stored; with XW > 0 also 4 local gradient slice ready (exchange starts), 5 two-shot: the
   // owned sums done (first hop), 6 exchange done -- 8 slots per wave then
   constexpr int TRN = XW > 0 ? 8 : 4;
-  unsigned long long* trw = TRACE ? tr + (size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * TRN : nullptr;
+  unsigned long long* trw = TRACE ? tr + (size_t)(bid * 4 + (threadIdx.x >> 6)) * TRN : nullptr;
   if (TRACE) trace_stamp(trw, 0);
   const int BP = NGT > 0 ? NGT * 16 : ((B + 15) >> 4) * 16;
   const int NG = NGT > 0 ? NGT : BP / 16;
@@ -919,7 +934,6 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
   constexpr int KSP = 4 / NCG;             // phase-A K splits (waves per column group)
   constexpr int G2 = (KWX + 15) / 16;      // phase-B 16-feature groups
   static_assert(KSX * KWX == D && KWX % 4 == 0 && NCG * KSP == 4, "K slicing");
-  const int bid = blockIdx.x;
   if (bid >= HT * KSX) {
     const int jt = bid - HT * KSX;
     wgrad_small<true, NGT, XW>(jt, wave, lane, MLP_XG_SMALL_EPOCH + jt * 4 + wave, p_new, lr,
@@ -1138,6 +1152,80 @@ __global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
     for (int i = 0; i < 4; ++i) out[(size_t)i * HP] = acc0[i] + acc1[i];
   }
   if (TRACE) trace_stamp(trw, 3);
+}
+
+template <int NGT, int XW = 0, bool TRACE = false, bool TWO = false, int KSX = KS2, bool FWD = true>
+__global__ __launch_bounds__(256) void mlp_fwdapply_kernel(
+    const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
+    const float* __restrict__ x_prev, const float* __restrict__ x, Bufs w, int* __restrict__ ctr,
+    float* __restrict__ stats, int stats_ring, int B, int stats_on, MlpXg xg,
+    unsigned long long* __restrict__ tr = nullptr) {
+  fwdapply_block<NGT, XW, TRACE, TWO, KSX, FWD>(blockIdx.x, p_old, p_new, lr, x_prev, x, w, ctr,
+                                                stats, stats_ring, B, stats_on, xg, tr);
+}
+
+// Terminal step of a launched region with the flush folded in (opt-in,
+// measured slower: see mlp_flush_fused): the head of
+// the region's last step AND the apply of that step's update -- what mlp_head_kernel + the
+// apply-only mlp_fwdapply_kernel<.., FWD = false> (mlp_apply_launch) do as two dependent
+// launches -- in ONE launch, so the region ends on the step's own second launch.
+//   blocks [0, NHB): head rows 4 * bid + wave (one wave per batch row, as mlp_head_kernel);
+//     each row's wave publishes with ONE agent-scope release add on sync[0] (its stores to
+//     hbuf / dz1T / dlT / rowstat retired and written back first).
+//   blocks [NHB, NHB + HT * KSX + HT): apply blocks: thread 0 waits (agent-scope acquire)
+//     until sync[0] == B, then the block runs the apply-only body on the step's parameters
+//     p_cur -> p_next (the same code, operands and summation order as the flush launch: the
+//     result is bit-identical).
+// Every wait is bounded (`ticks` of s_memrealtime): a timed-out block sets sync[2] and skips
+// its apply (the host raises: FusedMLPTrainer.check()).  The grid (25 + 203 blocks of 256
+// threads at batch 100) is a fraction of one wave slot per CU, so every head block is resident
+// while the apply blocks wait.  The last apply block to finish zeroes sync[0..1] for the next
+// region (stream order: no launch reads them before this one has ended).
+template <int NGT, int KSX>
+__global__ __launch_bounds__(256) void mlp_head_flush_kernel(
+    const float* __restrict__ p_cur, float* __restrict__ p_next, float lr,
+    const float* __restrict__ x, const int* __restrict__ labels, Bufs w, int* __restrict__ ctr,
+    float* __restrict__ stats, int stats_ring, int B, long long ticks) {
+  const int nhb = (B + 3) >> 2;
+  const int bid = blockIdx.x, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (bid < nhb) {
+    const int row = bid * 4 + wave;
+    if (row >= B) return;
+    head_row<false, false, 0, KSX>(row, lane, p_cur, p_cur, 0.f, nullptr, labels, w, B, nullptr,
+                                   MlpXg{}, nullptr);
+    // release at agent scope: the wave's stores are complete and written back past this
+    // XCD's L2 before the count moves (one add per row)
+    if (lane == 0) __hip_atomic_fetch_add(w.sync, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  __shared__ int ok_s;
+  if (threadIdx.x == 0) {
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    int ok = 1;
+    while (__hip_atomic_load(w.sync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < B) {
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks ||
+          __hip_atomic_load(w.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        ok = 0;
+        __hip_atomic_store(w.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    ok_s = ok;
+  }
+  __syncthreads();
+  if (ok_s)
+    fwdapply_block<NGT, 0, false, false, KSX, false>(bid - nhb, p_cur, p_next, lr, x, x, w, ctr,
+                                                     stats, stats_ring, B, 1, MlpXg{}, nullptr);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int napply = (int)gridDim.x - nhb;
+    if (__hip_atomic_fetch_add(w.sync + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == napply - 1) {
+      __hip_atomic_store(w.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(w.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 
@@ -1413,6 +1501,7 @@ static mlp::Bufs make_bufs(float* ws, int B) {
   b.dz1T = b.hbuf + (size_t)BP * HP;
   b.dlT = b.dz1T + (size_t)HP * BP;
   b.rowstat = b.dlT + (size_t)16 * BP;
+  b.sync = reinterpret_cast<int*>(b.rowstat + (size_t)2 * BP);
   return b;
 }
 
@@ -1474,7 +1563,7 @@ void mlp_tf_layout_launch(const float* src, float* dst, int to_tf, const float* 
 long long mlp_workspace_floats(int B) {
   using namespace mlp;
   const long long BP = ((B + 15) / 16) * 16;
-  return (long long)NSLAB_MAX * BP * HP + BP * HP + HP * BP + 16 * BP + 2 * BP;
+  return (long long)NSLAB_MAX * BP * HP + BP * HP + HP * BP + 16 * BP + 2 * BP + 4;
 }
 
 static void check_b(int B) {
@@ -1857,6 +1946,28 @@ void mlp_head2_launch(const float* p, const int* labels, float* ws, int B, hipSt
 // mirrors (batch position, parity, pending) by n.
 // flush != 0: the pending update of the last step is applied by one more launch
 // (mlp_apply_launch, into the other buffer: the parity then moves by n + 1).
+// DTFX_MLP_FLUSH_FUSED=1: the last step's head and the flush in ONE launch
+// (mlp_head_flush_kernel).  Opt-in: correct (bit-identical to the separate flush, tests/
+// test_kernels_gpu.py) but measured SLOWER in the driver-sized region -- 10.97-11.05 M vs
+// 11.37-11.46 M samples/s, six interleaved pairs on one box (profiles/r6/k20/flush_fused_ab/):
+// the in-kernel hand-off (release adds of 100 row waves, the apply blocks' acquire poll, their
+// cold operand loads after it) costs ~7 us more than the kernel boundary it replaces, as the
+// persistent engine's hand-offs did (mlp_persistent.hip).
+static int g_flush_fused = -1;  // -1: read DTFX_MLP_FLUSH_FUSED on first use
+static bool mlp_flush_fused() {
+  if (g_flush_fused < 0) {
+    const char* e = std::getenv("DTFX_MLP_FLUSH_FUSED");
+    g_flush_fused = e && std::atoi(e) == 1 ? 1 : 0;
+  }
+  return g_flush_fused == 1;
+}
+// tests: select the terminal form in-process (returns the previous setting)
+int mlp_set_flush_fused(int on) {
+  const int old = mlp_flush_fused() ? 1 : 0;
+  g_flush_fused = on ? 1 : 0;
+  return old;
+}
+
 void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float lr,
                               const float* x, const int* labels, int nbatches, int pos, int n,
                               float* ws, int* ctr, float* stats, int stats_ring, int B,
@@ -1872,6 +1983,7 @@ void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float 
   const size_t xb = (size_t)B * D;
   const bool rt7 = (B + 15) / 16 == 7;
   const bool ks3 = mlp_single_ks() == KS3;
+  const bool fused_flush = flush && n > 0 && mlp_flush_fused();
   for (int i = 0; i < n; ++i) {
     const int prev = (pos + nbatches - 1) % nbatches;
     const float* xcur = x + (size_t)pos * xb;
@@ -1880,6 +1992,33 @@ void mlp_run_pipelined_launch(float* p0, float* p1, int cur, int pending, float 
     float* pn = bufs[cur ^ 1];
     const float l = pending ? lr : 0.f;  // (pending doubles as the kernel's "apply / record
                                          //  the previous step" flag, as in step_pipelined)
+    if (fused_flush && i == n - 1) {
+      // the last step: its first launch as usual, then ONE launch for its head and the apply
+      // of its update (pn -> po: the flush's destination, the other buffer)
+      const int nhb = (B + 3) / 4;
+      const long long ticks = 200000000LL;  // 2 s of s_memrealtime (100 MHz)
+#define DTFX_HF(NGT, KSV)                                                                        \
+  do {                                                                                           \
+    hipLaunchKernelGGL((mlp_fwdapply_kernel<NGT, 0, false, false, KSV>), dim3(HT * KSV + HT),      \
+                       dim3(256), 0, stream, po, pn, l, xprev, xcur, w, ctr, stats, stats_ring, B, \
+                       pending, MlpXg{}, nullptr);                                               \
+    hipLaunchKernelGGL((mlp_head_flush_kernel<NGT, KSV>), dim3(nhb + HT * KSV + HT), dim3(256), 0, \
+                       stream, pn, bufs[cur], lr, xcur, labels + (size_t)pos * B, w, ctr, stats,  \
+                       stats_ring, B, ticks);                                                    \
+  } while (0)
+      if (ks3) {
+        if (rt7) DTFX_HF(7, KS3);
+        else DTFX_HF(0, KS3);
+      } else {
+        if (rt7) DTFX_HF(7, KS2);
+        else DTFX_HF(0, KS2);
+      }
+#undef DTFX_HF
+      cur ^= 1;  // (the step: po -> pn; the flush below moves it back -- net parity n + 1)
+      pending = 0;
+      pos = (pos + 1) % nbatches;
+      break;
+    }
     if (ks3) {
       if (rt7)
         hipLaunchKernelGGL((mlp_fwdapply_kernel<7, 0, false, false, KS3>), dim3(HT * KS3 + HT),

@@ -372,10 +372,18 @@ class FusedMLPTrainer:
         self._unchecked = True
 
     def check(self):
-        """Raise if an in-kernel wait of the persistent engine ever timed out."""
+        """Raise if an in-kernel wait of the persistent engine, or of the terminal head +
+        apply launch of ``run_launched(.., flush=True)``, ever timed out."""
         if self._ll is not None and int(self._ll[-32].item()) != 0:
             raise RuntimeError("persistent MLP engine: an in-kernel hand-off timed out "
                                "(parameters are not valid)")
+        ws = getattr(self, "ws", None)
+        if ws is not None and ws.buf.is_cuda:
+            sync = ws.buf[-4:].view(torch.int32)  # mlp::Bufs::sync (the workspace's last words)
+            if int(sync[2].item()) != 0:
+                sync.zero_()
+                raise RuntimeError("fused MLP step: the terminal head + apply hand-off timed "
+                                   "out (the last update was not applied)")
         self._unchecked = False  # verified
 
     def run(self, steps, use_graph=True, lead=0):

@@ -299,6 +299,46 @@ def test_host_loop_matches_graph_replay(gpu):
         assert runs[mode][3] == runs["graph"][3] == 23 % 13
 
 
+@pytest.mark.parametrize("B", [100, 7, 128])
+def test_terminal_head_flush_matches_separate_flush_and_fp64(gpu, B):
+    """run_launched(K, flush=True) ends on ONE launch that runs the last step's head and the
+    apply of its update (mlp_head_flush_kernel).  Against the same steps
+    with the flush as its own launch (FusedMLPTrainer.flush): bit-identical parameters,
+    global_step and loss / accuracy records, over back-to-back flushed regions of K = 1, 5, 20
+    (the hand-off words must reset between launches); and the applied trajectory against an
+    fp64 CPU reference of the reference's SGD (worker.py:59-79)."""
+    import __graft_entry__ as ge
+    from distributedtensorflowexample_amd.data.synthetic import mnist_like_device
+    from distributedtensorflowexample_amd.models.mlp import init_params
+    from distributedtensorflowexample_amd.train.fused_mlp import FusedMLPTrainer
+
+    from distributedtensorflowexample_amd.ops._ext import hip
+
+    p = init_params(gpu, seed=5)
+    nb = 30
+    x, y = mnist_like_device(nb * B, seed=6, device=gpu)
+    fused = FusedMLPTrainer(p, x, y, B, 0.001)
+    sep = FusedMLPTrainer(p, x, y, B, 0.001)
+    for k in (1, 5, 20):
+        old = hip().mlp_set_flush_fused(1)  # (opt-in: DTFX_MLP_FLUSH_FUSED=1)
+        try:
+            fused.run_launched(k, flush=True)
+        finally:
+            hip().mlp_set_flush_fused(old)
+        sep.run_launched(k)
+        sep.flush()
+        assert not fused.pending
+        assert torch.equal(fused.params, sep.params), k
+    fused.check()  # no hand-off timed out
+    sync = fused.ws.buf[-4:].view(torch.int32)
+    assert sync.tolist() == [0, 0, 0, 0]  # reset by the last apply block of every launch
+    assert fused.global_step() == sep.global_step() == 26
+    assert torch.equal(fused.stats_range(0, 26), sep.stats_range(0, 26))
+    p_ref, hist_ref = ge.reference_sgd(p, x, y, 0.001, 26, batch=B)
+    hist = [tuple(float(v) for v in r) for r in fused.stats_range(0, 26).cpu()]
+    ge.check_step_result(p, fused.params, hist, p_ref, hist_ref)
+
+
 @pytest.mark.parametrize("B", [100, 64, 128, 7])
 def test_persistent_trainer_matches_pipelined(gpu, B):
     """The persistent single-launch engine (workgroups hand z1 partials, backprop factors and

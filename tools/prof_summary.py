@@ -1,10 +1,22 @@
-"""Summarize a rocprofv3 --stats kernel_stats.csv: top kernels by total time."""
+"""Summarize a rocprofv3 --stats kernel_stats.csv (or the rocpd SQLite database rocprofv3
+writes without --output-format csv): top kernels by total time."""
 import csv
+import sqlite3
 import sys
 
 
+def _rows(path):
+    if path.endswith(".db"):
+        c = sqlite3.connect(path)
+        return [{"Name": n, "Calls": str(k), "TotalDurationNs": float(t) * 1e3,
+                 "AverageNs": float(a) * 1e3}
+                for n, k, t, a in c.execute(
+                    "select name, total_calls, total_duration, average from top_kernels")]
+    return list(csv.DictReader(open(path)))
+
+
 def main(path, top=25, steps=None):
-    rows = list(csv.DictReader(open(path)))
+    rows = _rows(path)
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     out = []
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:top]:
