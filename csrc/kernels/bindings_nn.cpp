@@ -8,6 +8,7 @@ namespace py = pybind11;
 
 namespace dtfx {
 void gemm_bf16_set_cfg(int);
+int gemm_bf16_set_pers(int);
 void attn_bwd_set_variant(int);
 void attn_set_swizzle(int);
 void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const void*, int, void*,
@@ -114,6 +115,10 @@ void register_nn(py::module_& m) {
   m.def("attn_bwd_set_variant", &dtfx::attn_bwd_set_variant,
         "force the attention-backward kernel (-1 = environment; 0: 8 waves, 1: 4 waves, "
         "2: two query halves, two blocks per CU)");
+  m.def("gemm_bf16_set_pers", &dtfx::gemm_bf16_set_pers,
+        "1: plain 8-phase GEMMs with more 256x256 tiles than CUs run the persistent tile loop "
+        "(opt-in, measured slower), 0: one block per tile (default); returns the previous "
+        "setting");
   m.def("gemm_bf16_set_cfg", &dtfx::gemm_bf16_set_cfg,
         "force the bf16 GEMM tile configuration (-1 = auto; 0: 128x128, 3: 256x256 2-stage, "
         "5: 256x256 8-phase)");

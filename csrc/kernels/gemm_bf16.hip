@@ -55,13 +55,21 @@ namespace dtfx {
 // 256x256: 8 waves of 128x64; 256x64 (conv fwd with 64 output channels): 4 waves of 64x64
 // stacked along M, 2 blocks/CU -- no MFMA work on a 128-wide tile's dead half).  NBUF = LDS stages (2: next tile in flight during
 // compute; 3: two tiles in flight, counted vmcnt + raw barrier).
-template <int MODE, bool TA, bool TB, bool OUT_F32, int BM_, int NBUF, int BN_, bool F1 = false>
+// a value the compiler cannot see through (no code): keeps per-tile address math in the tile loop
+__device__ __forceinline__ int opaque_v(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+template <int MODE, bool TA, bool TB, bool OUT_F32, int BM_, int NBUF, int BN_, bool F1 = false,
+          bool PERS = false>
 __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64,
                              (BM_ == 128 || BN_ == 64) && NBUF == 2 ? 2 : 1) void gemm_bf16_kernel(
     int M, int N, int K, const unsigned short* __restrict__ A, int lda,
     const unsigned short* __restrict__ B, int ldb, void* __restrict__ Cv, int ldc, GemmEpi e,
     long long sA, long long sB, long long sC, ConvDesc cd) {
   using namespace gb;
+  static_assert(!PERS || (NBUF == 8 && MODE == 0), "the persistent tile loop: 8-phase plain GEMM");
   constexpr int BM = BM_, BN = BN_;
   // wave tile WM x 64 (8-phase: 4 pieces of 32 x SW, one per block quadrant, 8 waves)
   constexpr int WM = (BN_ == 256 || NBUF == 8) ? 128 : 64;
@@ -98,24 +106,43 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
     split = 0;
     if (MODE == 2 && bid >= tiles_n * tiles_m) return;
   }
-  int tm = bid / tiles_n, tn = bid % tiles_n;
-  if (NBUF == 8 && gridDim.y == 1) {
-    // grouped raster: an XCD's consecutive tile ids walk GM tile-rows column by column, so
-    // its ~32 resident blocks share 4 A and ~8 B panels in its L2 instead of 1 A and 32 B
-    const int GM = 4, group = GM * tiles_n, fm = (bid / group) * GM;
-    const int gm = min(tiles_m - fm, GM), r = bid % group;
-    tm = fm + r % gm;
-    tn = r / gm;
-  }
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int wm = wave / NWN, wn = wave % NWN;
-
+  // tile id -> (first row, first column); grouped raster on the 8-phase tile: an XCD's
+  // consecutive tile ids walk GM tile-rows column by column, so its ~32 resident blocks share 4
+  // A and ~8 B panels in its L2 instead of 1 A and 32 B
+  auto tile_origin = [&](int tid, int& mo, int& no) {
+    int tm = tid / tiles_n, tn = tid % tiles_n;
+    if (NBUF == 8 && gridDim.y == 1) {
+      const int GM = 4, group = GM * tiles_n, fm = (tid / group) * GM;
+      const int gm = min(tiles_m - fm, GM), r = tid % group;
+      tm = fm + r % gm;
+      tn = r / gm;
+    }
+    mo = tm * BM;
+    no = tn * BN;
+  };
+  int m0, n0;
+  tile_origin(bid, m0, n0);
+  // PERS (persistent tile loop, one resident block per CU): this block runs virtual blocks
+  // blockIdx.x, + gridDim.x, ... -- tile xcd_remap(vb) of each, the tile the one-shot grid's
+  // block vb would run (gridDim.x % 8 == 0 keeps vb on this block's XCD), so every round of
+  // 256 tiles shares its panels in the XCDs' L2 exactly as before.  The next tile's first K
+  // tile is staged into LDS buffer 0 before this tile's epilogue (which then uses buffer 1 and
+  // the LDS past the 8 half images), so its HBM round trip overlaps the epilogue instead of
+  // following a fresh block's dispatch.
+  int vb = blockIdx.x;
+  bool pre = false;  // PERS: buffer 0 already holds this tile's first K tile
   // Clamp limits for edge tiles: k-contiguous rows clamp to the last row; k-strided
   // column chunks clamp to the last full 8-column chunk (ld % 8 == 0 makes it in-bounds).
   const int a_max = TA ? ((M - 1) & ~7) : M - 1;
   const int b_max = TB ? N - 1 : ((N - 1) & ~7);
 
+  for (;;) {  // PERS: one iteration per tile of this block (otherwise exactly one)
+  // (PERS: the lane / wave ids pass an opaque copy per tile, so the lane-dependent address math
+  // of the staging, the fragment reads and the epilogue is formed again per tile instead of
+  // being hoisted out of the tile loop and held live through it -- which spilled)
+  const int lane = PERS ? opaque_v(threadIdx.x & 63) : threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(PERS ? opaque_v(threadIdx.x >> 6) : threadIdx.x >> 6);
+  const int wm = wave / NWN, wn = wave % NWN;
   f32x4 acc[TM][4];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -307,12 +334,12 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
                                                  0, 0, 0);
       }
     };
-    auto voff = [&](bool isA, int which, int i) -> int {
+    auto voffx = [&](bool isA, int which, int i, int mo, int no) -> int {
       const bool kc = isA ? !TA : TB;
       const int ld = isA ? lda : ldb, omax = isA ? a_max : b_max;
       // B halves start NQN apart (BN = 192: 96-column halves staged as 128-column images,
       // the last 32 columns loaded but never read)
-      const int outer0 = isA ? m0 + which * 128 : n0 + (which - 2) * NQN;
+      const int outer0 = isA ? mo + which * 128 : no + (which - 2) * NQN;
       const int blk = i * NW + wave;
       if (kc) {
         const int row = blk * 8 + (lane >> 3), c = (lane & 7) ^ swz_kc(row);
@@ -321,10 +348,12 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
       const int kr = blk * 4 + (lane >> 4), c = (lane & 15) ^ swz_tr(kr);
       return (kr * ld + min(outer0 + c * 8, omax)) * 2;
     };
-    const int vo0_0 = voff(true, 0, 0), vo0_1 = voff(true, 0, 1);
-    const int vo1_0 = voff(true, 1, 0), vo1_1 = voff(true, 1, 1);
-    const int vo2_0 = voff(false, 2, 0), vo2_1 = voff(false, 2, 1);
-    const int vo3_0 = voff(false, 3, 0), vo3_1 = voff(false, 3, 1);
+    auto voff = [&](bool isA, int which, int i) { return voffx(isA, which, i, m0, n0); };
+    // (PERS: reassigned to the next tile's offsets for its buffer-0 prefetch after the K loop)
+    int vo0_0 = voff(true, 0, 0), vo0_1 = voff(true, 0, 1);
+    int vo1_0 = voff(true, 1, 0), vo1_1 = voff(true, 1, 1);
+    int vo2_0 = voff(false, 2, 0), vo2_1 = voff(false, 2, 1);
+    int vo3_0 = voff(false, 3, 0), vo3_1 = voff(false, 3, 1);
 #define DTFX_PH8_STAGE(BUF, WHICH, KT)                                                          \
   do {                                                                                          \
     if constexpr (CONV8 && (WHICH) < 2) {                                                       \
@@ -383,8 +412,9 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
     //     phase 4 (0,1): read A0      stage A1 of tile kt+2 -> b   (read ph2)
     //   vmcnt(4) in phase 4 retires tile kt+1 (its last half, A0, went out in phase 2).
     const bool late = wave >= NW / 2;
-    // prologue: tile 0 -> buffer 0; tile 1's B0 and A1 halves -> buffer 1
-    if (nk > 0) {
+    // prologue: tile 0 -> buffer 0 (PERS: staged before the previous tile's epilogue); tile
+    // 1's B0 and A1 halves -> buffer 1
+    if (nk > 0 && !pre) {
       DTFX_PH8_STAGE(0, 2, 0); DTFX_PH8_STAGE(0, 1, 0); DTFX_PH8_STAGE(0, 3, 0); DTFX_PH8_STAGE(0, 0, 0);
     }
     if (nk > 1) {
@@ -417,6 +447,25 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
     }
     if (!late) __builtin_amdgcn_s_barrier();  // the early group's share of the offset
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PERS) {
+      // every wave has read its last fragments: buffer 0 is free.  The next tile's first K tile
+      // (4 half images, soffset 0: MODE 0) goes out now, ahead of this tile's epilogue stores.
+      __syncthreads();
+      pre = false;
+      if (vb + (int)gridDim.x < tiles_n * tiles_m && nk > 0) {
+        int mn, nn;
+        tile_origin(xcd_remap(vb + (int)gridDim.x, tiles_n * tiles_m), mn, nn);
+        // (the prologue's order B0, A1, B1, A0: the DTFX_PH8_STAGE sites with the next
+        // tile's lane offsets and soffset 0)
+        vo2_0 = voffx(false, 2, 0, mn, nn); vo2_1 = voffx(false, 2, 1, mn, nn);
+        vo1_0 = voffx(true, 1, 0, mn, nn); vo1_1 = voffx(true, 1, 1, mn, nn);
+        vo3_0 = voffx(false, 3, 0, mn, nn); vo3_1 = voffx(false, 3, 1, mn, nn);
+        vo0_0 = voffx(true, 0, 0, mn, nn); vo0_1 = voffx(true, 0, 1, mn, nn);
+        DTFX_PH8_STAGE(0, 2, -kt0); DTFX_PH8_STAGE(0, 1, -kt0);
+        DTFX_PH8_STAGE(0, 3, -kt0); DTFX_PH8_STAGE(0, 0, -kt0);
+        pre = true;
+      }
+    }
 #undef DTFX_PH8_MMA
 #undef DTFX_PH8_STAGE
   } else if (NBUF == 2) {
@@ -447,7 +496,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
       cur = cur == 2 ? 0 : cur + 1;
     }
   }
-  __syncthreads();
+  if constexpr (!PERS) __syncthreads();
 
   // Epilogue.  The accumulators (C/D map: col = lane & 15, row = (lane >> 4) * 4 + r)
   // go through a per-wave LDS transpose, 32 rows at a time, so every lane then owns 8
@@ -466,7 +515,9 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   // then bn_x and the BN mean / rstd) -- ~25 us of exposed latency per block on the ResNet-50
   // layer3 / layer4 data gradients (3x3: 100 us against the forward's 75).
   constexpr bool LATE = NBUF == 8 && MODE == 2 && !OUT_F32;
-  float* ep = (float*)smem + wave * (32 * EP_LD);
+  // (PERS: past LDS buffer 0, which holds the next tile's first K tile by now)
+  constexpr int EP_BASE = PERS ? 65536 : 0, RED_BASE = PERS ? 65536 + 8 * 32 * EP_LD * 4 : 98304;
+  float* ep = (float*)(smem + EP_BASE) + wave * (32 * EP_LD);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
   float cs[8], cq[8];  // fused column sums / sums of squares of this lane's 8 columns
 #pragma unroll
@@ -763,7 +814,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
         cq[u] += __shfl_xor(cq[u], 16);
         cq[u] += __shfl_xor(cq[u], 32);
       }
-      float* red = (float*)(smem + 98304);  // [colsum|colsq][Nq][wn8][wm8 * 2 + Mq][64]
+      float* red = (float*)(smem + RED_BASE);  // [colsum|colsq][Nq][wn8][wm8 * 2 + Mq][64]
       const int slot = (((h & 1) * 2 + (wave & 1)) * 8 + (wave >> 1) * 2 + (h >> 1)) * 64;
       if (lane < SLW / 8)
 #pragma unroll
@@ -778,7 +829,7 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   if constexpr (NBUF == 8) {
     if (e.colsum || e.colsq) {
       __syncthreads();
-      const float* red = (const float*)(smem + 98304);
+      const float* red = (const float*)(smem + RED_BASE);
       if (e.col_partial && threadIdx.x < BN) {
         // partial rows, one per 64-row output slab (the conv launchers' layout, reduced by
         // colpart_reduce): slab g of the block is entries wm8 * 2 + Mq with Mq = g >> 1,
@@ -811,6 +862,12 @@ __global__ __launch_bounds__(NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) *
   } else if (e.colsum || e.colsq) {
     flush_cols(wn * 64);
   }
+  if constexpr (!PERS) break;
+  vb += gridDim.x;
+  if (vb >= tiles_n * tiles_m) break;
+  tile_origin(xcd_remap(vb, tiles_n * tiles_m), m0, n0);
+  __syncthreads();  // the epilogue's LDS (buffer 1's image, the colsum rows) is free again
+  }  // tile loop
 }
 
 // ---------------------------------------------------------------------------
@@ -903,18 +960,55 @@ static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
   return 0;
 }
 
-template <int MODE, bool TA, bool TB, bool F, int BM_, int NBUF, int BN_ = 128, bool F1 = false>
+// Persistent 8-phase tile loop (PERS) for a plain GEMM whose 256x256 tiles
+// fill more than one round of the CUs.  Opt-in (DTFX_GEMM_PERS=1): exact and bit-identical to
+// one block per tile (tests/test_bf16_gpu.py), but per call 1-2.4 % SLOWER on every bf16-output
+// shape (FFN1 forward 109.2 vs 106.5 us, QKV 72.6 vs 71.9, 8192^3 1415 vs 1432 TFLOP/s) and
+// +2.4 % only with an f32 output; BERT-base 8,377-8,394 vs 8,387-8,389 seq/s
+// (profiles/r6/gemm_pers/).  What the ~11 us per tile round is NOT, then: the block dispatch
+// and the prologue's first K tile (both overlapped here).  It is the epilogue itself -- the LDS
+// transpose and 128 KB of stores per block that the next tile's counted vmcnt waits out
+// (gfx9 counts stores and loads in one vmcnt), so a store-overlapping epilogue would need
+// separate store waves and LDS the 8-phase tile does not have free.
+static int g_gemm_pers = -1;  // -1: read DTFX_GEMM_PERS on first use
+static bool gemm_pers_on() {
+  if (g_gemm_pers < 0) {
+    const char* e = getenv("DTFX_GEMM_PERS");
+    g_gemm_pers = e && atoi(e) == 1 ? 1 : 0;
+  }
+  return g_gemm_pers == 1;
+}
+int gemm_bf16_set_pers(int on) {  // tests / A/B in one process; returns the previous setting
+  const int old = gemm_pers_on() ? 1 : 0;
+  g_gemm_pers = on ? 1 : 0;
+  return old;
+}
+static int gemm_num_cus() {
+  static const int n = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus > 0 ? cus : 256;
+  }();
+  return n;
+}
+
+template <int MODE, bool TA, bool TB, bool F, int BM_, int NBUF, int BN_ = 128, bool F1 = false,
+          bool PERS = false>
 static void launch_one(dim3 grid_yz, int M, int N, int K, const unsigned short* A, int lda,
                        const unsigned short* B, int ldb, void* C, int ldc, const GemmEpi& e,
                        long long sA, long long sB, long long sC, const ConvDesc& d,
                        hipStream_t stream) {
-  constexpr size_t lds = NBUF == 8 ? (size_t)131072  // 8 half-tile images of 16 KB
+  // 8-phase: 8 half-tile images of 16 KB; PERS: + the epilogue's transpose rows and column-sum
+  // rows past buffer 0 (65536 + 8 x 8704 + 16384)
+  constexpr size_t lds = PERS ? (size_t)151552
+                       : NBUF == 8 ? (size_t)131072
                                    : (size_t)NBUF * (BM_ * gb::BK * 2 + BN_ * gb::BK * 2);
   constexpr int threads = NBUF == 8 ? 512 : (BM_ / (BN_ == 256 ? 128 : 64)) * (BN_ / 64) * 64;
   static bool attr = false;
   if (!attr) {
     DTFX_HIP_CHECK(hipFuncSetAttribute(
-        (const void*)gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF, BN_, F1>,
+        (const void*)gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF, BN_, F1, PERS>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
@@ -933,8 +1027,10 @@ static void launch_one(dim3 grid_yz, int M, int N, int K, const unsigned short* 
     const size_t ep = (size_t)(threads / 64) * 32 * 68 * 4;
     lds_launch = stage > ep ? stage : ep;
   }
-  hipLaunchKernelGGL((gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF, BN_, F1>),
-                     dim3(tiles, grid_yz.y, grid_yz.z), dim3(threads), lds_launch, stream, M, N, K, A, lda,
+  // PERS: one block per CU (a multiple of 8: a block's virtual ids stay on its XCD)
+  const int gx = PERS ? (tiles < gemm_num_cus() ? tiles : gemm_num_cus() & ~7) : tiles;
+  hipLaunchKernelGGL((gemm_bf16_kernel<MODE, TA, TB, F, BM_, NBUF, BN_, F1, PERS>),
+                     dim3(gx, grid_yz.y, grid_yz.z), dim3(threads), lds_launch, stream, M, N, K, A, lda,
                      B, ldb, C, ldc, e, sA, sB, sC, d);
   DTFX_HIP_CHECK(hipGetLastError());
 }
@@ -946,8 +1042,19 @@ static void launch_cfg(int cfg, dim3 grid_yz, int M, int N, int K, const unsigne
                        hipStream_t stream) {
   if constexpr (MODE == 0) {
     if (cfg == 5) {
-      launch_one<MODE, TA, TB, F, 256, 8, 256>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA, sB, sC,
-                                               d, stream);
+      // PERS instantiations: A k-contiguous, and B k-contiguous or an f32 output (the bf16
+      // dY.W form with its prefetched epilogue side inputs spilled 15 VGPRs in the tile loop)
+      if constexpr (!TA && (TB || F)) {
+        const long long t5 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+        if (gemm_pers_on() && grid_yz.y == 1 && grid_yz.z == 1 && t5 > gemm_num_cus() &&
+            gemm_num_cus() >= 8) {
+          launch_one<MODE, TA, TB, F, 256, 8, 256, false, true>(grid_yz, M, N, K, A, lda, B, ldb,
+                                                                C, ldc, e, sA, sB, sC, d, stream);
+          return;
+        }
+      }
+      launch_one<MODE, TA, TB, F, 256, 8, 256>(grid_yz, M, N, K, A, lda, B, ldb, C, ldc, e, sA,
+                                               sB, sC, d, stream);
       return;
     }
     if (cfg == 6) {

@@ -64,7 +64,8 @@ def conv_specs(stages=STAGES, in_ch=IN_CH):
 
 
 class ResNetParams:
-    def __init__(self, device, seed=0, stages=STAGES, num_classes=NUM_CLASSES):
+    def __init__(self, device, seed=0, stages=STAGES, num_classes=NUM_CLASSES,
+                 bucket_multiple=ALIGN):
         self.convs = conv_specs(stages)
         self.stages = stages
         self.num_classes = num_classes
@@ -80,9 +81,22 @@ class ResNetParams:
         self.layout = layout
         self.offsets = {}
         off = 0
+        # a bucket (stem, each bottleneck block, the head) starts and ends on a multiple of
+        # ``bucket_multiple`` elements: the owner-sharded optimizer splits every bucket into W
+        # equal, ALIGN-aligned shards (trainer zero1: bucket_multiple = ALIGN * world)
+        bm = int(bucket_multiple)
+        if bm % ALIGN:
+            raise ValueError("bucket_multiple must be a multiple of %d" % ALIGN)
+
+        def opens_bucket(name):
+            return name == "fc.weight" or (name.endswith(".conv1.weight") and name != "conv1.weight")
+
         for name, shape, _ in layout:
+            if opens_bucket(name):
+                off = (off + bm - 1) // bm * bm
             self.offsets[name] = (off, shape)
             off += (math.prod(shape) + ALIGN - 1) // ALIGN * ALIGN
+        off = (off + bm - 1) // bm * bm
         self.numel = off
         dev = torch.device(device)
         self.master = torch.zeros(off, device=dev)
@@ -134,9 +148,10 @@ class ResNetParams:
 class ResNet50:
     """Explicit forward + backward over the HIP ops (training mode BatchNorm)."""
 
-    def __init__(self, device, seed=0, stages=STAGES, num_classes=NUM_CLASSES, bn_eps=1e-5):
+    def __init__(self, device, seed=0, stages=STAGES, num_classes=NUM_CLASSES, bn_eps=1e-5,
+                 bucket_multiple=ALIGN):
         self.device = torch.device(device)
-        self.params = ResNetParams(device, seed, stages, num_classes)
+        self.params = ResNetParams(device, seed, stages, num_classes, bucket_multiple)
         self.specs = {c[0]: c for c in self.params.convs}
         self.eps = bn_eps
         tot = sum(2 * c[2] for c in self.params.convs)
@@ -169,13 +184,17 @@ class ResNet50:
         return CN.bn_apply_stats(y, cs, cq, M, P.P(name + ".bn.gamma"), P.P(name + ".bn.beta"),
                                  residual, relu, self.eps, rm, rv, res_bn=res_bn)
 
-    def forward_backward(self, images, labels, on_bucket_ready=None):
-        """images: NHWC bf16 [N, H, W, 8]; labels int32 [N].  Returns (loss, accuracy)."""
+    def forward_backward(self, images, labels, on_bucket_ready=None, on_bucket_needed=None):
+        """images: NHWC bf16 [N, H, W, 8]; labels int32 [N].  Returns (loss, accuracy).
+        ``on_bucket_needed(b)``: called before the forward first reads bucket b's parameters
+        (the owner-sharded optimizer waits there for that bucket's all-gather)."""
         P = self.params
         N = images.shape[0]
+        need = on_bucket_needed if on_bucket_needed is not None else (lambda b: None)
         P.grad.zero_()
         self._stats_flat.zero_()  # every BN's (sum, sum of squares) accumulators, one memset
         saved = {}
+        need(0)
         c, st = self._conv_bn("conv1", images)
         if c.is_cuda and _STEM_POOL_BN:
             # the stem's relu(bn(c)) is formed inside the pool and never stored
@@ -192,6 +211,7 @@ class ResNet50:
         for si, (w, nb, st_) in enumerate(P.stages):
             for b in range(nb):
                 pre = "layer%d.%d." % (si + 1, b)
+                need(len(blocks) + 1)  # this block's bucket (its conv1 runs next)
                 if pend is None:
                     x_in = x
                     c1, s1 = self._conv_bn(pre + "conv1", x_in)
@@ -218,6 +238,7 @@ class ResNet50:
                 pend = (len(blocks) - 1, c3, s3, dsc)
         x, _, _ = self._finish_block(blocks, pend, None)
         pooled = CN.avgpool_fwd(x)                               # [N, 2048]
+        need(len(P.buckets) - 1)
         logits = B16.gemm(pooled, P.W("fc.weight"), False, True, bias=P.P("fc.bias"),
                           out_dtype=torch.float32)                # [N, 1024]
         loss_rows, correct, dlog = TR.mlm_xent(logits, labels, P.num_classes, 1.0 / N)

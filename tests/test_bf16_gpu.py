@@ -207,6 +207,54 @@ def test_gemm_8phase_epilogues_and_splitk(cfg8, gpu):
 
 
 @pytest.mark.parametrize("tb", [True, False])
+def test_gemm_persistent_tile_loop_exact_and_epilogue(gpu, tb):
+    """The persistent 8-phase tile loop (one block per CU walks tiles vb, vb + 256, ..; the
+    next tile's first K tile staged before this tile's epilogue): exact on integers and
+    bit-identical to the one-block-per-tile launch, for 1 / 2 / 3 K tiles (the prologue's
+    variants), an uneven last round (456 tiles: blocks with 2 and with 1 tile) and ragged M / N
+    edges; the epilogues (bias, GELU with aux, residual, column sums) on every tile."""
+    from distributedtensorflowexample_amd.ops._ext import hip
+
+    M, N = 19 * 256 - 100, 24 * 256 - 40  # 456 tiles of 256x256 (R = 200: no tail split)
+    g = torch.Generator().manual_seed(21)
+    for K in (64, 128, 192):
+        a = torch.randint(-3, 4, (M, K), generator=g).to(gpu, torch.bfloat16)
+        b = torch.randint(-3, 4, ((N, K) if tb else (K, N)), generator=g).to(gpu, torch.bfloat16)
+        old = hip().gemm_bf16_set_pers(1)
+        try:
+            y = bf16.gemm(a, b, False, tb, out_dtype=torch.float32)
+            hip().gemm_bf16_set_pers(0)
+            y0 = bf16.gemm(a, b, False, tb, out_dtype=torch.float32)
+        finally:
+            hip().gemm_bf16_set_pers(old)
+        assert torch.equal(y, _ref(a, b, False, tb)), K
+        assert torch.equal(y, y0), K
+    K = 192
+    x = _rand(M, K, dev=gpu, seed=22)
+    w = _rand(*((N, K) if tb else (K, N)), dev=gpu, seed=23, scale=0.3)
+    bias = torch.randn(N, device=gpu)
+    res = _rand(M, N, dev=gpu, seed=24)
+    outs = []
+    for pers in (1, 0):
+        aux = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        cs = torch.zeros(N, device=gpu)
+        old = hip().gemm_bf16_set_pers(pers)
+        try:
+            yb = bf16.gemm(x, w, False, tb, bias=bias, act="gelu", aux_out=aux, residual=res,
+                           colsum=cs)
+        finally:
+            hip().gemm_bf16_set_pers(old)
+        outs.append((yb, aux, cs))
+    yb, aux, cs = outs[0]
+    u = _ref(x, w, False, tb) + bias
+    ref = torch.nn.functional.gelu(u, approximate="tanh") + res.float()
+    assert torch.allclose(aux.float(), u, rtol=1e-2, atol=2e-2)
+    assert torch.allclose(yb.float(), ref, rtol=1e-2, atol=2e-2)
+    assert torch.allclose(cs, yb.float().sum(0), rtol=1e-3, atol=0.5)
+    assert torch.equal(yb, outs[1][0]) and torch.equal(aux, outs[1][1])
+
+
+@pytest.mark.parametrize("tb", [False, True])
 def test_gemm_tail_split_exact_and_epilogue(gpu, tb):
     """An 8-phase GEMM with one sparse last round (tiles 17 x 16 = 272: one round + 16 tiles)
     runs its last 256 rows on the 128x128 tile (gemm_tail_rows): exact on integers across the

@@ -75,27 +75,43 @@ def test_dp_replicas_identical_and_grad_is_shard_sum(kind):
     assert torch.allclose(res[0][1], ref, atol=1e-5, rtol=1e-4)
 
 
-def _zero1_worker(rank, world, port, q, zero1):
+def _zero1_worker(rank, world, port, q, zero1, kind="bert"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from distributedtensorflowexample_amd.models.bert import BertConfig
     from distributedtensorflowexample_amd.parallel.comm import TorchComm
-    from distributedtensorflowexample_amd.train.bert_trainer import BertTrainer
 
-    tr = BertTrainer(BertConfig.tiny(), 2, 32, "cpu", comm=TorchComm(), lr=1e-3,
-                     data_seed=10 + rank, zero1=zero1)
+    if kind == "bert":
+        from distributedtensorflowexample_amd.models.bert import BertConfig
+        from distributedtensorflowexample_amd.train.bert_trainer import BertTrainer
+
+        tr = BertTrainer(BertConfig.tiny(), 2, 32, "cpu", comm=TorchComm(), lr=1e-3,
+                         data_seed=10 + rank, zero1=zero1)
+    else:
+        from distributedtensorflowexample_amd.train.resnet_trainer import ResNetTrainer
+
+        tr = ResNetTrainer(2, "cpu", comm=TorchComm(), lr=0.05, image_size=32,
+                           stages=[(8, 1, 1), (16, 1, 2)], num_classes=10, data_seed=10 + rank,
+                           zero1=zero1)
     tr.run(3)
     tr.sync_params()
-    sd = {k: v.numpy().copy() for k, v in tr.model.params.state_dict().items()}
-    q.put((rank, sd, tr.model.params.master.numel(), tr.zero1))
+    P = tr.model.params
+    if kind == "bert":
+        sd = {k: v.numpy().copy() for k, v in P.state_dict().items()}
+    else:  # by name: the sharded layout pads every bucket to W shards
+        sd = {name: P.view(P.master, name).numpy().copy() for name, _, _ in P.layout}
+        sd.update({"bf/" + name: P.view(P.bf, name).float().numpy().copy()
+                   for name, _, _ in P.layout})
+        sd.update({"running/" + n + "/" + str(i): t.numpy().copy()
+                   for n, ts in P.running.items() for i, t in enumerate(ts)})
+    q.put((rank, sd, P.master.numel(), tr.zero1))
     dist.destroy_process_group()
 
 
-def _run(world, zero1):
+def _run(world, zero1, kind="bert"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_zero1_worker, args=(r, world, port, q, zero1))
+    procs = [ctx.Process(target=_zero1_worker, args=(r, world, port, q, zero1, kind))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -121,3 +137,25 @@ def test_bert_zero1_matches_replicated_adam(world):
     for k, v in rep[0][0].items():                # same trajectory as the replicated AdamW
         d = abs(torch.from_numpy(sh[0][0][k]) - torch.from_numpy(v)).max().item()
         assert d <= 1e-6 + 1e-5 * abs(torch.from_numpy(v)).max().item(), (k, d)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_resnet_zero1_matches_replicated_sgd(world):
+    """ResNet owner-sharded momentum SGD (reduce-scatter -> SGD on this rank's shard ->
+    all-gather beside the next forward) against the replicated optimizer over 3 steps: every
+    parameter, its bf16 working copy and the BatchNorm running statistics to f32 rounding,
+    replicas identical, every bucket padded to W aligned shards."""
+    sh = _run(world, True, "resnet")
+    rep = _run(world, False, "resnet")
+    assert all(z for _, _, z in sh.values()) and not any(z for _, _, z in rep.values())
+    assert sh[0][1] % (64 * world) == 0
+    for r in range(1, world):  # (BatchNorm running statistics are per-rank: local batches)
+        for k in sh[0][0]:
+            if not k.startswith("running/"):
+                assert (sh[r][0][k] == sh[0][0][k]).all(), (r, k)
+    for k, v in rep[0][0].items():
+        d = abs(torch.from_numpy(sh[0][0][k]) - torch.from_numpy(v)).max().item()
+        tol = 1e-6 + 1e-5 * abs(torch.from_numpy(v)).max().item()
+        if k.startswith("bf/"):
+            tol = 1e-2 * max(1.0, abs(torch.from_numpy(v)).max().item())  # one bf16 ulp
+        assert d <= tol, (k, d)

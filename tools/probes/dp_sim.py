@@ -16,7 +16,9 @@ fold).  Against the 1-GPU step, each switch A/B'd in the same process, interleav
   dp_prio_hi    the comm stream at the highest HIP stream priority (default: the lowest,
                 the compute stream's)
   BERT: dp_nows (no weight-gradient stream), 1gpu_nofold (the 1-GPU step without the fold)
-  ResNet: dp_ws (weight gradients on a side stream)
+  ResNet: dp_ws (weight gradients on a side stream), dp_zero1 (the owner-sharded momentum SGD:
+          reduce-scatter per bucket, SGD on the rank's shard, shards all-gathered beside the
+          next forward -- DTFX_RESNET_ZERO1=1)
 
 What this cannot show is link time: the all-reduce's bytes cross local HBM, not xGMI.
 
@@ -65,6 +67,8 @@ def make(model, variant, world, dev, a):
         env["DTFX_BERT_FOLD"] = "0"
     if variant == "dp_ws":
         env["DTFX_RESNET_WSTREAM"] = "1"
+    if variant == "dp_zero1":
+        env["DTFX_RESNET_ZERO1"] = "1"
     if variant == "dp_prio_hi":
         env["DTFX_COMM_PRIORITY"] = str(torch.cuda.Stream.priority_range()[1])
     old = {k: os.environ.get(k) for k in env}
@@ -111,7 +115,7 @@ def main():
         variants = ["1gpu", "dp", "dp_null", "dp_nows", "dp_bw256", "dp_bw64", "dp_prio_hi",
                     "1gpu_nofold"]
     else:
-        variants = ["1gpu", "dp", "dp_null", "dp_bw256", "dp_bw64", "dp_prio_hi", "dp_ws"]
+        variants = ["1gpu", "dp", "dp_zero1", "dp_null", "dp_bw256", "dp_bw64", "dp_prio_hi", "dp_ws"]
     trainers = {}
     for v in variants:
         tr = make(a.model, v, a.world, dev, a)
