@@ -60,6 +60,16 @@ void conv1x1_pro_launch(int, int, int, int, const void*, const void*, const floa
                         const void*, int, void*, const void*, const void*, const void*,
                         const float*, const float*, float*, float*, void*, hipStream_t,
                         int = 0, int = 0);
+void conv1x1_pro_fwdbn_launch(int, int, int, int, const void*, const void*, long long,
+                              const float*, const float*, float, float*, float*, float*, float*,
+                              float, const float*, const float*, const float*, const float*,
+                              const float*, const float*, float*, float*, float*, float*, void*,
+                              const void*, int, void*, float*, float*, hipStream_t);
+void conv1x1_pro_bwdbn_launch(int, int, int, const void*, const void*, long long, const float*,
+                              const float*, const float*, const float*, const float*, void*,
+                              const void*, int, void*, const void*, const void*, const void*,
+                              const float*, const float*, float*, float*, void*, hipStream_t, int,
+                              int);
 void bn_fwd_coef_launch(long long, int, const float*, const float*, float, float*, float*, float*,
                         float*, float, const float*, const float*, const float*, const float*,
                         const float*, const float*, float*, float*, float*, float*, float*,
@@ -338,6 +348,44 @@ void register_nn(py::module_& m) {
      py::arg("pq"), py::arg("wt"), py::arg("s"), py::arg("res_h") = 0, py::arg("res_w") = 0,
      "res_h / res_w (mode 2, wide): the residual is a stride-2 conv's data gradient stored "
      "compact [pixels / 4][N] for an res_h x res_w grid (zero at odd rows / columns)");
+  m.def("conv1x1_pro_fwdbn", [](int mode, int M, int K, int N, uintptr_t s0, uintptr_t s1,
+                                long long Mst, uintptr_t sum, uintptr_t sq, float eps,
+                                uintptr_t mean, uintptr_t rstd, uintptr_t run_mean,
+                                uintptr_t run_var, float momentum, uintptr_t g, uintptr_t b,
+                                uintptr_t sum2, uintptr_t sq2, uintptr_t g2, uintptr_t b2,
+                                uintptr_t mean2, uintptr_t rstd2, uintptr_t run_mean2,
+                                uintptr_t run_var2, uintptr_t xo, uintptr_t w, int ldw,
+                                uintptr_t y, uintptr_t ps, uintptr_t pq, uintptr_t s) {
+    dtfx::conv1x1_pro_fwdbn_launch(
+        mode, M, K, N, P<const void>(s0), P<const void>(s1), Mst, P<const float>(sum),
+        P<const float>(sq), eps, P<float>(mean), P<float>(rstd), P<float>(run_mean),
+        P<float>(run_var), momentum, P<const float>(g), P<const float>(b), P<const float>(sum2),
+        P<const float>(sq2), P<const float>(g2), P<const float>(b2), P<float>(mean2),
+        P<float>(rstd2), P<float>(run_mean2), P<float>(run_var2), P<void>(xo), P<const void>(w),
+        ldw, P<void>(y), P<float>(ps), P<float>(pq), S(s));
+  }, "conv1x1_pro mode 1 / 3 with the BatchNorm coefficients formed in the kernel from the "
+     "BN's column sums and affine (bn_fwd_coef's outputs written by block 0): no coefficient "
+     "launch");
+  m.def("conv1x1_pro_bwdbn", [](int M, int K, int N, uintptr_t s0, uintptr_t s1, long long Mst,
+                                uintptr_t bmean, uintptr_t brstd, uintptr_t g, uintptr_t sum_dy,
+                                uintptr_t sum_dyxh, uintptr_t xo, uintptr_t w, int ldw,
+                                uintptr_t y, uintptr_t res, uintptr_t relu_y, uintptr_t bn_x,
+                                uintptr_t mean, uintptr_t rstd, uintptr_t ps, uintptr_t pq,
+                                uintptr_t wt, uintptr_t s, int res_h, int res_w) {
+    dtfx::conv1x1_pro_bwdbn_launch(
+        M, K, N, P<const void>(s0), P<const void>(s1), Mst, P<const float>(bmean),
+        P<const float>(brstd), P<const float>(g), P<const float>(sum_dy),
+        P<const float>(sum_dyxh), P<void>(xo), P<const void>(w), ldw, P<void>(y),
+        P<const void>(res), P<const void>(relu_y), P<const void>(bn_x), P<const float>(mean),
+        P<const float>(rstd), P<float>(ps), P<float>(pq), P<void>(wt), S(s), res_h, res_w);
+  }, py::arg("M"), py::arg("K"), py::arg("N"), py::arg("s0"), py::arg("s1"), py::arg("Mst"),
+     py::arg("bmean"), py::arg("brstd"), py::arg("gamma"), py::arg("sum_dy"),
+     py::arg("sum_dyxh"), py::arg("xo"), py::arg("w"), py::arg("ldw"), py::arg("y"),
+     py::arg("res"), py::arg("relu_y"), py::arg("bn_x"), py::arg("mean"), py::arg("rstd"),
+     py::arg("ps"), py::arg("pq"), py::arg("wt"), py::arg("s"), py::arg("res_h") = 0,
+     py::arg("res_w") = 0,
+     "conv1x1_pro mode 2 with BatchNorm backward's coefficients formed in the kernel from "
+     "mean / rstd / gamma and the final reductions: no coefficient launch");
   m.def("bn_fwd_coef", [](long long M, int C, uintptr_t sum, uintptr_t sq, float eps, uintptr_t mean,
                           uintptr_t rstd, uintptr_t run_mean, uintptr_t run_var, float momentum,
                           uintptr_t g, uintptr_t b, uintptr_t sum2, uintptr_t sq2, uintptr_t g2,

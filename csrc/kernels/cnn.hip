@@ -6,6 +6,7 @@
 // North-star config 4 of BASELINE.json (ResNet-50 synthetic ImageNet); the
 // reference itself has no convolutional model (worker.py:47-54).
 #include "common.h"
+#include "bn_common.h"
 
 #include <algorithm>
 
@@ -110,37 +111,7 @@ __global__ void bn_finalize_kernel(int C, float inv_m, float unbias, const float
 // affine (gamma2 / beta2) before the add: a bottleneck's output relu(bn3(c3) + bn_ds(cds)) in
 // one pass over c3 and the raw downsample conv output cds -- the normalised shortcut is never
 // written and read back (the downsample backward only needs cds and its mean / rstd).
-struct BnStats {
-  const float* ssum;
-  const float* ssq;
-  float inv_m, eps, unbias, momentum;
-  float* mean_out;
-  float* rstd_out;
-  float* run_mean;
-  float* run_var;
-  const float* gamma2;  // st2 only: the residual BN's affine
-  const float* beta2;
-};
-__device__ __forceinline__ void bn_store_stats(const BnStats& st, int c, float mu, float rs) {
-  st.mean_out[c] = mu;
-  st.rstd_out[c] = rs;
-  if (st.run_mean) {
-    const float var = fmaxf(st.ssq[c] * st.inv_m - mu * mu, 0.f);
-    st.run_mean[c] = st.momentum * st.run_mean[c] + (1.f - st.momentum) * mu;
-    st.run_var[c] = st.momentum * st.run_var[c] + (1.f - st.momentum) * var * st.unbias;
-  }
-}
-template <bool STATS>
-__device__ __forceinline__ void bn_coef(const BnStats& st, const float* mean, const float* rstd, int c,
-                                        float& mu, float& rs) {
-  if (STATS) {
-    mu = st.ssum[c] * st.inv_m;
-    rs = rsqrtf(fmaxf(st.ssq[c] * st.inv_m - mu * mu, 0.f) + st.eps);
-  } else {
-    mu = mean[c];
-    rs = rstd[c];
-  }
-}
+// (BnStats, bn_store_stats, bn_coef: bn_common.h)
 // (STATS / RBN are template parameters: as run-time flags the per-element residual branch and
 // the coefficient loads ended up inside the streaming loop -- 4x slower)
 template <int U, bool STATS, bool RBN>

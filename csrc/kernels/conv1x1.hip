@@ -17,6 +17,7 @@
 // inputs move as 8-B vectors of NHWC rows, and a lane's statistics stay its own 4 channels
 // for the whole block.  Compute wave w owns 32 channels (2 MFMA row tiles) of the block's 256.
 #include "common.h"
+#include "bn_common.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -71,7 +72,7 @@ template <int K, int PRO = 0>
 __global__ __launch_bounds__(576, fbpc<K>() == 2 ? 5 : 3) void conv1x1_fwd_kernel(
     int M, int N, const unsigned short* __restrict__ x, const unsigned short* __restrict__ w,
     int ldw, unsigned short* __restrict__ y, float* __restrict__ ps, float* __restrict__ pq,
-    const float* __restrict__ coef, unsigned short* __restrict__ xo) {
+    BnCoefSrc coef, unsigned short* __restrict__ xo) {
   constexpr int FTM = ftm<K>(), KK = K / 32, MT = FTM / 16, CPR = K / 8;  // chunks per row
   constexpr int TB = FTM * K * 2, NQ = TB / 1024;  // tile bytes, DMA rounds per tile
   extern __shared__ __attribute__((aligned(16))) char sm[];
@@ -135,9 +136,12 @@ __global__ __launch_bounds__(576, fbpc<K>() == 2 ? 5 : 3) void conv1x1_fwd_kerne
   float* ctab = (float*)(stg + FTM * OPITCH);  // [2][K]
   if constexpr (PRO != 0) {
     for (int i = tid; i < K; i += NW * 64) {
-      ctab[i] = coef[i];
-      ctab[K + i] = coef[2 * K + i];
+      float a, b, c, d;
+      bn_coef_at(coef, K, i, a, b, c, d);
+      ctab[i] = a;
+      ctab[K + i] = c;
     }
+    if (blockIdx.x == 0) bn_coef_duty(coef, K, tid, NW * 64);
   }
   __syncthreads();  // tile 0 in LDS
   for (int it = 0; it < nmy; ++it) {
@@ -249,7 +253,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
     const unsigned short* __restrict__ relu_y, const unsigned short* __restrict__ bn_x,
     const float* __restrict__ bn_mean, const float* __restrict__ bn_rstd, float* __restrict__ ps,
     float* __restrict__ pq, const unsigned short* __restrict__ src1 = nullptr,
-    const float* __restrict__ coef = nullptr, unsigned short* __restrict__ xo = nullptr,
+    BnCoefSrc coef = BnCoefSrc{}, unsigned short* __restrict__ xo = nullptr,
     int rs_h = 0, int rs_w = 0) {
   constexpr int KK = K / 32, CPR = K / 8;
   constexpr int DYB = DTM * K * 2, SB = DTM * NC * 2, NSIDE = (RES ? 1 : 0) + (BN ? 2 : 0);
@@ -344,9 +348,8 @@ __global__ __launch_bounds__(576, 1) void conv1x1_dgrad_kernel(
   if constexpr (PRO != 0) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      ca[u] = coef[tcc * 8 + u];
-      cb_[u] = coef[K + tcc * 8 + u];
-      cd[u] = coef[3 * K + tcc * 8 + u];
+      float c_;
+      bn_coef_at(coef, K, tcc * 8 + u, ca[u], cb_[u], c_, cd[u]);
     }
   }
   const int c0 = wave * (NTW * 16);  // the wave's channels inside the slice
@@ -501,7 +504,7 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
     unsigned short* __restrict__ y, const unsigned short* __restrict__ relu_y,
     const unsigned short* __restrict__ bn_x, const float* __restrict__ bn_mean,
     const float* __restrict__ bn_rstd, float* __restrict__ ps, float* __restrict__ pq,
-    const unsigned short* __restrict__ src1, const float* __restrict__ coef,
+    const unsigned short* __restrict__ src1, BnCoefSrc coef,
     unsigned short* __restrict__ xo) {
   constexpr int NT = N_ / 16, KS = 8 / NT, KKW = K / 32 / KS, CPR = K / 8, NCH = N_ / 8;
   constexpr int TM = ntm<K, N_, DG, PRO>(), MT = TM / 16;
@@ -586,12 +589,8 @@ __global__ __launch_bounds__(576, 1) void conv1x1_narrow_kernel(
   float ca[8], cb[8], cc[8], cd[8];
   if constexpr (PRO != 0) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      ca[u] = coef[tcc * 8 + u];
-      cb[u] = coef[K + tcc * 8 + u];
-      cc[u] = coef[2 * K + tcc * 8 + u];
-      cd[u] = coef[3 * K + tcc * 8 + u];
-    }
+    for (int u = 0; u < 8; ++u) bn_coef_at(coef, K, tcc * 8 + u, ca[u], cb[u], cc[u], cd[u]);
+    if (PRO == 1 && blockIdx.x == 0) bn_coef_duty(coef, K, tid, 512);
   }
   __syncthreads();  // tile 0 in LDS
   for (int it = 0; it < nmy; ++it) {
@@ -745,7 +744,7 @@ template <int K, int N_, bool DG, int PRO = 0>
 static void conv1x1_narrow_go(int M, const void* x, const void* w, void* y, const void* relu_y,
                               const void* bn_x, const float* mean, const float* rstd, float* ps,
                               float* pq, hipStream_t s, const void* s1 = nullptr,
-                              const float* coef = nullptr, void* xo = nullptr) {
+                              const BnCoefSrc& coef = BnCoefSrc{}, void* xo = nullptr) {
   using namespace pw;
   constexpr int TM = ntm<K, N_, DG, PRO>(), NQT = nqt_narrow<K, N_, DG, PRO>();
   constexpr int DB = 2 * NQT <= 63 ? 4 : 3;
@@ -767,7 +766,7 @@ static void conv1x1_narrow_go(int M, const void* x, const void* w, void* y, cons
 
 template <int K, int PRO = 0>
 static void conv1x1_fwd_go(dim3 grid, int M, int N, const void* x, const void* w, int ldw, void* y,
-                           float* ps, float* pq, hipStream_t s, const float* coef = nullptr,
+                           float* ps, float* pq, hipStream_t s, const BnCoefSrc& coef = BnCoefSrc{},
                            void* xo = nullptr) {
   using namespace pw;
   const size_t lds = (size_t)NBUF * ftm<K>() * K * 2 + (size_t)ftm<K>() * OPITCH +
@@ -788,7 +787,7 @@ static void conv1x1_dgrad_go(dim3 grid, int M, int N, const void* dy, const void
                              void* dx, const void* res, const void* relu_y, const void* bn_x,
                              const float* mean, const float* rstd, float* ps, float* pq,
                              hipStream_t s, const void* src1 = nullptr,
-                             const float* coef = nullptr, void* xo = nullptr, int rs_h = 0,
+                             const BnCoefSrc& coef = BnCoefSrc{}, void* xo = nullptr, int rs_h = 0,
                              int rs_w = 0) {
   using namespace pw;
   const size_t lds =
@@ -816,7 +815,7 @@ static void conv1x1_dgrad_pick(dim3 grid, int M, int N, const void* dy, const vo
                                void* dx, const void* res, const void* relu_y, const void* bn_x,
                                const float* mean, const float* rstd, float* ps, float* pq,
                                hipStream_t s, const void* src1 = nullptr,
-                               const float* coef = nullptr, void* xo = nullptr, int rs_h = 0,
+                               const BnCoefSrc& coef = BnCoefSrc{}, void* xo = nullptr, int rs_h = 0,
                                int rs_w = 0) {
   if (res && ps)
     conv1x1_dgrad_go<K, true, true, PRO>(grid, M, N, dy, w, ldw, dx, res, relu_y, bn_x, mean, rstd, ps, pq, s, src1, coef, xo, rs_h, rs_w);
@@ -899,7 +898,9 @@ void conv1x1_launch(int mode, int M, int K, int N, const void* x, const void* w,
 //          conv1x1_launch mode 2 (+ residual, optional BN);
 //  mode 3 (wide forward):    op = relu(s0 a + c) -> xo; y = op W^T + statistics rows (a BN +
 //          ReLU inside the following expansion conv).
-// Partial statistics rows: conv1x1_rows().
+// Partial statistics rows: conv1x1_rows().  coef: the [4][K] rows of bn_fwd_coef /
+// bn_bwd_coef, or (rows null) the BatchNorm's own sources, the coefficients then formed by
+// every block (bn_common.h BnCoefSrc) -- no coefficient launch.
 bool conv1x1_pro_applies(int mode, int M, int K, int N) {
   if (M <= 0 || M % 64) return false;
   const bool narrow = conv1x1_narrow(K, N);
@@ -908,7 +909,7 @@ bool conv1x1_pro_applies(int mode, int M, int K, int N) {
   return mode == 2 && conv1x1_applies(M, K, N);
 }
 void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const void* s1,
-                        const float* coef, void* xo, const void* w, int ldw, void* y,
+                        const BnCoefSrc& coef, void* xo, const void* w, int ldw, void* y,
                         const void* res, const void* relu_y, const void* bn_x, const float* mean,
                         const float* rstd, float* ps, float* pq, void* wt, hipStream_t s,
                         int res_h, int res_w) {
@@ -919,7 +920,16 @@ void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const voi
                              "gradient and even res_h / res_w dividing the pixels");
   if (!conv1x1_pro_applies(mode, M, K, N)) throw std::runtime_error("conv1x1_pro: unsupported shape");
   const bool narrow = conv1x1_narrow(K, N);
-  if (!s0 || !coef || (mode != 3 && !s1) || ((mode == 1 || mode == 3) && (!xo || !ps || !pq)) ||
+  const bool formed = !coef.rows;  // coefficients formed in the kernel from the BN's sources
+  if (formed && (!coef.gamma || (coef.bwd ? (!coef.mean || !coef.rstd || !coef.sum_dy ||
+                                             !coef.sum_dyxh)
+                                           : (!coef.beta || !coef.st.ssum || !coef.st.ssq ||
+                                              !coef.st.mean_out || !coef.st.rstd_out)) ||
+                 (coef.bwd != 0) != (mode == 2)))
+    throw std::runtime_error("conv1x1_pro: formed coefficients need the BatchNorm's sources "
+                             "(forward: sums, affine, mean / rstd outputs; backward: mean, rstd, "
+                             "gamma, reductions)");
+  if (!s0 || (mode != 3 && !s1) || ((mode == 1 || mode == 3) && (!xo || !ps || !pq)) ||
       (mode == 1 && ldw != K) || (mode == 2 && !wt) ||
       (mode == 2 && narrow && res) || (mode == 2 && !ps && narrow && (relu_y || bn_x)) ||
       ((ps != nullptr) != (pq != nullptr)) || (mode == 2 && ps && (!relu_y || !bn_x || !mean || !rstd)))
@@ -927,7 +937,7 @@ void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const voi
                              "gradient wt, relu_y, bn_x, mean, rstd) required");
   if (ldw % 8 || (((uintptr_t)s0 | (uintptr_t)s1 | (uintptr_t)xo | (uintptr_t)w | (uintptr_t)y |
                    (uintptr_t)res | (uintptr_t)relu_y | (uintptr_t)bn_x | (uintptr_t)wt |
-                   (uintptr_t)coef) & 15))
+                   (uintptr_t)coef.rows) & 15))
     throw std::runtime_error("conv1x1_pro: ldw % 8, 16-B aligned tensors");
   const void* wv = w;
   if (mode == 2) {
@@ -965,6 +975,66 @@ void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const voi
     }
   }
   DTFX_HIP_CHECK(hipGetLastError());
+}
+
+// (host entry points: the coefficient rows of bn_fwd_coef / bn_bwd_coef ...)
+void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const void* s1,
+                        const float* coef, void* xo, const void* w, int ldw, void* y,
+                        const void* res, const void* relu_y, const void* bn_x, const float* mean,
+                        const float* rstd, float* ps, float* pq, void* wt, hipStream_t s,
+                        int res_h, int res_w) {
+  if (!coef) throw std::runtime_error("conv1x1_pro: coefficient rows required");
+  BnCoefSrc cs{};
+  cs.rows = coef;
+  conv1x1_pro_launch(mode, M, K, N, s0, s1, cs, xo, w, ldw, y, res, relu_y, bn_x, mean, rstd, ps,
+                     pq, wt, s, res_h, res_w);
+}
+// ... or the forward BatchNorm's sources (modes 1 / 3: the statistics of s0 over Mst rows, its
+// affine, the residual's own BN for mode 1 with sum2 set): mean / rstd / running statistics as
+// bn_fwd_coef_launch writes them, by block 0 of the conv
+void conv1x1_pro_fwdbn_launch(int mode, int M, int K, int N, const void* s0, const void* s1,
+                              long long Mst, const float* sum, const float* sq, float eps,
+                              float* mean_out, float* rstd_out, float* run_mean, float* run_var,
+                              float momentum, const float* gamma, const float* beta,
+                              const float* sum2, const float* sq2, const float* g2,
+                              const float* b2, float* mean2, float* rstd2, float* run_mean2,
+                              float* run_var2, void* xo, const void* w, int ldw, void* y,
+                              float* ps, float* pq, hipStream_t s) {
+  if (mode != 1 && mode != 3) throw std::runtime_error("conv1x1_pro_fwdbn: mode 1 or 3");
+  if (sum2 && (mode != 1 || !sq2 || !g2 || !b2 || !mean2 || !rstd2))
+    throw std::runtime_error("conv1x1_pro_fwdbn: the residual BN (mode 1) needs sq2, gamma2, "
+                             "beta2, mean2, rstd2");
+  const float inv_m = 1.f / (float)Mst, unbias = Mst > 1 ? (float)Mst / (float)(Mst - 1) : 1.f;
+  BnCoefSrc cs{};
+  cs.st = BnStats{sum, sq, inv_m, eps, unbias, momentum, mean_out, rstd_out, run_mean, run_var,
+                  nullptr, nullptr};
+  if (sum2)
+    cs.st2 = BnStats{sum2, sq2, inv_m, eps, unbias, momentum, mean2, rstd2, run_mean2, run_var2,
+                     g2, b2};
+  cs.gamma = gamma;
+  cs.beta = beta;
+  conv1x1_pro_launch(mode, M, K, N, s0, s1, cs, xo, w, ldw, y, nullptr, nullptr, nullptr,
+                     nullptr, nullptr, ps, pq, nullptr, s, 0, 0);
+}
+// ... or the backward BatchNorm's sources (mode 2: mean / rstd of the BN, its gamma and the
+// final reductions sum_dy / sum_dyxh over Mst rows)
+void conv1x1_pro_bwdbn_launch(int M, int K, int N, const void* s0, const void* s1,
+                              long long Mst, const float* bmean, const float* brstd,
+                              const float* gamma, const float* sum_dy, const float* sum_dyxh,
+                              void* xo, const void* w, int ldw, void* y, const void* res,
+                              const void* relu_y, const void* bn_x, const float* mean,
+                              const float* rstd, float* ps, float* pq, void* wt, hipStream_t s,
+                              int res_h, int res_w) {
+  BnCoefSrc cs{};
+  cs.bwd = 1;
+  cs.gamma = gamma;
+  cs.mean = bmean;
+  cs.rstd = brstd;
+  cs.sum_dy = sum_dy;
+  cs.sum_dyxh = sum_dyxh;
+  cs.inv_m = 1.f / (float)Mst;
+  conv1x1_pro_launch(2, M, K, N, s0, s1, cs, xo, w, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq,
+                     wt, s, res_h, res_w);
 }
 
 }  // namespace dtfx

@@ -270,6 +270,11 @@ def bn_prologue_applies(x, K, N, mode):
 
 
 _BN_PRO = os.environ.get("DTFX_BN_PROLOGUE", "1") != "0"
+# The prologue kernels form the BatchNorm coefficients themselves from the BN's sums / affine
+# (bn_common.h BnCoefSrc; block 0 writes mean / rstd / running statistics) instead of reading
+# the rows of a separate bn_fwd_coef / bn_bwd_coef launch.  DTFX_BN_COEF_FUSED=0: the separate
+# launch (A/B runs).
+_BN_COEF_FUSED = os.environ.get("DTFX_BN_COEF_FUSED", "1") != "0"
 _BN_PRO_WIDE = os.environ.get("DTFX_BN_PROLOGUE_WIDE", "1") != "0"
 
 
@@ -299,17 +304,25 @@ def bn_out_conv1x1(c, s, q, M, gamma, beta, residual, w, colsum, colsq, eps=1e-5
     s2 = q2 = g2 = b2 = rm2 = rv2 = None
     if res_bn is not None:
         s2, q2, g2, b2, rm2, rv2 = res_bn
-    hip().bn_fwd_coef(int(M), K, ptr(s), ptr(q), float(eps), ptr(st[0]), ptr(st[1]), ptr(run_mean),
-                      ptr(run_var), float(momentum), ptr(gamma), ptr(beta), ptr(s2), ptr(q2),
-                      ptr(g2), ptr(b2), ptr(st[2] if res_bn is not None else None),
-                      ptr(st[3] if res_bn is not None else None), ptr(rm2), ptr(rv2), ptr(coef),
-                      stream_handle())
     out = torch.empty_like(c)
     y = torch.empty(*c.shape[:-1], Nout, device=dev, dtype=BF16)
     part = torch.empty(2, hip().conv1x1_rows(1, Mrows, K, Nout), Nout, device=dev)
-    hip().conv1x1_pro(1, Mrows, K, Nout, ptr(c), ptr(residual), ptr(coef), ptr(out), ptr(w),
-                      w.stride(0), ptr(y), 0, 0, 0, 0, 0, ptr(part[0]), ptr(part[1]), 0,
-                      stream_handle())
+    m2 = ptr(st[2] if res_bn is not None else None)
+    r2 = ptr(st[3] if res_bn is not None else None)
+    if _BN_COEF_FUSED:
+        hip().conv1x1_pro_fwdbn(1, Mrows, K, Nout, ptr(c), ptr(residual), int(M), ptr(s), ptr(q),
+                                float(eps), ptr(st[0]), ptr(st[1]), ptr(run_mean), ptr(run_var),
+                                float(momentum), ptr(gamma), ptr(beta), ptr(s2), ptr(q2),
+                                ptr(g2), ptr(b2), m2, r2, ptr(rm2), ptr(rv2), ptr(out), ptr(w),
+                                w.stride(0), ptr(y), ptr(part[0]), ptr(part[1]), stream_handle())
+    else:
+        hip().bn_fwd_coef(int(M), K, ptr(s), ptr(q), float(eps), ptr(st[0]), ptr(st[1]),
+                          ptr(run_mean), ptr(run_var), float(momentum), ptr(gamma), ptr(beta),
+                          ptr(s2), ptr(q2), ptr(g2), ptr(b2), m2, r2, ptr(rm2), ptr(rv2),
+                          ptr(coef), stream_handle())
+        hip().conv1x1_pro(1, Mrows, K, Nout, ptr(c), ptr(residual), ptr(coef), ptr(out), ptr(w),
+                          w.stride(0), ptr(y), 0, 0, 0, 0, 0, ptr(part[0]), ptr(part[1]), 0,
+                          stream_handle())
     hip().colpart_reduce(part.shape[1], Nout, ptr(part[0]), ptr(part[1]), ptr(colsum), ptr(colsq),
                          stream_handle())
     if res_bn is None:
@@ -332,15 +345,22 @@ def bn_relu_conv1x1(c, s, q, M, gamma, beta, w, colsum, colsq, eps=1e-5, run_mea
     Nout = w.shape[0]
     Mrows = c.numel() // K
     st = torch.empty(2, K, device=c.device)
-    coef = torch.empty(4, K, device=c.device)
-    hip().bn_fwd_coef(int(M), K, ptr(s), ptr(q), float(eps), ptr(st[0]), ptr(st[1]), ptr(run_mean),
-                      ptr(run_var), float(momentum), ptr(gamma), ptr(beta), 0, 0, 0, 0, 0, 0, 0, 0,
-                      ptr(coef), stream_handle())
     a = torch.empty_like(c)
     y = torch.empty(*c.shape[:-1], Nout, device=c.device, dtype=BF16)
     part = torch.empty(2, hip().conv1x1_rows(1, Mrows, K, Nout), Nout, device=c.device)
-    hip().conv1x1_pro(3, Mrows, K, Nout, ptr(c), 0, ptr(coef), ptr(a), ptr(w), w.stride(0), ptr(y),
-                      0, 0, 0, 0, 0, ptr(part[0]), ptr(part[1]), 0, stream_handle())
+    if _BN_COEF_FUSED:
+        hip().conv1x1_pro_fwdbn(3, Mrows, K, Nout, ptr(c), 0, int(M), ptr(s), ptr(q), float(eps),
+                                ptr(st[0]), ptr(st[1]), ptr(run_mean), ptr(run_var),
+                                float(momentum), ptr(gamma), ptr(beta), 0, 0, 0, 0, 0, 0, 0, 0,
+                                ptr(a), ptr(w), w.stride(0), ptr(y), ptr(part[0]), ptr(part[1]),
+                                stream_handle())
+    else:
+        coef = torch.empty(4, K, device=c.device)
+        hip().bn_fwd_coef(int(M), K, ptr(s), ptr(q), float(eps), ptr(st[0]), ptr(st[1]),
+                          ptr(run_mean), ptr(run_var), float(momentum), ptr(gamma), ptr(beta), 0,
+                          0, 0, 0, 0, 0, 0, 0, ptr(coef), stream_handle())
+        hip().conv1x1_pro(3, Mrows, K, Nout, ptr(c), 0, ptr(coef), ptr(a), ptr(w), w.stride(0),
+                          ptr(y), 0, 0, 0, 0, 0, ptr(part[0]), ptr(part[1]), 0, stream_handle())
     hip().colpart_reduce(part.shape[1], Nout, ptr(part[0]), ptr(part[1]), ptr(colsum), ptr(colsq),
                          stream_handle())
     return a, y, st[0], st[1]
@@ -419,9 +439,11 @@ def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, 
     Cin = w.shape[1]
     M = c.numel() // K
     dev = c.device
-    coef = torch.empty(4, K, device=dev)
-    hip().bn_bwd_coef(M, K, ptr(mean), ptr(rstd), ptr(gamma), ptr(sum_dy), ptr(sum_dyxh),
-                      ptr(coef), stream_handle())
+    coef = None
+    if not _BN_COEF_FUSED:
+        coef = torch.empty(4, K, device=dev)
+        hip().bn_bwd_coef(M, K, ptr(mean), ptr(rstd), ptr(gamma), ptr(sum_dy), ptr(sum_dyxh),
+                          ptr(coef), stream_handle())
     dc = torch.empty_like(c) if want_dc else None
     dx = torch.empty(*c.shape[:-1], Cin, device=dev, dtype=BF16)
     wt = torch.empty(Cin, K, device=dev, dtype=BF16)
@@ -432,10 +454,19 @@ def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, 
             raise ValueError("fused BN backward: y and x must have the dgrad output's shape")
         part = torch.empty(2, hip().conv1x1_rows(2, M, K, Cin), Cin, device=dev)
     rh, rw = (c.shape[1], c.shape[2]) if residual is not None and residual_s2 else (0, 0)
-    hip().conv1x1_pro(2, M, K, Cin, ptr(de), ptr(c), ptr(coef), ptr(dc), ptr(w), w.stride(0),
-                      ptr(dx), ptr(residual), ptr(y), ptr(x), ptr(bmean), ptr(brstd),
-                      ptr(None if part is None else part[0]), ptr(None if part is None else part[1]),
-                      ptr(wt), stream_handle(), res_h=rh, res_w=rw)
+    if coef is None:
+        hip().conv1x1_pro_bwdbn(M, K, Cin, ptr(de), ptr(c), M, ptr(mean), ptr(rstd), ptr(gamma),
+                                ptr(sum_dy), ptr(sum_dyxh), ptr(dc), ptr(w), w.stride(0),
+                                ptr(dx), ptr(residual), ptr(y), ptr(x), ptr(bmean), ptr(brstd),
+                                ptr(None if part is None else part[0]),
+                                ptr(None if part is None else part[1]), ptr(wt),
+                                stream_handle(), res_h=rh, res_w=rw)
+    else:
+        hip().conv1x1_pro(2, M, K, Cin, ptr(de), ptr(c), ptr(coef), ptr(dc), ptr(w), w.stride(0),
+                          ptr(dx), ptr(residual), ptr(y), ptr(x), ptr(bmean), ptr(brstd),
+                          ptr(None if part is None else part[0]),
+                          ptr(None if part is None else part[1]), ptr(wt), stream_handle(),
+                          res_h=rh, res_w=rw)
     if part is not None:
         hip().colpart_reduce(part.shape[1], Cin, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
                              stream_handle())

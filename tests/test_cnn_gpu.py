@@ -509,3 +509,71 @@ def test_stem_wgrad_bn_prologue(gpu):
     assert torch.allclose(dg1, dg2) and torch.allclose(db1, db2)
     # (both form the same bf16 dc; the f32 atomics sum in different orders)
     assert (got - ref).abs().max() < 1e-3 * ref.abs().max()
+
+
+@pytest.mark.parametrize("N,H,W,K,Co,ds", [
+    (2, 16, 16, 256, 64, True),    # narrow forward (PRO 1) with the downsample's own BN
+    (4, 8, 8, 512, 128, False),    # narrow forward, identity shortcut
+])
+def test_bn_coefficients_formed_in_kernel_match_coef_launch(gpu, monkeypatch, N, H, W, K, Co, ds):
+    """the 1x1 prologue kernels form the BatchNorm coefficients themselves
+    (bn_common.h BnCoefSrc; block 0 writes mean / rstd / running statistics) instead of reading
+    the rows of a bn_fwd_coef / bn_bwd_coef launch.  Against that separate launch on the GPU:
+    the same outputs and statistics for the three prologue forms (bottleneck output -> narrow
+    conv1, BN + ReLU -> wide expansion, BN backward -> data gradients) -- at most one f32
+    rounding apart in the coefficients (the compiler may contract them differently)."""
+    M = N * H * W
+    c = (_r(N, H, W, K, seed=71, scale=2) + 0.5).to(BF).to(gpu)
+    r = (_r(N, H, W, K, seed=72, scale=1.5) - 0.25).to(BF).to(gpu)
+    cf, rf = c.float().reshape(M, K), r.float().reshape(M, K)
+    s, q, s2, q2 = cf.sum(0), (cf * cf).sum(0), rf.sum(0), (rf * rf).sum(0)
+    g1, b1 = (_r(K, seed=73) * 0.1 + 1).to(gpu), (_r(K, seed=74) * 0.1).to(gpu)
+    g2, b2 = (_r(K, seed=75) * 0.1 + 1).to(gpu), (_r(K, seed=76) * 0.1).to(gpu)
+    w = _r(Co, K, seed=77, scale=K ** -0.5).to(BF).to(gpu)
+    w_exp = _r(4 * Co, Co, seed=78, scale=Co ** -0.5).to(BF).to(gpu)
+    ys = (_r(N, H, W, Co, seed=82, scale=2) + 0.3).to(BF).to(gpu)
+    ysf = ys.float().reshape(M, Co)
+    ys_s, ys_q = ysf.sum(0), (ysf * ysf).sum(0)
+
+    def close(a, b, name):
+        bf = a.dtype == BF
+        a, b = a.float(), b.float()
+        d = (a - b).abs()
+        tol = (2 ** -7 * b.abs() + 1e-6) if bf else (1e-5 * b.abs().max() + 1e-7)
+        assert (d <= tol).all(), (name, d.max().item())
+
+    outs = {}
+    for fused in (True, False):
+        monkeypatch.setattr(cnn, "_BN_COEF_FUSED", fused)
+        res = {}
+        cs, cq = torch.zeros(Co, device=gpu), torch.zeros(Co, device=gpu)
+        rs = [torch.zeros(K, device=gpu), torch.ones(K, device=gpu),
+              torch.zeros(K, device=gpu), torch.ones(K, device=gpu)]
+        rb = (s2, q2, g2, b2, rs[2], rs[3]) if ds else None
+        o = cnn.bn_out_conv1x1(c, s, q, M, g1, b1, r, w, cs, cq, 1e-5, rs[0], rs[1], res_bn=rb)
+        res["out"] = list(o) + [cs, cq] + rs
+        # BN + ReLU of a Co-channel tensor inside the expansion (PRO 3), fixed inputs
+        ycs, ycq = torch.zeros(4 * Co, device=gpu), torch.zeros(4 * Co, device=gpu)
+        rm, rv = torch.zeros(Co, device=gpu), torch.ones(Co, device=gpu)
+        e = cnn.bn_relu_conv1x1(ys, ys_s, ys_q, M, g1[:Co].contiguous(), b1[:Co].contiguous(),
+                                w_exp, ycs, ycq, 1e-5, rm, rv)
+        res["exp"] = list(e) + [ycs, ycq, rm, rv]
+        # BN backward's apply inside the narrow data gradient of the K-output conv that
+        # produced c (PRO 2, with the fused BN reductions of that conv's Co-channel input)
+        de = (_r(N, H, W, K, seed=79)).to(BF).to(gpu)
+        m3, r3 = res["out"][2], res["out"][3]
+        dd = de.float().reshape(M, K)
+        sdy, sdx = dd.sum(0), (dd * (cf - m3) * r3).sum(0)
+        c2 = (_r(N, H, W, Co, seed=80, scale=2) + 0.5).to(BF).to(gpu)
+        c2f = c2.float().reshape(M, Co)
+        m2, r2 = cnn.bn_finalize(c2f.sum(0), (c2f * c2f).sum(0), M)
+        y2 = cnn.bn_apply(c2, m2, r2, g2[:Co].contiguous(), b2[:Co].contiguous(), None, relu=True)
+        w3 = _r(K, Co, seed=81, scale=Co ** -0.5).to(BF).to(gpu)
+        sd2, sx2 = torch.zeros(Co, device=gpu), torch.zeros(Co, device=gpu)
+        dx, dc = cnn.bn_in_conv1x1_dgrad(de, c, m3, r3, g1, sdy, sdx, w3,
+                                         (y2, c2, m2, r2, sd2, sx2))
+        res["bwd"] = [dx, dc, sd2, sx2]
+        outs[fused] = res
+    for key in ("out", "exp", "bwd"):
+        for i, (a, b) in enumerate(zip(outs[True][key], outs[False][key])):
+            close(a, b, "%s[%d]" % (key, i))
