@@ -11,6 +11,7 @@ void gemm_bf16_set_cfg(int);
 int gemm_bf16_set_pers(int);
 void attn_bwd_set_variant(int);
 void attn_set_swizzle(int);
+void attn_fwd_set_variant(int);
 void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const void*, int, void*,
                       int, float, float, const float*, int, const void*, void*, int, const void*,
                       int, int, int, int, long long, long long, long long,
@@ -21,7 +22,7 @@ long long conv_wgrad_ws_floats(int, int, int, int, int, int, int, int, int);
 long long conv_splitk_ws_floats(int, int, int, int, int, int, int, int, int, int);
 void conv_bf16_launch(int, int, int, int, int, int, int, int, int, int, const void*, const void*, int,
                       void*, float, const void*, float*, float*, int, hipStream_t, const void*,
-                      const void*, const float*, const float*, float*, long long);
+                      const void*, const float*, const float*, float*, long long, int);
 void bn_bwd_apply_launch(long long, int, const void*, const void*, const float*, const float*,
                          const float*, const float*, const float*, void*, hipStream_t);
 void bn_finalize_launch(int, long long, const float*, const float*, float, float*, float*, float*,
@@ -89,7 +90,7 @@ void maxpool_bwd_launch(int, int, int, int, const void*, const void*, void*, hip
 void avgpool_fwd_launch(int, int, int, const void*, void*, hipStream_t);
 void avgpool_bwd_launch(int, int, int, const void*, void*, hipStream_t);
 void sgd_momentum_mixed_launch(long long, float*, const float*, float*, void*, float, float, float,
-                               float, hipStream_t);
+                               float, hipStream_t, const long long*, int);
 void layernorm_fwd_launch(int, int, const void*, const float*, const float*, float, void*, float*,
                           float*, hipStream_t);
 void layernorm_bwd_launch(int, int, const void*, const void*, const float*, const float*,
@@ -125,6 +126,9 @@ void register_nn(py::module_& m) {
   m.def("attn_bwd_set_variant", &dtfx::attn_bwd_set_variant,
         "force the attention-backward kernel (-1 = environment; 0: 8 waves, 1: 4 waves, "
         "2: two query halves, two blocks per CU)");
+  m.def("attn_fwd_set_variant", &dtfx::attn_fwd_set_variant,
+        "attention forward: 1 = P in registers (attn_fwd_rp_kernel, default), 0 = P through "
+        "LDS (attn_fwd_kernel), -1 = from DTFX_ATTN_FWD");
   m.def("gemm_bf16_set_pers", &dtfx::gemm_bf16_set_pers,
         "1: plain 8-phase GEMMs with more 256x256 tiles than CUs run the persistent tile loop "
         "(opt-in, measured slower), 0: one block per tile (default); returns the previous "
@@ -230,18 +234,18 @@ void register_nn(py::module_& m) {
                         int pad, uintptr_t a, uintptr_t b, int ldw, uintptr_t out, float beta,
                         uintptr_t residual, uintptr_t colsum, uintptr_t colsq, int splitk,
                         uintptr_t s, uintptr_t relu_y, uintptr_t bn_x, uintptr_t bn_mean,
-                        uintptr_t bn_rstd, uintptr_t ws, long long ws_floats) {
+                        uintptr_t bn_rstd, uintptr_t ws, long long ws_floats, bool defer) {
     dtfx::conv_bf16_launch(mode, N, H, W, C, Cout, KH, KW, stride, pad, P<const void>(a),
                            P<const void>(b), ldw, P<void>(out), beta, P<const void>(residual),
                            P<float>(colsum), P<float>(colsq), splitk, S(s),
                            P<const void>(relu_y), P<const void>(bn_x), P<const float>(bn_mean),
-                           P<const float>(bn_rstd), P<float>(ws), ws_floats);
+                           P<const float>(bn_rstd), P<float>(ws), ws_floats, defer ? 1 : 0);
   }, py::arg("mode"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Cout"),
      py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("a"), py::arg("b"),
      py::arg("ldw"), py::arg("out"), py::arg("beta"), py::arg("residual"), py::arg("colsum"),
      py::arg("colsq"), py::arg("splitk"), py::arg("stream"), py::arg("relu_y") = 0,
      py::arg("bn_x") = 0, py::arg("bn_mean") = 0, py::arg("bn_rstd") = 0, py::arg("ws") = 0,
-     py::arg("ws_floats") = 0);
+     py::arg("ws_floats") = 0, py::arg("defer_reduce") = false);
   m.def("bn_bwd_apply", [](long long M, int C, uintptr_t de, uintptr_t x, uintptr_t mean,
                            uintptr_t rstd, uintptr_t g, uintptr_t sdy, uintptr_t sdyxh,
                            uintptr_t dx, uintptr_t s) {
@@ -448,10 +452,15 @@ void register_nn(py::module_& m) {
     dtfx::avgpool_bwd_launch(N, HW, C, P<const void>(dy), P<void>(dx), S(s));
   });
   m.def("sgd_momentum_mixed", [](long long n, uintptr_t p, uintptr_t g, uintptr_t v, uintptr_t pb,
-                                 float lr, float mu, float wd, float gscale, uintptr_t s) {
+                                 float lr, float mu, float wd, float gscale, uintptr_t s,
+                                 uintptr_t segs, int nseg) {
     dtfx::sgd_momentum_mixed_launch(n, P<float>(p), P<const float>(g), P<float>(v), P<void>(pb), lr,
-                                    mu, wd, gscale, S(s));
-  });
+                                    mu, wd, gscale, S(s), P<const long long>(segs), nseg);
+  }, py::arg("n"), py::arg("p"), py::arg("g"), py::arg("v"), py::arg("pb"), py::arg("lr"),
+     py::arg("mu"), py::arg("wd"), py::arg("gscale"), py::arg("s"), py::arg("segs") = 0,
+     py::arg("nseg") = 0,
+     "segs (int64 [nseg][5]: lo4, hi4, planes, plane stride in float4s, S): ranges whose "
+     "gradient is the sum of S split-K planes (conv_bf16 defer_reduce), summed here");
   m.def("flash_fwd", [](int Bn, int Sq, int nh, uintptr_t qkv, uintptr_t out, uintptr_t lse,
                         int ld_lse, uintptr_t kmask, float scale, uintptr_t s) {
     dtfx::flash_fwd_launch(Bn, Sq, nh, P<const void>(qkv), P<void>(out), P<float>(lse), ld_lse,

@@ -763,6 +763,79 @@ __global__ __launch_bounds__(256) void sgd_momentum_mixed_kernel(
   }
 }
 
+// The same momentum SGD with the weight gradients of some flat ranges ("segments") left as
+// split-K partial planes by their convolutions (conv_bf16 defer_reduce, one GPU): the planes are
+// summed here, in split order (the order splitk_reduce sums them), instead of by a reduce pass
+// per weight gradient that writes the gradient only for this kernel to read back (ResNet-50: 49
+// reduce launches per step).  Segment k (int64 x 5, sorted, disjoint): {lo4, hi4 (float4
+// indices into the flat buffer), planes (f32 pointer), plane stride in float4s, S}; a lane finds
+// its segment by binary search in LDS.  (As BERT's adam_mixed_segs_kernel.)
+constexpr int kSgdMaxSegs = 128;
+__global__ __launch_bounds__(256) void sgd_momentum_mixed_segs_kernel(
+    long long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ v,
+    unsigned short* __restrict__ pb, float lr, float mu, float wd, float gscale,
+    const long long* __restrict__ segs, int nseg) {
+  __shared__ long long s_lo[kSgdMaxSegs], s_hi[kSgdMaxSegs], s_pl[kSgdMaxSegs];
+  __shared__ const f32x4* s_w[kSgdMaxSegs];
+  __shared__ int s_S[kSgdMaxSegs];
+  for (int k = threadIdx.x; k < nseg; k += blockDim.x) {
+    s_lo[k] = segs[5 * k];
+    s_hi[k] = segs[5 * k + 1];
+    s_w[k] = (const f32x4*)segs[5 * k + 2];
+    s_pl[k] = segs[5 * k + 3];
+    s_S[k] = (int)segs[5 * k + 4];
+  }
+  __syncthreads();
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    int lo = 0, hi = nseg - 1, k = -1;  // last segment with lo <= i
+    while (lo <= hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_lo[mid] <= i) {
+        k = mid;
+        lo = mid + 1;
+      } else {
+        hi = mid - 1;
+      }
+    }
+    f32x4 gv;
+    if (k >= 0 && i < s_hi[k]) {
+      const f32x4* w = s_w[k] + (i - s_lo[k]);
+      const long long pl = s_pl[k];
+      const int S = s_S[k];
+      // four planes' loads in flight at a time, added in split order
+      gv = __builtin_nontemporal_load(w);
+      int q = 1;
+      for (; q + 3 < S; q += 4) {
+        const f32x4 a0 = __builtin_nontemporal_load(w + q * pl),
+                    a1 = __builtin_nontemporal_load(w + (q + 1) * pl),
+                    a2 = __builtin_nontemporal_load(w + (q + 2) * pl),
+                    a3 = __builtin_nontemporal_load(w + (q + 3) * pl);
+        gv += a0;
+        gv += a1;
+        gv += a2;
+        gv += a3;
+      }
+      for (; q < S; ++q) gv += __builtin_nontemporal_load(w + q * pl);
+    } else {
+      gv = ((const f32x4*)g)[i];
+    }
+    f32x4 pv = ((f32x4*)p)[i], vv = ((f32x4*)v)[i];
+    ushort4 o;
+    unsigned short* op = (unsigned short*)&o;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      vv[u] = mu * vv[u] + gv[u] * gscale + wd * pv[u];
+      pv[u] -= lr * vv[u];
+      op[u] = tobf(pv[u]);
+    }
+    __builtin_nontemporal_store(pv, (f32x4*)p + (i));
+    __builtin_nontemporal_store(vv, (f32x4*)v + (i));
+    if (pb) ((ushort4*)pb)[i] = o;
+  }
+}
+
 // Streaming BatchNorm kernels: each thread makes ONE pass with kEwU 16-B chunks in flight
 // (grid = chunks / (256 * kEwU)).  Measured at ResNet-50's largest activation (205M bf16):
 // bn_apply 165 -> 144 us (4.97 -> 5.71 TB/s), with residual 253 -> 211 us; the old fixed
@@ -986,8 +1059,17 @@ void avgpool_bwd_launch(int N, int HW, int C, const void* dy, void* dx, hipStrea
 }
 
 void sgd_momentum_mixed_launch(long long n, float* p, const float* g, float* v, void* pb, float lr,
-                               float mu, float wd, float gscale, hipStream_t st) {
+                               float mu, float wd, float gscale, hipStream_t st,
+                               const long long* segs, int nseg) {
   if (n % 4) throw std::runtime_error("sgd_momentum_mixed: n % 4 != 0");
+  if (nseg < 0 || nseg > kSgdMaxSegs || (nseg && !segs))
+    throw std::runtime_error("sgd_momentum_mixed: 0..128 segments with a table");
+  if (nseg) {
+    hipLaunchKernelGGL(sgd_momentum_mixed_segs_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, n,
+                       p, g, v, (unsigned short*)pb, lr, mu, wd, gscale, segs, nseg);
+    DTFX_HIP_CHECK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(sgd_momentum_mixed_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, n, p, g, v,
                      (unsigned short*)pb, lr, mu, wd, gscale);
   DTFX_HIP_CHECK(hipGetLastError());

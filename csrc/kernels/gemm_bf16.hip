@@ -1571,7 +1571,8 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
                       int pad, const void* a, const void* b, int ldw, void* out, float beta,
                       const void* residual, float* colsum, float* colsq, int splitk,
                       hipStream_t stream, const void* relu_y, const void* bn_x,
-                      const float* bn_mean, const float* bn_rstd, float* ws, long long ws_floats) {
+                      const float* bn_mean, const float* bn_rstd, float* ws, long long ws_floats,
+                      int defer_reduce) {
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   if (C % 8 || Cout % 8) throw std::runtime_error("conv_bf16: channel counts must be multiples of 8");
   if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) & 15)
@@ -1692,6 +1693,9 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
         DTFX_HIP_CHECK(hipMemset2DAsync(out, sizeof(float) * ldo, 0, sizeof(float) * Nn, M, stream));
     }
     const bool use_ws = splitk > 1 && splitk_ws_ok(ws, ws_floats, splitk, M, Nn, out, ldo);
+    if (defer_reduce && (!use_ws || ws_floats != (long long)splitk * M * Nn))
+      throw std::runtime_error("conv_bf16: defer_reduce needs the exact split-K workspace "
+                               "(conv_wgrad_ws_floats)");
     if (use_ws) e.ws = ws;
     static const bool plain1x1w = [] {  // DTFX_CONV1X1_WGRAD_GEMM=0: 1x1 wgrads on the gather path
       const char* v = getenv("DTFX_CONV1X1_WGRAD_GEMM");
@@ -1710,7 +1714,9 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
                                        (const unsigned short*)a, Cout, (const unsigned short*)b, 0,
                                        out, ldo, e, 0LL, 0LL, 0LL, d, stream);
     }
-    if (use_ws) splitk_reduce(M, Nn, splitk, ws, (float*)out, ldo, beta, stream);
+    // defer_reduce: the S partial planes [S][Cout][KH*KW*C] stay in ws for the optimizer to
+    // sum (sgd_momentum_mixed with segments: one GPU, nothing between the gradient and SGD)
+    if (use_ws && !defer_reduce) splitk_reduce(M, Nn, splitk, ws, (float*)out, ldo, beta, stream);
   } else {
     throw std::runtime_error("conv_bf16: mode must be 1 (fwd), 2 (dgrad) or 3 (wgrad)");
   }

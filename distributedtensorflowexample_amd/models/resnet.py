@@ -167,6 +167,9 @@ class ResNet50:
         self.wgrad_stream = None
         self.wgrad_sync_buckets = True
         self._keep = []  # operands the side stream still reads
+        self._fold = False   # enable_splitk_fold
+        self._planes = {}    # conv name -> its persistent split-K planes (0: not folded)
+        self._segs = None    # the optimizer's segment table (int64 [n][5])
 
     # conv + fused BN statistics (column sums in the conv epilogue)
     def _conv_bn(self, name, x):
@@ -376,16 +379,59 @@ class ResNet50:
         return (CN.bn_prologue_applies(c1, K, N, 2)
                 and not CN.hip().conv1x1_pro_applies(1, c1.numel() // K, K, N))
 
+    def enable_splitk_fold(self):
+        """Leave the split-K weight gradients as their partial planes and let momentum SGD sum
+        them (one GPU only: with data parallelism the bucket all-reduce needs the reduced
+        gradient).  Removes the reduce pass of every split weight-gradient launch (49 per
+        ResNet-50 step) -- it wrote the f32 gradient only for SGD to read it back.  The planes
+        are allocated at each conv's first backward (its shape is known then: the first,
+        eager step) and kept; ``p.grad`` no longer holds these gradients
+        (:meth:`materialize_grads` sums them there on demand)."""
+        if self.device.type != "cuda":
+            return False
+        self._fold = True
+        return True
+
+    def _fold_planes(self, name, x_in, cout, k, s, p):
+        if not self._fold:
+            return None
+        if name not in self._planes:
+            P = self.params
+            off, (rows, ldw) = P.offsets[name + ".weight"]
+            n = CN.wgrad_fold_planes(tuple(x_in.shape), cout, k, k, s, p, ldw)
+            self._planes[name] = None
+            if n > 0 and len([v for v in self._planes.values() if v is not None]) < 128:
+                S = n // (rows * ldw)
+                buf = torch.zeros(n, device=self.device)
+                self._planes[name] = (buf, off, rows * ldw, S)
+                rows_ = sorted((o // 4, (o + m) // 4, b.data_ptr(), m // 4, S_)
+                               for b, o, m, S_ in (v for v in self._planes.values() if v))
+                self._segs = torch.tensor(rows_, dtype=torch.int64, device=self.device)
+        v = self._planes[name]
+        return None if v is None else v[0]
+
+    def materialize_grads(self):
+        """Sum the folded split-K planes into ``params.grad`` (tests, debugging)."""
+        P = self.params
+        for name, v in self._planes.items():
+            if v is None:
+                continue
+            buf, off, m, S = v
+            P.grad[off:off + m] = buf.view(S, m).sum(0)
+        return P.grad
+
     def _wgrad_dgrad(self, name, dc, x_in, residual=None, need_dx=True, bn=None):
         P = self.params
         _, cin, cout, k, s, p = self.specs[name]
         ws = self.wgrad_stream
+        planes = self._fold_planes(name, x_in, cout, k, s, p)
         if ws is None:
-            CN.conv_wgrad(dc, x_in, P.G(name + ".weight"), k, k, s, p, beta=1.0)
+            CN.conv_wgrad(dc, x_in, P.G(name + ".weight"), k, k, s, p, beta=1.0, planes=planes)
         else:  # weight gradient beside the data gradient (operands kept alive until the join)
             ws.wait_stream(torch.cuda.current_stream(dc.device))
             with torch.cuda.stream(ws):
-                CN.conv_wgrad(dc, x_in, P.G(name + ".weight"), k, k, s, p, beta=1.0)
+                CN.conv_wgrad(dc, x_in, P.G(name + ".weight"), k, k, s, p, beta=1.0,
+                              planes=planes)
             self._keep.append((dc, x_in))
         if not need_dx:
             return None
@@ -473,7 +519,8 @@ class ResNet50:
 
     def sgd_step(self, lr, momentum=0.9, wd=5e-5, gscale=1.0):
         p = self.params
-        CN.sgd_momentum_mixed(p.master, p.grad, p.mom, p.bf, lr, momentum, wd, gscale)
+        CN.sgd_momentum_mixed(p.master, p.grad, p.mom, p.bf, lr, momentum, wd, gscale,
+                              segs=self._segs)
 
 
 def synthetic_imagenet(batch, device, size=224, seed=0, num_classes=NUM_CLASSES):

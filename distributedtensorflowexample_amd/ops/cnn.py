@@ -484,8 +484,23 @@ def stem_wgrad_bn_applies(x, Cout, k, stride, pad):
 _STEM_WGRAD_BN = os.environ.get("DTFX_STEM_WGRAD_BN", "1") != "0"
 
 
-def conv_wgrad(dy, x, dw, KH, KW, stride, pad, beta=1.0, bn_in=None):
+def wgrad_fold_planes(x_shape, Cout, KH, KW, stride, pad, ldw):
+    """How many f32 split-K planes conv_wgrad of this shape leaves behind with ``planes``
+    (0: the shape does not take the workspace path, or ``ldw`` pads the rows -- then it cannot
+    be folded into the optimizer)."""
+    N, H, W, C = x_shape
+    if (not _SPLITK_WS or ldw != KH * KW * C or hip().stem_conv_applies(H, W, C, Cout, KH, KW, stride, pad)
+            or hip().conv3x3_c64_applies(H, W, C, Cout, KH, KW, stride, pad)):
+        return 0
+    return int(hip().conv_wgrad_ws_floats(N, H, W, C, Cout, KH, KW, stride, pad))
+
+
+def conv_wgrad(dy, x, dw, KH, KW, stride, pad, beta=1.0, bn_in=None, planes=None):
     """dw[:, :KH*KW*C] (f32 [Cout, ldw]) (+)= dL/dW.
+
+    ``planes`` (GPU, :func:`wgrad_fold_planes` floats): the split-K partial planes are left
+    there and ``dw`` is not touched -- the optimizer sums them (``sgd_momentum_mixed`` with
+    segments; one GPU only: an all-reduce needs the reduced gradient).
 
     ``bn_in = (c, bcoef)`` (the ResNet stem only, see :func:`maxpool_bn_bwd`): ``dy`` is the
     gradient at the BatchNorm output behind this conv and the conv output gradient is formed
@@ -518,6 +533,12 @@ def conv_wgrad(dy, x, dw, KH, KW, stride, pad, beta=1.0, bn_in=None):
         # staged once per 4 x 28 tile, per-block partial gradient summed in registers)
         hip().conv3x3_c64_wgrad(N, H, W, ptr(x), ptr(dy), ptr(dw), dw.stride(0), float(beta),
                                 stream_handle())
+        return dw
+    if planes is not None:
+        nws = planes.numel()
+        hip().conv_bf16(3, N, H, W, C, Cout, KH, KW, stride, pad, ptr(dy), ptr(x), dw.stride(0),
+                        ptr(dw), float(beta), 0, 0, 0, 0, stream_handle(), ws=ptr(planes),
+                        ws_floats=nws, defer_reduce=True)
         return dw
     # split-K partials through a workspace + one reduce pass instead of f32 atomics
     nws = hip().conv_wgrad_ws_floats(N, H, W, C, Cout, KH, KW, stride, pad) if _SPLITK_WS else 0
@@ -732,7 +753,14 @@ def avgpool_bwd(dy, x_shape):
     return dx
 
 
-def sgd_momentum_mixed(p, g, v, pb, lr, momentum=0.9, wd=0.0, gscale=1.0):
+def sgd_momentum_mixed(p, g, v, pb, lr, momentum=0.9, wd=0.0, gscale=1.0, segs=None):
+    """Momentum SGD on the f32 master (bf16 copy refreshed).  ``segs`` (GPU): int64 [n][5]
+    table of ranges whose gradient is the sum of split-K planes (see conv_wgrad ``planes``)."""
+    if segs is not None and p.is_cuda:
+        hip().sgd_momentum_mixed(p.numel(), ptr(p), ptr(g), ptr(v), ptr(pb), float(lr),
+                                 float(momentum), float(wd), float(gscale), stream_handle(),
+                                 segs=ptr(segs), nseg=int(segs.shape[0]))
+        return
     if not p.is_cuda:
         v.mul_(momentum).add_(g * gscale + wd * p)
         p.sub_(lr * v)

@@ -64,6 +64,10 @@ class ResNetTrainer:
         if self.device.type == "cuda" and os.environ.get("DTFX_RESNET_WSTREAM", "0") == "1":
             self.model.wgrad_stream = torch.cuda.Stream(self.device)
             self.model.wgrad_sync_buckets = self.world > 1
+        if (self.device.type == "cuda" and self.world == 1
+                and os.environ.get("DTFX_RESNET_FOLD", "1") != "0"):
+            # one GPU: SGD sums the split-K weight-gradient planes itself (no reduce launches)
+            self.model.enable_splitk_fold()
         self.data = synthetic_imagenet(batch, device, image_size, seed=data_seed,
                                        num_classes=num_classes)
         self.graph = None
