@@ -705,6 +705,132 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   }
 }
 
+// Register-resident P (round 6): the scores are formed TRANSPOSED,
+// S^T = K Q^T (the same two fragments as Q K^T with the MFMA operands swapped), so each lane's
+// accumulators hold four consecutive keys of ONE query -- exactly the k-slots of the P . V
+// A operand once the two 16-key tiles of a 32-key chunk are paired: lane (query q, group g)
+// holds keys 32c + 4g + {0..3} (tile 2c) and 32c + 16 + 4g + {0..3} (tile 2c + 1) as its 8
+// k-slots.  The V fragment of P . V reads the same key order with two transposed LDS reads at
+// rows 32c + 4g and 32c + 16 + 4g.  P never touches LDS: K + V + the key mask are 36.5 KB,
+// four blocks per CU instead of two (attn_fwd_kernel's P image took 34 KB), and the K image
+// stages the output once every wave is past its scores.  Softmax over a query's keys: in-lane
+// over 32 values, then across the 4 lanes of its column (xor 16, 32).
+__global__ __launch_bounds__(256, 4) void attn_fwd_rp_kernel(
+    int S, int nh, const unsigned short* __restrict__ qkv, unsigned short* __restrict__ out,
+    float* __restrict__ lse, const float* __restrict__ kmask, float scale) {
+  using namespace at;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* Ks = sm;
+  char* Vs = sm + QB;
+  float* kms = (float*)(sm + 2 * QB);  // [SP] additive key mask, -inf past S
+  const int b = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int Hd = nh * D, ld = 3 * Hd;
+  const unsigned short* base = qkv + (size_t)b * S * ld + h * D;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int cl = lane & 15, g = lane >> 4;
+  bf16x8 qf[2][2];  // [row tile i][k half]: B operand of S^T, query 32 wave + 16 i + cl
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 32 * wave + 16 * i + cl;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      qf[i][kk] = *(const bf16x8*)(base + (size_t)(row < S ? row : S - 1) * ld + 32 * kk + 8 * g);
+      if (row >= S) qf[i][kk] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  {
+    char* const dst[2] = {Ks, Vs};
+    const unsigned short* const src[2] = {base + Hd, base + 2 * Hd};
+    const int lds[2] = {ld, ld};
+    at::load_heads<2, 256, false>(dst, src, lds, S);
+  }
+  if (threadIdx.x < SP) {
+    const int k = threadIdx.x;
+    kms[k] = k < S ? (kmask ? kmask[(size_t)b * S + k] : 0.f) : -INFINITY;
+  }
+  __syncthreads();
+  bf16x8 pf[2][4];  // P of row tile i: A fragments of the four 32-key chunks
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    f32x4 acc[8];  // acc[j][r] = score(query 32 wave + 16 i + cl, key 16 j + 4 g + r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = mma(lfrag<true>(Ks, LDQ, 16 * j, 32 * kk, lane), qf[i][kk], acc[j]);
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 km = *(const f32x4*)&kms[16 * j + 4 * g];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc[j][r] = acc[j][r] * scale + km[r];
+        m = fmaxf(m, acc[j][r]);
+      }
+    }
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    const float msafe = (m == -INFINITY) ? 0.f : m;
+    float l = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc[j][r] = __expf(acc[j][r] - msafe);
+        l += acc[j][r];
+      }
+    l += __shfl_xor(l, 16);
+    l += __shfl_xor(l, 32);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pf[i][c][r] = (short)tobf(acc[2 * c][r] * inv);
+        pf[i][c][4 + r] = (short)tobf(acc[2 * c + 1][r] * inv);
+      }
+    const int row = 32 * wave + 16 * i + cl;
+    if (g == 0 && row < S) lse[((size_t)b * nh + h) * SP + row] = msafe + __logf(l);
+  }
+  __syncthreads();  // every wave is past its scores: the K image becomes the output staging
+  // the V fragment of chunk c, columns o0 .. o0 + 15: k-slots e < 4 -> key 32c + 4g + e, e >= 4
+  // -> key 32c + 16 + 4g + e - 4 (the P fragment's key order)
+  const int q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    f32x4 o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const char* a = Vs + (32 * c + 4 * g + q) * LDQ + (16 * j + p4) * 2;
+        bf16x8 vf;
+        vf.lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)a);
+        vf.hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(a + 16 * LDQ));
+        o[j] = mma(pf[i][c], vf, o[j]);
+      }
+    // o[j][r] = O(query 32 wave + 16 i + 4 g + r, d 16 j + cl): staged in the wave's own 16
+    // rows of the K image, then 16-B stores
+    const int r0 = 32 * wave + 16 * i;
+    char* stg = Ks + (size_t)r0 * LDQ;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *(unsigned short*)(stg + (4 * g + r) * LDQ + (16 * j + cl) * 2) = tobf(o[j][r]);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = lane + 64 * u, row = r0 + (c >> 3), ch = c & 7;
+      const bf16x8 v = *(const bf16x8*)(stg + (c >> 3) * LDQ + ch * 16);
+      if (row < S) *(bf16x8*)(out + ((size_t)b * S + row) * Hd + h * D + ch * 8) = v;
+    }
+  }
+}
+
 // NW waves per (sequence, head): 4 (32 query / key rows per wave) or 8 (16 rows per wave:
 // the 144 KB of LDS allow one block per CU, so 8 waves give every SIMD two waves to
 // overlap LDS / global latency with the other's MFMAs).
@@ -1656,11 +1782,36 @@ static void attn_fwd_launch_t(int Bn, int S, int nh, const void* qkv, void* out,
                      (const unsigned short*)qkv, (unsigned short*)out, lse, kmask, scale);
 }
 
+// Attention forward: -1 = from DTFX_ATTN_FWD (default 1), 1: attn_fwd_rp_kernel (P in
+// registers), 0: attn_fwd_kernel (P through LDS; DTFX_ATTN_SWZ picks its swizzled variant)
+static int g_attn_fwd = -1;
+void attn_fwd_set_variant(int v) { g_attn_fwd = v; }
+static bool attn_fwd_rp() {
+  if (g_attn_fwd < 0) {
+    const char* e = getenv("DTFX_ATTN_FWD");
+    g_attn_fwd = e && atoi(e) == 0 ? 0 : 1;
+  }
+  return g_attn_fwd == 1;
+}
+
 void attn_fwd_launch(int Bn, int S, int nh, const void* qkv, void* out, float* lse,
                      const float* kmask, float scale, hipStream_t s) {
   check_attn(S, nh);
-  if (attn_swz()) attn_fwd_launch_t<true>(Bn, S, nh, qkv, out, lse, kmask, scale, s);
-  else attn_fwd_launch_t<false>(Bn, S, nh, qkv, out, lse, kmask, scale, s);
+  if (attn_fwd_rp()) {
+    constexpr size_t lds = 2 * (size_t)at::QB + (size_t)at::SP * 4;
+    static bool attr = false;
+    if (!attr) {
+      DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_rp_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      attr = true;
+    }
+    hipLaunchKernelGGL(attn_fwd_rp_kernel, dim3(Bn * nh), dim3(256), lds, s, S, nh,
+                       (const unsigned short*)qkv, (unsigned short*)out, lse, kmask, scale);
+  } else if (attn_swz()) {
+    attn_fwd_launch_t<true>(Bn, S, nh, qkv, out, lse, kmask, scale, s);
+  } else {
+    attn_fwd_launch_t<false>(Bn, S, nh, qkv, out, lse, kmask, scale, s);
+  }
   DTFX_HIP_CHECK(hipGetLastError());
 }
 

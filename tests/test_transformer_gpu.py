@@ -55,9 +55,11 @@ def test_embedding_fwd_bwd(gpu, B):
         assert torch.allclose(a.cpu(), b, atol=1e-3)
 
 
-# 3 / 4: persistent (4: 3 blocks, 4 pairs each); 5: the two-halves kernel and the forward with
-# the XOR-swizzled LDS images (opt-in DTFX_ATTN_SWZ=1)
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+# 3 / 4: persistent (4: 3 blocks, 4 pairs each); 5: the two-halves kernel and the P-through-LDS
+# forward with the XOR-swizzled LDS images (opt-in DTFX_ATTN_SWZ=1); 6: the two-halves kernel
+# and the P-through-LDS forward (DTFX_ATTN_FWD=0).  Variants 0-4 run the default forward with P
+# in registers (attn_fwd_rp_kernel).
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("S,masked", [(128, False), (128, True), (77, True), (64, False), (33, True)])
 def test_attention_fwd_bwd(gpu, S, masked, variant):
     B, nh = 3, 4
@@ -68,18 +70,20 @@ def test_attention_fwd_bwd(gpu, S, masked, variant):
         kmask = torch.where(torch.arange(S)[None, :] < valid[:, None], 0.0, -10000.0)
     hip = _ext.hip()
     hip.attn_set_swizzle(1 if variant == 5 else 0)
+    hip.attn_fwd_set_variant(0 if variant >= 5 else 1)
     try:
         o, lse = T.attn_fwd(qkv.to(gpu), B, S, nh, kmask.to(gpu) if masked else None)
         orf, lser = T.attn_fwd(qkv, B, S, nh, kmask)
         assert (o.cpu().float() - orf.float()).abs().max() < 2e-2
         assert (lse.cpu().view(B, nh, -1)[..., :S] - lser.view(B, nh, -1)[..., :S]).abs().max() < 1e-3
         dout = _r(B * S, nh * 64, seed=11).to(BF)
-        hip.attn_bwd_set_variant(2 if variant == 5 else variant)
+        hip.attn_bwd_set_variant(2 if variant >= 5 else variant)
         dq = T.attn_bwd(qkv.to(gpu), o, dout.to(gpu), lse, B, S, nh, kmask.to(gpu) if masked else None)
         torch.cuda.synchronize()
     finally:
         hip.attn_bwd_set_variant(-1)
         hip.attn_set_swizzle(-1)
+        hip.attn_fwd_set_variant(-1)
     dqr = T.attn_bwd(qkv, o.cpu(), dout, lse.cpu(), B, S, nh, kmask)
     err = (dq.cpu().float() - dqr.float()).abs().max().item()
     assert err < 3e-2 * max(1.0, dqr.float().abs().max().item()), err
@@ -163,3 +167,29 @@ def test_flash_attention_fwd_bwd(gpu, monkeypatch, S, masked, force):
     err = (dq.cpu().float() - dqr.float()).abs().max().item()
     assert err < 3e-2 * max(1.0, dqr.float().abs().max().item()), err
     assert torch.allclose(db.cpu(), dbr, atol=0.2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("S", [128, 77])
+def test_attention_fwd_register_p_matches_lds_p(gpu, S):
+    """The forward with P in registers (attn_fwd_rp_kernel: scores formed transposed, P . V's A
+    operand straight from the accumulators) against the P-through-LDS kernel on the same
+    inputs: outputs within two bf16 roundings (the scores' MFMA operands are swapped and P . V
+    sums its keys in another order, so a P element can round the other way), log-sum-exp
+    within f32 rounding."""
+    B, nh = 8, 12
+    qkv = (_r(B * S, 3 * nh * 64, seed=20) * 2).to(BF).to(gpu)
+    valid = torch.randint(S // 2, S + 1, (B,), generator=torch.Generator().manual_seed(3))
+    kmask = torch.where(torch.arange(S)[None, :] < valid[:, None], 0.0, -10000.0).to(gpu)
+    hip = _ext.hip()
+    res = []
+    try:
+        for v in (1, 0):
+            hip.attn_fwd_set_variant(v)
+            res.append(T.attn_fwd(qkv, B, S, nh, kmask))
+    finally:
+        hip.attn_fwd_set_variant(-1)
+    (o1, l1), (o0, l0) = res
+    d = (o1.float() - o0.float()).abs()
+    assert (d <= 2 ** -6 * o0.float().abs() + 4e-3).all(), d.max().item()
+    l1v, l0v = l1.view(B, nh, -1)[..., :S], l0.view(B, nh, -1)[..., :S]
+    assert (l1v - l0v).abs().max().item() < 1e-4
