@@ -12,6 +12,7 @@ int gemm_bf16_set_pers(int);
 void attn_bwd_set_variant(int);
 void attn_set_swizzle(int);
 void attn_fwd_set_variant(int);
+void transpose_bf16_batch_launch(const long long*, int, int, hipStream_t);
 void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const void*, int, void*,
                       int, float, float, const float*, int, const void*, void*, int, const void*,
                       int, int, int, int, long long, long long, long long,
@@ -334,6 +335,10 @@ void register_nn(py::module_& m) {
                          P<const float>(mean), P<const float>(rstd), P<float>(ps), P<float>(pq),
                          P<void>(wt), S(s));
   });
+  m.def("transpose_bf16_batch", [](uintptr_t tab, int n, int tiles, uintptr_t s) {
+    dtfx::transpose_bf16_batch_launch(P<const long long>(tab), n, tiles, S(s));
+  }, "n bf16 transposes in one launch: int64 table [n][6] {src, dst, rows, cols, ld_src, first "
+     "32x32 tile}; a 1x1 dgrad given w = 0 reads such a copy from wt");
   m.def("conv1x1_pro_applies", &dtfx::conv1x1_pro_applies,
         "(mode, M, K, N): a 1x1 kernel with the BatchNorm prologue takes this product");
   m.def("conv1x1_pro", [](int mode, int M, int K, int N, uintptr_t s0, uintptr_t s1, uintptr_t coef,

@@ -710,6 +710,40 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(int rows, int cols,
   }
 }
 
+// Many transposes in one launch (ResNet-50: the 1x1 convolutions' data gradients read their
+// weights transposed, 20 per step, each a ~5 us launch of its own): entry k of the int64 table
+// [n][6] = {src, dst, rows, cols, ld_src, first tile}; block b runs 32 x 32 tile b - first of the
+// entry whose tile range holds it (binary search), as transpose_bf16_kernel.
+__global__ __launch_bounds__(256) void transpose_bf16_batch_kernel(const long long* __restrict__ tab,
+                                                                  int n) {
+  __shared__ unsigned short t[32][33];
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1, k = 0;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    if (tab[6 * mid + 5] <= b) {
+      k = mid;
+      lo = mid + 1;
+    } else {
+      hi = mid - 1;
+    }
+  }
+  const unsigned short* src = (const unsigned short*)tab[6 * k];
+  unsigned short* dst = (unsigned short*)tab[6 * k + 1];
+  const int rows = (int)tab[6 * k + 2], cols = (int)tab[6 * k + 3], ld_src = (int)tab[6 * k + 4];
+  const int tl = b - (int)tab[6 * k + 5], tx_n = (cols + 31) / 32;
+  const int r0 = (tl / tx_n) * 32, c0 = (tl % tx_n) * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    t[i][tx] = r < rows && c < cols ? src[(size_t)r * ld_src + c] : 0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < cols && r < rows) dst[(size_t)c * rows + r] = t[tx][i];
+  }
+}
+
 }  // namespace pw
 
 static bool conv1x1_narrow(int K, int N) {
@@ -854,8 +888,9 @@ void conv1x1_launch(int mode, int M, int K, int N, const void* x, const void* w,
     const void* wv = w;
     if (mode == 2) {
       if (!wt || ((uintptr_t)wt & 15)) throw std::runtime_error("conv1x1 dgrad: 16-B aligned wt workspace");
-      hipLaunchKernelGGL(transpose_bf16_kernel, dim3((N + 31) / 32, K / 32), dim3(256), 0, s, K, N,
-                         (const unsigned short*)w, ldw, (unsigned short*)wt);
+      if (w)  // (w null: wt already holds the transposed copy, transpose_bf16_batch_launch)
+        hipLaunchKernelGGL(transpose_bf16_kernel, dim3((N + 31) / 32, K / 32), dim3(256), 0, s, K, N,
+                           (const unsigned short*)w, ldw, (unsigned short*)wt);
       wv = wt;
     }
 #define DTFX_PW_NARROW(KV, NV)                                                                  \
@@ -877,8 +912,9 @@ void conv1x1_launch(int mode, int M, int K, int N, const void* x, const void* w,
     else conv1x1_fwd_go<256>(grid, M, N, x, w, ldw, y, ps, pq, s);
   } else if (mode == 2) {
     if (!wt || ((uintptr_t)wt & 15)) throw std::runtime_error("conv1x1 dgrad: 16-B aligned wt workspace");
-    hipLaunchKernelGGL(transpose_bf16_kernel, dim3(N / 32, K / 32), dim3(256), 0, s, K, N,
-                       (const unsigned short*)w, ldw, (unsigned short*)wt);
+    if (w)  // (w null: wt already holds the transposed copy)
+      hipLaunchKernelGGL(transpose_bf16_kernel, dim3(N / 32, K / 32), dim3(256), 0, s, K, N,
+                         (const unsigned short*)w, ldw, (unsigned short*)wt);
     w = wt;
     if (K == 64) conv1x1_dgrad_pick<64>(grid, M, N, x, w, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s);
     else if (K == 128) conv1x1_dgrad_pick<128>(grid, M, N, x, w, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq, s);
@@ -941,8 +977,9 @@ void conv1x1_pro_launch(int mode, int M, int K, int N, const void* s0, const voi
     throw std::runtime_error("conv1x1_pro: ldw % 8, 16-B aligned tensors");
   const void* wv = w;
   if (mode == 2) {
-    hipLaunchKernelGGL(transpose_bf16_kernel, dim3((N + 31) / 32, K / 32), dim3(256), 0, s, K, N,
-                       (const unsigned short*)w, ldw, (unsigned short*)wt);
+    if (w)  // (w null: wt already holds the transposed copy)
+      hipLaunchKernelGGL(transpose_bf16_kernel, dim3((N + 31) / 32, K / 32), dim3(256), 0, s, K, N,
+                         (const unsigned short*)w, ldw, (unsigned short*)wt);
     wv = wt;
   }
   if (narrow) {
@@ -1035,6 +1072,14 @@ void conv1x1_pro_bwdbn_launch(int M, int K, int N, const void* s0, const void* s
   cs.inv_m = 1.f / (float)Mst;
   conv1x1_pro_launch(2, M, K, N, s0, s1, cs, xo, w, ldw, y, res, relu_y, bn_x, mean, rstd, ps, pq,
                      wt, s, res_h, res_w);
+}
+
+// tab: int64 [n][6] on the device (transpose_bf16_batch_kernel); tiles: the sum of every
+// entry's ceil(rows / 32) * ceil(cols / 32)
+void transpose_bf16_batch_launch(const long long* tab, int n, int tiles, hipStream_t s) {
+  if (n <= 0 || tiles <= 0 || !tab) throw std::runtime_error("transpose_bf16_batch: empty table");
+  hipLaunchKernelGGL(pw::transpose_bf16_batch_kernel, dim3(tiles), dim3(256), 0, s, tab, n);
+  DTFX_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace dtfx

@@ -41,6 +41,9 @@ ALIGN = 64
 _STEM_POOL_BN = os.environ.get("DTFX_STEM_POOL_BN", "1") != "0"
 _DS_PRO = os.environ.get("DTFX_DS_PROLOGUE", "1") != "0"  # stride-1 downsample BN apply in its dgrad
 _DS_COMPACT = os.environ.get("DTFX_DS_COMPACT", "1") != "0"  # stride-2 downsample dgrad kept compact
+# the 1x1 data gradients' transposed weights from one batched launch per step
+# (DTFX_RESNET_WT_BATCH=0: each dgrad transposes its own)
+_WT_BATCH = os.environ.get("DTFX_RESNET_WT_BATCH", "1") != "0"
 STAGES = [(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)]  # (width, blocks, stride)
 IN_CH = 8          # 3 image channels + 5 zero channels
 NUM_CLASSES = 1000
@@ -167,6 +170,8 @@ class ResNet50:
         self.wgrad_stream = None
         self.wgrad_sync_buckets = True
         self._keep = []  # operands the side stream still reads
+        self._wt = {}        # 1x1 conv name -> its persistent transposed bf16 weight copy
+        self._wt_tab = None  # (int64 table, n, tiles) of the per-step batched transpose
         self._fold = False   # enable_splitk_fold
         self._planes = {}    # conv name -> its persistent split-K planes (0: not folded)
         self._segs = None    # the optimizer's segment table (int64 [n][5])
@@ -248,6 +253,7 @@ class ResNet50:
         loss = loss_rows.sum() / N
         acc = correct.sum() / N
         # ---------------- backward
+        self._transpose_weights()  # the 1x1 data gradients' transposed weights, one launch
         B16.gemm(dlog, pooled, True, False, out=P.G("fc.weight"), beta=1.0)
         B16.colsum(dlog, out=P.G("fc.bias"), beta=1.0)
         dpool = B16.gemm(dlog, P.W("fc.weight"))
@@ -410,6 +416,36 @@ class ResNet50:
         v = self._planes[name]
         return None if v is None else v[0]
 
+    def _wt_for(self, name):
+        """The 1x1 conv's transposed weights for its data gradient, formed by the one batched
+        transpose at the start of the backward (``None`` the first time a conv asks: it is
+        registered then and its own launch transposes this once)."""
+        if self.device.type != "cuda" or not _WT_BATCH:
+            return None
+        if name in self._wt:
+            return self._wt[name]
+        P = self.params
+        w = P.W(name + ".weight")
+        cout, cin = self.specs[name][2], self.specs[name][1]
+        buf = torch.empty(cin, cout, device=self.device, dtype=w.dtype)
+        self._wt[name] = buf
+        rows, tiles = [], 0
+        for n_, b in self._wt.items():
+            src = P.W(n_ + ".weight")
+            r, c = self.specs[n_][2], self.specs[n_][1]
+            rows.append((src.data_ptr(), b.data_ptr(), r, c, src.stride(0), tiles))
+            tiles += ((r + 31) // 32) * ((c + 31) // 32)
+        self._wt_tab = (torch.tensor(rows, dtype=torch.int64, device=self.device), len(rows),
+                        tiles)
+        return None
+
+    def _transpose_weights(self):
+        """Start of the backward: every registered 1x1 weight transposed in ONE launch (the bf16
+        working copy is final for this step)."""
+        if self._wt_tab is not None:  # (the convs registered so far; a new one transposes itself)
+            tab, n, tiles = self._wt_tab
+            CN.hip().transpose_bf16_batch(tab.data_ptr(), n, tiles, CN.stream_handle())
+
     def materialize_grads(self):
         """Sum the folded split-K planes into ``params.grad`` (tests, debugging)."""
         P = self.params
@@ -435,8 +471,9 @@ class ResNet50:
             self._keep.append((dc, x_in))
         if not need_dx:
             return None
+        wt = self._wt_for(name) if k == 1 and s == 1 and p == 0 else None
         return CN.conv_dgrad(dc, P.W(name + ".weight"), x_in.shape, k, k, s, p, residual=residual,
-                             bn=bn)
+                             bn=bn, wt=wt)
 
     def _block_bwd(self, pre, dout, x_in, c1, m1, r1, a1, c2, m2, r2, a2, c3, m3, r3, ds, out,
                    dout_is_de=False, fuse_prev=None):
@@ -468,7 +505,7 @@ class ResNet50:
                 self._bn_bwd(nd, dres, None, cs_, ms, rs, relu=False, apply=False)
                 dshort, dcs = CN.bn_in_conv1x1_dgrad(dres, cs_, ms, rs, P.P(nd + ".bn.gamma"),
                                                      P.G(nd + ".bn.beta"), P.G(nd + ".bn.gamma"),
-                                                     P.W(nd + ".weight"))
+                                                     P.W(nd + ".weight"), wt=self._wt_for(nd))
                 self._wgrad_dgrad(nd, dcs, x_in, need_dx=False)
             elif (_DS_COMPACT and self.specs[nd][4] == 2 and self._conv1_pro_wide(pre, c1, x_in)
                   and x_in.shape[1] % 2 == 0 and x_in.shape[2] % 2 == 0
@@ -494,7 +531,7 @@ class ResNet50:
         if pro:
             de2, dc3 = CN.bn_in_conv1x1_dgrad(dout, c3, m3, r3, P.P(n3 + ".bn.gamma"),
                                               P.G(n3 + ".bn.beta"), P.G(n3 + ".bn.gamma"),
-                                              P.W(n3 + ".weight"), bn2)
+                                              P.W(n3 + ".weight"), bn2, wt=self._wt_for(n3))
             self._wgrad_dgrad(n3, dc3, a2, need_dx=False)
         else:
             de2 = self._wgrad_dgrad(n3, dc3, a2, bn=bn2)
@@ -510,7 +547,7 @@ class ResNet50:
             dx, dc1 = CN.bn_in_conv1x1_dgrad(de1, c1, m1, r1, P.P(n1 + ".bn.gamma"),
                                              P.G(n1 + ".bn.beta"), P.G(n1 + ".bn.gamma"),
                                              P.W(n1 + ".weight"), bn, residual=dshort,
-                                             residual_s2=short_s2)
+                                             residual_s2=short_s2, wt=self._wt_for(n1))
             self._wgrad_dgrad(n1, dc1, x_in, need_dx=False)
             return dx
         assert not short_s2

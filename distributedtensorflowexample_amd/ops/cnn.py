@@ -136,7 +136,7 @@ def conv_fwd(x, w, KH, KW, stride, pad, colsum=None, colsq=None, residual=None):
     return y
 
 
-def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
+def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None, wt=None):
     """dx = conv^T(dy, w) (+ residual), NHWC bf16.
 
     ``bn = (y, x, mean, rstd, sum_dy, sum_dyxh)``: the input of this conv is
@@ -199,16 +199,22 @@ def conv_dgrad(dy, w, x_shape, KH, KW, stride, pad, residual=None, bn=None):
         # and conv3's (256 / 512 -> 64 / 128): the streaming 1x1 kernels, ReLU mask and BN
         # reductions fused
         M = N * H * W
-        wt = torch.empty(C, Cout, device=dy.device, dtype=BF16)  # transposed weights
+        # transposed weights: formed here, or (``wt`` given) already there -- ResNet50 forms
+        # every 1x1 data gradient's copy in one batched launch per step (w passed as 0)
+        wp = ptr(w)
+        if wt is None:
+            wt = torch.empty(C, Cout, device=dy.device, dtype=BF16)
+        else:
+            wp = 0
         if bn is None:
-            hip().conv1x1(2, M, Cout, C, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(residual), 0,
+            hip().conv1x1(2, M, Cout, C, ptr(dy), wp, w.stride(0), ptr(dx), ptr(residual), 0,
                           0, 0, 0, 0, 0, ptr(wt), stream_handle())
             return dx
         y, x, mean, rstd, sdy, sdx = bn
         if y.shape != dx.shape or x.shape != dx.shape:
             raise ValueError("fused BN backward: y and x must have the dgrad output's shape")
         part = torch.empty(2, hip().conv1x1_rows(2, M, Cout, C), C, device=dy.device)
-        hip().conv1x1(2, M, Cout, C, ptr(dy), ptr(w), w.stride(0), ptr(dx), ptr(residual), ptr(y),
+        hip().conv1x1(2, M, Cout, C, ptr(dy), wp, w.stride(0), ptr(dx), ptr(residual), ptr(y),
                       ptr(x), ptr(mean), ptr(rstd), ptr(part[0]), ptr(part[1]), ptr(wt),
                       stream_handle())
         hip().colpart_reduce(part.shape[1], C, ptr(part[0]), ptr(part[1]), ptr(sdy), ptr(sdx),
@@ -409,7 +415,7 @@ def bn_relu_conv3x3(c, s, q, M, gamma, beta, w, colsum, colsq, eps=1e-5, run_mea
 
 
 def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, want_dc=True,
-                        residual=None, residual_s2=False):
+                        residual=None, residual_s2=False, wt=None):
     """BatchNorm backward's apply half and the data gradient of the 1x1 conv that produced the
     BatchNorm's input, in one pass.
 
@@ -446,7 +452,11 @@ def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, 
                           ptr(coef), stream_handle())
     dc = torch.empty_like(c) if want_dc else None
     dx = torch.empty(*c.shape[:-1], Cin, device=dev, dtype=BF16)
-    wt = torch.empty(Cin, K, device=dev, dtype=BF16)
+    wp = ptr(w)  # (wt given: the transposed copy is already there, see conv_dgrad)
+    if wt is None:
+        wt = torch.empty(Cin, K, device=dev, dtype=BF16)
+    else:
+        wp = 0
     y = x = bmean = brstd = sdy = sdx = part = None
     if bn is not None:
         y, x, bmean, brstd, sdy, sdx = bn
@@ -456,13 +466,13 @@ def bn_in_conv1x1_dgrad(de, c, mean, rstd, gamma, sum_dy, sum_dyxh, w, bn=None, 
     rh, rw = (c.shape[1], c.shape[2]) if residual is not None and residual_s2 else (0, 0)
     if coef is None:
         hip().conv1x1_pro_bwdbn(M, K, Cin, ptr(de), ptr(c), M, ptr(mean), ptr(rstd), ptr(gamma),
-                                ptr(sum_dy), ptr(sum_dyxh), ptr(dc), ptr(w), w.stride(0),
+                                ptr(sum_dy), ptr(sum_dyxh), ptr(dc), wp, w.stride(0),
                                 ptr(dx), ptr(residual), ptr(y), ptr(x), ptr(bmean), ptr(brstd),
                                 ptr(None if part is None else part[0]),
                                 ptr(None if part is None else part[1]), ptr(wt),
                                 stream_handle(), res_h=rh, res_w=rw)
     else:
-        hip().conv1x1_pro(2, M, K, Cin, ptr(de), ptr(c), ptr(coef), ptr(dc), ptr(w), w.stride(0),
+        hip().conv1x1_pro(2, M, K, Cin, ptr(de), ptr(c), ptr(coef), ptr(dc), wp, w.stride(0),
                           ptr(dx), ptr(residual), ptr(y), ptr(x), ptr(bmean), ptr(brstd),
                           ptr(None if part is None else part[0]),
                           ptr(None if part is None else part[1]), ptr(wt), stream_handle(),

@@ -195,7 +195,21 @@ DTFX_GEMM_TA8=1 timeout -k 10 300 python tools/gemm_cfg_ab.py --cfgs 0,1,2,5 --r
 cut -c 1-220 $OUT/gemm_wgrad.jsonl
 }
 
+exp_resnet_wt() {
+# Round 6: the 1x1 data gradients' transposed weights formed by ONE batched launch per step
+# (ResNet50._transpose_weights) instead of one transpose launch per dgrad -- tests, then
+# ResNet-50 end to end against the previous tree state (DTFX_RESNET_WT_BATCH=0), interleaved.
+cd "$ROOT"; OUT=gpurun_out/r6wt; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
+  tests/test_resnet_gpu.py tests/test_cnn_gpu.py > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
+for r in 1 2 3; do for v in 1 0; do
+  DTFX_RESNET_WT_BATCH=$v timeout -k 10 300 python bench.py --model resnet50 > $OUT/resnet_wt${v}_$r.json 2>&1 || { tail -5 $OUT/resnet_wt${v}_$r.json; exit 1; }
+  echo "resnet wt_batch=$v $r $(tail -1 $OUT/resnet_wt${v}_$r.json | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+done; done
+}
+
 case "${1:-}" in
-  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz) exp_"$1" ;;
-  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz}" >&2; exit 2 ;;
+  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt) exp_"$1" ;;
+  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt}" >&2; exit 2 ;;
 esac
