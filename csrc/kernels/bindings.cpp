@@ -166,6 +166,31 @@ PYBIND11_MODULE(_hip, m) {
         "run_launched(.., flush=True): 1 = the last step's head and the flush in one launch "
         "(mlp_head_flush_kernel; opt-in, measured slower), 0 = the flush as its own launch; "
         "returns the previous setting");
+  // The C++ host loop with its fixed arguments bound once (FusedMLPTrainer.run_launched): a
+  // driver-sized timed region starts on the host, so the per-call Python -> C++ argument
+  // conversion of the 17-argument form sits in front of the region's first kernel.
+  struct MlpRunPlan {
+    float *p0, *p1;
+    const float* x;
+    const int* labels;
+    int nbatches;
+    float* ws;
+    int* ctr;
+    float* stats;
+    int ring, B;
+  };
+  py::class_<MlpRunPlan>(m, "MlpRunPlan")
+      .def(py::init([](uintptr_t p0, uintptr_t p1, uintptr_t x, uintptr_t lab, int nbatches,
+                       uintptr_t ws, uintptr_t ctr, uintptr_t stats, int ring, int B) {
+        return MlpRunPlan{P<float>(p0), P<float>(p1), P<const float>(x), P<const int>(lab),
+                          nbatches, P<float>(ws), P<int>(ctr), P<float>(stats), ring, B};
+      }))
+      .def("run", [](const MlpRunPlan& p, int cur, int pending, float lr, int pos, int n,
+                     int flush, uintptr_t s) {
+        py::gil_scoped_release nogil;
+        dtfx::mlp_run_pipelined_launch(p.p0, p.p1, cur, pending, lr, p.x, p.labels, p.nbatches,
+                                       pos, n, p.ws, p.ctr, p.stats, p.ring, p.B, S(s), flush);
+      }, "(cur, pending, lr, pos, n, flush, stream): mlp_run_pipelined with the bound buffers");
   m.def("mlp_apply", [](uintptr_t p_old, uintptr_t p_new, float lr, uintptr_t x_prev, uintptr_t ws,
                         uintptr_t ctr, uintptr_t stats, int ring, int B, uintptr_t s) {
     dtfx::mlp_apply_launch(P<const float>(p_old), P<float>(p_new), lr, P<const float>(x_prev),

@@ -209,7 +209,21 @@ for r in 1 2 3; do for v in 1 0; do
 done; done
 }
 
+exp_mlp_plan() {
+# Round 6: the MLP host loop's buffers bound once in a C++ plan (7-argument call before the
+# region's first kernel instead of 17) -- host-loop tests, then the driver-sized bench
+# interleaved against the 17-argument entry point (DTFX_MLP_PLAN=0).
+cd "$ROOT"; OUT=gpurun_out/r6plan; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+  tests/test_kernels_gpu.py -k "host_loop or terminal_head_flush" > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
+for r in 1 2 3 4 5 6; do for v in 1 0; do
+  DTFX_MLP_PLAN=$v timeout -k 10 120 python bench.py --steps 20 --warmup 5 > $OUT/k20_plan${v}_$r.json 2>&1 || { tail -5 $OUT/k20_plan${v}_$r.json; exit 1; }
+  echo "plan=$v $r $(tail -1 $OUT/k20_plan${v}_$r.json | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["config"]["launch"])')"
+done; done
+}
+
 case "${1:-}" in
-  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt) exp_"$1" ;;
-  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt}" >&2; exit 2 ;;
+  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan) exp_"$1" ;;
+  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan}" >&2; exit 2 ;;
 esac
