@@ -108,6 +108,7 @@ void adam_mixed_launch(long long, float*, const float*, float*, float*, void*, f
                        float, float, float, const int*, int, hipStream_t, const long long*, int,
                        long long);
 void cast_f32_bf16_launch(long long, const float*, void*, hipStream_t);
+void zero_ranges_launch(const long long*, int, long long, hipStream_t);
 void act_grad_bf16_launch(long long, int, const void*, const void*, void*, hipStream_t);
 void flash_fwd_launch(int, int, int, const void*, void*, float*, int, const float*, float,
                       hipStream_t);
@@ -216,6 +217,9 @@ void register_nn(py::module_& m) {
      py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"),
      py::arg("gscale"), py::arg("step_ptr"), py::arg("step"), py::arg("stream"),
      py::arg("segs") = 0, py::arg("nseg") = 0, py::arg("base4") = 0);
+  m.def("zero_ranges", [](uintptr_t tab, int n, long long total, uintptr_t s) {
+    dtfx::zero_ranges_launch(P<const long long>(tab), n, total, S(s));
+  }, "zero n f32 ranges in one launch: int64 table [n][3] {pointer, length, prefix}");
   m.def("cast_f32_bf16", [](long long n, uintptr_t x, uintptr_t y, uintptr_t s) {
     dtfx::cast_f32_bf16_launch(n, P<const float>(x), P<void>(y), S(s));
   });

@@ -1955,6 +1955,35 @@ void act_grad_bf16_launch(long long n, int act, const void* dy, const void* u, v
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+// Zero many f32 ranges in one launch: table int64 [n][3] = {pointer, length, first element
+// (prefix of the lengths)}, thread i -> range by binary search.  The per-step zeroing of the
+// gradient slots the backward accumulates into (BERT: biases, LayerNorm parameters,
+// embeddings -- a handful of strided fills of ~8 us each) becomes one launch.
+__global__ __launch_bounds__(256) void zero_ranges_kernel(const long long* __restrict__ tab, int n,
+                                                          long long total) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    int lo = 0, hi = n - 1, k = 0;
+    while (lo <= hi) {
+      const int mid = (lo + hi) >> 1;
+      if (tab[3 * mid + 2] <= i) {
+        k = mid;
+        lo = mid + 1;
+      } else {
+        hi = mid - 1;
+      }
+    }
+    ((float*)tab[3 * k])[i - tab[3 * k + 2]] = 0.f;
+  }
+}
+void zero_ranges_launch(const long long* tab, int n, long long total, hipStream_t s) {
+  if (n <= 0 || total <= 0) return;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(zero_ranges_kernel, dim3((unsigned)blocks), dim3(256), 0, s, tab, n, total);
+  DTFX_HIP_CHECK(hipGetLastError());
+}
+
 void cast_f32_bf16_launch(long long n, const float* x, void* y, hipStream_t s) {
   if (n <= 0) return;
   long long blocks = (n + 255) / 256;

@@ -209,6 +209,21 @@ class FlatParams:
                     views.append(self.grad[a:b])
                     rs.discard((a, b))
             self._zero_views = views
+            self._zero_tab = None
+            if self.grad.is_cuda and os.environ.get("DTFX_ZERO_RANGES", "1") != "0":
+                # every range in ONE launch (zero_ranges_kernel) instead of a fill per view
+                rows, tot = [], 0
+                for a, b in sorted(ranges):
+                    rows.append((self.grad.data_ptr() + 4 * a, b - a, tot))
+                    tot += b - a
+                self._zero_tab = (torch.tensor(rows, dtype=torch.int64, device=self.grad.device),
+                                  len(rows), tot)
+        if self._zero_tab is not None:
+            from ..ops._ext import hip, stream_handle
+
+            tab, n, tot = self._zero_tab
+            hip().zero_ranges(tab.data_ptr(), n, tot, stream_handle())
+            return
         for v in self._zero_views:
             v.zero_()
 

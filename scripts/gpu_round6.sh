@@ -223,7 +223,20 @@ for r in 1 2 3 4 5 6; do for v in 1 0; do
 done; done
 }
 
+exp_zero_ranges() {
+# Round 6: BERT's per-step gradient zeroing as ONE zero_ranges launch (DTFX_ZERO_RANGES) --
+# BERT GPU tests, then BERT-base end to end interleaved.
+cd "$ROOT"; OUT=gpurun_out/r6zero; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
+  tests/test_bert_gpu.py > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
+for r in 1 2 3; do for v in 1 0; do
+  DTFX_ZERO_RANGES=$v timeout -k 10 200 python bench.py --model bert > $OUT/bert_z${v}_$r.json 2>&1 || { tail -5 $OUT/bert_z${v}_$r.json; exit 1; }
+  echo "bert zero_ranges=$v $r $(tail -1 $OUT/bert_z${v}_$r.json | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+done; done
+}
+
 case "${1:-}" in
-  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan) exp_"$1" ;;
-  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan}" >&2; exit 2 ;;
+  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges) exp_"$1" ;;
+  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges}" >&2; exit 2 ;;
 esac

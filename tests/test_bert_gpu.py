@@ -235,3 +235,21 @@ def test_bert_zero1_step_captures_and_runs(gpu):
     assert math.isfinite(loss)
     tr.sync_params()
     assert bool(torch.isfinite(tr.model.params.master).all())
+
+
+def test_zero_grad_one_launch_matches_views(gpu, monkeypatch):
+    """The per-step zeroing of the accumulated gradient slots as ONE zero_ranges launch (the
+    default) zeroes exactly the ranges the strided per-view fills do, and nothing else."""
+    from distributedtensorflowexample_amd.models.bert import FlatParams
+
+    cfg = BertConfig.tiny()
+    outs = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("DTFX_ZERO_RANGES", env)
+        p = FlatParams(cfg, gpu, seed=1)
+        p.grad.copy_(torch.arange(p.grad.numel(), device=gpu, dtype=torch.float32) + 1)
+        p.zero_grad()
+        assert (p._zero_tab is not None) == (env == "1")
+        outs.append(p.grad.clone())
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[0] == 0).any() and (outs[0] != 0).any()
