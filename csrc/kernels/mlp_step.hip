@@ -171,6 +171,72 @@ __global__ __launch_bounds__(64) void mlp_fwd_kernel(
 // ---------------------------------------------------------------------------
 // K2: per-row head (one wave per batch row)
 // ---------------------------------------------------------------------------
+// The factor engines' dz1 all-gather of one head row (mlp_head_kernel<.., XW>): BL = polls as
+// 16-byte buffer loads and pushes as global stores (DTFX_XG_SPLIT bit 4, as xg_exchange2p).
+template <int XW, bool BL>
+__device__ __forceinline__ void head_allgather(const MlpXg& xg, unsigned ep, int row, int lane,
+                                               int BP, const float (&dzv)[2],
+                                               float* __restrict__ dz1A, bool& fail) {
+  {
+    // the row's 100 factors travel as 50 16-byte word pairs {dz(2l), ep, dz(2l+1), ep} at
+    // word row * HP + 2l of slot (parity, me) -- a wave's pushes and polls are contiguous
+    // 800-B runs, one store / load per lane and peer -- and land in dz1A [XW][BP][HP] row-major
+    // (one 8-byte store per lane and rank).  Each 8-byte half carries the epoch (as
+    // xg_exchange16); every poll is issued before the pushes (xgll::first_loads).
+    using xgll::u64;
+    using xgll::u32x4;
+    const long long par = ep & 1u, plane = (long long)HP * BP;
+    const int me = xgll::uniform(xg.rank);
+    const bool act = lane < H / 2;
+    const long long woff = (long long)row * HP + 2 * (act ? lane : 0);
+    auto slot = [&](int dst, int src) {
+      return xgll::uniform_ptr((u64*)xg.peers.data[dst]) + (par * XW + src) * xg.S + woff;
+    };
+    const xgll::OwnPoll pr(BL ? xgll::uniform_ptr((const u64*)xg.peers.data[me]) : nullptr);
+    auto poll = [&](int q) {
+      if constexpr (BL) return pr.pair((par * XW + q) * xg.S, woff);
+      else return xgll::load_pair(slot(me, q));
+    };
+    u32x4 wq[XW];
+#pragma unroll
+    for (int q = 0; q < XW; ++q)
+      if (act && q != me) wq[q] = poll(q);
+    if (act) {
+      const u32x4 out = {__float_as_uint(dzv[0]), ep, __float_as_uint(dzv[1]), ep};
+#pragma unroll
+      for (int d = 0; d < XW; ++d)
+        if (d != me) {
+          if constexpr (BL) xgll::store_pair_g(slot(d, me), out);
+          else *(u32x4*)slot(d, me) = out;
+        }
+    }
+    if (act) {
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        bool ready = true;
+#pragma unroll
+        for (int q = 0; q < XW; ++q)
+          if (q != me && (wq[q].y != ep || wq[q].w != ep)) {
+            ready = false;
+            wq[q] = poll(q);
+          }
+        if (ready) break;
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xg.ticks) {
+          fail = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int q = 0; q < XW; ++q) {
+        const float2 v = q == me ? make_float2(dzv[0], dzv[1])
+                                 : make_float2(__uint_as_float(wq[q].x), __uint_as_float(wq[q].z));
+        *reinterpret_cast<float2*>(&dz1A[q * plane + woff]) = v;
+      }
+    }
+  }
+}
+
 // XW > 0 (factor exchange, MlpXg in xgmi.h): the row's dz1 values are also pushed as LL
 // words into slot (parity, me) of every peer and every peer's values for the same (j, row)
 // are gathered from local memory into dz1A [XW][BP][HP] -- the all-gather of the backprop
@@ -306,55 +372,9 @@ __device__ __forceinline__ void head_row(
     }
   }
   if constexpr (XW > 0) {
-    // the row's 100 factors travel as 50 16-byte word pairs {dz(2l), ep, dz(2l+1), ep} at
-    // word row * HP + 2l of slot (parity, me) -- a wave's pushes and polls are contiguous
-    // 800-B runs, one store / load per lane and peer -- and land in dz1A [XW][BP][HP] row-major
-    // (one 8-byte store per lane and rank).  Each 8-byte half carries the epoch (as
-    // xg_exchange16); every poll is issued before the pushes (xgll::first_loads).
-    using xgll::u64;
-    using xgll::u32x4;
-    const long long par = ep & 1u, plane = (long long)HP * BP;
-    const int me = xgll::uniform(xg.rank);
-    const bool act = lane < H / 2;
-    const long long woff = (long long)row * HP + 2 * (act ? lane : 0);
-    auto slot = [&](int dst, int src) {
-      return xgll::uniform_ptr((u64*)xg.peers.data[dst]) + (par * XW + src) * xg.S + woff;
-    };
-    u32x4 wq[XW];
-#pragma unroll
-    for (int q = 0; q < XW; ++q)
-      if (act && q != me) wq[q] = xgll::load_pair(slot(me, q));
-    if (act) {
-      const u32x4 out = {__float_as_uint(dzv[0]), ep, __float_as_uint(dzv[1]), ep};
-#pragma unroll
-      for (int d = 0; d < XW; ++d)
-        if (d != me) *(u32x4*)slot(d, me) = out;
-    }
     bool fail = false;
-    if (act) {
-      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-      for (;;) {
-        bool ready = true;
-#pragma unroll
-        for (int q = 0; q < XW; ++q)
-          if (q != me && (wq[q].y != ep || wq[q].w != ep)) {
-            ready = false;
-            wq[q] = xgll::load_pair(slot(me, q));
-          }
-        if (ready) break;
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xg.ticks) {
-          fail = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-#pragma unroll
-      for (int q = 0; q < XW; ++q) {
-        const float2 v = q == me ? make_float2(dzv[0], dzv[1])
-                                 : make_float2(__uint_as_float(wq[q].x), __uint_as_float(wq[q].z));
-        *reinterpret_cast<float2*>(&dz1A[q * plane + woff]) = v;
-      }
-    }
+    if (xg.split & 16) head_allgather<XW, true>(xg, ep, row, lane, BP, dzv, dz1A, fail);
+    else head_allgather<XW, false>(xg, ep, row, lane, BP, dzv, dz1A, fail);
     if (lane == 0) xg.epochs[MLP_XG_HEAD_EPOCH + row] = ep;
     if (fail) atomicExch(xg.err, 1);
   }
@@ -428,7 +448,8 @@ __device__ __forceinline__ void xg_exchange(const MlpXg& xg, unsigned ep, const 
 // XG_W1_BASE layout -- the same on every rank.  `live` = false (a pair of padding columns /
 // hidden rows, the same on every rank): neither pushed nor gathered -- 22 % of the layout's
 // pairs, so the links carry live parameters only (78,400 of 100,352 words).
-template <int XW>
+// BL: polls as 16-byte buffer loads, pushes as global stores (as xg_exchange2p<XW, true>).
+template <int XW, bool BL = false>
 __device__ __forceinline__ void xg_exchange16(const MlpXg& xg, unsigned ep, long long woff,
                                               float (&v)[2], bool& fail, bool live = true) {
   using xgll::u64;
@@ -436,17 +457,25 @@ __device__ __forceinline__ void xg_exchange16(const MlpXg& xg, unsigned ep, long
   const long long par = ep & 1u;
   const int me = xgll::uniform(xg.rank);
   const u64* mine = xgll::uniform_ptr((const u64*)xg.peers.data[me]) + woff;
+  const xgll::OwnPoll pr(BL ? mine - woff : nullptr);
+  auto poll = [&](int j) {
+    if constexpr (BL) return pr.pair((par * XW + j) * xg.S, woff);
+    else return xgll::load_pair(mine + (par * XW + j) * xg.S);
+  };
   const u32x4 out = {__float_as_uint(v[0]), ep, __float_as_uint(v[1]), ep};
   u32x4 w[XW];  // first polls before the pushes (xgll::first_loads: one vmcnt for both)
 #pragma unroll
   for (int j = 0; j < XW; ++j) {
     w[j] = u32x4{0u, ep, 0u, ep};
-    if (live && j != me) w[j] = xgll::load_pair(mine + (par * XW + j) * xg.S);
+    if (live && j != me) w[j] = poll(j);
   }
 #pragma unroll
   for (int d = 0; d < XW; ++d)
-    if (live && d != me)
-      *(u32x4*)(xgll::uniform_ptr((u64*)xg.peers.data[d]) + (par * XW + me) * xg.S + woff) = out;
+    if (live && d != me) {
+      u64* dst = xgll::uniform_ptr((u64*)xg.peers.data[d]) + (par * XW + me) * xg.S + woff;
+      if constexpr (BL) xgll::store_pair_g(dst, out);
+      else *(u32x4*)dst = out;
+    }
   const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
   for (;;) {
     bool ready = true;
@@ -454,7 +483,7 @@ __device__ __forceinline__ void xg_exchange16(const MlpXg& xg, unsigned ep, long
     for (int j = 0; j < XW; ++j)
       if (j != me && (w[j].y != ep || w[j].w != ep)) {
         ready = false;
-        w[j] = xgll::load_pair(mine + (par * XW + j) * xg.S);
+        w[j] = poll(j);
       }
     if (ready) break;
     if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xg.ticks) {
@@ -484,7 +513,10 @@ __device__ __forceinline__ void xg_exchange16(const MlpXg& xg, unsigned ep, long
 // is issued before the hop's own pushes (xgll::first_loads: stores and loads share one
 // in-order vmcnt).  Each 8-byte half carries the epoch, as in xg_exchange16.
 // `live` as in xg_exchange16: a dead pair is neither pushed, gathered nor broadcast.
-template <int XW>
+// BL (DTFX_XG_SPLIT bit 4, round 6): the polls of the own slot region as 16-byte raw buffer
+// loads and the pushes as GLOBAL stores (xgll::OwnPoll / store_pair_g) instead of FLAT
+// accesses -- same words, same coherence bits.
+template <int XW, bool BL = false>
 __device__ __forceinline__ void xg_exchange2p(const MlpXg& xg, unsigned ep, long long woff,
                                               float (&v)[2], bool& fail, int lane, int sp,
                                               unsigned long long* trw = nullptr,
@@ -503,17 +535,30 @@ __device__ __forceinline__ void xg_exchange2p(const MlpXg& xg, unsigned ep, long
   auto slot = [&](int dst, int src) { return base(dst) + (par * XW + src) * xg.S + woff; };
   auto result = [&](int dst) { return base(dst) + (2 * XW + par) * xg.S + woff; };
   auto ready2 = [&](const u32x4& w) { return w.y == ep && w.w == ep; };
+  const xgll::OwnPoll pr(BL ? base(me) : nullptr);
+  auto poll_slot = [&](int j) {
+    if constexpr (BL) return pr.pair((par * XW + j) * xg.S, woff);
+    else return xgll::load_pair(slot(me, j));
+  };
+  auto poll_result = [&]() {
+    if constexpr (BL) return pr.pair((2 * XW + par) * xg.S, woff);
+    else return xgll::load_pair(result(me));
+  };
+  auto put = [&](u64* p, const u32x4& w) {
+    if constexpr (BL) xgll::store_pair_g(p, w);
+    else *(u32x4*)p = w;
+  };
   // ---- hop 1: owners' first polls, then the non-owners' push to their owner
   u32x4 w[XW];
 #pragma unroll
   for (int j = 0; j < XW; ++j)
-    if (mine && j != me) w[j] = xgll::load_pair(slot(me, j));
+    if (mine && j != me) w[j] = poll_slot(j);
   const u32x4 out = {__float_as_uint(v[0]), ep, __float_as_uint(v[1]), ep};
   // uniform loop over destinations, per-lane predicate: a per-lane peer index would turn the
   // kernel-argument pointer table into a private (scratch) array
 #pragma unroll
   for (int d = 0; d < XW; ++d)
-    if (other && own == d) *(u32x4*)slot(d, me) = out;
+    if (other && own == d) put(slot(d, me), out);
   const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
   if (mine) {
     for (;;) {
@@ -522,7 +567,7 @@ __device__ __forceinline__ void xg_exchange2p(const MlpXg& xg, unsigned ep, long
       for (int j = 0; j < XW; ++j)
         if (j != me && !ready2(w[j])) {
           ready = false;
-          w[j] = xgll::load_pair(slot(me, j));
+          w[j] = poll_slot(j);
         }
       if (ready) break;
       if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xg.ticks) {
@@ -543,12 +588,12 @@ __device__ __forceinline__ void xg_exchange2p(const MlpXg& xg, unsigned ep, long
   if (trw) trace_stamp(trw, 5);  // probe builds: the owned sums are complete
   // ---- hop 2: non-owners' first poll of the result, then the owners' broadcast
   u32x4 r = {0u, 0u, 0u, 0u};
-  if (other) r = xgll::load_pair(result(me));
+  if (other) r = poll_result();
   if (mine && !fail) {
     const u32x4 sum = {__float_as_uint(v[0]), ep, __float_as_uint(v[1]), ep};
 #pragma unroll
     for (int d = 0; d < XW; ++d)
-      if (d != me) *(u32x4*)result(d) = sum;
+      if (d != me) put(result(d), sum);
   }
   if (other) {
     const long long t1 = (long long)__builtin_amdgcn_s_memrealtime();
@@ -558,7 +603,7 @@ __device__ __forceinline__ void xg_exchange2p(const MlpXg& xg, unsigned ep, long
         break;
       }
       __builtin_amdgcn_s_sleep(1);
-      r = xgll::load_pair(result(me));
+      r = poll_result();
     }
     v[0] = __uint_as_float(r.x);
     v[1] = __uint_as_float(r.z);
@@ -1057,10 +1102,16 @@ __device__ __forceinline__ void fwdapply_block(
       if constexpr (TWO) {
         if (xg.split & 4)  // (DTFX_XG_SPLIT bit 2: the round-4 per-element owners, A/B runs)
           xg_exchange2<XW, 2>(xg, ep, offw, okw, g2, fail, lane, TRACE ? trw : nullptr, 2 * sp);
+        else if (xg.split & 16)
+          xg_exchange2p<XW, true>(xg, ep, XG_W1_BASE + ((long long)(eslot * 2 + sp) * 64 + lane) * 2,
+                                  g2, fail, lane, sp, TRACE ? trw : nullptr, plive);
         else
           xg_exchange2p<XW>(xg, ep, XG_W1_BASE + ((long long)(eslot * 2 + sp) * 64 + lane) * 2,
                             g2, fail, lane, sp, TRACE ? trw : nullptr, plive);
-      } else
+      } else if (xg.split & 16)
+        xg_exchange16<XW, true>(xg, ep, XG_W1_BASE + ((long long)(eslot * 2 + sp) * 64 + lane) * 2,
+                                g2, fail, plive);
+      else
         xg_exchange16<XW>(xg, ep, XG_W1_BASE + ((long long)(eslot * 2 + sp) * 64 + lane) * 2,
                           g2, fail, plive);
       if (TRACE) trace_stamp(trw, 6);

@@ -17,11 +17,15 @@ using u64 = unsigned long long;
 __device__ __forceinline__ u64 word(float v, unsigned e) {
   return ((u64)e << 32) | __float_as_uint(v);
 }
+// Every LL word lives in device / IPC global memory, so the accesses are issued through the
+// global address space (`global_*` instructions, vmcnt only) rather than as FLAT ones (which
+// also count in lgkmcnt, so each wait on them waited for the wave's LDS traffic too).
+typedef __attribute__((address_space(1))) u64 gu64;
 __device__ __forceinline__ void store(u64* p, u64 w) {
-  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store((gu64*)p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ u64 load(const u64* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load((const gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // A 16-byte LL word pair {v0, epoch, v1, epoch} read as TWO relaxed system-scope 8-byte loads
@@ -32,6 +36,28 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ u32x4 load_pair(const u64* p) {
   const u64 a = load(p), b = load(p + 1);
   return u32x4{(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+}
+
+// Polls of a rank's OWN slot region as raw buffer loads (round 6): one 16-byte
+// `buffer_load_dwordx4 ... sc0 sc1` per pair instead of two FLAT 8-byte atomic loads.  The
+// aux bits are the system-scope coherence bits the relaxed system atomics set (sc0 | sc1), each
+// aligned 8-byte half of the access is one {value, epoch} word as before (the half is what
+// carries its epoch, so a reader never trusts more than 8 bytes), and unlike a `volatile`
+// 16-byte load the compiler tracks the buffer intrinsic like any load: the W - 1 polls stay in
+// flight together.  Buffer (and global) instructions count in vmcnt only; a FLAT access counts
+// in vmcnt AND lgkmcnt, so every wait on one also waited for the wave's LDS traffic.
+struct OwnPoll {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ explicit OwnPoll(const u64* base)
+      : r(__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000)) {}
+  // word offsets: `region` (wave-uniform, -> soffset) + `lane_off` (per lane, -> voffset)
+  __device__ __forceinline__ u32x4 pair(long long region, long long lane_off) const {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)(lane_off * 8), (int)(region * 8), 17);
+  }
+};
+// A 16-byte pair stored to a peer (or own) slot as a GLOBAL store (not FLAT: vmcnt only).
+__device__ __forceinline__ void store_pair_g(u64* p, const u32x4& w) {
+  *(__attribute__((address_space(1))) u32x4*)p = w;
 }
 
 // A wave-uniform value made provably uniform (scalar registers): the peer pointer table and

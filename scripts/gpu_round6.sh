@@ -236,7 +236,22 @@ for r in 1 2 3; do for v in 1 0; do
 done; done
 }
 
+exp_engines() {
+# Round 6: the MLP exchange engines' local cost at world 2 / 4 / 8 (simulated peers,
+# tools/probes/engine_local_cost.py) -- the xGMI simulation tests with the variant's
+# DTFX_XG_SPLIT first, then the default (${BASE_SPLIT:-3}) and the variant (${VAR_SPLIT:-19})
+# interleaved on one box.
+cd "$ROOT"; OUT=gpurun_out/r6eng; mkdir -p $OUT
+DTFX_XG_SPLIT=${VAR_SPLIT:-19} timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+  -p no:cacheprovider tests/test_xgmi_sim_gpu.py > $OUT/xgmi_sim_${VAR_SPLIT:-19}.log 2>&1 || { tail -30 $OUT/xgmi_sim_${VAR_SPLIT:-19}.log; exit 1; }
+tail -1 $OUT/xgmi_sim_${VAR_SPLIT:-19}.log
+for r in 1 2 3; do for v in ${BASE_SPLIT:-3} ${VAR_SPLIT:-19}; do
+  DTFX_XG_SPLIT=$v ENGINES=${ENGINES:-fused2x} timeout -k 10 200 python tools/probes/engine_local_cost.py > $OUT/elc_${v}_$r.json 2>$OUT/elc_${v}_$r.err || { tail -5 $OUT/elc_${v}_$r.err; exit 1; }
+  echo "split=$v $r $(python -c "import json;d=json.load(open('$OUT/elc_${v}_$r.json'));print(d['single_gpu_2launch_us'],{e:[d['world%d'%w][e] for w in (2,4,8)] for e in d['world2'] if e!='epoch_reset_us'})")"
+done; done
+}
+
 case "${1:-}" in
-  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges) exp_"$1" ;;
-  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges}" >&2; exit 2 ;;
+  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines) exp_"$1" ;;
+  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines}" >&2; exit 2 ;;
 esac
