@@ -1308,6 +1308,82 @@ constexpr int FX_SLOTS = (KS3 + 7) / 8 * HT;  // block slots per XCD (4 slice ro
 // instantiations; the generic ones keep 4 (512 threads: their small-parameter waves hold
 // 16 batch groups of operands, which 4 waves per SIMD would spill)
 template <int NGT> constexpr int fx_kspl() { return NGT > 0 ? 8 : 4; }
+// Phase A of mlp_fwdapply_factor_kernel in row-quad form (DTFX_XG_SPLIT bit 5, round 6): each
+// of the block's 16 waves covers ALL 28 features of the slice for its 1/16 of the K = XW x BP
+// rows.  Per quad of 4 rows a lane loads ONE float2 of x (features 2r, 2r + 1 of row base + q;
+// lanes r >= 14 are dead) and ONE dz1A value (hidden r of row base + q), and feeds two
+// 16x16x4 MFMAs (accumulator e: features 2r + e).  The column-group form loads four scalar x
+// and four dz1A values per 16 rows and column group -- twice the load instructions per
+// element, the one cost that grows with K = XW x BP (the global W1 gradient is 8x the 1-GPU
+// step's MFMA work at 8 ranks).  The 16 partials are added in split order (the same bits on
+// every rank); wave e in {0, 1} applies accumulator e.
+template <int XW, int NGT>
+__device__ __forceinline__ void fx_phase_a_quads(
+    const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
+    const float* __restrict__ x_prev, long long xstride, const float* __restrict__ dz1A, int B,
+    int BP, int jt, int f0, int me, int wave, int lane, float (&Wt)[16][D / KS3 + 4],
+    f32x4* red) {
+  constexpr int KWX = D / KS3;         // 28 features
+  constexpr int NQ = NGT * 4;          // row quads per rank
+  constexpr int GQ = XW * NQ;          // row quads in all
+  constexpr int QPW = (GQ + 15) / 16;  // per wave (14 at 8 ranks x 112 rows)
+  const int r = lane & 15, q = lane >> 4;
+  const bool lv = r < KWX / 2;
+  const int fo = 2 * (lv ? r : KWX / 2 - 1);
+  float pw[4];
+  if (wave < 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = jt * 16 + q * 4 + i;
+      pw[i] = p_old[OFF_W1 + (size_t)(j < H ? j : H - 1) * D + f0 + fo + wave];
+    }
+  }
+  float av[QPW];
+  float2 xv[QPW];
+  const int u0 = wave * QPW;
+#pragma unroll
+  for (int u = 0; u < QPW; ++u) {
+    const int g = u0 + u;
+    if (g < GQ) {  // wave-uniform
+      const int qq = g / NQ, row = (g - qq * NQ) * 4 + q;
+      av[u] = dz1A[((size_t)qq * BP + row) * HP + jt * 16 + r];  // rows >= B: zero
+      xv[u] = *reinterpret_cast<const float2*>(
+          x_prev + (long long)(qq - me) * xstride + (size_t)(row < B ? row : B - 1) * D + f0 + fo);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // the wave's loads in flight together
+  f32x4 a0 = {0, 0, 0, 0}, a1 = {0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < QPW; ++u) {
+    if (u0 + u < GQ) {
+      a0 = mfma16x16x4(av[u], xv[u].x, a0);
+      a1 = mfma16x16x4(av[u], xv[u].y, a1);
+    }
+  }
+  red[(wave * 2 + 0) * 64 + lane] = a0;
+  red[(wave * 2 + 1) * 64 + lane] = a1;
+  __syncthreads();
+  if (wave < 2) {
+    f32x4 part = red[wave * 64 + lane];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {  // split order: the same bits on every rank
+      const f32x4 o = red[(k * 2 + wave) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[i] += o[i];
+    }
+    const int fl = fo + wave;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hl = q * 4 + i, j = jt * 16 + hl;
+      const float v = pw[i] - lr * part[i];
+      if (lv) {
+        Wt[hl][fl] = j < H ? v : 0.f;
+        if (j < H) p_new[OFF_W1 + (size_t)j * D + f0 + fl] = v;
+      }
+    }
+  }
+}
+
 template <int XW, int NGT>
 __global__ __launch_bounds__(128 * fx_kspl<NGT>()) void mlp_fwdapply_factor_kernel(
     const float* __restrict__ p_old, float* __restrict__ p_new, float lr,
@@ -1335,7 +1411,8 @@ __global__ __launch_bounds__(128 * fx_kspl<NGT>()) void mlp_fwdapply_factor_kern
   constexpr int KWX = D / KS3;  // 28 features
   constexpr int LW = KWX + 4;
   __shared__ float Wt[16][LW];
-  __shared__ f32x4 red[2][FX_KSPL - 1][64];
+  // K-split partials: [c][k][lane] (column-group form) or [s][e][lane] (row-quad form)
+  __shared__ f32x4 red[32 * 64];
   const int f0 = ks * KWX;
   const int me = xgll::uniform(xg.rank);
   // phase B's x rows (wave w < RT owns row tile w; B <= 128): requested first
@@ -1350,6 +1427,14 @@ __global__ __launch_bounds__(128 * fx_kspl<NGT>()) void mlp_fwdapply_factor_kern
       xa[g] = f4(xr + (k < KWX ? k : 0));
     }
   }
+  if constexpr (NGT > 0) {
+    if (xg.split & 32) {
+      fx_phase_a_quads<XW, NGT>(p_old, p_new, lr, x_prev, xstride, dz1A, B, BP, jt, f0, me,
+                                wave, lane, Wt, red);
+      goto phase_b;
+    }
+  }
+  {
   // ---- phase A: column group c, K split sp (FX_KSPL splits) ------------------------------
   const int c = wave & 1, sp = wave >> 1;
   const int fl = c * 16 + r;
@@ -1400,12 +1485,12 @@ __global__ __launch_bounds__(128 * fx_kspl<NGT>()) void mlp_fwdapply_factor_kern
   f32x4 part;
 #pragma unroll
   for (int i = 0; i < 4; ++i) part[i] = acc0[i] + acc1[i];
-  if (sp > 0) red[c][sp - 1][lane] = part;
+  if (sp > 0) red[(c * (FX_KSPL - 1) + sp - 1) * 64 + lane] = part;
   __syncthreads();
   if (sp == 0) {
 #pragma unroll
     for (int k = 0; k < FX_KSPL - 1; ++k) {  // split order: the same bits on every rank
-      const f32x4 o = red[c][k][lane];
+      const f32x4 o = red[(c * (FX_KSPL - 1) + k) * 64 + lane];
 #pragma unroll
       for (int i = 0; i < 4; ++i) part[i] += o[i];
     }
@@ -1419,6 +1504,8 @@ __global__ __launch_bounds__(128 * fx_kspl<NGT>()) void mlp_fwdapply_factor_kern
       }
     }
   }
+  }
+phase_b:
   __syncthreads();
   // ---- phase B: z1 partial of row tile `wave` over the block's 28 features -------------
   if (wave >= RT) return;

@@ -42,9 +42,10 @@ struct MlpXg {
   unsigned* epochs;     // one counter per (block, wave) of the kernel, device resident
   int* err;             // set on a timed-out wait
   long long ticks;      // wait bound in s_memrealtime ticks (100 MHz)
-  // exchange work split (DTFX_XG_SPLIT, default 19): bit 0 -- mlp_fwdapply_kernel's W1 slices
+  // exchange work split (DTFX_XG_SPLIT, default 51): bit 0 -- mlp_fwdapply_kernel's W1 slices
   // over both K-split waves; bit 1 -- the small parameters' dW2 over two waves (A/B probes);
-  // bit 4 -- the pair exchanges' polls as 16-byte buffer loads, pushes as global stores
+  // bit 4 -- the pair exchanges' polls as 16-byte buffer loads, pushes as global stores;
+  // bit 5 -- the factor first launch's global W1 gradient in row-quad form (fx_phase_a_quads)
   int split;
 };
 constexpr int MLP_XG_EPOCHS = 1024;

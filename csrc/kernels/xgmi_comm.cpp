@@ -177,7 +177,7 @@ class XgmiAllReduce {
     xg.err = err_;
     xg.ticks = (long long)(timeout_s * 1e8);
     const char* sp = getenv("DTFX_XG_SPLIT");
-    xg.split = sp ? atoi(sp) : 19;
+    xg.split = sp ? atoi(sp) : 51;
     return xg;
   }
 
