@@ -1427,14 +1427,11 @@ __global__ __launch_bounds__(128 * fx_kspl<NGT>()) void mlp_fwdapply_factor_kern
       xa[g] = f4(xr + (k < KWX ? k : 0));
     }
   }
-  if constexpr (NGT > 0) {
-    if (xg.split & 32) {
+  if (NGT > 0 && (xg.split & 32)) {
+    if constexpr (NGT > 0)
       fx_phase_a_quads<XW, NGT>(p_old, p_new, lr, x_prev, xstride, dz1A, B, BP, jt, f0, me,
                                 wave, lane, Wt, red);
-      goto phase_b;
-    }
-  }
-  {
+  } else {
   // ---- phase A: column group c, K split sp (FX_KSPL splits) ------------------------------
   const int c = wave & 1, sp = wave >> 1;
   const int fl = c * 16 + r;
@@ -1505,7 +1502,6 @@ __global__ __launch_bounds__(128 * fx_kspl<NGT>()) void mlp_fwdapply_factor_kern
     }
   }
   }
-phase_b:
   __syncthreads();
   // ---- phase B: z1 partial of row tile `wave` over the block's 28 features -------------
   if (wave >= RT) return;
