@@ -10,6 +10,7 @@ namespace dtfx {
 void gemm_bf16_set_cfg(int);
 int gemm_bf16_set_pers(int);
 void attn_bwd_set_variant(int);
+void attn_bwd_set_pf(int);
 void attn_set_swizzle(int);
 void attn_fwd_set_variant(int);
 void transpose_bf16_batch_launch(const long long*, int, int, hipStream_t);
@@ -128,6 +129,9 @@ void register_nn(py::module_& m) {
   m.def("attn_bwd_set_variant", &dtfx::attn_bwd_set_variant,
         "force the attention-backward kernel (-1 = environment; 0: 8 waves, 1: 4 waves, "
         "2: two query halves, two blocks per CU)");
+  m.def("attn_bwd_set_pf", &dtfx::attn_bwd_set_pf,
+        "two-halves attention backward: 1 = V rows requested at block start (L2 warm-up, "
+        "opt-in, measured slower), 0 = not (default), -1 = from DTFX_ATTN_BWD_PF");
   m.def("attn_fwd_set_variant", &dtfx::attn_fwd_set_variant,
         "attention forward: 1 = P in registers (attn_fwd_rp_kernel, default), 0 = P through "
         "LDS (attn_fwd_kernel), -1 = from DTFX_ATTN_FWD");

@@ -1211,7 +1211,15 @@ template <bool SWZ> constexpr int LDS() { return KIMG<SWZ>() + 2 * QH<SWZ>() + 2
 // SWZ (DTFX_ATTN_SWZ=1, opt-in): every image XOR-swizzled (at::swz): LDS bank-conflict cycles
 // 56.2 M -> 8.7 M and LDS-wait cycles 134 M -> 24 M on the probe, but 58.7-62.4 -> 61.1-63.2
 // us per call (profiles/r6/attn_swizzle/): the kernel is not LDS-bound.
-template <bool SWZ>
+// PF (DTFX_ATTN_BWD_PF=1, opt-in; measured slower, profiles/r6/attn_pf/: 63.3-65.9 vs
+// 60.5-62.3 us per call, BERT-base 8,482-8,520 vs 8,494-8,529 seq/s interleaved): the block's
+// V rows are requested at the block's start with
+// the K rows, as LDS-destination loads into the not-yet-used P^T / dS^T images (the data is
+// never read there: the point is that phase 1's per-key-tile V fragment loads, one exposed
+// round trip per key tile and half, then hit this XCD's L2 instead of HBM).  It costs no VGPR:
+// the kernel sits at its 128-VGPR budget (staging the log-sum-exp values in LDS as well, so
+// phase 1 would issue no global load but V's, spilled 12 bytes per lane).
+template <bool SWZ, bool PF = false>
 __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
     int S, int nh, const unsigned short* __restrict__ qkv, const unsigned short* __restrict__ o,
     const unsigned short* __restrict__ dout, const float* __restrict__ lse,
@@ -1241,6 +1249,15 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_half_kernel(
       const int e = tid + 512 * k, r = e >> 3, c = e & 7;
       kv[k] = *(const bf16x8*)(base + Hd + (size_t)min(r, S - 1) * ld + c * 8);
       if (r >= S) kv[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    if constexpr (PF) {  // V rows -> L2 (landing in the P^T image, overwritten in phase 1)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int e = tid + 512 * k, r = e >> 3, c = e & 7;
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(base + 2 * Hd + (size_t)min(r, S - 1) * ld + c * 8),
+            (__attribute__((address_space(3))) void*)(PTs + (e - lane) * 16), 16, 0, 0);
+      }
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -1815,19 +1832,37 @@ void attn_fwd_launch(int Bn, int S, int nh, const void* qkv, void* out, float* l
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+template <bool SWZ, bool PF>
+static void attn_bwd_half_launch_t(int Bn, int S, int nh, const void* qkv, const void* o,
+                                   const void* dout, const float* lse, const float* kmask,
+                                   float scale, void* dqkv, float* dbias, hipStream_t s) {
+  static bool hattr = false;
+  if (!hattr) {
+    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_half_kernel<SWZ, PF>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, atb::LDS<SWZ>()));
+    hattr = true;
+  }
+  hipLaunchKernelGGL((attn_bwd_half_kernel<SWZ, PF>), dim3(Bn * nh), dim3(512), atb::LDS<SWZ>(), s,
+                     S, nh, (const unsigned short*)qkv, (const unsigned short*)o,
+                     (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv, dbias);
+}
+static int g_attn_bwd_pf = -1;  // -1: DTFX_ATTN_BWD_PF (tests set both forms)
+void attn_bwd_set_pf(int v) { g_attn_bwd_pf = v; }
+static bool attn_bwd_pf() {
+  static const bool env = [] {
+    const char* e = std::getenv("DTFX_ATTN_BWD_PF");
+    return e && std::atoi(e) == 1;
+  }();
+  return g_attn_bwd_pf >= 0 ? g_attn_bwd_pf == 1 : env;
+}
 template <bool SWZ>
 static void attn_bwd_half_launch(int Bn, int S, int nh, const void* qkv, const void* o,
                                  const void* dout, const float* lse, const float* kmask,
                                  float scale, void* dqkv, float* dbias, hipStream_t s) {
-  static bool hattr = false;
-  if (!hattr) {
-    DTFX_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_half_kernel<SWZ>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, atb::LDS<SWZ>()));
-    hattr = true;
-  }
-  hipLaunchKernelGGL(attn_bwd_half_kernel<SWZ>, dim3(Bn * nh), dim3(512), atb::LDS<SWZ>(), s, S, nh,
-                     (const unsigned short*)qkv, (const unsigned short*)o,
-                     (const unsigned short*)dout, lse, kmask, scale, (unsigned short*)dqkv, dbias);
+  if (attn_bwd_pf())
+    attn_bwd_half_launch_t<SWZ, true>(Bn, S, nh, qkv, o, dout, lse, kmask, scale, dqkv, dbias, s);
+  else
+    attn_bwd_half_launch_t<SWZ, false>(Bn, S, nh, qkv, o, dout, lse, kmask, scale, dqkv, dbias, s);
 }
 
 // Attention-backward kernel: -1 = from the environment, 0: attn_bwd_kernel<8>,

@@ -251,7 +251,25 @@ for r in 1 2 3; do for v in ${BASE_SPLIT:-3} ${VAR_SPLIT:-19}; do
 done; done
 }
 
+exp_attn_pf() {
+# Round 6: the two-halves attention backward with the block's V rows requested at its start
+# (L2 warm-up, DTFX_ATTN_BWD_PF=1, opt-in) against without (=0) -- attention GPU tests, the
+# standalone probe and BERT-base end to end, interleaved.
+cd "$ROOT"; OUT=gpurun_out/r6attnpf; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+  tests/test_transformer_gpu.py > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+for r in 1 2 3; do for v in 1 0; do
+  DTFX_ATTN_BWD_PF=$v timeout -k 10 120 python tools/probes/attn_one.py 40 > $OUT/attn_pf${v}_$r.json 2>&1 || { tail -5 $OUT/attn_pf${v}_$r.json; exit 1; }
+  echo "attn pf=$v $r $(tail -1 $OUT/attn_pf${v}_$r.json)"
+done; done
+for r in 1 2 3; do for v in 1 0; do
+  DTFX_ATTN_BWD_PF=$v timeout -k 10 200 python bench.py --model bert > $OUT/bert_pf${v}_$r.json 2>&1 || { tail -5 $OUT/bert_pf${v}_$r.json; exit 1; }
+  echo "bert pf=$v $r $(tail -1 $OUT/bert_pf${v}_$r.json | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+done; done
+}
+
 case "${1:-}" in
-  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines) exp_"$1" ;;
-  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines}" >&2; exit 2 ;;
+  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines|attn_pf) exp_"$1" ;;
+  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines|attn_pf}" >&2; exit 2 ;;
 esac

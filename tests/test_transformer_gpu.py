@@ -57,9 +57,10 @@ def test_embedding_fwd_bwd(gpu, B):
 
 # 3 / 4: persistent (4: 3 blocks, 4 pairs each); 5: the two-halves kernel and the P-through-LDS
 # forward with the XOR-swizzled LDS images (opt-in DTFX_ATTN_SWZ=1); 6: the two-halves kernel
-# and the P-through-LDS forward (DTFX_ATTN_FWD=0).  Variants 0-4 run the default forward with P
-# in registers (attn_fwd_rp_kernel).
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+# and the P-through-LDS forward (DTFX_ATTN_FWD=0); 7: the two-halves kernel with the opt-in V-row
+# L2 warm-up (DTFX_ATTN_BWD_PF=1).  Variants 0-4 and 7 run the default forward with P in
+# registers (attn_fwd_rp_kernel).
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("S,masked", [(128, False), (128, True), (77, True), (64, False), (33, True)])
 def test_attention_fwd_bwd(gpu, S, masked, variant):
     B, nh = 3, 4
@@ -70,7 +71,8 @@ def test_attention_fwd_bwd(gpu, S, masked, variant):
         kmask = torch.where(torch.arange(S)[None, :] < valid[:, None], 0.0, -10000.0)
     hip = _ext.hip()
     hip.attn_set_swizzle(1 if variant == 5 else 0)
-    hip.attn_fwd_set_variant(0 if variant >= 5 else 1)
+    hip.attn_fwd_set_variant(0 if variant in (5, 6) else 1)
+    hip.attn_bwd_set_pf(1 if variant == 7 else 0)
     try:
         o, lse = T.attn_fwd(qkv.to(gpu), B, S, nh, kmask.to(gpu) if masked else None)
         orf, lser = T.attn_fwd(qkv, B, S, nh, kmask)
@@ -82,6 +84,7 @@ def test_attention_fwd_bwd(gpu, S, masked, variant):
         torch.cuda.synchronize()
     finally:
         hip.attn_bwd_set_variant(-1)
+        hip.attn_bwd_set_pf(-1)
         hip.attn_set_swizzle(-1)
         hip.attn_fwd_set_variant(-1)
     dqr = T.attn_bwd(qkv, o.cpu(), dout, lse.cpu(), B, S, nh, kmask)
