@@ -269,7 +269,21 @@ for r in 1 2 3; do for v in 1 0; do
 done; done
 }
 
+exp_dp_ta8() {
+# Round 6: BERT-base's data-parallel shape (tools/probes/dp_sim.py, simulated world 8) with the
+# weight gradients on the 8-phase tile (DTFX_GEMM_TA8=1) against the 128x128 split-K default:
+# in DP mode the weight gradients run on a side stream, where the 128x128 blocks (64 KB of LDS,
+# two per CU) keep the data gradients' 8-phase blocks (128 KB) off those CUs.  Separate
+# processes (the switch is read once), interleaved.
+cd "$ROOT"; OUT=gpurun_out/r6dpta8; mkdir -p $OUT
+for r in 1 2; do for v in 0 1; do
+  DTFX_GEMM_TA8=$v timeout -k 10 500 python tools/probes/dp_sim.py --model bert --variants 1gpu,dp \
+    --steps 10 --rounds 2 > $OUT/dp_ta8${v}_$r.json 2> $OUT/dp_ta8${v}_$r.err || { tail -20 $OUT/dp_ta8${v}_$r.err; exit 1; }
+  echo "ta8=$v $r $(python -c "import json;d=json.load(open('$OUT/dp_ta8${v}_$r.json'))['ms_per_step'];print({k:(v['median'],v['vs_1gpu_pct']) for k,v in d.items()})")"
+done; done
+}
+
 case "${1:-}" in
-  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines|attn_pf) exp_"$1" ;;
-  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines|attn_pf}" >&2; exit 2 ;;
+  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines|attn_pf|dp_ta8) exp_"$1" ;;
+  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines|attn_pf|dp_ta8}" >&2; exit 2 ;;
 esac
