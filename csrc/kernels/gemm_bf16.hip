@@ -901,11 +901,14 @@ static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
     // tiles, two for 128x128 (cfg 6: 0.75 of a 256x256 block's work at 0.81 of its efficiency
     // -- the N = 768 GEMMs fill all 256 CUs instead of 192; cfg 0: 0.25 at 0.47).
     // A^T operands (weight gradients) stay on 128x128 + split-K (760 vs 705 TFLOP/s).
-    static const bool ta8 = [] {  // DTFX_GEMM_TA8=1: weight gradients on the 8-phase tile too
+    // DTFX_GEMM_TA8=1: weight gradients on the 8-phase tile too; =2: only the large ones
+    // (>= 2 M outputs: BERT-base's FFN weight gradients, 808 vs 731 TFLOP/s standalone, while
+    // the QKV one is slower there, 632 vs 730: profiles/r6/gemm/wgrad_cfg/)
+    static const int ta8 = [] {
       const char* e = getenv("DTFX_GEMM_TA8");
-      return e && atoi(e) == 1;
+      return e ? atoi(e) : 0;
     }();
-    if (ta && !ta8) return 0;
+    if (ta && (ta8 <= 0 || (ta8 == 2 && (long long)M * N < 2000000))) return 0;
     static const int big = [] {  // DTFX_GEMM_BIG=3: the previous 2-stage large tile (A/B runs)
       const char* e = getenv("DTFX_GEMM_BIG");
       return e && atoi(e) == 3 ? 3 : 5;

@@ -283,7 +283,20 @@ for r in 1 2; do for v in 0 1; do
 done; done
 }
 
+exp_ta8_ffn() {
+# Round 6: BERT-base with only the FFN weight gradients on the 8-phase tile (DTFX_GEMM_TA8=2)
+# against the 128x128 split-K default (=0), interleaved; the bf16 / BERT GPU tests first.
+cd "$ROOT"; OUT=gpurun_out/r6ta8ffn; mkdir -p $OUT
+DTFX_GEMM_TA8=2 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
+  tests/test_bert_gpu.py > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+for r in 1 2 3; do for v in 2 0; do
+  DTFX_GEMM_TA8=$v timeout -k 10 200 python bench.py --model bert > $OUT/bert_ta8${v}_$r.json 2>&1 || { tail -5 $OUT/bert_ta8${v}_$r.json; exit 1; }
+  echo "bert ta8=$v $r $(tail -1 $OUT/bert_ta8${v}_$r.json | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+done; done
+}
+
 case "${1:-}" in
-  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines|attn_pf|dp_ta8) exp_"$1" ;;
-  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines|attn_pf|dp_ta8}" >&2; exit 2 ;;
+  flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines|attn_pf|dp_ta8|ta8_ffn) exp_"$1" ;;
+  *) echo "usage: $0 {flush|pers|resnet_zero1|resnet_fold|attn_rp|k20_env|probe|attn_swz|resnet_wt|mlp_plan|zero_ranges|engines|attn_pf|dp_ta8|ta8_ffn}" >&2; exit 2 ;;
 esac
