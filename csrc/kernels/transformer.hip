@@ -210,7 +210,9 @@ __global__ __launch_bounds__(256) void layernorm_fwd_rows_kernel(
 // NC = ceil(H / 512) column chunks of 8 per lane.  Each of the NWV waves streams rows r0+wave, +NWV, ...
 // with the NEXT row's x / dy / dres loads issued before the current row is reduced
 // (software pipeline: one memory round trip per row instead of two) and gamma hoisted.
-template <int NC>
+// NS row slots per wave (NS - 1 rows in flight while one is reduced): 2 by default, 3 with
+// DTFX_LN_SLOTS=3 (H <= 1024 only: 4 slots spill at H = 768).
+template <int NC, int NS = 2>
 __global__ __launch_bounds__(NC <= 2 ? 512 : 256) void layernorm_bwd_kernel(
     int T, int H, int rows_per_block, const unsigned short* __restrict__ dy,
     const unsigned short* __restrict__ x, const float* __restrict__ mean_in,
@@ -238,8 +240,8 @@ __global__ __launch_bounds__(NC <= 2 ? 512 : 256) void layernorm_bwd_kernel(
   // Two rows in flight per wave beyond the one being reduced (register double buffer, two
   // rows per trip so the buffer index stays literal): with one, every row waited out most of
   // a memory round trip (the kernel ran at ~1/2 of its HBM bound at the BERT shape).
-  bf16x8 xb[2][NC], yb[2][NC], rb[2][NC];
-  float mb[2] = {0.f, 0.f}, rsb[2] = {0.f, 0.f};
+  bf16x8 xb[NS][NC], yb[NS][NC], rb[NS][NC];
+  float mb[NS] = {}, rsb[NS] = {};
   auto load = [&](int p, int row) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -253,11 +255,12 @@ __global__ __launch_bounds__(NC <= 2 ? 512 : 256) void layernorm_bwd_kernel(
   };
   const int first = r0 + wave;
   const int nrows = first < r1 ? (r1 - first + NWV - 1) / NWV : 0;  // rows of this wave
-  if (nrows > 0) load(0, first);
-  if (nrows > 1) load(1, first + NWV);
-  for (int i = 0; i < nrows; i += 2) {
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
+  for (int p = 0; p < NS; ++p)
+    if (nrows > p) load(p, first + p * NWV);
+  for (int i = 0; i < nrows; i += NS) {
+#pragma unroll
+    for (int p = 0; p < NS; ++p) {
       if (i + p >= nrows) break;
       const int row = first + (i + p) * NWV;
       float xh[NC][8], g[NC][8], dyv[NC][8], rv[NC][8];
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(NC <= 2 ? 512 : 256) void layernorm_bwd_kernel(
           db[c][u] += dyv[c][u];
         }
       }
-      if (i + p + 2 < nrows) load(p, row + 2 * NWV);  // in flight during the reductions
+      if (i + p + NS < nrows) load(p, row + NS * NWV);  // in flight during the reductions
       s1 = wave_sum(s1) / H;
       s2 = wave_sum(s2) / H;
 #pragma unroll
@@ -1718,6 +1721,9 @@ void layernorm_fwd_launch(int T, int H, const void* x, const float* gamma, const
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+static int g_ln_slots = -1;  // -1: DTFX_LN_SLOTS (tests set both forms)
+void ln_bwd_set_slots(int v) { g_ln_slots = v; }
+
 void layernorm_bwd_launch(int T, int H, const void* dy, const void* x, const float* mean,
                           const float* rstd, const float* gamma, const void* dres, void* dx,
                           float* dgamma, float* dbeta, float* dxsum, hipStream_t s) {
@@ -1730,15 +1736,22 @@ void layernorm_bwd_launch(int T, int H, const void* dy, const void* x, const flo
     return e ? atoi(e) : 0;
   }();
   const int rpb = rpb_env > 0 ? rpb_env : (T >= 8192 ? 64 : 16);
+  static const int slots_env = [] {
+    const char* e = getenv("DTFX_LN_SLOTS");
+    return e && atoi(e) >= 3 ? 3 : 2;
+  }();
+  const int slots = g_ln_slots >= 0 ? (g_ln_slots >= 3 ? 3 : 2) : slots_env;
   const int nc = (H / 8 + 63) / 64;
-#define DTFX_LNB(NC_)                                                                           \
-  hipLaunchKernelGGL(layernorm_bwd_kernel<NC_>, dim3((T + rpb - 1) / rpb), dim3(NC_ <= 2 ? 512 : 256), 0, s, T, H, \
+#define DTFX_LNB(NC_, NS_)                                                                      \
+  hipLaunchKernelGGL((layernorm_bwd_kernel<NC_, NS_>), dim3((T + rpb - 1) / rpb), dim3(NC_ <= 2 ? 512 : 256), 0, s, T, H, \
                      rpb, (const unsigned short*)dy, (const unsigned short*)x, mean, rstd, gamma,  \
                      (const unsigned short*)dres, (unsigned short*)dx, dgamma, dbeta, dxsum)
-  if (nc == 1) DTFX_LNB(1);
-  else if (nc == 2) DTFX_LNB(2);
-  else if (nc == 3) DTFX_LNB(3);
-  else DTFX_LNB(4);
+  if (nc == 1 && slots == 3) DTFX_LNB(1, 3);
+  else if (nc == 2 && slots == 3) DTFX_LNB(2, 3);
+  else if (nc == 1) DTFX_LNB(1, 2);
+  else if (nc == 2) DTFX_LNB(2, 2);
+  else if (nc == 3) DTFX_LNB(3, 2);
+  else DTFX_LNB(4, 2);
 #undef DTFX_LNB
   DTFX_HIP_CHECK(hipGetLastError());
 }

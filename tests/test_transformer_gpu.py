@@ -15,9 +15,11 @@ def _r(*shape, seed=0, scale=1.0):
     return (torch.randn(*shape, generator=g) * scale)
 
 
-@pytest.mark.parametrize("Tn,H", [(300, 768), (37, 136), (70, 2048), (129, 1000)])
-def test_layernorm_fwd_bwd(gpu, Tn, H):
-    # (row counts off the 16-row blocks of the 4-rows-per-wave forward; 1..4 column chunks)
+@pytest.mark.parametrize("slots", [2, 3])  # row slots per wave of the backward (DTFX_LN_SLOTS)
+@pytest.mark.parametrize("Tn,H", [(300, 768), (37, 136), (70, 2048), (129, 1000), (16384, 768)])
+def test_layernorm_fwd_bwd(gpu, Tn, H, slots):
+    # (row counts off the 16-row blocks of the 4-rows-per-wave forward; 1..4 column chunks;
+    # 16384 x 768: the BERT shape, 64 rows per block)
     x = _r(Tn, H, seed=1).to(BF)
     gamma, beta = _r(H, seed=2) * 0.1 + 1, _r(H, seed=3) * 0.1
     y, mean, rstd = T.layernorm_fwd(x.to(gpu), gamma.to(gpu), beta.to(gpu))
@@ -26,7 +28,13 @@ def test_layernorm_fwd_bwd(gpu, Tn, H):
     assert (y.cpu().float() - yr.float()).abs().max() < 3e-2
     dy, dres = _r(Tn, H, seed=4).to(BF), _r(Tn, H, seed=5).to(BF)
     dg, db = torch.zeros(H, device=gpu), torch.zeros(H, device=gpu)
-    dx = T.layernorm_bwd(dy.to(gpu), x.to(gpu), mean, rstd, gamma.to(gpu), dg, db, dres.to(gpu))
+    _ext.hip().ln_bwd_set_slots(slots)
+    try:
+        dx = T.layernorm_bwd(dy.to(gpu), x.to(gpu), mean, rstd, gamma.to(gpu), dg, db,
+                             dres.to(gpu))
+        torch.cuda.synchronize()
+    finally:
+        _ext.hip().ln_bwd_set_slots(-1)
     dgr, dbr = torch.zeros(H), torch.zeros(H)
     dxr = T.layernorm_bwd(dy, x, mr, rr, gamma, dgr, dbr, dres)
     assert (dx.cpu().float() - dxr.float()).abs().max() < 5e-2
