@@ -50,8 +50,25 @@ def main():
                 res[slots].append(e0.elapsed_time(e1) * 1e3 / a.iters)
     finally:
         hip.ln_bwd_set_slots(-1)
+    # what the default kernel's time is made of: without the column sums (1/3 of the
+    # cross-block atomics) and without the residual gradient (1/4 of the row traffic)
+    parts = {}
+    for name, kw in (("full", dict(dres=dres, dxsum=ds)), ("no_dxsum", dict(dres=dres)),
+                     ("no_dres", dict(dxsum=ds)), ("neither", {})):
+        v = []
+        for _ in range(a.rounds):
+            for _ in range(10):
+                T.layernorm_bwd(dy, x, mean, rstd, gamma, dg, db, **kw)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                T.layernorm_bwd(dy, x, mean, rstd, gamma, dg, db, **kw)
+            e1.record()
+            torch.cuda.synchronize()
+            v.append(e0.elapsed_time(e1) * 1e3 / a.iters)
+        parts[name] = round(sorted(v)[len(v) // 2], 2)
     nbytes = 4 * Tn * H * 2
-    out = {"rows": Tn, "hidden": H, "iters": a.iters}
+    out = {"rows": Tn, "hidden": H, "iters": a.iters, "default_slots_us": parts}
     for s, v in res.items():
         med = sorted(v)[len(v) // 2]
         out["slots%d" % s] = {"us_median": round(med, 2), "all": [round(t, 2) for t in v],
