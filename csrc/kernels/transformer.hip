@@ -336,6 +336,115 @@ __global__ __launch_bounds__(NC <= 2 ? 512 : 256) void layernorm_bwd_kernel(
   }
 }
 
+// H = 768 (BERT-base) form of layernorm_bwd_kernel with about half the registers: 12 columns
+// per lane as three 4-column chunks (lane l: columns 256 c + 4 l .. + 3, so each load
+// instruction covers 512 contiguous bytes), the row slots kept as bf16 and re-read in the
+// second pass instead of f32 copies of x-hat / g / dy / dres, gamma in LDS, both row sums in one
+// interleaved wave reduction.  <= 128 VGPRs: two 8-wave blocks share a CU (16 waves) and each
+// wave reduces 4 rows instead of 8 (the default kernel is bound by its per-wave row latency
+// chain, profiles/r6/ln_slots/).  Same outputs and accumulation targets.
+template <int NSL>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void layernorm_bwd_h768_kernel(
+    int T, int rows_per_block, const unsigned short* __restrict__ dy,
+    const unsigned short* __restrict__ x, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const float* __restrict__ gamma,
+    const unsigned short* __restrict__ dres, unsigned short* __restrict__ dx,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dxsum) {
+  constexpr int H = 768, NWV = 8;
+  __shared__ f32x4 red[3][NWV][H / 4];  // [dgamma|dbeta|dxsum][wave][column quad]
+  __shared__ f32x4 gms[H / 4];
+  // wave index made provably uniform: row addresses then live in scalar registers (one lane
+  // offset VGPR for every load) instead of a 64-bit VGPR pair per load
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (threadIdx.x < H / 4) gms[threadIdx.x] = ((const f32x4*)gamma)[threadIdx.x];
+  f32x4 dg[3], db[3], ds[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) dg[c] = db[c] = ds[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(T, r0 + rows_per_block);
+  bf16x4 xb[NSL][3], yb[NSL][3], rb[NSL][3];
+  float mb[NSL] = {}, rsb[NSL] = {};
+  auto load = [&](int p, int row) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const size_t off = (size_t)row * H + 256 * c + 4 * lane;
+      xb[p][c] = __builtin_nontemporal_load((const bf16x4*)(x + off));
+      yb[p][c] = __builtin_nontemporal_load((const bf16x4*)(dy + off));
+      if (dres) rb[p][c] = __builtin_nontemporal_load((const bf16x4*)(dres + off));
+    }
+    mb[p] = mean_in[row];
+    rsb[p] = rstd_in[row];
+  };
+  const int first = r0 + wave;
+  const int nrows = first < r1 ? (r1 - first + NWV - 1) / NWV : 0;  // rows of this wave
+#pragma unroll
+  for (int p = 0; p < NSL; ++p)
+    if (nrows > p) load(p, first + p * NWV);
+  __syncthreads();  // gamma in LDS
+  for (int i = 0; i < nrows; i += NSL) {
+#pragma unroll
+    for (int p = 0; p < NSL; ++p) {
+      if (i + p >= nrows) break;
+      const int row = first + (i + p) * NWV;
+      const float mu = mb[p], rs = rsb[p];
+      float sum[2] = {0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const f32x4 gm = gms[64 * c + lane];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float dyv = bf((unsigned short)yb[p][c][u]);
+          const float xh = (bf((unsigned short)xb[p][c][u]) - mu) * rs;
+          const float g = dyv * gm[u];
+          sum[0] += g;
+          sum[1] += g * xh;
+          dg[c][u] += dyv * xh;
+          db[c][u] += dyv;
+        }
+      }
+      wave_sum_n(sum);
+      const float s1 = sum[0] / H, s2 = sum[1] / H;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const f32x4 gm = gms[64 * c + lane];
+        bf16x4 o4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float xh = (bf((unsigned short)xb[p][c][u]) - mu) * rs;
+          float o = rs * (bf((unsigned short)yb[p][c][u]) * gm[u] - s1 - xh * s2);
+          if (dres) o += bf((unsigned short)rb[p][c][u]);
+          ds[c][u] += o;
+          o4[u] = (short)tobf(o);
+        }
+        __builtin_nontemporal_store(o4, (bf16x4*)(dx + (size_t)row * H + 256 * c + 4 * lane));
+      }
+      if (i + p + NSL < nrows) load(p, row + NSL * NWV);  // the slot is free after the second pass
+    }
+  }
+  // cross-wave reduction (one 16-byte LDS store per lane and array: conflict free), then one
+  // atomic per column and array
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    red[0][wave][64 * c + lane] = dg[c];
+    red[1][wave][64 * c + lane] = db[c];
+    red[2][wave][64 * c + lane] = ds[c];
+  }
+  __syncthreads();
+  const float* rf = (const float*)red;
+  for (int j = threadIdx.x; j < H; j += 64 * NWV) {
+    float a = 0.f, b = 0.f, d = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      a += rf[(0 * NWV + w) * H + j];
+      b += rf[(1 * NWV + w) * H + j];
+      d += rf[(2 * NWV + w) * H + j];
+    }
+    unsafeAtomicAdd(dgamma + j, a);
+    unsafeAtomicAdd(dbeta + j, b);
+    if (dxsum) unsafeAtomicAdd(dxsum + j, d);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Embedding: x = word[ids] + pos[t % S] + type[tt]; y = LN(x).  Saves x (bf16).
 // ---------------------------------------------------------------------------
@@ -1723,6 +1832,8 @@ void layernorm_fwd_launch(int T, int H, const void* x, const float* gamma, const
 
 static int g_ln_slots = -1;  // -1: DTFX_LN_SLOTS (tests set both forms)
 void ln_bwd_set_slots(int v) { g_ln_slots = v; }
+static int g_ln_h768 = -1;  // -1: DTFX_LN_H768
+void ln_bwd_set_h768(int v) { g_ln_h768 = v; }
 
 void layernorm_bwd_launch(int T, int H, const void* dy, const void* x, const float* mean,
                           const float* rstd, const float* gamma, const void* dres, void* dx,
@@ -1735,19 +1846,35 @@ void layernorm_bwd_launch(int T, int H, const void* dy, const void* x, const flo
     const char* e = getenv("DTFX_LN_RPB");
     return e ? atoi(e) : 0;
   }();
-  const int rpb = rpb_env > 0 ? rpb_env : (T >= 8192 ? 64 : 16);
   static const int slots_env = [] {
     const char* e = getenv("DTFX_LN_SLOTS");
-    return e && atoi(e) >= 3 ? 3 : 2;
+    return e ? std::max(1, std::min(3, atoi(e))) : 2;
   }();
-  const int slots = g_ln_slots >= 0 ? (g_ln_slots >= 3 ? 3 : 2) : slots_env;
+  // row slots per wave of the generic kernel: 2 (default) or 3
+  const int slots = g_ln_slots >= 0 ? std::max(1, std::min(3, g_ln_slots)) : slots_env;
+  static const int h768_env = [] {
+    const char* e = getenv("DTFX_LN_H768");
+    return e ? atoi(e) : 0;
+  }();
+  if (H == 768 && (g_ln_h768 >= 0 ? g_ln_h768 : h768_env) == 1 && !(((uintptr_t)gamma) & 15)) {
+    // 4 rows per wave at the BERT shape (512 blocks, two per CU)
+    const int rpb7 = rpb_env > 0 ? rpb_env : (T >= 8192 ? 32 : 8);
+    // one row slot per wave: the 16 resident waves per CU are the pipeline (two slots spill
+    // at the 128 VGPRs four waves per SIMD allow)
+    hipLaunchKernelGGL(layernorm_bwd_h768_kernel<1>, dim3((T + rpb7 - 1) / rpb7), dim3(512), 0, s,
+                         T, rpb7, (const unsigned short*)dy, (const unsigned short*)x, mean, rstd,
+                         gamma, (const unsigned short*)dres, (unsigned short*)dx, dgamma, dbeta, dxsum);
+    DTFX_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  const int rpb = rpb_env > 0 ? rpb_env : (T >= 8192 ? 64 : 16);
   const int nc = (H / 8 + 63) / 64;
 #define DTFX_LNB(NC_, NS_)                                                                      \
   hipLaunchKernelGGL((layernorm_bwd_kernel<NC_, NS_>), dim3((T + rpb - 1) / rpb), dim3(NC_ <= 2 ? 512 : 256), 0, s, T, H, \
                      rpb, (const unsigned short*)dy, (const unsigned short*)x, mean, rstd, gamma,  \
                      (const unsigned short*)dres, (unsigned short*)dx, dgamma, dbeta, dxsum)
-  if (nc == 1 && slots == 3) DTFX_LNB(1, 3);
-  else if (nc == 2 && slots == 3) DTFX_LNB(2, 3);
+  if (nc == 1 && slots >= 3) DTFX_LNB(1, 3);
+  else if (nc == 2 && slots >= 3) DTFX_LNB(2, 3);
   else if (nc == 1) DTFX_LNB(1, 2);
   else if (nc == 2) DTFX_LNB(2, 2);
   else if (nc == 3) DTFX_LNB(3, 2);

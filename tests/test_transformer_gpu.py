@@ -15,7 +15,9 @@ def _r(*shape, seed=0, scale=1.0):
     return (torch.randn(*shape, generator=g) * scale)
 
 
-@pytest.mark.parametrize("slots", [2, 3])  # row slots per wave of the backward (DTFX_LN_SLOTS)
+# backward variants: row slots per wave of the generic kernel (DTFX_LN_SLOTS 2 / 3) and the
+# H = 768 kernel (DTFX_LN_H768=1; the generic one at every other H)
+@pytest.mark.parametrize("slots", [2, 3, "h768"])
 @pytest.mark.parametrize("Tn,H", [(300, 768), (37, 136), (70, 2048), (129, 1000), (16384, 768)])
 def test_layernorm_fwd_bwd(gpu, Tn, H, slots):
     # (row counts off the 16-row blocks of the 4-rows-per-wave forward; 1..4 column chunks;
@@ -28,13 +30,16 @@ def test_layernorm_fwd_bwd(gpu, Tn, H, slots):
     assert (y.cpu().float() - yr.float()).abs().max() < 3e-2
     dy, dres = _r(Tn, H, seed=4).to(BF), _r(Tn, H, seed=5).to(BF)
     dg, db = torch.zeros(H, device=gpu), torch.zeros(H, device=gpu)
-    _ext.hip().ln_bwd_set_slots(slots)
+    hip = _ext.hip()
+    hip.ln_bwd_set_slots(2 if slots == "h768" else slots)
+    hip.ln_bwd_set_h768(1 if slots == "h768" else 0)
     try:
         dx = T.layernorm_bwd(dy.to(gpu), x.to(gpu), mean, rstd, gamma.to(gpu), dg, db,
                              dres.to(gpu))
         torch.cuda.synchronize()
     finally:
-        _ext.hip().ln_bwd_set_slots(-1)
+        hip.ln_bwd_set_slots(-1)
+        hip.ln_bwd_set_h768(-1)
     dgr, dbr = torch.zeros(H), torch.zeros(H)
     dxr = T.layernorm_bwd(dy, x, mr, rr, gamma, dgr, dbr, dres)
     assert (dx.cpu().float() - dxr.float()).abs().max() < 5e-2
