@@ -12,6 +12,7 @@ int gemm_bf16_set_pers(int);
 void attn_bwd_set_variant(int);
 void attn_bwd_set_pf(int);
 void ln_bwd_set_slots(int);
+void xent_set_regs(int);
 void ln_bwd_set_h768(int);
 void attn_set_swizzle(int);
 void attn_fwd_set_variant(int);
@@ -131,6 +132,9 @@ void register_nn(py::module_& m) {
   m.def("attn_bwd_set_variant", &dtfx::attn_bwd_set_variant,
         "force the attention-backward kernel (-1 = environment; 0: 8 waves, 1: 4 waves, "
         "2: two query halves, two blocks per CU)");
+  m.def("xent_set_regs", &dtfx::xent_set_regs,
+        "bf16 MLM cross-entropy: 1 = the row held in registers (one read of the logits), "
+        "0 = the two-pass kernel, -1 = from DTFX_XENT_REGS");
   m.def("ln_bwd_set_h768", &dtfx::ln_bwd_set_h768,
         "LayerNorm backward at H = 768: 1 = the 12-columns-per-lane kernel (two blocks per CU), "
         "0 = the generic one, -1 = from DTFX_LN_H768");

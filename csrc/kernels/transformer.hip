@@ -1759,6 +1759,97 @@ __global__ __launch_bounds__(256) void mlm_xent_kernel(int C, const LT* __restri
   }
 }
 
+// The bf16 form with the row held in registers (C <= 32768, rows 16-byte aligned): each thread
+// loads its <= 16 chunks of 8 logits once as 16-byte loads (all in flight together), takes the
+// max / argmax and then the sum of exponentials from the registers, and forms its dlogits
+// chunks from the same registers -- one read of the row instead of two (the second one an L2
+// or HBM re-read of 61 KB per row at the BERT vocabulary), 16-byte loads and stores.
+constexpr int kXentChunks = 16;
+__global__ __launch_bounds__(256) void mlm_xent_regs_kernel(int C, const unsigned short* __restrict__ logits,
+                                                            int ldl, const int* __restrict__ labels,
+                                                            float scale, float* __restrict__ loss,
+                                                            float* __restrict__ correct,
+                                                            unsigned short* __restrict__ dl, int ldd) {
+  __shared__ float sm_m[4], sm_s[4], sm_b[4];
+  __shared__ int sm_a[4];
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const unsigned short* l = logits + (size_t)row * ldl;
+  const int y = labels[row];
+  const int C8 = C >> 3;
+  bf16x8 v[kXentChunks];
+#pragma unroll
+  for (int k = 0; k < kXentChunks; ++k) {
+    const int i = t + 256 * k;
+    if (i < C8) v[k] = __builtin_nontemporal_load((const bf16x8*)l + i);
+  }
+  // max and argmax (first index on ties: chunks in increasing index order per thread)
+  float best = -INFINITY;
+  int am = 0x7fffffff;
+#pragma unroll
+  for (int k = 0; k < kXentChunks; ++k) {
+    const int i = t + 256 * k;
+    if (i < C8)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float x = bf((unsigned short)v[k][u]);
+        if (x > best) { best = x; am = 8 * i + u; }
+      }
+  }
+  for (int c = 8 * C8 + t; c < C; c += 256) {  // (C % 8 tail, one element per thread at most)
+    const float x = bf(l[c]);
+    if (x > best) { best = x; am = c; }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float b2 = __shfl_xor(best, o);
+    const int a2 = __shfl_xor(am, o);
+    if (b2 > best || (b2 == best && a2 < am)) { best = b2; am = a2; }
+  }
+  if (lane == 0) { sm_b[wave] = best; sm_a[wave] = am; }
+  __syncthreads();
+  float M = sm_b[0];
+  int A = sm_a[0];
+  for (int w = 1; w < 4; ++w)
+    if (sm_b[w] > M || (sm_b[w] == M && sm_a[w] < A)) { M = sm_b[w]; A = sm_a[w]; }
+  // sum of exponentials against the row max (exact: no rescaling)
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < kXentChunks; ++k) {
+    const int i = t + 256 * k;
+    if (i < C8)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += __expf(bf((unsigned short)v[k][u]) - M);
+  }
+  for (int c = 8 * C8 + t; c < C; c += 256) sum += __expf(bf(l[c]) - M);
+  sum = wave_sum(sum);
+  if (lane == 0) sm_s[wave] = sum;
+  __syncthreads();
+  const float Ssum = (sm_s[0] + sm_s[1]) + (sm_s[2] + sm_s[3]);
+  const bool valid = y >= 0 && y < C;
+  const float lse = M + __logf(Ssum);
+  if (t == 0) {
+    loss[row] = valid ? lse - bf(l[y]) : 0.f;
+    correct[row] = (valid && A == y) ? 1.f : 0.f;
+  }
+  unsigned short* d = dl + (size_t)row * ldd;
+  const float sc = valid ? scale : 0.f;
+  const int D8 = ldd >> 3;
+#pragma unroll
+  for (int k = 0; k < kXentChunks; ++k) {
+    const int i = t + 256 * k;
+    if (i >= D8) break;
+    bf16x8 o;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = 8 * i + u;
+      float g = 0.f;
+      if (i < C8) g = (__expf(bf((unsigned short)v[k][u]) - lse) - (c == y ? 1.f : 0.f)) * sc;
+      else if (c < C) g = (__expf(bf(l[c]) - lse) - (c == y ? 1.f : 0.f)) * sc;
+      o[u] = (short)tobf(g);
+    }
+    __builtin_nontemporal_store(o, (bf16x8*)d + i);
+  }
+}
+
 // dx = dy * act'(u), bf16 (gelu-tanh: act 1, relu: act 2); n % 8 == 0
 __global__ __launch_bounds__(256) void act_grad_bf16_kernel(long long n8, int act,
                                                             const unsigned short* __restrict__ dy,
@@ -2104,11 +2195,27 @@ void adam_mixed_launch(long long n, float* p, const float* g, float* m, float* v
   DTFX_HIP_CHECK(hipGetLastError());
 }
 
+static int g_xent_regs = -1;  // -1: DTFX_XENT_REGS (tests set both forms)
+void xent_set_regs(int v) { g_xent_regs = v; }
+
 void mlm_xent_launch(int N, int C, const void* logits, bool logits_bf16, int ldl, const int* labels,
                      float scale, float* loss, float* correct, void* dl, int ldd, hipStream_t s) {
   if (ldl % 4 || ldd % 4 || ldd < C || ldl < C)
     throw std::runtime_error("mlm_xent: ldl/ldd must be multiples of 4 and >= C");
   if (N <= 0) return;
+  static const int regs_env = [] {
+    const char* e = getenv("DTFX_XENT_REGS");
+    return e ? atoi(e) : 1;
+  }();
+  const bool regs = (g_xent_regs >= 0 ? g_xent_regs : regs_env) == 1;
+  if (logits_bf16 && regs && ldl % 8 == 0 && ldd % 8 == 0 && ldd <= 256 * 8 * kXentChunks &&
+      !(((uintptr_t)logits | (uintptr_t)dl) & 15)) {
+    hipLaunchKernelGGL(mlm_xent_regs_kernel, dim3(N), dim3(256), 0, s, C,
+                       (const unsigned short*)logits, ldl, labels, scale, loss, correct,
+                       (unsigned short*)dl, ldd);
+    DTFX_HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (logits_bf16)
     hipLaunchKernelGGL(mlm_xent_kernel<unsigned short>, dim3(N), dim3(256), 0, s, C,
                        (const unsigned short*)logits, ldl, labels, scale, loss, correct,

@@ -119,14 +119,24 @@ def test_adam_mixed_and_cast(gpu):
     assert torch.equal(T.cast_bf16(G).cpu(), g.to(BF))
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, BF])
-def test_mlm_xent_matches_reference(gpu, dtype):
+# regs: the bf16 kernel holding the row in registers (default) or the two-pass one; the
+# 30522 / 30528 case is the BERT vocabulary (15 chunks of 8 per thread, a 2-element tail)
+@pytest.mark.parametrize("regs", [1, 0])
+@pytest.mark.parametrize("dtype,N,C,ld", [(torch.float32, 70, 1003, 1024), (BF, 70, 1003, 1024),
+                                          (BF, 37, 30522, 30528), (BF, 5, 7, 8)])
+def test_mlm_xent_matches_reference(gpu, dtype, N, C, ld, regs):
     # bf16 logits: the kernel reads them as stored, the reference gets the same rounded values
-    N, C, ld = 70, 1003, 1024
     logits = (_r(N, ld, seed=20) * 3).to(dtype)
     lab = torch.randint(0, C, (N,), dtype=torch.int32)
-    lab[5] = -100
-    lg, cg, dg = T.mlm_xent(logits.to(gpu), lab.to(gpu), C, 1 / 69)
+    lab[min(5, N - 1)] = -100
+    lab[0] = int(logits[0, :C].float().argmax())  # at least one correct prediction
+    hip = _ext.hip()
+    hip.xent_set_regs(regs)
+    try:
+        lg, cg, dg = T.mlm_xent(logits.to(gpu), lab.to(gpu), C, 1 / 69)
+        torch.cuda.synchronize()
+    finally:
+        hip.xent_set_regs(-1)
     lr, cr, dr = T.mlm_xent(logits, lab, C, 1 / 69)
     assert torch.allclose(lg.cpu(), lr, atol=1e-4)
     assert torch.equal(cg.cpu(), cr)
