@@ -50,6 +50,10 @@ def main():
         ("qkv_dgrad", T, 768, 2304, False, False, None), ("ffn1_dgrad", T, 768, 3072, False, False, None),
         ("ffn2_dgrad_gelu", T, 3072, 768, False, False, "gelu_grad"),
         ("ffn1_wgrad", 3072, 768, T, True, False, "f32"), ("qkv_wgrad", 2304, 768, T, True, False, "f32"),
+        # the MLM decoder at batch 128 (2432 masked rows, vocabulary padded to 30528):
+        # logits, hidden-state gradient, weight gradient
+        ("dec_fwd", 2432, 30528, 768, False, True, None), ("dec_dgrad", 2432, 768, 30528, False, False, None),
+        ("dec_wgrad", 30528, 768, 2432, True, False, "f32"),
         ("sq4096", 4096, 4096, 4096, False, True, None), ("sq8192", 8192, 8192, 8192, False, True, None),
         # ResNet-50 1x1 convolutions at batch 256 as plain GEMMs (x [pixels][Cin] W[Cout][Cin]^T)
         ("r_l3c3_fwd", 50176, 1024, 256, False, True, None), ("r_l2c3_fwd", 200704, 512, 128, False, True, None),
