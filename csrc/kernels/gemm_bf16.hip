@@ -935,6 +935,14 @@ static int choose_cfg(int M, int N, int zdim, int mode, bool ta = false) {
       return e && atoi(e) == 1;
     }();
     if (use6 && est6 < est5 && est6 < est0 && N > 128) return 6;
+    // vocabulary-wide outputs (BERT's MLM logits, 2432 x 30528 x 768): the model rates the
+    // 128x128 tile 4 % ahead, the 8-phase tile measures 11 % ahead (735 vs 662 TFLOP/s,
+    // profiles/r6/gemm/decoder/) -- within 10 % of the model, wide outputs take the big tile
+    static const bool wide5 = [] {  // DTFX_GEMM_WIDE=0: the model's choice (A/B runs)
+      const char* e = getenv("DTFX_GEMM_WIDE");
+      return !(e && atoi(e) == 0);
+    }();
+    if (wide5 && zdim == 1 && !ta && N >= 16384 && t3 >= 256 && est5 <= est0 * 1.1) return 5;
     // the 8-phase tile with its sparse last round's rows on the 128x128 tile (gemm_tail_rows):
     // the whole rounds plus the tail's 128x128 rounds (BERT-base QKV: 2 + 0.53 against the
     // 128x128 tile's 2.66 -- 746 vs 737 TFLOP/s, profiles/r6/probe2/)
