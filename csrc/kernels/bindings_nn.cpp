@@ -22,6 +22,7 @@ void gemm_bf16_launch(bool, bool, bool, int, int, int, const void*, int, const v
                       int, int, int, int, long long, long long, long long,
                       float*, hipStream_t, float*, long long, bool);
 void colsum_bf16_launch(const void*, int, int, int, float*, float, hipStream_t);
+void colsum_set_rows_in_flight(int);
 long long gemm_bf16_ws_floats(bool, bool, int, int, int, int, float);
 long long conv_wgrad_ws_floats(int, int, int, int, int, int, int, int, int);
 long long conv_splitk_ws_floats(int, int, int, int, int, int, int, int, int, int);
@@ -132,6 +133,8 @@ void register_nn(py::module_& m) {
   m.def("attn_bwd_set_variant", &dtfx::attn_bwd_set_variant,
         "force the attention-backward kernel (-1 = environment; 0: 8 waves, 1: 4 waves, "
         "2: two query halves, two blocks per CU)");
+  m.def("colsum_set_rows_in_flight", &dtfx::colsum_set_rows_in_flight,
+        "bf16 column sums: rows in flight per thread, 4 or 8 (0 = from DTFX_COLSUM_U)");
   m.def("xent_set_regs", &dtfx::xent_set_regs,
         "bf16 MLM cross-entropy: 1 = the row held in registers (one read of the logits), "
         "0 = the two-pass kernel, -1 = from DTFX_XENT_REGS");

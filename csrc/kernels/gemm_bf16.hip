@@ -1737,6 +1737,7 @@ void conv_bf16_launch(int mode, int N, int H, int W, int C, int Cout, int KH, in
 // Vector form (ldg % 8 == 0, 16-B aligned G): each thread owns 8 columns and streams rows
 // with 16-B loads, 4 rows in flight; blockIdx.y splits the rows (partials combined with one
 // atomic per column and row group).
+template <int U>  // rows in flight per thread (4, or 8: DTFX_COLSUM_U)
 __global__ __launch_bounds__(256) void colsum8_bf16_kernel(const unsigned short* __restrict__ G,
                                                            int M, int N, int ldg,
                                                            float* __restrict__ out, float beta) {
@@ -1748,12 +1749,12 @@ __global__ __launch_bounds__(256) void colsum8_bf16_kernel(const unsigned short*
   const int per = (M + gridDim.y - 1) / gridDim.y;
   const int m0 = blockIdx.y * per, m1 = min(M, m0 + per);
   int m = m0;
-  for (; m + 4 <= m1; m += 4) {
-    bf16x8 v[4];
+  for (; m + U <= m1; m += U) {
+    bf16x8 v[U];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = *(const bf16x8*)(G + (size_t)(m + i) * ldg + n0);
+    for (int i = 0; i < U; ++i) v[i] = *(const bf16x8*)(G + (size_t)(m + i) * ldg + n0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < U; ++i)
 #pragma unroll
       for (int u = 0; u < 8; ++u) s[u] += bf2f((unsigned short)v[i][u]);
   }
@@ -1791,6 +1792,9 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const unsigned short* 
   }
 }
 
+static int g_colsum_u = 0;  // 0: DTFX_COLSUM_U; 4 / 8 forced (tests, probes)
+void colsum_set_rows_in_flight(int u) { g_colsum_u = (u == 4 || u == 8) ? u : 0; }
+
 void colsum_bf16_launch(const void* G, int M, int N, int ldg, float* out, float beta,
                         hipStream_t stream) {
   if (N <= 0) return;
@@ -1804,8 +1808,16 @@ void colsum_bf16_launch(const void* G, int M, int N, int ldg, float* out, float 
     if (beta == 0.f) DTFX_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * N, stream));
     else if (beta != 1.f) throw std::runtime_error("colsum_bf16: beta must be 0 or 1 for tall inputs");
   }
-  if (vec)
-    hipLaunchKernelGGL(colsum8_bf16_kernel, dim3(gx, gy), dim3(256), 0, stream,
+  static const int u_env = [] {
+    const char* e = getenv("DTFX_COLSUM_U");
+    return e && atoi(e) == 8 ? 8 : 4;
+  }();
+  const int u = g_colsum_u > 0 ? g_colsum_u : u_env;
+  if (vec && u == 8)
+    hipLaunchKernelGGL(colsum8_bf16_kernel<8>, dim3(gx, gy), dim3(256), 0, stream,
+                       (const unsigned short*)G, M, N, ldg, out, beta);
+  else if (vec)
+    hipLaunchKernelGGL(colsum8_bf16_kernel<4>, dim3(gx, gy), dim3(256), 0, stream,
                        (const unsigned short*)G, M, N, ldg, out, beta);
   else
     hipLaunchKernelGGL(colsum_bf16_kernel, dim3(gx, gy), dim3(256), 0, stream,

@@ -113,13 +113,22 @@ def test_gemm_gelu_dsave_and_mul(gpu, cfg, M, N, K):
         bf16.gemm(x, w, False, True, act="gelu_dsave")
 
 
-@pytest.mark.parametrize("M", [37, 5000])
-def test_colsum_bf16(gpu, M):
-    g = _rand(M, 300, dev=gpu, seed=9)
-    s = bf16.colsum(g)
+@pytest.mark.parametrize("u", [4, 8])  # rows in flight per thread (DTFX_COLSUM_U)
+@pytest.mark.parametrize("M,N", [(37, 300), (5000, 300), (2432, 30522)])
+def test_colsum_bf16(gpu, M, N, u):
+    # (2432 x 30522: the MLM decoder bias gradient; rows split over blocks, atomics)
+    from distributedtensorflowexample_amd.ops._ext import hip
+
+    g = _rand(M, N, dev=gpu, seed=9)
+    hip().colsum_set_rows_in_flight(u)
+    try:
+        s = bf16.colsum(g)
+        acc = torch.ones(N, device=gpu)
+        bf16.colsum(g, out=acc, beta=1.0)
+        torch.cuda.synchronize()
+    finally:
+        hip().colsum_set_rows_in_flight(0)
     assert (s - g.float().sum(0)).abs().max().item() < 1e-3 * (M ** 0.5)
-    acc = torch.ones(300, device=gpu)
-    bf16.colsum(g, out=acc, beta=1.0)
     assert (acc - 1 - g.float().sum(0)).abs().max().item() < 1e-3 * (M ** 0.5)
 
 
